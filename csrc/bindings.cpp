@@ -1,0 +1,274 @@
+// pybind11 bindings of the native core. Every op dispatches on the device of its tensors:
+// HIP tensors launch the gfx950 kernels on the current PyTorch HIP stream, CPU tensors run
+// the host C++ implementation. Shapes are validated here, before any kernel launch.
+#include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "scoring.h"
+#include "ops.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+#define FDX_CHECK(cond, msg) TORCH_CHECK(cond, "fdx: ", msg)
+
+template <class T>
+const T* cptr(const optional<Tensor>& t) {
+  return (t && t->defined()) ? t->data_ptr<T>() : nullptr;
+}
+template <class T>
+T* mptr(const optional<Tensor>& t) {
+  return (t && t->defined()) ? t->data_ptr<T>() : nullptr;
+}
+
+void check_dev(const Tensor& t, const at::Device& dev, const char* name) {
+  FDX_CHECK(t.device() == dev, std::string(name) + " must live on " + dev.str());
+  FDX_CHECK(t.is_contiguous(), std::string(name) + " must be contiguous");
+}
+
+fdx::StrTable make_table(const optional<std::vector<Tensor>>& tab, const at::Device& dev) {
+  fdx::StrTable t{nullptr, nullptr, nullptr, nullptr, -1};
+  if (!tab || tab->empty()) return t;
+  FDX_CHECK(tab->size() == 4, "string table = (slots, hashes, offs, bytes)");
+  const auto& v = *tab;
+  for (const auto& x : v) check_dev(x, dev, "string table");
+  FDX_CHECK(v[0].scalar_type() == at::kInt && v[1].scalar_type() == at::kInt &&
+                v[2].scalar_type() == at::kLong && v[3].scalar_type() == at::kByte,
+            "string table dtypes (int32, int32, int64, uint8)");
+  const int64_t size = v[0].numel();
+  FDX_CHECK(size > 0 && (size & (size - 1)) == 0, "table size must be a power of two");
+  FDX_CHECK(v[2].numel() == v[1].numel() + 1, "offs must have n+1 entries");
+  t.slots = v[0].data_ptr<int32_t>();
+  t.hashes = reinterpret_cast<const uint32_t*>(v[1].data_ptr<int32_t>());
+  t.offs = v[2].data_ptr<int64_t>();
+  t.bytes = v[3].data_ptr<uint8_t>();
+  t.mask = (int32_t)(size - 1);
+  return t;
+}
+
+fdx::TreeEnsemble make_trees(const optional<std::vector<Tensor>>& tr, int64_t K, const at::Device& dev) {
+  fdx::TreeEnsemble te{};
+  if (!tr || tr->empty()) return te;
+  FDX_CHECK(tr->size() == 7, "trees = (feat, thr, left, right, leaf, roots, weights)");
+  const auto& v = *tr;
+  for (const auto& x : v) check_dev(x, dev, "tree arrays");
+  const int64_t nodes = v[0].numel();
+  FDX_CHECK(v[1].numel() == nodes && v[2].numel() == nodes && v[3].numel() == nodes, "node arrays size");
+  FDX_CHECK(v[4].numel() == nodes * K, "leaf array must be nodes*K");
+  FDX_CHECK(v[5].numel() == v[6].numel(), "roots/weights size");
+  FDX_CHECK(v[0].scalar_type() == at::kInt && v[1].scalar_type() == at::kDouble &&
+                v[2].scalar_type() == at::kInt && v[3].scalar_type() == at::kInt &&
+                v[4].scalar_type() == at::kDouble && v[5].scalar_type() == at::kInt &&
+                v[6].scalar_type() == at::kDouble,
+            "tree dtypes");
+  te.feat = v[0].data_ptr<int32_t>();
+  te.thr = v[1].data_ptr<double>();
+  te.left = v[2].data_ptr<int32_t>();
+  te.right = v[3].data_ptr<int32_t>();
+  te.leaf = v[4].data_ptr<double>();
+  te.roots = v[5].data_ptr<int32_t>();
+  te.weights = v[6].data_ptr<double>();
+  te.num_trees = (int32_t)v[5].numel();
+  te.K = (int32_t)K;
+  return te;
+}
+
+void featurize_score(const Tensor& text, const Tensor& doc_off, int64_t flags, int64_t num_features,
+                     const optional<std::vector<Tensor>>& stop, const optional<std::vector<Tensor>>& vocab,
+                     double min_tf, const optional<Tensor>& idf, const optional<Tensor>& lr_w, double lr_b,
+                     const optional<std::vector<Tensor>>& trees, int64_t K, const Tensor& out_idx,
+                     const Tensor& out_val, const Tensor& out_nnz, const optional<Tensor>& out_ntok,
+                     const Tensor& out_raw, const Tensor& out_status, const optional<Tensor>& only_docs,
+                     int64_t threads) {
+  const auto dev = text.device();
+  check_dev(text, dev, "text");
+  check_dev(doc_off, dev, "doc_off");
+  FDX_CHECK(text.scalar_type() == at::kByte && doc_off.scalar_type() == at::kLong, "text u8 / doc_off i64");
+  const int64_t D = doc_off.numel() - 1;
+  FDX_CHECK(D >= 0, "doc_off needs at least one entry");
+  for (const Tensor* t : {&out_idx, &out_val, &out_nnz, &out_raw, &out_status}) check_dev(*t, dev, "outputs");
+  FDX_CHECK(out_nnz.numel() >= D && out_status.numel() >= D, "per-doc outputs too small");
+  FDX_CHECK(out_idx.numel() >= text.numel() + D || !(flags & fdx::kFlagWriteCsr), "CSR scratch too small");
+  FDX_CHECK(out_idx.numel() == out_val.numel(), "CSR idx/val size mismatch");
+  FDX_CHECK(num_features > 0 || (flags & fdx::kFlagVocab), "num_features must be positive");
+  if (flags & fdx::kFlagIdf) FDX_CHECK(idf && idf->numel() >= num_features && idf->scalar_type() == at::kDouble, "idf");
+  if (flags & fdx::kFlagLR) FDX_CHECK(lr_w && lr_w->numel() >= num_features && lr_w->scalar_type() == at::kDouble, "lr_w");
+  if (flags & fdx::kFlagTrees) FDX_CHECK(trees && K >= 1 && K <= 2, "trees");
+  FDX_CHECK(out_raw.numel() >= D * ((flags & fdx::kFlagTrees) ? K : 1), "out_raw too small");
+  if (idf) check_dev(*idf, dev, "idf");
+  if (lr_w) check_dev(*lr_w, dev, "lr_w");
+  if (out_ntok) check_dev(*out_ntok, dev, "out_ntok");
+
+  fdx::FeatArgs a{};
+  a.text = text.data_ptr<uint8_t>();
+  a.doc_off = doc_off.data_ptr<int64_t>();
+  a.num_docs = (int32_t)D;
+  a.flags = (int32_t)flags;
+  a.num_features = (int32_t)num_features;
+  a.stop = make_table(stop, dev);
+  a.vocab = make_table(vocab, dev);
+  a.min_tf = min_tf;
+  a.idf = cptr<double>(idf);
+  a.lr_w = cptr<double>(lr_w);
+  a.lr_b = lr_b;
+  a.trees = make_trees(trees, K, dev);
+  a.out_idx = out_idx.data_ptr<int32_t>();
+  a.out_val = out_val.data_ptr<float>();
+  a.out_nnz = out_nnz.data_ptr<int32_t>();
+  a.out_ntok = mptr<int32_t>(out_ntok);
+  a.out_raw = out_raw.data_ptr<double>();
+  a.out_status = out_status.data_ptr<int32_t>();
+  if (dev.is_cuda()) {
+    FDX_CHECK(!only_docs, "only_docs is a host-path option");
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_featurize_score(a, c10::hip::getCurrentHIPStream(dev.index()).stream());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    const int32_t* only = nullptr;
+    int32_t n_only = 0;
+    if (only_docs) {
+      FDX_CHECK(only_docs->scalar_type() == at::kInt && only_docs->is_contiguous(), "only_docs int32");
+      only = only_docs->data_ptr<int32_t>();
+      n_only = (int32_t)only_docs->numel();
+    }
+    fdx::featurize_score_cpu(a, only, n_only, (int)threads);
+  }
+}
+
+hipStream_t stream_of(const at::Device& dev) {
+  return c10::hip::getCurrentHIPStream(dev.index()).stream();
+}
+
+void check_csr(const Tensor& indptr, const Tensor& idx, const Tensor& val, const at::Device& dev) {
+  check_dev(indptr, dev, "indptr");
+  check_dev(idx, dev, "indices");
+  check_dev(val, dev, "values");
+  FDX_CHECK(indptr.scalar_type() == at::kLong && idx.scalar_type() == at::kInt, "indptr i64 / indices i32");
+  FDX_CHECK(val.scalar_type() == at::kFloat || val.scalar_type() == at::kDouble, "values f32|f64");
+  FDX_CHECK(idx.numel() == val.numel(), "indices/values size mismatch");
+  FDX_CHECK(indptr.numel() >= 1, "indptr needs rows+1 entries");
+}
+
+template <class V>
+void score_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& val, const optional<Tensor>& lr_w, double lr_b,
+                 const optional<std::vector<Tensor>>& trees, int64_t K, bool cmp_less, const Tensor& out,
+                 int64_t threads) {
+  const auto dev = indptr.device();
+  fdx::CsrArgs<V> a{};
+  a.indptr = indptr.data_ptr<int64_t>();
+  a.idx = idx.data_ptr<int32_t>();
+  a.val = val.data_ptr<V>();
+  a.rows = indptr.numel() - 1;
+  a.lr_w = cptr<double>(lr_w);
+  a.lr_b = lr_b;
+  a.trees = make_trees(trees, K, dev);
+  a.cmp_less = cmp_less;
+  a.out = out.data_ptr<double>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_score_csr<V>(a, stream_of(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::score_csr_cpu<V>(a, (int)threads);
+  }
+}
+
+void score_csr(const Tensor& indptr, const Tensor& idx, const Tensor& val, const optional<Tensor>& lr_w, double lr_b,
+               const optional<std::vector<Tensor>>& trees, int64_t K, bool cmp_less, const Tensor& out,
+               int64_t threads) {
+  const auto dev = indptr.device();
+  check_csr(indptr, idx, val, dev);
+  check_dev(out, dev, "out");
+  FDX_CHECK(out.scalar_type() == at::kDouble, "out must be float64");
+  const int64_t rows = indptr.numel() - 1;
+  FDX_CHECK(lr_w.has_value() != (trees.has_value() && !trees->empty()), "exactly one scorer (lr_w or trees)");
+  if (lr_w) {
+    check_dev(*lr_w, dev, "lr_w");
+    FDX_CHECK(lr_w->scalar_type() == at::kDouble, "lr_w must be float64");
+    FDX_CHECK(out.numel() >= rows, "out too small");
+  } else {
+    FDX_CHECK(K >= 1 && K <= 2 && out.numel() >= rows * K, "out too small for K");
+  }
+  if (val.scalar_type() == at::kFloat)
+    score_csr_t<float>(indptr, idx, val, lr_w, lr_b, trees, K, cmp_less, out, threads);
+  else
+    score_csr_t<double>(indptr, idx, val, lr_w, lr_b, trees, K, cmp_less, out, threads);
+}
+
+void spmv(const Tensor& indptr, const Tensor& idx, const Tensor& val, const Tensor& x, const Tensor& y,
+          int64_t threads) {
+  const auto dev = indptr.device();
+  check_csr(indptr, idx, val, dev);
+  check_dev(x, dev, "x");
+  check_dev(y, dev, "y");
+  FDX_CHECK(x.scalar_type() == at::kDouble && y.scalar_type() == at::kDouble, "x/y float64");
+  const int64_t rows = indptr.numel() - 1;
+  FDX_CHECK(y.numel() >= rows, "y too small");
+  auto run = [&](auto* vp) {
+    using V = std::remove_const_t<std::remove_pointer_t<decltype(vp)>>;
+    if (dev.is_cuda()) {
+      c10::hip::HIPGuard guard(dev.index());
+      fdx::launch_spmv<V>(indptr.data_ptr<int64_t>(), idx.data_ptr<int32_t>(), val.data_ptr<V>(),
+                          x.data_ptr<double>(), y.data_ptr<double>(), rows, stream_of(dev));
+      C10_HIP_KERNEL_LAUNCH_CHECK();
+    } else {
+      fdx::spmv_cpu<V>(indptr.data_ptr<int64_t>(), idx.data_ptr<int32_t>(), val.data_ptr<V>(),
+                       x.data_ptr<double>(), y.data_ptr<double>(), rows, (int)threads);
+    }
+  };
+  if (val.scalar_type() == at::kFloat) run((float*)nullptr); else run((double*)nullptr);
+}
+
+void spmv_t(const Tensor& indptr, const Tensor& idx, const Tensor& val, const Tensor& r, const Tensor& g,
+            int64_t threads) {
+  const auto dev = indptr.device();
+  check_csr(indptr, idx, val, dev);
+  check_dev(r, dev, "r");
+  check_dev(g, dev, "g");
+  FDX_CHECK(r.scalar_type() == at::kDouble && g.scalar_type() == at::kDouble, "r/g float64");
+  const int64_t rows = indptr.numel() - 1;
+  FDX_CHECK(r.numel() >= rows, "r too small");
+  auto run = [&](auto* vp) {
+    using V = std::remove_const_t<std::remove_pointer_t<decltype(vp)>>;
+    if (dev.is_cuda()) {
+      c10::hip::HIPGuard guard(dev.index());
+      fdx::launch_spmv_t<V>(indptr.data_ptr<int64_t>(), idx.data_ptr<int32_t>(), val.data_ptr<V>(),
+                            r.data_ptr<double>(), g.data_ptr<double>(), rows, stream_of(dev));
+      C10_HIP_KERNEL_LAUNCH_CHECK();
+    } else {
+      fdx::spmv_t_cpu<V>(indptr.data_ptr<int64_t>(), idx.data_ptr<int32_t>(), val.data_ptr<V>(),
+                         r.data_ptr<double>(), g.data_ptr<double>(), rows, g.numel(), (int)threads);
+    }
+  };
+  if (val.scalar_type() == at::kFloat) run((float*)nullptr); else run((double*)nullptr);
+}
+
+void doc_freq(const Tensor& idx, const Tensor& val, const Tensor& df) {
+  const auto dev = idx.device();
+  check_dev(idx, dev, "indices");
+  check_dev(val, dev, "values");
+  check_dev(df, dev, "df");
+  FDX_CHECK(dev.is_cuda(), "doc_freq is a device kernel (host path uses torch.bincount)");
+  FDX_CHECK(idx.scalar_type() == at::kInt && df.scalar_type() == at::kLong, "indices i32 / df i64");
+  c10::hip::HIPGuard guard(dev.index());
+  if (val.scalar_type() == at::kFloat)
+    fdx::launch_doc_freq<float>(idx.data_ptr<int32_t>(), val.data_ptr<float>(), idx.numel(), df.data_ptr<int64_t>(), stream_of(dev));
+  else
+    fdx::launch_doc_freq<double>(idx.data_ptr<int32_t>(), val.data_ptr<double>(), idx.numel(), df.data_ptr<int64_t>(), stream_of(dev));
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X-native core of fraud_detection_spark_kafka_llm_amd";
+  m.def("featurize_score", &featurize_score, "Fused clean/tokenize/stopword/hash/idf/score");
+  m.def("score_csr", &score_csr, "LR / tree-ensemble scoring of a CSR feature matrix");
+  m.def("spmv", &spmv, "y = X x (CSR, fp64 accumulate)");
+  m.def("spmv_t", &spmv_t, "g += X^T r (CSR, fp64)");
+  m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
+  m.attr("gfx_arch") = "gfx950";
+}

@@ -1,0 +1,58 @@
+"""Sparse ops over ``VectorColumn`` CSR data (native: ``csrc/sparse_kernels.hip`` / ``sparse_cpu.cpp``)."""
+from __future__ import annotations
+
+import torch
+
+from . import native
+from .text import LinearScorer, TreeArrays
+
+
+def _csr(vc):
+    indptr, idx, val = vc.csr()
+    if val.dtype not in (torch.float32, torch.float64):
+        val = val.to(torch.float64)
+    return indptr.contiguous(), idx.to(torch.int32).contiguous(), val.contiguous()
+
+
+def score_csr(vc, scorer, threads: int = 0) -> torch.Tensor:
+    """Raw scores ``[N, K]`` fp64: LR margin (K=1) or tree-ensemble sums (K = leaf width)."""
+    indptr, idx, val = _csr(vc)
+    dev = indptr.device
+    n = indptr.numel() - 1
+    C = native.lib()
+    if isinstance(scorer, LinearScorer):
+        if scorer.w.size > vc.size:
+            raise ValueError("coefficient vector longer than the feature space")
+        out = torch.empty((n, 1), dtype=torch.float64, device=dev)
+        w = scorer.weights(dev)
+        if w.numel() < vc.size:   # features beyond the model's width contribute nothing
+            w = torch.cat([w, torch.zeros(vc.size - w.numel(), dtype=torch.float64, device=dev)])
+        C.score_csr(indptr, idx, val, w, scorer.b, None, 1, False, out, threads)
+        return out
+    if isinstance(scorer, TreeArrays):
+        if scorer.max_feature() >= vc.size:
+            raise ValueError("tree references a feature beyond the feature space")
+        out = torch.empty((n, scorer.K), dtype=torch.float64, device=dev)
+        C.score_csr(indptr, idx, val, None, 0.0, scorer.tensors(dev), scorer.K, scorer.cmp_less, out, threads)
+        return out
+    raise TypeError(f"unknown scorer {type(scorer)}")
+
+
+def spmv(indptr, idx, val, x: torch.Tensor, threads: int = 0) -> torch.Tensor:
+    y = torch.empty(indptr.numel() - 1, dtype=torch.float64, device=indptr.device)
+    native.lib().spmv(indptr, idx, val, x, y, threads)
+    return y
+
+
+def spmv_t(indptr, idx, val, r: torch.Tensor, cols: int, threads: int = 0) -> torch.Tensor:
+    g = torch.zeros(cols, dtype=torch.float64, device=indptr.device)
+    native.lib().spmv_t(indptr, idx, val, r, g, threads)
+    return g
+
+
+def doc_freq(idx: torch.Tensor, val: torch.Tensor, size: int) -> torch.Tensor:
+    if idx.is_cuda:
+        df = torch.zeros(size, dtype=torch.int64, device=idx.device)
+        native.lib().doc_freq(idx.to(torch.int32).contiguous(), val.contiguous(), df)
+        return df
+    return torch.bincount(idx[val != 0].to(torch.int64), minlength=size)

@@ -1,0 +1,108 @@
+"""Typed runtime configuration.
+
+Defaults equal the reference's hard-coded values; every field can be overridden from the
+environment (``FDX_*``), a YAML file, or CLI flags (``add_cli_args``/``from_cli``). The Kafka and
+LLM environment variables of the reference (``KAFKA_*``, ``DEEPSEEK_API_KEY``) are read unchanged
+by the drop-in modules under ``utils/``.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+
+@dataclass
+class Config:
+    device: str = ""                      # "" -> cuda:LOCAL_RANK if available else cpu
+    world_size: int = 1
+    num_features: int = 1 << 18           # HashingTF default
+    vocab_size: int = 20000               # fraud_detection_spark.py:52
+    max_depth: int = 5                    # fraud_detection_spark.py:62,71,81
+    num_trees: int = 100                  # fraud_detection_spark.py:70,82
+    max_bins: int = 32                    # Spark DecisionTree default
+    gbdt_max_bin: int = 64
+    seed: int = 42                        # fraud_detection_spark.py:72,338-339
+    deterministic: bool = False
+    llm_backend: str = "deepseek"         # deepseek | openai | stub
+    llm_base_url: str = "https://api.deepseek.com/v1"   # agent_api.py:36
+    llm_model: str = "deepseek-chat"      # agent_api.py:35
+    llm_timeout: float = 90.0             # agent_api.py:42
+    llm_max_tokens: int = 1000            # agent_api.py:62
+    stream_batch: int = 4096
+    stream_max_latency_ms: float = 5.0
+    profile: bool = False
+    extra: dict = field(default_factory=dict)
+
+    @classmethod
+    def from_env(cls) -> "Config":
+        c = cls()
+        for f in dataclasses.fields(cls):
+            key = "FDX_" + f.name.upper()
+            if key in os.environ and f.name != "extra":
+                setattr(c, f.name, _coerce(f.type, os.environ[key]))
+        return c
+
+    @classmethod
+    def from_yaml(cls, path: str) -> "Config":
+        import yaml
+
+        with open(path) as fh:
+            data = yaml.safe_load(fh) or {}
+        c = cls.from_env()
+        for k, v in data.items():
+            if hasattr(c, k):
+                setattr(c, k, v)
+            else:
+                c.extra[k] = v
+        return c
+
+    @staticmethod
+    def add_cli_args(ap: argparse.ArgumentParser) -> None:
+        for f in dataclasses.fields(Config):
+            if f.name == "extra":
+                continue
+            flag = "--" + f.name.replace("_", "-")
+            if f.type in ("bool", bool):
+                ap.add_argument(flag, action="store_true", default=None)
+            else:
+                ap.add_argument(flag, default=None)
+
+    @classmethod
+    def from_cli(cls, ns: argparse.Namespace, base: Optional["Config"] = None) -> "Config":
+        c = base or cls.from_env()
+        for f in dataclasses.fields(cls):
+            v = getattr(ns, f.name, None)
+            if v is not None and f.name != "extra":
+                setattr(c, f.name, _coerce(f.type, v))
+        return c
+
+    def torch_device(self) -> torch.device:
+        if self.device:
+            return torch.device(self.device)
+        return default_device()
+
+
+def _coerce(typ, v):
+    t = typ if isinstance(typ, str) else getattr(typ, "__name__", str(typ))
+    if isinstance(v, str):
+        if t == "bool":
+            return v.lower() in ("1", "true", "yes", "on")
+        if t == "int":
+            return int(v)
+        if t == "float":
+            return float(v)
+    return v
+
+
+def default_device() -> torch.device:
+    env = os.environ.get("FDX_DEVICE")
+    if env:
+        return torch.device(env)
+    if torch.cuda.is_available():
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+    return torch.device("cpu")
