@@ -1,0 +1,84 @@
+"""GBDT training benchmark on synthetic dialogues (HashingTF(2^18) -> IDF -> GBDT) on one GPU.
+
+Phases timed separately: corpus generation (on device), fused featurization, IDF fit, quantize
++ CSC build, boosting rounds. Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from fraud_detection_spark_kafka_llm_amd.data import synth
+from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH
+from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+from fraud_detection_spark_kafka_llm_amd.ops import text as T
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import doc_freq
+from fraud_detection_spark_kafka_llm_amd.utils import tracing
+
+
+def build_features(rows: int, dev, chunk: int = 500_000, num_features: int = 1 << 18, seed: int = 11):
+    spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=num_features)
+    ptrs, idxs, vals, labels = [], [], [], []
+    t_gen = t_feat = 0.0
+    off = 0
+    for start in range(0, rows, chunk):
+        n = min(chunk, rows - start)
+        t0 = time.perf_counter()
+        pt, y = synth.generate(synth.SynthConfig(n=n, seed=seed), device=dev, start=start)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        res = T.featurize_score(pt, spec, want_csr=True, device=dev)
+        ip, ix, v = res.csr()
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        t_gen += t1 - t0
+        t_feat += t2 - t1
+        ptrs.append(ip[1:] + off)
+        off += int(ip[-1])
+        idxs.append(ix)
+        vals.append(v)
+        labels.append(y)
+        del pt, res
+    indptr = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev)] + ptrs)
+    idx = torch.cat(idxs)
+    counts = torch.cat(vals)
+    y = torch.cat(labels)
+    return indptr, idx, counts, y, t_gen, t_feat
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--trees", type=int, default=20)
+    ap.add_argument("--depth", type=int, default=6)
+    ap.add_argument("--trace", default="")
+    args = ap.parse_args()
+    if args.trace:
+        tracing.enable(args.trace)
+    dev = torch.device("cuda:0")
+    t0 = time.perf_counter()
+    indptr, idx, counts, y, t_gen, t_feat = build_features(args.rows, dev)
+    t1 = time.perf_counter()
+    F = 1 << 18
+    df = doc_freq(idx, counts, F)
+    idf = torch.log((args.rows + 1.0) / (df.double() + 1.0))
+    vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
+    vc.tf_counts, vc.tf_scale = counts, idf
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)
+    t3 = time.perf_counter()
+    print(json.dumps({"rows": args.rows, "nnz": int(idx.numel()), "trees": args.trees, "depth": args.depth,
+                      "gen_s": t_gen, "featurize_s": t_feat, "idf_s": t2 - t1, "gbdt_total_s": res.train_seconds,
+                      "per_tree_ms": (t3 - t2) / args.trees * 1e3, "wall_s": t3 - t0,
+                      "nodes_tree0": res.trees[0].num_nodes}))
+
+
+if __name__ == "__main__":
+    main()

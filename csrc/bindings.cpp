@@ -263,8 +263,11 @@ void doc_freq(const Tensor& idx, const Tensor& val, const Tensor& df) {
 
 }  // namespace
 
+void register_tree_ops(pybind11::module& m);
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native core of fraud_detection_spark_kafka_llm_amd";
+  register_tree_ops(m);
   m.def("featurize_score", &featurize_score, "Fused clean/tokenize/stopword/hash/idf/score");
   m.def("score_csr", &score_csr, "LR / tree-ensemble scoring of a CSR feature matrix");
   m.def("spmv", &spmv, "y = X x (CSR, fp64 accumulate)");

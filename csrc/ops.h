@@ -33,6 +33,31 @@ template <class V> void launch_spmv_t(const int64_t* indptr, const int32_t* idx,
 template <class V> void launch_doc_freq(const int32_t* idx, const V* val, int64_t nnz, int64_t* df,
                                        hipStream_t stream);
 
+// ---------------------------------------------------------------- tree engine (tree_kernels.hip / tree_cpu.cpp)
+struct RowStateArgs;
+struct HistArgs;
+struct HistReduceArgs;
+struct SplitArgs;
+struct PartitionArgs;
+void launch_rowstate(const RowStateArgs& a, hipStream_t s);
+void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s);
+void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s);
+void launch_hist_subtract(const double* parent, double* cur, const int32_t* dst, const int32_t* par,
+                          const int32_t* sib, int32_t n_pairs, int64_t TB, hipStream_t s);
+void launch_split(const SplitArgs& a, hipStream_t s);
+void launch_partition(const PartitionArgs& a, hipStream_t s);
+void launch_logistic_grad(const double* margin, const float* label, const float* weight, float* g, float* h,
+                          int64_t N, hipStream_t s);
+void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s);
+void rowstate_cpu(const RowStateArgs& a);
+void hist_cpu(const HistArgs& h, const HistReduceArgs& r, int slots);
+void hist_subtract_cpu(const double* parent, double* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
+                       int32_t n_pairs, int64_t TB);
+void split_cpu(const SplitArgs& a);
+void partition_cpu(const PartitionArgs& a);
+void logistic_grad_cpu(const double* margin, const float* label, const float* weight, float* g, float* h, int64_t N);
+void leaf_update_cpu(double* margin, const int32_t* row_node, const double* node_value, int64_t N);
+
 template <class V> void score_csr_cpu(const CsrArgs<V>& a, int threads);
 template <class V> void spmv_cpu(const int64_t* indptr, const int32_t* idx, const V* val, const double* x, double* y,
                                  int64_t rows, int threads);

@@ -135,12 +135,17 @@ def generate(cfg: SynthConfig = SynthConfig(), device="cpu", start: int = 0) -> 
     base_b = base_s + V.n_scam
     # Zipf-ish choice inside each lexicon: floor(len * pick^2)
     zc = (pick * pick * V.n_common).to(torch.int64).clamp_max(V.n_common - 1)
-    zs = (pick * V.n_scam).to(torch.int64).clamp_max(V.n_scam - 1)
-    zb = (pick * V.n_benign).to(torch.int64).clamp_max(V.n_benign - 1)
+    # own-class cue words are Zipfian (a few dominant cues, like the reference's top features);
+    # cross-class noise is uniform so the dominant cues stay discriminative
+    p3 = pick.pow(3)
+    zs = (p3 * V.n_scam).to(torch.int64).clamp_max(V.n_scam - 1)
+    zb = (p3 * V.n_benign).to(torch.int64).clamp_max(V.n_benign - 1)
+    us = (pick * V.n_scam).to(torch.int64).clamp_max(V.n_scam - 1)
+    ub = (pick * V.n_benign).to(torch.int64).clamp_max(V.n_benign - 1)
     base_t = base_b + V.n_benign
-    zt = (pick.pow(3) * V.n_tail).to(torch.int64).clamp_max(V.n_tail - 1)
+    zt = (p3 * V.n_tail).to(torch.int64).clamp_max(V.n_tail - 1)
     own = torch.where(is_scam, base_s + zs, base_b + zb)
-    other = torch.where(is_scam, base_b + zb, base_s + zs)
+    other = torch.where(is_scam, base_b + ub, base_s + us)
     word = torch.where(u < p_cls, own, torch.where(u < p_cls + p_oth, other,
                        torch.where(u > 1.0 - cfg.p_tail, base_t + zt, base_c + zc)))
     tag_here = (pos % cfg.turn_len) == 0

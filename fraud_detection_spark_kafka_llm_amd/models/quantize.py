@@ -1,0 +1,269 @@
+"""Feature binning + quantized CSC layout for the histogram tree engine (K-09, X-09/X-13).
+
+Two binning paths:
+
+* **count path** — HashingTF/CountVectorizer features (optionally IDF-scaled: value = tf * s_f with
+  s_f > 0) are binned by the integer term count: bin = min(tf, max_bins - 1), the zero bin is 0.
+  Because v = tf * s_f is monotone in tf, these bins give exactly the split candidates Spark's
+  ``findSplitsForContinuousFeature`` produces for TF-IDF data (midpoints between consecutive
+  distinct values) as long as a feature has < max_bins distinct counts; no sort is needed.
+* **generic path** — arbitrary float features: distinct (feature, value) pairs via a sort; a
+  feature with < max_bins distinct values gets one bin per value, otherwise equal-count groups.
+  Values are keyed at float32 precision (XGBoost bins at float32 as well).
+
+In both paths the thresholds are value-space midpoints, so the same tree scores raw feature
+values with either ``x <= t`` (Spark) or ``x < t`` (XGBoost) semantics. Under data parallelism
+the per-rank statistics (max counts / distinct values) are merged with collectives so every rank
+holds identical bins.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+
+CHUNK = 16384          # entries per histogram work item (one wavefront)
+
+
+@dataclass
+class BinGroup:
+    """Work items of the features whose bin count fits ``32 * bt`` (one MFMA template)."""
+    bt: int
+    item_start: torch.Tensor     # int64 [I]
+    item_end: torch.Tensor       # int64 [I]
+    item_feat: torch.Tensor      # int32 [I]
+    feat: torch.Tensor           # int32 [L]
+    feat_item0: torch.Tensor     # int64 [L]
+    feat_nitems: torch.Tensor    # int32 [L]
+
+    def subset(self, feat_mask: torch.Tensor) -> "BinGroup":
+        """Restrict to features with ``feat_mask[fid]`` (RF per-level feature union)."""
+        keep_items = feat_mask[self.item_feat.to(torch.int64)]
+        keep_feat = feat_mask[self.feat.to(torch.int64)]
+        item_start, item_end = self.item_start[keep_items], self.item_end[keep_items]
+        item_feat = self.item_feat[keep_items]
+        feat = self.feat[keep_feat]
+        nitems = self.feat_nitems[keep_feat]
+        item0 = torch.zeros_like(nitems, dtype=torch.int64)
+        if nitems.numel():
+            item0[1:] = torch.cumsum(nitems.to(torch.int64), 0)[:-1]
+        return BinGroup(self.bt, item_start, item_end, item_feat, feat, item0, nitems)
+
+    @property
+    def num_items(self) -> int:
+        return int(self.item_start.numel())
+
+
+@dataclass
+class Quantized:
+    n_rows: int
+    num_features: int
+    fid_orig: torch.Tensor       # int64 [Fa]
+    nbins: torch.Tensor          # int32 [Fa]
+    zbin: torch.Tensor           # int32 [Fa]
+    boff: torch.Tensor           # int64 [Fa+1]
+    thresholds: np.ndarray       # float64 [TB]: split "bin <= b goes left" <=> "x <= thresholds[boff+b]"
+    colptr: torch.Tensor         # int64 [Fa+1]
+    csc_row: torch.Tensor        # int32 [nnz]
+    csc_bin: torch.Tensor        # uint8 [nnz]
+    groups: list = field(default_factory=list)
+    boff_host: np.ndarray = None
+    zbin_host: np.ndarray = None
+    fid_host: np.ndarray = None
+
+    @property
+    def Fa(self) -> int:  # noqa: N802
+        return int(self.nbins.numel())
+
+    @property
+    def TB(self) -> int:  # noqa: N802
+        return int(self.boff_host[-1])
+
+    @property
+    def device(self) -> torch.device:
+        return self.csc_row.device
+
+    def threshold(self, fid: int, b: int) -> float:
+        return float(self.thresholds[int(self.boff_host[fid]) + int(b)])
+
+
+def _ordered_f32_bits(v: torch.Tensor) -> torch.Tensor:
+    b = v.to(torch.float32).view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    neg = (b >> 31) == 1
+    return torch.where(neg, b ^ 0xFFFFFFFF, b | 0x80000000)
+
+
+def _decode_f32_bits(k: torch.Tensor) -> torch.Tensor:
+    neg = (k >> 31) == 0
+    b = torch.where(neg, k ^ 0xFFFFFFFF, k & 0x7FFFFFFF)
+    b = torch.where(b >= (1 << 31), b - (1 << 32), b).to(torch.int32)
+    return b.view(torch.float32).to(torch.float64)
+
+
+def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
+             all_reduce_max: Optional[Callable] = None, all_gather: Optional[Callable] = None,
+             chunk: int = CHUNK) -> Quantized:
+    """Bin a ``VectorColumn`` and build the CSC. ``counts``/``scale`` select the count path
+    (per-entry integer counts and per-feature positive scale); integral non-negative values
+    take it automatically with scale 1."""
+    if max_bins < 2 or max_bins > 64:
+        raise ValueError("max_bins must be in [2, 64] (bins are held in one or two 32-row MFMA tiles)")
+    indptr, idx, val = vc.csr()
+    dev = indptr.device
+    N = int(indptr.numel() - 1)
+    F = int(vc.size)
+    idx64 = idx.to(torch.int64)
+    val64 = val.to(torch.float64)
+    if counts is None and val64.numel() and bool(torch.all(val64 >= 0)) and bool(torch.all(val64 == torch.round(val64))) \
+            and float(val64.max()) < 65536:
+        counts = val64
+        scale = torch.ones(F, dtype=torch.float64, device=dev)
+    row = torch.repeat_interleave(torch.arange(N, device=dev, dtype=torch.int32), (indptr[1:] - indptr[:-1]),
+                                  output_size=int(idx.numel()))
+    if counts is not None:
+        q = _count_path(idx64, counts.to(torch.float64), scale.to(device=dev, dtype=torch.float64), F, max_bins,
+                        all_reduce_max)
+    else:
+        q = _generic_path(idx64, val64, F, max_bins, all_gather)
+    remap, nbins, zbin, thresholds, entry_bin, keep = q
+    fid = remap[idx64]
+    keep = keep & (fid >= 0)
+    fid, row, entry_bin = fid[keep], row[keep], entry_bin[keep]
+    Fa = int(nbins.numel())
+    order = torch.sort(fid.to(torch.int32), stable=True).indices
+    csc_row = row[order].contiguous()
+    csc_bin = entry_bin[order].to(torch.uint8).contiguous()
+    cnt = torch.bincount(fid, minlength=Fa)
+    colptr = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt, 0, out=colptr[1:])
+    boff = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nbins.to(torch.int64), 0, out=boff[1:])
+    fid_orig = torch.nonzero(remap >= 0).flatten()
+    Q = Quantized(N, F, fid_orig, nbins.to(torch.int32).contiguous(), zbin.to(torch.int32).contiguous(), boff,
+                  thresholds, colptr, csc_row, csc_bin)
+    Q.boff_host = boff.cpu().numpy()
+    Q.zbin_host = Q.zbin.cpu().numpy()
+    Q.fid_host = fid_orig.cpu().numpy()
+    Q.groups = _make_groups(colptr, nbins, chunk)
+    return Q
+
+
+def _count_path(idx, counts, scale, F, max_bins, all_reduce_max):
+    dev = idx.device
+    keep = counts > 0
+    b = torch.clamp(counts, max=max_bins - 1).to(torch.int64)
+    maxb = torch.zeros(F, dtype=torch.int64, device=dev)
+    maxb.scatter_reduce_(0, idx[keep], b[keep], reduce="amax")
+    maxb = torch.where(scale > 0, maxb, torch.zeros_like(maxb))
+    if all_reduce_max is not None:
+        maxb = all_reduce_max(maxb)
+    active = maxb > 0
+    remap = torch.full((F,), -1, dtype=torch.int64, device=dev)
+    Fa = int(active.sum())
+    remap[active] = torch.arange(Fa, device=dev)
+    nbins = (maxb[active] + 1).to(torch.int32)
+    zbin = torch.zeros(Fa, dtype=torch.int32, device=dev)
+    # thresholds: after bin k (count k) -> (k + 0.5) * s_f
+    nb = nbins.to(torch.int64)
+    TB = int(nb.sum())
+    f_of_bin = torch.repeat_interleave(torch.arange(Fa, device=dev), nb, output_size=TB)
+    start = torch.cumsum(nb, 0) - nb
+    k = torch.arange(TB, device=dev) - start[f_of_bin]
+    s = scale[active][f_of_bin]
+    thresholds = ((k.to(torch.float64) + 0.5) * s).cpu().numpy()
+    return remap, nbins, zbin, thresholds, b, keep
+
+
+def _generic_path(idx, val, F, max_bins, all_gather):
+    dev = idx.device
+    keep = val != 0
+    keys = (idx[keep] << 32) | _ordered_f32_bits(val[keep])
+    uk, inv, cnt = torch.unique(keys, return_inverse=True, return_counts=True)
+    if all_gather is not None:
+        allk, allc = all_gather(uk, cnt)
+        gk, ginv = torch.unique(allk, return_inverse=True)
+        gc = torch.zeros(gk.numel(), dtype=torch.int64, device=dev).index_add_(0, ginv, allc)
+        local_to_global = torch.searchsorted(gk, uk)
+        inv = local_to_global[inv]
+        uk, cnt = gk, gc
+    ufeat = uk >> 32
+    uval = _decode_f32_bits(uk & 0xFFFFFFFF)
+    U = uk.numel()
+    # per-feature segments of the sorted distinct keys
+    fcnt = torch.bincount(ufeat, minlength=F)
+    active = fcnt > 0
+    remap = torch.full((F,), -1, dtype=torch.int64, device=dev)
+    Fa = int(active.sum())
+    remap[active] = torch.arange(Fa, device=dev)
+    seg = remap[ufeat]
+    nd = fcnt[active]                                          # distinct nonzero values per feature
+    seg_start = torch.cumsum(nd, 0) - nd
+    rank = torch.arange(U, device=dev) - seg_start[seg]
+    # equal-count grouping for features with too many distinct values
+    ccum = torch.cumsum(cnt, 0)
+    seg_tot = torch.zeros(Fa, dtype=torch.int64, device=dev).index_add_(0, seg, cnt)
+    seg_cstart = torch.zeros(Fa, dtype=torch.int64, device=dev)
+    seg_cstart[1:] = torch.cumsum(seg_tot, 0)[:-1]
+    before = ccum - cnt - seg_cstart[seg]
+    slots = max_bins - 1
+    grp = torch.where(nd[seg] <= slots, rank,
+                      (before.to(torch.float64) * slots / seg_tot[seg].to(torch.float64)).to(torch.int64))
+    # compact group ids per feature (monotone, may have gaps)
+    key2 = seg * (1 << 20) + grp
+    ug, ginv2 = torch.unique(key2, return_inverse=True)
+    gseg = ug >> 20
+    gcnt = torch.bincount(gseg, minlength=Fa)
+    gstart = torch.cumsum(gcnt, 0) - gcnt
+    grank = torch.arange(ug.numel(), device=dev) - gstart[gseg]
+    # zero bin goes before the first positive group
+    negg = torch.zeros(ug.numel(), dtype=torch.bool, device=dev)
+    gmin = torch.full((ug.numel(),), float("inf"), dtype=torch.float64, device=dev)
+    gmax = torch.full((ug.numel(),), float("-inf"), dtype=torch.float64, device=dev)
+    gmin.scatter_reduce_(0, ginv2, uval, reduce="amin")
+    gmax.scatter_reduce_(0, ginv2, uval, reduce="amax")
+    negg = gmax < 0
+    zb = torch.zeros(Fa, dtype=torch.int64, device=dev).index_add_(0, gseg, negg.to(torch.int64))
+    gbin = grank + torch.where(negg, torch.zeros_like(grank), torch.ones_like(grank))
+    nbins = (gcnt + 1).to(torch.int32)
+    # bin value ranges (with the zero bin) -> midpoint thresholds
+    nb = nbins.to(torch.int64)
+    TB = int(nb.sum())
+    boff = torch.cumsum(nb, 0) - nb
+    bmin = torch.zeros(TB, dtype=torch.float64, device=dev)
+    bmax = torch.zeros(TB, dtype=torch.float64, device=dev)
+    gpos = boff[gseg] + gbin
+    bmin[gpos] = gmin
+    bmax[gpos] = gmax
+    nxt = torch.roll(bmin, -1)
+    thresholds = ((bmax + nxt) / 2.0).cpu().numpy()
+    entry_group = ginv2[inv]
+    entry_bin = gbin[entry_group]
+    full_keep = keep.clone()
+    eb = torch.zeros(idx.numel(), dtype=torch.int64, device=dev)
+    eb[keep] = entry_bin
+    return remap, nbins, zb.to(torch.int32), thresholds, eb, full_keep
+
+
+def _make_groups(colptr: torch.Tensor, nbins: torch.Tensor, chunk: int) -> list:
+    dev = colptr.device
+    n = colptr[1:] - colptr[:-1]
+    nchunks = torch.clamp((n + chunk - 1) // chunk, min=1)
+    groups = []
+    for bt in (1, 2):
+        lo, hi = (0, 32) if bt == 1 else (33, 64)
+        sel = (nbins >= lo) & (nbins <= hi) & (n > 0)
+        feats = torch.nonzero(sel).flatten()
+        if feats.numel() == 0:
+            continue
+        nc = nchunks[feats]
+        I = int(nc.sum())
+        item_feat = torch.repeat_interleave(feats, nc, output_size=I)
+        first = torch.cumsum(nc, 0) - nc
+        k = torch.arange(I, device=dev) - torch.repeat_interleave(first, nc, output_size=I)
+        start = colptr[item_feat] + k * chunk
+        end = torch.minimum(start + chunk, colptr[item_feat + 1])
+        groups.append(BinGroup(bt, start.contiguous(), end.contiguous(), item_feat.to(torch.int32).contiguous(),
+                               feats.to(torch.int32).contiguous(), first.contiguous(), nc.to(torch.int32).contiguous()))
+    return groups

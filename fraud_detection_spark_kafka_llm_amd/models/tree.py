@@ -1,0 +1,95 @@
+"""DecisionTree / RandomForest training on the histogram engine (X-09, X-10, X-12).
+
+Spark semantics reproduced: gini (or entropy) impurity, maxBins=32 candidate
+thresholds, minInstancesPerNode / minInfoGain, a node splits only if its best gain > 0, children
+with zero impurity become leaves, and ``toNode(prune=true)`` merges sibling leaves with the same
+prediction. RandomForest adds Poisson(1) bootstrap row weights (counter-based, regenerated per
+tree, never stored) and per-node feature subsampling (``featureSubsetStrategy="auto"`` = sqrt).
+Reference configs: /root/reference/fraud_detection_spark.py:59-74.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..ml.linalg import VectorColumn
+from ..ml.tree_model import Tree
+from ..parallel.dist import Collectives
+from ..utils.config import default_device
+from ..utils import tracing
+from .grower import GrowParams, Workspace, grow_tree
+from .quantize import quantize
+from .rf_sampling import features_per_node
+
+
+@dataclass
+class ForestResult:
+    trees: list
+    num_features: int
+
+
+def prepare(features, labels, device=None, max_bins: int = 32, coll: Collectives = None):
+    dev = torch.device(device) if device is not None else default_device()
+    vc = features if isinstance(features, VectorColumn) else VectorColumn.from_rows(list(features))
+    vc = vc.to(dev)
+    y = labels
+    if not isinstance(y, torch.Tensor):
+        y = torch.as_tensor(np.asarray([float(v) for v in y], dtype=np.float32))
+    y = y.to(device=dev, dtype=torch.float32).contiguous()
+    if y.numel() != len(vc):
+        raise ValueError("labels and features have different row counts")
+    coll = coll or Collectives()
+    counts, scale = getattr(vc, "tf_counts", None), getattr(vc, "tf_scale", None)
+    with tracing.span("tree.quantize"):
+        Q = quantize(vc, max_bins=max_bins, counts=counts, scale=scale,
+                     all_reduce_max=coll.max if coll.active else None,
+                     all_gather=coll.gather_keys if coll.active else None)
+    return Q, y, vc.size, vc
+
+
+def prune_same_prediction(t: Tree) -> Tree:
+    """Spark ``LearningNode.toNode(prune = true)``: collapse internal nodes whose two children
+    are leaves with the same prediction (bottom-up)."""
+    feat, left, right = t.feature.copy(), t.left.copy(), t.right.copy()
+    gain = t.gain.copy()
+
+    def rec(i):
+        if feat[i] < 0:
+            return True
+        lleaf, rleaf = rec(left[i]), rec(right[i])
+        if lleaf and rleaf and t.prediction[left[i]] == t.prediction[right[i]]:
+            feat[i], left[i], right[i], gain[i] = -1, -1, -1, -1.0
+            return True
+        return False
+
+    rec(t.root)
+    return Tree(feat, t.threshold, left, right, t.stats, t.impurity, gain, t.raw_count, t.prediction, t.root).compacted()
+
+
+def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bins: int = 32, min_instances: int = 1,
+               min_info_gain: float = 0.0, bootstrap: bool = False, feature_subset: str = "all", seed: int = 0,
+               impurity: str = "gini", subsampling_rate: float = 1.0, device=None, weights=None,
+               prune: bool = True) -> ForestResult:
+    if subsampling_rate != 1.0:
+        raise NotImplementedError("subsamplingRate != 1.0 is not supported (Poisson(1) bootstrap only)")
+    coll = Collectives()
+    Q, y, F, _ = prepare(features, labels, device, max_bins, coll)
+    w = None
+    if weights is not None:
+        w = torch.as_tensor(np.asarray(weights, dtype=np.float32)).to(Q.device)
+    strategy = feature_subset
+    if str(strategy).lower() == "auto":
+        strategy = "all" if num_trees == 1 else "sqrt"
+    k = features_per_node(strategy, F)
+    params = GrowParams(max_depth=max_depth, mode=2 if impurity == "entropy" else 1, min_child=float(min_instances),
+                        min_gain=float(min_info_gain), feat_prob=min(1.0, k / F), seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
+    ws = Workspace(Q, 2 ** max_depth)
+    trees = []
+    for t in range(num_trees):
+        with tracing.span("forest.tree", tree=t):
+            tr = grow_tree(Q, ws, params, t, label=y, weight=w, bootstrap=bootstrap,
+                           all_reduce=coll.sum if coll.active else None)
+        trees.append(prune_same_prediction(tr) if prune else tr.compacted())
+    return ForestResult(trees, F)

@@ -1,0 +1,144 @@
+"""Data-parallel process group helpers (PAR-01..PAR-04, C-01/C-02).
+
+One process per GPU; ``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm, over xGMI
+inside a node) for device tensors, ``gloo`` for CPU-only runs/tests. Collectives used by the
+engine are all *sums/max of statistics* (histograms, docFreq, gradients, root totals) whose
+results are bitwise identical on every rank, so every rank takes the same split decisions and no
+model broadcast is needed during training.
+
+Launch: ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...`` or
+``launch.spawn(fn, world_size)`` for tests.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def world_size() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def local_rank() -> int:
+    return int(os.environ.get("LOCAL_RANK", rank()))
+
+
+def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> bool:
+    """Initialise from torchrun's env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT). Returns True if a
+    multi-process group is active."""
+    if dist.is_initialized():
+        return dist.get_world_size() > 1
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return False
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank() % max(1, torch.cuda.device_count()))
+    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+    return True
+
+
+def backend() -> str:
+    return dist.get_backend() if dist.is_initialized() else "none"
+
+
+def _on_comm_device(t: torch.Tensor):
+    """gloo needs host tensors; nccl device tensors."""
+    if backend() == "gloo" and t.is_cuda:
+        return t.cpu(), True
+    return t, False
+
+
+def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    if not is_dist():
+        return t
+    x, moved = _on_comm_device(t.contiguous())
+    dist.all_reduce(x, op=op)
+    return x.to(t.device) if moved else x
+
+
+def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
+    return all_reduce(t, dist.ReduceOp.SUM)
+
+
+def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
+    return all_reduce(t, dist.ReduceOp.MAX)
+
+
+def all_gather_var(*tensors: torch.Tensor) -> tuple:
+    """All-gather 1-D tensors of different lengths per rank; returns the concatenation."""
+    if not is_dist():
+        return tensors
+    dev = tensors[0].device
+    n = torch.tensor([tensors[0].numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world_size())]
+    n_c, _ = _on_comm_device(n)
+    sizes_c = [s.to(n_c.device) for s in sizes]
+    dist.all_gather(sizes_c, n_c)
+    sizes = [int(s.item()) for s in sizes_c]
+    m = max(sizes)
+    out = []
+    for t in tensors:
+        pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+        pad[: t.numel()] = t
+        p, moved = _on_comm_device(pad)
+        bufs = [torch.empty_like(p) for _ in range(world_size())]
+        dist.all_gather(bufs, p)
+        cat = torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+        out.append(cat.to(t.device) if moved else cat)
+    return tuple(out)
+
+
+def broadcast_object(obj, src: int = 0):
+    if not is_dist():
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src)
+    return lst[0]
+
+
+def barrier() -> None:
+    if is_dist():
+        if backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def shard_range(n: int, r: Optional[int] = None, w: Optional[int] = None) -> tuple:
+    """Contiguous row shard [lo, hi) of ``n`` rows for rank ``r`` of ``w``."""
+    r = rank() if r is None else r
+    w = world_size() if w is None else w
+    base, extra = divmod(n, w)
+    lo = r * base + min(r, extra)
+    return lo, lo + base + (1 if r < extra else 0)
+
+
+class Collectives:
+    """Bundle of the collectives the trainers need (no-ops when not distributed)."""
+
+    def __init__(self):
+        self.active = is_dist()
+
+    def sum(self, t):
+        return all_reduce_sum(t) if self.active else t
+
+    def max(self, t):
+        return all_reduce_max(t) if self.active else t
+
+    def gather_keys(self, keys, counts):
+        return all_gather_var(keys, counts) if self.active else (keys, counts)

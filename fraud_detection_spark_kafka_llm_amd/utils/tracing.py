@@ -1,0 +1,65 @@
+"""Tracing spans.
+
+``span(name)`` marks a region with a ROCm ``roctx`` range when the roctx library is loadable (so
+rocprofv3 ``--marker-trace`` shows the framework phases next to the kernels) and, when
+``FDX_TRACE=<path>`` is set, appends one JSON line per span with wall-clock start/duration.
+Spans nest. When neither sink is active a span costs one attribute lookup.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import json
+import os
+import threading
+import time
+
+_roctx = None
+_trace_path = os.environ.get("FDX_TRACE")
+_lock = threading.Lock()
+_depth = threading.local()
+
+
+def _load_roctx():
+    global _roctx
+    if _roctx is not None:
+        return _roctx
+    _roctx = False
+    if os.environ.get("FDX_ROCTX", "1") == "0":
+        return _roctx
+    for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so", "librocprofiler-sdk-roctx.so",
+                 "/opt/rocm/lib/librocprofiler-sdk-roctx.so"):
+        try:
+            lib = ctypes.CDLL(name)
+            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+            _roctx = lib
+            break
+        except OSError:
+            continue
+    return _roctx
+
+
+def enable(path: str) -> None:
+    global _trace_path
+    _trace_path = path
+
+
+@contextlib.contextmanager
+def span(name: str, **attrs):
+    rt = _load_roctx() if os.environ.get("FDX_ROCTX") == "1" else None
+    if rt:
+        rt.roctxRangePushA(name.encode())
+    t0 = time.perf_counter()
+    d = getattr(_depth, "v", 0)
+    _depth.v = d + 1
+    try:
+        yield
+    finally:
+        _depth.v = d
+        dt = time.perf_counter() - t0
+        if rt:
+            rt.roctxRangePop()
+        if _trace_path:
+            rec = {"name": name, "t": t0, "dur_ms": dt * 1e3, "depth": d, "pid": os.getpid(), **attrs}
+            with _lock, open(_trace_path, "a") as fh:
+                fh.write(json.dumps(rec) + "\n")
