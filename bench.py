@@ -1,0 +1,200 @@
+"""Headline benchmark (BASELINE.json): "dialogues/sec streaming inference + GBDT train sec on 10M rows,
+1/2/4/8 GPU".
+
+Per rank (one process per MI355X, RCCL over xGMI when N > 1):
+  1. GBDT training — HashingTF(2^18) -> IDF -> GBDT (100 trees, depth 6, XGBoost binary:logistic)
+     on 10M synthetic dialogues row-sharded across the N ranks: on-device corpus generation,
+     fused featurization, all-reduced docFreq/IDF, quantization and boosting with per-level
+     histogram all-reduce. Wall time (max over ranks) is reported as ``gbdt_train_sec``.
+  2. Streaming inference (the timed K steps) — every step each rank takes one micro-batch of
+     raw UTF-8 dialogues from a pinned host ring, copies it to HBM, runs the fused
+     clean/tokenize/stop-word/murmur3/IDF/100-tree-GBDT kernel and copies the scores back; H2D,
+     kernel and D2H of consecutive steps overlap on three HIP streams. ``value`` = dialogues/s
+     summed over all ranks (weak scaling: fixed micro-batch per GPU).
+Data is synthetic (the reference dataset is not available) with random-init-free trained trees;
+compute dtype: fp64 scores / fp32-accumulated bf16-MFMA histograms (text is bytes).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1 is launched by the driver via torch.distributed.run (RANK/WORLD_SIZE/MASTER_* in env).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from fraud_detection_spark_kafka_llm_amd.data import synth  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ml.xgboost import SparkXGBClassifierModel  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops import text as T  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import doc_freq  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.parallel import dist as D  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing  # noqa: E402
+
+METRIC = "dialogues/sec streaming inference + GBDT train sec on 10M rows, 1/2/4/8 GPU"
+F = 1 << 18
+
+
+def sync_all(dev):
+    torch.cuda.synchronize(dev)
+    D.barrier()
+    torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(x: float, dev) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    return float(D.all_reduce_max(t).item())
+
+
+def featurize_shard(lo: int, hi: int, dev, spec, seed: int, chunk: int = 500_000):
+    ptrs, idxs, vals, labels = [], [], [], []
+    off = 0
+    for start in range(lo, hi, chunk):
+        n = min(chunk, hi - start)
+        pt, y = synth.generate(synth.SynthConfig(n=n, seed=seed), device=dev, start=start)
+        res = T.featurize_score(pt, spec, want_csr=True, device=dev)
+        ip, ix, v = res.csr()
+        ptrs.append(ip[1:] + off)
+        off += int(ip[-1])
+        idxs.append(ix)
+        vals.append(v)
+        labels.append(y)
+        del pt, res
+    indptr = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev)] + ptrs)
+    return indptr, torch.cat(idxs), torch.cat(vals), torch.cat(labels)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=10_000_000, help="GBDT training rows (total over ranks)")
+    ap.add_argument("--trees", type=int, default=100)
+    ap.add_argument("--depth", type=int, default=6)
+    ap.add_argument("--batch", type=int, default=65536, help="dialogues per GPU per streaming step")
+    ap.add_argument("--pool", type=int, default=6, help="distinct pinned micro-batches per GPU")
+    ap.add_argument("--depth-pipeline", type=int, default=2)
+    args = ap.parse_args()
+
+    D.init_from_env("nccl")
+    rank, world = D.rank(), D.world_size()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    dev = torch.device("cuda", D.local_rank() % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=F)
+
+    # ------------------------------------------------------------------ 1. GBDT training
+    sync_all(dev)
+    t0 = time.perf_counter()
+    lo, hi = D.shard_range(args.rows)
+    indptr, idx, counts, y = featurize_shard(lo, hi, dev, spec, seed=11)
+    df = D.all_reduce_sum(doc_freq(idx, counts, F))
+    idf = torch.log((args.rows + 1.0) / (df.double() + 1.0))
+    vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
+    vc.tf_counts, vc.tf_scale = counts, idf
+    t_feat = time.perf_counter() - t0
+    res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)
+    sync_all(dev)
+    train_sec = max_over_ranks(time.perf_counter() - t0, dev)
+    feat_sec = max_over_ranks(t_feat, dev)
+    model = SparkXGBClassifierModel(res.trees, F, res.base_margin)
+    idf_np = idf.cpu().numpy()
+    del vc, indptr, idx, counts, y
+    torch.cuda.empty_cache()
+
+    # ------------------------------------------------------------------ 2. streaming inference
+    scorer = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=args.batch, max_bytes=args.batch * 4096,
+                       depth=args.depth_pipeline)
+    ring = PinnedRing(slots=args.pool, max_docs=args.batch, max_bytes=args.batch * 4096)
+    pool_labels = []
+    for i, slot in enumerate(ring.slots):
+        pt, yb = synth.generate(synth.SynthConfig(n=args.batch, seed=1000 + rank), device=dev,
+                                start=10**9 + i * args.batch)
+        slot.fill_packed(pt.data.cpu().numpy(), pt.offsets.cpu().numpy())
+        pool_labels.append(yb.cpu().numpy())
+    avg_bytes = float(np.mean([s.n_bytes / max(s.n_docs, 1) for s in ring.slots]))
+
+    def run(steps: int):
+        correct = total = 0
+        for i in range(steps):
+            if scorer.inflight == scorer.depth:
+                slot, raw = scorer.collect()
+                pred, _ = model.postprocess_numpy(raw)
+                correct += int((pred == pool_labels[slot.index]).sum())
+                total += len(pred)
+            scorer.submit(ring.slots[i % len(ring.slots)])
+        while scorer.inflight:
+            slot, raw = scorer.collect()
+            pred, _ = model.postprocess_numpy(raw)
+            correct += int((pred == pool_labels[slot.index]).sum())
+            total += len(pred)
+        return correct, total
+
+    run(args.warmup)
+    sync_all(dev)
+    t0 = time.perf_counter()
+    correct, total = run(args.steps)
+    sync_all(dev)
+    dt = max_over_ranks(time.perf_counter() - t0, dev)
+    acc = correct / max(total, 1)
+
+    # single-dialogue end-to-end classify latency (unpipelined: H2D + kernel + D2H + postprocess)
+    one = PinnedRing(slots=1, max_docs=1, max_bytes=8192)
+    lat_scorer = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=1, max_bytes=8192, depth=1)
+    text = ring.slots[0]
+    first = bytes(text.data[: int(text.offsets[1])].numpy()).decode()
+    one.slots[0].fill([first])
+    lats = []
+    for _ in range(60):
+        t1 = time.perf_counter()
+        raw = lat_scorer.score_packed(one.slots[0])
+        model.postprocess_numpy(raw)
+        lats.append((time.perf_counter() - t1) * 1e3)
+    p50 = float(np.percentile(lats[10:], 50))
+
+    docs = args.steps * args.batch * world
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": docs / dt,
+            "unit": "dialogues/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"model": f"HashingTF(2^18)->IDF->GBDT({args.trees} trees, depth {args.depth})",
+                       "global_batch": args.batch * world, "seq_len": round(avg_bytes),
+                       "parallelism": f"dp{world}"},
+            "gbdt_train_sec": train_sec,
+            "gbdt_train_rows": args.rows,
+            "gbdt_featurize_sec": feat_sec,
+            "gbdt_nodes_tree0": res.trees[0].num_nodes,
+            "stream_accuracy": acc,
+            "p50_single_dialogue_ms": p50,
+        }
+        print(json.dumps(out), flush=True)
+    D.barrier()
+    if D.is_dist():
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

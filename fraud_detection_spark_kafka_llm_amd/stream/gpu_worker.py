@@ -1,0 +1,142 @@
+"""Per-GPU micro-batch scorer with overlapped H2D / compute / D2H (C-03 consumer side).
+
+Three HIP streams per device: ``h2d`` copies a pinned ring slot into one of ``depth`` device
+buffers, ``compute`` runs the fused featurize+score kernel on it, ``d2h`` copies the fp64 scores
+back into pinned host memory. Events chain the stages, so with depth >= 2 the copy of batch i+1
+and the result copy of batch i-1 run underneath the kernel of batch i. Device buffers are
+preallocated at the maximum micro-batch size: steady state allocates nothing.
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ops import native
+from ..ops.text import (FLAG_IDF, FLAG_LR, FLAG_TREES, PAD, STATUS_OK, FeatureSpec, LinearScorer, PackedText,
+                        TreeArrays, _flags, featurize_score)
+from .ring import Slot
+
+
+@dataclass
+class _Stage:
+    text: torch.Tensor
+    offsets: torch.Tensor
+    nnz: torch.Tensor
+    ntok: torch.Tensor
+    raw: torch.Tensor
+    status: torch.Tensor
+    h_raw: torch.Tensor
+    h_status: torch.Tensor
+    ev_h2d: torch.cuda.Event
+    ev_compute: torch.cuda.Event
+    ev_d2h: torch.cuda.Event
+    slot: Optional[Slot] = None
+    n: int = 0
+
+
+class GpuScorer:
+    def __init__(self, spec: FeatureSpec, idf: Optional[np.ndarray], scorer, device, max_docs: int = 65536,
+                 max_bytes: int = 256 << 20, depth: int = 2):
+        if not isinstance(scorer, (LinearScorer, TreeArrays)):
+            raise TypeError("scorer must be LinearScorer or TreeArrays")
+        self.spec, self.scorer = spec, scorer
+        self.dev = torch.device(device)
+        self.C = native.lib()
+        self.K = scorer.K if isinstance(scorer, TreeArrays) else 1
+        self.idf = torch.as_tensor(np.asarray(idf, dtype=np.float64)).to(self.dev) if idf is not None else None
+        lr = scorer if isinstance(scorer, LinearScorer) else None
+        trees = scorer if isinstance(scorer, TreeArrays) else None
+        self.flags = _flags(spec, self.idf, lr, trees, want_csr=False)
+        self.stop = spec.stop_table().tensors(self.dev) if spec.stop_table() else None
+        self.vocab = spec.vocab_table().tensors(self.dev) if spec.vocab_table() else None
+        self.lr_w = lr.weights(self.dev) if lr is not None else None
+        self.tree_t = trees.tensors(self.dev) if trees is not None else None
+        self.max_docs, self.max_bytes = max_docs, max_bytes
+        self.h2d = torch.cuda.Stream(self.dev)
+        self.compute = torch.cuda.Stream(self.dev)
+        self.d2h = torch.cuda.Stream(self.dev)
+        i32 = dict(dtype=torch.int32, device=self.dev)
+        self.dummy_i = torch.zeros(1, **i32)
+        self.dummy_f = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        self.stages = []
+        for _ in range(depth):
+            self.stages.append(_Stage(
+                torch.zeros(max_bytes + PAD, dtype=torch.uint8, device=self.dev),
+                torch.zeros(max_docs + 1, dtype=torch.int64, device=self.dev),
+                torch.zeros(max_docs, **i32), torch.zeros(max_docs, **i32),
+                torch.zeros((max_docs, self.K), dtype=torch.float64, device=self.dev),
+                torch.zeros(max_docs, **i32),
+                torch.zeros((max_docs, self.K), dtype=torch.float64).pin_memory(),
+                torch.zeros(max_docs, dtype=torch.int32).pin_memory(),
+                torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()))
+        self._next = 0
+        self._inflight: deque = deque()
+        torch.cuda.synchronize(self.dev)
+
+    # ------------------------------------------------------------------ pipeline
+    def submit(self, slot: Slot) -> None:
+        """Enqueue one slot. Blocks only if all ``depth`` stages are busy (waits the oldest)."""
+        if slot.n_docs > self.max_docs or slot.n_bytes > self.max_bytes:
+            raise ValueError("micro-batch exceeds the scorer's buffers")
+        if len(self._inflight) == len(self.stages):
+            raise RuntimeError("pipeline full: call collect() first")
+        st = self.stages[self._next]
+        self._next = (self._next + 1) % len(self.stages)
+        n, nb = slot.n_docs, slot.n_bytes
+        st.slot, st.n = slot, n
+        with torch.cuda.stream(self.h2d):
+            self.h2d.wait_event(st.ev_d2h)   # previous use of this stage fully drained
+            st.text[: nb + PAD].copy_(slot.data[: nb + PAD], non_blocking=True)
+            st.offsets[: n + 1].copy_(slot.offsets[: n + 1], non_blocking=True)
+            st.ev_h2d.record(self.h2d)
+        with torch.cuda.stream(self.compute):
+            self.compute.wait_event(st.ev_h2d)
+            if n:
+                self.C.featurize_score(st.text[: nb + PAD], st.offsets[: n + 1], self.flags, self.spec.dim, self.stop,
+                                       self.vocab, float(self.spec.min_tf), self.idf, self.lr_w,
+                                       float(self.scorer.b) if self.lr_w is not None else 0.0, self.tree_t, self.K,
+                                       self.dummy_i, self.dummy_f, st.nnz, st.ntok, st.raw, st.status, None, 0)
+            st.ev_compute.record(self.compute)
+        with torch.cuda.stream(self.d2h):
+            self.d2h.wait_event(st.ev_compute)
+            st.h_raw[:n].copy_(st.raw[:n], non_blocking=True)
+            st.h_status[:n].copy_(st.status[:n], non_blocking=True)
+            st.ev_d2h.record(self.d2h)
+        self._inflight.append(st)
+
+    def collect(self) -> tuple:
+        """Wait for the oldest in-flight batch; returns (slot, raw scores [n, K] numpy)."""
+        st = self._inflight.popleft()
+        st.ev_d2h.synchronize()
+        n = st.n
+        raw = st.h_raw[:n].numpy().copy()
+        status = st.h_status[:n].numpy()
+        if n and np.any(status != STATUS_OK):
+            bad = np.nonzero(status != STATUS_OK)[0]
+            sub = PackedText.from_strings([bytes(st.slot.data[int(st.slot.offsets[i]):int(st.slot.offsets[i + 1])]
+                                                 .numpy()).decode("utf-8", "replace") for i in bad])
+            lr = self.scorer if isinstance(self.scorer, LinearScorer) else None
+            tr = self.scorer if isinstance(self.scorer, TreeArrays) else None
+            fix = featurize_score(sub, self.spec, idf=self.idf.cpu() if self.idf is not None else None, lr=lr,
+                                  trees=tr, device="cpu")
+            raw[bad] = fix.raw.numpy()
+        slot = st.slot
+        st.slot = None
+        return slot, raw
+
+    @property
+    def inflight(self) -> int:
+        return len(self._inflight)
+
+    @property
+    def depth(self) -> int:
+        return len(self.stages)
+
+    def score_packed(self, slot: Slot) -> np.ndarray:
+        """Synchronous single batch (latency path)."""
+        self.submit(slot)
+        return self.collect()[1]

@@ -174,7 +174,9 @@ def test_gpu_mfma_histograms_match_host(ct, nslots, max_bins):
                                   slab, grp.feat, grp.feat_item0, grp.feat_nitems, Q.boff, Q.nbins, s2n.to(dev),
                                   hist, Q.TB)
         out[dev] = hist.cpu().numpy()
-    np.testing.assert_allclose(out["cuda:0"], out["cpu"], rtol=2e-6, atol=1e-6)
+    # device chunks accumulate in fp32 (MFMA), host in fp64: allow fp32 rounding of the partials
+    scale = np.abs(out["cpu"]).max()
+    np.testing.assert_allclose(out["cuda:0"], out["cpu"], rtol=2e-6, atol=2e-7 * scale)
 
 
 @pytest.mark.gpu
