@@ -1,0 +1,119 @@
+"""ML API: pipelines end to end (fit/transform/save/load), evaluators vs brute force, LR trainer."""
+import numpy as np
+import pytest
+import torch
+
+from fraud_detection_spark_kafka_llm_amd.data import synth
+from fraud_detection_spark_kafka_llm_amd.ml import (IDF, CountVectorizer, DecisionTreeClassifier, Frame, HashingTF,
+                                                     LogisticRegression, Pipeline, PipelineModel,
+                                                     RandomForestClassifier, StopWordsRemover, TextColumn, Tokenizer)
+from fraud_detection_spark_kafka_llm_amd.ml.evaluation import (BinaryClassificationEvaluator,
+                                                                MulticlassClassificationEvaluator, area_under_roc)
+from fraud_detection_spark_kafka_llm_amd.ml.xgboost import SparkXGBClassifier, SparkXGBClassifierModel
+
+
+@pytest.fixture(scope="module")
+def frames():
+    pt, y = synth.generate(synth.SynthConfig(n=900, seed=5))
+    raw = TextColumn(pt.strings())
+    df = Frame({"dialogue": raw, "clean_text": TextColumn.cleaned_from(raw), "labels": y.numpy()})
+    return df.randomSplit([0.7, 0.3], seed=42)
+
+
+def exact_auc(s, y):
+    pos, neg = s[y == 1], s[y == 0]
+    gt = (pos[:, None] > neg[None, :]).sum() + 0.5 * (pos[:, None] == neg[None, :]).sum()
+    return gt / (len(pos) * len(neg))
+
+
+def test_auc_matches_mann_whitney():
+    rng = np.random.default_rng(0)
+    s = np.round(rng.random(500), 2)
+    y = (rng.random(500) < 0.4).astype(float)
+    assert area_under_roc(torch.from_numpy(s), torch.from_numpy(y), num_bins=0) == pytest.approx(exact_auc(s, y))
+    # <1000 distinct scores -> no down-sampling even with the default numBins
+    assert area_under_roc(torch.from_numpy(s), torch.from_numpy(y)) == pytest.approx(exact_auc(s, y))
+
+
+def test_multiclass_weighted_metrics():
+    y = np.array([0, 0, 0, 1, 1, 1, 1, 0], dtype=float)
+    p = np.array([0, 1, 0, 1, 1, 0, 1, 0], dtype=float)
+    df = Frame({"label": y, "prediction": p})
+    ev = MulticlassClassificationEvaluator(labelCol="label")
+    # class 0: tp=3 fp=1 fn=1 ; class 1: tp=3 fp=1 fn=1 -> all 0.75
+    assert ev.evaluate(df, {"metricName": "accuracy"}) == pytest.approx(0.75)
+    assert ev.evaluate(df, {"metricName": "weightedPrecision"}) == pytest.approx(0.75)
+    assert ev.evaluate(df, {"metricName": "weightedRecall"}) == pytest.approx(0.75)
+    assert ev.evaluate(df) == pytest.approx(0.75)
+
+
+def _feature_stages(cv=False):
+    tf = CountVectorizer(inputCol="filtered_words", outputCol="raw_features", vocabSize=20000) if cv else \
+        HashingTF(inputCol="filtered_words", outputCol="raw_features", numFeatures=4096)
+    return [Tokenizer(inputCol="clean_text", outputCol="words"),
+            StopWordsRemover(inputCol="words", outputCol="filtered_words"), tf,
+            IDF(inputCol="raw_features", outputCol="features")]
+
+
+@pytest.mark.parametrize("make", [
+    lambda: DecisionTreeClassifier(featuresCol="features", labelCol="labels", maxDepth=5),
+    lambda: RandomForestClassifier(featuresCol="features", labelCol="labels", numTrees=10, maxDepth=4, seed=42),
+    lambda: SparkXGBClassifier(features_col="features", label_col="labels", max_depth=4, n_estimators=15),
+    lambda: LogisticRegression(featuresCol="features", labelCol="labels", maxIter=30, regParam=0.01),
+])
+@pytest.mark.parametrize("cv", [False, True])
+def test_pipeline_fit_transform_save_load(frames, tmp_path, make, cv):
+    train, test = frames
+    model = Pipeline(stages=_feature_stages(cv) + [make()]).fit(train)
+    out = model.transform(test)
+    auc = BinaryClassificationEvaluator(labelCol="labels").evaluate(out)
+    acc = MulticlassClassificationEvaluator(labelCol="labels", metricName="accuracy").evaluate(out)
+    assert auc > 0.85 and acc > 0.8, (auc, acc)
+    path = tmp_path / "m"
+    model.write().overwrite().save(str(path))
+    again = PipelineModel.load(str(path))
+    out2 = again.transform(test)
+    np.testing.assert_allclose(out2.column("probability").cpu().numpy(), out.column("probability").cpu().numpy(),
+                               rtol=1e-9, atol=1e-12)
+    # the fused serving path agrees with the staged transform
+    pred, prob, _ = again.compile().predict(test.column("dialogue").strings, clean=True)
+    np.testing.assert_allclose(prob.cpu().numpy(), out.column("probability").cpu().numpy(), rtol=1e-9, atol=1e-12)
+
+
+def test_xgboost_json_roundtrip(frames, tmp_path):
+    train, test = frames
+    model = Pipeline(stages=_feature_stages() + [SparkXGBClassifier(features_col="features", label_col="labels",
+                                                                       n_estimators=5, max_depth=3)]).fit(train)
+    xgbm = model.stages[-1]
+    js = xgbm.to_xgboost_json()
+    back = SparkXGBClassifierModel.from_xgboost_json(js)
+    feats = model.stages[-2].transform(model.stages[-3].transform(
+        model.stages[1].transform(model.stages[0].transform(test)))).column("features")
+    from fraud_detection_spark_kafka_llm_amd.ops.sparse import score_csr
+
+    a = score_csr(feats, xgbm.scorer())
+    b = score_csr(feats, back.scorer())
+    np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-6)
+    assert back.base_margin == pytest.approx(xgbm.base_margin, abs=1e-6)
+
+
+def test_lr_trainer_converges_on_separable_margin():
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+    from fraud_detection_spark_kafka_llm_amd.models.lr import train_logistic_regression
+
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(400, 5))
+    wtrue = np.array([1.5, -2.0, 0.0, 0.5, 1.0])
+    y = (rng.random(400) < 1 / (1 + np.exp(-(X @ wtrue - 0.3)))).astype(float)
+    vc = VectorColumn(5, dense=torch.from_numpy(X))
+    coef, b, hist = train_logistic_regression(vc, y, max_iter=100, tol=1e-10, device="cpu")
+    # compare with a plain Newton solve of the same (unregularised) objective
+    Xb = np.hstack([X, np.ones((400, 1))])
+    th = np.zeros(6)
+    for _ in range(50):
+        p = 1 / (1 + np.exp(-Xb @ th))
+        H = Xb.T @ (Xb * (p * (1 - p))[:, None])
+        th -= np.linalg.solve(H, Xb.T @ (p - y))
+    np.testing.assert_allclose(coef, th[:5], rtol=1e-4, atol=1e-4)
+    assert b == pytest.approx(th[5], abs=1e-4)
+    assert hist[-1] <= hist[0]
