@@ -261,6 +261,21 @@ void doc_freq(const Tensor& idx, const Tensor& val, const Tensor& df) {
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+int64_t extract_json_field(const Tensor& in, const Tensor& in_off, const std::string& field, const Tensor& out,
+                           const Tensor& out_off, const Tensor& status, int64_t threads) {
+  for (const Tensor* t : {&in, &in_off, &out, &out_off, &status})
+    FDX_CHECK(!t->is_cuda() && t->is_contiguous(), "json extraction runs on host tensors");
+  FDX_CHECK(in.scalar_type() == at::kByte && out.scalar_type() == at::kByte && in_off.scalar_type() == at::kLong &&
+                out_off.scalar_type() == at::kLong && status.scalar_type() == at::kInt,
+            "dtypes u8/i64/u8/i64/i32");
+  const int64_t n = in_off.numel() - 1;
+  FDX_CHECK(n >= 0 && out_off.numel() >= n + 1 && status.numel() >= n, "offset/status sizes");
+  return fdx::extract_json_field(in.data_ptr<uint8_t>(), in_off.data_ptr<int64_t>(), n,
+                                 reinterpret_cast<const uint8_t*>(field.data()), (int64_t)field.size(),
+                                 out.data_ptr<uint8_t>(), out.numel(), out_off.data_ptr<int64_t>(),
+                                 status.data_ptr<int32_t>(), (int)threads);
+}
+
 }  // namespace
 
 void register_tree_ops(pybind11::module& m);
@@ -273,5 +288,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spmv", &spmv, "y = X x (CSR, fp64 accumulate)");
   m.def("spmv_t", &spmv_t, "g += X^T r (CSR, fp64)");
   m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
+  m.def("extract_json_field", &extract_json_field, "Bulk JSON string-field extraction into a packed buffer");
   m.attr("gfx_arch") = "gfx950";
 }

@@ -58,6 +58,10 @@ void partition_cpu(const PartitionArgs& a);
 void logistic_grad_cpu(const double* margin, const float* label, const float* weight, float* g, float* h, int64_t N);
 void leaf_update_cpu(double* margin, const int32_t* row_node, const double* node_value, int64_t N);
 
+// json_text.cpp
+int64_t extract_json_field(const uint8_t* in, const int64_t* in_off, int64_t n, const uint8_t* field, int64_t flen,
+                           uint8_t* out, int64_t out_cap, int64_t* out_off, int32_t* status, int threads);
+
 template <class V> void score_csr_cpu(const CsrArgs<V>& a, int threads);
 template <class V> void spmv_cpu(const int64_t* indptr, const int32_t* idx, const V* val, const double* x, double* y,
                                  int64_t rows, int threads);

@@ -140,3 +140,48 @@ class GpuScorer:
         """Synchronous single batch (latency path)."""
         self.submit(slot)
         return self.collect()[1]
+
+
+class HostScorer:
+    """Same submit/collect interface on the host path (CPU-only deployments and tests)."""
+
+    def __init__(self, spec: FeatureSpec, idf: Optional[np.ndarray], scorer, max_docs: int = 65536,
+                 max_bytes: int = 256 << 20, depth: int = 1):
+        self.spec, self.scorer = spec, scorer
+        self.idf = torch.as_tensor(np.asarray(idf, dtype=np.float64)) if idf is not None else None
+        self.max_docs, self.max_bytes = max_docs, max_bytes
+        self._depth = max(1, depth)
+        self._inflight: deque = deque()
+
+    def submit(self, slot: Slot) -> None:
+        if len(self._inflight) == self._depth:
+            raise RuntimeError("pipeline full: call collect() first")
+        n, nb = slot.n_docs, slot.n_bytes
+        pt = PackedText(slot.data[: nb + PAD], slot.offsets[: n + 1].clone())
+        lr = self.scorer if isinstance(self.scorer, LinearScorer) else None
+        tr = self.scorer if isinstance(self.scorer, TreeArrays) else None
+        res = featurize_score(pt, self.spec, idf=self.idf, lr=lr, trees=tr, device="cpu")
+        self._inflight.append((slot, res.raw.numpy().copy()))
+
+    def collect(self) -> tuple:
+        return self._inflight.popleft()
+
+    @property
+    def inflight(self) -> int:
+        return len(self._inflight)
+
+    @property
+    def depth(self) -> int:
+        return self._depth
+
+    def score_packed(self, slot: Slot) -> np.ndarray:
+        self.submit(slot)
+        return self.collect()[1]
+
+
+def make_scorer(spec: FeatureSpec, idf, scorer, device, max_docs: int = 65536, max_bytes: int = 256 << 20,
+                depth: int = 2):
+    device = torch.device(device)
+    if device.type == "cuda":
+        return GpuScorer(spec, idf, scorer, device, max_docs, max_bytes, depth)
+    return HostScorer(spec, idf, scorer, max_docs, max_bytes, depth)

@@ -1,0 +1,82 @@
+"""Kafka consumer/producer factories (R-18, R-19), reading the reference's environment variables.
+
+``KAFKA_BOOTSTRAP_SERVERS`` (default ``localhost:9092``), ``KAFKA_CONSUMER_GROUP``
+(``dialogue-classifier-group``), ``KAFKA_INPUT_TOPIC`` (``customer-dialogues-raw``),
+``KAFKA_SECURITY_PROTOCOL=SASL_SSL`` + ``KAFKA_USERNAME``/``KAFKA_PASSWORD`` (SASL PLAIN);
+consumer: ``auto.offset.reset=earliest``, ``enable.auto.commit=False`` (/root/reference/utils/
+kafka_utils.py:11-49). The backend is confluent_kafka (librdkafka) when importable and the
+bootstrap is a real address; ``memory://...`` bootstraps (or ``FDX_KAFKA=memory``) select the
+in-memory broker of ``fake_kafka`` — used by tests, benchmarks and offline demos.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+from . import fake_kafka
+
+DEFAULT_BOOTSTRAP = "localhost:9092"
+DEFAULT_GROUP = "dialogue-classifier-group"
+DEFAULT_INPUT = "customer-dialogues-raw"
+DEFAULT_OUTPUT = "dialogues-classified"
+
+
+def _security(conf: dict) -> dict:
+    if os.getenv("KAFKA_SECURITY_PROTOCOL") == "SASL_SSL":
+        conf.update({"security.protocol": "SASL_SSL", "sasl.mechanisms": "PLAIN",
+                     "sasl.username": os.getenv("KAFKA_USERNAME"), "sasl.password": os.getenv("KAFKA_PASSWORD")})
+    return conf
+
+
+def _use_memory(bootstrap: str) -> bool:
+    if bootstrap.startswith("memory://") or os.getenv("FDX_KAFKA", "").lower() == "memory":
+        return True
+    try:
+        import confluent_kafka  # noqa: F401
+    except ImportError:
+        return True
+    return False
+
+
+def consumer_config(group: Optional[str] = None) -> dict:
+    return _security({"bootstrap.servers": os.getenv("KAFKA_BOOTSTRAP_SERVERS", DEFAULT_BOOTSTRAP),
+                      "group.id": group or os.getenv("KAFKA_CONSUMER_GROUP", DEFAULT_GROUP),
+                      "auto.offset.reset": "earliest", "enable.auto.commit": False})
+
+
+def producer_config() -> dict:
+    return _security({"bootstrap.servers": os.getenv("KAFKA_BOOTSTRAP_SERVERS", DEFAULT_BOOTSTRAP)})
+
+
+def get_kafka_consumer(topics=None, group: Optional[str] = None):
+    conf = consumer_config(group)
+    if _use_memory(conf["bootstrap.servers"]):
+        c = fake_kafka.Consumer(conf)
+    else:
+        from confluent_kafka import Consumer
+
+        c = Consumer(conf)
+    c.subscribe(list(topics) if topics else [os.getenv("KAFKA_INPUT_TOPIC", DEFAULT_INPUT)])
+    return c
+
+
+def get_kafka_producer():
+    conf = producer_config()
+    if _use_memory(conf["bootstrap.servers"]):
+        return fake_kafka.Producer(conf)
+    from confluent_kafka import Producer
+
+    return Producer(conf)
+
+
+def output_topic() -> Optional[str]:
+    return os.getenv("KAFKA_OUTPUT_TOPIC")
+
+
+def kafka_exception_class():
+    try:
+        from confluent_kafka import KafkaException
+
+        return KafkaException
+    except ImportError:
+        return fake_kafka.KafkaException

@@ -99,6 +99,40 @@ def _coerce(typ, v):
     return v
 
 
+def load_dotenv(path=None, override: bool = False) -> bool:
+    """Minimal ``python-dotenv`` replacement: ``KEY=VALUE`` lines (``export`` prefix, quotes and
+    ``#`` comments allowed) are copied into ``os.environ``. Without ``path`` the nearest ``.env``
+    from the current directory upwards is used. Returns whether a file was read."""
+    from pathlib import Path
+
+    if path is None:
+        cur = Path.cwd()
+        for d in [cur, *cur.parents]:
+            if (d / ".env").is_file():
+                path = d / ".env"
+                break
+        if path is None:
+            return False
+    p = Path(path)
+    if not p.is_file():
+        return False
+    for line in p.read_text(encoding="utf-8", errors="replace").splitlines():
+        line = line.strip()
+        if not line or line.startswith("#") or "=" not in line:
+            continue
+        if line.startswith("export "):
+            line = line[7:]
+        k, v = line.split("=", 1)
+        k, v = k.strip(), v.strip()
+        if len(v) >= 2 and v[0] == v[-1] and v[0] in "\"'":
+            v = v[1:-1]
+        elif " #" in v:
+            v = v.split(" #", 1)[0].rstrip()
+        if override or k not in os.environ:
+            os.environ[k] = v
+    return True
+
+
 def default_device() -> torch.device:
     env = os.environ.get("FDX_DEVICE")
     if env:
