@@ -1,0 +1,79 @@
+"""Data parallelism (PAR-01..PAR-04) with 2 CPU ranks over gloo: the DP models equal DP=1 models."""
+import numpy as np
+import pytest
+import torch
+
+from fraud_detection_spark_kafka_llm_amd.parallel.launch import spawn
+
+
+def _dataset(n=1200, F=80, seed=0):
+    rng = np.random.default_rng(seed)
+    dense = (rng.random((n, F)) < 0.15) * rng.integers(1, 5, (n, F))
+    y = ((dense[:, 0] > 0) ^ (dense[:, 3] >= 2)).astype(np.float32)
+    flip = rng.random(n) < 0.04
+    y[flip] = 1 - y[flip]
+    return dense.astype(np.float64), y
+
+
+def _vc(dense):
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+
+    return VectorColumn(dense.shape[1], dense=torch.from_numpy(dense))
+
+
+def _train(rank, world, kind):
+    from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+    from fraud_detection_spark_kafka_llm_amd.models.lr import train_logistic_regression
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+    from fraud_detection_spark_kafka_llm_amd.parallel.dist import shard_range
+
+    dense, y = _dataset()
+    lo, hi = shard_range(len(y), rank, world)
+    vc, yy = _vc(dense[lo:hi]), torch.from_numpy(y[lo:hi])
+    if kind == "gbdt":
+        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=6, max_depth=4), device="cpu")
+        return [(t.feature.tolist(), t.stats[:, 0].tolist()) for t in r.trees], r.base_margin
+    if kind == "rf":
+        r = fit_forest(vc, yy, num_trees=3, max_depth=4, bootstrap=False, feature_subset="sqrt", seed=5, device="cpu")
+        return [(t.feature.tolist(), t.stats.tolist()) for t in r.trees], 0.0
+    if kind == "lr":
+        coef, b, _ = train_logistic_regression(vc, yy.numpy(), max_iter=50, reg_param=0.01, device="cpu")
+        return coef.tolist(), b
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["gbdt", "rf", "lr"])
+def test_two_ranks_equal_single_process(kind):
+    single = _train(0, 1, kind)
+    outs = spawn(_train, 2, kind, backend="gloo")
+    assert outs[0] == outs[1] or kind == "lr" and np.allclose(outs[0][0], outs[1][0])   # identical on both ranks
+    dp = outs[0]
+    if kind == "lr":
+        np.testing.assert_allclose(dp[0], single[0], rtol=1e-6, atol=1e-8)
+        assert dp[1] == pytest.approx(single[1], rel=1e-6)
+        return
+    for (f1, v1), (f2, v2) in zip(dp[0], single[0]):
+        assert f1 == f2
+        np.testing.assert_allclose(np.asarray(v1), np.asarray(v2), rtol=1e-6, atol=1e-9)
+    assert dp[1] == pytest.approx(single[1])
+
+
+def _idf_rank(rank, world):
+    from fraud_detection_spark_kafka_llm_amd.ml.feature import idf_fit
+    from fraud_detection_spark_kafka_llm_amd.parallel.dist import all_reduce_sum, shard_range
+
+    dense, _ = _dataset()
+    lo, hi = shard_range(len(dense), rank, world)
+    idf, df, n = idf_fit(_vc(dense[lo:hi]), 0, all_reduce=all_reduce_sum)
+    return idf.tolist(), df.tolist(), n
+
+
+def test_distributed_idf_equals_global():
+    from fraud_detection_spark_kafka_llm_amd.ml.feature import idf_fit
+
+    dense, _ = _dataset()
+    idf, df, n = idf_fit(_vc(dense))
+    outs = spawn(_idf_rank, 3, backend="gloo")
+    for o in outs:
+        assert o[2] == n and o[1] == df.tolist()
+        np.testing.assert_array_equal(np.asarray(o[0]), idf)
