@@ -59,15 +59,30 @@ def _logit(p: float) -> float:
 
 
 def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, weights=None,
-             eval_fn=None, checkpoint=None, start_trees: Optional[list] = None) -> GBDTResult:
+             eval_fn=None, checkpoint=None, start_trees: Optional[list] = None,
+             checkpoint_dir: Optional[str] = None, checkpoint_every: int = 10, resume: bool = False) -> GBDTResult:
+    """``checkpoint_dir``: write the partial ensemble every ``checkpoint_every`` trees; with
+    ``resume=True`` continue from the last checkpoint there (any world size)."""
+    from ..parallel.checkpoint import EnsembleCheckpointer, maybe_fail
+
     C = native.lib()
     coll = Collectives()
     t0 = time.perf_counter()
+    ckpt = EnsembleCheckpointer(checkpoint_dir, checkpoint_every, "gbdt") if checkpoint_dir else None
+    resume_state = ckpt.load() if (ckpt is not None and resume) else None
+    if resume_state is not None:
+        start_trees = ckpt.load_trees()
+        params = GBDTParams(**{**params.__dict__, "base_score": None})
+        forced_base = float(resume_state["base_margin"])
+    else:
+        forced_base = None
     Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll)
     dev = Q.device
     w = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float32)).to(dev)
     N = Q.n_rows
-    if params.base_score is None:
+    if forced_base is not None:
+        base = forced_base
+    elif params.base_score is None:
         s = coll.sum(torch.stack([(y * (w if w is not None else 1.0)).sum().double(),
                                   (w.sum() if w is not None else torch.tensor(float(N), device=dev)).double()]))
         base = _logit(float(s[0] / max(float(s[1]), 1e-12)))
@@ -98,6 +113,9 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
             history.append(eval_fn(t, trees, margin))
         if checkpoint is not None:
             checkpoint(t, trees, base)
+        if ckpt is not None:
+            ckpt.maybe_save(len(trees), trees, base, F, params, force=len(trees) == params.n_estimators)
+        maybe_fail(t)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0)
