@@ -147,6 +147,117 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
       }
 }
 
+// v2: U groups of 64 entries are loaded per step (U dependent-gather chains in flight per wave
+// instead of one), and MFMA K-steps whose 16 entries belong to no built node are skipped
+// (wave-uniform ballot test), which at deep levels removes most of the VALU/MFMA work.
+template <int BT, int CT, int U>
+__global__ __launch_bounds__(256) void hist_mfma_v2_kernel(HistArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_bin[4][U * kWave];
+  __shared__ __attribute__((aligned(16))) int8_t s_slot[4][U * kWave];
+  __shared__ __attribute__((aligned(16))) uint16_t s_comp[4][4][U * kWave];
+
+  const int wid = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int item = blockIdx.x * 4 + wid;
+  if (item >= a.num_items) return;
+  const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
+
+  const int col = lane & 31;
+  const int half = lane >> 5;
+  const int comp = col & 3;
+  const int slot_sub = col >> 2;
+
+  f32x16 acc[BT][CT];
+#pragma unroll
+  for (int bt = 0; bt < BT; ++bt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[bt][ct][i] = 0.0f;
+
+  for (int64_t base = e0; base < e1; base += U * kWave) {
+    int32_t row[U];
+    uint8_t bin[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = base + u * kWave + lane;
+      row[u] = (e < e1) ? a.csc_row[e] : -1;
+      bin[u] = (e < e1) ? a.csc_bin[e] : (uint8_t)0xff;
+    }
+    uint4 st[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      st[u] = make_uint4(0xffffffffu, 0, 0, 0);
+      if (row[u] >= 0) st[u] = reinterpret_cast<const uint4*>(a.rowstate)[row[u]];
+    }
+    unsigned long long live[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int s = (int)st[u].x - a.slot_base;
+      const bool ok = s >= 0 && s < 8 * CT;
+      live[u] = __ballot(ok);
+      const int k = u * kWave + lane;
+      s_bin[wid][k] = bin[u];
+      s_slot[wid][k] = ok ? (int8_t)s : (int8_t)-1;
+      s_comp[wid][0][k] = ok ? (uint16_t)(st[u].y & 0xffffu) : (uint16_t)0;
+      s_comp[wid][1][k] = ok ? (uint16_t)(st[u].y >> 16) : (uint16_t)0;
+      s_comp[wid][2][k] = ok ? (uint16_t)(st[u].z & 0xffffu) : (uint16_t)0;
+      s_comp[wid][3][k] = ok ? (uint16_t)(st[u].z >> 16) : (uint16_t)0;
+    }
+    lds_sync();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (live[u] == 0ull) continue;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (((live[u] >> (16 * ks)) & 0xffffull) == 0ull) continue;
+        const int k0 = u * kWave + ks * 16 + 8 * half;
+        const uint64_t bins8 = *reinterpret_cast<const uint64_t*>(&s_bin[wid][k0]);
+        const uint64_t slots8 = *reinterpret_cast<const uint64_t*>(&s_slot[wid][k0]);
+        const s16x8 cv = *reinterpret_cast<const s16x8*>(&s_comp[wid][comp][k0]);
+        bf16x8 A[BT];
+#pragma unroll
+        for (int bt = 0; bt < BT; ++bt) {
+          s16x8 av;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            av[j] = (((bins8 >> (8 * j)) & 0xffu) == (uint64_t)(col + 32 * bt)) ? (short)0x3f80 : (short)0;
+          A[bt] = __builtin_bit_cast(bf16x8, av);
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          s16x8 bv;
+          const uint64_t want = (uint64_t)(ct * 8 + slot_sub);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bv[j] = (((slots8 >> (8 * j)) & 0xffu) == want) ? cv[j] : (short)0;
+          const bf16x8 B = __builtin_bit_cast(bf16x8, bv);
+#pragma unroll
+          for (int bt = 0; bt < BT; ++bt)
+            acc[bt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
+        }
+      }
+    }
+    lds_sync();
+  }
+
+  float* out = a.slab + (int64_t)item * (8 * CT) * (32 * BT) * 2;
+#pragma unroll
+  for (int bt = 0; bt < BT; ++bt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float v = acc[bt][ct][reg];
+        const float w = __shfl_xor(v, 1, kWave);
+        if ((col & 1) == 0) {
+          const int r = (reg & 3) + 8 * (reg >> 2) + 4 * half + 32 * bt;
+          const int slot = ct * 8 + slot_sub;
+          const int stat = (col >> 1) & 1;
+          out[((int64_t)slot * (32 * BT) + r) * 2 + stat] = v + w;
+        }
+      }
+}
+
 // ------------------------------------------------------------------ reduce chunk partials
 __global__ __launch_bounds__(256) void hist_reduce_kernel(HistReduceArgs a) {
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -260,14 +371,30 @@ void launch_rowstate(const RowStateArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(rowstate_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
+int hist_kernel_version() {
+  static int v = [] {
+    const char* e = getenv("FDX_HIST_KERNEL");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s) {
   if (a.num_items <= 0) return;
   const dim3 grid((a.num_items + 3) / 4), block(256);
+  if (hist_kernel_version() == 1) {
 #define FDX_HIST_CASE(B, C) \
   if (bt == B && ct == C) { hipLaunchKernelGGL((hist_mfma_kernel<B, C>), grid, block, 0, s, a); return; }
-  FDX_HIST_CASE(1, 1) FDX_HIST_CASE(1, 2) FDX_HIST_CASE(1, 4)
-  FDX_HIST_CASE(2, 1) FDX_HIST_CASE(2, 2) FDX_HIST_CASE(2, 4)
+    FDX_HIST_CASE(1, 1) FDX_HIST_CASE(1, 2) FDX_HIST_CASE(1, 4)
+    FDX_HIST_CASE(2, 1) FDX_HIST_CASE(2, 2) FDX_HIST_CASE(2, 4)
 #undef FDX_HIST_CASE
+    return;
+  }
+#define FDX_HIST2_CASE(B, C) \
+  if (bt == B && ct == C) { hipLaunchKernelGGL((hist_mfma_v2_kernel<B, C, 4>), grid, block, 0, s, a); return; }
+  FDX_HIST2_CASE(1, 1) FDX_HIST2_CASE(1, 2) FDX_HIST2_CASE(1, 4)
+  FDX_HIST2_CASE(2, 1) FDX_HIST2_CASE(2, 2) FDX_HIST2_CASE(2, 4)
+#undef FDX_HIST2_CASE
 }
 
 void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s) {

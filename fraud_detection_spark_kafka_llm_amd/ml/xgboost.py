@@ -128,8 +128,10 @@ class SparkXGBClassifierModel(_XGBParams, ClassificationModelBase):
 
     def postprocess_numpy(self, raw: np.ndarray):
         m = raw[:, 0] + self.base_margin
-        p = 1.0 / (1.0 + np.exp(-m))
-        return (p > 0.5).astype(np.float64), p
+        p = np.exp(-m)
+        np.add(p, 1.0, out=p)
+        np.reciprocal(p, out=p)
+        return (m > 0.0).astype(np.float64), p
 
     def get_booster(self):
         return self

@@ -108,12 +108,17 @@ class GpuScorer:
             st.ev_d2h.record(self.d2h)
         self._inflight.append(st)
 
-    def collect(self) -> tuple:
-        """Wait for the oldest in-flight batch; returns (slot, raw scores [n, K] numpy)."""
+    def collect(self, copy: bool = True) -> tuple:
+        """Wait for the oldest in-flight batch; returns (slot, raw scores [n, K] numpy).
+
+        ``copy=False`` returns a view of the pinned result buffer, valid until this pipeline
+        stage is reused (``depth`` submits later) — the zero-copy path of the streaming loop."""
         st = self._inflight.popleft()
         st.ev_d2h.synchronize()
         n = st.n
-        raw = st.h_raw[:n].numpy().copy()
+        raw = st.h_raw[:n].numpy()
+        if copy:
+            raw = raw.copy()
         status = st.h_status[:n].numpy()
         if n and np.any(status != STATUS_OK):
             bad = np.nonzero(status != STATUS_OK)[0]
@@ -123,6 +128,7 @@ class GpuScorer:
             tr = self.scorer if isinstance(self.scorer, TreeArrays) else None
             fix = featurize_score(sub, self.spec, idf=self.idf.cpu() if self.idf is not None else None, lr=lr,
                                   trees=tr, device="cpu")
+            raw = raw.copy()
             raw[bad] = fix.raw.numpy()
         slot = st.slot
         st.slot = None

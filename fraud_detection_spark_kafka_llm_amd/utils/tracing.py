@@ -16,6 +16,7 @@ import time
 
 _roctx = None
 _trace_path = os.environ.get("FDX_TRACE")
+_sync = os.environ.get("FDX_TRACE_SYNC") == "1"   # synchronise the device at span exit (attribution)
 _lock = threading.Lock()
 _depth = threading.local()
 
@@ -55,6 +56,11 @@ def span(name: str, **attrs):
     try:
         yield
     finally:
+        if _sync and _trace_path:
+            import torch
+
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
         _depth.v = d
         dt = time.perf_counter() - t0
         if rt:
