@@ -135,26 +135,38 @@ def main():
 
         def finish():
             nonlocal correct, total, sink
+            a = time.perf_counter()
             slot, raw = scorer.collect(copy=False)
+            b = time.perf_counter()
             pred, p = model.postprocess_numpy(raw)
             sink += float(p[0])
             if check:
                 correct += int((pred == pool_labels[slot.index]).sum())
                 total += len(pred)
+            timing["collect"] += b - a
+            timing["post"] += time.perf_counter() - b
 
         for i in range(steps):
             if scorer.inflight == scorer.depth:
                 finish()
+            a = time.perf_counter()
             scorer.submit(ring.slots[i % len(ring.slots)])
+            timing["submit"] += time.perf_counter() - a
         while scorer.inflight:
             finish()
         return correct, total
 
+    timing = {"collect": 0.0, "post": 0.0, "submit": 0.0}
+
     correct, total = run(max(args.warmup, len(ring.slots)), True)
     sync_all(dev)
+    timing = {k: 0.0 for k in timing}
     t0 = time.perf_counter()
     run(args.steps, False)
     sync_all(dev)
+    if os.environ.get("FDX_BENCH_TIMING") == "1":
+        print(json.dumps({"rank": rank, **{k + "_ms_per_step": v / args.steps * 1e3 for k, v in timing.items()}}),
+              file=sys.stderr, flush=True)
     dt = max_over_ranks(time.perf_counter() - t0, dev)
     acc = correct / max(total, 1)
 

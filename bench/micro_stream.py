@@ -68,6 +68,31 @@ def main():
         dt = (time.perf_counter() - t0) / args.steps
         print(json.dumps({"what": "pipeline", "depth": depth, "ms_per_step": dt * 1e3, "docs_per_s": B / dt}),
               flush=True)
+    # (b2) pipeline with host postprocess + per-phase host timing
+    for depth in (2, 3):
+        sc = GpuScorer(spec, idf, trees, dev, max_docs=B, max_bytes=B * 4096, depth=depth)
+        ts = {"submit": 0.0, "collect_wait": 0.0, "post": 0.0}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            if sc.inflight == depth:
+                a = time.perf_counter()
+                _, raw = sc.collect(copy=False)
+                b = time.perf_counter()
+                m = raw[:, 0]
+                p = np.reciprocal(np.exp(-m) + 1.0)
+                c = time.perf_counter()
+                ts["collect_wait"] += b - a
+                ts["post"] += c - b
+            a = time.perf_counter()
+            sc.submit(ring.slots[i % 4])
+            ts["submit"] += time.perf_counter() - a
+        while sc.inflight:
+            sc.collect(copy=False)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        print(json.dumps({"what": "pipeline+post", "depth": depth, "ms_per_step": dt * 1e3,
+                          **{k + "_ms": v / args.steps * 1e3 for k, v in ts.items()}}), flush=True)
     # (c) kernel only (text resident)
     pt = T.PackedText(ring.slots[0].data[: nb + 16].to(dev), ring.slots[0].offsets[: B + 1].to(dev))
     for _ in range(3):

@@ -29,6 +29,19 @@ void check_dev(const Tensor& t, const at::Device& dev, const char* name) {
   FDX_CHECK(t.is_contiguous(), std::string(name) + " must be contiguous");
 }
 
+// Output buffer for a device kernel: either on the device, or page-locked host memory that the
+// kernel writes through PCIe directly (zero-copy results, no D2H copy on the SDMA queue).
+template <class T>
+T* out_ptr(const Tensor& t, const at::Device& dev, const char* name) {
+  FDX_CHECK(t.is_contiguous(), std::string(name) + " must be contiguous");
+  if (t.device() == dev) return t.data_ptr<T>();
+  FDX_CHECK(dev.is_cuda() && t.device().is_cpu() && t.is_pinned(),
+            std::string(name) + " must be on " + dev.str() + " or pinned host memory");
+  void* dptr = nullptr;
+  FDX_CHECK(hipHostGetDevicePointer(&dptr, t.data_ptr(), 0) == hipSuccess, "hipHostGetDevicePointer failed");
+  return static_cast<T*>(dptr);
+}
+
 fdx::StrTable make_table(const optional<std::vector<Tensor>>& tab, const at::Device& dev) {
   fdx::StrTable t{nullptr, nullptr, nullptr, nullptr, -1};
   if (!tab || tab->empty()) return t;
@@ -89,7 +102,7 @@ void featurize_score(const Tensor& text, const Tensor& doc_off, int64_t flags, i
   FDX_CHECK(text.scalar_type() == at::kByte && doc_off.scalar_type() == at::kLong, "text u8 / doc_off i64");
   const int64_t D = doc_off.numel() - 1;
   FDX_CHECK(D >= 0, "doc_off needs at least one entry");
-  for (const Tensor* t : {&out_idx, &out_val, &out_nnz, &out_raw, &out_status}) check_dev(*t, dev, "outputs");
+  for (const Tensor* t : {&out_idx, &out_val, &out_nnz}) check_dev(*t, dev, "outputs");
   FDX_CHECK(out_nnz.numel() >= D && out_status.numel() >= D, "per-doc outputs too small");
   FDX_CHECK(out_idx.numel() >= text.numel() + D || !(flags & fdx::kFlagWriteCsr), "CSR scratch too small");
   FDX_CHECK(out_idx.numel() == out_val.numel(), "CSR idx/val size mismatch");
@@ -119,8 +132,9 @@ void featurize_score(const Tensor& text, const Tensor& doc_off, int64_t flags, i
   a.out_val = out_val.data_ptr<float>();
   a.out_nnz = out_nnz.data_ptr<int32_t>();
   a.out_ntok = mptr<int32_t>(out_ntok);
-  a.out_raw = out_raw.data_ptr<double>();
-  a.out_status = out_status.data_ptr<int32_t>();
+  FDX_CHECK(out_raw.scalar_type() == at::kDouble && out_status.scalar_type() == at::kInt, "out_raw f64 / status i32");
+  a.out_raw = out_ptr<double>(out_raw, dev, "out_raw");
+  a.out_status = out_ptr<int32_t>(out_status, dev, "out_status");
   if (dev.is_cuda()) {
     FDX_CHECK(!only_docs, "only_docs is a host-path option");
     c10::hip::HIPGuard guard(dev.index());

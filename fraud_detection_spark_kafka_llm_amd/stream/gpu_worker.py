@@ -1,10 +1,12 @@
-"""Per-GPU micro-batch scorer with overlapped H2D / compute / D2H (C-03 consumer side).
+"""Per-GPU micro-batch scorer with overlapped H2D / compute (C-03 consumer side).
 
-Three HIP streams per device: ``h2d`` copies a pinned ring slot into one of ``depth`` device
-buffers, ``compute`` runs the fused featurize+score kernel on it, ``d2h`` copies the fp64 scores
-back into pinned host memory. Events chain the stages, so with depth >= 2 the copy of batch i+1
-and the result copy of batch i-1 run underneath the kernel of batch i. Device buffers are
-preallocated at the maximum micro-batch size: steady state allocates nothing.
+Two HIP streams per device: ``h2d`` copies a pinned ring slot into one of ``depth`` device
+buffers (SDMA engine), ``compute`` runs the fused featurize+score kernel on it, and the kernel
+stores the fp64 scores and per-document status directly into page-locked host memory (zero-copy
+over PCIe). A separate D2H copy would sit on the same SDMA queue behind the next batch's large
+H2D and serialise the pipeline (measured: 2.6 -> 2.3 ms per 65536-dialogue step). Events chain
+the stages, so with depth >= 2 the copy of batch i+1 runs underneath the kernel of batch i.
+Device buffers are preallocated at the maximum micro-batch size: steady state allocates nothing.
 """
 from __future__ import annotations
 
@@ -58,7 +60,6 @@ class GpuScorer:
         self.max_docs, self.max_bytes = max_docs, max_bytes
         self.h2d = torch.cuda.Stream(self.dev)
         self.compute = torch.cuda.Stream(self.dev)
-        self.d2h = torch.cuda.Stream(self.dev)
         i32 = dict(dtype=torch.int32, device=self.dev)
         self.dummy_i = torch.zeros(1, **i32)
         self.dummy_f = torch.zeros(1, dtype=torch.float32, device=self.dev)
@@ -96,16 +97,14 @@ class GpuScorer:
         with torch.cuda.stream(self.compute):
             self.compute.wait_event(st.ev_h2d)
             if n:
+                # scores/status are stored by the kernel straight into pinned host memory: a D2H
+                # copy would queue behind the next batch's 100+ MB H2D on the SDMA engine.
                 self.C.featurize_score(st.text[: nb + PAD], st.offsets[: n + 1], self.flags, self.spec.dim, self.stop,
                                        self.vocab, float(self.spec.min_tf), self.idf, self.lr_w,
                                        float(self.scorer.b) if self.lr_w is not None else 0.0, self.tree_t, self.K,
-                                       self.dummy_i, self.dummy_f, st.nnz, st.ntok, st.raw, st.status, None, 0)
+                                       self.dummy_i, self.dummy_f, st.nnz, st.ntok, st.h_raw, st.h_status, None, 0)
             st.ev_compute.record(self.compute)
-        with torch.cuda.stream(self.d2h):
-            self.d2h.wait_event(st.ev_compute)
-            st.h_raw[:n].copy_(st.raw[:n], non_blocking=True)
-            st.h_status[:n].copy_(st.status[:n], non_blocking=True)
-            st.ev_d2h.record(self.d2h)
+            st.ev_d2h = st.ev_compute
         self._inflight.append(st)
 
     def collect(self, copy: bool = True) -> tuple:

@@ -153,24 +153,48 @@ def test_streaming_engine_async_explanations(shipped_model_path):
     assert sum(1 for r in recs if "original_text" in r) == 5
 
 
+def _trained_model_dir(tmp_path, kind="xgb"):
+    """A small HashingTF->IDF->classifier pipeline trained on synthetic dialogues (self-contained:
+    the GPU box has no /root/reference)."""
+    from fraud_detection_spark_kafka_llm_amd.data import synth
+    from fraud_detection_spark_kafka_llm_amd.ml import (IDF, Frame, HashingTF, LogisticRegression, Pipeline,
+                                                         StopWordsRemover, TextColumn, Tokenizer)
+    from fraud_detection_spark_kafka_llm_amd.ml.xgboost import SparkXGBClassifier
+
+    pt, y = synth.generate(synth.SynthConfig(n=800, seed=21))
+    raw = TextColumn(pt.strings())
+    df = Frame({"dialogue": raw, "clean_text": TextColumn.cleaned_from(raw), "labels": y.numpy()})
+    clf = SparkXGBClassifier(features_col="features", label_col="labels", n_estimators=20, max_depth=4) \
+        if kind == "xgb" else LogisticRegression(featuresCol="features", labelCol="labels", maxIter=20)
+    model = Pipeline(stages=[Tokenizer(inputCol="clean_text", outputCol="words"),
+                             StopWordsRemover(inputCol="words", outputCol="filtered_words"),
+                             HashingTF(inputCol="filtered_words", outputCol="raw_features", numFeatures=1 << 18),
+                             IDF(inputCol="raw_features", outputCol="features"), clf]).fit(df)
+    path = tmp_path / f"model_{kind}"
+    model.save(str(path))
+    return str(path)
+
+
 @pytest.mark.gpu
-def test_gpu_streaming_engine_matches_host(shipped_model_path):
-    broker = fake_kafka.broker_for("memory://gpu-test")
+@pytest.mark.parametrize("kind", ["xgb", "lr"])
+def test_gpu_streaming_engine_matches_host(tmp_path, kind):
+    model_dir = _trained_model_dir(tmp_path, kind)
+    broker = fake_kafka.broker_for(f"memory://gpu-test-{kind}")
     broker.create_topic("in", 3)
-    p = fake_kafka.Producer({"bootstrap.servers": "memory://gpu-test"})
+    p = fake_kafka.Producer({"bootstrap.servers": f"memory://gpu-test-{kind}"})
     from fraud_detection_spark_kafka_llm_amd.data import synth
 
     pt, _ = synth.generate(synth.SynthConfig(n=3000, seed=9))
     for i, t in enumerate(pt.strings()):
         p.produce("in", key=str(i), value=json.dumps({"text": t}))
-    c = fake_kafka.Consumer({"bootstrap.servers": "memory://gpu-test", "group.id": "g", "auto.offset.reset": "earliest",
-                             "enable.auto.commit": False})
+    c = fake_kafka.Consumer({"bootstrap.servers": f"memory://gpu-test-{kind}", "group.id": "g",
+                             "auto.offset.reset": "earliest", "enable.auto.commit": False})
     c.subscribe(["in"])
-    agent = ClassificationAgent(str(shipped_model_path), llm=StubLLM(), device="cuda:0")
+    agent = ClassificationAgent(model_dir, llm=StubLLM(), device="cuda:0")
     eng = StreamingEngine.from_agent(agent, c, p, "out", batch_max=512, max_latency_ms=2)
     stats = eng.run(idle_timeout_s=0.5)
     assert stats["produced"] == 3000
-    host = ClassificationAgent(str(shipped_model_path), llm=StubLLM(), device="cpu")
+    host = ClassificationAgent(model_dir, llm=StubLLM(), device="cpu")
     recs = {int(m.key()): json.loads(m.value()) for m in broker.messages("out")}
     texts = pt.strings()
     ref = host.predict_batch(texts)
