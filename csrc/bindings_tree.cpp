@@ -19,20 +19,24 @@ void chk(const Tensor& t, const at::Device& dev, at::ScalarType st, const char* 
   FDX_CHECK(t.scalar_type() == st, std::string(name) + " has wrong dtype");
 }
 
+// t's storage extends at least `extra` elements past the end of t (views into padded buffers)
+bool readable_tail(const Tensor& t, int64_t extra) {
+  const int64_t have = (int64_t)t.storage().nbytes() / (int64_t)t.element_size();
+  return t.storage_offset() + t.numel() + extra <= have;
+}
+
 template <class T>
 const T* opt(const optional<Tensor>& t) { return (t && t->defined()) ? t->data_ptr<T>() : nullptr; }
 
 hipStream_t stream(const at::Device& d) { return c10::hip::getCurrentHIPStream(d.index()).stream(); }
 
-void rowstate(const Tensor& row_node, const Tensor& node_slot, const optional<Tensor>& g, const optional<Tensor>& h,
-              const optional<Tensor>& label, const optional<Tensor>& weight, int64_t seed, int64_t tree,
-              bool bootstrap, int64_t mode, const Tensor& out) {
-  const auto dev = row_node.device();
-  chk(row_node, dev, at::kInt, "row_node");
-  chk(node_slot, dev, at::kInt, "node_slot");
-  chk(out, dev, at::kInt, "rowstate");
-  const int64_t N = row_node.numel();
-  FDX_CHECK(out.numel() == 4 * N, "rowstate must be [N,4] int32");
+void rowstats(const optional<Tensor>& g, const optional<Tensor>& h, const optional<Tensor>& label,
+              const optional<Tensor>& weight, int64_t seed, int64_t tree, bool bootstrap, int64_t mode,
+              const Tensor& out) {
+  const auto dev = out.device();
+  chk(out, dev, at::kInt, "rowstats");
+  FDX_CHECK(out.dim() == 2 && out.size(1) == 2, "rowstats must be [N,2] int32");
+  const int64_t N = out.size(0);
   if (mode == 0) {
     FDX_CHECK(g && h, "gbdt mode needs g,h");
     chk(*g, dev, at::kFloat, "g");
@@ -44,10 +48,7 @@ void rowstate(const Tensor& row_node, const Tensor& node_slot, const optional<Te
     FDX_CHECK(label->numel() == N, "label size");
   }
   if (weight) { chk(*weight, dev, at::kFloat, "weight"); FDX_CHECK(weight->numel() == N, "weight size"); }
-  fdx::RowStateArgs a{};
-  a.row_node = row_node.data_ptr<int32_t>();
-  a.node_slot = node_slot.data_ptr<int32_t>();
-  a.num_nodes = (int32_t)node_slot.numel();
+  fdx::RowStatsArgs a{};
   a.g = opt<float>(g);
   a.h = opt<float>(h);
   a.label = opt<float>(label);
@@ -57,19 +58,67 @@ void rowstate(const Tensor& row_node, const Tensor& node_slot, const optional<Te
   a.bootstrap = bootstrap ? 1 : 0;
   a.mode = (int32_t)mode;
   a.N = N;
-  a.rowstate = reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>());
+  a.rowstats = reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>());
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_rowstate(a, stream(dev));
+    fdx::launch_rowstats(a, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
-    fdx::rowstate_cpu(a);
+    fdx::rowstats_cpu(a);
   }
 }
 
-// Build histograms of the listed features for slots [slot_base, slot_base + 8*ct).
+// est[e] = rowstats[csc_row[e]] (once per tree)
+void entry_stats(const Tensor& csc_row, const Tensor& rowstats, const Tensor& est) {
+  const auto dev = csc_row.device();
+  chk(csc_row, dev, at::kInt, "csc_row");
+  chk(rowstats, dev, at::kInt, "rowstats");
+  chk(est, dev, at::kInt, "est");
+  const int64_t nnz = csc_row.numel();
+  FDX_CHECK(est.numel() >= 2 * nnz, "est must hold [nnz,2] int32");
+  FDX_CHECK(rowstats.dim() == 2 && rowstats.size(1) == 2, "rowstats must be [N,2]");
+  FDX_CHECK(reinterpret_cast<uintptr_t>(csc_row.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(est.data_ptr()) % 16 == 0,
+            "csc_row/est must be 16-byte aligned");
+  const auto* rs = reinterpret_cast<const uint32_t*>(rowstats.data_ptr<int32_t>());
+  auto* out = reinterpret_cast<uint32_t*>(est.data_ptr<int32_t>());
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_entry_stats(csc_row.data_ptr<int32_t>(), rs, nnz, out, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::entry_stats_cpu(csc_row.data_ptr<int32_t>(), rs, nnz, out);
+  }
+}
+
+// slot8[r] = node_slot[row_node[r]] - slot_base if in [0, nslots), else 0xff
+void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, int64_t nslots, const Tensor& out) {
+  const auto dev = row_node.device();
+  chk(row_node, dev, at::kInt, "row_node");
+  chk(node_slot, dev, at::kInt, "node_slot");
+  chk(out, dev, at::kByte, "slot8");
+  FDX_CHECK(out.numel() == row_node.numel(), "slot8 must be [N] uint8");
+  FDX_CHECK(nslots >= 0 && nslots <= 255, "at most 255 slots per pass");
+  fdx::SlotArgs a{};
+  a.row_node = row_node.data_ptr<int32_t>();
+  a.node_slot = node_slot.data_ptr<int32_t>();
+  a.num_nodes = (int32_t)node_slot.numel();
+  a.slot_base = (int32_t)slot_base;
+  a.nslots = (int32_t)nslots;
+  a.N = row_node.numel();
+  a.slot8 = out.data_ptr<uint8_t>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_slot8(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::slot8_cpu(a);
+  }
+}
+
+// Build histograms of the listed features for the 8*ct slots of one pass. slot8 = None: root pass
+// (every entry in slot 0).
 void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& csc_row, const Tensor& csc_bin,
-                const Tensor& rowstate, int64_t slot_base, int64_t bt, int64_t ct, const Tensor& slab,
+                const optional<Tensor>& slot8_t, const Tensor& est, int64_t bt, int64_t ct, const Tensor& slab,
                 const Tensor& feat, const Tensor& feat_item0, const Tensor& feat_nitems, const Tensor& boff,
                 const Tensor& nbins, const Tensor& slot_to_node, const Tensor& hist, int64_t TB) {
   const auto dev = csc_row.device();
@@ -77,7 +126,8 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   chk(item_end, dev, at::kLong, "item_end");
   chk(csc_row, dev, at::kInt, "csc_row");
   chk(csc_bin, dev, at::kByte, "csc_bin");
-  chk(rowstate, dev, at::kInt, "rowstate");
+  if (slot8_t) chk(*slot8_t, dev, at::kByte, "slot8");
+  chk(est, dev, at::kInt, "est");
   chk(feat, dev, at::kInt, "feat");
   chk(feat_item0, dev, at::kLong, "feat_item0");
   chk(feat_nitems, dev, at::kInt, "feat_nitems");
@@ -89,17 +139,23 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   FDX_CHECK(bt >= 1 && bt <= 2 && (ct == 1 || ct == 2 || ct == 4), "bt in {1,2}, ct in {1,2,4}");
   FDX_CHECK(slot_to_node.numel() == 8 * ct, "slot_to_node must have 8*ct entries");
   FDX_CHECK(csc_row.numel() == csc_bin.numel(), "csc arrays");
+  FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2]");
   FDX_CHECK(TB >= 0 && boff.numel() == nbins.numel() + 1, "boff must be [Fa+1]");
   FDX_CHECK(hist.numel() % (2 * std::max<int64_t>(TB, 1)) == 0, "hist must be [nodes, TB, 2]");
+  FDX_CHECK(reinterpret_cast<uintptr_t>(csc_row.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(est.data_ptr()) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(csc_bin.data_ptr()) % 4 == 0,
+            "csc_row/est must be 16-byte and csc_bin 4-byte aligned");
 
+  FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_bin, 4) && readable_tail(est, 8),
+            "csc_row/csc_bin/est need 4 readable padding entries behind their end (see quantize.CSC_PAD)");
   fdx::HistArgs h{};
   h.item_start = item_start.data_ptr<int64_t>();
   h.item_end = item_end.data_ptr<int64_t>();
   h.num_items = (int32_t)item_start.numel();
   h.csc_row = csc_row.data_ptr<int32_t>();
   h.csc_bin = csc_bin.data_ptr<uint8_t>();
-  h.rowstate = reinterpret_cast<const uint32_t*>(rowstate.data_ptr<int32_t>());
-  h.slot_base = (int32_t)slot_base;
+  h.slot8 = slot8_t ? slot8_t->data_ptr<uint8_t>() : nullptr;
+  h.est = reinterpret_cast<const uint32_t*>(est.data_ptr<int32_t>());
   fdx::HistReduceArgs r{};
   r.slab_slots = (int32_t)(8 * ct);
   r.slab_bins = (int32_t)(32 * bt);
@@ -110,7 +166,7 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   r.boff = boff.data_ptr<int64_t>();
   r.nbins = nbins.data_ptr<int32_t>();
   r.slot_to_node = slot_to_node.data_ptr<int32_t>();
-  r.slot_base = (int32_t)slot_base;
+  r.slot_base = 0;
   r.total_bins = TB;
   r.hist = hist.data_ptr<double>();
   if (dev.is_cuda()) {
@@ -276,7 +332,9 @@ void leaf_update(const Tensor& margin, const Tensor& row_node, const Tensor& nod
 }  // namespace
 
 void register_tree_ops(pybind11::module& m) {
-  m.def("tree_rowstate", &rowstate);
+  m.def("tree_rowstats", &rowstats);
+  m.def("tree_entry_stats", &entry_stats);
+  m.def("tree_slot8", &slot8);
   m.def("tree_hist_build", &hist_build);
   m.def("tree_hist_subtract", &hist_subtract);
   m.def("tree_split_find", &split_find);

@@ -34,12 +34,15 @@ template <class V> void launch_doc_freq(const int32_t* idx, const V* val, int64_
                                        hipStream_t stream);
 
 // ---------------------------------------------------------------- tree engine (tree_kernels.hip / tree_cpu.cpp)
-struct RowStateArgs;
+struct RowStatsArgs;
+struct SlotArgs;
 struct HistArgs;
 struct HistReduceArgs;
 struct SplitArgs;
 struct PartitionArgs;
-void launch_rowstate(const RowStateArgs& a, hipStream_t s);
+void launch_rowstats(const RowStatsArgs& a, hipStream_t s);
+void launch_entry_stats(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est, hipStream_t s);
+void launch_slot8(const SlotArgs& a, hipStream_t s);
 void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s);
 void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s);
 void launch_hist_subtract(const double* parent, double* cur, const int32_t* dst, const int32_t* par,
@@ -49,7 +52,9 @@ void launch_partition(const PartitionArgs& a, hipStream_t s);
 void launch_logistic_grad(const double* margin, const float* label, const float* weight, float* g, float* h,
                           int64_t N, hipStream_t s);
 void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s);
-void rowstate_cpu(const RowStateArgs& a);
+void rowstats_cpu(const RowStatsArgs& a);
+void entry_stats_cpu(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est);
+void slot8_cpu(const SlotArgs& a);
 void hist_cpu(const HistArgs& h, const HistReduceArgs& r, int slots);
 void hist_subtract_cpu(const double* parent, double* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
                        int32_t n_pairs, int64_t TB);

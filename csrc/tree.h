@@ -4,9 +4,13 @@
 //   * quantized CSC: for each active feature fid, entries [colptr[fid], colptr[fid+1]) hold
 //     (row int32, bin uint8) sorted by row; bins are ordered by value, bin zbin[fid] is the
 //     implicit "value == 0" bin for rows absent from the column;
-//   * rowstate[row] (16 B): slot of the node being built (or -1) + the two statistics the
-//     histogram sums, each split into bf16 hi/lo halves so one bf16 MFMA reproduces ~fp32 sums;
+//   * rowstats[row] (8 B): the two statistics the histogram sums, each split into bf16 hi/lo
+//     halves so one bf16 MFMA reproduces ~fp32 sums;
 //       GBDT: (g, h);  classification: (w*[y==0], w*[y==1]);
+//     gathered ONCE per tree into CSC entry order (est[e] = rowstats[csc_row[e]]), so every
+//     level streams them sequentially instead of gathering 16 B per entry per level;
+//   * slot8[row] (1 B): which of the <= 32 nodes built by the current histogram pass the row
+//     belongs to (0xff: none) -- N bytes, L2-resident, the only per-level random access;
 //   * histograms: hist[node][bin] = double2, bins of all features concatenated (boff[fid]).
 #pragma once
 #include <math.h>
@@ -16,10 +20,7 @@
 
 namespace fdx {
 
-struct RowStateArgs {
-  const int32_t* row_node;    // [N] current node id of each row
-  const int32_t* node_slot;   // [num_nodes] slot being built, -1 otherwise
-  int32_t num_nodes;
+struct RowStatsArgs {
   const float* g;             // GBDT gradients (mode 0)
   const float* h;
   const float* label;         // classification labels 0/1 (mode 1)
@@ -29,7 +30,17 @@ struct RowStateArgs {
   int32_t bootstrap;
   int32_t mode;               // 0 = gbdt, 1 = classification counts
   int64_t N;
-  uint32_t* rowstate;         // [N * 4]
+  uint32_t* rowstats;         // [N * 2]
+};
+
+struct SlotArgs {
+  const int32_t* row_node;    // [N] current node id of each row
+  const int32_t* node_slot;   // [num_nodes] slot being built (absolute), -1 otherwise
+  int32_t num_nodes;
+  int32_t slot_base;          // this pass covers slots [slot_base, slot_base + nslots)
+  int32_t nslots;
+  int64_t N;
+  uint8_t* slot8;             // [N] slot - slot_base, or 0xff
 };
 
 struct HistArgs {
@@ -38,8 +49,8 @@ struct HistArgs {
   int32_t num_items;
   const int32_t* csc_row;
   const uint8_t* csc_bin;
-  const uint32_t* rowstate;       // [N * 4]
-  int32_t slot_base;              // slots [slot_base, slot_base + 8*CT) handled by this launch
+  const uint8_t* slot8;           // [N] relative slot, 0xff = not built; nullptr = root pass (all slot 0)
+  const uint32_t* est;            // [nnz * 2] packed statistics in entry order
   float* slab;                    // [I][8*CT][32*BT][2]
 };
 

@@ -11,27 +11,40 @@
 
 namespace fdx {
 
-void rowstate_cpu(const RowStateArgs& a) {
+void rowstats_cpu(const RowStatsArgs& a) {
   parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
     for (int64_t r = lo; r < hi; ++r) {
-      const int32_t node = a.row_node[r];
-      const int32_t slot = (node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1;
-      uint32_t* st = a.rowstate + 4 * r;
-      st[0] = (uint32_t)slot;
-      st[3] = 0;
-      if (slot < 0) {
-        st[1] = st[2] = 0;
-      } else if (a.mode == 0) {
+      uint32_t* st = a.rowstats + 2 * r;
+      if (a.mode == 0) {
         const float w = a.weight ? a.weight[r] : 1.0f;
-        st[1] = split_bf16(a.g[r] * w);
-        st[2] = split_bf16(a.h[r] * w);
+        st[0] = split_bf16(a.g[r] * w);
+        st[1] = split_bf16(a.h[r] * w);
       } else {
         float w = a.weight ? a.weight[r] : 1.0f;
         if (a.bootstrap) w *= (float)poisson1(hash_uniform(a.seed, (uint64_t)a.tree, (uint64_t)r));
         const float y = a.label[r];
-        st[1] = split_bf16(w * (1.0f - y));
-        st[2] = split_bf16(w * y);
+        st[0] = split_bf16(w * (1.0f - y));
+        st[1] = split_bf16(w * y);
       }
+    }
+  });
+}
+
+void entry_stats_cpu(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est) {
+  parallel_for(nnz, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
+    for (int64_t e = lo; e < hi; ++e) {
+      est[2 * e] = rowstats[2 * (int64_t)csc_row[e]];
+      est[2 * e + 1] = rowstats[2 * (int64_t)csc_row[e] + 1];
+    }
+  });
+}
+
+void slot8_cpu(const SlotArgs& a) {
+  parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
+    for (int64_t r = lo; r < hi; ++r) {
+      const int32_t node = a.row_node[r];
+      const int32_t s = ((node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1) - a.slot_base;
+      a.slot8[r] = (s >= 0 && s < a.nslots) ? (uint8_t)s : (uint8_t)0xff;
     }
   });
 }
@@ -48,13 +61,12 @@ void hist_cpu(const HistArgs& h, const HistReduceArgs& r, int slots) {
       for (int i = 0; i < r.feat_nitems[li]; ++i) {
         const int64_t it = r.feat_item0[li] + i;
         for (int64_t e = h.item_start[it]; e < h.item_end[it]; ++e) {
-          const uint32_t* st = h.rowstate + 4 * (int64_t)h.csc_row[e];
-          const int s = (int)st[0] - h.slot_base;
-          if (s < 0 || s >= slots) continue;
+          const int s = h.slot8 ? (int)h.slot8[h.csc_row[e]] : 0;
+          if (s >= slots) continue;
           const int b = h.csc_bin[e];
           if (b >= nb) continue;
-          acc[((size_t)s * nb + b) * 2] += unpack(st[1]);
-          acc[((size_t)s * nb + b) * 2 + 1] += unpack(st[2]);
+          acc[((size_t)s * nb + b) * 2] += unpack(h.est[2 * e]);
+          acc[((size_t)s * nb + b) * 2 + 1] += unpack(h.est[2 * e + 1]);
         }
       }
       for (int s = 0; s < slots; ++s) {

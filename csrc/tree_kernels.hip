@@ -21,43 +21,107 @@ constexpr int kWave = 64;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 0x01 in every byte of x that is zero, 0x00 elsewhere (SWAR, no carries across bytes).
+__device__ __forceinline__ uint32_t match_bytes(uint32_t x) {
+  const uint32_t y = (x & 0x7f7f7f7fu) + 0x7f7f7f7fu;
+  return ~(y | x | 0x7f7f7f7fu) >> 7;
+}
+// bytes b0,b1 (lo) / b2,b3 (hi) of z -> b | b' << 16: one flag per 16-bit MFMA operand element,
+// then a 24-bit multiply turns each flag into the element value (0x3f80 = bf16 1.0, 0xffff mask).
+__device__ __forceinline__ uint32_t spread_lo(uint32_t z) { return __builtin_amdgcn_perm(z, z, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t spread_hi(uint32_t z) { return __builtin_amdgcn_perm(z, z, 0x0c030c02u); }
 
 __device__ __forceinline__ void lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 
-// ------------------------------------------------------------------ rowstate
-__global__ __launch_bounds__(256) void rowstate_kernel(RowStateArgs a) {
+// ------------------------------------------------------------------ per-tree / per-pass row state
+__global__ __launch_bounds__(256) void rowstats_kernel(RowStatsArgs a) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
-    const int32_t node = a.row_node[r];
-    const int32_t slot = (node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1;
-    uint4 st;
-    st.x = (uint32_t)slot;
-    st.w = 0;
-    if (slot < 0) {
-      st.y = st.z = 0;
-    } else if (a.mode == 0) {
+    uint2 st;
+    if (a.mode == 0) {
       const float w = a.weight ? a.weight[r] : 1.0f;
-      st.y = split_bf16(a.g[r] * w);
-      st.z = split_bf16(a.h[r] * w);
+      st.x = split_bf16(a.g[r] * w);
+      st.y = split_bf16(a.h[r] * w);
     } else {
       float w = a.weight ? a.weight[r] : 1.0f;
       if (a.bootstrap) w *= (float)poisson1(hash_uniform(a.seed, (uint64_t)a.tree, (uint64_t)r));
       const float y = a.label[r];
-      st.y = split_bf16(w * (1.0f - y));
-      st.z = split_bf16(w * y);
+      st.x = split_bf16(w * (1.0f - y));
+      st.y = split_bf16(w * y);
     }
-    reinterpret_cast<uint4*>(a.rowstate)[r] = st;
+    reinterpret_cast<uint2*>(a.rowstats)[r] = st;
   }
 }
 
+// est[e] = rowstats[csc_row[e]]: the one random gather of the tree (4 entries per thread).
+__global__ __launch_bounds__(256) void entry_stats_kernel(const int32_t* __restrict__ csc_row,
+                                                          const uint2* __restrict__ rowstats, int64_t nnz,
+                                                          uint2* __restrict__ est) {
+  const int64_t n4 = nnz / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int4 r = reinterpret_cast<const int4*>(csc_row)[i];
+    const uint2 a = rowstats[r.x], b = rowstats[r.y], c = rowstats[r.z], d = rowstats[r.w];
+    reinterpret_cast<uint4*>(est)[2 * i] = make_uint4(a.x, a.y, b.x, b.y);
+    reinterpret_cast<uint4*>(est)[2 * i + 1] = make_uint4(c.x, c.y, d.x, d.y);
+  }
+  const int64_t t = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < nnz) est[t] = rowstats[csc_row[t]];
+}
+
+__global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
+    const int32_t node = a.row_node[r];
+    const int32_t s = ((node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1) - a.slot_base;
+    a.slot8[r] = (s >= 0 && s < a.nslots) ? (uint8_t)s : (uint8_t)0xff;
+  }
+}
+
+// One lane's 4 consecutive entries of a histogram step: rows (root: 0 = valid, -1 = outside the
+// item), bins (0xff outside) and the packed statistics (0 outside). Branch-free, so the compiler
+// can keep the next step's loads in flight across the current step: lanes past the item's end
+// re-read its last 4-group (clamped address), and the CSC arrays carry >= 4 readable entries of
+// padding, so a 4-group never leaves the allocation.
+struct StepData {
+  int4 r4;
+  uint32_t bins4;
+  uint4 p, q;
+};
+
+template <bool ROOT>
+__device__ __forceinline__ void load_step(const HistArgs& a, int64_t e, int64_t e0, int64_t e1, int64_t e_last,
+                                          StepData& d) {
+  const int64_t el = e < e_last ? e : e_last;
+  const uint32_t bins = *reinterpret_cast<const uint32_t*>(a.csc_bin + el);
+  int4 r = make_int4(0, 0, 0, 0);
+  if constexpr (!ROOT) r = *reinterpret_cast<const int4*>(a.csc_row + el);
+  uint4 p = reinterpret_cast<const uint4*>(a.est)[el / 2];
+  uint4 q = reinterpret_cast<const uint4*>(a.est)[el / 2 + 1];
+  const bool v0 = e >= e0 && e < e1, v1 = e + 1 >= e0 && e + 1 < e1;
+  const bool v2 = e + 2 >= e0 && e + 2 < e1, v3 = e + 3 >= e0 && e + 3 < e1;
+  const uint32_t keep = (v0 ? 0xffu : 0u) | (v1 ? 0xff00u : 0u) | (v2 ? 0xff0000u : 0u) | (v3 ? 0xff000000u : 0u);
+  d.bins4 = (bins & keep) | ~keep;
+  d.r4 = make_int4(v0 ? r.x : -1, v1 ? r.y : -1, v2 ? r.z : -1, v3 ? r.w : -1);
+  d.p = make_uint4(v0 ? p.x : 0u, v0 ? p.y : 0u, v1 ? p.z : 0u, v1 ? p.w : 0u);
+  d.q = make_uint4(v2 ? q.x : 0u, v2 ? q.y : 0u, v3 ? q.z : 0u, v3 ? q.w : 0u);
+}
+
 // ------------------------------------------------------------------ MFMA histogram
-template <int BT, int CT>
+// One wave per work item (a chunk of one feature column); per step the wave takes 256 entries,
+// 4 consecutive ones per lane so that rows (int4), bins (u32) and statistics (2 x uint4) are
+// single vector loads. Only lanes with a live entry fetch statistics, and MFMA K-steps whose 16
+// entries belong to no built node are skipped (wave-uniform ballot test).
+// ROOT: the pass builds only the root, so every entry is live in slot 0 and neither rows nor
+// the slot table are read.
+template <int BT, int CT, bool ROOT>
 __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_bin[4][kWave];
-  __shared__ __attribute__((aligned(16))) int8_t s_slot[4][kWave];
-  __shared__ __attribute__((aligned(16))) uint16_t s_comp[4][4][kWave];
+  constexpr int G = 4 * kWave;
+  __shared__ __attribute__((aligned(16))) uint8_t s_bin[4][G + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_slot[4][G + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t s_comp[4][4][G + 16];
 
   const int wid = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
@@ -67,7 +131,7 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
 
   const int col = lane & 31;        // MFMA column / A-row index owned by this lane
   const int half = lane >> 5;       // k half (entries 8*half .. 8*half+7 of each 16-step)
-  const int comp = col & 3;         // 0 g_hi, 1 g_lo, 2 h_hi, 3 h_lo
+  const int comp = col & 3;         // 0 stat0_hi, 1 stat0_lo, 2 stat1_hi, 3 stat1_lo
   const int slot_sub = col >> 2;
 
   f32x16 acc[BT][CT];
@@ -78,53 +142,113 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[bt][ct][i] = 0.0f;
 
-  for (int64_t base = e0; base < e1; base += kWave) {
-    const int64_t e = base + lane;
-    uint8_t bin = 0xff;
-    int8_t slot = -1;
-    uint32_t y = 0, z = 0;
-    if (e < e1) {
-      const int32_t row = a.csc_row[e];
-      bin = a.csc_bin[e];
-      const uint4 st = reinterpret_cast<const uint4*>(a.rowstate)[row];
-      const int s = (int)st.x - a.slot_base;
-      if (s >= 0 && s < 8 * CT) { slot = (int8_t)s; y = st.y; z = st.z; }
+  const int64_t first = e0 & ~(int64_t)3;
+  const int64_t e_last = (e1 - 1) & ~(int64_t)3;   // last 4-group holding an entry of the item
+  StepData cur, nxt;
+  load_step<ROOT>(a, first + 4 * lane, e0, e1, e_last, cur);
+  for (int64_t base = first; base < e1; base += G) {
+    // slot of each of the lane's 4 entries (the only random access: slot8 is N bytes, L2-resident)
+    uint32_t slots4;
+    if constexpr (ROOT) {
+      slots4 = (cur.r4.x >= 0 ? 0u : 0xffu) | (cur.r4.y >= 0 ? 0u : 0xff00u) | (cur.r4.z >= 0 ? 0u : 0xff0000u) |
+               (cur.r4.w >= 0 ? 0u : 0xff000000u);
+    } else {
+      const uint32_t s0 = a.slot8[cur.r4.x >= 0 ? cur.r4.x : 0];
+      const uint32_t s1 = a.slot8[cur.r4.y >= 0 ? cur.r4.y : 0];
+      const uint32_t s2 = a.slot8[cur.r4.z >= 0 ? cur.r4.z : 0];
+      const uint32_t s3 = a.slot8[cur.r4.w >= 0 ? cur.r4.w : 0];
+      slots4 = (cur.r4.x >= 0 ? s0 : 0xffu) | ((cur.r4.y >= 0 ? s1 : 0xffu) << 8) |
+               ((cur.r4.z >= 0 ? s2 : 0xffu) << 16) | ((cur.r4.w >= 0 ? s3 : 0xffu) << 24);
     }
-    s_bin[wid][lane] = bin;
-    s_slot[wid][lane] = slot;
-    s_comp[wid][0][lane] = (uint16_t)(y & 0xffffu);
-    s_comp[wid][1][lane] = (uint16_t)(y >> 16);
-    s_comp[wid][2][lane] = (uint16_t)(z & 0xffffu);
-    s_comp[wid][3][lane] = (uint16_t)(z >> 16);
+    // prefetch the next step (clamped, so unconditional) while this one is staged and multiplied
+    load_step<ROOT>(a, base + G + 4 * lane, e0, e1, e_last, nxt);
+    const uint32_t bins4 = cur.bins4;
+    const bool any = slots4 != 0xffffffffu;
+    const uint32_t w[8] = {cur.p.x, cur.p.y, cur.p.z, cur.p.w, cur.q.x, cur.q.y, cur.q.z, cur.q.w};
+    // Stage the step's entries in LDS. Root: all entries live, stored in place. Otherwise only
+    // the live entries (row in a node built by this pass, ~half or fewer at deep levels, spread
+    // at random) are compacted to the front, so MFMA K-steps run on ceil(live / 16) groups.
+    unsigned long long live = 0;
+    int n_live = G;
+    if constexpr (ROOT) {
+      live = __ballot(any);
+      *reinterpret_cast<uint32_t*>(&s_bin[wid][4 * lane]) = bins4;
+      *reinterpret_cast<uint32_t*>(&s_slot[wid][4 * lane]) = slots4;
+      // comp c of entry j = 16-bit half (c & 1) of word (c >> 1) of entry j
+      *reinterpret_cast<uint2*>(&s_comp[wid][0][4 * lane]) =
+          make_uint2((w[0] & 0xffffu) | (w[2] << 16), (w[4] & 0xffffu) | (w[6] << 16));
+      *reinterpret_cast<uint2*>(&s_comp[wid][1][4 * lane]) =
+          make_uint2((w[0] >> 16) | (w[2] & 0xffff0000u), (w[4] >> 16) | (w[6] & 0xffff0000u));
+      *reinterpret_cast<uint2*>(&s_comp[wid][2][4 * lane]) =
+          make_uint2((w[1] & 0xffffu) | (w[3] << 16), (w[5] & 0xffffu) | (w[7] << 16));
+      *reinterpret_cast<uint2*>(&s_comp[wid][3][4 * lane]) =
+          make_uint2((w[1] >> 16) | (w[3] & 0xffff0000u), (w[5] >> 16) | (w[7] & 0xffff0000u));
+    } else {
+      int nb = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t sj = (slots4 >> (8 * j)) & 0xffu;
+        const unsigned long long bj = __ballot(sj != 0xffu);
+        if (sj != 0xffu) {
+          const int p = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bj, 0u));
+          s_bin[wid][p] = (uint8_t)(bins4 >> (8 * j));
+          s_slot[wid][p] = (uint8_t)sj;
+          s_comp[wid][0][p] = (uint16_t)w[2 * j];
+          s_comp[wid][1][p] = (uint16_t)(w[2 * j] >> 16);
+          s_comp[wid][2][p] = (uint16_t)w[2 * j + 1];
+          s_comp[wid][3][p] = (uint16_t)(w[2 * j + 1] >> 16);
+        }
+        nb += __popcll(bj);
+      }
+      n_live = nb;
+      // pad the last partial K-step: bin/slot 0xff match no row/column, so stale comps drop out
+      if (lane < 16) {
+        s_bin[wid][nb + lane] = 0xffu;
+        s_slot[wid][nb + lane] = 0xffu;
+      }
+    }
     lds_sync();
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < G / 16; ++ks) {
+      if constexpr (ROOT) {
+        if (((live >> (4 * ks)) & 0xfull) == 0ull) continue;   // lanes 4ks..4ks+3 hold these 16 entries
+      } else {
+        if (ks * 16 >= n_live) break;
+      }
       const int k0 = ks * 16 + 8 * half;
-      const uint64_t bins8 = *reinterpret_cast<const uint64_t*>(&s_bin[wid][k0]);
-      const uint64_t slots8 = *reinterpret_cast<const uint64_t*>(&s_slot[wid][k0]);
-      const s16x8 cv = *reinterpret_cast<const s16x8*>(&s_comp[wid][comp][k0]);
+      const uint2 bins8 = *reinterpret_cast<const uint2*>(&s_bin[wid][k0]);
+      const uint2 slots8 = *reinterpret_cast<const uint2*>(&s_slot[wid][k0]);
+      const uint4 cv = *reinterpret_cast<const uint4*>(&s_comp[wid][comp][k0]);
       bf16x8 A[BT];
 #pragma unroll
       for (int bt = 0; bt < BT; ++bt) {
-        s16x8 av;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          av[j] = (((bins8 >> (8 * j)) & 0xffu) == (uint64_t)(col + 32 * bt)) ? (short)0x3f80 : (short)0;
+        const uint32_t rep = (uint32_t)(col + 32 * bt) * 0x01010101u;
+        const uint32_t zl = match_bytes(bins8.x ^ rep), zh = match_bytes(bins8.y ^ rep);
+        const u32x4 av = {spread_lo(zl) * 0x3f80u, spread_hi(zl) * 0x3f80u,    // bf16 1.0 where bin == row
+                          spread_lo(zh) * 0x3f80u, spread_hi(zh) * 0x3f80u};
         A[bt] = __builtin_bit_cast(bf16x8, av);
       }
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        s16x8 bv;
-        const uint64_t want = (uint64_t)(ct * 8 + slot_sub);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bv[j] = (((slots8 >> (8 * j)) & 0xffu) == want) ? cv[j] : (short)0;
-        const bf16x8 B = __builtin_bit_cast(bf16x8, bv);
+        bf16x8 B;
+        if constexpr (ROOT) {
+          // one node: no slot mask; columns of slots 1..7 collect junk the reduce never reads
+          B = __builtin_bit_cast(bf16x8, cv);
+        } else {
+          const uint32_t rep = (uint32_t)(ct * 8 + slot_sub) * 0x01010101u;
+          const uint32_t zl = match_bytes(slots8.x ^ rep), zh = match_bytes(slots8.y ^ rep);
+          const u32x4 bv = {cv.x & (spread_lo(zl) * 0xffffu), cv.y & (spread_hi(zl) * 0xffffu),
+                            cv.z & (spread_lo(zh) * 0xffffu), cv.w & (spread_hi(zh) * 0xffffu)};
+          B = __builtin_bit_cast(bf16x8, bv);
+        }
 #pragma unroll
         for (int bt = 0; bt < BT; ++bt)
           acc[bt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
       }
     }
     lds_sync();
+    cur = nxt;
   }
 
   // C[row][col]: row = (reg&3) + 8*(reg>>2) + 4*half (+32*bt), col = lane&31.
@@ -137,123 +261,12 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const float v = acc[bt][ct][reg];
-        const float w = __shfl_xor(v, 1, kWave);
+        const float w2 = __shfl_xor(v, 1, kWave);
         if ((col & 1) == 0) {
           const int row = (reg & 3) + 8 * (reg >> 2) + 4 * half + 32 * bt;
           const int slot = ct * 8 + slot_sub;
           const int stat = (col >> 1) & 1;
-          out[((int64_t)slot * (32 * BT) + row) * 2 + stat] = v + w;
-        }
-      }
-}
-
-// v2: U groups of 64 entries are loaded per step (U dependent-gather chains in flight per wave
-// instead of one), and MFMA K-steps whose 16 entries belong to no built node are skipped
-// (wave-uniform ballot test), which at deep levels removes most of the VALU/MFMA work.
-template <int BT, int CT, int U>
-__global__ __launch_bounds__(256) void hist_mfma_v2_kernel(HistArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_bin[4][U * kWave];
-  __shared__ __attribute__((aligned(16))) int8_t s_slot[4][U * kWave];
-  __shared__ __attribute__((aligned(16))) uint16_t s_comp[4][4][U * kWave];
-
-  const int wid = threadIdx.x / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int item = blockIdx.x * 4 + wid;
-  if (item >= a.num_items) return;
-  const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
-
-  const int col = lane & 31;
-  const int half = lane >> 5;
-  const int comp = col & 3;
-  const int slot_sub = col >> 2;
-
-  f32x16 acc[BT][CT];
-#pragma unroll
-  for (int bt = 0; bt < BT; ++bt)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[bt][ct][i] = 0.0f;
-
-  for (int64_t base = e0; base < e1; base += U * kWave) {
-    int32_t row[U];
-    uint8_t bin[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = base + u * kWave + lane;
-      row[u] = (e < e1) ? a.csc_row[e] : -1;
-      bin[u] = (e < e1) ? a.csc_bin[e] : (uint8_t)0xff;
-    }
-    uint4 st[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      st[u] = make_uint4(0xffffffffu, 0, 0, 0);
-      if (row[u] >= 0) st[u] = reinterpret_cast<const uint4*>(a.rowstate)[row[u]];
-    }
-    unsigned long long live[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int s = (int)st[u].x - a.slot_base;
-      const bool ok = s >= 0 && s < 8 * CT;
-      live[u] = __ballot(ok);
-      const int k = u * kWave + lane;
-      s_bin[wid][k] = bin[u];
-      s_slot[wid][k] = ok ? (int8_t)s : (int8_t)-1;
-      s_comp[wid][0][k] = ok ? (uint16_t)(st[u].y & 0xffffu) : (uint16_t)0;
-      s_comp[wid][1][k] = ok ? (uint16_t)(st[u].y >> 16) : (uint16_t)0;
-      s_comp[wid][2][k] = ok ? (uint16_t)(st[u].z & 0xffffu) : (uint16_t)0;
-      s_comp[wid][3][k] = ok ? (uint16_t)(st[u].z >> 16) : (uint16_t)0;
-    }
-    lds_sync();
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (live[u] == 0ull) continue;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        if (((live[u] >> (16 * ks)) & 0xffffull) == 0ull) continue;
-        const int k0 = u * kWave + ks * 16 + 8 * half;
-        const uint64_t bins8 = *reinterpret_cast<const uint64_t*>(&s_bin[wid][k0]);
-        const uint64_t slots8 = *reinterpret_cast<const uint64_t*>(&s_slot[wid][k0]);
-        const s16x8 cv = *reinterpret_cast<const s16x8*>(&s_comp[wid][comp][k0]);
-        bf16x8 A[BT];
-#pragma unroll
-        for (int bt = 0; bt < BT; ++bt) {
-          s16x8 av;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            av[j] = (((bins8 >> (8 * j)) & 0xffu) == (uint64_t)(col + 32 * bt)) ? (short)0x3f80 : (short)0;
-          A[bt] = __builtin_bit_cast(bf16x8, av);
-        }
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          s16x8 bv;
-          const uint64_t want = (uint64_t)(ct * 8 + slot_sub);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) bv[j] = (((slots8 >> (8 * j)) & 0xffu) == want) ? cv[j] : (short)0;
-          const bf16x8 B = __builtin_bit_cast(bf16x8, bv);
-#pragma unroll
-          for (int bt = 0; bt < BT; ++bt)
-            acc[bt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
-        }
-      }
-    }
-    lds_sync();
-  }
-
-  float* out = a.slab + (int64_t)item * (8 * CT) * (32 * BT) * 2;
-#pragma unroll
-  for (int bt = 0; bt < BT; ++bt)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float v = acc[bt][ct][reg];
-        const float w = __shfl_xor(v, 1, kWave);
-        if ((col & 1) == 0) {
-          const int r = (reg & 3) + 8 * (reg >> 2) + 4 * half + 32 * bt;
-          const int slot = ct * 8 + slot_sub;
-          const int stat = (col >> 1) & 1;
-          out[((int64_t)slot * (32 * BT) + r) * 2 + stat] = v + w;
+          out[((int64_t)slot * (32 * BT) + row) * 2 + stat] = v + w2;
         }
       }
 }
@@ -366,35 +379,33 @@ inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
 }
 }  // namespace
 
-void launch_rowstate(const RowStateArgs& a, hipStream_t s) {
-  if (a.N <= 0) return;
-  hipLaunchKernelGGL(rowstate_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
+void launch_rowstats(const RowStatsArgs& a, hipStream_t s) {
+  if (a.N > 0) hipLaunchKernelGGL(rowstats_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
-int hist_kernel_version() {
-  static int v = [] {
-    const char* e = getenv("FDX_HIST_KERNEL");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
+void launch_entry_stats(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est, hipStream_t s) {
+  if (nnz <= 0) return;
+  hipLaunchKernelGGL(entry_stats_kernel, dim3(grid_for(nnz / 4 + 1, 16384)), dim3(256), 0, s, csc_row,
+                     reinterpret_cast<const uint2*>(rowstats), nnz, reinterpret_cast<uint2*>(est));
+}
+
+void launch_slot8(const SlotArgs& a, hipStream_t s) {
+  if (a.N > 0) hipLaunchKernelGGL(slot8_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
 void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s) {
   if (a.num_items <= 0) return;
   const dim3 grid((a.num_items + 3) / 4), block(256);
-  if (hist_kernel_version() == 1) {
-#define FDX_HIST_CASE(B, C) \
-  if (bt == B && ct == C) { hipLaunchKernelGGL((hist_mfma_kernel<B, C>), grid, block, 0, s, a); return; }
-    FDX_HIST_CASE(1, 1) FDX_HIST_CASE(1, 2) FDX_HIST_CASE(1, 4)
-    FDX_HIST_CASE(2, 1) FDX_HIST_CASE(2, 2) FDX_HIST_CASE(2, 4)
-#undef FDX_HIST_CASE
-    return;
+  const bool root = a.slot8 == nullptr;
+#define FDX_HIST_CASE(B, C)                                                                   \
+  if (bt == B && ct == C) {                                                                  \
+    if (root) hipLaunchKernelGGL((hist_mfma_kernel<B, C, true>), grid, block, 0, s, a);      \
+    else hipLaunchKernelGGL((hist_mfma_kernel<B, C, false>), grid, block, 0, s, a);          \
+    return;                                                                                  \
   }
-#define FDX_HIST2_CASE(B, C) \
-  if (bt == B && ct == C) { hipLaunchKernelGGL((hist_mfma_v2_kernel<B, C, 4>), grid, block, 0, s, a); return; }
-  FDX_HIST2_CASE(1, 1) FDX_HIST2_CASE(1, 2) FDX_HIST2_CASE(1, 4)
-  FDX_HIST2_CASE(2, 1) FDX_HIST2_CASE(2, 2) FDX_HIST2_CASE(2, 4)
-#undef FDX_HIST2_CASE
+  FDX_HIST_CASE(1, 1) FDX_HIST_CASE(1, 2) FDX_HIST_CASE(1, 4)
+  FDX_HIST_CASE(2, 1) FDX_HIST_CASE(2, 2) FDX_HIST_CASE(2, 4)
+#undef FDX_HIST_CASE
 }
 
 void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s) {

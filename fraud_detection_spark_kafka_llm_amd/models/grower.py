@@ -1,8 +1,9 @@
 """Level-wise histogram tree grower shared by DecisionTree, RandomForest and GBDT (X-09, X-10, X-13).
 
 Per level (all nodes of the level batched into every launch):
-  1. ``tree_rowstate``     pack (slot of the node being built, bf16 hi/lo statistics) per row
-  2. ``tree_hist_build``   MFMA histograms of the smaller child of each sibling pair (+ reduce)
+  1. ``tree_slot8``        1-byte slot of the node being built per row (0xff: not built)
+  2. ``tree_hist_build``   MFMA histograms of the smaller child of each sibling pair (+ reduce),
+                           streaming the per-tree entry-order statistics (``tree_entry_stats``)
   3. all-reduce            histograms of the built nodes across data-parallel ranks (RCCL)
   4. ``tree_hist_subtract`` larger sibling = parent - built sibling
   5. ``tree_split_find``   best (feature, bin) per (node, feature); argmax per node on device
@@ -23,7 +24,7 @@ import torch
 from ..ml.tree_model import Tree
 from ..ops import native
 from ..utils import tracing
-from .quantize import Quantized
+from .quantize import CSC_PAD, Quantized
 
 NEG_INF = float("-inf")
 
@@ -42,11 +43,14 @@ class GrowParams:
 
 
 class Workspace:
-    """Per-engine device buffers reused across trees (slab, rowstate, split outputs)."""
+    """Per-engine device buffers reused across trees (slab, row/entry statistics, slot table)."""
 
     def __init__(self, Q: Quantized, max_nodes_per_level: int):
         dev = Q.device
-        self.rowstate = torch.empty((Q.n_rows, 4), dtype=torch.int32, device=dev)
+        self.rowstats = torch.empty((Q.n_rows, 2), dtype=torch.int32, device=dev)
+        nnz = Q.csc_row.numel()
+        self.est = torch.zeros((nnz + CSC_PAD, 2), dtype=torch.int32, device=dev)[:nnz]
+        self.slot8 = torch.empty(Q.n_rows, dtype=torch.uint8, device=dev)
         self.row_node = torch.zeros(Q.n_rows, dtype=torch.int32, device=dev)
         self.max_items = max((g.num_items for g in Q.groups), default=0)
         self.slab = torch.empty(0, dtype=torch.float32, device=dev)
@@ -67,11 +71,8 @@ def _unpack_bf16_pair(col: torch.Tensor) -> torch.Tensor:
 
 
 def root_totals(ws: Workspace) -> torch.Tensor:
-    st = ws.rowstate
-    mask = st[:, 0] == 0
-    t0 = torch.where(mask, _unpack_bf16_pair(st[:, 1].to(torch.int64)), 0.0).sum()
-    t1 = torch.where(mask, _unpack_bf16_pair(st[:, 2].to(torch.int64)), 0.0).sum()
-    return torch.stack([t0, t1])
+    st = ws.rowstats.to(torch.int64)
+    return torch.stack([_unpack_bf16_pair(st[:, 0]).sum(), _unpack_bf16_pair(st[:, 1]).sum()])
 
 
 def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
@@ -95,11 +96,10 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     is_leaf = [False]
 
     ws.row_node.zero_()
-    node_slot = torch.full((max_nodes,), -1, dtype=torch.int32, device=dev)
-    node_slot[0] = 0
-    with tracing.span("tree.rowstate"):
-        C.tree_rowstate(ws.row_node, node_slot, g, h, label, weight, int(params.seed), int(tree_index),
-                        bool(bootstrap), mode_rs, ws.rowstate)
+    with tracing.span("tree.rowstats"):
+        C.tree_rowstats(g, h, label, weight, int(params.seed), int(tree_index), bool(bootstrap), mode_rs,
+                        ws.rowstats)
+        C.tree_entry_stats(Q.csc_row, ws.rowstats, ws.est)
     tot = root_totals(ws)
     if all_reduce is not None:
         tot = all_reduce(tot)
@@ -142,15 +142,12 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         local = {n: i for i, n in enumerate(open_nodes)}
         nl = len(open_nodes)
         cur_hist = torch.zeros((nl, TB, 2), dtype=torch.float64, device=dev)
-        # --- rowstate for the built nodes (slot = position in `build`)
+        # --- node -> slot of the built nodes (slot = position in `build`); the root pass needs none
         if d > 0:
             ns = torch.full((max_nodes,), -1, dtype=torch.int32)
             for s, n in enumerate(build):
                 ns[n] = s
             node_slot = ns.to(dev)
-            with tracing.span("tree.rowstate"):
-                C.tree_rowstate(ws.row_node, node_slot, g, h, label, weight, int(params.seed), int(tree_index),
-                                bool(bootstrap), mode_rs, ws.rowstate)
         # --- histograms, 8*ct slots per pass
         nb = len(build)
         with tracing.span("tree.hist"):
@@ -161,13 +158,17 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 for k in range(cnt):
                     s2n[k] = local[build[s0 + k]]
                 s2n = s2n.to(dev)
+                slot8 = None
+                if d > 0:
+                    C.tree_slot8(ws.row_node, node_slot, s0, cnt, ws.slot8)
+                    slot8 = ws.slot8
                 for grp in feat_groups:
                     gsel = grp if params.feat_prob >= 1.0 else _rf_subset(grp, Q, params, tree_index,
                                                                           [build[s0 + k] for k in range(cnt)])
                     if gsel.num_items == 0:
                         continue
                     slab = ws.slab_for(gsel.num_items, grp.bt, ct)
-                    C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, ws.rowstate, s0,
+                    C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est,
                                       grp.bt, ct, slab, gsel.feat, gsel.feat_item0, gsel.feat_nitems, Q.boff,
                                       Q.nbins, s2n, cur_hist, TB)
         if all_reduce is not None:

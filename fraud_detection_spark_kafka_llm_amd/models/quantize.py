@@ -24,6 +24,8 @@ from typing import Callable, Optional
 import numpy as np
 import torch
 
+CSC_PAD = 16
+
 CHUNK = 16384          # entries per histogram work item (one wavefront)
 
 
@@ -66,8 +68,8 @@ class Quantized:
     boff: torch.Tensor           # int64 [Fa+1]
     thresholds: np.ndarray       # float64 [TB]: split "bin <= b goes left" <=> "x <= thresholds[boff+b]"
     colptr: torch.Tensor         # int64 [Fa+1]
-    csc_row: torch.Tensor        # int32 [nnz]
-    csc_bin: torch.Tensor        # uint8 [nnz]
+    csc_row: torch.Tensor        # int32 [nnz] (view; CSC_PAD readable entries follow)
+    csc_bin: torch.Tensor        # uint8 [nnz] (view; CSC_PAD readable entries follow)
     groups: list = field(default_factory=list)
     boff_host: np.ndarray = None
     zbin_host: np.ndarray = None
@@ -133,8 +135,14 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
     fid, row, entry_bin = fid[keep], row[keep], entry_bin[keep]
     Fa = int(nbins.numel())
     order = torch.sort(fid.to(torch.int32), stable=True).indices
-    csc_row = row[order].contiguous()
-    csc_bin = entry_bin[order].to(torch.uint8).contiguous()
+    nnz = int(order.numel())
+    # the histogram kernel loads 4-entry groups without per-lane branches: keep CSC_PAD readable
+    # entries behind the end of both arrays (bin 0xff = no bin)
+    csc_row = torch.zeros(nnz + CSC_PAD, dtype=torch.int32, device=dev)
+    csc_row[:nnz] = row[order]
+    csc_bin = torch.full((nnz + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
+    csc_bin[:nnz] = entry_bin[order].to(torch.uint8)
+    csc_row, csc_bin = csc_row[:nnz], csc_bin[:nnz]
     cnt = torch.bincount(fid, minlength=Fa)
     colptr = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
     torch.cumsum(cnt, 0, out=colptr[1:])

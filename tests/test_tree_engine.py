@@ -142,41 +142,73 @@ def test_random_forest_bootstrap_and_sampling_are_deterministic():
 
 
 # --------------------------------------------------------------------------------------------- GPU
+def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
+    C = native.lib()
+    n = row_node_np.shape[0]
+    Q = quantize(vc.to(dev), max_bins=max_bins, chunk=509)   # odd chunk: unaligned item starts
+    ws = Workspace(Q, 64)
+    row_node = torch.from_numpy(row_node_np).to(dev)
+    node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
+    node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
+    node_slot = node_slot.to(dev)
+    gg = torch.from_numpy(np.linspace(-1, 1, n).astype(np.float32)).to(dev)
+    hh = torch.from_numpy(np.linspace(0.01, 0.25, n).astype(np.float32)).to(dev)
+    C.tree_rowstats(gg, hh, None, None, 0, 0, False, 0, ws.rowstats)
+    C.tree_entry_stats(Q.csc_row, ws.rowstats, ws.est)
+    hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.float64, device=dev)
+    for s0 in range(0, nslots, 8 * ct):
+        cnt = min(8 * ct, nslots - s0)
+        s2n = torch.full((8 * ct,), -1, dtype=torch.int32)
+        s2n[:cnt] = torch.arange(s0, s0 + cnt, dtype=torch.int32)
+        slot8 = None
+        if not root:
+            C.tree_slot8(row_node, node_slot, s0, cnt, ws.slot8)
+            slot8 = ws.slot8
+        for grp in Q.groups:
+            slab = ws.slab_for(grp.num_items, grp.bt, ct)
+            C.tree_hist_build(grp.item_start, grp.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est, grp.bt, ct,
+                              slab, grp.feat, grp.feat_item0, grp.feat_nitems, Q.boff, Q.nbins, s2n.to(dev),
+                              hist, Q.TB)
+    return hist.cpu().numpy()
+
+
+def test_host_histogram_matches_numpy():
+    """Host tree_hist_build (slot table + entry-order statistics) against a direct numpy sum."""
+    rng = np.random.default_rng(5)
+    n, F = 3000, 40
+    dense = (rng.random((n, F)) < 0.1) * rng.integers(1, 9, (n, F))
+    vc = vc_from_dense(dense.astype(np.float64))
+    row_node = rng.integers(-1, 7, n).astype(np.int32)
+    hist = _hist_on("cpu", vc, 16, 1, 5, row_node)
+    Q = quantize(vc, max_bins=16, chunk=509)
+    g = np.linspace(-1, 1, n).astype(np.float32).astype(np.float64)
+    colptr, rows, bins = Q.colptr.numpy(), Q.csc_row.numpy(), Q.csc_bin.numpy()
+    boff = Q.boff.numpy()
+    ref = np.zeros((5, Q.TB))
+    for f in range(Q.Fa):
+        e = np.arange(colptr[f], colptr[f + 1])
+        s = row_node[rows[e]]
+        ok = (s >= 0) & (s < 5)
+        np.add.at(ref, (s[ok], boff[f] + bins[e][ok]), g[rows[e][ok]])
+    np.testing.assert_allclose(hist[:, :, 0], ref, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("ct,nslots", [(1, 3), (2, 13), (4, 29)])
 @pytest.mark.parametrize("max_bins", [8, 64])
 def test_gpu_mfma_histograms_match_host(ct, nslots, max_bins):
-    C = native.lib()
     rng = np.random.default_rng(ct * 100 + max_bins)
     n, F = 20000, 300
     dense = (rng.random((n, F)) < 0.05) * rng.integers(1, 80, (n, F))
     vc = vc_from_dense(dense.astype(np.float64))
-    out = {}
-    for dev in ("cpu", "cuda:0"):
-        Q = quantize(vc.to(dev), max_bins=max_bins, chunk=512)
-        ws = Workspace(Q, 64)
-        row_node = torch.from_numpy(rng.integers(-1, nslots + 2, n).astype(np.int32) if dev == "cpu" else
-                                    out["row_node"]).to(dev)
-        out["row_node"] = row_node.cpu().numpy()
-        node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
-        node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
-        gg = torch.from_numpy(np.linspace(-1, 1, n).astype(np.float32)).to(dev)
-        hh = torch.from_numpy(np.linspace(0.01, 0.25, n).astype(np.float32)).to(dev)
-        C.tree_rowstate(row_node.contiguous(), node_slot.to(dev), gg, hh, None, None, 0, 0, False, 0, ws.rowstate)
-        hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.float64, device=dev)
-        for s0 in range(0, nslots, 8 * ct):
-            s2n = torch.full((8 * ct,), -1, dtype=torch.int32)
-            for k in range(min(8 * ct, nslots - s0)):
-                s2n[k] = s0 + k
-            for grp in Q.groups:
-                slab = ws.slab_for(grp.num_items, grp.bt, ct)
-                C.tree_hist_build(grp.item_start, grp.item_end, Q.csc_row, Q.csc_bin, ws.rowstate, s0, grp.bt, ct,
-                                  slab, grp.feat, grp.feat_item0, grp.feat_nitems, Q.boff, Q.nbins, s2n.to(dev),
-                                  hist, Q.TB)
-        out[dev] = hist.cpu().numpy()
-    # device chunks accumulate in fp32 (MFMA), host in fp64: allow fp32 rounding of the partials
-    scale = np.abs(out["cpu"]).max()
-    np.testing.assert_allclose(out["cuda:0"], out["cpu"], rtol=2e-6, atol=2e-7 * scale)
+    row_node = rng.integers(-1, nslots + 2, n).astype(np.int32)
+    for root in (False, True):
+        ns = 1 if root else nslots
+        a = _hist_on("cpu", vc, max_bins, ct, ns, row_node, root)
+        b = _hist_on("cuda:0", vc, max_bins, ct, ns, row_node, root)
+        # device chunks accumulate in fp32 (MFMA), host in fp64: allow fp32 rounding of the partials
+        scale = np.abs(a).max()
+        np.testing.assert_allclose(b, a, rtol=2e-6, atol=2e-7 * scale)
 
 
 @pytest.mark.gpu
