@@ -47,7 +47,8 @@ class _XGBParams:
                Param("eval_metric", "evaluation metric", "auc", str),
                Param("objective", "objective", "binary:logistic", str),
                Param("tree_method", "tree method", "hist", str),
-               Param("seed", "random seed", 0, int)]
+               Param("seed", "random seed", 0, int),
+               Param("deterministic", "bitwise-reproducible fixed-point gradients (any world size)", False, bool)]
 
     # ClassificationModelBase reads Spark-style column getters
     def getFeaturesCol(self):  # noqa: N802
@@ -83,7 +84,8 @@ class SparkXGBClassifier(_XGBParams, Estimator):
                        learning_rate=self.getOrDefault("learning_rate"), reg_lambda=self.getOrDefault("reg_lambda"),
                        gamma=self.getOrDefault("gamma"), min_child_weight=self.getOrDefault("min_child_weight"),
                        max_bin=self.getOrDefault("max_bin"), max_delta_step=self.getOrDefault("max_delta_step"),
-                       base_score=self._paramMap.get("base_score"), seed=self.getOrDefault("seed"))
+                       base_score=self._paramMap.get("base_score"), seed=self.getOrDefault("seed"),
+                       deterministic=bool(self.getOrDefault("deterministic")))
         w = frame.column(self.getOrDefault("weight_col")) if self.isSet("weight_col") else None
         res = fit_gbdt(frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol()), p, weights=w)
         m = SparkXGBClassifierModel(res.trees, res.num_features, res.base_margin, uid=self.uid)

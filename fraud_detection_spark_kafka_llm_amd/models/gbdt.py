@@ -41,6 +41,14 @@ class GBDTParams:
     max_delta_step: float = 0.0
     base_score: Optional[float] = None
     seed: int = 0
+    # Bitwise-reproducible training for any world size / reduction order: g and h (times the
+    # instance weight, which must be <= 1) are rounded to multiples of 2^-12 and histogram work
+    # items hold <= 4096 entries, so every fp32 MFMA partial and every fp64 reduction is exact.
+    deterministic: bool = False
+
+
+DET_SCALE = 4096.0          # 2^12 grid for g, h in deterministic mode
+DET_CHUNK = 4096            # entries per histogram item: |sum| <= 4096 * 4096 = 2^24 (exact in fp32)
 
 
 @dataclass
@@ -76,9 +84,12 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
         forced_base = float(resume_state["base_margin"])
     else:
         forced_base = None
-    Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll)
+    Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll,
+                          chunk=DET_CHUNK if params.deterministic else None)
     dev = Q.device
     w = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float32)).to(dev)
+    if params.deterministic and w is not None and float(w.max()) > 1.0:
+        raise ValueError("deterministic mode needs instance weights <= 1")
     N = Q.n_rows
     if forced_base is not None:
         base = forced_base
@@ -105,7 +116,10 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     for t in range(len(trees), params.n_estimators):
         with tracing.span("gbdt.round", round=t):
             C.tree_logistic_grad(margin, y, w, g, h)
-            tree = grow_tree(Q, ws, gp, t, g=g, h=h, all_reduce=coll.sum if coll.active else None)
+            if params.deterministic:
+                g.mul_(DET_SCALE).round_().div_(DET_SCALE)
+                h.mul_(DET_SCALE).round_().div_(DET_SCALE)
+            tree = grow_tree(Q, ws, gp, t, g=g, h=h, coll=coll)
             node_value = torch.from_numpy(np.ascontiguousarray(tree.stats[:, 0])).to(dev)
             C.tree_leaf_update(margin, ws.row_node, node_value)
         trees.append(tree.compacted())

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Callable, Optional
+from typing import Optional
 
 import numpy as np
 import torch
@@ -56,12 +56,81 @@ class Workspace:
         self.slab = torch.empty(0, dtype=torch.float32, device=dev)
         self.Fa = Q.Fa
         self.dev = dev
+        self.Q = Q
+        self._shards = None
+
+    def shards(self, coll) -> "FeatureShards":
+        if getattr(self, "_shards", None) is None or self._shards.S != coll.world:
+            self._shards = FeatureShards(self.Q, coll.world, coll.rank)
+        return self._shards
 
     def slab_for(self, items: int, bt: int, ct: int) -> torch.Tensor:
         need = items * 8 * ct * 32 * bt * 2
         if self.slab.numel() < need:
             self.slab = torch.empty(need, dtype=torch.float32, device=self.dev)
         return self.slab
+
+
+class FeatureShards:
+    """Split-find ownership for data-parallel training: rank r owns the contiguous feature range
+    [fs[r], fs[r+1]) (balanced by bin count). ``pack_idx`` reorders a [.., TB+1] histogram into
+    [S][Bs] equal-size chunks (pad bin TB is zero) for one reduce-scatter per level; the shard's
+    own boff/nbins/zbin/fid_orig drive the split kernel on the reduced slice."""
+
+    def __init__(self, Q: Quantized, S: int, rank: int):
+        boff = np.asarray(Q.boff_host, dtype=np.int64)
+        TB, Fa = int(boff[-1]), Q.Fa
+        cuts = np.searchsorted(boff, [TB * s / S for s in range(1, S)], side="left")
+        fs = np.concatenate([[0], np.clip(cuts, 0, Fa), [Fa]]).astype(np.int64)
+        fs = np.maximum.accumulate(fs)
+        lo, hi = boff[fs[:-1]], boff[fs[1:]]
+        self.S, self.fs = S, fs
+        self.Bs = max(1, int((hi - lo).max()))
+        idx = np.full(S * self.Bs, TB, dtype=np.int64)
+        for k in range(S):
+            idx[k * self.Bs: k * self.Bs + int(hi[k] - lo[k])] = np.arange(lo[k], hi[k])
+        dev = Q.device
+        self.pack_idx = torch.from_numpy(idx).to(dev)
+        f0, f1 = int(fs[rank]), int(fs[rank + 1])
+        self.f0, self.Fa, self.bins = f0, f1 - f0, int(hi[rank] - lo[rank])
+        self.boff = (Q.boff[f0: f1 + 1] - Q.boff[f0]).contiguous()
+        self.nbins = Q.nbins[f0:f1].contiguous()
+        self.zbin = Q.zbin[f0:f1].contiguous()
+        self.fid_orig = Q.fid_orig[f0:f1].contiguous()
+
+
+def _subtract(C, prev_hist, cur_hist, subtract, local, prev_index, TB):
+    """Larger sibling = parent - built sibling (sibling subtraction, K-11)."""
+    if not subtract:
+        return
+    dev = cur_hist.device
+    dst = torch.tensor([local[a] for a, _, _ in subtract], dtype=torch.int32, device=dev)
+    par = torch.tensor([prev_index[p] for _, p, _ in subtract], dtype=torch.int32, device=dev)
+    sib = torch.tensor([local[s] for _, _, s in subtract], dtype=torch.int32, device=dev)
+    C.tree_hist_subtract(prev_hist, cur_hist, dst, par, sib, TB)
+
+
+def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, params, tree_index, Fa, f0):
+    """Per node: (gain, feature (+f0), bin, left stat0, left stat1) of the best split over Fa
+    features of ``hist`` [nodes, boff[Fa], 2]; gain -inf when there is no valid candidate."""
+    dev = hist.device
+    nl = int(node_ids.numel())
+    if Fa == 0:
+        out = torch.zeros((nl, 5), dtype=torch.float64, device=dev)
+        out[:, 0] = NEG_INF
+        out[:, 1:3] = -1
+        return out
+    out_gain = torch.empty((nl, Fa), dtype=torch.float64, device=dev)
+    out_bin = torch.empty((nl, Fa), dtype=torch.int32, device=dev)
+    out_left = torch.empty((nl, Fa, 2), dtype=torch.float64, device=dev)
+    C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, int(params.mode), float(params.lambda_),
+                      float(params.min_child), float(params.feat_prob), int(params.seed), int(tree_index), out_gain,
+                      out_bin, out_left)
+    best_gain, best_f = torch.max(out_gain, dim=1)
+    ar = torch.arange(nl, device=dev)
+    best_bin = out_bin[ar, best_f]
+    best_left = out_left[ar, best_f]
+    return torch.cat([best_gain[:, None], (best_f + f0)[:, None].double(), best_bin[:, None].double(), best_left], 1)
 
 
 def _unpack_bf16_pair(col: torch.Tensor) -> torch.Tensor:
@@ -78,8 +147,13 @@ def root_totals(ws: Workspace) -> torch.Tensor:
 def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
               g: Optional[torch.Tensor] = None, h: Optional[torch.Tensor] = None,
               label: Optional[torch.Tensor] = None, weight: Optional[torch.Tensor] = None,
-              bootstrap: bool = False, all_reduce: Optional[Callable] = None) -> Tree:
+              bootstrap: bool = False, coll=None) -> Tree:
+    """``coll`` (parallel.dist.Collectives, world > 1): data-parallel level with feature-sharded
+    split finding -- partial histograms are reduce-scattered by feature shard, every rank searches
+    splits of its own shard, and the per-node best tuples are all-gathered (SURVEY PAR-02)."""
     C = native.lib()
+    shards = ws.shards(coll) if coll is not None and coll.active and coll.world > 1 else None
+    all_reduce = coll.sum if coll is not None and coll.active else None
     dev = Q.device
     mode_rs = 0 if params.mode == 0 else 1
     max_nodes = 2 ** (params.max_depth + 1)
@@ -141,7 +215,14 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                     build.append(b)
         local = {n: i for i, n in enumerate(open_nodes)}
         nl = len(open_nodes)
-        cur_hist = torch.zeros((nl, TB, 2), dtype=torch.float64, device=dev)
+        nb = len(build)
+        if shards is None:
+            cur_hist = torch.zeros((nl, TB, 2), dtype=torch.float64, device=dev)
+            hist_target, stride, target_of = cur_hist, TB, local
+        else:
+            # local partials of the built nodes (+1 zero pad bin for the shard packing)
+            hist_target = torch.zeros((nb, TB + 1, 2), dtype=torch.float64, device=dev)
+            stride, target_of = TB + 1, {n: k for k, n in enumerate(build)}
         # --- node -> slot of the built nodes (slot = position in `build`); the root pass needs none
         if d > 0:
             ns = torch.full((max_nodes,), -1, dtype=torch.int32)
@@ -149,14 +230,13 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 ns[n] = s
             node_slot = ns.to(dev)
         # --- histograms, 8*ct slots per pass
-        nb = len(build)
         with tracing.span("tree.hist"):
             for s0 in range(0, nb, 32):
                 cnt = min(32, nb - s0)
                 ct = 1 if cnt <= 8 else (2 if cnt <= 16 else 4)
                 s2n = torch.full((8 * ct,), -1, dtype=torch.int32)
                 for k in range(cnt):
-                    s2n[k] = local[build[s0 + k]]
+                    s2n[k] = target_of[build[s0 + k]]
                 s2n = s2n.to(dev)
                 slot8 = None
                 if d > 0:
@@ -170,34 +250,34 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                     slab = ws.slab_for(gsel.num_items, grp.bt, ct)
                     C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est,
                                       grp.bt, ct, slab, gsel.feat, gsel.feat_item0, gsel.feat_nitems, Q.boff,
-                                      Q.nbins, s2n, cur_hist, TB)
-        if all_reduce is not None:
-            with tracing.span("tree.allreduce"):
-                idx = torch.tensor([local[n] for n in build], device=dev)
-                part = cur_hist.index_select(0, idx)
-                part = all_reduce(part)
-                cur_hist.index_copy_(0, idx, part)
-        if subtract:
-            dst = torch.tensor([local[a] for a, _, _ in subtract], dtype=torch.int32, device=dev)
-            par = torch.tensor([prev_index[p] for _, p, _ in subtract], dtype=torch.int32, device=dev)
-            sib = torch.tensor([local[s] for _, _, s in subtract], dtype=torch.int32, device=dev)
-            C.tree_hist_subtract(prev_hist, cur_hist, dst, par, sib, TB)
-        # --- split search
+                                      Q.nbins, s2n, hist_target, stride)
         totals = torch.tensor(np.stack([stats[n] for n in open_nodes]), dtype=torch.float64, device=dev)
         node_ids = torch.tensor(open_nodes, dtype=torch.int32, device=dev)
-        out_gain = torch.empty((nl, Q.Fa), dtype=torch.float64, device=dev)
-        out_bin = torch.empty((nl, Q.Fa), dtype=torch.int32, device=dev)
-        out_left = torch.empty((nl, Q.Fa, 2), dtype=torch.float64, device=dev)
-        with tracing.span("tree.split"):
-            C.tree_split_find(cur_hist, totals, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, node_ids, int(params.mode),
-                              float(params.lambda_), float(params.min_child), float(params.feat_prob),
-                              int(params.seed), int(tree_index), out_gain, out_bin, out_left)
-            best_gain, best_f = torch.max(out_gain, dim=1)
-            ar = torch.arange(nl, device=dev)
-            best_bin = out_bin[ar, best_f]
-            best_left = out_left[ar, best_f]
-            packed = torch.cat([best_gain[:, None], best_f[:, None].double(), best_bin[:, None].double(), best_left], 1)
-            packed = packed.cpu().numpy()
+        if shards is None:
+            if all_reduce is not None:
+                with tracing.span("tree.allreduce"):
+                    idx = torch.tensor([local[n] for n in build], device=dev)
+                    cur_hist.index_copy_(0, idx, all_reduce(cur_hist.index_select(0, idx)))
+            _subtract(C, prev_hist, cur_hist, subtract, local, prev_index, TB)
+            with tracing.span("tree.split"):
+                packed = _best_splits(C, cur_hist, totals, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, node_ids, params,
+                                      tree_index, Q.Fa, 0)
+                packed = packed.cpu().numpy()
+        else:
+            with tracing.span("tree.reduce_scatter"):
+                cur_hist = torch.zeros((nl, shards.bins, 2), dtype=torch.float64, device=dev)
+                if nb:
+                    packed_in = hist_target.index_select(1, shards.pack_idx).view(nb, shards.S, shards.Bs, 2)
+                    mine = coll.reduce_scatter(packed_in.permute(1, 0, 2, 3))
+                    idx = torch.tensor([local[n] for n in build], device=dev)
+                    cur_hist.index_copy_(0, idx, mine[:, : shards.bins].contiguous())
+            _subtract(C, prev_hist, cur_hist, subtract, local, prev_index, shards.bins)
+            with tracing.span("tree.split"):
+                mine = _best_splits(C, cur_hist, totals, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
+                                    node_ids, params, tree_index, shards.Fa, shards.f0)
+                allt = coll.all_gather(mine)                       # [S, nl, 5]
+                best_s = torch.argmax(allt[:, :, 0], dim=0)        # ties -> lowest shard = lowest feature
+                packed = allt[best_s, torch.arange(nl, device=dev)].cpu().numpy()
         # --- create children
         next_level = []
         default_child = torch.full((max_nodes,), -1, dtype=torch.int32)

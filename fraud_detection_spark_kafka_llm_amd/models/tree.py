@@ -30,7 +30,7 @@ class ForestResult:
     num_features: int
 
 
-def prepare(features, labels, device=None, max_bins: int = 32, coll: Collectives = None):
+def prepare(features, labels, device=None, max_bins: int = 32, coll: Collectives = None, chunk: int = None):
     dev = torch.device(device) if device is not None else default_device()
     vc = features if isinstance(features, VectorColumn) else VectorColumn.from_rows(list(features))
     vc = vc.to(dev)
@@ -45,7 +45,8 @@ def prepare(features, labels, device=None, max_bins: int = 32, coll: Collectives
     with tracing.span("tree.quantize"):
         Q = quantize(vc, max_bins=max_bins, counts=counts, scale=scale,
                      all_reduce_max=coll.max if coll.active else None,
-                     all_gather=coll.gather_keys if coll.active else None)
+                     all_gather=coll.gather_keys if coll.active else None,
+                     **({"chunk": chunk} if chunk else {}))
     return Q, y, vc.size, vc
 
 
@@ -89,7 +90,6 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
     trees = []
     for t in range(num_trees):
         with tracing.span("forest.tree", tree=t):
-            tr = grow_tree(Q, ws, params, t, label=y, weight=w, bootstrap=bootstrap,
-                           all_reduce=coll.sum if coll.active else None)
+            tr = grow_tree(Q, ws, params, t, label=y, weight=w, bootstrap=bootstrap, coll=coll)
         trees.append(prune_same_prediction(tr) if prune else tr.compacted())
     return ForestResult(trees, F)

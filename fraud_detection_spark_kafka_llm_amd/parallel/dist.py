@@ -128,11 +128,50 @@ def shard_range(n: int, r: Optional[int] = None, w: Optional[int] = None) -> tup
     return lo, lo + base + (1 if r < extra else 0)
 
 
+def reduce_scatter(x: torch.Tensor) -> torch.Tensor:
+    """Sum ``x`` [world, ...] over ranks and return this rank's slice [...]. RCCL
+    ``reduce_scatter_tensor`` on nccl (each rank sends (N-1)/N of the buffer instead of an
+    all-reduce's 2(N-1)/N); gloo has no reduce-scatter, so it all-reduces and slices."""
+    if not is_dist():
+        return x[0]
+    x = x.contiguous()
+    if backend() == "nccl":
+        out = torch.empty(x.shape[1:], dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out, x)
+        return out
+    y = all_reduce_sum(x)
+    return y[rank()].clone()
+
+
+def all_gather(x: torch.Tensor) -> torch.Tensor:
+    """[...] on every rank -> [world, ...] (same shape on every rank)."""
+    if not is_dist():
+        return x.unsqueeze(0)
+    x = x.contiguous()
+    if backend() == "nccl":
+        out = torch.empty((world_size(),) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x)
+        return out
+    xc, moved = _on_comm_device(x)
+    bufs = [torch.empty_like(xc) for _ in range(world_size())]
+    dist.all_gather(bufs, xc)
+    out = torch.stack(bufs)
+    return out.to(x.device) if moved else out
+
+
 class Collectives:
     """Bundle of the collectives the trainers need (no-ops when not distributed)."""
 
     def __init__(self):
         self.active = is_dist()
+        self.world = world_size()
+        self.rank = rank()
+
+    def reduce_scatter(self, x):
+        return reduce_scatter(x) if self.active else x[0]
+
+    def all_gather(self, x):
+        return all_gather(x) if self.active else x.unsqueeze(0)
 
     def sum(self, t):
         return all_reduce_sum(t) if self.active else t

@@ -21,7 +21,7 @@ def _vc(dense):
     return VectorColumn(dense.shape[1], dense=torch.from_numpy(dense))
 
 
-def _train(rank, world, kind):
+def _train(rank, world, kind, deterministic=False):
     from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
     from fraud_detection_spark_kafka_llm_amd.models.lr import train_logistic_regression
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
@@ -31,7 +31,7 @@ def _train(rank, world, kind):
     lo, hi = shard_range(len(y), rank, world)
     vc, yy = _vc(dense[lo:hi]), torch.from_numpy(y[lo:hi])
     if kind == "gbdt":
-        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=6, max_depth=4), device="cpu")
+        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=6, max_depth=4, deterministic=deterministic), device="cpu")
         return [(t.feature.tolist(), t.stats[:, 0].tolist()) for t in r.trees], r.base_margin
     if kind == "rf":
         r = fit_forest(vc, yy, num_trees=3, max_depth=4, bootstrap=False, feature_subset="sqrt", seed=5, device="cpu")
@@ -56,6 +56,25 @@ def test_two_ranks_equal_single_process(kind):
         assert f1 == f2
         np.testing.assert_allclose(np.asarray(v1), np.asarray(v2), rtol=1e-6, atol=1e-9)
     assert dp[1] == pytest.approx(single[1])
+
+
+def test_three_ranks_feature_sharded_split_equals_single_process():
+    """world 3: uneven feature shards (reduce-scatter + all-gather of best splits) give the DP=1 trees."""
+    single = _train(0, 1, "rf")
+    outs = spawn(_train, 3, "rf", backend="gloo")
+    assert outs[0] == outs[1] == outs[2]
+    for (f1, v1), (f2, v2) in zip(outs[0][0], single[0]):
+        assert f1 == f2
+        np.testing.assert_allclose(np.asarray(v1), np.asarray(v2), rtol=1e-9)
+
+
+def test_deterministic_gbdt_is_bitwise_identical_across_world_sizes():
+    """Fixed-point g/h: DP=1, DP=2 and DP=3 produce bit-identical trees and leaf values."""
+    single = _train(0, 1, "gbdt", True)
+    for world in (2, 3):
+        outs = spawn(_train, world, "gbdt", True, backend="gloo")
+        assert all(o == outs[0] for o in outs)
+        assert outs[0] == single, f"world {world} differs from single process"
 
 
 def _idf_rank(rank, world):

@@ -227,3 +227,20 @@ def test_gpu_trees_match_host_trees():
     for ta, tb in zip(ga.trees, gb.trees):
         np.testing.assert_array_equal(ta.feature, tb.feature)
         np.testing.assert_allclose(ta.stats[:, 0], tb.stats[:, 0], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_deterministic_gbdt_bitwise_equals_host_and_repeats():
+    """Deterministic mode: every histogram sum is exact, so the MFMA device path and the fp64 host
+    path give bit-identical trees, and two device runs match bit for bit (race oracle)."""
+    dense, y = random_counts_matrix(4000, 80, 0.2, 13)
+    vc = vc_from_dense(dense)
+    p = GBDTParams(n_estimators=6, max_depth=5, deterministic=True)
+    host = fit_gbdt(vc, torch.from_numpy(y), p, device="cpu")
+    dev1 = fit_gbdt(vc, torch.from_numpy(y), p, device="cuda:0")
+    dev2 = fit_gbdt(vc, torch.from_numpy(y), p, device="cuda:0")
+    for a, b, c in zip(host.trees, dev1.trees, dev2.trees):
+        np.testing.assert_array_equal(a.feature, b.feature)
+        np.testing.assert_array_equal(a.stats, b.stats)
+        np.testing.assert_array_equal(b.stats, c.stats)
+        np.testing.assert_array_equal(b.threshold, c.threshold)
