@@ -89,6 +89,56 @@ fdx::TreeEnsemble make_trees(const optional<std::vector<Tensor>>& tr, int64_t K,
   return te;
 }
 
+// CountVectorizer fit (K-05): per kept token a 64-bit key (murmur3 seed 42 << 32 | murmur3 seed 2)
+// after clean / tokenize / stop-word removal. Without key_off/out_keys only the per-document token
+// counts are written (pass 1); with them the keys land at key_off[d] + i (pass 2).
+void token_keys(const Tensor& text, const Tensor& doc_off, int64_t flags, const optional<std::vector<Tensor>>& stop,
+                const Tensor& out_ntok, const Tensor& out_status, const optional<Tensor>& key_off,
+                const optional<Tensor>& out_keys, const optional<Tensor>& only_docs, int64_t threads) {
+  const auto dev = text.device();
+  check_dev(text, dev, "text");
+  check_dev(doc_off, dev, "doc_off");
+  check_dev(out_ntok, dev, "out_ntok");
+  check_dev(out_status, dev, "out_status");
+  FDX_CHECK(text.scalar_type() == at::kByte && doc_off.scalar_type() == at::kLong, "text u8 / doc_off i64");
+  const int64_t D = doc_off.numel() - 1;
+  FDX_CHECK(out_ntok.scalar_type() == at::kInt && out_status.scalar_type() == at::kInt && out_ntok.numel() >= D &&
+                out_status.numel() >= D, "out_ntok/out_status int32 [D]");
+  FDX_CHECK(key_off.has_value() == out_keys.has_value(), "key_off and out_keys go together");
+  if (out_keys) {
+    check_dev(*key_off, dev, "key_off");
+    check_dev(*out_keys, dev, "out_keys");
+    FDX_CHECK(key_off->scalar_type() == at::kLong && key_off->numel() >= D + 1, "key_off int64 [D+1]");
+    FDX_CHECK(out_keys->scalar_type() == at::kLong, "out_keys int64");
+  }
+  fdx::FeatArgs a{};
+  a.text = text.data_ptr<uint8_t>();
+  a.doc_off = doc_off.data_ptr<int64_t>();
+  a.num_docs = (int32_t)D;
+  a.flags = (int32_t)((flags & (fdx::kFlagClean | fdx::kFlagPreLowered | fdx::kFlagStopwords)) | fdx::kFlagKeys);
+  a.num_features = 1;
+  a.stop = make_table(stop, dev);
+  a.out_ntok = out_ntok.data_ptr<int32_t>();
+  a.out_status = out_status.data_ptr<int32_t>();
+  a.key_off = out_keys ? key_off->data_ptr<int64_t>() : nullptr;
+  a.out_keys = out_keys ? reinterpret_cast<uint64_t*>(out_keys->data_ptr<int64_t>()) : nullptr;
+  if (dev.is_cuda()) {
+    FDX_CHECK(!only_docs, "only_docs is a host-path option");
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_featurize_score(a, c10::hip::getCurrentHIPStream(dev.index()).stream());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    const int32_t* only = nullptr;
+    int32_t n_only = 0;
+    if (only_docs) {
+      FDX_CHECK(only_docs->scalar_type() == at::kInt && only_docs->is_contiguous(), "only_docs int32");
+      only = only_docs->data_ptr<int32_t>();
+      n_only = (int32_t)only_docs->numel();
+    }
+    fdx::featurize_score_cpu(a, only, n_only, (int)threads);
+  }
+}
+
 void featurize_score(const Tensor& text, const Tensor& doc_off, int64_t flags, int64_t num_features,
                      const optional<std::vector<Tensor>>& stop, const optional<std::vector<Tensor>>& vocab,
                      double min_tf, const optional<Tensor>& idf, const optional<Tensor>& lr_w, double lr_b,
@@ -297,6 +347,7 @@ void register_tree_ops(pybind11::module& m);
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native core of fraud_detection_spark_kafka_llm_amd";
   register_tree_ops(m);
+  m.def("token_keys", &token_keys, "CountVectorizer fit: 64-bit token keys (count pass / key pass)");
   m.def("featurize_score", &featurize_score, "Fused clean/tokenize/stopword/hash/idf/score");
   m.def("score_csr", &score_csr, "LR / tree-ensemble scoring of a CSR feature matrix");
   m.def("spmv", &spmv, "y = X x (CSR, fp64 accumulate)");

@@ -60,6 +60,9 @@ struct Murmur3 {
   }
 };
 
+// second seed of the 64-bit token key (murmur3 seed 42 in the high word, this in the low word)
+constexpr uint32_t kKeySeed2 = 0x9747b28cu;
+
 FDX_HD uint32_t murmur3_bytes(const uint8_t* p, uint32_t len, uint32_t seed) {
   Murmur3 m; m.init(seed);
   for (uint32_t i = 0; i < len; ++i) m.push(p[i]);
@@ -106,6 +109,7 @@ enum : int {
   kFlagStopwords = 1 << 7,    // apply stop-word filtering
   kFlagCmpLess = 1 << 8,      // tree split: go left iff x < thr (XGBoost); else x <= thr (Spark)
   kFlagPreLowered = 1 << 9,   // text already Unicode-lowercased by the host: pass UTF-8 through
+  kFlagKeys = 1 << 10,        // CountVectorizer fit: emit a 64-bit key per kept token (no vectors)
 };
 
 // Status codes written per document.

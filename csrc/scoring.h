@@ -83,6 +83,9 @@ struct FeatArgs {
   int32_t* out_ntok;         // [num_docs] tokens after stop-word removal (may be null)
   double* out_raw;           // [num_docs * K] (K = trees.K, or 1 for LR)
   int32_t* out_status;       // [num_docs]
+  // kFlagKeys: key of token i of doc d at out_keys[key_off[d] + i]; out_keys == nullptr -> count only
+  const int64_t* key_off;
+  uint64_t* out_keys;
 };
 
 }  // namespace fdx

@@ -55,9 +55,16 @@ void process_doc(const FeatArgs& a, int32_t d, std::string& clean, std::vector<u
   int32_t nall = 0;
   const bool use_vocab = (a.flags & kFlagVocab) != 0;
   const bool use_stop = (a.flags & kFlagStopwords) != 0;
+  const bool keys_mode = (a.flags & kFlagKeys) != 0;
   auto emit = [&](int64_t start, int64_t len) {
     const uint32_t h = murmur3_bytes(cb + start, (uint32_t)len, 42u);
     if (use_stop && table_find(a.stop, h, cb + start, (int32_t)len) >= 0) return;
+    if (keys_mode) {
+      if (a.out_keys)
+        a.out_keys[a.key_off[d] + nall] = ((uint64_t)h << 32) | murmur3_bytes(cb + start, (uint32_t)len, kKeySeed2);
+      ++nall;
+      return;
+    }
     ++nall;
     int32_t bucket = use_vocab ? table_find(a.vocab, h, cb + start, (int32_t)len)
                                : non_negative_mod(h, a.num_features);
@@ -73,6 +80,11 @@ void process_doc(const FeatArgs& a, int32_t d, std::string& clean, std::vector<u
     int64_t end = start;
     while (end < n && !delim(cb[end])) ++end;
     emit(start, end - start);
+  }
+  if (keys_mode) {
+    if (a.out_ntok) a.out_ntok[d] = nall;
+    a.out_status[d] = kStatusOk;
+    return;
   }
   std::sort(toks.begin(), toks.end());
   runs.clear();

@@ -160,18 +160,24 @@ __global__ __launch_bounds__(256) void featurize_score_kernel(FeatArgs a) {
   const bool use_vocab = (a.flags & kFlagVocab) != 0;
   const bool use_stop = (a.flags & kFlagStopwords) != 0;
 
+  const bool keys_mode = (a.flags & kFlagKeys) != 0;
   auto emit = [&](int start, bool valid) {
     int len = 0;
     bool keep_sw = false;   // survived stop-word removal
     int32_t bucket = -1;
+    uint32_t h = 0;
     if (valid) {
-      const uint32_t h = hash_token(s_clean, start, n, cleaned, &len);
+      h = hash_token(s_clean, start, n, cleaned, &len);
       keep_sw = !(use_stop && table_find(a.stop, h, s_clean + start, len) >= 0);
-      if (keep_sw)
+      if (keep_sw && !keys_mode)
         bucket = use_vocab ? table_find(a.vocab, h, s_clean + start, len)
                            : non_negative_mod(h, a.num_features);
     }
-    nall += __popcll(__ballot(keep_sw));
+    const unsigned long long sm = __ballot(keep_sw);
+    if (keys_mode && keep_sw && a.out_keys)
+      a.out_keys[a.key_off[d] + nall + popc_below(sm)] =
+          ((uint64_t)h << 32) | murmur3_bytes(s_clean + start, (uint32_t)len, kKeySeed2);
+    nall += __popcll(sm);
     const bool keep = keep_sw && bucket >= 0;
     const unsigned long long km = __ballot(keep);
     const int slot = ntok + popc_below(km);
@@ -204,6 +210,13 @@ __global__ __launch_bounds__(256) void featurize_score_kernel(FeatArgs a) {
       const int start = (lane < qn) ? s_q[lane] : 0;
       emit(start, lane < qn);
     }
+  }
+  if (keys_mode) {
+    if (lane == 0) {
+      if (a.out_ntok) a.out_ntok[d] = nall;
+      a.out_status[d] = kStatusOk;
+    }
+    return;
   }
   if (ntok > kCapT) {
     if (lane == 0) a.out_status[d] = kStatusTooLong;

@@ -132,7 +132,18 @@ class CountVectorizer(HasInOut, _CVParams, Estimator):
     _uid_prefix = "CountVectorizer"
 
     def _fit(self, frame: Frame) -> "CountVectorizerModel":
-        toks = _tokens_of(frame.column(self.getInputCol()))
+        col = frame.column(self.getInputCol())
+        if isinstance(col, TokenColumn) and col.fusable and len(col):
+            vocab = cv_fit_native(col, self.getVocabSize(), self.getMinDF(), self.getMaxDF())
+        else:
+            vocab = self._fit_python(_tokens_of(col))
+        m = CountVectorizerModel(vocab, uid=self.uid)
+        for k in ("inputCol", "outputCol", "minTF", "binary", "vocabSize", "minDF", "maxDF"):
+            if self.isSet(k):
+                m.set(k, self.getOrDefault(k))
+        return m
+
+    def _fit_python(self, toks: list) -> list:
         n_docs = len(toks)
         tf, df = Counter(), Counter()
         for t in toks:
@@ -147,12 +158,51 @@ class CountVectorizer(HasInOut, _CVParams, Estimator):
         # top vocabSize by corpus term count (Spark `top(vocSize)(Ordering.by(count))`);
         # ties broken by the term itself for determinism.
         cands.sort(key=lambda wc: (-wc[1], wc[0]))
-        vocab = [w for w, _ in cands[: self.getVocabSize()]]
-        m = CountVectorizerModel(vocab, uid=self.uid)
-        for k in ("inputCol", "outputCol", "minTF", "binary", "vocabSize", "minDF", "maxDF"):
-            if self.isSet(k):
-                m.set(k, self.getOrDefault(k))
-        return m
+        return [w for w, _ in cands[: self.getVocabSize()]]
+
+
+def _df_bounds(min_df: float, max_df: float, n_docs: int) -> tuple:
+    return (min_df if min_df >= 1.0 else min_df * n_docs), (max_df if max_df >= 1.0 else max_df * n_docs)
+
+
+def cv_fit_native(col: TokenColumn, vocab_size: int, min_df: float = 1.0, max_df: float = float(2 ** 63 - 1),
+                  device=None) -> list:
+    """CountVectorizer fit on the device (K-05, X-05): the fused text kernel emits a 64-bit key per
+    kept token, a device sort yields corpus term counts and document frequencies, the minDF/maxDF
+    filter and the top-``vocab_size`` selection run on device; only the selected terms are turned
+    back into strings, from the first document containing each (host re-tokenisation of those
+    documents only). Ordering: count descending, ties by term (same as the host fit)."""
+    from ..ops.text import term_doc_counts, token_key, token_keys
+
+    raw, clean = col.text.lineage()
+    spec = FeatureSpec(clean=clean, stopwords=col.stopwords, num_features=1)
+    dev = torch.device(device) if device is not None else default_device()
+    keys, ntok = token_keys(raw.packed(), spec, dev)
+    uk, tf, df, first = term_doc_counts(keys, ntok)
+    lo, hi = _df_bounds(min_df, max_df, int(ntok.numel()))
+    keep = (df.double() >= lo) & (df.double() <= hi)
+    uk, tf, first = uk[keep], tf[keep], first[keep]
+    if uk.numel() > vocab_size > 0:
+        kth = torch.topk(tf, vocab_size).values[-1]
+        sel = tf >= kth                                   # top-K plus the ties at the boundary
+        uk, tf, first = uk[sel], tf[sel], first[sel]
+    uk, tf, first = uk.cpu().numpy(), tf.cpu().numpy(), first.cpu().numpy()
+    want = {int(k): None for k in uk}
+    strings = raw.strings
+    for d in np.unique(first):
+        s = strings[int(d)] or ""
+        toks = oracle.tokenize(oracle.clean_text(s) if clean else s)
+        if col.stopwords is not None:
+            toks = oracle.remove_stopwords(toks, col.stopwords)
+        for t in toks:
+            k = token_key(t)
+            if k in want and want[k] is None:
+                want[k] = t
+    missing = [k for k, v in want.items() if v is None]
+    if missing:
+        raise RuntimeError(f"{len(missing)} token keys could not be mapped back to strings")
+    cands = sorted(((want[int(k)], int(c)) for k, c in zip(uk, tf)), key=lambda wc: (-wc[1], wc[0]))
+    return [w for w, _ in cands[:vocab_size]]
 
 
 @register("org.apache.spark.ml.feature.CountVectorizerModel")

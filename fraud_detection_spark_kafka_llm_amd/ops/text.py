@@ -375,3 +375,80 @@ def _finish_on_host(res: FeatureResult, text: PackedText, bad: np.ndarray, spec,
             dst = res.base[bad_t].cpu()[row] + within
             res.idx[dst.to(dev)] = idx[src].to(dev)
             res.val[dst.to(dev)] = val[src].to(dev)
+
+
+# ------------------------------------------------------------------ CountVectorizer fit (K-05)
+def _text_flags(spec: FeatureSpec) -> int:
+    return (FLAG_CLEAN if spec.clean else 0) | (FLAG_STOPWORDS if spec.stopwords else 0)
+
+
+def token_keys(text: PackedText, spec: FeatureSpec, device=None) -> tuple:
+    """64-bit key of every token kept by clean -> tokenize -> stop-word removal, in document order:
+    (keys int64 [T], ntok int64 [D]) on ``device``. Key = murmur3_x86_32(token, 42) << 32 |
+    murmur3_x86_32(token, 0x9747b28c). Two passes of the fused text kernel (count, then write at
+    the scanned offsets); documents the device path flags (too long / non-ASCII without cleaning)
+    are redone on the host path."""
+    C = native.lib()
+    device = torch.device(device) if device is not None else text.device
+    host_text = text
+    text = text.to(device, non_blocking=True)
+    D = len(text)
+    st = spec.stop_table()
+    stop = st.tensors(device) if st else None
+    flags = _text_flags(spec)
+    i32 = dict(dtype=torch.int32, device=device)
+    ntok, status = torch.zeros(D, **i32), torch.full((D,), -1, **i32)
+    C.token_keys(text.data, text.offsets, flags, stop, ntok, status, None, None, None, 0)
+    bad = torch.nonzero(status != STATUS_OK).flatten().cpu().numpy() if D else np.zeros(0, np.int64)
+    sub = sub_ntok = None
+    if bad.size:
+        strings = host_text.strings()
+        sub = PackedText.from_strings([(strings[int(i)] or "") if spec.clean else (strings[int(i)] or "").lower()
+                                       for i in bad])
+        sub_flags = flags | (0 if spec.clean else FLAG_PRELOWERED)
+        sub_ntok, sub_status = torch.zeros(len(bad), dtype=torch.int32), torch.full((len(bad),), -1, dtype=torch.int32)
+        stop_c = st.tensors(torch.device("cpu")) if st else None
+        C.token_keys(sub.data, sub.offsets, sub_flags, stop_c, sub_ntok, sub_status, None, None, None, 0)
+        ntok[torch.from_numpy(bad).to(device)] = sub_ntok.to(device)
+    n64 = ntok.to(torch.int64)
+    key_off = torch.zeros(D + 1, dtype=torch.int64, device=device)
+    torch.cumsum(n64, 0, out=key_off[1:])
+    keys = torch.empty(int(key_off[-1]) if D else 0, dtype=torch.int64, device=device)
+    status.fill_(-1)
+    C.token_keys(text.data, text.offsets, flags, stop, ntok, status, key_off, keys, None, 0)
+    if bad.size:
+        sub_off = torch.zeros(len(bad) + 1, dtype=torch.int64)
+        torch.cumsum(sub_ntok.to(torch.int64), 0, out=sub_off[1:])
+        sub_keys = torch.empty(int(sub_off[-1]), dtype=torch.int64)
+        C.token_keys(sub.data, sub.offsets, sub_flags, stop_c, sub_ntok, sub_status, sub_off, sub_keys, None, 0)
+        ko = key_off.cpu()
+        for j, i in enumerate(bad):
+            a, b = int(sub_off[j]), int(sub_off[j + 1])
+            keys[int(ko[i]): int(ko[i]) + (b - a)] = sub_keys[a:b].to(device)
+    return keys, n64
+
+
+def token_key(token: str) -> int:
+    """Host value of the device token key (for mapping keys back to strings), as signed int64."""
+    from . import oracle
+
+    b = token.encode("utf-8")
+    k = (oracle.murmur3_x86_32(b, 42) << 32) | oracle.murmur3_x86_32(b, 0x9747B28C)
+    return k - (1 << 64) if k >= (1 << 63) else k
+
+
+def term_doc_counts(keys: torch.Tensor, ntok: torch.Tensor) -> tuple:
+    """Distinct keys with corpus term count and document frequency (sorted by key)."""
+    dev = keys.device
+    D = int(ntok.numel())
+    if keys.numel() == 0:
+        z = torch.zeros(0, dtype=torch.int64, device=dev)
+        return z, z, z, z
+    uk, inv, tf = torch.unique(keys, sorted=True, return_inverse=True, return_counts=True)
+    doc = torch.repeat_interleave(torch.arange(D, device=dev, dtype=torch.int64), ntok, output_size=keys.numel())
+    pairs = torch.unique(doc * uk.numel() + inv)          # distinct (doc, term)
+    df = torch.bincount(pairs % uk.numel(), minlength=uk.numel())
+    # first document of every term (to recover its string)
+    first_doc = torch.full((uk.numel(),), D, dtype=torch.int64, device=dev)
+    first_doc.scatter_reduce_(0, inv, doc, reduce="amin")
+    return uk, tf, df, first_doc

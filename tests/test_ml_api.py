@@ -117,3 +117,47 @@ def test_lr_trainer_converges_on_separable_margin():
     np.testing.assert_allclose(coef, th[:5], rtol=1e-4, atol=1e-4)
     assert b == pytest.approx(th[5], abs=1e-4)
     assert hist[-1] <= hist[0]
+
+
+def _cv_corpus(n=400, seed=3):
+    from fraud_detection_spark_kafka_llm_amd.data import synth
+
+    pt, _ = synth.generate(synth.SynthConfig(n=n, seed=seed))
+    docs = pt.strings()
+    docs[3] = "Ünïcödé Straße CAFÉ café the THE"      # non-ASCII
+    docs[7] = ""                                     # empty
+    docs[11] = " ".join(["longword%d" % (i % 50) for i in range(1200)])   # > 4 KB (device cap)
+    return docs
+
+
+@pytest.mark.parametrize("clean", [True, False])
+def test_count_vectorizer_native_fit_equals_python_fit(clean):
+    from fraud_detection_spark_kafka_llm_amd.ml import CountVectorizer, StopWordsRemover, Tokenizer
+    from fraud_detection_spark_kafka_llm_amd.ml.frame import TokenColumn
+
+    raw = TextColumn(_cv_corpus())
+    text = TextColumn.cleaned_from(raw) if clean else raw
+    df = Frame({"t": text})
+    df = Tokenizer(inputCol="t", outputCol="w").transform(df)
+    df = StopWordsRemover(inputCol="w", outputCol="f").transform(df)
+    col = df.column("f")
+    assert isinstance(col, TokenColumn) and col.fusable
+    for kw in (dict(vocabSize=300), dict(vocabSize=50, minDF=3.0), dict(vocabSize=10_000, minDF=0.05, maxDF=0.9)):
+        cv = CountVectorizer(inputCol="f", outputCol="v", **kw)
+        native = cv.fit(df).vocabulary
+        python = cv._fit_python(col.tokens)
+        assert native == python, kw
+
+
+@pytest.mark.gpu
+def test_count_vectorizer_fit_on_gpu_equals_python_fit():
+    from fraud_detection_spark_kafka_llm_amd.ml import CountVectorizer, StopWordsRemover, Tokenizer
+    from fraud_detection_spark_kafka_llm_amd.ml.feature import cv_fit_native
+
+    raw = TextColumn(_cv_corpus(2000, 5))
+    df = Frame({"t": TextColumn.cleaned_from(raw)})
+    df = Tokenizer(inputCol="t", outputCol="w").transform(df)
+    df = StopWordsRemover(inputCol="w", outputCol="f").transform(df)
+    col = df.column("f")
+    cv = CountVectorizer(inputCol="f", outputCol="v", vocabSize=500, minDF=2.0)
+    assert cv_fit_native(col, 500, 2.0, device="cuda:0") == cv._fit_python(col.tokens)
