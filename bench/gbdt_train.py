@@ -22,7 +22,8 @@ from fraud_detection_spark_kafka_llm_amd.ops.sparse import doc_freq
 from fraud_detection_spark_kafka_llm_amd.utils import tracing
 
 
-def build_features(rows: int, dev, chunk: int = 500_000, num_features: int = 1 << 18, seed: int = 11):
+def build_features(rows: int, dev, chunk: int = 500_000, num_features: int = 1 << 18, seed: int = 11,
+                   first_row: int = 0):
     spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=num_features)
     ptrs, idxs, vals, labels = [], [], [], []
     t_gen = t_feat = 0.0
@@ -30,7 +31,7 @@ def build_features(rows: int, dev, chunk: int = 500_000, num_features: int = 1 <
     for start in range(0, rows, chunk):
         n = min(chunk, rows - start)
         t0 = time.perf_counter()
-        pt, y = synth.generate(synth.SynthConfig(n=n, seed=seed), device=dev, start=start)
+        pt, y = synth.generate(synth.SynthConfig(n=n, seed=seed), device=dev, start=first_row + start)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         res = T.featurize_score(pt, spec, want_csr=True, device=dev)

@@ -1,0 +1,201 @@
+"""Benchmarks for the BASELINE.json configs other than the bench.py headline (one JSON line each).
+
+  dt_cpu    DecisionTree pipeline on a 1,600-row dialogue CSV stand-in, CPU only (train.py flow)
+  gbdt_1m   HashingTF(2^18) -> IDF -> GBDT (100 trees, depth 6) on 1M synthetic dialogues, 1 GPU;
+            train seconds + held-out accuracy / weighted F1 / AUC
+  rf        RandomForest (500 trees, depth 5, sqrt features, Poisson bootstrap) on --rows rows
+            (default 10M = the BASELINE config's total on one GPU)
+  xgb       XGBoost-compatible GBDT with 1000 trees on --rows rows (default 12.5M = one rank's
+            shard of the 100M-row DP=8 config); train seconds + peak HBM
+  kafka     in-memory Kafka topic with 3 partitions -> StreamingEngine (pinned ring -> GPU fused
+            featurize+score) -> output topic, with explanations from the stub LLM; dialogues/s and
+            p50 / p95 batch latency
+
+Data are synthetic (data/synth.py); weights are trained, not random. Usage:
+  python bench/suite.py {dt_cpu,gbdt_1m,rf,xgb,kafka,all} [--rows N] [--trees T]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))   # bench/ (the repo root has bench.py)
+
+import numpy as np
+import torch
+
+from gbdt_train import build_features  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ml.tree_model import ensemble_arrays  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import doc_freq, score_csr  # noqa: E402
+
+F = 1 << 18
+
+
+def _metrics(y_true: np.ndarray, score: np.ndarray, pred: np.ndarray) -> dict:
+    from sklearn.metrics import accuracy_score, f1_score, roc_auc_score
+
+    return {"accuracy": float(accuracy_score(y_true, pred)), "f1": float(f1_score(y_true, pred, average="weighted")),
+            "auc": float(roc_auc_score(y_true, score))}
+
+
+def _tfidf(rows, dev, seed, first_row=0, idf=None):
+    indptr, idx, counts, y, _, _ = build_features(rows, dev, seed=seed, first_row=first_row)
+    if idf is None:
+        df = doc_freq(idx, counts, F)
+        idf = torch.log((rows + 1.0) / (df.double() + 1.0))
+    vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
+    vc.tf_counts, vc.tf_scale = counts, idf
+    return vc, y, idf
+
+
+def bench_dt_cpu(args) -> dict:
+    from fraud_detection_spark_kafka_llm_amd import train
+
+    os.environ["FDX_DEVICE"] = "cpu"
+    out = tempfile.mkdtemp()
+    t0 = time.perf_counter()
+    res = train.main(["--data", "", "--synthetic", "1600", "--no-plots", "--out-dir", out])
+    dt = time.perf_counter() - t0
+    return {"bench": "dt_cpu", "rows": 1600, "wall_s": dt, "device": "cpu",
+            "test": {m: res[m]["Test"] for m in res}}
+
+
+def bench_gbdt_1m(args) -> dict:
+    from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+
+    dev = torch.device("cuda:0")
+    rows = args.rows or 1_000_000
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vc, y, idf = _tfidf(rows, dev, seed=11)
+    torch.cuda.synchronize()
+    t_feat = time.perf_counter() - t0
+    res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees or 100, max_depth=6), device=dev)
+    torch.cuda.synchronize()
+    t_train = time.perf_counter() - t0
+    tv, ty, _ = _tfidf(200_000, dev, seed=11, first_row=10 ** 9, idf=idf)
+    m = res.base_margin + score_csr(tv, ensemble_arrays(res.trees, "value"))[:, 0]
+    m = m.cpu().numpy()
+    return {"bench": "gbdt_1m", "rows": rows, "trees": len(res.trees), "depth": 6, "featurize_s": t_feat,
+            "train_s": t_train, "heldout_rows": 200_000, **_metrics(ty.cpu().numpy(), m, (m > 0).astype(float))}
+
+
+def bench_rf(args) -> dict:
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+
+    dev = torch.device("cuda:0")
+    rows = args.rows or 10_000_000
+    trees = args.trees or 500
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vc, y, idf = _tfidf(rows, dev, seed=21)
+    torch.cuda.synchronize()
+    t_feat = time.perf_counter() - t0
+    res = fit_forest(vc, y, num_trees=trees, max_depth=5, max_bins=32, bootstrap=True, feature_subset="sqrt",
+                     seed=42, device=dev)
+    torch.cuda.synchronize()
+    t_train = time.perf_counter() - t0
+    tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
+    raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()
+    p1 = raw[:, 1] / np.maximum(raw.sum(1), 1e-300)
+    return {"bench": "rf", "rows": rows, "trees": trees, "depth": 5, "featurize_s": t_feat, "train_s": t_train,
+            "peak_hbm_gb": torch.cuda.max_memory_allocated() / 2 ** 30, "heldout_rows": 200_000,
+            **_metrics(ty.cpu().numpy(), p1, (raw[:, 1] > raw[:, 0]).astype(float))}
+
+
+def bench_xgb(args) -> dict:
+    from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+
+    dev = torch.device("cuda:0")
+    rows = args.rows or 12_500_000
+    trees = args.trees or 1000
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vc, y, idf = _tfidf(rows, dev, seed=31)
+    torch.cuda.synchronize()
+    t_feat = time.perf_counter() - t0
+    res = fit_gbdt(vc, y, GBDTParams(n_estimators=trees, max_depth=6), device=dev)
+    torch.cuda.synchronize()
+    t_train = time.perf_counter() - t0
+    return {"bench": "xgb", "rows": rows, "trees": trees, "depth": 6, "featurize_s": t_feat, "train_s": t_train,
+            "per_tree_ms": (t_train - t_feat) / trees * 1e3, "peak_hbm_gb": torch.cuda.max_memory_allocated() / 2 ** 30}
+
+
+def bench_kafka(args) -> dict:
+    from fraud_detection_spark_kafka_llm_amd.data import synth
+    from fraud_detection_spark_kafka_llm_amd.ml import (IDF, Frame, HashingTF, Pipeline, StopWordsRemover, TextColumn,
+                                                         Tokenizer)
+    from fraud_detection_spark_kafka_llm_amd.ml.xgboost import SparkXGBClassifier
+    from fraud_detection_spark_kafka_llm_amd.serve.agent import ClassificationAgent
+    from fraud_detection_spark_kafka_llm_amd.serve.llm import StubLLM
+    from fraud_detection_spark_kafka_llm_amd.stream import fake_kafka
+    from fraud_detection_spark_kafka_llm_amd.stream.engine import StreamingEngine
+
+    pt, y = synth.generate(synth.SynthConfig(n=20_000, seed=3))
+    raw = TextColumn(pt.strings())
+    df = Frame({"dialogue": raw, "clean_text": TextColumn.cleaned_from(raw), "labels": y.numpy()})
+    model = Pipeline(stages=[Tokenizer(inputCol="clean_text", outputCol="words"),
+                             StopWordsRemover(inputCol="words", outputCol="filtered_words"),
+                             HashingTF(inputCol="filtered_words", outputCol="raw_features", numFeatures=F),
+                             IDF(inputCol="raw_features", outputCol="features"),
+                             SparkXGBClassifier(features_col="features", label_col="labels", n_estimators=100,
+                                                max_depth=6)]).fit(df)
+    path = os.path.join(tempfile.mkdtemp(), "model")
+    model.save(path)
+    n = args.rows or 200_000
+    msgs, _ = synth.generate(synth.SynthConfig(n=n, seed=4), start=10 ** 8)
+    payloads = [json.dumps({"text": t}) for t in msgs.strings()]
+    out = {"bench": "kafka", "messages": n, "partitions": 3}
+    for explain in ("none", "async"):
+        url = f"memory://bench-{explain}"
+        broker = fake_kafka.broker_for(url)
+        broker.create_topic("customer-dialogues-raw", 3)
+        broker.create_topic("dialogues-classified", 3)
+        prod = fake_kafka.Producer({"bootstrap.servers": url})
+        for i, p in enumerate(payloads):
+            prod.produce("customer-dialogues-raw", key=str(i), value=p)
+        cons = fake_kafka.Consumer({"bootstrap.servers": url, "group.id": "bench", "auto.offset.reset": "earliest",
+                                    "enable.auto.commit": False})
+        cons.subscribe(["customer-dialogues-raw"])
+        agent = ClassificationAgent(path, llm=StubLLM(), device="cuda:0")
+        eng = StreamingEngine.from_agent(agent, cons, fake_kafka.Producer({"bootstrap.servers": url}),
+                                         "dialogues-classified", batch_max=4096, explain=explain)
+        t0 = time.perf_counter()
+        stats = eng.run(max_messages=n)
+        dt = time.perf_counter() - t0
+        lat = np.asarray(eng.stats.batch_latency_ms)
+        out[f"explain_{explain}"] = {"dialogues_per_s": n / dt, "p50_batch_ms": float(np.percentile(lat, 50)),
+                                     "p95_batch_ms": float(np.percentile(lat, 95)), "batches": stats["batches"],
+                                     "produced": stats["produced"]}
+    # single-dialogue classify latency through the agent API (the reference's "sub-second" claim)
+    agent = ClassificationAgent(path, llm=StubLLM(), device="cuda:0")
+    one = msgs.strings()[0]
+    lats = []
+    for _ in range(50):
+        t1 = time.perf_counter()
+        agent.predict_and_get_label(one)
+        lats.append((time.perf_counter() - t1) * 1e3)
+    out["agent_single_p50_ms"] = float(np.percentile(lats[5:], 50))
+    out["agent_single_p95_ms"] = float(np.percentile(lats[5:], 95))
+    return out
+
+
+BENCHES = {"dt_cpu": bench_dt_cpu, "gbdt_1m": bench_gbdt_1m, "rf": bench_rf, "xgb": bench_xgb, "kafka": bench_kafka}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("which", choices=list(BENCHES) + ["all"])
+    ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--trees", type=int, default=0)
+    args = ap.parse_args()
+    for name in (list(BENCHES) if args.which == "all" else [args.which]):
+        print(json.dumps(BENCHES[name](args)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

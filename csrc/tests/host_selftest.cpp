@@ -1,0 +1,227 @@
+// Host-path self-test for sanitizer builds: exercises the multi-threaded CPU
+// implementations (featurizer incl. token keys, JSON extraction, tree engine) on edge cases and
+// checks them against simple scalar references. Built with -fsanitize=address,undefined by
+// fraud_detection_spark_kafka_llm_amd/_build.py:build_host_selftest(); exits non-zero on failure.
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ops.h"
+#include "tree.h"
+
+using namespace fdx;
+
+static int g_fail = 0;
+#define EXPECT(c)                                                       \
+  do {                                                                  \
+    if (!(c)) { std::fprintf(stderr, "FAIL %s:%d %s\n", __FILE__, __LINE__, #c); ++g_fail; } \
+  } while (0)
+
+struct OwnedTable {
+  std::vector<int32_t> slots;
+  std::vector<uint32_t> hashes;
+  std::vector<int64_t> offs;
+  std::vector<uint8_t> bytes;
+  StrTable view() const { return StrTable{slots.data(), hashes.data(), offs.data(), bytes.data(), (int32_t)slots.size() - 1}; }
+};
+
+static OwnedTable make_table(const std::vector<std::string>& words) {
+  OwnedTable t;
+  size_t size = 16;
+  while (size < 2 * words.size()) size <<= 1;
+  t.slots.assign(size, -1);
+  t.offs.push_back(0);
+  for (size_t i = 0; i < words.size(); ++i) {
+    const auto* p = reinterpret_cast<const uint8_t*>(words[i].data());
+    const uint32_t h = murmur3_bytes(p, (uint32_t)words[i].size(), 42u);
+    t.hashes.push_back(h);
+    size_t j = h & (size - 1);
+    while (t.slots[j] >= 0) j = (j + 1) & (size - 1);
+    t.slots[j] = (int32_t)i;
+    t.bytes.insert(t.bytes.end(), p, p + words[i].size());
+    t.offs.push_back((int64_t)t.bytes.size());
+  }
+  t.bytes.push_back(0);
+  return t;
+}
+
+// scalar reference: lower + keep [a-z ], split on ' ' (Java semantics), drop stop words
+static std::vector<std::string> ref_tokens(const std::string& s, const std::vector<std::string>& stop) {
+  std::string c;
+  for (unsigned char ch : s) {
+    const unsigned char l = (ch >= 'A' && ch <= 'Z') ? ch + 32 : ch;
+    if ((l >= 'a' && l <= 'z') || l == ' ') c.push_back((char)l);
+  }
+  std::vector<std::string> parts;
+  size_t q = c.find_last_not_of(' ');
+  if (q == std::string::npos) {
+    if (c.empty()) parts.push_back("");
+  } else {
+    std::string cur;
+    for (size_t i = 0; i <= q; ++i) {
+      if (c[i] == ' ') { parts.push_back(cur); cur.clear(); } else { cur.push_back(c[i]); }
+    }
+    parts.push_back(cur);
+  }
+  std::vector<std::string> out;
+  for (auto& p : parts) {
+    bool sw = false;
+    for (auto& w : stop) sw = sw || (w == p);
+    if (!sw) out.push_back(p);
+  }
+  return out;
+}
+
+static void test_featurizer() {
+  const std::vector<std::string> stop = {"the", "a", "is"};
+  OwnedTable st = make_table(stop);
+  std::vector<std::string> docs = {"Hello World, the END is near!", "", "   ", "a  b  c ", "ABC d\xc3\xa9" "f 123",
+                                   "the the the", std::string(9000, 'x') + " tail words here"};
+  for (int i = 0; i < 200; ++i) docs.push_back("doc " + std::to_string(i) + " scam bank verify account please");
+  std::vector<uint8_t> text;
+  std::vector<int64_t> off = {0};
+  for (auto& d : docs) { text.insert(text.end(), d.begin(), d.end()); off.push_back((int64_t)text.size()); }
+  text.resize(text.size() + 16, 0);
+  const int64_t D = (int64_t)docs.size();
+  const int F = 1 << 10;
+
+  // 1. CSR counts (HashingTF) on 4 threads
+  std::vector<int32_t> idx(text.size() + D), nnz(D), ntok(D), status(D, -1);
+  std::vector<float> val(text.size() + D);
+  std::vector<double> raw(D);
+  FeatArgs a{};
+  a.text = text.data();
+  a.doc_off = off.data();
+  a.num_docs = (int32_t)D;
+  a.flags = kFlagClean | kFlagStopwords | kFlagWriteCsr;
+  a.num_features = F;
+  a.stop = st.view();
+  a.vocab.mask = -1;
+  a.min_tf = 1.0;
+  a.out_idx = idx.data();
+  a.out_val = val.data();
+  a.out_nnz = nnz.data();
+  a.out_ntok = ntok.data();
+  a.out_raw = raw.data();
+  a.out_status = status.data();
+  featurize_score_cpu(a, nullptr, 0, 4);
+  for (int64_t d = 0; d < D; ++d) {
+    EXPECT(status[d] == kStatusOk);
+    const auto toks = ref_tokens(docs[d], stop);
+    EXPECT(ntok[d] == (int32_t)toks.size());
+    std::map<int, double> ref;
+    for (auto& t : toks)
+      ref[non_negative_mod(murmur3_bytes(reinterpret_cast<const uint8_t*>(t.data()), (uint32_t)t.size(), 42u), F)] += 1;
+    EXPECT(nnz[d] == (int32_t)ref.size());
+    const int64_t base = off[d] + d;
+    for (int32_t j = 0; j < nnz[d] && j < (int32_t)ref.size(); ++j) EXPECT(ref.count(idx[base + j]) && ref[idx[base + j]] == val[base + j]);
+  }
+
+  // 2. token keys: count pass, then key pass at the scanned offsets
+  std::vector<int32_t> kt(D), ks(D, -1);
+  FeatArgs k = a;
+  k.flags = kFlagClean | kFlagStopwords | kFlagKeys;
+  k.out_ntok = kt.data();
+  k.out_status = ks.data();
+  featurize_score_cpu(k, nullptr, 0, 3);
+  std::vector<int64_t> koff(D + 1, 0);
+  for (int64_t d = 0; d < D; ++d) koff[d + 1] = koff[d] + kt[d];
+  std::vector<uint64_t> keys(koff[D]);
+  k.key_off = koff.data();
+  k.out_keys = keys.data();
+  featurize_score_cpu(k, nullptr, 0, 3);
+  for (int64_t d = 0; d < D; ++d) {
+    const auto toks = ref_tokens(docs[d], stop);
+    EXPECT(kt[d] == (int32_t)toks.size());
+    for (size_t i = 0; i < toks.size() && (int64_t)i < kt[d]; ++i) {
+      const auto* p = reinterpret_cast<const uint8_t*>(toks[i].data());
+      const uint64_t want = ((uint64_t)murmur3_bytes(p, (uint32_t)toks[i].size(), 42u) << 32) |
+                            murmur3_bytes(p, (uint32_t)toks[i].size(), kKeySeed2);
+      EXPECT(keys[koff[d] + i] == want);
+    }
+  }
+}
+
+static void test_json() {
+  const std::vector<std::string> msgs = {R"({"text": "hi \"there\" é\n"})", R"({"other": 1, "text":"x"})",
+                                         R"({"no": "field"})", "not json", R"({"text": 5})", ""};
+  std::vector<uint8_t> in;
+  std::vector<int64_t> off = {0};
+  for (auto& m : msgs) { in.insert(in.end(), m.begin(), m.end()); off.push_back((int64_t)in.size()); }
+  in.resize(in.size() + 16, 0);
+  std::vector<uint8_t> out(in.size() * 2 + 64);
+  std::vector<int64_t> out_off(msgs.size() + 1);
+  std::vector<int32_t> st(msgs.size());
+  const char* field = "text";
+  extract_json_field(in.data(), off.data(), (int64_t)msgs.size(), reinterpret_cast<const uint8_t*>(field), 4,
+                     out.data(), (int64_t)out.size(), out_off.data(), st.data(), 2);
+  EXPECT(st[0] == 0 && std::string(out.begin() + out_off[0], out.begin() + out_off[1]) == "hi \"there\" \xc3\xa9\n");
+  EXPECT(st[1] == 0 && std::string(out.begin() + out_off[1], out.begin() + out_off[2]) == "x");
+  EXPECT(st[2] != 0 && st[3] != 0 && st[4] != 0 && st[5] != 0);
+}
+
+static void test_tree() {
+  // 6 rows x 3 features, CSC with bins; stats g = row, h = 1
+  const int64_t N = 6;
+  const std::vector<int64_t> colptr = {0, 3, 5, 8};
+  std::vector<int32_t> rows = {0, 2, 5, 1, 2, 0, 3, 4};
+  std::vector<uint8_t> bins = {1, 2, 1, 1, 3, 2, 2, 1};
+  rows.resize(rows.size() + 16, 0);
+  bins.resize(bins.size() + 16, 0xff);
+  const int64_t nnz = 8;
+  std::vector<float> g(N), h(N, 1.0f);
+  for (int i = 0; i < N; ++i) g[i] = (float)i - 2.5f;
+  std::vector<uint32_t> rs(2 * N), est(2 * (nnz + 16));
+  RowStatsArgs ra{};
+  ra.g = g.data();
+  ra.h = h.data();
+  ra.N = N;
+  ra.rowstats = rs.data();
+  rowstats_cpu(ra);
+  entry_stats_cpu(rows.data(), rs.data(), nnz, est.data());
+  std::vector<int32_t> row_node = {0, 1, 0, 1, 0, 1}, node_slot = {0, 1};
+  std::vector<uint8_t> slot8(N);
+  SlotArgs sa{row_node.data(), node_slot.data(), 2, 0, 2, N, slot8.data()};
+  slot8_cpu(sa);
+  const std::vector<int64_t> item_start = {0, 3, 5}, item_end = {3, 5, 8}, feat_item0 = {0, 1, 2}, boff = {0, 4, 8, 12};
+  const std::vector<int32_t> feat = {0, 1, 2}, nitems = {1, 1, 1}, nbins = {4, 4, 4}, s2n = {0, 1};
+  std::vector<double> hist(2 * 12 * 2, 0.0);
+  HistArgs ha{};
+  ha.item_start = item_start.data();
+  ha.item_end = item_end.data();
+  ha.num_items = 3;
+  ha.csc_row = rows.data();
+  ha.csc_bin = bins.data();
+  ha.slot8 = slot8.data();
+  ha.est = est.data();
+  HistReduceArgs hr{};
+  hr.feat = feat.data();
+  hr.feat_item0 = feat_item0.data();
+  hr.feat_nitems = nitems.data();
+  hr.L = 3;
+  hr.boff = boff.data();
+  hr.nbins = nbins.data();
+  hr.slot_to_node = s2n.data();
+  hr.total_bins = 12;
+  hr.hist = hist.data();
+  hist_cpu(ha, hr, 2);
+  double ref[2][12] = {};
+  for (int f = 0; f < 3; ++f)
+    for (int64_t e = colptr[f]; e < colptr[f + 1]; ++e) ref[row_node[rows[e]]][boff[f] + bins[e]] += g[rows[e]];
+  for (int n = 0; n < 2; ++n)
+    for (int b = 0; b < 12; ++b) EXPECT(hist[((size_t)n * 12 + b) * 2] == ref[n][b]);
+}
+
+int main() {
+  test_featurizer();
+  test_json();
+  test_tree();
+  if (g_fail) {
+    std::fprintf(stderr, "%d failures\n", g_fail);
+    return 1;
+  }
+  std::printf("host selftest OK\n");
+  return 0;
+}

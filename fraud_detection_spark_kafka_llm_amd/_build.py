@@ -135,12 +135,45 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     return TARGET
 
 
+# identical private string literals that libstdc++ headers instantiate in several TUs trip ASan's
+# ODR check (false positive); every other check stays on, and UBSan findings abort.
+SELFTEST_ENV = {"ASAN_OPTIONS": "detect_odr_violation=0:abort_on_error=1:detect_leaks=1",
+                "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}
+HOST_SOURCES = ("text_cpu.cpp", "sparse_cpu.cpp", "tree_cpu.cpp", "json_text.cpp")
+
+
+def build_host_selftest(sanitize: bool = True, out: Path | None = None) -> Path:
+    """Debug target of SURVEY §5.2: the host (CPU) implementations + ``csrc/tests/host_selftest.cpp``
+    as a standalone executable, built with AddressSanitizer + UndefinedBehaviorSanitizer (host
+    code only: no device code is compiled into it)."""
+    hipcc = _hipcc()
+    out = out or (BUILD / ("host_selftest_asan" if sanitize else "host_selftest"))
+    out.parent.mkdir(parents=True, exist_ok=True)
+    flags = ["-O1", "-g", "-std=c++17", f"-I{CSRC}", "-I/opt/rocm/include", "-x", "c++", "-D__HIP_PLATFORM_AMD__=1",
+             "-pthread", "-ffp-contract=off", "-fno-omit-frame-pointer"]
+    if sanitize:
+        flags += ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-gpu-sanitize",
+                  ]
+    # one translation unit (unity build): inline functions of libstdc++ then exist once, so ASan
+    # does not see the same COMDAT string literal registered by several objects (false ODR report)
+    unity = out.parent / "host_selftest_unity.cpp"
+    unity.write_text("".join(f'#include "{CSRC / s}"\n' for s in HOST_SOURCES)
+                     + f'#include "{CSRC / "tests" / "host_selftest.cpp"}"\n')
+    link = ["-fsanitize=address,undefined"] if sanitize else []
+    _run([hipcc, *flags, str(unity), "-o", str(out), "-pthread", *link])
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--host-selftest", action="store_true", help="build + run the ASan/UBSan host self-test")
     args = ap.parse_args(argv)
+    if args.host_selftest:
+        exe = build_host_selftest()
+        return subprocess.run([str(exe)], env={**os.environ, **SELFTEST_ENV}).returncode
     path = build(force=args.force, jobs=args.jobs, verbose=args.verbose)
     print(f"built {path}")
     return 0
