@@ -98,13 +98,15 @@ class StreamingEngine:
         self._m_lat = REGISTRY.histogram("stream_batch_latency_ms")
 
     @classmethod
-    def from_agent(cls, agent, consumer, producer, output_topic, device=None, **kw) -> "StreamingEngine":
-        from .gpu_worker import make_scorer
+    def from_agent(cls, agent, consumer, producer, output_topic, device=None, devices=None, **kw) -> "StreamingEngine":
+        """``devices``: several GPUs of this process (round-robin micro-batches, MultiGpuScorer)."""
+        from .gpu_worker import make_multi_scorer
 
         fp = agent.fused
         idf = fp.idf.idf if fp.idf is not None else None
-        scorer = make_scorer(fp.spec(True), idf, fp.model.scorer(), device or agent.device,
-                             max_docs=kw.get("batch_max", 4096), max_bytes=kw.get("max_bytes", 64 << 20))
+        devs = list(devices) if devices else [device or agent.device]
+        scorer = make_multi_scorer(fp.spec(True), idf, fp.model.scorer(), devs,
+                                   max_docs=kw.get("batch_max", 4096), max_bytes=kw.get("max_bytes", 64 << 20))
         return cls(scorer, fp.model.postprocess, consumer, producer, output_topic, agent=agent, **kw)
 
     def stop(self) -> None:

@@ -190,3 +190,53 @@ def make_scorer(spec: FeatureSpec, idf, scorer, device, max_docs: int = 65536, m
     if device.type == "cuda":
         return GpuScorer(spec, idf, scorer, device, max_docs, max_bytes, depth)
     return HostScorer(spec, idf, scorer, max_docs, max_bytes, depth)
+
+
+class MultiGpuScorer:
+    """N per-device scorers behind the single-scorer interface (SURVEY PAR-06: partition
+    consumers -> one pinned ring -> N GPU workers). Inference needs no collectives: micro-batches
+    go round-robin to the devices and are collected in submission order, so downstream produce /
+    commit order is the consume order. Each device keeps its own ``depth``-deep copy/compute
+    pipeline, so up to ``sum(depth)`` micro-batches are in flight."""
+
+    def __init__(self, scorers: list):
+        if not scorers:
+            raise ValueError("need at least one scorer")
+        self.scorers = scorers
+        self.max_docs = min(s.max_docs for s in scorers)
+        self.max_bytes = min(s.max_bytes for s in scorers)
+        self._order: deque = deque()
+        self._rr = 0
+
+    @property
+    def depth(self) -> int:
+        return sum(s.depth for s in self.scorers)
+
+    @property
+    def inflight(self) -> int:
+        return len(self._order)
+
+    def submit(self, slot: Slot) -> None:
+        for _ in range(len(self.scorers)):
+            s = self.scorers[self._rr]
+            self._rr = (self._rr + 1) % len(self.scorers)
+            if s.inflight < s.depth:
+                s.submit(slot)
+                self._order.append(s)
+                return
+        raise RuntimeError("pipeline full: call collect() first")
+
+    def collect(self, copy: bool = True) -> tuple:
+        s = self._order.popleft()
+        return s.collect(copy=copy) if isinstance(s, GpuScorer) else s.collect()
+
+    def score_packed(self, slot: Slot) -> np.ndarray:
+        self.submit(slot)
+        return self.collect()[1]
+
+
+def make_multi_scorer(spec: FeatureSpec, idf, scorer, devices: list, max_docs: int = 65536,
+                      max_bytes: int = 256 << 20, depth: int = 2):
+    if len(devices) == 1:
+        return make_scorer(spec, idf, scorer, devices[0], max_docs, max_bytes, depth)
+    return MultiGpuScorer([make_scorer(spec, idf, scorer, d, max_docs, max_bytes, depth) for d in devices])

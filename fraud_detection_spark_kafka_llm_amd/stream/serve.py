@@ -1,0 +1,94 @@
+"""Streaming classification service (the reference's Streamlit tab-3 loop as a headless process,
+/root/reference/app_ui.py:168-248, without its per-message Spark job and without losing offsets).
+
+  python -m fraud_detection_spark_kafka_llm_amd.stream.serve --model dialogue_classification_model \
+      [--gpus N] [--explain none|sync|async] [--batch 4096] [--max-messages M] [--metrics-port 9108]
+
+Kafka settings come from the reference's environment variables (utils/kafka_utils.py; `.env` in the
+working directory is honoured): the consumer group reads KAFKA_INPUT_TOPIC, classifications go to
+KAFKA_OUTPUT_TOPIC as JSON {prediction, confidence, analysis, historical_insight, original_text}
+keyed like the input; offsets are committed after the outputs are produced (at-least-once).
+With --gpus N the micro-batches of the consumer are spread over N devices of this process.
+``/metrics`` serves the Prometheus text format of the metrics registry when --metrics-port is set.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import threading
+from http.server import BaseHTTPRequestHandler, HTTPServer
+
+import torch
+
+from ..utils.config import load_dotenv
+from ..utils.metrics import REGISTRY
+from .kafka import DEFAULT_OUTPUT, get_kafka_consumer, get_kafka_producer
+
+log = logging.getLogger("fdx.serve")
+
+
+def start_metrics_server(port: int) -> HTTPServer:
+    class Handler(BaseHTTPRequestHandler):
+        def do_GET(self):  # noqa: N802
+            if self.path.rstrip("/") not in ("/metrics", ""):
+                self.send_response(404)
+                self.end_headers()
+                return
+            body = REGISTRY.to_prometheus().encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "text/plain; version=0.0.4")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srv = HTTPServer(("0.0.0.0", port), Handler)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    return srv
+
+
+def main(argv=None) -> int:
+    from ..serve.agent import ClassificationAgent
+    from ..serve.llm import StubLLM, make_llm
+    from .engine import StreamingEngine
+
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--model", default="dialogue_classification_model")
+    ap.add_argument("--gpus", type=int, default=1, help="devices of this process (0 = CPU host path)")
+    ap.add_argument("--explain", choices=["none", "sync", "async"], default="none")
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--max-latency-ms", type=float, default=5.0)
+    ap.add_argument("--max-messages", type=int, default=None)
+    ap.add_argument("--idle-timeout", type=float, default=float("inf"), help="exit after this many idle seconds")
+    ap.add_argument("--metrics-port", type=int, default=0)
+    args = ap.parse_args(argv)
+    load_dotenv()
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    if args.gpus > 0 and torch.cuda.is_available():
+        devices = [torch.device("cuda", i) for i in range(min(args.gpus, torch.cuda.device_count()))]
+    else:
+        devices = [torch.device("cpu")]
+    llm = make_llm() if args.explain != "none" else StubLLM()   # no LLM calls without --explain
+    agent = ClassificationAgent(args.model, llm=llm, device=devices[0])
+    consumer, producer = get_kafka_consumer(), get_kafka_producer()
+    out_topic = os.getenv("KAFKA_OUTPUT_TOPIC", DEFAULT_OUTPUT)
+    if args.metrics_port:
+        start_metrics_server(args.metrics_port)
+    eng = StreamingEngine.from_agent(agent, consumer, producer, out_topic, devices=devices, batch_max=args.batch,
+                                     max_latency_ms=args.max_latency_ms, explain=args.explain)
+    log.info("serving %s on %s -> %s", args.model, [str(d) for d in devices], out_topic)
+    try:
+        stats = eng.run(max_messages=args.max_messages, idle_timeout_s=args.idle_timeout)
+    finally:
+        consumer.close()
+    print(json.dumps(stats), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -201,3 +201,50 @@ def test_gpu_streaming_engine_matches_host(tmp_path, kind):
     for i in range(0, 3000, 97):
         assert recs[i]["prediction"] == ref[i]["prediction"]
         assert recs[i]["confidence"] == pytest.approx(ref[i]["confidence"], rel=1e-12, abs=1e-15)
+
+
+def test_multi_scorer_round_robin_keeps_submission_order(tmp_path):
+    from fraud_detection_spark_kafka_llm_amd.ops.text import FeatureSpec, LinearScorer
+    from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import HostScorer, MultiGpuScorer
+    from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing
+
+    spec = FeatureSpec(clean=True, num_features=64)
+    w = np.arange(64, dtype=np.float64) / 64.0
+    scorers = [HostScorer(spec, None, LinearScorer(w, 0.1), max_docs=8, depth=2) for _ in range(3)]
+    multi = MultiGpuScorer(scorers)
+    assert multi.depth == 6
+    ring = PinnedRing(slots=6, max_docs=8, max_bytes=4096, pin=False)
+    single = HostScorer(spec, None, LinearScorer(w, 0.1), max_docs=8)
+    want, got = [], []
+    for i, slot in enumerate(ring.slots):
+        slot.fill([f"message {i} number {j} bank" for j in range(i + 1)])
+        want.append(single.score_packed(slot))
+        multi.submit(slot)
+    assert multi.inflight == 6
+    while multi.inflight:
+        got.append(multi.collect()[1])
+    for a, b in zip(want, got):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_serve_cli_consumes_classifies_and_commits(tmp_path, monkeypatch):
+    from fraud_detection_spark_kafka_llm_amd.stream import serve
+
+    model_dir = _trained_model_dir(tmp_path, "lr")
+    url = "memory://serve-cli"
+    monkeypatch.setenv("KAFKA_BOOTSTRAP_SERVERS", url)
+    monkeypatch.setenv("KAFKA_OUTPUT_TOPIC", "out")
+    broker = fake_kafka.broker_for(url)
+    broker.create_topic("customer-dialogues-raw", 3)
+    broker.create_topic("out", 3)
+    p = fake_kafka.Producer({"bootstrap.servers": url})
+    texts = ["please verify your bank account now", "see you at the dentist on friday", "urgent gift card payment"]
+    for i in range(300):
+        p.produce("customer-dialogues-raw", key=str(i), value=json.dumps({"text": texts[i % 3]}))
+    assert serve.main(["--model", model_dir, "--gpus", "0", "--max-messages", "300", "--idle-timeout", "2"]) == 0
+    c = fake_kafka.Consumer({"bootstrap.servers": url, "group.id": "check", "auto.offset.reset": "earliest"})
+    c.subscribe(["out"])
+    outs = c.consume(num_messages=1000, timeout=0.5)
+    assert len(outs) == 300
+    rec = json.loads(outs[0].value())
+    assert set(rec) >= {"prediction", "confidence", "analysis", "historical_insight", "original_text"}
