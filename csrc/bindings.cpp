@@ -325,6 +325,25 @@ void doc_freq(const Tensor& idx, const Tensor& val, const Tensor& df) {
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+// Python-json.dumps-identical output records of the streaming classifier (see json_encode.cpp).
+// Returns the total size, or -(needed size) when `out` is too small.
+int64_t encode_records(const Tensor& pred, const Tensor& conf, const Tensor& text, const Tensor& off,
+                       const optional<Tensor>& skip, const Tensor& out, const Tensor& out_off, const Tensor& status,
+                       int64_t threads) {
+  for (const Tensor* t : {&pred, &conf, &text, &off, &out, &out_off, &status})
+    FDX_CHECK(t->device().is_cpu() && t->is_contiguous(), "encode_records: contiguous host tensors");
+  const int64_t n = pred.numel();
+  FDX_CHECK(pred.scalar_type() == at::kDouble && conf.scalar_type() == at::kDouble && conf.numel() == n, "pred/conf f64 [n]");
+  FDX_CHECK(text.scalar_type() == at::kByte && off.scalar_type() == at::kLong && off.numel() >= n + 1, "text u8 / off i64 [n+1]");
+  FDX_CHECK(out.scalar_type() == at::kByte && out_off.scalar_type() == at::kLong && out_off.numel() >= n + 1, "out u8 / out_off i64");
+  FDX_CHECK(status.scalar_type() == at::kInt && status.numel() >= n, "status i32 [n]");
+  if (skip) FDX_CHECK(skip->scalar_type() == at::kInt && skip->numel() >= n && skip->is_contiguous(), "skip i32 [n]");
+  return fdx::encode_records(pred.data_ptr<double>(), conf.data_ptr<double>(), text.data_ptr<uint8_t>(),
+                             off.data_ptr<int64_t>(), skip ? skip->data_ptr<int32_t>() : nullptr, n,
+                             out.data_ptr<uint8_t>(), out.numel(), out_off.data_ptr<int64_t>(),
+                             status.data_ptr<int32_t>(), (int)threads);
+}
+
 int64_t extract_json_field(const Tensor& in, const Tensor& in_off, const std::string& field, const Tensor& out,
                            const Tensor& out_off, const Tensor& status, int64_t threads) {
   for (const Tensor* t : {&in, &in_off, &out, &out_off, &status})
@@ -353,6 +372,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spmv", &spmv, "y = X x (CSR, fp64 accumulate)");
   m.def("spmv_t", &spmv_t, "g += X^T r (CSR, fp64)");
   m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
+  m.def("encode_records", &encode_records, "json.dumps-identical classification records (batch)");
   m.def("extract_json_field", &extract_json_field, "Bulk JSON string-field extraction into a packed buffer");
   m.attr("gfx_arch") = "gfx950";
 }

@@ -67,6 +67,10 @@ void leaf_update_cpu(double* margin, const int32_t* row_node, const double* node
 int64_t extract_json_field(const uint8_t* in, const int64_t* in_off, int64_t n, const uint8_t* field, int64_t flen,
                            uint8_t* out, int64_t out_cap, int64_t* out_off, int32_t* status, int threads);
 
+int64_t encode_records(const double* pred, const double* conf, const uint8_t* text, const int64_t* off,
+                       const int32_t* skip, int64_t n, uint8_t* out, int64_t cap, int64_t* out_off, int32_t* status,
+                       int threads);
+
 template <class V> void score_csr_cpu(const CsrArgs<V>& a, int threads);
 template <class V> void spmv_cpu(const int64_t* indptr, const int32_t* idx, const V* val, const double* x, double* y,
                                  int64_t rows, int threads);

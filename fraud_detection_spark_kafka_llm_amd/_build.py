@@ -139,7 +139,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 # ODR check (false positive); every other check stays on, and UBSan findings abort.
 SELFTEST_ENV = {"ASAN_OPTIONS": "detect_odr_violation=0:abort_on_error=1:detect_leaks=1",
                 "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}
-HOST_SOURCES = ("text_cpu.cpp", "sparse_cpu.cpp", "tree_cpu.cpp", "json_text.cpp")
+HOST_SOURCES = ("text_cpu.cpp", "sparse_cpu.cpp", "tree_cpu.cpp", "json_text.cpp", "json_encode.cpp")
 
 
 def build_host_selftest(sanitize: bool = True, out: Path | None = None) -> Path:

@@ -96,6 +96,7 @@ class StreamingEngine:
         self._pool = cf.ThreadPoolExecutor(max_workers=8) if explain == "async" else None
         self._m_msgs = REGISTRY.counter("stream_messages_total")
         self._m_lat = REGISTRY.histogram("stream_batch_latency_ms")
+        self._enc_buf = torch.empty(1 << 22, dtype=torch.uint8)
 
     @classmethod
     def from_agent(cls, agent, consumer, producer, output_topic, device=None, devices=None, **kw) -> "StreamingEngine":
@@ -157,24 +158,33 @@ class StreamingEngine:
         _, prob, pred = self.postprocess(torch.from_numpy(raw))
         pred = pred.numpy()
         p1 = prob[:, 1].numpy()
-        texts = None
         offs = slot.offsets.numpy()
         data = slot.data.numpy()
-        for i, m in enumerate(msgs):
-            if status[i] != 0:
-                self.stats.bad_messages += 1
-                continue
-            text = bytes(data[offs[i]:offs[i + 1]]).decode("utf-8", "replace")
-            rec = {"prediction": float(pred[i]), "confidence": float(p1[i]), "analysis": None,
-                   "historical_insight": None}
-            if self.explain == "sync":
-                r = self.agent.classify_and_explain(text, prediction={"prediction": rec["prediction"],
-                                                                      "confidence": rec["confidence"]})
-                rec["analysis"], rec["historical_insight"] = r["analysis"], r["historical_insight"]
-            rec["original_text"] = text
-            self.producer.produce(self.topic, key=m.key(), value=json.dumps(rec))
-            if self.explain == "async":
-                self._pool.submit(self._explain_async, m.key(), text, rec["prediction"], rec["confidence"])
+        self.stats.bad_messages += int(np.sum(status != 0))
+        if self.explain == "sync":
+            keys, values = [], []
+            for i, m in enumerate(msgs):
+                if status[i] != 0:
+                    continue
+                text = bytes(data[offs[i]:offs[i + 1]]).decode("utf-8", "replace")
+                r = self.agent.classify_and_explain(text, prediction={"prediction": float(pred[i]),
+                                                                      "confidence": float(p1[i])})
+                keys.append(m.key())
+                values.append(json.dumps({"prediction": float(pred[i]), "confidence": float(p1[i]),
+                                          "analysis": r["analysis"], "historical_insight": r["historical_insight"],
+                                          "original_text": text}))
+        else:
+            keys, values = self._encode_outputs(msgs, status, pred, p1, slot.data, slot.offsets)
+        if hasattr(self.producer, "produce_batch"):
+            self.producer.produce_batch(self.topic, keys, values)
+        else:
+            for k, v in zip(keys, values):
+                self.producer.produce(self.topic, key=k, value=v)
+        if self.explain == "async":
+            for i, m in enumerate(msgs):
+                if status[i] == 0:
+                    text = bytes(data[offs[i]:offs[i + 1]]).decode("utf-8", "replace")
+                    self._pool.submit(self._explain_async, m.key(), text, float(pred[i]), float(p1[i]))
         self.producer.poll(0)
         self.producer.flush()
         self.stats.produced += int(np.sum(status == 0))
@@ -192,6 +202,38 @@ class StreamingEngine:
         self.stats.batches += 1
         slot.meta = None
         self.ring.release(slot)
+
+    def _encode_outputs(self, msgs, status, pred, p1, data: torch.Tensor, offsets: torch.Tensor) -> tuple:
+        """Output values {prediction, confidence, analysis: null, historical_insight: null,
+        original_text} for the whole micro-batch in one native call (json.dumps-identical bytes);
+        records whose text is not valid UTF-8 are encoded here with the "replace" decoding."""
+        n = len(msgs)
+        C = native.lib()
+        pred_t = torch.from_numpy(np.ascontiguousarray(pred, dtype=np.float64))
+        conf_t = torch.from_numpy(np.ascontiguousarray(p1, dtype=np.float64))
+        skip = torch.from_numpy(np.ascontiguousarray(status != 0, dtype=np.int32))
+        out_off = torch.empty(n + 1, dtype=torch.int64)
+        st = torch.empty(n, dtype=torch.int32)
+        need = C.encode_records(pred_t, conf_t, data, offsets, skip, self._enc_buf, out_off, st, 0)
+        if need < 0:
+            self._enc_buf = torch.empty(int(-need * 1.25) + 4096, dtype=torch.uint8)
+            need = C.encode_records(pred_t, conf_t, data, offsets, skip, self._enc_buf, out_off, st, 0)
+        buf = self._enc_buf.numpy()
+        oo = out_off.numpy()
+        st = st.numpy()
+        offs = offsets.numpy()
+        keys, values = [], []
+        for i, m in enumerate(msgs):
+            if st[i] == 0:
+                values.append(buf[oo[i]:oo[i + 1]].tobytes())
+            elif st[i] == 1:
+                text = bytes(data.numpy()[offs[i]:offs[i + 1]]).decode("utf-8", "replace")
+                values.append(json.dumps({"prediction": float(pred[i]), "confidence": float(p1[i]), "analysis": None,
+                                          "historical_insight": None, "original_text": text}))
+            else:
+                continue
+            keys.append(m.key())
+        return keys, values
 
     def _explain_async(self, key, text, pred, conf) -> None:
         try:

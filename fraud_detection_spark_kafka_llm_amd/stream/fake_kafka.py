@@ -105,6 +105,17 @@ class Broker:
             self.cond.notify_all()
             return m
 
+    def append_many(self, topic: str, keys: list, values: list) -> None:
+        """Batch append (one lock / one wake-up for the whole batch); same partitioning as append."""
+        with self.lock:
+            self.create_topic(topic)
+            parts = self.topics[topic]
+            np_ = len(parts)
+            for key, value in zip(keys, values):
+                partition = (zlib.crc32(key) if key else zlib.crc32(value or b"") ^ len(parts[0])) % np_
+                parts[partition].append(Message(topic, partition, len(parts[partition]), key, value))
+            self.cond.notify_all()
+
     def inject_error(self, topic: str, count: int = 1) -> None:
         with self.lock:
             self._errors[topic] += count
@@ -244,6 +255,13 @@ class Producer:
         if cb is not None:
             with self.lock:
                 self._pending.append((cb, m))
+
+    def produce_batch(self, topic: str, keys: list, values: list) -> None:
+        """Many messages at once (no delivery callbacks): what the streaming engine uses when the
+        producer offers it; librdkafka producers get per-message ``produce`` calls instead."""
+        if topic is None:
+            raise TypeError("topic must be a str (KAFKA_OUTPUT_TOPIC unset?)")
+        self.broker.append_many(topic, [_b(k) for k in keys], [_b(v) for v in values])
 
     def poll(self, timeout: float = 0) -> int:
         with self.lock:
