@@ -248,3 +248,43 @@ def test_serve_cli_consumes_classifies_and_commits(tmp_path, monkeypatch):
     assert len(outs) == 300
     rec = json.loads(outs[0].value())
     assert set(rec) >= {"prediction", "confidence", "analysis", "historical_insight", "original_text"}
+
+
+def test_native_record_encoding_is_byte_identical_to_json_dumps():
+    import random
+
+    import torch
+
+    from fraud_detection_spark_kafka_llm_amd.ops import native
+
+    C = native.lib()
+    raw = [t.encode("utf-8") for t in ["say \"hi\" \\ \n\t\r\b\f \x01 \x7f é 中文 😀", "", "plain text"]]
+    raw += [b"bad \xff utf8", b"\xed\xa0\x80 surrogate", b"over \xc0\xaf long", b"trunc \xe4\xb8"]
+    vals = [0.0, 1.0, 0.0001, 1e-05, 4.13167538969518e-05, 0.9999999999165088, 1e16, 9999999999999998.0, 5e-324,
+            float("nan"), float("inf"), -0.0, 0.1 + 0.2, 1.7976931348623157e308]
+    rng = random.Random(1)
+    vals += [rng.choice([rng.random(), rng.random() * 1e-6, 10 ** rng.uniform(-320, 300)]) for _ in range(3000)]
+    n = len(vals)
+    texts = [raw[i % len(raw)] for i in range(n)]
+    data = torch.from_numpy(np.frombuffer(b"".join(texts) + b"\0" * 16, dtype=np.uint8).copy())
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum([len(t) for t in texts])]).astype(np.int64))
+    pred, conf = torch.tensor(vals, dtype=torch.float64), torch.tensor(vals[::-1], dtype=torch.float64)
+    skip = torch.zeros(n, dtype=torch.int32)
+    skip[5] = 1
+    out, oo, st = torch.empty(16, dtype=torch.uint8), torch.empty(n + 1, dtype=torch.int64), torch.empty(n, dtype=torch.int32)
+    need = C.encode_records(pred, conf, data, off, skip, out, oo, st, 0)
+    assert need < 0                                        # buffer too small -> required size
+    out = torch.empty(-need, dtype=torch.uint8)
+    assert C.encode_records(pred, conf, data, off, skip, out, oo, st, 0) == -need
+    for i in range(n):
+        if i == 5:
+            assert st[i] == 2
+            continue
+        try:
+            text = texts[i].decode("utf-8")
+        except UnicodeDecodeError:
+            assert st[i] == 1
+            continue
+        want = json.dumps({"prediction": vals[i], "confidence": vals[::-1][i], "analysis": None,
+                           "historical_insight": None, "original_text": text})
+        assert bytes(out[oo[i]:oo[i + 1]].numpy()).decode("ascii") == want
