@@ -39,7 +39,7 @@ from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH  # noqa: E4
 from fraud_detection_spark_kafka_llm_amd.ml.xgboost import SparkXGBClassifierModel  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ops import text as T  # noqa: E402
-from fraud_detection_spark_kafka_llm_amd.ops.sparse import doc_freq  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.parallel import dist as D  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing  # noqa: E402
@@ -118,10 +118,11 @@ def main():
     sync_all(dev)
     t0 = time.perf_counter()
     indptr, idx, counts, y = featurize_shard(chunks, dev, spec)
-    df = D.all_reduce_sum(doc_freq(idx, counts, F))
+    fo = feature_order(indptr, idx, counts, F)          # CSC by feature: docFreq now, quantize later
+    df = D.all_reduce_sum(fo.df)
     idf = torch.log((args.rows + 1.0) / (df.double() + 1.0))
     vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-    vc.tf_counts, vc.tf_scale = counts, idf
+    vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
     t_feat = time.perf_counter() - t0
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)
     sync_all(dev)
@@ -129,7 +130,7 @@ def main():
     feat_sec = max_over_ranks(t_feat, dev)
     model = SparkXGBClassifierModel(res.trees, F, res.base_margin)
     idf_np = idf.cpu().numpy()
-    del vc, indptr, idx, counts, y, chunks
+    del vc, indptr, idx, counts, y, chunks, fo
     torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ 2. streaming inference

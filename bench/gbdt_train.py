@@ -18,7 +18,7 @@ from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
 from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH
 from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
 from fraud_detection_spark_kafka_llm_amd.ops import text as T
-from fraud_detection_spark_kafka_llm_amd.ops.sparse import doc_freq
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order
 from fraud_detection_spark_kafka_llm_amd.utils import tracing
 
 
@@ -67,10 +67,10 @@ def main():
     indptr, idx, counts, y, t_gen, t_feat = build_features(args.rows, dev)
     t1 = time.perf_counter()
     F = 1 << 18
-    df = doc_freq(idx, counts, F)
-    idf = torch.log((args.rows + 1.0) / (df.double() + 1.0))
+    fo = feature_order(indptr, idx, counts, F)
+    idf = torch.log((args.rows + 1.0) / (fo.df.double() + 1.0))
     vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-    vc.tf_counts, vc.tf_scale = counts, idf
+    vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)

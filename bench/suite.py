@@ -30,7 +30,7 @@ import torch
 from gbdt_train import build_features  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ml.tree_model import ensemble_arrays  # noqa: E402
-from fraud_detection_spark_kafka_llm_amd.ops.sparse import doc_freq, score_csr  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order, score_csr  # noqa: E402
 
 F = 1 << 18
 
@@ -44,11 +44,12 @@ def _metrics(y_true: np.ndarray, score: np.ndarray, pred: np.ndarray) -> dict:
 
 def _tfidf(rows, dev, seed, first_row=0, idf=None):
     indptr, idx, counts, y, _, _ = build_features(rows, dev, seed=seed, first_row=first_row)
+    fo = None
     if idf is None:
-        df = doc_freq(idx, counts, F)
-        idf = torch.log((rows + 1.0) / (df.double() + 1.0))
+        fo = feature_order(indptr, idx, counts, F)
+        idf = torch.log((rows + 1.0) / (fo.df.double() + 1.0))
     vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-    vc.tf_counts, vc.tf_scale = counts, idf
+    vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
     return vc, y, idf
 
 

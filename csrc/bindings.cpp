@@ -325,6 +325,81 @@ void doc_freq(const Tensor& idx, const Tensor& val, const Tensor& df) {
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+// Feature-major order of a count CSR (see sort_kernels.hip). csc_row/csc_cnt may be views into
+// larger (padded) buffers; they must hold nnz entries.
+template <class V>
+void feature_order_t(const Tensor& indptr, const Tensor& idx, const Tensor& counts, int64_t F, const Tensor& csc_row,
+                     const Tensor& csc_cnt, const Tensor& colptr, const Tensor& df, const Tensor& maxc) {
+  const auto dev = idx.device();
+  for (const Tensor* t : {&indptr, &counts, &csc_row, &csc_cnt, &colptr, &df, &maxc}) check_dev(*t, dev, "feature_order");
+  FDX_CHECK(indptr.scalar_type() == at::kLong && idx.scalar_type() == at::kInt, "indptr i64 / idx i32");
+  FDX_CHECK(csc_row.scalar_type() == at::kInt && csc_cnt.scalar_type() == at::kByte, "csc_row i32 / csc_cnt u8");
+  FDX_CHECK(colptr.scalar_type() == at::kLong && df.scalar_type() == at::kLong && maxc.scalar_type() == at::kInt,
+            "colptr/df i64, maxc i32");
+  const int64_t nnz = idx.numel();
+  FDX_CHECK(counts.numel() == nnz && csc_row.numel() >= nnz && csc_cnt.numel() >= nnz, "entry arrays");
+  FDX_CHECK(colptr.numel() == F + 1 && df.numel() == F && maxc.numel() == F && F > 0 && F < (1ll << 31), "F");
+  fdx::FeatureOrderArgs<V> a{};
+  a.indptr = indptr.data_ptr<int64_t>();
+  a.idx = idx.data_ptr<int32_t>();
+  a.counts = counts.data_ptr<V>();
+  a.rows = indptr.numel() - 1;
+  a.nnz = nnz;
+  a.F = (int32_t)F;
+  a.csc_row = csc_row.data_ptr<int32_t>();
+  a.csc_cnt = csc_cnt.data_ptr<uint8_t>();
+  a.colptr = colptr.data_ptr<int64_t>();
+  a.df = df.data_ptr<int64_t>();
+  a.maxc = maxc.data_ptr<int32_t>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    const auto o32 = idx.options();
+    const auto o64 = indptr.options();
+    Tensor keys_tmp = at::empty({std::max<int64_t>(nnz, 1)}, o32), keys_sorted = at::empty({std::max<int64_t>(nnz, 1)}, o32);
+    Tensor pay_tmp = at::empty({std::max<int64_t>(nnz, 1)}, o64), pay_sorted = at::empty({std::max<int64_t>(nnz, 1)}, o64);
+    const size_t tb = fdx::feature_order_temp_bytes(nnz, (int32_t)F);
+    Tensor temp = at::empty({(int64_t)std::max<size_t>(tb, 1)}, idx.options().dtype(at::kByte));
+    a.keys_tmp = keys_tmp.data_ptr<int32_t>();
+    a.keys_sorted = keys_sorted.data_ptr<int32_t>();
+    a.payload_tmp = reinterpret_cast<uint64_t*>(pay_tmp.data_ptr<int64_t>());
+    a.payload_sorted = reinterpret_cast<uint64_t*>(pay_sorted.data_ptr<int64_t>());
+    a.temp = temp.data_ptr();
+    a.temp_bytes = tb;
+    fdx::launch_feature_order<V>(a, c10::hip::getCurrentHIPStream(dev.index()).stream());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::feature_order_cpu<V>(a);
+  }
+}
+
+void feature_order(const Tensor& indptr, const Tensor& idx, const Tensor& counts, int64_t F, const Tensor& csc_row,
+                   const Tensor& csc_cnt, const Tensor& colptr, const Tensor& df, const Tensor& maxc) {
+  FDX_CHECK(indptr.is_contiguous() && idx.is_contiguous() && counts.is_contiguous(), "contiguous inputs");
+  if (counts.scalar_type() == at::kFloat) feature_order_t<float>(indptr, idx, counts, F, csc_row, csc_cnt, colptr, df, maxc);
+  else if (counts.scalar_type() == at::kDouble) feature_order_t<double>(indptr, idx, counts, F, csc_row, csc_cnt, colptr, df, maxc);
+  else FDX_CHECK(false, "counts must be float32 or float64");
+}
+
+// Row-block segment bounds of sorted-row columns (XCD-aware histogram items).
+void block_bounds(const Tensor& csc_row, const Tensor& colptr, const Tensor& cols, int64_t nblk, int64_t row_block,
+                  const Tensor& bounds) {
+  const auto dev = csc_row.device();
+  for (const Tensor* t : {&colptr, &cols, &bounds}) check_dev(*t, dev, "block_bounds");
+  FDX_CHECK(csc_row.scalar_type() == at::kInt && colptr.scalar_type() == at::kLong && cols.scalar_type() == at::kInt &&
+                bounds.scalar_type() == at::kLong, "dtypes");
+  FDX_CHECK(bounds.numel() == cols.numel() * (nblk + 1) && row_block > 0, "bounds [ncols, nblk+1]");
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_block_bounds(csc_row.data_ptr<int32_t>(), colptr.data_ptr<int64_t>(), cols.data_ptr<int32_t>(),
+                             (int32_t)cols.numel(), (int32_t)nblk, row_block, bounds.data_ptr<int64_t>(),
+                             c10::hip::getCurrentHIPStream(dev.index()).stream());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::block_bounds_cpu(csc_row.data_ptr<int32_t>(), colptr.data_ptr<int64_t>(), cols.data_ptr<int32_t>(),
+                          (int32_t)cols.numel(), (int32_t)nblk, row_block, bounds.data_ptr<int64_t>());
+  }
+}
+
 // Python-json.dumps-identical output records of the streaming classifier (see json_encode.cpp).
 // Returns the total size, or -(needed size) when `out` is too small.
 int64_t encode_records(const Tensor& pred, const Tensor& conf, const Tensor& text, const Tensor& off,
@@ -372,6 +447,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spmv", &spmv, "y = X x (CSR, fp64 accumulate)");
   m.def("spmv_t", &spmv_t, "g += X^T r (CSR, fp64)");
   m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
+  m.def("block_bounds", &block_bounds, "row-block segment bounds of sorted-row columns");
+  m.def("feature_order", &feature_order, "CSR -> CSC by feature (radix sort), docFreq and max count per feature");
   m.def("encode_records", &encode_records, "json.dumps-identical classification records (batch)");
   m.def("extract_json_field", &extract_json_field, "Bulk JSON string-field extraction into a packed buffer");
   m.attr("gfx_arch") = "gfx950";

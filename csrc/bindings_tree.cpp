@@ -90,6 +90,33 @@ void entry_stats(const Tensor& csc_row, const Tensor& rowstats, const Tensor& es
   }
 }
 
+// est[e] = rowstats[csc_row[e]] for the entries of the listed work items, in wave order
+void entry_stats_items(const Tensor& item_start, const Tensor& item_end, const Tensor& wave_item,
+                       const Tensor& csc_row, const Tensor& rowstats, const Tensor& est) {
+  const auto dev = csc_row.device();
+  chk(item_start, dev, at::kLong, "item_start");
+  chk(item_end, dev, at::kLong, "item_end");
+  chk(wave_item, dev, at::kInt, "wave_item");
+  chk(csc_row, dev, at::kInt, "csc_row");
+  chk(rowstats, dev, at::kInt, "rowstats");
+  chk(est, dev, at::kInt, "est");
+  FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2] int32");
+  FDX_CHECK(wave_item.numel() % 4 == 0, "wave_item: 4 slots per workgroup");
+  const auto* rs = reinterpret_cast<const uint32_t*>(rowstats.data_ptr<int32_t>());
+  auto* out = reinterpret_cast<uint32_t*>(est.data_ptr<int32_t>());
+  const int32_t ni = (int32_t)item_start.numel();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_entry_stats_items(item_start.data_ptr<int64_t>(), item_end.data_ptr<int64_t>(),
+                                  wave_item.data_ptr<int32_t>(), (int32_t)wave_item.numel(), ni,
+                                  csc_row.data_ptr<int32_t>(), rs, out, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::entry_stats_items_cpu(item_start.data_ptr<int64_t>(), item_end.data_ptr<int64_t>(), ni,
+                               csc_row.data_ptr<int32_t>(), rs, out);
+  }
+}
+
 // slot8[r] = node_slot[row_node[r]] - slot_base if in [0, nslots), else 0xff
 void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, int64_t nslots, const Tensor& out) {
   const auto dev = row_node.device();
@@ -120,7 +147,8 @@ void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, i
 void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& csc_row, const Tensor& csc_bin,
                 const optional<Tensor>& slot8_t, const Tensor& est, int64_t bt, int64_t ct, const Tensor& slab,
                 const Tensor& feat, const Tensor& feat_item0, const Tensor& feat_nitems, const Tensor& boff,
-                const Tensor& nbins, const Tensor& slot_to_node, const Tensor& hist, int64_t TB) {
+                const Tensor& nbins, const Tensor& slot_to_node, const Tensor& hist, int64_t TB,
+                const optional<Tensor>& wave_item) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
@@ -156,6 +184,12 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   h.csc_bin = csc_bin.data_ptr<uint8_t>();
   h.slot8 = slot8_t ? slot8_t->data_ptr<uint8_t>() : nullptr;
   h.est = reinterpret_cast<const uint32_t*>(est.data_ptr<int32_t>());
+  if (wave_item) {
+    chk(*wave_item, dev, at::kInt, "wave_item");
+    FDX_CHECK(wave_item->numel() % 4 == 0, "wave_item: 4 slots per workgroup");
+    h.wave_item = wave_item->data_ptr<int32_t>();
+    h.num_slots = (int32_t)wave_item->numel();
+  }
   fdx::HistReduceArgs r{};
   r.slab_slots = (int32_t)(8 * ct);
   r.slab_bins = (int32_t)(32 * bt);
@@ -335,6 +369,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rowstats", &rowstats);
   m.def("tree_entry_stats", &entry_stats);
   m.def("tree_slot8", &slot8);
+  m.def("tree_entry_stats_items", &entry_stats_items);
   m.def("tree_hist_build", &hist_build);
   m.def("tree_hist_subtract", &hist_subtract);
   m.def("tree_split_find", &split_find);

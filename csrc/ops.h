@@ -33,6 +33,36 @@ template <class V> void launch_spmv_t(const int64_t* indptr, const int32_t* idx,
 template <class V> void launch_doc_freq(const int32_t* idx, const V* val, int64_t nnz, int64_t* df,
                                        hipStream_t stream);
 
+// ---------------------------------------------------------------- feature-major order (sort_kernels.hip)
+template <class V>
+struct FeatureOrderArgs {
+  const int64_t* indptr;      // [rows + 1] CSR
+  const int32_t* idx;         // [nnz] feature ids (sorted unique within a row)
+  const V* counts;            // [nnz] term counts
+  int64_t rows, nnz;
+  int32_t F;
+  // device scratch (nullptr on the host path)
+  int32_t* keys_tmp;
+  uint64_t* payload_tmp;
+  int32_t* keys_sorted;
+  uint64_t* payload_sorted;
+  void* temp;
+  size_t temp_bytes;
+  // outputs
+  int32_t* csc_row;           // [nnz] rows, column-major, increasing within a column
+  uint8_t* csc_cnt;           // [nnz] min(count, 255) (0 for count <= 0)
+  int64_t* colptr;            // [F + 1]
+  int64_t* df;                // [F] entries with count > 0 (document frequency)
+  int32_t* maxc;              // [F] max min(count, 255)
+};
+size_t feature_order_temp_bytes(int64_t nnz, int32_t F);
+template <class V> void launch_feature_order(const FeatureOrderArgs<V>& a, hipStream_t s);
+template <class V> void feature_order_cpu(const FeatureOrderArgs<V>& a);
+void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
+                         int64_t row_block, int64_t* bounds, hipStream_t s);
+void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
+                      int64_t row_block, int64_t* bounds);
+
 // ---------------------------------------------------------------- tree engine (tree_kernels.hip / tree_cpu.cpp)
 struct RowStatsArgs;
 struct SlotArgs;
@@ -43,6 +73,9 @@ struct PartitionArgs;
 void launch_rowstats(const RowStatsArgs& a, hipStream_t s);
 void launch_entry_stats(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);
+void launch_entry_stats_items(const int64_t* item_start, const int64_t* item_end, const int32_t* wave_item,
+                              int32_t num_slots, int32_t num_items, const int32_t* csc_row, const uint32_t* rowstats,
+                              uint32_t* est, hipStream_t s);
 void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s);
 void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s);
 void launch_hist_subtract(const double* parent, double* cur, const int32_t* dst, const int32_t* par,
@@ -55,6 +88,8 @@ void launch_leaf_update(double* margin, const int32_t* row_node, const double* n
 void rowstats_cpu(const RowStatsArgs& a);
 void entry_stats_cpu(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est);
 void slot8_cpu(const SlotArgs& a);
+void entry_stats_items_cpu(const int64_t* item_start, const int64_t* item_end, int32_t num_items,
+                           const int32_t* csc_row, const uint32_t* rowstats, uint32_t* est);
 void hist_cpu(const HistArgs& h, const HistReduceArgs& r, int slots);
 void hist_subtract_cpu(const double* parent, double* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
                        int32_t n_pairs, int64_t TB);

@@ -1,0 +1,148 @@
+// Feature-major ordering of a CSR matrix for gfx950 (K-06 docFreq, K-09 binning, CSC build).
+//
+// A count-valued CSR (rows = documents, sorted unique feature ids per row) is turned into its CSC
+// without atomics:
+//   1. pack:   one wave per row writes key = feature id and payload = min(count, 255) << 32 | row
+//              for every entry (coalesced, the row's entries are contiguous);
+//   2. sort:   rocPRIM radix sort of (key, payload) pairs over only ceil(log2 F) key bits
+//              (stable, so each column keeps its rows in increasing order);
+//   3. unpack: csc_row / csc_bin streams (no random gathers: the payload carried everything);
+//   4. per feature (one wave each): docFreq = #entries with count > 0 and max count.
+// The previous torch formulation spent most of its time in contended scatter-max / bincount
+// atomics on the hottest features; here every per-feature quantity is a segmented reduction.
+#include <hipcub/hipcub.hpp>
+
+#include "ops.h"
+
+namespace fdx {
+
+namespace {
+constexpr int kWave = 64;
+
+template <class V>
+__global__ __launch_bounds__(256) void pack_entries_kernel(const int64_t* __restrict__ indptr,
+                                                           const int32_t* __restrict__ idx,
+                                                           const V* __restrict__ counts, int64_t rows,
+                                                           int32_t* __restrict__ keys, uint64_t* __restrict__ payload) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  if (r >= rows) return;
+  const int64_t e1 = indptr[r + 1];
+  for (int64_t e = indptr[r] + lane; e < e1; e += kWave) {
+    const double c = (double)counts[e];
+    const uint64_t b = c <= 0.0 ? 0u : (c >= 255.0 ? 255u : (uint64_t)c);
+    keys[e] = idx[e];
+    payload[e] = (b << 32) | (uint64_t)(uint32_t)r;
+  }
+}
+
+__global__ __launch_bounds__(256) void unpack_entries_kernel(const uint64_t* __restrict__ payload, int64_t n,
+                                                             int32_t* __restrict__ csc_row, uint8_t* __restrict__ csc_cnt) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const uint64_t p = payload[e];
+    csc_row[e] = (int32_t)(uint32_t)p;
+    csc_cnt[e] = (uint8_t)(p >> 32);
+  }
+}
+
+// colptr from the sorted keys: every boundary between key k0 and k1 > k0 fills colptr[k0+1..k1]
+__global__ __launch_bounds__(256) void colptr_kernel(const int32_t* __restrict__ sorted_keys, int64_t n, int32_t F,
+                                                     int64_t* __restrict__ colptr) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e <= n; e += (int64_t)gridDim.x * 256) {
+    const int32_t prev = e == 0 ? -1 : sorted_keys[e - 1];
+    const int32_t cur = e == n ? F : sorted_keys[e];
+    for (int32_t k = prev + 1; k <= cur; ++k) colptr[k] = e;
+  }
+}
+
+__global__ __launch_bounds__(256) void feature_stats_kernel(const uint8_t* __restrict__ csc_cnt,
+                                                            const int64_t* __restrict__ colptr, int32_t F,
+                                                            int64_t* __restrict__ df, int32_t* __restrict__ maxc) {
+  const int32_t f = (int32_t)((int64_t)blockIdx.x * 4 + threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  if (f >= F) return;
+  int64_t nz = 0;
+  int32_t mx = 0;
+  for (int64_t e = colptr[f] + lane; e < colptr[f + 1]; e += kWave) {
+    const int32_t c = csc_cnt[e];
+    nz += c > 0;
+    mx = c > mx ? c : mx;
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    nz += __shfl_xor(nz, o, kWave);
+    const int32_t m = __shfl_xor(mx, o, kWave);
+    mx = m > mx ? m : mx;
+  }
+  if (lane == 0) {
+    df[f] = nz;
+    maxc[f] = mx;
+  }
+}
+
+// bounds[i][b] = first entry of column cols[i] whose row >= b * row_block (b = 0..nblk), i.e. the
+// row-block segments of a column whose rows are sorted (XCD-aware work items, quantize.py).
+__global__ __launch_bounds__(256) void block_bounds_kernel(const int32_t* __restrict__ csc_row,
+                                                           const int64_t* __restrict__ colptr,
+                                                           const int32_t* __restrict__ cols, int32_t ncols,
+                                                           int32_t nblk, int64_t row_block, int64_t* __restrict__ bounds) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)ncols * (nblk + 1)) return;
+  const int32_t i = (int32_t)(t / (nblk + 1)), b = (int32_t)(t % (nblk + 1));
+  const int32_t c = cols[i];
+  int64_t lo = colptr[c], hi = colptr[c + 1];
+  const int64_t target = (int64_t)b * row_block;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)csc_row[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  bounds[t] = lo;
+}
+
+inline unsigned grid_for(int64_t n, int64_t cap = 16384) {
+  const int64_t b = (n + 255) / 256;
+  return (unsigned)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+inline int key_bits(int32_t F) {
+  int b = 1;
+  while (b < 31 && (1ll << b) < (int64_t)F) ++b;
+  return b;
+}
+}  // namespace
+
+size_t feature_order_temp_bytes(int64_t nnz, int32_t F) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                     (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)nnz, 0, key_bits(F));
+  return bytes;
+}
+
+template <class V>
+void launch_feature_order(const FeatureOrderArgs<V>& a, hipStream_t s) {
+  if (a.nnz > 0) {
+    hipLaunchKernelGGL((pack_entries_kernel<V>), dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a.indptr, a.idx,
+                       a.counts, a.rows, a.keys_tmp, a.payload_tmp);
+    size_t bytes = a.temp_bytes;
+    hipcub::DeviceRadixSort::SortPairs(a.temp, bytes, a.keys_tmp, a.keys_sorted, a.payload_tmp, a.payload_sorted,
+                                       (size_t)a.nnz, 0, key_bits(a.F), s);
+    hipLaunchKernelGGL(unpack_entries_kernel, dim3(grid_for(a.nnz)), dim3(256), 0, s, a.payload_sorted, a.nnz, a.csc_row,
+                       a.csc_cnt);
+  }
+  hipLaunchKernelGGL(colptr_kernel, dim3(grid_for(a.nnz + 1)), dim3(256), 0, s, a.keys_sorted, a.nnz, a.F, a.colptr);
+  hipLaunchKernelGGL(feature_stats_kernel, dim3((unsigned)((a.F + 3) / 4)), dim3(256), 0, s, a.csc_cnt, a.colptr, a.F,
+                     a.df, a.maxc);
+}
+
+void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
+                         int64_t row_block, int64_t* bounds, hipStream_t s) {
+  const int64_t n = (int64_t)ncols * (nblk + 1);
+  if (n > 0)
+    hipLaunchKernelGGL(block_bounds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, csc_row, colptr, cols, ncols,
+                       nblk, row_block, bounds);
+}
+
+template void launch_feature_order<float>(const FeatureOrderArgs<float>&, hipStream_t);
+template void launch_feature_order<double>(const FeatureOrderArgs<double>&, hipStream_t);
+
+}  // namespace fdx

@@ -1,5 +1,7 @@
 // Host implementations of the sparse kernels (same contracts and summation order as
 // sparse_kernels.hip: lane-strided partials over 64 "lanes" + xor butterfly).
+#include <algorithm>
+#include <climits>
 #include <cstring>
 #include <vector>
 
@@ -89,5 +91,49 @@ void spmv_t_cpu(const int64_t* indptr, const int32_t* idx, const V* val, const d
 }
 template void spmv_t_cpu<float>(const int64_t*, const int32_t*, const float*, const double*, double*, int64_t, int64_t, int);
 template void spmv_t_cpu<double>(const int64_t*, const int32_t*, const double*, const double*, double*, int64_t, int64_t, int);
+
+// Stable counting sort by feature (host twin of launch_feature_order).
+template <class V>
+void feature_order_cpu(const FeatureOrderArgs<V>& a) {
+  for (int32_t f = 0; f <= a.F; ++f) a.colptr[f] = 0;
+  for (int64_t e = 0; e < a.nnz; ++e) a.colptr[a.idx[e] + 1]++;
+  for (int32_t f = 0; f < a.F; ++f) a.colptr[f + 1] += a.colptr[f];
+  std::vector<int64_t> cur(a.colptr, a.colptr + a.F);
+  for (int64_t r = 0; r < a.rows; ++r)
+    for (int64_t e = a.indptr[r]; e < a.indptr[r + 1]; ++e) {
+      const int64_t p = cur[a.idx[e]]++;
+      const double c = (double)a.counts[e];
+      a.csc_row[p] = (int32_t)r;
+      a.csc_cnt[p] = (uint8_t)(c <= 0.0 ? 0 : (c >= 255.0 ? 255 : (int)c));
+    }
+  parallel_for(a.F, 0, 1024, [&](int64_t lo, int64_t hi) {
+    for (int64_t f = lo; f < hi; ++f) {
+      int64_t nz = 0;
+      int32_t mx = 0;
+      for (int64_t e = a.colptr[f]; e < a.colptr[f + 1]; ++e) {
+        nz += a.csc_cnt[e] > 0;
+        mx = a.csc_cnt[e] > mx ? a.csc_cnt[e] : mx;
+      }
+      a.df[f] = nz;
+      a.maxc[f] = mx;
+    }
+  });
+}
+
+void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
+                      int64_t row_block, int64_t* bounds) {
+  parallel_for((int64_t)ncols * (nblk + 1), 0, 4096, [&](int64_t lo_t, int64_t hi_t) {
+    for (int64_t t = lo_t; t < hi_t; ++t) {
+      const int32_t c = cols[t / (nblk + 1)];
+      const int64_t target = (t % (nblk + 1)) * row_block;
+      const int32_t* b = csc_row + colptr[c];
+      const int32_t* e = csc_row + colptr[c + 1];
+      bounds[t] = colptr[c] + (std::lower_bound(b, e, (int32_t)std::min<int64_t>(target, INT32_MAX)) - b);
+    }
+  });
+}
+
+template void feature_order_cpu<float>(const FeatureOrderArgs<float>&);
+template void feature_order_cpu<double>(const FeatureOrderArgs<double>&);
 
 }  // namespace fdx

@@ -52,6 +52,8 @@ struct HistArgs {
   const uint8_t* slot8;           // [N] relative slot, 0xff = not built; nullptr = root pass (all slot 0)
   const uint32_t* est;            // [nnz * 2] packed statistics in entry order
   float* slab;                    // [I][8*CT][32*BT][2]
+  const int32_t* wave_item;       // [num_slots] item of each wave slot (-1 idle); nullptr: slot = item
+  int32_t num_slots;
 };
 
 struct HistReduceArgs {

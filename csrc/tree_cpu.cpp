@@ -39,6 +39,17 @@ void entry_stats_cpu(const int32_t* csc_row, const uint32_t* rowstats, int64_t n
   });
 }
 
+void entry_stats_items_cpu(const int64_t* item_start, const int64_t* item_end, int32_t num_items,
+                           const int32_t* csc_row, const uint32_t* rowstats, uint32_t* est) {
+  parallel_for(num_items, 0, 16, [&](int64_t lo, int64_t hi) {
+    for (int64_t it = lo; it < hi; ++it)
+      for (int64_t e = item_start[it]; e < item_end[it]; ++e) {
+        est[2 * e] = rowstats[2 * (int64_t)csc_row[e]];
+        est[2 * e + 1] = rowstats[2 * (int64_t)csc_row[e] + 1];
+      }
+  });
+}
+
 void slot8_cpu(const SlotArgs& a) {
   parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
     for (int64_t r = lo; r < hi; ++r) {

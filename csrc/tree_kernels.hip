@@ -72,6 +72,22 @@ __global__ __launch_bounds__(256) void entry_stats_kernel(const int32_t* __restr
   if (t < nnz) est[t] = rowstats[csc_row[t]];
 }
 
+// Item-ordered variant (same wave -> item table as the histogram launches): each XCD gathers from
+// the ~1 MB row-statistics slice of the row block it is working on, which stays in its L2.
+__global__ __launch_bounds__(256) void entry_stats_items_kernel(const int64_t* __restrict__ item_start,
+                                                                const int64_t* __restrict__ item_end,
+                                                                const int32_t* __restrict__ wave_item, int32_t num_items,
+                                                                const int32_t* __restrict__ csc_row,
+                                                                const uint2* __restrict__ rowstats,
+                                                                uint2* __restrict__ est) {
+  const int wslot = blockIdx.x * 4 + threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int item = wave_item[wslot];
+  if (item < 0 || item >= num_items) return;
+  const int64_t e1 = item_end[item];
+  for (int64_t e = item_start[item] + lane; e < e1; e += kWave) est[e] = rowstats[csc_row[e]];
+}
+
 __global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
     const int32_t node = a.row_node[r];
@@ -125,8 +141,9 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
 
   const int wid = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
-  const int item = blockIdx.x * 4 + wid;
-  if (item >= a.num_items) return;
+  const int wslot = blockIdx.x * 4 + wid;
+  const int item = a.wave_item ? a.wave_item[wslot] : wslot;
+  if (item < 0 || item >= a.num_items) return;
   const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
 
   const int col = lane & 31;        // MFMA column / A-row index owned by this lane
@@ -389,13 +406,23 @@ void launch_entry_stats(const int32_t* csc_row, const uint32_t* rowstats, int64_
                      reinterpret_cast<const uint2*>(rowstats), nnz, reinterpret_cast<uint2*>(est));
 }
 
+void launch_entry_stats_items(const int64_t* item_start, const int64_t* item_end, const int32_t* wave_item,
+                              int32_t num_slots, int32_t num_items, const int32_t* csc_row, const uint32_t* rowstats,
+                              uint32_t* est, hipStream_t s) {
+  if (num_slots <= 0) return;
+  hipLaunchKernelGGL(entry_stats_items_kernel, dim3((unsigned)(num_slots / 4)), dim3(256), 0, s, item_start, item_end,
+                     wave_item, num_items, csc_row, reinterpret_cast<const uint2*>(rowstats),
+                     reinterpret_cast<uint2*>(est));
+}
+
 void launch_slot8(const SlotArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(slot8_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
 void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s) {
   if (a.num_items <= 0) return;
-  const dim3 grid((a.num_items + 3) / 4), block(256);
+  const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
+  const dim3 grid((slots + 3) / 4), block(256);
   const bool root = a.slot8 == nullptr;
 #define FDX_HIST_CASE(B, C)                                                                   \
   if (bt == B && ct == C) {                                                                  \

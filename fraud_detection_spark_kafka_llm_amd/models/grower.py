@@ -173,7 +173,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     with tracing.span("tree.rowstats"):
         C.tree_rowstats(g, h, label, weight, int(params.seed), int(tree_index), bool(bootstrap), mode_rs,
                         ws.rowstats)
-        C.tree_entry_stats(Q.csc_row, ws.rowstats, ws.est)
+        for grp in Q.groups:   # XCD-ordered items: each XCD gathers within its current row block
+            C.tree_entry_stats_items(grp.item_start, grp.item_end, grp.wave_order(), Q.csc_row, ws.rowstats, ws.est)
     tot = root_totals(ws)
     if all_reduce is not None:
         tot = all_reduce(tot)
@@ -250,7 +251,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                     slab = ws.slab_for(gsel.num_items, grp.bt, ct)
                     C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est,
                                       grp.bt, ct, slab, gsel.feat, gsel.feat_item0, gsel.feat_nitems, Q.boff,
-                                      Q.nbins, s2n, hist_target, stride)
+                                      Q.nbins, s2n, hist_target, stride, gsel.wave_order())
         totals = torch.tensor(np.stack([stats[n] for n in open_nodes]), dtype=torch.float64, device=dev)
         node_ids = torch.tensor(open_nodes, dtype=torch.int32, device=dev)
         if shards is None:

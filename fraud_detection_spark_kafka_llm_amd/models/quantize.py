@@ -24,6 +24,8 @@ from typing import Callable, Optional
 import numpy as np
 import torch
 
+from ..utils import tracing
+
 CSC_PAD = 16
 
 CHUNK = 16384          # entries per histogram work item (one wavefront)
@@ -39,6 +41,8 @@ class BinGroup:
     feat: torch.Tensor           # int32 [L]
     feat_item0: torch.Tensor     # int64 [L]
     feat_nitems: torch.Tensor    # int32 [L]
+    item_blk: Optional[torch.Tensor] = None   # int32 [I] row block of the item (-1: whole column)
+    _order: Optional[torch.Tensor] = None
 
     def subset(self, feat_mask: torch.Tensor) -> "BinGroup":
         """Restrict to features with ``feat_mask[fid]`` (RF per-level feature union)."""
@@ -51,11 +55,49 @@ class BinGroup:
         item0 = torch.zeros_like(nitems, dtype=torch.int64)
         if nitems.numel():
             item0[1:] = torch.cumsum(nitems.to(torch.int64), 0)[:-1]
-        return BinGroup(self.bt, item_start, item_end, item_feat, feat, item0, nitems)
+        blk = self.item_blk[keep_items] if self.item_blk is not None else None
+        return BinGroup(self.bt, item_start, item_end, item_feat, feat, item0, nitems, blk)
 
     @property
     def num_items(self) -> int:
         return int(self.item_start.numel())
+
+    def wave_order(self) -> torch.Tensor:
+        """Item of every wave slot of the histogram / entry-statistics launches (-1: idle)."""
+        if self._order is None:
+            self._order = wave_order(self.item_blk, self.num_items, self.item_start.device)
+        return self._order
+
+
+def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.Tensor:
+    """XCD-aware item placement. Workgroups are dealt round-robin over the 8 XCDs (observed
+    dispatch, speed only), so workgroups b and b + 8 share an L2: the 4 wave slots of workgroup
+    b = 8k + x get items of row blocks = x (mod 8) in block order, i.e. each XCD walks its own
+    row blocks one after another and the block's 1-byte slot table and 8-byte row statistics
+    (~1 MB) stay in that XCD's 4 MB L2. Whole-column items (row block -1) are spread round-robin
+    and run last."""
+    if num_items == 0:
+        return torch.full((4,), -1, dtype=torch.int32, device=dev)
+    idx = torch.arange(num_items, device=dev, dtype=torch.int64)
+    if item_blk is None:
+        blk = torch.full((num_items,), -1, dtype=torch.int64, device=dev)
+    else:
+        blk = item_blk.to(torch.int64)
+    blocked = blk >= 0
+    label = torch.where(blocked, blk % 8, idx % 8)
+    phase = torch.where(blocked, blk // 8, torch.full_like(blk, 1 << 20))
+    key = (label << 52) | (phase << 30) | idx
+    order = torch.argsort(key)
+    lab_sorted = label[order]
+    counts = torch.bincount(lab_sorted, minlength=8)
+    first = torch.cumsum(counts, 0) - counts
+    pos = torch.arange(num_items, device=dev) - first[lab_sorted]
+    per = int(counts.max())
+    groups = (per + 3) // 4
+    slot = (pos // 4) * 32 + lab_sorted * 4 + pos % 4
+    out = torch.full((groups * 32,), -1, dtype=torch.int32, device=dev)
+    out[slot] = order.to(torch.int32)
+    return out
 
 
 @dataclass
@@ -106,7 +148,7 @@ def _decode_f32_bits(k: torch.Tensor) -> torch.Tensor:
 
 def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
              all_reduce_max: Optional[Callable] = None, all_gather: Optional[Callable] = None,
-             chunk: int = CHUNK) -> Quantized:
+             chunk: int = CHUNK, row_block: int = None, split_min: int = None) -> Quantized:
     """Bin a ``VectorColumn`` and build the CSC. ``counts``/``scale`` select the count path
     (per-entry integer counts and per-feature positive scale); integral non-negative values
     take it automatically with scale 1."""
@@ -122,27 +164,40 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
             and float(val64.max()) < 65536:
         counts = val64
         scale = torch.ones(F, dtype=torch.float64, device=dev)
-    row = torch.repeat_interleave(torch.arange(N, device=dev, dtype=torch.int32), (indptr[1:] - indptr[:-1]),
-                                  output_size=int(idx.numel()))
-    if counts is not None:
-        q = _count_path(idx64, counts.to(torch.float64), scale.to(device=dev, dtype=torch.float64), F, max_bins,
-                        all_reduce_max)
-    else:
-        q = _generic_path(idx64, val64, F, max_bins, all_gather)
+    if counts is not None and F < (1 << 31):
+        Q = _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_max)
+        with tracing.span("q.groups"):
+            Q.groups = _make_groups(Q.colptr, Q.nbins, chunk, Q.csc_row, N, row_block or ROW_BLOCK,
+                                    split_min or SPLIT_MIN)
+        return Q
+    with tracing.span("q.rows"):
+        row = torch.repeat_interleave(torch.arange(N, device=dev, dtype=torch.int32), (indptr[1:] - indptr[:-1]),
+                                      output_size=int(idx.numel()))
+    with tracing.span("q.bins"):
+        if counts is not None:
+            q = _count_path(idx64, counts.to(torch.float64), scale.to(device=dev, dtype=torch.float64), F, max_bins,
+                            all_reduce_max)
+        else:
+            q = _generic_path(idx64, val64, F, max_bins, all_gather)
     remap, nbins, zbin, thresholds, entry_bin, keep = q
-    fid = remap[idx64]
-    keep = keep & (fid >= 0)
-    fid, row, entry_bin = fid[keep], row[keep], entry_bin[keep]
+    with tracing.span("q.filter"):
+        fid = remap[idx64]
+        keep = keep & (fid >= 0)
+        fid, row, entry_bin = fid[keep], row[keep], entry_bin[keep]
     Fa = int(nbins.numel())
-    order = torch.sort(fid.to(torch.int32), stable=True).indices
+    with tracing.span("q.sort"):
+        order = torch.sort(fid.to(torch.int32), stable=True).indices
     nnz = int(order.numel())
     # the histogram kernel loads 4-entry groups without per-lane branches: keep CSC_PAD readable
     # entries behind the end of both arrays (bin 0xff = no bin)
+    sp = tracing.span("q.gather")
+    sp.__enter__()
     csc_row = torch.zeros(nnz + CSC_PAD, dtype=torch.int32, device=dev)
     csc_row[:nnz] = row[order]
     csc_bin = torch.full((nnz + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
     csc_bin[:nnz] = entry_bin[order].to(torch.uint8)
     csc_row, csc_bin = csc_row[:nnz], csc_bin[:nnz]
+    sp.__exit__(None, None, None)
     cnt = torch.bincount(fid, minlength=Fa)
     colptr = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
     torch.cumsum(cnt, 0, out=colptr[1:])
@@ -154,7 +209,66 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
     Q.boff_host = boff.cpu().numpy()
     Q.zbin_host = Q.zbin.cpu().numpy()
     Q.fid_host = fid_orig.cpu().numpy()
-    Q.groups = _make_groups(colptr, nbins, chunk)
+    with tracing.span("q.groups"):
+        Q.groups = _make_groups(colptr, nbins, chunk, csc_row, N, row_block or ROW_BLOCK, split_min or SPLIT_MIN)
+    return Q
+
+
+def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_max) -> "Quantized":
+    """Count path on the native feature-major order (sort_kernels.hip): bins = min(count,
+    max_bins - 1) with thresholds (k + 0.5) * scale_f; the CSC comes straight from the radix sort
+    (cached on the VectorColumn as ``_feature_order`` when the caller already built it for IDF)."""
+    from ..ops.sparse import feature_order
+
+    dev = indptr.device
+    fo = getattr(vc, "_feature_order", None)
+    if fo is None or fo.colptr.numel() != F + 1 or fo.csc_row.device != dev:
+        with tracing.span("q.order"):
+            fo = feature_order(indptr, idx, counts, F)
+    scale = scale.to(device=dev, dtype=torch.float64)
+    maxb = torch.clamp(fo.maxc.to(torch.int64), max=max_bins - 1)
+    maxb = torch.where(scale > 0, maxb, torch.zeros_like(maxb))
+    if all_reduce_max is not None:
+        maxb = all_reduce_max(maxb)
+    active = maxb > 0
+    Fa = int(active.sum())
+    fid_orig = torch.nonzero(active).flatten()
+    nbins = (maxb[active] + 1).to(torch.int32)
+    nb = nbins.to(torch.int64)
+    TB = int(nb.sum())
+    f_of_bin = torch.repeat_interleave(torch.arange(Fa, device=dev), nb, output_size=TB)
+    bstart = torch.cumsum(nb, 0) - nb
+    k = torch.arange(TB, device=dev) - bstart[f_of_bin]
+    thresholds = ((k.to(torch.float64) + 0.5) * scale[fid_orig][f_of_bin]).cpu().numpy()
+    lens = fo.colptr[1:] - fo.colptr[:-1]
+    nnz_all = int(fo.colptr[-1])
+    with tracing.span("q.csc"):
+        if int(lens[~active].sum()) == 0:        # every non-empty feature is active: the order is the CSC
+            csc_row = fo.csc_row
+            cnt = fo.csc_cnt
+            colptr = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
+            if Fa:
+                colptr[:-1] = fo.colptr[:-1][active]
+                colptr[-1] = fo.colptr[1:][active][-1]
+        else:                                     # drop the entries of inactive features (scale 0)
+            keep = torch.repeat_interleave(active, lens, output_size=nnz_all)
+            n_keep = int(keep.sum())
+            row_buf = torch.zeros(n_keep + CSC_PAD, dtype=torch.int32, device=dev)
+            row_buf[:n_keep] = fo.csc_row[keep]
+            csc_row = row_buf[:n_keep]
+            cnt = fo.csc_cnt[keep]
+            colptr = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(lens[active], 0, out=colptr[1:])
+        n = int(csc_row.numel())
+        bin_buf = torch.full((n + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
+        torch.clamp(cnt, max=max_bins - 1, out=bin_buf[:n])
+    boff = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nb, 0, out=boff[1:])
+    Q = Quantized(N, F, fid_orig, nbins.contiguous(), torch.zeros(Fa, dtype=torch.int32, device=dev), boff,
+                  thresholds, colptr, csc_row, bin_buf[:n])
+    Q.boff_host = boff.cpu().numpy()
+    Q.zbin_host = Q.zbin.cpu().numpy()
+    Q.fid_host = fid_orig.cpu().numpy()
     return Q
 
 
@@ -254,24 +368,76 @@ def _generic_path(idx, val, F, max_bins, all_gather):
     return remap, nbins, zb.to(torch.int32), thresholds, eb, full_keep
 
 
-def _make_groups(colptr: torch.Tensor, nbins: torch.Tensor, chunk: int) -> list:
+ROW_BLOCK = 1 << 17         # rows per XCD row block: 1 B slot + 8 B statistics per row ~ 1.1 MB
+SPLIT_MIN = 1 << 13         # columns with fewer entries stay whole (their gathers are few)
+
+
+def _segments(colptr: torch.Tensor, csc_row: torch.Tensor, n_rows: int, row_block: int = ROW_BLOCK,
+              split_min: int = SPLIT_MIN):
+    """(start, end, feature, row block) of every column segment: columns with >= SPLIT_MIN entries
+    are cut where the row block changes (rows are sorted inside a column, so a block's entries are
+    contiguous); smaller columns are one segment with block -1."""
     dev = colptr.device
+    Fa = colptr.numel() - 1
     n = colptr[1:] - colptr[:-1]
-    nchunks = torch.clamp((n + chunk - 1) // chunk, min=1)
+    nonempty = torch.nonzero(n > 0).flatten()
+    starts = colptr[:-1][nonempty]
+    feats = nonempty
+    nblk = (n_rows + row_block - 1) // row_block
+    split_cols = torch.nonzero(n >= split_min).flatten().to(torch.int32) if nblk > 1 else None
+    if split_cols is not None and split_cols.numel():
+        from ..ops import native
+
+        S = int(split_cols.numel())
+        bounds = torch.empty((S, nblk + 1), dtype=torch.int64, device=dev)
+        native.lib().block_bounds(csc_row, colptr, split_cols, int(nblk), int(row_block), bounds)
+        bounds[:, -1] = colptr[split_cols.to(torch.int64) + 1]
+        b_start, b_end = bounds[:, :-1].reshape(-1), bounds[:, 1:].reshape(-1)
+        b_feat = split_cols.to(torch.int64).repeat_interleave(nblk)
+        b_blk = torch.arange(nblk, device=dev, dtype=torch.int64).repeat(S)
+        ne = b_end > b_start
+        unsplit = (n > 0) & (n < split_min)
+        u_feat = torch.nonzero(unsplit).flatten()
+        starts = torch.cat([colptr[:-1][u_feat], b_start[ne]])
+        feats = torch.cat([u_feat, b_feat[ne]])
+        seg_blk = torch.cat([torch.full_like(u_feat, -1), b_blk[ne]])
+        starts, o = torch.sort(starts, stable=True)
+        feats, seg_blk = feats[o], seg_blk[o]
+    else:
+        seg_blk = torch.full_like(starts, -1)
+    ends = colptr[feats + 1]
+    if starts.numel() > 1:
+        nxt = starts[1:]
+        same = feats[1:] == feats[:-1]
+        ends = ends.clone()
+        ends[:-1] = torch.where(same, nxt, ends[:-1])
+    return starts, ends, feats, seg_blk
+
+
+def _make_groups(colptr: torch.Tensor, nbins: torch.Tensor, chunk: int, csc_row: Optional[torch.Tensor] = None,
+                 n_rows: int = 0, row_block: int = ROW_BLOCK, split_min: int = SPLIT_MIN) -> list:
+    dev = colptr.device
+    if csc_row is None:
+        csc_row = torch.zeros(0, dtype=torch.int32, device=dev)
+    s0, e0, f0, b0 = _segments(colptr, csc_row, n_rows, row_block, split_min)
     groups = []
     for bt in (1, 2):
         lo, hi = (0, 32) if bt == 1 else (33, 64)
-        sel = (nbins >= lo) & (nbins <= hi) & (n > 0)
-        feats = torch.nonzero(sel).flatten()
-        if feats.numel() == 0:
+        sel = (nbins[f0] >= lo) & (nbins[f0] <= hi)
+        if not bool(sel.any()):
             continue
-        nc = nchunks[feats]
+        s, e, f, b = s0[sel], e0[sel], f0[sel], b0[sel]
+        nc = (e - s + chunk - 1) // chunk
         I = int(nc.sum())
-        item_feat = torch.repeat_interleave(feats, nc, output_size=I)
+        seg = torch.repeat_interleave(torch.arange(s.numel(), device=dev), nc, output_size=I)
         first = torch.cumsum(nc, 0) - nc
-        k = torch.arange(I, device=dev) - torch.repeat_interleave(first, nc, output_size=I)
-        start = colptr[item_feat] + k * chunk
-        end = torch.minimum(start + chunk, colptr[item_feat + 1])
+        k = torch.arange(I, device=dev) - first[seg]
+        start = s[seg] + k * chunk
+        end = torch.minimum(start + chunk, e[seg])
+        item_feat = f[seg]
+        feats, nitems = torch.unique_consecutive(item_feat, return_counts=True)
+        item0 = torch.cumsum(nitems, 0) - nitems
         groups.append(BinGroup(bt, start.contiguous(), end.contiguous(), item_feat.to(torch.int32).contiguous(),
-                               feats.to(torch.int32).contiguous(), first.contiguous(), nc.to(torch.int32).contiguous()))
+                               feats.to(torch.int32).contiguous(), item0.contiguous(),
+                               nitems.to(torch.int32).contiguous(), b[seg].to(torch.int32).contiguous()))
     return groups

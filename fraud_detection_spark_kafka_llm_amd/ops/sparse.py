@@ -1,6 +1,8 @@
 """Sparse ops over ``VectorColumn`` CSR data (native: ``csrc/sparse_kernels.hip`` / ``sparse_cpu.cpp``)."""
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import torch
 
 from . import native
@@ -74,3 +76,32 @@ def doc_freq(idx: torch.Tensor, val: torch.Tensor, size: int) -> torch.Tensor:
         native.lib().doc_freq(idx.to(torch.int32).contiguous(), val.contiguous(), df)
         return df
     return torch.bincount(idx[val != 0].to(torch.int64), minlength=size)
+
+
+@dataclass
+class FeatureOrder:
+    """Column-major (CSC) view of a count CSR: ``csc_row`` / ``csc_cnt`` (min(count, 255)) are
+    views with >= 16 readable padding entries behind them, ``colptr`` [F+1], ``df`` document
+    frequencies and ``maxc`` per-feature maximum count."""
+    csc_row: torch.Tensor
+    csc_cnt: torch.Tensor
+    colptr: torch.Tensor
+    df: torch.Tensor
+    maxc: torch.Tensor
+
+
+def feature_order(indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor, num_features: int) -> FeatureOrder:
+    """CSR (rows, sorted unique feature ids per row, term counts) -> CSC by feature with a native
+    radix sort; docFreq and the per-feature max count are segmented reductions (no atomics)."""
+    C = native.lib()
+    dev = idx.device
+    nnz = int(idx.numel())
+    pad = 16
+    row_buf = torch.zeros(nnz + pad, dtype=torch.int32, device=dev)
+    cnt_buf = torch.zeros(nnz + pad, dtype=torch.uint8, device=dev)
+    colptr = torch.empty(num_features + 1, dtype=torch.int64, device=dev)
+    df = torch.empty(num_features, dtype=torch.int64, device=dev)
+    maxc = torch.empty(num_features, dtype=torch.int32, device=dev)
+    C.feature_order(indptr.contiguous(), idx.to(torch.int32).contiguous(), counts.contiguous(), int(num_features),
+                    row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)
+    return FeatureOrder(row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)

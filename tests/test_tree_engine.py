@@ -145,7 +145,8 @@ def test_random_forest_bootstrap_and_sampling_are_deterministic():
 def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
     C = native.lib()
     n = row_node_np.shape[0]
-    Q = quantize(vc.to(dev), max_bins=max_bins, chunk=509)   # odd chunk: unaligned item starts
+    # odd chunk: unaligned item starts; small row blocks: dense columns split per block (XCD order)
+    Q = quantize(vc.to(dev), max_bins=max_bins, chunk=509, row_block=1500, split_min=64)
     ws = Workspace(Q, 64)
     row_node = torch.from_numpy(row_node_np).to(dev)
     node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
@@ -154,7 +155,8 @@ def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
     gg = torch.from_numpy(np.linspace(-1, 1, n).astype(np.float32)).to(dev)
     hh = torch.from_numpy(np.linspace(0.01, 0.25, n).astype(np.float32)).to(dev)
     C.tree_rowstats(gg, hh, None, None, 0, 0, False, 0, ws.rowstats)
-    C.tree_entry_stats(Q.csc_row, ws.rowstats, ws.est)
+    for grp in Q.groups:
+        C.tree_entry_stats_items(grp.item_start, grp.item_end, grp.wave_order(), Q.csc_row, ws.rowstats, ws.est)
     hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.float64, device=dev)
     for s0 in range(0, nslots, 8 * ct):
         cnt = min(8 * ct, nslots - s0)
@@ -168,8 +170,43 @@ def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
             slab = ws.slab_for(grp.num_items, grp.bt, ct)
             C.tree_hist_build(grp.item_start, grp.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est, grp.bt, ct,
                               slab, grp.feat, grp.feat_item0, grp.feat_nitems, Q.boff, Q.nbins, s2n.to(dev),
-                              hist, Q.TB)
+                              hist, Q.TB, grp.wave_order())
     return hist.cpu().numpy()
+
+
+def test_row_blocked_items_cover_columns_and_wave_order_is_xcd_grouped():
+    from fraud_detection_spark_kafka_llm_amd.models.quantize import wave_order
+
+    rng = np.random.default_rng(2)
+    n, F = 5000, 30
+    dense = (rng.random((n, F)) < np.linspace(0.01, 0.6, F)) * rng.integers(1, 5, (n, F))
+    Q = quantize(vc_from_dense(dense.astype(np.float64)), max_bins=8, chunk=100, row_block=700, split_min=200)
+    colptr = Q.colptr.numpy()
+    rows = Q.csc_row.numpy()
+    for grp in Q.groups:
+        st, en = grp.item_start.numpy(), grp.item_end.numpy()
+        feat, blk = grp.item_feat.numpy(), grp.item_blk.numpy()
+        # items tile every column exactly; a blocked item stays inside its row block
+        for f in np.unique(feat):
+            sel = np.nonzero(feat == f)[0]
+            assert st[sel[0]] == colptr[f] and en[sel[-1]] == colptr[f + 1]
+            assert np.all(st[sel[1:]] == en[sel[:-1]]) and np.all(en[sel] - st[sel] <= 100)
+        for i in np.nonzero(blk >= 0)[0]:
+            assert np.all(rows[st[i]:en[i]] // 700 == blk[i])
+        assert (blk >= 0).any() and (blk < 0).any()
+        order = grp.wave_order().numpy()
+        used = order[order >= 0]
+        assert sorted(used.tolist()) == list(range(grp.num_items))   # every item exactly once
+        slots = np.nonzero(order >= 0)[0]
+        lab = (slots // 4) % 8                                     # workgroup % 8 = XCD group
+        b = blk[order[slots]]
+        assert np.all((b < 0) | (b % 8 == lab))
+        # within one XCD group, row blocks are visited in increasing order, whole columns last
+        for x in range(8):
+            bx = b[lab == x]
+            key = np.where(bx < 0, 1 << 30, bx)
+            assert np.all(np.diff(key) >= 0)
+    assert wave_order(None, 0, torch.device("cpu")).tolist() == [-1] * 4
 
 
 def test_host_histogram_matches_numpy():
@@ -180,7 +217,7 @@ def test_host_histogram_matches_numpy():
     vc = vc_from_dense(dense.astype(np.float64))
     row_node = rng.integers(-1, 7, n).astype(np.int32)
     hist = _hist_on("cpu", vc, 16, 1, 5, row_node)
-    Q = quantize(vc, max_bins=16, chunk=509)
+    Q = quantize(vc, max_bins=16, chunk=509, row_block=1500, split_min=64)
     g = np.linspace(-1, 1, n).astype(np.float32).astype(np.float64)
     colptr, rows, bins = Q.colptr.numpy(), Q.csc_row.numpy(), Q.csc_bin.numpy()
     boff = Q.boff.numpy()
@@ -244,3 +281,24 @@ def test_gpu_deterministic_gbdt_bitwise_equals_host_and_repeats():
         np.testing.assert_array_equal(a.stats, b.stats)
         np.testing.assert_array_equal(b.stats, c.stats)
         np.testing.assert_array_equal(b.threshold, c.threshold)
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_feature_order_is_stable_csc_with_docfreq_and_max(dev):
+    from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order
+
+    rng = np.random.default_rng(4)
+    n, F = 3000, 700
+    dense = (rng.random((n, F)) < 0.03) * rng.integers(1, 400, (n, F))
+    dense[:, 5] = 0                                    # empty column
+    vc = vc_from_dense(dense.astype(np.float64))
+    ip, ix, v = vc.csr()
+    fo = feature_order(ip.to(dev), ix.to(dev), v.to(torch.float32).to(dev), F)
+    colptr = fo.colptr.cpu().numpy()
+    rows, cnt = fo.csc_row.cpu().numpy(), fo.csc_cnt.cpu().numpy()
+    for f in range(F):
+        r = np.nonzero(dense[:, f])[0]
+        np.testing.assert_array_equal(rows[colptr[f]:colptr[f + 1]], r)        # stable: rows increasing
+        np.testing.assert_array_equal(cnt[colptr[f]:colptr[f + 1]], np.minimum(dense[r, f], 255))
+    np.testing.assert_array_equal(fo.df.cpu().numpy(), (dense > 0).sum(0))
+    np.testing.assert_array_equal(fo.maxc.cpu().numpy(), np.minimum(dense.max(0), 255))
