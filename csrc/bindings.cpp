@@ -145,7 +145,7 @@ void featurize_score(const Tensor& text, const Tensor& doc_off, int64_t flags, i
                      const optional<std::vector<Tensor>>& trees, int64_t K, const Tensor& out_idx,
                      const Tensor& out_val, const Tensor& out_nnz, const optional<Tensor>& out_ntok,
                      const Tensor& out_raw, const Tensor& out_status, const optional<Tensor>& only_docs,
-                     int64_t threads) {
+                     int64_t threads, const optional<Tensor>& long_docs) {
   const auto dev = text.device();
   check_dev(text, dev, "text");
   check_dev(doc_off, dev, "doc_off");
@@ -187,6 +187,12 @@ void featurize_score(const Tensor& text, const Tensor& doc_off, int64_t flags, i
   a.out_status = out_ptr<int32_t>(out_status, dev, "out_status");
   if (dev.is_cuda()) {
     FDX_CHECK(!only_docs, "only_docs is a host-path option");
+    if (long_docs) {      // second launch: the long-dialogue kernel on the listed documents only
+      check_dev(*long_docs, dev, "long_docs");
+      FDX_CHECK(long_docs->scalar_type() == at::kInt && long_docs->is_contiguous(), "long_docs int32");
+      a.doc_list = long_docs->data_ptr<int32_t>();
+      a.n_list = (int32_t)long_docs->numel();
+    }
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_featurize_score(a, c10::hip::getCurrentHIPStream(dev.index()).stream());
     C10_HIP_KERNEL_LAUNCH_CHECK();

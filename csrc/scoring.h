@@ -86,6 +86,9 @@ struct FeatArgs {
   // kFlagKeys: key of token i of doc d at out_keys[key_off[d] + i]; out_keys == nullptr -> count only
   const int64_t* key_off;
   uint64_t* out_keys;
+  // long-dialogue launch: process only doc_list[0 .. n_list) (nullptr: every document)
+  const int32_t* doc_list;
+  int32_t n_list;
 };
 
 }  // namespace fdx

@@ -13,8 +13,11 @@
 //   7. score   : LR margin (fp64 wave reduction) or tree-ensemble traversal
 //                with binary search over the LDS-resident sorted indices     (X-07, X-11)
 // Only the score (and optionally the sparse vector) is written back to HBM.
-// Documents longer than CAPB bytes or with more than CAPT kept tokens are flagged
-// kStatusTooLong and finished by the host path (rare; 1 in >10^4 for the reference data).
+// Two instantiations: the streaming one (4 dialogues per 256-thread workgroup, 4 KB of cleaned
+// text / 1024 kept tokens per dialogue, ~34 KB LDS per workgroup) and a long-dialogue one (one
+// dialogue per single-wave workgroup, 64 KB / 16384 tokens, ~128 KB LDS -- CDNA4 lets one
+// workgroup take up to 160 KB) that runs only on the documents the first launch flags as too
+// long (long transcripts stay on the GPU). Longer ones are finished by the host.
 #include "scoring.h"
 #include "ops.h"
 
@@ -24,9 +27,11 @@
 namespace fdx {
 
 constexpr int kWave = 64;
-constexpr int kCapB = 4096;   // cleaned bytes per dialogue held in LDS
-constexpr int kCapT = 1024;   // kept tokens per dialogue held in LDS
+constexpr int kCapB = 4096;       // streaming variant: cleaned bytes per dialogue held in LDS
+constexpr int kCapT = 1024;       //                    kept tokens per dialogue held in LDS
 constexpr int kWavesPerBlock = 4;
+constexpr int kLongCapB = 65536;  // long-dialogue variant
+constexpr int kLongCapT = 16384;
 
 __device__ __forceinline__ void lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -73,15 +78,18 @@ __device__ __forceinline__ uint32_t hash_token(const uint8_t* s_clean, int p, in
   return m.finish();
 }
 
-__global__ __launch_bounds__(256) void featurize_score_kernel(FeatArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_clean_all[kWavesPerBlock][kCapB];
-  __shared__ uint32_t s_tok_all[kWavesPerBlock][kCapT];
-  __shared__ uint16_t s_q_all[kWavesPerBlock][2 * kWave];
+template <int CAPB, int CAPT, int WAVES>
+__global__ __launch_bounds__(kWave * WAVES) void featurize_score_kernel(FeatArgs a) {
+  static_assert(CAPB / 4 >= CAPT && CAPB <= 65536, "counts reuse the byte buffer; token starts are 16-bit");
+  __shared__ __attribute__((aligned(16))) uint8_t s_clean_all[WAVES][CAPB];
+  __shared__ uint32_t s_tok_all[WAVES][CAPT];
+  __shared__ uint16_t s_q_all[WAVES][2 * kWave];
 
   const int wid = threadIdx.x / kWave;
   const int lane = lane_id();
-  const int d = blockIdx.x * kWavesPerBlock + wid;
-  if (d >= a.num_docs) return;
+  const int slot = blockIdx.x * WAVES + wid;
+  if (slot >= (a.doc_list ? a.n_list : a.num_docs)) return;
+  const int d = a.doc_list ? a.doc_list[slot] : slot;
 
   uint8_t* s_clean = s_clean_all[wid];
   uint32_t* s_tok = s_tok_all[wid];
@@ -92,7 +100,7 @@ __global__ __launch_bounds__(256) void featurize_score_kernel(FeatArgs a) {
   const bool prelowered = (a.flags & kFlagPreLowered) != 0;
   const int64_t s = a.doc_off[d], e = a.doc_off[d + 1];
   const int K = (a.flags & kFlagTrees) ? a.trees.K : 1;
-  if (e - s > kCapB) {
+  if (e - s > CAPB) {
     if (lane == 0) a.out_status[d] = kStatusTooLong;
     return;
   }
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(256) void featurize_score_kernel(FeatArgs a) {
     const bool keep = keep_sw && bucket >= 0;
     const unsigned long long km = __ballot(keep);
     const int slot = ntok + popc_below(km);
-    if (keep && slot < kCapT) s_tok[slot] = (uint32_t)bucket;
+    if (keep && slot < CAPT) s_tok[slot] = (uint32_t)bucket;
     ntok += __popcll(km);
   };
 
@@ -218,7 +226,7 @@ __global__ __launch_bounds__(256) void featurize_score_kernel(FeatArgs a) {
     }
     return;
   }
-  if (ntok > kCapT) {
+  if (ntok > CAPT) {
     if (lane == 0) a.out_status[d] = kStatusTooLong;
     return;
   }
@@ -344,9 +352,15 @@ __global__ __launch_bounds__(256) void featurize_score_kernel(FeatArgs a) {
 }
 
 void launch_featurize_score(const FeatArgs& a, hipStream_t stream) {
+  if (a.doc_list) {          // long dialogues: one per single-wave workgroup
+    if (a.n_list > 0)
+      hipLaunchKernelGGL((featurize_score_kernel<kLongCapB, kLongCapT, 1>), dim3(a.n_list), dim3(kWave), 0, stream, a);
+    return;
+  }
   if (a.num_docs <= 0) return;
   const int blocks = (a.num_docs + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(featurize_score_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, a);
+  hipLaunchKernelGGL((featurize_score_kernel<kCapB, kCapT, kWavesPerBlock>), dim3(blocks), dim3(kWave * kWavesPerBlock),
+                     0, stream, a);
 }
 
 }  // namespace fdx

@@ -282,7 +282,10 @@ def _flags(spec: FeatureSpec, idf, lr, trees, want_csr: bool) -> int:
     return f
 
 
-def _launch(C, text: PackedText, spec, flags, idf_t, lr, trees, out, device, only=None, threads=0):
+LONG_DOC_BYTES = 65536   # documents up to this size stay on the GPU (long-dialogue kernel)
+
+
+def _launch(C, text: PackedText, spec, flags, idf_t, lr, trees, out, device, only=None, threads=0, long_docs=None):
     nnz, ntok, raw, status, idx, val = out
     st = spec.stop_table()
     vt = spec.vocab_table()
@@ -293,7 +296,7 @@ def _launch(C, text: PackedText, spec, flags, idf_t, lr, trees, out, device, onl
         float(spec.min_tf), idf_t, lr.weights(device) if lr is not None else None,
         float(lr.b) if lr is not None else 0.0,
         trees.tensors(device) if trees is not None else None, K,
-        idx, val, nnz, ntok, raw, status, only, int(threads))
+        idx, val, nnz, ntok, raw, status, only, int(threads), long_docs)
 
 
 def featurize_score(text: PackedText, spec: FeatureSpec, idf: Optional[torch.Tensor] = None,
@@ -324,6 +327,13 @@ def featurize_score(text: PackedText, spec: FeatureSpec, idf: Optional[torch.Ten
     flags = _flags(spec, idf_t, lr, trees, want_csr)
     _launch(C, text, spec, flags, idf_t, lr, trees, out, device, None, threads)
     nnz, ntok, raw, status, idx, val = out
+    if device.type == "cuda" and D:
+        # documents over the streaming kernel's LDS capacity: rerun them on the long-dialogue kernel
+        lens = text.offsets[1:] - text.offsets[:-1]
+        long_docs = torch.nonzero((status == STATUS_TOO_LONG) & (lens <= LONG_DOC_BYTES)).flatten()
+        if long_docs.numel():
+            _launch(C, text, spec, flags, idf_t, lr, trees, out, device, None, threads,
+                    long_docs.to(torch.int32).contiguous())
     base = text.offsets[:-1] + torch.arange(D, device=device, dtype=torch.int64)
     res = FeatureResult(nnz, ntok, raw, status, idx if want_csr else None, val if want_csr else None, base, spec.dim)
     if fix_fallbacks and D:

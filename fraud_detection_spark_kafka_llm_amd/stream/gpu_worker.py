@@ -18,9 +18,12 @@ import numpy as np
 import torch
 
 from ..ops import native
-from ..ops.text import (FLAG_IDF, FLAG_LR, FLAG_TREES, PAD, STATUS_OK, FeatureSpec, LinearScorer, PackedText,
-                        TreeArrays, _flags, featurize_score)
+from ..ops.text import (FLAG_IDF, FLAG_LR, FLAG_TREES, LONG_DOC_BYTES, PAD, STATUS_OK, FeatureSpec, LinearScorer,
+                        PackedText, TreeArrays, _flags, featurize_score)
 from .ring import Slot
+
+
+LONG_DOC_MIN = 4096      # raw bytes above which the streaming kernel defers to the long-dialogue kernel
 
 
 @dataclass
@@ -89,6 +92,14 @@ class GpuScorer:
         self._next = (self._next + 1) % len(self.stages)
         n, nb = slot.n_docs, slot.n_bytes
         st.slot, st.n = slot, n
+        long_idx = None
+        if n:
+            offs = slot.offsets[: n + 1].numpy()
+            lens = offs[1:] - offs[:-1]
+            if int(lens.max()) > LONG_DOC_MIN:
+                sel = np.nonzero((lens > LONG_DOC_MIN) & (lens <= LONG_DOC_BYTES))[0].astype(np.int32)
+                if sel.size:
+                    long_idx = torch.from_numpy(sel).to(self.dev, non_blocking=False)
         with torch.cuda.stream(self.h2d):
             self.h2d.wait_event(st.ev_d2h)   # previous use of this stage fully drained
             st.text[: nb + PAD].copy_(slot.data[: nb + PAD], non_blocking=True)
@@ -99,10 +110,13 @@ class GpuScorer:
             if n:
                 # scores/status are stored by the kernel straight into pinned host memory: a D2H
                 # copy would queue behind the next batch's 100+ MB H2D on the SDMA engine.
-                self.C.featurize_score(st.text[: nb + PAD], st.offsets[: n + 1], self.flags, self.spec.dim, self.stop,
-                                       self.vocab, float(self.spec.min_tf), self.idf, self.lr_w,
-                                       float(self.scorer.b) if self.lr_w is not None else 0.0, self.tree_t, self.K,
-                                       self.dummy_i, self.dummy_f, st.nnz, st.ntok, st.h_raw, st.h_status, None, 0)
+                args = (st.text[: nb + PAD], st.offsets[: n + 1], self.flags, self.spec.dim, self.stop, self.vocab,
+                        float(self.spec.min_tf), self.idf, self.lr_w,
+                        float(self.scorer.b) if self.lr_w is not None else 0.0, self.tree_t, self.K, self.dummy_i,
+                        self.dummy_f, st.nnz, st.ntok, st.h_raw, st.h_status, None, 0)
+                self.C.featurize_score(*args, None)
+                if long_idx is not None:      # dialogues over 4 KB: long-dialogue kernel, same stream
+                    self.C.featurize_score(*args, long_idx)
             st.ev_compute.record(self.compute)
             st.ev_d2h = st.ev_compute
         self._inflight.append(st)

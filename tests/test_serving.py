@@ -288,3 +288,24 @@ def test_native_record_encoding_is_byte_identical_to_json_dumps():
         want = json.dumps({"prediction": vals[i], "confidence": vals[::-1][i], "analysis": None,
                            "historical_insight": None, "original_text": text})
         assert bytes(out[oo[i]:oo[i + 1]].numpy()).decode("ascii") == want
+
+
+@pytest.mark.gpu
+def test_gpu_scorer_long_dialogues_match_host():
+    from fraud_detection_spark_kafka_llm_amd.ops.text import FeatureSpec, LinearScorer
+    from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer, HostScorer
+    from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing
+
+    rng = np.random.default_rng(0)
+    words = ["bank", "verify", "account", "please", "hello", "prize", "meeting", "doctor"]
+    docs = [" ".join(rng.choice(words, int(k))) for k in rng.integers(1, 3000, 200)]   # up to ~20 KB
+    docs += ["x" * 80000, "short one"]
+    F = 1 << 12
+    spec = FeatureSpec(clean=True, num_features=F)
+    lr = LinearScorer(rng.standard_normal(F), -0.1)
+    idf = rng.random(F)
+    ring = PinnedRing(slots=1, max_docs=256, max_bytes=1 << 20)
+    ring.slots[0].fill(docs)
+    gpu = GpuScorer(spec, idf, lr, "cuda:0", max_docs=256, max_bytes=1 << 20)
+    host = HostScorer(spec, idf, lr, max_docs=256, max_bytes=1 << 20)
+    np.testing.assert_array_equal(gpu.score_packed(ring.slots[0]), host.score_packed(ring.slots[0]))

@@ -192,12 +192,33 @@ def test_gpu_vocab_mode():
 
 
 @pytest.mark.gpu
-def test_gpu_long_docs_fall_back_to_host():
-    docs = ["word " * 2000, "a " * 3000, fixtures.SCAM_SAMPLE]
-    spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=1000)
+@pytest.mark.parametrize("scorer", ["lr", "trees"])
+def test_gpu_long_dialogues_stay_on_device_and_match_host(scorer):
+    """Dialogues over the streaming kernel's 4 KB capacity run on the long-dialogue kernel (64 KB,
+    16K tokens); only larger ones reach the host path. Results are bitwise equal to the host."""
+    rng = np.random.default_rng(3)
+    words = ["bank", "verify", "account", "please", "the", "hello", "prize", "ssn", "x", "zebra"]
+    docs = ["word " * 2000,                                   # 10 KB
+            "a " * 3000,                                      # 1 token x 3000 (token cap, short text)
+            " ".join(rng.choice(words, 6000)),                # ~33 KB
+            " ".join(f"w{i}" for i in range(9000)),           # 9000 distinct tokens
+            "z" * 70000,                                      # > 64 KB -> host
+            fixtures.SCAM_SAMPLE] + random_docs(300, seed=4)
     pt = T.PackedText.from_strings(docs)
-    cpu = T.featurize_score(pt, spec, want_csr=True, device="cpu")
-    gpu = T.featurize_score(pt, spec, want_csr=True, device="cuda:0")
+    F = 1 << 14
+    spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=F)
+    idf = torch.rand(F, dtype=torch.float64)
+    kw = dict(idf=idf)
+    if scorer == "lr":
+        kw["lr"] = T.LinearScorer(torch.randn(F, dtype=torch.float64).numpy(), 0.25)
+    else:
+        kw["trees"] = random_forest_arrays(40, F, 6, 2, seed=5)
+    cpu = T.featurize_score(pt, spec, want_csr=True, device="cpu", **kw)
+    gpu = T.featurize_score(pt, spec, want_csr=True, device="cuda:0", fix_fallbacks=False, **kw)
+    st = gpu.status.cpu()
+    assert st[:4].eq(T.STATUS_OK).all() and st[4] == T.STATUS_TOO_LONG   # only the 70 KB one left
+    gpu = T.featurize_score(pt, spec, want_csr=True, device="cuda:0", **kw)
     assert torch.equal(cpu.nnz, gpu.nnz.cpu())
     for a, b in zip(cpu.csr(), gpu.csr()):
         assert torch.equal(a, b.cpu())
+    assert torch.equal(cpu.raw, gpu.raw.cpu())
