@@ -164,8 +164,11 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   chk(slot_to_node, dev, at::kInt, "slot_to_node");
   chk(hist, dev, at::kDouble, "hist");
   FDX_CHECK(item_start.numel() == item_end.numel(), "item arrays");
-  FDX_CHECK(bt >= 1 && bt <= 2 && (ct == 1 || ct == 2 || ct == 4), "bt in {1,2}, ct in {1,2,4}");
-  FDX_CHECK(slot_to_node.numel() == 8 * ct, "slot_to_node must have 8*ct entries");
+  // bt 0: narrow 16-bin tile, 4*ct slots (ct 1/2/4/8); bt 1/2: 32*bt bins, 8*ct slots (ct 1/2/4)
+  FDX_CHECK((bt == 0 && (ct == 1 || ct == 2 || ct == 4 || ct == 8)) ||
+                (bt >= 1 && bt <= 2 && (ct == 1 || ct == 2 || ct == 4)), "unsupported (bt, ct)");
+  const int64_t tile_slots = bt == 0 ? 4 * ct : 8 * ct, tile_bins = bt == 0 ? 16 : 32 * bt;
+  FDX_CHECK(slot_to_node.numel() == tile_slots, "slot_to_node must have one entry per tile slot");
   FDX_CHECK(csc_row.numel() == csc_bin.numel(), "csc arrays");
   FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2]");
   FDX_CHECK(TB >= 0 && boff.numel() == nbins.numel() + 1, "boff must be [Fa+1]");
@@ -191,8 +194,8 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
     h.num_slots = (int32_t)wave_item->numel();
   }
   fdx::HistReduceArgs r{};
-  r.slab_slots = (int32_t)(8 * ct);
-  r.slab_bins = (int32_t)(32 * bt);
+  r.slab_slots = (int32_t)tile_slots;
+  r.slab_bins = (int32_t)tile_bins;
   r.feat = feat.data_ptr<int32_t>();
   r.feat_item0 = feat_item0.data_ptr<int64_t>();
   r.feat_nitems = feat_nitems.data_ptr<int32_t>();
@@ -205,7 +208,7 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   r.hist = hist.data_ptr<double>();
   if (dev.is_cuda()) {
     chk(slab, dev, at::kFloat, "slab");
-    FDX_CHECK(slab.numel() >= (int64_t)h.num_items * 8 * ct * 32 * bt * 2, "slab too small");
+    FDX_CHECK(slab.numel() >= (int64_t)h.num_items * tile_slots * tile_bins * 2, "slab too small");
     h.slab = slab.data_ptr<float>();
     r.slab = h.slab;
     c10::hip::HIPGuard guard(dev.index());
@@ -214,7 +217,7 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
     fdx::launch_hist_reduce(r, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
-    fdx::hist_cpu(h, r, (int)(8 * ct));
+    fdx::hist_cpu(h, r, (int)tile_slots);
   }
 }
 

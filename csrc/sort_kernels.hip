@@ -7,7 +7,8 @@
 //   2. sort:   rocPRIM radix sort of (key, payload) pairs over only ceil(log2 F) key bits
 //              (stable, so each column keeps its rows in increasing order);
 //   3. unpack: csc_row / csc_bin streams (no random gathers: the payload carried everything);
-//   4. per feature (one wave each): docFreq = #entries with count > 0 and max count.
+//   4. per feature: max count by a wave-segmented max over the sorted keys (one atomic per key
+//      run per wave) and docFreq = column length - zero-count entries.
 // The previous torch formulation spent most of its time in contended scatter-max / bincount
 // atomics on the hottest features; here every per-feature quantity is a segmented reduction.
 #include <hipcub/hipcub.hpp>
@@ -55,28 +56,37 @@ __global__ __launch_bounds__(256) void colptr_kernel(const int32_t* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void feature_stats_kernel(const uint8_t* __restrict__ csc_cnt,
-                                                            const int64_t* __restrict__ colptr, int32_t F,
-                                                            int64_t* __restrict__ df, int32_t* __restrict__ maxc) {
-  const int32_t f = (int32_t)((int64_t)blockIdx.x * 4 + threadIdx.x / kWave);
+// Per-feature max count and count of zero-count entries over the key-sorted entries: a wave
+// covers 64 consecutive entries, a segmented max over runs of equal keys (sorted, so runs are
+// contiguous) leaves the run maximum in the run's first lane, which issues the only atomic. Hot
+// features (millions of entries) thus cost one atomic per wave instead of a serial walk.
+__global__ __launch_bounds__(256) void feature_stats_kernel(const int32_t* __restrict__ sorted_keys,
+                                                            const uint8_t* __restrict__ csc_cnt, int64_t n,
+                                                            int32_t* __restrict__ maxc, int64_t* __restrict__ zeros) {
   const int lane = threadIdx.x & (kWave - 1);
-  if (f >= F) return;
-  int64_t nz = 0;
-  int32_t mx = 0;
-  for (int64_t e = colptr[f] + lane; e < colptr[f + 1]; e += kWave) {
-    const int32_t c = csc_cnt[e];
-    nz += c > 0;
-    mx = c > mx ? c : mx;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~(kWave - 1)); base < n; base += stride) {
+    const int64_t e = base + lane;
+    const int32_t k = e < n ? sorted_keys[e] : -1;
+    const int32_t c = e < n ? (int32_t)csc_cnt[e] : 0;
+    if (e < n && c == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&zeros[k]), 1ull);
+    int32_t m = c;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int32_t km = __shfl_down(k, o, kWave);
+      const int32_t mm = __shfl_down(m, o, kWave);
+      if (lane + o < kWave && km == k) m = mm > m ? mm : m;
+    }
+    const int32_t kp = __shfl_up(k, 1, kWave);
+    if (k >= 0 && (lane == 0 || kp != k) && m > 0) atomicMax(&maxc[k], m);
   }
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    nz += __shfl_xor(nz, o, kWave);
-    const int32_t m = __shfl_xor(mx, o, kWave);
-    mx = m > mx ? m : mx;
-  }
-  if (lane == 0) {
-    df[f] = nz;
-    maxc[f] = mx;
-  }
+}
+
+// in place: `zeros` and `df` are the same buffer
+__global__ __launch_bounds__(256) void df_kernel(const int64_t* __restrict__ colptr, const int64_t* zeros, int32_t F,
+                                                 int64_t* df) {
+  const int32_t f = (int32_t)((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (f < F) df[f] = colptr[f + 1] - colptr[f] - zeros[f];
 }
 
 // bounds[i][b] = first entry of column cols[i] whose row >= b * row_block (b = 0..nblk), i.e. the
@@ -130,8 +140,12 @@ void launch_feature_order(const FeatureOrderArgs<V>& a, hipStream_t s) {
                        a.csc_cnt);
   }
   hipLaunchKernelGGL(colptr_kernel, dim3(grid_for(a.nnz + 1)), dim3(256), 0, s, a.keys_sorted, a.nnz, a.F, a.colptr);
-  hipLaunchKernelGGL(feature_stats_kernel, dim3((unsigned)((a.F + 3) / 4)), dim3(256), 0, s, a.csc_cnt, a.colptr, a.F,
-                     a.df, a.maxc);
+  hipMemsetAsync(a.maxc, 0, sizeof(int32_t) * (size_t)a.F, s);
+  hipMemsetAsync(a.df, 0, sizeof(int64_t) * (size_t)a.F, s);          // zero-count entries first
+  if (a.nnz > 0)
+    hipLaunchKernelGGL(feature_stats_kernel, dim3(grid_for(a.nnz)), dim3(256), 0, s, a.keys_sorted, a.csc_cnt, a.nnz,
+                       a.maxc, a.df);
+  hipLaunchKernelGGL(df_kernel, dim3((unsigned)((a.F + 255) / 256)), dim3(256), 0, s, a.colptr, a.df, a.F, a.df);
 }
 
 void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,

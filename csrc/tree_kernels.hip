@@ -84,8 +84,20 @@ __global__ __launch_bounds__(256) void entry_stats_items_kernel(const int64_t* _
   const int lane = threadIdx.x & (kWave - 1);
   const int item = wave_item[wslot];
   if (item < 0 || item >= num_items) return;
-  const int64_t e1 = item_end[item];
-  for (int64_t e = item_start[item] + lane; e < e1; e += kWave) est[e] = rowstats[csc_row[e]];
+  const int64_t e0 = item_start[item], e1 = item_end[item];
+  // 4 consecutive entries per lane: one 16-B row load, 4 independent gathers, two 16-B stores
+  for (int64_t base = e0 & ~(int64_t)3; base < e1; base += 4 * kWave) {
+    const int64_t e = base + 4 * lane;
+    if (e >= e0 && e + 4 <= e1) {
+      const int4 r = *reinterpret_cast<const int4*>(csc_row + e);
+      const uint2 a = rowstats[r.x], b = rowstats[r.y], c = rowstats[r.z], d = rowstats[r.w];
+      reinterpret_cast<uint4*>(est)[e / 2] = make_uint4(a.x, a.y, b.x, b.y);
+      reinterpret_cast<uint4*>(est)[e / 2 + 1] = make_uint4(c.x, c.y, d.x, d.y);
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (e + j >= e0 && e + j < e1) est[e + j] = rowstats[csc_row[e + j]];
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
@@ -128,16 +140,25 @@ __device__ __forceinline__ void load_step(const HistArgs& a, int64_t e, int64_t 
 // ------------------------------------------------------------------ MFMA histogram
 // One wave per work item (a chunk of one feature column); per step the wave takes 256 entries,
 // 4 consecutive ones per lane so that rows (int4), bins (u32) and statistics (2 x uint4) are
-// single vector loads. Only lanes with a live entry fetch statistics, and MFMA K-steps whose 16
-// entries belong to no built node are skipped (wave-uniform ballot test).
+// single vector loads; the next step's loads are in flight while this one is multiplied.
 // ROOT: the pass builds only the root, so every entry is live in slot 0 and neither rows nor
-// the slot table are read.
-template <int BT, int CT, bool ROOT>
+// the slot table are read. Otherwise only live entries (row in a node of this pass) are
+// compacted into LDS and MFMA K-steps run on ceil(live / KS) groups.
+// Tiles: NARROW (features with <= 16 bins, ~90 % of entries on text data) uses
+// v_mfma_f32_16x16x32_bf16: 16 bins x (4 slots x 4 stat halves), 32 entries per K-step; otherwise
+// v_mfma_f32_32x32x16_bf16: 32 bins x (8 slots x 4 stat halves), 16 entries per K-step. Operand
+// construction is VALU-issue bound, so the narrow tile halves the one-hot work per entry.
+template <int BT, int CT, bool ROOT, bool NARROW>
 __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
-  constexpr int G = 4 * kWave;
-  __shared__ __attribute__((aligned(16))) uint8_t s_bin[4][G + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_slot[4][G + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t s_comp[4][4][G + 16];
+  constexpr int G = 4 * kWave;                 // entries per wave step
+  constexpr int KS = NARROW ? 32 : 16;         // entries per MFMA K-step
+  constexpr int NSLOT = NARROW ? 4 : 8;        // node slots per column tile
+  constexpr int NBIN = NARROW ? 16 : 32;       // bins per row tile
+  constexpr int NREG = NARROW ? 4 : 16;        // accumulator registers per lane
+  typedef float acc_t __attribute__((ext_vector_type(NREG)));
+  __shared__ __attribute__((aligned(16))) uint8_t s_bin[4][G + KS];
+  __shared__ __attribute__((aligned(16))) uint8_t s_slot[4][G + KS];
+  __shared__ __attribute__((aligned(16))) uint16_t s_comp[4][4][G + KS];
 
   const int wid = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
@@ -146,25 +167,25 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
   if (item < 0 || item >= a.num_items) return;
   const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
 
-  const int col = lane & 31;        // MFMA column / A-row index owned by this lane
-  const int half = lane >> 5;       // k half (entries 8*half .. 8*half+7 of each 16-step)
-  const int comp = col & 3;         // 0 stat0_hi, 1 stat0_lo, 2 stat1_hi, 3 stat1_lo
+  const int col = NARROW ? (lane & 15) : (lane & 31);   // MFMA column / A-row index owned by this lane
+  const int kgrp = NARROW ? (lane >> 4) : (lane >> 5);  // which 8 entries of a K-step the lane supplies
+  const int comp = col & 3;                             // 0 stat0_hi, 1 stat0_lo, 2 stat1_hi, 3 stat1_lo
   const int slot_sub = col >> 2;
 
-  f32x16 acc[BT][CT];
+  acc_t acc[BT][CT];
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[bt][ct][i] = 0.0f;
+      for (int i = 0; i < NREG; ++i) acc[bt][ct][i] = 0.0f;
 
   const int64_t first = e0 & ~(int64_t)3;
   const int64_t e_last = (e1 - 1) & ~(int64_t)3;   // last 4-group holding an entry of the item
   StepData cur, nxt;
   load_step<ROOT>(a, first + 4 * lane, e0, e1, e_last, cur);
   for (int64_t base = first; base < e1; base += G) {
-    // slot of each of the lane's 4 entries (the only random access: slot8 is N bytes, L2-resident)
+    // slot of each of the lane's 4 entries (the only random access: a 1-byte table, L2-resident)
     uint32_t slots4;
     if constexpr (ROOT) {
       slots4 = (cur.r4.x >= 0 ? 0u : 0xffu) | (cur.r4.y >= 0 ? 0u : 0xff00u) | (cur.r4.z >= 0 ? 0u : 0xff0000u) |
@@ -182,9 +203,6 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
     const uint32_t bins4 = cur.bins4;
     const bool any = slots4 != 0xffffffffu;
     const uint32_t w[8] = {cur.p.x, cur.p.y, cur.p.z, cur.p.w, cur.q.x, cur.q.y, cur.q.z, cur.q.w};
-    // Stage the step's entries in LDS. Root: all entries live, stored in place. Otherwise only
-    // the live entries (row in a node built by this pass, ~half or fewer at deep levels, spread
-    // at random) are compacted to the front, so MFMA K-steps run on ceil(live / 16) groups.
     unsigned long long live = 0;
     int n_live = G;
     if constexpr (ROOT) {
@@ -220,27 +238,28 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
       }
       n_live = nb;
       // pad the last partial K-step: bin/slot 0xff match no row/column, so stale comps drop out
-      if (lane < 16) {
+      if (lane < KS) {
         s_bin[wid][nb + lane] = 0xffu;
         s_slot[wid][nb + lane] = 0xffu;
       }
     }
     lds_sync();
 #pragma unroll
-    for (int ks = 0; ks < G / 16; ++ks) {
+    for (int ks = 0; ks < G / KS; ++ks) {
       if constexpr (ROOT) {
-        if (((live >> (4 * ks)) & 0xfull) == 0ull) continue;   // lanes 4ks..4ks+3 hold these 16 entries
+        constexpr unsigned long long kLaneMask = (1ull << (KS / 4)) - 1ull;   // lanes holding the K-step
+        if (((live >> (ks * (KS / 4))) & kLaneMask) == 0ull) continue;
       } else {
-        if (ks * 16 >= n_live) break;
+        if (ks * KS >= n_live) break;
       }
-      const int k0 = ks * 16 + 8 * half;
+      const int k0 = ks * KS + 8 * kgrp;
       const uint2 bins8 = *reinterpret_cast<const uint2*>(&s_bin[wid][k0]);
       const uint2 slots8 = *reinterpret_cast<const uint2*>(&s_slot[wid][k0]);
       const uint4 cv = *reinterpret_cast<const uint4*>(&s_comp[wid][comp][k0]);
       bf16x8 A[BT];
 #pragma unroll
       for (int bt = 0; bt < BT; ++bt) {
-        const uint32_t rep = (uint32_t)(col + 32 * bt) * 0x01010101u;
+        const uint32_t rep = (uint32_t)(col + NBIN * bt) * 0x01010101u;
         const uint32_t zl = match_bytes(bins8.x ^ rep), zh = match_bytes(bins8.y ^ rep);
         const u32x4 av = {spread_lo(zl) * 0x3f80u, spread_hi(zl) * 0x3f80u,    // bf16 1.0 where bin == row
                           spread_lo(zh) * 0x3f80u, spread_hi(zh) * 0x3f80u};
@@ -250,40 +269,44 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
       for (int ct = 0; ct < CT; ++ct) {
         bf16x8 B;
         if constexpr (ROOT) {
-          // one node: no slot mask; columns of slots 1..7 collect junk the reduce never reads
+          // one node: no slot mask; columns of the other slots collect junk the reduce never reads
           B = __builtin_bit_cast(bf16x8, cv);
         } else {
-          const uint32_t rep = (uint32_t)(ct * 8 + slot_sub) * 0x01010101u;
+          const uint32_t rep = (uint32_t)(ct * NSLOT + slot_sub) * 0x01010101u;
           const uint32_t zl = match_bytes(slots8.x ^ rep), zh = match_bytes(slots8.y ^ rep);
           const u32x4 bv = {cv.x & (spread_lo(zl) * 0xffffu), cv.y & (spread_hi(zl) * 0xffffu),
                             cv.z & (spread_lo(zh) * 0xffffu), cv.w & (spread_hi(zh) * 0xffffu)};
           B = __builtin_bit_cast(bf16x8, bv);
         }
 #pragma unroll
-        for (int bt = 0; bt < BT; ++bt)
-          acc[bt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
+        for (int bt = 0; bt < BT; ++bt) {
+          if constexpr (NARROW)
+            acc[bt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
+          else
+            acc[bt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
+        }
       }
     }
     lds_sync();
     cur = nxt;
   }
 
-  // C[row][col]: row = (reg&3) + 8*(reg>>2) + 4*half (+32*bt), col = lane&31.
-  // Combine hi+lo halves (adjacent columns) and store [item][slot][bin][stat].
-  float* out = a.slab + (int64_t)item * (8 * CT) * (32 * BT) * 2;
+  // C[row][col]: 32x32 tile row = (reg&3) + 8*(reg>>2) + 4*kgrp, 16x16 tile row = 4*kgrp + reg;
+  // col = lane's column. Combine hi+lo halves (adjacent columns), store [item][slot][bin][stat].
+  float* out = a.slab + (int64_t)item * (NSLOT * CT) * (NBIN * BT) * 2;
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
+      for (int reg = 0; reg < NREG; ++reg) {
         const float v = acc[bt][ct][reg];
         const float w2 = __shfl_xor(v, 1, kWave);
         if ((col & 1) == 0) {
-          const int row = (reg & 3) + 8 * (reg >> 2) + 4 * half + 32 * bt;
-          const int slot = ct * 8 + slot_sub;
+          const int row = (NARROW ? 4 * kgrp + reg : (reg & 3) + 8 * (reg >> 2) + 4 * kgrp) + NBIN * bt;
+          const int slot = ct * NSLOT + slot_sub;
           const int stat = (col >> 1) & 1;
-          out[((int64_t)slot * (32 * BT) + row) * 2 + stat] = v + w2;
+          out[((int64_t)slot * (NBIN * BT) + row) * 2 + stat] = v + w2;
         }
       }
 }
@@ -424,14 +447,16 @@ void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s) {
   const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
   const dim3 grid((slots + 3) / 4), block(256);
   const bool root = a.slot8 == nullptr;
-#define FDX_HIST_CASE(B, C)                                                                   \
-  if (bt == B && ct == C) {                                                                  \
-    if (root) hipLaunchKernelGGL((hist_mfma_kernel<B, C, true>), grid, block, 0, s, a);      \
-    else hipLaunchKernelGGL((hist_mfma_kernel<B, C, false>), grid, block, 0, s, a);          \
-    return;                                                                                  \
+  // bt 0: narrow 16-bin tile (ct = 1/2/4/8 groups of 4 slots); bt 1/2: 32-bin tiles (ct groups of 8)
+#define FDX_HIST_CASE(B, C, N)                                                                  \
+  if (bt == (N ? 0 : B) && ct == C) {                                                          \
+    if (root) hipLaunchKernelGGL((hist_mfma_kernel<B, C, true, N>), grid, block, 0, s, a);     \
+    else hipLaunchKernelGGL((hist_mfma_kernel<B, C, false, N>), grid, block, 0, s, a);         \
+    return;                                                                                    \
   }
-  FDX_HIST_CASE(1, 1) FDX_HIST_CASE(1, 2) FDX_HIST_CASE(1, 4)
-  FDX_HIST_CASE(2, 1) FDX_HIST_CASE(2, 2) FDX_HIST_CASE(2, 4)
+  FDX_HIST_CASE(1, 1, true) FDX_HIST_CASE(1, 2, true) FDX_HIST_CASE(1, 4, true) FDX_HIST_CASE(1, 8, true)
+  FDX_HIST_CASE(1, 1, false) FDX_HIST_CASE(1, 2, false) FDX_HIST_CASE(1, 4, false)
+  FDX_HIST_CASE(2, 1, false) FDX_HIST_CASE(2, 2, false) FDX_HIST_CASE(2, 4, false)
 #undef FDX_HIST_CASE
 }
 

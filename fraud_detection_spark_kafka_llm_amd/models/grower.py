@@ -65,10 +65,25 @@ class Workspace:
         return self._shards
 
     def slab_for(self, items: int, bt: int, ct: int) -> torch.Tensor:
-        need = items * 8 * ct * 32 * bt * 2
+        slots, bins = tile_shape(bt, ct)
+        need = items * slots * bins * 2
         if self.slab.numel() < need:
             self.slab = torch.empty(need, dtype=torch.float32, device=self.dev)
         return self.slab
+
+
+def tile_shape(bt: int, ct: int) -> tuple:
+    """(node slots, bins) of one histogram work item's partial for tile shape ``bt``."""
+    return (4 * ct, 16) if bt == 0 else (8 * ct, 32 * bt)
+
+
+def pass_ct(bt: int, cnt: int) -> int:
+    """Column tiles for ``cnt`` (<= 32) node slots: groups of 4 (narrow) or 8 slots, power of two."""
+    per = 4 if bt == 0 else 8
+    ct = 1
+    while ct * per < cnt:
+        ct *= 2
+    return ct
 
 
 class FeatureShards:
@@ -173,8 +188,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     with tracing.span("tree.rowstats"):
         C.tree_rowstats(g, h, label, weight, int(params.seed), int(tree_index), bool(bootstrap), mode_rs,
                         ws.rowstats)
-        for grp in Q.groups:   # XCD-ordered items: each XCD gathers within its current row block
-            C.tree_entry_stats_items(grp.item_start, grp.item_end, grp.wave_order(), Q.csc_row, ws.rowstats, ws.est)
+        st, en, order = Q.all_items()   # XCD-ordered items: each XCD gathers within its current row block
+        C.tree_entry_stats_items(st, en, order, Q.csc_row, ws.rowstats, ws.est)
     tot = root_totals(ws)
     if all_reduce is not None:
         tot = all_reduce(tot)
@@ -234,24 +249,27 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         with tracing.span("tree.hist"):
             for s0 in range(0, nb, 32):
                 cnt = min(32, nb - s0)
-                ct = 1 if cnt <= 8 else (2 if cnt <= 16 else 4)
-                s2n = torch.full((8 * ct,), -1, dtype=torch.int32)
-                for k in range(cnt):
-                    s2n[k] = target_of[build[s0 + k]]
-                s2n = s2n.to(dev)
                 slot8 = None
                 if d > 0:
                     C.tree_slot8(ws.row_node, node_slot, s0, cnt, ws.slot8)
                     slot8 = ws.slot8
+                s2n_by_cap = {}
                 for grp in feat_groups:
                     gsel = grp if params.feat_prob >= 1.0 else _rf_subset(grp, Q, params, tree_index,
                                                                           [build[s0 + k] for k in range(cnt)])
                     if gsel.num_items == 0:
                         continue
+                    ct = pass_ct(grp.bt, cnt)
+                    cap = tile_shape(grp.bt, ct)[0]
+                    if cap not in s2n_by_cap:
+                        s2n = torch.full((cap,), -1, dtype=torch.int32)
+                        for k in range(cnt):
+                            s2n[k] = target_of[build[s0 + k]]
+                        s2n_by_cap[cap] = s2n.to(dev)
                     slab = ws.slab_for(gsel.num_items, grp.bt, ct)
                     C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est,
                                       grp.bt, ct, slab, gsel.feat, gsel.feat_item0, gsel.feat_nitems, Q.boff,
-                                      Q.nbins, s2n, hist_target, stride, gsel.wave_order())
+                                      Q.nbins, s2n_by_cap[cap], hist_target, stride, gsel.wave_order())
         totals = torch.tensor(np.stack([stats[n] for n in open_nodes]), dtype=torch.float64, device=dev)
         node_ids = torch.tensor(open_nodes, dtype=torch.int32, device=dev)
         if shards is None:

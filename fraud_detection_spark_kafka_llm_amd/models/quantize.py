@@ -18,6 +18,7 @@ holds identical bins.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -28,12 +29,13 @@ from ..utils import tracing
 
 CSC_PAD = 16
 
-CHUNK = 16384          # entries per histogram work item (one wavefront)
+CHUNK = int(os.environ.get("FDX_HIST_CHUNK", 32768))   # entries per histogram work item (one wavefront)
 
 
 @dataclass
 class BinGroup:
-    """Work items of the features whose bin count fits ``32 * bt`` (one MFMA template)."""
+    """Work items of the features of one MFMA tile shape: ``bt`` 0 = at most 16 bins (narrow
+    16x16x32 tile), 1 / 2 = at most 32 / 64 bins (one or two 32-row 32x32x16 tiles)."""
     bt: int
     item_start: torch.Tensor     # int64 [I]
     item_end: torch.Tensor       # int64 [I]
@@ -113,6 +115,24 @@ class Quantized:
     csc_row: torch.Tensor        # int32 [nnz] (view; CSC_PAD readable entries follow)
     csc_bin: torch.Tensor        # uint8 [nnz] (view; CSC_PAD readable entries follow)
     groups: list = field(default_factory=list)
+    _all_items: Optional[tuple] = None
+
+    def all_items(self) -> tuple:
+        """(item_start, item_end, wave_order) over the items of every group: one XCD-ordered launch
+        for per-entry work that does not depend on the tile shape (entry statistics)."""
+        if self._all_items is None:
+            dev = self.csc_row.device
+            gs = self.groups
+            if not gs:
+                z = torch.zeros(0, dtype=torch.int64, device=dev)
+                self._all_items = (z, z, wave_order(None, 0, dev))
+            else:
+                st = torch.cat([g.item_start for g in gs])
+                en = torch.cat([g.item_end for g in gs])
+                blk = torch.cat([g.item_blk if g.item_blk is not None else
+                                 torch.full((g.num_items,), -1, dtype=torch.int32, device=dev) for g in gs])
+                self._all_items = (st, en, wave_order(blk, int(st.numel()), dev))
+        return self._all_items
     boff_host: np.ndarray = None
     zbin_host: np.ndarray = None
     fid_host: np.ndarray = None
@@ -421,8 +441,8 @@ def _make_groups(colptr: torch.Tensor, nbins: torch.Tensor, chunk: int, csc_row:
         csc_row = torch.zeros(0, dtype=torch.int32, device=dev)
     s0, e0, f0, b0 = _segments(colptr, csc_row, n_rows, row_block, split_min)
     groups = []
-    for bt in (1, 2):
-        lo, hi = (0, 32) if bt == 1 else (33, 64)
+    for bt in (0, 1, 2):    # 0: <= 16 bins (16x16x32 MFMA tile), 1: <= 32, 2: <= 64 bins
+        lo, hi = ((0, 16), (17, 32), (33, 64))[bt]
         sel = (nbins[f0] >= lo) & (nbins[f0] <= hi)
         if not bool(sel.any()):
             continue

@@ -158,17 +158,21 @@ def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
     for grp in Q.groups:
         C.tree_entry_stats_items(grp.item_start, grp.item_end, grp.wave_order(), Q.csc_row, ws.rowstats, ws.est)
     hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.float64, device=dev)
-    for s0 in range(0, nslots, 8 * ct):
-        cnt = min(8 * ct, nslots - s0)
-        s2n = torch.full((8 * ct,), -1, dtype=torch.int32)
-        s2n[:cnt] = torch.arange(s0, s0 + cnt, dtype=torch.int32)
+    from fraud_detection_spark_kafka_llm_amd.models.grower import pass_ct, tile_shape
+
+    P = 8 * ct      # node slots per pass; each tile shape picks its own column-tile count
+    for s0 in range(0, nslots, P):
+        cnt = min(P, nslots - s0)
         slot8 = None
         if not root:
             C.tree_slot8(row_node, node_slot, s0, cnt, ws.slot8)
             slot8 = ws.slot8
         for grp in Q.groups:
-            slab = ws.slab_for(grp.num_items, grp.bt, ct)
-            C.tree_hist_build(grp.item_start, grp.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est, grp.bt, ct,
+            c = pass_ct(grp.bt, cnt)
+            s2n = torch.full((tile_shape(grp.bt, c)[0],), -1, dtype=torch.int32)
+            s2n[:cnt] = torch.arange(s0, s0 + cnt, dtype=torch.int32)
+            slab = ws.slab_for(grp.num_items, grp.bt, c)
+            C.tree_hist_build(grp.item_start, grp.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est, grp.bt, c,
                               slab, grp.feat, grp.feat_item0, grp.feat_nitems, Q.boff, Q.nbins, s2n.to(dev),
                               hist, Q.TB, grp.wave_order())
     return hist.cpu().numpy()
