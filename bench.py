@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--depth-pipeline", type=int, default=2)
     args = ap.parse_args()
 
-    D.init_from_env("nccl")
+    D.init_from_env(os.environ.get("FDX_DIST_BACKEND", "nccl"))   # gloo: rehearse N ranks on one GPU
     rank, world = D.rank(), D.world_size()
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)

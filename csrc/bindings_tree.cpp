@@ -102,6 +102,7 @@ void entry_stats_items(const Tensor& item_start, const Tensor& item_end, const T
   chk(est, dev, at::kInt, "est");
   FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2] int32");
   FDX_CHECK(wave_item.numel() % 4 == 0, "wave_item: 4 slots per workgroup");
+  FDX_CHECK(readable_tail(csc_row, 4), "csc_row needs 4 readable padding entries (quantize.CSC_PAD)");
   const auto* rs = reinterpret_cast<const uint32_t*>(rowstats.data_ptr<int32_t>());
   auto* out = reinterpret_cast<uint32_t*>(est.data_ptr<int32_t>());
   const int32_t ni = (int32_t)item_start.numel();

@@ -85,17 +85,34 @@ __global__ __launch_bounds__(256) void entry_stats_items_kernel(const int64_t* _
   const int item = wave_item[wslot];
   if (item < 0 || item >= num_items) return;
   const int64_t e0 = item_start[item], e1 = item_end[item];
-  // 4 consecutive entries per lane: one 16-B row load, 4 independent gathers, two 16-B stores
-  for (int64_t base = e0 & ~(int64_t)3; base < e1; base += 4 * kWave) {
-    const int64_t e = base + 4 * lane;
-    if (e >= e0 && e + 4 <= e1) {
-      const int4 r = *reinterpret_cast<const int4*>(csc_row + e);
-      const uint2 a = rowstats[r.x], b = rowstats[r.y], c = rowstats[r.z], d = rowstats[r.w];
-      reinterpret_cast<uint4*>(est)[e / 2] = make_uint4(a.x, a.y, b.x, b.y);
-      reinterpret_cast<uint4*>(est)[e / 2 + 1] = make_uint4(c.x, c.y, d.x, d.y);
-    } else {
-      for (int j = 0; j < 4; ++j)
-        if (e + j >= e0 && e + j < e1) est[e + j] = rowstats[csc_row[e + j]];
+  const int64_t e_last = (e1 - 1) & ~(int64_t)3;   // csc_row is padded, so a clamped 4-group is readable
+  // 4 consecutive entries per lane and U steps per round: U 16-B row loads, then 4U independent
+  // gathers in flight, then the 16-B stores (masked at the item's ends).
+  constexpr int U = 4;
+  for (int64_t base = e0 & ~(int64_t)3; base < e1; base += U * 4 * kWave) {
+    int4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = base + (int64_t)u * 4 * kWave + 4 * lane;
+      r[u] = *reinterpret_cast<const int4*>(csc_row + (e < e_last ? e : e_last));
+    }
+    uint2 g[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      g[u][0] = rowstats[r[u].x]; g[u][1] = rowstats[r[u].y];
+      g[u][2] = rowstats[r[u].z]; g[u][3] = rowstats[r[u].w];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = base + (int64_t)u * 4 * kWave + 4 * lane;
+      if (e >= e0 && e + 4 <= e1) {
+        reinterpret_cast<uint4*>(est)[e / 2] = make_uint4(g[u][0].x, g[u][0].y, g[u][1].x, g[u][1].y);
+        reinterpret_cast<uint4*>(est)[e / 2 + 1] = make_uint4(g[u][2].x, g[u][2].y, g[u][3].x, g[u][3].y);
+      } else if (e < e1 && e + 4 > e0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (e + j >= e0 && e + j < e1) est[e + j] = g[u][j];
+      }
     }
   }
 }

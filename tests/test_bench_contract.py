@@ -1,0 +1,46 @@
+"""bench.py output contract (one JSON line from rank 0 with the driver's required keys), at N=1 and
+at N=2 ranks sharing one GPU over gloo (rehearses the multi-rank path: reduce-scatter histograms,
+all-gathered splits, per-rank streaming, max-over-ranks timing)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+TINY = ["--steps", "4", "--warmup", "2", "--rows", "100000", "--trees", "3", "--batch", "4096", "--pool", "2"]
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _check(rec: dict, n: int):
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == n and rec["steps"] == 4 and rec["warmup"] == 2
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0 and rec["higher_is_better"] is True
+    assert rec["config"]["parallelism"] == f"dp{n}" and rec["config"]["global_batch"] == 4096 * n
+    assert rec["stream_accuracy"] > 0.9
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu_contract():
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *TINY], cwd=REPO, capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    _check(_json_line(out.stdout), 1)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_contract_gloo_rehearsal():
+    env = {**os.environ, "FDX_DIST_BACKEND": "gloo"}
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29547", "bench.py", "--gpus", "2", *TINY],
+                         cwd=REPO, capture_output=True, text=True, timeout=900, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    _check(_json_line(out.stdout), 2)
