@@ -386,6 +386,26 @@ void feature_order(const Tensor& indptr, const Tensor& idx, const Tensor& counts
   else FDX_CHECK(false, "counts must be float32 or float64");
 }
 
+// out = min(in, maxv) over uint8 (bin clamp of the count path); in/out 16-byte aligned on the device
+void clamp_u8(const Tensor& in, int64_t maxv, const Tensor& out) {
+  const auto dev = in.device();
+  check_dev(out, dev, "clamp_u8");
+  FDX_CHECK(in.scalar_type() == at::kByte && out.scalar_type() == at::kByte && out.numel() >= in.numel() &&
+                in.is_contiguous() && out.is_contiguous() && maxv >= 0 && maxv <= 255, "clamp_u8 args");
+  if (dev.is_cuda()) {
+    FDX_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "clamp_u8: 16-byte aligned buffers");
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_clamp_u8(in.data_ptr<uint8_t>(), in.numel(), (uint8_t)maxv, out.data_ptr<uint8_t>(),
+                         c10::hip::getCurrentHIPStream(dev.index()).stream());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    const uint8_t* a = in.data_ptr<uint8_t>();
+    uint8_t* b = out.data_ptr<uint8_t>();
+    for (int64_t i = 0; i < in.numel(); ++i) b[i] = a[i] > maxv ? (uint8_t)maxv : a[i];
+  }
+}
+
 // Row-block segment bounds of sorted-row columns (XCD-aware histogram items).
 void block_bounds(const Tensor& csc_row, const Tensor& colptr, const Tensor& cols, int64_t nblk, int64_t row_block,
                   const Tensor& bounds) {
@@ -453,6 +473,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spmv", &spmv, "y = X x (CSR, fp64 accumulate)");
   m.def("spmv_t", &spmv_t, "g += X^T r (CSR, fp64)");
   m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
+  m.def("clamp_u8", &clamp_u8, "uint8 clamp (bins)");
   m.def("block_bounds", &block_bounds, "row-block segment bounds of sorted-row columns");
   m.def("feature_order", &feature_order, "CSR -> CSC by feature (radix sort), docFreq and max count per feature");
   m.def("encode_records", &encode_records, "json.dumps-identical classification records (batch)");

@@ -58,6 +58,7 @@ struct FeatureOrderArgs {
 size_t feature_order_temp_bytes(int64_t nnz, int32_t F);
 template <class V> void launch_feature_order(const FeatureOrderArgs<V>& a, hipStream_t s);
 template <class V> void feature_order_cpu(const FeatureOrderArgs<V>& a);
+void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, hipStream_t s);
 void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
                          int64_t row_block, int64_t* bounds, hipStream_t s);
 void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,

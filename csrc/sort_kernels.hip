@@ -109,6 +109,28 @@ __global__ __launch_bounds__(256) void block_bounds_kernel(const int32_t* __rest
   bounds[t] = lo;
 }
 
+__global__ __launch_bounds__(256) void clamp_u8_kernel(const uint8_t* __restrict__ in, int64_t n, uint8_t maxv,
+                                                       uint8_t* __restrict__ out) {
+  const int64_t n16 = n / 16;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+    uint4 v = reinterpret_cast<const uint4*>(in)[i];
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t x = w[k], y = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t c = (x >> (8 * b)) & 0xffu;
+        y |= (c > maxv ? (uint32_t)maxv : c) << (8 * b);
+      }
+      w[k] = y;
+    }
+    reinterpret_cast<uint4*>(out)[i] = v;
+  }
+  const int64_t t = 16 * n16 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < n && blockIdx.x * 256 + threadIdx.x < 16) out[t] = in[t] > maxv ? maxv : in[t];
+}
+
 inline unsigned grid_for(int64_t n, int64_t cap = 16384) {
   const int64_t b = (n + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > cap ? cap : b));
@@ -154,6 +176,10 @@ void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const in
   if (n > 0)
     hipLaunchKernelGGL(block_bounds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, csc_row, colptr, cols, ncols,
                        nblk, row_block, bounds);
+}
+
+void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(clamp_u8_kernel, dim3(grid_for(n / 16 + 1)), dim3(256), 0, s, in, n, maxv, out);
 }
 
 template void launch_feature_order<float>(const FeatureOrderArgs<float>&, hipStream_t);

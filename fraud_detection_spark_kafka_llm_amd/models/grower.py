@@ -58,6 +58,7 @@ class Workspace:
         self.dev = dev
         self.Q = Q
         self._shards = None
+        self.staging = Staging(dev)
 
     def shards(self, coll) -> "FeatureShards":
         if getattr(self, "_shards", None) is None or self._shards.S != coll.world:
@@ -70,6 +71,74 @@ class Workspace:
         if self.slab.numel() < need:
             self.slab = torch.empty(need, dtype=torch.float32, device=self.dev)
         return self.slab
+
+
+class Staging:
+    """Per-level small host arrays (slot maps, subtraction triples, node totals, partition lists)
+    gathered into one pinned buffer and sent with ONE async H2D copy, instead of a synchronous
+    pageable copy per array (~15 per level, the bulk of the grower's host overhead). Two pinned
+    buffers alternate; an event guards reuse. Tensors returned by ``upload`` are views into a
+    device buffer that the next upload overwrites in stream order, so callers consume them before
+    uploading again (the grower uploads at level start and after the split decisions)."""
+
+    def __init__(self, dev: torch.device, cap: int = 1 << 16):
+        self.dev = dev
+        self.cuda = dev.type == "cuda"
+        self._cap = 0
+        self._host, self._events, self._flip = [None, None], [None, None], 0
+        self._reserve(cap)
+        self._items: list = []
+        self._off = 0
+
+    def _reserve(self, cap: int) -> None:
+        if cap <= self._cap:
+            return
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+        self._cap = cap
+        mk = (lambda: torch.empty(cap, dtype=torch.uint8).pin_memory()) if self.cuda else \
+            (lambda: torch.empty(cap, dtype=torch.uint8))
+        self._host = [mk(), mk()]
+        self._events = [None, None]
+        self._dev = torch.empty(cap, dtype=torch.uint8, device=self.dev)
+
+    def add(self, arr) -> int:
+        a = np.ascontiguousarray(arr)
+        self._items.append(a)
+        return len(self._items) - 1
+
+    def upload(self) -> list:
+        offs, total = [], 0
+        for a in self._items:
+            total = (total + 7) & ~7
+            offs.append(total)
+            total += a.nbytes
+        if total > self._cap:
+            self._reserve(max(total, 2 * self._cap))
+        k = self._flip
+        self._flip ^= 1
+        if self._events[k] is not None:
+            self._events[k].synchronize()
+        host = self._host[k].numpy()
+        for a, o in zip(self._items, offs):
+            host[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        if self.cuda:
+            self._dev[:total].copy_(self._host[k][:total], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._events[k] = ev
+            src = self._dev
+        else:
+            src = self._host[k].clone()
+        out = []
+        for a, o in zip(self._items, offs):
+            t = src[o:o + a.nbytes].view(_TORCH_DTYPE[a.dtype.str[1:]]).view(a.shape)
+            out.append(t)
+        self._items = []
+        return out
+
+
+_TORCH_DTYPE = {"i4": torch.int32, "i8": torch.int64, "f8": torch.float64, "f4": torch.float32}
 
 
 def tile_shape(bt: int, ct: int) -> tuple:
@@ -112,17 +181,6 @@ class FeatureShards:
         self.nbins = Q.nbins[f0:f1].contiguous()
         self.zbin = Q.zbin[f0:f1].contiguous()
         self.fid_orig = Q.fid_orig[f0:f1].contiguous()
-
-
-def _subtract(C, prev_hist, cur_hist, subtract, local, prev_index, TB):
-    """Larger sibling = parent - built sibling (sibling subtraction, K-11)."""
-    if not subtract:
-        return
-    dev = cur_hist.device
-    dst = torch.tensor([local[a] for a, _, _ in subtract], dtype=torch.int32, device=dev)
-    par = torch.tensor([prev_index[p] for _, p, _ in subtract], dtype=torch.int32, device=dev)
-    sib = torch.tensor([local[s] for _, _, s in subtract], dtype=torch.int32, device=dev)
-    C.tree_hist_subtract(prev_hist, cur_hist, dst, par, sib, TB)
 
 
 def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, params, tree_index, Fa, f0):
@@ -239,21 +297,43 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             # local partials of the built nodes (+1 zero pad bin for the shard packing)
             hist_target = torch.zeros((nb, TB + 1, 2), dtype=torch.float64, device=dev)
             stride, target_of = TB + 1, {n: k for k, n in enumerate(build)}
-        # --- node -> slot of the built nodes (slot = position in `build`); the root pass needs none
+        # --- small per-level arrays, one staged upload: node -> slot of the built nodes (slot =
+        # position in `build`), slot -> histogram row per pass and tile shape, subtraction
+        # triples, open-node totals and ids
+        stg = ws.staging
+        h_ns = None
         if d > 0:
-            ns = torch.full((max_nodes,), -1, dtype=torch.int32)
-            for s, n in enumerate(build):
-                ns[n] = s
-            node_slot = ns.to(dev)
-        # --- histograms, 8*ct slots per pass
+            ns = np.full(max_nodes, -1, dtype=np.int32)
+            ns[np.asarray(build, dtype=np.int64)] = np.arange(nb, dtype=np.int32)
+            h_ns = stg.add(ns)
+        passes = []
+        for s0 in range(0, nb, 32):
+            cnt = min(32, nb - s0)
+            caps = {}
+            for grp in feat_groups:
+                cap = tile_shape(grp.bt, pass_ct(grp.bt, cnt))[0]
+                if cap not in caps:
+                    s2n = np.full(cap, -1, dtype=np.int32)
+                    s2n[:cnt] = [target_of[build[s0 + k]] for k in range(cnt)]
+                    caps[cap] = stg.add(s2n)
+            passes.append((s0, cnt, caps))
+        h_sub = None
+        if subtract:
+            h_sub = (stg.add(np.array([local[a] for a, _, _ in subtract], dtype=np.int32)),
+                     stg.add(np.array([prev_index[p] for _, p, _ in subtract], dtype=np.int32)),
+                     stg.add(np.array([local[s] for _, _, s in subtract], dtype=np.int32)))
+        h_tot = stg.add(np.stack([stats[n] for n in open_nodes]).astype(np.float64))
+        h_ids = stg.add(np.array(open_nodes, dtype=np.int32))
+        h_bidx = stg.add(np.array([local[n] for n in build], dtype=np.int64))
+        up = stg.upload()
+        node_slot = up[h_ns] if h_ns is not None else None
+        # --- histograms, up to 32 node slots per pass
         with tracing.span("tree.hist"):
-            for s0 in range(0, nb, 32):
-                cnt = min(32, nb - s0)
+            for s0, cnt, caps in passes:
                 slot8 = None
                 if d > 0:
                     C.tree_slot8(ws.row_node, node_slot, s0, cnt, ws.slot8)
                     slot8 = ws.slot8
-                s2n_by_cap = {}
                 for grp in feat_groups:
                     gsel = grp if params.feat_prob >= 1.0 else _rf_subset(grp, Q, params, tree_index,
                                                                           [build[s0 + k] for k in range(cnt)])
@@ -261,23 +341,19 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                         continue
                     ct = pass_ct(grp.bt, cnt)
                     cap = tile_shape(grp.bt, ct)[0]
-                    if cap not in s2n_by_cap:
-                        s2n = torch.full((cap,), -1, dtype=torch.int32)
-                        for k in range(cnt):
-                            s2n[k] = target_of[build[s0 + k]]
-                        s2n_by_cap[cap] = s2n.to(dev)
                     slab = ws.slab_for(gsel.num_items, grp.bt, ct)
                     C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est,
                                       grp.bt, ct, slab, gsel.feat, gsel.feat_item0, gsel.feat_nitems, Q.boff,
-                                      Q.nbins, s2n_by_cap[cap], hist_target, stride, gsel.wave_order())
-        totals = torch.tensor(np.stack([stats[n] for n in open_nodes]), dtype=torch.float64, device=dev)
-        node_ids = torch.tensor(open_nodes, dtype=torch.int32, device=dev)
+                                      Q.nbins, up[caps[cap]], hist_target, stride, gsel.wave_order())
+        totals, node_ids = up[h_tot], up[h_ids]
+        sub_t = tuple(up[h] for h in h_sub) if h_sub is not None else None
         if shards is None:
             if all_reduce is not None:
                 with tracing.span("tree.allreduce"):
-                    idx = torch.tensor([local[n] for n in build], device=dev)
+                    idx = up[h_bidx]
                     cur_hist.index_copy_(0, idx, all_reduce(cur_hist.index_select(0, idx)))
-            _subtract(C, prev_hist, cur_hist, subtract, local, prev_index, TB)
+            if sub_t is not None:
+                C.tree_hist_subtract(prev_hist, cur_hist, *sub_t, TB)
             with tracing.span("tree.split"):
                 packed = _best_splits(C, cur_hist, totals, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, node_ids, params,
                                       tree_index, Q.Fa, 0)
@@ -288,9 +364,9 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 if nb:
                     packed_in = hist_target.index_select(1, shards.pack_idx).view(nb, shards.S, shards.Bs, 2)
                     mine = coll.reduce_scatter(packed_in.permute(1, 0, 2, 3))
-                    idx = torch.tensor([local[n] for n in build], device=dev)
-                    cur_hist.index_copy_(0, idx, mine[:, : shards.bins].contiguous())
-            _subtract(C, prev_hist, cur_hist, subtract, local, prev_index, shards.bins)
+                    cur_hist.index_copy_(0, up[h_bidx], mine[:, : shards.bins].contiguous())
+            if sub_t is not None:
+                C.tree_hist_subtract(prev_hist, cur_hist, *sub_t, shards.bins)
             with tracing.span("tree.split"):
                 mine = _best_splits(C, cur_hist, totals, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
                                     node_ids, params, tree_index, shards.Fa, shards.f0)
@@ -299,7 +375,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 packed = allt[best_s, torch.arange(nl, device=dev)].cpu().numpy()
         # --- create children
         next_level = []
-        default_child = torch.full((max_nodes,), -1, dtype=torch.int32)
+        default_child = np.full(max_nodes, -1, dtype=np.int32)
         splits = []
         for i, n in enumerate(open_nodes):
             gval, fid, b, l0, l1 = packed[i]
@@ -337,7 +413,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             next_level += [li, ri]
         if splits:
             with tracing.span("tree.partition"):
-                _partition(C, Q, ws, default_child.to(dev), splits)
+                _partition(C, Q, ws, default_child, splits)
         prev_hist = cur_hist
         prev_index = local
         level = next_level
@@ -386,7 +462,9 @@ def _impurity(st, mode) -> float:
     return 1.0 - p0 * p0 - p1 * p1
 
 
-def _partition(C, Q: Quantized, ws: Workspace, default_child: torch.Tensor, splits: list, chunk: int = 1 << 16):
+def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits: list, chunk: int = 1 << 16):
+    """Rows -> children (K-13): every row of a split node moves to the default child, then one pass
+    over the split columns moves the rows present in them whose bin falls on the other side."""
     colptr = Q.colptr.cpu().numpy() if not hasattr(Q, "_colptr_host") else Q._colptr_host
     Q._colptr_host = colptr
     starts, ends, item_split = [], [], []
@@ -396,12 +474,12 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: torch.Tensor, spli
             starts.append(s)
             ends.append(min(b, s + chunk))
             item_split.append(si)
-    dev = Q.device
-    t = lambda v, dt: torch.tensor(v, dtype=dt, device=dev)  # noqa: E731
-    C.tree_partition(ws.row_node, default_child, t(starts, torch.int64), t(ends, torch.int64),
-                     t(item_split, torch.int32), t([s[1] for s in splits], torch.int32),
-                     t([s[2] for s in splits], torch.int32), t([s[3] for s in splits], torch.int32),
-                     t([s[4] for s in splits], torch.int32), Q.csc_row, Q.csc_bin)
+    stg = ws.staging
+    hs = [stg.add(default_child), stg.add(np.array(starts, dtype=np.int64)), stg.add(np.array(ends, dtype=np.int64)),
+          stg.add(np.array(item_split, dtype=np.int32))]
+    hs += [stg.add(np.array([sp[k] for sp in splits], dtype=np.int32)) for k in (1, 2, 3, 4)]
+    up = stg.upload()
+    C.tree_partition(ws.row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin)
 
 
 def _rf_subset(grp, Q: Quantized, params: GrowParams, tree_index: int, nodes: list):

@@ -25,6 +25,7 @@ from typing import Callable, Optional
 import numpy as np
 import torch
 
+from ..ops import native
 from ..utils import tracing
 
 CSC_PAD = 16
@@ -281,7 +282,9 @@ def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_
             torch.cumsum(lens[active], 0, out=colptr[1:])
         n = int(csc_row.numel())
         bin_buf = torch.full((n + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
-        torch.clamp(cnt, max=max_bins - 1, out=bin_buf[:n])
+        if cnt.is_cuda and cnt.data_ptr() % 16:           # compacted copy: realign for the native clamp
+            cnt = cnt.clone()
+        native.lib().clamp_u8(cnt.contiguous(), max_bins - 1, bin_buf[:n])
     boff = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
     torch.cumsum(nb, 0, out=boff[1:])
     Q = Quantized(N, F, fid_orig, nbins.contiguous(), torch.zeros(Fa, dtype=torch.int32, device=dev), boff,
