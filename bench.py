@@ -41,6 +41,7 @@ from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
 from fraud_detection_spark_kafka_llm_amd.ops import text as T  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.parallel import dist as D  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.parallel.affinity import bind_to_gpu  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing  # noqa: E402
 
@@ -108,6 +109,7 @@ def main():
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
     dev = torch.device("cuda", D.local_rank() % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    numa = bind_to_gpu(dev.index)      # pinned rings on the GPU's NUMA node (before any pinned alloc)
     spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=F)
 
     # ------------------------------------------------------------------ 1. GBDT training
@@ -227,6 +229,7 @@ def main():
             "gbdt_nodes_tree0": res.trees[0].num_nodes,
             "stream_accuracy": acc,
             "p50_single_dialogue_ms": p50,
+            "numa_bind_rank0": numa,
         }
         print(json.dumps(out), flush=True)
     D.barrier()

@@ -96,3 +96,12 @@ def test_distributed_idf_equals_global():
     for o in outs:
         assert o[2] == n and o[1] == df.tolist()
         np.testing.assert_array_equal(np.asarray(o[0]), idf)
+
+
+def test_parse_cpulist_and_bind_noop_without_gpu():
+    from fraud_detection_spark_kafka_llm_amd.parallel.affinity import bind_to_gpu, parse_cpulist
+
+    assert parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert parse_cpulist("") == []
+    if not torch.cuda.is_available():
+        assert bind_to_gpu(0)["bound"] is False
