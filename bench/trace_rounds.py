@@ -1,0 +1,41 @@
+"""Per-boosting-round breakdown of a rocprofv3 kernel trace (``*_kernel_trace.csv``).
+
+Rounds are delimited by the ``logistic_grad`` kernel that starts each GBDT round. Prints, for a
+few rounds, the wall time between round starts, the summed kernel time (GPU busy) and the
+per-kernel split of one round.
+
+Usage: python bench/trace_rounds.py gpurun_out/.../run_kernel_trace.csv [--round 6]
+"""
+import argparse
+import collections
+import csv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--round", type=int, default=6)
+    ap.add_argument("--marker", default="logistic_grad")
+    args = ap.parse_args()
+    rows = list(csv.DictReader(open(args.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]]
+    print(f"{len(idx)} rounds")
+    for a, b in zip(idx[1:-1], idx[2:]):
+        seg = rows[a:b]
+        t0, t1 = int(seg[0]["Start_Timestamp"]), int(rows[b]["Start_Timestamp"])
+        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
+        print(f"round wall {(t1 - t0) / 1e6:7.2f} ms  busy {busy / 1e6:7.2f} ms  kernels {len(seg)}")
+    k = min(args.round, len(idx) - 2)
+    seg = rows[idx[k]:idx[k + 1]]
+    c = collections.defaultdict(lambda: [0, 0])
+    for r in seg:
+        name = r["Kernel_Name"][:110]
+        c[name][0] += 1
+        c[name][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for name, (n, t) in sorted(c.items(), key=lambda x: -x[1][1]):
+        print(f"{t / 1e6:8.3f} ms {n:4d}  {name}")
+
+
+if __name__ == "__main__":
+    main()

@@ -149,7 +149,7 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
                 const optional<Tensor>& slot8_t, const Tensor& est, int64_t bt, int64_t ct, const Tensor& slab,
                 const Tensor& feat, const Tensor& feat_item0, const Tensor& feat_nitems, const Tensor& boff,
                 const Tensor& nbins, const Tensor& slot_to_node, const Tensor& hist, int64_t TB,
-                const optional<Tensor>& wave_item) {
+                const optional<Tensor>& wave_item, const optional<Tensor>& rowstats) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
@@ -171,15 +171,25 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   const int64_t tile_slots = bt == 0 ? 4 * ct : 8 * ct, tile_bins = bt == 0 ? 16 : 32 * bt;
   FDX_CHECK(slot_to_node.numel() == tile_slots, "slot_to_node must have one entry per tile slot");
   FDX_CHECK(csc_row.numel() == csc_bin.numel(), "csc arrays");
-  FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2]");
+  const bool gather = rowstats.has_value() && rowstats->defined();
+  if (gather) {
+    // gather mode: statistics per row, est is not read
+    chk(*rowstats, dev, at::kInt, "rowstats");
+    FDX_CHECK(rowstats->dim() == 2 && rowstats->size(1) == 2, "rowstats must be [N,2] int32");
+    FDX_CHECK(reinterpret_cast<uintptr_t>(rowstats->data_ptr()) % 8 == 0, "rowstats must be 8-byte aligned");
+    FDX_CHECK(!slot8_t || slot8_t->numel() == rowstats->size(0), "slot8 and rowstats row counts differ");
+  } else {
+    FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2]");
+    FDX_CHECK(reinterpret_cast<uintptr_t>(est.data_ptr()) % 16 == 0 && readable_tail(est, 8),
+              "est must be 16-byte aligned with 4 readable padding entries (see quantize.CSC_PAD)");
+  }
   FDX_CHECK(TB >= 0 && boff.numel() == nbins.numel() + 1, "boff must be [Fa+1]");
   FDX_CHECK(hist.numel() % (2 * std::max<int64_t>(TB, 1)) == 0, "hist must be [nodes, TB, 2]");
-  FDX_CHECK(reinterpret_cast<uintptr_t>(csc_row.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(est.data_ptr()) % 16 == 0 &&
+  FDX_CHECK(reinterpret_cast<uintptr_t>(csc_row.data_ptr()) % 16 == 0 &&
                 reinterpret_cast<uintptr_t>(csc_bin.data_ptr()) % 4 == 0,
-            "csc_row/est must be 16-byte and csc_bin 4-byte aligned");
-
-  FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_bin, 4) && readable_tail(est, 8),
-            "csc_row/csc_bin/est need 4 readable padding entries behind their end (see quantize.CSC_PAD)");
+            "csc_row must be 16-byte and csc_bin 4-byte aligned");
+  FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_bin, 4),
+            "csc_row/csc_bin need 4 readable padding entries behind their end (see quantize.CSC_PAD)");
   fdx::HistArgs h{};
   h.item_start = item_start.data_ptr<int64_t>();
   h.item_end = item_end.data_ptr<int64_t>();
@@ -187,7 +197,8 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   h.csc_row = csc_row.data_ptr<int32_t>();
   h.csc_bin = csc_bin.data_ptr<uint8_t>();
   h.slot8 = slot8_t ? slot8_t->data_ptr<uint8_t>() : nullptr;
-  h.est = reinterpret_cast<const uint32_t*>(est.data_ptr<int32_t>());
+  h.est = gather ? nullptr : reinterpret_cast<const uint32_t*>(est.data_ptr<int32_t>());
+  h.rowstats = gather ? reinterpret_cast<const uint32_t*>(rowstats->data_ptr<int32_t>()) : nullptr;
   if (wave_item) {
     chk(*wave_item, dev, at::kInt, "wave_item");
     FDX_CHECK(wave_item->numel() % 4 == 0, "wave_item: 4 slots per workgroup");

@@ -51,7 +51,8 @@ struct HistArgs {
   const uint8_t* csc_bin;
   const uint8_t* slot8;           // [N] relative slot, 0xff = not built; nullptr = root pass (all slot 0)
   const uint32_t* est;            // [nnz * 2] packed statistics in entry order
-  float* slab;                    // [I][slots][bins][2]: 32-bin tiles [8*CT][32*BT], narrow [4*CT][16]
+  const uint32_t* rowstats;       // [N * 2] gather mode (est unused): statistics gathered per live entry
+  float* slab;                   // [I][slots][bins][2]: 32-bin tiles [8*CT][32*BT], narrow [4*CT][16]
   const int32_t* wave_item;       // [num_slots] item of each wave slot (-1 idle); nullptr: slot = item
   int32_t num_slots;
 };

@@ -72,12 +72,14 @@ void hist_cpu(const HistArgs& h, const HistReduceArgs& r, int slots) {
       for (int i = 0; i < r.feat_nitems[li]; ++i) {
         const int64_t it = r.feat_item0[li] + i;
         for (int64_t e = h.item_start[it]; e < h.item_end[it]; ++e) {
-          const int s = h.slot8 ? (int)h.slot8[h.csc_row[e]] : 0;
+          const int64_t row = h.csc_row[e];
+          const int s = h.slot8 ? (int)h.slot8[row] : 0;
           if (s >= slots) continue;
           const int b = h.csc_bin[e];
           if (b >= nb) continue;
-          acc[((size_t)s * nb + b) * 2] += unpack(h.est[2 * e]);
-          acc[((size_t)s * nb + b) * 2 + 1] += unpack(h.est[2 * e + 1]);
+          const uint32_t* st = h.rowstats ? h.rowstats + 2 * row : h.est + 2 * e;
+          acc[((size_t)s * nb + b) * 2] += unpack(st[0]);
+          acc[((size_t)s * nb + b) * 2 + 1] += unpack(st[1]);
         }
       }
       for (int s = 0; s < slots; ++s) {

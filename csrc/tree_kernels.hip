@@ -154,6 +154,55 @@ __device__ __forceinline__ void load_step(const HistArgs& a, int64_t e, int64_t 
   d.q = make_uint4(v2 ? q.x : 0u, v2 ? q.y : 0u, v3 ? q.z : 0u, v3 ? q.w : 0u);
 }
 
+// Gather mode: only rows and bins stream (5 B per entry); the 1-byte slot and, for live entries
+// only, the 8-byte row statistics are gathered from the current row block's slice (~1.1 MB,
+// resident in the XCD's L2 under the XCD-ordered item placement). No per-tree entry-order copy
+// of the statistics is made, and entries outside the nodes being built cost no statistics bytes.
+struct RowStep {
+  int4 r4;
+  uint32_t bins4;
+};
+
+__device__ __forceinline__ void load_rows(const HistArgs& a, int64_t e, int64_t e0, int64_t e1, int64_t e_last,
+                                          RowStep& d) {
+  const int64_t el = e < e_last ? e : e_last;
+  const uint32_t bins = *reinterpret_cast<const uint32_t*>(a.csc_bin + el);
+  const int4 r = *reinterpret_cast<const int4*>(a.csc_row + el);
+  const bool v0 = e >= e0 && e < e1, v1 = e + 1 >= e0 && e + 1 < e1;
+  const bool v2 = e + 2 >= e0 && e + 2 < e1, v3 = e + 3 >= e0 && e + 3 < e1;
+  const uint32_t keep = (v0 ? 0xffu : 0u) | (v1 ? 0xff00u : 0u) | (v2 ? 0xff0000u : 0u) | (v3 ? 0xff000000u : 0u);
+  d.bins4 = (bins & keep) | ~keep;
+  d.r4 = make_int4(v0 ? r.x : -1, v1 ? r.y : -1, v2 ? r.z : -1, v3 ? r.w : -1);
+}
+
+// slot byte of each of the 4 entries (0xff: outside the item or not in a node of this pass)
+template <bool ROOT>
+__device__ __forceinline__ uint32_t entry_slots(const HistArgs& a, int4 r4) {
+  if constexpr (ROOT) {
+    return (r4.x >= 0 ? 0u : 0xffu) | (r4.y >= 0 ? 0u : 0xff00u) | (r4.z >= 0 ? 0u : 0xff0000u) |
+           (r4.w >= 0 ? 0u : 0xff000000u);
+  } else {
+    const uint32_t s0 = a.slot8[r4.x >= 0 ? r4.x : 0];
+    const uint32_t s1 = a.slot8[r4.y >= 0 ? r4.y : 0];
+    const uint32_t s2 = a.slot8[r4.z >= 0 ? r4.z : 0];
+    const uint32_t s3 = a.slot8[r4.w >= 0 ? r4.w : 0];
+    return (r4.x >= 0 ? s0 : 0xffu) | ((r4.y >= 0 ? s1 : 0xffu) << 8) | ((r4.z >= 0 ? s2 : 0xffu) << 16) |
+           ((r4.w >= 0 ? s3 : 0xffu) << 24);
+  }
+}
+
+// packed statistics of the live entries among the 4 (0 for dead ones: they are never staged)
+__device__ __forceinline__ void gather_stats(const uint2* __restrict__ rs, int4 r4, uint32_t slots4, uint32_t w[8]) {
+  const int32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint2 v = make_uint2(0u, 0u);
+    if (((slots4 >> (8 * j)) & 0xffu) != 0xffu) v = rs[rr[j]];
+    w[2 * j] = v.x;
+    w[2 * j + 1] = v.y;
+  }
+}
+
 // ------------------------------------------------------------------ MFMA histogram
 // One wave per work item (a chunk of one feature column); per step the wave takes 256 entries,
 // 4 consecutive ones per lane so that rows (int4), bins (u32) and statistics (2 x uint4) are
@@ -165,7 +214,15 @@ __device__ __forceinline__ void load_step(const HistArgs& a, int64_t e, int64_t 
 // v_mfma_f32_16x16x32_bf16: 16 bins x (4 slots x 4 stat halves), 32 entries per K-step; otherwise
 // v_mfma_f32_32x32x16_bf16: 32 bins x (8 slots x 4 stat halves), 16 entries per K-step. Operand
 // construction is VALU-issue bound, so the narrow tile halves the one-hot work per entry.
-template <int BT, int CT, bool ROOT, bool NARROW>
+// GATHER selects where the statistics come from:
+//   false  per-tree entry-order copy streamed with the rows and bins (load_step);
+//   true   row gathers (see load_rows): rows/bins of step i+3, slots of step i+2 and statistics
+//          of step i+1 are in flight while step i is staged and multiplied. (Measured at 10M
+//          rows / 1B entries: 34 ms per depth-6 round against 38.5 ms streaming, which also
+//          pays a per-tree entry-statistics pass; a 16-byte (slot, statistics) record per row
+//          and level, gathered once per entry, was slower still at 45 ms: the gathers are bound
+//          by L2 lines moved, not by instructions.)
+template <int BT, int CT, bool ROOT, bool NARROW, bool GATHER>
 __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
   constexpr int G = 4 * kWave;                 // entries per wave step
   constexpr int KS = NARROW ? 32 : 16;         // entries per MFMA K-step
@@ -200,26 +257,49 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
   const int64_t first = e0 & ~(int64_t)3;
   const int64_t e_last = (e1 - 1) & ~(int64_t)3;   // last 4-group holding an entry of the item
   StepData cur, nxt;
-  load_step<ROOT>(a, first + 4 * lane, e0, e1, e_last, cur);
+  // gather-mode pipeline state: statistics/slots/bins of step i, slots of step i+1, rows of i+1, i+2
+  const uint2* rs = reinterpret_cast<const uint2*>(a.rowstats);
+  RowStep g1, g2;
+  uint32_t g_sl0 = 0, g_sl1 = 0, g_bins0 = 0, g_w[8];
+  if constexpr (GATHER) {
+    RowStep g0;
+    load_rows(a, first + 4 * lane, e0, e1, e_last, g0);
+    load_rows(a, first + G + 4 * lane, e0, e1, e_last, g1);
+    g_sl0 = entry_slots<ROOT>(a, g0.r4);
+    g_bins0 = g0.bins4;
+    g_sl1 = entry_slots<ROOT>(a, g1.r4);
+    gather_stats(rs, g0.r4, g_sl0, g_w);
+    load_rows(a, first + 2 * G + 4 * lane, e0, e1, e_last, g2);
+  } else {
+    load_step<ROOT>(a, first + 4 * lane, e0, e1, e_last, cur);
+  }
   for (int64_t base = first; base < e1; base += G) {
-    // slot of each of the lane's 4 entries (the only random access: a 1-byte table, L2-resident)
-    uint32_t slots4;
-    if constexpr (ROOT) {
-      slots4 = (cur.r4.x >= 0 ? 0u : 0xffu) | (cur.r4.y >= 0 ? 0u : 0xff00u) | (cur.r4.z >= 0 ? 0u : 0xff0000u) |
-               (cur.r4.w >= 0 ? 0u : 0xff000000u);
+    uint32_t slots4, bins4, w[8];
+    if constexpr (GATHER) {
+      slots4 = g_sl0;
+      bins4 = g_bins0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = g_w[j];
+      // statistics of step i+1, slots of step i+2, rows of step i+3 (clamped, so unconditional)
+      gather_stats(rs, g1.r4, g_sl1, g_w);
+      const uint32_t sl2 = entry_slots<ROOT>(a, g2.r4);
+      RowStep g3;
+      load_rows(a, base + 3 * G + 4 * lane, e0, e1, e_last, g3);
+      g_sl0 = g_sl1;
+      g_bins0 = g1.bins4;
+      g_sl1 = sl2;
+      g1 = g2;
+      g2 = g3;
     } else {
-      const uint32_t s0 = a.slot8[cur.r4.x >= 0 ? cur.r4.x : 0];
-      const uint32_t s1 = a.slot8[cur.r4.y >= 0 ? cur.r4.y : 0];
-      const uint32_t s2 = a.slot8[cur.r4.z >= 0 ? cur.r4.z : 0];
-      const uint32_t s3 = a.slot8[cur.r4.w >= 0 ? cur.r4.w : 0];
-      slots4 = (cur.r4.x >= 0 ? s0 : 0xffu) | ((cur.r4.y >= 0 ? s1 : 0xffu) << 8) |
-               ((cur.r4.z >= 0 ? s2 : 0xffu) << 16) | ((cur.r4.w >= 0 ? s3 : 0xffu) << 24);
+      // slot of each of the lane's 4 entries (the only random access: a 1-byte table, L2-resident)
+      slots4 = entry_slots<ROOT>(a, cur.r4);
+      // prefetch the next step (clamped, so unconditional) while this one is staged and multiplied
+      load_step<ROOT>(a, base + G + 4 * lane, e0, e1, e_last, nxt);
+      bins4 = cur.bins4;
+      w[0] = cur.p.x; w[1] = cur.p.y; w[2] = cur.p.z; w[3] = cur.p.w;
+      w[4] = cur.q.x; w[5] = cur.q.y; w[6] = cur.q.z; w[7] = cur.q.w;
     }
-    // prefetch the next step (clamped, so unconditional) while this one is staged and multiplied
-    load_step<ROOT>(a, base + G + 4 * lane, e0, e1, e_last, nxt);
-    const uint32_t bins4 = cur.bins4;
     const bool any = slots4 != 0xffffffffu;
-    const uint32_t w[8] = {cur.p.x, cur.p.y, cur.p.z, cur.p.w, cur.q.x, cur.q.y, cur.q.z, cur.q.w};
     unsigned long long live = 0;
     int n_live = G;
     if constexpr (ROOT) {
@@ -305,7 +385,7 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
       }
     }
     lds_sync();
-    cur = nxt;
+    if constexpr (!GATHER) cur = nxt;
   }
 
   // C[row][col]: 32x32 tile row = (reg&3) + 8*(reg>>2) + 4*kgrp, 16x16 tile row = 4*kgrp + reg;
@@ -464,17 +544,23 @@ void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s) {
   const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
   const dim3 grid((slots + 3) / 4), block(256);
   const bool root = a.slot8 == nullptr;
+  const bool gather = a.rowstats != nullptr;
   // bt 0: narrow 16-bin tile (ct = 1/2/4/8 groups of 4 slots); bt 1/2: 32-bin tiles (ct groups of 8)
-#define FDX_HIST_CASE(B, C, N)                                                                  \
-  if (bt == (N ? 0 : B) && ct == C) {                                                          \
-    if (root) hipLaunchKernelGGL((hist_mfma_kernel<B, C, true, N>), grid, block, 0, s, a);     \
-    else hipLaunchKernelGGL((hist_mfma_kernel<B, C, false, N>), grid, block, 0, s, a);         \
-    return;                                                                                    \
+#define FDX_HIST_SRC(B, C, N, S)                                                                         \
+  if (gather == S) {                                                                                    \
+    if (root) hipLaunchKernelGGL((hist_mfma_kernel<B, C, true, N, S>), grid, block, 0, s, a);           \
+    else hipLaunchKernelGGL((hist_mfma_kernel<B, C, false, N, S>), grid, block, 0, s, a);               \
+  }
+#define FDX_HIST_CASE(B, C, N)                                                                           \
+  if (bt == (N ? 0 : B) && ct == C) {                                                                   \
+    FDX_HIST_SRC(B, C, N, false) FDX_HIST_SRC(B, C, N, true)                                            \
+    return;                                                                                             \
   }
   FDX_HIST_CASE(1, 1, true) FDX_HIST_CASE(1, 2, true) FDX_HIST_CASE(1, 4, true) FDX_HIST_CASE(1, 8, true)
   FDX_HIST_CASE(1, 1, false) FDX_HIST_CASE(1, 2, false) FDX_HIST_CASE(1, 4, false)
   FDX_HIST_CASE(2, 1, false) FDX_HIST_CASE(2, 2, false) FDX_HIST_CASE(2, 4, false)
 #undef FDX_HIST_CASE
+#undef FDX_HIST_SRC
 }
 
 void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s) {

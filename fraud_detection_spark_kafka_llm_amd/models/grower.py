@@ -2,8 +2,9 @@
 
 Per level (all nodes of the level batched into every launch):
   1. ``tree_slot8``        1-byte slot of the node being built per row (0xff: not built)
-  2. ``tree_hist_build``   MFMA histograms of the smaller child of each sibling pair (+ reduce),
-                           streaming the per-tree entry-order statistics (``tree_entry_stats``)
+  2. ``tree_hist_build``   MFMA histograms of the smaller child of each sibling pair (+ reduce);
+                           rows/bins stream, row statistics are gathered for live entries only
+                           (device), or streamed from a per-tree entry-order copy (host)
   3. all-reduce            histograms of the built nodes across data-parallel ranks (RCCL)
   4. ``tree_hist_subtract`` larger sibling = parent - built sibling
   5. ``tree_split_find``   best (feature, bin) per (node, feature); argmax per node on device
@@ -15,6 +16,7 @@ needed. Node statistics of children come from the parent's split (as in Spark an
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -45,11 +47,17 @@ class GrowParams:
 class Workspace:
     """Per-engine device buffers reused across trees (slab, row/entry statistics, slot table)."""
 
-    def __init__(self, Q: Quantized, max_nodes_per_level: int):
+    def __init__(self, Q: Quantized, max_nodes_per_level: int, src: Optional[str] = None):
         dev = Q.device
         self.rowstats = torch.empty((Q.n_rows, 2), dtype=torch.int32, device=dev)
         nnz = Q.csc_row.numel()
-        self.est = torch.zeros((nnz + CSC_PAD, 2), dtype=torch.int32, device=dev)[:nnz]
+        # where the histogram kernels read the row statistics (see stats_source)
+        self.src = stats_source(dev) if src is None else src
+        if self.src not in STATS_SOURCES:
+            raise ValueError(f"statistics source must be one of {STATS_SOURCES}")
+        self.gather = self.src != "stream"
+        n_est = 0 if self.gather else nnz
+        self.est = torch.zeros((n_est + CSC_PAD, 2), dtype=torch.int32, device=dev)[:n_est]
         self.slot8 = torch.empty(Q.n_rows, dtype=torch.uint8, device=dev)
         self.row_node = torch.zeros(Q.n_rows, dtype=torch.int32, device=dev)
         self.max_items = max((g.num_items for g in Q.groups), default=0)
@@ -71,6 +79,21 @@ class Workspace:
         if self.slab.numel() < need:
             self.slab = torch.empty(need, dtype=torch.float32, device=self.dev)
         return self.slab
+
+
+STATS_SOURCES = ("stream", "gather")
+
+
+def stats_source(dev: torch.device) -> str:
+    """Where histogram kernels read row statistics (``FDX_HIST_SRC`` overrides):
+    ``stream``  a per-tree entry-order copy (est) streamed with rows and bins (host default);
+    ``gather``  1-byte slot + 8-byte statistics gathered per live entry from the row-block slice
+                that the XCD-ordered item placement keeps in L2 (device default: no per-tree
+                copy pass, no statistics bytes for entries outside the nodes being built)."""
+    env = os.environ.get("FDX_HIST_SRC")
+    if env:
+        return env
+    return "gather" if dev.type == "cuda" else "stream"
 
 
 class Staging:
@@ -246,8 +269,9 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     with tracing.span("tree.rowstats"):
         C.tree_rowstats(g, h, label, weight, int(params.seed), int(tree_index), bool(bootstrap), mode_rs,
                         ws.rowstats)
-        st, en, order = Q.all_items()   # XCD-ordered items: each XCD gathers within its current row block
-        C.tree_entry_stats_items(st, en, order, Q.csc_row, ws.rowstats, ws.est)
+        if not ws.gather:
+            st, en, order = Q.all_items()   # XCD-ordered items: each XCD gathers within its current row block
+            C.tree_entry_stats_items(st, en, order, Q.csc_row, ws.rowstats, ws.est)
     tot = root_totals(ws)
     if all_reduce is not None:
         tot = all_reduce(tot)
@@ -344,7 +368,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                     slab = ws.slab_for(gsel.num_items, grp.bt, ct)
                     C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est,
                                       grp.bt, ct, slab, gsel.feat, gsel.feat_item0, gsel.feat_nitems, Q.boff,
-                                      Q.nbins, up[caps[cap]], hist_target, stride, gsel.wave_order())
+                                      Q.nbins, up[caps[cap]], hist_target, stride, gsel.wave_order(),
+                                      ws.rowstats if ws.gather else None)
         totals, node_ids = up[h_tot], up[h_ids]
         sub_t = tuple(up[h] for h in h_sub) if h_sub is not None else None
         if shards is None:

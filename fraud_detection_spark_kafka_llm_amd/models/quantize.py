@@ -391,7 +391,7 @@ def _generic_path(idx, val, F, max_bins, all_gather):
     return remap, nbins, zb.to(torch.int32), thresholds, eb, full_keep
 
 
-ROW_BLOCK = 1 << 17         # rows per XCD row block: 1 B slot + 8 B statistics per row ~ 1.1 MB
+ROW_BLOCK = int(os.environ.get("FDX_ROW_BLOCK", 1 << 17))   # rows per XCD row block: 1 B slot + 8 B statistics per row ~ 1.1 MB
 SPLIT_MIN = 1 << 13         # columns with fewer entries stay whole (their gathers are few)
 
 

@@ -142,12 +142,15 @@ def test_random_forest_bootstrap_and_sampling_are_deterministic():
 
 
 # --------------------------------------------------------------------------------------------- GPU
-def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
+def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False, src="stream"):
+    """``src``: where the kernel reads row statistics (grower.stats_source): the per-tree
+    entry-order copy or per-entry row gathers."""
     C = native.lib()
     n = row_node_np.shape[0]
     # odd chunk: unaligned item starts; small row blocks: dense columns split per block (XCD order)
     Q = quantize(vc.to(dev), max_bins=max_bins, chunk=509, row_block=1500, split_min=64)
-    ws = Workspace(Q, 64)
+    ws = Workspace(Q, 64, src=src)
+    gather = src != "stream"
     row_node = torch.from_numpy(row_node_np).to(dev)
     node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
     node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
@@ -155,8 +158,9 @@ def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
     gg = torch.from_numpy(np.linspace(-1, 1, n).astype(np.float32)).to(dev)
     hh = torch.from_numpy(np.linspace(0.01, 0.25, n).astype(np.float32)).to(dev)
     C.tree_rowstats(gg, hh, None, None, 0, 0, False, 0, ws.rowstats)
-    for grp in Q.groups:
-        C.tree_entry_stats_items(grp.item_start, grp.item_end, grp.wave_order(), Q.csc_row, ws.rowstats, ws.est)
+    if not gather:
+        for grp in Q.groups:
+            C.tree_entry_stats_items(grp.item_start, grp.item_end, grp.wave_order(), Q.csc_row, ws.rowstats, ws.est)
     hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.float64, device=dev)
     from fraud_detection_spark_kafka_llm_amd.models.grower import pass_ct, tile_shape
 
@@ -174,7 +178,7 @@ def _hist_on(dev, vc, max_bins, ct, nslots, row_node_np, root=False):
             slab = ws.slab_for(grp.num_items, grp.bt, c)
             C.tree_hist_build(grp.item_start, grp.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est, grp.bt, c,
                               slab, grp.feat, grp.feat_item0, grp.feat_nitems, Q.boff, Q.nbins, s2n.to(dev),
-                              hist, Q.TB, grp.wave_order())
+                              hist, Q.TB, grp.wave_order(), ws.rowstats if gather else None)
     return hist.cpu().numpy()
 
 
@@ -232,6 +236,8 @@ def test_host_histogram_matches_numpy():
         ok = (s >= 0) & (s < 5)
         np.add.at(ref, (s[ok], boff[f] + bins[e][ok]), g[rows[e][ok]])
     np.testing.assert_allclose(hist[:, :, 0], ref, rtol=1e-4, atol=1e-4)
+    # row-gather mode reads the same statistics: identical sums
+    np.testing.assert_array_equal(_hist_on("cpu", vc, 16, 1, 5, row_node, src="gather"), hist)
 
 
 @pytest.mark.gpu
@@ -246,10 +252,11 @@ def test_gpu_mfma_histograms_match_host(ct, nslots, max_bins):
     for root in (False, True):
         ns = 1 if root else nslots
         a = _hist_on("cpu", vc, max_bins, ct, ns, row_node, root)
-        b = _hist_on("cuda:0", vc, max_bins, ct, ns, row_node, root)
         # device chunks accumulate in fp32 (MFMA), host in fp64: allow fp32 rounding of the partials
         scale = np.abs(a).max()
-        np.testing.assert_allclose(b, a, rtol=2e-6, atol=2e-7 * scale)
+        for src in ("stream", "gather"):
+            b = _hist_on("cuda:0", vc, max_bins, ct, ns, row_node, root, src)
+            np.testing.assert_allclose(b, a, rtol=2e-6, atol=2e-7 * scale)
 
 
 @pytest.mark.gpu
