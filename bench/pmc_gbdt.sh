@@ -1,19 +1,23 @@
 #!/bin/bash
-# PMC counter passes over a short GBDT run on one MI355X (one rocprofv3 run per counter group,
-# each within the per-block hardware limits). Usage (GPU box, repo root):
-#   bash bench/pmc_gbdt.sh [rows] [trees] [outdir]
+# PMC counter passes over a short GBDT run on one MI355X: one rocprofv3 run per argument, each
+# argument a space-separated counter group within the per-block hardware limits (<= 8 SQ,
+# 4 TCC, 4 TCP, 2 TA, 2 TD, 2 GRBM). Usage (GPU box, repo root):
+#   ROWS=2000000 TREES=3 OUT=gpurun_out/pmc bash bench/pmc_gbdt.sh "SQ_WAVES SQ_INSTS_VALU" "TCC_HIT_sum TCC_MISS_sum"
 set -e
-ROWS=${1:-2000000}
-TREES=${2:-3}
-OUT=${3:-gpurun_out/pmc_gbdt}
+ROWS=${ROWS:-2000000}
+TREES=${TREES:-3}
+OUT=${OUT:-gpurun_out/pmc_gbdt}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-run() {
-  local tag=$1
-  shift
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$OUT/$tag" -o run -- \
-    python3 bench/gbdt_train.py --rows "$ROWS" --trees "$TREES" > "$OUT/$tag.log" 2>&1
-}
-run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES
-run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAIT_ANY TA_TA_BUSY TA_FLAT_READ_WAVEFRONTS GRBM_GUI_ACTIVE
-run mem TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE
+i=0
+dirs=()
+for group in "$@"; do
+  i=$((i + 1))
+  # shellcheck disable=SC2086
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $group --output-format csv -d "$OUT/p$i" -o run -- \
+    python3 bench/gbdt_train.py --rows "$ROWS" --trees "$TREES" > "$OUT/p$i.log" 2>&1
+  dirs+=("$OUT/p$i")
+done
+# the raw per-dispatch CSVs of a 10M-row run exceed what gpurun copies back: keep the summary
+python3 bench/pmc_summary.py "${dirs[@]}" --match "${MATCH:-fdx::}" > "$OUT/summary.txt"
+if [ -z "$KEEP_RAW" ]; then rm -rf "${dirs[@]}"; fi
