@@ -392,7 +392,7 @@ def _generic_path(idx, val, F, max_bins, all_gather):
 
 
 ROW_BLOCK = int(os.environ.get("FDX_ROW_BLOCK", 1 << 17))   # rows per XCD row block: 1 B slot + 8 B statistics per row ~ 1.1 MB
-SPLIT_MIN = 1 << 13         # columns with fewer entries stay whole (their gathers are few)
+SPLIT_MIN = int(os.environ.get("FDX_SPLIT_MIN", 1 << 13))   # columns with fewer entries stay whole (their gathers are few)
 
 
 def _segments(colptr: torch.Tensor, csc_row: torch.Tensor, n_rows: int, row_block: int = ROW_BLOCK,
