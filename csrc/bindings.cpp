@@ -407,6 +407,31 @@ void clamp_u8(const Tensor& in, int64_t maxv, const Tensor& out) {
 }
 
 // Row-block segment bounds of sorted-row columns (XCD-aware histogram items).
+void copy_segments(const Tensor& src_row, const Tensor& src_key, const Tensor& seg_src, const Tensor& seg_dst,
+                   const Tensor& seg_len, const Tensor& dst_row, const Tensor& dst_key) {
+  const auto dev = src_row.device();
+  for (const Tensor* t : {&src_key, &seg_src, &seg_dst, &seg_len, &dst_row, &dst_key}) check_dev(*t, dev, "copy_segments");
+  TORCH_CHECK(src_row.scalar_type() == at::kInt && dst_row.scalar_type() == at::kInt && src_key.scalar_type() == at::kByte &&
+                  dst_key.scalar_type() == at::kByte && seg_src.scalar_type() == at::kLong &&
+                  seg_dst.scalar_type() == at::kLong && seg_len.scalar_type() == at::kLong,
+              "copy_segments dtypes");
+  TORCH_CHECK(src_row.numel() == src_key.numel() && dst_row.numel() == dst_key.numel() &&
+                  seg_src.numel() == seg_dst.numel() && seg_src.numel() == seg_len.numel(),
+              "copy_segments sizes");
+  const int64_t n = seg_src.numel();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_copy_segments(src_row.data_ptr<int32_t>(), src_key.data_ptr<uint8_t>(), seg_src.data_ptr<int64_t>(),
+                              seg_dst.data_ptr<int64_t>(), seg_len.data_ptr<int64_t>(), n, dst_row.data_ptr<int32_t>(),
+                              dst_key.data_ptr<uint8_t>(), c10::hip::getCurrentHIPStream(dev.index()).stream());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::copy_segments_cpu(src_row.data_ptr<int32_t>(), src_key.data_ptr<uint8_t>(), seg_src.data_ptr<int64_t>(),
+                           seg_dst.data_ptr<int64_t>(), seg_len.data_ptr<int64_t>(), n, dst_row.data_ptr<int32_t>(),
+                           dst_key.data_ptr<uint8_t>());
+  }
+}
+
 void block_bounds(const Tensor& csc_row, const Tensor& colptr, const Tensor& cols, int64_t nblk, int64_t row_block,
                   const Tensor& bounds) {
   const auto dev = csc_row.device();
@@ -474,6 +499,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spmv_t", &spmv_t, "g += X^T r (CSR, fp64)");
   m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
   m.def("clamp_u8", &clamp_u8, "uint8 clamp (bins)");
+  m.def("copy_segments", &copy_segments, "segment copy of (row, key) arrays");
   m.def("block_bounds", &block_bounds, "row-block segment bounds of sorted-row columns");
   m.def("feature_order", &feature_order, "CSR -> CSC by feature (radix sort), docFreq and max count per feature");
   m.def("encode_records", &encode_records, "json.dumps-identical classification records (batch)");

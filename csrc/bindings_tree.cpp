@@ -30,13 +30,9 @@ const T* opt(const optional<Tensor>& t) { return (t && t->defined()) ? t->data_p
 
 hipStream_t stream(const at::Device& d) { return c10::hip::getCurrentHIPStream(d.index()).stream(); }
 
-void rowstats(const optional<Tensor>& g, const optional<Tensor>& h, const optional<Tensor>& label,
-              const optional<Tensor>& weight, int64_t seed, int64_t tree, bool bootstrap, int64_t mode,
-              const Tensor& out) {
-  const auto dev = out.device();
-  chk(out, dev, at::kInt, "rowstats");
-  FDX_CHECK(out.dim() == 2 && out.size(1) == 2, "rowstats must be [N,2] int32");
-  const int64_t N = out.size(0);
+fdx::QuantArgs quant_args(const optional<Tensor>& g, const optional<Tensor>& h, const optional<Tensor>& label,
+                           const optional<Tensor>& weight, int64_t seed, int64_t tree, bool bootstrap, int64_t mode,
+                           const at::Device& dev, int64_t N) {
   if (mode == 0) {
     FDX_CHECK(g && h, "gbdt mode needs g,h");
     chk(*g, dev, at::kFloat, "g");
@@ -48,7 +44,7 @@ void rowstats(const optional<Tensor>& g, const optional<Tensor>& h, const option
     FDX_CHECK(label->numel() == N, "label size");
   }
   if (weight) { chk(*weight, dev, at::kFloat, "weight"); FDX_CHECK(weight->numel() == N, "weight size"); }
-  fdx::RowStatsArgs a{};
+  fdx::QuantArgs a{};
   a.g = opt<float>(g);
   a.h = opt<float>(h);
   a.label = opt<float>(label);
@@ -58,63 +54,60 @@ void rowstats(const optional<Tensor>& g, const optional<Tensor>& h, const option
   a.bootstrap = bootstrap ? 1 : 0;
   a.mode = (int32_t)mode;
   a.N = N;
-  a.rowstats = reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>());
+  return a;
+}
+
+// out_max[2] (float64) = max |statistic| over the rows (exponent choice; all-reduce MAX under DP)
+void quant_max(const optional<Tensor>& g, const optional<Tensor>& h, const optional<Tensor>& label,
+               const optional<Tensor>& weight, int64_t seed, int64_t tree, bool bootstrap, int64_t mode, int64_t N,
+               const Tensor& out_max) {
+  const auto dev = out_max.device();
+  chk(out_max, dev, at::kDouble, "out_max");
+  FDX_CHECK(out_max.numel() == 2, "out_max must have 2 entries");
+  fdx::QuantArgs a = quant_args(g, h, label, weight, seed, tree, bootstrap, mode, dev, N);
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_rowstats(a, stream(dev));
+    fdx::launch_quant_max(a, out_max.data_ptr<double>(), stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
-    fdx::rowstats_cpu(a);
+    fdx::quant_max_cpu(a, out_max.data_ptr<double>());
   }
 }
 
-// est[e] = rowstats[csc_row[e]] (once per tree)
-void entry_stats(const Tensor& csc_row, const Tensor& rowstats, const Tensor& est) {
-  const auto dev = csc_row.device();
-  chk(csc_row, dev, at::kInt, "csc_row");
-  chk(rowstats, dev, at::kInt, "rowstats");
-  chk(est, dev, at::kInt, "est");
-  const int64_t nnz = csc_row.numel();
-  FDX_CHECK(est.numel() >= 2 * nnz, "est must hold [nnz,2] int32");
-  FDX_CHECK(rowstats.dim() == 2 && rowstats.size(1) == 2, "rowstats must be [N,2]");
-  FDX_CHECK(reinterpret_cast<uintptr_t>(csc_row.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(est.data_ptr()) % 16 == 0,
-            "csc_row/est must be 16-byte aligned");
-  const auto* rs = reinterpret_cast<const uint32_t*>(rowstats.data_ptr<int32_t>());
-  auto* out = reinterpret_cast<uint32_t*>(est.data_ptr<int32_t>());
-  if (dev.is_cuda()) {
-    c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_entry_stats(csc_row.data_ptr<int32_t>(), rs, nnz, out, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  } else {
-    fdx::entry_stats_cpu(csc_row.data_ptr<int32_t>(), rs, nnz, out);
+// rowdig [N,2] int32 = digits of the quantised statistics; kexp [2] int32 = exponents used
+// (from max_abs, or 0 when max_abs is None: integer counts); totals [2] int64 = exact sums.
+void quant(const optional<Tensor>& g, const optional<Tensor>& h, const optional<Tensor>& label,
+           const optional<Tensor>& weight, int64_t seed, int64_t tree, bool bootstrap, int64_t mode, int64_t np,
+           const optional<Tensor>& max_abs, const Tensor& rowdig, const Tensor& kexp, const Tensor& totals,
+           const optional<Tensor>& digp) {
+  const auto dev = rowdig.device();
+  chk(rowdig, dev, at::kInt, "rowdig");
+  chk(kexp, dev, at::kInt, "kexp");
+  chk(totals, dev, at::kLong, "totals");
+  FDX_CHECK(rowdig.dim() == 2 && rowdig.size(1) == 2, "rowdig must be [N,2] int32");
+  FDX_CHECK(kexp.numel() == 2 && totals.numel() == 2, "kexp/totals must have 2 entries");
+  FDX_CHECK(np == 1 || np == 4, "np must be 1 or 4");
+  if (max_abs) { chk(*max_abs, dev, at::kDouble, "max_abs"); FDX_CHECK(max_abs->numel() == 2, "max_abs size"); }
+  FDX_CHECK(np == 4 || !max_abs, "np == 1 is for integer counts (exponent 0, no max_abs)");
+  fdx::QuantArgs a = quant_args(g, h, label, weight, seed, tree, bootstrap, mode, dev, rowdig.size(0));
+  a.np = (int32_t)np;
+  a.kexp_out = kexp.data_ptr<int32_t>();
+  a.rowdig = reinterpret_cast<uint32_t*>(rowdig.data_ptr<int32_t>());
+  a.totals = totals.data_ptr<int64_t>();
+  if (digp) {
+    chk(*digp, dev, at::kByte, "digp");
+    FDX_CHECK(digp->dim() == 2 && digp->size(0) >= 2 * np && digp->size(1) >= rowdig.size(0),
+              "digp must be [>= 2*np, >= N] uint8");
+    a.digp = digp->data_ptr<uint8_t>();
+    a.n_pad = digp->size(1);
   }
-}
-
-// est[e] = rowstats[csc_row[e]] for the entries of the listed work items, in wave order
-void entry_stats_items(const Tensor& item_start, const Tensor& item_end, const Tensor& wave_item,
-                       const Tensor& csc_row, const Tensor& rowstats, const Tensor& est) {
-  const auto dev = csc_row.device();
-  chk(item_start, dev, at::kLong, "item_start");
-  chk(item_end, dev, at::kLong, "item_end");
-  chk(wave_item, dev, at::kInt, "wave_item");
-  chk(csc_row, dev, at::kInt, "csc_row");
-  chk(rowstats, dev, at::kInt, "rowstats");
-  chk(est, dev, at::kInt, "est");
-  FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2] int32");
-  FDX_CHECK(wave_item.numel() % 4 == 0, "wave_item: 4 slots per workgroup");
-  FDX_CHECK(readable_tail(csc_row, 4), "csc_row needs 4 readable padding entries (quantize.CSC_PAD)");
-  const auto* rs = reinterpret_cast<const uint32_t*>(rowstats.data_ptr<int32_t>());
-  auto* out = reinterpret_cast<uint32_t*>(est.data_ptr<int32_t>());
-  const int32_t ni = (int32_t)item_start.numel();
+  const double* mx = max_abs ? max_abs->data_ptr<double>() : nullptr;
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_entry_stats_items(item_start.data_ptr<int64_t>(), item_end.data_ptr<int64_t>(),
-                                  wave_item.data_ptr<int32_t>(), (int32_t)wave_item.numel(), ni,
-                                  csc_row.data_ptr<int32_t>(), rs, out, stream(dev));
+    fdx::launch_quant(a, mx, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
-    fdx::entry_stats_items_cpu(item_start.data_ptr<int64_t>(), item_end.data_ptr<int64_t>(), ni,
-                               csc_row.data_ptr<int32_t>(), rs, out);
+    fdx::quant_cpu(a, mx);
   }
 }
 
@@ -143,138 +136,185 @@ void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, i
   }
 }
 
-// Build histograms of the listed features for the 8*ct slots of one pass. slot8 = None: root pass
-// (every entry in slot 0).
-void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& csc_row, const Tensor& csc_bin,
-                const optional<Tensor>& slot8_t, const Tensor& est, int64_t bt, int64_t ct, const Tensor& slab,
-                const Tensor& feat, const Tensor& feat_item0, const Tensor& feat_nitems, const Tensor& boff,
-                const Tensor& nbins, const Tensor& slot_to_node, const Tensor& hist, int64_t TB,
-                const optional<Tensor>& wave_item, const optional<Tensor>& rowstats) {
+// hist[slot_node[s]][boff[f] + b][stat] += exact sums of the quantised statistics of the entries of
+// the listed work items whose row is in slot s of this pass (slot8 = None: root pass, slot 0).
+void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
+                const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
+                const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
+                const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
+  chk(item_f0, dev, at::kInt, "item_f0");
+  chk(item_meta, dev, at::kInt, "item_meta");
   chk(csc_row, dev, at::kInt, "csc_row");
-  chk(csc_bin, dev, at::kByte, "csc_bin");
+  chk(csc_key, dev, at::kByte, "csc_key");
   if (slot8_t) chk(*slot8_t, dev, at::kByte, "slot8");
-  chk(est, dev, at::kInt, "est");
-  chk(feat, dev, at::kInt, "feat");
-  chk(feat_item0, dev, at::kLong, "feat_item0");
-  chk(feat_nitems, dev, at::kInt, "feat_nitems");
+  chk(rowdig, dev, at::kInt, "rowdig");
   chk(boff, dev, at::kLong, "boff");
   chk(nbins, dev, at::kInt, "nbins");
-  chk(slot_to_node, dev, at::kInt, "slot_to_node");
-  chk(hist, dev, at::kDouble, "hist");
-  FDX_CHECK(item_start.numel() == item_end.numel(), "item arrays");
-  // bt 0: narrow 16-bin tile, 4*ct slots (ct 1/2/4/8); bt 1/2: 32*bt bins, 8*ct slots (ct 1/2/4)
-  FDX_CHECK((bt == 0 && (ct == 1 || ct == 2 || ct == 4 || ct == 8)) ||
-                (bt >= 1 && bt <= 2 && (ct == 1 || ct == 2 || ct == 4)), "unsupported (bt, ct)");
-  const int64_t tile_slots = bt == 0 ? 4 * ct : 8 * ct, tile_bins = bt == 0 ? 16 : 32 * bt;
-  FDX_CHECK(slot_to_node.numel() == tile_slots, "slot_to_node must have one entry per tile slot");
-  FDX_CHECK(csc_row.numel() == csc_bin.numel(), "csc arrays");
-  const bool gather = rowstats.has_value() && rowstats->defined();
-  if (gather) {
-    // gather mode: statistics per row, est is not read
-    chk(*rowstats, dev, at::kInt, "rowstats");
-    FDX_CHECK(rowstats->dim() == 2 && rowstats->size(1) == 2, "rowstats must be [N,2] int32");
-    FDX_CHECK(reinterpret_cast<uintptr_t>(rowstats->data_ptr()) % 8 == 0, "rowstats must be 8-byte aligned");
-    FDX_CHECK(!slot8_t || slot8_t->numel() == rowstats->size(0), "slot8 and rowstats row counts differ");
-  } else {
-    FDX_CHECK(est.numel() >= 2 * csc_row.numel(), "est must hold [nnz,2]");
-    FDX_CHECK(reinterpret_cast<uintptr_t>(est.data_ptr()) % 16 == 0 && readable_tail(est, 8),
-              "est must be 16-byte aligned with 4 readable padding entries (see quantize.CSC_PAD)");
-  }
-  FDX_CHECK(TB >= 0 && boff.numel() == nbins.numel() + 1, "boff must be [Fa+1]");
-  FDX_CHECK(hist.numel() % (2 * std::max<int64_t>(TB, 1)) == 0, "hist must be [nodes, TB, 2]");
+  chk(slot_node, dev, at::kInt, "slot_node");
+  chk(hist, dev, at::kLong, "hist");
+  const int64_t I = item_start.numel();
+  FDX_CHECK(item_end.numel() == I && item_f0.numel() == I && item_meta.numel() == I, "item arrays");
+  FDX_CHECK((bt == 1 || bt == 2 || bt == 4) && (ct == 1 || ct == 2 || ct == 4 || ct == 8), "unsupported (bt, ct)");
+  FDX_CHECK(np == 1 || np == 4, "np must be 1 or 4");
+  const int64_t spt = 16 / (2 * np);
+  const int64_t nslots = slot_node.numel();
+  FDX_CHECK(nslots >= 1 && nslots <= spt * ct, "slot_node must have 1 .. 16*ct/(2*np) entries");
+  FDX_CHECK(slot8_t || nslots == 1, "the root pass builds one slot");
+  FDX_CHECK(csc_row.numel() == csc_key.numel(), "csc arrays");
+  FDX_CHECK(rowdig.dim() == 2 && rowdig.size(1) == 2, "rowdig must be [N,2] int32");
+  FDX_CHECK(reinterpret_cast<uintptr_t>(rowdig.data_ptr()) % 8 == 0, "rowdig must be 8-byte aligned");
+  FDX_CHECK(!slot8_t || slot8_t->numel() == rowdig.size(0), "slot8 and rowdig row counts differ");
+  FDX_CHECK(boff.numel() == nbins.numel() + 1, "boff must be [Fa+1]");
+  FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2, "hist must be [rows, stride, 2] int64");
+  FDX_CHECK(boff.numel() - 1 == nbins.numel() && hist.size(1) >= TB, "hist stride smaller than the total bin count");
   FDX_CHECK(reinterpret_cast<uintptr_t>(csc_row.data_ptr()) % 16 == 0 &&
-                reinterpret_cast<uintptr_t>(csc_bin.data_ptr()) % 4 == 0,
-            "csc_row must be 16-byte and csc_bin 4-byte aligned");
-  FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_bin, 4),
-            "csc_row/csc_bin need 4 readable padding entries behind their end (see quantize.CSC_PAD)");
-  fdx::HistArgs h{};
-  h.item_start = item_start.data_ptr<int64_t>();
-  h.item_end = item_end.data_ptr<int64_t>();
-  h.num_items = (int32_t)item_start.numel();
-  h.csc_row = csc_row.data_ptr<int32_t>();
-  h.csc_bin = csc_bin.data_ptr<uint8_t>();
-  h.slot8 = slot8_t ? slot8_t->data_ptr<uint8_t>() : nullptr;
-  h.est = gather ? nullptr : reinterpret_cast<const uint32_t*>(est.data_ptr<int32_t>());
-  h.rowstats = gather ? reinterpret_cast<const uint32_t*>(rowstats->data_ptr<int32_t>()) : nullptr;
+                reinterpret_cast<uintptr_t>(csc_key.data_ptr()) % 4 == 0,
+            "csc_row must be 16-byte and csc_key 4-byte aligned");
+  FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_key, 4),
+            "csc_row/csc_key need 4 readable padding entries behind their end (see quantize.CSC_PAD)");
+  fdx::HistArgs a{};
+  a.item_start = item_start.data_ptr<int64_t>();
+  a.item_end = item_end.data_ptr<int64_t>();
+  a.item_f0 = item_f0.data_ptr<int32_t>();
+  a.item_meta = item_meta.data_ptr<int32_t>();
+  a.num_items = (int32_t)I;
+  a.csc_row = csc_row.data_ptr<int32_t>();
+  a.csc_key = csc_key.data_ptr<uint8_t>();
+  a.slot8 = slot8_t ? slot8_t->data_ptr<uint8_t>() : nullptr;
+  a.rowdig = reinterpret_cast<const uint32_t*>(rowdig.data_ptr<int32_t>());
+  a.boff = boff.data_ptr<int64_t>();
+  a.nbins = nbins.data_ptr<int32_t>();
+  a.slot_node = slot_node.data_ptr<int32_t>();
+  a.nslots = (int32_t)nslots;
+  a.hist_stride = hist.size(1);
+  a.hist = hist.data_ptr<int64_t>();
   if (wave_item) {
     chk(*wave_item, dev, at::kInt, "wave_item");
     FDX_CHECK(wave_item->numel() % 4 == 0, "wave_item: 4 slots per workgroup");
-    h.wave_item = wave_item->data_ptr<int32_t>();
-    h.num_slots = (int32_t)wave_item->numel();
+    a.wave_item = wave_item->data_ptr<int32_t>();
+    a.num_slots = (int32_t)wave_item->numel();
   }
-  fdx::HistReduceArgs r{};
-  r.slab_slots = (int32_t)tile_slots;
-  r.slab_bins = (int32_t)tile_bins;
-  r.feat = feat.data_ptr<int32_t>();
-  r.feat_item0 = feat_item0.data_ptr<int64_t>();
-  r.feat_nitems = feat_nitems.data_ptr<int32_t>();
-  r.L = (int32_t)feat.numel();
-  r.boff = boff.data_ptr<int64_t>();
-  r.nbins = nbins.data_ptr<int32_t>();
-  r.slot_to_node = slot_to_node.data_ptr<int32_t>();
-  r.slot_base = 0;
-  r.total_bins = TB;
-  r.hist = hist.data_ptr<double>();
   if (dev.is_cuda()) {
-    chk(slab, dev, at::kFloat, "slab");
-    FDX_CHECK(slab.numel() >= (int64_t)h.num_items * tile_slots * tile_bins * 2, "slab too small");
-    h.slab = slab.data_ptr<float>();
-    r.slab = h.slab;
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_hist_mfma(h, (int)bt, (int)ct, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-    fdx::launch_hist_reduce(r, stream(dev));
+    fdx::launch_hist(a, (int)bt, (int)ct, (int)np, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
-    fdx::hist_cpu(h, r, (int)tile_slots);
+    fdx::hist_cpu(a, (int)bt, (int)np);
   }
 }
+
+// Dense hot-feature histograms (see DenseHistArgs): gfid/gdense [ngroups * fg] with fg =
+// tree_dense_fg(bt, ct); rows are processed in ranges of range_rows (multiple of 64).
+void hist_dense(const Tensor& dense, const Tensor& digp, const Tensor& rowdig, const optional<Tensor>& slot8_t,
+                const Tensor& gfid, const Tensor& gdense, const Tensor& boff, const Tensor& nbins,
+                const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t n_rows, int64_t range_rows,
+                int64_t bt, int64_t ct, int64_t np) {
+  const auto dev = dense.device();
+  chk(dense, dev, at::kByte, "dense");
+  chk(digp, dev, at::kByte, "digp");
+  chk(rowdig, dev, at::kInt, "rowdig");
+  if (slot8_t) chk(*slot8_t, dev, at::kByte, "slot8");
+  chk(gfid, dev, at::kInt, "gfid");
+  chk(gdense, dev, at::kInt, "gdense");
+  chk(boff, dev, at::kLong, "boff");
+  chk(nbins, dev, at::kInt, "nbins");
+  chk(slot_node, dev, at::kInt, "slot_node");
+  chk(hist, dev, at::kLong, "hist");
+  FDX_CHECK((bt == 1 || bt == 2 || bt == 4) && (ct == 1 || ct == 2 || ct == 4 || ct == 8), "unsupported (bt, ct)");
+  FDX_CHECK(np == 1 || np == 4, "np must be 1 or 4");
+  const int64_t fg = fdx::dense_features_per_wave((int)bt, slot8_t ? (int)ct : 1);
+  FDX_CHECK(gfid.numel() == gdense.numel() && gfid.numel() % (fg * fdx::dense_waves_per_group()) == 0,
+            "gfid/gdense must be [ngroups * fg], ngroups a multiple of tree_dense_waves()");
+  const int64_t n_pad = dense.size(1);
+  FDX_CHECK(dense.dim() == 2 && n_pad % 64 == 0 && n_pad >= n_rows, "dense must be [Fh, n_pad], n_pad % 64 == 0");
+  FDX_CHECK(digp.dim() == 2 && digp.size(0) >= 2 * np && digp.size(1) == n_pad, "digp must be [2*np, n_pad]");
+  FDX_CHECK(rowdig.dim() == 2 && rowdig.size(0) == n_rows, "rowdig rows");
+  FDX_CHECK(!slot8_t || slot8_t->numel() >= n_pad, "slot8 must be padded to n_pad (0xff)");
+  FDX_CHECK(range_rows > 0 && range_rows % 64 == 0, "range_rows must be a positive multiple of 64");
+  const int64_t nslots = slot_node.numel();
+  FDX_CHECK(nslots >= 1 && nslots <= (16 / (2 * np)) * ct, "slot_node size");
+  FDX_CHECK(slot8_t || nslots == 1, "the root pass builds one slot");
+  FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && hist.size(1) >= TB, "hist must be [rows, >= TB, 2] int64");
+  FDX_CHECK(boff.numel() == nbins.numel() + 1, "boff must be [Fa+1]");
+  fdx::DenseHistArgs a{};
+  a.dense = dense.data_ptr<uint8_t>();
+  a.digp = digp.data_ptr<uint8_t>();
+  a.rowdig = reinterpret_cast<const uint32_t*>(rowdig.data_ptr<int32_t>());
+  a.n_rows = n_rows;
+  a.slot8 = slot8_t ? slot8_t->data_ptr<uint8_t>() : nullptr;
+  a.n_pad = n_pad;
+  a.range_rows = range_rows;
+  a.nranges = (int32_t)((n_pad + range_rows - 1) / range_rows);
+  a.ngroups = (int32_t)(gfid.numel() / fg);
+  a.gfid = gfid.data_ptr<int32_t>();
+  a.gdense = gdense.data_ptr<int32_t>();
+  a.boff = boff.data_ptr<int64_t>();
+  a.nbins = nbins.data_ptr<int32_t>();
+  a.slot_node = slot_node.data_ptr<int32_t>();
+  a.nslots = (int32_t)nslots;
+  a.hist_stride = hist.size(1);
+  a.hist = hist.data_ptr<int64_t>();
+  if (a.ngroups == 0) return;
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_hist_dense(a, (int)bt, (int)ct, (int)np, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::hist_dense_cpu(a, (int)fg, (int)np);
+  }
+}
+
+int64_t dense_fg(int64_t bt, int64_t ct) { return fdx::dense_features_per_wave((int)bt, (int)ct); }
+int64_t dense_waves() { return fdx::dense_waves_per_group(); }
 
 void hist_subtract(const Tensor& parent, const Tensor& cur, const Tensor& dst, const Tensor& par, const Tensor& sib,
                    int64_t TB) {
   const auto dev = cur.device();
-  chk(parent, dev, at::kDouble, "parent");
-  chk(cur, dev, at::kDouble, "cur");
+  chk(parent, dev, at::kLong, "parent");
+  chk(cur, dev, at::kLong, "cur");
   chk(dst, dev, at::kInt, "dst");
   chk(par, dev, at::kInt, "par");
   chk(sib, dev, at::kInt, "sib");
   const int32_t n = (int32_t)dst.numel();
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_hist_subtract(parent.data_ptr<double>(), cur.data_ptr<double>(), dst.data_ptr<int32_t>(),
+    fdx::launch_hist_subtract(parent.data_ptr<int64_t>(), cur.data_ptr<int64_t>(), dst.data_ptr<int32_t>(),
                               par.data_ptr<int32_t>(), sib.data_ptr<int32_t>(), n, TB, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
-    fdx::hist_subtract_cpu(parent.data_ptr<double>(), cur.data_ptr<double>(), dst.data_ptr<int32_t>(),
+    fdx::hist_subtract_cpu(parent.data_ptr<int64_t>(), cur.data_ptr<int64_t>(), dst.data_ptr<int32_t>(),
                            par.data_ptr<int32_t>(), sib.data_ptr<int32_t>(), n, TB);
   }
 }
 
 void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, const Tensor& nbins, const Tensor& zbin,
-                const Tensor& fid_orig, const Tensor& node_ids, int64_t mode, double lambda_, double mcw,
-                double feat_prob, int64_t seed, int64_t tree, const Tensor& out_gain, const Tensor& out_bin,
-                const Tensor& out_left) {
+                const Tensor& fid_orig, const Tensor& node_ids, const Tensor& kexp, int64_t mode, double lambda_,
+                double mcw, const optional<Tensor>& feat_thr, int64_t seed, int64_t tree, const Tensor& out_gain,
+                const Tensor& out_bin, const Tensor& out_left) {
   const auto dev = hist.device();
-  chk(hist, dev, at::kDouble, "hist");
-  chk(totals, dev, at::kDouble, "totals");
+  chk(hist, dev, at::kLong, "hist");
+  chk(totals, dev, at::kLong, "totals");
   chk(boff, dev, at::kLong, "boff");
   chk(nbins, dev, at::kInt, "nbins");
   chk(zbin, dev, at::kInt, "zbin");
   chk(fid_orig, dev, at::kLong, "fid_orig");
   chk(node_ids, dev, at::kInt, "node_ids");
+  chk(kexp, dev, at::kInt, "kexp");
   chk(out_gain, dev, at::kDouble, "out_gain");
   chk(out_bin, dev, at::kInt, "out_bin");
-  chk(out_left, dev, at::kDouble, "out_left");
+  chk(out_left, dev, at::kLong, "out_left");
   const int32_t nodes = (int32_t)node_ids.numel();
   const int32_t Fa = (int32_t)nbins.numel();
   FDX_CHECK(out_gain.numel() >= (int64_t)nodes * Fa && out_left.numel() >= 2ll * nodes * Fa, "outputs too small");
   FDX_CHECK(totals.numel() >= 2 * nodes, "totals size");
+  FDX_CHECK(kexp.numel() == 2, "kexp size");
+  if (feat_thr) { chk(*feat_thr, dev, at::kDouble, "feat_thr"); FDX_CHECK(feat_thr->numel() >= nodes, "feat_thr size"); }
   fdx::SplitArgs a{};
-  a.hist = hist.data_ptr<double>();
-  a.totals = totals.data_ptr<double>();
+  a.hist = hist.data_ptr<int64_t>();
+  a.totals = totals.data_ptr<int64_t>();
   a.num_nodes = nodes;
   a.Fa = Fa;
   a.boff = boff.data_ptr<int64_t>();
@@ -282,15 +322,16 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
   a.zbin = zbin.data_ptr<int32_t>();
   a.fid_orig = fid_orig.data_ptr<int64_t>();
   a.node_ids = node_ids.data_ptr<int32_t>();
+  a.kexp = kexp.data_ptr<int32_t>();
   a.mode = (int32_t)mode;
   a.lambda_ = lambda_;
   a.min_child_weight = mcw;
-  a.feat_prob = feat_prob;
+  a.feat_thr = opt<double>(feat_thr);
   a.seed = (uint64_t)seed;
   a.tree = (int32_t)tree;
   a.out_gain = out_gain.data_ptr<double>();
   a.out_bin = out_bin.data_ptr<int32_t>();
-  a.out_left = out_left.data_ptr<double>();
+  a.out_left = out_left.data_ptr<int64_t>();
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_split(a, stream(dev));
@@ -381,11 +422,13 @@ void leaf_update(const Tensor& margin, const Tensor& row_node, const Tensor& nod
 }  // namespace
 
 void register_tree_ops(pybind11::module& m) {
-  m.def("tree_rowstats", &rowstats);
-  m.def("tree_entry_stats", &entry_stats);
+  m.def("tree_quant_max", &quant_max);
+  m.def("tree_quant", &quant);
   m.def("tree_slot8", &slot8);
-  m.def("tree_entry_stats_items", &entry_stats_items);
   m.def("tree_hist_build", &hist_build);
+  m.def("tree_hist_dense", &hist_dense);
+  m.def("tree_dense_fg", &dense_fg);
+  m.def("tree_dense_waves", &dense_waves);
   m.def("tree_hist_subtract", &hist_subtract);
   m.def("tree_split_find", &split_find);
   m.def("tree_partition", &partition);

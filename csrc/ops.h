@@ -61,38 +61,40 @@ template <class V> void feature_order_cpu(const FeatureOrderArgs<V>& a);
 void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, hipStream_t s);
 void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
                          int64_t row_block, int64_t* bounds, hipStream_t s);
+void launch_copy_segments(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
+                          const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key, hipStream_t s);
+void copy_segments_cpu(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
+                       const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key);
 void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
                       int64_t row_block, int64_t* bounds);
 
 // ---------------------------------------------------------------- tree engine (tree_kernels.hip / tree_cpu.cpp)
-struct RowStatsArgs;
+struct QuantArgs;
 struct SlotArgs;
 struct HistArgs;
-struct HistReduceArgs;
+struct DenseHistArgs;
 struct SplitArgs;
 struct PartitionArgs;
-void launch_rowstats(const RowStatsArgs& a, hipStream_t s);
-void launch_entry_stats(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est, hipStream_t s);
+void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s);
+void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);
-void launch_entry_stats_items(const int64_t* item_start, const int64_t* item_end, const int32_t* wave_item,
-                              int32_t num_slots, int32_t num_items, const int32_t* csc_row, const uint32_t* rowstats,
-                              uint32_t* est, hipStream_t s);
-void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s);
-void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s);
-void launch_hist_subtract(const double* parent, double* cur, const int32_t* dst, const int32_t* par,
+void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s);
+void launch_hist_dense(const DenseHistArgs& a, int bt, int ct, int np, hipStream_t s);
+int dense_features_per_wave(int bt, int ct);
+int dense_waves_per_group();
+void launch_hist_subtract(const int64_t* parent, int64_t* cur, const int32_t* dst, const int32_t* par,
                           const int32_t* sib, int32_t n_pairs, int64_t TB, hipStream_t s);
 void launch_split(const SplitArgs& a, hipStream_t s);
 void launch_partition(const PartitionArgs& a, hipStream_t s);
 void launch_logistic_grad(const double* margin, const float* label, const float* weight, float* g, float* h,
                           int64_t N, hipStream_t s);
 void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s);
-void rowstats_cpu(const RowStatsArgs& a);
-void entry_stats_cpu(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est);
+void quant_max_cpu(const QuantArgs& a, double* out);
+void quant_cpu(const QuantArgs& a, const double* maxv);
 void slot8_cpu(const SlotArgs& a);
-void entry_stats_items_cpu(const int64_t* item_start, const int64_t* item_end, int32_t num_items,
-                           const int32_t* csc_row, const uint32_t* rowstats, uint32_t* est);
-void hist_cpu(const HistArgs& h, const HistReduceArgs& r, int slots);
-void hist_subtract_cpu(const double* parent, double* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
+void hist_cpu(const HistArgs& h, int bt, int np);
+void hist_dense_cpu(const DenseHistArgs& a, int fg, int np);
+void hist_subtract_cpu(const int64_t* parent, int64_t* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
                        int32_t n_pairs, int64_t TB);
 void split_cpu(const SplitArgs& a);
 void partition_cpu(const PartitionArgs& a);

@@ -109,6 +109,23 @@ __global__ __launch_bounds__(256) void block_bounds_kernel(const int32_t* __rest
   bounds[t] = lo;
 }
 
+// dst[seg_dst[i] + k] = src[seg_src[i] + k] for k < seg_len[i], rows (int32) and keys (uint8):
+// one workgroup per segment (the super-block-major copy of the histogram CSC).
+__global__ __launch_bounds__(256) void copy_segments_kernel(const int32_t* __restrict__ src_row,
+                                                            const uint8_t* __restrict__ src_key,
+                                                            const int64_t* __restrict__ seg_src,
+                                                            const int64_t* __restrict__ seg_dst,
+                                                            const int64_t* __restrict__ seg_len, int64_t nseg,
+                                                            int32_t* __restrict__ dst_row, uint8_t* __restrict__ dst_key) {
+  for (int64_t i = blockIdx.x; i < nseg; i += gridDim.x) {
+    const int64_t a = seg_src[i], d = seg_dst[i], n = seg_len[i];
+    for (int64_t k = threadIdx.x; k < n; k += 256) {
+      dst_row[d + k] = src_row[a + k];
+      dst_key[d + k] = src_key[a + k];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void clamp_u8_kernel(const uint8_t* __restrict__ in, int64_t n, uint8_t maxv,
                                                        uint8_t* __restrict__ out) {
   const int64_t n16 = n / 16;
@@ -176,6 +193,14 @@ void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const in
   if (n > 0)
     hipLaunchKernelGGL(block_bounds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, csc_row, colptr, cols, ncols,
                        nblk, row_block, bounds);
+}
+
+void launch_copy_segments(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
+                          const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key, hipStream_t s) {
+  if (nseg <= 0) return;
+  const unsigned grid = (unsigned)(nseg < 65536 ? nseg : 65536);
+  hipLaunchKernelGGL(copy_segments_kernel, dim3(grid), dim3(256), 0, s, src_row, src_key, seg_src, seg_dst, seg_len, nseg,
+                     dst_row, dst_key);
 }
 
 void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, hipStream_t s) {

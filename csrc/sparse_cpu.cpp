@@ -133,6 +133,16 @@ void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32
   });
 }
 
+void copy_segments_cpu(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
+                       const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key) {
+  parallel_for(nseg, 0, 64, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      std::copy(src_row + seg_src[i], src_row + seg_src[i] + seg_len[i], dst_row + seg_dst[i]);
+      std::copy(src_key + seg_src[i], src_key + seg_src[i] + seg_len[i], dst_key + seg_dst[i]);
+    }
+  });
+}
+
 template void feature_order_cpu<float>(const FeatureOrderArgs<float>&);
 template void feature_order_cpu<double>(const FeatureOrderArgs<double>&);
 

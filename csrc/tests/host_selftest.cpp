@@ -2,6 +2,7 @@
 // implementations (featurizer incl. token keys, JSON extraction, tree engine) on edge cases and
 // checks them against simple scalar references. Built with -fsanitize=address,undefined by
 // fraud_detection_spark_kafka_llm_amd/_build.py:build_host_selftest(); exits non-zero on failure.
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -163,53 +164,63 @@ static void test_json() {
 }
 
 static void test_tree() {
-  // 6 rows x 3 features, CSC with bins; stats g = row, h = 1
+  // 6 rows x 3 features, CSC with bins; statistics g = row - 2.5, h = 1 (exact in the quantised grid)
   const int64_t N = 6;
   const std::vector<int64_t> colptr = {0, 3, 5, 8};
   std::vector<int32_t> rows = {0, 2, 5, 1, 2, 0, 3, 4};
   std::vector<uint8_t> bins = {1, 2, 1, 1, 3, 2, 2, 1};
   rows.resize(rows.size() + 16, 0);
   bins.resize(bins.size() + 16, 0xff);
-  const int64_t nnz = 8;
   std::vector<float> g(N), h(N, 1.0f);
   for (int i = 0; i < N; ++i) g[i] = (float)i - 2.5f;
-  std::vector<uint32_t> rs(2 * N), est(2 * (nnz + 16));
-  RowStatsArgs ra{};
-  ra.g = g.data();
-  ra.h = h.data();
-  ra.N = N;
-  ra.rowstats = rs.data();
-  rowstats_cpu(ra);
-  entry_stats_cpu(rows.data(), rs.data(), nnz, est.data());
+  std::vector<uint32_t> rd(2 * N);
+  std::vector<int32_t> kexp(2);
+  std::vector<int64_t> totals(2);
+  QuantArgs qa{};
+  qa.g = g.data();
+  qa.h = h.data();
+  qa.N = N;
+  qa.np = 4;
+  qa.rowdig = rd.data();
+  qa.kexp_out = kexp.data();
+  qa.totals = totals.data();
+  double mx[2];
+  quant_max_cpu(qa, mx);
+  EXPECT(mx[0] == 2.5 && mx[1] == 1.0);
+  quant_cpu(qa, mx);
+  EXPECT(kexp[0] == 28 && kexp[1] == 29);
+  for (int i = 0; i < N; ++i) EXPECT(undigits4(rd[2 * i]) == (int64_t)std::ldexp((double)g[i], 28));
+  EXPECT(totals[0] == 0 && totals[1] == 6 * (int64_t(1) << 29));
   std::vector<int32_t> row_node = {0, 1, 0, 1, 0, 1}, node_slot = {0, 1};
   std::vector<uint8_t> slot8(N);
   SlotArgs sa{row_node.data(), node_slot.data(), 2, 0, 2, N, slot8.data()};
   slot8_cpu(sa);
-  const std::vector<int64_t> item_start = {0, 3, 5}, item_end = {3, 5, 8}, feat_item0 = {0, 1, 2}, boff = {0, 4, 8, 12};
-  const std::vector<int32_t> feat = {0, 1, 2}, nitems = {1, 1, 1}, nbins = {4, 4, 4}, s2n = {0, 1};
-  std::vector<double> hist(2 * 12 * 2, 0.0);
+  // one single-feature item per column (key = bin, stride 256)
+  const std::vector<int64_t> item_start = {0, 3, 5}, item_end = {3, 5, 8}, boff = {0, 4, 8, 12};
+  const std::vector<int32_t> f0 = {0, 1, 2}, meta = {8 | (1 << 8), 8 | (1 << 8), 8 | (1 << 8)};
+  const std::vector<int32_t> nbins = {4, 4, 4}, s2n = {0, 1};
+  std::vector<int64_t> hist(2 * 12 * 2, 0);
   HistArgs ha{};
   ha.item_start = item_start.data();
   ha.item_end = item_end.data();
+  ha.item_f0 = f0.data();
+  ha.item_meta = meta.data();
   ha.num_items = 3;
   ha.csc_row = rows.data();
-  ha.csc_bin = bins.data();
+  ha.csc_key = bins.data();
   ha.slot8 = slot8.data();
-  ha.est = est.data();
-  HistReduceArgs hr{};
-  hr.feat = feat.data();
-  hr.feat_item0 = feat_item0.data();
-  hr.feat_nitems = nitems.data();
-  hr.L = 3;
-  hr.boff = boff.data();
-  hr.nbins = nbins.data();
-  hr.slot_to_node = s2n.data();
-  hr.total_bins = 12;
-  hr.hist = hist.data();
-  hist_cpu(ha, hr, 2);
-  double ref[2][12] = {};
+  ha.rowdig = rd.data();
+  ha.boff = boff.data();
+  ha.nbins = nbins.data();
+  ha.slot_node = s2n.data();
+  ha.nslots = 2;
+  ha.hist_stride = 12;
+  ha.hist = hist.data();
+  hist_cpu(ha, 1, 4);
+  int64_t ref[2][12] = {};
   for (int f = 0; f < 3; ++f)
-    for (int64_t e = colptr[f]; e < colptr[f + 1]; ++e) ref[row_node[rows[e]]][boff[f] + bins[e]] += g[rows[e]];
+    for (int64_t e = colptr[f]; e < colptr[f + 1]; ++e)
+      ref[row_node[rows[e]]][boff[f] + bins[e]] += (int64_t)std::ldexp((double)g[rows[e]], 28);
   for (int n = 0; n < 2; ++n)
     for (int b = 0; b < 12; ++b) EXPECT(hist[((size_t)n * 12 + b) * 2] == ref[n][b]);
 }

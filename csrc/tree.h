@@ -1,17 +1,26 @@
 // Tree-engine argument structs shared by tree_kernels.hip (gfx950) and tree_cpu.cpp (host).
 //
+// Exact integer histograms. Every per-row statistic v (GBDT g*w / h*w, or a class count) is
+// quantised to q = rint(v * 2^k) with one exponent k per statistic and boosting round (chosen
+// from the global max |v| so |q| <= 2^30), and q is stored as NP balanced base-256 digits
+// d_i in [-128, 127] (q = sum_i d_i 256^i; NP = 4, or NP = 1 for small integer counts). The
+// histogram kernel multiplies one-hot(bin) by digit planes on the i8 matrix cores
+// (v_mfma_i32_16x16x64_i8: exact int32 sums), and the per-plane sums are recombined into int64
+// histograms. Integer sums do not depend on the order of summation, so histograms, splits and
+// trees are bitwise identical on host and device, for any work-item split and any number of
+// data-parallel ranks (the int64 partial histograms are summed exactly by the collectives).
+//
 // Data layout (per data-parallel rank):
 //   * quantized CSC: for each active feature fid, entries [colptr[fid], colptr[fid+1]) hold
-//     (row int32, bin uint8) sorted by row; bins are ordered by value, bin zbin[fid] is the
-//     implicit "value == 0" bin for rows absent from the column;
-//   * rowstats[row] (8 B): the two statistics the histogram sums, each split into bf16 hi/lo
-//     halves so one bf16 MFMA reproduces ~fp32 sums;
-//       GBDT: (g, h);  classification: (w*[y==0], w*[y==1]);
-//     gathered ONCE per tree into CSC entry order (est[e] = rowstats[csc_row[e]]), so every
-//     level streams them sequentially instead of gathering 16 B per entry per level;
-//   * slot8[row] (1 B): which of the <= 32 nodes built by the current histogram pass the row
-//     belongs to (0xff: none) -- N bytes, L2-resident, the only per-level random access;
-//   * histograms: hist[node][bin] = double2, bins of all features concatenated (boff[fid]).
+//     (row int32, bin uint8) sorted by row (row partition, dense-block build);
+//   * histogram CSC (models/quantize.py): the entries of the non-dense features re-laid out
+//     row-super-block-major (one block's slot/digit slice stays in one XCD's L2), as (row, key)
+//     with key = kbase[fid] + bin: work items that pack several small features into one 64-key
+//     MFMA tile give each its own key range; single-feature items have kbase 0;
+//   * rowdig[row] (2 x uint32): the digits of (q0, q1), plane i in byte i;
+//   * slot8[row] (1 B): which of the nodes built by the current pass the row belongs to (0xff:
+//     none) -- the only per-level random access besides the statistics;
+//   * histograms: hist[node][gbin][stat] int64, bins of all features concatenated (boff[fid]).
 #pragma once
 #include <math.h>
 #include <stdint.h>
@@ -20,7 +29,25 @@
 
 namespace fdx {
 
-struct RowStatsArgs {
+// --------------------------------------------------------------------------------- quantisation
+// Exponent k for a statistic whose max |v| is m: |rint(v * 2^k)| <= 2^30.
+FDX_HD int32_t quant_exponent(double m) {
+  if (!(m > 0.0)) return 0;
+  int e = 0;
+  (void)frexp(m, &e);            // m = f * 2^e, f in [0.5, 1)  ->  m <= 2^e
+  return 30 - e;
+}
+
+FDX_HD int64_t quantize_value(double v, int32_t k) { return (int64_t)rint(ldexp(v, k)); }
+
+// q (|q| < 2^31 - 2^23) -> 4 balanced base-256 digits, byte i = d_i (two's complement)
+FDX_HD uint32_t digits4(int64_t q) { return (uint32_t)(q + 0x80808080ll) ^ 0x80808080u; }
+FDX_HD int64_t undigits4(uint32_t d) { return (int64_t)(d ^ 0x80808080u) - 0x80808080ll; }
+// NP = 1: the value itself (|q| <= 127) in byte 0
+FDX_HD uint32_t digits1(int64_t q) { return (uint32_t)(uint8_t)(int8_t)q; }
+FDX_HD int64_t undigits1(uint32_t d) { return (int64_t)(int8_t)(uint8_t)(d & 0xffu); }
+
+struct QuantArgs {
   const float* g;             // GBDT gradients (mode 0)
   const float* h;
   const float* label;         // classification labels 0/1 (mode 1)
@@ -28,9 +55,14 @@ struct RowStatsArgs {
   uint64_t seed;              // Poisson(1) bootstrap when bootstrap != 0 (mode 1)
   int32_t tree;
   int32_t bootstrap;
-  int32_t mode;               // 0 = gbdt, 1 = classification counts
+  int32_t mode;               // 0 = gbdt (g, h), 1 = classification counts (w[y==0], w[y==1])
+  int32_t np;                 // digits per statistic: 4, or 1 for integer counts <= 127
+  int32_t* kexp_out;          // [2] quantisation exponents used (written once)
   int64_t N;
-  uint32_t* rowstats;         // [N * 2]
+  uint32_t* rowdig;           // [N * 2]
+  int64_t* totals;            // [2] += sum of q over the rows (exact)
+  uint8_t* digp;              // optional plane-major copy [2 * np][n_pad] (dense histogram path)
+  int64_t n_pad;
 };
 
 struct SlotArgs {
@@ -43,39 +75,60 @@ struct SlotArgs {
   uint8_t* slot8;             // [N] slot - slot_base, or 0xff
 };
 
+// Work item meta (item_meta): stride_log2 | nfeat << 8 | koff << 16. The item covers keys
+// [koff, koff + 16*BT); key ek belongs to feature f0 + (ek >> stride_log2), bin ek & (stride-1).
+FDX_HD int32_t item_stride_log2(int32_t m) { return m & 0xff; }
+FDX_HD int32_t item_nfeat(int32_t m) { return (m >> 8) & 0xff; }
+FDX_HD int32_t item_koff(int32_t m) { return (m >> 16) & 0xff; }
+
 struct HistArgs {
   const int64_t* item_start;      // [I] entry range of each work item
   const int64_t* item_end;
+  const int32_t* item_f0;         // [I] first feature of the item
+  const int32_t* item_meta;       // [I]
   int32_t num_items;
-  const int32_t* csc_row;
-  const uint8_t* csc_bin;
-  const uint8_t* slot8;           // [N] relative slot, 0xff = not built; nullptr = root pass (all slot 0)
-  const uint32_t* est;            // [nnz * 2] packed statistics in entry order
-  const uint32_t* rowstats;       // [N * 2] gather mode (est unused): statistics gathered per live entry
-  float* slab;                   // [I][slots][bins][2]: 32-bin tiles [8*CT][32*BT], narrow [4*CT][16]
   const int32_t* wave_item;       // [num_slots] item of each wave slot (-1 idle); nullptr: slot = item
   int32_t num_slots;
-};
-
-struct HistReduceArgs {
-  const float* slab;
-  int32_t slab_slots;             // 8*CT
-  int32_t slab_bins;              // 32*BT
-  const int32_t* feat;            // [L] fid of each listed feature
-  const int64_t* feat_item0;      // [L] first item of the feature in the item list
-  const int32_t* feat_nitems;     // [L]
-  int32_t L;
+  const int32_t* csc_row;
+  const uint8_t* csc_key;
+  const uint8_t* slot8;           // [N] relative slot, 0xff = not built; nullptr = root pass (all slot 0)
+  const uint32_t* rowdig;         // [N * 2]
   const int64_t* boff;            // [Fa + 1]
   const int32_t* nbins;           // [Fa]
-  const int32_t* slot_to_node;    // [8*CT] level-local node index or -1
-  int32_t slot_base;
-  int64_t total_bins;             // TB
-  double* hist;                   // [nodes][TB][2]
+  const int32_t* slot_node;       // [nslots] histogram row of each slot of the pass (-1: none)
+  int32_t nslots;
+  int64_t hist_stride;            // bins per histogram row (TB, or TB + 1 when padded)
+  int64_t* hist;                  // [rows][hist_stride][2], accumulated (+=)
+};
+
+// Dense path for high-density features: dense[d][row] = bin of hot feature d (zbin when absent),
+// column-major with n_pad (multiple of 64) bytes per feature; the row statistics are streamed from
+// the plane-major digit copy, the slots from slot8 (padded to n_pad with 0xff). A wave builds the
+// histograms of FG features (gfid[grp * FG + j]: Fa index, -1 none; gdense: row of `dense`) over a
+// range of range_rows rows; ranges are placed so that all groups of one range share an XCD.
+struct DenseHistArgs {
+  const uint8_t* dense;           // [Fh][n_pad]
+  const uint8_t* digp;            // [2 * NP][n_pad]
+  const uint32_t* rowdig;         // [N * 2] (host path)
+  int64_t n_rows;
+  const uint8_t* slot8;           // [n_pad] (nullptr: root pass)
+  int64_t n_pad;
+  int64_t range_rows;             // multiple of 64
+  int32_t nranges;
+  int32_t ngroups;
+  const int32_t* gfid;            // [ngroups * FG]
+  const int32_t* gdense;          // [ngroups * FG]
+  const int64_t* boff;
+  const int32_t* nbins;
+  const int32_t* slot_node;
+  int32_t nslots;
+  int64_t hist_stride;
+  int64_t* hist;
 };
 
 struct SplitArgs {
-  const double* hist;             // [nodes][TB][2]
-  const double* totals;           // [nodes][2]
+  const int64_t* hist;            // [nodes][TB][2]
+  const int64_t* totals;          // [nodes][2]
   int32_t num_nodes;
   int32_t Fa;
   const int64_t* boff;
@@ -83,15 +136,16 @@ struct SplitArgs {
   const int32_t* zbin;
   const int64_t* fid_orig;        // [Fa] original feature index (RF sampling key)
   const int32_t* node_ids;        // [nodes] tree-global node id (RF sampling key)
+  const int32_t* kexp;            // [2] quantisation exponents of the two statistics
   int32_t mode;                   // 0 = xgboost newton gain, 1 = gini, 2 = entropy
   double lambda_;                 // L2 (gbdt)
   double min_child_weight;        // gbdt: min hessian per child; cls: min instances per child
-  double feat_prob;               // RF per-node feature sampling probability (1 = all)
+  const double* feat_thr;         // RF: [nodes] sampling threshold (feature kept iff u <= thr); nullptr: all
   uint64_t seed;
   int32_t tree;
   double* out_gain;               // [nodes][Fa]
   int32_t* out_bin;               // [nodes][Fa]
-  double* out_left;               // [nodes][Fa][2]
+  int64_t* out_left;              // [nodes][Fa][2]
 };
 
 struct PartitionArgs {
@@ -108,7 +162,7 @@ struct PartitionArgs {
   const int32_t* split_other;     // [S] the other child id
   const int32_t* split_bin;       // [S] threshold bin: bin <= thr goes left
   const int32_t* split_left_is_default;  // [S]
-  const int32_t* csc_row;
+  const int32_t* csc_row;         // feature-major CSC (all features)
   const uint8_t* csc_bin;
 };
 
@@ -125,7 +179,13 @@ FDX_HD double hash_uniform(uint64_t a, uint64_t b, uint64_t c) {
   return (double)(x >> 11) * (1.0 / 9007199254740992.0);
 }
 
-// Poisson(1) draw by inversion of the CDF on a counter-based uniform.
+// RF per-node feature priority (uniform in [0,1)): the node samples the features with the k
+// smallest priorities (exactly k, without replacement).
+FDX_HD double feature_priority(uint64_t seed, int32_t tree, int32_t node, int64_t fid) {
+  return hash_uniform(seed ^ 0x5bd1e995ull, ((uint64_t)(uint32_t)tree << 32) | (uint32_t)node, (uint64_t)fid);
+}
+
+// Poisson(1) draw by inversion of the CDF on a counter-based uniform (at most 32).
 FDX_HD int poisson1(double u) {
   double p = 0.36787944117144233, cdf = p;
   int k = 0;
@@ -133,22 +193,19 @@ FDX_HD int poisson1(double u) {
   return k;
 }
 
-// round-to-nearest-even float -> bf16 bits, and back
-FDX_HD uint32_t f2bf(float f) {
-  union { float f; uint32_t u; } x; x.f = f;
-  uint32_t u = x.u;
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return u >> 16;
-}
-FDX_HD float bf2f(uint32_t b) {
-  union { float f; uint32_t u; } x; x.u = b << 16;
-  return x.f;
-}
-// pack v as (hi | lo << 16) with v ~= hi + lo
-FDX_HD uint32_t split_bf16(float v) {
-  const uint32_t hi = f2bf(v);
-  const uint32_t lo = f2bf(v - bf2f(hi));
-  return hi | (lo << 16);
+// The two statistics of one row before quantisation.
+FDX_HD void row_stats(const QuantArgs& a, int64_t r, double* v0, double* v1) {
+  if (a.mode == 0) {
+    const double w = a.weight ? (double)a.weight[r] : 1.0;
+    *v0 = (double)a.g[r] * w;
+    *v1 = (double)a.h[r] * w;
+  } else {
+    double w = a.weight ? (double)a.weight[r] : 1.0;
+    if (a.bootstrap) w *= (double)poisson1(hash_uniform(a.seed, (uint64_t)a.tree, (uint64_t)r));
+    const double y = (double)a.label[r];
+    *v0 = w * (1.0 - y);
+    *v1 = w * y;
+  }
 }
 
 FDX_HD double gini(double c0, double c1) {
@@ -172,33 +229,36 @@ FDX_HD double impurity(int mode, double c0, double c1) {
   return mode == 2 ? entropy2(c0, c1) : gini(c0, c1);
 }
 
-// Best split of one (node, feature) histogram: bins are scanned in value order, the zero bin
-// is node_total - sum(stored bins). Returns the gain (or -inf) and writes bin/left stats.
+// Best split of one (node, feature) histogram of exact integer sums: bins are scanned in value
+// order, the zero bin is node_total - sum(stored bins). s0/s1 = 2^-k of the two statistics.
+// Returns the gain (or -inf) and writes the bin and the left sums.
 // mode 0: XGBoost loss_chg = GL^2/(HL+l) + GR^2/(HR+l) - G^2/(H+l), children need H >= mcw.
 // mode 1/2: Spark impurity gain, children need (c0+c1) >= min instances.
-FDX_HD double best_split_scan(const double* hb, int nb, int zb, double T0, double T1, int mode,
-                              double lambda_, double mcw, int* out_bin, double* out_l0, double* out_l1) {
-  double s0 = 0.0, s1 = 0.0;
+FDX_HD double best_split_scan(const int64_t* hb, int nb, int zb, int64_t T0, int64_t T1, double s0, double s1,
+                              int mode, double lambda_, double mcw, int* out_bin, int64_t* out_l0, int64_t* out_l1) {
+  int64_t a0 = 0, a1 = 0;
   for (int b = 0; b < nb; ++b)
-    if (b != zb) { s0 += hb[2 * b]; s1 += hb[2 * b + 1]; }
-  const double z0 = T0 - s0, z1 = T1 - s1;
+    if (b != zb) { a0 += hb[2 * b]; a1 += hb[2 * b + 1]; }
+  const int64_t z0 = T0 - a0, z1 = T1 - a1;
   double best = -1.0 / 0.0;
   int best_b = -1;
-  double bl0 = 0, bl1 = 0;
-  double l0 = 0.0, l1 = 0.0;
-  const double parent = (mode == 0) ? (T0 * T0) / (T1 + lambda_) : impurity(mode, T0, T1);
+  int64_t bl0 = 0, bl1 = 0;
+  int64_t l0 = 0, l1 = 0;
+  const double G = (double)T0 * s0, H = (double)T1 * s1;
+  const double parent = (mode == 0) ? (G * G) / (H + lambda_) : impurity(mode, G, H);
   for (int b = 0; b + 1 < nb; ++b) {
     l0 += (b == zb) ? z0 : hb[2 * b];
     l1 += (b == zb) ? z1 : hb[2 * b + 1];
-    const double r0 = T0 - l0, r1 = T1 - l1;
+    const double L0 = (double)l0 * s0, L1 = (double)l1 * s1;
+    const double R0 = (double)(T0 - l0) * s0, R1 = (double)(T1 - l1) * s1;
     double gain;
     if (mode == 0) {
-      if (l1 < mcw || r1 < mcw) continue;
-      gain = (l0 * l0) / (l1 + lambda_) + (r0 * r0) / (r1 + lambda_) - parent;
+      if (L1 < mcw || R1 < mcw) continue;
+      gain = (L0 * L0) / (L1 + lambda_) + (R0 * R0) / (R1 + lambda_) - parent;
     } else {
-      const double nl = l0 + l1, nr = r0 + r1, n = nl + nr;
+      const double nl = L0 + L1, nr = R0 + R1, n = nl + nr;
       if (nl < mcw || nr < mcw || n <= 0) continue;
-      gain = parent - (nl / n) * impurity(mode, l0, l1) - (nr / n) * impurity(mode, r0, r1);
+      gain = parent - (nl / n) * impurity(mode, L0, L1) - (nr / n) * impurity(mode, R0, R1);
     }
     if (gain > best) { best = gain; best_b = b; bl0 = l0; bl1 = l1; }
   }

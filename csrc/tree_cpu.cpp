@@ -1,8 +1,9 @@
-// Host implementation of the tree engine (same contracts as tree_kernels.hip). The histogram is
-// accumulated in fp64 straight from the bf16 hi/lo statistics, so it agrees with the MFMA path
-// to ~1e-7 relative (the device accumulates each chunk in fp32); split decisions match except
-// for exact gain ties within that tolerance.
+// Host implementation of the tree engine (same contracts as tree_kernels.hip). Histograms are the
+// same exact int64 sums of quantised statistics as on the device, so host and device trees are
+// bitwise identical.
+#include <atomic>
 #include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "ops.h"
@@ -11,43 +12,49 @@
 
 namespace fdx {
 
-void rowstats_cpu(const RowStatsArgs& a) {
+void quant_max_cpu(const QuantArgs& a, double* out) {
+  std::mutex mu;
+  out[0] = out[1] = 0.0;
   parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
+    double x0 = 0.0, x1 = 0.0;
     for (int64_t r = lo; r < hi; ++r) {
-      uint32_t* st = a.rowstats + 2 * r;
-      if (a.mode == 0) {
-        const float w = a.weight ? a.weight[r] : 1.0f;
-        st[0] = split_bf16(a.g[r] * w);
-        st[1] = split_bf16(a.h[r] * w);
-      } else {
-        float w = a.weight ? a.weight[r] : 1.0f;
-        if (a.bootstrap) w *= (float)poisson1(hash_uniform(a.seed, (uint64_t)a.tree, (uint64_t)r));
-        const float y = a.label[r];
-        st[0] = split_bf16(w * (1.0f - y));
-        st[1] = split_bf16(w * y);
-      }
+      double v0, v1;
+      row_stats(a, r, &v0, &v1);
+      x0 = std::fmax(x0, std::fabs(v0));
+      x1 = std::fmax(x1, std::fabs(v1));
     }
+    std::lock_guard<std::mutex> lk(mu);   // max is order-independent
+    out[0] = std::fmax(out[0], x0);
+    out[1] = std::fmax(out[1], x1);
   });
 }
 
-void entry_stats_cpu(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est) {
-  parallel_for(nnz, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
-    for (int64_t e = lo; e < hi; ++e) {
-      est[2 * e] = rowstats[2 * (int64_t)csc_row[e]];
-      est[2 * e + 1] = rowstats[2 * (int64_t)csc_row[e] + 1];
+void quant_cpu(const QuantArgs& a, const double* maxv) {
+  const int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
+  a.kexp_out[0] = k0;
+  a.kexp_out[1] = k1;
+  std::atomic<int64_t> t0{0}, t1{0};
+  parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
+    int64_t s0 = 0, s1 = 0;
+    for (int64_t r = lo; r < hi; ++r) {
+      double v0, v1;
+      row_stats(a, r, &v0, &v1);
+      const int64_t q0 = quantize_value(v0, k0), q1 = quantize_value(v1, k1);
+      s0 += q0;
+      s1 += q1;
+      a.rowdig[2 * r] = a.np == 1 ? digits1(q0) : digits4(q0);
+      a.rowdig[2 * r + 1] = a.np == 1 ? digits1(q1) : digits4(q1);
+      if (a.digp)
+        for (int p = 0; p < a.np; ++p) {
+          a.digp[(int64_t)p * a.n_pad + r] = (uint8_t)(a.rowdig[2 * r] >> (8 * p));
+          a.digp[(int64_t)(a.np + p) * a.n_pad + r] = (uint8_t)(a.rowdig[2 * r + 1] >> (8 * p));
+        }
     }
+    t0 += s0;
+    t1 += s1;
   });
-}
-
-void entry_stats_items_cpu(const int64_t* item_start, const int64_t* item_end, int32_t num_items,
-                           const int32_t* csc_row, const uint32_t* rowstats, uint32_t* est) {
-  parallel_for(num_items, 0, 16, [&](int64_t lo, int64_t hi) {
-    for (int64_t it = lo; it < hi; ++it)
-      for (int64_t e = item_start[it]; e < item_end[it]; ++e) {
-        est[2 * e] = rowstats[2 * (int64_t)csc_row[e]];
-        est[2 * e + 1] = rowstats[2 * (int64_t)csc_row[e] + 1];
-      }
-  });
+  a.totals[0] = t0.load();
+  a.totals[1] = t1.load();
 }
 
 void slot8_cpu(const SlotArgs& a) {
@@ -60,42 +67,56 @@ void slot8_cpu(const SlotArgs& a) {
   });
 }
 
-static inline double unpack(uint32_t v) { return (double)bf2f(v & 0xffffu) + (double)bf2f(v >> 16); }
-
-void hist_cpu(const HistArgs& h, const HistReduceArgs& r, int slots) {
-  parallel_for(r.L, 0, 16, [&](int64_t lo, int64_t hi) {
-    std::vector<double> acc;
-    for (int64_t li = lo; li < hi; ++li) {
-      const int fid = r.feat[li];
-      const int nb = r.nbins[fid];
-      acc.assign((size_t)slots * nb * 2, 0.0);
-      for (int i = 0; i < r.feat_nitems[li]; ++i) {
-        const int64_t it = r.feat_item0[li] + i;
-        for (int64_t e = h.item_start[it]; e < h.item_end[it]; ++e) {
-          const int64_t row = h.csc_row[e];
-          const int s = h.slot8 ? (int)h.slot8[row] : 0;
-          if (s >= slots) continue;
-          const int b = h.csc_bin[e];
-          if (b >= nb) continue;
-          const uint32_t* st = h.rowstats ? h.rowstats + 2 * row : h.est + 2 * e;
-          acc[((size_t)s * nb + b) * 2] += unpack(st[0]);
-          acc[((size_t)s * nb + b) * 2 + 1] += unpack(st[1]);
-        }
-      }
-      for (int s = 0; s < slots; ++s) {
-        const int node = r.slot_to_node[s];
-        if (node < 0) continue;
-        double* dst = r.hist + ((int64_t)node * r.total_bins + r.boff[fid]) * 2;
-        for (int b = 0; b < nb; ++b) {
-          dst[2 * b] = acc[((size_t)s * nb + b) * 2];
-          dst[2 * b + 1] = acc[((size_t)s * nb + b) * 2 + 1];
-        }
+void hist_cpu(const HistArgs& h, int bt, int np) {
+  parallel_for(h.num_items, 0, 4, [&](int64_t lo, int64_t hi) {
+    for (int64_t it = lo; it < hi; ++it) {
+      const int32_t meta = h.item_meta[it];
+      const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta), koff = item_koff(meta);
+      const int32_t f0 = h.item_f0[it];
+      for (int64_t e = h.item_start[it]; e < h.item_end[it]; ++e) {
+        const int64_t row = h.csc_row[e];
+        const int s = h.slot8 ? (int)h.slot8[row] : 0;
+        if (s >= h.nslots) continue;
+        const int node = h.slot_node[s];
+        const int key = h.csc_key[e];
+        if (node < 0 || key < koff || key >= koff + 16 * bt) continue;
+        const int fl = key >> sl2, b = key & ((1 << sl2) - 1);
+        if (fl >= nfeat) continue;
+        const int f = f0 + fl;
+        if (b >= h.nbins[f]) continue;
+        const uint32_t* d = h.rowdig + 2 * row;
+        const int64_t q0 = np == 1 ? undigits1(d[0]) : undigits4(d[0]);
+        const int64_t q1 = np == 1 ? undigits1(d[1]) : undigits4(d[1]);
+        int64_t* dst = h.hist + ((int64_t)node * h.hist_stride + h.boff[f] + b) * 2;
+        __atomic_fetch_add(dst, q0, __ATOMIC_RELAXED);
+        __atomic_fetch_add(dst + 1, q1, __ATOMIC_RELAXED);
       }
     }
   });
 }
 
-void hist_subtract_cpu(const double* parent, double* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
+void hist_dense_cpu(const DenseHistArgs& a, int fg, int np) {
+  parallel_for((int64_t)a.ngroups * fg, 0, 1, [&](int64_t lo, int64_t hi) {
+    for (int64_t t = lo; t < hi; ++t) {
+      const int f = a.gfid[t];
+      if (f < 0) continue;
+      const uint8_t* col = a.dense + (int64_t)a.gdense[t] * a.n_pad;
+      for (int64_t row = 0; row < a.n_rows; ++row) {
+        const int s = a.slot8 ? (int)a.slot8[row] : 0;
+        if (s >= a.nslots) continue;
+        const int node = a.slot_node[s];
+        const int b = col[row];
+        if (node < 0 || b >= a.nbins[f]) continue;
+        const uint32_t* d = a.rowdig + 2 * row;
+        int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2;
+        __atomic_fetch_add(dst, np == 1 ? undigits1(d[0]) : undigits4(d[0]), __ATOMIC_RELAXED);
+        __atomic_fetch_add(dst + 1, np == 1 ? undigits1(d[1]) : undigits4(d[1]), __ATOMIC_RELAXED);
+      }
+    }
+  });
+}
+
+void hist_subtract_cpu(const int64_t* parent, int64_t* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
                        int32_t n_pairs, int64_t TB) {
   const int64_t per = TB * 2;
   for (int p = 0; p < n_pairs; ++p)
@@ -104,19 +125,19 @@ void hist_subtract_cpu(const double* parent, double* cur, const int32_t* dst, co
 }
 
 void split_cpu(const SplitArgs& a) {
+  const double s0 = std::ldexp(1.0, -a.kexp[0]), s1 = std::ldexp(1.0, -a.kexp[1]);
   parallel_for((int64_t)a.num_nodes * a.Fa, 0, 4096, [&](int64_t lo, int64_t hi) {
     for (int64_t t = lo; t < hi; ++t) {
       const int n = (int)(t / a.Fa), f = (int)(t % a.Fa);
-      double gain = -INFINITY, l0 = 0, l1 = 0;
+      double gain = -INFINITY;
+      int64_t l0 = 0, l1 = 0;
       int bin = -1;
       bool use = true;
-      if (a.feat_prob < 1.0)
-        use = hash_uniform(a.seed ^ 0x5bd1e995ull, ((uint64_t)a.tree << 32) | (uint32_t)a.node_ids[n],
-                           (uint64_t)a.fid_orig[f]) < a.feat_prob;
+      if (a.feat_thr) use = feature_priority(a.seed, a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
       if (use) {
-        const double* hb = a.hist + ((int64_t)n * a.boff[a.Fa] + a.boff[f]) * 2;
-        gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], a.mode, a.lambda_,
-                               a.min_child_weight, &bin, &l0, &l1);
+        const int64_t* hb = a.hist + ((int64_t)n * a.boff[a.Fa] + a.boff[f]) * 2;
+        gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], s0, s1, a.mode,
+                               a.lambda_, a.min_child_weight, &bin, &l0, &l1);
       }
       a.out_gain[t] = gain;
       a.out_bin[t] = bin;

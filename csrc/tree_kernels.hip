@@ -1,13 +1,15 @@
-// Histogram tree engine for gfx950 (K-10..K-15 of SURVEY.md §2.5).
+// Histogram tree engine for gfx950 (K-10..K-15 of SURVEY.md §2.5), exact integer arithmetic.
 //
-// Histogram build on the matrix cores: for one feature column chunk, the per-(bin, node, stat)
-// sums are the product  C[bin][col] = sum_k A[bin][k] * B[k][col]  over the chunk's entries k,
-// with A = one-hot(bin_k) (exact in bf16) and B[k][col] = (slot_k == node(col)) * stat(col)_k,
-// stat split into bf16 hi/lo halves so the fp32-accumulating v_mfma_f32_32x32x16_bf16 yields
-// ~fp32-accurate sums (class counts are small integers and exact). One wave per work item,
-// 16 entries per MFMA K-step, no atomics, fixed summation order -> deterministic histograms.
-// The rest of the level (reduce of chunk partials, sibling subtraction, split search, row
-// partition) are small bandwidth-bound kernels.
+// Histogram build on the i8 matrix cores: for one work item (a chunk of one feature column, or
+// several small whole columns packed into one 64-key tile), the per-(key, node slot, statistic)
+// sums are the product  C[key][col] = sum_k A[key][k] * B[k][col]  over the item's entries k,
+// with A = one-hot(key_k) (0x80 = -128 in the matching byte) and B[k][col] = the entry's digit
+// of (statistic, plane) of col, masked to the entries in col's node slot. v_mfma_i32_16x16x64_i8
+// accumulates exactly in int32; the epilogue divides by -128, recombines the NP digit planes into
+// int64 and adds them to the int64 histogram with integer atomics (order-independent, so the
+// result is bitwise deterministic). One wave per work item, 64 entries per MFMA K-step.
+// The rest of the level (sibling subtraction, split search, row partition) are small
+// bandwidth-bound kernels on the same int64 histograms.
 #include "ops.h"
 #include "tree.h"
 
@@ -18,102 +20,115 @@ namespace fdx {
 namespace {
 constexpr int kWave = 64;
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// 0x01 in every byte of x that is zero, 0x00 elsewhere (SWAR, no carries across bytes).
-__device__ __forceinline__ uint32_t match_bytes(uint32_t x) {
+// 0x80 in every byte of x that is zero, 0x00 elsewhere (SWAR, no carries across bytes).
+__device__ __forceinline__ uint32_t zero_bytes80(uint32_t x) {
   const uint32_t y = (x & 0x7f7f7f7fu) + 0x7f7f7f7fu;
-  return ~(y | x | 0x7f7f7f7fu) >> 7;
+  return ~(y | x | 0x7f7f7f7fu);
 }
-// bytes b0,b1 (lo) / b2,b3 (hi) of z -> b | b' << 16: one flag per 16-bit MFMA operand element,
-// then a 24-bit multiply turns each flag into the element value (0x3f80 = bf16 1.0, 0xffff mask).
-__device__ __forceinline__ uint32_t spread_lo(uint32_t z) { return __builtin_amdgcn_perm(z, z, 0x0c010c00u); }
-__device__ __forceinline__ uint32_t spread_hi(uint32_t z) { return __builtin_amdgcn_perm(z, z, 0x0c030c02u); }
+// 0xff in every byte of x that is zero
+__device__ __forceinline__ uint32_t zero_bytes_ff(uint32_t x) {
+  const uint32_t z = zero_bytes80(x);
+  return z | (z - (z >> 7));
+}
+// Slot masks for B with NP = 4 (2 slots per 16-column tile, lane's slot_sub b): a row with slot
+// byte s (0..15; 0xff = not built) feeds column tile ct iff s = 2 ct + b. Per K-step the digits
+// are masked once to the live rows of parity b (live_parity_mask), then per tile one byte-
+// permute table lookup on s >> 1 selects tile ct (ct_select): 2 VALU per dword per tile.
+__device__ __forceinline__ uint32_t live_parity_mask(uint32_t s, uint32_t pat) {   // pat = (0x80 | (b ^ 1)) * 0x01010101
+  const uint32_t u = (s ^ pat) & 0x81818181u;
+  return ((u >> 7) & u & 0x01010101u) * 0xffu;
+}
+__device__ __forceinline__ uint32_t ct_select(uint32_t sel, int ct) {            // sel = (s >> 1) & 0x07070707
+  const uint32_t lo = ct < 4 ? 0xffu << (8 * ct) : 0u, hi = ct < 4 ? 0u : 0xffu << (8 * (ct - 4));
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+template <int CT, int NP>
+__device__ __forceinline__ void slot_masked_b(uint4 d, uint4 sv, int slot_sub, i32x4 B[CT]) {
+  if constexpr (NP == 4) {
+    const uint32_t pat = (0x80u | (uint32_t)(slot_sub ^ 1)) * 0x01010101u;
+    const uint4 dm = make_uint4(d.x & live_parity_mask(sv.x, pat), d.y & live_parity_mask(sv.y, pat),
+                                d.z & live_parity_mask(sv.z, pat), d.w & live_parity_mask(sv.w, pat));
+    const uint4 sel = make_uint4((sv.x >> 1) & 0x07070707u, (sv.y >> 1) & 0x07070707u, (sv.z >> 1) & 0x07070707u,
+                                 (sv.w >> 1) & 0x07070707u);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      B[ct] = i32x4{(int)(dm.x & ct_select(sel.x, ct)), (int)(dm.y & ct_select(sel.y, ct)),
+                    (int)(dm.z & ct_select(sel.z, ct)), (int)(dm.w & ct_select(sel.w, ct))};
+  } else {
+    constexpr int SPT = 16 / (2 * NP);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const uint32_t rep = (uint32_t)(ct * SPT + slot_sub) * 0x01010101u;
+      B[ct] = i32x4{(int)(d.x & zero_bytes_ff(sv.x ^ rep)), (int)(d.y & zero_bytes_ff(sv.y ^ rep)),
+                    (int)(d.z & zero_bytes_ff(sv.z ^ rep)), (int)(d.w & zero_bytes_ff(sv.w ^ rep))};
+    }
+  }
+}
+
+// byte p of a, b, c, d -> [a.p, b.p, c.p, d.p]
+__device__ __forceinline__ uint32_t gather_byte(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t p) {
+  const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0000u | ((4u + p) << 8) | p);
+  const uint32_t hi = __builtin_amdgcn_perm(d, c, ((4u + p) << 24) | (p << 16) | 0x0c0cu);
+  return lo | hi;
+}
 
 __device__ __forceinline__ void lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 
-// ------------------------------------------------------------------ per-tree / per-pass row state
-__global__ __launch_bounds__(256) void rowstats_kernel(RowStatsArgs a) {
+// ------------------------------------------------------------------ quantised row statistics
+// max |v| of the two statistics over the rows (doubles are >= 0, so their bit patterns order
+// like unsigned integers: exact, order-independent atomic max).
+__global__ __launch_bounds__(256) void quant_max_kernel(QuantArgs a, unsigned long long* out) {
+  double m0 = 0.0, m1 = 0.0;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
-    uint2 st;
-    if (a.mode == 0) {
-      const float w = a.weight ? a.weight[r] : 1.0f;
-      st.x = split_bf16(a.g[r] * w);
-      st.y = split_bf16(a.h[r] * w);
-    } else {
-      float w = a.weight ? a.weight[r] : 1.0f;
-      if (a.bootstrap) w *= (float)poisson1(hash_uniform(a.seed, (uint64_t)a.tree, (uint64_t)r));
-      const float y = a.label[r];
-      st.x = split_bf16(w * (1.0f - y));
-      st.y = split_bf16(w * y);
-    }
-    reinterpret_cast<uint2*>(a.rowstats)[r] = st;
+    double v0, v1;
+    row_stats(a, r, &v0, &v1);
+    m0 = fmax(m0, fabs(v0));
+    m1 = fmax(m1, fabs(v1));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    m0 = fmax(m0, __shfl_xor(m0, o, kWave));
+    m1 = fmax(m1, __shfl_xor(m1, o, kWave));
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    atomicMax(out, (unsigned long long)__double_as_longlong(m0));
+    atomicMax(out + 1, (unsigned long long)__double_as_longlong(m1));
   }
 }
 
-// est[e] = rowstats[csc_row[e]]: the one random gather of the tree (4 entries per thread).
-__global__ __launch_bounds__(256) void entry_stats_kernel(const int32_t* __restrict__ csc_row,
-                                                          const uint2* __restrict__ rowstats, int64_t nnz,
-                                                          uint2* __restrict__ est) {
-  const int64_t n4 = nnz / 4;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const int4 r = reinterpret_cast<const int4*>(csc_row)[i];
-    const uint2 a = rowstats[r.x], b = rowstats[r.y], c = rowstats[r.z], d = rowstats[r.w];
-    reinterpret_cast<uint4*>(est)[2 * i] = make_uint4(a.x, a.y, b.x, b.y);
-    reinterpret_cast<uint4*>(est)[2 * i + 1] = make_uint4(c.x, c.y, d.x, d.y);
-  }
-  const int64_t t = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t < nnz) est[t] = rowstats[csc_row[t]];
-}
-
-// Item-ordered variant (same wave -> item table as the histogram launches): each XCD gathers from
-// the ~1 MB row-statistics slice of the row block it is working on, which stays in its L2.
-__global__ __launch_bounds__(256) void entry_stats_items_kernel(const int64_t* __restrict__ item_start,
-                                                                const int64_t* __restrict__ item_end,
-                                                                const int32_t* __restrict__ wave_item, int32_t num_items,
-                                                                const int32_t* __restrict__ csc_row,
-                                                                const uint2* __restrict__ rowstats,
-                                                                uint2* __restrict__ est) {
-  const int wslot = blockIdx.x * 4 + threadIdx.x / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int item = wave_item[wslot];
-  if (item < 0 || item >= num_items) return;
-  const int64_t e0 = item_start[item], e1 = item_end[item];
-  const int64_t e_last = (e1 - 1) & ~(int64_t)3;   // csc_row is padded, so a clamped 4-group is readable
-  // 4 consecutive entries per lane and U steps per round: U 16-B row loads, then 4U independent
-  // gathers in flight, then the 16-B stores (masked at the item's ends).
-  constexpr int U = 4;
-  for (int64_t base = e0 & ~(int64_t)3; base < e1; base += U * 4 * kWave) {
-    int4 r[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = base + (int64_t)u * 4 * kWave + 4 * lane;
-      r[u] = *reinterpret_cast<const int4*>(csc_row + (e < e_last ? e : e_last));
-    }
-    uint2 g[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      g[u][0] = rowstats[r[u].x]; g[u][1] = rowstats[r[u].y];
-      g[u][2] = rowstats[r[u].z]; g[u][3] = rowstats[r[u].w];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = base + (int64_t)u * 4 * kWave + 4 * lane;
-      if (e >= e0 && e + 4 <= e1) {
-        reinterpret_cast<uint4*>(est)[e / 2] = make_uint4(g[u][0].x, g[u][0].y, g[u][1].x, g[u][1].y);
-        reinterpret_cast<uint4*>(est)[e / 2 + 1] = make_uint4(g[u][2].x, g[u][2].y, g[u][3].x, g[u][3].y);
-      } else if (e < e1 && e + 4 > e0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (e + j >= e0 && e + j < e1) est[e + j] = g[u][j];
+// rowdig[r] = digits of (q0, q1); totals += (sum q0, sum q1) (int64 atomics, exact)
+__global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* maxv) {
+  const int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { a.kexp_out[0] = k0; a.kexp_out[1] = k1; }
+  int64_t t0 = 0, t1 = 0;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
+    double v0, v1;
+    row_stats(a, r, &v0, &v1);
+    const int64_t q0 = quantize_value(v0, k0), q1 = quantize_value(v1, k1);
+    t0 += q0;
+    t1 += q1;
+    uint2 d;
+    d.x = a.np == 1 ? digits1(q0) : digits4(q0);
+    d.y = a.np == 1 ? digits1(q1) : digits4(q1);
+    reinterpret_cast<uint2*>(a.rowdig)[r] = d;
+    if (a.digp) {
+      for (int p = 0; p < a.np; ++p) {
+        a.digp[(int64_t)p * a.n_pad + r] = (uint8_t)(d.x >> (8 * p));
+        a.digp[(int64_t)(a.np + p) * a.n_pad + r] = (uint8_t)(d.y >> (8 * p));
       }
     }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    t0 += __shfl_xor(t0, o, kWave);
+    t1 += __shfl_xor(t1, o, kWave);
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.totals), (unsigned long long)t0);
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.totals) + 1, (unsigned long long)t1);
   }
 }
 
@@ -125,53 +140,21 @@ __global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
   }
 }
 
-// One lane's 4 consecutive entries of a histogram step: rows (root: 0 = valid, -1 = outside the
-// item), bins (0xff outside) and the packed statistics (0 outside). Branch-free, so the compiler
-// can keep the next step's loads in flight across the current step: lanes past the item's end
-// re-read its last 4-group (clamped address), and the CSC arrays carry >= 4 readable entries of
-// padding, so a 4-group never leaves the allocation.
-struct StepData {
-  int4 r4;
-  uint32_t bins4;
-  uint4 p, q;
-};
-
-template <bool ROOT>
-__device__ __forceinline__ void load_step(const HistArgs& a, int64_t e, int64_t e0, int64_t e1, int64_t e_last,
-                                          StepData& d) {
-  const int64_t el = e < e_last ? e : e_last;
-  const uint32_t bins = *reinterpret_cast<const uint32_t*>(a.csc_bin + el);
-  int4 r = make_int4(0, 0, 0, 0);
-  if constexpr (!ROOT) r = *reinterpret_cast<const int4*>(a.csc_row + el);
-  uint4 p = reinterpret_cast<const uint4*>(a.est)[el / 2];
-  uint4 q = reinterpret_cast<const uint4*>(a.est)[el / 2 + 1];
-  const bool v0 = e >= e0 && e < e1, v1 = e + 1 >= e0 && e + 1 < e1;
-  const bool v2 = e + 2 >= e0 && e + 2 < e1, v3 = e + 3 >= e0 && e + 3 < e1;
-  const uint32_t keep = (v0 ? 0xffu : 0u) | (v1 ? 0xff00u : 0u) | (v2 ? 0xff0000u : 0u) | (v3 ? 0xff000000u : 0u);
-  d.bins4 = (bins & keep) | ~keep;
-  d.r4 = make_int4(v0 ? r.x : -1, v1 ? r.y : -1, v2 ? r.z : -1, v3 ? r.w : -1);
-  d.p = make_uint4(v0 ? p.x : 0u, v0 ? p.y : 0u, v1 ? p.z : 0u, v1 ? p.w : 0u);
-  d.q = make_uint4(v2 ? q.x : 0u, v2 ? q.y : 0u, v3 ? q.z : 0u, v3 ? q.w : 0u);
-}
-
-// Gather mode: only rows and bins stream (5 B per entry); the 1-byte slot and, for live entries
-// only, the 8-byte row statistics are gathered from the current row block's slice (~1.1 MB,
-// resident in the XCD's L2 under the XCD-ordered item placement). No per-tree entry-order copy
-// of the statistics is made, and entries outside the nodes being built cost no statistics bytes.
+// One lane's 4 consecutive entries of a histogram step: rows (-1 outside the item) and keys.
+// Branch-free, so the next steps' loads stay in flight: lanes past the item's end re-read its
+// last 4-group (clamped address), and the CSC arrays carry >= 4 readable entries of padding.
 struct RowStep {
   int4 r4;
-  uint32_t bins4;
+  uint32_t keys4;
 };
 
 __device__ __forceinline__ void load_rows(const HistArgs& a, int64_t e, int64_t e0, int64_t e1, int64_t e_last,
                                           RowStep& d) {
   const int64_t el = e < e_last ? e : e_last;
-  const uint32_t bins = *reinterpret_cast<const uint32_t*>(a.csc_bin + el);
+  d.keys4 = *reinterpret_cast<const uint32_t*>(a.csc_key + el);
   const int4 r = *reinterpret_cast<const int4*>(a.csc_row + el);
   const bool v0 = e >= e0 && e < e1, v1 = e + 1 >= e0 && e + 1 < e1;
   const bool v2 = e + 2 >= e0 && e + 2 < e1, v3 = e + 3 >= e0 && e + 3 < e1;
-  const uint32_t keep = (v0 ? 0xffu : 0u) | (v1 ? 0xff00u : 0u) | (v2 ? 0xff0000u : 0u) | (v3 ? 0xff000000u : 0u);
-  d.bins4 = (bins & keep) | ~keep;
   d.r4 = make_int4(v0 ? r.x : -1, v1 ? r.y : -1, v2 ? r.z : -1, v3 ? r.w : -1);
 }
 
@@ -191,48 +174,38 @@ __device__ __forceinline__ uint32_t entry_slots(const HistArgs& a, int4 r4) {
   }
 }
 
-// packed statistics of the live entries among the 4 (0 for dead ones: they are never staged)
-__device__ __forceinline__ void gather_stats(const uint2* __restrict__ rs, int4 r4, uint32_t slots4, uint32_t w[8]) {
+// digit words of the live entries among the 4 (0 for dead ones: they never contribute)
+__device__ __forceinline__ void gather_digits(const uint2* __restrict__ rd, int4 r4, uint32_t slots4, uint32_t w[8]) {
   const int32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     uint2 v = make_uint2(0u, 0u);
-    if (((slots4 >> (8 * j)) & 0xffu) != 0xffu) v = rs[rr[j]];
+    if (((slots4 >> (8 * j)) & 0xffu) != 0xffu) v = rd[rr[j]];
     w[2 * j] = v.x;
     w[2 * j + 1] = v.y;
   }
 }
 
-// ------------------------------------------------------------------ MFMA histogram
-// One wave per work item (a chunk of one feature column); per step the wave takes 256 entries,
-// 4 consecutive ones per lane so that rows (int4), bins (u32) and statistics (2 x uint4) are
-// single vector loads; the next step's loads are in flight while this one is multiplied.
-// ROOT: the pass builds only the root, so every entry is live in slot 0 and neither rows nor
-// the slot table are read. Otherwise only live entries (row in a node of this pass) are
-// compacted into LDS and MFMA K-steps run on ceil(live / KS) groups.
-// Tiles: NARROW (features with <= 16 bins, ~90 % of entries on text data) uses
-// v_mfma_f32_16x16x32_bf16: 16 bins x (4 slots x 4 stat halves), 32 entries per K-step; otherwise
-// v_mfma_f32_32x32x16_bf16: 32 bins x (8 slots x 4 stat halves), 16 entries per K-step. Operand
-// construction is VALU-issue bound, so the narrow tile halves the one-hot work per entry.
-// GATHER selects where the statistics come from:
-//   false  per-tree entry-order copy streamed with the rows and bins (load_step);
-//   true   row gathers (see load_rows): rows/bins of step i+3, slots of step i+2 and statistics
-//          of step i+1 are in flight while step i is staged and multiplied. (Measured at 10M
-//          rows / 1B entries: 34 ms per depth-6 round against 38.5 ms streaming, which also
-//          pays a per-tree entry-statistics pass; a 16-byte (slot, statistics) record per row
-//          and level, gathered once per entry, was slower still at 45 ms: the gathers are bound
-//          by L2 lines moved, not by instructions.)
-template <int BT, int CT, bool ROOT, bool NARROW, bool GATHER>
-__global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
+// ------------------------------------------------------------------ i8 MFMA histogram
+// One wave per work item; per step the wave takes 256 entries, 4 consecutive ones per lane (rows
+// int4, keys u32: single vector loads), with rows/keys of step i+3, slots of step i+2 and digits
+// of step i+1 in flight while step i is staged in LDS and multiplied.
+// Tile: v_mfma_i32_16x16x64_i8, lane l: r = l & 15 (A row = key r + 16 bt + koff, B column r),
+// g = l >> 4 (entries 16g .. 16g+15 of the K-step); C[key 4g + i][col r] in register i.
+// Columns: slot_sub = r / (2 NP) within the tile, q = r % (2 NP) = statistic * NP + plane.
+// ROOT: every entry of the item is live in slot 0 (no slot table, no compaction: the lane's 4
+// digit words are transposed into plane-major LDS rows in registers). Otherwise the live entries
+// (row in a node of this pass) are compacted, and K-steps run on ceil(live / 64) groups.
+template <int BT, int CT, int NP, bool ROOT>
+__global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   constexpr int G = 4 * kWave;                 // entries per wave step
-  constexpr int KS = NARROW ? 32 : 16;         // entries per MFMA K-step
-  constexpr int NSLOT = NARROW ? 4 : 8;        // node slots per column tile
-  constexpr int NBIN = NARROW ? 16 : 32;       // bins per row tile
-  constexpr int NREG = NARROW ? 4 : 16;        // accumulator registers per lane
-  typedef float acc_t __attribute__((ext_vector_type(NREG)));
-  __shared__ __attribute__((aligned(16))) uint8_t s_bin[4][G + KS];
+  constexpr int KS = 64;                       // entries per MFMA K-step
+  constexpr int CPS = 2 * NP;                  // columns per node slot
+  constexpr int SPT = 16 / CPS;                // node slots per 16-column tile
+  constexpr int NQ = 2 * NP;                   // staged digit planes
+  __shared__ __attribute__((aligned(16))) uint8_t s_key[4][G + KS];
   __shared__ __attribute__((aligned(16))) uint8_t s_slot[4][G + KS];
-  __shared__ __attribute__((aligned(16))) uint16_t s_comp[4][4][G + KS];
+  __shared__ __attribute__((aligned(16))) uint8_t s_dig[4][NQ][G + KS];
 
   const int wid = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
@@ -240,81 +213,59 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
   const int item = a.wave_item ? a.wave_item[wslot] : wslot;
   if (item < 0 || item >= a.num_items) return;
   const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
+  const int32_t meta = a.item_meta[item];
+  const uint32_t koff = (uint32_t)item_koff(meta);
 
-  const int col = NARROW ? (lane & 15) : (lane & 31);   // MFMA column / A-row index owned by this lane
-  const int kgrp = NARROW ? (lane >> 4) : (lane >> 5);  // which 8 entries of a K-step the lane supplies
-  const int comp = col & 3;                             // 0 stat0_hi, 1 stat0_lo, 2 stat1_hi, 3 stat1_lo
-  const int slot_sub = col >> 2;
+  const int r = lane & 15, g = lane >> 4;
+  const int slot_sub = r / CPS, q = r % CPS;
 
-  acc_t acc[BT][CT];
+  i32x4 acc[BT][CT];
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int i = 0; i < NREG; ++i) acc[bt][ct][i] = 0.0f;
+    for (int ct = 0; ct < CT; ++ct) acc[bt][ct] = i32x4{0, 0, 0, 0};
 
   const int64_t first = e0 & ~(int64_t)3;
   const int64_t e_last = (e1 - 1) & ~(int64_t)3;   // last 4-group holding an entry of the item
-  StepData cur, nxt;
-  // gather-mode pipeline state: statistics/slots/bins of step i, slots of step i+1, rows of i+1, i+2
-  const uint2* rs = reinterpret_cast<const uint2*>(a.rowstats);
+  const uint2* rd = reinterpret_cast<const uint2*>(a.rowdig);
   RowStep g1, g2;
-  uint32_t g_sl0 = 0, g_sl1 = 0, g_bins0 = 0, g_w[8];
-  if constexpr (GATHER) {
+  uint32_t sl0, sl1, keys0, w0[8];
+  {
     RowStep g0;
     load_rows(a, first + 4 * lane, e0, e1, e_last, g0);
     load_rows(a, first + G + 4 * lane, e0, e1, e_last, g1);
-    g_sl0 = entry_slots<ROOT>(a, g0.r4);
-    g_bins0 = g0.bins4;
-    g_sl1 = entry_slots<ROOT>(a, g1.r4);
-    gather_stats(rs, g0.r4, g_sl0, g_w);
+    sl0 = entry_slots<ROOT>(a, g0.r4);
+    keys0 = g0.keys4;
+    sl1 = entry_slots<ROOT>(a, g1.r4);
+    gather_digits(rd, g0.r4, sl0, w0);
     load_rows(a, first + 2 * G + 4 * lane, e0, e1, e_last, g2);
-  } else {
-    load_step<ROOT>(a, first + 4 * lane, e0, e1, e_last, cur);
   }
   for (int64_t base = first; base < e1; base += G) {
-    uint32_t slots4, bins4, w[8];
-    if constexpr (GATHER) {
-      slots4 = g_sl0;
-      bins4 = g_bins0;
+    const uint32_t slots4 = sl0, keys4 = keys0;
+    uint32_t w[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) w[j] = g_w[j];
-      // statistics of step i+1, slots of step i+2, rows of step i+3 (clamped, so unconditional)
-      gather_stats(rs, g1.r4, g_sl1, g_w);
-      const uint32_t sl2 = entry_slots<ROOT>(a, g2.r4);
-      RowStep g3;
-      load_rows(a, base + 3 * G + 4 * lane, e0, e1, e_last, g3);
-      g_sl0 = g_sl1;
-      g_bins0 = g1.bins4;
-      g_sl1 = sl2;
-      g1 = g2;
-      g2 = g3;
-    } else {
-      // slot of each of the lane's 4 entries (the only random access: a 1-byte table, L2-resident)
-      slots4 = entry_slots<ROOT>(a, cur.r4);
-      // prefetch the next step (clamped, so unconditional) while this one is staged and multiplied
-      load_step<ROOT>(a, base + G + 4 * lane, e0, e1, e_last, nxt);
-      bins4 = cur.bins4;
-      w[0] = cur.p.x; w[1] = cur.p.y; w[2] = cur.p.z; w[3] = cur.p.w;
-      w[4] = cur.q.x; w[5] = cur.q.y; w[6] = cur.q.z; w[7] = cur.q.w;
-    }
-    const bool any = slots4 != 0xffffffffu;
-    unsigned long long live = 0;
+    for (int j = 0; j < 8; ++j) w[j] = w0[j];
+    // digits of step i+1, slots of step i+2, rows of step i+3 (clamped, so unconditional)
+    gather_digits(rd, g1.r4, sl1, w0);
+    const uint32_t sl2 = entry_slots<ROOT>(a, g2.r4);
+    RowStep g3;
+    load_rows(a, base + 3 * G + 4 * lane, e0, e1, e_last, g3);
+    sl0 = sl1;
+    keys0 = g1.keys4;
+    sl1 = sl2;
+    g1 = g2;
+    g2 = g3;
+
     int n_live = G;
     if constexpr (ROOT) {
-      live = __ballot(any);
-      *reinterpret_cast<uint32_t*>(&s_bin[wid][4 * lane]) = bins4;
-      *reinterpret_cast<uint32_t*>(&s_slot[wid][4 * lane]) = slots4;
-      // comp c of entry j = 16-bit half (c & 1) of word (c >> 1) of entry j
-      *reinterpret_cast<uint2*>(&s_comp[wid][0][4 * lane]) =
-          make_uint2((w[0] & 0xffffu) | (w[2] << 16), (w[4] & 0xffffu) | (w[6] << 16));
-      *reinterpret_cast<uint2*>(&s_comp[wid][1][4 * lane]) =
-          make_uint2((w[0] >> 16) | (w[2] & 0xffff0000u), (w[4] >> 16) | (w[6] & 0xffff0000u));
-      *reinterpret_cast<uint2*>(&s_comp[wid][2][4 * lane]) =
-          make_uint2((w[1] & 0xffffu) | (w[3] << 16), (w[5] & 0xffffu) | (w[7] << 16));
-      *reinterpret_cast<uint2*>(&s_comp[wid][3][4 * lane]) =
-          make_uint2((w[1] >> 16) | (w[3] & 0xffff0000u), (w[5] >> 16) | (w[7] & 0xffff0000u));
+      // plane-major rows: s_dig[stat * NP + p][4 lane + j] = digit p of statistic stat of entry j
+      *reinterpret_cast<uint32_t*>(&s_key[wid][4 * lane]) = keys4;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          *reinterpret_cast<uint32_t*>(&s_dig[wid][st * NP + p][4 * lane]) =
+              gather_byte(w[st], w[2 + st], w[4 + st], w[6 + st], (uint32_t)p);
     } else {
       int nb = 0;
 #pragma unroll
@@ -322,118 +273,198 @@ __global__ __launch_bounds__(256) void hist_mfma_kernel(HistArgs a) {
         const uint32_t sj = (slots4 >> (8 * j)) & 0xffu;
         const unsigned long long bj = __ballot(sj != 0xffu);
         if (sj != 0xffu) {
-          const int p = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bj, 0u));
-          s_bin[wid][p] = (uint8_t)(bins4 >> (8 * j));
-          s_slot[wid][p] = (uint8_t)sj;
-          s_comp[wid][0][p] = (uint16_t)w[2 * j];
-          s_comp[wid][1][p] = (uint16_t)(w[2 * j] >> 16);
-          s_comp[wid][2][p] = (uint16_t)w[2 * j + 1];
-          s_comp[wid][3][p] = (uint16_t)(w[2 * j + 1] >> 16);
+          const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bj, 0u));
+          s_key[wid][pos] = (uint8_t)(keys4 >> (8 * j));
+          s_slot[wid][pos] = (uint8_t)sj;
+#pragma unroll
+          for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int p = 0; p < NP; ++p) s_dig[wid][st * NP + p][pos] = (uint8_t)(w[2 * j + st] >> (8 * p));
         }
         nb += __popcll(bj);
       }
       n_live = nb;
-      // pad the last partial K-step: bin/slot 0xff match no row/column, so stale comps drop out
-      if (lane < KS) {
-        s_bin[wid][nb + lane] = 0xffu;
-        s_slot[wid][nb + lane] = 0xffu;
-      }
+      // pad the last partial K-step: slot 0xff matches no column, so stale digits drop out
+      s_slot[wid][nb + lane] = 0xffu;
     }
     lds_sync();
 #pragma unroll
     for (int ks = 0; ks < G / KS; ++ks) {
-      if constexpr (ROOT) {
-        constexpr unsigned long long kLaneMask = (1ull << (KS / 4)) - 1ull;   // lanes holding the K-step
-        if (((live >> (ks * (KS / 4))) & kLaneMask) == 0ull) continue;
-      } else {
-        if (ks * KS >= n_live) break;
-      }
-      const int k0 = ks * KS + 8 * kgrp;
-      const uint2 bins8 = *reinterpret_cast<const uint2*>(&s_bin[wid][k0]);
-      const uint2 slots8 = *reinterpret_cast<const uint2*>(&s_slot[wid][k0]);
-      const uint4 cv = *reinterpret_cast<const uint4*>(&s_comp[wid][comp][k0]);
-      bf16x8 A[BT];
+      if (ks * KS >= n_live) break;
+      const int k0 = ks * KS + 16 * g;
+      const uint4 kv = *reinterpret_cast<const uint4*>(&s_key[wid][k0]);
+      const uint4 dv = *reinterpret_cast<const uint4*>(&s_dig[wid][q][k0]);
+      i32x4 A[BT];
 #pragma unroll
       for (int bt = 0; bt < BT; ++bt) {
-        const uint32_t rep = (uint32_t)(col + NBIN * bt) * 0x01010101u;
-        const uint32_t zl = match_bytes(bins8.x ^ rep), zh = match_bytes(bins8.y ^ rep);
-        const u32x4 av = {spread_lo(zl) * 0x3f80u, spread_hi(zl) * 0x3f80u,    // bf16 1.0 where bin == row
-                          spread_lo(zh) * 0x3f80u, spread_hi(zh) * 0x3f80u};
-        A[bt] = __builtin_bit_cast(bf16x8, av);
+        const uint32_t rep = ((uint32_t)(r + 16 * bt) + koff) * 0x01010101u;
+        A[bt] = i32x4{(int)zero_bytes80(kv.x ^ rep), (int)zero_bytes80(kv.y ^ rep), (int)zero_bytes80(kv.z ^ rep),
+                      (int)zero_bytes80(kv.w ^ rep)};
       }
+      if constexpr (ROOT) {
+        const i32x4 B = {(int)dv.x, (int)dv.y, (int)dv.z, (int)dv.w};
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        bf16x8 B;
-        if constexpr (ROOT) {
-          // one node: no slot mask; columns of the other slots collect junk the reduce never reads
-          B = __builtin_bit_cast(bf16x8, cv);
-        } else {
-          const uint32_t rep = (uint32_t)(ct * NSLOT + slot_sub) * 0x01010101u;
-          const uint32_t zl = match_bytes(slots8.x ^ rep), zh = match_bytes(slots8.y ^ rep);
-          const u32x4 bv = {cv.x & (spread_lo(zl) * 0xffffu), cv.y & (spread_hi(zl) * 0xffffu),
-                            cv.z & (spread_lo(zh) * 0xffffu), cv.w & (spread_hi(zh) * 0xffffu)};
-          B = __builtin_bit_cast(bf16x8, bv);
-        }
+        for (int bt = 0; bt < BT; ++bt) acc[bt][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[bt], B, acc[bt][0], 0, 0, 0);
+      } else {
+        const uint4 sv = *reinterpret_cast<const uint4*>(&s_slot[wid][k0]);
+        i32x4 B[CT];
+        slot_masked_b<CT, NP>(dv, sv, slot_sub, B);
 #pragma unroll
-        for (int bt = 0; bt < BT; ++bt) {
-          if constexpr (NARROW)
-            acc[bt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
-          else
-            acc[bt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[bt], B, acc[bt][ct], 0, 0, 0);
-        }
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int bt = 0; bt < BT; ++bt)
+            acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[bt], B[ct], acc[bt][ct], 0, 0, 0);
       }
     }
     lds_sync();
-    if constexpr (!GATHER) cur = nxt;
   }
 
-  // C[row][col]: 32x32 tile row = (reg&3) + 8*(reg>>2) + 4*kgrp, 16x16 tile row = 4*kgrp + reg;
-  // col = lane's column. Combine hi+lo halves (adjacent columns), store [item][slot][bin][stat].
-  float* out = a.slab + (int64_t)item * (NSLOT * CT) * (NBIN * BT) * 2;
+  // Epilogue: C = -128 * (plane sum); lanes r .. r+NP-1 hold the NP planes of one (slot, stat)
+  // column: the plane-0 lane recombines them into int64 and adds the nonzero sums to the histogram.
+  const int32_t f0 = a.item_f0[item];
+  const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta);
+  const int stat = q / NP;
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-      for (int reg = 0; reg < NREG; ++reg) {
-        const float v = acc[bt][ct][reg];
-        const float w2 = __shfl_xor(v, 1, kWave);
-        if ((col & 1) == 0) {
-          const int row = (NARROW ? 4 * kgrp + reg : (reg & 3) + 8 * (reg >> 2) + 4 * kgrp) + NBIN * bt;
-          const int slot = ct * NSLOT + slot_sub;
-          const int stat = (col >> 1) & 1;
-          out[((int64_t)slot * (NBIN * BT) + row) * 2 + stat] = v + w2;
+      for (int i = 0; i < 4; ++i) {
+        const int64_t s = -(int64_t)(acc[bt][ct][i] >> 7);
+        int64_t v = s;
+        if constexpr (NP == 4) {
+          const int64_t s1 = __shfl_down(s, 1, kWave), s2 = __shfl_down(s, 2, kWave), s3 = __shfl_down(s, 3, kWave);
+          v = s + s1 * 256 + s2 * 65536 + s3 * 16777216;
         }
+        const int slot = ct * SPT + slot_sub;
+        if ((q % NP) != 0 || v == 0 || slot >= a.nslots) continue;
+        const int node = a.slot_node[slot];
+        const int ek = 16 * bt + 4 * g + i + (int)koff;
+        const int fl = ek >> sl2, b = ek & ((1 << sl2) - 1);
+        if (node < 0 || fl >= nfeat) continue;
+        const int f = f0 + fl;
+        if (b >= a.nbins[f]) continue;
+        int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2 + stat;
+        atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
       }
 }
 
-// ------------------------------------------------------------------ reduce chunk partials
-__global__ __launch_bounds__(256) void hist_reduce_kernel(HistReduceArgs a) {
-  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t per_feat = (int64_t)a.slab_slots * a.slab_bins;
-  if (tid >= (int64_t)a.L * per_feat) return;
-  const int li = (int)(tid / per_feat);
-  const int rem = (int)(tid % per_feat);
-  const int s = rem / a.slab_bins, b = rem % a.slab_bins;
-  const int fid = a.feat[li];
-  if (b >= a.nbins[fid]) return;
-  const int node = a.slot_to_node[s];
-  if (node < 0) return;
-  double g = 0.0, h = 0.0;
-  const int64_t i0 = a.feat_item0[li];
-  for (int i = 0; i < a.feat_nitems[li]; ++i) {
-    const float* p = a.slab + ((i0 + i) * per_feat + (int64_t)s * a.slab_bins + b) * 2;
-    g += (double)p[0];
-    h += (double)p[1];
+// ------------------------------------------------------------------ dense i8 MFMA histogram
+// Same tile as hist_i8_kernel; the K dimension runs over 64 consecutive rows, so the row state
+// (digit planes, slot bytes) is streamed once per K-step and shared by the FG features of the
+// wave. The FG x 64 bin bytes of a K-step arrive by ONE coalesced 16-byte load per lane (lane l:
+// feature l / 4, rows 16 (l & 3) ..), are staged in a per-wave double-buffered LDS tile and read
+// back as MFMA A fragments (16 lanes of a k-group share one 16-byte row: LDS broadcast). No
+// compaction: dead rows (slot 0xff) are masked out of B. Loads run two K-steps ahead.
+template <int BT, int CT, int NP, bool ROOT, int FG>
+__global__ __launch_bounds__(256) void hist_dense_kernel(DenseHistArgs a) {
+  constexpr int CPS = 2 * NP, SPT = 16 / CPS;
+  static_assert(FG <= 16, "one 16-byte load per lane covers at most 16 features x 64 rows");
+  __shared__ __attribute__((aligned(16))) uint8_t s_bins[4][2][FG][64];
+  const int wid = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  // XCD-aware placement: workgroups b and b + 8 share an L2 (observed round-robin dispatch,
+  // speed only): XCD label x = b % 8 walks ranges x, x + 8, ... and all groups of a range.
+  const int x = blockIdx.x & 7;
+  const int k = (int)(blockIdx.x >> 3) * 4 + wid;
+  const int grp = k % a.ngroups;
+  const int range = x + 8 * (k / a.ngroups);
+  if (range >= a.nranges) return;
+  const int64_t r0 = (int64_t)range * a.range_rows;
+  const int64_t r1 = r0 + a.range_rows < a.n_pad ? r0 + a.range_rows : a.n_pad;
+  const int r = lane & 15, g = lane >> 4;
+  const int slot_sub = r / CPS, q = r % CPS;
+  int fid[FG];
+#pragma unroll
+  for (int j = 0; j < FG; ++j) fid[j] = a.gfid[grp * FG + j];
+  // loader lane: feature lj = lane / 4 (if < FG), rows 16 * (lane & 3) .. + 15 of the K-step
+  const int lj = lane >> 2;
+  const bool loader = lj < FG && a.gfid[grp * FG + (lj < FG ? lj : 0)] >= 0;
+  const uint8_t* lcol = a.dense + (int64_t)(loader ? a.gdense[grp * FG + lj] : 0) * a.n_pad + 16 * (lane & 3);
+  const uint8_t* dig = a.digp + (int64_t)q * a.n_pad + 16 * g;
+  const uint8_t* slt = a.slot8 + 16 * g;
+
+  i32x4 acc[FG][BT][CT];
+#pragma unroll
+  for (int j = 0; j < FG; ++j)
+#pragma unroll
+    for (int bt = 0; bt < BT; ++bt)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[j][bt][ct] = i32x4{0, 0, 0, 0};
+
+  // two K-steps of loads in flight: (bins, digits, slots) of steps i+1 and i+2
+  uint4 lb1 = make_uint4(0, 0, 0, 0), lb2 = lb1, d1 = lb1, d2 = lb1, s1 = lb1, s2 = lb1;
+  auto load = [&](int64_t base, uint4& lb, uint4& d, uint4& sv) {
+    if (base < r1) {
+      if (loader) lb = *reinterpret_cast<const uint4*>(lcol + base);
+      d = *reinterpret_cast<const uint4*>(dig + base);
+      if constexpr (!ROOT) sv = *reinterpret_cast<const uint4*>(slt + base);
+    }
+  };
+  uint4 lb0 = lb1, d0 = lb1, s0 = lb1;
+  load(r0, lb0, d0, s0);
+  load(r0 + 64, lb1, d1, s1);
+  if (lj < FG) *reinterpret_cast<uint4*>(&s_bins[wid][0][lj][16 * (lane & 3)]) = lb0;
+  int buf = 0;
+  for (int64_t base = r0; base < r1; base += 64) {
+    load(base + 128, lb2, d2, s2);
+    lds_sync();                                             // bins of this step staged
+    i32x4 B[CT];
+    if constexpr (ROOT) B[0] = i32x4{(int)d0.x, (int)d0.y, (int)d0.z, (int)d0.w};
+    else slot_masked_b<CT, NP>(d0, s0, slot_sub, B);
+#pragma unroll
+    for (int j = 0; j < FG; ++j) {
+      if (fid[j] < 0) continue;
+      const uint4 kv = *reinterpret_cast<const uint4*>(&s_bins[wid][buf][j][16 * g]);
+#pragma unroll
+      for (int bt = 0; bt < BT; ++bt) {
+        const uint32_t rep = (uint32_t)(r + 16 * bt) * 0x01010101u;
+        const i32x4 A = {(int)zero_bytes80(kv.x ^ rep), (int)zero_bytes80(kv.y ^ rep), (int)zero_bytes80(kv.z ^ rep),
+                         (int)zero_bytes80(kv.w ^ rep)};
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          acc[j][bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[ct], acc[j][bt][ct], 0, 0, 0);
+      }
+    }
+    // stage the next step's bins into the other buffer (read two steps from now)
+    if (lj < FG) *reinterpret_cast<uint4*>(&s_bins[wid][buf ^ 1][lj][16 * (lane & 3)]) = lb1;
+    buf ^= 1;
+    lb1 = lb2;
+    d0 = d1;
+    d1 = d2;
+    s0 = s1;
+    s1 = s2;
   }
-  double* dst = a.hist + ((int64_t)node * a.total_bins + a.boff[fid] + b) * 2;
-  dst[0] = g;
-  dst[1] = h;
+
+  const int stat = q / NP;
+#pragma unroll
+  for (int j = 0; j < FG; ++j)
+#pragma unroll
+    for (int bt = 0; bt < BT; ++bt)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t s = -(int64_t)(acc[j][bt][ct][i] >> 7);
+          int64_t v = s;
+          if constexpr (NP == 4) {
+            const int64_t t1 = __shfl_down(s, 1, kWave), t2 = __shfl_down(s, 2, kWave), t3 = __shfl_down(s, 3, kWave);
+            v = s + t1 * 256 + t2 * 65536 + t3 * 16777216;
+          }
+          const int slot = ct * SPT + slot_sub;
+          const int f = fid[j];
+          if ((q % NP) != 0 || v == 0 || slot >= a.nslots || f < 0) continue;
+          const int node = a.slot_node[slot];
+          const int b = 16 * bt + 4 * g + i;
+          if (node < 0 || b >= a.nbins[f]) continue;
+          int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2 + stat;
+          atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
+        }
 }
 
 // ------------------------------------------------------------------ sibling subtraction
-__global__ __launch_bounds__(256) void hist_subtract_kernel(const double* parent_hist, double* cur_hist,
+__global__ __launch_bounds__(256) void hist_subtract_kernel(const int64_t* parent_hist, int64_t* cur_hist,
                                                             const int32_t* dst, const int32_t* par,
                                                             const int32_t* sib, int32_t n_pairs, int64_t TB) {
   const int64_t per = TB * 2;
@@ -452,15 +483,13 @@ __global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
   const int n = (int)(t / a.Fa), f = (int)(t % a.Fa);
   double gain = -1.0 / 0.0;
   int bin = -1;
-  double l0 = 0, l1 = 0;
+  int64_t l0 = 0, l1 = 0;
   bool use = true;
-  if (a.feat_prob < 1.0)
-    use = hash_uniform(a.seed ^ 0x5bd1e995ull, ((uint64_t)a.tree << 32) | (uint32_t)a.node_ids[n],
-                       (uint64_t)a.fid_orig[f]) < a.feat_prob;
+  if (a.feat_thr) use = feature_priority(a.seed, a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
   if (use) {
-    const double* hb = a.hist + ((int64_t)n * (a.boff[a.Fa]) + a.boff[f]) * 2;
-    gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], a.mode, a.lambda_,
-                           a.min_child_weight, &bin, &l0, &l1);
+    const int64_t* hb = a.hist + ((int64_t)n * (a.boff[a.Fa]) + a.boff[f]) * 2;
+    gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], ldexp(1.0, -a.kexp[0]),
+                           ldexp(1.0, -a.kexp[1]), a.mode, a.lambda_, a.min_child_weight, &bin, &l0, &l1);
   }
   a.out_gain[t] = gain;
   a.out_bin[t] = bin;
@@ -516,60 +545,70 @@ inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
 }
 }  // namespace
 
-void launch_rowstats(const RowStatsArgs& a, hipStream_t s) {
-  if (a.N > 0) hipLaunchKernelGGL(rowstats_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
+void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, 2 * sizeof(double), s);
+  if (a.N > 0)
+    hipLaunchKernelGGL(quant_max_kernel, dim3(grid_for(a.N, 2048)), dim3(256), 0, s, a,
+                       reinterpret_cast<unsigned long long*>(out));
 }
 
-void launch_entry_stats(const int32_t* csc_row, const uint32_t* rowstats, int64_t nnz, uint32_t* est, hipStream_t s) {
-  if (nnz <= 0) return;
-  hipLaunchKernelGGL(entry_stats_kernel, dim3(grid_for(nnz / 4 + 1, 16384)), dim3(256), 0, s, csc_row,
-                     reinterpret_cast<const uint2*>(rowstats), nnz, reinterpret_cast<uint2*>(est));
-}
-
-void launch_entry_stats_items(const int64_t* item_start, const int64_t* item_end, const int32_t* wave_item,
-                              int32_t num_slots, int32_t num_items, const int32_t* csc_row, const uint32_t* rowstats,
-                              uint32_t* est, hipStream_t s) {
-  if (num_slots <= 0) return;
-  hipLaunchKernelGGL(entry_stats_items_kernel, dim3((unsigned)(num_slots / 4)), dim3(256), 0, s, item_start, item_end,
-                     wave_item, num_items, csc_row, reinterpret_cast<const uint2*>(rowstats),
-                     reinterpret_cast<uint2*>(est));
+void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s) {
+  (void)hipMemsetAsync(a.totals, 0, 2 * sizeof(int64_t), s);
+  hipLaunchKernelGGL(quant_kernel, dim3(grid_for(a.N, 2048)), dim3(256), 0, s, a, maxv);
 }
 
 void launch_slot8(const SlotArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(slot8_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
-void launch_hist_mfma(const HistArgs& a, int bt, int ct, hipStream_t s) {
+void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s) {
   if (a.num_items <= 0) return;
   const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
   const dim3 grid((slots + 3) / 4), block(256);
   const bool root = a.slot8 == nullptr;
-  const bool gather = a.rowstats != nullptr;
-  // bt 0: narrow 16-bin tile (ct = 1/2/4/8 groups of 4 slots); bt 1/2: 32-bin tiles (ct groups of 8)
-#define FDX_HIST_SRC(B, C, N, S)                                                                         \
-  if (gather == S) {                                                                                    \
-    if (root) hipLaunchKernelGGL((hist_mfma_kernel<B, C, true, N, S>), grid, block, 0, s, a);           \
-    else hipLaunchKernelGGL((hist_mfma_kernel<B, C, false, N, S>), grid, block, 0, s, a);               \
-  }
-#define FDX_HIST_CASE(B, C, N)                                                                           \
-  if (bt == (N ? 0 : B) && ct == C) {                                                                   \
-    FDX_HIST_SRC(B, C, N, false) FDX_HIST_SRC(B, C, N, true)                                            \
+#define FDX_HIST_NP(B, C, P)                                                                             \
+  if (np == P) {                                                                                        \
+    if (root) hipLaunchKernelGGL((hist_i8_kernel<B, 1, P, true>), grid, block, 0, s, a);                \
+    else hipLaunchKernelGGL((hist_i8_kernel<B, C, P, false>), grid, block, 0, s, a);                    \
     return;                                                                                             \
   }
-  FDX_HIST_CASE(1, 1, true) FDX_HIST_CASE(1, 2, true) FDX_HIST_CASE(1, 4, true) FDX_HIST_CASE(1, 8, true)
-  FDX_HIST_CASE(1, 1, false) FDX_HIST_CASE(1, 2, false) FDX_HIST_CASE(1, 4, false)
-  FDX_HIST_CASE(2, 1, false) FDX_HIST_CASE(2, 2, false) FDX_HIST_CASE(2, 4, false)
+#define FDX_HIST_CASE(B, C)                                                                              \
+  if (bt == B && ct == C) { FDX_HIST_NP(B, C, 1) FDX_HIST_NP(B, C, 4) }
+  FDX_HIST_CASE(1, 1) FDX_HIST_CASE(1, 2) FDX_HIST_CASE(1, 4) FDX_HIST_CASE(1, 8)
+  FDX_HIST_CASE(2, 1) FDX_HIST_CASE(2, 2) FDX_HIST_CASE(2, 4) FDX_HIST_CASE(2, 8)
+  FDX_HIST_CASE(4, 1) FDX_HIST_CASE(4, 2) FDX_HIST_CASE(4, 4) FDX_HIST_CASE(4, 8)
 #undef FDX_HIST_CASE
-#undef FDX_HIST_SRC
+#undef FDX_HIST_NP
 }
 
-void launch_hist_reduce(const HistReduceArgs& a, hipStream_t s) {
-  const int64_t n = (int64_t)a.L * a.slab_slots * a.slab_bins;
-  if (n <= 0) return;
-  hipLaunchKernelGGL(hist_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+// features per wave of the dense kernel: accumulators FG * BT * CT * 4 registers <= 64
+constexpr int dense_fg(int bt, int ct) { return bt * ct >= 16 ? 1 : 16 / (bt * ct) > 8 ? 8 : 16 / (bt * ct); }
+
+int dense_features_per_wave(int bt, int ct) { return dense_fg(bt, ct); }
+int dense_waves_per_group() { return 1; }
+
+void launch_hist_dense(const DenseHistArgs& a, int bt, int ct, int np, hipStream_t s) {
+  if (a.ngroups <= 0 || a.nranges <= 0) return;
+  const int per_x = (a.nranges + 7) / 8;                  // ranges per XCD label
+  const int64_t waves = (int64_t)per_x * a.ngroups;      // per XCD label
+  const dim3 grid((unsigned)(8 * ((waves + 3) / 4))), block(256);
+  const bool root = a.slot8 == nullptr;
+#define FDX_DENSE_NP(B, C, P)                                                                            \
+  if (np == P) {                                                                                        \
+    if (root) hipLaunchKernelGGL((hist_dense_kernel<B, 1, P, true, dense_fg(B, 1)>), grid, block, 0, s, a); \
+    else hipLaunchKernelGGL((hist_dense_kernel<B, C, P, false, dense_fg(B, C)>), grid, block, 0, s, a);    \
+    return;                                                                                             \
+  }
+#define FDX_DENSE_CASE(B, C)                                                                             \
+  if (bt == B && ct == C) { FDX_DENSE_NP(B, C, 1) FDX_DENSE_NP(B, C, 4) }
+  FDX_DENSE_CASE(1, 1) FDX_DENSE_CASE(1, 2) FDX_DENSE_CASE(1, 4) FDX_DENSE_CASE(1, 8)
+  FDX_DENSE_CASE(2, 1) FDX_DENSE_CASE(2, 2) FDX_DENSE_CASE(2, 4) FDX_DENSE_CASE(2, 8)
+  FDX_DENSE_CASE(4, 1) FDX_DENSE_CASE(4, 2) FDX_DENSE_CASE(4, 4) FDX_DENSE_CASE(4, 8)
+#undef FDX_DENSE_CASE
+#undef FDX_DENSE_NP
 }
 
-void launch_hist_subtract(const double* parent, double* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
+void launch_hist_subtract(const int64_t* parent, int64_t* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
                           int32_t n_pairs, int64_t TB, hipStream_t s) {
   if (n_pairs <= 0 || TB <= 0) return;
   hipLaunchKernelGGL(hist_subtract_kernel, dim3(grid_for((int64_t)n_pairs * TB * 2)), dim3(256), 0, s, parent, cur,

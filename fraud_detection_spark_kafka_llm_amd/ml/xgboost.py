@@ -41,14 +41,15 @@ class _XGBParams:
                Param("reg_lambda", "L2 regularisation", 1.0, float),
                Param("gamma", "min split loss", 0.0, float),
                Param("min_child_weight", "min hessian per child", 1.0, float),
-               Param("max_bin", "histogram bins per feature", 64, int),
+               Param("max_bin", "histogram bins per feature", 256, int),
                Param("max_delta_step", "max leaf step", 0.0, float),
                Param("base_score", "initial prediction (None = estimated)", None, float, has_default=False),
                Param("eval_metric", "evaluation metric", "auc", str),
                Param("objective", "objective", "binary:logistic", str),
                Param("tree_method", "tree method", "hist", str),
                Param("seed", "random seed", 0, int),
-               Param("deterministic", "bitwise-reproducible fixed-point gradients (any world size)", False, bool)]
+               Param("deterministic", "accepted for compatibility: training is always bitwise reproducible", True,
+                     bool)]
 
     # ClassificationModelBase reads Spark-style column getters
     def getFeaturesCol(self):  # noqa: N802

@@ -3,10 +3,16 @@
 Per round: ``tree_logistic_grad`` (g = p - y, h = p(1-p)) -> level-wise histogram tree with
 Newton gain ``GL^2/(HL+l) + GR^2/(HR+l) - G^2/(H+l)`` and ``min_child_weight`` on the hessian ->
 leaf weights ``-eta * G / (H + l)`` -> ``tree_leaf_update`` (margin += leaf of each row, read from
-the final row->node map; training rows are never re-scored). Defaults follow xgboost.spark as
-used by the reference (``max_depth=5, n_estimators=100``, eta 0.3, lambda 1, gamma 0,
-min_child_weight 1; /root/reference/fraud_detection_spark.py:76-83); ``base_score=None``
-estimates the intercept from the label mean like XGBoost >= 2.0.
+the final row->node map; training rows are never re-scored). ``GBDTParams`` defaults are
+XGBoost's own (max_depth 6, eta 0.3, lambda 1, gamma 0, min_child_weight 1, max_bin 256, the
+BASELINE config's depth 6); the reference's ``SparkXGBClassifier(max_depth=5, n_estimators=100)``
+(/root/reference/fraud_detection_spark.py:76-83) sets its own through the ML API.
+``base_score=None`` estimates the intercept from the label mean like XGBoost >= 2.0.
+
+Precision: g and h are the fp32 values of the logistic loss; histograms are exact int64 sums of
+rint(v * 2^k) with k from the round's max |v| (|q| <= 2^30), so a bin sum differs from the fp64
+sum of the fp32 g * w by at most count * 2^-(k+1) -- well inside fp32 accumulation error --
+and is bitwise identical on host, device and every data-parallel world size.
 
 Data parallel: rows are sharded across ranks, histograms and root totals are all-reduced
 (RCCL over xGMI), every rank grows the identical tree.
@@ -37,18 +43,13 @@ class GBDTParams:
     reg_lambda: float = 1.0
     gamma: float = 0.0
     min_child_weight: float = 1.0
-    max_bin: int = 64
+    max_bin: int = 256
     max_delta_step: float = 0.0
     base_score: Optional[float] = None
     seed: int = 0
-    # Bitwise-reproducible training for any world size / reduction order: g and h (times the
-    # instance weight, which must be <= 1) are rounded to multiples of 2^-12 and histogram work
-    # items hold <= 4096 entries, so every fp32 MFMA partial and every fp64 reduction is exact.
-    deterministic: bool = False
-
-
-DET_SCALE = 4096.0          # 2^12 grid for g, h in deterministic mode
-DET_CHUNK = 4096            # entries per histogram item: |sum| <= 4096 * 4096 = 2^24 (exact in fp32)
+    # Accepted for API compatibility: training is always bitwise reproducible for any world size
+    # and work split (exact int64 histograms of quantised g, h; see models/grower.py).
+    deterministic: bool = True
 
 
 @dataclass
@@ -84,12 +85,9 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
         forced_base = float(resume_state["base_margin"])
     else:
         forced_base = None
-    Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll,
-                          chunk=DET_CHUNK if params.deterministic else None)
+    Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll)
     dev = Q.device
     w = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float32)).to(dev)
-    if params.deterministic and w is not None and float(w.max()) > 1.0:
-        raise ValueError("deterministic mode needs instance weights <= 1")
     N = Q.n_rows
     if forced_base is not None:
         base = forced_base
@@ -105,7 +103,7 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     gp = GrowParams(max_depth=params.max_depth, mode=0, lambda_=params.reg_lambda, min_child=params.min_child_weight,
                     min_gain=params.gamma, seed=params.seed, eta=params.learning_rate,
                     max_delta_step=params.max_delta_step)
-    ws = Workspace(Q, 2 ** params.max_depth)
+    ws = Workspace(Q)
     trees = list(start_trees or [])
     if trees:   # resume: replay the checkpointed trees on this rank's training rows
         from ..ml.tree_model import ensemble_arrays
@@ -116,9 +114,6 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     for t in range(len(trees), params.n_estimators):
         with tracing.span("gbdt.round", round=t):
             C.tree_logistic_grad(margin, y, w, g, h)
-            if params.deterministic:
-                g.mul_(DET_SCALE).round_().div_(DET_SCALE)
-                h.mul_(DET_SCALE).round_().div_(DET_SCALE)
             tree = grow_tree(Q, ws, gp, t, g=g, h=h, coll=coll)
             node_value = torch.from_numpy(np.ascontiguousarray(tree.stats[:, 0])).to(dev)
             C.tree_leaf_update(margin, ws.row_node, node_value)

@@ -1,22 +1,25 @@
 """Level-wise histogram tree grower shared by DecisionTree, RandomForest and GBDT (X-09, X-10, X-13).
 
-Per level (all nodes of the level batched into every launch):
-  1. ``tree_slot8``        1-byte slot of the node being built per row (0xff: not built)
-  2. ``tree_hist_build``   MFMA histograms of the smaller child of each sibling pair (+ reduce);
-                           rows/bins stream, row statistics are gathered for live entries only
-                           (device), or streamed from a per-tree entry-order copy (host)
-  3. all-reduce            histograms of the built nodes across data-parallel ranks (RCCL)
-  4. ``tree_hist_subtract`` larger sibling = parent - built sibling
-  5. ``tree_split_find``   best (feature, bin) per (node, feature); argmax per node on device
+Per tree: ``tree_quant`` quantises the two row statistics (GBDT g*w, h*w, or class counts
+w*[y==0], w*[y==1]) to integers q = rint(v * 2^k) stored as i8 digit planes (csrc/tree.h); the
+exponent k comes from the global max |v| (all-reduced under data parallelism). Per level (all
+nodes of the level batched into every launch):
+  1. ``tree_slot8``         1-byte slot of the node being built per row (0xff: not built)
+  2. ``tree_hist_build``    i8-MFMA histograms of the smaller child of each sibling pair: exact
+                            int64 sums added straight into the level's histogram
+  3. reduce-scatter         int64 histograms of the built nodes across data-parallel ranks (RCCL);
+                            sums of integers are exact, so every rank holds the same bits
+  4. ``tree_hist_subtract`` larger sibling = parent - built sibling (exact)
+  5. ``tree_split_find``    best (feature, bin) per (node, feature); argmax per node on device
   6. host: create children (tiny D2H of one best split per node)
-  7. ``tree_partition``    rows -> children (default side for rows absent from the split column)
+  7. ``tree_partition``     rows -> children (default side for rows absent from the split column)
 Every rank makes identical decisions from identical reduced histograms, so no split broadcast is
-needed. Node statistics of children come from the parent's split (as in Spark and XGBoost).
+needed. Node statistics of children come from the parent's split (as in Spark and XGBoost), as
+exact integers; leaf values / class counts are scaled by 2^-k only when the tree is emitted.
 """
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -26,9 +29,11 @@ import torch
 from ..ml.tree_model import Tree
 from ..ops import native
 from ..utils import tracing
-from .quantize import CSC_PAD, Quantized
+from .quantize import Quantized
 
 NEG_INF = float("-inf")
+MAX_CT = 8                      # column tiles per pass (csrc/tree_kernels.hip launch_hist)
+DENSE_RANGE_ROWS = 32768        # rows per wave of the dense hot-feature histogram kernel
 
 
 @dataclass
@@ -38,62 +43,57 @@ class GrowParams:
     lambda_: float = 1.0          # gbdt L2
     min_child: float = 1.0        # gbdt: min_child_weight (hessian); cls: minInstancesPerNode
     min_gain: float = 0.0         # cls: minInfoGain ; gbdt: gamma (min_split_loss)
-    feat_prob: float = 1.0        # RF per-node feature sampling probability
+    feat_k: int = 0               # RF: features sampled per node (0 = all)
     seed: int = 0
     eta: float = 0.3              # gbdt learning rate (applied to leaf values)
     max_delta_step: float = 0.0
 
 
 class Workspace:
-    """Per-engine device buffers reused across trees (slab, row/entry statistics, slot table)."""
+    """Per-engine device buffers reused across trees (digits, slot table, row -> node map)."""
 
-    def __init__(self, Q: Quantized, max_nodes_per_level: int, src: Optional[str] = None):
+    def __init__(self, Q: Quantized, max_nodes_per_level: int = 0):
         dev = Q.device
-        self.rowstats = torch.empty((Q.n_rows, 2), dtype=torch.int32, device=dev)
-        nnz = Q.csc_row.numel()
-        # where the histogram kernels read the row statistics (see stats_source)
-        self.src = stats_source(dev) if src is None else src
-        if self.src not in STATS_SOURCES:
-            raise ValueError(f"statistics source must be one of {STATS_SOURCES}")
-        self.gather = self.src != "stream"
-        n_est = 0 if self.gather else nnz
-        self.est = torch.zeros((n_est + CSC_PAD, 2), dtype=torch.int32, device=dev)[:n_est]
-        self.slot8 = torch.empty(Q.n_rows, dtype=torch.uint8, device=dev)
+        self.rowdig = torch.empty((Q.n_rows, 2), dtype=torch.int32, device=dev)
+        self.kexp = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.totals = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.maxabs = torch.zeros(2, dtype=torch.float64, device=dev)
+        # padded to a multiple of 64 rows for the dense kernel (pad bytes stay 0xff = no slot)
+        self.slot8_pad = torch.full((Q.n_pad,), 0xFF, dtype=torch.uint8, device=dev)
+        self.slot8 = self.slot8_pad[:Q.n_rows]
+        self.digp = torch.zeros((8, Q.n_pad), dtype=torch.uint8, device=dev) if Q.dense is not None else None
+        self._dense_groups: dict = {}
+        self.dense_waves = int(native.lib().tree_dense_waves())
         self.row_node = torch.zeros(Q.n_rows, dtype=torch.int32, device=dev)
-        self.max_items = max((g.num_items for g in Q.groups), default=0)
-        self.slab = torch.empty(0, dtype=torch.float32, device=dev)
         self.Fa = Q.Fa
         self.dev = dev
         self.Q = Q
         self._shards = None
         self.staging = Staging(dev)
 
+    def dense_groups(self, bt: int, fg: int, keep: Optional[np.ndarray] = None):
+        """(gfid, gdense) device arrays [ngroups * fg] of the hot features with ``bt`` row tiles
+        (optionally only those with ``keep[d]``), -1 padded; cached when ``keep`` is None."""
+        key = (bt, fg)
+        if keep is None and key in self._dense_groups:
+            return self._dense_groups[key]
+        Q = self.Q
+        d = np.nonzero((Q.hot_bt == bt) & (keep if keep is not None else True))[0]
+        per_wg = fg * self.dense_waves
+        ng = (d.size + per_wg - 1) // per_wg * self.dense_waves
+        gfid = np.full(ng * fg, -1, dtype=np.int32)
+        gden = np.zeros(ng * fg, dtype=np.int32)
+        gfid[:d.size] = Q.hot[d]
+        gden[:d.size] = d
+        out = (torch.from_numpy(gfid).to(self.dev), torch.from_numpy(gden).to(self.dev))
+        if keep is None:
+            self._dense_groups[key] = out
+        return out
+
     def shards(self, coll) -> "FeatureShards":
         if getattr(self, "_shards", None) is None or self._shards.S != coll.world:
             self._shards = FeatureShards(self.Q, coll.world, coll.rank)
         return self._shards
-
-    def slab_for(self, items: int, bt: int, ct: int) -> torch.Tensor:
-        slots, bins = tile_shape(bt, ct)
-        need = items * slots * bins * 2
-        if self.slab.numel() < need:
-            self.slab = torch.empty(need, dtype=torch.float32, device=self.dev)
-        return self.slab
-
-
-STATS_SOURCES = ("stream", "gather")
-
-
-def stats_source(dev: torch.device) -> str:
-    """Where histogram kernels read row statistics (``FDX_HIST_SRC`` overrides):
-    ``stream``  a per-tree entry-order copy (est) streamed with rows and bins (host default);
-    ``gather``  1-byte slot + 8-byte statistics gathered per live entry from the row-block slice
-                that the XCD-ordered item placement keeps in L2 (device default: no per-tree
-                copy pass, no statistics bytes for entries outside the nodes being built)."""
-    env = os.environ.get("FDX_HIST_SRC")
-    if env:
-        return env
-    return "gather" if dev.type == "cuda" else "stream"
 
 
 class Staging:
@@ -164,14 +164,14 @@ class Staging:
 _TORCH_DTYPE = {"i4": torch.int32, "i8": torch.int64, "f8": torch.float64, "f4": torch.float32}
 
 
-def tile_shape(bt: int, ct: int) -> tuple:
-    """(node slots, bins) of one histogram work item's partial for tile shape ``bt``."""
-    return (4 * ct, 16) if bt == 0 else (8 * ct, 32 * bt)
+def slots_per_tile(np_: int) -> int:
+    """Node slots per 16-column MFMA tile: 2 statistics x ``np_`` digit planes per slot."""
+    return 16 // (2 * np_)
 
 
-def pass_ct(bt: int, cnt: int) -> int:
-    """Column tiles for ``cnt`` (<= 32) node slots: groups of 4 (narrow) or 8 slots, power of two."""
-    per = 4 if bt == 0 else 8
+def pass_ct(np_: int, cnt: int) -> int:
+    """Column tiles (power of two) for ``cnt`` node slots."""
+    per = slots_per_tile(np_)
     ct = 1
     while ct * per < cnt:
         ct *= 2
@@ -206,81 +206,80 @@ class FeatureShards:
         self.fid_orig = Q.fid_orig[f0:f1].contiguous()
 
 
-def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, params, tree_index, Fa, f0):
-    """Per node: (gain, feature (+f0), bin, left stat0, left stat1) of the best split over Fa
-    features of ``hist`` [nodes, boff[Fa], 2]; gain -inf when there is no valid candidate."""
+def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, params, feat_thr, tree_index, Fa,
+                 f0):
+    """Per node: (gain float64, feature (+f0) int64, bin int64, left sums int64 [2]) of the best
+    split over Fa features of ``hist`` [nodes, boff[Fa], 2]; gain -inf without a valid candidate.
+    Returned as one int64 tensor [nodes, 5] (gain bit-cast) for a single device->host copy."""
     dev = hist.device
     nl = int(node_ids.numel())
     if Fa == 0:
-        out = torch.zeros((nl, 5), dtype=torch.float64, device=dev)
-        out[:, 0] = NEG_INF
+        out = torch.zeros((nl, 5), dtype=torch.int64, device=dev)
+        out[:, 0] = torch.tensor(NEG_INF, dtype=torch.float64).view(torch.int64)
         out[:, 1:3] = -1
         return out
     out_gain = torch.empty((nl, Fa), dtype=torch.float64, device=dev)
     out_bin = torch.empty((nl, Fa), dtype=torch.int32, device=dev)
-    out_left = torch.empty((nl, Fa, 2), dtype=torch.float64, device=dev)
-    C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, int(params.mode), float(params.lambda_),
-                      float(params.min_child), float(params.feat_prob), int(params.seed), int(tree_index), out_gain,
-                      out_bin, out_left)
+    out_left = torch.empty((nl, Fa, 2), dtype=torch.int64, device=dev)
+    C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, int(params.mode),
+                      float(params.lambda_), float(params.min_child), feat_thr, int(params.seed), int(tree_index),
+                      out_gain, out_bin, out_left)
     best_gain, best_f = torch.max(out_gain, dim=1)
     ar = torch.arange(nl, device=dev)
-    best_bin = out_bin[ar, best_f]
+    best_bin = out_bin[ar, best_f].to(torch.int64)
     best_left = out_left[ar, best_f]
-    return torch.cat([best_gain[:, None], (best_f + f0)[:, None].double(), best_bin[:, None].double(), best_left], 1)
+    return torch.cat([best_gain.view(torch.int64)[:, None], (best_f + f0)[:, None], best_bin[:, None], best_left], 1)
 
 
-def _unpack_bf16_pair(col: torch.Tensor) -> torch.Tensor:
-    hi = ((col & 0xFFFF) << 16).to(torch.int32).view(torch.float32).to(torch.float64)
-    lo = (((col >> 16) & 0xFFFF) << 16).to(torch.int32).view(torch.float32).to(torch.float64)
-    return hi + lo
-
-
-def root_totals(ws: Workspace) -> torch.Tensor:
-    st = ws.rowstats.to(torch.int64)
-    return torch.stack([_unpack_bf16_pair(st[:, 0]).sum(), _unpack_bf16_pair(st[:, 1]).sum()])
+def _choose_np(params: GrowParams, weight) -> int:
+    """Digit planes per statistic: integer class counts (Poisson(1) <= 32, no instance weights)
+    fit one signed byte; everything else uses 4 planes (30-bit fixed point)."""
+    return 1 if (params.mode != 0 and weight is None) else 4
 
 
 def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
               g: Optional[torch.Tensor] = None, h: Optional[torch.Tensor] = None,
               label: Optional[torch.Tensor] = None, weight: Optional[torch.Tensor] = None,
               bootstrap: bool = False, coll=None) -> Tree:
-    """``coll`` (parallel.dist.Collectives, world > 1): data-parallel level with feature-sharded
-    split finding -- partial histograms are reduce-scattered by feature shard, every rank searches
-    splits of its own shard, and the per-node best tuples are all-gathered (SURVEY PAR-02)."""
+    """``coll`` (parallel.dist.Collectives): data-parallel level with feature-sharded split
+    finding when world > 1 -- partial histograms are reduce-scattered by feature shard, every
+    rank searches splits of its own shard, and the per-node best tuples are all-gathered
+    (SURVEY PAR-02). ``coll.force`` runs the same collective path at world size 1 (RCCL check)."""
     C = native.lib()
-    shards = ws.shards(coll) if coll is not None and coll.active and coll.world > 1 else None
-    all_reduce = coll.sum if coll is not None and coll.active else None
+    use_coll = coll is not None and coll.active
+    shards = ws.shards(coll) if use_coll and (coll.world > 1 or getattr(coll, "force", False)) else None
     dev = Q.device
     mode_rs = 0 if params.mode == 0 else 1
+    np_ = _choose_np(params, weight)
+    spt = slots_per_tile(np_)
+    pass_slots = spt * MAX_CT
     max_nodes = 2 ** (params.max_depth + 1)
     # host node table
-    parent = [-1]
-    depth = [0]
-    feature = [-1]
-    binv = [-1]
-    thr = [0.0]
-    left = [-1]
-    right = [-1]
-    gain = [-1.0]
-    stats = [None]
-    is_leaf = [False]
+    parent, depth, feature, binv, thr = [-1], [0], [-1], [-1], [0.0]
+    left, right, gain, stats, is_leaf = [-1], [-1], [-1.0], [None], [False]
 
     ws.row_node.zero_()
-    with tracing.span("tree.rowstats"):
-        C.tree_rowstats(g, h, label, weight, int(params.seed), int(tree_index), bool(bootstrap), mode_rs,
-                        ws.rowstats)
-        if not ws.gather:
-            st, en, order = Q.all_items()   # XCD-ordered items: each XCD gathers within its current row block
-            C.tree_entry_stats_items(st, en, order, Q.csc_row, ws.rowstats, ws.est)
-    tot = root_totals(ws)
-    if all_reduce is not None:
-        tot = all_reduce(tot)
-    stats[0] = tot.cpu().numpy().astype(np.float64)
+    with tracing.span("tree.quant"):
+        seed = int(params.seed)
+        if np_ == 4:
+            C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
+                             ws.maxabs)
+            mx = coll.max(ws.maxabs) if use_coll else ws.maxabs
+            C.tree_quant(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, 4, mx, ws.rowdig,
+                         ws.kexp, ws.totals, ws.digp)
+        else:
+            C.tree_quant(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, 1, None, ws.rowdig,
+                         ws.kexp, ws.totals, ws.digp)
+    tot = coll.sum(ws.totals) if use_coll else ws.totals
+    head = torch.cat([tot, ws.kexp.to(torch.int64)]).cpu().numpy()
+    stats[0] = head[:2].astype(np.int64)
+    kexp = head[2:4].astype(np.int64)
+    scale = np.ldexp(1.0, -kexp)                    # value of one quantisation step per statistic
     level = [0]
     prev_hist = None
     prev_index: dict = {}
     TB = Q.TB
-    feat_groups = Q.groups
+    feat_thr_all = None
 
     for d in range(params.max_depth + 1):
         open_nodes = [n for n in level if not is_leaf[n]]
@@ -290,8 +289,10 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             break
         # --- decide which nodes to build (smaller sibling) and which to subtract
         build, subtract = [], []
-        if d == 0:
-            build = open_nodes
+        if d == 0 or params.feat_k:
+            # RF: a feature sampled at this level may not have been built for the parent, so
+            # sibling subtraction would read a missing parent histogram: build every open node
+            build = list(open_nodes)
         else:
             seen = set()
             for n in open_nodes:
@@ -314,16 +315,21 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         local = {n: i for i, n in enumerate(open_nodes)}
         nl = len(open_nodes)
         nb = len(build)
+        # RF: exact k-of-F feature sample per open node (threshold on the node's priorities)
+        feat_thr = None
+        if params.feat_k:
+            from .rf_sampling import node_thresholds
+
+            feat_thr_all = node_thresholds(Q.num_features, params.seed, tree_index, open_nodes, params.feat_k, dev)
+            feat_thr = feat_thr_all
         if shards is None:
-            cur_hist = torch.zeros((nl, TB, 2), dtype=torch.float64, device=dev)
-            hist_target, stride, target_of = cur_hist, TB, local
+            cur_hist = torch.zeros((nl, TB, 2), dtype=torch.int64, device=dev)
+            hist_target, target_of = cur_hist, local
         else:
             # local partials of the built nodes (+1 zero pad bin for the shard packing)
-            hist_target = torch.zeros((nb, TB + 1, 2), dtype=torch.float64, device=dev)
-            stride, target_of = TB + 1, {n: k for k, n in enumerate(build)}
-        # --- small per-level arrays, one staged upload: node -> slot of the built nodes (slot =
-        # position in `build`), slot -> histogram row per pass and tile shape, subtraction
-        # triples, open-node totals and ids
+            hist_target = torch.zeros((nb, TB + 1, 2), dtype=torch.int64, device=dev)
+            target_of = {n: k for k, n in enumerate(build)}
+        # --- small per-level arrays, one staged upload
         stg = ws.staging
         h_ns = None
         if d > 0:
@@ -331,61 +337,62 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             ns[np.asarray(build, dtype=np.int64)] = np.arange(nb, dtype=np.int32)
             h_ns = stg.add(ns)
         passes = []
-        for s0 in range(0, nb, 32):
-            cnt = min(32, nb - s0)
-            caps = {}
-            for grp in feat_groups:
-                cap = tile_shape(grp.bt, pass_ct(grp.bt, cnt))[0]
-                if cap not in caps:
-                    s2n = np.full(cap, -1, dtype=np.int32)
-                    s2n[:cnt] = [target_of[build[s0 + k]] for k in range(cnt)]
-                    caps[cap] = stg.add(s2n)
-            passes.append((s0, cnt, caps))
+        for s0 in range(0, nb, pass_slots):
+            cnt = min(pass_slots, nb - s0)
+            s2n = np.array([target_of[build[s0 + k]] for k in range(cnt)], dtype=np.int32)
+            passes.append((s0, cnt, stg.add(s2n)))
         h_sub = None
         if subtract:
             h_sub = (stg.add(np.array([local[a] for a, _, _ in subtract], dtype=np.int32)),
                      stg.add(np.array([prev_index[p] for _, p, _ in subtract], dtype=np.int32)),
                      stg.add(np.array([local[s] for _, _, s in subtract], dtype=np.int32)))
-        h_tot = stg.add(np.stack([stats[n] for n in open_nodes]).astype(np.float64))
+        h_tot = stg.add(np.stack([stats[n] for n in open_nodes]).astype(np.int64))
         h_ids = stg.add(np.array(open_nodes, dtype=np.int32))
         h_bidx = stg.add(np.array([local[n] for n in build], dtype=np.int64))
         up = stg.upload()
         node_slot = up[h_ns] if h_ns is not None else None
-        # --- histograms, up to 32 node slots per pass
+        # --- histograms, up to `pass_slots` node slots per pass
         with tracing.span("tree.hist"):
-            for s0, cnt, caps in passes:
+            sel_groups = Q.groups
+            hot_keep = None
+            if feat_thr is not None:
+                from .rf_sampling import level_feature_mask
+
+                mask = level_feature_mask(Q, params.seed, tree_index, open_nodes, feat_thr)
+                sel_groups = [grp.subset(mask) for grp in Q.groups]
+                if Q.dense is not None:
+                    hot_keep = mask[torch.from_numpy(Q.hot).to(dev)].cpu().numpy()
+            for s0, cnt, h_s2n in passes:
                 slot8 = None
                 if d > 0:
                     C.tree_slot8(ws.row_node, node_slot, s0, cnt, ws.slot8)
                     slot8 = ws.slot8
-                for grp in feat_groups:
-                    gsel = grp if params.feat_prob >= 1.0 else _rf_subset(grp, Q, params, tree_index,
-                                                                          [build[s0 + k] for k in range(cnt)])
-                    if gsel.num_items == 0:
+                ct = pass_ct(np_, cnt)
+                for grp in sel_groups:
+                    if grp.num_items == 0:
                         continue
-                    ct = pass_ct(grp.bt, cnt)
-                    cap = tile_shape(grp.bt, ct)[0]
-                    slab = ws.slab_for(gsel.num_items, grp.bt, ct)
-                    C.tree_hist_build(gsel.item_start, gsel.item_end, Q.csc_row, Q.csc_bin, slot8, ws.est,
-                                      grp.bt, ct, slab, gsel.feat, gsel.feat_item0, gsel.feat_nitems, Q.boff,
-                                      Q.nbins, up[caps[cap]], hist_target, stride, gsel.wave_order(),
-                                      ws.rowstats if ws.gather else None)
+                    C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
+                                      Q.h_row, Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, up[h_s2n],
+                                      hist_target, TB, grp.bt, ct, np_)
+                if Q.dense is not None:
+                    for bt in (1, 2, 4):
+                        gfid, gden = ws.dense_groups(bt, C.tree_dense_fg(bt, ct if d > 0 else 1), hot_keep)
+                        if gfid.numel():
+                            C.tree_hist_dense(Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad, gfid,
+                                              gden, Q.boff, Q.nbins, up[h_s2n], hist_target, TB, Q.n_rows,
+                                              DENSE_RANGE_ROWS, bt, ct, np_)
         totals, node_ids = up[h_tot], up[h_ids]
         sub_t = tuple(up[h] for h in h_sub) if h_sub is not None else None
         if shards is None:
-            if all_reduce is not None:
-                with tracing.span("tree.allreduce"):
-                    idx = up[h_bidx]
-                    cur_hist.index_copy_(0, idx, all_reduce(cur_hist.index_select(0, idx)))
             if sub_t is not None:
                 C.tree_hist_subtract(prev_hist, cur_hist, *sub_t, TB)
             with tracing.span("tree.split"):
-                packed = _best_splits(C, cur_hist, totals, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, node_ids, params,
-                                      tree_index, Q.Fa, 0)
+                packed = _best_splits(C, cur_hist, totals, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, node_ids, ws.kexp,
+                                      params, feat_thr, tree_index, Q.Fa, 0)
                 packed = packed.cpu().numpy()
         else:
             with tracing.span("tree.reduce_scatter"):
-                cur_hist = torch.zeros((nl, shards.bins, 2), dtype=torch.float64, device=dev)
+                cur_hist = torch.zeros((nl, shards.bins, 2), dtype=torch.int64, device=dev)
                 if nb:
                     packed_in = hist_target.index_select(1, shards.pack_idx).view(nb, shards.S, shards.Bs, 2)
                     mine = coll.reduce_scatter(packed_in.permute(1, 0, 2, 3))
@@ -394,17 +401,19 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 C.tree_hist_subtract(prev_hist, cur_hist, *sub_t, shards.bins)
             with tracing.span("tree.split"):
                 mine = _best_splits(C, cur_hist, totals, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
-                                    node_ids, params, tree_index, shards.Fa, shards.f0)
-                allt = coll.all_gather(mine)                       # [S, nl, 5]
-                best_s = torch.argmax(allt[:, :, 0], dim=0)        # ties -> lowest shard = lowest feature
+                                    node_ids, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0)
+                allt = coll.all_gather(mine)                                  # [S, nl, 5]
+                gains = allt[:, :, 0].contiguous().view(torch.float64)
+                best_s = torch.argmax(gains, dim=0)                           # ties -> lowest shard = lowest feature
                 packed = allt[best_s, torch.arange(nl, device=dev)].cpu().numpy()
         # --- create children
         next_level = []
         default_child = np.full(max_nodes, -1, dtype=np.int32)
         splits = []
+        gains_host = packed[:, 0].copy().view(np.float64)
         for i, n in enumerate(open_nodes):
-            gval, fid, b, l0, l1 = packed[i]
-            fid, b = int(fid), int(b)
+            gval = float(gains_host[i])
+            fid, b = int(packed[i, 1]), int(packed[i, 2])
             ok = b >= 0 and math.isfinite(gval)
             if params.mode == 0:
                 ok = ok and gval > max(params.min_gain, 1e-6)
@@ -413,7 +422,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             if not ok:
                 is_leaf[n] = True
                 continue
-            tl = np.array([l0, l1])
+            tl = packed[i, 3:5].astype(np.int64)
             tr = stats[n] - tl
             li, ri = len(parent), len(parent) + 1
             for child, st in ((li, tl), (ri, tr)):
@@ -428,7 +437,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 stats.append(st)
                 leafy = (d + 1 >= params.max_depth)
                 if params.mode != 0:
-                    leafy = leafy or _impurity(st, params.mode) == 0.0
+                    leafy = leafy or _impurity(st * scale, params.mode) == 0.0
                 is_leaf.append(leafy)
             feature[n], binv[n], thr[n], left[n], right[n], gain[n] = fid, b, Q.threshold(fid, b), li, ri, gval
             left_default = int(Q.zbin_host[fid]) <= b
@@ -444,14 +453,13 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         level = next_level
 
     n = len(parent)
-    K = 2
-    st = np.zeros((n, K))
+    st = np.zeros((n, 2), dtype=np.float64)
     for i in range(n):
-        st[i] = stats[i]
+        st[i] = stats[i].astype(np.float64) * scale
     feat_orig = np.array([int(Q.fid_host[f]) if f >= 0 and not is_leaf[i] else -1 for i, f in enumerate(feature)],
                          dtype=np.int32)
-    left_a = np.array([l if not is_leaf[i] else -1 for i, l in enumerate(left)], dtype=np.int32)
-    right_a = np.array([r if not is_leaf[i] else -1 for i, r in enumerate(right)], dtype=np.int32)
+    left_a = np.array([lc if not is_leaf[i] else -1 for i, lc in enumerate(left)], dtype=np.int32)
+    right_a = np.array([rc if not is_leaf[i] else -1 for i, rc in enumerate(right)], dtype=np.int32)
     thr_a = np.array(thr, dtype=np.float64)
     gain_a = np.array([gv if not is_leaf[i] else -1.0 for i, gv in enumerate(gain)], dtype=np.float64)
     if params.mode == 0:
@@ -472,8 +480,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     return Tree(feat_orig, thr_a, left_a, right_a, stats_out, imp, gain_a, raw_count, pred, 0)
 
 
-def _weight(st, mode) -> float:
-    return float(st[1]) if mode == 0 else float(st[0] + st[1])
+def _weight(st, mode) -> int:
+    return int(st[1]) if mode == 0 else int(st[0] + st[1])
 
 
 def _impurity(st, mode) -> float:
@@ -493,8 +501,8 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits
     colptr = Q.colptr.cpu().numpy() if not hasattr(Q, "_colptr_host") else Q._colptr_host
     Q._colptr_host = colptr
     starts, ends, item_split = [], [], []
-    for si, (fid, _, _, _, _) in enumerate(splits):
-        a, b = int(colptr[fid]), int(colptr[fid + 1])
+    for si, sp in enumerate(splits):
+        a, b = int(colptr[sp[0]]), int(colptr[sp[0] + 1])
         for s in range(a, b, chunk):
             starts.append(s)
             ends.append(min(b, s + chunk))
@@ -505,11 +513,3 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits
     hs += [stg.add(np.array([sp[k] for sp in splits], dtype=np.int32)) for k in (1, 2, 3, 4)]
     up = stg.upload()
     C.tree_partition(ws.row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin)
-
-
-def _rf_subset(grp, Q: Quantized, params: GrowParams, tree_index: int, nodes: list):
-    """Features sampled by at least one node of this pass (same hash as the split kernel)."""
-    from .rf_sampling import node_feature_mask
-
-    mask = node_feature_mask(Q, params, tree_index, nodes)
-    return grp.subset(mask)

@@ -12,7 +12,16 @@ Two binning paths:
   Values are keyed at float32 precision (XGBoost bins at float32 as well).
 
 In both paths the thresholds are value-space midpoints, so the same tree scores raw feature
-values with either ``x <= t`` (Spark) or ``x < t`` (XGBoost) semantics. Under data parallelism
+values with either ``x <= t`` (Spark) or ``x < t`` (XGBoost) semantics.
+
+Histogram layout (``_finish_items``): features present in >= HOT_DENSITY of the rows go to a
+dense column-major bin block (their row state is streamed, not gathered). The other features'
+entries are copied into a histogram CSC laid out row-super-block-major (super-block = a range of
+rows whose 1-byte slot and 8-byte digit slices fit one XCD's 4 MB L2; the XCD-ordered item
+placement keeps each XCD inside one super-block at a time), as (row, key) with key = kbase + bin.
+One wave of the i8 MFMA histogram kernel per work item: a chunk of one feature inside one
+super-block, or several consecutive small features packed into one 64-key tile (``stride`` keys
+per feature, kbase = position * stride), so the ~28K small text features do not each cost a wave. Under data parallelism
 the per-rank statistics (max counts / distinct values) are merged with collectives so every rank
 holds identical bins.
 """
@@ -31,42 +40,39 @@ from ..utils import tracing
 CSC_PAD = 16
 
 CHUNK = int(os.environ.get("FDX_HIST_CHUNK", 32768))   # entries per histogram work item (one wavefront)
+PACK_KEYS = int(os.environ.get("FDX_PACK_KEYS", 16))   # keys of a packed multi-feature item (16 = one MFMA row tile)
 
 
 @dataclass
-class BinGroup:
-    """Work items of the features of one MFMA tile shape: ``bt`` 0 = at most 16 bins (narrow
-    16x16x32 tile), 1 / 2 = at most 32 / 64 bins (one or two 32-row 32x32x16 tiles)."""
+class ItemGroup:
+    """Work items of one MFMA row-tile count ``bt`` (16 * bt keys per item): a chunk of one
+    feature (``meta`` stride 256, nfeat 1; ``koff`` windows for features with > 64 bins) or
+    several whole small features packed into one tile."""
     bt: int
     item_start: torch.Tensor     # int64 [I]
     item_end: torch.Tensor       # int64 [I]
-    item_feat: torch.Tensor      # int32 [I]
-    feat: torch.Tensor           # int32 [L]
-    feat_item0: torch.Tensor     # int64 [L]
-    feat_nitems: torch.Tensor    # int32 [L]
+    item_f0: torch.Tensor        # int32 [I] first feature of the item
+    item_meta: torch.Tensor      # int32 [I] stride_log2 | nfeat << 8 | koff << 16 (csrc/tree.h)
     item_blk: Optional[torch.Tensor] = None   # int32 [I] row block of the item (-1: whole column)
     _order: Optional[torch.Tensor] = None
 
-    def subset(self, feat_mask: torch.Tensor) -> "BinGroup":
-        """Restrict to features with ``feat_mask[fid]`` (RF per-level feature union)."""
-        keep_items = feat_mask[self.item_feat.to(torch.int64)]
-        keep_feat = feat_mask[self.feat.to(torch.int64)]
-        item_start, item_end = self.item_start[keep_items], self.item_end[keep_items]
-        item_feat = self.item_feat[keep_items]
-        feat = self.feat[keep_feat]
-        nitems = self.feat_nitems[keep_feat]
-        item0 = torch.zeros_like(nitems, dtype=torch.int64)
-        if nitems.numel():
-            item0[1:] = torch.cumsum(nitems.to(torch.int64), 0)[:-1]
-        blk = self.item_blk[keep_items] if self.item_blk is not None else None
-        return BinGroup(self.bt, item_start, item_end, item_feat, feat, item0, nitems, blk)
+    def subset(self, feat_mask: torch.Tensor) -> "ItemGroup":
+        """Items with at least one feature in ``feat_mask`` (RF per-level feature union)."""
+        cs = torch.zeros(feat_mask.numel() + 1, dtype=torch.int64, device=feat_mask.device)
+        torch.cumsum(feat_mask.to(torch.int64), 0, out=cs[1:])
+        f0 = self.item_f0.to(torch.int64)
+        nf = (self.item_meta.to(torch.int64) >> 8) & 0xFF
+        keep = (cs[f0 + nf] - cs[f0]) > 0
+        blk = self.item_blk[keep] if self.item_blk is not None else None
+        return ItemGroup(self.bt, self.item_start[keep], self.item_end[keep], self.item_f0[keep],
+                         self.item_meta[keep], blk)
 
     @property
     def num_items(self) -> int:
         return int(self.item_start.numel())
 
     def wave_order(self) -> torch.Tensor:
-        """Item of every wave slot of the histogram / entry-statistics launches (-1: idle)."""
+        """Item of every wave slot of the histogram launches (-1: idle)."""
         if self._order is None:
             self._order = wave_order(self.item_blk, self.num_items, self.item_start.device)
         return self._order
@@ -115,32 +121,28 @@ class Quantized:
     colptr: torch.Tensor         # int64 [Fa+1]
     csc_row: torch.Tensor        # int32 [nnz] (view; CSC_PAD readable entries follow)
     csc_bin: torch.Tensor        # uint8 [nnz] (view; CSC_PAD readable entries follow)
+    kbase: torch.Tensor = None   # int32 [Fa] key base of each feature in its packed work item
     groups: list = field(default_factory=list)
-    _all_items: Optional[tuple] = None
-
-    def all_items(self) -> tuple:
-        """(item_start, item_end, wave_order) over the items of every group: one XCD-ordered launch
-        for per-entry work that does not depend on the tile shape (entry statistics)."""
-        if self._all_items is None:
-            dev = self.csc_row.device
-            gs = self.groups
-            if not gs:
-                z = torch.zeros(0, dtype=torch.int64, device=dev)
-                self._all_items = (z, z, wave_order(None, 0, dev))
-            else:
-                st = torch.cat([g.item_start for g in gs])
-                en = torch.cat([g.item_end for g in gs])
-                blk = torch.cat([g.item_blk if g.item_blk is not None else
-                                 torch.full((g.num_items,), -1, dtype=torch.int32, device=dev) for g in gs])
-                self._all_items = (st, en, wave_order(blk, int(st.numel()), dev))
-        return self._all_items
+    h_row: torch.Tensor = None   # int32: histogram CSC (non-dense features, super-block-major)
+    h_key: torch.Tensor = None   # uint8: kbase[f] + bin
+    n_super: int = 1             # row super-blocks of the histogram CSC
+    # dense path for high-density features (K-10 dense variant): dense[d][row] = bin of feature
+    # hot[d] (its zero bin when absent), rows padded to n_pad (multiple of 64)
+    hot: np.ndarray = None       # int64 [Fh] Fa indices
+    hot_bt: np.ndarray = None    # int64 [Fh] MFMA row tiles (16 bins each) of each hot feature
+    dense: torch.Tensor = None   # uint8 [Fh, n_pad]
     boff_host: np.ndarray = None
     zbin_host: np.ndarray = None
     fid_host: np.ndarray = None
+    kbase_host: np.ndarray = None
 
     @property
     def Fa(self) -> int:  # noqa: N802
         return int(self.nbins.numel())
+
+    @property
+    def n_pad(self) -> int:
+        return (self.n_rows + 63) // 64 * 64
 
     @property
     def TB(self) -> int:  # noqa: N802
@@ -152,6 +154,11 @@ class Quantized:
 
     def threshold(self, fid: int, b: int) -> float:
         return float(self.thresholds[int(self.boff_host[fid]) + int(b)])
+
+    def bins_of(self, fid: int) -> torch.Tensor:
+        """Bins of the entries of feature ``fid`` (feature-major CSC order)."""
+        a, b = int(self.colptr[fid]), int(self.colptr[fid + 1])
+        return self.csc_bin[a:b]
 
 
 def _ordered_f32_bits(v: torch.Tensor) -> torch.Tensor:
@@ -169,12 +176,12 @@ def _decode_f32_bits(k: torch.Tensor) -> torch.Tensor:
 
 def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
              all_reduce_max: Optional[Callable] = None, all_gather: Optional[Callable] = None,
-             chunk: int = CHUNK, row_block: int = None, split_min: int = None) -> Quantized:
+             chunk: int = CHUNK, super_rows: int = None, hot_density: float = None) -> Quantized:
     """Bin a ``VectorColumn`` and build the CSC. ``counts``/``scale`` select the count path
     (per-entry integer counts and per-feature positive scale); integral non-negative values
     take it automatically with scale 1."""
-    if max_bins < 2 or max_bins > 64:
-        raise ValueError("max_bins must be in [2, 64] (bins are held in one or two 32-row MFMA tiles)")
+    if max_bins < 2 or max_bins > 256:
+        raise ValueError("max_bins must be in [2, 256] (bins are one byte)")
     indptr, idx, val = vc.csr()
     dev = indptr.device
     N = int(indptr.numel() - 1)
@@ -187,9 +194,8 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
         scale = torch.ones(F, dtype=torch.float64, device=dev)
     if counts is not None and F < (1 << 31):
         Q = _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_max)
-        with tracing.span("q.groups"):
-            Q.groups = _make_groups(Q.colptr, Q.nbins, chunk, Q.csc_row, N, row_block or ROW_BLOCK,
-                                    split_min or SPLIT_MIN)
+        with tracing.span("q.items"):
+            _finish_items(Q, chunk, super_rows or SUPER_ROWS, HOT_DENSITY if hot_density is None else hot_density)
         return Q
     with tracing.span("q.rows"):
         row = torch.repeat_interleave(torch.arange(N, device=dev, dtype=torch.int32), (indptr[1:] - indptr[:-1]),
@@ -230,8 +236,8 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
     Q.boff_host = boff.cpu().numpy()
     Q.zbin_host = Q.zbin.cpu().numpy()
     Q.fid_host = fid_orig.cpu().numpy()
-    with tracing.span("q.groups"):
-        Q.groups = _make_groups(colptr, nbins, chunk, csc_row, N, row_block or ROW_BLOCK, split_min or SPLIT_MIN)
+    with tracing.span("q.items"):
+        _finish_items(Q, chunk, super_rows or SUPER_ROWS, HOT_DENSITY if hot_density is None else hot_density)
     return Q
 
 
@@ -391,76 +397,158 @@ def _generic_path(idx, val, F, max_bins, all_gather):
     return remap, nbins, zb.to(torch.int32), thresholds, eb, full_keep
 
 
-ROW_BLOCK = int(os.environ.get("FDX_ROW_BLOCK", 1 << 17))   # rows per XCD row block: 1 B slot + 8 B statistics per row ~ 1.1 MB
-SPLIT_MIN = int(os.environ.get("FDX_SPLIT_MIN", 1 << 13))   # columns with fewer entries stay whole (their gathers are few)
+HOT_DENSITY = float(os.environ.get("FDX_HOT_DENSITY", 0.1))  # dense path for features in >= this fraction of rows
 
 
-def _segments(colptr: torch.Tensor, csc_row: torch.Tensor, n_rows: int, row_block: int = ROW_BLOCK,
-              split_min: int = SPLIT_MIN):
-    """(start, end, feature, row block) of every column segment: columns with >= SPLIT_MIN entries
-    are cut where the row block changes (rows are sorted inside a column, so a block's entries are
-    contiguous); smaller columns are one segment with block -1."""
-    dev = colptr.device
-    Fa = colptr.numel() - 1
-    n = colptr[1:] - colptr[:-1]
-    nonempty = torch.nonzero(n > 0).flatten()
-    starts = colptr[:-1][nonempty]
-    feats = nonempty
-    nblk = (n_rows + row_block - 1) // row_block
-    split_cols = torch.nonzero(n >= split_min).flatten().to(torch.int32) if nblk > 1 else None
-    if split_cols is not None and split_cols.numel():
-        from ..ops import native
+def _pow2_at_least(x: np.ndarray, lo: int = 1) -> np.ndarray:
+    out = np.full(x.shape, lo, dtype=np.int64)
+    while True:
+        small = out < x
+        if not small.any():
+            return out
+        out[small] *= 2
 
-        S = int(split_cols.numel())
-        bounds = torch.empty((S, nblk + 1), dtype=torch.int64, device=dev)
-        native.lib().block_bounds(csc_row, colptr, split_cols, int(nblk), int(row_block), bounds)
-        bounds[:, -1] = colptr[split_cols.to(torch.int64) + 1]
-        b_start, b_end = bounds[:, :-1].reshape(-1), bounds[:, 1:].reshape(-1)
-        b_feat = split_cols.to(torch.int64).repeat_interleave(nblk)
-        b_blk = torch.arange(nblk, device=dev, dtype=torch.int64).repeat(S)
-        ne = b_end > b_start
-        unsplit = (n > 0) & (n < split_min)
-        u_feat = torch.nonzero(unsplit).flatten()
-        starts = torch.cat([colptr[:-1][u_feat], b_start[ne]])
-        feats = torch.cat([u_feat, b_feat[ne]])
-        seg_blk = torch.cat([torch.full_like(u_feat, -1), b_blk[ne]])
-        starts, o = torch.sort(starts, stable=True)
-        feats, seg_blk = feats[o], seg_blk[o]
+
+def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
+    """Column-major dense bins of the hot features (zero bin for rows absent from a column)."""
+    Q.hot = hot.astype(np.int64)
+    nb = Q.nbins.cpu().numpy()[Q.hot]
+    Q.hot_bt = np.where(nb <= 16, 1, np.where(nb <= 32, 2, 4)).astype(np.int64)
+    if not hot.size:
+        Q.dense = None
+        return
+    zb = Q.zbin.cpu().numpy()[Q.hot]
+    dense = torch.empty((hot.size, Q.n_pad), dtype=torch.uint8, device=Q.device)
+    colptr = Q.colptr.cpu().numpy()
+    for d, f in enumerate(Q.hot.tolist()):
+        dense[d].fill_(int(zb[d]))
+        a, b = int(colptr[f]), int(colptr[f + 1])
+        dense[d].index_copy_(0, Q.csc_row[a:b].to(torch.int64), Q.csc_bin[a:b])
+    Q.dense = dense
+
+
+SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
+
+
+def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS, hot_density: float = HOT_DENSITY) \
+        -> None:
+    """Dense block, histogram CSC and work items (see the module docstring).
+
+    * hot: features in >= ``hot_density`` of the rows with <= 64 bins -> dense block;
+    * packed: consecutive features with <= 16 bins and few entries (<= ``chunk`` per super-block on
+      average) share one <= 64-key item per super-block (stride = the largest pow2 bin count);
+    * single: every other feature, per super-block, in chunks of <= ``chunk`` entries; features
+      with > 64 bins get one item per 64-key window."""
+    from ..ops import native
+
+    C = native.lib()
+    dev = Q.device
+    colptr = Q.colptr.cpu().numpy().astype(np.int64)
+    n = np.diff(colptr)
+    nb = Q.nbins.cpu().numpy().astype(np.int64)
+    Fa = int(nb.size)
+    hot = (n >= hot_density * max(Q.n_rows, 1)) & (nb <= 64) & (n > 0) if hot_density > 0 else np.zeros(Fa, bool)
+    _build_dense(Q, np.nonzero(hot)[0])
+    cols = np.nonzero(~hot & (n > 0))[0]
+    nsb = max(1, (Q.n_rows + super_rows - 1) // super_rows)
+    sb_rows = (Q.n_rows + nsb - 1) // nsb if Q.n_rows else 1
+    # --- per (super-block, feature) segments of the feature-major CSC and their new offsets
+    S = int(cols.size)
+    if S:
+        cols_t = torch.from_numpy(cols.astype(np.int32)).to(dev)
+        bounds = torch.empty((S, nsb + 1), dtype=torch.int64, device=dev)
+        C.block_bounds(Q.csc_row, Q.colptr, cols_t, int(nsb), int(sb_rows), bounds)
+        bounds[:, -1] = Q.colptr[cols_t.to(torch.int64) + 1]
+        seg_src = bounds[:, :-1].t().contiguous()                    # [nsb, S]
+        seg_len = (bounds[:, 1:] - bounds[:, :-1]).t().contiguous()
+        flat = seg_len.reshape(-1)
+        seg_dst = torch.cumsum(flat, 0) - flat
+        total = int(flat.sum())
+        h_row = torch.zeros(total + CSC_PAD, dtype=torch.int32, device=dev)
+        h_key = torch.full((total + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
+        C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total])
+        hptr = np.zeros((nsb, S + 1), dtype=np.int64)                  # [sb][i] start of cols[i] in super-block sb
+        dst_host = seg_dst.cpu().numpy().reshape(nsb, S)
+        hptr[:, :S] = dst_host
+        hptr[:, S] = np.append(dst_host[1:, 0], total) if nsb > 1 else total
+        seg_n = seg_len.cpu().numpy()                                  # [nsb, S]
     else:
-        seg_blk = torch.full_like(starts, -1)
-    ends = colptr[feats + 1]
-    if starts.numel() > 1:
-        nxt = starts[1:]
-        same = feats[1:] == feats[:-1]
-        ends = ends.clone()
-        ends[:-1] = torch.where(same, nxt, ends[:-1])
-    return starts, ends, feats, seg_blk
-
-
-def _make_groups(colptr: torch.Tensor, nbins: torch.Tensor, chunk: int, csc_row: Optional[torch.Tensor] = None,
-                 n_rows: int = 0, row_block: int = ROW_BLOCK, split_min: int = SPLIT_MIN) -> list:
-    dev = colptr.device
-    if csc_row is None:
-        csc_row = torch.zeros(0, dtype=torch.int32, device=dev)
-    s0, e0, f0, b0 = _segments(colptr, csc_row, n_rows, row_block, split_min)
-    groups = []
-    for bt in (0, 1, 2):    # 0: <= 16 bins (16x16x32 MFMA tile), 1: <= 32, 2: <= 64 bins
-        lo, hi = ((0, 16), (17, 32), (33, 64))[bt]
-        sel = (nbins[f0] >= lo) & (nbins[f0] <= hi)
-        if not bool(sel.any()):
+        h_row = torch.zeros(CSC_PAD, dtype=torch.int32, device=dev)
+        h_key = torch.full((CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
+        hptr = np.zeros((nsb, 1), dtype=np.int64)
+        seg_n = np.zeros((nsb, 0), dtype=np.int64)
+    total = int(hptr[-1, -1]) if S else 0
+    # --- packing (global: the same kbase in every super-block)
+    ncol = n[cols]
+    packable = (ncol <= chunk * nsb) & (nb[cols] <= 16)
+    stride = _pow2_at_least(nb[cols], 2)
+    kbase = np.zeros(Fa, dtype=np.int64)
+    groups_pk = []   # (i0, i1, sl2)
+    i = 0
+    while i < S:
+        if not packable[i]:
+            i += 1
             continue
-        s, e, f, b = s0[sel], e0[sel], f0[sel], b0[sel]
-        nc = (e - s + chunk - 1) // chunk
-        I = int(nc.sum())
-        seg = torch.repeat_interleave(torch.arange(s.numel(), device=dev), nc, output_size=I)
-        first = torch.cumsum(nc, 0) - nc
-        k = torch.arange(I, device=dev) - first[seg]
-        start = s[seg] + k * chunk
-        end = torch.minimum(start + chunk, e[seg])
-        item_feat = f[seg]
-        feats, nitems = torch.unique_consecutive(item_feat, return_counts=True)
-        item0 = torch.cumsum(nitems, 0) - nitems
-        groups.append(BinGroup(bt, start.contiguous(), end.contiguous(), item_feat.to(torch.int32).contiguous(),
-                               feats.to(torch.int32).contiguous(), item0.contiguous(),
-                               nitems.to(torch.int32).contiguous(), b[seg].to(torch.int32).contiguous()))
-    return groups
+        i0, st_max, ent, k = i, int(stride[i]), 0, 0
+        while i < S and packable[i]:
+            s2 = max(st_max, int(stride[i]))
+            if (k + 1) * s2 > PACK_KEYS or ent + int(ncol[i]) > chunk * nsb:
+                break
+            st_max, ent, k = s2, ent + int(ncol[i]), k + 1
+            i += 1
+        kbase[cols[i0:i0 + k]] = np.arange(k) * st_max
+        groups_pk.append((i0, i0 + k, int(np.log2(st_max))))
+    parts = []   # arrays of (start, end, f0, sl2, nfeat, koff, bt, blk)
+    if groups_pk:
+        gp = np.asarray(groups_pk, dtype=np.int64)
+        i0s, i1s, sl2s = gp[:, 0], gp[:, 1], gp[:, 2]
+        keys = (i1s - i0s) << sl2s
+        bts = np.where(keys <= 16, 1, np.where(keys <= 32, 2, 4))
+        a = hptr[:, i0s]                                   # [nsb, G]: consecutive features are contiguous
+        e = hptr[:, i1s - 1] + seg_n[:, i1s - 1]
+        G = gp.shape[0]
+        rows_ = np.stack([a.reshape(-1), e.reshape(-1), np.tile(cols[i0s], nsb), np.tile(sl2s, nsb),
+                          np.tile(i1s - i0s, nsb), np.zeros(nsb * G, np.int64), np.tile(bts, nsb),
+                          np.repeat(np.arange(nsb), G)], 1)
+        parts.append(rows_[rows_[:, 1] > rows_[:, 0]])
+    single = np.nonzero(~packable)[0]
+    if single.size:
+        a0 = hptr[:, single].reshape(-1)                   # [nsb * len(single)]
+        ln = seg_n[:, single].reshape(-1)
+        fs = np.tile(cols[single], nsb)
+        bk = np.repeat(np.arange(nsb), single.size)
+        nc = (ln + chunk - 1) // chunk
+        seg = np.repeat(np.arange(ln.size), nc)
+        k = np.arange(seg.size) - np.repeat(np.cumsum(nc) - nc, nc)
+        st = a0[seg] + k * chunk
+        en = np.minimum(st + chunk, a0[seg] + ln[seg])
+        f_, b_ = fs[seg], bk[seg]
+        for w in range(int((nb[f_].max() + 63) // 64) if f_.size else 0):
+            sel = nb[f_] > 64 * w
+            nbw = np.minimum(nb[f_[sel]] - 64 * w, 64)
+            btw = np.where(nbw <= 16, 1, np.where(nbw <= 32, 2, 4))
+            m = int(sel.sum())
+            parts.append(np.stack([st[sel], en[sel], f_[sel], np.full(m, 8), np.ones(m, np.int64),
+                                   np.full(m, 64 * w), btw, b_[sel]], 1))
+    items = np.concatenate(parts) if parts else np.zeros((0, 8), np.int64)
+    # --- keys of the histogram CSC: kbase + bin
+    if S and kbase.any():
+        lens = torch.from_numpy(seg_n.reshape(-1)).to(dev)
+        kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev)
+        h_key[:total].add_(torch.repeat_interleave(kb, lens, output_size=total))
+    groups = []
+    arr = items.astype(np.int64)
+    for bt in (1, 2, 4):
+        g = arr[arr[:, 6] == bt]
+        if not g.shape[0]:
+            continue
+        g = g[np.lexsort((g[:, 0],))]
+        meta = g[:, 3] | (g[:, 4] << 8) | (g[:, 5] << 16)
+        t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).astype(dt)).to(dev)   # noqa: E731
+        groups.append(ItemGroup(bt, t(g[:, 0], np.int64), t(g[:, 1], np.int64), t(g[:, 2], np.int32),
+                                t(meta, np.int32), t(g[:, 7], np.int32)))
+    Q.groups = groups
+    Q.h_row, Q.h_key = h_row[:total], h_key[:total]
+    Q.n_super = nsb
+    Q.kbase_host = kbase.astype(np.int32)
+    Q.kbase = torch.from_numpy(Q.kbase_host).to(dev)

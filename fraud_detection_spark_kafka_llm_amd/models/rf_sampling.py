@@ -1,11 +1,14 @@
 """Random-forest per-node feature subsampling (X-10, K-14).
 
-Spark samples ``numFeaturesPerNode`` features without replacement per node (``auto`` = sqrt for
-classification). Here every (tree, node, feature) draws an independent counter-based uniform and
-keeps the feature with probability ``k / numFeatures`` — same expected subset size, no state, and
-identical on every rank and on host/device (``hash_uniform`` in csrc/tree.h). This module mirrors
-that hash in torch to compute, per level, the union of sampled features so histograms are only
-built for features some node can actually split on.
+Spark samples exactly ``numFeaturesPerNode`` of the ``numFeatures`` feature indices without
+replacement per node (``featureSubsetStrategy="auto"`` = ceil(sqrt(F)) for a forest;
+/root/reference/fraud_detection_spark.py:67-74). Here every (tree, node, feature index) has a
+counter-based priority (``feature_priority`` in csrc/tree.h, uniform in [0, 1)), and a node samples
+the k features with the smallest priorities: exactly k, without replacement, no state, identical
+on every rank and on host/device. ``node_thresholds`` finds each node's k-th smallest priority over
+all F indices (the split kernel keeps a feature iff its priority <= the threshold);
+``level_feature_mask`` is the union over the level's nodes, so histograms are only built for
+features some node can actually split on.
 """
 from __future__ import annotations
 
@@ -58,11 +61,28 @@ def features_per_node(strategy: str, num_features: int) -> int:
     return int(math.ceil(v * num_features)) if v <= 1.0 else min(num_features, int(v))
 
 
-def node_feature_mask(Q, params, tree_index: int, nodes: list) -> torch.Tensor:
+def _priorities(seed: int, tree_index: int, node: int, fid: torch.Tensor) -> torch.Tensor:
+    a = _u64(int(seed) ^ 0x5BD1E995)
+    b = _u64(((int(tree_index) & 0xFFFFFFFF) << 32) | (int(node) & 0xFFFFFFFF))
+    return hash_uniform(a, b, fid)
+
+
+def node_thresholds(num_features: int, seed: int, tree_index: int, nodes: list, k: int, dev) -> torch.Tensor:
+    """[len(nodes)] float64: the k-th smallest priority of each node over feature indices 0..F-1
+    (1.0 when k >= F: every feature)."""
+    out = torch.ones(len(nodes), dtype=torch.float64, device=dev)
+    if k >= num_features:
+        return out
+    fid = torch.arange(num_features, dtype=torch.int64, device=dev)
+    for i, n in enumerate(nodes):
+        out[i] = torch.kthvalue(_priorities(seed, tree_index, n, fid), k).values
+    return out
+
+
+def level_feature_mask(Q, seed: int, tree_index: int, nodes: list, thr: torch.Tensor) -> torch.Tensor:
+    """[Fa] bool: active features sampled by at least one of ``nodes``."""
     fid = Q.fid_orig
     mask = torch.zeros(fid.numel(), dtype=torch.bool, device=fid.device)
-    a = _u64(int(params.seed) ^ 0x5BD1E995)
-    for n in nodes:
-        b = _u64((int(tree_index) << 32) | (int(n) & 0xFFFFFFFF))
-        mask |= hash_uniform(a, b, fid) < params.feat_prob
+    for i, n in enumerate(nodes):
+        mask |= _priorities(seed, tree_index, n, fid) <= thr[i]
     return mask

@@ -4,7 +4,8 @@ Spark semantics reproduced: gini (or entropy) impurity, maxBins=
 thresholds, minInstancesPerNode / minInfoGain, a node splits only if its best gain > 0, children
 with zero impurity become leaves, and ``toNode(prune=true)`` merges sibling leaves with the same
 prediction. RandomForest adds Poisson(1) bootstrap row weights (counter-based, regenerated per
-tree, never stored) and per-node feature subsampling (``featureSubsetStrategy="auto"`` = sqrt).
+tree, never stored) and per-node sampling of exactly k features without replacement
+(``featureSubsetStrategy="auto"`` = ceil(sqrt(F)), models/rf_sampling.py).
 Reference configs: /root/reference/fraud_detection_spark.py:59-74.
 """
 from __future__ import annotations
@@ -85,8 +86,9 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
         strategy = "all" if num_trees == 1 else "sqrt"
     k = features_per_node(strategy, F)
     params = GrowParams(max_depth=max_depth, mode=2 if impurity == "entropy" else 1, min_child=float(min_instances),
-                        min_gain=float(min_info_gain), feat_prob=min(1.0, k / F), seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
-    ws = Workspace(Q, 2 ** max_depth)
+                        min_gain=float(min_info_gain), feat_k=0 if k >= F else int(k),
+                        seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
+    ws = Workspace(Q)
     trees = []
     for t in range(num_trees):
         with tracing.span("forest.tree", tree=t):

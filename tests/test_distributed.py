@@ -21,7 +21,7 @@ def _vc(dense):
     return VectorColumn(dense.shape[1], dense=torch.from_numpy(dense))
 
 
-def _train(rank, world, kind, deterministic=False):
+def _train(rank, world, kind):
     from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
     from fraud_detection_spark_kafka_llm_amd.models.lr import train_logistic_regression
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
@@ -31,7 +31,7 @@ def _train(rank, world, kind, deterministic=False):
     lo, hi = shard_range(len(y), rank, world)
     vc, yy = _vc(dense[lo:hi]), torch.from_numpy(y[lo:hi])
     if kind == "gbdt":
-        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=6, max_depth=4, deterministic=deterministic), device="cpu")
+        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=6, max_depth=4), device="cpu")
         return [(t.feature.tolist(), t.stats[:, 0].tolist()) for t in r.trees], r.base_margin
     if kind == "rf":
         r = fit_forest(vc, yy, num_trees=3, max_depth=4, bootstrap=False, feature_subset="sqrt", seed=5, device="cpu")
@@ -68,11 +68,12 @@ def test_three_ranks_feature_sharded_split_equals_single_process():
         np.testing.assert_allclose(np.asarray(v1), np.asarray(v2), rtol=1e-9)
 
 
-def test_deterministic_gbdt_is_bitwise_identical_across_world_sizes():
-    """Fixed-point g/h: DP=1, DP=2 and DP=3 produce bit-identical trees and leaf values."""
-    single = _train(0, 1, "gbdt", True)
+def test_gbdt_is_bitwise_identical_across_world_sizes():
+    """Exact int64 histograms of quantised g/h: DP=1, DP=2 and DP=3 produce bit-identical trees and
+    leaf values."""
+    single = _train(0, 1, "gbdt")
     for world in (2, 3):
-        outs = spawn(_train, world, "gbdt", True, backend="gloo")
+        outs = spawn(_train, world, "gbdt", backend="gloo")
         assert all(o == outs[0] for o in outs)
         assert outs[0] == single, f"world {world} differs from single process"
 
