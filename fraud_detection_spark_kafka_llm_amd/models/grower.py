@@ -20,6 +20,7 @@ exact integers; leaf values / class counts are scaled by 2^-k only when the tree
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -34,6 +35,9 @@ from .quantize import Quantized
 NEG_INF = float("-inf")
 MAX_CT = 8                      # column tiles per pass (csrc/tree_kernels.hip launch_hist)
 DENSE_RANGE_ROWS = 32768        # rows per wave of the dense hot-feature histogram kernel
+# levels 0..DENSE_MAX_DEPTH build the hot features' histograms with the dense kernel (every row
+# streamed, slot-masked); deeper levels use their CSC items (only live entries multiplied)
+DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
 
 
 @dataclass
@@ -353,14 +357,15 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         node_slot = up[h_ns] if h_ns is not None else None
         # --- histograms, up to `pass_slots` node slots per pass
         with tracing.span("tree.hist"):
-            sel_groups = Q.groups
+            use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH
+            sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
             hot_keep = None
             if feat_thr is not None:
                 from .rf_sampling import level_feature_mask
 
                 mask = level_feature_mask(Q, params.seed, tree_index, open_nodes, feat_thr)
-                sel_groups = [grp.subset(mask) for grp in Q.groups]
-                if Q.dense is not None:
+                sel_groups = [grp.subset(mask) for grp in sel_groups]
+                if use_dense:
                     hot_keep = mask[torch.from_numpy(Q.hot).to(dev)].cpu().numpy()
             for s0, cnt, h_s2n in passes:
                 slot8 = None
@@ -374,7 +379,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                     C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
                                       Q.h_row, Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, up[h_s2n],
                                       hist_target, TB, grp.bt, ct, np_)
-                if Q.dense is not None:
+                if use_dense:
                     for bt in (1, 2, 4):
                         gfid, gden = ws.dense_groups(bt, C.tree_dense_fg(bt, ct if d > 0 else 1), hot_keep)
                         if gfid.numel():

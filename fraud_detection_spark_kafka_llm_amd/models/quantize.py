@@ -15,8 +15,9 @@ In both paths the thresholds are value-space midpoints, so the same tree scores 
 values with either ``x <= t`` (Spark) or ``x < t`` (XGBoost) semantics.
 
 Histogram layout (``_finish_items``): features present in >= HOT_DENSITY of the rows go to a
-dense column-major bin block (their row state is streamed, not gathered). The other features'
-entries are copied into a histogram CSC laid out row-super-block-major (super-block = a range of
+dense column-major bin block (their row state is streamed, not gathered; used for the shallow
+levels where most rows are live). All features' entries are copied into a histogram CSC laid out
+row-super-block-major (super-block = a range of
 rows whose 1-byte slot and 8-byte digit slices fit one XCD's 4 MB L2; the XCD-ordered item
 placement keeps each XCD inside one super-block at a time), as (row, key) with key = kbase + bin.
 One wave of the i8 MFMA histogram kernel per work item: a chunk of one feature inside one
@@ -123,7 +124,8 @@ class Quantized:
     csc_bin: torch.Tensor        # uint8 [nnz] (view; CSC_PAD readable entries follow)
     kbase: torch.Tensor = None   # int32 [Fa] key base of each feature in its packed work item
     groups: list = field(default_factory=list)
-    h_row: torch.Tensor = None   # int32: histogram CSC (non-dense features, super-block-major)
+    hot_groups: list = field(default_factory=list)   # CSC items of the dense-block features
+    h_row: torch.Tensor = None   # int32: histogram CSC (all features, super-block-major)
     h_key: torch.Tensor = None   # uint8: kbase[f] + bin
     n_super: int = 1             # row super-blocks of the histogram CSC
     # dense path for high-density features (K-10 dense variant): dense[d][row] = bin of feature
@@ -449,7 +451,9 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     Fa = int(nb.size)
     hot = (n >= hot_density * max(Q.n_rows, 1)) & (nb <= 64) & (n > 0) if hot_density > 0 else np.zeros(Fa, bool)
     _build_dense(Q, np.nonzero(hot)[0])
-    cols = np.nonzero(~hot & (n > 0))[0]
+    # hot features stay in the histogram CSC too (deep levels use it: only their live entries are
+    # multiplied there, while the dense kernel masks every row); they are never packed
+    cols = np.nonzero(n > 0)[0]
     nsb = max(1, (Q.n_rows + super_rows - 1) // super_rows)
     sb_rows = (Q.n_rows + nsb - 1) // nsb if Q.n_rows else 1
     # --- per (super-block, feature) segments of the feature-major CSC and their new offsets
@@ -480,7 +484,7 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     total = int(hptr[-1, -1]) if S else 0
     # --- packing (global: the same kbase in every super-block)
     ncol = n[cols]
-    packable = (ncol <= chunk * nsb) & (nb[cols] <= 16)
+    packable = (ncol <= chunk * nsb) & (nb[cols] <= 16) & ~hot[cols]
     stride = _pow2_at_least(nb[cols], 2)
     kbase = np.zeros(Fa, dtype=np.int64)
     groups_pk = []   # (i0, i1, sl2)
@@ -536,18 +540,24 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
         lens = torch.from_numpy(seg_n.reshape(-1)).to(dev)
         kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev)
         h_key[:total].add_(torch.repeat_interleave(kb, lens, output_size=total))
-    groups = []
     arr = items.astype(np.int64)
-    for bt in (1, 2, 4):
-        g = arr[arr[:, 6] == bt]
-        if not g.shape[0]:
-            continue
-        g = g[np.lexsort((g[:, 0],))]
-        meta = g[:, 3] | (g[:, 4] << 8) | (g[:, 5] << 16)
-        t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).astype(dt)).to(dev)   # noqa: E731
-        groups.append(ItemGroup(bt, t(g[:, 0], np.int64), t(g[:, 1], np.int64), t(g[:, 2], np.int32),
-                                t(meta, np.int32), t(g[:, 7], np.int32)))
-    Q.groups = groups
+    is_hot = hot[arr[:, 2]] & (arr[:, 4] == 1) if arr.shape[0] else np.zeros(0, bool)
+    t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).astype(dt)).to(dev)   # noqa: E731
+
+    def make(sel):
+        out = []
+        for bt in (1, 2, 4):
+            g = arr[sel & (arr[:, 6] == bt)]
+            if not g.shape[0]:
+                continue
+            g = g[np.lexsort((g[:, 0],))]
+            meta = g[:, 3] | (g[:, 4] << 8) | (g[:, 5] << 16)
+            out.append(ItemGroup(bt, t(g[:, 0], np.int64), t(g[:, 1], np.int64), t(g[:, 2], np.int32),
+                                 t(meta, np.int32), t(g[:, 7], np.int32)))
+        return out
+
+    Q.groups = make(~is_hot)
+    Q.hot_groups = make(is_hot)
     Q.h_row, Q.h_key = h_row[:total], h_key[:total]
     Q.n_super = nsb
     Q.kbase_host = kbase.astype(np.int32)

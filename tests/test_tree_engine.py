@@ -255,30 +255,36 @@ def test_work_items_cover_histogram_csc_once_and_wave_order_is_xcd_grouped():
     Qh = quantize(vc_from_dense(dense.astype(np.float64)), max_bins=8, chunk=100, super_rows=700, hot_density=0.3)
     hot = set(Qh.hot.tolist())
     assert hot == {f for f in range(Qh.Fa) if (dense[:, Qh.fid_host[f]] > 0).mean() >= 0.3}
-    assert Qh.h_row.numel() == int(Qh.colptr[-1]) - sum(int(Qh.colptr[f + 1] - Qh.colptr[f]) for f in hot)
+    assert Qh.h_row.numel() == int(Qh.colptr[-1])      # hot columns stay in the CSC (deep levels)
+    for grp in Qh.groups:
+        assert not any(int(f) in hot for f in grp.item_f0.numpy())
+    assert {int(f) for grp in Qh.hot_groups for f in grp.item_f0.numpy()} == hot
     for d, f in enumerate(Qh.hot.tolist()):
         np.testing.assert_array_equal(Qh.dense[d, :n].numpy(), np.minimum(dense[:, Qh.fid_host[f]], 7))
     assert wave_order(None, 0, torch.device("cpu")).tolist() == [-1] * 4
 
 
 def test_dense_and_csc_paths_give_identical_trees():
-    """Hot features through the dense column-major kernel or through CSC work items: the same
-    exact histograms, so the same DT / RF (feature-sampled, no sibling subtraction) / GBDT trees."""
+    """Hot features through the dense column-major kernel (at every level, at the shallow levels
+    only) or through CSC work items: the same exact histograms, so the same DT / RF
+    (feature-sampled, no sibling subtraction) / GBDT trees."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower as gr
     from fraud_detection_spark_kafka_llm_amd.models import quantize as qz
 
     dense, y = random_counts_matrix(500, 12, 0.35, 3)
     out = {}
-    for hd in (0.0, 0.1):
+    for hd, depth in ((0.0, 9), (0.1, 9), (0.1, 1)):
         old, qz.HOT_DENSITY = qz.HOT_DENSITY, hd
+        old_d, gr.DENSE_MAX_DEPTH = gr.DENSE_MAX_DEPTH, depth
         try:
             vc, yy = vc_from_dense(dense), torch.from_numpy(y)
             dt = fit_forest(vc, yy, num_trees=1, max_depth=4, prune=False)
             rf = fit_forest(vc, yy, num_trees=3, max_depth=4, bootstrap=True, feature_subset="sqrt", seed=7)
             gb = fit_gbdt(vc, yy, GBDTParams(n_estimators=3, max_depth=3))
-            out[hd] = [(t.feature.tolist(), t.stats.tolist()) for t in dt.trees + rf.trees + gb.trees]
+            out[(hd, depth)] = [(t.feature.tolist(), t.stats.tolist()) for t in dt.trees + rf.trees + gb.trees]
         finally:
-            qz.HOT_DENSITY = old
-    assert out[0.0] == out[0.1]
+            qz.HOT_DENSITY, gr.DENSE_MAX_DEPTH = old, old_d
+    assert out[(0.0, 9)] == out[(0.1, 9)] == out[(0.1, 1)]
 
 
 def test_host_histogram_is_exact():
