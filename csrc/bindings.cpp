@@ -464,6 +464,7 @@ int64_t encode_records(const Tensor& pred, const Tensor& conf, const Tensor& tex
   FDX_CHECK(out.scalar_type() == at::kByte && out_off.scalar_type() == at::kLong && out_off.numel() >= n + 1, "out u8 / out_off i64");
   FDX_CHECK(status.scalar_type() == at::kInt && status.numel() >= n, "status i32 [n]");
   if (skip) FDX_CHECK(skip->scalar_type() == at::kInt && skip->numel() >= n && skip->is_contiguous(), "skip i32 [n]");
+  pybind11::gil_scoped_release nogil;   // partition reader / output threads run this concurrently
   return fdx::encode_records(pred.data_ptr<double>(), conf.data_ptr<double>(), text.data_ptr<uint8_t>(),
                              off.data_ptr<int64_t>(), skip ? skip->data_ptr<int32_t>() : nullptr, n,
                              out.data_ptr<uint8_t>(), out.numel(), out_off.data_ptr<int64_t>(),
@@ -479,6 +480,7 @@ int64_t extract_json_field(const Tensor& in, const Tensor& in_off, const std::st
             "dtypes u8/i64/u8/i64/i32");
   const int64_t n = in_off.numel() - 1;
   FDX_CHECK(n >= 0 && out_off.numel() >= n + 1 && status.numel() >= n, "offset/status sizes");
+  pybind11::gil_scoped_release nogil;
   return fdx::extract_json_field(in.data_ptr<uint8_t>(), in_off.data_ptr<int64_t>(), n,
                                  reinterpret_cast<const uint8_t*>(field.data()), (int64_t)field.size(),
                                  out.data_ptr<uint8_t>(), out.numel(), out_off.data_ptr<int64_t>(),

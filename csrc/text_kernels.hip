@@ -90,6 +90,7 @@ __global__ __launch_bounds__(kWave * WAVES) void featurize_score_kernel(FeatArgs
   const int slot = blockIdx.x * WAVES + wid;
   if (slot >= (a.doc_list ? a.n_list : a.num_docs)) return;
   const int d = a.doc_list ? a.doc_list[slot] : slot;
+  if (d < 0 || d >= a.num_docs) return;      // a stale / foreign doc list never indexes out of range
 
   uint8_t* s_clean = s_clean_all[wid];
   uint32_t* s_tok = s_tok_all[wid];

@@ -1,20 +1,30 @@
 """In-memory Kafka broker with the confluent_kafka Consumer/Producer surface (test double, X-20).
 
 Implements what the reference and the streaming engine use: topics with N partitions, keyed
-partitioning (murmur-free: stable hash of the key), consumer groups with committed offsets,
-``auto.offset.reset`` earliest/latest, ``enable.auto.commit``, ``subscribe / poll / consume /
-commit / committed / close``, ``produce(topic, value, key, on_delivery) / poll / flush``,
-``Message.key/value/topic/partition/offset/error``. Fault injection: ``broker.inject_error``
-makes the next poll of a topic return an error message (the reference kills its loop on these,
-app_ui.py:200-201; the engine skips and logs them).
+partitioning (stable crc32 of the key), consumer groups with committed offsets,
+``auto.offset.reset`` earliest/latest, ``enable.auto.commit``, ``subscribe / assign / poll /
+consume / commit / committed / close``, ``produce(topic, value, key, on_delivery) / poll / flush``,
+``Message.key/value/topic/partition/offset/error``, ``TopicPartition``. Fault injection:
+``broker.inject_error`` makes the next poll of a topic return an error message (the reference
+kills its loop on these, app_ui.py:200-201; the engine skips and logs them).
+
+Partitions store columnar record batches (keys / values as one byte buffer + offsets each, like
+Kafka's own record batches), so the streaming engine can move a whole micro-batch per call
+(``Consumer.consume_batches``, ``Producer.produce_records``) without a Python object per message;
+``poll``/``consume`` materialise per-message ``Message`` objects for the reference-style API.
+``Consumer.commit`` type-checks like confluent_kafka: ``message=`` must be a ``Message``; offsets go
+through ``offsets=[TopicPartition(topic, partition, next_offset)]``.
 """
 from __future__ import annotations
 
+import bisect
 import threading
 import time
 import zlib
 from collections import defaultdict
 from typing import Callable, Optional
+
+import numpy as np
 
 
 class KafkaError:
@@ -41,13 +51,29 @@ class KafkaException(Exception):
     pass
 
 
+class TopicPartition:
+    """confluent_kafka.TopicPartition: (topic, partition, offset)."""
+
+    def __init__(self, topic: str, partition: int = -1, offset: int = -1001):
+        self.topic, self.partition, self.offset = topic, int(partition), int(offset)
+
+    def __repr__(self) -> str:
+        return f"TopicPartition({self.topic!r}, {self.partition}, {self.offset})"
+
+    def __eq__(self, o) -> bool:
+        return (self.topic, self.partition, self.offset) == (o.topic, o.partition, o.offset)
+
+    def __hash__(self) -> int:
+        return hash((self.topic, self.partition, self.offset))
+
+
 class Message:
     __slots__ = ("_topic", "_partition", "_offset", "_key", "_value", "_error", "_ts")
 
-    def __init__(self, topic, partition, offset, key, value, error=None):
+    def __init__(self, topic, partition, offset, key, value, error=None, ts=None):
         self._topic, self._partition, self._offset = topic, partition, offset
         self._key, self._value, self._error = key, value, error
-        self._ts = time.time()
+        self._ts = time.time() if ts is None else ts
 
     def topic(self):
         return self._topic
@@ -77,6 +103,83 @@ def _b(v) -> Optional[bytes]:
     return v.encode("utf-8") if isinstance(v, str) else bytes(v)
 
 
+def pack(items: list) -> tuple:
+    """bytes-like items (None allowed) -> (uint8 buffer, int64 offsets [n+1], null mask or None)."""
+    null = [v is None for v in items]
+    bs = [b"" if v is None else _b(v) for v in items]
+    off = np.zeros(len(bs) + 1, dtype=np.int64)
+    np.cumsum(np.fromiter((len(v) for v in bs), dtype=np.int64, count=len(bs)), out=off[1:])
+    buf = np.frombuffer(b"".join(bs), dtype=np.uint8).copy() if bs else np.zeros(0, np.uint8)
+    return buf, off, (np.asarray(null) if any(null) else None)
+
+
+class RecordBatch:
+    """Columnar records of one partition: keys/values as byte buffers + offsets, consecutive
+    offsets from ``base_offset``, one append timestamp (seconds, ``time.perf_counter`` clock)."""
+    __slots__ = ("topic", "partition", "base_offset", "keys", "key_off", "values", "val_off", "null_keys", "ts")
+
+    def __init__(self, topic, partition, base_offset, keys, key_off, values, val_off, null_keys=None, ts=None):
+        self.topic, self.partition, self.base_offset = topic, partition, base_offset
+        self.keys, self.key_off, self.values, self.val_off = keys, key_off, values, val_off
+        self.null_keys = null_keys
+        self.ts = time.perf_counter() if ts is None else ts
+
+    @property
+    def n(self) -> int:
+        return int(self.val_off.size - 1)
+
+    @property
+    def last_offset(self) -> int:
+        return self.base_offset + self.n - 1
+
+    def slice(self, a: int, b: int) -> "RecordBatch":
+        """Records [a, b) (views of the byte buffers, rebased offsets)."""
+        ko, vo = self.key_off[a:b + 1], self.val_off[a:b + 1]
+        nk = self.null_keys[a:b] if self.null_keys is not None else None
+        return RecordBatch(self.topic, self.partition, self.base_offset + a, self.keys[ko[0]:ko[-1]], ko - ko[0],
+                           self.values[vo[0]:vo[-1]], vo - vo[0], nk, self.ts)
+
+    def key(self, i: int) -> Optional[bytes]:
+        if self.null_keys is not None and self.null_keys[i]:
+            return None
+        return self.keys[self.key_off[i]:self.key_off[i + 1]].tobytes()
+
+    def value(self, i: int) -> bytes:
+        return self.values[self.val_off[i]:self.val_off[i + 1]].tobytes()
+
+    def message(self, i: int) -> Message:
+        return Message(self.topic, self.partition, self.base_offset + i, self.key(i), self.value(i))
+
+
+class _Partition:
+    def __init__(self):
+        self.batches: list = []
+        self.starts: list = []
+        self.size = 0
+
+    def append(self, rb: RecordBatch) -> None:
+        rb.base_offset = self.size
+        self.batches.append(rb)
+        self.starts.append(self.size)
+        self.size += rb.n
+
+    def read(self, pos: int, max_n: int) -> Optional[RecordBatch]:
+        """Records from offset ``pos`` (at most ``max_n``, never across stored batches)."""
+        if pos >= self.size:
+            return None
+        i = bisect.bisect_right(self.starts, pos) - 1
+        rb = self.batches[i]
+        a = pos - rb.base_offset
+        return rb.slice(a, min(rb.n, a + max_n)) if (a or max_n < rb.n) else rb
+
+    def __len__(self) -> int:
+        return self.size
+
+    def __getitem__(self, off: int) -> Message:
+        rb = self.batches[bisect.bisect_right(self.starts, off) - 1]
+        return rb.message(off - rb.base_offset)
+
+
 class Broker:
     def __init__(self):
         self.lock = threading.RLock()
@@ -87,33 +190,61 @@ class Broker:
 
     def create_topic(self, name: str, partitions: int = 3) -> None:
         with self.lock:
-            self.topics.setdefault(name, [[] for _ in range(partitions)])
+            self.topics.setdefault(name, [_Partition() for _ in range(partitions)])
 
     def partitions(self, topic: str) -> int:
         with self.lock:
             self.create_topic(topic)
             return len(self.topics[topic])
 
+    @staticmethod
+    def _route(key, value, nparts: int) -> int:
+        return (zlib.crc32(key) if key else zlib.crc32(value or b"")) % nparts
+
     def append(self, topic: str, key, value, partition: Optional[int] = None) -> Message:
         with self.lock:
             self.create_topic(topic)
             parts = self.topics[topic]
             if partition is None or partition < 0:
-                partition = (zlib.crc32(key) if key else zlib.crc32(value or b"") ^ len(parts[0])) % len(parts)
-            m = Message(topic, partition, len(parts[partition]), key, value)
-            parts[partition].append(m)
+                partition = self._route(key, value, len(parts))
+            kb, ko, nk = pack([key])
+            vb, vo, _ = pack([value])
+            rb = RecordBatch(topic, partition, 0, kb, ko, vb, vo, nk)
+            parts[partition].append(rb)
             self.cond.notify_all()
-            return m
+            return rb.message(0)
 
-    def append_many(self, topic: str, keys: list, values: list) -> None:
-        """Batch append (one lock / one wake-up for the whole batch); same partitioning as append."""
+    def append_records(self, topic: str, partition: int, keys, key_off, values, val_off, null_keys=None,
+                       copy: bool = True) -> RecordBatch:
+        """One columnar batch into one partition (the buffers are copied unless ``copy=False``)."""
         with self.lock:
             self.create_topic(topic)
             parts = self.topics[topic]
-            np_ = len(parts)
-            for key, value in zip(keys, values):
-                partition = (zlib.crc32(key) if key else zlib.crc32(value or b"") ^ len(parts[0])) % np_
-                parts[partition].append(Message(topic, partition, len(parts[partition]), key, value))
+            if partition is None or partition < 0:
+                partition = 0
+            partition %= len(parts)
+            cp = (lambda a: np.array(a, copy=True)) if copy else np.asarray
+            rb = RecordBatch(topic, partition, 0, cp(keys), cp(key_off), cp(values), cp(val_off),
+                             None if null_keys is None else cp(null_keys))
+            parts[partition].append(rb)
+            self.cond.notify_all()
+            return rb
+
+    def append_many(self, topic: str, keys: list, values: list) -> None:
+        """Batch append with keyed partitioning (one columnar batch per partition)."""
+        with self.lock:
+            self.create_topic(topic)
+            np_ = len(self.topics[topic])
+            by: dict = defaultdict(lambda: ([], []))
+            for k, v in zip(keys, values):
+                k, v = _b(k), _b(v)
+                kk, vv = by[self._route(k, v, np_)]
+                kk.append(k)
+                vv.append(v)
+            for p, (kk, vv) in sorted(by.items()):
+                kb, ko, nk = pack(kk)
+                vb, vo, _ = pack(vv)
+                self.topics[topic][p].append(RecordBatch(topic, p, 0, kb, ko, vb, vo, nk))
             self.cond.notify_all()
 
     def inject_error(self, topic: str, count: int = 1) -> None:
@@ -133,7 +264,7 @@ class Broker:
 
     def messages(self, topic: str) -> list:
         with self.lock:
-            return [m for p in self.topics.get(topic, []) for m in p]
+            return [rb.message(i) for p in self.topics.get(topic, []) for rb in p.batches for i in range(rb.n)]
 
 
 _DEFAULT = Broker()
@@ -158,76 +289,127 @@ class Consumer:
         self.closed = False
         self._rr = 0
 
+    def _start(self, t: str, p: int) -> int:
+        c = self.broker.committed[self.group].get((t, p))
+        if c is None:
+            c = 0 if self.reset in ("earliest", "smallest", "beginning") else len(self.broker.topics[t][p])
+        return c
+
     def subscribe(self, topics, on_assign=None, on_revoke=None) -> None:
         self.topics = list(topics)
         with self.broker.lock:
             for t in self.topics:
                 for p in range(self.broker.partitions(t)):
-                    c = self.broker.committed[self.group].get((t, p))
-                    if c is None:
-                        c = 0 if self.reset in ("earliest", "smallest", "beginning") else len(self.broker.topics[t][p])
-                    self.positions[(t, p)] = c
+                    self.positions[(t, p)] = self._start(t, p)
+
+    def assign(self, partitions: list) -> None:
+        """Static assignment (one consumer per partition, as the engine's partition readers use)."""
+        with self.broker.lock:
+            for tp in partitions:
+                self.broker.create_topic(tp.topic)
+                if tp.topic not in self.topics:
+                    self.topics.append(tp.topic)
+                self.positions[(tp.topic, tp.partition)] = tp.offset if tp.offset >= 0 else \
+                    self._start(tp.topic, tp.partition)
 
     def assignment(self) -> list:
-        return list(self.positions)
+        return [TopicPartition(t, p) for t, p in self.positions]
 
-    def _next(self) -> Optional[Message]:
-        with self.broker.lock:
-            for t in self.topics:
-                if self.broker.take_error(t):
-                    return Message(t, -1, -1, None, None, KafkaError(KafkaError.UNKNOWN, "injected broker error"))
-            keys = list(self.positions)
-            for i in range(len(keys)):
-                k = keys[(self._rr + i) % len(keys)]
-                t, p = k
-                log = self.broker.topics[t][p]
-                if self.positions[k] < len(log):
-                    m = log[self.positions[k]]
-                    self.positions[k] += 1
-                    self._rr = (self._rr + i + 1) % len(keys)
-                    if self.auto_commit:
-                        self.broker.committed[self.group][k] = self.positions[k]
-                    return m
+    def _error(self) -> Optional[Message]:
+        for t in self.topics:
+            if self.broker.take_error(t):
+                return Message(t, -1, -1, None, None, KafkaError(KafkaError.UNKNOWN, "injected broker error"))
         return None
+
+    def _take(self, max_n: int) -> Optional[RecordBatch]:
+        keys = list(self.positions)
+        for i in range(len(keys)):
+            k = keys[(self._rr + i) % len(keys)]
+            t, p = k
+            rb = self.broker.topics[t][p].read(self.positions[k], max_n)
+            if rb is not None:
+                self.positions[k] += rb.n
+                self._rr = (self._rr + i + 1) % len(keys)
+                if self.auto_commit:
+                    self.broker.committed[self.group][k] = self.positions[k]
+                return rb
+        return None
+
+    def _wait(self, deadline: float) -> bool:
+        now = time.time()
+        if now >= deadline:
+            return False
+        with self.broker.cond:
+            self.broker.cond.wait(timeout=min(0.05, deadline - now))
+        return True
 
     def poll(self, timeout: float = -1) -> Optional[Message]:
         if self.closed:
             raise RuntimeError("Consumer closed")
         deadline = time.time() + (timeout if timeout and timeout > 0 else 0)
         while True:
-            m = self._next()
-            if m is not None or time.time() >= deadline:
-                return m
-            with self.broker.cond:
-                self.broker.cond.wait(timeout=min(0.05, max(0.0, deadline - time.time())))
+            with self.broker.lock:
+                err = self._error()
+                if err is not None:
+                    return err
+                rb = self._take(1)
+            if rb is not None:
+                return rb.message(0)
+            if not self._wait(deadline):
+                return None
 
     def consume(self, num_messages: int = 1, timeout: float = -1) -> list:
         out = []
+        for item in self.consume_batches(num_messages, timeout):
+            if isinstance(item, Message):
+                out.append(item)
+            else:
+                out.extend(item.message(i) for i in range(item.n))
+        return out
+
+    def consume_batches(self, max_messages: int = 1, timeout: float = -1) -> list:
+        """Up to ``max_messages`` records as columnar ``RecordBatch`` views (an error, if any, is
+        returned as a ``Message`` with ``error()`` set, last)."""
+        if self.closed:
+            raise RuntimeError("Consumer closed")
+        out, n = [], 0
         deadline = time.time() + (timeout if timeout and timeout > 0 else 0)
-        while len(out) < num_messages:
-            m = self._next()
-            if m is None:
-                if time.time() >= deadline:
+        while n < max_messages:
+            with self.broker.lock:
+                err = self._error()
+                if err is not None:
+                    out.append(err)
                     break
-                with self.broker.cond:
-                    self.broker.cond.wait(timeout=min(0.05, max(0.0, deadline - time.time())))
+                rb = self._take(max_messages - n)
+            if rb is not None:
+                out.append(rb)
+                n += rb.n
                 continue
-            out.append(m)
-            if m.error():
+            if n or not self._wait(deadline):
                 break
         return out
 
     def commit(self, message: Optional[Message] = None, offsets=None, asynchronous: bool = True):
+        if message is not None and not isinstance(message, Message):
+            raise TypeError("expected message=Message (confluent_kafka type-checks cimpl.Message)")
         with self.broker.lock:
             if message is not None:
                 self.broker.committed[self.group][(message.topic(), message.partition())] = message.offset() + 1
             elif offsets:
                 for tp in offsets:
+                    if not isinstance(tp, TopicPartition):
+                        raise TypeError("offsets must be TopicPartition objects")
                     self.broker.committed[self.group][(tp.topic, tp.partition)] = tp.offset
             else:
                 for k, v in self.positions.items():
                     self.broker.committed[self.group][k] = v
         return None
+
+    def committed(self, partitions: list, timeout: float = -1) -> list:
+        with self.broker.lock:
+            return [TopicPartition(tp.topic, tp.partition,
+                                   self.broker.committed[self.group].get((tp.topic, tp.partition), -1001))
+                    for tp in partitions]
 
     def committed_offsets(self) -> dict:
         with self.broker.lock:
@@ -245,29 +427,48 @@ class Producer:
         self.broker = broker or broker_for(self.config.get("bootstrap.servers", ""))
         self._pending: list = []
         self.lock = threading.Lock()
+        self.fail_next = 0            # fault injection: fail the next N deliveries
+
+    def _deliver_later(self, cb, err, what) -> None:
+        if cb is not None:
+            with self.lock:
+                self._pending.append((cb, err, what))
+
+    def _maybe_fail(self):
+        with self.lock:
+            if self.fail_next > 0:
+                self.fail_next -= 1
+                return KafkaError(KafkaError.UNKNOWN, "injected delivery failure")
+        return None
 
     def produce(self, topic: str, value=None, key=None, partition: int = -1, on_delivery: Optional[Callable] = None,
                 callback: Optional[Callable] = None, **kw) -> None:
         if topic is None:
             raise TypeError("topic must be a str (KAFKA_OUTPUT_TOPIC unset?)")
-        m = self.broker.append(topic, _b(key), _b(value), partition)
-        cb = on_delivery or callback
-        if cb is not None:
-            with self.lock:
-                self._pending.append((cb, m))
+        err = self._maybe_fail()
+        m = None if err else self.broker.append(topic, _b(key), _b(value), partition)
+        self._deliver_later(on_delivery or callback, err, m)
 
     def produce_batch(self, topic: str, keys: list, values: list) -> None:
-        """Many messages at once (no delivery callbacks): what the streaming engine uses when the
-        producer offers it; librdkafka producers get per-message ``produce`` calls instead."""
+        """Many messages at once, keyed partitioning, no delivery callbacks."""
         if topic is None:
             raise TypeError("topic must be a str (KAFKA_OUTPUT_TOPIC unset?)")
-        self.broker.append_many(topic, [_b(k) for k in keys], [_b(v) for v in values])
+        self.broker.append_many(topic, keys, values)
+
+    def produce_records(self, topic: str, partition: int, keys, key_off, values, val_off, null_keys=None,
+                        on_delivery: Optional[Callable] = None) -> None:
+        """One columnar batch into one partition; ``on_delivery(err, RecordBatch)`` from poll/flush."""
+        if topic is None:
+            raise TypeError("topic must be a str (KAFKA_OUTPUT_TOPIC unset?)")
+        err = self._maybe_fail()
+        rb = None if err else self.broker.append_records(topic, partition, keys, key_off, values, val_off, null_keys)
+        self._deliver_later(on_delivery, err, rb)
 
     def poll(self, timeout: float = 0) -> int:
         with self.lock:
             pend, self._pending = self._pending, []
-        for cb, m in pend:
-            cb(None, m)
+        for cb, err, what in pend:
+            cb(err, what)
         return len(pend)
 
     def flush(self, timeout: float = -1) -> int:

@@ -39,6 +39,8 @@ class _Stage:
     ev_h2d: torch.cuda.Event
     ev_compute: torch.cuda.Event
     ev_d2h: torch.cuda.Event
+    long_host: torch.Tensor       # int32 pinned [max_docs]: indices of dialogues over LONG_DOC_MIN bytes
+    long_dev: torch.Tensor        # its device copy (preallocated: no allocator traffic across streams)
     slot: Optional[Slot] = None
     n: int = 0
 
@@ -76,7 +78,8 @@ class GpuScorer:
                 torch.zeros(max_docs, **i32),
                 torch.zeros((max_docs, self.K), dtype=torch.float64).pin_memory(),
                 torch.zeros(max_docs, dtype=torch.int32).pin_memory(),
-                torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()))
+                torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event(),
+                torch.zeros(max_docs, dtype=torch.int32).pin_memory(), torch.zeros(max_docs, **i32)))
         self._next = 0
         self._inflight: deque = deque()
         torch.cuda.synchronize(self.dev)
@@ -93,17 +96,24 @@ class GpuScorer:
         n, nb = slot.n_docs, slot.n_bytes
         st.slot, st.n = slot, n
         long_idx = None
+        n_long = 0
         if n:
             offs = slot.offsets[: n + 1].numpy()
             lens = offs[1:] - offs[:-1]
             if int(lens.max()) > LONG_DOC_MIN:
-                sel = np.nonzero((lens > LONG_DOC_MIN) & (lens <= LONG_DOC_BYTES))[0].astype(np.int32)
-                if sel.size:
-                    long_idx = torch.from_numpy(sel).to(self.dev, non_blocking=False)
+                sel = np.nonzero((lens > LONG_DOC_MIN) & (lens <= LONG_DOC_BYTES))[0]
+                n_long = int(sel.size)
+        # the stage's previous batch has fully drained (collect() synchronised on its event), so
+        # its pinned index buffer may be rewritten here
+        if n_long:
+            st.long_host.numpy()[:n_long] = sel
+            long_idx = st.long_dev[:n_long]
         with torch.cuda.stream(self.h2d):
             self.h2d.wait_event(st.ev_d2h)   # previous use of this stage fully drained
             st.text[: nb + PAD].copy_(slot.data[: nb + PAD], non_blocking=True)
             st.offsets[: n + 1].copy_(slot.offsets[: n + 1], non_blocking=True)
+            if n_long:
+                long_idx.copy_(st.long_host[:n_long], non_blocking=True)
             st.ev_h2d.record(self.h2d)
         with torch.cuda.stream(self.compute):
             self.compute.wait_event(st.ev_h2d)
@@ -151,6 +161,10 @@ class GpuScorer:
     def inflight(self) -> int:
         return len(self._inflight)
 
+    def ready(self) -> bool:
+        """True when the oldest in-flight batch has finished (collect() would not block)."""
+        return bool(self._inflight) and self._inflight[0].ev_d2h.query()
+
     @property
     def depth(self) -> int:
         return len(self.stages)
@@ -182,12 +196,15 @@ class HostScorer:
         res = featurize_score(pt, self.spec, idf=self.idf, lr=lr, trees=tr, device="cpu")
         self._inflight.append((slot, res.raw.numpy().copy()))
 
-    def collect(self) -> tuple:
+    def collect(self, copy: bool = True) -> tuple:
         return self._inflight.popleft()
 
     @property
     def inflight(self) -> int:
         return len(self._inflight)
+
+    def ready(self) -> bool:
+        return bool(self._inflight)
 
     @property
     def depth(self) -> int:
@@ -230,6 +247,9 @@ class MultiGpuScorer:
     def inflight(self) -> int:
         return len(self._order)
 
+    def ready(self) -> bool:
+        return bool(self._order) and self._order[0].ready()
+
     def submit(self, slot: Slot) -> None:
         for _ in range(len(self.scorers)):
             s = self.scorers[self._rr]
@@ -241,8 +261,7 @@ class MultiGpuScorer:
         raise RuntimeError("pipeline full: call collect() first")
 
     def collect(self, copy: bool = True) -> tuple:
-        s = self._order.popleft()
-        return s.collect(copy=copy) if isinstance(s, GpuScorer) else s.collect()
+        return self._order.popleft().collect(copy=copy)
 
     def score_packed(self, slot: Slot) -> np.ndarray:
         self.submit(slot)

@@ -29,12 +29,15 @@ def _security(conf: dict) -> dict:
 
 
 def _use_memory(bootstrap: str) -> bool:
+    """In-memory broker only when asked for (``memory://`` or ``FDX_KAFKA=memory``): a real
+    bootstrap without confluent_kafka is an error, never a silent switch to a private broker."""
     if bootstrap.startswith("memory://") or os.getenv("FDX_KAFKA", "").lower() == "memory":
         return True
     try:
         import confluent_kafka  # noqa: F401
-    except ImportError:
-        return True
+    except ImportError as e:
+        raise ImportError(f"confluent_kafka is required for bootstrap {bootstrap!r}; install it, or use a "
+                          "memory:// bootstrap / FDX_KAFKA=memory for the in-memory broker") from e
     return False
 
 
@@ -58,6 +61,32 @@ def get_kafka_consumer(topics=None, group: Optional[str] = None):
         c = Consumer(conf)
     c.subscribe(list(topics) if topics else [os.getenv("KAFKA_INPUT_TOPIC", DEFAULT_INPUT)])
     return c
+
+
+def get_partition_consumers(topic: Optional[str] = None, group: Optional[str] = None) -> list:
+    """One consumer per partition of ``topic`` (static ``assign``, same group): the streaming
+    engine runs one reader thread per consumer. Starting offsets are the group's commits."""
+    conf = consumer_config(group)
+    topic = topic or os.getenv("KAFKA_INPUT_TOPIC", DEFAULT_INPUT)
+    if _use_memory(conf["bootstrap.servers"]):
+        nparts = fake_kafka.broker_for(conf["bootstrap.servers"]).partitions(topic)
+        out = []
+        for p in range(nparts):
+            c = fake_kafka.Consumer(conf)
+            c.assign([fake_kafka.TopicPartition(topic, p)])
+            out.append(c)
+        return out
+    from confluent_kafka import Consumer, TopicPartition
+
+    probe = Consumer(conf)
+    nparts = len(probe.list_topics(topic, timeout=10).topics[topic].partitions)
+    probe.close()
+    out = []
+    for p in range(nparts):
+        c = Consumer(conf)
+        c.assign([TopicPartition(topic, p)])
+        out.append(c)
+    return out
 
 
 def get_kafka_producer():

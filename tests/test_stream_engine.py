@@ -1,0 +1,166 @@
+"""Streaming engine v2: per-partition readers, carry-over of slot overflow, delivery-gated commits,
+the in-memory broker's confluent-compatible contracts (test strategy: SURVEY.md §4, X-20)."""
+import json
+
+import numpy as np
+import pytest
+
+from fraud_detection_spark_kafka_llm_amd.data import fixtures
+from fraud_detection_spark_kafka_llm_amd.serve.agent import ClassificationAgent
+from fraud_detection_spark_kafka_llm_amd.serve.llm import StubLLM
+from fraud_detection_spark_kafka_llm_amd.stream import fake_kafka, kafka
+from fraud_detection_spark_kafka_llm_amd.stream.engine import LatencyHistogram, StreamingEngine
+
+
+def _conf(url, group="g"):
+    return {"bootstrap.servers": url, "group.id": group, "auto.offset.reset": "earliest",
+            "enable.auto.commit": False}
+
+
+def _fill(url, topic, texts, parts=3):
+    broker = fake_kafka.broker_for(url)
+    broker.create_topic(topic, parts)
+    p = fake_kafka.Producer({"bootstrap.servers": url})
+    for i, t in enumerate(texts):
+        p.produce(topic, key=f"k{i}", value=json.dumps({"text": t}))
+    return broker
+
+
+@pytest.fixture(scope="module")
+def agent(shipped_model_path):
+    return ClassificationAgent(str(shipped_model_path), llm=StubLLM(), device="cpu")
+
+
+def test_commit_contract_matches_confluent():
+    url = "memory://contract"
+    broker = _fill(url, "t", ["a", "b"], parts=1)
+    c = fake_kafka.Consumer(_conf(url))
+    c.subscribe(["t"])
+    m = c.poll(0.1)
+    with pytest.raises(TypeError):
+        c.commit(message=object())               # confluent type-checks cimpl.Message
+    with pytest.raises(TypeError):
+        c.commit(offsets=[("t", 0, 1)])
+    c.commit(offsets=[fake_kafka.TopicPartition("t", 0, m.offset() + 1)])
+    assert c.committed([fake_kafka.TopicPartition("t", 0)])[0].offset == 1
+    assert len(broker.topics["t"][0]) == 2
+
+
+def test_columnar_consume_and_produce_records():
+    url = "memory://columnar"
+    broker = _fill(url, "t", [f"m{i}" for i in range(10)], parts=1)
+    c = fake_kafka.Consumer(_conf(url))
+    c.assign([fake_kafka.TopicPartition("t", 0)])
+    rbs = c.consume_batches(7, 0.1)
+    assert sum(r.n for r in rbs) == 7 and rbs[0].base_offset == 0
+    rest = c.consume_batches(100, 0.1)
+    assert sum(r.n for r in rest) == 3 and rest[0].base_offset == 7
+    assert json.loads(rest[-1].value(rest[-1].n - 1))["text"] == "m9"
+    p = fake_kafka.Producer({"bootstrap.servers": url})
+    got = []
+    keys, ko, _ = fake_kafka.pack([b"x", b"yy"])
+    vals, vo, _ = fake_kafka.pack([b"1", b"22"])
+    p.produce_records("o", 0, keys, ko, vals, vo, on_delivery=lambda err, rb: got.append((err, rb.n)))
+    assert got == []                      # delivery reports are served by poll/flush
+    p.flush()
+    assert got == [(None, 2)]
+    assert [(m.key(), m.value()) for m in broker.messages("o")] == [(b"x", b"1"), (b"yy", b"22")]
+
+
+def test_partition_readers_commit_only_delivered(agent, monkeypatch):
+    url = "memory://readers"
+    texts = [fixtures.SCAM_SAMPLE, fixtures.BENIGN_SAMPLE, "hello there"] * 100
+    broker = _fill(url, "in", texts)
+    monkeypatch.setenv("KAFKA_BOOTSTRAP_SERVERS", url)
+    consumers = kafka.get_partition_consumers("in", group="g2")
+    assert len(consumers) == 3
+    prod = fake_kafka.Producer({"bootstrap.servers": url})
+    eng = StreamingEngine.from_agent(agent, consumers, prod, "out", batch_max=64, max_latency_ms=2)
+    st = eng.run(idle_timeout_s=0.3)
+    assert st["messages"] == 300 and st["produced"] == 300 and st["delivery_errors"] == 0
+    assert st["p50_ms"] > 0 and st["p95_ms"] >= st["p50_ms"]
+    committed = consumers[0].committed_offsets()
+    for p in range(3):
+        assert committed[("in", p)] == len(broker.topics["in"][p])
+    recs = {m.key(): json.loads(m.value()) for m in broker.messages("out")}
+    assert recs[b"k0"]["prediction"] == 1.0 and recs[b"k0"]["original_text"] == fixtures.SCAM_SAMPLE
+
+
+def test_failed_delivery_blocks_that_partitions_commit(agent):
+    url = "memory://faildeliver"
+    broker = _fill(url, "in", ["a b c"] * 30, parts=1)
+    c = fake_kafka.Consumer(_conf(url))
+    c.subscribe(["in"])
+    prod = fake_kafka.Producer({"bootstrap.servers": url})
+    prod.fail_next = 1                    # the first micro-batch's output is rejected
+    eng = StreamingEngine.from_agent(agent, c, prod, "out", batch_max=8, max_latency_ms=1)
+    st = eng.run(idle_timeout_s=0.2)
+    assert st["delivery_errors"] == 1 and st["produced"] == 30 - 8
+    # at-least-once: nothing past the failed segment is committed, so a restart re-reads it
+    assert c.committed_offsets().get(("in", 0), 0) == 0
+
+
+def test_slot_overflow_is_carried_over_not_lost(agent):
+    url = "memory://overflow"
+    texts = [("word " * 150)[:700] + str(i) for i in range(40)] + ["x" * 5000]
+    broker = _fill(url, "in", texts, parts=1)
+    c = fake_kafka.Consumer(_conf(url))
+    c.subscribe(["in"])
+    prod = fake_kafka.Producer({"bootstrap.servers": url})
+    eng = StreamingEngine.from_agent(agent, c, prod, "out", batch_max=32, max_latency_ms=1, max_bytes=4096)
+    st = eng.run(idle_timeout_s=0.2)
+    # 40 records of ~700 bytes do not fit a 4 KB slot in one go: every one is carried over and
+    # scored; the 5 KB record can never fit and is rejected as a bad message (and committed)
+    assert st["messages"] == 41 and st["produced"] == 40 and st["bad_messages"] == 1
+    out = {m.key(): json.loads(m.value())["original_text"] for m in broker.messages("out")}
+    assert all(out[f"k{i}".encode()] == texts[i] for i in range(40))
+    assert c.committed_offsets()[("in", 0)] == 41
+
+
+def test_max_messages_quota_is_exact(agent):
+    url = "memory://quota"
+    broker = _fill(url, "in", ["some dialogue text"] * 200)
+    consumers = []
+    for p in range(3):
+        c = fake_kafka.Consumer(_conf(url, "q"))
+        c.assign([fake_kafka.TopicPartition("in", p)])
+        consumers.append(c)
+    prod = fake_kafka.Producer({"bootstrap.servers": url})
+    eng = StreamingEngine.from_agent(agent, consumers, prod, "out", batch_max=16, max_latency_ms=1)
+    st = eng.run(max_messages=50, idle_timeout_s=0.2)
+    assert st["messages"] == 50 and broker.size("out") == 50
+    assert sum(consumers[0].committed_offsets().values()) == 50
+
+
+def test_async_explanations_are_sampled_and_bounded(agent):
+    url = "memory://explain-sample"
+    _fill(url, "in", [fixtures.SCAM_SAMPLE] * 40, parts=1)
+    c = fake_kafka.Consumer(_conf(url))
+    c.subscribe(["in"])
+    prod = fake_kafka.Producer({"bootstrap.servers": url})
+    eng = StreamingEngine.from_agent(agent, c, prod, "out", batch_max=16, max_latency_ms=1, explain="async",
+                                     explain_every=10)
+    st = eng.run(idle_timeout_s=0.2)
+    recs = [json.loads(m.value()) for m in fake_kafka.broker_for(url).messages("out")]
+    assert st["explanations"] == 4 and sum(1 for r in recs if r.get("type") == "explanation") == 4
+
+
+def test_real_bootstrap_without_client_library_raises(monkeypatch):
+    try:
+        import confluent_kafka  # noqa: F401
+        pytest.skip("confluent_kafka installed")
+    except ImportError:
+        pass
+    monkeypatch.setenv("KAFKA_BOOTSTRAP_SERVERS", "broker-1:9092")
+    monkeypatch.delenv("FDX_KAFKA", raising=False)
+    with pytest.raises(ImportError):
+        kafka.get_kafka_producer()
+    monkeypatch.setenv("FDX_KAFKA", "memory")
+    assert isinstance(kafka.get_kafka_producer(), fake_kafka.Producer)
+
+
+def test_latency_histogram_percentiles():
+    h = LatencyHistogram()
+    h.add(np.linspace(1.0, 100.0, 10000))
+    assert h.percentile(50) == pytest.approx(50.5, rel=0.02)
+    assert h.percentile(95) == pytest.approx(95.05, rel=0.02)
