@@ -13,8 +13,16 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      scores straight into pinned host memory; the host then applies the sigmoid/threshold. The
      copy of step i+1 overlaps the kernel of step i. ``value`` = dialogues/s summed over all ranks
      (weak scaling: fixed micro-batch per GPU).
-Data is synthetic (the reference dataset is not available) with random-init-free trained trees;
-compute dtype: fp64 scores / fp32-accumulated bf16-MFMA histograms (text is bytes).
+  3. Kafka end-to-end (BASELINE config 5) — an in-memory broker topic with 3 partitions of
+     ``{"text": ...}`` JSON records -> StreamingEngine (one reader thread per partition, native JSON
+     extraction into the pinned ring, GPU scoring, native output encoding, async produce, commits
+     gated on delivery callbacks). ``kafka_dialogues_per_s``: a pre-filled topic drained end to end
+     (consume -> score -> produce -> commit); ``kafka_p50_ms`` / ``kafka_p95_ms``: per-message
+     latency (broker append -> output delivered) under a paced producer at ``kafka_offered_per_s``.
+Data is synthetic (the reference dataset is not available) with random-init-free trained trees.
+Compute dtype: the GBDT histograms are exact integer sums (gradients quantised to 2^-k with k
+from the all-reduced max, i8 MFMA digit planes, int64 accumulation) — at least fp32-accurate and
+bitwise reproducible; gains, leaves and scores are fp64; text is bytes. Reported as "fp32".
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
   N > 1 is launched by the driver via torch.distributed.run (RANK/WORLD_SIZE/MASTER_* in env).
@@ -112,6 +120,38 @@ def featurize_shard(chunks: list, dev, spec):
     return indptr, torch.cat(idxs), torch.cat(vals), torch.cat(labels)
 
 
+def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
+    """BASELINE config 5 on this rank's GPU against its own in-memory broker (3 partitions)."""
+    import gc
+
+    from fraud_detection_spark_kafka_llm_amd.stream import loadgen
+    from fraud_detection_spark_kafka_llm_amd.stream.engine import StreamingEngine
+
+    pt, _ = synth.generate(synth.SynthConfig(n=65536, seed=77 + rank), device=dev, start=2 * 10**9)
+    pool = loadgen.MessagePool(pt.strings())
+    del pt
+
+    def make(batch: int, latency_ms: float):
+        def mk(consumers, producer, topic):
+            sc = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=batch, max_bytes=batch * 4096, depth=2)
+            return StreamingEngine(sc, model.postprocess_numpy, consumers, producer, topic, batch_max=batch,
+                                   max_latency_ms=latency_ms, max_bytes=batch * 4096)
+        return mk
+
+    loadgen.throughput_run(make(16384, 5.0), pool, 100_000, url=f"memory://bench-warm-{rank}")   # warmup
+    gc.collect()
+    tp = loadgen.throughput_run(make(16384, 5.0), pool, args.kafka_msgs, url=f"memory://bench-tp-{rank}")
+    gc.collect()
+    lat = loadgen.latency_run(make(4096, 1.0), pool, args.kafka_rate, args.kafka_sec,
+                              url=f"memory://bench-lat-{rank}")
+    ok = tp["produced"] == args.kafka_msgs and tp["committed"] == args.kafka_msgs and lat["produced"] == lat["sent"]
+    return {"kafka_dialogues_per_s": tp["dialogues_per_s"], "kafka_msgs": args.kafka_msgs,
+            "kafka_throughput_sec": tp["sec"], "kafka_p50_ms": lat["p50_ms"], "kafka_p95_ms": lat["p95_ms"],
+            "kafka_p99_ms": lat["p99_ms"], "kafka_offered_per_s": args.kafka_rate,
+            "kafka_latency_msgs": lat["sent"], "kafka_all_delivered_and_committed": bool(ok),
+            "kafka_avg_record_bytes": round(pool.avg_bytes, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +163,9 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="dialogues per GPU per streaming step")
     ap.add_argument("--pool", type=int, default=6, help="distinct pinned micro-batches per GPU")
     ap.add_argument("--depth-pipeline", type=int, default=2)
+    ap.add_argument("--kafka-msgs", type=int, default=1_000_000, help="records drained in the Kafka throughput run")
+    ap.add_argument("--kafka-rate", type=float, default=300_000, help="paced producer rate of the latency run")
+    ap.add_argument("--kafka-sec", type=float, default=2.0, help="duration of the latency run")
     args = ap.parse_args()
 
     D.init_from_env(os.environ.get("FDX_DIST_BACKEND", "nccl"))   # gloo: rehearse N ranks on one GPU
@@ -226,6 +269,13 @@ def main():
         lats.append((time.perf_counter() - t1) * 1e3)
     p50 = float(np.percentile(lats[10:], 50))
 
+    kafka = kafka_phase(args, spec, idf_np, model, dev, rank) if args.kafka_msgs > 0 else {}
+    if kafka:
+        kafka["kafka_dialogues_per_s"] = float(D.all_reduce_sum(
+            torch.tensor([kafka["kafka_dialogues_per_s"]], dtype=torch.float64, device=dev)).item())
+        for k in ("kafka_p50_ms", "kafka_p95_ms", "kafka_p99_ms"):
+            kafka[k] = max_over_ranks(kafka[k], dev)
+
     docs = args.steps * args.batch * world
     if rank == 0:
         out = {
@@ -239,7 +289,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp32",
             "data": "synthetic",
             "config": {"model": f"HashingTF(2^18)->IDF->GBDT({args.trees} trees, depth {args.depth})",
                        "global_batch": args.batch * world, "seq_len": round(avg_bytes),
@@ -252,6 +302,7 @@ def main():
             "stream_accuracy": acc,
             "p50_single_dialogue_ms": p50,
             "numa_bind_rank0": numa,
+            **kafka,
         }
         print(json.dumps(out), flush=True)
     D.barrier()

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "parallel_for.h"
+#include "swar.h"
 
 namespace fdx {
 
@@ -108,6 +109,14 @@ int64_t escape_ascii(const uint8_t* s, int64_t n, uint8_t* out) {
   int64_t len = 0;
   uint8_t* o = out;
   for (int64_t i = 0; i < n;) {
+    while (n - i >= 8) {             // printable ASCII without quote / backslash: 8 at a time
+      const uint64_t w = swar_load(s + i);
+      if (swar_has_less(w, 0x20) || swar_has_byte(w, '"') || swar_has_byte(w, '\\') || swar_has_7f_or_high(w)) break;
+      if (o) { std::memcpy(o, s + i, 8); o += 8; }
+      len += 8;
+      i += 8;
+    }
+    if (i >= n) break;
     uint32_t cp;
     const int k = utf8_next(s, n, i, &cp);
     if (k == 0) return -1;
@@ -154,7 +163,7 @@ int64_t encode_records(const double* pred, const double* conf, const uint8_t* te
                        const int32_t* skip, int64_t n, uint8_t* out, int64_t cap, int64_t* out_off, int32_t* status,
                        int threads) {
   std::vector<int64_t> lens((size_t)n, 0);
-  parallel_for(n, threads, 256, [&](int64_t lo, int64_t hi) {
+  parallel_for(n, threads, 64, [&](int64_t lo, int64_t hi) {
     char num[64];
     for (int64_t i = lo; i < hi; ++i) {
       if (skip && skip[i]) { status[i] = 2; lens[i] = 0; continue; }
@@ -168,7 +177,7 @@ int64_t encode_records(const double* pred, const double* conf, const uint8_t* te
   out_off[0] = 0;
   for (int64_t i = 0; i < n; ++i) out_off[i + 1] = out_off[i] + lens[(size_t)i];
   if (out_off[n] > cap) return -out_off[n];   // caller grows the buffer and retries
-  parallel_for(n, threads, 256, [&](int64_t lo, int64_t hi) {
+  parallel_for(n, threads, 64, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
       if (status[i] != 0) continue;
       uint8_t* o = out + out_off[i];

@@ -47,6 +47,11 @@ class ClassificationModelBase(_PredictorParams, Model):
         """raw kernel output [N, K] fp64 -> (rawPrediction [N,2], probability [N,2], prediction [N])."""
         raise NotImplementedError
 
+    def postprocess_numpy(self, raw: np.ndarray):
+        """Streaming hot path: raw [N, K] fp64 numpy -> (prediction [N], P(class 1) [N])."""
+        _, prob, pred = self.postprocess(torch.from_numpy(raw))
+        return pred.numpy(), prob[:, 1].numpy()
+
     def _transform(self, frame: Frame) -> Frame:
         from ..ops.sparse import score_csr
 
@@ -157,6 +162,12 @@ class LogisticRegressionModel(_LRParams, ClassificationModelBase):
         prob = 1.0 / (1.0 + torch.exp(-rp))           # Spark raw2probability on [-m, m]
         pred = (prob[:, 1] > self.getThreshold()).to(torch.float64)
         return rp, prob, pred
+
+    def postprocess_numpy(self, raw: np.ndarray):
+        p = np.exp(-raw[:, 0])
+        np.add(p, 1.0, out=p)
+        np.reciprocal(p, out=p)
+        return (p > self.getThreshold()).astype(np.float64), p
 
     def _metadata_extra(self):
         return None

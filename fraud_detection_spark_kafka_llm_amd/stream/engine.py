@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import functools
+import gc
 import json
 import queue
 import threading
@@ -51,7 +52,8 @@ from .ring import PinnedRing, Slot
 
 log = get_logger("stream")
 
-_LAT_EDGES = np.geomspace(1e-3, 1e6, 1201)   # ms, ~1.7 % wide log bins
+_LAT_LO, _LAT_BINS_PER_DECADE = 1e-3, 133         # ms; ~1.7 % wide log bins from 1 us to 1000 s
+_LAT_EDGES = _LAT_LO * 10.0 ** (np.arange(9 * _LAT_BINS_PER_DECADE + 1) / _LAT_BINS_PER_DECADE)
 
 
 class LatencyHistogram:
@@ -63,7 +65,10 @@ class LatencyHistogram:
         self.lock = threading.Lock()
 
     def add(self, ms: np.ndarray) -> None:
-        c = np.bincount(np.searchsorted(_LAT_EDGES, ms), minlength=self.counts.size)
+        idx = np.log10(np.maximum(ms, _LAT_LO) / _LAT_LO)
+        idx *= _LAT_BINS_PER_DECADE
+        k = np.minimum(np.ceil(idx).astype(np.int64), self.counts.size - 1)
+        c = np.bincount(k, minlength=self.counts.size)
         with self.lock:
             self.counts += c
             self.n += int(ms.size)
@@ -265,27 +270,33 @@ class _Reader(threading.Thread):
         eng = self.eng
         want = eng._claim(want)
         if want == 0:
+            time.sleep(0.0005)        # another reader holds the remaining quota
             return
+        if eng._quota is not None:    # never hold a reservation across a blocking wait
+            timeout = 0
         got = 0
-        if self.columnar:
-            items = self.consumer.consume_batches(want, timeout)
-        else:
-            items = self.consumer.consume(num_messages=want, timeout=timeout)
-        good = []
-        for it in items:
-            if isinstance(it, fake_kafka.RecordBatch):
-                self.carry.append(_Piece(it))
-                got += it.n
-            elif it.error() is not None:
-                eng._count("broker_errors", 1)
-                log.warning("kafka error: %s", it.error())
+        try:
+            if self.columnar:
+                items = self.consumer.consume_batches(want, timeout)
             else:
-                good.append(it)
-        if good:
-            pieces = _to_pieces(good)
-            self.carry.extend(pieces)
-            got += len(good)
-        eng._unclaim(want - got)
+                items = self.consumer.consume(num_messages=want, timeout=timeout)
+            good = []
+            for it in items:
+                if isinstance(it, fake_kafka.RecordBatch):
+                    self.carry.append(_Piece(it))
+                    got += it.n
+                elif it.error() is not None:
+                    eng._count("broker_errors", 1)
+                    log.warning("kafka error: %s", it.error())
+                else:
+                    good.append(it)
+            if good:
+                self.carry.extend(_to_pieces(good))
+                got += len(good)
+        finally:
+            eng._settle(want, got)
+        if not got and timeout == 0:
+            time.sleep(0.001)
         if got:
             eng._last_read = time.time()
 
@@ -415,13 +426,15 @@ class StreamingEngine:
         self._reader_error: Optional[BaseException] = None
         self._lock = threading.Lock()
         self._quota: Optional[int] = None
+        self._claimed = 0
         self._last_read = time.time()
         self._pool = cf.ThreadPoolExecutor(max_workers=8) if explain == "async" else None
         self._explain_pending = 0
         self._seen = 0
         self._m_msgs = REGISTRY.counter("stream_messages_total")
         self._m_lat = REGISTRY.histogram("stream_batch_latency_ms")
-        self._enc_buf = torch.empty(1 << 22, dtype=torch.uint8)
+        self._enc_meta = (torch.empty(self.batch_max + 1, dtype=torch.int64),
+                          torch.empty(self.batch_max, dtype=torch.int32))
         self._columnar_out = hasattr(producer, "produce_records")
         self._out_parts = producer.broker.partitions(output_topic) if isinstance(producer, fake_kafka.Producer) else 1
         self._tp_cls = [fake_kafka.TopicPartition if isinstance(c, fake_kafka.Consumer) else _confluent_tp()
@@ -437,29 +450,33 @@ class StreamingEngine:
         devs = list(devices) if devices else [device or agent.device]
         scorer = make_multi_scorer(fp.spec(True), idf, fp.model.scorer(), devs,
                                    max_docs=kw.get("batch_max", 4096), max_bytes=kw.get("max_bytes", 64 << 20))
-        return cls(scorer, fp.model.postprocess, consumer, producer, output_topic, agent=agent, **kw)
+        return cls(scorer, fp.model.postprocess_numpy, consumer, producer, output_topic, agent=agent, **kw)
 
     def stop(self) -> None:
         self._stop.set()
 
     # ------------------------------------------------------------------ reader coordination
     def _claim(self, want: int) -> int:
+        """Reserve up to ``want`` of the remaining ``max_messages`` before a consume call."""
         with self._lock:
             if self._quota is None:
                 return want
             g = min(want, self._quota)
             self._quota -= g
+            self._claimed += g
             return g
 
-    def _unclaim(self, k: int) -> None:
-        if k > 0:
-            with self._lock:
-                if self._quota is not None:
-                    self._quota += k
+    def _settle(self, claimed: int, got: int) -> None:
+        """Return the unused part of a reservation once its consume call is done."""
+        with self._lock:
+            if self._quota is not None:
+                self._quota += claimed - got
+                self._claimed -= claimed
 
     def _quota_done(self) -> bool:
+        """All of ``max_messages`` consumed (reservations in flight may still be returned)."""
         with self._lock:
-            return self._quota is not None and self._quota <= 0
+            return self._quota is not None and self._quota <= 0 and self._claimed == 0
 
     def _count(self, name: str, k: int) -> None:
         with self._lock:
@@ -467,6 +484,9 @@ class StreamingEngine:
 
     # ------------------------------------------------------------------ main loop
     def run(self, max_messages: Optional[int] = None, idle_timeout_s: float = 1.0) -> dict:
+        # long-lived objects (model, tables, torch/numpy internals) leave the collector's young
+        # generations: full collections would otherwise stall the readers for 50-100 ms
+        gc.freeze()
         self._quota = max_messages
         self._readers_stop.clear()
         self._last_read = time.time()
@@ -525,9 +545,7 @@ class StreamingEngine:
         slot, raw = self.scorer.collect(copy=False)
         b: _Batch = slot.meta
         n = slot.n_docs
-        _, prob, pred = self.postprocess(torch.from_numpy(raw))
-        pred = pred.numpy()
-        p1 = prob[:, 1].numpy()
+        pred, p1 = self.postprocess(raw)
         status = b.status
         bad = status != 0
         self.stats.bad_messages += int(bad.sum())
@@ -556,13 +574,19 @@ class StreamingEngine:
         pred_t = torch.from_numpy(np.ascontiguousarray(pred, dtype=np.float64))
         conf_t = torch.from_numpy(np.ascontiguousarray(p1, dtype=np.float64))
         skip = torch.from_numpy(np.ascontiguousarray(status != 0, dtype=np.int32))
-        out_off = torch.empty(n + 1, dtype=torch.int64)
-        st = torch.empty(n, dtype=torch.int32)
-        need = C.encode_records(pred_t, conf_t, slot.data, slot.offsets, skip, self._enc_buf, out_off, st, 0)
+        out_off, st = self._enc_meta
+        if out_off.numel() < n + 1:
+            out_off, st = torch.empty(n + 1, dtype=torch.int64), torch.empty(n, dtype=torch.int32)
+            self._enc_meta = (out_off, st)
+        out_off, st = out_off[: n + 1], st[:n]
+        # a fresh buffer per batch, handed to the producer without a copy (the in-memory broker
+        # keeps it as the log segment; librdkafka copies on produce)
+        buf = torch.empty(slot.n_bytes + 160 * n + 4096, dtype=torch.uint8)
+        need = C.encode_records(pred_t, conf_t, slot.data, slot.offsets, skip, buf, out_off, st, 0)
         if need < 0:
-            self._enc_buf = torch.empty(int(-need * 1.25) + 4096, dtype=torch.uint8)
-            need = C.encode_records(pred_t, conf_t, slot.data, slot.offsets, skip, self._enc_buf, out_off, st, 0)
-        return self._enc_buf.numpy(), out_off.numpy(), st.numpy()
+            buf = torch.empty(-need, dtype=torch.uint8)
+            need = C.encode_records(pred_t, conf_t, slot.data, slot.offsets, skip, buf, out_off, st, 0)
+        return buf.numpy(), out_off.numpy(), st.numpy()
 
     @staticmethod
     def _record_py(pred, conf, text: str, analysis=None, insight=None) -> bytes:
@@ -609,7 +633,8 @@ class StreamingEngine:
         if self._columnar_out:
             try:
                 self.producer.produce_records(self.topic, seg.partition % self._out_parts, keys, koff, vals, voff,
-                                              nulls, on_delivery=functools.partial(self._on_delivery_cb, seg, entry))
+                                              nulls, on_delivery=functools.partial(self._on_delivery_cb, seg, entry),
+                                              copy=False)
             except Exception as e:
                 log.error("produce failed: %s", e)
                 self._on_delivery(seg, entry, e)

@@ -456,12 +456,14 @@ class Producer:
         self.broker.append_many(topic, keys, values)
 
     def produce_records(self, topic: str, partition: int, keys, key_off, values, val_off, null_keys=None,
-                        on_delivery: Optional[Callable] = None) -> None:
-        """One columnar batch into one partition; ``on_delivery(err, RecordBatch)`` from poll/flush."""
+                        on_delivery: Optional[Callable] = None, copy: bool = True) -> None:
+        """One columnar batch into one partition; ``on_delivery(err, RecordBatch)`` from poll/flush.
+        ``copy=False`` hands the buffers to the broker (the caller must not reuse them)."""
         if topic is None:
             raise TypeError("topic must be a str (KAFKA_OUTPUT_TOPIC unset?)")
         err = self._maybe_fail()
-        rb = None if err else self.broker.append_records(topic, partition, keys, key_off, values, val_off, null_keys)
+        rb = None if err else self.broker.append_records(topic, partition, keys, key_off, values, val_off, null_keys,
+                                                         copy=copy)
         self._deliver_later(on_delivery, err, rb)
 
     def poll(self, timeout: float = 0) -> int:
