@@ -161,21 +161,52 @@ class SparkXGBClassifierModel(_XGBParams, ClassificationModelBase):
                 "baseMargin": self.base_margin}
 
     def _save_data(self, path) -> None:
+        """xgboost.spark's writer layout: ``metadata/`` (Spark DefaultParamsWriter JSON, written by
+        the base class) and ``model/part-00000`` — the booster JSON as a one-line text part, what
+        ``SparkXGBModelWriter`` writes with ``saveAsTextFile``. The fp64 split thresholds and node
+        statistics of this engine ride in ``learner.attributes["fdx_trees"]`` (XGBoost keeps
+        string attributes and ignores unknown ones) so a reload scores bitwise identically."""
+        d = Path(path) / "model"
+        d.mkdir(parents=True, exist_ok=True)
+        booster = self.to_xgboost_json()
+        booster["learner"]["attributes"]["fdx_trees"] = json.dumps([t.to_node_rows() for t in self._trees])
+        booster["learner"]["attributes"]["fdx_base_margin"] = repr(self.base_margin)
+        (d / "part-00000").write_text(json.dumps(booster) + "\n")
+        (d / "_SUCCESS").write_text("")
+
+    def _load_data(self, path, md) -> None:
+        """Reads the xgboost.spark layout (``model/`` text part), and the earlier layout of this
+        package (``data/`` parquet node rows)."""
+        part = Path(path) / "model" / "part-00000"
+        if part.exists():
+            booster = json.loads(part.read_text().splitlines()[0])
+            attrs = booster["learner"].get("attributes", {})
+            if "fdx_trees" in attrs:
+                self._trees = [Tree.from_node_rows(rows) for rows in json.loads(attrs["fdx_trees"])]
+                self.base_margin = float(attrs["fdx_base_margin"])
+                self._num_features = int(booster["learner"]["learner_model_param"]["num_feature"])
+            else:                                   # a booster written by xgboost itself
+                other = SparkXGBClassifierModel.from_xgboost_json(booster)
+                self._trees, self._num_features, self.base_margin = other._trees, other._num_features, \
+                    other.base_margin
+        else:
+            rows = sf.read_data_parquet(path).to_pylist()
+            by_tree: dict = {}
+            for r in rows:
+                by_tree.setdefault(r["treeID"], []).append(r["nodeData"])
+            self._trees = [Tree.from_node_rows(by_tree[k]) for k in sorted(by_tree)]
+            self._num_features = int(md.get("numFeatures", 0))
+            self.base_margin = float(md.get("baseMargin", 0.0))
+        self._arrays = None
+        self.training_seconds = 0.0
+
+    def _save_data_legacy(self, path) -> None:
+        """The round-1 layout (``data/`` parquet node rows + ``xgboost_model.json``), kept for tests
+        of the backward-compatible reader."""
         rows = [{"treeID": t, "nodeData": r} for t, tree in enumerate(self._trees) for r in tree.to_node_rows()]
         sf.write_data_parquet(path, [sf.Field.simple("treeID", "integer"), sf.Field.struct("nodeData", NODE_FIELDS)],
                               rows)
         self.save_xgboost_json(Path(path) / "xgboost_model.json")
-
-    def _load_data(self, path, md) -> None:
-        rows = sf.read_data_parquet(path).to_pylist()
-        by_tree: dict = {}
-        for r in rows:
-            by_tree.setdefault(r["treeID"], []).append(r["nodeData"])
-        self._trees = [Tree.from_node_rows(by_tree[k]) for k in sorted(by_tree)]
-        self._num_features = int(md.get("numFeatures", 0))
-        self.base_margin = float(md.get("baseMargin", 0.0))
-        self._arrays = None
-        self.training_seconds = 0.0
 
     def to_xgboost_json(self) -> dict:
         """XGBoost >= 1.6 JSON model (gbtree, binary:logistic). Split conditions are float32 in

@@ -23,6 +23,17 @@ def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def forced() -> bool:
+    """``FDX_FORCE_COLLECTIVES=1`` with an initialised group of any size (including 1): run every
+    collective through the backend instead of short-circuiting, so a one-GPU box exercises the
+    RCCL reduce-scatter / all-gather path of the trainers."""
+    return (os.environ.get("FDX_FORCE_COLLECTIVES") == "1" and dist.is_available() and dist.is_initialized())
+
+
+def _comm() -> bool:
+    return is_dist() or forced()
+
+
 def world_size() -> int:
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
@@ -37,19 +48,26 @@ def local_rank() -> int:
 
 def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> bool:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT). Returns True if a
-    multi-process group is active."""
+    multi-process group is active. A world-size-1 group is only created in forced-collectives
+    mode (``FDX_FORCE_COLLECTIVES=1``)."""
     if dist.is_initialized():
         return dist.get_world_size() > 1
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1:
+    if ws <= 1 and os.environ.get("FDX_FORCE_COLLECTIVES") != "1":
         return False
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", str(ws))
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend == "nccl":
         torch.cuda.set_device(local_rank() % max(1, torch.cuda.device_count()))
+    if "MASTER_PORT" not in os.environ:
+        from .launch import free_port
+
+        os.environ["MASTER_PORT"] = str(free_port())
     dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
-    return True
+    return ws > 1
 
 
 def backend() -> str:
@@ -64,7 +82,7 @@ def _on_comm_device(t: torch.Tensor):
 
 
 def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
-    if not is_dist():
+    if not _comm():
         return t
     x, moved = _on_comm_device(t.contiguous())
     dist.all_reduce(x, op=op)
@@ -81,7 +99,7 @@ def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
 
 def all_gather_var(*tensors: torch.Tensor) -> tuple:
     """All-gather 1-D tensors of different lengths per rank; returns the concatenation."""
-    if not is_dist():
+    if not _comm():
         return tensors
     dev = tensors[0].device
     n = torch.tensor([tensors[0].numel()], dtype=torch.int64, device=dev)
@@ -132,7 +150,7 @@ def reduce_scatter(x: torch.Tensor) -> torch.Tensor:
     """Sum ``x`` [world, ...] over ranks and return this rank's slice [...]. RCCL
     ``reduce_scatter_tensor`` on nccl (each rank sends (N-1)/N of the buffer instead of an
     all-reduce's 2(N-1)/N); gloo has no reduce-scatter, so it all-reduces and slices."""
-    if not is_dist():
+    if not _comm():
         return x[0]
     x = x.contiguous()
     if backend() == "nccl":
@@ -145,7 +163,7 @@ def reduce_scatter(x: torch.Tensor) -> torch.Tensor:
 
 def all_gather(x: torch.Tensor) -> torch.Tensor:
     """[...] on every rank -> [world, ...] (same shape on every rank)."""
-    if not is_dist():
+    if not _comm():
         return x.unsqueeze(0)
     x = x.contiguous()
     if backend() == "nccl":
@@ -163,7 +181,8 @@ class Collectives:
     """Bundle of the collectives the trainers need (no-ops when not distributed)."""
 
     def __init__(self):
-        self.active = is_dist()
+        self.force = forced()
+        self.active = is_dist() or self.force
         self.world = world_size()
         self.rank = rank()
 

@@ -21,7 +21,7 @@ def _vc(dense):
     return VectorColumn(dense.shape[1], dense=torch.from_numpy(dense))
 
 
-def _train(rank, world, kind):
+def _train(rank, world, kind, device="cpu"):
     from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
     from fraud_detection_spark_kafka_llm_amd.models.lr import train_logistic_regression
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
@@ -31,10 +31,11 @@ def _train(rank, world, kind):
     lo, hi = shard_range(len(y), rank, world)
     vc, yy = _vc(dense[lo:hi]), torch.from_numpy(y[lo:hi])
     if kind == "gbdt":
-        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=6, max_depth=4), device="cpu")
+        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=6, max_depth=4), device=device)
         return [(t.feature.tolist(), t.stats[:, 0].tolist()) for t in r.trees], r.base_margin
     if kind == "rf":
-        r = fit_forest(vc, yy, num_trees=3, max_depth=4, bootstrap=False, feature_subset="sqrt", seed=5, device="cpu")
+        r = fit_forest(vc, yy, num_trees=3, max_depth=4, bootstrap=False, feature_subset="sqrt", seed=5,
+                       device=device)
         return [(t.feature.tolist(), t.stats.tolist()) for t in r.trees], 0.0
     if kind == "lr":
         coef, b, _ = train_logistic_regression(vc, yy.numpy(), max_iter=50, reg_param=0.01, device="cpu")
@@ -106,3 +107,41 @@ def test_parse_cpulist_and_bind_noop_without_gpu():
     assert parse_cpulist("") == []
     if not torch.cuda.is_available():
         assert bind_to_gpu(0)["bound"] is False
+
+
+def _train_counting(rank, world, kind, device):
+    """_train with the backend's reduce-scatter / all-gather / all-reduce calls counted."""
+    import torch.distributed as td
+
+    calls = {"reduce_scatter_tensor": 0, "all_gather_into_tensor": 0, "all_gather": 0, "all_reduce": 0}
+    for name in calls:
+        orig = getattr(td, name)
+
+        def wrapped(*a, _orig=orig, _name=name, **k):
+            calls[_name] += 1
+            return _orig(*a, **k)
+
+        setattr(td, name, wrapped)
+    return _train(rank, world, kind, device), calls
+
+
+@pytest.mark.parametrize("kind", ["gbdt", "rf"])
+def test_forced_collectives_at_world_one_equal_plain_path(kind, monkeypatch):
+    """FDX_FORCE_COLLECTIVES=1 runs the feature-sharded reduce-scatter / all-gather split path on
+    a world-size-1 group (gloo here; RCCL on the GPU box): same trees as the plain path."""
+    single = _train(0, 1, kind)
+    monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
+    (forced, calls), = spawn(_train_counting, 1, kind, "cpu", backend="gloo")
+    assert calls["all_gather"] > 0 and calls["all_reduce"] > 0      # gloo: reduce-scatter = all-reduce + slice
+    assert forced == single
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_forced_collectives_trees_equal_non_dp(monkeypatch):
+    """RCCL (backend nccl) at world size 1: reduce_scatter_tensor / all_gather_into_tensor carry
+    the int64 histogram partials and best-split tuples; the trees equal the non-DP GPU trees."""
+    single = spawn(_train, 1, "gbdt", "cuda:0", backend="gloo")[0]
+    monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
+    (forced, calls), = spawn(_train_counting, 1, "gbdt", "cuda:0", backend="nccl")
+    assert calls["reduce_scatter_tensor"] > 0 and calls["all_gather_into_tensor"] > 0
+    assert forced == single

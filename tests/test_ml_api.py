@@ -97,6 +97,42 @@ def test_xgboost_json_roundtrip(frames, tmp_path):
     assert back.base_margin == pytest.approx(xgbm.base_margin, abs=1e-6)
 
 
+def test_xgboost_spark_writer_layout_and_legacy_reader(frames, tmp_path):
+    """SparkXGBClassifierModel.save writes xgboost.spark's layout (metadata/ + model/part-00000 with
+    the booster JSON); reload is bitwise; the round-1 data/ layout still loads."""
+    import json
+
+    train, test = frames
+    feats_model = Pipeline(stages=_feature_stages()).fit(train)
+    tr, te = feats_model.transform(train), feats_model.transform(test)
+    m = SparkXGBClassifier(features_col="features", label_col="labels", n_estimators=6, max_depth=3).fit(tr)
+    path = tmp_path / "xgb"
+    m.save(str(path))
+    assert (path / "metadata" / "part-00000").exists() and (path / "model" / "part-00000").exists()
+    assert not (path / "data").exists()
+    md = json.loads((path / "metadata" / "part-00000").read_text().splitlines()[0])
+    assert md["class"] == "xgboost.spark.core.SparkXGBClassifierModel"
+    booster = json.loads((path / "model" / "part-00000").read_text().splitlines()[0])
+    assert booster["learner"]["objective"]["name"] == "binary:logistic"
+    assert len(booster["learner"]["gradient_booster"]["model"]["trees"]) == 6
+    back = SparkXGBClassifierModel.load(str(path))
+    np.testing.assert_array_equal(back.transform(te).column("probability").cpu().numpy(),
+                                  m.transform(te).column("probability").cpu().numpy())
+    # a booster without this engine's attributes (as xgboost writes it) loads through the JSON trees
+    del booster["learner"]["attributes"]["fdx_trees"], booster["learner"]["attributes"]["fdx_base_margin"]
+    (path / "model" / "part-00000").write_text(json.dumps(booster) + "\n")
+    plain = SparkXGBClassifierModel.load(str(path))
+    np.testing.assert_allclose(plain.transform(te).column("probability").cpu().numpy(),
+                               m.transform(te).column("probability").cpu().numpy(), rtol=1e-6)
+    # legacy layout
+    legacy = tmp_path / "legacy"
+    m._save_metadata(legacy)
+    m._save_data_legacy(legacy)
+    old = SparkXGBClassifierModel.load(str(legacy))
+    np.testing.assert_array_equal(old.transform(te).column("probability").cpu().numpy(),
+                                  m.transform(te).column("probability").cpu().numpy())
+
+
 def test_lr_trainer_converges_on_separable_margin():
     from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
     from fraud_detection_spark_kafka_llm_amd.models.lr import train_logistic_regression
