@@ -60,11 +60,12 @@ fdx::QuantArgs quant_args(const optional<Tensor>& g, const optional<Tensor>& h, 
 // out_max[2] (float64) = max |statistic| over the rows (exponent choice; all-reduce MAX under DP)
 void quant_max(const optional<Tensor>& g, const optional<Tensor>& h, const optional<Tensor>& label,
                const optional<Tensor>& weight, int64_t seed, int64_t tree, bool bootstrap, int64_t mode, int64_t N,
-               const Tensor& out_max) {
+               const Tensor& out_max, int64_t row0) {
   const auto dev = out_max.device();
   chk(out_max, dev, at::kDouble, "out_max");
   FDX_CHECK(out_max.numel() == 2, "out_max must have 2 entries");
   fdx::QuantArgs a = quant_args(g, h, label, weight, seed, tree, bootstrap, mode, dev, N);
+  a.row0 = row0;
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_quant_max(a, out_max.data_ptr<double>(), stream(dev));
@@ -79,7 +80,7 @@ void quant_max(const optional<Tensor>& g, const optional<Tensor>& h, const optio
 void quant(const optional<Tensor>& g, const optional<Tensor>& h, const optional<Tensor>& label,
            const optional<Tensor>& weight, int64_t seed, int64_t tree, bool bootstrap, int64_t mode, int64_t np,
            const optional<Tensor>& max_abs, const Tensor& rowdig, const Tensor& kexp, const Tensor& totals,
-           const optional<Tensor>& digp) {
+           const optional<Tensor>& digp, int64_t row0) {
   const auto dev = rowdig.device();
   chk(rowdig, dev, at::kInt, "rowdig");
   chk(kexp, dev, at::kInt, "kexp");
@@ -91,6 +92,7 @@ void quant(const optional<Tensor>& g, const optional<Tensor>& h, const optional<
   FDX_CHECK(np == 4 || !max_abs, "np == 1 is for integer counts (exponent 0, no max_abs)");
   fdx::QuantArgs a = quant_args(g, h, label, weight, seed, tree, bootstrap, mode, dev, rowdig.size(0));
   a.np = (int32_t)np;
+  a.row0 = row0;
   a.kexp_out = kexp.data_ptr<int32_t>();
   a.rowdig = reinterpret_cast<uint32_t*>(rowdig.data_ptr<int32_t>());
   a.totals = totals.data_ptr<int64_t>();

@@ -63,6 +63,7 @@ struct QuantArgs {
   int64_t* totals;            // [2] += sum of q over the rows (exact)
   uint8_t* digp;              // optional plane-major copy [2 * np][n_pad] (dense histogram path)
   int64_t n_pad;
+  int64_t row0;               // global index of row 0 of this shard (bootstrap draws are per global row)
 };
 
 struct SlotArgs {
@@ -201,7 +202,7 @@ FDX_HD void row_stats(const QuantArgs& a, int64_t r, double* v0, double* v1) {
     *v1 = (double)a.h[r] * w;
   } else {
     double w = a.weight ? (double)a.weight[r] : 1.0;
-    if (a.bootstrap) w *= (double)poisson1(hash_uniform(a.seed, (uint64_t)a.tree, (uint64_t)r));
+    if (a.bootstrap) w *= (double)poisson1(hash_uniform(a.seed, (uint64_t)a.tree, (uint64_t)(a.row0 + r)));
     const double y = (double)a.label[r];
     *v0 = w * (1.0 - y);
     *v1 = w * y;

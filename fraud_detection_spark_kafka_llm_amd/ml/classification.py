@@ -306,20 +306,32 @@ class _RFParams(_TreeParams):
 
 @register("org.apache.spark.ml.classification.RandomForestClassifier")
 class RandomForestClassifier(_RFParams, Estimator):
+    """``numWorkers`` (extension, not a Spark param): data-parallel rank processes for ``fit``
+    (parallel/estimator_dp.py); never persisted, so saved stages stay loadable by Spark."""
     _uid_prefix = "RandomForestClassifier"
+    _params = [Param("numWorkers", "data-parallel rank processes (extension)", 1, int)]
+    _persist_defaults_only = ("numWorkers",)
 
     def _fit(self, frame: Frame):
         from ..models.tree import fit_forest
+        from ..parallel import dist as D
 
         n = self.getNumTrees()
-        res = fit_forest(frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol()),
-                         num_trees=n, max_depth=self.getMaxDepth(), max_bins=self.getMaxBins(),
-                         min_instances=self.getMinInstancesPerNode(), min_info_gain=self.getMinInfoGain(),
-                         bootstrap=bool(self.getBootstrap()) and n > 1,
-                         feature_subset=self.getFeatureSubsetStrategy(), seed=self.getSeed(),
-                         impurity=self.getImpurity(), subsampling_rate=self.getSubsamplingRate())
-        m = RandomForestClassificationModel(res.trees, res.num_features, uid=self.uid)
-        m._paramMap.update(self._paramMap)
+        kw = dict(num_trees=n, max_depth=self.getMaxDepth(), max_bins=self.getMaxBins(),
+                  min_instances=self.getMinInstancesPerNode(), min_info_gain=self.getMinInfoGain(),
+                  bootstrap=bool(self.getBootstrap()) and n > 1, feature_subset=self.getFeatureSubsetStrategy(),
+                  seed=self.getSeed(), impurity=self.getImpurity(), subsampling_rate=self.getSubsamplingRate())
+        X, y = frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol())
+        nw = int(self.getOrDefault("numWorkers"))
+        if nw > 1 and not D.is_dist():
+            from ..parallel.estimator_dp import fit_data_parallel
+
+            (trees, nf), _ = fit_data_parallel("rf", X, y, None, kw, nw)
+        else:
+            res = fit_forest(X, y, **kw)
+            trees, nf = res.trees, res.num_features
+        m = RandomForestClassificationModel(trees, nf, uid=self.uid)
+        m._paramMap.update({k: v for k, v in self._paramMap.items() if k != "numWorkers"})
         return m
 
 

@@ -3,8 +3,9 @@
 Same constructor surface the reference uses (``features_col, label_col, num_workers, max_depth,
 n_estimators, eval_metric``; /root/reference/fraud_detection_spark.py:76-83) plus the usual XGBoost
 knobs. ``num_workers`` maps to data-parallel ranks: inside a ``torch.distributed`` job each rank
-trains on its row shard and histograms are all-reduced over RCCL (the reference's Rabit ring);
-in a single process it is accepted and ignored.
+trains on its row shard and histograms are reduce-scattered over RCCL (the reference's Rabit
+ring); from a single process ``num_workers > 1`` launches that many rank processes
+(parallel/estimator_dp.py) and returns rank 0's model (identical on every rank).
 
 Outputs follow xgboost.spark: ``rawPrediction = [-margin, margin]``, ``probability = [1-p, p]``,
 ``prediction = p > 0.5``. Models persist in the Spark ML layout (metadata + ``data/`` trees) and
@@ -88,10 +89,23 @@ class SparkXGBClassifier(_XGBParams, Estimator):
                        base_score=self._paramMap.get("base_score"), seed=self.getOrDefault("seed"),
                        deterministic=bool(self.getOrDefault("deterministic")))
         w = frame.column(self.getOrDefault("weight_col")) if self.isSet("weight_col") else None
-        res = fit_gbdt(frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol()), p, weights=w)
-        m = SparkXGBClassifierModel(res.trees, res.num_features, res.base_margin, uid=self.uid)
+        X, y = frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol())
+        nw = int(self.getOrDefault("num_workers"))
+        from ..parallel import dist as D
+
+        if nw > 1 and not D.is_dist():
+            # N rank processes (one per GPU over RCCL, else gloo CPU ranks) behind the watchdog
+            from dataclasses import asdict
+
+            from ..parallel.estimator_dp import fit_data_parallel
+
+            (trees, nf, base, secs), _ = fit_data_parallel("gbdt", X, y, w, asdict(p), nw)
+        else:          # one process, or already one rank of a torchrun job
+            res = fit_gbdt(X, y, p, weights=w)
+            trees, nf, base, secs = res.trees, res.num_features, res.base_margin, res.train_seconds
+        m = SparkXGBClassifierModel(trees, nf, base, uid=self.uid)
         m._paramMap.update(self._paramMap)
-        m.training_seconds = res.train_seconds
+        m.training_seconds = secs
         return m
 
 

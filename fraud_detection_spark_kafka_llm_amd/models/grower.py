@@ -267,13 +267,13 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         seed = int(params.seed)
         if np_ == 4:
             C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
-                             ws.maxabs)
+                             ws.maxabs, Q.row0)
             mx = coll.max(ws.maxabs) if use_coll else ws.maxabs
             C.tree_quant(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, 4, mx, ws.rowdig,
-                         ws.kexp, ws.totals, ws.digp)
+                         ws.kexp, ws.totals, ws.digp, Q.row0)
         else:
             C.tree_quant(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, 1, None, ws.rowdig,
-                         ws.kexp, ws.totals, ws.digp)
+                         ws.kexp, ws.totals, ws.digp, Q.row0)
     tot = coll.sum(ws.totals) if use_coll else ws.totals
     head = torch.cat([tot, ws.kexp.to(torch.int64)]).cpu().numpy()
     stats[0] = head[:2].astype(np.int64)

@@ -137,6 +137,7 @@ class Quantized:
     zbin_host: np.ndarray = None
     fid_host: np.ndarray = None
     kbase_host: np.ndarray = None
+    row0: int = 0                # global index of row 0 (data-parallel shards; bootstrap draws)
 
     @property
     def Fa(self) -> int:  # noqa: N802

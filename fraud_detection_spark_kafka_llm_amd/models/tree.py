@@ -11,6 +11,7 @@ Reference configs: /root/reference/fraud_detection_spark.py:59-74.
 from __future__ import annotations
 
 from dataclasses import dataclass
+from typing import Optional
 
 import numpy as np
 import torch
@@ -48,6 +49,12 @@ def prepare(features, labels, device=None, max_bins: int = 32, coll: Collectives
                      all_reduce_max=coll.max if coll.active else None,
                      all_gather=coll.gather_keys if coll.active else None,
                      **({"chunk": chunk} if chunk else {}))
+    # global index of this shard's first row (contiguous rank-ordered shards): bootstrap draws
+    # are keyed by global row, so a sharded forest equals the single-process one
+    Q.row0 = 0
+    if coll.active:
+        sizes = coll.all_gather(torch.tensor([len(vc)], dtype=torch.int64, device=dev)).view(-1).cpu()
+        Q.row0 = int(sizes[: coll.rank].sum())
     return Q, y, vc.size, vc
 
 
@@ -73,9 +80,17 @@ def prune_same_prediction(t: Tree) -> Tree:
 def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bins: int = 32, min_instances: int = 1,
                min_info_gain: float = 0.0, bootstrap: bool = False, feature_subset: str = "all", seed: int = 0,
                impurity: str = "gini", subsampling_rate: float = 1.0, device=None, weights=None,
-               prune: bool = True) -> ForestResult:
+               prune: bool = True, checkpoint_dir: Optional[str] = None, checkpoint_every: int = 50,
+               resume: bool = False) -> ForestResult:
+    """``checkpoint_dir``: the forest so far is written every ``checkpoint_every`` trees (a usable
+    RandomForestClassificationModel + ``_resume.json``); ``resume=True`` continues from it. Tree
+    t depends only on (seed, t) — bootstrap weights and feature samples are counter-based — so a
+    resumed forest equals an uninterrupted one at any world size."""
+    from ..parallel.checkpoint import EnsembleCheckpointer, maybe_fail
+
     if subsampling_rate != 1.0:
         raise NotImplementedError("subsamplingRate != 1.0 is not supported (Poisson(1) bootstrap only)")
+    ckpt = EnsembleCheckpointer(checkpoint_dir, checkpoint_every, "rf") if checkpoint_dir else None
     coll = Collectives()
     Q, y, F, _ = prepare(features, labels, device, max_bins, coll)
     w = None
@@ -89,9 +104,12 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
                         min_gain=float(min_info_gain), feat_k=0 if k >= F else int(k),
                         seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
     ws = Workspace(Q)
-    trees = []
-    for t in range(num_trees):
+    trees = ckpt.load_trees() if (ckpt is not None and resume) else []
+    for t in range(len(trees), num_trees):
         with tracing.span("forest.tree", tree=t):
             tr = grow_tree(Q, ws, params, t, label=y, weight=w, bootstrap=bootstrap, coll=coll)
         trees.append(prune_same_prediction(tr) if prune else tr.compacted())
+        if ckpt is not None:
+            ckpt.maybe_save(len(trees), trees, 0.0, F, None, force=len(trees) == num_trees)
+        maybe_fail(t)
     return ForestResult(trees, F)

@@ -41,10 +41,15 @@ def parse_fault(spec: Optional[str] = None) -> Optional[dict]:
 
 
 def maybe_fail(tree: int, fault: Optional[dict] = None) -> None:
+    """``attempt:A`` limits the fault to relaunch A of an elastic job; ``hard:1`` kills the
+    process outright (``os._exit``) instead of raising, like a lost GPU or an OOM kill."""
     f = fault if fault is not None else parse_fault()
     if not f or "tree" not in f:
         return
-    if f["tree"] == tree and f.get("rank", dist.rank()) == dist.rank():
+    att = int(os.environ.get("FDX_ATTEMPT", "0"))
+    if f["tree"] == tree and f.get("rank", dist.rank()) == dist.rank() and f.get("attempt", att) == att:
+        if f.get("hard"):
+            os._exit(17)
         raise InjectedFault(f"injected fault at tree {tree} on rank {dist.rank()}")
 
 

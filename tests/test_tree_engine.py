@@ -161,11 +161,11 @@ def _hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, np_=4, g=None, 
     if np_ == 4:
         gg = torch.from_numpy(np.linspace(-1, 1, n).astype(np.float32) if g is None else g).to(dev)
         hh = torch.from_numpy(np.linspace(0.01, 0.25, n).astype(np.float32) if h is None else h).to(dev)
-        C.tree_quant_max(gg, hh, None, None, 0, 0, False, 0, n, ws.maxabs)
-        C.tree_quant(gg, hh, None, None, 0, 0, False, 0, 4, ws.maxabs, ws.rowdig, ws.kexp, ws.totals, ws.digp)
+        C.tree_quant_max(gg, hh, None, None, 0, 0, False, 0, n, ws.maxabs, 0)
+        C.tree_quant(gg, hh, None, None, 0, 0, False, 0, 4, ws.maxabs, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
     else:   # class counts: Poisson(1) bootstrap weights, exact in one digit
         lab = torch.from_numpy((np.arange(n) % 3 == 0).astype(np.float32)).to(dev)
-        C.tree_quant(None, None, lab, None, 5, 2, True, 1, 1, None, ws.rowdig, ws.kexp, ws.totals, ws.digp)
+        C.tree_quant(None, None, lab, None, 5, 2, True, 1, 1, None, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
     hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
     P = slots_per_tile(np_) * 8
     for s0 in range(0, nslots, P):
