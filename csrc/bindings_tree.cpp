@@ -140,10 +140,47 @@ void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, i
 
 // hist[slot_node[s]][boff[f] + b][stat] += exact sums of the quantised statistics of the entries of
 // the listed work items whose row is in slot s of this pass (slot8 = None: root pass, slot 0).
+// RF per-level sampling: thr [n] f64 (k-th smallest priority of each node over 0..F-1) and the
+// union mask [Fa] u8 over the active features fid_orig.
+void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64_t k, const Tensor& fid_orig,
+               const Tensor& thr, const Tensor& mask) {
+  const auto dev = fid_orig.device();
+  chk(nodes, dev, at::kInt, "nodes");
+  chk(fid_orig, dev, at::kLong, "fid_orig");
+  chk(thr, dev, at::kDouble, "thr");
+  chk(mask, dev, at::kByte, "mask");
+  FDX_CHECK(thr.numel() == nodes.numel() && mask.numel() == fid_orig.numel(), "thr [n], mask [Fa]");
+  FDX_CHECK(k >= 1 && F >= 1, "k, F >= 1");
+  if (k >= F) {
+    thr.fill_(1.0);
+    mask.fill_(1);
+    return;
+  }
+  fdx::RfSampleArgs a{};
+  a.seed = (uint64_t)seed;
+  a.tree = (int32_t)tree;
+  a.nodes = nodes.data_ptr<int32_t>();
+  a.nnodes = (int32_t)nodes.numel();
+  a.F = F;
+  a.k = k;
+  a.fid_orig = fid_orig.data_ptr<int64_t>();
+  a.Fa = fid_orig.numel();
+  a.thr = thr.data_ptr<double>();
+  a.mask = mask.data_ptr<uint8_t>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rf_sample(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rf_sample_cpu(a);
+  }
+}
+
 void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
                 const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
                 const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
-                const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np) {
+                const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np,
+                const optional<Tensor>& feat_active) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
@@ -198,6 +235,11 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
     FDX_CHECK(wave_item->numel() % 4 == 0, "wave_item: 4 slots per workgroup");
     a.wave_item = wave_item->data_ptr<int32_t>();
     a.num_slots = (int32_t)wave_item->numel();
+  }
+  if (feat_active) {
+    chk(*feat_active, dev, at::kByte, "feat_active");
+    FDX_CHECK(feat_active->numel() == nbins.numel(), "feat_active must be [Fa] uint8");
+    a.feat_active = feat_active->data_ptr<uint8_t>();
   }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
@@ -428,6 +470,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_quant", &quant);
   m.def("tree_slot8", &slot8);
   m.def("tree_hist_build", &hist_build);
+  m.def("tree_rf_sample", &rf_sample);
   m.def("tree_hist_dense", &hist_dense);
   m.def("tree_dense_fg", &dense_fg);
   m.def("tree_dense_waves", &dense_waves);

@@ -75,6 +75,9 @@ struct HistArgs;
 struct DenseHistArgs;
 struct SplitArgs;
 struct PartitionArgs;
+struct RfSampleArgs;
+void launch_rf_sample(const RfSampleArgs& a, hipStream_t s);
+void rf_sample_cpu(const RfSampleArgs& a);
 void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s);
 void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);

@@ -1,0 +1,118 @@
+// Random-forest per-level feature sampling on the device (X-10, K-14).
+//
+// Spark samples exactly k = ceil(sqrt(F)) feature indices per node without replacement
+// (/root/reference/fraud_detection_spark.py:67-74). Node n keeps the k indices with the smallest
+// counter-based priority u53(seed, tree, n, fid) (csrc/tree.h), so its sample is defined by the
+// k-th smallest priority. rf_threshold_kernel finds it exactly with one workgroup per node: radix
+// passes of 12 bits build LDS histograms of the priorities that still match the selected prefix
+// (priorities are recomputed, never stored), until the k-th element's bucket holds <= CAP
+// candidates; those are gathered into LDS and ranked exactly. With F = 2^18 one pass leaves ~64
+// candidates. rf_mask_kernel then marks the active features any node of the level samples (the
+// histogram work items of unsampled features are skipped). One launch pair per tree level
+// replaces ~40 small torch launches per node.
+#include "ops.h"
+#include "tree.h"
+
+namespace fdx {
+
+namespace {
+constexpr int kThreads = 256;
+constexpr int kRadixBits = 12;
+constexpr int kBuckets = 1 << kRadixBits;
+constexpr int kCap = 2048;
+
+__global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a) {
+  __shared__ uint32_t s_hist[kBuckets];
+  __shared__ uint64_t s_cand[kCap];
+  __shared__ uint32_t s_ncand;
+  __shared__ uint64_t s_prefix;
+  __shared__ int s_known;
+  __shared__ int64_t s_k;
+  __shared__ int64_t s_count;
+
+  const int node = a.nodes[blockIdx.x];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    s_prefix = 0;
+    s_known = 0;
+    s_k = a.k;                // 1-based rank of the wanted priority among those matching the prefix
+    s_count = a.F;
+  }
+  __syncthreads();
+  // radix passes until the wanted bucket is small enough to rank in LDS
+  while (s_count > kCap && s_known < 53) {
+    const int known = s_known;
+    const uint64_t prefix = s_prefix;
+    const int nbits = min(kRadixBits, 53 - known);
+    const int shift = 53 - known - nbits;
+    for (int i = tid; i < kBuckets; i += kThreads) s_hist[i] = 0;
+    __syncthreads();
+    for (int64_t f = tid; f < a.F; f += kThreads) {
+      const uint64_t u = feature_priority_u53(a.seed, a.tree, node, f);
+      if (known == 0 || (u >> (53 - known)) == prefix)
+        atomicAdd(&s_hist[(u >> shift) & ((1u << nbits) - 1)], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int64_t k = s_k, cum = 0;
+      int b = 0;
+      for (; b < (1 << nbits); ++b) {
+        if (cum + (int64_t)s_hist[b] >= k) break;
+        cum += s_hist[b];
+      }
+      s_k = k - cum;
+      s_count = s_hist[b];
+      s_prefix = (prefix << nbits) | (uint64_t)b;
+      s_known = known + nbits;
+    }
+    __syncthreads();
+  }
+  // gather the candidates of the selected prefix and rank them exactly
+  if (tid == 0) s_ncand = 0;
+  __syncthreads();
+  const int known = s_known;
+  const uint64_t prefix = s_prefix;
+  for (int64_t f = tid; f < a.F; f += kThreads) {
+    const uint64_t u = feature_priority_u53(a.seed, a.tree, node, f);
+    if (known == 0 || (u >> (53 - known)) == prefix) {
+      const uint32_t i = atomicAdd(&s_ncand, 1u);
+      if (i < (uint32_t)kCap) s_cand[i] = u;
+    }
+  }
+  __syncthreads();
+  const int n = (int)min(s_ncand, (uint32_t)kCap);
+  const int64_t k = s_k;
+  for (int i = tid; i < n; i += kThreads) {
+    const uint64_t ui = s_cand[i];
+    int64_t less = 0, eq = 0;
+    for (int j = 0; j < n; ++j) {
+      less += s_cand[j] < ui;
+      eq += s_cand[j] == ui;
+    }
+    if (less < k && k <= less + eq)    // ties: every holder of the k-th value writes the same result
+      a.thr[blockIdx.x] = (double)ui * (1.0 / 9007199254740992.0);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
+  const int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (f >= a.Fa) return;
+  const int64_t fid = a.fid_orig[f];
+  uint8_t m = 0;
+  for (int i = 0; i < a.nnodes && !m; ++i) {
+    const uint64_t u = feature_priority_u53(a.seed, a.tree, a.nodes[i], fid);
+    m = ((double)u * (1.0 / 9007199254740992.0) <= a.thr[i]) ? 1 : 0;
+  }
+  a.mask[f] = m;
+}
+}  // namespace
+
+void launch_rf_sample(const RfSampleArgs& a, hipStream_t s) {
+  // k >= F (every feature) is handled by the caller: thresholds 1.0, mask all ones
+  if (a.nnodes <= 0 || a.k >= a.F) return;
+  hipLaunchKernelGGL(rf_threshold_kernel, dim3(a.nnodes), dim3(kThreads), 0, s, a);
+  if (a.Fa > 0)
+    hipLaunchKernelGGL(rf_mask_kernel, dim3((unsigned)((a.Fa + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
+}
+
+}  // namespace fdx

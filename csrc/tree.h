@@ -100,6 +100,23 @@ struct HistArgs {
   int32_t nslots;
   int64_t hist_stride;            // bins per histogram row (TB, or TB + 1 when padded)
   int64_t* hist;                  // [rows][hist_stride][2], accumulated (+=)
+  const uint8_t* feat_active;     // [Fa] optional: items without an active feature are skipped (RF)
+};
+
+// RF per-level feature sampling (rf_kernels.hip / tree_cpu.cpp): for each of `nnodes` nodes the
+// k-th smallest feature_priority over feature indices 0..F-1 (exact, as a 53-bit integer u with
+// priority = u * 2^-53), and the union mask over the active features fid_orig[0..Fa).
+struct RfSampleArgs {
+  uint64_t seed;
+  int32_t tree;
+  const int32_t* nodes;           // [nnodes]
+  int32_t nnodes;
+  int64_t F;
+  int64_t k;
+  const int64_t* fid_orig;        // [Fa]
+  int64_t Fa;
+  double* thr;                    // [nnodes] out
+  uint8_t* mask;                  // [Fa] out
 };
 
 // Dense path for high-density features: dense[d][row] = bin of hot feature d (zbin when absent),
@@ -184,6 +201,23 @@ FDX_HD double hash_uniform(uint64_t a, uint64_t b, uint64_t c) {
 // smallest priorities (exactly k, without replacement).
 FDX_HD double feature_priority(uint64_t seed, int32_t tree, int32_t node, int64_t fid) {
   return hash_uniform(seed ^ 0x5bd1e995ull, ((uint64_t)(uint32_t)tree << 32) | (uint32_t)node, (uint64_t)fid);
+}
+
+// The 53-bit integer behind feature_priority (priority == u * 2^-53 exactly).
+FDX_HD uint64_t feature_priority_u53(uint64_t seed, int32_t tree, int32_t node, int64_t fid) {
+  const uint64_t x = mix64((seed ^ 0x5bd1e995ull) ^
+                           mix64((((uint64_t)(uint32_t)tree << 32) | (uint32_t)node) ^ mix64((uint64_t)fid)));
+  return x >> 11;
+}
+
+// Work item `item` holds at least one active feature (always true without a mask).
+FDX_HD bool item_active(const HistArgs& a, int64_t item) {
+  if (!a.feat_active) return true;
+  const int32_t f0 = a.item_f0[item];
+  const int nf = (a.item_meta[item] >> 8) & 0xFF;
+  for (int j = 0; j < nf; ++j)
+    if (a.feat_active[f0 + j]) return true;
+  return false;
 }
 
 // Poisson(1) draw by inversion of the CDF on a counter-based uniform (at most 32).

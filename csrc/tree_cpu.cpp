@@ -1,6 +1,7 @@
 // Host implementation of the tree engine (same contracts as tree_kernels.hip). Histograms are the
 // same exact int64 sums of quantised statistics as on the device, so host and device trees are
 // bitwise identical.
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <mutex>
@@ -67,9 +68,31 @@ void slot8_cpu(const SlotArgs& a) {
   });
 }
 
+void rf_sample_cpu(const RfSampleArgs& a) {
+  if (a.nnodes <= 0 || a.k >= a.F) return;
+  parallel_for(a.nnodes, 0, 1, [&](int64_t lo, int64_t hi) {
+    std::vector<uint64_t> u((size_t)a.F);
+    for (int64_t i = lo; i < hi; ++i) {
+      for (int64_t f = 0; f < a.F; ++f) u[(size_t)f] = feature_priority_u53(a.seed, a.tree, a.nodes[i], f);
+      std::nth_element(u.begin(), u.begin() + (a.k - 1), u.end());
+      a.thr[i] = (double)u[(size_t)(a.k - 1)] * (1.0 / 9007199254740992.0);
+    }
+  });
+  parallel_for(a.Fa, 0, 4096, [&](int64_t lo, int64_t hi) {
+    for (int64_t f = lo; f < hi; ++f) {
+      uint8_t m = 0;
+      for (int i = 0; i < a.nnodes && !m; ++i)
+        m = ((double)feature_priority_u53(a.seed, a.tree, a.nodes[i], a.fid_orig[f]) * (1.0 / 9007199254740992.0) <=
+             a.thr[i]) ? 1 : 0;
+      a.mask[f] = m;
+    }
+  });
+}
+
 void hist_cpu(const HistArgs& h, int bt, int np) {
   parallel_for(h.num_items, 0, 4, [&](int64_t lo, int64_t hi) {
     for (int64_t it = lo; it < hi; ++it) {
+      if (!item_active(h, it)) continue;
       const int32_t meta = h.item_meta[it];
       const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta), koff = item_koff(meta);
       const int32_t f0 = h.item_f0[it];

@@ -212,6 +212,7 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   const int wslot = blockIdx.x * 4 + wid;
   const int item = a.wave_item ? a.wave_item[wslot] : wslot;
   if (item < 0 || item >= a.num_items) return;
+  if (!item_active(a, item)) return;          // RF: no feature of the item is sampled at this level
   const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
   const int32_t meta = a.item_meta[item];
   const uint32_t koff = (uint32_t)item_koff(meta);

@@ -319,13 +319,6 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         local = {n: i for i, n in enumerate(open_nodes)}
         nl = len(open_nodes)
         nb = len(build)
-        # RF: exact k-of-F feature sample per open node (threshold on the node's priorities)
-        feat_thr = None
-        if params.feat_k:
-            from .rf_sampling import node_thresholds
-
-            feat_thr_all = node_thresholds(Q.num_features, params.seed, tree_index, open_nodes, params.feat_k, dev)
-            feat_thr = feat_thr_all
         if shards is None:
             cur_hist = torch.zeros((nl, TB, 2), dtype=torch.int64, device=dev)
             hist_target, target_of = cur_hist, local
@@ -355,18 +348,21 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         h_bidx = stg.add(np.array([local[n] for n in build], dtype=np.int64))
         up = stg.upload()
         node_slot = up[h_ns] if h_ns is not None else None
+        # RF: exact k-of-F feature sample per open node (k-th smallest priority, on device) and
+        # the level's union mask; histogram items without a sampled feature are skipped
+        feat_thr = feat_mask = None
+        if params.feat_k:
+            feat_thr = torch.empty(nl, dtype=torch.float64, device=dev)
+            feat_mask = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
+            C.tree_rf_sample(int(params.seed), int(tree_index), up[h_ids], int(Q.num_features), int(params.feat_k),
+                             Q.fid_orig, feat_thr, feat_mask)
         # --- histograms, up to `pass_slots` node slots per pass
         with tracing.span("tree.hist"):
-            use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH
+            # RF levels read only the sampled features' CSC items (the dense block would stream
+            # every hot feature for a handful of sampled ones)
+            use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH and not params.feat_k
             sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
             hot_keep = None
-            if feat_thr is not None:
-                from .rf_sampling import level_feature_mask
-
-                mask = level_feature_mask(Q, params.seed, tree_index, open_nodes, feat_thr)
-                sel_groups = [grp.subset(mask) for grp in sel_groups]
-                if use_dense:
-                    hot_keep = mask[torch.from_numpy(Q.hot).to(dev)].cpu().numpy()
             for s0, cnt, h_s2n in passes:
                 slot8 = None
                 if d > 0:
@@ -378,7 +374,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                         continue
                     C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
                                       Q.h_row, Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, up[h_s2n],
-                                      hist_target, TB, grp.bt, ct, np_)
+                                      hist_target, TB, grp.bt, ct, np_, feat_mask)
                 if use_dense:
                     for bt in (1, 2, 4):
                         gfid, gden = ws.dense_groups(bt, C.tree_dense_fg(bt, ct if d > 0 else 1), hot_keep)

@@ -178,7 +178,7 @@ def _hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, np_=4, g=None, 
         ct = pass_ct(np_, cnt)
         for grp in Q.groups:
             C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(), Q.h_row,
-                              Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, hist, Q.TB, grp.bt, ct, np_)
+                              Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, hist, Q.TB, grp.bt, ct, np_, None)
         if Q.dense is not None:   # hot features: dense column-major kernel
             for bt in (1, 2, 4):
                 gfid, gden = ws.dense_groups(bt, C.tree_dense_fg(bt, 1 if root else ct))
@@ -413,3 +413,39 @@ def test_feature_order_is_stable_csc_with_docfreq_and_max(dev):
         np.testing.assert_array_equal(cnt[colptr[f]:colptr[f + 1]], np.minimum(dense[r, f], 255))
     np.testing.assert_array_equal(fo.df.cpu().numpy(), (dense > 0).sum(0))
     np.testing.assert_array_equal(fo.maxc.cpu().numpy(), np.minimum(dense.max(0), 255))
+
+
+def _rf_sample(dev, F=5000, k=71, nodes=(0, 1, 2, 5, 9), seed=123456789, tree=7):
+    from fraud_detection_spark_kafka_llm_amd.ops import native
+
+    fid = torch.arange(0, F, 3, dtype=torch.int64, device=dev)     # a subset of active features
+    nd = torch.tensor(nodes, dtype=torch.int32, device=dev)
+    thr = torch.empty(len(nodes), dtype=torch.float64, device=dev)
+    mask = torch.empty(fid.numel(), dtype=torch.uint8, device=dev)
+    native.lib().tree_rf_sample(seed, tree, nd, F, k, fid, thr, mask)
+    return thr.cpu(), mask.cpu(), fid.cpu()
+
+
+def test_rf_sampling_native_equals_python_oracle():
+    """Exactly k of F features per node: the native k-th smallest priority equals torch.kthvalue
+    over the oracle priorities, and the union mask equals the oracle's."""
+    from fraud_detection_spark_kafka_llm_amd.models.rf_sampling import _priorities, node_thresholds
+
+    F, k, nodes, seed, tree = 5000, 71, [0, 1, 2, 5, 9], 123456789, 7
+    thr, mask, fid = _rf_sample("cpu", F, k, tuple(nodes), seed, tree)
+    ref = node_thresholds(F, seed, tree, nodes, k, torch.device("cpu"))
+    assert torch.equal(thr, ref)
+    for i, n in enumerate(nodes):
+        assert int((_priorities(seed, tree, n, torch.arange(F)) <= thr[i]).sum()) == k
+    want = torch.zeros(fid.numel(), dtype=torch.bool)
+    for i, n in enumerate(nodes):
+        want |= _priorities(seed, tree, n, fid) <= ref[i]
+    assert torch.equal(mask.bool(), want)
+
+
+@pytest.mark.gpu
+def test_gpu_rf_sampling_equals_host():
+    for F, k in ((5000, 71), (1 << 18, 512)):
+        h = _rf_sample("cpu", F, k)
+        g = _rf_sample("cuda:0", F, k)
+        assert torch.equal(h[0], g[0]) and torch.equal(h[1], g[1])
