@@ -104,6 +104,7 @@ def bench_rf(args) -> dict:
     raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()
     p1 = raw[:, 1] / np.maximum(raw.sum(1), 1e-300)
     return {"bench": "rf", "rows": rows, "trees": trees, "depth": 5, "featurize_s": t_feat, "train_s": t_train,
+            "train_only_s": t_train - t_feat,
             "peak_hbm_gb": torch.cuda.max_memory_allocated() / 2 ** 30, "heldout_rows": 200_000,
             **_metrics(ty.cpu().numpy(), p1, (raw[:, 1] > raw[:, 0]).astype(float))}
 
