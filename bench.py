@@ -52,6 +52,7 @@ from fraud_detection_spark_kafka_llm_amd.parallel import dist as D  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.parallel.affinity import bind_to_gpu  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.utils.config import Config  # noqa: E402
 
 METRIC = "dialogues/sec streaming inference + GBDT train sec on 10M rows, 1/2/4/8 GPU"
 F = 1 << 18
@@ -166,7 +167,9 @@ def main():
     ap.add_argument("--kafka-msgs", type=int, default=1_000_000, help="records drained in the Kafka throughput run")
     ap.add_argument("--kafka-rate", type=float, default=300_000, help="paced producer rate of the latency run")
     ap.add_argument("--kafka-sec", type=float, default=2.0, help="duration of the latency run")
+    Config.add_cli_args(ap)          # --gbdt-max-bin, --seed, --config, ... (utils/config.py)
     args = ap.parse_args()
+    cfg = Config.from_cli(args)
 
     D.init_from_env(os.environ.get("FDX_DIST_BACKEND", "nccl"))   # gloo: rehearse N ranks on one GPU
     rank, world = D.rank(), D.world_size()
@@ -191,7 +194,8 @@ def main():
     vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
     vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
     t_feat = time.perf_counter() - t0
-    res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)
+    res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth, max_bin=cfg.gbdt_max_bin),
+                   device=dev)
     sync_all(dev)
     train_sec = max_over_ranks(time.perf_counter() - t0, dev)
     feat_sec = max_over_ranks(t_feat, dev)

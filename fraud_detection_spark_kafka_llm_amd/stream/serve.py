@@ -23,9 +23,9 @@ from http.server import BaseHTTPRequestHandler, HTTPServer
 
 import torch
 
-from ..utils.config import load_dotenv
+from ..utils.config import Config, load_dotenv
 from ..utils.metrics import REGISTRY
-from .kafka import DEFAULT_OUTPUT, get_kafka_consumer, get_kafka_producer
+from .kafka import DEFAULT_OUTPUT, get_kafka_consumer, get_kafka_producer, get_partition_consumers
 
 log = logging.getLogger("fdx.serve")
 
@@ -61,13 +61,19 @@ def main(argv=None) -> int:
     ap.add_argument("--model", default="dialogue_classification_model")
     ap.add_argument("--gpus", type=int, default=1, help="devices of this process (0 = CPU host path)")
     ap.add_argument("--explain", choices=["none", "sync", "async"], default="none")
-    ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--max-latency-ms", type=float, default=5.0)
+    ap.add_argument("--batch", type=int, default=None, help="micro-batch size (default: Config.stream_batch)")
+    ap.add_argument("--max-latency-ms", type=float, default=None, help="default: Config.stream_max_latency_ms")
     ap.add_argument("--max-messages", type=int, default=None)
     ap.add_argument("--idle-timeout", type=float, default=float("inf"), help="exit after this many idle seconds")
     ap.add_argument("--metrics-port", type=int, default=0)
+    ap.add_argument("--partition-readers", action="store_true",
+                    help="one consumer (and reader thread) per input partition instead of one subscriber")
+    Config.add_cli_args(ap)
     args = ap.parse_args(argv)
     load_dotenv()
+    cfg = Config.from_cli(args)
+    args.batch = args.batch if args.batch is not None else cfg.stream_batch
+    args.max_latency_ms = args.max_latency_ms if args.max_latency_ms is not None else cfg.stream_max_latency_ms
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
     if args.gpus > 0 and torch.cuda.is_available():
         devices = [torch.device("cuda", i) for i in range(min(args.gpus, torch.cuda.device_count()))]
@@ -75,7 +81,8 @@ def main(argv=None) -> int:
         devices = [torch.device("cpu")]
     llm = make_llm() if args.explain != "none" else StubLLM()   # no LLM calls without --explain
     agent = ClassificationAgent(args.model, llm=llm, device=devices[0])
-    consumer, producer = get_kafka_consumer(), get_kafka_producer()
+    consumer = get_partition_consumers() if args.partition_readers else get_kafka_consumer()
+    producer = get_kafka_producer()
     out_topic = os.getenv("KAFKA_OUTPUT_TOPIC", DEFAULT_OUTPUT)
     if args.metrics_port:
         start_metrics_server(args.metrics_port)
@@ -85,7 +92,8 @@ def main(argv=None) -> int:
     try:
         stats = eng.run(max_messages=args.max_messages, idle_timeout_s=args.idle_timeout)
     finally:
-        consumer.close()
+        for c in (consumer if isinstance(consumer, list) else [consumer]):
+            c.close()
     print(json.dumps(stats), flush=True)
     return 0
 

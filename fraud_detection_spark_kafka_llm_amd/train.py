@@ -31,6 +31,7 @@ from .ml.evaluation import evaluate_all
 from .ml.xgboost import SparkXGBClassifier
 from .ops.sparse import term_presence_by_label
 from .session import SparkSession
+from .utils.config import Config
 from .utils.logging import get_logger
 
 DATA_URL = ("https://huggingface.co/datasets/BothBosu/multi-agent-scam-conversation/raw/main/"
@@ -139,12 +140,11 @@ def main(argv=None) -> dict:
     ap.add_argument("--synthetic", type=int, default=1600, help="synthetic dialogues when the CSV is unavailable")
     ap.add_argument("--out-dir", default=".")
     ap.add_argument("--model-path", default="fraud_detection_model")
-    ap.add_argument("--num-trees", type=int, default=100)
-    ap.add_argument("--max-depth", type=int, default=5)
-    ap.add_argument("--vocab-size", type=int, default=20000)
     ap.add_argument("--no-plots", action="store_true")
-    ap.add_argument("--seed", type=int, default=42)
+    Config.add_cli_args(ap)          # --num-trees, --max-depth, --vocab-size, --seed, --device, --config ...
     args = ap.parse_args(argv)
+    cfg = Config.from_cli(args)
+    args.num_trees, args.max_depth, args.vocab_size, args.seed = cfg.num_trees, cfg.max_depth, cfg.vocab_size, cfg.seed
 
     spark = initialize_spark()
     try:

@@ -25,9 +25,9 @@ class Config:
     max_depth: int = 5                    # fraud_detection_spark.py:62,71,81
     num_trees: int = 100                  # fraud_detection_spark.py:70,82
     max_bins: int = 32                    # Spark DecisionTree default
-    gbdt_max_bin: int = 64
+    gbdt_max_bin: int = 256               # XGBoost hist default; histograms are exact at any width
     seed: int = 42                        # fraud_detection_spark.py:72,338-339
-    deterministic: bool = False
+    deterministic: bool = True            # training is always bitwise reproducible (exact histograms)
     llm_backend: str = "deepseek"         # deepseek | openai | stub
     llm_base_url: str = "https://api.deepseek.com/v1"   # agent_api.py:36
     llm_model: str = "deepseek-chat"      # agent_api.py:35
@@ -63,22 +63,33 @@ class Config:
 
     @staticmethod
     def add_cli_args(ap: argparse.ArgumentParser) -> None:
+        """``--config FILE.yaml`` plus one ``--<field>`` flag per field (``--num-trees``,
+        ``--stream-batch``, ...) in a "runtime configuration" group; flags the parser already
+        defines are left to it. Precedence: CLI > YAML > ``FDX_*`` environment > defaults."""
+        grp = ap.add_argument_group("runtime configuration (utils/config.py)")
+        if "--config" not in ap._option_string_actions:
+            grp.add_argument("--config", default=None, help="YAML file of Config fields")
         for f in dataclasses.fields(Config):
             if f.name == "extra":
                 continue
             flag = "--" + f.name.replace("_", "-")
+            if flag in ap._option_string_actions:
+                continue
             if f.type in ("bool", bool):
-                ap.add_argument(flag, action="store_true", default=None)
+                grp.add_argument(flag, action=argparse.BooleanOptionalAction, default=None)
             else:
-                ap.add_argument(flag, default=None)
+                grp.add_argument(flag, default=None, help=f"default {f.default!r}")
 
     @classmethod
     def from_cli(cls, ns: argparse.Namespace, base: Optional["Config"] = None) -> "Config":
-        c = base or cls.from_env()
+        path = getattr(ns, "config", None)
+        c = base or (cls.from_yaml(path) if path else cls.from_env())
         for f in dataclasses.fields(cls):
             v = getattr(ns, f.name, None)
             if v is not None and f.name != "extra":
                 setattr(c, f.name, _coerce(f.type, v))
+        if c.device:
+            os.environ["FDX_DEVICE"] = c.device
         return c
 
     def torch_device(self) -> torch.device:
