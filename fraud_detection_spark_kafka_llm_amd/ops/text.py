@@ -336,11 +336,43 @@ def featurize_score(text: PackedText, spec: FeatureSpec, idf: Optional[torch.Ten
                     long_docs.to(torch.int32).contiguous())
     base = text.offsets[:-1] + torch.arange(D, device=device, dtype=torch.int64)
     res = FeatureResult(nnz, ntok, raw, status, idx if want_csr else None, val if want_csr else None, base, spec.dim)
+    if device.type == "cuda" and D:
+        _long_docs_on_device(res, text, host_text, spec, idf_t, lr, trees, want_csr, device)
     if fix_fallbacks and D:
         bad = torch.nonzero(status != STATUS_OK).flatten()
         if bad.numel():
             _finish_on_host(res, host_text, bad.cpu().numpy(), spec, idf, lr, trees, want_csr, flags)
     return res
+
+
+def _long_docs_on_device(res: FeatureResult, text: PackedText, host_text: PackedText, spec, idf_t, lr, trees,
+                         want_csr: bool, device) -> None:
+    """Dialogues over LONG_DOC_BYTES: segmented device path (ops/longdoc.py), patched into ``res``."""
+    from .longdoc import featurize_long
+
+    lens = text.offsets[1:] - text.offsets[:-1]
+    very = torch.nonzero((res.status == STATUS_TOO_LONG) & (lens > LONG_DOC_BYTES)).flatten()
+    if not very.numel():
+        return
+    docs = very.cpu().numpy()
+    host_buf = host_text.data.cpu().numpy() if host_text.data.is_cuda else host_text.data.numpy()
+    done, raw, nnz, ntok, csr = featurize_long(text.data, host_buf, text.offsets.cpu().numpy(), docs, spec, idf_t,
+                                               lr, trees, device)
+    if not done.any():
+        return
+    d = torch.from_numpy(docs[done].astype(np.int64)).to(device)
+    res.raw[d] = raw if raw.shape[1] == res.raw.shape[1] else raw[:, : res.raw.shape[1]]
+    res.nnz[d] = nnz.to(device)
+    res.ntok[d] = ntok.to(device)
+    res.status[d] = STATUS_OK
+    if want_csr:
+        indptr, col, v = csr
+        per = indptr[1:] - indptr[:-1]
+        total = int(indptr[-1])
+        owner = torch.repeat_interleave(torch.arange(per.numel(), device=device), per, output_size=total)
+        pos = res.base[d][owner] + (torch.arange(total, device=device) - indptr[owner])
+        res.idx[pos] = col
+        res.val[pos] = v.to(torch.float32)
 
 
 def _finish_on_host(res: FeatureResult, text: PackedText, bad: np.ndarray, spec, idf, lr, trees,

@@ -42,6 +42,7 @@ class _Stage:
     long_host: torch.Tensor       # int32 pinned [max_docs]: indices of dialogues over LONG_DOC_MIN bytes
     long_dev: torch.Tensor        # its device copy (preallocated: no allocator traffic across streams)
     slot: Optional[Slot] = None
+    very_long: Optional[tuple] = None   # (doc indices, raw [n, K]) of > 64 KB dialogues scored by segments
     n: int = 0
 
 
@@ -97,12 +98,15 @@ class GpuScorer:
         st.slot, st.n = slot, n
         long_idx = None
         n_long = 0
+        very = None
+        st.very_long = None
         if n:
             offs = slot.offsets[: n + 1].numpy()
             lens = offs[1:] - offs[:-1]
             if int(lens.max()) > LONG_DOC_MIN:
                 sel = np.nonzero((lens > LONG_DOC_MIN) & (lens <= LONG_DOC_BYTES))[0]
                 n_long = int(sel.size)
+                very = np.nonzero(lens > LONG_DOC_BYTES)[0]
         # the stage's previous batch has fully drained (collect() synchronised on its event), so
         # its pinned index buffer may be rewritten here
         if n_long:
@@ -127,6 +131,14 @@ class GpuScorer:
                 self.C.featurize_score(*args, None)
                 if long_idx is not None:      # dialogues over 4 KB: long-dialogue kernel, same stream
                     self.C.featurize_score(*args, long_idx)
+                if very is not None and very.size:    # over 64 KB: segmented device path (rare; syncs)
+                    from ..ops.longdoc import featurize_long
+
+                    lr = self.scorer if isinstance(self.scorer, LinearScorer) else None
+                    tr = self.scorer if isinstance(self.scorer, TreeArrays) else None
+                    done, raw_l, *_ = featurize_long(st.text, slot.data.numpy(), offs, very, self.spec, self.idf, lr,
+                                                     tr, self.dev)
+                    st.very_long = (very[done], raw_l.cpu().numpy())
             st.ev_compute.record(self.compute)
             st.ev_d2h = st.ev_compute
         self._inflight.append(st)
@@ -143,6 +155,12 @@ class GpuScorer:
         if copy:
             raw = raw.copy()
         status = st.h_status[:n].numpy()
+        if st.very_long is not None and st.very_long[0].size:
+            docs, vals = st.very_long
+            raw = raw.copy() if not copy else raw
+            raw[docs] = vals
+            status = status.copy()
+            status[docs] = STATUS_OK
         if n and np.any(status != STATUS_OK):
             bad = np.nonzero(status != STATUS_OK)[0]
             sub = PackedText.from_strings([bytes(st.slot.data[int(st.slot.offsets[i]):int(st.slot.offsets[i + 1])]
