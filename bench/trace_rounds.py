@@ -16,6 +16,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--round", type=int, default=6)
     ap.add_argument("--marker", default="logistic_grad")
+    ap.add_argument("--sequence", action="store_true", help="also list the kernels of the round in order")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -35,6 +36,11 @@ def main():
         c[name][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     for name, (n, t) in sorted(c.items(), key=lambda x: -x[1][1]):
         print(f"{t / 1e6:8.3f} ms {n:4d}  {name}")
+    if args.sequence:
+        t0 = int(seg[0]["Start_Timestamp"])
+        for r in seg:
+            a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            print(f"{(a - t0) / 1e6:8.3f} +{(b - a) / 1e6:7.3f} ms  {r['Kernel_Name'][:100]}")
 
 
 if __name__ == "__main__":

@@ -169,6 +169,8 @@ void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64
   a.mask = mask.data_ptr<uint8_t>();
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
+    Tensor scratch = at::empty({fdx::rf_scratch_bytes(a.nnodes)}, fid_orig.options().dtype(at::kByte));
+    a.scratch = scratch.data_ptr<uint8_t>();
     fdx::launch_rf_sample(a, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {

@@ -21,7 +21,37 @@ constexpr int kRadixBits = 12;
 constexpr int kBuckets = 1 << kRadixBits;
 constexpr int kCap = 2048;
 
-__global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a) {
+constexpr int kSlices = 64;       // workgroups per node of the window scan
+
+// Fast path, pass 1: every priority below the window [ulo, uhi] is counted, those inside are
+// appended to the node's candidate list. The window holds the k-th smallest with probability
+// 1 - 1e-15 (+-8 sigma of the binomial count around k); rf_select_kernel checks it and falls back
+// to the exact radix search otherwise.
+__global__ __launch_bounds__(kThreads) void rf_window_kernel(RfSampleArgs a, uint64_t ulo, uint64_t uhi,
+                                                             unsigned int* below, unsigned int* ncand,
+                                                             uint64_t* cand) {
+  __shared__ unsigned int s_below;
+  const int i = blockIdx.y;
+  const int node = a.nodes[i];
+  if (threadIdx.x == 0) s_below = 0;
+  __syncthreads();
+  unsigned int mine = 0;
+  for (int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x; f < a.F; f += (int64_t)gridDim.x * kThreads) {
+    const uint64_t u = feature_priority_u53(a.seed, a.tree, node, f);
+    if (u < ulo) {
+      ++mine;
+    } else if (u <= uhi) {
+      const unsigned int j = atomicAdd(&ncand[i], 1u);
+      if (j < (unsigned int)kCap) cand[(int64_t)i * kCap + j] = u;
+    }
+  }
+  atomicAdd(&s_below, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_below) atomicAdd(&below[i], s_below);
+}
+
+__global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, const unsigned int* below,
+                                                                const unsigned int* ncand, const uint64_t* cand) {
   __shared__ uint32_t s_hist[kBuckets];
   __shared__ uint64_t s_cand[kCap];
   __shared__ uint32_t s_ncand;
@@ -32,6 +62,24 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a) 
 
   const int node = a.nodes[blockIdx.x];
   const int tid = threadIdx.x;
+  if (below != nullptr) {
+    const int64_t r = a.k - (int64_t)below[blockIdx.x];     // rank of the k-th inside the window
+    const int n = (int)ncand[blockIdx.x];
+    if (r >= 1 && r <= n && n <= kCap) {
+      for (int j = tid; j < n; j += kThreads) s_cand[j] = cand[(int64_t)blockIdx.x * kCap + j];
+      __syncthreads();
+      for (int j = tid; j < n; j += kThreads) {
+        const uint64_t uj = s_cand[j];
+        int64_t less = 0, eq = 0;
+        for (int t = 0; t < n; ++t) {
+          less += s_cand[t] < uj;
+          eq += s_cand[t] == uj;
+        }
+        if (less < r && r <= less + eq) a.thr[blockIdx.x] = (double)uj * (1.0 / 9007199254740992.0);
+      }
+      return;                  // uniform per workgroup: every thread took this branch
+    }
+  }
   if (tid == 0) {
     s_prefix = 0;
     s_known = 0;
@@ -110,7 +158,22 @@ __global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s) {
   // k >= F (every feature) is handled by the caller: thresholds 1.0, mask all ones
   if (a.nnodes <= 0 || a.k >= a.F) return;
-  hipLaunchKernelGGL(rf_threshold_kernel, dim3(a.nnodes), dim3(kThreads), 0, s, a);
+  if (a.scratch != nullptr) {
+    // window [lo, hi] of expected counts k -+ (8 sqrt(k) + 8), as 53-bit priorities
+    const double sd = 8.0 * sqrt((double)a.k) + 8.0;
+    const double lo = fmax(0.0, (double)a.k - sd) / (double)a.F, hi = fmin((double)a.F, (double)a.k + sd) / (double)a.F;
+    const uint64_t ulo = (uint64_t)(lo * 9007199254740992.0);
+    const uint64_t uhi = hi >= 1.0 ? (1ull << 53) : (uint64_t)(hi * 9007199254740992.0);
+    unsigned int* below = reinterpret_cast<unsigned int*>(a.scratch);
+    unsigned int* ncand = below + a.nnodes;
+    uint64_t* cand = reinterpret_cast<uint64_t*>(a.scratch + 8 * ((2 * a.nnodes * 4 + 7) / 8));
+    hipMemsetAsync(below, 0, sizeof(unsigned int) * 2 * (size_t)a.nnodes, s);
+    hipLaunchKernelGGL(rf_window_kernel, dim3(kSlices, a.nnodes), dim3(kThreads), 0, s, a, ulo, uhi, below, ncand,
+                       cand);
+    hipLaunchKernelGGL(rf_threshold_kernel, dim3(a.nnodes), dim3(kThreads), 0, s, a, below, ncand, cand);
+  } else {
+    hipLaunchKernelGGL(rf_threshold_kernel, dim3(a.nnodes), dim3(kThreads), 0, s, a, nullptr, nullptr, nullptr);
+  }
   if (a.Fa > 0)
     hipLaunchKernelGGL(rf_mask_kernel, dim3((unsigned)((a.Fa + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
 }

@@ -117,7 +117,10 @@ struct RfSampleArgs {
   int64_t Fa;
   double* thr;                    // [nnodes] out
   uint8_t* mask;                  // [Fa] out
+  uint8_t* scratch;               // device: rf_scratch_bytes(nnodes) for the window fast path (or null)
 };
+
+inline int64_t rf_scratch_bytes(int64_t nnodes) { return 8 * ((2 * nnodes * 4 + 7) / 8) + nnodes * 2048 * 8; }
 
 // Dense path for high-density features: dense[d][row] = bin of hot feature d (zbin when absent),
 // column-major with n_pad (multiple of 64) bytes per feature; the row statistics are streamed from

@@ -19,6 +19,7 @@ exact integers; leaf values / class counts are scaled by 2^-k only when the tree
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 from dataclasses import dataclass
@@ -38,6 +39,10 @@ DENSE_RANGE_ROWS = 32768        # rows per wave of the dense hot-feature histogr
 # levels 0..DENSE_MAX_DEPTH build the hot features' histograms with the dense kernel (every row
 # streamed, slot-masked); deeper levels use their CSC items (only live entries multiplied)
 DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
+# histogram launches of one pass (CSC groups, dense groups) run concurrently on this many HIP
+# streams: they add into disjoint feature ranges with integer atomics, so the order is free and
+# the kernels fill each other's tails
+HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 3))
 
 
 @dataclass
@@ -74,6 +79,26 @@ class Workspace:
         self.Q = Q
         self._shards = None
         self.staging = Staging(dev)
+        self._streams = None
+
+    def run_concurrent(self, launches: list) -> None:
+        """Run the launches on HIST_STREAMS side streams joined back into the current stream
+        (serially on the current stream on the host or with one stream)."""
+        if self.dev.type != "cuda" or HIST_STREAMS <= 1 or len(launches) <= 1:
+            for fn in launches:
+                fn()
+            return
+        if self._streams is None:
+            self._streams = [torch.cuda.Stream(self.dev) for _ in range(HIST_STREAMS)]
+        main = torch.cuda.current_stream(self.dev)
+        start = main.record_event()
+        for i, fn in enumerate(launches):
+            s = self._streams[i % len(self._streams)]
+            s.wait_event(start)
+            with torch.cuda.stream(s):
+                fn()
+        for s in self._streams[:len(launches)]:
+            main.wait_stream(s)
 
     def dense_groups(self, bt: int, fg: int, keep: Optional[np.ndarray] = None):
         """(gfid, gdense) device arrays [ngroups * fg] of the hot features with ``bt`` row tiles
@@ -369,19 +394,24 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                     C.tree_slot8(ws.row_node, node_slot, s0, cnt, ws.slot8)
                     slot8 = ws.slot8
                 ct = pass_ct(np_, cnt)
+                s2n = up[h_s2n]
+                launches = []
                 for grp in sel_groups:
                     if grp.num_items == 0:
                         continue
-                    C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
-                                      Q.h_row, Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, up[h_s2n],
-                                      hist_target, TB, grp.bt, ct, np_, feat_mask)
+                    launches.append(functools.partial(
+                        C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
+                        Q.h_row, Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, hist_target, TB, grp.bt, ct, np_,
+                        feat_mask))
                 if use_dense:
                     for bt in (1, 2, 4):
                         gfid, gden = ws.dense_groups(bt, C.tree_dense_fg(bt, ct if d > 0 else 1), hot_keep)
                         if gfid.numel():
-                            C.tree_hist_dense(Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad, gfid,
-                                              gden, Q.boff, Q.nbins, up[h_s2n], hist_target, TB, Q.n_rows,
-                                              DENSE_RANGE_ROWS, bt, ct, np_)
+                            launches.append(functools.partial(
+                                C.tree_hist_dense, Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad,
+                                gfid, gden, Q.boff, Q.nbins, s2n, hist_target, TB, Q.n_rows, DENSE_RANGE_ROWS, bt,
+                                ct, np_))
+                ws.run_concurrent(launches)
         totals, node_ids = up[h_tot], up[h_ids]
         sub_t = tuple(up[h] for h in h_sub) if h_sub is not None else None
         if shards is None:
