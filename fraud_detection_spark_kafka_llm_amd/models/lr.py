@@ -9,9 +9,10 @@ iterate sequence (Breeze line search, virtual centering) is not reproduced, so c
 Spark only at the optimum ("parity unpinned" for separable data, where both diverge until maxIter).
 
 Hot ops run natively: margins ``X @ (s * beta)`` via ``csrc/sparse_kernels.hip::spmv_kernel`` and
-the gradient ``X^T r`` via ``spmv_t_kernel`` (fp64 atomics into the L2-resident gradient). Under
-data parallelism each rank holds a row shard and the gradient / loss / weight sums are
-all-reduced once per function evaluation (PAR-04).
+the gradient ``X^T r`` as the same row-wise SpMV over ``X^T`` (built once per fit by a stable sort
+of the entries by feature): every output is one fixed-order lane-strided dot product, no atomics,
+so repeated fits are bitwise identical on the GPU. Under data parallelism each rank holds a row
+shard and the gradient / loss / weight sums are all-reduced once per function evaluation (PAR-04).
 """
 from __future__ import annotations
 
@@ -22,9 +23,21 @@ import numpy as np
 import torch
 
 from ..ml.linalg import VectorColumn
-from ..ops.sparse import spmv, spmv_t
+from ..ops.sparse import spmv
 from ..parallel.dist import Collectives
 from ..utils.config import default_device
+
+
+def transpose_csr(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, num_cols: int) -> tuple:
+    """CSR of X^T: entries stably sorted by column, so each column keeps its rows ascending."""
+    n = indptr.numel() - 1
+    counts = indptr[1:] - indptr[:-1]
+    rows = torch.repeat_interleave(torch.arange(n, dtype=torch.int32, device=idx.device), counts,
+                                   output_size=int(idx.numel()))
+    order = torch.sort(idx.to(torch.int64), stable=True).indices
+    t_indptr = torch.zeros(num_cols + 1, dtype=torch.int64, device=idx.device)
+    torch.cumsum(torch.bincount(idx.to(torch.int64), minlength=num_cols), 0, out=t_indptr[1:])
+    return t_indptr, rows[order].contiguous(), val[order].contiguous()
 
 
 def train_logistic_regression(features, labels, weights=None, max_iter: int = 100, tol: float = 1e-6,
@@ -46,11 +59,15 @@ def train_logistic_regression(features, labels, weights=None, max_iter: int = 10
         torch.as_tensor(np.asarray(weights, dtype=np.float64)).to(dev)
     coll = Collectives()
     wsum = float(coll.sum(w.sum().reshape(1))[0])
+    t_indptr, t_idx, t_val = transpose_csr(indptr, idx, val, F)
+
+    def xt(v: torch.Tensor, vals: Optional[torch.Tensor] = None) -> torch.Tensor:     # X^T v, fixed order
+        return spmv(t_indptr, t_idx, t_val if vals is None else vals, v)
 
     # feature scaling (sample std over all ranks)
     if standardization:
-        s1 = coll.sum(spmv_t(indptr, idx, val, w, F))
-        s2 = coll.sum(spmv_t(indptr, idx, val * val, w, F))
+        s1 = coll.sum(xt(w))
+        s2 = coll.sum(xt(w, t_val * t_val))
         mean = s1 / wsum
         var = (s2 - wsum * mean * mean) / max(wsum - 1.0, 1.0)
         std = torch.sqrt(torch.clamp(var, min=0.0))
@@ -64,7 +81,7 @@ def train_logistic_regression(features, labels, weights=None, max_iter: int = 10
         # stable log(1 + e^m) - y m
         loss_i = torch.clamp(m, min=0) - m * y + torch.log1p(torch.exp(-torch.abs(m)))
         r = w * (torch.sigmoid(m) - y)
-        parts = torch.cat([(w * loss_i).sum().reshape(1), r.sum().reshape(1), spmv_t(indptr, idx, val, r, F)])
+        parts = torch.cat([(w * loss_i).sum().reshape(1), r.sum().reshape(1), xt(r)])
         parts = coll.sum(parts)
         loss = parts[0] / wsum + 0.5 * reg_param * torch.dot(beta, beta)
         g = torch.empty_like(theta)
