@@ -322,7 +322,9 @@ class RandomForestClassifier(_RFParams, Estimator):
                   bootstrap=bool(self.getBootstrap()) and n > 1, feature_subset=self.getFeatureSubsetStrategy(),
                   seed=self.getSeed(), impurity=self.getImpurity(), subsampling_rate=self.getSubsamplingRate())
         X, y = frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol())
-        nw = int(self.getOrDefault("numWorkers"))
+        from ..parallel.estimator_dp import effective_workers
+
+        nw = effective_workers(self.getOrDefault("numWorkers"), len(X))
         if nw > 1 and not D.is_dist():
             from ..parallel.estimator_dp import fit_data_parallel
 

@@ -90,9 +90,10 @@ class SparkXGBClassifier(_XGBParams, Estimator):
                        deterministic=bool(self.getOrDefault("deterministic")))
         w = frame.column(self.getOrDefault("weight_col")) if self.isSet("weight_col") else None
         X, y = frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol())
-        nw = int(self.getOrDefault("num_workers"))
         from ..parallel import dist as D
+        from ..parallel.estimator_dp import effective_workers
 
+        nw = effective_workers(self.getOrDefault("num_workers"), len(X))
         if nw > 1 and not D.is_dist():
             # N rank processes (one per GPU over RCCL, else gloo CPU ranks) behind the watchdog
             from dataclasses import asdict

@@ -84,6 +84,21 @@ def _worker(rank: int, world: int, tmp: str, kind: str, kw: dict, dev_kind: str,
     raise ValueError(kind)
 
 
+def effective_workers(num_workers: int, n_rows: int, device=None) -> int:
+    """Rank processes worth launching: one per GPU at most when GPUs are used (never several
+    ranks on one device), and none below ``FDX_DP_MIN_ROWS`` rows per rank (default 100000) —
+    a process launch costs more than training such a shard, and the model is bitwise the same
+    either way (exact histograms)."""
+    n = int(num_workers)
+    dev = torch.device(device) if device is not None else None
+    if (dev is not None and dev.type == "cuda") or (dev is None and torch.cuda.is_available()):
+        n = min(n, max(1, torch.cuda.device_count()))
+    min_rows = int(os.environ.get("FDX_DP_MIN_ROWS", "100000"))
+    if min_rows > 0:
+        n = min(n, max(1, n_rows // min_rows))
+    return max(1, n)
+
+
 def fit_data_parallel(kind: str, vc, labels, weights, kw: dict, num_workers: int, device=None,
                       checkpoint_dir: Optional[str] = None, checkpoint_every: int = 10, min_workers: int = 1):
     """Train ``kind`` ("gbdt" | "rf") on ``num_workers`` rank processes; returns rank 0's result

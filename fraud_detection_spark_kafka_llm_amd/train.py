@@ -88,18 +88,45 @@ def make_classifiers(num_trees: int = 100, max_depth: int = 5, seed: int = 42) -
     }
 
 
-def train_models(train_df: Frame, feature_stages: list, classifiers: Optional[dict] = None) -> dict:
-    """Fit the feature stages once, then every classifier on the shared feature matrix."""
+def train_models(train_df: Frame, feature_stages: list, classifiers: Optional[dict] = None,
+                 concurrent: Optional[bool] = None) -> dict:
+    """Fit the feature stages once, then every classifier on the shared feature matrix.
+
+    On a GPU the classifiers train concurrently (PAR-07): one host thread and one HIP stream per
+    fit, so the small per-level kernels of DT, RF and GBDT fill each other's gaps (the reference
+    fits them one after another, fraud_detection_spark.py:86-97). ``FDX_CONCURRENT_FITS=0`` or
+    ``concurrent=False`` fits sequentially; the models are identical either way."""
+    from .utils.config import default_device
+
     classifiers = classifiers or make_classifiers()
     feat_model = Pipeline(stages=feature_stages).fit(train_df)
     feats = feat_model.transform(train_df)
-    models = {}
-    for name, clf in classifiers.items():
+    dev = default_device()
+    if concurrent is None:
+        concurrent = dev.type == "cuda" and os.environ.get("FDX_CONCURRENT_FITS", "1") == "1"
+
+    def fit_one(name, clf):
         t0 = time.perf_counter()
-        m = clf.fit(feats)
+        if concurrent:
+            stream = torch.cuda.Stream(dev)
+            with torch.cuda.stream(stream):
+                m = clf.fit(feats)
+            stream.synchronize()
+        else:
+            m = clf.fit(feats)
         log.info("trained %s in %.3fs", name, time.perf_counter() - t0)
-        models[name] = PipelineModel(list(feat_model.stages) + [m])
-    return models
+        return m
+
+    if concurrent and len(classifiers) > 1:
+        import concurrent.futures as cf
+
+        torch.cuda.synchronize(dev)            # features ready before the side streams read them
+        with cf.ThreadPoolExecutor(max_workers=len(classifiers)) as pool:
+            futs = {name: pool.submit(fit_one, name, clf) for name, clf in classifiers.items()}
+            fitted = {name: f.result() for name, f in futs.items()}
+    else:
+        fitted = {name: fit_one(name, clf) for name, clf in classifiers.items()}
+    return {name: PipelineModel(list(feat_model.stages) + [fitted[name]]) for name in classifiers}
 
 
 def evaluate_model(model: PipelineModel, datasets: dict) -> dict:

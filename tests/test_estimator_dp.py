@@ -27,6 +27,19 @@ def _sig(model):
     return [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in model.trees]
 
 
+@pytest.fixture(autouse=True)
+def _dp_on_small_data(monkeypatch):
+    monkeypatch.setenv("FDX_DP_MIN_ROWS", "0")      # launch ranks even for these tiny frames
+
+
+def test_effective_workers_policy(monkeypatch):
+    from fraud_detection_spark_kafka_llm_amd.parallel.estimator_dp import effective_workers
+
+    assert effective_workers(4, 10, "cpu") == 4
+    monkeypatch.setenv("FDX_DP_MIN_ROWS", "1000")
+    assert effective_workers(4, 2500, "cpu") == 2 and effective_workers(4, 500, "cpu") == 1
+
+
 @pytest.mark.parametrize("workers", [2, 3])
 def test_xgb_num_workers_trains_identical_trees(workers):
     df = _frame()
