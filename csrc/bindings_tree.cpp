@@ -178,6 +178,110 @@ void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64
   }
 }
 
+// RF batch rows: rw [N, kRfTrees * 2] u8 class counts, totals [kRfTrees, 2] int64 (+=)
+void rf_rows(const Tensor& label, const Tensor& tree_ids, int64_t seed, bool bootstrap, int64_t row0,
+             const Tensor& rw, const Tensor& totals) {
+  const auto dev = label.device();
+  chk(label, dev, at::kFloat, "label");
+  chk(tree_ids, dev, at::kInt, "tree_ids");
+  chk(rw, dev, at::kByte, "rw");
+  chk(totals, dev, at::kLong, "totals");
+  FDX_CHECK(tree_ids.numel() == fdx::kRfTrees && totals.numel() == 2 * fdx::kRfTrees, "tree_ids / totals size");
+  FDX_CHECK(rw.numel() == label.numel() * 2 * fdx::kRfTrees, "rw must be [N, 2 * kRfTrees]");
+  fdx::RfRowsArgs a{label.data_ptr<float>(), tree_ids.data_ptr<int32_t>(), (uint64_t)seed, bootstrap ? 1 : 0, row0,
+                    label.numel(), rw.data_ptr<uint8_t>(), totals.data_ptr<int64_t>()};
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rf_rows(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rf_rows_cpu(a);
+  }
+}
+
+// RF batch pass slots: rs [N, kRfTrees] u8 from row_node [kRfTrees, N] and node_slot [kRfTrees, M]
+void rf_slots(const Tensor& row_node, const Tensor& node_slot, int64_t s0, int64_t cnt, const Tensor& rs) {
+  const auto dev = row_node.device();
+  chk(row_node, dev, at::kInt, "row_node");
+  chk(node_slot, dev, at::kInt, "node_slot");
+  chk(rs, dev, at::kByte, "rs");
+  FDX_CHECK(row_node.dim() == 2 && row_node.size(0) == fdx::kRfTrees && node_slot.dim() == 2 &&
+                node_slot.size(0) == fdx::kRfTrees && rs.numel() == row_node.size(1) * fdx::kRfTrees,
+            "row_node [kRfTrees, N], node_slot [kRfTrees, M], rs [N, kRfTrees]");
+  FDX_CHECK(cnt >= 0 && cnt <= 64, "at most 64 slots per pass");
+  fdx::RfSlotsArgs a{row_node.data_ptr<int32_t>(), node_slot.data_ptr<int32_t>(), (int32_t)node_slot.size(1),
+                     (int32_t)s0, (int32_t)cnt, row_node.size(1), rs.data_ptr<uint8_t>()};
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rf_slots(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rf_slots_cpu(a);
+  }
+}
+
+// Multi-tree RF histogram pass (hist_rf_kernel): slot_node / slot_tree [nslots <= 8 * ct]
+void hist_rf(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
+             const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key, const Tensor& rs,
+             const Tensor& rw, const Tensor& boff, const Tensor& nbins, const Tensor& slot_node,
+             const Tensor& slot_tree, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct,
+             const optional<Tensor>& feat_active) {
+  const auto dev = csc_row.device();
+  chk(item_start, dev, at::kLong, "item_start");
+  chk(item_end, dev, at::kLong, "item_end");
+  chk(item_f0, dev, at::kInt, "item_f0");
+  chk(item_meta, dev, at::kInt, "item_meta");
+  chk(csc_row, dev, at::kInt, "csc_row");
+  chk(csc_key, dev, at::kByte, "csc_key");
+  chk(rs, dev, at::kByte, "rs");
+  chk(rw, dev, at::kByte, "rw");
+  chk(boff, dev, at::kLong, "boff");
+  chk(nbins, dev, at::kInt, "nbins");
+  chk(slot_node, dev, at::kInt, "slot_node");
+  chk(slot_tree, dev, at::kInt, "slot_tree");
+  chk(hist, dev, at::kLong, "hist");
+  FDX_CHECK(bt == 1 || bt == 2 || bt == 4, "bt in {1,2,4}");
+  FDX_CHECK(ct == 1 || ct == 2 || ct == 4 || ct == 8, "ct in {1,2,4,8}");
+  FDX_CHECK(slot_node.numel() <= 8 * ct && slot_tree.numel() == slot_node.numel(), "slots <= 8 * ct");
+  FDX_CHECK(rs.numel() == rw.numel() / 2 && rs.numel() % fdx::kRfTrees == 0, "rs [N, kRfTrees], rw [N, 2 kRfTrees]");
+  FDX_CHECK(hist.dim() == 3 && hist.size(1) >= TB && hist.size(2) == 2, "hist [rows, >= TB, 2]");
+  FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_key, 4), "CSC views need 4 readable padding entries");
+  fdx::HistArgs a{};
+  a.item_start = item_start.data_ptr<int64_t>();
+  a.item_end = item_end.data_ptr<int64_t>();
+  a.item_f0 = item_f0.data_ptr<int32_t>();
+  a.item_meta = item_meta.data_ptr<int32_t>();
+  a.num_items = (int32_t)item_start.numel();
+  a.csc_row = csc_row.data_ptr<int32_t>();
+  a.csc_key = csc_key.data_ptr<uint8_t>();
+  a.boff = boff.data_ptr<int64_t>();
+  a.nbins = nbins.data_ptr<int32_t>();
+  a.slot_node = slot_node.data_ptr<int32_t>();
+  a.nslots = (int32_t)slot_node.numel();
+  a.hist_stride = hist.size(1);
+  a.hist = hist.data_ptr<int64_t>();
+  a.rf_rs = rs.data_ptr<uint8_t>();
+  a.rf_rw = rw.data_ptr<uint8_t>();
+  a.rf_slot_tree = slot_tree.data_ptr<int32_t>();
+  if (wave_item) {
+    chk(*wave_item, dev, at::kInt, "wave_item");
+    a.wave_item = wave_item->data_ptr<int32_t>();
+    a.num_slots = (int32_t)wave_item->numel();
+  }
+  if (feat_active) {
+    chk(*feat_active, dev, at::kByte, "feat_active");
+    FDX_CHECK(feat_active->numel() == nbins.numel(), "feat_active must be [Fa] uint8");
+    a.feat_active = feat_active->data_ptr<uint8_t>();
+  }
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_hist_rf(a, (int)bt, (int)ct, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::hist_rf_cpu(a, (int)bt);
+  }
+}
+
 void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
                 const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
                 const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
@@ -339,7 +443,7 @@ void hist_subtract(const Tensor& parent, const Tensor& cur, const Tensor& dst, c
 void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, const Tensor& nbins, const Tensor& zbin,
                 const Tensor& fid_orig, const Tensor& node_ids, const Tensor& kexp, int64_t mode, double lambda_,
                 double mcw, const optional<Tensor>& feat_thr, int64_t seed, int64_t tree, const Tensor& out_gain,
-                const Tensor& out_bin, const Tensor& out_left) {
+                const Tensor& out_bin, const Tensor& out_left, const optional<Tensor>& node_tree) {
   const auto dev = hist.device();
   chk(hist, dev, at::kLong, "hist");
   chk(totals, dev, at::kLong, "totals");
@@ -375,6 +479,11 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
   a.feat_thr = opt<double>(feat_thr);
   a.seed = (uint64_t)seed;
   a.tree = (int32_t)tree;
+  if (node_tree) {
+    chk(*node_tree, dev, at::kInt, "node_tree");
+    FDX_CHECK(node_tree->numel() >= nodes, "node_tree size");
+    a.node_tree = node_tree->data_ptr<int32_t>();
+  }
   a.out_gain = out_gain.data_ptr<double>();
   a.out_bin = out_bin.data_ptr<int32_t>();
   a.out_left = out_left.data_ptr<int64_t>();
@@ -473,6 +582,9 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_slot8", &slot8);
   m.def("tree_hist_build", &hist_build);
   m.def("tree_rf_sample", &rf_sample);
+  m.def("tree_rf_rows", &rf_rows);
+  m.def("tree_rf_slots", &rf_slots);
+  m.def("tree_hist_rf", &hist_rf);
   m.def("tree_hist_dense", &hist_dense);
   m.def("tree_dense_fg", &dense_fg);
   m.def("tree_dense_waves", &dense_waves);

@@ -101,6 +101,35 @@ struct HistArgs {
   int64_t hist_stride;            // bins per histogram row (TB, or TB + 1 when padded)
   int64_t* hist;                  // [rows][hist_stride][2], accumulated (+=)
   const uint8_t* feat_active;     // [Fa] optional: items without an active feature are skipped (RF)
+  // multi-tree RF passes (hist_rf_kernel): kRfTrees trees per pass, row-major per-row records
+  const uint8_t* rf_rs;           // [N][kRfTrees] pass slot of the row in tree j (0xff: none)
+  const uint8_t* rf_rw;           // [N][kRfTrees][2] class counts (Poisson weight x indicator, <= 32)
+  const int32_t* rf_slot_tree;    // [nslots] tree (0..kRfTrees-1) of each pass slot
+};
+
+constexpr int kRfTrees = 8;       // trees per multi-tree RF batch (one 8-byte slot record per row)
+
+// Per-row records of an RF batch: rw[row][j] = (w (1 - y), w y) with w = Poisson(1) draw of
+// (seed, tree_ids[j], row0 + row) (1 without bootstrap); totals[j] = column sums (root counts).
+struct RfRowsArgs {
+  const float* label;             // [N]
+  const int32_t* tree_ids;        // [kRfTrees] (-1: unused)
+  uint64_t seed;
+  int32_t bootstrap;
+  int64_t row0;
+  int64_t N;
+  uint8_t* rw;                    // [N][kRfTrees][2]
+  int64_t* totals;                // [kRfTrees][2] +=
+};
+
+// rs[row][j] = node_slot[j][row_node[j][row]] - s0 when inside [0, cnt), else 0xff.
+struct RfSlotsArgs {
+  const int32_t* row_node;        // [kRfTrees][N]
+  const int32_t* node_slot;       // [kRfTrees][max_nodes] pass-global slot (-1: none)
+  int32_t max_nodes;
+  int32_t s0, cnt;
+  int64_t N;
+  uint8_t* rs;                    // [N][kRfTrees]
 };
 
 // RF per-level feature sampling (rf_kernels.hip / tree_cpu.cpp): for each of `nnodes` nodes the
@@ -164,6 +193,7 @@ struct SplitArgs {
   const double* feat_thr;         // RF: [nodes] sampling threshold (feature kept iff u <= thr); nullptr: all
   uint64_t seed;
   int32_t tree;
+  const int32_t* node_tree;       // RF batches: [nodes] tree index of each node (nullptr: `tree`)
   double* out_gain;               // [nodes][Fa]
   int32_t* out_bin;               // [nodes][Fa]
   int64_t* out_left;              // [nodes][Fa][2]

@@ -236,7 +236,7 @@ class FeatureShards:
 
 
 def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, params, feat_thr, tree_index, Fa,
-                 f0):
+                 f0, node_tree=None):
     """Per node: (gain float64, feature (+f0) int64, bin int64, left sums int64 [2]) of the best
     split over Fa features of ``hist`` [nodes, boff[Fa], 2]; gain -inf without a valid candidate.
     Returned as one int64 tensor [nodes, 5] (gain bit-cast) for a single device->host copy."""
@@ -252,8 +252,12 @@ def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, p
     out_left = torch.empty((nl, Fa, 2), dtype=torch.int64, device=dev)
     C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, int(params.mode),
                       float(params.lambda_), float(params.min_child), feat_thr, int(params.seed), int(tree_index),
-                      out_gain, out_bin, out_left)
-    best_gain, best_f = torch.max(out_gain, dim=1)
+                      out_gain, out_bin, out_left, node_tree)
+    # best gain per node, ties to the lowest feature index (deterministic whatever the batch shape)
+    best_gain = torch.max(out_gain, dim=1).values
+    cand = torch.arange(Fa, device=dev).expand(nl, Fa)
+    best_f = torch.where(out_gain == best_gain[:, None], cand, Fa).min(dim=1).values
+    best_f = torch.where(best_f >= Fa, 0, best_f)
     ar = torch.arange(nl, device=dev)
     best_bin = out_bin[ar, best_f].to(torch.int64)
     best_left = out_left[ar, best_f]
@@ -284,8 +288,6 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     pass_slots = spt * MAX_CT
     max_nodes = 2 ** (params.max_depth + 1)
     # host node table
-    parent, depth, feature, binv, thr = [-1], [0], [-1], [-1], [0.0]
-    left, right, gain, stats, is_leaf = [-1], [-1], [-1.0], [None], [False]
 
     ws.row_node.zero_()
     with tracing.span("tree.quant"):
@@ -301,7 +303,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                          ws.kexp, ws.totals, ws.digp, Q.row0)
     tot = coll.sum(ws.totals) if use_coll else ws.totals
     head = torch.cat([tot, ws.kexp.to(torch.int64)]).cpu().numpy()
-    stats[0] = head[:2].astype(np.int64)
+    tab = TreeTable(head[:2].astype(np.int64))
+    parent, left, right, stats, is_leaf = tab.parent, tab.left, tab.right, tab.stats, tab.is_leaf
     kexp = head[2:4].astype(np.int64)
     scale = np.ldexp(1.0, -kexp)                    # value of one quantisation step per statistic
     level = [0]
@@ -438,6 +441,29 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 best_s = torch.argmax(gains, dim=0)                           # ties -> lowest shard = lowest feature
                 packed = allt[best_s, torch.arange(nl, device=dev)].cpu().numpy()
         # --- create children
+        next_level, default_child, splits = tab.apply_splits(open_nodes, packed, d, Q, params, scale, max_nodes)
+        if splits:
+            with tracing.span("tree.partition"):
+                _partition(C, Q, ws, default_child, splits)
+        prev_hist = cur_hist
+        prev_index = local
+        level = next_level
+
+    return tab.build(Q, params, scale)
+
+
+class TreeTable:
+    """Host node table of one tree under construction (shared by grow_tree and the multi-tree RF
+    batches, so both create exactly the same nodes from the same best-split tuples)."""
+
+    def __init__(self, root_stats: np.ndarray):
+        self.parent, self.depth, self.feature, self.binv, self.thr = [-1], [0], [-1], [-1], [0.0]
+        self.left, self.right, self.gain, self.stats, self.is_leaf = [-1], [-1], [-1.0], [root_stats], [False]
+
+    def apply_splits(self, open_nodes: list, packed: np.ndarray, d: int, Q: Quantized, params: GrowParams,
+                     scale: np.ndarray, max_nodes: int) -> tuple:
+        """Best-split tuples [len(open_nodes), 5] -> children; returns (next level, default child
+        table [max_nodes], partition splits)."""
         next_level = []
         default_child = np.full(max_nodes, -1, dtype=np.int32)
         splits = []
@@ -451,64 +477,62 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             else:
                 ok = ok and gval > 0.0 and gval >= params.min_gain
             if not ok:
-                is_leaf[n] = True
+                self.is_leaf[n] = True
                 continue
             tl = packed[i, 3:5].astype(np.int64)
-            tr = stats[n] - tl
-            li, ri = len(parent), len(parent) + 1
-            for child, st in ((li, tl), (ri, tr)):
-                parent.append(n)
-                depth.append(d + 1)
-                feature.append(-1)
-                binv.append(-1)
-                thr.append(0.0)
-                left.append(-1)
-                right.append(-1)
-                gain.append(-1.0)
-                stats.append(st)
+            tr = self.stats[n] - tl
+            li, ri = len(self.parent), len(self.parent) + 1
+            for st in (tl, tr):
+                self.parent.append(n)
+                self.depth.append(d + 1)
+                self.feature.append(-1)
+                self.binv.append(-1)
+                self.thr.append(0.0)
+                self.left.append(-1)
+                self.right.append(-1)
+                self.gain.append(-1.0)
+                self.stats.append(st)
                 leafy = (d + 1 >= params.max_depth)
                 if params.mode != 0:
                     leafy = leafy or _impurity(st * scale, params.mode) == 0.0
-                is_leaf.append(leafy)
-            feature[n], binv[n], thr[n], left[n], right[n], gain[n] = fid, b, Q.threshold(fid, b), li, ri, gval
+                self.is_leaf.append(leafy)
+            self.feature[n], self.binv[n], self.thr[n] = fid, b, Q.threshold(fid, b)
+            self.left[n], self.right[n], self.gain[n] = li, ri, gval
             left_default = int(Q.zbin_host[fid]) <= b
             dflt, other = (li, ri) if left_default else (ri, li)
             default_child[n] = dflt
             splits.append((fid, dflt, other, b, int(left_default)))
             next_level += [li, ri]
-        if splits:
-            with tracing.span("tree.partition"):
-                _partition(C, Q, ws, default_child, splits)
-        prev_hist = cur_hist
-        prev_index = local
-        level = next_level
+        return next_level, default_child, splits
 
-    n = len(parent)
-    st = np.zeros((n, 2), dtype=np.float64)
-    for i in range(n):
-        st[i] = stats[i].astype(np.float64) * scale
-    feat_orig = np.array([int(Q.fid_host[f]) if f >= 0 and not is_leaf[i] else -1 for i, f in enumerate(feature)],
-                         dtype=np.int32)
-    left_a = np.array([lc if not is_leaf[i] else -1 for i, lc in enumerate(left)], dtype=np.int32)
-    right_a = np.array([rc if not is_leaf[i] else -1 for i, rc in enumerate(right)], dtype=np.int32)
-    thr_a = np.array(thr, dtype=np.float64)
-    gain_a = np.array([gv if not is_leaf[i] else -1.0 for i, gv in enumerate(gain)], dtype=np.float64)
-    if params.mode == 0:
-        G, H = st[:, 0], st[:, 1]
-        w = -G / (H + params.lambda_)
-        if params.max_delta_step > 0:
-            w = np.clip(w, -params.max_delta_step, params.max_delta_step)
-        value = params.eta * w
-        imp = np.zeros(n)
-        pred = value
-        stats_out = np.stack([value, H], 1)
-        raw_count = np.zeros(n, dtype=np.int64)
-    else:
-        imp = np.array([_impurity(s, params.mode) for s in st])
-        pred = np.argmax(st, axis=1).astype(np.float64)
-        stats_out = st
-        raw_count = np.rint(st.sum(1)).astype(np.int64)
-    return Tree(feat_orig, thr_a, left_a, right_a, stats_out, imp, gain_a, raw_count, pred, 0)
+    def build(self, Q: Quantized, params: GrowParams, scale: np.ndarray) -> Tree:
+        is_leaf = self.is_leaf
+        n = len(self.parent)
+        st = np.zeros((n, 2), dtype=np.float64)
+        for i in range(n):
+            st[i] = self.stats[i].astype(np.float64) * scale
+        feat_orig = np.array([int(Q.fid_host[f]) if f >= 0 and not is_leaf[i] else -1
+                              for i, f in enumerate(self.feature)], dtype=np.int32)
+        left_a = np.array([lc if not is_leaf[i] else -1 for i, lc in enumerate(self.left)], dtype=np.int32)
+        right_a = np.array([rc if not is_leaf[i] else -1 for i, rc in enumerate(self.right)], dtype=np.int32)
+        thr_a = np.array(self.thr, dtype=np.float64)
+        gain_a = np.array([gv if not is_leaf[i] else -1.0 for i, gv in enumerate(self.gain)], dtype=np.float64)
+        if params.mode == 0:
+            G, H = st[:, 0], st[:, 1]
+            w = -G / (H + params.lambda_)
+            if params.max_delta_step > 0:
+                w = np.clip(w, -params.max_delta_step, params.max_delta_step)
+            value = params.eta * w
+            imp = np.zeros(n)
+            pred = value
+            stats_out = np.stack([value, H], 1)
+            raw_count = np.zeros(n, dtype=np.int64)
+        else:
+            imp = np.array([_impurity(s, params.mode) for s in st])
+            pred = np.argmax(st, axis=1).astype(np.float64)
+            stats_out = st
+            raw_count = np.rint(st.sum(1)).astype(np.int64)
+        return Tree(feat_orig, thr_a, left_a, right_a, stats_out, imp, gain_a, raw_count, pred, 0)
 
 
 def _weight(st, mode) -> int:
@@ -526,7 +550,8 @@ def _impurity(st, mode) -> float:
     return 1.0 - p0 * p0 - p1 * p1
 
 
-def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits: list, chunk: int = 1 << 16):
+def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits: list, chunk: int = 1 << 16,
+               row_node: Optional[torch.Tensor] = None):
     """Rows -> children (K-13): every row of a split node moves to the default child, then one pass
     over the split columns moves the rows present in them whose bin falls on the other side."""
     colptr = Q.colptr.cpu().numpy() if not hasattr(Q, "_colptr_host") else Q._colptr_host
@@ -543,4 +568,4 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits
           stg.add(np.array(item_split, dtype=np.int32))]
     hs += [stg.add(np.array([sp[k] for sp in splits], dtype=np.int32)) for k in (1, 2, 3, 4)]
     up = stg.upload()
-    C.tree_partition(ws.row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin)
+    C.tree_partition(ws.row_node if row_node is None else row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin)

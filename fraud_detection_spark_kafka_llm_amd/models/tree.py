@@ -10,6 +10,7 @@ Reference configs: /root/reference/fraud_detection_spark.py:59-74.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -21,6 +22,7 @@ from ..ml.tree_model import Tree
 from ..parallel.dist import Collectives
 from ..utils.config import default_device
 from ..utils import tracing
+from .forest_batch import K_RF_TREES, BatchWorkspace, grow_forest_batch
 from .grower import GrowParams, Workspace, grow_tree
 from .quantize import quantize
 from .rf_sampling import features_per_node
@@ -105,11 +107,27 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
                         seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
     ws = Workspace(Q)
     trees = ckpt.load_trees() if (ckpt is not None and resume) else []
-    for t in range(len(trees), num_trees):
-        with tracing.span("forest.tree", tree=t):
-            tr = grow_tree(Q, ws, params, t, label=y, weight=w, bootstrap=bootstrap, coll=coll)
-        trees.append(prune_same_prediction(tr) if prune else tr.compacted())
-        if ckpt is not None:
-            ckpt.maybe_save(len(trees), trees, 0.0, F, None, force=len(trees) == num_trees)
-        maybe_fail(t)
+    # PAR-05: 8 trees per level pass when this process holds all rows (the data-parallel path
+    # keeps one tree per pass: its reduce-scatter is per tree); identical trees either way
+    batch = (w is None and not coll.active and num_trees - len(trees) > 1
+             and os.environ.get("FDX_RF_BATCH", "1") != "0")
+    bw = BatchWorkspace(Q) if batch else None
+    t = len(trees)
+    while t < num_trees:
+        if batch:
+            ids = list(range(t, min(num_trees, t + K_RF_TREES)))
+            with tracing.span("forest.batch", first=t, trees=len(ids)):
+                grown = grow_forest_batch(Q, ws, bw, params, ids, y, bootstrap)
+        else:
+            ids = [t]
+            with tracing.span("forest.tree", tree=t):
+                grown = [grow_tree(Q, ws, params, t, label=y, weight=w, bootstrap=bootstrap, coll=coll)]
+        for tid, tr in zip(ids, grown):
+            before = len(trees)
+            trees.append(prune_same_prediction(tr) if prune else tr.compacted())
+            if ckpt is not None:
+                crossed = (len(trees) // ckpt.every) > (before // ckpt.every)
+                ckpt.maybe_save(len(trees), trees, 0.0, F, None, force=crossed or len(trees) == num_trees)
+            maybe_fail(tid)
+        t += len(ids)
     return ForestResult(trees, F)

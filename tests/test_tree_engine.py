@@ -449,3 +449,42 @@ def test_gpu_rf_sampling_equals_host():
         h = _rf_sample("cpu", F, k)
         g = _rf_sample("cuda:0", F, k)
         assert torch.equal(h[0], g[0]) and torch.equal(h[1], g[1])
+
+
+@pytest.mark.parametrize("bootstrap,subset,n_trees", [(True, "sqrt", 11), (False, "all", 3), (True, "onethird", 9)])
+def test_multi_tree_rf_batches_equal_single_tree_growth(monkeypatch, bootstrap, subset, n_trees):
+    """PAR-05: 8 trees per level pass (tree_hist_rf) give exactly the trees of one-at-a-time growth."""
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+
+    rng = np.random.default_rng(17)
+    n, F = 1500, 90
+    dense = (rng.random((n, F)) < 0.12) * rng.integers(1, 6, (n, F))
+    y = ((dense[:, 3] > 0) ^ (dense[:, 11] >= 3)).astype(np.float32)
+    vc = VectorColumn(F, dense=torch.from_numpy(dense.astype(np.float64)))
+    kw = dict(num_trees=n_trees, max_depth=5, max_bins=16, bootstrap=bootstrap, feature_subset=subset, seed=7,
+              device="cpu")
+    monkeypatch.setenv("FDX_RF_BATCH", "0")
+    ref = fit_forest(vc, torch.from_numpy(y), **kw)
+    monkeypatch.setenv("FDX_RF_BATCH", "1")
+    got = fit_forest(vc, torch.from_numpy(y), **kw)
+    sig = lambda r: [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]  # noqa: E731
+    assert sig(got) == sig(ref)
+
+
+@pytest.mark.gpu
+def test_gpu_multi_tree_rf_batches_equal_single_tree_and_host(monkeypatch):
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+
+    rng = np.random.default_rng(23)
+    n, F = 20000, 400
+    dense = (rng.random((n, F)) < 0.05) * rng.integers(1, 6, (n, F))
+    y = ((dense[:, 3] > 0) ^ (dense[:, 11] >= 3)).astype(np.float32)
+    vc = VectorColumn(F, dense=torch.from_numpy(dense.astype(np.float64)))
+    kw = dict(num_trees=13, max_depth=5, max_bins=32, bootstrap=True, feature_subset="sqrt", seed=5)
+    sig = lambda r: [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]  # noqa: E731
+    monkeypatch.setenv("FDX_RF_BATCH", "1")
+    g = sig(fit_forest(vc, torch.from_numpy(y), device="cuda:0", **kw))
+    h = sig(fit_forest(vc, torch.from_numpy(y), device="cpu", **kw))
+    monkeypatch.setenv("FDX_RF_BATCH", "0")
+    g1 = sig(fit_forest(vc, torch.from_numpy(y), device="cuda:0", **kw))
+    assert g == g1 == h
