@@ -499,7 +499,7 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
 void partition(const Tensor& row_node, const Tensor& default_child, const Tensor& item_start, const Tensor& item_end,
                const Tensor& item_split, const Tensor& split_default, const Tensor& split_other,
                const Tensor& split_bin, const Tensor& split_left_is_default, const Tensor& csc_row,
-               const Tensor& csc_bin) {
+               const Tensor& csc_bin, const optional<Tensor>& node_dense, const optional<Tensor>& dense) {
   const auto dev = row_node.device();
   chk(row_node, dev, at::kInt, "row_node");
   chk(default_child, dev, at::kInt, "default_child");
@@ -527,6 +527,16 @@ void partition(const Tensor& row_node, const Tensor& default_child, const Tensor
   a.split_left_is_default = split_left_is_default.data_ptr<int32_t>();
   a.csc_row = csc_row.data_ptr<int32_t>();
   a.csc_bin = csc_bin.data_ptr<uint8_t>();
+  if (node_dense) {
+    FDX_CHECK(dense.has_value(), "node_dense needs the dense bin block");
+    chk(*node_dense, dev, at::kInt, "node_dense");
+    chk(*dense, dev, at::kByte, "dense");
+    FDX_CHECK(node_dense->numel() == 4ll * a.num_nodes, "node_dense must be [num_nodes, 4]");
+    FDX_CHECK(dense->dim() == 2 && dense->size(1) >= a.N, "dense must be [Fh, n_pad >= N]");
+    a.node_dense = node_dense->data_ptr<int32_t>();
+    a.dense = dense->data_ptr<uint8_t>();
+    a.n_pad = dense->size(1);
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_partition(a, stream(dev));

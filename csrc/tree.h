@@ -215,7 +215,21 @@ struct PartitionArgs {
   const int32_t* split_left_is_default;  // [S]
   const int32_t* csc_row;         // feature-major CSC (all features)
   const uint8_t* csc_bin;
+  // splits on dense-block (hot) features are applied in the row pass from the column-major bins:
+  // node_dense[4 n] = {dense row (-1: column pass), threshold bin, left child, right child}
+  const int32_t* node_dense;
+  const uint8_t* dense;           // [Fh][n_pad]
+  int64_t n_pad;
 };
+
+// Child of row r of split node n in the row pass.
+FDX_HD int32_t partition_row_child(const PartitionArgs& a, int32_t n, int64_t r) {
+  const int32_t c = a.default_child[n];
+  if (c < 0 || a.node_dense == nullptr) return c;
+  const int32_t* nd = a.node_dense + 4 * (int64_t)n;
+  if (nd[0] < 0) return c;
+  return (int32_t)a.dense[(int64_t)nd[0] * a.n_pad + r] <= nd[1] ? nd[2] : nd[3];
+}
 
 // counter-based hash -> uniform in [0,1) (splitmix64 finaliser)
 FDX_HD uint64_t mix64(uint64_t x) {

@@ -235,10 +235,15 @@ void split_cpu(const SplitArgs& a) {
 }
 
 void partition_cpu(const PartitionArgs& a) {
-  for (int64_t r = 0; r < a.N; ++r) {
-    const int32_t n = a.row_node[r];
-    if (n >= 0 && n < a.num_nodes && a.default_child[n] >= 0) a.row_node[r] = a.default_child[n];
-  }
+  parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
+    for (int64_t r = lo; r < hi; ++r) {
+      const int32_t n = a.row_node[r];
+      if (n >= 0 && n < a.num_nodes) {
+        const int32_t c = partition_row_child(a, n, r);
+        if (c >= 0) a.row_node[r] = c;
+      }
+    }
+  });
   for (int it = 0; it < a.num_items; ++it) {
     const int sp = a.item_split[it];
     const bool left_default = a.split_left_is_default[sp] != 0;

@@ -662,7 +662,7 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
     const int32_t n = a.row_node[r];
     if (n >= 0 && n < a.num_nodes) {
-      const int32_t c = a.default_child[n];
+      const int32_t c = partition_row_child(a, n, r);
       if (c >= 0) a.row_node[r] = c;
     }
   }

@@ -43,6 +43,8 @@ DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
 # streams: they add into disjoint feature ranges with integer atomics, so the order is free and
 # the kernels fill each other's tails
 HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 3))
+# partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
+PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 
 
 @dataclass
@@ -501,7 +503,7 @@ class TreeTable:
             left_default = int(Q.zbin_host[fid]) <= b
             dflt, other = (li, ri) if left_default else (ri, li)
             default_child[n] = dflt
-            splits.append((fid, dflt, other, b, int(left_default)))
+            splits.append((fid, dflt, other, b, int(left_default), n))
             next_level += [li, ri]
         return next_level, default_child, splits
 
@@ -556,6 +558,24 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits
     over the split columns moves the rows present in them whose bin falls on the other side."""
     colptr = Q.colptr.cpu().numpy() if not hasattr(Q, "_colptr_host") else Q._colptr_host
     Q._colptr_host = colptr
+    # splits on hot features: the row pass reads the node's bin from the dense block (1 byte per
+    # row, coalesced) instead of scattering the column's millions of CSC entries
+    node_dense = None
+    col_splits = splits
+    if Q.dense is not None and PARTITION_DENSE:
+        if getattr(Q, "_hot_row", None) is None:
+            Q._hot_row = np.full(Q.Fa, -1, dtype=np.int32)
+            Q._hot_row[Q.hot] = np.arange(len(Q.hot), dtype=np.int32)
+        node_dense = np.full((len(default_child), 4), -1, dtype=np.int32)
+        col_splits = []
+        for sp in splits:
+            fid, dflt, other, b, left_default, n = sp
+            hr = int(Q._hot_row[fid])
+            if hr >= 0:
+                node_dense[n] = (hr, b, dflt if left_default else other, other if left_default else dflt)
+            else:
+                col_splits.append(sp)
+    splits = col_splits
     starts, ends, item_split = [], [], []
     for si, sp in enumerate(splits):
         a, b = int(colptr[sp[0]]), int(colptr[sp[0] + 1])
@@ -567,5 +587,7 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits
     hs = [stg.add(default_child), stg.add(np.array(starts, dtype=np.int64)), stg.add(np.array(ends, dtype=np.int64)),
           stg.add(np.array(item_split, dtype=np.int32))]
     hs += [stg.add(np.array([sp[k] for sp in splits], dtype=np.int32)) for k in (1, 2, 3, 4)]
+    h_nd = stg.add(node_dense) if node_dense is not None else None
     up = stg.upload()
-    C.tree_partition(ws.row_node if row_node is None else row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin)
+    C.tree_partition(ws.row_node if row_node is None else row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin,
+                     up[h_nd] if h_nd is not None else None, Q.dense if h_nd is not None else None)
