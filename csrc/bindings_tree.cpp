@@ -220,12 +220,38 @@ void rf_slots(const Tensor& row_node, const Tensor& node_slot, int64_t s0, int64
   }
 }
 
+// RF batch pass: out [Fa] int64 bit masks of the pass slots that sampled each feature, any [Fa] u8
+void rf_slot_mask(int64_t seed, const Tensor& slot_tree, const Tensor& slot_node, const Tensor& thr,
+                  const Tensor& fid_orig, const Tensor& out, const Tensor& any) {
+  const auto dev = fid_orig.device();
+  chk(slot_tree, dev, at::kInt, "slot_tree");
+  chk(slot_node, dev, at::kInt, "slot_node");
+  chk(thr, dev, at::kDouble, "thr");
+  chk(fid_orig, dev, at::kLong, "fid_orig");
+  chk(out, dev, at::kLong, "out");
+  chk(any, dev, at::kByte, "any");
+  FDX_CHECK(slot_tree.numel() <= 64 && slot_node.numel() == slot_tree.numel() && thr.numel() == slot_tree.numel(),
+            "<= 64 slots");
+  FDX_CHECK(out.numel() == fid_orig.numel() && any.numel() == fid_orig.numel(), "out / any [Fa]");
+  fdx::RfSlotMaskArgs a{(uint64_t)seed, slot_tree.data_ptr<int32_t>(), slot_node.data_ptr<int32_t>(),
+                        thr.data_ptr<double>(), (int32_t)slot_tree.numel(), fid_orig.data_ptr<int64_t>(),
+                        fid_orig.numel(), reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()),
+                        any.data_ptr<uint8_t>()};
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rf_slot_mask(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rf_slot_mask_cpu(a);
+  }
+}
+
 // Multi-tree RF histogram pass (hist_rf_kernel): slot_node / slot_tree [nslots <= 8 * ct]
 void hist_rf(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
              const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key, const Tensor& rs,
              const Tensor& rw, const Tensor& boff, const Tensor& nbins, const Tensor& slot_node,
              const Tensor& slot_tree, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct,
-             const optional<Tensor>& feat_active) {
+             const optional<Tensor>& feat_active, const optional<Tensor>& feat_slots) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
@@ -272,6 +298,11 @@ void hist_rf(const Tensor& item_start, const Tensor& item_end, const Tensor& ite
     chk(*feat_active, dev, at::kByte, "feat_active");
     FDX_CHECK(feat_active->numel() == nbins.numel(), "feat_active must be [Fa] uint8");
     a.feat_active = feat_active->data_ptr<uint8_t>();
+  }
+  if (feat_slots) {
+    chk(*feat_slots, dev, at::kLong, "feat_slots");
+    FDX_CHECK(feat_slots->numel() == nbins.numel(), "feat_slots must be [Fa] int64 bit masks");
+    a.rf_feat_slots = reinterpret_cast<const uint64_t*>(feat_slots->data_ptr<int64_t>());
   }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
@@ -595,6 +626,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rf_rows", &rf_rows);
   m.def("tree_rf_slots", &rf_slots);
   m.def("tree_hist_rf", &hist_rf);
+  m.def("tree_rf_slot_mask", &rf_slot_mask);
   m.def("tree_hist_dense", &hist_dense);
   m.def("tree_dense_fg", &dense_fg);
   m.def("tree_dense_waves", &dense_waves);

@@ -83,6 +83,9 @@ void rf_sample_cpu(const RfSampleArgs& a);
 void launch_rf_rows(const RfRowsArgs& a, hipStream_t s);
 void launch_rf_slots(const RfSlotsArgs& a, hipStream_t s);
 void launch_hist_rf(const HistArgs& a, int bt, int ct, hipStream_t s);
+struct RfSlotMaskArgs;
+void launch_rf_slot_mask(const RfSlotMaskArgs& a, hipStream_t s);
+void rf_slot_mask_cpu(const RfSlotMaskArgs& a);
 void rf_rows_cpu(const RfRowsArgs& a);
 void rf_slots_cpu(const RfSlotsArgs& a);
 void hist_rf_cpu(const HistArgs& h, int bt);

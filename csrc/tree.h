@@ -105,6 +105,20 @@ struct HistArgs {
   const uint8_t* rf_rs;           // [N][kRfTrees] pass slot of the row in tree j (0xff: none)
   const uint8_t* rf_rw;           // [N][kRfTrees][2] class counts (Poisson weight x indicator, <= 32)
   const int32_t* rf_slot_tree;    // [nslots] tree (0..kRfTrees-1) of each pass slot
+  const uint64_t* rf_feat_slots;  // [Fa] optional: bit s = pass slot s sampled the feature (tiles skipped)
+};
+
+// RF batch pass: which of the (<= 64) pass slots sampled each active feature.
+struct RfSlotMaskArgs {
+  uint64_t seed;
+  const int32_t* slot_tree;       // [nslots] global tree index
+  const int32_t* slot_node;       // [nslots] tree-local node id
+  const double* thr;              // [nslots] sampling threshold
+  int32_t nslots;
+  const int64_t* fid_orig;        // [Fa]
+  int64_t Fa;
+  uint64_t* out;                  // [Fa]
+  uint8_t* any;                   // [Fa] out != 0 (item filter)
 };
 
 constexpr int kRfTrees = 8;       // trees per multi-tree RF batch (one 8-byte slot record per row)

@@ -89,6 +89,18 @@ void rf_sample_cpu(const RfSampleArgs& a) {
   });
 }
 
+void rf_slot_mask_cpu(const RfSlotMaskArgs& a) {
+  parallel_for(a.Fa, 0, 1024, [&](int64_t lo, int64_t hi) {
+    for (int64_t f = lo; f < hi; ++f) {
+      uint64_t m = 0;
+      for (int s = 0; s < a.nslots; ++s)
+        if (feature_priority(a.seed, a.slot_tree[s], a.slot_node[s], a.fid_orig[f]) <= a.thr[s]) m |= 1ull << s;
+      a.out[f] = m;
+      a.any[f] = m ? 1 : 0;
+    }
+  });
+}
+
 void rf_rows_cpu(const RfRowsArgs& a) {
   std::mutex mu;
   parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
@@ -140,6 +152,7 @@ void hist_rf_cpu(const HistArgs& h, int bt) {
         for (int j = 0; j < kRfTrees; ++j) {
           const int s = h.rf_rs[row * kRfTrees + j];
           if (s >= h.nslots || h.rf_slot_tree[s] != j) continue;
+          if (h.rf_feat_slots && !((h.rf_feat_slots[f] >> s) & 1ull)) continue;   // unsampled: never read
           const int node = h.slot_node[s];
           if (node < 0) continue;
           int64_t* dst = h.hist + ((int64_t)node * h.hist_stride + h.boff[f] + b) * 2;

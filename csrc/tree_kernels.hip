@@ -569,11 +569,22 @@ __global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
   const uint32_t koff = (uint32_t)item_koff(meta);
   const int r = lane & 15, g = lane >> 4;
   const int slot_sub = r >> 1, q = r & 1;
+  // tiles whose 8 slots sampled none of the item's features are skipped (wave-uniform)
+  uint64_t im = ~0ull;
+  if (a.rf_feat_slots) {
+    im = 0;
+    const int32_t fi = a.item_f0[item];
+    const int nfi = item_nfeat(meta);
+    for (int j = 0; j < nfi; ++j) im |= a.rf_feat_slots[fi + j];
+    if (im == 0) return;
+  }
   int jt[CT];
+  bool on[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     const int sl = ct * 8 + slot_sub;
     jt[ct] = sl < a.nslots ? a.rf_slot_tree[sl] : -1;
+    on[ct] = ((im >> (8 * ct)) & 0xffull) != 0;
   }
   i32x4 acc[BT][CT];
 #pragma unroll
@@ -622,6 +633,7 @@ __global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
       }
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
+        if (!on[ct]) continue;
         const int j = jt[ct] < 0 ? 0 : jt[ct];
         const uint4 s4 = *reinterpret_cast<const uint4*>(&s_rs[wid][j][k0]);
         const uint4 d4 = *reinterpret_cast<const uint4*>(&s_rw[wid][2 * j + q][k0]);

@@ -98,11 +98,10 @@ def grow_forest_batch(Q: Quantized, ws: Workspace, bw: BatchWorkspace, params: G
         h_tot = stg.add(np.stack([tabs[j].stats[n] for j, n in nodes]).astype(np.int64))
         per_tree = [stg.add(np.array(opens[j], dtype=np.int32)) if opens[j] else None for j in range(T)]
         up = stg.upload()
-        # exact k-of-F sampling per (tree, node) on the device; the level's mask is the union
+        # exact k-of-F sampling per (tree, node) on the device: thresholds per node; per pass, a
+        # bit mask of the slots that sampled each feature selects work items and MFMA tiles
         feat_thr = torch.ones(nl, dtype=torch.float64, device=dev)
-        feat_mask = None
         if params.feat_k:
-            feat_mask = torch.zeros(Q.Fa, dtype=torch.uint8, device=dev)
             m_j = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
             k0 = 0
             for j in range(T):
@@ -111,8 +110,9 @@ def grow_forest_batch(Q: Quantized, ws: Workspace, bw: BatchWorkspace, params: G
                 thr_j = feat_thr[k0:k0 + len(opens[j])]
                 C.tree_rf_sample(int(params.seed), int(tree_ids[j]), up[per_tree[j]], int(Q.num_features),
                                  int(params.feat_k), Q.fid_orig, thr_j, m_j)
-                feat_mask |= m_j
                 k0 += len(opens[j])
+            slot_bits = torch.empty(Q.Fa, dtype=torch.int64, device=dev)
+            slot_any = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
         hist = torch.zeros((nl, TB, 2), dtype=torch.int64, device=dev)
         with tracing.span("forest.hist"):
             ns_dev = up[h_ns].view(K_RF_TREES, max_nodes)
@@ -122,12 +122,17 @@ def grow_forest_batch(Q: Quantized, ws: Workspace, bw: BatchWorkspace, params: G
                 ct = _ct_for(cnt)
                 slot_node = up[h_slot_node][s0:s0 + cnt]
                 slot_tree = up[h_slot_tree][s0:s0 + cnt]
+                bits = anyf = None
+                if params.feat_k:
+                    C.tree_rf_slot_mask(int(params.seed), up[h_tree][s0:s0 + cnt], up[h_ids][s0:s0 + cnt],
+                                        feat_thr[s0:s0 + cnt], Q.fid_orig, slot_bits, slot_any)
+                    bits, anyf = slot_bits, slot_any
                 for grp in groups:
                     if grp.num_items == 0:
                         continue
                     C.tree_hist_rf(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
                                    Q.h_row, Q.h_key, bw.rs, bw.rw, Q.boff, Q.nbins, slot_node, slot_tree, hist, TB,
-                                   grp.bt, ct, feat_mask)
+                                   grp.bt, ct, anyf, bits)
         with tracing.span("forest.split"):
             packed = _best_splits(C, hist, up[h_tot], Q.boff, Q.nbins, Q.zbin, Q.fid_orig, up[h_ids], bw.kexp, params,
                                   feat_thr if params.feat_k else None, 0, Q.Fa, 0, up[h_tree]).cpu().numpy()
