@@ -143,7 +143,7 @@ void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, i
 // RF per-level sampling: thr [n] f64 (k-th smallest priority of each node over 0..F-1) and the
 // union mask [Fa] u8 over the active features fid_orig.
 void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64_t k, const Tensor& fid_orig,
-               const Tensor& thr, const Tensor& mask) {
+               const Tensor& thr, const Tensor& mask, const optional<Tensor>& node_trees) {
   const auto dev = fid_orig.device();
   chk(nodes, dev, at::kInt, "nodes");
   chk(fid_orig, dev, at::kLong, "fid_orig");
@@ -161,6 +161,11 @@ void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64
   a.tree = (int32_t)tree;
   a.nodes = nodes.data_ptr<int32_t>();
   a.nnodes = (int32_t)nodes.numel();
+  if (node_trees) {
+    chk(*node_trees, dev, at::kInt, "node_trees");
+    FDX_CHECK(node_trees->numel() == nodes.numel(), "node_trees [n]");
+    a.node_trees = node_trees->data_ptr<int32_t>();
+  }
   a.F = F;
   a.k = k;
   a.fid_orig = fid_orig.data_ptr<int64_t>();

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(kThreads) void rf_window_kernel(RfSampleArgs a, uin
   __syncthreads();
   unsigned int mine = 0;
   for (int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x; f < a.F; f += (int64_t)gridDim.x * kThreads) {
-    const uint64_t u = feature_priority_u53(a.seed, a.tree, node, f);
+    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, i), node, f);
     if (u < ulo) {
       ++mine;
     } else if (u <= uhi) {
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
     for (int i = tid; i < kBuckets; i += kThreads) s_hist[i] = 0;
     __syncthreads();
     for (int64_t f = tid; f < a.F; f += kThreads) {
-      const uint64_t u = feature_priority_u53(a.seed, a.tree, node, f);
+      const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, blockIdx.x), node, f);
       if (known == 0 || (u >> (53 - known)) == prefix)
         atomicAdd(&s_hist[(u >> shift) & ((1u << nbits) - 1)], 1u);
     }
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
   const int known = s_known;
   const uint64_t prefix = s_prefix;
   for (int64_t f = tid; f < a.F; f += kThreads) {
-    const uint64_t u = feature_priority_u53(a.seed, a.tree, node, f);
+    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, blockIdx.x), node, f);
     if (known == 0 || (u >> (53 - known)) == prefix) {
       const uint32_t i = atomicAdd(&s_ncand, 1u);
       if (i < (uint32_t)kCap) s_cand[i] = u;
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
   const int64_t fid = a.fid_orig[f];
   uint8_t m = 0;
   for (int i = 0; i < a.nnodes && !m; ++i) {
-    const uint64_t u = feature_priority_u53(a.seed, a.tree, a.nodes[i], fid);
+    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, i), a.nodes[i], fid);
     m = ((double)u * (1.0 / 9007199254740992.0) <= a.thr[i]) ? 1 : 0;
   }
   a.mask[f] = m;

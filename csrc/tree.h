@@ -153,6 +153,7 @@ struct RfSampleArgs {
   uint64_t seed;
   int32_t tree;
   const int32_t* nodes;           // [nnodes]
+  const int32_t* node_trees;      // [nnodes] optional per-node tree (RF batches); nullptr: `tree`
   int32_t nnodes;
   int64_t F;
   int64_t k;
@@ -162,6 +163,8 @@ struct RfSampleArgs {
   uint8_t* mask;                  // [Fa] out
   uint8_t* scratch;               // device: rf_scratch_bytes(nnodes) for the window fast path (or null)
 };
+
+FDX_HD int32_t rf_tree_of(const RfSampleArgs& a, int64_t i) { return a.node_trees ? a.node_trees[i] : a.tree; }
 
 inline int64_t rf_scratch_bytes(int64_t nnodes) { return 8 * ((2 * nnodes * 4 + 7) / 8) + nnodes * 2048 * 8; }
 

@@ -19,6 +19,7 @@ bitwise identical to growing the trees one at a time (tested).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -26,11 +27,12 @@ import torch
 
 from ..ops import native
 from ..utils import tracing
-from .grower import GrowParams, TreeTable, Workspace, _best_splits, _partition
+from .grower import GrowParams, TreeTable, Workspace, _best_splits, _partition_launch, _partition_stage
 from .quantize import Quantized
 
 K_RF_TREES = 8
 MAX_PASS_SLOTS = 64
+TILE_SKIP = os.environ.get("FDX_RF_TILE_SKIP", "1") != "0"
 
 
 class BatchWorkspace:
@@ -96,21 +98,14 @@ def grow_forest_batch(Q: Quantized, ws: Workspace, bw: BatchWorkspace, params: G
         h_slot_tree = stg.add(np.array([j for j, _ in nodes], dtype=np.int32))
         h_slot_node = stg.add(np.arange(nl, dtype=np.int32))
         h_tot = stg.add(np.stack([tabs[j].stats[n] for j, n in nodes]).astype(np.int64))
-        per_tree = [stg.add(np.array(opens[j], dtype=np.int32)) if opens[j] else None for j in range(T)]
         up = stg.upload()
         # exact k-of-F sampling per (tree, node) on the device: thresholds per node; per pass, a
         # bit mask of the slots that sampled each feature selects work items and MFMA tiles
         feat_thr = torch.ones(nl, dtype=torch.float64, device=dev)
         if params.feat_k:
-            m_j = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
-            k0 = 0
-            for j in range(T):
-                if not opens[j]:
-                    continue
-                thr_j = feat_thr[k0:k0 + len(opens[j])]
-                C.tree_rf_sample(int(params.seed), int(tree_ids[j]), up[per_tree[j]], int(Q.num_features),
-                                 int(params.feat_k), Q.fid_orig, thr_j, m_j)
-                k0 += len(opens[j])
+            m_all = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
+            C.tree_rf_sample(int(params.seed), 0, up[h_ids], int(Q.num_features), int(params.feat_k), Q.fid_orig,
+                             feat_thr, m_all, up[h_tree])                # every (tree, node) in one launch
             slot_bits = torch.empty(Q.Fa, dtype=torch.int64, device=dev)
             slot_any = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
         hist = torch.zeros((nl, TB, 2), dtype=torch.int64, device=dev)
@@ -126,7 +121,7 @@ def grow_forest_batch(Q: Quantized, ws: Workspace, bw: BatchWorkspace, params: G
                 if params.feat_k:
                     C.tree_rf_slot_mask(int(params.seed), up[h_tree][s0:s0 + cnt], up[h_ids][s0:s0 + cnt],
                                         feat_thr[s0:s0 + cnt], Q.fid_orig, slot_bits, slot_any)
-                    bits, anyf = slot_bits, slot_any
+                    bits, anyf = (slot_bits if TILE_SKIP else None), slot_any
                 for grp in groups:
                     if grp.num_items == 0:
                         continue
@@ -138,12 +133,17 @@ def grow_forest_batch(Q: Quantized, ws: Workspace, bw: BatchWorkspace, params: G
                                   feat_thr if params.feat_k else None, 0, Q.Fa, 0, up[h_tree]).cpu().numpy()
         with tracing.span("forest.partition"):
             k0 = 0
+            staged = []
             for j in range(T):
                 cnt = len(opens[j])
                 nxt, default_child, splits = tabs[j].apply_splits(opens[j], packed[k0:k0 + cnt], d, Q, params, scale,
                                                                   max_nodes)
                 k0 += cnt
                 if splits:
-                    _partition(native.lib(), Q, ws, default_child, splits, row_node=bw.row_node[j])
+                    staged.append((j, _partition_stage(Q, stg, default_child, splits)))
                 levels[j] = nxt
+            if staged:                          # one upload for the 8 trees' partition tables
+                up = stg.upload()
+                for j, hs in staged:
+                    _partition_launch(C, Q, up, hs, bw.row_node[j])
     return [tabs[j].build(Q, params, scale) for j in range(T)]

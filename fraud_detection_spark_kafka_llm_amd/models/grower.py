@@ -385,7 +385,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             feat_thr = torch.empty(nl, dtype=torch.float64, device=dev)
             feat_mask = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
             C.tree_rf_sample(int(params.seed), int(tree_index), up[h_ids], int(Q.num_features), int(params.feat_k),
-                             Q.fid_orig, feat_thr, feat_mask)
+                             Q.fid_orig, feat_thr, feat_mask, None)
         # --- histograms, up to `pass_slots` node slots per pass
         with tracing.span("tree.hist"):
             # RF levels read only the sampled features' CSC items (the dense block would stream
@@ -556,6 +556,13 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits
                row_node: Optional[torch.Tensor] = None):
     """Rows -> children (K-13): every row of a split node moves to the default child, then one pass
     over the split columns moves the rows present in them whose bin falls on the other side."""
+    hs = _partition_stage(Q, ws.staging, default_child, splits, chunk)
+    up = ws.staging.upload()
+    _partition_launch(C, Q, up, hs, ws.row_node if row_node is None else row_node)
+
+
+def _partition_stage(Q: Quantized, stg, default_child: np.ndarray, splits: list, chunk: int = 1 << 16) -> tuple:
+    """Host arrays of one tree's level partition, added to ``stg`` (upload separately)."""
     colptr = Q.colptr.cpu().numpy() if not hasattr(Q, "_colptr_host") else Q._colptr_host
     Q._colptr_host = colptr
     # splits on hot features: the row pass reads the node's bin from the dense block (1 byte per
@@ -583,11 +590,14 @@ def _partition(C, Q: Quantized, ws: Workspace, default_child: np.ndarray, splits
             starts.append(s)
             ends.append(min(b, s + chunk))
             item_split.append(si)
-    stg = ws.staging
     hs = [stg.add(default_child), stg.add(np.array(starts, dtype=np.int64)), stg.add(np.array(ends, dtype=np.int64)),
           stg.add(np.array(item_split, dtype=np.int32))]
     hs += [stg.add(np.array([sp[k] for sp in splits], dtype=np.int32)) for k in (1, 2, 3, 4)]
     h_nd = stg.add(node_dense) if node_dense is not None else None
-    up = stg.upload()
-    C.tree_partition(ws.row_node if row_node is None else row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin,
+    return hs, h_nd
+
+
+def _partition_launch(C, Q: Quantized, up: list, staged: tuple, row_node: torch.Tensor) -> None:
+    hs, h_nd = staged
+    C.tree_partition(row_node, *(up[h] for h in hs), Q.csc_row, Q.csc_bin,
                      up[h_nd] if h_nd is not None else None, Q.dense if h_nd is not None else None)

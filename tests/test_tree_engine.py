@@ -422,7 +422,7 @@ def _rf_sample(dev, F=5000, k=71, nodes=(0, 1, 2, 5, 9), seed=123456789, tree=7)
     nd = torch.tensor(nodes, dtype=torch.int32, device=dev)
     thr = torch.empty(len(nodes), dtype=torch.float64, device=dev)
     mask = torch.empty(fid.numel(), dtype=torch.uint8, device=dev)
-    native.lib().tree_rf_sample(seed, tree, nd, F, k, fid, thr, mask)
+    native.lib().tree_rf_sample(seed, tree, nd, F, k, fid, thr, mask, None)
     return thr.cpu(), mask.cpu(), fid.cpu()
 
 
