@@ -96,14 +96,15 @@ def bench_rf(args) -> dict:
     vc, y, idf = _tfidf(rows, dev, seed=21)
     torch.cuda.synchronize()
     t_feat = time.perf_counter() - t0
-    res = fit_forest(vc, y, num_trees=trees, max_depth=5, max_bins=32, bootstrap=True, feature_subset="sqrt",
+    res = fit_forest(vc, y, num_trees=trees, max_depth=5, max_bins=32, bootstrap=True, feature_subset=args.subset,
                      seed=42, device=dev)
     torch.cuda.synchronize()
     t_train = time.perf_counter() - t0
     tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
     raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()
     p1 = raw[:, 1] / np.maximum(raw.sum(1), 1e-300)
-    return {"bench": "rf", "rows": rows, "trees": trees, "depth": 5, "featurize_s": t_feat, "train_s": t_train,
+    return {"bench": "rf", "rows": rows, "trees": trees, "depth": 5, "subset": args.subset, "featurize_s": t_feat,
+            "train_s": t_train,
             "train_only_s": t_train - t_feat,
             "peak_hbm_gb": torch.cuda.max_memory_allocated() / 2 ** 30, "heldout_rows": 200_000,
             **_metrics(ty.cpu().numpy(), p1, (raw[:, 1] > raw[:, 0]).astype(float))}
@@ -194,6 +195,7 @@ def main():
     ap.add_argument("which", choices=list(BENCHES) + ["all"])
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--trees", type=int, default=0)
+    ap.add_argument("--subset", default="sqrt", help="rf: featureSubsetStrategy")
     args = ap.parse_args()
     for name in (list(BENCHES) if args.which == "all" else [args.which]):
         print(json.dumps(BENCHES[name](args)), flush=True)
