@@ -107,15 +107,15 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
                         seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
     ws = Workspace(Q)
     trees = ckpt.load_trees() if (ckpt is not None and resume) else []
-    # PAR-05: 8 trees per level pass (models/forest_batch.py) when this process holds all rows
-    # (the data-parallel path keeps one tree per pass: its reduce-scatter is per tree). Default:
-    # batched when every node may split on every feature (each pass then reads all entries, and a
-    # batch reads them once for 8 trees); per-tree passes under feature subsampling, where each
-    # pass reads only its nodes' sampled features (measured ~8% faster at 10M rows, 500 trees).
-    # FDX_RF_BATCH=1 / 0 forces either; the trees are identical.
-    mode = os.environ.get("FDX_RF_BATCH", "auto")
-    want = params.feat_k == 0 if mode == "auto" else mode != "0"
-    batch = want and w is None and not coll.active and num_trees - len(trees) > 1
+    # PAR-05: FDX_RF_BATCH=1 grows 8 trees per level pass (models/forest_batch.py; single-process
+    # only: the data-parallel path reduce-scatters per tree). The trees are identical, but on
+    # MI355X the per-tree passes are faster: the single-tree kernel compacts each pass to the live
+    # entries of one tree (1-byte slot, 2 count bytes per entry), the 8-tree kernel carries 24
+    # bytes of records per entry and up to 8 MFMA tiles. Measured at 10M rows, depth 5: 200 trees
+    # sqrt-sampled 1.21-1.26 s per-tree vs 1.34-1.36 s batched; 40 trees with all features
+    # 1.05 s vs 1.45 s (profiles/r2_rf_batch_ab.txt). Per-tree passes are therefore the default.
+    batch = (os.environ.get("FDX_RF_BATCH", "0") == "1" and w is None and not coll.active
+             and num_trees - len(trees) > 1)
     bw = BatchWorkspace(Q) if batch else None
     t = len(trees)
     while t < num_trees:
