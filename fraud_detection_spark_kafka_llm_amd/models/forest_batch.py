@@ -15,7 +15,12 @@ Spark's RandomForest grows the nodes of many trees per pass over the data (node 
     device→host copy returns all best splits; rows are partitioned per tree.
 
 The node tables are the same ``TreeTable`` the single-tree grower uses, so a batched forest is
-bitwise identical to growing the trees one at a time (tested).
+bitwise identical to growing the trees one at a time (tested). Per-feature slot bit masks skip
+the MFMA tiles of slots that did not sample an item's features.
+
+Status: opt-in (``FDX_RF_BATCH=1``). On MI355X the per-tree passes win: they compact each pass to
+one tree's live entries with a 1-byte slot and 2 count bytes per entry, while the batch carries
+24 bytes of records per entry (measured in profiles/r2_rf_batch_ab.txt).
 """
 from __future__ import annotations
 
