@@ -27,6 +27,31 @@ __device__ __forceinline__ uint32_t zero_bytes80(uint32_t x) {
   const uint32_t y = (x & 0x7f7f7f7fu) + 0x7f7f7f7fu;
   return ~(y | x | 0x7f7f7f7fu);
 }
+// One-hot A operand bytes (0x80 where the key byte equals the lane's key) when every byte of kv
+// and of the key is < 128: 0x80 - (kv ^ key) per byte lies in [1, 128] (no borrow between bytes)
+// and has its high bit set iff the bytes are equal. (kv ^ ~key) + 0x80808081 is that difference
+// mod 2^32, a single v_xad_u32, so one dword of A costs 2 VALU instead of 5.
+__device__ __forceinline__ uint32_t onehot7(uint32_t kv7, uint32_t nkey) {
+  return ((kv7 ^ nkey) + 0x80808081u) & 0x80808080u;
+}
+template <int BT>
+__device__ __forceinline__ void onehot_a(uint4 kv, uint32_t key0, bool fast, i32x4 A[BT]) {
+  if (fast) {
+    const uint4 k7 = make_uint4(kv.x & 0x7f7f7f7fu, kv.y & 0x7f7f7f7fu, kv.z & 0x7f7f7f7fu, kv.w & 0x7f7f7f7fu);
+#pragma unroll
+    for (int bt = 0; bt < BT; ++bt) {
+      const uint32_t nk = ~((key0 + 16u * bt) * 0x01010101u);
+      A[bt] = i32x4{(int)onehot7(k7.x, nk), (int)onehot7(k7.y, nk), (int)onehot7(k7.z, nk), (int)onehot7(k7.w, nk)};
+    }
+  } else {
+#pragma unroll
+    for (int bt = 0; bt < BT; ++bt) {
+      const uint32_t rep = (key0 + 16u * bt) * 0x01010101u;
+      A[bt] = i32x4{(int)zero_bytes80(kv.x ^ rep), (int)zero_bytes80(kv.y ^ rep), (int)zero_bytes80(kv.z ^ rep),
+                    (int)zero_bytes80(kv.w ^ rep)};
+    }
+  }
+}
 // 0xff in every byte of x that is zero
 __device__ __forceinline__ uint32_t zero_bytes_ff(uint32_t x) {
   const uint32_t z = zero_bytes80(x);
@@ -143,19 +168,26 @@ __global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
 // One lane's 4 consecutive entries of a histogram step: rows (-1 outside the item) and keys.
 // Branch-free, so the next steps' loads stay in flight: lanes past the item's end re-read its
 // last 4-group (clamped address), and the CSC arrays carry >= 4 readable entries of padding.
+// The loaded rows stay raw in the pipeline: invalid entries are set to -1 only where the step is
+// consumed (rows()), so no arithmetic on a load sits next to it and forces an early vmcnt wait.
 struct RowStep {
-  int4 r4;
+  int4 raw;
   uint32_t keys4;
+  uint32_t inval;            // bit j: entry j lies outside the item
+  __device__ __forceinline__ int4 rows() const {
+    return make_int4(raw.x | -(int)(inval & 1u), raw.y | -(int)((inval >> 1) & 1u), raw.z | -(int)((inval >> 2) & 1u),
+                     raw.w | -(int)(inval >> 3));
+  }
 };
 
 __device__ __forceinline__ void load_rows(const HistArgs& a, int64_t e, int64_t e0, int64_t e1, int64_t e_last,
                                           RowStep& d) {
   const int64_t el = e < e_last ? e : e_last;
   d.keys4 = *reinterpret_cast<const uint32_t*>(a.csc_key + el);
-  const int4 r = *reinterpret_cast<const int4*>(a.csc_row + el);
+  d.raw = *reinterpret_cast<const int4*>(__builtin_assume_aligned(a.csc_row + el, 16));
   const bool v0 = e >= e0 && e < e1, v1 = e + 1 >= e0 && e + 1 < e1;
   const bool v2 = e + 2 >= e0 && e + 2 < e1, v3 = e + 3 >= e0 && e + 3 < e1;
-  d.r4 = make_int4(v0 ? r.x : -1, v1 ? r.y : -1, v2 ? r.z : -1, v3 ? r.w : -1);
+  d.inval = (v0 ? 0u : 1u) | (v1 ? 0u : 2u) | (v2 ? 0u : 4u) | (v3 ? 0u : 8u);
 }
 
 // slot byte of each of the 4 entries (0xff: outside the item or not in a node of this pass)
@@ -169,33 +201,49 @@ __device__ __forceinline__ uint32_t entry_slots(const HistArgs& a, int4 r4) {
     const uint32_t s1 = a.slot8[r4.y >= 0 ? r4.y : 0];
     const uint32_t s2 = a.slot8[r4.z >= 0 ? r4.z : 0];
     const uint32_t s3 = a.slot8[r4.w >= 0 ? r4.w : 0];
-    return (r4.x >= 0 ? s0 : 0xffu) | ((r4.y >= 0 ? s1 : 0xffu) << 8) | ((r4.z >= 0 ? s2 : 0xffu) << 16) |
-           ((r4.w >= 0 ? s3 : 0xffu) << 24);
+    const uint32_t dead = (r4.x < 0 ? 0xffu : 0u) | (r4.y < 0 ? 0xff00u : 0u) | (r4.z < 0 ? 0xff0000u : 0u) |
+                          (r4.w < 0 ? 0xff000000u : 0u);
+    return (s0 | (s1 << 8) | (s2 << 16) | (s3 << 24)) | dead;
   }
 }
 
-// digit words of the live entries among the 4 (0 for dead ones: they never contribute)
+// digit words of the live entries among the 4 (0 for dead ones: they never contribute). The loads
+// are unconditional (dead entries read row 0, one shared line) so that the compiler can count them
+// in vmcnt: a conditional load makes it drain every outstanding load (vmcnt(0)) before the next use,
+// which serialised the software pipeline.
 __device__ __forceinline__ void gather_digits(const uint2* __restrict__ rd, int4 r4, uint32_t slots4, uint32_t w[8]) {
   const int32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
+  uint2 v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    uint2 v = make_uint2(0u, 0u);
-    if (((slots4 >> (8 * j)) & 0xffu) != 0xffu) v = rd[rr[j]];
-    w[2 * j] = v.x;
-    w[2 * j + 1] = v.y;
+    const bool live = ((slots4 >> (8 * j)) & 0xffu) != 0xffu;
+    v[j] = rd[live ? rr[j] : 0];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t m = ((slots4 >> (8 * j)) & 0xffu) != 0xffu ? 0xffffffffu : 0u;
+    w[2 * j] = v[j].x & m;
+    w[2 * j + 1] = v[j].y & m;
   }
 }
 
 // ------------------------------------------------------------------ i8 MFMA histogram
 // One wave per work item; per step the wave takes 256 entries, 4 consecutive ones per lane (rows
 // int4, keys u32: single vector loads), with rows/keys of step i+3, slots of step i+2 and digits
-// of step i+1 in flight while step i is staged in LDS and multiplied.
+// of step i+1 in flight while step i is staged in LDS and multiplied. Every load is unconditional
+// (clamped addresses, dead entries read row 0), so the compiler keeps them counted in vmcnt and the
+// steps overlap; a conditional load made it drain the queue (vmcnt(0)) every step.
 // Tile: v_mfma_i32_16x16x64_i8, lane l: r = l & 15 (A row = key r + 16 bt + koff, B column r),
 // g = l >> 4 (entries 16g .. 16g+15 of the K-step); C[key 4g + i][col r] in register i.
 // Columns: slot_sub = r / (2 NP) within the tile, q = r % (2 NP) = statistic * NP + plane.
+// The bins of an item's keys are contiguous: bin of key ek = boff[f0] + ek (packed features are
+// laid out with the item's key stride, models/quantize.py), so the epilogue needs one offset.
 // ROOT: every entry of the item is live in slot 0 (no slot table, no compaction: the lane's 4
 // digit words are transposed into plane-major LDS rows in registers). Otherwise the live entries
 // (row in a node of this pass) are compacted, and K-steps run on ceil(live / 64) groups.
+// Measured and kept out: dword staging of all entries with slot-masked B (0-20 % slower), and
+// waves streaming lists of consecutive items through one pipeline (no faster for the ~1K-entry
+// text-feature items, slower for the rest).
 template <int BT, int CT, int NP, bool ROOT>
 __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   constexpr int G = 4 * kWave;                 // entries per wave step
@@ -215,10 +263,21 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   if (!item_active(a, item)) return;          // RF: no feature of the item is sampled at this level
   const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
   const int32_t meta = a.item_meta[item];
+  const int32_t f0 = a.item_f0[item];
   const uint32_t koff = (uint32_t)item_koff(meta);
+  // every key of the item's entries is < 128 (packed items: < 64; single features: < nbins)
+  const bool fast7 = item_nfeat(meta) > 1 || a.nbins[f0] <= 128;
+  const int64_t hbase = a.boff[f0];
 
   const int r = lane & 15, g = lane >> 4;
   const int slot_sub = r / CPS, q = r % CPS;
+  int node_of[CT];                              // histogram row of each column tile's slot (-1: none)
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int slot = ct * SPT + slot_sub;
+    const int n = a.slot_node[slot < a.nslots ? slot : a.nslots - 1];
+    node_of[ct] = slot < a.nslots ? n : -1;
+  }
 
   i32x4 acc[BT][CT];
 #pragma unroll
@@ -235,10 +294,10 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
     RowStep g0;
     load_rows(a, first + 4 * lane, e0, e1, e_last, g0);
     load_rows(a, first + G + 4 * lane, e0, e1, e_last, g1);
-    sl0 = entry_slots<ROOT>(a, g0.r4);
+    sl0 = entry_slots<ROOT>(a, g0.rows());
     keys0 = g0.keys4;
-    sl1 = entry_slots<ROOT>(a, g1.r4);
-    gather_digits(rd, g0.r4, sl0, w0);
+    sl1 = entry_slots<ROOT>(a, g1.rows());
+    gather_digits(rd, g0.rows(), sl0, w0);
     load_rows(a, first + 2 * G + 4 * lane, e0, e1, e_last, g2);
   }
   for (int64_t base = first; base < e1; base += G) {
@@ -247,8 +306,8 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) w[j] = w0[j];
     // digits of step i+1, slots of step i+2, rows of step i+3 (clamped, so unconditional)
-    gather_digits(rd, g1.r4, sl1, w0);
-    const uint32_t sl2 = entry_slots<ROOT>(a, g2.r4);
+    gather_digits(rd, g1.rows(), sl1, w0);
+    const uint32_t sl2 = entry_slots<ROOT>(a, g2.rows());
     RowStep g3;
     load_rows(a, base + 3 * G + 4 * lane, e0, e1, e_last, g3);
     sl0 = sl1;
@@ -297,12 +356,7 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
       const uint4 kv = *reinterpret_cast<const uint4*>(&s_key[wid][k0]);
       const uint4 dv = *reinterpret_cast<const uint4*>(&s_dig[wid][q][k0]);
       i32x4 A[BT];
-#pragma unroll
-      for (int bt = 0; bt < BT; ++bt) {
-        const uint32_t rep = ((uint32_t)(r + 16 * bt) + koff) * 0x01010101u;
-        A[bt] = i32x4{(int)zero_bytes80(kv.x ^ rep), (int)zero_bytes80(kv.y ^ rep), (int)zero_bytes80(kv.z ^ rep),
-                      (int)zero_bytes80(kv.w ^ rep)};
-      }
+      onehot_a<BT>(kv, (uint32_t)r + koff, fast7, A);
       if constexpr (ROOT) {
         const i32x4 B = {(int)dv.x, (int)dv.y, (int)dv.z, (int)dv.w};
 #pragma unroll
@@ -322,9 +376,8 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   }
 
   // Epilogue: C = -128 * (plane sum); lanes r .. r+NP-1 hold the NP planes of one (slot, stat)
-  // column: the plane-0 lane recombines them into int64 and adds the nonzero sums to the histogram.
-  const int32_t f0 = a.item_f0[item];
-  const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta);
+  // column: the plane-0 lane recombines them into int64 and adds the nonzero sums to the
+  // histogram (keys without entries, past the item's features or bins, sum to 0).
   const int stat = q / NP;
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
@@ -332,21 +385,15 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int64_t s = -(int64_t)(acc[bt][ct][i] >> 7);
+        const int32_t s = -(acc[bt][ct][i] >> 7);
         int64_t v = s;
         if constexpr (NP == 4) {
-          const int64_t s1 = __shfl_down(s, 1, kWave), s2 = __shfl_down(s, 2, kWave), s3 = __shfl_down(s, 3, kWave);
-          v = s + s1 * 256 + s2 * 65536 + s3 * 16777216;
+          const int32_t s1 = __shfl_down(s, 1, kWave), s2 = __shfl_down(s, 2, kWave), s3 = __shfl_down(s, 3, kWave);
+          v = (int64_t)s + (int64_t)s1 * 256 + (int64_t)s2 * 65536 + (int64_t)s3 * 16777216;
         }
-        const int slot = ct * SPT + slot_sub;
-        if ((q % NP) != 0 || v == 0 || slot >= a.nslots) continue;
-        const int node = a.slot_node[slot];
+        if ((q % NP) != 0 || v == 0 || node_of[ct] < 0) continue;
         const int ek = 16 * bt + 4 * g + i + (int)koff;
-        const int fl = ek >> sl2, b = ek & ((1 << sl2) - 1);
-        if (node < 0 || fl >= nfeat) continue;
-        const int f = f0 + fl;
-        if (b >= a.nbins[f]) continue;
-        int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2 + stat;
+        int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + hbase + ek) * 2 + stat;
         atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
       }
 }
@@ -394,14 +441,16 @@ __global__ __launch_bounds__(256) void hist_dense_kernel(DenseHistArgs a) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[j][bt][ct] = i32x4{0, 0, 0, 0};
 
-  // two K-steps of loads in flight: (bins, digits, slots) of steps i+1 and i+2
+  // two K-steps of loads in flight: (bins, digits, slots) of steps i+1 and i+2. Unconditional
+  // loads from clamped addresses (steps past the range re-read its last step, non-loader lanes read
+  // column 0), so the compiler counts them in vmcnt instead of draining the queue every step.
   uint4 lb1 = make_uint4(0, 0, 0, 0), lb2 = lb1, d1 = lb1, d2 = lb1, s1 = lb1, s2 = lb1;
+  const int64_t last = r1 - 64;
   auto load = [&](int64_t base, uint4& lb, uint4& d, uint4& sv) {
-    if (base < r1) {
-      if (loader) lb = *reinterpret_cast<const uint4*>(lcol + base);
-      d = *reinterpret_cast<const uint4*>(dig + base);
-      if constexpr (!ROOT) sv = *reinterpret_cast<const uint4*>(slt + base);
-    }
+    const int64_t bc = base < last ? base : last;
+    lb = *reinterpret_cast<const uint4*>(lcol + bc);
+    d = *reinterpret_cast<const uint4*>(dig + bc);
+    if constexpr (!ROOT) sv = *reinterpret_cast<const uint4*>(slt + bc);
   };
   uint4 lb0 = lb1, d0 = lb1, s0 = lb1;
   load(r0, lb0, d0, s0);
@@ -417,12 +466,12 @@ __global__ __launch_bounds__(256) void hist_dense_kernel(DenseHistArgs a) {
 #pragma unroll
     for (int j = 0; j < FG; ++j) {
       if (fid[j] < 0) continue;
+      // hot features have <= 64 bins, so every bin byte is < 64: the 2-VALU one-hot, unmasked
       const uint4 kv = *reinterpret_cast<const uint4*>(&s_bins[wid][buf][j][16 * g]);
 #pragma unroll
       for (int bt = 0; bt < BT; ++bt) {
-        const uint32_t rep = (uint32_t)(r + 16 * bt) * 0x01010101u;
-        const i32x4 A = {(int)zero_bytes80(kv.x ^ rep), (int)zero_bytes80(kv.y ^ rep), (int)zero_bytes80(kv.z ^ rep),
-                         (int)zero_bytes80(kv.w ^ rep)};
+        const uint32_t nk = ~((uint32_t)(r + 16 * bt) * 0x01010101u);
+        const i32x4 A = {(int)onehot7(kv.x, nk), (int)onehot7(kv.y, nk), (int)onehot7(kv.z, nk), (int)onehot7(kv.w, nk)};
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
           acc[j][bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[ct], acc[j][bt][ct], 0, 0, 0);
@@ -438,7 +487,23 @@ __global__ __launch_bounds__(256) void hist_dense_kernel(DenseHistArgs a) {
     s1 = s2;
   }
 
+  // destinations first (independent loads), then the atomics
   const int stat = q / NP;
+  int node_of[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int slot = ct * SPT + slot_sub;
+    const int n = a.slot_node[slot < a.nslots ? slot : a.nslots - 1];
+    node_of[ct] = slot < a.nslots ? n : -1;
+  }
+  int nb_of[FG];
+  int64_t bo_of[FG];
+#pragma unroll
+  for (int j = 0; j < FG; ++j) {
+    const int f = fid[j] >= 0 ? fid[j] : 0;
+    nb_of[j] = fid[j] >= 0 ? a.nbins[f] : 0;
+    bo_of[j] = a.boff[f];
+  }
 #pragma unroll
   for (int j = 0; j < FG; ++j)
 #pragma unroll
@@ -447,19 +512,15 @@ __global__ __launch_bounds__(256) void hist_dense_kernel(DenseHistArgs a) {
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int64_t s = -(int64_t)(acc[j][bt][ct][i] >> 7);
+          const int32_t s = -(acc[j][bt][ct][i] >> 7);
           int64_t v = s;
           if constexpr (NP == 4) {
-            const int64_t t1 = __shfl_down(s, 1, kWave), t2 = __shfl_down(s, 2, kWave), t3 = __shfl_down(s, 3, kWave);
-            v = s + t1 * 256 + t2 * 65536 + t3 * 16777216;
+            const int32_t t1 = __shfl_down(s, 1, kWave), t2 = __shfl_down(s, 2, kWave), t3 = __shfl_down(s, 3, kWave);
+            v = (int64_t)s + (int64_t)t1 * 256 + (int64_t)t2 * 65536 + (int64_t)t3 * 16777216;
           }
-          const int slot = ct * SPT + slot_sub;
-          const int f = fid[j];
-          if ((q % NP) != 0 || v == 0 || slot >= a.nslots || f < 0) continue;
-          const int node = a.slot_node[slot];
           const int b = 16 * bt + 4 * g + i;
-          if (node < 0 || b >= a.nbins[f]) continue;
-          int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2 + stat;
+          if ((q % NP) != 0 || v == 0 || node_of[ct] < 0 || b >= nb_of[j]) continue;
+          int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + bo_of[j] + b) * 2 + stat;
           atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
         }
 }
@@ -567,6 +628,7 @@ __global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
   const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
   const int32_t meta = a.item_meta[item];
   const uint32_t koff = (uint32_t)item_koff(meta);
+  const bool fast7 = item_nfeat(meta) > 1 || a.nbins[a.item_f0[item]] <= 128;
   const int r = lane & 15, g = lane >> 4;
   const int slot_sub = r >> 1, q = r & 1;
   // tiles whose 8 slots sampled none of the item's features are skipped (wave-uniform)
@@ -601,13 +663,21 @@ __global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
   for (int64_t base = first; base < e1; base += G) {
     const RowStep cur = nx;
     load_rows(a, base + G + 4 * lane, e0, e1, e_last, nx);     // rows of the next step in flight
-    const int32_t rr[4] = {cur.r4.x, cur.r4.y, cur.r4.z, cur.r4.w};
+    const int4 cr = cur.rows();
+    const int32_t rr[4] = {cr.x, cr.y, cr.z, cr.w};
     uint2 sv[4];
     uint4 wv[4];
 #pragma unroll
+    for (int i = 0; i < 4; ++i) {       // unconditional loads (clamped row), then select
+      sv[i] = rs[rr[i] >= 0 ? rr[i] : 0];
+      wv[i] = rw[rr[i] >= 0 ? rr[i] : 0];
+    }
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
-      sv[i] = rr[i] >= 0 ? rs[rr[i]] : make_uint2(0xffffffffu, 0xffffffffu);
-      wv[i] = rr[i] >= 0 ? rw[rr[i]] : make_uint4(0u, 0u, 0u, 0u);
+      if (rr[i] < 0) {
+        sv[i] = make_uint2(0xffffffffu, 0xffffffffu);
+        wv[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
     }
     *reinterpret_cast<uint32_t*>(&s_key[wid][4 * lane]) = cur.keys4;
 #pragma unroll
@@ -625,12 +695,7 @@ __global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
       const int k0 = ks * KS + 16 * g;
       const uint4 kv = *reinterpret_cast<const uint4*>(&s_key[wid][k0]);
       i32x4 A[BT];
-#pragma unroll
-      for (int bt = 0; bt < BT; ++bt) {
-        const uint32_t rep = ((uint32_t)(r + 16 * bt) + koff) * 0x01010101u;
-        A[bt] = i32x4{(int)zero_bytes80(kv.x ^ rep), (int)zero_bytes80(kv.y ^ rep), (int)zero_bytes80(kv.z ^ rep),
-                      (int)zero_bytes80(kv.w ^ rep)};
-      }
+      onehot_a<BT>(kv, (uint32_t)r + koff, fast7, A);
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         if (!on[ct]) continue;
@@ -649,6 +714,25 @@ __global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
   }
   const int32_t f0 = a.item_f0[item];
   const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta);
+  int node_of[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int slot = ct * 8 + slot_sub;
+    const int n = a.slot_node[slot < a.nslots ? slot : a.nslots - 1];
+    node_of[ct] = slot < a.nslots ? n : -1;
+  }
+  int64_t bin_of[BT][4];
+#pragma unroll
+  for (int bt = 0; bt < BT; ++bt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ek = 16 * bt + 4 * g + i + (int)koff;
+      const int fl = ek >> sl2, b = ek & ((1 << sl2) - 1);
+      const int f = f0 + (fl < nfeat ? fl : 0);
+      const int nb = a.nbins[f];
+      const int64_t bo = a.boff[f];
+      bin_of[bt][i] = (fl < nfeat && b < nb) ? bo + b : -1;
+    }
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
 #pragma unroll
@@ -656,15 +740,8 @@ __global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t v = -(int64_t)(acc[bt][ct][i] >> 7);
-        const int slot = ct * 8 + slot_sub;
-        if (v == 0 || slot >= a.nslots) continue;
-        const int node = a.slot_node[slot];
-        const int ek = 16 * bt + 4 * g + i + (int)koff;
-        const int fl = ek >> sl2, b = ek & ((1 << sl2) - 1);
-        if (node < 0 || fl >= nfeat) continue;
-        const int f = f0 + fl;
-        if (b >= a.nbins[f]) continue;
-        int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2 + q;
+        if (v == 0 || node_of[ct] < 0 || bin_of[bt][i] < 0) continue;
+        int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + bin_of[bt][i]) * 2 + q;
         atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
       }
 }

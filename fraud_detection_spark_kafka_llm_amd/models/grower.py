@@ -35,7 +35,20 @@ from .quantize import Quantized
 
 NEG_INF = float("-inf")
 MAX_CT = 8                      # column tiles per pass (csrc/tree_kernels.hip launch_hist)
-DENSE_RANGE_ROWS = 32768        # rows per wave of the dense hot-feature histogram kernel
+DENSE_RANGE_ROWS = 32768        # max rows per wave of the dense hot-feature histogram kernel
+# waves per dense launch to aim for (>= ~8 per SIMD on 1024 SIMDs): launches with few feature
+# groups (e.g. the handful of hot features with 17..64 bins) get proportionally shorter row ranges
+DENSE_TARGET_WAVES = int(os.environ.get("FDX_DENSE_WAVES", 0))   # 0: always DENSE_RANGE_ROWS
+DENSE_MIN_RANGE = 2048
+
+
+def dense_range_rows(n_rows: int, ngroups: int) -> int:
+    """Rows per wave (multiple of 64) so that ceil(n / rows) * ngroups reaches DENSE_TARGET_WAVES."""
+    if DENSE_TARGET_WAVES <= 0:
+        return DENSE_RANGE_ROWS
+    want = -(-max(n_rows, 1) * max(ngroups, 1) // DENSE_TARGET_WAVES)
+    rows = -(-want // 64) * 64
+    return int(min(DENSE_RANGE_ROWS, max(DENSE_MIN_RANGE, rows)))
 # levels 0..DENSE_MAX_DEPTH build the hot features' histograms with the dense kernel (every row
 # streamed, slot-masked); deeper levels use their CSC items (only live entries multiplied)
 DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
@@ -410,12 +423,13 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                         feat_mask))
                 if use_dense:
                     for bt in (1, 2, 4):
-                        gfid, gden = ws.dense_groups(bt, C.tree_dense_fg(bt, ct if d > 0 else 1), hot_keep)
+                        fg = C.tree_dense_fg(bt, ct if d > 0 else 1)
+                        gfid, gden = ws.dense_groups(bt, fg, hot_keep)
                         if gfid.numel():
+                            rr = dense_range_rows(Q.n_rows, gfid.numel() // fg)
                             launches.append(functools.partial(
                                 C.tree_hist_dense, Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad,
-                                gfid, gden, Q.boff, Q.nbins, s2n, hist_target, TB, Q.n_rows, DENSE_RANGE_ROWS, bt,
-                                ct, np_))
+                                gfid, gden, Q.boff, Q.nbins, s2n, hist_target, TB, Q.n_rows, rr, bt, ct, np_))
                 ws.run_concurrent(launches)
         totals, node_ids = up[h_tot], up[h_ids]
         sub_t = tuple(up[h] for h in h_sub) if h_sub is not None else None

@@ -430,6 +430,22 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
     Q.dense = dense
 
 
+def _relayout_bins(Q: Quantized, width: np.ndarray) -> None:
+    """Give feature f ``width[f] >= nbins[f]`` histogram bins (boff = cumsum(width)); moves the
+    per-bin thresholds to the new offsets."""
+    nb = Q.nbins.cpu().numpy().astype(np.int64)
+    old = np.asarray(Q.boff_host, dtype=np.int64)
+    new = np.zeros(nb.size + 1, dtype=np.int64)
+    np.cumsum(width, out=new[1:])
+    f_of = np.repeat(np.arange(nb.size), nb)
+    off = np.arange(int(old[-1])) - old[:-1][f_of]
+    thr = np.zeros(int(new[-1]), dtype=np.float64)
+    thr[new[:-1][f_of] + off] = np.asarray(Q.thresholds, dtype=np.float64)
+    Q.thresholds = thr
+    Q.boff_host = new
+    Q.boff = torch.from_numpy(new).to(Q.device)
+
+
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
 
@@ -503,6 +519,13 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
             i += 1
         kbase[cols[i0:i0 + k]] = np.arange(k) * st_max
         groups_pk.append((i0, i0 + k, int(np.log2(st_max))))
+    # histogram bin layout: a packed item's features get `stride` bins each (padding bins stay 0),
+    # so the bin of key ek of an item is boff[f0] + ek for every item (one offset per flush)
+    width = nb.copy()
+    for i0, i1, sl2 in groups_pk:
+        width[cols[i0:i1]] = 1 << sl2
+    if np.any(width != nb):
+        _relayout_bins(Q, width)
     parts = []   # arrays of (start, end, f0, sl2, nfeat, koff, bt, blk)
     if groups_pk:
         gp = np.asarray(groups_pk, dtype=np.int64)
