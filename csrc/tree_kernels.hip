@@ -830,8 +830,14 @@ void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s) {
 #undef FDX_HIST_NP
 }
 
-// features per wave of the dense kernel: accumulators FG * BT * CT * 4 registers <= 64
-constexpr int dense_fg(int bt, int ct) { return bt * ct >= 16 ? 1 : 16 / (bt * ct) > 8 ? 8 : 16 / (bt * ct); }
+// features per wave of the dense kernel: accumulators FG * BT * CT * 4 registers <= 64. Only the
+// 16-bin (BT = 1) hot features are numerous enough (~130) to share the row state of a wave; the
+// few wider ones (BT 2 / 4: ~10) take one wave each, otherwise their launches ran ~600 waves on
+// 1,024 SIMDs (measured 2.0 -> 0.85 ms for 9 features; 4 instead of 8 16-bin features per wave
+// doubled that launch instead: 1.7 -> 3.6 ms).
+constexpr int dense_fg(int bt, int ct) {
+  return bt > 1 ? 1 : (ct >= 16 ? 1 : 16 / ct > 8 ? 8 : 16 / ct);
+}
 
 int dense_features_per_wave(int bt, int ct) { return dense_fg(bt, ct); }
 int dense_waves_per_group() { return 1; }
