@@ -407,8 +407,9 @@ void clamp_u8(const Tensor& in, int64_t maxv, const Tensor& out) {
 }
 
 // Row-block segment bounds of sorted-row columns (XCD-aware histogram items).
+// dst[seg_dst[i] + k] = src[seg_src[i] + k] for k < seg_len[i]; keys get + seg_add[i] (uint8, optional)
 void copy_segments(const Tensor& src_row, const Tensor& src_key, const Tensor& seg_src, const Tensor& seg_dst,
-                   const Tensor& seg_len, const Tensor& dst_row, const Tensor& dst_key) {
+                   const Tensor& seg_len, const Tensor& dst_row, const Tensor& dst_key, const optional<Tensor>& seg_add) {
   const auto dev = src_row.device();
   for (const Tensor* t : {&src_key, &seg_src, &seg_dst, &seg_len, &dst_row, &dst_key}) check_dev(*t, dev, "copy_segments");
   TORCH_CHECK(src_row.scalar_type() == at::kInt && dst_row.scalar_type() == at::kInt && src_key.scalar_type() == at::kByte &&
@@ -419,17 +420,64 @@ void copy_segments(const Tensor& src_row, const Tensor& src_key, const Tensor& s
                   seg_src.numel() == seg_dst.numel() && seg_src.numel() == seg_len.numel(),
               "copy_segments sizes");
   const int64_t n = seg_src.numel();
+  const uint8_t* add = nullptr;
+  if (seg_add) {
+    check_dev(*seg_add, dev, "copy_segments");
+    TORCH_CHECK(seg_add->scalar_type() == at::kByte && seg_add->numel() == n && seg_add->is_contiguous(),
+                "seg_add must be [nseg] uint8");
+    add = seg_add->data_ptr<uint8_t>();
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_copy_segments(src_row.data_ptr<int32_t>(), src_key.data_ptr<uint8_t>(), seg_src.data_ptr<int64_t>(),
-                              seg_dst.data_ptr<int64_t>(), seg_len.data_ptr<int64_t>(), n, dst_row.data_ptr<int32_t>(),
+                              seg_dst.data_ptr<int64_t>(), seg_len.data_ptr<int64_t>(), n, add, dst_row.data_ptr<int32_t>(),
                               dst_key.data_ptr<uint8_t>(), c10::hip::getCurrentHIPStream(dev.index()).stream());
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
     fdx::copy_segments_cpu(src_row.data_ptr<int32_t>(), src_key.data_ptr<uint8_t>(), seg_src.data_ptr<int64_t>(),
-                           seg_dst.data_ptr<int64_t>(), seg_len.data_ptr<int64_t>(), n, dst_row.data_ptr<int32_t>(),
+                           seg_dst.data_ptr<int64_t>(), seg_len.data_ptr<int64_t>(), n, add, dst_row.data_ptr<int32_t>(),
                            dst_key.data_ptr<uint8_t>());
   }
+}
+
+// Greedy packing of histogram work items (models/quantize.py _finish_items): runs of consecutive
+// packable features, each run at most `pack_keys` keys at the run's largest stride and at most
+// `max_entries` entries. Returns [runs, 3] int64 (first, end, log2 stride). Host-only.
+Tensor pack_runs(const Tensor& packable, const Tensor& stride, const Tensor& ncol, int64_t pack_keys,
+                 int64_t max_entries) {
+  TORCH_CHECK(!packable.is_cuda() && packable.scalar_type() == at::kByte && stride.scalar_type() == at::kLong &&
+                  ncol.scalar_type() == at::kLong && packable.numel() == stride.numel() &&
+                  stride.numel() == ncol.numel(),
+              "pack_runs: host uint8 packable, int64 stride/ncol of equal length");
+  const auto pk = packable.contiguous();
+  const auto st = stride.contiguous();
+  const auto nc = ncol.contiguous();
+  const uint8_t* p = pk.data_ptr<uint8_t>();
+  const int64_t* s = st.data_ptr<int64_t>();
+  const int64_t* c = nc.data_ptr<int64_t>();
+  const int64_t S = pk.numel();
+  std::vector<int64_t> out;
+  int64_t i = 0;
+  while (i < S) {
+    if (!p[i]) { ++i; continue; }
+    const int64_t i0 = i;
+    int64_t st_max = s[i], ent = 0, k = 0;
+    while (i < S && p[i]) {
+      const int64_t s2 = std::max(st_max, s[i]);
+      if ((k + 1) * s2 > pack_keys || ent + c[i] > max_entries) break;
+      st_max = s2;
+      ent += c[i];
+      ++k;
+      ++i;
+    }
+    if (k == 0) { ++i; continue; }   // a single feature over the limits: not packed (caller treats it as single)
+    int64_t l2 = 0;
+    while ((int64_t(1) << l2) < st_max) ++l2;
+    out.insert(out.end(), {i0, i0 + k, l2});
+  }
+  auto res = torch::empty({(int64_t)out.size() / 3, 3}, torch::kLong);
+  std::copy(out.begin(), out.end(), res.data_ptr<int64_t>());
+  return res;
 }
 
 void block_bounds(const Tensor& csc_row, const Tensor& colptr, const Tensor& cols, int64_t nblk, int64_t row_block,
@@ -501,7 +549,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spmv_t", &spmv_t, "g += X^T r (CSR, fp64)");
   m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
   m.def("clamp_u8", &clamp_u8, "uint8 clamp (bins)");
-  m.def("copy_segments", &copy_segments, "segment copy of (row, key) arrays");
+  m.def("copy_segments", &copy_segments, "segment copy of (row, key) arrays (+ per-segment key offset)");
+  m.def("pack_runs", &pack_runs, "greedy packing runs of histogram work items (host)");
   m.def("block_bounds", &block_bounds, "row-block segment bounds of sorted-row columns");
   m.def("feature_order", &feature_order, "CSR -> CSC by feature (radix sort), docFreq and max count per feature");
   m.def("encode_records", &encode_records, "json.dumps-identical classification records (batch)");

@@ -62,9 +62,10 @@ void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, h
 void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
                          int64_t row_block, int64_t* bounds, hipStream_t s);
 void launch_copy_segments(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
-                          const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key, hipStream_t s);
+                          const int64_t* seg_len, int64_t nseg, const uint8_t* seg_add, int32_t* dst_row, uint8_t* dst_key,
+                          hipStream_t s);
 void copy_segments_cpu(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
-                       const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key);
+                       const int64_t* seg_len, int64_t nseg, const uint8_t* seg_add, int32_t* dst_row, uint8_t* dst_key);
 void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
                       int64_t row_block, int64_t* bounds);
 

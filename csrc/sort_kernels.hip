@@ -116,12 +116,14 @@ __global__ __launch_bounds__(256) void copy_segments_kernel(const int32_t* __res
                                                             const int64_t* __restrict__ seg_src,
                                                             const int64_t* __restrict__ seg_dst,
                                                             const int64_t* __restrict__ seg_len, int64_t nseg,
+                                                            const uint8_t* __restrict__ seg_add,
                                                             int32_t* __restrict__ dst_row, uint8_t* __restrict__ dst_key) {
   for (int64_t i = blockIdx.x; i < nseg; i += gridDim.x) {
     const int64_t a = seg_src[i], d = seg_dst[i], n = seg_len[i];
+    const uint8_t add = seg_add ? seg_add[i] : (uint8_t)0;
     for (int64_t k = threadIdx.x; k < n; k += 256) {
       dst_row[d + k] = src_row[a + k];
-      dst_key[d + k] = src_key[a + k];
+      dst_key[d + k] = (uint8_t)(src_key[a + k] + add);
     }
   }
 }
@@ -196,11 +198,12 @@ void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const in
 }
 
 void launch_copy_segments(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
-                          const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key, hipStream_t s) {
+                          const int64_t* seg_len, int64_t nseg, const uint8_t* seg_add, int32_t* dst_row, uint8_t* dst_key,
+                          hipStream_t s) {
   if (nseg <= 0) return;
   const unsigned grid = (unsigned)(nseg < 65536 ? nseg : 65536);
   hipLaunchKernelGGL(copy_segments_kernel, dim3(grid), dim3(256), 0, s, src_row, src_key, seg_src, seg_dst, seg_len, nseg,
-                     dst_row, dst_key);
+                     seg_add, dst_row, dst_key);
 }
 
 void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, hipStream_t s) {

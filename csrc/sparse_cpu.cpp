@@ -134,11 +134,12 @@ void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32
 }
 
 void copy_segments_cpu(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
-                       const int64_t* seg_len, int64_t nseg, int32_t* dst_row, uint8_t* dst_key) {
+                       const int64_t* seg_len, int64_t nseg, const uint8_t* seg_add, int32_t* dst_row, uint8_t* dst_key) {
   parallel_for(nseg, 0, 64, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
       std::copy(src_row + seg_src[i], src_row + seg_src[i] + seg_len[i], dst_row + seg_dst[i]);
-      std::copy(src_key + seg_src[i], src_key + seg_src[i] + seg_len[i], dst_key + seg_dst[i]);
+      const uint8_t add = seg_add ? seg_add[i] : (uint8_t)0;
+      for (int64_t k = 0; k < seg_len[i]; ++k) dst_key[seg_dst[i] + k] = (uint8_t)(src_key[seg_src[i] + k] + add);
     }
   });
 }

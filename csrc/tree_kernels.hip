@@ -236,8 +236,6 @@ __device__ __forceinline__ void gather_digits(const uint2* __restrict__ rd, int4
 // Tile: v_mfma_i32_16x16x64_i8, lane l: r = l & 15 (A row = key r + 16 bt + koff, B column r),
 // g = l >> 4 (entries 16g .. 16g+15 of the K-step); C[key 4g + i][col r] in register i.
 // Columns: slot_sub = r / (2 NP) within the tile, q = r % (2 NP) = statistic * NP + plane.
-// The bins of an item's keys are contiguous: bin of key ek = boff[f0] + ek (packed features are
-// laid out with the item's key stride, models/quantize.py), so the epilogue needs one offset.
 // ROOT: every entry of the item is live in slot 0 (no slot table, no compaction: the lane's 4
 // digit words are transposed into plane-major LDS rows in registers). Otherwise the live entries
 // (row in a node of this pass) are compacted, and K-steps run on ceil(live / 64) groups.
@@ -267,7 +265,6 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   const uint32_t koff = (uint32_t)item_koff(meta);
   // every key of the item's entries is < 128 (packed items: < 64; single features: < nbins)
   const bool fast7 = item_nfeat(meta) > 1 || a.nbins[f0] <= 128;
-  const int64_t hbase = a.boff[f0];
 
   const int r = lane & 15, g = lane >> 4;
   const int slot_sub = r / CPS, q = r % CPS;
@@ -377,7 +374,22 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
 
   // Epilogue: C = -128 * (plane sum); lanes r .. r+NP-1 hold the NP planes of one (slot, stat)
   // column: the plane-0 lane recombines them into int64 and adds the nonzero sums to the
-  // histogram (keys without entries, past the item's features or bins, sum to 0).
+  // histogram. The bin offset of each of the lane's key rows is loaded first, all at once (clamped
+  // indices), so no atomic waits on a dependent load. (A padded bin layout with one offset per item
+  // would depend on each rank's local packing and break the data-parallel histogram shapes.)
+  const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta);
+  int64_t bin_of[BT][4];
+#pragma unroll
+  for (int bt = 0; bt < BT; ++bt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ek = 16 * bt + 4 * g + i + (int)koff;
+      const int fl = ek >> sl2, b = ek & ((1 << sl2) - 1);
+      const int f = f0 + (fl < nfeat ? fl : 0);
+      const int nb = a.nbins[f];
+      const int64_t bo = a.boff[f];
+      bin_of[bt][i] = (fl < nfeat && b < nb) ? bo + b : -1;
+    }
   const int stat = q / NP;
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
@@ -391,9 +403,8 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
           const int32_t s1 = __shfl_down(s, 1, kWave), s2 = __shfl_down(s, 2, kWave), s3 = __shfl_down(s, 3, kWave);
           v = (int64_t)s + (int64_t)s1 * 256 + (int64_t)s2 * 65536 + (int64_t)s3 * 16777216;
         }
-        if ((q % NP) != 0 || v == 0 || node_of[ct] < 0) continue;
-        const int ek = 16 * bt + 4 * g + i + (int)koff;
-        int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + hbase + ek) * 2 + stat;
+        if ((q % NP) != 0 || v == 0 || node_of[ct] < 0 || bin_of[bt][i] < 0) continue;
+        int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + bin_of[bt][i]) * 2 + stat;
         atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
       }
 }

@@ -281,19 +281,28 @@ def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_
                 colptr[:-1] = fo.colptr[:-1][active]
                 colptr[-1] = fo.colptr[1:][active][-1]
         else:                                     # drop the entries of inactive features (scale 0)
-            keep = torch.repeat_interleave(active, lens, output_size=nnz_all)
-            n_keep = int(keep.sum())
-            row_buf = torch.zeros(n_keep + CSC_PAD, dtype=torch.int32, device=dev)
-            row_buf[:n_keep] = fo.csc_row[keep]
-            csc_row = row_buf[:n_keep]
-            cnt = fo.csc_cnt[keep]
             colptr = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
             torch.cumsum(lens[active], 0, out=colptr[1:])
+            n_keep = int(colptr[-1])
+            row_buf = torch.zeros(n_keep + CSC_PAD, dtype=torch.int32, device=dev)
+            csc_row = row_buf[:n_keep]
+            cnt = None
         n = int(csc_row.numel())
         bin_buf = torch.full((n + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
-        if cnt.is_cuda and cnt.data_ptr() % 16:           # compacted copy: realign for the native clamp
-            cnt = cnt.clone()
-        native.lib().clamp_u8(cnt.contiguous(), max_bins - 1, bin_buf[:n])
+        if cnt is not None:
+            if cnt.is_cuda and cnt.data_ptr() % 16:           # realign for the native clamp
+                cnt = cnt.clone()
+            native.lib().clamp_u8(cnt.contiguous(), max_bins - 1, bin_buf[:n])
+        else:
+            # bins of every entry in feature order, then one segment copy of the active features'
+            # (row, bin) ranges (instead of a boolean mask over all nnz entries)
+            full_bin = torch.empty(nnz_all + CSC_PAD, dtype=torch.uint8, device=dev)
+            native.lib().clamp_u8(fo.csc_cnt[:nnz_all].contiguous(), max_bins - 1, full_bin[:nnz_all])
+            if Fa:
+                native.lib().copy_segments(fo.csc_row[:nnz_all], full_bin[:nnz_all], fo.colptr[:-1][active].contiguous(),
+                                           colptr[:-1].contiguous(), lens[active].contiguous(), csc_row, bin_buf[:n],
+                                           None)
+            del full_bin
     boff = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
     torch.cumsum(nb, 0, out=boff[1:])
     Q = Quantized(N, F, fid_orig, nbins.contiguous(), torch.zeros(Fa, dtype=torch.int32, device=dev), boff,
@@ -430,22 +439,6 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
     Q.dense = dense
 
 
-def _relayout_bins(Q: Quantized, width: np.ndarray) -> None:
-    """Give feature f ``width[f] >= nbins[f]`` histogram bins (boff = cumsum(width)); moves the
-    per-bin thresholds to the new offsets."""
-    nb = Q.nbins.cpu().numpy().astype(np.int64)
-    old = np.asarray(Q.boff_host, dtype=np.int64)
-    new = np.zeros(nb.size + 1, dtype=np.int64)
-    np.cumsum(width, out=new[1:])
-    f_of = np.repeat(np.arange(nb.size), nb)
-    off = np.arange(int(old[-1])) - old[:-1][f_of]
-    thr = np.zeros(int(new[-1]), dtype=np.float64)
-    thr[new[:-1][f_of] + off] = np.asarray(Q.thresholds, dtype=np.float64)
-    Q.thresholds = thr
-    Q.boff_host = new
-    Q.boff = torch.from_numpy(new).to(Q.device)
-
-
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
 
@@ -467,7 +460,8 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     nb = Q.nbins.cpu().numpy().astype(np.int64)
     Fa = int(nb.size)
     hot = (n >= hot_density * max(Q.n_rows, 1)) & (nb <= 64) & (n > 0) if hot_density > 0 else np.zeros(Fa, bool)
-    _build_dense(Q, np.nonzero(hot)[0])
+    with tracing.span("q.dense"):
+        _build_dense(Q, np.nonzero(hot)[0])
     # hot features stay in the histogram CSC too (deep levels use it: only their live entries are
     # multiplied there, while the dense kernel masks every row); they are never packed
     cols = np.nonzero(n > 0)[0]
@@ -487,7 +481,6 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
         total = int(flat.sum())
         h_row = torch.zeros(total + CSC_PAD, dtype=torch.int32, device=dev)
         h_key = torch.full((total + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
-        C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total])
         hptr = np.zeros((nsb, S + 1), dtype=np.int64)                  # [sb][i] start of cols[i] in super-block sb
         dst_host = seg_dst.cpu().numpy().reshape(nsb, S)
         hptr[:, :S] = dst_host
@@ -504,28 +497,13 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     packable = (ncol <= chunk * nsb) & (nb[cols] <= 16) & ~hot[cols]
     stride = _pow2_at_least(nb[cols], 2)
     kbase = np.zeros(Fa, dtype=np.int64)
-    groups_pk = []   # (i0, i1, sl2)
-    i = 0
-    while i < S:
-        if not packable[i]:
-            i += 1
-            continue
-        i0, st_max, ent, k = i, int(stride[i]), 0, 0
-        while i < S and packable[i]:
-            s2 = max(st_max, int(stride[i]))
-            if (k + 1) * s2 > PACK_KEYS or ent + int(ncol[i]) > chunk * nsb:
-                break
-            st_max, ent, k = s2, ent + int(ncol[i]), k + 1
-            i += 1
-        kbase[cols[i0:i0 + k]] = np.arange(k) * st_max
-        groups_pk.append((i0, i0 + k, int(np.log2(st_max))))
-    # histogram bin layout: a packed item's features get `stride` bins each (padding bins stay 0),
-    # so the bin of key ek of an item is boff[f0] + ek for every item (one offset per flush)
-    width = nb.copy()
+    # greedy runs of consecutive packable features (native: a Python loop over ~30K features cost
+    # tens of ms): each run <= PACK_KEYS keys at the run's largest stride, <= chunk * nsb entries
+    gp = native.lib().pack_runs(torch.from_numpy(packable.astype(np.uint8)), torch.from_numpy(stride.astype(np.int64)),
+                                torch.from_numpy(ncol.astype(np.int64)), int(PACK_KEYS), int(chunk * nsb)).numpy()
+    groups_pk = [(int(a), int(b), int(c)) for a, b, c in gp]
     for i0, i1, sl2 in groups_pk:
-        width[cols[i0:i1]] = 1 << sl2
-    if np.any(width != nb):
-        _relayout_bins(Q, width)
+        kbase[cols[i0:i1]] = np.arange(i1 - i0) << sl2
     parts = []   # arrays of (start, end, f0, sl2, nfeat, koff, bt, blk)
     if groups_pk:
         gp = np.asarray(groups_pk, dtype=np.int64)
@@ -559,11 +537,10 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
             parts.append(np.stack([st[sel], en[sel], f_[sel], np.full(m, 8), np.ones(m, np.int64),
                                    np.full(m, 64 * w), btw, b_[sel]], 1))
     items = np.concatenate(parts) if parts else np.zeros((0, 8), np.int64)
-    # --- keys of the histogram CSC: kbase + bin
-    if S and kbase.any():
-        lens = torch.from_numpy(seg_n.reshape(-1)).to(dev)
-        kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev)
-        h_key[:total].add_(torch.repeat_interleave(kb, lens, output_size=total))
+    # --- the histogram CSC: (row, kbase + bin) of every (super-block, feature) segment
+    if S:
+        kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev) if kbase.any() else None
+        C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total], kb)
     arr = items.astype(np.int64)
     is_hot = hot[arr[:, 2]] & (arr[:, 4] == 1) if arr.shape[0] else np.zeros(0, bool)
     t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).astype(dt)).to(dev)   # noqa: E731
