@@ -11,7 +11,8 @@
             featurize+score) -> output topic, with explanations from the stub LLM; dialogues/s and
             p50 / p95 batch latency
 
-Data are synthetic (data/synth.py); weights are trained, not random. Usage:
+Data are synthetic (data/synth.py); weights are trained, not random. Each GPU bench first runs an
+untimed 2-tree warm-up fit (models/warmup.py: lazy kernel code-object loading). Usage:
   python bench/suite.py {dt_cpu,gbdt_1m,rf,xgb,kafka,all} [--rows N] [--trees T]
 """
 import argparse
@@ -30,6 +31,7 @@ import torch
 from gbdt_train import build_features  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ml.tree_model import ensemble_arrays  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order, score_csr  # noqa: E402
 
 F = 1 << 18
@@ -70,6 +72,7 @@ def bench_gbdt_1m(args) -> dict:
 
     dev = torch.device("cuda:0")
     rows = args.rows or 1_000_000
+    warm_tree_kernels(dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     vc, y, idf = _tfidf(rows, dev, seed=11)
@@ -78,11 +81,13 @@ def bench_gbdt_1m(args) -> dict:
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees or 100, max_depth=6), device=dev)
     torch.cuda.synchronize()
     t_train = time.perf_counter() - t0
+    t_fit = t_train - t_feat
     tv, ty, _ = _tfidf(200_000, dev, seed=11, first_row=10 ** 9, idf=idf)
     m = res.base_margin + score_csr(tv, ensemble_arrays(res.trees, "value"))[:, 0]
     m = m.cpu().numpy()
     return {"bench": "gbdt_1m", "rows": rows, "trees": len(res.trees), "depth": 6, "featurize_s": t_feat,
-            "train_s": t_train, "heldout_rows": 200_000, **_metrics(ty.cpu().numpy(), m, (m > 0).astype(float))}
+            "train_s": t_train, "fit_only_s": t_fit, "per_tree_ms": t_fit / max(len(res.trees), 1) * 1e3,
+            "heldout_rows": 200_000, **_metrics(ty.cpu().numpy(), m, (m > 0).astype(float))}
 
 
 def bench_rf(args) -> dict:
@@ -91,6 +96,7 @@ def bench_rf(args) -> dict:
     dev = torch.device("cuda:0")
     rows = args.rows or 10_000_000
     trees = args.trees or 500
+    warm_tree_kernels(dev, gbdt_depth=0, forest_depth=5, forest_subset=args.subset)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     vc, y, idf = _tfidf(rows, dev, seed=21)
@@ -116,6 +122,7 @@ def bench_xgb(args) -> dict:
     dev = torch.device("cuda:0")
     rows = args.rows or 12_500_000
     trees = args.trees or 1000
+    warm_tree_kernels(dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     vc, y, idf = _tfidf(rows, dev, seed=31)

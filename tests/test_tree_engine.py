@@ -488,3 +488,10 @@ def test_gpu_multi_tree_rf_batches_equal_single_tree_and_host(monkeypatch):
     monkeypatch.setenv("FDX_RF_BATCH", "0")
     g1 = sig(fit_forest(vc, torch.from_numpy(y), device="cuda:0", **kw))
     assert g == g1 == h
+
+
+def test_warm_tree_kernels_runs_the_production_path_on_the_host():
+    """models/warmup.py (the untimed warm-up of bench.py / bench/suite.py) on the host path."""
+    from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels
+
+    warm_tree_kernels("cpu", rows=1500, gbdt_depth=3, forest_depth=3)
