@@ -476,6 +476,27 @@ void hist_subtract(const Tensor& parent, const Tensor& cur, const Tensor& dst, c
   }
 }
 
+// best split per node: packed [nodes, 5] int64 {gain bits, feature + f0, bin, left0, left1}
+void split_best(const Tensor& gain, const Tensor& bin, const Tensor& left, int64_t f0, const Tensor& out) {
+  const auto dev = gain.device();
+  chk(gain, dev, at::kDouble, "gain");
+  chk(bin, dev, at::kInt, "bin");
+  chk(left, dev, at::kLong, "left");
+  chk(out, dev, at::kLong, "out");
+  FDX_CHECK(gain.dim() == 2 && bin.sizes() == gain.sizes() && left.numel() == 2 * gain.numel(), "gain/bin [n, Fa], left [n, Fa, 2]");
+  const int32_t nodes = (int32_t)gain.size(0), Fa = (int32_t)gain.size(1);
+  FDX_CHECK(out.numel() == 5ll * nodes, "out must be [nodes, 5]");
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_split_best(gain.data_ptr<double>(), bin.data_ptr<int32_t>(), left.data_ptr<int64_t>(), nodes, Fa, f0,
+                           out.data_ptr<int64_t>(), stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::split_best_cpu(gain.data_ptr<double>(), bin.data_ptr<int32_t>(), left.data_ptr<int64_t>(), nodes, Fa, f0,
+                        out.data_ptr<int64_t>());
+  }
+}
+
 void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, const Tensor& nbins, const Tensor& zbin,
                 const Tensor& fid_orig, const Tensor& node_ids, const Tensor& kexp, int64_t mode, double lambda_,
                 double mcw, const optional<Tensor>& feat_thr, int64_t seed, int64_t tree, const Tensor& out_gain,
@@ -626,6 +647,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_quant_max", &quant_max);
   m.def("tree_quant", &quant);
   m.def("tree_slot8", &slot8);
+  m.def("tree_split_best", &split_best);
   m.def("tree_hist_build", &hist_build);
   m.def("tree_rf_sample", &rf_sample);
   m.def("tree_rf_rows", &rf_rows);

@@ -93,6 +93,8 @@ void hist_rf_cpu(const HistArgs& h, int bt);
 void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s);
 void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);
+void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
+                       int64_t f0, int64_t* out, hipStream_t s);
 void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s);
 void launch_hist_dense(const DenseHistArgs& a, int bt, int ct, int np, hipStream_t s);
 int dense_features_per_wave(int bt, int ct);
@@ -107,6 +109,8 @@ void launch_leaf_update(double* margin, const int32_t* row_node, const double* n
 void quant_max_cpu(const QuantArgs& a, double* out);
 void quant_cpu(const QuantArgs& a, const double* maxv);
 void slot8_cpu(const SlotArgs& a);
+void split_best_cpu(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa, int64_t f0,
+                    int64_t* out);
 void hist_cpu(const HistArgs& h, int bt, int np);
 void hist_dense_cpu(const DenseHistArgs& a, int fg, int np);
 void hist_subtract_cpu(const int64_t* parent, int64_t* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,

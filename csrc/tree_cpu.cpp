@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -245,6 +246,29 @@ void split_cpu(const SplitArgs& a) {
       a.out_left[2 * t + 1] = l1;
     }
   });
+}
+
+void split_best_cpu(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa, int64_t f0,
+                    int64_t* out) {
+  for (int n = 0; n < nodes; ++n) {
+    const double* g = gain + (int64_t)n * Fa;
+    double best = -INFINITY;
+    int bf = Fa;
+    bool nan = false;
+    for (int f = 0; f < Fa; ++f) {
+      if (std::isnan(g[f])) nan = true;
+      else if (g[f] > best) { best = g[f]; bf = f; }
+    }
+    if (nan) { best = std::nan(""); bf = 0; }
+    if (bf >= Fa) bf = 0;
+    const int64_t t = (int64_t)n * Fa + bf;
+    int64_t* o = out + 5 * (int64_t)n;
+    std::memcpy(&o[0], &best, sizeof(double));
+    o[1] = bf + f0;
+    o[2] = bin[t];
+    o[3] = left[2 * t];
+    o[4] = left[2 * t + 1];
+  }
 }
 
 void partition_cpu(const PartitionArgs& a) {

@@ -119,7 +119,15 @@ __global__ __launch_bounds__(256) void quant_max_kernel(QuantArgs a, unsigned lo
     m0 = fmax(m0, __shfl_xor(m0, o, kWave));
     m1 = fmax(m1, __shfl_xor(m1, o, kWave));
   }
-  if ((threadIdx.x & (kWave - 1)) == 0) {
+  // one atomic per block: per-wave atomics on the same two addresses serialised in L2 (16K of
+  // them took ~0.2 ms per round at 10M rows)
+  __shared__ double s_m[2][4];
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) { s_m[0][w] = m0; s_m[1][w] = m1; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m0 = fmax(fmax(s_m[0][0], s_m[0][1]), fmax(s_m[0][2], s_m[0][3]));
+    m1 = fmax(fmax(s_m[1][0], s_m[1][1]), fmax(s_m[1][2], s_m[1][3]));
     atomicMax(out, (unsigned long long)__double_as_longlong(m0));
     atomicMax(out + 1, (unsigned long long)__double_as_longlong(m1));
   }
@@ -151,7 +159,13 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
     t0 += __shfl_xor(t0, o, kWave);
     t1 += __shfl_xor(t1, o, kWave);
   }
-  if ((threadIdx.x & (kWave - 1)) == 0) {
+  __shared__ int64_t s_t[2][4];                 // one (exact, order-free) atomic per block
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) { s_t[0][w] = t0; s_t[1][w] = t1; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    t0 = s_t[0][0] + s_t[0][1] + s_t[0][2] + s_t[0][3];
+    t1 = s_t[1][0] + s_t[1][1] + s_t[1][2] + s_t[1][3];
     atomicAdd(reinterpret_cast<unsigned long long*>(a.totals), (unsigned long long)t0);
     atomicAdd(reinterpret_cast<unsigned long long*>(a.totals) + 1, (unsigned long long)t1);
   }
@@ -346,9 +360,13 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
       s_slot[wid][nb + lane] = 0xffu;
     }
     lds_sync();
-#pragma unroll
-    for (int ks = 0; ks < G / KS; ++ks) {
-      if (ks * KS >= n_live) break;
+    // K-steps over the live entries only. CT >= 4: a rolled loop (one exit), because breaking
+    // out of the unrolled one made the compiler copy all CT * 4 accumulators between AGPRs and
+    // VGPRs at each exit (32 extra VGPRs at CT = 8: 2 instead of 3 waves per SIMD)
+    const int nks = (n_live + KS - 1) / KS;
+    constexpr int KUNROLL = CT >= 4 ? 1 : G / KS;
+#pragma unroll KUNROLL
+    for (int ks = 0; ks < nks; ++ks) {
       const int k0 = ks * KS + 16 * g;
       const uint4 kv = *reinterpret_cast<const uint4*>(&s_key[wid][k0]);
       const uint4 dv = *reinterpret_cast<const uint4*>(&s_dig[wid][q][k0]);
@@ -360,13 +378,31 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
         for (int bt = 0; bt < BT; ++bt) acc[bt][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[bt], B, acc[bt][0], 0, 0, 0);
       } else {
         const uint4 sv = *reinterpret_cast<const uint4*>(&s_slot[wid][k0]);
-        i32x4 B[CT];
-        slot_masked_b<CT, NP>(dv, sv, slot_sub, B);
+        if constexpr (NP == 4) {
+          // B of one column tile at a time (the parity-masked digits and the tile selectors stay
+          // live, not CT built operands: CT = 8 needed 32 more VGPRs and ran at 2 waves per SIMD)
+          const uint32_t pat = (0x80u | (uint32_t)(slot_sub ^ 1)) * 0x01010101u;
+          const uint4 dm = make_uint4(dv.x & live_parity_mask(sv.x, pat), dv.y & live_parity_mask(sv.y, pat),
+                                      dv.z & live_parity_mask(sv.z, pat), dv.w & live_parity_mask(sv.w, pat));
+          const uint4 sel = make_uint4((sv.x >> 1) & 0x07070707u, (sv.y >> 1) & 0x07070707u,
+                                       (sv.z >> 1) & 0x07070707u, (sv.w >> 1) & 0x07070707u);
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
+          for (int ct = 0; ct < CT; ++ct) {
+            const i32x4 B = {(int)(dm.x & ct_select(sel.x, ct)), (int)(dm.y & ct_select(sel.y, ct)),
+                             (int)(dm.z & ct_select(sel.z, ct)), (int)(dm.w & ct_select(sel.w, ct))};
 #pragma unroll
-          for (int bt = 0; bt < BT; ++bt)
-            acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[bt], B[ct], acc[bt][ct], 0, 0, 0);
+            for (int bt = 0; bt < BT; ++bt)
+              acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[bt], B, acc[bt][ct], 0, 0, 0);
+          }
+        } else {
+          i32x4 B[CT];
+          slot_masked_b<CT, NP>(dv, sv, slot_sub, B);
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int bt = 0; bt < BT; ++bt)
+              acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[bt], B[ct], acc[bt][ct], 0, 0, 0);
+        }
       }
     }
     lds_sync();
@@ -403,9 +439,10 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
           const int32_t s1 = __shfl_down(s, 1, kWave), s2 = __shfl_down(s, 2, kWave), s3 = __shfl_down(s, 3, kWave);
           v = (int64_t)s + (int64_t)s1 * 256 + (int64_t)s2 * 65536 + (int64_t)s3 * 16777216;
         }
-        if ((q % NP) != 0 || v == 0 || node_of[ct] < 0 || bin_of[bt][i] < 0) continue;
-        int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + bin_of[bt][i]) * 2 + stat;
-        atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
+        if ((q % NP) == 0 && v != 0 && node_of[ct] >= 0 && bin_of[bt][i] >= 0) {
+          int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + bin_of[bt][i]) * 2 + stat;
+          atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
+        }
       }
 }
 
@@ -569,6 +606,56 @@ __global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
   a.out_bin[t] = bin;
   a.out_left[2 * t] = l0;
   a.out_left[2 * t + 1] = l1;
+}
+
+// Best split per node over the per-feature results of split_kernel, as one int64 row
+// {gain bits, feature + f0, bin, left0, left1}: the largest gain, ties to the lowest feature; a
+// NaN gain anywhere makes the node's gain NaN (feature 0), like the torch max/where it replaces.
+__global__ __launch_bounds__(256) void split_best_kernel(const double* gain, const int32_t* bin, const int64_t* left,
+                                                         int32_t Fa, int64_t f0, int64_t* out) {
+  const int n = blockIdx.x;
+  const double* g = gain + (int64_t)n * Fa;
+  double best = -1.0 / 0.0;
+  int bf = Fa;
+  bool nan = false;
+  for (int f = threadIdx.x; f < Fa; f += 256) {
+    const double v = g[f];
+    if (v != v) nan = true;
+    else if (v > best || (v == best && f < bf)) { best = v; bf = f; }
+  }
+  __shared__ double s_g[256];
+  __shared__ int s_f[256];
+  __shared__ int s_nan;
+  if (threadIdx.x == 0) s_nan = 0;
+  __syncthreads();
+  if (nan) s_nan = 1;
+  s_g[threadIdx.x] = best;
+  s_f[threadIdx.x] = bf;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const double v = s_g[threadIdx.x + o];
+      const int f = s_f[threadIdx.x + o];
+      if (v > s_g[threadIdx.x] || (v == s_g[threadIdx.x] && f < s_f[threadIdx.x])) {
+        s_g[threadIdx.x] = v;
+        s_f[threadIdx.x] = f;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double bg = s_g[0];
+    int f = s_f[0];
+    if (s_nan) { bg = __longlong_as_double(0x7ff8000000000000ll); f = 0; }
+    if (f >= Fa) f = 0;                      // every gain -inf: feature 0 (its bin is -1)
+    const int64_t t = (int64_t)n * Fa + f;
+    int64_t* o = out + 5 * (int64_t)n;
+    o[0] = __double_as_longlong(bg);
+    o[1] = f + f0;
+    o[2] = bin[t];
+    o[3] = left[2 * t];
+    o[4] = left[2 * t + 1];
+  }
 }
 
 // ------------------------------------------------------------------ multi-tree RF passes (PAR-05)
@@ -885,6 +972,11 @@ void launch_split(const SplitArgs& a, hipStream_t s) {
   const int64_t n = (int64_t)a.num_nodes * a.Fa;
   if (n <= 0) return;
   hipLaunchKernelGGL(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
+                       int64_t f0, int64_t* out, hipStream_t s) {
+  if (nodes > 0 && Fa > 0) hipLaunchKernelGGL(split_best_kernel, dim3(nodes), dim3(256), 0, s, gain, bin, left, Fa, f0, out);
 }
 
 void launch_partition(const PartitionArgs& a, hipStream_t s) {

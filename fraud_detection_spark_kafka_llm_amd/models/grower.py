@@ -268,15 +268,12 @@ def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, p
     C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, int(params.mode),
                       float(params.lambda_), float(params.min_child), feat_thr, int(params.seed), int(tree_index),
                       out_gain, out_bin, out_left, node_tree)
-    # best gain per node, ties to the lowest feature index (deterministic whatever the batch shape)
-    best_gain = torch.max(out_gain, dim=1).values
-    cand = torch.arange(Fa, device=dev).expand(nl, Fa)
-    best_f = torch.where(out_gain == best_gain[:, None], cand, Fa).min(dim=1).values
-    best_f = torch.where(best_f >= Fa, 0, best_f)
-    ar = torch.arange(nl, device=dev)
-    best_bin = out_bin[ar, best_f].to(torch.int64)
-    best_left = out_left[ar, best_f]
-    return torch.cat([best_gain.view(torch.int64)[:, None], (best_f + f0)[:, None], best_bin[:, None], best_left], 1)
+    # best gain per node, ties to the lowest feature index (deterministic whatever the batch shape):
+    # one native reduction instead of ~9 small torch launches per level
+    out = torch.empty((nl, 5), dtype=torch.int64, device=dev)
+    if nl:
+        C.tree_split_best(out_gain, out_bin, out_left, int(f0), out)
+    return out
 
 
 def _choose_np(params: GrowParams, weight) -> int:
