@@ -114,7 +114,8 @@ void quant(const optional<Tensor>& g, const optional<Tensor>& h, const optional<
 }
 
 // slot8[r] = node_slot[row_node[r]] - slot_base if in [0, nslots), else 0xff
-void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, int64_t nslots, const Tensor& out) {
+void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, int64_t nslots, const Tensor& out,
+           const optional<Tensor>& rowdig, const optional<Tensor>& masked) {
   const auto dev = row_node.device();
   chk(row_node, dev, at::kInt, "row_node");
   chk(node_slot, dev, at::kInt, "node_slot");
@@ -129,6 +130,14 @@ void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, i
   a.nslots = (int32_t)nslots;
   a.N = row_node.numel();
   a.slot8 = out.data_ptr<uint8_t>();
+  if (masked) {   // single-slot pass: digit words of the slot's rows, zero elsewhere (root-style pass)
+    FDX_CHECK(rowdig.has_value() && nslots == 1, "masked digits: single-slot passes with rowdig");
+    chk(*rowdig, dev, at::kInt, "rowdig");
+    chk(*masked, dev, at::kInt, "masked");
+    FDX_CHECK(rowdig->numel() == 2 * a.N && masked->numel() == 2 * a.N, "rowdig / masked must be [N, 2] int32");
+    a.rowdig = reinterpret_cast<const uint32_t*>(rowdig->data_ptr<int32_t>());
+    a.masked = reinterpret_cast<uint32_t*>(masked->data_ptr<int32_t>());
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_slot8(a, stream(dev));
@@ -603,6 +612,133 @@ void partition(const Tensor& row_node, const Tensor& default_child, const Tensor
   }
 }
 
+// Device level loop (tree.h level_plan): applies the level's best splits and plans the next level.
+void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_depth, double min_gain, const Tensor& zbin,
+                const optional<Tensor>& hot_row, const Tensor& n_nodes, const Tensor& stats, const Tensor& parent,
+                const Tensor& left, const Tensor& right, const Tensor& feat, const Tensor& bin, const Tensor& leaf,
+                const Tensor& gain, const Tensor& open, const Tensor& n_open, const Tensor& default_child,
+                const optional<Tensor>& node_dense, const Tensor& cs_feat, const Tensor& cs_default,
+                const Tensor& cs_other, const Tensor& cs_bin, const Tensor& cs_left_default, const Tensor& counts,
+                const Tensor& next_open, const Tensor& next_totals, const Tensor& node_slot, const Tensor& s2n,
+                const Tensor& sub_dst, const Tensor& sub_par, const Tensor& sub_sib) {
+  const auto dev = packed.device();
+  chk(packed, dev, at::kLong, "packed");
+  chk(stats, dev, at::kLong, "stats");
+  chk(next_totals, dev, at::kLong, "next_totals");
+  chk(gain, dev, at::kDouble, "gain");
+  chk(leaf, dev, at::kByte, "leaf");
+  for (const Tensor* t : {&zbin, &n_nodes, &parent, &left, &right, &feat, &bin, &open, &n_open, &default_child, &cs_feat,
+                          &cs_default, &cs_other, &cs_bin, &cs_left_default, &counts, &next_open, &node_slot, &s2n,
+                          &sub_dst, &sub_par, &sub_sib})
+    chk(*t, dev, at::kInt, "level_plan int32 array");
+  const int64_t M = parent.numel();
+  FDX_CHECK(L >= 1 && packed.numel() >= 5 * L && open.numel() >= L, "packed [L, 5], open [L]");
+  FDX_CHECK(stats.numel() == 2 * M && left.numel() == M && right.numel() == M && feat.numel() == M &&
+                bin.numel() == M && leaf.numel() == M && gain.numel() == M && default_child.numel() == M &&
+                node_slot.numel() == M, "node tables must be [max_nodes]");
+  FDX_CHECK(next_open.numel() >= 2 * L && next_totals.numel() >= 4 * L && s2n.numel() >= L && sub_dst.numel() >= L &&
+                sub_par.numel() >= L && sub_sib.numel() >= L && cs_feat.numel() >= L && cs_default.numel() >= L &&
+                cs_other.numel() >= L && cs_bin.numel() >= L && cs_left_default.numel() >= L && counts.numel() >= 4,
+            "level_plan output capacities");
+  fdx::LevelPlanArgs a{};
+  a.packed = packed.data_ptr<int64_t>();
+  a.L = (int32_t)L;
+  a.depth = (int32_t)depth;
+  a.max_depth = (int32_t)max_depth;
+  a.min_gain = min_gain;
+  a.zbin = zbin.data_ptr<int32_t>();
+  if (hot_row) {
+    chk(*hot_row, dev, at::kInt, "hot_row");
+    FDX_CHECK(hot_row->numel() == zbin.numel(), "hot_row must be [Fa]");
+    a.hot_row = hot_row->data_ptr<int32_t>();
+  }
+  a.max_nodes = (int32_t)M;
+  a.n_nodes = n_nodes.data_ptr<int32_t>();
+  a.stats = stats.data_ptr<int64_t>();
+  a.parent = parent.data_ptr<int32_t>();
+  a.left = left.data_ptr<int32_t>();
+  a.right = right.data_ptr<int32_t>();
+  a.feat = feat.data_ptr<int32_t>();
+  a.bin = bin.data_ptr<int32_t>();
+  a.leaf = leaf.data_ptr<uint8_t>();
+  a.gain = gain.data_ptr<double>();
+  a.open = open.data_ptr<int32_t>();
+  a.n_open = n_open.data_ptr<int32_t>();
+  a.default_child = default_child.data_ptr<int32_t>();
+  if (node_dense) {
+    chk(*node_dense, dev, at::kInt, "node_dense");
+    FDX_CHECK(node_dense->numel() == 4 * M, "node_dense must be [max_nodes, 4]");
+    a.node_dense = node_dense->data_ptr<int32_t>();
+  }
+  a.cs_feat = cs_feat.data_ptr<int32_t>();
+  a.cs_default = cs_default.data_ptr<int32_t>();
+  a.cs_other = cs_other.data_ptr<int32_t>();
+  a.cs_bin = cs_bin.data_ptr<int32_t>();
+  a.cs_left_default = cs_left_default.data_ptr<int32_t>();
+  a.counts = counts.data_ptr<int32_t>();
+  a.next_open = next_open.data_ptr<int32_t>();
+  a.next_totals = next_totals.data_ptr<int64_t>();
+  a.node_slot = node_slot.data_ptr<int32_t>();
+  a.s2n = s2n.data_ptr<int32_t>();
+  a.sub_dst = sub_dst.data_ptr<int32_t>();
+  a.sub_par = sub_par.data_ptr<int32_t>();
+  a.sub_sib = sub_sib.data_ptr<int32_t>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_level_plan(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::level_plan_cpu(a);
+  }
+}
+
+// Partition of the device level loop: default pass over the rows, then the column pass of the
+// (device-counted, counts[0]) column splits, wps blocks per split.
+void partition_cols(const Tensor& row_node, const Tensor& default_child, const Tensor& cs_feat,
+                    const Tensor& cs_default, const Tensor& cs_other, const Tensor& cs_bin,
+                    const Tensor& cs_left_default, const Tensor& counts, const Tensor& colptr, const Tensor& csc_row,
+                    const Tensor& csc_bin, const optional<Tensor>& node_dense, const optional<Tensor>& dense,
+                    int64_t max_splits, int64_t wps) {
+  const auto dev = row_node.device();
+  chk(row_node, dev, at::kInt, "row_node");
+  chk(default_child, dev, at::kInt, "default_child");
+  for (const Tensor* t : {&cs_feat, &cs_default, &cs_other, &cs_bin, &cs_left_default, &counts})
+    chk(*t, dev, at::kInt, "column split arrays");
+  chk(colptr, dev, at::kLong, "colptr");
+  chk(csc_row, dev, at::kInt, "csc_row");
+  chk(csc_bin, dev, at::kByte, "csc_bin");
+  FDX_CHECK(cs_feat.numel() >= max_splits && wps >= 1, "cs arrays hold max_splits entries");
+  fdx::PartitionArgs a{};
+  a.row_node = row_node.data_ptr<int32_t>();
+  a.default_child = default_child.data_ptr<int32_t>();
+  a.num_nodes = (int32_t)default_child.numel();
+  a.N = row_node.numel();
+  a.split_default = cs_default.data_ptr<int32_t>();
+  a.split_other = cs_other.data_ptr<int32_t>();
+  a.split_bin = cs_bin.data_ptr<int32_t>();
+  a.split_left_is_default = cs_left_default.data_ptr<int32_t>();
+  a.csc_row = csc_row.data_ptr<int32_t>();
+  a.csc_bin = csc_bin.data_ptr<uint8_t>();
+  if (node_dense) {
+    FDX_CHECK(dense.has_value(), "node_dense needs the dense bin block");
+    chk(*node_dense, dev, at::kInt, "node_dense");
+    chk(*dense, dev, at::kByte, "dense");
+    FDX_CHECK(node_dense->numel() == 4ll * a.num_nodes, "node_dense must be [num_nodes, 4]");
+    FDX_CHECK(dense->dim() == 2 && dense->size(1) >= a.N, "dense must be [Fh, n_pad >= N]");
+    a.node_dense = node_dense->data_ptr<int32_t>();
+    a.dense = dense->data_ptr<uint8_t>();
+    a.n_pad = dense->size(1);
+  }
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_partition_cols(a, colptr.data_ptr<int64_t>(), cs_feat.data_ptr<int32_t>(), counts.data_ptr<int32_t>(),
+                               (int32_t)max_splits, (int32_t)wps, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::partition_cols_cpu(a, colptr.data_ptr<int64_t>(), cs_feat.data_ptr<int32_t>(), counts.data_ptr<int32_t>());
+  }
+}
+
 void logistic_grad(const Tensor& margin, const Tensor& label, const optional<Tensor>& weight, const Tensor& g,
                    const Tensor& h) {
   const auto dev = margin.device();
@@ -647,6 +783,8 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_quant_max", &quant_max);
   m.def("tree_quant", &quant);
   m.def("tree_slot8", &slot8);
+  m.def("tree_level_plan", &level_plan);
+  m.def("tree_partition_cols", &partition_cols);
   m.def("tree_split_best", &split_best);
   m.def("tree_hist_build", &hist_build);
   m.def("tree_rf_sample", &rf_sample);

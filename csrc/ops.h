@@ -76,6 +76,7 @@ struct HistArgs;
 struct DenseHistArgs;
 struct SplitArgs;
 struct PartitionArgs;
+struct LevelPlanArgs;
 struct RfSampleArgs;
 struct RfRowsArgs;
 struct RfSlotsArgs;
@@ -93,6 +94,9 @@ void hist_rf_cpu(const HistArgs& h, int bt);
 void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s);
 void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);
+void launch_level_plan(const LevelPlanArgs& a, hipStream_t s);
+void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
+                           int32_t max_splits, int32_t wps, hipStream_t s);
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
                        int64_t f0, int64_t* out, hipStream_t s);
 void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s);
@@ -109,6 +113,8 @@ void launch_leaf_update(double* margin, const int32_t* row_node, const double* n
 void quant_max_cpu(const QuantArgs& a, double* out);
 void quant_cpu(const QuantArgs& a, const double* maxv);
 void slot8_cpu(const SlotArgs& a);
+void level_plan_cpu(const LevelPlanArgs& a);
+void partition_cols_cpu(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs);
 void split_best_cpu(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa, int64_t f0,
                     int64_t* out);
 void hist_cpu(const HistArgs& h, int bt, int np);

@@ -65,6 +65,10 @@ void slot8_cpu(const SlotArgs& a) {
       const int32_t node = a.row_node[r];
       const int32_t s = ((node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1) - a.slot_base;
       a.slot8[r] = (s >= 0 && s < a.nslots) ? (uint8_t)s : (uint8_t)0xff;
+      if (a.masked) {
+        a.masked[2 * r] = s == 0 ? a.rowdig[2 * r] : 0u;
+        a.masked[2 * r + 1] = s == 0 ? a.rowdig[2 * r + 1] : 0u;
+      }
     }
   });
 }
@@ -219,7 +223,8 @@ void hist_subtract_cpu(const int64_t* parent, int64_t* cur, const int32_t* dst, 
                        int32_t n_pairs, int64_t TB) {
   const int64_t per = TB * 2;
   for (int p = 0; p < n_pairs; ++p)
-    for (int64_t k = 0; k < per; ++k)
+    if (dst[p] >= 0)
+      for (int64_t k = 0; k < per; ++k)
       cur[(int64_t)dst[p] * per + k] = parent[(int64_t)par[p] * per + k] - cur[(int64_t)sib[p] * per + k];
 }
 
@@ -231,8 +236,8 @@ void split_cpu(const SplitArgs& a) {
       double gain = -INFINITY;
       int64_t l0 = 0, l1 = 0;
       int bin = -1;
-      bool use = true;
-      if (a.feat_thr)
+      bool use = a.node_ids[n] >= 0;
+      if (use && a.feat_thr)
         use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <=
               a.feat_thr[n];
       if (use) {
@@ -268,6 +273,24 @@ void split_best_cpu(const double* gain, const int32_t* bin, const int64_t* left,
     o[2] = bin[t];
     o[3] = left[2 * t];
     o[4] = left[2 * t + 1];
+  }
+}
+
+void level_plan_cpu(const LevelPlanArgs& a) { level_plan(a); }
+
+void partition_cols_cpu(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs) {
+  PartitionArgs d = a;
+  d.num_items = 0;
+  partition_cpu(d);                                  // default pass
+  for (int32_t sp = 0; sp < *n_cs; ++sp) {
+    const int32_t dflt = a.split_default[sp], other = a.split_other[sp], thr = a.split_bin[sp];
+    const bool left_default = a.split_left_is_default[sp] != 0;
+    const int32_t f = cs_feat[sp];
+    for (int64_t e = colptr[f]; e < colptr[f + 1]; ++e) {
+      const int32_t row = a.csc_row[e];
+      const bool left = (int32_t)a.csc_bin[e] <= thr;
+      if (left != left_default && a.row_node[row] == dflt) a.row_node[row] = other;
+    }
   }
 }
 

@@ -176,6 +176,8 @@ __global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
     const int32_t node = a.row_node[r];
     const int32_t s = ((node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1) - a.slot_base;
     a.slot8[r] = (s >= 0 && s < a.nslots) ? (uint8_t)s : (uint8_t)0xff;
+    if (a.masked)
+      reinterpret_cast<uint2*>(a.masked)[r] = s == 0 ? reinterpret_cast<const uint2*>(a.rowdig)[r] : make_uint2(0u, 0u);
   }
 }
 
@@ -582,6 +584,7 @@ __global__ __launch_bounds__(256) void hist_subtract_kernel(const int64_t* paren
        t += (int64_t)gridDim.x * 256) {
     const int p = (int)(t / per);
     const int64_t k = t % per;
+    if (dst[p] < 0) continue;                 // padded triple (device level loop)
     cur_hist[(int64_t)dst[p] * per + k] = parent_hist[(int64_t)par[p] * per + k] - cur_hist[(int64_t)sib[p] * per + k];
   }
 }
@@ -594,8 +597,8 @@ __global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
   double gain = -1.0 / 0.0;
   int bin = -1;
   int64_t l0 = 0, l1 = 0;
-  bool use = true;
-  if (a.feat_thr)
+  bool use = a.node_ids[n] >= 0;              // -1: padded row of a device level loop
+  if (use && a.feat_thr)
     use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
   if (use) {
     const int64_t* hb = a.hist + ((int64_t)n * (a.boff[a.Fa]) + a.boff[f]) * 2;
@@ -869,6 +872,28 @@ __global__ __launch_bounds__(256) void partition_column_kernel(PartitionArgs a) 
   }
 }
 
+// Column pass of the device level loop: block b handles split b / wps, entries
+// part = b % wps of its column, grid-strided (the splits and their count live on the device).
+__global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, const int64_t* colptr, const int32_t* cs_feat,
+                                                             const int32_t* n_cs, int32_t wps) {
+  const int sp = blockIdx.x / wps, part = blockIdx.x % wps;
+  if (sp >= *n_cs) return;
+  const int32_t dflt = a.split_default[sp], other = a.split_other[sp];
+  const int32_t thr = a.split_bin[sp];
+  const bool left_default = a.split_left_is_default[sp] != 0;
+  const int32_t f = cs_feat[sp];
+  const int64_t e1 = colptr[f + 1];
+  for (int64_t e = colptr[f] + (int64_t)part * 256 + threadIdx.x; e < e1; e += (int64_t)wps * 256) {
+    const int32_t row = a.csc_row[e];
+    const bool left = (int32_t)a.csc_bin[e] <= thr;
+    if (left != left_default && a.row_node[row] == dflt) a.row_node[row] = other;
+  }
+}
+
+__global__ void level_plan_kernel(LevelPlanArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) level_plan(a);
+}
+
 // ------------------------------------------------------------------ gbdt helpers
 __global__ __launch_bounds__(256) void logistic_grad_kernel(const double* margin, const float* label,
                                                             const float* weight, float* g, float* h, int64_t N) {
@@ -982,6 +1007,17 @@ void launch_split_best(const double* gain, const int32_t* bin, const int64_t* le
 void launch_partition(const PartitionArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(partition_default_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
   if (a.num_items > 0) hipLaunchKernelGGL(partition_column_kernel, dim3(a.num_items), dim3(256), 0, s, a);
+}
+
+void launch_level_plan(const LevelPlanArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(64), 0, s, a);
+}
+
+void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
+                           int32_t max_splits, int32_t wps, hipStream_t s) {
+  if (a.N > 0) hipLaunchKernelGGL(partition_default_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
+  if (max_splits > 0)
+    hipLaunchKernelGGL(partition_cols_kernel, dim3(max_splits * wps), dim3(256), 0, s, a, colptr, cs_feat, n_cs, wps);
 }
 
 void launch_logistic_grad(const double* margin, const float* label, const float* weight, float* g, float* h,

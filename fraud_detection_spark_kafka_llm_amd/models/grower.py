@@ -55,9 +55,16 @@ DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
 # histogram launches of one pass (CSC groups, dense groups) run concurrently on this many HIP
 # streams: they add into disjoint feature ranges with integer atomics, so the order is free and
 # the kernels fill each other's tails
-HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 3))
+HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
+
+
+# GBDT trees grow with the device-resident level loop (grow_tree_device): split application and
+# next-level planning run on the GPU, the host reads 16 bytes per level and the node table once
+# per tree (FDX_DEVICE_LEVELS=0: host loop)
+DEVICE_LEVELS = os.environ.get("FDX_DEVICE_LEVELS", "1") != "0"
+PARTITION_WPS = 16              # blocks per column split in the device partition pass
 
 
 @dataclass
@@ -98,7 +105,9 @@ class Workspace:
 
     def run_concurrent(self, launches: list) -> None:
         """Run the launches on HIST_STREAMS side streams joined back into the current stream
-        (serially on the current stream on the host or with one stream)."""
+        (serially on the current stream on the host or with one stream). The first launch (the
+        long cold-feature CSC pass) gets a stream of its own; the others share the rest, so none
+        queues behind it (a short launch behind it added 0.15-0.25 ms to every level)."""
         if self.dev.type != "cuda" or HIST_STREAMS <= 1 or len(launches) <= 1:
             for fn in launches:
                 fn()
@@ -107,12 +116,13 @@ class Workspace:
             self._streams = [torch.cuda.Stream(self.dev) for _ in range(HIST_STREAMS)]
         main = torch.cuda.current_stream(self.dev)
         start = main.record_event()
+        ns = len(self._streams)
         for i, fn in enumerate(launches):
-            s = self._streams[i % len(self._streams)]
+            s = self._streams[0 if i == 0 else 1 + (i - 1) % (ns - 1)]
             s.wait_event(start)
             with torch.cuda.stream(s):
                 fn()
-        for s in self._streams[:len(launches)]:
+        for s in self._streams[:min(len(launches), ns)]:
             main.wait_stream(s)
 
     def dense_groups(self, bt: int, fg: int, keep: Optional[np.ndarray] = None):
@@ -292,6 +302,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     (SURVEY PAR-02). ``coll.force`` runs the same collective path at world size 1 (RCCL check)."""
     C = native.lib()
     use_coll = coll is not None and coll.active
+    if not use_coll and device_levels_ok(params, weight):
+        return grow_tree_device(Q, ws, params, tree_index, g, h, weight)
     shards = ws.shards(coll) if use_coll and (coll.world > 1 or getattr(coll, "force", False)) else None
     dev = Q.device
     mode_rs = 0 if params.mode == 0 else 1
@@ -406,7 +418,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             for s0, cnt, h_s2n in passes:
                 slot8 = None
                 if d > 0:
-                    C.tree_slot8(ws.row_node, node_slot, s0, cnt, ws.slot8)
+                    C.tree_slot8(ws.row_node, node_slot, s0, cnt, ws.slot8, None, None)
                     slot8 = ws.slot8
                 ct = pass_ct(np_, cnt)
                 s2n = up[h_s2n]
@@ -472,6 +484,23 @@ class TreeTable:
     def __init__(self, root_stats: np.ndarray):
         self.parent, self.depth, self.feature, self.binv, self.thr = [-1], [0], [-1], [-1], [0.0]
         self.left, self.right, self.gain, self.stats, self.is_leaf = [-1], [-1], [-1.0], [root_stats], [False]
+
+    @classmethod
+    def from_arrays(cls, Q: Quantized, parent, feat, binv, left, right, gain, stats, leaf) -> "TreeTable":
+        """The node table the device level loop built (tree.h level_plan), same numbering."""
+        t = cls(stats[0])
+        n = len(parent)
+        t.parent = [int(v) for v in parent]
+        t.depth = [0] * n
+        t.feature = [int(v) for v in feat]
+        t.binv = [int(v) for v in binv]
+        t.thr = [Q.threshold(int(f), int(b)) if f >= 0 else 0.0 for f, b in zip(feat, binv)]
+        t.left = [int(v) for v in left]
+        t.right = [int(v) for v in right]
+        t.gain = [float(v) for v in gain]
+        t.stats = [np.asarray(st, dtype=np.int64) for st in stats]
+        t.is_leaf = [bool(v) for v in leaf]
+        return t
 
     def apply_splits(self, open_nodes: list, packed: np.ndarray, d: int, Q: Quantized, params: GrowParams,
                      scale: np.ndarray, max_nodes: int) -> tuple:
@@ -546,6 +575,161 @@ class TreeTable:
             stats_out = st
             raw_count = np.rint(st.sum(1)).astype(np.int64)
         return Tree(feat_orig, thr_a, left_a, right_a, stats_out, imp, gain_a, raw_count, pred, 0)
+
+
+def device_levels_ok(params: GrowParams, weight, device_levels: Optional[bool] = None) -> bool:
+    """The device level loop covers single-process GBDT (Newton gain, all features) trees whose
+    deepest level builds <= one pass of node slots (max_depth <= 6)."""
+    on = DEVICE_LEVELS if device_levels is None else device_levels
+    return (on and params.mode == 0 and not params.feat_k and _choose_np(params, weight) == 4
+            and 2 ** max(params.max_depth - 2, 0) <= slots_per_tile(4) * MAX_CT)
+
+
+class LevelState:
+    """Device buffers of the level loop (node table, ping-pong open lists, partition and plan
+    tables), allocated once per workspace and depth."""
+
+    def __init__(self, Q: Quantized, max_depth: int):
+        dev = Q.device
+        M = 2 ** (max_depth + 1)
+        cap = 2 ** max_depth
+        i32 = lambda n: torch.full((n,), -1, dtype=torch.int32, device=dev)   # noqa: E731
+        self.M, self.cap, self.max_depth = M, cap, max_depth
+        self.n_nodes = torch.ones(1, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros((M, 2), dtype=torch.int64, device=dev)
+        self.parent, self.left, self.right, self.feat, self.bin = i32(M), i32(M), i32(M), i32(M), i32(M)
+        self.leaf = torch.zeros(M, dtype=torch.uint8, device=dev)
+        self.gain = torch.full((M,), -1.0, dtype=torch.float64, device=dev)
+        self.open = [i32(cap), i32(cap)]
+        self.totals = [torch.zeros((cap, 2), dtype=torch.int64, device=dev) for _ in range(2)]
+        self.counts = torch.zeros((max_depth + 1, 4), dtype=torch.int32, device=dev)
+        self.counts_host = torch.zeros((max_depth + 1, 4), dtype=torch.int32)
+        if dev.type == "cuda":
+            self.counts_host = self.counts_host.pin_memory()
+        self.one = torch.ones(1, dtype=torch.int32, device=dev)
+        self.default_child, self.node_slot = i32(M), i32(M)
+        self.cs = [i32(cap) for _ in range(5)]          # feat, default, other, bin, left_default
+        self.s2n, self.sub_dst, self.sub_par, self.sub_sib = i32(cap), i32(cap), i32(cap), i32(cap)
+        self.node_dense = self.hot_row = None
+        if Q.dense is not None and PARTITION_DENSE:
+            hot_row = np.full(Q.Fa, -1, dtype=np.int32)
+            hot_row[Q.hot] = np.arange(len(Q.hot), dtype=np.int32)
+            self.hot_row = torch.from_numpy(hot_row).to(dev)
+            self.node_dense = i32(4 * M)
+
+
+def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
+                     h: torch.Tensor, weight: Optional[torch.Tensor] = None) -> Tree:
+    """GBDT tree with the level loop on the device (same trees as grow_tree's host loop, bit for
+    bit). Per level: histogram passes -> sibling subtraction -> split search -> best split per
+    node -> ``tree_level_plan`` (one thread: apply the splits to the device node table, this
+    level's partition tables, the next level's open list / builds / subtraction triples) ->
+    partition. The host waits only for the plan's 16-byte counts (copied while the partition
+    runs) to size the next level's launches, and reads the node table once at the end."""
+    C = native.lib()
+    dev = Q.device
+    np_ = 4
+    st = getattr(ws, "_levels", None)
+    if st is None or st.max_depth != params.max_depth:
+        st = ws._levels = LevelState(Q, params.max_depth)
+    ws.row_node.zero_()
+    with tracing.span("tree.quant"):
+        C.tree_quant_max(g, h, None, weight, int(params.seed), int(tree_index), False, 0, Q.n_rows, ws.maxabs, Q.row0)
+        C.tree_quant(g, h, None, weight, int(params.seed), int(tree_index), False, 0, 4, ws.maxabs, ws.rowdig,
+                     ws.kexp, ws.totals, ws.digp, Q.row0)
+    # root: node 0, open list [0] with the exact totals (no host round trip)
+    st.n_nodes.fill_(1)
+    st.stats[0].copy_(ws.totals)
+    for t_ in (st.parent, st.left, st.right, st.feat, st.bin):
+        t_[:1].fill_(-1)
+    st.leaf[:1].zero_()
+    st.gain[:1].fill_(-1.0)
+    st.open[0][:1].zero_()
+    st.totals[0][:1].copy_(ws.totals[None])
+    TB = Q.TB
+    n_open, n_build = 1, 1
+    prev_hist = None
+    ev = None
+    for d in range(params.max_depth):
+        cur = d % 2
+        if d > 0:
+            ev.synchronize()
+            cnt = st.counts_host[d - 1].tolist()
+            n_open, n_build = int(cnt[1]), int(cnt[2])
+            if n_open == 0:
+                break
+        open_d, totals_d = st.open[cur][:n_open], st.totals[cur][:n_open]
+        n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
+        cur_hist = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
+        with tracing.span("tree.hist"):
+            use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH
+            sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
+            slot8 = None
+            csc_slot8, csc_dig = None, ws.rowdig
+            if d > 0:
+                # a single built node: the CSC passes run the root kernel on digit words zeroed
+                # outside it (no per-entry slot gather, no compaction; zero rows add nothing)
+                single = n_build == 1
+                if single and getattr(ws, "rowdig_masked", None) is None:
+                    ws.rowdig_masked = torch.empty_like(ws.rowdig)
+                C.tree_slot8(ws.row_node, st.node_slot, 0, n_build, ws.slot8, ws.rowdig if single else None,
+                             ws.rowdig_masked if single else None)
+                slot8 = ws.slot8
+                csc_slot8, csc_dig = (None, ws.rowdig_masked) if single else (slot8, ws.rowdig)
+                s2n = st.s2n[:n_build]
+            else:
+                s2n = st.one.new_zeros(1)
+            ct = pass_ct(np_, n_build)
+            launches = []
+            for grp in sel_groups:
+                if grp.num_items == 0:
+                    continue
+                launches.append(functools.partial(
+                    C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
+                    Q.h_row, Q.h_key, csc_slot8, csc_dig, Q.boff, Q.nbins, s2n, cur_hist, TB, grp.bt, ct, np_, None))
+            if use_dense:
+                for bt in (1, 2, 4):
+                    fg = C.tree_dense_fg(bt, ct if d > 0 else 1)
+                    gfid, gden = ws.dense_groups(bt, fg)
+                    if gfid.numel():
+                        rr = dense_range_rows(Q.n_rows, gfid.numel() // fg)
+                        launches.append(functools.partial(
+                            C.tree_hist_dense, Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad,
+                            gfid, gden, Q.boff, Q.nbins, s2n, cur_hist, TB, Q.n_rows, rr, bt, ct, np_))
+            ws.run_concurrent(launches)
+        if d > 0:
+            C.tree_hist_subtract(prev_hist, cur_hist, st.sub_dst[:n_build], st.sub_par[:n_build],
+                                 st.sub_sib[:n_build], TB)
+        with tracing.span("tree.split"):
+            packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
+                                  params, None, tree_index, Q.Fa, 0)
+        nxt = 1 - cur
+        C.tree_level_plan(packed, n_open, d, params.max_depth, float(params.min_gain), Q.zbin, st.hot_row,
+                          st.n_nodes, st.stats, st.parent, st.left, st.right, st.feat, st.bin, st.leaf, st.gain,
+                          open_d, n_open_ptr, st.default_child, st.node_dense, *st.cs, st.counts[d],
+                          st.open[nxt], st.totals[nxt], st.node_slot, st.s2n, st.sub_dst, st.sub_par, st.sub_sib)
+        if dev.type == "cuda":
+            st.counts_host[d].copy_(st.counts[d], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            st.counts_host[d].copy_(st.counts[d])
+            ev = _Done()
+        with tracing.span("tree.partition"):
+            C.tree_partition_cols(ws.row_node, st.default_child, *st.cs, st.counts[d], Q.colptr, Q.csc_row, Q.csc_bin,
+                                  st.node_dense, Q.dense if st.node_dense is not None else None, n_open, PARTITION_WPS)
+        prev_hist = cur_hist
+    # one read of the node table per tree
+    nn = int(st.n_nodes.item())
+    arr = [t_[:nn].cpu().numpy() for t_ in (st.parent, st.feat, st.bin, st.left, st.right, st.gain, st.stats, st.leaf)]
+    kexp = ws.kexp.cpu().numpy().astype(np.int64)
+    tab = TreeTable.from_arrays(Q, *arr)
+    return tab.build(Q, params, np.ldexp(1.0, -kexp))
+
+
+class _Done:
+    def synchronize(self):
+        pass
 
 
 def _weight(st, mode) -> int:

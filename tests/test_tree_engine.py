@@ -172,7 +172,7 @@ def _hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, np_=4, g=None, 
         cnt = min(P, nslots - s0)
         slot8 = None
         if not root:
-            C.tree_slot8(row_node, node_slot, s0, cnt, ws.slot8)
+            C.tree_slot8(row_node, node_slot, s0, cnt, ws.slot8, None, None)
             slot8 = ws.slot8
         s2n = torch.arange(s0, s0 + cnt, dtype=torch.int32).to(dev)
         ct = pass_ct(np_, cnt)
@@ -495,3 +495,35 @@ def test_warm_tree_kernels_runs_the_production_path_on_the_host():
     from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels
 
     warm_tree_kernels("cpu", rows=1500, gbdt_depth=3, forest_depth=3)
+
+
+def _same_trees(ta_list, tb_list):
+    assert len(ta_list) == len(tb_list)
+    for ta, tb in zip(ta_list, tb_list):
+        np.testing.assert_array_equal(ta.feature, tb.feature)
+        np.testing.assert_array_equal(ta.threshold, tb.threshold)
+        np.testing.assert_array_equal(ta.left, tb.left)
+        np.testing.assert_array_equal(ta.right, tb.right)
+        np.testing.assert_array_equal(ta.stats, tb.stats)
+        np.testing.assert_array_equal(ta.gain, tb.gain)
+
+
+@pytest.mark.parametrize("depth,hot", [(6, 0.2), (4, 0.0), (1, 0.2)])
+def test_device_level_loop_grows_the_host_loop_trees(monkeypatch, depth, hot):
+    """The device-resident level loop (tree.h level_plan + split-driven partition, run through its
+    host twins here) grows the host loop's GBDT trees bit for bit: node numbering, smaller-sibling
+    builds, subtraction, dense-block (hot feature) and column partitions, leaves at max depth."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower, quantize as qmod
+
+    monkeypatch.setattr(qmod, "HOT_DENSITY", hot)
+    dense, y = random_counts_matrix(3000, 80, 0.15, 21)
+    dense[:, :6] = np.random.default_rng(1).integers(0, 5, (3000, 6))     # dense columns -> hot block
+    vc = vc_from_dense(dense)
+    params = GBDTParams(n_estimators=4, max_depth=depth, gamma=0.0)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(grower, "DEVICE_LEVELS", flag)
+        out[flag] = fit_gbdt(vc, torch.from_numpy(y), params, device="cpu")
+    _same_trees(out[False].trees, out[True].trees)
+    assert max(t.num_nodes for t in out[True].trees) == (3 if depth == 1 else max(t.num_nodes for t in out[True].trees))
+    assert depth == 1 or max(t.num_nodes for t in out[True].trees) > 7
