@@ -302,9 +302,9 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     (SURVEY PAR-02). ``coll.force`` runs the same collective path at world size 1 (RCCL check)."""
     C = native.lib()
     use_coll = coll is not None and coll.active
-    if not use_coll and device_levels_ok(params, weight):
-        return grow_tree_device(Q, ws, params, tree_index, g, h, weight)
     shards = ws.shards(coll) if use_coll and (coll.world > 1 or getattr(coll, "force", False)) else None
+    if device_levels_ok(params, weight):
+        return grow_tree_device(Q, ws, params, tree_index, g, h, weight, coll if use_coll else None, shards)
     dev = Q.device
     mode_rs = 0 if params.mode == 0 else 1
     np_ = _choose_np(params, weight)
@@ -619,13 +619,17 @@ class LevelState:
 
 
 def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
-                     h: torch.Tensor, weight: Optional[torch.Tensor] = None) -> Tree:
+                     h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
+                     shards: Optional["FeatureShards"] = None) -> Tree:
     """GBDT tree with the level loop on the device (same trees as grow_tree's host loop, bit for
     bit). Per level: histogram passes -> sibling subtraction -> split search -> best split per
     node -> ``tree_level_plan`` (one thread: apply the splits to the device node table, this
     level's partition tables, the next level's open list / builds / subtraction triples) ->
     partition. The host waits only for the plan's 16-byte counts (copied while the partition
-    runs) to size the next level's launches, and reads the node table once at the end."""
+    runs) to size the next level's launches, and reads the node table once at the end.
+    Data parallel (``shards``): the built nodes' partial histograms are reduce-scattered by
+    feature shard and the per-shard best splits all-gathered, all stream-ordered on the device;
+    every rank plans the identical next level from the identical gathered splits."""
     C = native.lib()
     dev = Q.device
     np_ = 4
@@ -635,17 +639,19 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
     ws.row_node.zero_()
     with tracing.span("tree.quant"):
         C.tree_quant_max(g, h, None, weight, int(params.seed), int(tree_index), False, 0, Q.n_rows, ws.maxabs, Q.row0)
-        C.tree_quant(g, h, None, weight, int(params.seed), int(tree_index), False, 0, 4, ws.maxabs, ws.rowdig,
+        mx = coll.max(ws.maxabs) if coll is not None else ws.maxabs
+        C.tree_quant(g, h, None, weight, int(params.seed), int(tree_index), False, 0, 4, mx, ws.rowdig,
                      ws.kexp, ws.totals, ws.digp, Q.row0)
+    tot = coll.sum(ws.totals) if coll is not None else ws.totals
     # root: node 0, open list [0] with the exact totals (no host round trip)
     st.n_nodes.fill_(1)
-    st.stats[0].copy_(ws.totals)
+    st.stats[0].copy_(tot)
     for t_ in (st.parent, st.left, st.right, st.feat, st.bin):
         t_[:1].fill_(-1)
     st.leaf[:1].zero_()
     st.gain[:1].fill_(-1.0)
     st.open[0][:1].zero_()
-    st.totals[0][:1].copy_(ws.totals[None])
+    st.totals[0][:1].copy_(tot[None])
     TB = Q.TB
     n_open, n_build = 1, 1
     prev_hist = None
@@ -660,7 +666,10 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 break
         open_d, totals_d = st.open[cur][:n_open], st.totals[cur][:n_open]
         n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
-        cur_hist = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
+        if shards is None:
+            cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
+        else:   # local partials of the built nodes (+1 zero pad bin for the shard packing)
+            hist_target = torch.zeros((n_build, TB + 1, 2), dtype=torch.int64, device=dev)
         with tracing.span("tree.hist"):
             use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH
             sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
@@ -679,6 +688,9 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 s2n = st.s2n[:n_build]
             else:
                 s2n = st.one.new_zeros(1)
+            bidx = s2n
+            if shards is not None:      # slot k -> partial row k
+                s2n = torch.arange(n_build, dtype=torch.int32, device=dev)
             ct = pass_ct(np_, n_build)
             launches = []
             for grp in sel_groups:
@@ -686,7 +698,8 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                     continue
                 launches.append(functools.partial(
                     C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
-                    Q.h_row, Q.h_key, csc_slot8, csc_dig, Q.boff, Q.nbins, s2n, cur_hist, TB, grp.bt, ct, np_, None))
+                    Q.h_row, Q.h_key, csc_slot8, csc_dig, Q.boff, Q.nbins, s2n, hist_target, TB, grp.bt, ct, np_,
+                    None))
             if use_dense:
                 for bt in (1, 2, 4):
                     fg = C.tree_dense_fg(bt, ct if d > 0 else 1)
@@ -695,14 +708,28 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                         rr = dense_range_rows(Q.n_rows, gfid.numel() // fg)
                         launches.append(functools.partial(
                             C.tree_hist_dense, Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad,
-                            gfid, gden, Q.boff, Q.nbins, s2n, cur_hist, TB, Q.n_rows, rr, bt, ct, np_))
+                            gfid, gden, Q.boff, Q.nbins, s2n, hist_target, TB, Q.n_rows, rr, bt, ct, np_))
             ws.run_concurrent(launches)
+        if shards is not None:
+            with tracing.span("tree.reduce_scatter"):
+                packed_in = hist_target.index_select(1, shards.pack_idx).view(n_build, shards.S, shards.Bs, 2)
+                mine = coll.reduce_scatter(packed_in.permute(1, 0, 2, 3))
+                cur_hist = torch.zeros((n_open, shards.bins, 2), dtype=torch.int64, device=dev)
+                cur_hist.index_copy_(0, bidx.to(torch.int64), mine[:, : shards.bins].contiguous())
         if d > 0:
             C.tree_hist_subtract(prev_hist, cur_hist, st.sub_dst[:n_build], st.sub_par[:n_build],
-                                 st.sub_sib[:n_build], TB)
+                                 st.sub_sib[:n_build], TB if shards is None else shards.bins)
         with tracing.span("tree.split"):
-            packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
-                                  params, None, tree_index, Q.Fa, 0)
+            if shards is None:
+                packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
+                                      params, None, tree_index, Q.Fa, 0)
+            else:
+                mine = _best_splits(C, cur_hist, totals_d, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
+                                    open_d, ws.kexp, params, None, tree_index, shards.Fa, shards.f0)
+                allt = coll.all_gather(mine)                                  # [S, n_open, 5]
+                gains = allt[:, :, 0].contiguous().view(torch.float64)
+                best_s = torch.argmax(gains, dim=0)                           # ties -> lowest shard = lowest feature
+                packed = allt[best_s, torch.arange(n_open, device=dev)].contiguous()
         nxt = 1 - cur
         C.tree_level_plan(packed, n_open, d, params.max_depth, float(params.min_gain), Q.zbin, st.hot_row,
                           st.n_nodes, st.stats, st.parent, st.left, st.right, st.feat, st.bin, st.leaf, st.gain,

@@ -79,6 +79,15 @@ class ItemGroup:
         return self._order
 
 
+def _h2d(x: np.ndarray, dev) -> torch.Tensor:
+    """Host array -> device through a pinned staging copy (one async DMA instead of ROCm's
+    synchronous pageable path)."""
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    if torch.device(dev).type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.Tensor:
     """XCD-aware item placement. Workgroups are dealt round-robin over the 8 XCDs (observed
     dispatch, speed only), so workgroups b and b + 8 share an L2: the 4 wave slots of workgroup
@@ -255,6 +264,8 @@ def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_
     if fo is None or fo.colptr.numel() != F + 1 or fo.csc_row.device != dev:
         with tracing.span("q.order"):
             fo = feature_order(indptr, idx, counts, F)
+    sp_h = tracing.span("q.head")
+    sp_h.__enter__()
     scale = scale.to(device=dev, dtype=torch.float64)
     maxb = torch.clamp(fo.maxc.to(torch.int64), max=max_bins - 1)
     maxb = torch.where(scale > 0, maxb, torch.zeros_like(maxb))
@@ -272,6 +283,7 @@ def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_
     thresholds = ((k.to(torch.float64) + 0.5) * scale[fid_orig][f_of_bin]).cpu().numpy()
     lens = fo.colptr[1:] - fo.colptr[:-1]
     nnz_all = int(fo.colptr[-1])
+    sp_h.__exit__(None, None, None)
     with tracing.span("q.csc"):
         if int(lens[~active].sum()) == 0:        # every non-empty feature is active: the order is the CSC
             csc_row = fo.csc_row
@@ -465,6 +477,8 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     # hot features stay in the histogram CSC too (deep levels use it: only their live entries are
     # multiplied there, while the dense kernel masks every row); they are never packed
     cols = np.nonzero(n > 0)[0]
+    sp_b = tracing.span("q.bounds")
+    sp_b.__enter__()
     nsb = max(1, (Q.n_rows + super_rows - 1) // super_rows)
     sb_rows = (Q.n_rows + nsb - 1) // nsb if Q.n_rows else 1
     # --- per (super-block, feature) segments of the feature-major CSC and their new offsets
@@ -492,6 +506,9 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
         hptr = np.zeros((nsb, 1), dtype=np.int64)
         seg_n = np.zeros((nsb, 0), dtype=np.int64)
     total = int(hptr[-1, -1]) if S else 0
+    sp_b.__exit__(None, None, None)
+    sp_p = tracing.span("q.pack")
+    sp_p.__enter__()
     # --- packing (global: the same kbase in every super-block)
     ncol = n[cols]
     packable = (ncol <= chunk * nsb) & (nb[cols] <= 16) & ~hot[cols]
@@ -501,12 +518,13 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     # tens of ms): each run <= PACK_KEYS keys at the run's largest stride, <= chunk * nsb entries
     gp = native.lib().pack_runs(torch.from_numpy(packable.astype(np.uint8)), torch.from_numpy(stride.astype(np.int64)),
                                 torch.from_numpy(ncol.astype(np.int64)), int(PACK_KEYS), int(chunk * nsb)).numpy()
-    groups_pk = [(int(a), int(b), int(c)) for a, b, c in gp]
-    for i0, i1, sl2 in groups_pk:
-        kbase[cols[i0:i1]] = np.arange(i1 - i0) << sl2
+    gp = np.asarray(gp, dtype=np.int64).reshape(-1, 3)
+    if gp.shape[0]:       # kbase of feature j of a run = j << stride_log2 (vectorised over the runs)
+        run_len = gp[:, 1] - gp[:, 0]
+        pos = np.arange(int(run_len.sum())) - np.repeat(np.cumsum(run_len) - run_len, run_len)
+        kbase[cols[np.repeat(gp[:, 0], run_len) + pos]] = pos << np.repeat(gp[:, 2], run_len)
     parts = []   # arrays of (start, end, f0, sl2, nfeat, koff, bt, blk)
-    if groups_pk:
-        gp = np.asarray(groups_pk, dtype=np.int64)
+    if gp.shape[0]:
         i0s, i1s, sl2s = gp[:, 0], gp[:, 1], gp[:, 2]
         keys = (i1s - i0s) << sl2s
         bts = np.where(keys <= 16, 1, np.where(keys <= 32, 2, 4))
@@ -537,28 +555,39 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
             parts.append(np.stack([st[sel], en[sel], f_[sel], np.full(m, 8), np.ones(m, np.int64),
                                    np.full(m, 64 * w), btw, b_[sel]], 1))
     items = np.concatenate(parts) if parts else np.zeros((0, 8), np.int64)
+    sp_p.__exit__(None, None, None)
     # --- the histogram CSC: (row, kbase + bin) of every (super-block, feature) segment
     if S:
-        kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev) if kbase.any() else None
-        C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total], kb)
+        with tracing.span("q.copy"):
+            kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev) if kbase.any() else None
+            C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total], kb)
+    sp_g = tracing.span("q.groups")
+    sp_g.__enter__()
     arr = items.astype(np.int64)
     is_hot = hot[arr[:, 2]] & (arr[:, 4] == 1) if arr.shape[0] else np.zeros(0, bool)
-    t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).astype(dt)).to(dev)   # noqa: E731
-
-    def make(sel):
-        out = []
+    # the item table and every group's row order (by entry offset; the parts are sorted runs, so
+    # the stable host sort is linear) go up in two pinned copies: ~20 synchronous pageable copies
+    # of small arrays cost ~100 ms at 10M rows
+    sels = []
+    for sel in (~is_hot, is_hot):
         for bt in (1, 2, 4):
-            g = arr[sel & (arr[:, 6] == bt)]
-            if not g.shape[0]:
-                continue
-            g = g[np.lexsort((g[:, 0],))]
+            ix = np.nonzero(sel & (arr[:, 6] == bt))[0]
+            sels.append((sel is is_hot, bt, ix[np.argsort(arr[ix, 0], kind="stable")]))
+    arr_d = _h2d(arr, dev)
+    all_ix = _h2d(np.concatenate([ix for _, _, ix in sels]) if sels else np.zeros(0, np.int64), dev)
+    groups = {False: [], True: []}
+    o = 0
+    for hot_sel, bt, ix in sels:
+        if ix.size:
+            g = arr_d[all_ix[o:o + ix.size]]
             meta = g[:, 3] | (g[:, 4] << 8) | (g[:, 5] << 16)
-            out.append(ItemGroup(bt, t(g[:, 0], np.int64), t(g[:, 1], np.int64), t(g[:, 2], np.int32),
-                                 t(meta, np.int32), t(g[:, 7], np.int32)))
-        return out
+            groups[hot_sel].append(ItemGroup(bt, g[:, 0].contiguous(), g[:, 1].contiguous(), g[:, 2].to(torch.int32),
+                                             meta.to(torch.int32), g[:, 7].to(torch.int32)))
+        o += ix.size
 
-    Q.groups = make(~is_hot)
-    Q.hot_groups = make(is_hot)
+    Q.groups = groups[False]
+    Q.hot_groups = groups[True]
+    sp_g.__exit__(None, None, None)
     Q.h_row, Q.h_key = h_row[:total], h_key[:total]
     Q.n_super = nsb
     Q.kbase_host = kbase.astype(np.int32)
