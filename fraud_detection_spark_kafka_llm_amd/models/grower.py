@@ -610,6 +610,12 @@ class LevelState:
         self.default_child, self.node_slot = i32(M), i32(M)
         self.cs = [i32(cap) for _ in range(5)]          # feat, default, other, bin, left_default
         self.s2n, self.sub_dst, self.sub_par, self.sub_sib = i32(cap), i32(cap), i32(cap), i32(cap)
+        # pinned host mirror of the node table: one batch of async copies + one wait per tree
+        self.table = (self.n_nodes, self.parent, self.feat, self.bin, self.left, self.right, self.gain, self.stats,
+                      self.leaf)
+        self.table_host = [torch.empty(t_.shape, dtype=t_.dtype) for t_ in self.table]
+        if dev.type == "cuda":
+            self.table_host = [t_.pin_memory() for t_ in self.table_host]
         self.node_dense = self.hot_row = None
         if Q.dense is not None and PARTITION_DENSE:
             hot_row = np.full(Q.Fa, -1, dtype=np.int32)
@@ -746,9 +752,13 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             C.tree_partition_cols(ws.row_node, st.default_child, *st.cs, st.counts[d], Q.colptr, Q.csc_row, Q.csc_bin,
                                   st.node_dense, Q.dense if st.node_dense is not None else None, n_open, PARTITION_WPS)
         prev_hist = cur_hist
-    # one read of the node table per tree
-    nn = int(st.n_nodes.item())
-    arr = [t_[:nn].cpu().numpy() for t_ in (st.parent, st.feat, st.bin, st.left, st.right, st.gain, st.stats, st.leaf)]
+    # one read of the node table per tree (async copies into the pinned mirror, one wait)
+    for hst, t_ in zip(st.table_host, st.table):
+        hst.copy_(t_, non_blocking=True)
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
+    nn = int(st.table_host[0][0])
+    arr = [t_[:nn].numpy() for t_ in st.table_host[1:]]
     kexp = ws.kexp.cpu().numpy().astype(np.int64)
     tab = TreeTable.from_arrays(Q, *arr)
     return tab.build(Q, params, np.ldexp(1.0, -kexp))
