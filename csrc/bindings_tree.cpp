@@ -613,7 +613,8 @@ void partition(const Tensor& row_node, const Tensor& default_child, const Tensor
 }
 
 // Device level loop (tree.h level_plan): applies the level's best splits and plans the next level.
-void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_depth, double min_gain, const Tensor& zbin,
+void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_depth, int64_t mode, bool build_all,
+                const Tensor& kexp, double min_gain, const Tensor& zbin,
                 const optional<Tensor>& hot_row, const Tensor& n_nodes, const Tensor& stats, const Tensor& parent,
                 const Tensor& left, const Tensor& right, const Tensor& feat, const Tensor& bin, const Tensor& leaf,
                 const Tensor& gain, const Tensor& open, const Tensor& n_open, const Tensor& default_child,
@@ -645,6 +646,11 @@ void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_dept
   a.L = (int32_t)L;
   a.depth = (int32_t)depth;
   a.max_depth = (int32_t)max_depth;
+  a.mode = (int32_t)mode;
+  a.build_all = build_all ? 1 : 0;
+  chk(kexp, dev, at::kInt, "kexp");
+  FDX_CHECK(kexp.numel() == 2, "kexp [2]");
+  a.kexp = kexp.data_ptr<int32_t>();
   a.min_gain = min_gain;
   a.zbin = zbin.data_ptr<int32_t>();
   if (hot_row) {

@@ -242,159 +242,6 @@ struct PartitionArgs {
   int64_t n_pad;
 };
 
-// Device-resident level loop of a GBDT tree (models/grower.py grow_tree_device): after the split
-// search of level d, ONE thread applies the best splits of the level's open nodes to the node
-// table, writes this level's partition tables and plans level d + 1 (open list, smaller-sibling
-// builds, subtraction triples), exactly as the host loop (grower.TreeTable.apply_splits and the
-// build selection of grow_tree) does -- same node numbering, same tie rules -- so the host only
-// reads two counts per level and the node table once per tree. Newton gain (mode 0) only.
-struct LevelPlanArgs {
-  const int64_t* packed;          // [L][5] best split per open node {gain bits, feature, bin, left0, left1}
-  int32_t L;                      // open-list capacity of this level
-  int32_t depth, max_depth;
-  double min_gain;                // gamma: a split needs gain > max(gamma, 1e-6)
-  const int32_t* zbin;            // [Fa] zero bin of each feature (missing entries)
-  const int32_t* hot_row;         // [Fa] row of the feature in the dense block (-1), nullptr: none
-  int32_t max_nodes;
-  // node table (in/out)
-  int32_t* n_nodes;               // [1]
-  int64_t* stats;                 // [max_nodes][2] exact integer sums
-  int32_t* parent;
-  int32_t* left;
-  int32_t* right;
-  int32_t* feat;                  // Fa index of the split feature (-1 leaf / not split)
-  int32_t* bin;
-  uint8_t* leaf;
-  double* gain;
-  // this level (in): open nodes, local index i = row i of the level's histogram
-  const int32_t* open;            // [L] (-1 pad)
-  const int32_t* n_open;          // [1]
-  // this level's partition (out)
-  int32_t* default_child;         // [max_nodes]
-  int32_t* node_dense;            // [max_nodes][4] or nullptr
-  int32_t* cs_feat;               // [L] column-pass splits
-  int32_t* cs_default;
-  int32_t* cs_other;
-  int32_t* cs_bin;
-  int32_t* cs_left_default;
-  int32_t* counts;                // [4] out: n_cs, n_next_open, n_build, n_nodes
-  // level d + 1 (out; capacity 2L open, L built)
-  int32_t* next_open;             // [2L] (-1 pad)
-  int64_t* next_totals;           // [2L][2]
-  int32_t* node_slot;             // [max_nodes] pass slot of the built nodes (-1)
-  int32_t* s2n;                   // [L] histogram row of slot s (-1)
-  int32_t* sub_dst;               // [L] subtraction: larger sibling (row in level d + 1) =
-  int32_t* sub_par;               //     parent (row in level d) - smaller sibling (row in level d + 1)
-  int32_t* sub_sib;
-};
-
-FDX_HD void level_plan(const LevelPlanArgs& a) {
-  for (int32_t n = 0; n < a.max_nodes; ++n) {
-    a.default_child[n] = -1;
-    a.node_slot[n] = -1;
-    if (a.node_dense) for (int k = 0; k < 4; ++k) a.node_dense[4 * n + k] = -1;
-  }
-  for (int32_t i = 0; i < 2 * a.L; ++i) {
-    a.next_open[i] = -1;
-    a.next_totals[2 * i] = a.next_totals[2 * i + 1] = 0;
-  }
-  for (int32_t i = 0; i < a.L; ++i) a.s2n[i] = a.sub_dst[i] = a.sub_par[i] = a.sub_sib[i] = -1;
-  const double thr = a.min_gain > 1e-6 ? a.min_gain : 1e-6;
-  int32_t nn = *a.n_nodes, n_cs = 0, n_next = 0;
-  const int32_t no = *a.n_open;
-  for (int32_t i = 0; i < no; ++i) {
-    const int32_t n = a.open[i];
-    const int64_t* p = a.packed + 5 * (int64_t)i;
-    double g;
-    memcpy(&g, &p[0], sizeof(double));
-    const int32_t f = (int32_t)p[1], b = (int32_t)p[2];
-    if (!(b >= 0 && isfinite(g) && g > thr) || nn + 2 > a.max_nodes) {
-      a.leaf[n] = 1;
-      continue;
-    }
-    const int32_t li = nn, ri = nn + 1;
-    nn += 2;
-    const int64_t l0 = p[3], l1 = p[4];
-    a.stats[2 * li] = l0;
-    a.stats[2 * li + 1] = l1;
-    a.stats[2 * ri] = a.stats[2 * n] - l0;
-    a.stats[2 * ri + 1] = a.stats[2 * n + 1] - l1;
-    const uint8_t leafy = (a.depth + 1 >= a.max_depth) ? 1 : 0;
-    for (int32_t c = li; c <= ri; ++c) {
-      a.parent[c] = n;
-      a.left[c] = a.right[c] = -1;
-      a.feat[c] = -1;
-      a.bin[c] = -1;
-      a.gain[c] = -1.0;
-      a.leaf[c] = leafy;
-    }
-    a.feat[n] = f;
-    a.bin[n] = b;
-    a.left[n] = li;
-    a.right[n] = ri;
-    a.gain[n] = g;
-    const bool left_default = a.zbin[f] <= b;
-    const int32_t dflt = left_default ? li : ri, other = left_default ? ri : li;
-    a.default_child[n] = dflt;
-    const int32_t hr = a.hot_row ? a.hot_row[f] : -1;
-    if (a.node_dense && hr >= 0) {
-      int32_t* nd = a.node_dense + 4 * (int64_t)n;
-      nd[0] = hr; nd[1] = b; nd[2] = li; nd[3] = ri;
-    } else {
-      a.cs_feat[n_cs] = f;
-      a.cs_default[n_cs] = dflt;
-      a.cs_other[n_cs] = other;
-      a.cs_bin[n_cs] = b;
-      a.cs_left_default[n_cs] = left_default ? 1 : 0;
-      ++n_cs;
-    }
-    for (int32_t c = li; c <= ri; ++c)
-      if (!a.leaf[c]) {
-        a.next_open[n_next] = c;
-        a.next_totals[2 * n_next] = a.stats[2 * c];
-        a.next_totals[2 * n_next + 1] = a.stats[2 * c + 1];
-        ++n_next;
-      }
-  }
-  // builds of level d + 1: per parent (in order of first appearance), the smaller open child
-  // (hessian sum, ties to the left child), the larger one by subtraction
-  int32_t nb = 0;
-  for (int32_t j = 0; j < n_next; ++j) {
-    const int32_t c = a.next_open[j], pnode = a.parent[c];
-    if (j > 0 && a.parent[a.next_open[j - 1]] == pnode) continue;      // siblings are adjacent
-    const int32_t lc = a.left[pnode], rc = a.right[pnode];
-    const bool lo = !a.leaf[lc], ro = !a.leaf[rc];
-    int32_t build, large = -1;
-    if (lo && ro) {
-      const bool lsmall = a.stats[2 * lc + 1] <= a.stats[2 * rc + 1];
-      build = lsmall ? lc : rc;
-      large = lsmall ? rc : lc;
-    } else {
-      build = lo ? lc : rc;
-    }
-    int32_t jb = -1, jl = -1, ip = -1;
-    for (int32_t k = 0; k < n_next; ++k) {
-      if (a.next_open[k] == build) jb = k;
-      if (a.next_open[k] == large) jl = k;
-    }
-    for (int32_t k = 0; k < no; ++k)
-      if (a.open[k] == pnode) ip = k;
-    a.node_slot[build] = nb;
-    a.s2n[nb] = jb;
-    if (large >= 0) {
-      a.sub_dst[nb] = jl;
-      a.sub_par[nb] = ip;
-      a.sub_sib[nb] = jb;
-    }
-    ++nb;
-  }
-  *a.n_nodes = nn;
-  a.counts[0] = n_cs;
-  a.counts[1] = n_next;
-  a.counts[2] = nb;
-  a.counts[3] = nn;
-}
-
 // Child of row r of split node n in the row pass.
 FDX_HD int32_t partition_row_child(const PartitionArgs& a, int32_t n, int64_t r) {
   const int32_t c = a.default_child[n];
@@ -521,6 +368,178 @@ FDX_HD double best_split_scan(const int64_t* hb, int nb, int zb, int64_t T0, int
   *out_l0 = bl0;
   *out_l1 = bl1;
   return best;
+}
+
+// Device-resident level loop of a tree (models/grower.py grow_tree_device): after the split
+// search of level d, ONE thread applies the best splits of the level's open nodes to the node
+// table, writes this level's partition tables and plans level d + 1 (open list, smaller-sibling
+// builds, subtraction triples), exactly as the host loop (grower.TreeTable.apply_splits and the
+// build selection of grow_tree) does -- same node numbering, same tie rules -- so the host only
+// reads two counts per level and the node table once per tree. Newton gain (GBDT) and Spark's
+// gini / entropy (DT / RF, optionally building every open node for per-node feature sampling).
+struct LevelPlanArgs {
+  const int64_t* packed;          // [L][5] best split per open node {gain bits, feature, bin, left0, left1}
+  int32_t L;                      // open-list capacity of this level
+  int32_t depth, max_depth;
+  int32_t mode;                   // 0 newton (gain > max(min_gain, 1e-6)), 1 gini / 2 entropy (gain > 0, >= min_gain)
+  int32_t build_all;              // build every open node (RF: no sibling subtraction)
+  const int32_t* kexp;            // [2] quantisation exponents (classification purity test)
+  double min_gain;
+  const int32_t* zbin;            // [Fa] zero bin of each feature (missing entries)
+  const int32_t* hot_row;         // [Fa] row of the feature in the dense block (-1), nullptr: none
+  int32_t max_nodes;
+  // node table (in/out)
+  int32_t* n_nodes;               // [1]
+  int64_t* stats;                 // [max_nodes][2] exact integer sums
+  int32_t* parent;
+  int32_t* left;
+  int32_t* right;
+  int32_t* feat;                  // Fa index of the split feature (-1 leaf / not split)
+  int32_t* bin;
+  uint8_t* leaf;
+  double* gain;
+  // this level (in): open nodes, local index i = row i of the level's histogram
+  const int32_t* open;            // [L] (-1 pad)
+  const int32_t* n_open;          // [1]
+  // this level's partition (out)
+  int32_t* default_child;         // [max_nodes]
+  int32_t* node_dense;            // [max_nodes][4] or nullptr
+  int32_t* cs_feat;               // [L] column-pass splits
+  int32_t* cs_default;
+  int32_t* cs_other;
+  int32_t* cs_bin;
+  int32_t* cs_left_default;
+  int32_t* counts;                // [4] out: n_cs, n_next_open, n_build, n_nodes
+  // level d + 1 (out; capacity 2L open, L built)
+  int32_t* next_open;             // [2L] (-1 pad)
+  int64_t* next_totals;           // [2L][2]
+  int32_t* node_slot;             // [max_nodes] pass slot of the built nodes (-1)
+  int32_t* s2n;                   // [L] histogram row of slot s (-1)
+  int32_t* sub_dst;               // [L] subtraction: larger sibling (row in level d + 1) =
+  int32_t* sub_par;               //     parent (row in level d) - smaller sibling (row in level d + 1)
+  int32_t* sub_sib;
+};
+
+FDX_HD void level_plan(const LevelPlanArgs& a) {
+  for (int32_t n = 0; n < a.max_nodes; ++n) {
+    a.default_child[n] = -1;
+    a.node_slot[n] = -1;
+    if (a.node_dense) for (int k = 0; k < 4; ++k) a.node_dense[4 * n + k] = -1;
+  }
+  for (int32_t i = 0; i < 2 * a.L; ++i) {
+    a.next_open[i] = -1;
+    a.next_totals[2 * i] = a.next_totals[2 * i + 1] = 0;
+  }
+  for (int32_t i = 0; i < a.L; ++i) a.s2n[i] = a.sub_dst[i] = a.sub_par[i] = a.sub_sib[i] = -1;
+  const double thr = a.min_gain > 1e-6 ? a.min_gain : 1e-6;
+  const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
+  int32_t nn = *a.n_nodes, n_cs = 0, n_next = 0;
+  const int32_t no = *a.n_open;
+  for (int32_t i = 0; i < no; ++i) {
+    const int32_t n = a.open[i];
+    const int64_t* p = a.packed + 5 * (int64_t)i;
+    double g;
+    memcpy(&g, &p[0], sizeof(double));
+    const int32_t f = (int32_t)p[1], b = (int32_t)p[2];
+    const bool ok = a.mode == 0 ? (b >= 0 && isfinite(g) && g > thr)
+                                : (b >= 0 && isfinite(g) && g > 0.0 && g >= a.min_gain);
+    if (!ok || nn + 2 > a.max_nodes) {
+      a.leaf[n] = 1;
+      continue;
+    }
+    const int32_t li = nn, ri = nn + 1;
+    nn += 2;
+    const int64_t l0 = p[3], l1 = p[4];
+    a.stats[2 * li] = l0;
+    a.stats[2 * li + 1] = l1;
+    a.stats[2 * ri] = a.stats[2 * n] - l0;
+    a.stats[2 * ri + 1] = a.stats[2 * n + 1] - l1;
+    for (int32_t c = li; c <= ri; ++c) {
+      bool leafy = a.depth + 1 >= a.max_depth;
+      if (a.mode != 0)   // pure node (grower._impurity == 0)
+        leafy = leafy || impurity(a.mode, (double)a.stats[2 * c] * s0, (double)a.stats[2 * c + 1] * s1) == 0.0;
+      a.parent[c] = n;
+      a.left[c] = a.right[c] = -1;
+      a.feat[c] = -1;
+      a.bin[c] = -1;
+      a.gain[c] = -1.0;
+      a.leaf[c] = leafy ? 1 : 0;
+    }
+    a.feat[n] = f;
+    a.bin[n] = b;
+    a.left[n] = li;
+    a.right[n] = ri;
+    a.gain[n] = g;
+    const bool left_default = a.zbin[f] <= b;
+    const int32_t dflt = left_default ? li : ri, other = left_default ? ri : li;
+    a.default_child[n] = dflt;
+    const int32_t hr = a.hot_row ? a.hot_row[f] : -1;
+    if (a.node_dense && hr >= 0) {
+      int32_t* nd = a.node_dense + 4 * (int64_t)n;
+      nd[0] = hr; nd[1] = b; nd[2] = li; nd[3] = ri;
+    } else {
+      a.cs_feat[n_cs] = f;
+      a.cs_default[n_cs] = dflt;
+      a.cs_other[n_cs] = other;
+      a.cs_bin[n_cs] = b;
+      a.cs_left_default[n_cs] = left_default ? 1 : 0;
+      ++n_cs;
+    }
+    for (int32_t c = li; c <= ri; ++c)
+      if (!a.leaf[c]) {
+        a.next_open[n_next] = c;
+        a.next_totals[2 * n_next] = a.stats[2 * c];
+        a.next_totals[2 * n_next + 1] = a.stats[2 * c + 1];
+        ++n_next;
+      }
+  }
+  // builds of level d + 1: per parent (in order of first appearance), the smaller open child
+  // (hessian sum / instance count, ties to the left child), the larger one by subtraction; or
+  // every open node (build_all)
+  int32_t nb = 0;
+  if (a.build_all) {
+    for (int32_t j = 0; j < n_next; ++j) {
+      a.node_slot[a.next_open[j]] = j;
+      a.s2n[j] = j;
+    }
+    nb = n_next;
+  }
+  for (int32_t j = 0; j < n_next && !a.build_all; ++j) {
+    const int32_t c = a.next_open[j], pnode = a.parent[c];
+    if (j > 0 && a.parent[a.next_open[j - 1]] == pnode) continue;      // siblings are adjacent
+    const int32_t lc = a.left[pnode], rc = a.right[pnode];
+    const bool lo = !a.leaf[lc], ro = !a.leaf[rc];
+    int32_t build, large = -1;
+    if (lo && ro) {
+      const int64_t wl = a.mode == 0 ? a.stats[2 * lc + 1] : a.stats[2 * lc] + a.stats[2 * lc + 1];
+      const int64_t wr = a.mode == 0 ? a.stats[2 * rc + 1] : a.stats[2 * rc] + a.stats[2 * rc + 1];
+      const bool lsmall = wl <= wr;
+      build = lsmall ? lc : rc;
+      large = lsmall ? rc : lc;
+    } else {
+      build = lo ? lc : rc;
+    }
+    int32_t jb = -1, jl = -1, ip = -1;
+    for (int32_t k = 0; k < n_next; ++k) {
+      if (a.next_open[k] == build) jb = k;
+      if (a.next_open[k] == large) jl = k;
+    }
+    for (int32_t k = 0; k < no; ++k)
+      if (a.open[k] == pnode) ip = k;
+    a.node_slot[build] = nb;
+    a.s2n[nb] = jb;
+    if (large >= 0) {
+      a.sub_dst[nb] = jl;
+      a.sub_par[nb] = ip;
+      a.sub_sib[nb] = jb;
+    }
+    ++nb;
+  }
+  *a.n_nodes = nn;
+  a.counts[0] = n_cs;
+  a.counts[1] = n_next;
+  a.counts[2] = nb;
+  a.counts[3] = nn;
 }
 
 }  // namespace fdx

@@ -304,7 +304,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     use_coll = coll is not None and coll.active
     shards = ws.shards(coll) if use_coll and (coll.world > 1 or getattr(coll, "force", False)) else None
     if device_levels_ok(params, weight):
-        return grow_tree_device(Q, ws, params, tree_index, g, h, weight, coll if use_coll else None, shards)
+        return grow_tree_device(Q, ws, params, tree_index, g, h, weight, coll if use_coll else None, shards,
+                                label=label, bootstrap=bootstrap)
     dev = Q.device
     mode_rs = 0 if params.mode == 0 else 1
     np_ = _choose_np(params, weight)
@@ -578,11 +579,12 @@ class TreeTable:
 
 
 def device_levels_ok(params: GrowParams, weight, device_levels: Optional[bool] = None) -> bool:
-    """The device level loop covers single-process GBDT (Newton gain, all features) trees whose
-    deepest level builds <= one pass of node slots (max_depth <= 6)."""
+    """The device level loop covers every tree whose deepest level builds <= one pass of node
+    slots: GBDT to depth 6, class-count trees to depth 7 (RF with per-node feature sampling,
+    which builds every open node, to depth 7; weighted ones to depth 5)."""
     on = DEVICE_LEVELS if device_levels is None else device_levels
-    return (on and params.mode == 0 and not params.feat_k and _choose_np(params, weight) == 4
-            and 2 ** max(params.max_depth - 2, 0) <= slots_per_tile(4) * MAX_CT)
+    deepest = 2 ** max(params.max_depth - (1 if params.feat_k else 2), 0)
+    return on and deepest <= slots_per_tile(_choose_np(params, weight)) * MAX_CT
 
 
 class LevelState:
@@ -626,7 +628,8 @@ class LevelState:
 
 def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
                      h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
-                     shards: Optional["FeatureShards"] = None) -> Tree:
+                     shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
+                     bootstrap: bool = False) -> Tree:
     """GBDT tree with the level loop on the device (same trees as grow_tree's host loop, bit for
     bit). Per level: histogram passes -> sibling subtraction -> split search -> best split per
     node -> ``tree_level_plan`` (one thread: apply the splits to the device node table, this
@@ -638,16 +641,24 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
     every rank plans the identical next level from the identical gathered splits."""
     C = native.lib()
     dev = Q.device
-    np_ = 4
+    np_ = _choose_np(params, weight)
+    mode_rs = 0 if params.mode == 0 else 1
+    build_all = bool(params.feat_k)
     st = getattr(ws, "_levels", None)
     if st is None or st.max_depth != params.max_depth:
         st = ws._levels = LevelState(Q, params.max_depth)
     ws.row_node.zero_()
+    seed = int(params.seed)
     with tracing.span("tree.quant"):
-        C.tree_quant_max(g, h, None, weight, int(params.seed), int(tree_index), False, 0, Q.n_rows, ws.maxabs, Q.row0)
-        mx = coll.max(ws.maxabs) if coll is not None else ws.maxabs
-        C.tree_quant(g, h, None, weight, int(params.seed), int(tree_index), False, 0, 4, mx, ws.rowdig,
-                     ws.kexp, ws.totals, ws.digp, Q.row0)
+        if np_ == 4:
+            C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
+                             ws.maxabs, Q.row0)
+            mx = coll.max(ws.maxabs) if coll is not None else ws.maxabs
+            C.tree_quant(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, 4, mx, ws.rowdig,
+                         ws.kexp, ws.totals, ws.digp, Q.row0)
+        else:
+            C.tree_quant(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, 1, None, ws.rowdig,
+                         ws.kexp, ws.totals, ws.digp, Q.row0)
     tot = coll.sum(ws.totals) if coll is not None else ws.totals
     # root: node 0, open list [0] with the exact totals (no host round trip)
     st.n_nodes.fill_(1)
@@ -676,8 +687,15 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
         else:   # local partials of the built nodes (+1 zero pad bin for the shard packing)
             hist_target = torch.zeros((n_build, TB + 1, 2), dtype=torch.int64, device=dev)
+        # RF: exact k-of-F feature sample per open node and the level's union mask (device)
+        feat_thr = feat_mask = None
+        if build_all:
+            feat_thr = torch.empty(n_open, dtype=torch.float64, device=dev)
+            feat_mask = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
+            C.tree_rf_sample(seed, int(tree_index), open_d, int(Q.num_features), int(params.feat_k), Q.fid_orig,
+                             feat_thr, feat_mask, None)
         with tracing.span("tree.hist"):
-            use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH
+            use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH and not build_all
             sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
             slot8 = None
             csc_slot8, csc_dig = None, ws.rowdig
@@ -705,7 +723,7 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 launches.append(functools.partial(
                     C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
                     Q.h_row, Q.h_key, csc_slot8, csc_dig, Q.boff, Q.nbins, s2n, hist_target, TB, grp.bt, ct, np_,
-                    None))
+                    feat_mask))
             if use_dense:
                 for bt in (1, 2, 4):
                     fg = C.tree_dense_fg(bt, ct if d > 0 else 1)
@@ -722,22 +740,23 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 mine = coll.reduce_scatter(packed_in.permute(1, 0, 2, 3))
                 cur_hist = torch.zeros((n_open, shards.bins, 2), dtype=torch.int64, device=dev)
                 cur_hist.index_copy_(0, bidx.to(torch.int64), mine[:, : shards.bins].contiguous())
-        if d > 0:
+        if d > 0 and not build_all:
             C.tree_hist_subtract(prev_hist, cur_hist, st.sub_dst[:n_build], st.sub_par[:n_build],
                                  st.sub_sib[:n_build], TB if shards is None else shards.bins)
         with tracing.span("tree.split"):
             if shards is None:
                 packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
-                                      params, None, tree_index, Q.Fa, 0)
+                                      params, feat_thr, tree_index, Q.Fa, 0)
             else:
                 mine = _best_splits(C, cur_hist, totals_d, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
-                                    open_d, ws.kexp, params, None, tree_index, shards.Fa, shards.f0)
+                                    open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0)
                 allt = coll.all_gather(mine)                                  # [S, n_open, 5]
                 gains = allt[:, :, 0].contiguous().view(torch.float64)
                 best_s = torch.argmax(gains, dim=0)                           # ties -> lowest shard = lowest feature
                 packed = allt[best_s, torch.arange(n_open, device=dev)].contiguous()
         nxt = 1 - cur
-        C.tree_level_plan(packed, n_open, d, params.max_depth, float(params.min_gain), Q.zbin, st.hot_row,
+        C.tree_level_plan(packed, n_open, d, params.max_depth, int(params.mode), build_all, ws.kexp,
+                          float(params.min_gain), Q.zbin, st.hot_row,
                           st.n_nodes, st.stats, st.parent, st.left, st.right, st.feat, st.bin, st.leaf, st.gain,
                           open_d, n_open_ptr, st.default_child, st.node_dense, *st.cs, st.counts[d],
                           st.open[nxt], st.totals[nxt], st.node_slot, st.s2n, st.sub_dst, st.sub_par, st.sub_sib)

@@ -527,3 +527,27 @@ def test_device_level_loop_grows_the_host_loop_trees(monkeypatch, depth, hot):
     _same_trees(out[False].trees, out[True].trees)
     assert max(t.num_nodes for t in out[True].trees) == (3 if depth == 1 else max(t.num_nodes for t in out[True].trees))
     assert depth == 1 or max(t.num_nodes for t in out[True].trees) > 7
+
+
+@pytest.mark.parametrize("kw", [dict(num_trees=1, max_depth=6),                                   # DT, subtraction
+                                dict(num_trees=3, max_depth=5, bootstrap=True, feature_subset="sqrt", seed=7),
+                                dict(num_trees=2, max_depth=4, impurity="entropy", feature_subset="onethird",
+                                     bootstrap=True, seed=3),
+                                dict(num_trees=1, max_depth=4, weights=True)])                    # 4-plane counts
+def test_device_level_loop_grows_the_host_loop_forests(monkeypatch, kw):
+    """DT / RF (per-node k-of-F sampling builds every open node, Poisson bootstrap, gini and
+    entropy purity leaves) and weighted class counts: the device level loop's trees equal the host
+    loop's bit for bit."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+
+    dense, y = random_counts_matrix(2500, 70, 0.2, 33)
+    vc = vc_from_dense(dense)
+    kw = dict(kw)
+    if kw.pop("weights", False):
+        kw["weights"] = np.random.default_rng(2).uniform(0.2, 3.0, len(y))
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(grower, "DEVICE_LEVELS", flag)
+        out[flag] = fit_forest(vc, torch.from_numpy(y), device="cpu", prune=False, **kw)
+    _same_trees(out[False].trees, out[True].trees)
+    assert max(t.num_nodes for t in out[True].trees) > 7
