@@ -64,7 +64,7 @@ PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 # next-level planning run on the GPU, the host reads 16 bytes per level and the node table once
 # per tree (FDX_DEVICE_LEVELS=0: host loop)
 DEVICE_LEVELS = os.environ.get("FDX_DEVICE_LEVELS", "1") != "0"
-PARTITION_WPS = 16              # blocks per column split in the device partition pass
+PARTITION_WPS = int(os.environ.get("FDX_PARTITION_WPS", 256))  # blocks per column split (device partition)
 
 
 @dataclass
