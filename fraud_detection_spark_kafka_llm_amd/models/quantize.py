@@ -563,11 +563,10 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
             C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total], kb)
     sp_g = tracing.span("q.groups")
     sp_g.__enter__()
-    arr = items.astype(np.int64)
+    arr = np.asarray(items, dtype=np.int64)
     is_hot = hot[arr[:, 2]] & (arr[:, 4] == 1) if arr.shape[0] else np.zeros(0, bool)
     # the item table and every group's row order (by entry offset; the parts are sorted runs, so
-    # the stable host sort is linear) go up in two pinned copies: ~20 synchronous pageable copies
-    # of small arrays cost ~100 ms at 10M rows
+    # the stable host sort is linear) go up in two pinned copies instead of five per group
     sels = []
     for sel in (~is_hot, is_hot):
         for bt in (1, 2, 4):
