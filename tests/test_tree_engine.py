@@ -551,3 +551,23 @@ def test_device_level_loop_grows_the_host_loop_forests(monkeypatch, kw):
         out[flag] = fit_forest(vc, torch.from_numpy(y), device="cpu", prune=False, **kw)
     _same_trees(out[False].trees, out[True].trees)
     assert max(t.num_nodes for t in out[True].trees) > 7
+
+
+@pytest.mark.gpu
+def test_gpu_device_level_loop_equals_gpu_host_loop(monkeypatch):
+    """On the GPU, the device-resident level loop (level_plan / partition_cols kernels, masked
+    single-slot passes) grows the same GBDT and RF trees as the host level loop."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+
+    dense, y = random_counts_matrix(6000, 90, 0.2, 44)
+    dense[:, :5] = np.random.default_rng(4).integers(0, 6, (6000, 5))
+    vc = vc_from_dense(dense)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(grower, "DEVICE_LEVELS", flag)
+        g = fit_gbdt(vc, torch.from_numpy(y), GBDTParams(n_estimators=4, max_depth=6), device="cuda:0")
+        r = fit_forest(vc, torch.from_numpy(y), num_trees=3, max_depth=5, bootstrap=True, feature_subset="sqrt",
+                       seed=5, device="cuda:0", prune=False)
+        out[flag] = (g.trees, r.trees)
+    _same_trees(out[False][0], out[True][0])
+    _same_trees(out[False][1], out[True][1])
