@@ -31,7 +31,7 @@ from ..ml.tree_model import Tree
 from ..ops import native
 from ..parallel.dist import Collectives
 from ..utils import tracing
-from .grower import GrowParams, Workspace, grow_tree
+from .grower import GrowParams, PendingTree, Workspace, grow_tree
 from .tree import prepare
 
 
@@ -111,10 +111,24 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
 
         margin += score_csr(vc, ensemble_arrays(trees, "value", cmp_less=False))[:, 0]
     history = []
+    # without per-round hooks, tree t's host table is built while tree t + 1's root level runs on
+    # the GPU (its leaf values come from the device node table, bitwise the host's)
+    defer = eval_fn is None and checkpoint is None and ckpt is None
+    pending = None
     for t in range(len(trees), params.n_estimators):
         with tracing.span("gbdt.round", round=t):
             C.tree_logistic_grad(margin, y, w, g, h)
-            tree = grow_tree(Q, ws, gp, t, g=g, h=h, coll=coll)
+            res = grow_tree(Q, ws, gp, t, g=g, h=h, coll=coll, deferred=defer,
+                            on_first_wait=pending.finish if pending is not None else None)
+            if pending is not None:
+                trees.append(pending.result().compacted())
+                pending = None
+            if isinstance(res, PendingTree):
+                C.tree_leaf_update(margin, ws.row_node, res.node_value)
+                pending = res
+                maybe_fail(t)
+                continue
+            tree = res
             node_value = torch.from_numpy(np.ascontiguousarray(tree.stats[:, 0])).to(dev)
             C.tree_leaf_update(margin, ws.row_node, node_value)
         trees.append(tree.compacted())
@@ -125,6 +139,8 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
         if ckpt is not None:
             ckpt.maybe_save(len(trees), trees, base, F, params, force=len(trees) == params.n_estimators)
         maybe_fail(t)
+    if pending is not None:
+        trees.append(pending.result().compacted())
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0)

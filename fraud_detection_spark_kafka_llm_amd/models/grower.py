@@ -295,7 +295,7 @@ def _choose_np(params: GrowParams, weight) -> int:
 def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
               g: Optional[torch.Tensor] = None, h: Optional[torch.Tensor] = None,
               label: Optional[torch.Tensor] = None, weight: Optional[torch.Tensor] = None,
-              bootstrap: bool = False, coll=None) -> Tree:
+              bootstrap: bool = False, coll=None, deferred: bool = False, on_first_wait=None):
     """``coll`` (parallel.dist.Collectives): data-parallel level with feature-sharded split
     finding when world > 1 -- partial histograms are reduce-scattered by feature shard, every
     rank searches splits of its own shard, and the per-node best tuples are all-gathered
@@ -305,7 +305,9 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     shards = ws.shards(coll) if use_coll and (coll.world > 1 or getattr(coll, "force", False)) else None
     if device_levels_ok(params, weight):
         return grow_tree_device(Q, ws, params, tree_index, g, h, weight, coll if use_coll else None, shards,
-                                label=label, bootstrap=bootstrap)
+                                label=label, bootstrap=bootstrap, deferred=deferred, on_first_wait=on_first_wait)
+    if on_first_wait is not None:
+        on_first_wait()
     dev = Q.device
     mode_rs = 0 if params.mode == 0 else 1
     np_ = _choose_np(params, weight)
@@ -597,11 +599,38 @@ class LevelState:
         cap = 2 ** max_depth
         i32 = lambda n: torch.full((n,), -1, dtype=torch.int32, device=dev)   # noqa: E731
         self.M, self.cap, self.max_depth = M, cap, max_depth
-        self.n_nodes = torch.ones(1, dtype=torch.int32, device=dev)
-        self.stats = torch.zeros((M, 2), dtype=torch.int64, device=dev)
-        self.parent, self.left, self.right, self.feat, self.bin = i32(M), i32(M), i32(M), i32(M), i32(M)
-        self.leaf = torch.zeros(M, dtype=torch.uint8, device=dev)
-        self.gain = torch.full((M,), -1.0, dtype=torch.float64, device=dev)
+        # the node table (+ the tree's quantisation exponents) lives in ONE device arena, mirrored by
+        # one pinned host arena: the host reads a finished tree with a single D2H copy (eleven
+        # separate small copies cost ~0.4 ms per tree at ~25-30 us each)
+        layout = [("stats", torch.int64, (M, 2)), ("gain", torch.float64, (M,)), ("n_nodes", torch.int32, (1,)),
+                  ("kexp", torch.int32, (2,)), ("parent", torch.int32, (M,)), ("feat", torch.int32, (M,)),
+                  ("bin", torch.int32, (M,)), ("left", torch.int32, (M,)), ("right", torch.int32, (M,)),
+                  ("leaf", torch.uint8, (M,))]
+        offs, nbytes = [], 0
+        for _, dt, shape in layout:
+            isz = torch.empty(0, dtype=dt).element_size()
+            nbytes = (nbytes + 7) // 8 * 8
+            offs.append(nbytes)
+            nbytes += isz * int(np.prod(shape))
+        self.arena = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        self.arena_host = torch.zeros(nbytes, dtype=torch.uint8)
+        if dev.type == "cuda":
+            self.arena_host = self.arena_host.pin_memory()
+        host = {}
+        for (name, dt, shape), o in zip(layout, offs):
+            n = torch.empty(0, dtype=dt).element_size() * int(np.prod(shape))
+            setattr(self, name if name != "kexp" else "kexp_slot", self.arena[o:o + n].view(dt).view(shape))
+            host[name] = self.arena_host[o:o + n].view(dt).view(shape)
+        self.host = host
+        self.n_nodes.fill_(1)
+        for t_ in (self.parent, self.left, self.right, self.feat, self.bin):
+            t_.fill_(-1)
+        self.gain.fill_(-1.0)
+        # the root state of every tree (node 0 only, stats filled per tree): one H2D copy of this
+        # image replaces ~9 fill launches at the start of each tree
+        self.arena_init = self.arena.to("cpu", copy=True)       # (a copy also when dev is the CPU)
+        if dev.type == "cuda":
+            self.arena_init = self.arena_init.pin_memory()
         self.open = [i32(cap), i32(cap)]
         self.totals = [torch.zeros((cap, 2), dtype=torch.int64, device=dev) for _ in range(2)]
         self.counts = torch.zeros((max_depth + 1, 4), dtype=torch.int32, device=dev)
@@ -612,12 +641,6 @@ class LevelState:
         self.default_child, self.node_slot = i32(M), i32(M)
         self.cs = [i32(cap) for _ in range(5)]          # feat, default, other, bin, left_default
         self.s2n, self.sub_dst, self.sub_par, self.sub_sib = i32(cap), i32(cap), i32(cap), i32(cap)
-        # pinned host mirror of the node table: one batch of async copies + one wait per tree
-        self.table = (self.n_nodes, self.parent, self.feat, self.bin, self.left, self.right, self.gain, self.stats,
-                      self.leaf)
-        self.table_host = [torch.empty(t_.shape, dtype=t_.dtype) for t_ in self.table]
-        if dev.type == "cuda":
-            self.table_host = [t_.pin_memory() for t_ in self.table_host]
         self.node_dense = self.hot_row = None
         if Q.dense is not None and PARTITION_DENSE:
             hot_row = np.full(Q.Fa, -1, dtype=np.int32)
@@ -629,7 +652,7 @@ class LevelState:
 def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
                      h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
                      shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
-                     bootstrap: bool = False) -> Tree:
+                     bootstrap: bool = False, deferred: bool = False, on_first_wait=None):
     """GBDT tree with the level loop on the device (same trees as grow_tree's host loop, bit for
     bit). Per level: histogram passes -> sibling subtraction -> split search -> best split per
     node -> ``tree_level_plan`` (one thread: apply the splits to the device node table, this
@@ -638,7 +661,10 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
     runs) to size the next level's launches, and reads the node table once at the end.
     Data parallel (``shards``): the built nodes' partial histograms are reduce-scattered by
     feature shard and the per-shard best splits all-gathered, all stream-ordered on the device;
-    every rank plans the identical next level from the identical gathered splits."""
+    every rank plans the identical next level from the identical gathered splits.
+    ``deferred`` (GBDT): return a :class:`PendingTree` whose leaf values were computed on the
+    device; the host table is built later (``on_first_wait`` of the next tree runs it while that
+    tree's root level is on the GPU), so the GPU never idles on the host's tree build."""
     C = native.lib()
     dev = Q.device
     np_ = _choose_np(params, weight)
@@ -661,12 +687,8 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                          ws.kexp, ws.totals, ws.digp, Q.row0)
     tot = coll.sum(ws.totals) if coll is not None else ws.totals
     # root: node 0, open list [0] with the exact totals (no host round trip)
-    st.n_nodes.fill_(1)
+    st.arena.copy_(st.arena_init, non_blocking=True)
     st.stats[0].copy_(tot)
-    for t_ in (st.parent, st.left, st.right, st.feat, st.bin):
-        t_[:1].fill_(-1)
-    st.leaf[:1].zero_()
-    st.gain[:1].fill_(-1.0)
     st.open[0][:1].zero_()
     st.totals[0][:1].copy_(tot[None])
     TB = Q.TB
@@ -676,6 +698,9 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
     for d in range(params.max_depth):
         cur = d % 2
         if d > 0:
+            if on_first_wait is not None:
+                on_first_wait()
+                on_first_wait = None
             ev.synchronize()
             cnt = st.counts_host[d - 1].tolist()
             n_open, n_build = int(cnt[1]), int(cnt[2])
@@ -771,16 +796,58 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             C.tree_partition_cols(ws.row_node, st.default_child, *st.cs, st.counts[d], Q.colptr, Q.csc_row, Q.csc_bin,
                                   st.node_dense, Q.dense if st.node_dense is not None else None, n_open, PARTITION_WPS)
         prev_hist = cur_hist
-    # one read of the node table per tree (async copies into the pinned mirror, one wait)
-    for hst, t_ in zip(st.table_host, st.table):
-        hst.copy_(t_, non_blocking=True)
+    if on_first_wait is not None:          # (a one-level tree) the previous table first
+        on_first_wait()
+    # one read of the node table per tree: the arena (table + exponents) in one D2H copy, one wait
+    st.kexp_slot.copy_(ws.kexp)
+    node_value = leaf_values_device(st.stats, ws.kexp, params) if deferred and params.mode == 0 else None
+    st.arena_host.copy_(st.arena, non_blocking=True)
+    done = torch.cuda.Event() if dev.type == "cuda" else _Done()
     if dev.type == "cuda":
-        torch.cuda.current_stream(dev).synchronize()
-    nn = int(st.table_host[0][0])
-    arr = [t_[:nn].numpy() for t_ in st.table_host[1:]]
-    kexp = ws.kexp.cpu().numpy().astype(np.int64)
-    tab = TreeTable.from_arrays(Q, *arr)
-    return tab.build(Q, params, np.ldexp(1.0, -kexp))
+        done.record()
+
+    def finish() -> Tree:
+        done.synchronize()
+        hv = st.host
+        nn = int(hv["n_nodes"][0])
+        arr = [hv[k][:nn].numpy().copy() for k in ("parent", "feat", "bin", "left", "right", "gain", "stats", "leaf")]
+        kexp = hv["kexp"].numpy().astype(np.int64)
+        tab = TreeTable.from_arrays(Q, *arr)
+        return tab.build(Q, params, np.ldexp(1.0, -kexp))
+
+    if node_value is not None:
+        return PendingTree(node_value, finish)
+    return finish()
+
+
+def leaf_values_device(stats: torch.Tensor, kexp: torch.Tensor, params: GrowParams) -> torch.Tensor:
+    """GBDT leaf values of the device node table, the same fp64 operations as TreeTable.build
+    (so bitwise the host's values): G, H = stats * 2^-k (exact), eta * clip(-G / (H + lambda))."""
+    scale = ((1023 - kexp.to(torch.int64)) << 52).view(torch.float64)      # exactly 2^-k
+    G = stats[:, 0].to(torch.float64) * scale[0]
+    H = stats[:, 1].to(torch.float64) * scale[1]
+    w = -G / (H + params.lambda_)
+    if params.max_delta_step > 0:
+        w = torch.clamp(w, -params.max_delta_step, params.max_delta_step)
+    return params.eta * w
+
+
+class PendingTree:
+    """A grown GBDT tree whose host table is not built yet: ``node_value`` (device, per node id)
+    is ready in stream order for the margin update; ``result()`` builds the Tree once."""
+
+    def __init__(self, node_value: torch.Tensor, finish):
+        self.node_value = node_value
+        self._finish = finish
+        self._tree = None
+
+    def finish(self) -> None:
+        if self._tree is None:
+            self._tree = self._finish()
+
+    def result(self) -> Tree:
+        self.finish()
+        return self._tree
 
 
 class _Done:
