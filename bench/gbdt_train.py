@@ -62,6 +62,10 @@ def main():
     ap.add_argument("--no-warmup", action="store_true", help="skip the untimed warm-up fit (models/warmup.py)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    # CPUs of the GPU's NUMA node, as bench.py does (without it, the first quantize on the box
+    # showed a ~0.1 s host stall: profiles/r2s4/NOTES.md)
+    from fraud_detection_spark_kafka_llm_amd.parallel.affinity import bind_to_gpu
+    bind_to_gpu(dev.index)
     if not args.no_warmup:     # lazily loaded code objects and cold allocators, as in bench.py
         from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels
         warm_tree_kernels(dev, gbdt_depth=args.depth)
