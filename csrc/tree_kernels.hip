@@ -258,6 +258,8 @@ __device__ __forceinline__ void gather_digits(const uint2* __restrict__ rd, int4
 // Measured and kept out: dword staging of all entries with slot-masked B (0-20 % slower), and
 // waves streaming lists of consecutive items through one pipeline (no faster for the ~1K-entry
 // text-feature items, slower for the rest).
+// (Forcing 4 waves per SIMD on the CT = 8 pass -- 128 registers, 15 spilled -- measured no
+// faster than its 3 waves: profiles/r2s4/hist_REJECTED_w4_ab.txt)
 template <int BT, int CT, int NP, bool ROOT>
 __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   constexpr int G = 4 * kWave;                 // entries per wave step
@@ -284,14 +286,6 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
 
   const int r = lane & 15, g = lane >> 4;
   const int slot_sub = r / CPS, q = r % CPS;
-  int node_of[CT];                              // histogram row of each column tile's slot (-1: none)
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    const int slot = ct * SPT + slot_sub;
-    const int n = a.slot_node[slot < a.nslots ? slot : a.nslots - 1];
-    node_of[ct] = slot < a.nslots ? n : -1;
-  }
-
   i32x4 acc[BT][CT];
 #pragma unroll
   for (int bt = 0; bt < BT; ++bt)
@@ -415,6 +409,15 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   // histogram. The bin offset of each of the lane's key rows is loaded first, all at once (clamped
   // indices), so no atomic waits on a dependent load. (A padded bin layout with one offset per item
   // would depend on each rank's local packing and break the data-parallel histogram shapes.)
+  // histogram row of each column tile's slot (-1: none), loaded here rather than kept live
+  // through the main loop (8 registers at CT = 8)
+  int node_of[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int slot = ct * SPT + slot_sub;
+    const int n = a.slot_node[slot < a.nslots ? slot : a.nslots - 1];
+    node_of[ct] = slot < a.nslots ? n : -1;
+  }
   const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta);
   int64_t bin_of[BT][4];
 #pragma unroll
