@@ -571,3 +571,60 @@ def test_gpu_device_level_loop_equals_gpu_host_loop(monkeypatch):
         out[flag] = (g.trees, r.trees)
     _same_trees(out[False][0], out[True][0])
     _same_trees(out[False][1], out[True][1])
+
+
+@pytest.mark.parametrize("max_delta_step", [0.0, 0.7])
+def test_deferred_tree_build_equals_immediate(max_delta_step):
+    """GBDT without per-round hooks builds tree t's host table during tree t + 1 and updates the
+    margins with leaf values computed from the device node table (models/grower.py
+    leaf_values_device); with an eval hook every tree is built immediately from host leaf values.
+    Both give the same trees and the same final margins, bit for bit."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+
+    dense, y = random_counts_matrix(2500, 60, 0.2, 57)
+    vc = vc_from_dense(dense)
+    params = GBDTParams(n_estimators=5, max_depth=5, max_delta_step=max_delta_step)
+    margins = []
+    immediate = fit_gbdt(vc, torch.from_numpy(y), params, device="cpu",
+                         eval_fn=lambda t, trees, m: margins.append(m.clone()))
+    deferred = fit_gbdt(vc, torch.from_numpy(y), params, device="cpu")
+    _same_trees(immediate.trees, deferred.trees)
+    base = torch.full((len(y),), deferred.base_margin, dtype=torch.float64)
+    replay = base + score_csr(vc, ensemble_arrays(deferred.trees, "value", cmp_less=False))[:, 0]
+    assert torch.allclose(replay, margins[-1], rtol=0, atol=1e-12)
+
+
+def test_leaf_values_device_bitwise_equal_host_table():
+    """The device leaf values are the host table's values bit for bit (exact 2^-k scaling)."""
+    from fraud_detection_spark_kafka_llm_amd.models.grower import GrowParams, leaf_values_device
+
+    rng = np.random.default_rng(3)
+    stats = torch.from_numpy(np.stack([rng.integers(-2**50, 2**50, 64), rng.integers(0, 2**54, 64)], 1))
+    kexp = torch.tensor([31, 29], dtype=torch.int32)
+    for mds in (0.0, 0.5):
+        p = GrowParams(mode=0, lambda_=1.0, eta=0.3, max_delta_step=mds)
+        dev = leaf_values_device(stats, kexp, p).numpy()
+        st = stats.numpy().astype(np.float64) * np.ldexp(1.0, -kexp.numpy().astype(np.int64))
+        w = -st[:, 0] / (st[:, 1] + p.lambda_)
+        if mds > 0:
+            w = np.clip(w, -mds, mds)
+        assert np.array_equal((p.eta * w).view(np.int64), dev.view(np.int64))
+
+
+@pytest.mark.gpu
+def test_gpu_leaf_values_device_bitwise_equal_host_table():
+    """On the GPU (int64 -> fp64 conversion, fp64 division on the device): the same bits as the
+    host table's leaf values."""
+    from fraud_detection_spark_kafka_llm_amd.models.grower import GrowParams, leaf_values_device
+
+    rng = np.random.default_rng(5)
+    stats = torch.from_numpy(np.stack([rng.integers(-2**55, 2**55, 4096), rng.integers(0, 2**56, 4096)], 1))
+    kexp = torch.tensor([33, 27], dtype=torch.int32)
+    for mds in (0.0, 0.5):
+        p = GrowParams(mode=0, lambda_=1.0, eta=0.3, max_delta_step=mds)
+        dev = leaf_values_device(stats.cuda(), kexp.cuda(), p).cpu().numpy()
+        st = stats.numpy().astype(np.float64) * np.ldexp(1.0, -kexp.numpy().astype(np.int64))
+        w = -st[:, 0] / (st[:, 1] + p.lambda_)
+        if mds > 0:
+            w = np.clip(w, -mds, mds)
+        assert np.array_equal((p.eta * w).view(np.int64), dev.view(np.int64))
