@@ -208,8 +208,7 @@ def main():
     fo = feature_order(indptr, idx, counts, F)          # CSC by feature: docFreq now, quantize later
     df = D.all_reduce_sum(fo.df)
     idf = torch.log((args.rows + 1.0) / (df.double() + 1.0))
-    vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-    vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
+    vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)
     t_feat = time.perf_counter() - t0
     res = fit_gbdt(vc, y, gparams, device=dev)
     sync_all(dev)

@@ -77,8 +77,7 @@ def main():
     F = 1 << 18
     fo = feature_order(indptr, idx, counts, F)
     idf = torch.log((args.rows + 1.0) / (fo.df.double() + 1.0))
-    vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-    vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
+    vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)

@@ -22,8 +22,7 @@ indptr, idx, counts, y, _, _ = build_features(args.rows, dev)
 F = 1 << 18
 fo = feature_order(indptr, idx, counts, F)
 idf = torch.log((args.rows + 1.0) / (fo.df.double() + 1.0))
-vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
+vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)
 Q = quantize(vc, max_bins=256, counts=counts, scale=idf)
 nb = Q.nbins.cpu().numpy()
 cnt = np.diff(Q.colptr.cpu().numpy())

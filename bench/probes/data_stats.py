@@ -32,8 +32,7 @@ def main():
     F = 1 << 18
     fo = feature_order(indptr, idx, counts, F)
     idf = torch.log((args.rows + 1.0) / (fo.df.double() + 1.0))
-    vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-    vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
+    vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)
     Q = quantize(vc, max_bins=args.max_bins, counts=counts, scale=idf)
     colptr = Q.colptr.cpu().numpy()
     n = np.diff(colptr)

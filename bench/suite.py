@@ -50,8 +50,7 @@ def _tfidf(rows, dev, seed, first_row=0, idf=None):
     if idf is None:
         fo = feature_order(indptr, idx, counts, F)
         idf = torch.log((rows + 1.0) / (fo.df.double() + 1.0))
-    vc = VectorColumn(F, indptr, idx, counts.double() * idf[idx.long()])
-    vc.tf_counts, vc.tf_scale, vc._feature_order = counts, idf, fo
+    vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)
     return vc, y, idf
 
 

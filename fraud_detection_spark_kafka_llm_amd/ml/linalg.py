@@ -99,9 +99,40 @@ class VectorColumn:
     def __init__(self, size: int, indptr: Optional[torch.Tensor] = None, indices: Optional[torch.Tensor] = None,
                  values: Optional[torch.Tensor] = None, dense: Optional[torch.Tensor] = None):
         self.size = int(size)
-        self.indptr, self.indices, self.values, self.dense = indptr, indices, values, dense
+        self.indptr, self.indices, self._values, self.dense = indptr, indices, values, dense
+        # TF-IDF columns built by the featurizer keep the integer term counts and the per-feature
+        # IDF instead of fp64 values (8 B per entry, ~8 GB at 10M dialogues): the tree trainers
+        # bin the counts directly, and ``values`` is only materialised if something asks for it
+        self.tf_counts: Optional[torch.Tensor] = None
+        self.tf_scale: Optional[torch.Tensor] = None
         if dense is None and indptr is None:
             raise ValueError("VectorColumn needs CSR arrays or a dense matrix")
+
+    @property
+    def values(self) -> Optional[torch.Tensor]:
+        if self._values is None and self.tf_counts is not None and self.indices is not None:
+            self._values = self.tf_counts.to(torch.float64) * self.tf_scale.to(
+                device=self.indices.device, dtype=torch.float64)[self.indices.long()]
+        return self._values
+
+    @values.setter
+    def values(self, v: Optional[torch.Tensor]) -> None:
+        self._values = v
+
+    @property
+    def values_materialized(self) -> bool:
+        return self._values is not None
+
+    @classmethod
+    def tfidf(cls, size: int, indptr: torch.Tensor, indices: torch.Tensor, counts: torch.Tensor,
+              idf: torch.Tensor, feature_order=None) -> "VectorColumn":
+        """A CSR TF-IDF column kept as (term counts, IDF vector): values = counts * idf[index],
+        computed lazily (SURVEY §7.5 sizing: 4 B index + 4 B count per entry instead of + 8 B)."""
+        vc = cls(size, indptr, indices, None)
+        vc.tf_counts, vc.tf_scale = counts, idf
+        if feature_order is not None:
+            vc._feature_order = feature_order
+        return vc
 
     # -------------------------------------------------------------- construction
     @classmethod
@@ -141,6 +172,9 @@ class VectorColumn:
             return self
         if self.dense is not None:
             return VectorColumn(self.size, dense=self.dense.to(device))
+        if self._values is None and self.tf_counts is not None:
+            return VectorColumn.tfidf(self.size, self.indptr.to(device), self.indices.to(device),
+                                      self.tf_counts.to(device), self.tf_scale.to(device))
         return VectorColumn(self.size, self.indptr.to(device), self.indices.to(device), self.values.to(device))
 
     def csr(self):

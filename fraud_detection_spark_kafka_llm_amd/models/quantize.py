@@ -194,12 +194,15 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
     take it automatically with scale 1."""
     if max_bins < 2 or max_bins > 256:
         raise ValueError("max_bins must be in [2, 256] (bins are one byte)")
-    indptr, idx, val = vc.csr()
+    if counts is not None and vc.dense is None:
+        indptr, idx, val = vc.indptr, vc.indices, None      # count path: the fp64 values are never read
+    else:
+        indptr, idx, val = vc.csr()
     dev = indptr.device
     N = int(indptr.numel() - 1)
     F = int(vc.size)
     idx64 = idx.to(torch.int64)
-    val64 = val.to(torch.float64)
+    val64 = val.to(torch.float64) if val is not None else None
     if counts is None and val64.numel() and bool(torch.all(val64 >= 0)) and bool(torch.all(val64 == torch.round(val64))) \
             and float(val64.max()) < 65536:
         counts = val64

@@ -33,8 +33,7 @@ def warm_tree_kernels(dev, rows: int = 1 << 16, gbdt_depth: int = 6, gbdt_max_bi
     ip, ix, v = T.featurize_score(pt, spec, want_csr=True, device=dev).csr()
     fo = feature_order(ip, ix, v, NUM_FEATURES)
     idf = torch.log((rows + 1.0) / (fo.df.double() + 1.0))
-    vc = VectorColumn(NUM_FEATURES, ip, ix, v.double() * idf[ix.long()])
-    vc.tf_counts, vc.tf_scale, vc._feature_order = v, idf, fo
+    vc = VectorColumn.tfidf(NUM_FEATURES, ip, ix, v, idf, fo)
     if gbdt_depth > 0:
         fit_gbdt(vc, y, GBDTParams(n_estimators=2, max_depth=gbdt_depth, max_bin=gbdt_max_bin), device=dev)
     if forest_depth > 0:
