@@ -13,6 +13,11 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      scores straight into pinned host memory; the host then applies the sigmoid/threshold. The
      copy of step i+1 overlaps the kernel of step i. ``value`` = dialogues/s summed over all ranks
      (weak scaling: fixed micro-batch per GPU).
+  1b. RandomForest training (BASELINE config 3) — RandomForestClassifier(500 trees, depth 5,
+     featureSubsetStrategy sqrt = ceil(sqrt(2^18)) features per node, Poisson(1) bootstrap, 32
+     bins) on the SAME row-sharded 10M-row TF-IDF features (features are fitted once and shared, as
+     train.py does; the reference refits them per model): ``rf_train_sec`` (max over ranks) =
+     quantisation to 32 bins + 500 trees with per-level histogram reduce-scatter under DP.
   3. Kafka end-to-end (BASELINE config 5) — an in-memory broker topic with 3 partitions of
      ``{"text": ...}`` JSON records -> StreamingEngine (one reader thread per partition, native JSON
      extraction into the pinned ring, GPU scoring, native output encoding, async produce, commits
@@ -48,6 +53,7 @@ from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn  # noqa: 
 from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ml.xgboost import SparkXGBClassifierModel  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ops import text as T  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order  # noqa: E402
@@ -124,14 +130,15 @@ def featurize_shard(chunks: list, dev, spec):
     return indptr, torch.cat(idxs), torch.cat(vals), torch.cat(labels)
 
 
-def warmup_training(dev, spec, params: GBDTParams) -> None:
+def warmup_training(dev, spec, params: GBDTParams, rf_depth: int = 0) -> None:
     """Untimed: the pinned H2D copy path plus a small fit through the production path
     (models/warmup.py: lazily loaded kernel code objects, cold caching allocators). Every rank runs
     it on the same rows, so under data parallelism its collectives warm RCCL too."""
     pt, _ = synth.generate(synth.SynthConfig(n=1 << 14, seed=5), device=dev, start=3 * 10**9)
     host = T.PackedText(pt.data.cpu().pin_memory(), pt.offsets.cpu().pin_memory())
     T.featurize_score(host.to(dev, non_blocking=True), spec, want_csr=True, device=dev).csr()
-    warm_tree_kernels(dev, gbdt_depth=params.max_depth, gbdt_max_bin=params.max_bin)
+    warm_tree_kernels(dev, gbdt_depth=params.max_depth, gbdt_max_bin=params.max_bin, forest_depth=rf_depth,
+                      forest_subset="sqrt")
 
 
 def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
@@ -174,6 +181,8 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000, help="GBDT training rows (total over ranks)")
     ap.add_argument("--trees", type=int, default=100)
     ap.add_argument("--depth", type=int, default=6)
+    ap.add_argument("--rf-trees", type=int, default=500, help="RandomForest trees (BASELINE config 3; 0: skip)")
+    ap.add_argument("--rf-depth", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="dialogues per GPU per streaming step")
     ap.add_argument("--pool", type=int, default=6, help="distinct pinned micro-batches per GPU")
     ap.add_argument("--depth-pipeline", type=int, default=2)
@@ -196,7 +205,7 @@ def main():
     # ------------------------------------------------------------------ 1. GBDT training
     gparams = GBDTParams(n_estimators=args.trees, max_depth=args.depth, max_bin=cfg.gbdt_max_bin)
     t0 = time.perf_counter()
-    warmup_training(dev, spec, gparams)
+    warmup_training(dev, spec, gparams, args.rf_depth if args.rf_trees > 0 else 0)
     warm_sec = time.perf_counter() - t0
     lo, hi = D.shard_range(args.rows)
     t0 = time.perf_counter()
@@ -216,7 +225,23 @@ def main():
     feat_sec = max_over_ranks(t_feat, dev)
     model = SparkXGBClassifierModel(res.trees, F, res.base_margin)
     idf_np = idf.cpu().numpy()
-    del vc, indptr, idx, counts, y, chunks, fo
+    gbdt_peak = torch.cuda.max_memory_allocated(dev)
+    del chunks
+    rf = {}
+    if args.rf_trees > 0:
+        # ------------------------------------------------------------------ 1b. RandomForest
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(dev)
+        sync_all(dev)
+        t0 = time.perf_counter()
+        forest = fit_forest(vc, y, num_trees=args.rf_trees, max_depth=args.rf_depth, max_bins=32, bootstrap=True,
+                            feature_subset="sqrt", seed=42, device=dev)
+        sync_all(dev)
+        rf = {"rf_train_sec": max_over_ranks(time.perf_counter() - t0, dev), "rf_trees": len(forest.trees),
+              "rf_depth": args.rf_depth, "rf_nodes_tree0": int(forest.trees[0].num_nodes),
+              "rf_peak_hbm_gb": max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}
+        del forest
+    del vc, indptr, idx, counts, y, fo
     torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ 2. streaming inference
@@ -295,6 +320,7 @@ def main():
         for k in ("kafka_p50_ms", "kafka_p95_ms", "kafka_p99_ms"):
             kafka[k] = max_over_ranks(kafka[k], dev)
 
+    gbdt_peak_gb = max_over_ranks(gbdt_peak / 2 ** 30, dev)
     docs = args.steps * args.batch * world
     if rank == 0:
         out = {
@@ -319,6 +345,8 @@ def main():
             "gbdt_datagen_sec_untimed": gen_sec,
             "gbdt_warmup_sec_untimed": warm_sec,
             "gbdt_nodes_tree0": res.trees[0].num_nodes,
+            "gbdt_peak_hbm_gb": gbdt_peak_gb,
+            **rf,
             "stream_accuracy": acc,
             "p50_single_dialogue_ms": p50,
             "numa_bind_rank0": numa,

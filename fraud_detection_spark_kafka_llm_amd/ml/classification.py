@@ -324,13 +324,16 @@ class RandomForestClassifier(_RFParams, Estimator):
         X, y = frame.column(self.getFeaturesCol()), frame.column(self.getLabelCol())
         from ..parallel.estimator_dp import effective_workers
 
-        nw = effective_workers(self.getOrDefault("numWorkers"), len(X))
+        from ..utils.config import default_device
+
+        dev = default_device()
+        nw = effective_workers(self.getOrDefault("numWorkers"), len(X), dev)
         if nw > 1 and not D.is_dist():
             from ..parallel.estimator_dp import fit_data_parallel
 
-            (trees, nf), _ = fit_data_parallel("rf", X, y, None, kw, nw)
+            (trees, nf), self.last_dp_report = fit_data_parallel("rf", X, y, None, kw, nw, device=dev)
         else:
-            res = fit_forest(X, y, **kw)
+            res = fit_forest(X, y, device=dev, **kw)
             trees, nf = res.trees, res.num_features
         m = RandomForestClassificationModel(trees, nf, uid=self.uid)
         m._paramMap.update({k: v for k, v in self._paramMap.items() if k != "numWorkers"})

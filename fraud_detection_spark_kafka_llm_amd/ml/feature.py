@@ -294,7 +294,7 @@ class IDFModel(HasInOut, Model):
         vc = frame.column(self.getInputCol())
         indptr, idx, val = vc.csr()
         w = self.idf_tensor(val.device)
-        out = VectorColumn(vc.size, indptr, idx, val.to(torch.float64) * w[idx.to(torch.int64)])
+        out = VectorColumn.scaled_counts(vc.size, indptr, idx, val, w)
         return frame.withColumn(self.getOutputCol(), out)
 
     def _save_data(self, path) -> None:

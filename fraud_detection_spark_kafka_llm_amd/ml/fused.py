@@ -129,7 +129,7 @@ class _Plan:
                 vc = tf_col.get()
                 ip, ix, v = vc.csr()
                 w = idf.idf_tensor(v.device)
-                return VectorColumn(vc.size, ip, ix, v.to(torch.float64) * w[ix.to(torch.int64)])
+                return VectorColumn.scaled_counts(vc.size, ip, ix, v, w)
             frame = frame.withColumn(idf.getOutputCol(), Lazy(_idf, n))
         if model is not None:
             fp = FusedPipeline(tok, rem, tf, idf, model)

@@ -105,6 +105,7 @@ class VectorColumn:
         # bin the counts directly, and ``values`` is only materialised if something asks for it
         self.tf_counts: Optional[torch.Tensor] = None
         self.tf_scale: Optional[torch.Tensor] = None
+        self.count_bins = False
         if dense is None and indptr is None:
             raise ValueError("VectorColumn needs CSR arrays or a dense matrix")
 
@@ -125,14 +126,32 @@ class VectorColumn:
 
     @classmethod
     def tfidf(cls, size: int, indptr: torch.Tensor, indices: torch.Tensor, counts: torch.Tensor,
-              idf: torch.Tensor, feature_order=None) -> "VectorColumn":
-        """A CSR TF-IDF column kept as (term counts, IDF vector): values = counts * idf[index],
-        computed lazily (SURVEY §7.5 sizing: 4 B index + 4 B count per entry instead of + 8 B)."""
+              idf: torch.Tensor, feature_order=None, count_bins: bool = True) -> "VectorColumn":
+        """A CSR TF-IDF column kept as (term counts, IDF vector): values = counts * idf[index]
+        (fp64, bitwise the eager product), computed lazily (SURVEY §7.5 sizing: 4 B index + 4 B
+        count per entry instead of + 8 B of values). ``count_bins``: the tree trainers bin the
+        integer counts (bin = min(count, maxBins - 1)); False keeps Spark's value-space binning
+        (midpoints between observed distinct values) on the materialised values."""
         vc = cls(size, indptr, indices, None)
         vc.tf_counts, vc.tf_scale = counts, idf
+        vc.count_bins = bool(count_bins)
         if feature_order is not None:
             vc._feature_order = feature_order
         return vc
+
+    @classmethod
+    def scaled_counts(cls, size: int, indptr: torch.Tensor, indices: torch.Tensor, tf: torch.Tensor,
+                      scale: torch.Tensor) -> "VectorColumn":
+        """IDF of a term-frequency column: the TF values, when they are integral counts, are kept
+        as int32 counts with the per-feature scale (lazy fp64 values, Spark value-space binning);
+        otherwise the fp64 product is materialised."""
+        if tf.numel() and tf.is_floating_point():
+            integral = bool(torch.all((tf >= 0) & (tf == torch.round(tf)) & (tf < 2 ** 31)))
+        else:
+            integral = not tf.is_floating_point()
+        if integral:
+            return cls.tfidf(size, indptr, indices, tf.to(torch.int32), scale, count_bins=False)
+        return cls(size, indptr, indices, tf.to(torch.float64) * scale[indices.to(torch.int64)])
 
     # -------------------------------------------------------------- construction
     @classmethod
@@ -174,7 +193,7 @@ class VectorColumn:
             return VectorColumn(self.size, dense=self.dense.to(device))
         if self._values is None and self.tf_counts is not None:
             return VectorColumn.tfidf(self.size, self.indptr.to(device), self.indices.to(device),
-                                      self.tf_counts.to(device), self.tf_scale.to(device))
+                                      self.tf_counts.to(device), self.tf_scale.to(device), count_bins=self.count_bins)
         return VectorColumn(self.size, self.indptr.to(device), self.indices.to(device), self.values.to(device))
 
     def csr(self):

@@ -93,16 +93,19 @@ class SparkXGBClassifier(_XGBParams, Estimator):
         from ..parallel import dist as D
         from ..parallel.estimator_dp import effective_workers
 
-        nw = effective_workers(self.getOrDefault("num_workers"), len(X))
+        from ..utils.config import default_device
+
+        dev = default_device()
+        nw = effective_workers(self.getOrDefault("num_workers"), len(X), dev)
         if nw > 1 and not D.is_dist():
             # N rank processes (one per GPU over RCCL, else gloo CPU ranks) behind the watchdog
             from dataclasses import asdict
 
             from ..parallel.estimator_dp import fit_data_parallel
 
-            (trees, nf, base, secs), _ = fit_data_parallel("gbdt", X, y, w, asdict(p), nw)
+            (trees, nf, base, secs), self.last_dp_report = fit_data_parallel("gbdt", X, y, w, asdict(p), nw, device=dev)
         else:          # one process, or already one rank of a torchrun job
-            res = fit_gbdt(X, y, p, weights=w)
+            res = fit_gbdt(X, y, p, weights=w, device=dev)
             trees, nf, base, secs = res.trees, res.num_features, res.base_margin, res.train_seconds
         m = SparkXGBClassifierModel(trees, nf, base, uid=self.uid)
         m._paramMap.update(self._paramMap)

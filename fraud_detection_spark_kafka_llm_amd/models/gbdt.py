@@ -72,12 +72,18 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
              checkpoint_dir: Optional[str] = None, checkpoint_every: int = 10, resume: bool = False) -> GBDTResult:
     """``checkpoint_dir``: write the partial ensemble every ``checkpoint_every`` trees; with
     ``resume=True`` continue from the last checkpoint there (any world size)."""
-    from ..parallel.checkpoint import EnsembleCheckpointer, maybe_fail
+    from dataclasses import asdict
+
+    from ..parallel.checkpoint import EnsembleCheckpointer, data_fingerprint, maybe_fail
 
     C = native.lib()
     coll = Collectives()
     t0 = time.perf_counter()
-    ckpt = EnsembleCheckpointer(checkpoint_dir, checkpoint_every, "gbdt") if checkpoint_dir else None
+    Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll)
+    ckpt = None
+    if checkpoint_dir:
+        ckpt = EnsembleCheckpointer(checkpoint_dir, checkpoint_every, "gbdt", data_fingerprint(vc, y, coll),
+                                    asdict(params))
     resume_state = ckpt.load() if (ckpt is not None and resume) else None
     if resume_state is not None:
         start_trees = ckpt.load_trees()
@@ -85,7 +91,6 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
         forced_base = float(resume_state["base_margin"])
     else:
         forced_base = None
-    Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll)
     dev = Q.device
     w = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float32)).to(dev)
     N = Q.n_rows
@@ -109,7 +114,11 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
         from ..ml.tree_model import ensemble_arrays
         from ..ops.sparse import score_csr
 
-        margin += score_csr(vc, ensemble_arrays(trees, "value", cmp_less=False))[:, 0]
+        # one tree at a time, in training order: each adds its fp64 leaf value to the margin
+        # exactly like tree_leaf_update did ((base + v0) + v1) + ..., so a resumed run is bitwise
+        # the uninterrupted one (one summed ensemble score would round in another order)
+        for tr in trees:
+            margin += score_csr(vc, ensemble_arrays([tr], "value", cmp_less=False))[:, 0]
     history = []
     # without per-round hooks, tree t's host table is built while tree t + 1's root level runs on
     # the GPU (its leaf values come from the device node table, bitwise the host's)

@@ -240,9 +240,11 @@ def pass_ct(np_: int, cnt: int) -> int:
 
 class FeatureShards:
     """Split-find ownership for data-parallel training: rank r owns the contiguous feature range
-    [fs[r], fs[r+1]) (balanced by bin count). ``pack_idx`` reorders a [.., TB+1] histogram into
-    [S][Bs] equal-size chunks (pad bin TB is zero) for one reduce-scatter per level; the shard's
-    own boff/nbins/zbin/fid_orig drive the split kernel on the reduced slice."""
+    [fs[r], fs[r+1]) (balanced by bin count). The histogram passes of a DP level write straight
+    into a SHARD-MAJOR buffer [S, n_build, Bs, 2] (``boff_packed``: per-feature bin offsets that
+    fold in the feature's shard), so the level's ONE reduce-scatter sends that buffer as it
+    stands, with no repacking copy; the shard's own boff/nbins/zbin/fid_orig drive the split
+    kernel on the reduced slice."""
 
     def __init__(self, Q: Quantized, S: int, rank: int):
         boff = np.asarray(Q.boff_host, dtype=np.int64)
@@ -253,17 +255,33 @@ class FeatureShards:
         lo, hi = boff[fs[:-1]], boff[fs[1:]]
         self.S, self.fs = S, fs
         self.Bs = max(1, int((hi - lo).max()))
-        idx = np.full(S * self.Bs, TB, dtype=np.int64)
-        for k in range(S):
-            idx[k * self.Bs: k * self.Bs + int(hi[k] - lo[k])] = np.arange(lo[k], hi[k])
         dev = Q.device
-        self.pack_idx = torch.from_numpy(idx).to(dev)
+        shard_of = np.searchsorted(fs[1:], np.arange(Fa + 1), side="right").clip(0, S - 1).astype(np.int64)
+        local = boff - lo[shard_of]
+        local[Fa] = 0
+        shard_of[Fa] = S                      # boff[Fa] -> the end of the buffer
+        self._shard_of = torch.from_numpy(shard_of).to(dev)
+        self._local = torch.from_numpy(local).to(dev)
+        self._boffp: dict = {}
         f0, f1 = int(fs[rank]), int(fs[rank + 1])
         self.f0, self.Fa, self.bins = f0, f1 - f0, int(hi[rank] - lo[rank])
         self.boff = (Q.boff[f0: f1 + 1] - Q.boff[f0]).contiguous()
         self.nbins = Q.nbins[f0:f1].contiguous()
         self.zbin = Q.zbin[f0:f1].contiguous()
         self.fid_orig = Q.fid_orig[f0:f1].contiguous()
+
+    def boff_packed(self, nb: int) -> torch.Tensor:
+        """[Fa+1] bin offsets into the shard-major [S * nb, Bs] histogram rows: bin b of feature f
+        (shard s) of node slot n lands in row s * nb + n at column local(f) + b, i.e. at offset
+        n * Bs + (s * nb * Bs + local(f)) + b with the kernels' hist_stride = Bs. Cached per nb."""
+        t = self._boffp.get(nb)
+        if t is None:
+            t = self._boffp[nb] = (self._shard_of * (nb * self.Bs) + self._local).contiguous()
+        return t
+
+    def target(self, nb: int, dev) -> torch.Tensor:
+        """Zeroed shard-major partial histograms [S, nb, Bs, 2] of a DP level."""
+        return torch.zeros((self.S, nb, self.Bs, 2), dtype=torch.int64, device=dev)
 
 
 def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, params, feat_thr, tree_index, Fa,
@@ -382,11 +400,13 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
         nb = len(build)
         if shards is None:
             cur_hist = torch.zeros((nl, TB, 2), dtype=torch.int64, device=dev)
-            hist_target, target_of = cur_hist, local
+            hist_target, target_of, h_boff, h_stride = cur_hist, local, Q.boff, TB
         else:
-            # local partials of the built nodes (+1 zero pad bin for the shard packing)
-            hist_target = torch.zeros((nb, TB + 1, 2), dtype=torch.int64, device=dev)
+            # local partials of the built nodes, shard-major (reduce-scattered as they stand)
+            rs_buf = shards.target(nb, dev)
+            hist_target = rs_buf.view(shards.S * nb, shards.Bs, 2)
             target_of = {n: k for k, n in enumerate(build)}
+            h_boff, h_stride = shards.boff_packed(nb), shards.Bs
         # --- small per-level arrays, one staged upload
         stg = ws.staging
         h_ns = None
@@ -437,8 +457,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                         continue
                     launches.append(functools.partial(
                         C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
-                        Q.h_row, Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, hist_target, TB, grp.bt, ct, np_,
-                        feat_mask))
+                        Q.h_row, Q.h_key, slot8, ws.rowdig, h_boff, Q.nbins, s2n, hist_target, h_stride, grp.bt, ct,
+                        np_, feat_mask))
                 if use_dense:
                     for bt in (1, 2, 4):
                         fg = C.tree_dense_fg(bt, ct if d > 0 else 1)
@@ -447,7 +467,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                             rr = dense_range_rows(Q.n_rows, gfid.numel() // fg)
                             launches.append(functools.partial(
                                 C.tree_hist_dense, Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad,
-                                gfid, gden, Q.boff, Q.nbins, s2n, hist_target, TB, Q.n_rows, rr, bt, ct, np_))
+                                gfid, gden, h_boff, Q.nbins, s2n, hist_target, h_stride, Q.n_rows, rr, bt, ct, np_))
                 ws.run_concurrent(launches)
         totals, node_ids = up[h_tot], up[h_ids]
         sub_t = tuple(up[h] for h in h_sub) if h_sub is not None else None
@@ -462,8 +482,7 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
             with tracing.span("tree.reduce_scatter"):
                 cur_hist = torch.zeros((nl, shards.bins, 2), dtype=torch.int64, device=dev)
                 if nb:
-                    packed_in = hist_target.index_select(1, shards.pack_idx).view(nb, shards.S, shards.Bs, 2)
-                    mine = coll.reduce_scatter(packed_in.permute(1, 0, 2, 3))
+                    mine = coll.reduce_scatter(rs_buf)                         # [nb, Bs, 2]
                     cur_hist.index_copy_(0, up[h_bidx], mine[:, : shards.bins].contiguous())
             if sub_t is not None:
                 C.tree_hist_subtract(prev_hist, cur_hist, *sub_t, shards.bins)
@@ -716,8 +735,11 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
         n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
         if shards is None:
             cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
-        else:   # local partials of the built nodes (+1 zero pad bin for the shard packing)
-            hist_target = torch.zeros((n_build, TB + 1, 2), dtype=torch.int64, device=dev)
+            h_boff, h_stride = Q.boff, TB
+        else:   # local partials of the built nodes, shard-major (reduce-scattered as they stand)
+            rs_buf = shards.target(n_build, dev)
+            hist_target = rs_buf.view(shards.S * n_build, shards.Bs, 2)
+            h_boff, h_stride = shards.boff_packed(n_build), shards.Bs
         # RF: exact k-of-F feature sample per open node and the level's union mask (device)
         feat_thr = feat_mask = None
         if build_all:
@@ -753,8 +775,8 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                     continue
                 launches.append(functools.partial(
                     C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
-                    Q.h_row, Q.h_key, csc_slot8, csc_dig, Q.boff, Q.nbins, s2n, hist_target, TB, grp.bt, ct, np_,
-                    feat_mask))
+                    Q.h_row, Q.h_key, csc_slot8, csc_dig, h_boff, Q.nbins, s2n, hist_target, h_stride, grp.bt, ct,
+                    np_, feat_mask))
             if use_dense:
                 for bt in (1, 2, 4):
                     fg = C.tree_dense_fg(bt, ct if d > 0 else 1)
@@ -763,12 +785,11 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                         rr = dense_range_rows(Q.n_rows, gfid.numel() // fg)
                         launches.append(functools.partial(
                             C.tree_hist_dense, Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad,
-                            gfid, gden, Q.boff, Q.nbins, s2n, hist_target, TB, Q.n_rows, rr, bt, ct, np_))
+                            gfid, gden, h_boff, Q.nbins, s2n, hist_target, h_stride, Q.n_rows, rr, bt, ct, np_))
             ws.run_concurrent(launches)
         if shards is not None:
             with tracing.span("tree.reduce_scatter"):
-                packed_in = hist_target.index_select(1, shards.pack_idx).view(n_build, shards.S, shards.Bs, 2)
-                mine = coll.reduce_scatter(packed_in.permute(1, 0, 2, 3))
+                mine = coll.reduce_scatter(rs_buf)                             # [n_build, Bs, 2]
                 cur_hist = torch.zeros((n_open, shards.bins, 2), dtype=torch.int64, device=dev)
                 cur_hist.index_copy_(0, bidx.to(torch.int64), mine[:, : shards.bins].contiguous())
         if d > 0 and not build_all:

@@ -41,6 +41,9 @@ from ..utils import tracing
 CSC_PAD = 16
 
 CHUNK = int(os.environ.get("FDX_HIST_CHUNK", 32768))   # entries per histogram work item (one wavefront)
+# A work item's int32 MFMA accumulators gain at most 128 * 128 = 2^14 per entry, so one item may
+# hold at most this many entries before a (key, column) sum could overflow (csrc/tree_kernels.hip)
+MAX_ITEM_ENTRIES = (1 << 31) // (1 << 14) - 1
 PACK_KEYS = int(os.environ.get("FDX_PACK_KEYS", 16))   # keys of a packed multi-feature item (16 = one MFMA row tile)
 
 
@@ -457,6 +460,22 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
 
+def _split_long(rows_: np.ndarray, chunk: int) -> np.ndarray:
+    """Items (start, end, ...) longer than ``chunk`` entries -> consecutive pieces of <= chunk (a
+    packed run can gather more than ``chunk`` entries inside one super-block; item sums are
+    order-free, so any split gives the same histogram)."""
+    ln = rows_[:, 1] - rows_[:, 0]
+    if rows_.shape[0] == 0 or int(ln.max()) <= chunk:
+        return rows_
+    nc = (ln + chunk - 1) // chunk
+    rep = np.repeat(np.arange(rows_.shape[0]), nc)
+    k = np.arange(rep.size) - np.repeat(np.cumsum(nc) - nc, nc)
+    out = rows_[rep].copy()
+    out[:, 0] = rows_[rep, 0] + k * chunk
+    out[:, 1] = np.minimum(out[:, 0] + chunk, rows_[rep, 1])
+    return out
+
+
 def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS, hot_density: float = HOT_DENSITY) \
         -> None:
     """Dense block, histogram CSC and work items (see the module docstring).
@@ -469,6 +488,8 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     from ..ops import native
 
     C = native.lib()
+    if not 0 < chunk <= MAX_ITEM_ENTRIES:
+        raise ValueError(f"FDX_HIST_CHUNK must be in [1, {MAX_ITEM_ENTRIES}] (int32 MFMA accumulators)")
     dev = Q.device
     colptr = Q.colptr.cpu().numpy().astype(np.int64)
     n = np.diff(colptr)
@@ -537,7 +558,7 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
         rows_ = np.stack([a.reshape(-1), e.reshape(-1), np.tile(cols[i0s], nsb), np.tile(sl2s, nsb),
                           np.tile(i1s - i0s, nsb), np.zeros(nsb * G, np.int64), np.tile(bts, nsb),
                           np.repeat(np.arange(nsb), G)], 1)
-        parts.append(rows_[rows_[:, 1] > rows_[:, 0]])
+        parts.append(_split_long(rows_[rows_[:, 1] > rows_[:, 0]], chunk))
     single = np.nonzero(~packable)[0]
     if single.size:
         a0 = hptr[:, single].reshape(-1)                   # [nsb * len(single)]

@@ -45,7 +45,7 @@ def prepare(features, labels, device=None, max_bins: int = 32, coll: Collectives
     if y.numel() != len(vc):
         raise ValueError("labels and features have different row counts")
     coll = coll or Collectives()
-    counts, scale = getattr(vc, "tf_counts", None), getattr(vc, "tf_scale", None)
+    counts, scale = (vc.tf_counts, vc.tf_scale) if getattr(vc, "count_bins", False) else (None, None)
     with tracing.span("tree.quantize"):
         Q = quantize(vc, max_bins=max_bins, counts=counts, scale=scale,
                      all_reduce_max=coll.max if coll.active else None,
@@ -88,13 +88,18 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
     RandomForestClassificationModel + ``_resume.json``); ``resume=True`` continues from it. Tree
     t depends only on (seed, t) — bootstrap weights and feature samples are counter-based — so a
     resumed forest equals an uninterrupted one at any world size."""
-    from ..parallel.checkpoint import EnsembleCheckpointer, maybe_fail
+    from ..parallel.checkpoint import EnsembleCheckpointer, data_fingerprint, maybe_fail
 
     if subsampling_rate != 1.0:
         raise NotImplementedError("subsamplingRate != 1.0 is not supported (Poisson(1) bootstrap only)")
-    ckpt = EnsembleCheckpointer(checkpoint_dir, checkpoint_every, "rf") if checkpoint_dir else None
     coll = Collectives()
-    Q, y, F, _ = prepare(features, labels, device, max_bins, coll)
+    Q, y, F, vc = prepare(features, labels, device, max_bins, coll)
+    ckpt = None
+    if checkpoint_dir:
+        shape = dict(num_trees=num_trees, max_depth=max_depth, max_bins=max_bins, min_instances=min_instances,
+                     min_info_gain=min_info_gain, bootstrap=bool(bootstrap), feature_subset=str(feature_subset),
+                     seed=int(seed), impurity=impurity, weighted=weights is not None)
+        ckpt = EnsembleCheckpointer(checkpoint_dir, checkpoint_every, "rf", data_fingerprint(vc, y, coll), shape)
     w = None
     if weights is not None:
         w = torch.as_tensor(np.asarray(weights, dtype=np.float32)).to(Q.device)

@@ -96,6 +96,8 @@ def feature_order(indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor,
     C = native.lib()
     dev = idx.device
     nnz = int(idx.numel())
+    if not counts.is_floating_point():      # integer term counts (exact in fp32 below 2^24)
+        counts = counts.to(torch.float32)
     pad = 16
     row_buf = torch.zeros(nnz + pad, dtype=torch.int32, device=dev)
     cnt_buf = torch.zeros(nnz + pad, dtype=torch.uint8, device=dev)

@@ -3,7 +3,13 @@
 Ensembles are checkpointed every ``every`` trees as a Spark-layout model directory (the same
 format as the final model, so a checkpoint is also a usable model) plus ``_resume.json``:
 ``{"kind", "trees_done", "base_margin", "num_features", "params", "world_size", "data_id"}``.
-Written atomically (``.tmp`` dir + rename) by rank 0 only; every rank reads it on resume.
+Written by rank 0 only as a complete versioned directory ``<dir>/ckpt-<trees>/``; the pointer
+file ``<dir>/LATEST`` is then replaced atomically (``os.replace``), so a process killed at any
+point (the elastic watchdog SIGKILLs survivors) leaves either the previous or the new checkpoint
+readable, never none. Older versions are pruned after the pointer moves. On load, the stored
+kind, data fingerprint (global rows / nnz / index and label sums: the same at any world size)
+and tree-shaping parameters must match the run, or it fails loudly instead of replaying a
+foreign ensemble.
 
 Because histogram sums do not depend on how rows are sharded, a run may resume with a different
 world size (elastic resume): the trees so far are replayed on each rank's new shard to rebuild
@@ -53,32 +59,89 @@ def maybe_fail(tree: int, fault: Optional[dict] = None) -> None:
         raise InjectedFault(f"injected fault at tree {tree} on rank {dist.rank()}")
 
 
+def data_fingerprint(vc, labels, coll=None) -> str:
+    """World-size-independent id of a (features, labels) training set: global row / entry counts
+    and sums of the feature indices, of the entry values' bit patterns (or term counts) and of the
+    labels, all-reduced over the data-parallel ranks (any row sharding gives the same id)."""
+    import torch
+
+    y = labels.to(torch.float64) if isinstance(labels, torch.Tensor) else torch.as_tensor(labels, dtype=torch.float64)
+    if getattr(vc, "dense", None) is not None:
+        d = vc.dense
+        parts = [d.shape[0], int((d != 0).sum()), 0, int((d.to(torch.float64) * 1024).round().sum())]
+    else:
+        cnt = getattr(vc, "tf_counts", None)
+        v = cnt.to(torch.int64) if cnt is not None else (vc.values.to(torch.float64) * 1024).round().to(torch.int64)
+        parts = [len(vc), int(vc.indices.numel()), int(vc.indices.to(torch.int64).sum()), int(v.sum())]
+    parts.append(int((y.cpu() * 1024).round().sum()))
+    t = torch.tensor(parts, dtype=torch.int64)
+    if coll is not None and coll.active:
+        dev = y.device if y.is_cuda else torch.device("cpu")
+        t = coll.sum(t.to(dev)).cpu()
+    return "-".join(str(int(x)) for x in t.tolist())
+
+
 class EnsembleCheckpointer:
-    def __init__(self, directory: str, every: int = 10, kind: str = "gbdt", data_id: str = ""):
+    """``params``: the tree-shaping parameters of the run (dict); a checkpoint whose stored
+    params differ in any key except the ensemble size (and the intercept, stored on its own)
+    is refused."""
+
+    IGNORED = ("n_estimators", "num_trees", "base_score", "deterministic")
+
+    def __init__(self, directory: str, every: int = 10, kind: str = "gbdt", data_id: str = "",
+                 params: Optional[dict] = None):
         self.dir = Path(directory)
         self.every = max(1, int(every))
         self.kind = kind
         self.data_id = data_id
+        self.params = params
+
+    def _current(self) -> Optional[Path]:
+        """Directory of the newest complete checkpoint (pointer first, then a scan, then the
+        pre-versioning single-directory layout)."""
+        ptr = self.dir / "LATEST"
+        if ptr.exists():
+            d = self.dir / ptr.read_text().strip()
+            if (d / "_resume.json").exists():
+                return d
+        if self.dir.is_dir():
+            vers = sorted((p for p in self.dir.glob("ckpt-*") if (p / "_resume.json").exists()),
+                          key=lambda p: int(p.name.split("-")[1]))
+            if vers:
+                return vers[-1]
+            if (self.dir / "_resume.json").exists():
+                return self.dir
+        return None
 
     @property
     def state_path(self) -> Path:
-        return self.dir / "_resume.json"
+        cur = self._current()
+        return (cur if cur is not None else self.dir) / "_resume.json"
 
     def load(self) -> Optional[dict]:
-        if not self.state_path.exists():
+        cur = self._current()
+        if cur is None:
             return None
-        st = json.loads(self.state_path.read_text())
+        st = json.loads((cur / "_resume.json").read_text())
+        if st.get("kind", self.kind) != self.kind:
+            raise RuntimeError(f"checkpoint {cur} holds a {st.get('kind')} ensemble, not {self.kind}")
         if self.data_id and st.get("data_id") and st["data_id"] != self.data_id:
-            raise RuntimeError(f"checkpoint {self.dir} was written for different data ({st['data_id']})")
+            raise RuntimeError(f"checkpoint {cur} was written for different data ({st['data_id']} != {self.data_id})")
+        if self.params is not None and isinstance(st.get("params"), dict):
+            diff = sorted(k for k in set(self.params) | set(st["params"])
+                          if k not in self.IGNORED and self.params.get(k) != st["params"].get(k))
+            if diff:
+                raise RuntimeError(f"checkpoint {cur} was written with different parameters: {diff}")
         return st
 
     def load_trees(self) -> list:
         st = self.load()
         if st is None:
             return []
+        from ..ml import classification, xgboost  # noqa: F401  (register the model readers)
         from ..ml.base import Params
 
-        model = Params.load(self.dir / "model")
+        model = Params.load(self._current() / "model")
         return list(model.trees)[: st["trees_done"]]
 
     def maybe_save(self, trees_done: int, trees: list, base_margin: float, num_features: int, params=None,
@@ -90,26 +153,36 @@ class EnsembleCheckpointer:
         from ..ml.classification import RandomForestClassificationModel
         from ..ml.xgboost import SparkXGBClassifierModel
 
-        tmp = self.dir.with_name(self.dir.name + ".tmp")
+        self.dir.mkdir(parents=True, exist_ok=True)
+        name = f"ckpt-{int(trees_done):06d}"
+        tmp = self.dir / (name + ".tmp")
         if tmp.exists():
             shutil.rmtree(tmp)
-        tmp.mkdir(parents=True)
+        tmp.mkdir()
         if self.kind == "gbdt":
             m = SparkXGBClassifierModel(trees, num_features, base_margin)
         else:
             m = RandomForestClassificationModel(trees, num_features)
         m.save(tmp / "model")
+        p = params if params is not None else self.params
         state = {"kind": self.kind, "trees_done": trees_done, "base_margin": base_margin,
                  "num_features": num_features, "world_size": dist.world_size(), "data_id": self.data_id,
-                 "params": asdict(params) if is_dataclass(params) else params}
-        (tmp / "_resume.json").write_text(json.dumps(state, indent=1))
-        if self.dir.exists():
-            old = self.dir.with_name(self.dir.name + ".old")
-            if old.exists():
-                shutil.rmtree(old)
-            self.dir.rename(old)
-            tmp.rename(self.dir)
-            shutil.rmtree(old)
-        else:
-            tmp.rename(self.dir)
+                 "params": asdict(p) if is_dataclass(p) else p}
+        _write_durable(tmp / "_resume.json", json.dumps(state, indent=1))
+        final = self.dir / name
+        if final.exists():
+            shutil.rmtree(final)
+        tmp.rename(final)
+        _write_durable(self.dir / "LATEST.tmp", name)
+        os.replace(self.dir / "LATEST.tmp", self.dir / "LATEST")       # the atomic switch
+        for old in self.dir.glob("ckpt-*"):
+            if old.name != name:
+                shutil.rmtree(old, ignore_errors=True)
         return True
+
+
+def _write_durable(path: Path, text: str) -> None:
+    with open(path, "w") as f:
+        f.write(text)
+        f.flush()
+        os.fsync(f.fileno())

@@ -85,6 +85,7 @@ def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
     if not _comm():
         return t
     x, moved = _on_comm_device(t.contiguous())
+    BYTES["all_reduce"] += x.numel() * x.element_size()
     dist.all_reduce(x, op=op)
     return x.to(t.device) if moved else x
 
@@ -98,16 +99,13 @@ def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
 
 
 def all_gather_var(*tensors: torch.Tensor) -> tuple:
-    """All-gather 1-D tensors of different lengths per rank; returns the concatenation."""
+    """All-gather 1-D tensors of different lengths per rank; returns the concatenation. The
+    lengths travel in one all-gather and are read back with ONE host sync."""
     if not _comm():
         return tensors
     dev = tensors[0].device
     n = torch.tensor([tensors[0].numel()], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world_size())]
-    n_c, _ = _on_comm_device(n)
-    sizes_c = [s.to(n_c.device) for s in sizes]
-    dist.all_gather(sizes_c, n_c)
-    sizes = [int(s.item()) for s in sizes_c]
+    sizes = all_gather(n).view(-1).tolist()
     m = max(sizes)
     out = []
     for t in tensors:
@@ -146,34 +144,43 @@ def shard_range(n: int, r: Optional[int] = None, w: Optional[int] = None) -> tup
     return lo, lo + base + (1 if r < extra else 0)
 
 
+# bytes this process handed to each collective (payload sizes, for the per-level DP accounting)
+BYTES = {"reduce_scatter": 0, "all_gather": 0, "all_reduce": 0}
+
+
+def reset_bytes() -> None:
+    for k in BYTES:
+        BYTES[k] = 0
+
+
 def reduce_scatter(x: torch.Tensor) -> torch.Tensor:
-    """Sum ``x`` [world, ...] over ranks and return this rank's slice [...]. RCCL
-    ``reduce_scatter_tensor`` on nccl (each rank sends (N-1)/N of the buffer instead of an
-    all-reduce's 2(N-1)/N); gloo has no reduce-scatter, so it all-reduces and slices."""
+    """Sum ``x`` [world, ...] over ranks and return this rank's slice [...] with
+    ``reduce_scatter_tensor``: each rank sends (N-1)/N of the buffer instead of an all-reduce's
+    2(N-1)/N. The same call runs on RCCL (device tensors) and on gloo (host copies), so the CPU
+    multi-process tests exercise the code path the GPUs take."""
     if not _comm():
         return x[0]
     x = x.contiguous()
-    if backend() == "nccl":
-        out = torch.empty(x.shape[1:], dtype=x.dtype, device=x.device)
-        dist.reduce_scatter_tensor(out, x)
-        return out
-    y = all_reduce_sum(x)
-    return y[rank()].clone()
+    BYTES["reduce_scatter"] += x.numel() * x.element_size()
+    xc, moved = _on_comm_device(x)
+    # flat buffers (gloo wants the concatenated form; RCCL takes either)
+    out = torch.empty(xc.numel() // xc.shape[0], dtype=xc.dtype, device=xc.device)
+    dist.reduce_scatter_tensor(out, xc.view(-1))
+    out = out.view(xc.shape[1:])
+    return out.to(x.device) if moved else out
 
 
 def all_gather(x: torch.Tensor) -> torch.Tensor:
-    """[...] on every rank -> [world, ...] (same shape on every rank)."""
+    """[...] on every rank -> [world, ...] (same shape on every rank), ``all_gather_into_tensor``
+    on RCCL and gloo alike."""
     if not _comm():
         return x.unsqueeze(0)
     x = x.contiguous()
-    if backend() == "nccl":
-        out = torch.empty((world_size(),) + tuple(x.shape), dtype=x.dtype, device=x.device)
-        dist.all_gather_into_tensor(out, x)
-        return out
+    BYTES["all_gather"] += x.numel() * x.element_size()
     xc, moved = _on_comm_device(x)
-    bufs = [torch.empty_like(xc) for _ in range(world_size())]
-    dist.all_gather(bufs, xc)
-    out = torch.stack(bufs)
+    out = torch.empty(world_size() * xc.numel(), dtype=xc.dtype, device=xc.device)
+    dist.all_gather_into_tensor(out, xc.view(-1))
+    out = out.view((world_size(),) + tuple(xc.shape))
     return out.to(x.device) if moved else out
 
 

@@ -132,7 +132,8 @@ def test_forced_collectives_at_world_one_equal_plain_path(kind, monkeypatch):
     single = _train(0, 1, kind)
     monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
     (forced, calls), = spawn(_train_counting, 1, kind, "cpu", backend="gloo")
-    assert calls["all_gather"] > 0 and calls["all_reduce"] > 0      # gloo: reduce-scatter = all-reduce + slice
+    # gloo runs the same reduce_scatter_tensor / all_gather_into_tensor calls as RCCL
+    assert calls["reduce_scatter_tensor"] > 0 and calls["all_gather_into_tensor"] > 0
     assert forced == single
 
 
@@ -145,3 +146,67 @@ def test_gpu_rccl_forced_collectives_trees_equal_non_dp(monkeypatch):
     (forced, calls), = spawn(_train_counting, 1, "gbdt", "cuda:0", backend="nccl")
     assert calls["reduce_scatter_tensor"] > 0 and calls["all_gather_into_tensor"] > 0
     assert forced == single
+
+
+def _tfidf_dataset(n=1500, F=300, seed=1):
+    """Sparse term-count rows (a few frequent terms, a long tail) + labels tied to two terms."""
+    rng = np.random.default_rng(seed)
+    p = 0.6 / (1.0 + np.arange(F)) ** 0.8
+    counts = (rng.random((n, F)) < p) * rng.integers(1, 4, (n, F))
+    y = ((counts[:, 1] > 0) ^ (counts[:, 7] >= 2)).astype(np.float32)
+    flip = rng.random(n) < 0.05
+    y[flip] = 1 - y[flip]
+    return counts, y
+
+
+def _train_tfidf(rank, world, kind):
+    """The bench shape: a TF-IDF column kept as (counts, idf), row-sharded, with the
+    collectives counted (world > 1 must run reduce_scatter_tensor itself)."""
+    import torch.distributed as td
+
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+    from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    calls = {"reduce_scatter_tensor": 0}
+    if td.is_initialized():
+        orig = td.reduce_scatter_tensor
+
+        def rs(*a, **k):
+            calls["reduce_scatter_tensor"] += 1
+            return orig(*a, **k)
+
+        td.reduce_scatter_tensor = rs
+    counts, y = _tfidf_dataset()
+    df = (counts > 0).sum(0)
+    idf = torch.from_numpy(np.log((len(y) + 1.0) / (df + 1.0)))
+    lo, hi = D.shard_range(len(y), rank, world)
+    c = counts[lo:hi]
+    nz = c != 0
+    indptr = torch.from_numpy(np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64))
+    rr, cc = np.nonzero(nz)
+    vc = VectorColumn.tfidf(counts.shape[1], indptr, torch.from_numpy(cc.astype(np.int32)),
+                            torch.from_numpy(c[rr, cc].astype(np.int32)), idf)
+    yy = torch.from_numpy(y[lo:hi])
+    D.reset_bytes()
+    if kind == "rf":
+        r = fit_forest(vc, yy, num_trees=4, max_depth=5, max_bins=32, bootstrap=True, feature_subset="sqrt", seed=42,
+                       device="cpu")
+        out = [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]
+    else:
+        r = fit_gbdt(vc, yy, GBDTParams(n_estimators=5, max_depth=6), device="cpu")
+        out = [(t.feature.tolist(), t.threshold.tolist(), t.stats[:, 0].tolist()) for t in r.trees]
+    assert not vc.values_materialized          # the count path never builds the fp64 values
+    return out, calls["reduce_scatter_tensor"], D.BYTES["reduce_scatter"]
+
+
+@pytest.mark.parametrize("kind", ["rf", "gbdt"])
+def test_tfidf_dp_world2_trees_equal_single_process(kind):
+    """BASELINE configs 3 (RF, bootstrap + sqrt features) and 4 (XGB-compatible GBDT) on the
+    bench's TF-IDF column: 2 gloo ranks running reduce_scatter_tensor give bitwise the DP=1 trees."""
+    single, _, _ = _train_tfidf(0, 1, kind)
+    outs = spawn(_train_tfidf, 2, kind, backend="gloo")
+    for trees, n_rs, nbytes in outs:
+        assert n_rs > 0 and nbytes > 0
+        assert trees == single

@@ -107,3 +107,45 @@ def test_rf_checkpoint_resume_equals_uninterrupted(tmp_path, monkeypatch):
     res = fit_forest(vc, y, checkpoint_dir=ck, checkpoint_every=2, resume=True, **kw)
     assert [(t.feature.tolist(), t.stats.tolist()) for t in res.trees] == \
         [(t.feature.tolist(), t.stats.tolist()) for t in ref.trees]
+
+
+def test_tfidf_estimator_dp_stages_counts_not_values_and_matches_single():
+    """SparkXGBClassifier(num_workers=N) on a HashingTF -> IDF column stages int32
+    indices + int32 term counts (8 B per entry) and the IDF vector through shared memory -- no
+    fp64 values -- and the ranks rebuild the values bitwise (trees equal num_workers=1)."""
+    from fraud_detection_spark_kafka_llm_amd.data import synth
+    from fraud_detection_spark_kafka_llm_amd.ml import (IDF, HashingTF, Pipeline, StopWordsRemover, TextColumn,
+                                                         Tokenizer)
+
+    pt, y = synth.generate(synth.SynthConfig(n=3000, seed=8))
+    raw = TextColumn(pt.strings())
+    df = Frame({"dialogue": raw, "clean_text": TextColumn.cleaned_from(raw), "labels": y.numpy().astype(np.float64)})
+    feats = Pipeline(stages=[Tokenizer(inputCol="clean_text", outputCol="words"),
+                             StopWordsRemover(inputCol="words", outputCol="filtered_words"),
+                             HashingTF(inputCol="filtered_words", outputCol="raw_features", numFeatures=1 << 12),
+                             IDF(inputCol="raw_features", outputCol="features")]).fit(df).transform(df)
+    col = feats.column("features")
+    assert col.tf_counts is not None and not col.values_materialized
+    kw = dict(features_col="features", label_col="labels", n_estimators=4, max_depth=4)
+    single = SparkXGBClassifier(**kw).fit(feats)
+    est = SparkXGBClassifier(num_workers=2, **kw)
+    multi = est.fit(feats)
+    assert _sig(multi) == _sig(single) and multi.base_margin == single.base_margin
+    staged = est.last_dp_report.staged_bytes
+    nnz, n = int(col.indices.numel()), len(col)
+    assert "values.npy" not in staged
+    assert staged["indices.npy"] + staged["tf_counts.npy"] <= 8 * nnz + 256
+    per_row = (staged["indptr.npy"] + staged["labels.npy"] - 256) / n
+    assert per_row <= 12.5
+
+
+def test_estimator_dp_follows_the_configured_device(monkeypatch):
+    """FDX_DEVICE=cpu keeps num_workers CPU ranks even where GPUs are visible."""
+    from fraud_detection_spark_kafka_llm_amd.parallel import estimator_dp as E
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("FDX_DEVICE", "cpu")
+    assert E.effective_workers(4, 10) == 4 and E._resolve_device(None).type == "cpu"
+    monkeypatch.setenv("FDX_DEVICE", "cuda:0")
+    assert E.effective_workers(4, 10) == 1

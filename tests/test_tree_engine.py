@@ -628,3 +628,31 @@ def test_gpu_leaf_values_device_bitwise_equal_host_table():
         if mds > 0:
             w = np.clip(w, -mds, mds)
         assert np.array_equal((p.eta * w).view(np.int64), dev.view(np.int64))
+
+
+@pytest.mark.gpu
+def test_gpu_packed_item_cannot_overflow_int32_accumulators():
+    """a packed run whose entries concentrate in one super-block used to form one work
+    item of > 131,071 entries; with a plane digit of -128 on every row each entry adds 2^14 to one
+    int32 MFMA accumulator, which overflowed. Items are now capped at ``chunk`` entries (and chunk
+    at 131,071), so the device histogram still equals the host's exact int64 sums."""
+    n, F = 280_000, 6
+    rng = np.random.default_rng(5)
+    cols = [np.arange(140_000)] + [np.sort(rng.choice(n, 3000, replace=False)) for _ in range(F - 1)]
+    rows_of = np.concatenate(cols)
+    feat_of = np.concatenate([np.full(c.size, f) for f, c in enumerate(cols)])
+    order = np.lexsort((feat_of, rows_of))
+    rows_of, feat_of = rows_of[order], feat_of[order]
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(indptr, rows_of + 1, 1)
+    vc = VectorColumn(F, torch.from_numpy(np.cumsum(indptr)), torch.from_numpy(feat_of.astype(np.int32)),
+                      torch.ones(rows_of.size, dtype=torch.float64))
+    g = np.full(n, 1.0 + 2.0 ** -22, dtype=np.float32)        # q = 2^29 + 128: plane-0 digit -128
+    h = np.full(n, 0.25, dtype=np.float32)
+    row_node = np.zeros(n, dtype=np.int32)
+    qkw = dict(chunk=131071, super_rows=140_000, hot_density=0.0)
+    hist, k, Q = _hist_on("cuda:0", vc, 16, 1, row_node, root=True, g=g, h=h, qkw=qkw)
+    q0 = np.rint(np.ldexp(g.astype(np.float64), int(k[0]))).astype(np.int64)
+    q1 = np.rint(np.ldexp(h.astype(np.float64), int(k[1]))).astype(np.int64)
+    assert int(q0[0]) % 256 == 128
+    np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, 1, q0, q1))
