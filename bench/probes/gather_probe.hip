@@ -55,7 +55,7 @@ struct Items {
   int nslots;
 };
 
-template <int MODE>   // 0 stream, 1 g8, 2 g8s1
+template <int MODE>   // 0 stream, 1 g8, 2 g8s1, 3 g16 (one 16-byte record: digits + slot)
 __global__ __launch_bounds__(256) void walk_kernel(Items it, const int32_t* __restrict__ rows, const uint8_t* __restrict__ keys,
                                                    const uint2* __restrict__ dig, const uint8_t* __restrict__ slot,
                                                    uint32_t* out) {
@@ -83,11 +83,15 @@ __global__ __launch_bounds__(256) void walk_kernel(Items it, const int32_t* __re
       nk = *reinterpret_cast<const uint32_t*>(keys + e);
     }
     acc ^= k4 ^ (uint32_t)r4.x ^ (uint32_t)r4.w;
-    if constexpr (MODE >= 1) {
+    if constexpr (MODE == 3) {
+      const uint4* rec = reinterpret_cast<const uint4*>(slot);
+      const uint4 a = rec[r4.x], b = rec[r4.y], c = rec[r4.z], d = rec[r4.w];
+      acc += a.x ^ b.y ^ c.z ^ d.w;
+    } else if constexpr (MODE >= 1) {
       const uint2 a = dig[r4.x], b = dig[r4.y], c = dig[r4.z], d = dig[r4.w];
       acc += a.x ^ b.y ^ c.x ^ d.y;
     }
-    if constexpr (MODE >= 2) {
+    if constexpr (MODE == 2) {
       acc += (uint32_t)slot[r4.x] + slot[r4.y] + slot[r4.z] + slot[r4.w];
     }
   }
@@ -230,10 +234,10 @@ int main(int argc, char** argv) {
   uint8_t* slot;
   uint32_t* out;
   CK(hipMalloc(&dig, (N + 64) * 8));
-  CK(hipMalloc(&slot, N + 64));
+  CK(hipMalloc(&slot, (N + 64) * 16));
   CK(hipMalloc(&out, 1 << 24));
   CK(hipMemset(dig, 0x5a, (N + 64) * 8));
-  CK(hipMemset(slot, 3, N + 64));
+  CK(hipMemset(slot, 3, (N + 64) * 16));
   struct Cfg { int64_t blk; int fpi; };
   const Cfg cfgs[] = {{262144, 4}, {16384, 64}, {8192, 128}};
   for (const Cfg& c : cfgs) {
@@ -254,6 +258,7 @@ int main(int argc, char** argv) {
     report("stream_xcd", time_ms([&] { walk_kernel<0><<<gx, 256>>>(ix, L.rows, L.keys, dig, slot, out); }, reps));
     report("g8_xcd", time_ms([&] { walk_kernel<1><<<gx, 256>>>(ix, L.rows, L.keys, dig, slot, out); }, reps));
     report("g8s1_xcd", time_ms([&] { walk_kernel<2><<<gx, 256>>>(ix, L.rows, L.keys, dig, slot, out); }, reps));
+    report("g16_xcd", time_ms([&] { walk_kernel<3><<<gx, 256>>>(ix, L.rows, L.keys, dig, slot, out); }, reps));
     if (c.blk <= 16384) {
       const size_t lds = (size_t)c.blk * 8;
       CK(hipFuncSetAttribute((const void*)lds_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
