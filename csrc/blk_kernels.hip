@@ -1,0 +1,291 @@
+// Row-blocked i8-MFMA histogram engine (gfx950): the blocked CSC build and the histogram pass of
+// tree.h "row-blocked histogram engine". Replaces, at the levels that build at most four node
+// slots, the gather-bound CSC passes of tree_kernels.hip: there every entry fetched its row's
+// slot byte and 8-byte digit word from global memory -- one distinct cache line per entry, since
+// a sparse feature's entries are ~700 rows apart -- which bound a level at ~3 ms on 10M rows
+// (profiles/r2s3/NOTES.md). Here a workgroup stages each 4096-row chunk's row state in LDS with
+// coalesced loads and its 16 waves look the rows up there (bench/probes/gather_probe.hip: the
+// same ~0.39 B entries take 0.34-0.45 ms with LDS-staged row state against 1.6-3.4 ms with global
+// gathers). Histogram sums stay exact integers, so every tree is bitwise the one the CSC passes
+// (and the host) grow.
+#include "hist_i8.h"
+#include "ops.h"
+#include "tree.h"
+
+#pragma clang fp contract(off)
+
+namespace fdx {
+
+namespace {
+
+// ------------------------------------------------------------------ blocked CSC build
+// largest f with colptr[f] <= e (empty features share their successor's start: the search lands
+// on the non-empty one)
+__device__ __forceinline__ int32_t feature_of_entry(const int64_t* colptr, int32_t Fa, int64_t e) {
+  int32_t lo = 0, hi = Fa;
+  while (hi - lo > 1) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (colptr[mid] <= e) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Thread t walks entries [t * ept, (t + 1) * ept) of the feature-major CSC. Consecutive entries of
+// one feature fall into the same (chunk, group) segment for runs of several entries, so the
+// segment counters take one atomic per run: pass 0 counts, pass 1 reserves the run's slots with
+// one returning atomic and writes the (row offset, key) pairs. The order of runs inside a segment
+// depends on the atomics; histogram sums are exact, so no result depends on it.
+__global__ __launch_bounds__(256) void blk_build_kernel(BlkBuildArgs a, int pass) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t e0 = t * a.entries_per_thread;
+  if (e0 >= a.nnz) return;
+  const int64_t e1 = e0 + a.entries_per_thread < a.nnz ? e0 + a.entries_per_thread : a.nnz;
+  int32_t f = feature_of_entry(a.colptr, a.Fa, e0);
+  int64_t fend = a.colptr[f + 1];
+  int64_t run_key = -1, run_start = e0;
+  int32_t run_f = f, run_len = 0;
+  auto flush = [&]() {
+    if (run_len == 0) return;
+    if (pass == 0) {
+      atomicAdd(a.counts + run_key, run_len);
+      return;
+    }
+    const int64_t base =
+        (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(a.cursor + run_key), (unsigned long long)run_len);
+    int32_t g = run_f;
+    int64_t gend = a.colptr[g + 1];
+    for (int32_t j = 0; j < run_len; ++j) {
+      const int64_t e = run_start + j;
+      while (e >= gend) gend = a.colptr[++g + 1];
+      const int64_t gb = a.boff[g] + a.csc_bin[e];
+      a.ent_row[base + j] = (uint16_t)(a.csc_row[e] % a.chunk_rows);
+      a.ent_key[base + j] = (uint8_t)(gb & (kBlkKeys - 1));
+    }
+  };
+  for (int64_t e = e0; e < e1; ++e) {
+    while (e >= fend) fend = a.colptr[++f + 1];
+    const int64_t gb = a.boff[f] + a.csc_bin[e];
+    const int64_t key = (int64_t)(a.csc_row[e] / a.chunk_rows) * a.NG + gb / kBlkKeys;
+    if (key != run_key) {
+      flush();
+      run_key = key;
+      run_start = e;
+      run_f = f;
+      run_len = 0;
+    }
+    ++run_len;
+  }
+  flush();
+}
+
+// ------------------------------------------------------------------ histogram pass
+// LDS: double-buffered chunk row state (digit words + slot bytes) shared by the workgroup, and per
+// compute wave one 256-entry step staged plane-major (keys, 8 digit planes, slots) as MFMA operands.
+template <bool ROOT>
+struct BlkShared {
+  uint2 dig[2][kBlkRows];
+  uint8_t slot[2][ROOT ? 16 : kBlkRows];
+  uint8_t key[kBlkCompute][256];
+  uint8_t pl[kBlkCompute][8][256];
+  uint8_t sl[kBlkCompute][ROOT ? 16 : 256];
+};
+
+// The staging wave: chunk c's row state -> LDS buffer buf (rows past N read as zero / no slot).
+// It waits only on its own loads, 4 x 16 B in flight per lane.
+template <bool ROOT>
+__device__ __forceinline__ void stage_chunk(const BlkHistArgs& a, BlkShared<ROOT>& sh, int buf, int32_t c, int lane) {
+  const int64_t r0 = (int64_t)c * kBlkRows;
+  const int64_t nrow = a.N - r0 < kBlkRows ? a.N - r0 : kBlkRows;
+  const uint4* src = reinterpret_cast<const uint4*>(a.rowdig + 2 * r0);     // 2 rows per uint4
+  uint4* dst = reinterpret_cast<uint4*>(&sh.dig[buf][0]);
+  if (nrow == kBlkRows) {
+    for (int k = 0; k < kBlkRows / 2; k += 4 * 64) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = src[k + u * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dst[k + u * 64 + lane] = v[u];
+    }
+    if constexpr (!ROOT) {
+      const uint4* ss = reinterpret_cast<const uint4*>(a.slot8 + r0);
+      uint4* sd = reinterpret_cast<uint4*>(&sh.slot[buf][0]);
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ss[u * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sd[u * 64 + lane] = v[u];
+    }
+  } else {
+    for (int i = lane; i < kBlkRows; i += 64) {
+      const bool in = i < nrow;
+      sh.dig[buf][i] = in ? make_uint2(a.rowdig[2 * (r0 + i)], a.rowdig[2 * (r0 + i) + 1]) : make_uint2(0u, 0u);
+      if constexpr (!ROOT) sh.slot[buf][i] = in ? a.slot8[r0 + i] : (uint8_t)0xff;
+    }
+  }
+}
+
+// One segment (chunk c, group) of one wave: 256 entries per step (4 per lane), staged
+// plane-major, then up to 4 K-steps of 64 entries on the MFMA, A = one-hot(key) over the group's
+// 4 row tiles, B = digit planes (masked to the column's slot on non-root passes).
+template <int CT, bool ROOT>
+__device__ __forceinline__ void blk_segment(const BlkHistArgs& a, BlkShared<ROOT>& sh, int buf, int wid, int lane,
+                                            int64_t e0, int64_t e1, i32x4 (&acc)[4][CT]) {
+  const int r = lane & 15, g = lane >> 4;
+  const int slot_sub = r / 8, q = r % 8;                 // NP = 4: 8 columns per slot, 2 slots per tile
+  const int64_t first = e0 & ~(int64_t)3;
+  // 32-bit offsets relative to the 4-aligned segment start: [lo, hi) live, loads clamped to last4
+  const uint16_t* rp = a.ent_row + first;
+  const uint8_t* kp = a.ent_key + first;
+  const int32_t lo = (int32_t)(e0 - first), hi = (int32_t)(e1 - first), last4 = (hi - 1) & ~3;
+#pragma unroll 1
+  for (int32_t base = 0; base < hi; base += 256) {
+    const int32_t e = base + 4 * lane;
+    const int32_t el = e < last4 ? e : last4;
+    const uint2 rr = *reinterpret_cast<const uint2*>(rp + el);
+    uint32_t keys4 = *reinterpret_cast<const uint32_t*>(kp + el);
+    uint32_t w[8];
+    uint32_t slots4 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = (int)(((j < 2 ? rr.x : rr.y) >> (16 * (j & 1))) & 0xffffu);
+      const bool live = e + j >= lo && e + j < hi;
+      const uint2 d = sh.dig[buf][row];
+      w[2 * j] = live ? d.x : 0u;
+      w[2 * j + 1] = live ? d.y : 0u;
+      if (!live) keys4 |= 0xffu << (8 * j);
+      if constexpr (!ROOT) slots4 |= (uint32_t)(live ? sh.slot[buf][row] : (uint8_t)0xff) << (8 * j);
+    }
+    *reinterpret_cast<uint32_t*>(&sh.key[wid][4 * lane]) = keys4;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        *reinterpret_cast<uint32_t*>(&sh.pl[wid][st * 4 + p][4 * lane]) =
+            gather_byte(w[st], w[2 + st], w[4 + st], w[6 + st], (uint32_t)p);
+    if constexpr (!ROOT) *reinterpret_cast<uint32_t*>(&sh.sl[wid][4 * lane]) = slots4;
+    lds_sync();
+    const int32_t span = hi - base < 256 ? hi - base : 256;
+    const int nks = (span + 63) >> 6;
+#pragma unroll 1
+    for (int ks = 0; ks < nks; ++ks) {
+      const int k0 = ks * 64 + 16 * g;
+      const uint4 kv = *reinterpret_cast<const uint4*>(&sh.key[wid][k0]);
+      const uint4 dv = *reinterpret_cast<const uint4*>(&sh.pl[wid][q][k0]);
+      const uint4 k7 = make_uint4(kv.x & 0x7f7f7f7fu, kv.y & 0x7f7f7f7fu, kv.z & 0x7f7f7f7fu, kv.w & 0x7f7f7f7fu);
+      i32x4 B[CT];
+      if constexpr (ROOT) {
+        B[0] = i32x4{(int)dv.x, (int)dv.y, (int)dv.z, (int)dv.w};
+      } else {
+        const uint4 sv = *reinterpret_cast<const uint4*>(&sh.sl[wid][k0]);
+        slot_masked_b<CT, 4>(dv, sv, slot_sub, B);
+      }
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        const uint32_t nk = ~((uint32_t)(r + 16 * bt) * 0x01010101u);
+        const i32x4 A = {(int)onehot7(k7.x, nk), (int)onehot7(k7.y, nk), (int)onehot7(k7.z, nk), (int)onehot7(k7.w, nk)};
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[ct], acc[bt][ct], 0, 0, 0);
+      }
+    }
+    lds_sync();
+  }
+}
+
+// acc of one group -> int64 histogram (exact: -128 * plane sums recombined over the 4 planes),
+// then zeroed. Lanes q % 4 == 0 hold a (slot, statistic) column's recombined sums.
+template <int CT>
+__device__ __forceinline__ void blk_flush(const BlkHistArgs& a, int grp, int lane, i32x4 (&acc)[4][CT]) {
+  const int r = lane & 15, g = lane >> 4;
+  const int slot_sub = r / 8, q = r % 8, stat = q / 4;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int slot = ct * 2 + slot_sub;
+    const int node = slot < a.nslots ? a.slot_node[slot] : -1;
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int32_t s = -(acc[bt][ct][i] >> 7);
+        const int32_t s1 = __shfl_down(s, 1, kWave), s2 = __shfl_down(s, 2, kWave), s3 = __shfl_down(s, 3, kWave);
+        const int64_t v = (int64_t)s + (int64_t)s1 * 256 + (int64_t)s2 * 65536 + (int64_t)s3 * 16777216;
+        const int64_t bin = (int64_t)grp * kBlkKeys + 16 * bt + 4 * g + i;
+        if ((q & 3) == 0 && v != 0 && node >= 0 && bin < a.TB) {
+          int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + blk_bin_offset(a, bin)) * 2 + stat;
+          atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
+        }
+        acc[bt][ct][i] = 0;
+      }
+  }
+}
+
+// GW groups per compute wave (GW * CT * 16 accumulator registers <= 128). The accumulators are
+// flushed once, at the end: the planner keeps every workgroup's chunk range short enough that no
+// int32 (key, column) sum can overflow (models/quantize.py blk_plan; an in-loop flush made the
+// compiler spill the accumulators).
+template <int CT, bool ROOT, int GW>
+__global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a) {
+  __shared__ BlkShared<ROOT> sh;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool stager = wid == kBlkCompute;
+  const int w = blockIdx.x;
+  if (w >= a.n_wg) return;
+  const int band = a.wg_band[w];
+  const int32_t c0 = a.wg_c0[w], c1 = a.wg_c1[w];
+  int grp[GW];
+#pragma unroll
+  for (int j = 0; j < GW; ++j)
+    grp[j] = stager ? -1 : a.band_groups[((int64_t)band * kBlkCompute + wid) * a.gw + j];
+  i32x4 acc[GW][4][CT];
+#pragma unroll
+  for (int j = 0; j < GW; ++j)
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[j][bt][ct] = i32x4{0, 0, 0, 0};
+  if (stager) stage_chunk<ROOT>(a, sh, 0, c0, lane);
+  __syncthreads();
+  for (int32_t c = c0; c < c1; ++c) {
+    const int buf = (c - c0) & 1;
+    const bool more = c + 1 < c1;
+    if (stager) {
+      if (more) stage_chunk<ROOT>(a, sh, buf ^ 1, c + 1, lane);   // overlaps the compute waves' chunk c
+    } else {
+      const int64_t* sg = a.seg + (int64_t)c * a.NG;
+#pragma unroll
+      for (int j = 0; j < GW; ++j) {
+        if (grp[j] < 0) continue;
+        const int64_t e0 = sg[grp[j]], e1 = sg[grp[j] + 1];
+        if (e1 > e0) blk_segment<CT, ROOT>(a, sh, buf, wid, lane, e0, e1, acc[j]);
+      }
+    }
+    __syncthreads();
+  }
+  if (!stager) {
+#pragma unroll
+    for (int j = 0; j < GW; ++j)
+      if (grp[j] >= 0) blk_flush<CT>(a, grp[j], lane, acc[j]);
+  }
+}
+
+}  // namespace
+
+void launch_blk_build(const BlkBuildArgs& a, int pass, hipStream_t s) {
+  if (a.nnz <= 0) return;
+  const int64_t threads = (a.nnz + a.entries_per_thread - 1) / a.entries_per_thread;
+  hipLaunchKernelGGL(blk_build_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a, pass);
+}
+
+int blk_groups_per_wave(int ct) { return ct <= 1 ? kBlkGroupsMax : kBlkGroupsMax / 2; }
+
+void launch_hist_blk(const BlkHistArgs& a, int ct, hipStream_t s) {
+  if (a.n_wg <= 0) return;
+  const bool root = a.slot8 == nullptr;
+  const dim3 grid(a.n_wg), block(kBlkWaves * 64);
+  if (root) hipLaunchKernelGGL((hist_blk_kernel<1, true, kBlkGroupsMax>), grid, block, 0, s, a);
+  else if (ct == 1) hipLaunchKernelGGL((hist_blk_kernel<1, false, kBlkGroupsMax>), grid, block, 0, s, a);
+  else if (ct == 2) hipLaunchKernelGGL((hist_blk_kernel<2, false, kBlkGroupsMax / 2>), grid, block, 0, s, a);
+}
+
+}  // namespace fdx

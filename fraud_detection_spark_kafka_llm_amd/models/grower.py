@@ -56,6 +56,11 @@ DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
 # streams: they add into disjoint feature ranges with integer atomics, so the order is free and
 # the kernels fill each other's tails
 HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
+# levels that build at most BLK_MAX_SLOTS node slots (GBDT) take the row-blocked histogram pass
+# (models/quantize.BlockedCSC, csrc/blk_kernels.hip): row state staged in LDS per 4096-row chunk
+# instead of a global gather per entry (FDX_BLK=0: the CSC / dense passes at every level)
+BLK = os.environ.get("FDX_BLK", "1") != "0"
+BLK_MAX_SLOTS = 4
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 
@@ -264,6 +269,7 @@ class FeatureShards:
         self._local = torch.from_numpy(local).to(dev)
         self._boffp: dict = {}
         f0, f1 = int(fs[rank]), int(fs[rank + 1])
+        self.bin_lo = torch.from_numpy(np.append(lo, boff[-1]).astype(np.int64)).to(dev)   # [S + 1] shard bin starts
         self.f0, self.Fa, self.bins = f0, f1 - f0, int(hi[rank] - lo[rank])
         self.boff = (Q.boff[f0: f1 + 1] - Q.boff[f0]).contiguous()
         self.nbins = Q.nbins[f0:f1].contiguous()
@@ -770,6 +776,19 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 s2n = torch.arange(n_build, dtype=torch.int32, device=dev)
             ct = pass_ct(np_, n_build)
             launches = []
+            if BLK and np_ == 4 and not build_all and n_build <= BLK_MAX_SLOTS:
+                # row-blocked pass: every feature (hot ones included) in one launch
+                blk = Q.blocked()
+                root = d == 0 or n_build == 1
+                ct_b = 1 if root else ct
+                plan = blk.plan(int(C.tree_blk_gw(ct_b)))
+                dig = ws.rowdig if d == 0 else csc_dig
+                launches.append(functools.partial(
+                    C.tree_hist_blk, blk.ent_row, blk.ent_key, blk.seg, blk.NG, dig, None if root else slot8,
+                    *plan, int(C.tree_blk_gw(ct_b)), s2n, hist_target, TB, ct_b,
+                    shards.bin_lo if shards is not None else None,
+                    n_build * shards.Bs if shards is not None else 0))
+                sel_groups, use_dense = [], False
             for grp in sel_groups:
                 if grp.num_items == 0:
                     continue
