@@ -402,8 +402,8 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
 }
 
 // Blocked CSC build (tree.h "row-blocked histogram engine"): pass 0 adds the entry count of every
-// (chunk, group) segment to counts [n_chunks * NG] (int32); pass 1 writes ent_row / ent_key at the
-// segment cursors [n_chunks * NG] (int64, advanced).
+// (chunk, 16-bin tile) sub-segment to counts [n_chunks * NG * 4] (int32); pass 1 writes ent_row /
+// ent_key at the sub-segment cursors [n_chunks * NG * 4] (int64, advanced).
 void blk_build(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& colptr, const Tensor& boff,
                int64_t chunk_rows, int64_t NG, int64_t pass, const optional<Tensor>& counts,
                const optional<Tensor>& cursor, const optional<Tensor>& ent_row, const optional<Tensor>& ent_key) {
@@ -477,7 +477,7 @@ void hist_blk(const Tensor& ent_row, const Tensor& ent_key, const Tensor& seg, i
   FDX_CHECK(!slot8_t || (slot8_t->numel() >= N && reinterpret_cast<uintptr_t>(slot8_t->data_ptr()) % 16 == 0),
             "slot8 must cover the rows, 16-byte aligned");
   const int64_t n_chunks = (N + fdx::kBlkRows - 1) / fdx::kBlkRows;
-  FDX_CHECK(seg.numel() == n_chunks * NG + 1, "seg must be [n_chunks * NG + 1]");
+  FDX_CHECK(seg.numel() == n_chunks * NG * fdx::kBlkTiles + 1, "seg must be [n_chunks * NG * 4 + 1]");
   FDX_CHECK(readable_tail(ent_row, 4) && readable_tail(ent_key, 4), "entry arrays need 4 readable padding entries");
   FDX_CHECK(reinterpret_cast<uintptr_t>(ent_row.data_ptr()) % 8 == 0 &&
                 reinterpret_cast<uintptr_t>(ent_key.data_ptr()) % 4 == 0, "entry arrays alignment");

@@ -32,7 +32,7 @@ __device__ __forceinline__ int32_t feature_of_entry(const int64_t* colptr, int32
 }
 
 // Thread t walks entries [t * ept, (t + 1) * ept) of the feature-major CSC. Consecutive entries of
-// one feature fall into the same (chunk, group) segment for runs of several entries, so the
+// one feature fall into the same (chunk, 16-bin tile) sub-segment for runs of several entries, so the
 // segment counters take one atomic per run: pass 0 counts, pass 1 reserves the run's slots with
 // one returning atomic and writes the (row offset, key) pairs. The order of runs inside a segment
 // depends on the atomics; histogram sums are exact, so no result depends on it.
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void blk_build_kernel(BlkBuildArgs a, int pass
   for (int64_t e = e0; e < e1; ++e) {
     while (e >= fend) fend = a.colptr[++f + 1];
     const int64_t gb = a.boff[f] + a.csc_bin[e];
-    const int64_t key = (int64_t)(a.csc_row[e] / a.chunk_rows) * a.NG + gb / kBlkKeys;
+    const int64_t key = (int64_t)(a.csc_row[e] / a.chunk_rows) * (kBlkTiles * a.NG) + gb / 16;
     if (key != run_key) {
       flush();
       run_key = key;
@@ -80,6 +80,11 @@ __global__ __launch_bounds__(256) void blk_build_kernel(BlkBuildArgs a, int pass
 }
 
 // ------------------------------------------------------------------ histogram pass
+// Plane rows of the staged step are 288 B apart (256 + 32): the 16 lanes of one ds_read_b128
+// group read planes q = 0..7 at K offsets 16 g, and at a 256-B stride all 8 planes hit the same
+// banks (8-way conflicts, measured 70 % of the LDS cycles); at 288 B = 72 dwords the 16 reads of
+// a lane group start at 8 q + 4 g (mod 64) dwords: 16 distinct 4-bank blocks.
+constexpr int kBlkPlaneStride = 288;
 // LDS: double-buffered chunk row state (digit words + slot bytes) shared by the workgroup, and per
 // compute wave one 256-entry step staged plane-major (keys, 8 digit planes, slots) as MFMA operands.
 template <bool ROOT>
@@ -87,34 +92,36 @@ struct BlkShared {
   uint2 dig[2][kBlkRows];
   uint8_t slot[2][ROOT ? 16 : kBlkRows];
   uint8_t key[kBlkCompute][256];
-  uint8_t pl[kBlkCompute][8][256];
+  uint8_t pl[kBlkCompute][8][kBlkPlaneStride];
   uint8_t sl[kBlkCompute][ROOT ? 16 : 256];
 };
 
 // The staging wave: chunk c's row state -> LDS buffer buf (rows past N read as zero / no slot).
-// It waits only on its own loads, 4 x 16 B in flight per lane.
+// All 36 KB of the chunk are requested at once (36 x 16 B per lane in registers: the staging wave
+// holds no accumulators), so a chunk costs one memory latency, not one per 4 KB.
 template <bool ROOT>
 __device__ __forceinline__ void stage_chunk(const BlkHistArgs& a, BlkShared<ROOT>& sh, int buf, int32_t c, int lane) {
   const int64_t r0 = (int64_t)c * kBlkRows;
   const int64_t nrow = a.N - r0 < kBlkRows ? a.N - r0 : kBlkRows;
-  const uint4* src = reinterpret_cast<const uint4*>(a.rowdig + 2 * r0);     // 2 rows per uint4
-  uint4* dst = reinterpret_cast<uint4*>(&sh.dig[buf][0]);
   if (nrow == kBlkRows) {
-    for (int k = 0; k < kBlkRows / 2; k += 4 * 64) {
-      uint4 v[4];
+    constexpr int KD = kBlkRows / 2 / 64;                      // uint4 (2 rows) per lane: 32
+    const uint4* src = reinterpret_cast<const uint4*>(a.rowdig + 2 * r0);
+    uint4* dst = reinterpret_cast<uint4*>(&sh.dig[buf][0]);
+    uint4 v[KD];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = src[k + u * 64 + lane];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) dst[k + u * 64 + lane] = v[u];
-    }
+    for (int u = 0; u < KD; ++u) v[u] = src[u * 64 + lane];
+    uint4 sv[4];
     if constexpr (!ROOT) {
       const uint4* ss = reinterpret_cast<const uint4*>(a.slot8 + r0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sv[u] = ss[u * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < KD; ++u) dst[u * 64 + lane] = v[u];
+    if constexpr (!ROOT) {
       uint4* sd = reinterpret_cast<uint4*>(&sh.slot[buf][0]);
-      uint4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = ss[u * 64 + lane];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) sd[u * 64 + lane] = v[u];
+      for (int u = 0; u < 4; ++u) sd[u * 64 + lane] = sv[u];
     }
   } else {
     for (int i = lane; i < kBlkRows; i += 64) {
@@ -125,71 +132,70 @@ __device__ __forceinline__ void stage_chunk(const BlkHistArgs& a, BlkShared<ROOT
   }
 }
 
-// One segment (chunk c, group) of one wave: 256 entries per step (4 per lane), staged
-// plane-major, then up to 4 K-steps of 64 entries on the MFMA, A = one-hot(key) over the group's
+// One 256-entry step of a segment [e0, e1): 4 entries per lane, their row state looked up in the
+// chunk's LDS image and staged plane-major (keys, 8 digit planes, slots) for the K-steps.
+template <bool ROOT>
+__device__ __forceinline__ void blk_stage_step(BlkShared<ROOT>& sh, int buf, int wid, int lane, int32_t base,
+                                               int32_t e0, int32_t e1, uint2 rr, uint32_t keys4) {
+  const int32_t e = base + 4 * lane;
+  uint32_t w[8];
+  uint32_t slots4 = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (int)(((j < 2 ? rr.x : rr.y) >> (16 * (j & 1))) & 0xffffu);
+    const bool live = e + j >= e0 && e + j < e1;
+    const uint2 d = sh.dig[buf][row];
+    w[2 * j] = live ? d.x : 0u;
+    w[2 * j + 1] = live ? d.y : 0u;
+    if (!live) keys4 |= 0xffu << (8 * j);
+    if constexpr (!ROOT) slots4 |= (uint32_t)(live ? sh.slot[buf][row] : (uint8_t)0xff) << (8 * j);
+  }
+  *reinterpret_cast<uint32_t*>(&sh.key[wid][4 * lane]) = keys4;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      *reinterpret_cast<uint32_t*>(&sh.pl[wid][st * 4 + p][4 * lane]) =
+          gather_byte(w[st], w[2 + st], w[4 + st], w[6 + st], (uint32_t)p);
+  if constexpr (!ROOT) *reinterpret_cast<uint32_t*>(&sh.sl[wid][4 * lane]) = slots4;
+}
+
+// The K-steps of one staged step into one group's accumulators: A = one-hot(key) over the group's
 // 4 row tiles, B = digit planes (masked to the column's slot on non-root passes).
+// Entries of a segment are ordered by 16-bin tile (tile t = entries [t_t, t_{t+1}) relative to
+// the segment start), so each 64-entry K-step multiplies only the 1-2 tiles it actually holds.
 template <int CT, bool ROOT>
-__device__ __forceinline__ void blk_segment(const BlkHistArgs& a, BlkShared<ROOT>& sh, int buf, int wid, int lane,
-                                            int64_t e0, int64_t e1, i32x4 (&acc)[4][CT]) {
+__device__ __forceinline__ void blk_ksteps(BlkShared<ROOT>& sh, int wid, int lane, int32_t base, int32_t n,
+                                           int32_t t1, int32_t t2, int32_t t3, i32x4 (&acc)[4][CT]) {
   const int r = lane & 15, g = lane >> 4;
   const int slot_sub = r / 8, q = r % 8;                 // NP = 4: 8 columns per slot, 2 slots per tile
-  const int64_t first = e0 & ~(int64_t)3;
-  // 32-bit offsets relative to the 4-aligned segment start: [lo, hi) live, loads clamped to last4
-  const uint16_t* rp = a.ent_row + first;
-  const uint8_t* kp = a.ent_key + first;
-  const int32_t lo = (int32_t)(e0 - first), hi = (int32_t)(e1 - first), last4 = (hi - 1) & ~3;
+  const int32_t span = n - base < 256 ? n - base : 256;
+  const int nks = (span + 63) >> 6;
 #pragma unroll 1
-  for (int32_t base = 0; base < hi; base += 256) {
-    const int32_t e = base + 4 * lane;
-    const int32_t el = e < last4 ? e : last4;
-    const uint2 rr = *reinterpret_cast<const uint2*>(rp + el);
-    uint32_t keys4 = *reinterpret_cast<const uint32_t*>(kp + el);
-    uint32_t w[8];
-    uint32_t slots4 = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = (int)(((j < 2 ? rr.x : rr.y) >> (16 * (j & 1))) & 0xffffu);
-      const bool live = e + j >= lo && e + j < hi;
-      const uint2 d = sh.dig[buf][row];
-      w[2 * j] = live ? d.x : 0u;
-      w[2 * j + 1] = live ? d.y : 0u;
-      if (!live) keys4 |= 0xffu << (8 * j);
-      if constexpr (!ROOT) slots4 |= (uint32_t)(live ? sh.slot[buf][row] : (uint8_t)0xff) << (8 * j);
+  for (int ks = 0; ks < nks; ++ks) {
+    const int32_t lo = base + 64 * ks > 0 ? base + 64 * ks : 0;          // first live entry (segment-relative)
+    const int32_t hi = (base + 64 * ks + 64 < n ? base + 64 * ks + 64 : n) - 1;   // last live entry
+    const int tlo = (lo >= t1) + (lo >= t2) + (lo >= t3), thi = (hi >= t1) + (hi >= t2) + (hi >= t3);
+    const int k0 = ks * 64 + 16 * g;
+    const uint4 kv = *reinterpret_cast<const uint4*>(&sh.key[wid][k0]);
+    const uint4 dv = *reinterpret_cast<const uint4*>(&sh.pl[wid][q][k0]);
+    const uint4 k7 = make_uint4(kv.x & 0x7f7f7f7fu, kv.y & 0x7f7f7f7fu, kv.z & 0x7f7f7f7fu, kv.w & 0x7f7f7f7fu);
+    i32x4 B[CT];
+    if constexpr (ROOT) {
+      B[0] = i32x4{(int)dv.x, (int)dv.y, (int)dv.z, (int)dv.w};
+    } else {
+      const uint4 sv = *reinterpret_cast<const uint4*>(&sh.sl[wid][k0]);
+      slot_masked_b<CT, 4>(dv, sv, slot_sub, B);
     }
-    *reinterpret_cast<uint32_t*>(&sh.key[wid][4 * lane]) = keys4;
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+    for (int bt = 0; bt < 4; ++bt) {
+      if (bt < tlo || bt > thi) continue;                 // wave-uniform
+      const uint32_t nk = ~((uint32_t)(r + 16 * bt) * 0x01010101u);
+      const i32x4 A = {(int)onehot7(k7.x, nk), (int)onehot7(k7.y, nk), (int)onehot7(k7.z, nk), (int)onehot7(k7.w, nk)};
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-        *reinterpret_cast<uint32_t*>(&sh.pl[wid][st * 4 + p][4 * lane]) =
-            gather_byte(w[st], w[2 + st], w[4 + st], w[6 + st], (uint32_t)p);
-    if constexpr (!ROOT) *reinterpret_cast<uint32_t*>(&sh.sl[wid][4 * lane]) = slots4;
-    lds_sync();
-    const int32_t span = hi - base < 256 ? hi - base : 256;
-    const int nks = (span + 63) >> 6;
-#pragma unroll 1
-    for (int ks = 0; ks < nks; ++ks) {
-      const int k0 = ks * 64 + 16 * g;
-      const uint4 kv = *reinterpret_cast<const uint4*>(&sh.key[wid][k0]);
-      const uint4 dv = *reinterpret_cast<const uint4*>(&sh.pl[wid][q][k0]);
-      const uint4 k7 = make_uint4(kv.x & 0x7f7f7f7fu, kv.y & 0x7f7f7f7fu, kv.z & 0x7f7f7f7fu, kv.w & 0x7f7f7f7fu);
-      i32x4 B[CT];
-      if constexpr (ROOT) {
-        B[0] = i32x4{(int)dv.x, (int)dv.y, (int)dv.z, (int)dv.w};
-      } else {
-        const uint4 sv = *reinterpret_cast<const uint4*>(&sh.sl[wid][k0]);
-        slot_masked_b<CT, 4>(dv, sv, slot_sub, B);
-      }
-#pragma unroll
-      for (int bt = 0; bt < 4; ++bt) {
-        const uint32_t nk = ~((uint32_t)(r + 16 * bt) * 0x01010101u);
-        const i32x4 A = {(int)onehot7(k7.x, nk), (int)onehot7(k7.y, nk), (int)onehot7(k7.z, nk), (int)onehot7(k7.w, nk)};
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-          acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[ct], acc[bt][ct], 0, 0, 0);
-      }
+      for (int ct = 0; ct < CT; ++ct)
+        acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[ct], acc[bt][ct], 0, 0, 0);
     }
-    lds_sync();
   }
 }
 
@@ -220,10 +226,64 @@ __device__ __forceinline__ void blk_flush(const BlkHistArgs& a, int grp, int lan
   }
 }
 
+// A compute wave's walk over its (chunk, group, 256-entry step) sequence. The entries of the next
+// step are loaded while the current one is staged and multiplied (one load in flight across every
+// step, chunk boundaries included), so a short segment does not expose a memory latency per step.
+constexpr int kBlkAhead = 4;       // 256-entry steps of entry loads in flight per compute wave
+
+struct BlkCursor {
+  int32_t c;          // chunk (>= c1: done)
+  int j;              // group slot of the wave
+  int64_t e0;         // segment start
+  int32_t n;          // segment length
+  int32_t base;       // step start relative to e0 (e0 + base is 4-aligned; may be -1 .. -3)
+  int32_t t1, t2, t3; // tile starts relative to e0
+};
+
+__device__ __forceinline__ void blk_seek(const BlkHistArgs& a, const int* grp, int gw, int32_t c1, BlkCursor& k) {
+  // from (c, j) onwards, the first non-empty segment
+  while (k.c < c1) {
+    while (k.j < gw) {
+      const int g = grp[k.j];
+      if (g >= 0) {
+        const int64_t* sg = a.seg + ((int64_t)k.c * a.NG + g) * kBlkTiles;
+        k.e0 = sg[0];
+        k.n = (int32_t)(sg[4] - k.e0);
+        if (k.n > 0) {
+          k.base = -(int32_t)(k.e0 & 3);
+          k.t1 = (int32_t)(sg[1] - k.e0);
+          k.t2 = (int32_t)(sg[2] - k.e0);
+          k.t3 = (int32_t)(sg[3] - k.e0);
+          return;
+        }
+      }
+      ++k.j;
+    }
+    ++k.c;
+    k.j = 0;
+  }
+}
+
+__device__ __forceinline__ void blk_advance(const BlkHistArgs& a, const int* grp, int gw, int32_t c1, BlkCursor& k) {
+  k.base += 256;
+  if (k.base < k.n) return;
+  ++k.j;
+  blk_seek(a, grp, gw, c1, k);
+}
+
+__device__ __forceinline__ void blk_load(const BlkHistArgs& a, const BlkCursor& k, int lane, uint2& rr, uint32_t& keys4) {
+  const int32_t e = k.base + 4 * lane;
+  const int64_t abs_last4 = (k.e0 + k.n - 1) & ~(int64_t)3;       // last 4-group holding an entry
+  const int64_t abs_e = k.e0 + e;
+  const int64_t el = abs_e < abs_last4 ? abs_e : abs_last4;
+  rr = *reinterpret_cast<const uint2*>(a.ent_row + el);
+  keys4 = *reinterpret_cast<const uint32_t*>(a.ent_key + el);
+}
+
 // GW groups per compute wave (GW * CT * 16 accumulator registers <= 128). The accumulators are
 // flushed once, at the end: the planner keeps every workgroup's chunk range short enough that no
-// int32 (key, column) sum can overflow (models/quantize.py blk_plan; an in-loop flush made the
-// compiler spill the accumulators).
+// int32 (key, column) sum can overflow (models/quantize.py BlockedCSC.plan; an in-loop flush made
+// the compiler spill the accumulators).
 template <int CT, bool ROOT, int GW>
 __global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a) {
   __shared__ BlkShared<ROOT> sh;
@@ -244,29 +304,68 @@ __global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a)
     for (int bt = 0; bt < 4; ++bt)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[j][bt][ct] = i32x4{0, 0, 0, 0};
-  if (stager) stage_chunk<ROOT>(a, sh, 0, c0, lane);
-  __syncthreads();
+  if (stager) {
+    stage_chunk<ROOT>(a, sh, 0, c0, lane);
+    __syncthreads();
+    for (int32_t c = c0; c < c1; ++c) {
+      if (c + 1 < c1) stage_chunk<ROOT>(a, sh, (c - c0 + 1) & 1, c + 1, lane);   // overlaps chunk c
+      __syncthreads();
+    }
+    return;
+  }
+  // kBlkAhead steps of entries in flight: q[0] is the step being processed
+  BlkCursor q[kBlkAhead];
+  uint2 rq[kBlkAhead];
+  uint32_t kq[kBlkAhead];
+  q[0] = BlkCursor{c0, 0, 0, 0, 0, 0, 0, 0};
+  blk_seek(a, grp, GW, c1, q[0]);
+#pragma unroll
+  for (int i = 0; i < kBlkAhead; ++i) {
+    if (i > 0) {
+      q[i] = q[i - 1];
+      if (q[i].c < c1) blk_advance(a, grp, GW, c1, q[i]);
+    }
+    rq[i] = make_uint2(0u, 0u);
+    kq[i] = 0;
+    if (q[i].c < c1) blk_load(a, q[i], lane, rq[i], kq[i]);
+  }
+  __syncthreads();                                         // chunk c0 staged
   for (int32_t c = c0; c < c1; ++c) {
     const int buf = (c - c0) & 1;
-    const bool more = c + 1 < c1;
-    if (stager) {
-      if (more) stage_chunk<ROOT>(a, sh, buf ^ 1, c + 1, lane);   // overlaps the compute waves' chunk c
-    } else {
-      const int64_t* sg = a.seg + (int64_t)c * a.NG;
+    while (q[0].c == c) {
+      const BlkCursor now = q[0];
+      const uint2 rr_now = rq[0];
+      const uint32_t k_now = kq[0];
 #pragma unroll
-      for (int j = 0; j < GW; ++j) {
-        if (grp[j] < 0) continue;
-        const int64_t e0 = sg[grp[j]], e1 = sg[grp[j] + 1];
-        if (e1 > e0) blk_segment<CT, ROOT>(a, sh, buf, wid, lane, e0, e1, acc[j]);
+      for (int i = 0; i + 1 < kBlkAhead; ++i) {
+        q[i] = q[i + 1];
+        rq[i] = rq[i + 1];
+        kq[i] = kq[i + 1];
       }
+      q[kBlkAhead - 1] = q[kBlkAhead - 2 >= 0 ? kBlkAhead - 2 : 0];
+      if (q[kBlkAhead - 1].c < c1) {
+        blk_advance(a, grp, GW, c1, q[kBlkAhead - 1]);
+        if (q[kBlkAhead - 1].c < c1) blk_load(a, q[kBlkAhead - 1], lane, rq[kBlkAhead - 1], kq[kBlkAhead - 1]);
+      }
+      blk_stage_step<ROOT>(sh, buf, wid, lane, now.base, 0, now.n, rr_now, k_now);
+      lds_sync();
+      switch (now.j) {
+#define FDX_BLK_CASE(J) \
+  case J:               \
+    if constexpr (J < GW) blk_ksteps<CT, ROOT>(sh, wid, lane, now.base, now.n, now.t1, now.t2, now.t3, acc[J]); \
+    break;
+        FDX_BLK_CASE(0) FDX_BLK_CASE(1) FDX_BLK_CASE(2) FDX_BLK_CASE(3)
+        FDX_BLK_CASE(4) FDX_BLK_CASE(5) FDX_BLK_CASE(6) FDX_BLK_CASE(7)
+#undef FDX_BLK_CASE
+        default: break;
+      }
+      lds_sync();
     }
-    __syncthreads();
+    __syncthreads();                                       // chunk c done; chunk c + 1 staged
   }
-  if (!stager) {
 #pragma unroll
-    for (int j = 0; j < GW; ++j)
-      if (grp[j] >= 0) blk_flush<CT>(a, grp[j], lane, acc[j]);
-  }
+  for (int j = 0; j < GW; ++j)
+    if (grp[j] >= 0) blk_flush<CT>(a, grp[j], lane, acc[j]);
 }
 
 }  // namespace

@@ -115,7 +115,9 @@ struct HistArgs {
 // Blocked CSC ("BCSC", models/quantize.py build_blocked): the rows are cut into chunks of
 // kBlkRows and the global bin space (all features' bins concatenated, boff) into groups of
 // kBlkKeys consecutive bins. The entries of chunk c and group g form segment c * NG + g
-// (chunk-major), each entry a (uint16 row offset inside the chunk, uint8 bin - 64 g) pair.
+// (chunk-major), each entry a (uint16 row offset inside the chunk, uint8 bin - 64 g) pair. Inside a
+// segment the entries are ordered by 16-bin tile: the offset table has one start per (chunk,
+// tile) -- seg[(c * NG + g) * 4 + t] -- so segment (c, g) is [seg[4 (c NG + g)], seg[4 (c NG + g) + 4]).
 // The histogram kernel (blk_kernels.hip) gives a workgroup a range of chunks and every wave a
 // few groups: per chunk the workgroup stages the chunk's row state (8-byte digit words, slot
 // bytes) in LDS with coalesced loads, so no entry gathers anything from global memory, and the
@@ -125,6 +127,7 @@ struct HistArgs {
 // order per wave, so a compute wave's own prefetch would be waited for at its next entry load).
 constexpr int kBlkRows = 4096;
 constexpr int kBlkKeys = 64;
+constexpr int kBlkTiles = 4;                // 16-bin MFMA row tiles per group: segments are tile-sorted
 constexpr int kBlkWaves = 8;                // 512 threads: 2 waves per SIMD, 256 registers each
 constexpr int kBlkCompute = kBlkWaves - 1;
 constexpr int kBlkGroupsMax = 8;            // groups per compute wave at CT = 1 (128 accumulator registers)
@@ -139,8 +142,8 @@ struct BlkBuildArgs {
   int32_t NG;                     // bin groups
   int32_t chunk_rows;
   int32_t entries_per_thread;
-  int32_t* counts;                // pass 0: [n_chunks * NG] += entries per segment
-  int64_t* cursor;                // pass 1: [n_chunks * NG] next free slot of each segment (advanced)
+  int32_t* counts;                // pass 0: [n_chunks * NG * 4] += entries per (chunk, tile)
+  int64_t* cursor;                // pass 1: [n_chunks * NG * 4] next free slot of each (chunk, tile) (advanced)
   uint16_t* ent_row;              // pass 1 out
   uint8_t* ent_key;
 };
@@ -148,7 +151,7 @@ struct BlkBuildArgs {
 struct BlkHistArgs {
   const uint16_t* ent_row;        // BCSC entries (readable padding behind the end)
   const uint8_t* ent_key;
-  const int64_t* seg;             // [n_chunks * NG + 1] segment starts
+  const int64_t* seg;             // [n_chunks * NG * 4 + 1] (chunk, tile) starts
   int32_t NG;
   int32_t n_chunks;
   int64_t N;                      // rows

@@ -206,7 +206,7 @@ void blk_build_cpu(const BlkBuildArgs& a, int pass) {
   for (int64_t e = 0; e < a.nnz; ++e) {
     while (e >= a.colptr[f + 1]) ++f;
     const int64_t gb = a.boff[f] + a.csc_bin[e];
-    const int64_t key = (int64_t)(a.csc_row[e] / a.chunk_rows) * a.NG + gb / kBlkKeys;
+    const int64_t key = (int64_t)(a.csc_row[e] / a.chunk_rows) * (kBlkTiles * a.NG) + gb / 16;
     if (pass == 0) {
       a.counts[key] += 1;
     } else {
@@ -228,7 +228,8 @@ void hist_blk_cpu(const BlkHistArgs& a) {
           const int32_t grp = a.band_groups[((int64_t)band * kBlkCompute + wv) * a.gw + j];
           if (grp < 0) continue;
           for (int32_t c = a.wg_c0[w]; c < a.wg_c1[w]; ++c) {
-            const int64_t s0 = a.seg[(int64_t)c * a.NG + grp], s1 = a.seg[(int64_t)c * a.NG + grp + 1];
+            const int64_t* sg = a.seg + ((int64_t)c * a.NG + grp) * kBlkTiles;
+            const int64_t s0 = sg[0], s1 = sg[kBlkTiles];
             for (int64_t e = s0; e < s1; ++e) {
               const int64_t row = (int64_t)c * kBlkRows + a.ent_row[e];
               const int s = a.slot8 ? (int)a.slot8[row] : 0;

@@ -133,15 +133,16 @@ BLK_MAX_CELL = (1 << 31) // (1 << 14) - 1     # entries one int32 (key, column) 
 class BlockedCSC:
     """Row-blocked CSC of every active feature (csrc/tree.h "row-blocked histogram engine"):
     segment (chunk c, group g) holds the entries of rows [4096 c, 4096 (c + 1)) whose global bin
-    lies in [64 g, 64 (g + 1)) as (uint16 row offset, uint8 bin - 64 g). Built on the device in two
-    passes over the quantized CSC (count, then place), ~3 B per entry."""
+    lies in [64 g, 64 (g + 1)) as (uint16 row offset, uint8 bin - 64 g), ordered by 16-bin tile
+    (``seg`` has one start per (chunk, tile)). Built on the device in two passes over the quantized
+    CSC (count, then place), ~3 B per entry."""
 
     def __init__(self, Q: "Quantized"):
         C = native.lib()
         dev = Q.device
         self.NG = max(1, (Q.TB + BLK_KEYS - 1) // BLK_KEYS)
         self.n_chunks = max(1, (Q.n_rows + BLK_ROWS - 1) // BLK_ROWS)
-        ns = self.n_chunks * self.NG
+        ns = self.n_chunks * self.NG * 4               # (chunk, 16-bin tile) sub-segments
         counts = torch.zeros(ns, dtype=torch.int32, device=dev)
         C.tree_blk_build(Q.csc_row, Q.csc_bin, Q.colptr, Q.boff, BLK_ROWS, self.NG, 0, counts, None, None, None)
         self.seg = torch.zeros(ns + 1, dtype=torch.int64, device=dev)
@@ -153,7 +154,7 @@ class BlockedCSC:
         self.ent_key = torch.zeros(nnz + CSC_PAD, dtype=torch.uint8, device=dev)[:nnz]
         C.tree_blk_build(Q.csc_row, Q.csc_bin, Q.colptr, Q.boff, BLK_ROWS, self.NG, 1, None, cursor,
                          self.ent_row, self.ent_key)
-        self.seg_counts = counts.cpu().numpy().reshape(self.n_chunks, self.NG).astype(np.int64)
+        self.seg_counts = counts.cpu().numpy().reshape(self.n_chunks, self.NG, 4).sum(-1).astype(np.int64)
         self.nnz = nnz
         self._plans: dict = {}
 

@@ -187,30 +187,27 @@ def _subset(buf: np.ndarray, off: np.ndarray, keep: np.ndarray) -> tuple:
     return buf[off[0]:off[-1]][sel], new
 
 
-def _ts_perf(msg) -> float:
-    try:
-        kind, ms = msg.timestamp()
-        if kind and ms > 0:
-            return ms / 1000.0 - (time.time() - time.perf_counter())
-    except Exception:
-        pass
-    return time.perf_counter()
-
-
-def _to_pieces(msgs: list) -> list:
-    """confluent Messages -> per-partition columnar pieces (consume order kept per partition)."""
-    groups: dict = {}
-    for m in msgs:
-        groups.setdefault((m.topic(), m.partition()), []).append(m)
+def _to_pieces(msgs: list) -> tuple:
+    """confluent Messages -> (per-partition columnar pieces in consume order, [(index, error)]).
+    One native pass over the list (csrc/bindings_kafka.cpp pack_messages): the per-message method
+    calls (error, topic, partition, key, value, offset, timestamp) run from C, not bytecode."""
+    part_of, parts, kb, ko, nk, vb, vo, offs, ts_ms, errors = native.lib().pack_messages(msgs)
+    now = time.perf_counter()
+    ts = np.where(ts_ms > 0, ts_ms / 1000.0 - (time.time() - now), now)
     out = []
-    for (t, p), ms in groups.items():
-        kb, ko, nk = fake_kafka.pack([m.key() for m in ms])
-        vb, vo, _ = fake_kafka.pack([m.value() or b"" for m in ms])
-        offs = np.fromiter((m.offset() for m in ms), dtype=np.int64, count=len(ms))
-        ts = np.fromiter((_ts_perf(m) for m in ms), dtype=np.float64, count=len(ms))
-        rb = fake_kafka.RecordBatch(t, p, int(offs[0]), kb, ko, vb, vo, nk, float(ts.min()))
-        out.append(_Piece(rb, offs, ts))
-    return out
+    for pi, (t, p) in enumerate(parts):
+        if len(parts) == 1:
+            sel = None
+            kk, kof, vv, vof, nn, oo, tt = kb, ko, vb, vo, nk, offs, ts
+        else:                                   # several partitions in one consume: split
+            sel = np.flatnonzero(part_of == pi)
+            kk, kof = _subset(kb, ko, part_of == pi)
+            vv, vof = _subset(vb, vo, part_of == pi)
+            nn, oo, tt = nk[sel], offs[sel], ts[sel]
+        nulls = nn.astype(bool) if nn.any() else None
+        rb = fake_kafka.RecordBatch(t, p, int(oo[0]), kk, kof, vv, vof, nulls, float(tt.min()))
+        out.append(_Piece(rb, oo, tt))
+    return out, errors
 
 
 def extract_into(slot: Slot, pos: int, n: int, rb, field_name: str, status: np.ndarray) -> int:
@@ -280,19 +277,21 @@ class _Reader(threading.Thread):
                 items = self.consumer.consume_batches(want, timeout)
             else:
                 items = self.consumer.consume(num_messages=want, timeout=timeout)
-            good = []
-            for it in items:
-                if isinstance(it, fake_kafka.RecordBatch):
-                    self.carry.append(_Piece(it))
-                    got += it.n
-                elif it.error() is not None:
+            if self.columnar:
+                for it in items:
+                    if isinstance(it, fake_kafka.RecordBatch):
+                        self.carry.append(_Piece(it))
+                        got += it.n
+                    elif it.error() is not None:
+                        eng._count("broker_errors", 1)
+                        log.warning("kafka error: %s", it.error())
+            elif items:
+                pieces, errors = _to_pieces(items if isinstance(items, list) else list(items))
+                for _, err in errors:
                     eng._count("broker_errors", 1)
-                    log.warning("kafka error: %s", it.error())
-                else:
-                    good.append(it)
-            if good:
-                self.carry.extend(_to_pieces(good))
-                got += len(good)
+                    log.warning("kafka error: %s", err)
+                self.carry.extend(pieces)
+                got += sum(pc.rb.n for pc in pieces)
         finally:
             eng._settle(want, got)
         if not got and timeout == 0:
@@ -654,19 +653,12 @@ class StreamingEngine:
             if left[0] == 0:
                 self._on_delivery(seg, entry, err_box[0])
 
-        for i in range(seg.n_out):
-            key = None if (nulls is not None and nulls[i]) else keys[koff[i]:koff[i + 1]].tobytes()
-            val = vals[voff[i]:voff[i + 1]].tobytes()
-            while True:
-                try:
-                    self.producer.produce(self.topic, value=val, key=key, on_delivery=cb)
-                    break
-                except BufferError:         # local queue full: serve delivery reports, retry
-                    self.producer.poll(0.05)
-                except Exception as e:
-                    log.error("produce failed: %s", e)
-                    cb(e, None)
-                    break
+        # one C loop of produce() calls (BufferError: poll(0.05) and retry; other errors: cb(err))
+        native.lib().produce_each(self.producer, self.topic, np.ascontiguousarray(keys, dtype=np.uint8),
+                                  np.ascontiguousarray(koff, dtype=np.int64),
+                                  None if nulls is None else np.ascontiguousarray(nulls, dtype=np.uint8),
+                                  np.ascontiguousarray(vals, dtype=np.uint8), np.ascontiguousarray(voff, dtype=np.int64),
+                                  cb)
 
     def _on_delivery_cb(self, seg, entry, err, _msg) -> None:
         self._on_delivery(seg, entry, err)

@@ -67,34 +67,35 @@ class TopicPartition:
         return hash((self.topic, self.partition, self.offset))
 
 
-class Message:
-    __slots__ = ("_topic", "_partition", "_offset", "_key", "_value", "_error", "_ts")
+class Message(tuple):
+    """confluent_kafka.Message: (topic, partition, offset, key, value, error, timestamp ms), a tuple
+    underneath so a consume of many records builds them without a Python __init__ per record."""
+    __slots__ = ()
 
-    def __init__(self, topic, partition, offset, key, value, error=None, ts=None):
-        self._topic, self._partition, self._offset = topic, partition, offset
-        self._key, self._value, self._error = key, value, error
-        self._ts = time.time() if ts is None else ts
+    def __new__(cls, topic, partition, offset, key, value, error=None, ts=None):
+        return tuple.__new__(cls, (topic, partition, offset, key, value, error,
+                                   int((time.time() if ts is None else ts) * 1000)))
 
     def topic(self):
-        return self._topic
+        return self[0]
 
     def partition(self):
-        return self._partition
+        return self[1]
 
     def offset(self):
-        return self._offset
+        return self[2]
 
     def key(self):
-        return self._key
+        return self[3]
 
     def value(self):
-        return self._value
+        return self[4]
 
     def error(self):
-        return self._error
+        return self[5]
 
     def timestamp(self):
-        return (1, int(self._ts * 1000))
+        return (1, self[6])
 
 
 def _b(v) -> Optional[bytes]:
@@ -150,14 +151,51 @@ class RecordBatch:
     def message(self, i: int) -> Message:
         return Message(self.topic, self.partition, self.base_offset + i, self.key(i), self.value(i))
 
+    def messages(self) -> list:
+        """Every record as a ``Message`` (bytes sliced out of one copy of each buffer)."""
+        vb, kb = self.values.tobytes(), self.keys.tobytes()
+        vo, ko = self.val_off.tolist(), self.key_off.tolist()
+        nk = self.null_keys
+        t, p, b = self.topic, self.partition, self.base_offset
+        ms = int((self.ts + (time.time() - time.perf_counter())) * 1000)
+        new = tuple.__new__
+        return [new(Message, (t, p, b + i, None if (nk is not None and nk[i]) else kb[ko[i]:ko[i + 1]],
+                              vb[vo[i]:vo[i + 1]], None, ms)) for i in range(len(vo) - 1)]
+
 
 class _Partition:
-    def __init__(self):
+    """Stored record batches plus a tail of single appends (``produce``), sealed into one columnar
+    batch when the partition is next read: a per-record produce costs two list appends."""
+
+    def __init__(self, topic: str = "", index: int = 0):
         self.batches: list = []
         self.starts: list = []
         self.size = 0
+        self.topic, self.index = topic, index
+        self._tk: list = []
+        self._tv: list = []
+        self._tts = 0.0
+
+    def append_one(self, key: Optional[bytes], value: Optional[bytes]) -> int:
+        if not self._tk:
+            self._tts = time.perf_counter()
+        self._tk.append(key)
+        self._tv.append(value)
+        self.size += 1
+        return self.size - 1
+
+    def _seal(self) -> None:
+        if self._tk:
+            kb, ko, nk = pack(self._tk)
+            vb, vo, _ = pack(self._tv)
+            n = len(self._tk)
+            self._tk, self._tv = [], []
+            rb = RecordBatch(self.topic, self.index, self.size - n, kb, ko, vb, vo, nk, self._tts)
+            self.batches.append(rb)
+            self.starts.append(self.size - n)
 
     def append(self, rb: RecordBatch) -> None:
+        self._seal()
         rb.base_offset = self.size
         self.batches.append(rb)
         self.starts.append(self.size)
@@ -167,6 +205,7 @@ class _Partition:
         """Records from offset ``pos`` (at most ``max_n``, never across stored batches)."""
         if pos >= self.size:
             return None
+        self._seal()
         i = bisect.bisect_right(self.starts, pos) - 1
         rb = self.batches[i]
         a = pos - rb.base_offset
@@ -176,6 +215,7 @@ class _Partition:
         return self.size
 
     def __getitem__(self, off: int) -> Message:
+        self._seal()
         rb = self.batches[bisect.bisect_right(self.starts, off) - 1]
         return rb.message(off - rb.base_offset)
 
@@ -190,7 +230,8 @@ class Broker:
 
     def create_topic(self, name: str, partitions: int = 3) -> None:
         with self.lock:
-            self.topics.setdefault(name, [_Partition() for _ in range(partitions)])
+            if name not in self.topics:
+                self.topics[name] = [_Partition(name, i) for i in range(partitions)]
 
     def partitions(self, topic: str) -> int:
         with self.lock:
@@ -201,18 +242,17 @@ class Broker:
     def _route(key, value, nparts: int) -> int:
         return (zlib.crc32(key) if key else zlib.crc32(value or b"")) % nparts
 
-    def append(self, topic: str, key, value, partition: Optional[int] = None) -> Message:
+    def append(self, topic: str, key, value, partition: Optional[int] = None, want_message: bool = True):
         with self.lock:
-            self.create_topic(topic)
-            parts = self.topics[topic]
+            parts = self.topics.get(topic)
+            if parts is None:
+                self.create_topic(topic)
+                parts = self.topics[topic]
             if partition is None or partition < 0:
                 partition = self._route(key, value, len(parts))
-            kb, ko, nk = pack([key])
-            vb, vo, _ = pack([value])
-            rb = RecordBatch(topic, partition, 0, kb, ko, vb, vo, nk)
-            parts[partition].append(rb)
+            off = parts[partition].append_one(key, value)
             self.cond.notify_all()
-            return rb.message(0)
+        return Message(topic, partition, off, key, value) if want_message else None
 
     def append_records(self, topic: str, partition: int, keys, key_off, values, val_off, null_keys=None,
                        copy: bool = True) -> RecordBatch:
@@ -264,6 +304,8 @@ class Broker:
 
     def messages(self, topic: str) -> list:
         with self.lock:
+            for p in self.topics.get(topic, []):
+                p._seal()
             return [rb.message(i) for p in self.topics.get(topic, []) for rb in p.batches for i in range(rb.n)]
 
 
@@ -364,7 +406,7 @@ class Consumer:
             if isinstance(item, Message):
                 out.append(item)
             else:
-                out.extend(item.message(i) for i in range(item.n))
+                out.extend(item.messages())
         return out
 
     def consume_batches(self, max_messages: int = 1, timeout: float = -1) -> list:
@@ -445,9 +487,15 @@ class Producer:
                 callback: Optional[Callable] = None, **kw) -> None:
         if topic is None:
             raise TypeError("topic must be a str (KAFKA_OUTPUT_TOPIC unset?)")
-        err = self._maybe_fail()
-        m = None if err else self.broker.append(topic, _b(key), _b(value), partition)
-        self._deliver_later(on_delivery or callback, err, m)
+        cb = on_delivery or callback
+        err = self._maybe_fail() if self.fail_next else None
+        if type(key) is not bytes and key is not None:
+            key = _b(key)
+        if type(value) is not bytes and value is not None:
+            value = _b(value)
+        m = None if err else self.broker.append(topic, key, value, partition, want_message=cb is not None)
+        if cb is not None:
+            self._pending.append((cb, err, m))     # list.append is atomic under the GIL
 
     def produce_batch(self, topic: str, keys: list, values: list) -> None:
         """Many messages at once, keyed partitioning, no delivery callbacks."""
@@ -473,9 +521,43 @@ class Producer:
             cb(err, what)
         return len(pend)
 
+
     def flush(self, timeout: float = -1) -> int:
         self.poll(0)
         return 0
 
     def __len__(self) -> int:
         return len(self._pending)
+
+
+class ConfluentConsumer:
+    """Only the confluent_kafka.Consumer surface of an in-memory consumer (no columnar
+    ``consume_batches``): what the streaming engine sees with a real librdkafka client. Selected
+    by ``FDX_KAFKA_COLUMNAR=0`` (stream/kafka.py) and by the loadgen's confluent-API runs."""
+    _API = frozenset(("subscribe", "assign", "assignment", "poll", "consume", "commit", "committed", "close",
+                      "unsubscribe", "position"))
+
+    def __init__(self, inner: Consumer):
+        self._inner = inner
+
+    def __getattr__(self, name):
+        if name in ConfluentConsumer._API:
+            return getattr(self._inner, name)
+        raise AttributeError(name)
+
+
+class ConfluentProducer:
+    """Only the confluent_kafka.Producer surface (per-record ``produce`` with delivery callbacks,
+    ``poll``, ``flush``; no columnar ``produce_records``)."""
+    _API = frozenset(("produce", "poll", "flush"))
+
+    def __init__(self, inner: Producer):
+        self._inner = inner
+
+    def __getattr__(self, name):
+        if name in ConfluentProducer._API:
+            return getattr(self._inner, name)
+        raise AttributeError(name)
+
+    def __len__(self) -> int:
+        return len(self._inner)

@@ -7,6 +7,9 @@ consumer: ``auto.offset.reset=earliest``, ``enable.auto.commit=False`` (/root/re
 kafka_utils.py:11-49). The backend is confluent_kafka (librdkafka) when importable and the
 bootstrap is a real address; ``memory://...`` bootstraps (or ``FDX_KAFKA=memory``) select the
 in-memory broker of ``fake_kafka`` — used by tests, benchmarks and offline demos.
+``FDX_KAFKA_COLUMNAR=0`` hands out in-memory clients restricted to the confluent_kafka surface
+(per-record Messages / produce calls, no columnar batches): the path a real librdkafka client
+takes through the streaming engine, measurable without a broker.
 """
 from __future__ import annotations
 
@@ -41,6 +44,20 @@ def _use_memory(bootstrap: str) -> bool:
     return False
 
 
+def _columnar() -> bool:
+    return os.getenv("FDX_KAFKA_COLUMNAR", "1") != "0"
+
+
+def _mem_consumer(conf: dict):
+    c = fake_kafka.Consumer(conf)
+    return c if _columnar() else fake_kafka.ConfluentConsumer(c)
+
+
+def _mem_producer(conf: dict):
+    p = fake_kafka.Producer(conf)
+    return p if _columnar() else fake_kafka.ConfluentProducer(p)
+
+
 def consumer_config(group: Optional[str] = None) -> dict:
     return _security({"bootstrap.servers": os.getenv("KAFKA_BOOTSTRAP_SERVERS", DEFAULT_BOOTSTRAP),
                       "group.id": group or os.getenv("KAFKA_CONSUMER_GROUP", DEFAULT_GROUP),
@@ -54,7 +71,7 @@ def producer_config() -> dict:
 def get_kafka_consumer(topics=None, group: Optional[str] = None):
     conf = consumer_config(group)
     if _use_memory(conf["bootstrap.servers"]):
-        c = fake_kafka.Consumer(conf)
+        c = _mem_consumer(conf)
     else:
         from confluent_kafka import Consumer
 
@@ -72,7 +89,7 @@ def get_partition_consumers(topic: Optional[str] = None, group: Optional[str] = 
         nparts = fake_kafka.broker_for(conf["bootstrap.servers"]).partitions(topic)
         out = []
         for p in range(nparts):
-            c = fake_kafka.Consumer(conf)
+            c = _mem_consumer(conf)
             c.assign([fake_kafka.TopicPartition(topic, p)])
             out.append(c)
         return out
@@ -92,7 +109,7 @@ def get_partition_consumers(topic: Optional[str] = None, group: Optional[str] = 
 def get_kafka_producer():
     conf = producer_config()
     if _use_memory(conf["bootstrap.servers"]):
-        return fake_kafka.Producer(conf)
+        return _mem_producer(conf)
     from confluent_kafka import Producer
 
     return Producer(conf)

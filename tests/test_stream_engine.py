@@ -86,6 +86,33 @@ def test_partition_readers_commit_only_delivered(agent, monkeypatch):
     assert recs[b"k0"]["prediction"] == 1.0 and recs[b"k0"]["original_text"] == fixtures.SCAM_SAMPLE
 
 
+def test_confluent_surface_clients_take_the_per_record_path(agent, monkeypatch):
+    """FDX_KAFKA_COLUMNAR=0: clients expose only the confluent_kafka API (per-record Messages and
+    produce calls) — the path a librdkafka client takes (native pack_messages / produce_each)."""
+    url = "memory://confluent-surface"
+    texts = [fixtures.SCAM_SAMPLE, fixtures.BENIGN_SAMPLE, "hello there"] * 40
+    broker = _fill(url, "in", texts)
+    nullkey = fake_kafka.Producer({"bootstrap.servers": url})
+    nullkey.produce("in", key=None, value=json.dumps({"text": "no key here"}), partition=0)
+    nullkey.produce("in", key=b"bad", value=b"{not json", partition=1)
+    monkeypatch.setenv("KAFKA_BOOTSTRAP_SERVERS", url)
+    monkeypatch.setenv("FDX_KAFKA_COLUMNAR", "0")
+    c = kafka.get_kafka_consumer(["in"], group="cs")        # one consumer over all 3 partitions
+    prod = kafka.get_kafka_producer()
+    assert not hasattr(c, "consume_batches") and not hasattr(prod, "produce_records")
+    eng = StreamingEngine.from_agent(agent, c, prod, "out", batch_max=32, max_latency_ms=1)
+    st = eng.run(idle_timeout_s=0.3)
+    assert st["messages"] == 122 and st["produced"] == 121 and st["bad_messages"] == 1
+    assert st["delivery_errors"] == 0
+    out = broker.messages("out")
+    recs = {m.key(): json.loads(m.value()) for m in out}
+    assert all(recs[f"k{i}".encode()]["original_text"] == texts[i] for i in range(len(texts)))
+    assert recs[b"k0"]["prediction"] == 1.0
+    assert [json.loads(m.value())["original_text"] for m in out if m.key() is None] == ["no key here"]
+    got = c.committed([fake_kafka.TopicPartition("in", p) for p in range(3)])
+    assert [tp.offset for tp in got] == [len(broker.topics["in"][p]) for p in range(3)]
+
+
 def test_failed_delivery_blocks_that_partitions_commit(agent):
     url = "memory://faildeliver"
     broker = _fill(url, "in", ["a b c"] * 30, parts=1)

@@ -710,8 +710,10 @@ def test_blocked_csc_covers_every_entry_and_plan_covers_every_segment_once():
     rows, keys = blk.ent_row.numpy().view(np.uint16), blk.ent_key.numpy()
     for c in range(blk.n_chunks):
         for g in range(blk.NG):
-            a, b = seg[c * blk.NG + g], seg[c * blk.NG + g + 1]
-            got += [(c * 4096 + int(r), g * 64 + int(k)) for r, k in zip(rows[a:b], keys[a:b])]
+            for t in range(4):
+                a, b = seg[(c * blk.NG + g) * 4 + t], seg[(c * blk.NG + g) * 4 + t + 1]
+                assert all(int(k) // 16 == t for k in keys[a:b])          # sub-segments are tile-pure
+                got += [(c * 4096 + int(r), g * 64 + int(k)) for r, k in zip(rows[a:b], keys[a:b])]
     assert sorted(got) == want
     for gw in (8, 4):
         band, c0, c1, groups = (t.numpy() for t in blk.plan(gw, target_wgs=37))
