@@ -87,6 +87,13 @@ __global__ __launch_bounds__(256) void blk_build_kernel(BlkBuildArgs a, int pass
 constexpr int kBlkPlaneStride = 288;
 // LDS: double-buffered chunk row state (digit words + slot bytes) shared by the workgroup, and per
 // compute wave one 256-entry step staged plane-major (keys, 8 digit planes, slots) as MFMA operands.
+// Segment descriptors of the workgroup's groups for kBlkDescBufs chunks (a ring the staging wave
+// keeps kBlkDescBufs - 2 chunks ahead of the chunk being processed), so that a compute wave walks
+// its (chunk, group, step) sequence -- and issues the entry loads of steps ahead -- without a
+// dependent global load per segment.
+constexpr int kBlkDescBufs = 8;
+constexpr int kBlkSlots = kBlkCompute * kBlkGroupsMax;    // (wave, group) slots of a workgroup
+
 template <bool ROOT>
 struct BlkShared {
   uint2 dig[2][kBlkRows];
@@ -94,6 +101,9 @@ struct BlkShared {
   uint8_t key[kBlkCompute][256];
   uint8_t pl[kBlkCompute][8][kBlkPlaneStride];
   uint8_t sl[kBlkCompute][ROOT ? 16 : 256];
+  int64_t d_e0[kBlkDescBufs][kBlkSlots];                 // segment start
+  int32_t d_n[kBlkDescBufs][kBlkSlots];                  // segment length
+  int32_t d_t[kBlkDescBufs][3][kBlkSlots];               // tile 1..3 starts relative to d_e0
 };
 
 // The staging wave: chunk c's row state -> LDS buffer buf (rows past N read as zero / no slot).
@@ -226,64 +236,120 @@ __device__ __forceinline__ void blk_flush(const BlkHistArgs& a, int grp, int lan
   }
 }
 
-// A compute wave's walk over its (chunk, group, 256-entry step) sequence. The entries of the next
-// step are loaded while the current one is staged and multiplied (one load in flight across every
-// step, chunk boundaries included), so a short segment does not expose a memory latency per step.
-constexpr int kBlkAhead = 4;       // 256-entry steps of entry loads in flight per compute wave
-
-struct BlkCursor {
-  int32_t c;          // chunk (>= c1: done)
-  int j;              // group slot of the wave
-  int64_t e0;         // segment start
-  int32_t n;          // segment length
-  int32_t base;       // step start relative to e0 (e0 + base is 4-aligned; may be -1 .. -3)
-  int32_t t1, t2, t3; // tile starts relative to e0
+// The staging wave's segment descriptors of chunk cc for the workgroup's (wave, group) slots:
+// lane s < 7 gw loads slot s's five segment bounds (one latency for the whole table).
+struct BlkDescRegs {
+  int64_t s[5];
 };
 
-__device__ __forceinline__ void blk_seek(const BlkHistArgs& a, const int* grp, int gw, int32_t c1, BlkCursor& k) {
-  // from (c, j) onwards, the first non-empty segment
-  while (k.c < c1) {
-    while (k.j < gw) {
-      const int g = grp[k.j];
-      if (g >= 0) {
-        const int64_t* sg = a.seg + ((int64_t)k.c * a.NG + g) * kBlkTiles;
-        k.e0 = sg[0];
-        k.n = (int32_t)(sg[4] - k.e0);
-        if (k.n > 0) {
-          k.base = -(int32_t)(k.e0 & 3);
-          k.t1 = (int32_t)(sg[1] - k.e0);
-          k.t2 = (int32_t)(sg[2] - k.e0);
-          k.t3 = (int32_t)(sg[3] - k.e0);
-          return;
-        }
-      }
-      ++k.j;
-    }
-    ++k.c;
-    k.j = 0;
+__device__ __forceinline__ BlkDescRegs load_descs(const BlkHistArgs& a, int32_t cc, int my_g) {
+  BlkDescRegs r{};
+  if (my_g >= 0) {
+    const int64_t* sg = a.seg + ((int64_t)cc * a.NG + my_g) * kBlkTiles;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.s[i] = sg[i];
   }
+  return r;
 }
 
-__device__ __forceinline__ void blk_advance(const BlkHistArgs& a, const int* grp, int gw, int32_t c1, BlkCursor& k) {
-  k.base += 256;
-  if (k.base < k.n) return;
-  ++k.j;
-  blk_seek(a, grp, gw, c1, k);
+template <bool ROOT>
+__device__ __forceinline__ void store_descs(BlkShared<ROOT>& sh, int32_t rel, int lane, int nslots, const BlkDescRegs& r) {
+  if (lane >= nslots) return;
+  const int b = rel & (kBlkDescBufs - 1);
+  sh.d_e0[b][lane] = r.s[0];
+  sh.d_n[b][lane] = (int32_t)(r.s[4] - r.s[0]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) sh.d_t[b][i][lane] = (int32_t)(r.s[i + 1] - r.s[0]);
 }
 
-__device__ __forceinline__ void blk_load(const BlkHistArgs& a, const BlkCursor& k, int lane, uint2& rr, uint32_t& keys4) {
-  const int32_t e = k.base + 4 * lane;
-  const int64_t abs_last4 = (k.e0 + k.n - 1) & ~(int64_t)3;       // last 4-group holding an entry
-  const int64_t abs_e = k.e0 + e;
-  const int64_t el = abs_e < abs_last4 ? abs_e : abs_last4;
+// One 256-entry step of a compute wave: chunk c, the wave's group slot j, segment [e0, e0 + n),
+// entries [e0 + base, e0 + base + 256) (e0 + base 4-aligned; base may be -1 .. -3). n == 0 marks
+// a step without work: a bubble (the walk may not look further ahead yet) or, at c == c1, the end.
+struct BlkStep {
+  int32_t c, j, n, base, t1, t2, t3;
+  int64_t e0;
+};
+
+// The wave's walk: the next step of its sequence, read from the descriptor ring in LDS. The walk
+// may enter chunks <= limit only (their descriptors are staged); beyond, it yields bubbles.
+struct BlkWalk {
+  int32_t c, j;
+  bool ready;
+  BlkStep cur;
+};
+
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <bool ROOT>
+__device__ __forceinline__ BlkStep blk_take(const BlkShared<ROOT>& sh, BlkWalk& w, int wid, int gw, int32_t c0,
+                                            int32_t c1, int32_t limit) {
+  while (!w.ready && w.c < c1 && w.c <= limit) {
+    if (w.j >= gw) {
+      ++w.c;
+      w.j = 0;
+      continue;
+    }
+    const int b = (w.c - c0) & (kBlkDescBufs - 1), s = wid * gw + w.j;
+    const int32_t n = uni(sh.d_n[b][s]);
+    if (n > 0) {
+      w.cur.c = w.c;
+      w.cur.j = w.j;
+      w.cur.n = n;
+      w.cur.e0 = uni64(sh.d_e0[b][s]);
+      w.cur.base = -(int32_t)(w.cur.e0 & 3);
+      w.cur.t1 = uni(sh.d_t[b][0][s]);
+      w.cur.t2 = uni(sh.d_t[b][1][s]);
+      w.cur.t3 = uni(sh.d_t[b][2][s]);
+      w.ready = true;
+    } else {
+      ++w.j;
+    }
+  }
+  if (w.ready) {
+    const BlkStep s = w.cur;
+    w.cur.base += 256;
+    if (w.cur.base >= w.cur.n) {
+      w.ready = false;
+      ++w.j;
+    }
+    return s;
+  }
+  BlkStep s{};
+  s.c = w.c < c1 ? w.c : c1;        // bubble at the chunk the walk waits in, or the end
+  return s;
+}
+
+__device__ __forceinline__ void blk_load(const BlkHistArgs& a, const BlkStep& k, int lane, uint2& rr, uint32_t& keys4) {
+  // always one load pair per step (a step without work reads entry 0): the wave's loads stay a
+  // fixed-depth ring, so the wait for a step's entries is vmcnt(2 * (kBlkAhead - 1)), never 0
+  int64_t el = 0;
+  if (k.n > 0) {
+    const int64_t abs_last4 = (k.e0 + k.n - 1) & ~(int64_t)3;       // last 4-group holding an entry
+    const int64_t abs_e = k.e0 + k.base + 4 * lane;
+    el = abs_e < abs_last4 ? abs_e : abs_last4;
+  }
   rr = *reinterpret_cast<const uint2*>(a.ent_row + el);
   keys4 = *reinterpret_cast<const uint32_t*>(a.ent_key + el);
 }
+
+constexpr int kBlkAhead = 4;       // steps of entry loads in flight per compute wave
 
 // GW groups per compute wave (GW * CT * 16 accumulator registers <= 128). The accumulators are
 // flushed once, at the end: the planner keeps every workgroup's chunk range short enough that no
 // int32 (key, column) sum can overflow (models/quantize.py BlockedCSC.plan; an in-loop flush made
 // the compiler spill the accumulators).
+//
+// Chunk protocol (all 8 waves execute 1 + (c1 - c0) barriers): before the first barrier the
+// staging wave writes chunk c0's row state and the descriptors of chunks c0 .. c0 + kBlkDescBufs
+// - 2; between barriers c and c + 1 the compute waves process chunk c while it writes chunk c +
+// 1's row state and chunk c + kBlkDescBufs - 1's descriptors into the buffers chunk c - 1 used.
+// A compute wave passes barrier c when its walk reaches a step of a later chunk (a bubble
+// included); its ring of kBlkAhead steps is indexed statically (the loop is unrolled kBlkAhead
+// times), so no loaded register is ever moved -- a move would wait for the load.
 template <int CT, bool ROOT, int GW>
 __global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a) {
   __shared__ BlkShared<ROOT> sh;
@@ -293,10 +359,26 @@ __global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a)
   if (w >= a.n_wg) return;
   const int band = a.wg_band[w];
   const int32_t c0 = a.wg_c0[w], c1 = a.wg_c1[w];
-  int grp[GW];
+  const int gw = a.gw;
+  if (stager) {
+    const int nslots = kBlkCompute * gw;
+    const int my_g = lane < nslots ? a.band_groups[(int64_t)band * nslots + lane] : -1;
+    BlkDescRegs d[kBlkDescBufs - 1];
 #pragma unroll
-  for (int j = 0; j < GW; ++j)
-    grp[j] = stager ? -1 : a.band_groups[((int64_t)band * kBlkCompute + wid) * a.gw + j];
+    for (int k = 0; k < kBlkDescBufs - 1; ++k) d[k] = c0 + k < c1 ? load_descs(a, c0 + k, my_g) : BlkDescRegs{};
+    stage_chunk<ROOT>(a, sh, 0, c0, lane);
+#pragma unroll
+    for (int k = 0; k < kBlkDescBufs - 1; ++k) store_descs<ROOT>(sh, k, lane, nslots, d[k]);
+    __syncthreads();
+    for (int32_t c = c0; c < c1; ++c) {
+      const int32_t cd = c + kBlkDescBufs - 1;
+      const BlkDescRegs dn = cd < c1 ? load_descs(a, cd, my_g) : BlkDescRegs{};
+      if (c + 1 < c1) stage_chunk<ROOT>(a, sh, (c - c0 + 1) & 1, c + 1, lane);   // overlaps chunk c
+      if (cd < c1) store_descs<ROOT>(sh, cd - c0, lane, nslots, dn);
+      __syncthreads();
+    }
+    return;
+  }
   i32x4 acc[GW][4][CT];
 #pragma unroll
   for (int j = 0; j < GW; ++j)
@@ -304,68 +386,65 @@ __global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a)
     for (int bt = 0; bt < 4; ++bt)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[j][bt][ct] = i32x4{0, 0, 0, 0};
-  if (stager) {
-    stage_chunk<ROOT>(a, sh, 0, c0, lane);
-    __syncthreads();
-    for (int32_t c = c0; c < c1; ++c) {
-      if (c + 1 < c1) stage_chunk<ROOT>(a, sh, (c - c0 + 1) & 1, c + 1, lane);   // overlaps chunk c
-      __syncthreads();
-    }
-    return;
-  }
-  // kBlkAhead steps of entries in flight: q[0] is the step being processed
-  BlkCursor q[kBlkAhead];
+  __syncthreads();                                         // chunk c0 and the first descriptors staged
+  int32_t cur = c0;
+  BlkWalk walk{c0, 0, false, BlkStep{}};
+  BlkStep ring[kBlkAhead];
   uint2 rq[kBlkAhead];
   uint32_t kq[kBlkAhead];
-  q[0] = BlkCursor{c0, 0, 0, 0, 0, 0, 0, 0};
-  blk_seek(a, grp, GW, c1, q[0]);
 #pragma unroll
   for (int i = 0; i < kBlkAhead; ++i) {
-    if (i > 0) {
-      q[i] = q[i - 1];
-      if (q[i].c < c1) blk_advance(a, grp, GW, c1, q[i]);
-    }
-    rq[i] = make_uint2(0u, 0u);
-    kq[i] = 0;
-    if (q[i].c < c1) blk_load(a, q[i], lane, rq[i], kq[i]);
+    ring[i] = blk_take<ROOT>(sh, walk, wid, gw, c0, c1, cur + kBlkDescBufs - 2);
+    // issue order fixed (slot 0 first): the loop header's wait for slot 0 is then vmcnt(6), not 0
+    __builtin_amdgcn_sched_barrier(0);
+    blk_load(a, ring[i], lane, rq[i], kq[i]);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  __syncthreads();                                         // chunk c0 staged
-  for (int32_t c = c0; c < c1; ++c) {
-    const int buf = (c - c0) & 1;
-    while (q[0].c == c) {
-      const BlkCursor now = q[0];
-      const uint2 rr_now = rq[0];
-      const uint32_t k_now = kq[0];
+  // trips of kBlkAhead steps; the exit test sits at the trip end only, so every slot's loads are
+  // issued on every path (a mid-trip exit let the compiler skip a slot's load on the path that
+  // leaves, and the merged wait state then drained the whole ring at each step)
+  bool more = true;
+  while (more) {
 #pragma unroll
-      for (int i = 0; i + 1 < kBlkAhead; ++i) {
-        q[i] = q[i + 1];
-        rq[i] = rq[i + 1];
-        kq[i] = kq[i + 1];
+    for (int u = 0; u < kBlkAhead; ++u) {
+      const BlkStep now = ring[u];
+      while (cur < now.c) {                                // chunk cur done
+        __syncthreads();
+        ++cur;
       }
-      q[kBlkAhead - 1] = q[kBlkAhead - 2 >= 0 ? kBlkAhead - 2 : 0];
-      if (q[kBlkAhead - 1].c < c1) {
-        blk_advance(a, grp, GW, c1, q[kBlkAhead - 1]);
-        if (q[kBlkAhead - 1].c < c1) blk_load(a, q[kBlkAhead - 1], lane, rq[kBlkAhead - 1], kq[kBlkAhead - 1]);
-      }
-      blk_stage_step<ROOT>(sh, buf, wid, lane, now.base, 0, now.n, rr_now, k_now);
-      lds_sync();
-      switch (now.j) {
+      const bool work = now.n > 0 && cur < c1;
+      // staged unconditionally (a step without work stages nothing live): every path consumes the
+      // slot's loads before the slot is reloaded, so no path waits for younger loads
+      blk_stage_step<ROOT>(sh, (cur - c0) & 1, wid, lane, now.base, 0, work ? now.n : 0, rq[u], kq[u]);
+      ring[u] = blk_take<ROOT>(sh, walk, wid, gw, c0, c1, cur + kBlkDescBufs - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      blk_load(a, ring[u], lane, rq[u], kq[u]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (work) {
+        lds_sync();
+        switch (now.j) {
 #define FDX_BLK_CASE(J) \
   case J:               \
     if constexpr (J < GW) blk_ksteps<CT, ROOT>(sh, wid, lane, now.base, now.n, now.t1, now.t2, now.t3, acc[J]); \
     break;
-        FDX_BLK_CASE(0) FDX_BLK_CASE(1) FDX_BLK_CASE(2) FDX_BLK_CASE(3)
-        FDX_BLK_CASE(4) FDX_BLK_CASE(5) FDX_BLK_CASE(6) FDX_BLK_CASE(7)
+          FDX_BLK_CASE(0) FDX_BLK_CASE(1) FDX_BLK_CASE(2) FDX_BLK_CASE(3)
+          FDX_BLK_CASE(4) FDX_BLK_CASE(5) FDX_BLK_CASE(6) FDX_BLK_CASE(7)
 #undef FDX_BLK_CASE
-        default: break;
+          default: break;
+        }
+        lds_sync();
       }
-      lds_sync();
     }
-    __syncthreads();                                       // chunk c done; chunk c + 1 staged
+    more = cur < c1;
   }
+  {
+    const int nslots = kBlkCompute * gw;
 #pragma unroll
-  for (int j = 0; j < GW; ++j)
-    if (grp[j] >= 0) blk_flush<CT>(a, grp[j], lane, acc[j]);
+    for (int j = 0; j < GW; ++j) {
+      const int g = j < gw ? a.band_groups[(int64_t)band * nslots + wid * gw + j] : -1;
+      if (g >= 0) blk_flush<CT>(a, g, lane, acc[j]);
+    }
+  }
 }
 
 }  // namespace
