@@ -24,6 +24,11 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      gated on delivery callbacks). ``kafka_dialogues_per_s``: a pre-filled topic drained end to end
      (consume -> score -> produce -> commit); ``kafka_p50_ms`` / ``kafka_p95_ms``: per-message
      latency (broker append -> output delivered) under a paced producer at ``kafka_offered_per_s``.
+     Per GPU (rank 0's engine on its own broker; not summed over ranks). ``kafka_confluent_*``: the
+     same runs through clients restricted to the confluent_kafka surface (per-record Messages,
+     produce + delivery callback per record). ``kafka_multi_gpu_dialogues_per_s``: ONE 3-partition
+     topic drained by one engine fanning micro-batches out to a scorer per GPU (rank 0; a 1-GPU
+     job runs 2 scorers on the device as a rehearsal).
 Data is synthetic (the reference dataset is not available) with random-init-free trained trees.
 Before the timed training, an untimed 2-tree fit on 65,536 rows loads the kernels' code objects
 (lazily loaded on first launch by ROCm) and warms the allocators (``gbdt_warmup_sec_untimed``).
@@ -141,6 +146,42 @@ def warmup_training(dev, spec, params: GBDTParams, rf_depth: int = 0) -> None:
                       forest_subset="sqrt")
 
 
+def multi_gpu_kafka(args, spec, idf_np, model, dev, pool, make_engine) -> dict:
+    """BASELINE config 5's topology: ONE 3-partition topic drained by one engine (3 partition
+    readers -> one pinned ring) whose micro-batches go round-robin to a scorer per visible GPU
+    (stream/gpu_worker.py MultiGpuScorer). Run by rank 0 while the other ranks wait (their GPUs
+    are the scorers' devices); on a 1-GPU job two scorers share the device (a rehearsal of the
+    fan-out, not a multi-GPU number)."""
+    import gc
+
+    from fraud_detection_spark_kafka_llm_amd.stream import loadgen
+    from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import MultiGpuScorer
+
+    world = D.world_size()
+    out = {}
+    if D.rank() == 0:
+        n_dev = torch.cuda.device_count() if world > 1 else 1
+        devices = [torch.device("cuda", i) for i in range(min(n_dev, max(world, 1)))] if world > 1 else [dev, dev]
+        batch = 16384
+
+        def mk(consumers, producer, topic):
+            sc = MultiGpuScorer([GpuScorer(spec, idf_np, model.scorer(), d, max_docs=batch, max_bytes=batch * 4096,
+                                           depth=2) for d in devices])
+            return make_engine(sc, model.postprocess_numpy, consumers, producer, topic, batch_max=batch,
+                               max_latency_ms=5.0, max_bytes=batch * 4096)
+
+        gc.collect()
+        loadgen.throughput_run(mk, pool, 50_000, url="memory://bench-multi-warm")
+        gc.collect()
+        r = loadgen.throughput_run(mk, pool, args.kafka_multi_msgs, url="memory://bench-multi")
+        out = {"kafka_multi_gpu_dialogues_per_s": r["dialogues_per_s"],
+               "kafka_multi_gpu_n_devices": len({str(d) for d in devices}),
+               "kafka_multi_gpu_scorers": len(devices), "kafka_multi_gpu_msgs": args.kafka_multi_msgs,
+               "kafka_multi_gpu_all_committed": bool(r["committed"] == r["produced"] == args.kafka_multi_msgs)}
+    D.barrier()
+    return out
+
+
 def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
     """BASELINE config 5 on this rank's GPU against its own in-memory broker (3 partitions)."""
     import gc
@@ -166,11 +207,31 @@ def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
     lat = loadgen.latency_run(make(4096, 1.0), pool, args.kafka_rate, args.kafka_sec,
                               url=f"memory://bench-lat-{rank}")
     ok = tp["produced"] == args.kafka_msgs and tp["committed"] == args.kafka_msgs and lat["produced"] == lat["sent"]
-    return {"kafka_dialogues_per_s": tp["dialogues_per_s"], "kafka_msgs": args.kafka_msgs,
+    conf = {}
+    if args.kafka_confluent_msgs > 0:
+        # the same engine through clients restricted to the confluent_kafka surface (per-record
+        # Message objects on consume, one produce call + delivery callback per record): the path a
+        # librdkafka client takes. The in-memory broker's own per-record Python work is inside
+        # the timed region, as librdkafka's would be.
+        gc.collect()
+        ctp = loadgen.throughput_run(make(16384, 5.0), pool, args.kafka_confluent_msgs,
+                                     url=f"memory://bench-ctp-{rank}", confluent=True)
+        gc.collect()
+        clat = loadgen.latency_run(make(4096, 1.0), pool, args.kafka_confluent_rate, args.kafka_sec,
+                                   url=f"memory://bench-clat-{rank}", confluent=True)
+        ok = ok and ctp["produced"] == ctp["committed"] == args.kafka_confluent_msgs and \
+            clat["produced"] == clat["sent"]
+        conf = {"kafka_confluent_dialogues_per_s": ctp["dialogues_per_s"],
+                "kafka_confluent_msgs": args.kafka_confluent_msgs,
+                "kafka_confluent_p50_ms": clat["p50_ms"], "kafka_confluent_p95_ms": clat["p95_ms"],
+                "kafka_confluent_offered_per_s": args.kafka_confluent_rate}
+    multi = multi_gpu_kafka(args, spec, idf_np, model, dev, pool, make_engine=StreamingEngine) \
+        if args.kafka_multi_msgs > 0 else {}
+    return {**multi, "kafka_dialogues_per_s": tp["dialogues_per_s"], "kafka_msgs": args.kafka_msgs,
             "kafka_throughput_sec": tp["sec"], "kafka_p50_ms": lat["p50_ms"], "kafka_p95_ms": lat["p95_ms"],
             "kafka_p99_ms": lat["p99_ms"], "kafka_offered_per_s": args.kafka_rate,
             "kafka_latency_msgs": lat["sent"], "kafka_all_delivered_and_committed": bool(ok),
-            "kafka_avg_record_bytes": round(pool.avg_bytes, 1)}
+            "kafka_avg_record_bytes": round(pool.avg_bytes, 1), "kafka_api": "columnar (in-memory broker)", **conf}
 
 
 def main():
@@ -189,6 +250,12 @@ def main():
     ap.add_argument("--kafka-msgs", type=int, default=1_000_000, help="records drained in the Kafka throughput run")
     ap.add_argument("--kafka-rate", type=float, default=300_000, help="paced producer rate of the latency run")
     ap.add_argument("--kafka-sec", type=float, default=2.0, help="duration of the latency run")
+    ap.add_argument("--kafka-multi-msgs", type=int, default=1_000_000,
+                    help="records of the shared 3-partition topic drained by rank 0 over every GPU (0: skip)")
+    ap.add_argument("--kafka-confluent-msgs", type=int, default=300_000,
+                    help="records drained through the confluent_kafka-surface clients (0: skip)")
+    ap.add_argument("--kafka-confluent-rate", type=float, default=100_000,
+                    help="paced producer rate of the confluent-surface latency run")
     Config.add_cli_args(ap)          # --gbdt-max-bin, --seed, --config, ... (utils/config.py)
     args = ap.parse_args()
     cfg = Config.from_cli(args)
@@ -315,10 +382,11 @@ def main():
 
     kafka = kafka_phase(args, spec, idf_np, model, dev, rank) if args.kafka_msgs > 0 else {}
     if kafka:
-        kafka["kafka_dialogues_per_s"] = float(D.all_reduce_sum(
-            torch.tensor([kafka["kafka_dialogues_per_s"]], dtype=torch.float64, device=dev)).item())
-        for k in ("kafka_p50_ms", "kafka_p95_ms", "kafka_p99_ms"):
-            kafka[k] = max_over_ranks(kafka[k], dev)
+        # every rank drains its own broker with one GPU: reported per GPU (rank 0's engine), not
+        # summed -- the shared-topic -> N-GPU topology is kafka_multi_gpu_dialogues_per_s
+        for k in ("kafka_p50_ms", "kafka_p95_ms", "kafka_p99_ms", "kafka_confluent_p50_ms", "kafka_confluent_p95_ms"):
+            if k in kafka:
+                kafka[k] = max_over_ranks(kafka[k], dev)
 
     gbdt_peak_gb = max_over_ranks(gbdt_peak / 2 ** 30, dev)
     docs = args.steps * args.batch * world

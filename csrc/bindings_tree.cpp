@@ -1,5 +1,7 @@
 // pybind11 bindings of the tree engine (registered from bindings.cpp via register_tree_ops).
 #include <torch/extension.h>
+
+#include <cstdlib>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
@@ -514,6 +516,9 @@ void hist_blk(const Tensor& ent_row, const Tensor& ent_key, const Tensor& seg, i
   } else {
     FDX_CHECK(hist.size(1) >= TB, "hist stride smaller than the total bin count");
   }
+  const char* dbg = std::getenv("FDX_BLK_DBG");
+  a.dbg = dbg ? std::atoi(dbg) : 0;
+
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_hist_blk(a, (int)ct, stream(dev));

@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a)
     for (int32_t c = c0; c < c1; ++c) {
       const int32_t cd = c + kBlkDescBufs - 1;
       const BlkDescRegs dn = cd < c1 ? load_descs(a, cd, my_g) : BlkDescRegs{};
-      if (c + 1 < c1) stage_chunk<ROOT>(a, sh, (c - c0 + 1) & 1, c + 1, lane);   // overlaps chunk c
+      if (c + 1 < c1 && !(a.dbg & 4)) stage_chunk<ROOT>(a, sh, (c - c0 + 1) & 1, c + 1, lane);   // overlaps chunk c
       if (cd < c1) store_descs<ROOT>(sh, cd - c0, lane, nslots, dn);
       __syncthreads();
     }
@@ -415,12 +415,12 @@ __global__ __launch_bounds__(kBlkWaves * 64) void hist_blk_kernel(BlkHistArgs a)
       const bool work = now.n > 0 && cur < c1;
       // staged unconditionally (a step without work stages nothing live): every path consumes the
       // slot's loads before the slot is reloaded, so no path waits for younger loads
-      blk_stage_step<ROOT>(sh, (cur - c0) & 1, wid, lane, now.base, 0, work ? now.n : 0, rq[u], kq[u]);
+      if (!(a.dbg & 2)) blk_stage_step<ROOT>(sh, (cur - c0) & 1, wid, lane, now.base, 0, work ? now.n : 0, rq[u], kq[u]);
       ring[u] = blk_take<ROOT>(sh, walk, wid, gw, c0, c1, cur + kBlkDescBufs - 2);
       __builtin_amdgcn_sched_barrier(0);
       blk_load(a, ring[u], lane, rq[u], kq[u]);
       __builtin_amdgcn_sched_barrier(0);
-      if (work) {
+      if (work && !(a.dbg & 1)) {
         lds_sync();
         switch (now.j) {
 #define FDX_BLK_CASE(J) \

@@ -175,6 +175,9 @@ struct BlkHistArgs {
   int32_t nshards;                // 0: off(bin) = bin
   const int64_t* shard_lo;        // [nshards + 1]
   int64_t shard_stride;
+  // diagnostics (bench/probes/blk_probe.py; FDX_BLK_DBG, results wrong when set): bit 0 skips the
+  // K-steps, bit 1 the step staging, bit 2 the staging wave's row-state loads
+  int32_t dbg;
 };
 
 // histogram column offset of global bin b (shard-major DP layout or plain)

@@ -23,6 +23,7 @@ import time
 import zlib
 from collections import defaultdict
 from typing import Callable, Optional
+from zlib import crc32
 
 import numpy as np
 
@@ -227,6 +228,7 @@ class Broker:
         self.committed: dict = defaultdict(dict)    # group -> {(topic, part): next offset}
         self._errors: dict = defaultdict(int)
         self.cond = threading.Condition(self.lock)
+        self.waiting = 0          # consumers blocked in cond.wait (appends notify only then)
 
     def create_topic(self, name: str, partitions: int = 3) -> None:
         with self.lock:
@@ -243,16 +245,19 @@ class Broker:
         return (zlib.crc32(key) if key else zlib.crc32(value or b"")) % nparts
 
     def append(self, topic: str, key, value, partition: Optional[int] = None, want_message: bool = True):
+        """One record (the per-record ``produce`` path: kept to a few list appends under the lock)."""
         with self.lock:
             parts = self.topics.get(topic)
             if parts is None:
                 self.create_topic(topic)
                 parts = self.topics[topic]
             if partition is None or partition < 0:
-                partition = self._route(key, value, len(parts))
+                partition = (crc32(key) if key else crc32(value or b"")) % len(parts)
             off = parts[partition].append_one(key, value)
-            self.cond.notify_all()
-        return Message(topic, partition, off, key, value) if want_message else None
+            if self.waiting:
+                self.cond.notify_all()
+        return tuple.__new__(Message, (topic, partition, off, key, value, None, int(time.time() * 1000))) \
+            if want_message else None
 
     def append_records(self, topic: str, partition: int, keys, key_off, values, val_off, null_keys=None,
                        copy: bool = True) -> RecordBatch:
@@ -382,7 +387,11 @@ class Consumer:
         if now >= deadline:
             return False
         with self.broker.cond:
-            self.broker.cond.wait(timeout=min(0.05, deadline - now))
+            self.broker.waiting += 1
+            try:
+                self.broker.cond.wait(timeout=min(0.05, deadline - now))
+            finally:
+                self.broker.waiting -= 1
         return True
 
     def poll(self, timeout: float = -1) -> Optional[Message]:
@@ -493,7 +502,7 @@ class Producer:
             key = _b(key)
         if type(value) is not bytes and value is not None:
             value = _b(value)
-        m = None if err else self.broker.append(topic, key, value, partition, want_message=cb is not None)
+        m = None if err else self.broker.append(topic, key, value, partition, cb is not None)
         if cb is not None:
             self._pending.append((cb, err, m))     # list.append is atomic under the GIL
 

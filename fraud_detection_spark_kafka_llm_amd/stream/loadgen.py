@@ -94,28 +94,39 @@ class PacedProducer(threading.Thread):
             time.sleep(max(0.0, nxt - time.perf_counter()))
 
 
-def _consumers(url: str, topic: str, partitions: int, group: str) -> list:
+def _consumers(url: str, topic: str, partitions: int, group: str, confluent: bool = False) -> list:
     out = []
     for p in range(partitions):
         c = fake_kafka.Consumer({"bootstrap.servers": url, "group.id": group, "auto.offset.reset": "earliest",
                                  "enable.auto.commit": False})
         c.assign([fake_kafka.TopicPartition(topic, p)])
-        out.append(c)
+        out.append(fake_kafka.ConfluentConsumer(c) if confluent else c)
     return out
 
 
+def _producer(url: str, confluent: bool):
+    p = fake_kafka.Producer({"bootstrap.servers": url})
+    return fake_kafka.ConfluentProducer(p) if confluent else p
+
+
+def _committed(consumers: list) -> int:
+    c = consumers[0]
+    return sum(getattr(c, "_inner", c).committed_offsets().values())
+
+
 def throughput_run(make_engine: Callable, pool: MessagePool, n: int, partitions: int = 3,
-                   url: str = "memory://loadgen-tp") -> dict:
-    """``make_engine(consumers, producer, output_topic)`` -> StreamingEngine."""
+                   url: str = "memory://loadgen-tp", confluent: bool = False) -> dict:
+    """``make_engine(consumers, producer, output_topic)`` -> StreamingEngine. ``confluent``: the
+    clients expose only the confluent_kafka surface (per-record Messages and produce calls)."""
     broker = fake_kafka.broker_for(url)
     prefill(broker, "in", pool, n, partitions)
     broker.create_topic("out", partitions)
-    consumers = _consumers(url, "in", partitions, "tp")
-    eng = make_engine(consumers, fake_kafka.Producer({"bootstrap.servers": url}), "out")
+    consumers = _consumers(url, "in", partitions, "tp", confluent)
+    eng = make_engine(consumers, _producer(url, confluent), "out")
     t0 = time.perf_counter()
     st = eng.run(max_messages=n, idle_timeout_s=5.0)
     dt = time.perf_counter() - t0
-    committed = sum(consumers[0].committed_offsets().values())
+    committed = _committed(consumers)
     out_n = broker.size("out")
     _drop(url)
     return {"dialogues_per_s": n / dt, "sec": dt, "messages": st["messages"], "produced": st["produced"],
@@ -124,12 +135,12 @@ def throughput_run(make_engine: Callable, pool: MessagePool, n: int, partitions:
 
 
 def latency_run(make_engine: Callable, pool: MessagePool, rate: float, duration_s: float, partitions: int = 3,
-                url: str = "memory://loadgen-lat", warmup_s: float = 0.3) -> dict:
+                url: str = "memory://loadgen-lat", warmup_s: float = 0.3, confluent: bool = False) -> dict:
     broker = fake_kafka.broker_for(url)
     broker.create_topic("in", partitions)
     broker.create_topic("out", partitions)
-    consumers = _consumers(url, "in", partitions, "lat")
-    eng = make_engine(consumers, fake_kafka.Producer({"bootstrap.servers": url}), "out")
+    consumers = _consumers(url, "in", partitions, "lat", confluent)
+    eng = make_engine(consumers, _producer(url, confluent), "out")
     gen = PacedProducer(broker, "in", pool, rate, duration_s + warmup_s, partitions)
     res = {}
 
@@ -145,7 +156,7 @@ def latency_run(make_engine: Callable, pool: MessagePool, rate: float, duration_
     res.update({"offered_per_s": rate, "sent": gen.sent, "messages": st["messages"], "produced": st["produced"],
                 "p50_ms": st["p50_ms"], "p95_ms": st["p95_ms"], "p99_ms": st["p99_ms"],
                 "p50_batch_ms": st["p50_batch_ms"], "batches": st["batches"], "sec": time.perf_counter() - t0,
-                "committed": sum(consumers[0].committed_offsets().values())})
+                "committed": _committed(consumers)})
     _drop(url)
     return res
 
