@@ -67,6 +67,7 @@ from fraud_detection_spark_kafka_llm_amd.parallel.affinity import bind_to_gpu  #
 from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.utils.config import Config  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.utils.profiling import run_profiled_if_requested  # noqa: E402
 
 METRIC = "dialogues/sec streaming inference + GBDT train sec on 10M rows, 1/2/4/8 GPU"
 F = 1 << 18
@@ -259,6 +260,7 @@ def main():
     Config.add_cli_args(ap)          # --gbdt-max-bin, --seed, --config, ... (utils/config.py)
     args = ap.parse_args()
     cfg = Config.from_cli(args)
+    run_profiled_if_requested(cfg.profile)    # --profile: re-run under rocprofv3 (GPU untouched so far)
 
     D.init_from_env(os.environ.get("FDX_DIST_BACKEND", "nccl"))   # gloo: rehearse N ranks on one GPU
     rank, world = D.rank(), D.world_size()

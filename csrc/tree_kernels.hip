@@ -494,16 +494,21 @@ __global__ __launch_bounds__(256) void hist_dense_kernel(DenseHistArgs a) {
 }
 
 // ------------------------------------------------------------------ sibling subtraction
+// grid.y = pair (node triple), grid.x strides the pair's 2 TB int64 sums with 16-byte accesses:
+// no per-element 64-bit div/mod. A padded triple (dst < 0, device level loop) exits at once.
 __global__ __launch_bounds__(256) void hist_subtract_kernel(const int64_t* parent_hist, int64_t* cur_hist,
                                                             const int32_t* dst, const int32_t* par,
                                                             const int32_t* sib, int32_t n_pairs, int64_t TB) {
-  const int64_t per = TB * 2;
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < (int64_t)n_pairs * per;
-       t += (int64_t)gridDim.x * 256) {
-    const int p = (int)(t / per);
-    const int64_t k = t % per;
-    if (dst[p] < 0) continue;                 // padded triple (device level loop)
-    cur_hist[(int64_t)dst[p] * per + k] = parent_hist[(int64_t)par[p] * per + k] - cur_hist[(int64_t)sib[p] * per + k];
+  const int p = blockIdx.y;
+  const int32_t d = dst[p];
+  if (d < 0) return;
+  const int64_t per = TB;                     // (g, h) pairs = 16 B each
+  const longlong2* src = reinterpret_cast<const longlong2*>(parent_hist) + (int64_t)par[p] * per;
+  const longlong2* sb = reinterpret_cast<const longlong2*>(cur_hist) + (int64_t)sib[p] * per;
+  longlong2* out = reinterpret_cast<longlong2*>(cur_hist) + (int64_t)d * per;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < per; k += (int64_t)gridDim.x * 256) {
+    const longlong2 a = src[k], b = sb[k];
+    out[k] = make_longlong2(a.x - b.x, a.y - b.y);
   }
 }
 
@@ -920,8 +925,9 @@ void launch_hist_dense(const DenseHistArgs& a, int bt, int ct, int np, hipStream
 void launch_hist_subtract(const int64_t* parent, int64_t* cur, const int32_t* dst, const int32_t* par, const int32_t* sib,
                           int32_t n_pairs, int64_t TB, hipStream_t s) {
   if (n_pairs <= 0 || TB <= 0) return;
-  hipLaunchKernelGGL(hist_subtract_kernel, dim3(grid_for((int64_t)n_pairs * TB * 2)), dim3(256), 0, s, parent, cur,
-                     dst, par, sib, n_pairs, TB);
+  const int64_t bx = (TB + 255) / 256;
+  hipLaunchKernelGGL(hist_subtract_kernel, dim3((unsigned)(bx < 1024 ? bx : 1024), (unsigned)n_pairs), dim3(256), 0, s,
+                     parent, cur, dst, par, sib, n_pairs, TB);
 }
 
 void launch_split(const SplitArgs& a, hipStream_t s) {

@@ -24,6 +24,7 @@ from http.server import BaseHTTPRequestHandler, HTTPServer
 import torch
 
 from ..utils.config import Config, load_dotenv
+from ..utils.profiling import run_profiled_if_requested
 from ..utils.metrics import REGISTRY
 from .kafka import DEFAULT_OUTPUT, get_kafka_consumer, get_kafka_producer, get_partition_consumers
 
@@ -72,6 +73,7 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     load_dotenv()
     cfg = Config.from_cli(args)
+    run_profiled_if_requested(cfg.profile, argv, module="fraud_detection_spark_kafka_llm_amd.stream.serve")
     args.batch = args.batch if args.batch is not None else cfg.stream_batch
     args.max_latency_ms = args.max_latency_ms if args.max_latency_ms is not None else cfg.stream_max_latency_ms
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")

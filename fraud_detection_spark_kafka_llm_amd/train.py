@@ -32,6 +32,7 @@ from .ml.xgboost import SparkXGBClassifier
 from .ops.sparse import term_presence_by_label
 from .session import SparkSession
 from .utils.config import Config
+from .utils.profiling import run_profiled_if_requested
 from .utils.logging import get_logger
 
 DATA_URL = ("https://huggingface.co/datasets/BothBosu/multi-agent-scam-conversation/raw/main/"
@@ -171,6 +172,7 @@ def main(argv=None) -> dict:
     Config.add_cli_args(ap)          # --num-trees, --max-depth, --vocab-size, --seed, --device, --config ...
     args = ap.parse_args(argv)
     cfg = Config.from_cli(args)
+    run_profiled_if_requested(cfg.profile, argv, module="fraud_detection_spark_kafka_llm_amd.train")
     args.num_trees, args.max_depth, args.vocab_size, args.seed = cfg.num_trees, cfg.max_depth, cfg.vocab_size, cfg.seed
 
     spark = initialize_spark()
