@@ -16,6 +16,7 @@ import torch
 from fraud_detection_spark_kafka_llm_amd.data import synth
 from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
 from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH
+from fraud_detection_spark_kafka_llm_amd.models import grower
 from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
 from fraud_detection_spark_kafka_llm_amd.ops import text as T
 from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order
@@ -23,7 +24,7 @@ from fraud_detection_spark_kafka_llm_amd.utils import tracing
 
 
 def build_features(rows: int, dev, chunk: int = 500_000, num_features: int = 1 << 18, seed: int = 11,
-                   first_row: int = 0):
+                   first_row: int = 0, tail_words: int = 30000):
     spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=num_features)
     ptrs, idxs, vals, labels = [], [], [], []
     t_gen = t_feat = 0.0
@@ -31,7 +32,8 @@ def build_features(rows: int, dev, chunk: int = 500_000, num_features: int = 1 <
     for start in range(0, rows, chunk):
         n = min(chunk, rows - start)
         t0 = time.perf_counter()
-        pt, y = synth.generate(synth.SynthConfig(n=n, seed=seed), device=dev, start=first_row + start)
+        pt, y = synth.generate(synth.SynthConfig(n=n, seed=seed, tail_words=tail_words), device=dev,
+                               start=first_row + start)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         res = T.featurize_score(pt, spec, want_csr=True, device=dev)
@@ -59,6 +61,8 @@ def main():
     ap.add_argument("--trees", type=int, default=20)
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--trace", default="")
+    ap.add_argument("--tail-words", type=int, default=30000,
+                    help="synthetic long-tail vocabulary (1000000: >200K active features of 2^18)")
     ap.add_argument("--no-warmup", action="store_true", help="skip the untimed warm-up fit (models/warmup.py)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -72,7 +76,7 @@ def main():
     if args.trace:
         tracing.enable(args.trace)
     t0 = time.perf_counter()
-    indptr, idx, counts, y, t_gen, t_feat = build_features(args.rows, dev)
+    indptr, idx, counts, y, t_gen, t_feat = build_features(args.rows, dev, tail_words=args.tail_words)
     t1 = time.perf_counter()
     F = 1 << 18
     fo = feature_order(indptr, idx, counts, F)
@@ -80,11 +84,19 @@ def main():
     vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
+    torch.cuda.reset_peak_memory_stats(dev)
+    for k in grower.LEVEL_STATS:
+        grower.LEVEL_STATS[k] = 0
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)
     t3 = time.perf_counter()
+    ls = grower.LEVEL_STATS
     print(json.dumps({"rows": args.rows, "nnz": int(idx.numel()), "trees": args.trees, "depth": args.depth,
+                      "tail_words": args.tail_words, **res.shape,
                       "gen_s": t_gen, "featurize_s": t_feat, "idf_s": t2 - t1, "gbdt_total_s": res.train_seconds,
                       "per_tree_ms": (t3 - t2) / args.trees * 1e3, "wall_s": t3 - t0,
+                      "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
+                      "built_nodes_per_level": ls["built_nodes"] / max(ls["levels"], 1),
+                      "dp_hist_bytes_per_level": ls["hist_bytes"] / max(ls["levels"], 1),
                       "nodes_tree0": res.trees[0].num_nodes}))
 
 

@@ -3,10 +3,10 @@
   dt_cpu    DecisionTree pipeline on a 1,600-row dialogue CSV stand-in, CPU only (train.py flow)
   gbdt_1m   HashingTF(2^18) -> IDF -> GBDT (100 trees, depth 6) on 1M synthetic dialogues, 1 GPU;
             train seconds + held-out accuracy / weighted F1 / AUC
-  rf        RandomForest (500 trees, depth 5, sqrt features, Poisson bootstrap) on --rows rows
-            (default 10M = the BASELINE config's total on one GPU)
-  xgb       XGBoost-compatible GBDT with 1000 trees on --rows rows (default 12.5M = one rank's
-            shard of the 100M-row DP=8 config); train seconds + peak HBM
+  rf        RandomForest (500 trees, depth 5, sqrt features, Poisson bootstrap) on --rows GLOBAL
+            rows (default 10M), row-sharded over torchrun ranks
+  xgb       XGBoost-compatible GBDT with 1000 trees on --rows GLOBAL rows (default 12.5M per rank:
+            100M at DP=8), row-sharded over torchrun ranks; train seconds + peak HBM
   kafka     in-memory Kafka topic with 3 partitions -> StreamingEngine (pinned ring -> GPU fused
             featurize+score) -> output topic, with explanations from the stub LLM; dialogues/s and
             p50 / p95 batch latency
@@ -14,6 +14,7 @@
 Data are synthetic (data/synth.py); weights are trained, not random. Each GPU bench first runs an
 untimed 2-tree warm-up fit (models/warmup.py: lazy kernel code-object loading). Usage:
   python bench/suite.py {dt_cpu,gbdt_1m,rf,xgb,kafka,all} [--rows N] [--trees T]
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/suite.py xgb
 """
 import argparse
 import json
@@ -54,6 +55,46 @@ def _tfidf(rows, dev, seed, first_row=0, idf=None):
     return vc, y, idf
 
 
+def _dist():
+    """(rank, world, device): torchrun ranks (RANK/WORLD_SIZE in the environment) join one
+    process group (RCCL; FDX_DIST_BACKEND=gloo rehearses ranks on one GPU), one GPU each."""
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    D.init_from_env(os.environ.get("FDX_DIST_BACKEND", "nccl"))     # no-op at WORLD_SIZE 1 / when done
+    dev = torch.device("cuda", D.local_rank() % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    return D.rank(), D.world_size(), dev
+
+
+def _shard_tfidf(rows_global: int, dev, seed: int):
+    """This rank's contiguous row shard of ``rows_global`` synthetic dialogues; the IDF comes from
+    the all-reduced document frequencies (global, as one process over all rows computes it)."""
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    rank, world = D.rank(), D.world_size()
+    lo, hi = rows_global * rank // world, rows_global * (rank + 1) // world
+    indptr, idx, counts, y, _, _ = build_features(hi - lo, dev, seed=seed, first_row=lo)
+    fo = feature_order(indptr, idx, counts, F)
+    df = D.all_reduce_sum(fo.df) if world > 1 else fo.df
+    idf = torch.log((rows_global + 1.0) / (df.double() + 1.0))
+    return VectorColumn.tfidf(F, indptr, idx, counts, idf, fo), y, idf
+
+
+def _max_over_ranks(x: float, dev) -> float:
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    if D.world_size() == 1:
+        return x
+    return float(D.all_reduce_max(torch.tensor([x], dtype=torch.float64, device=dev)).item())
+
+
+def _sync(dev):
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    torch.cuda.synchronize(dev)
+    D.barrier()
+
+
 def bench_dt_cpu(args) -> dict:
     from fraud_detection_spark_kafka_llm_amd import train
 
@@ -90,48 +131,57 @@ def bench_gbdt_1m(args) -> dict:
 
 
 def bench_rf(args) -> dict:
+    """BASELINE config 3: --rows is the GLOBAL row count (default 10M), row-sharded over the
+    torchrun ranks; trees equal the single-process forest (exact histograms, tests/test_distributed.py)."""
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
 
-    dev = torch.device("cuda:0")
+    rank, world, dev = _dist()
     rows = args.rows or 10_000_000
     trees = args.trees or 500
     warm_tree_kernels(dev, gbdt_depth=0, forest_depth=5, forest_subset=args.subset)
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
-    vc, y, idf = _tfidf(rows, dev, seed=21)
-    torch.cuda.synchronize()
+    vc, y, idf = _shard_tfidf(rows, dev, seed=21)
+    _sync(dev)
     t_feat = time.perf_counter() - t0
+    torch.cuda.reset_peak_memory_stats(dev)
     res = fit_forest(vc, y, num_trees=trees, max_depth=5, max_bins=32, bootstrap=True, feature_subset=args.subset,
                      seed=42, device=dev)
-    torch.cuda.synchronize()
+    _sync(dev)
     t_train = time.perf_counter() - t0
-    tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
-    raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()
-    p1 = raw[:, 1] / np.maximum(raw.sum(1), 1e-300)
-    return {"bench": "rf", "rows": rows, "trees": trees, "depth": 5, "subset": args.subset, "featurize_s": t_feat,
-            "train_s": t_train,
-            "train_only_s": t_train - t_feat,
-            "peak_hbm_gb": torch.cuda.max_memory_allocated() / 2 ** 30, "heldout_rows": 200_000,
-            **_metrics(ty.cpu().numpy(), p1, (raw[:, 1] > raw[:, 0]).astype(float))}
+    out = {"bench": "rf", "rows": rows, "world": world, "rows_per_rank": len(vc), "trees": trees, "depth": 5,
+           "subset": args.subset, "featurize_s": _max_over_ranks(t_feat, dev),
+           "train_s": _max_over_ranks(t_train, dev), "train_only_s": _max_over_ranks(t_train - t_feat, dev),
+           "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}
+    if rank == 0:
+        tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
+        raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()
+        p1 = raw[:, 1] / np.maximum(raw.sum(1), 1e-300)
+        out.update({"heldout_rows": 200_000, **_metrics(ty.cpu().numpy(), p1, (raw[:, 1] > raw[:, 0]).astype(float))})
+    return out
 
 
 def bench_xgb(args) -> dict:
+    """BASELINE config 4: --rows is the GLOBAL row count (default 12.5M x ranks, so each GPU holds a
+    12.5M-row shard: 100M rows at DP=8); histograms are reduce-scattered per level."""
     from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
 
-    dev = torch.device("cuda:0")
-    rows = args.rows or 12_500_000
+    rank, world, dev = _dist()
+    rows = args.rows or 12_500_000 * world
     trees = args.trees or 1000
     warm_tree_kernels(dev)
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
-    vc, y, idf = _tfidf(rows, dev, seed=31)
-    torch.cuda.synchronize()
+    vc, y, idf = _shard_tfidf(rows, dev, seed=31)
+    _sync(dev)
     t_feat = time.perf_counter() - t0
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=trees, max_depth=6), device=dev)
-    torch.cuda.synchronize()
+    _sync(dev)
     t_train = time.perf_counter() - t0
-    return {"bench": "xgb", "rows": rows, "trees": trees, "depth": 6, "featurize_s": t_feat, "train_s": t_train,
-            "per_tree_ms": (t_train - t_feat) / trees * 1e3, "peak_hbm_gb": torch.cuda.max_memory_allocated() / 2 ** 30}
+    return {"bench": "xgb", "rows": rows, "world": world, "rows_per_rank": len(vc), "trees": len(res.trees),
+            "depth": 6, "featurize_s": _max_over_ranks(t_feat, dev), "train_s": _max_over_ranks(t_train, dev),
+            "per_tree_ms": _max_over_ranks((t_train - t_feat) / trees * 1e3, dev),
+            "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}
 
 
 def bench_kafka(args) -> dict:
@@ -204,7 +254,9 @@ def main():
     ap.add_argument("--subset", default="sqrt", help="rf: featureSubsetStrategy")
     args = ap.parse_args()
     for name in (list(BENCHES) if args.which == "all" else [args.which]):
-        print(json.dumps(BENCHES[name](args)), flush=True)
+        res = BENCHES[name](args)
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

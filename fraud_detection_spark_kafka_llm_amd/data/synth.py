@@ -15,6 +15,7 @@ on the GPU for the 10M-row benchmark configuration.
 """
 from __future__ import annotations
 
+import functools
 from dataclasses import dataclass
 from typing import Optional
 
@@ -47,8 +48,13 @@ checkin hotel booking balance statement question recipe catalog volunteer charit
 TAGS = ["Innocent:", "Suspect:"]
 
 
+@functools.lru_cache(maxsize=4)
 def _tail_words(n: int = 30000, seed: int = 7) -> list:
-    """Deterministic long-tail pseudo-words (names, places, rare terms) from syllables."""
+    """Deterministic long-tail pseudo-words (names, places, rare terms) from syllables; the first
+    30,000 are the same for every ``n`` (a wider vocabulary extends the default one)."""
+    if n > 30000 and seed == 7:
+        base = _tail_words(30000, 7)
+        return base + _more_words(n - len(base), set(base))
     rng = np.random.default_rng(seed)
     syl = ["ka", "lo", "mi", "ren", "sta", "vi", "dor", "el", "an", "tor", "bri", "qu", "zen", "mar", "po",
            "li", "son", "ber", "ga", "ni", "ro", "che", "ty", "wen", "ha", "lu", "fe", "dra", "is", "om"]
@@ -58,6 +64,27 @@ def _tail_words(n: int = 30000, seed: int = 7) -> list:
         if w not in seen:
             seen.add(w)
             out.append(w)
+    return out
+
+
+def _more_words(n: int, seen: set) -> list:
+    """``n`` further distinct pseudo-words (6-9 syllables from a wider syllable set)."""
+    rng = np.random.default_rng(1234)
+    syl = np.array(["ka", "lo", "mi", "ren", "sta", "vi", "dor", "el", "an", "tor", "bri", "qu", "zen", "mar",
+                    "po", "li", "son", "ber", "ga", "ni", "ro", "che", "ty", "wen", "ha", "lu", "fe", "dra", "is",
+                    "om", "xu", "jo", "pe", "sku", "ta", "vo", "gri", "ny", "bo", "ze"])
+    out = []
+    while len(out) < n:
+        k = max(2 * (n - len(out)), 1024)
+        lens = rng.integers(6, 10, k)
+        picks = rng.integers(0, len(syl), (k, 9))
+        for row, ln in zip(picks, lens):
+            w = "".join(syl[row[:ln]])
+            if w not in seen:
+                seen.add(w)
+                out.append(w)
+                if len(out) == n:
+                    break
     return out
 
 
@@ -79,14 +106,17 @@ class SynthConfig:
     p_hard: float = 0.03        # fraction of low-signal dialogues
     hard_scale: float = 0.03
     p_tail: float = 0.12        # long-tail vocabulary share (sets the feature-space width)
+    tail_words: int = 30000     # long-tail vocabulary size: 30K -> ~28K active of 2^18 buckets at
+                                # 10M rows; 1M -> >200K active (a realistic wide vocabulary)
 
 
 class _Vocab:
-    def __init__(self, device):
-        words = TAGS + COMMON + SCAM + BENIGN + TAIL
+    def __init__(self, device, tail_words: int = 30000):
+        tail = TAIL if tail_words == len(TAIL) else _tail_words(tail_words)
+        words = TAGS + COMMON + SCAM + BENIGN + tail
         enc = [w.encode() for w in words]
         self.n_tags, self.n_common, self.n_scam, self.n_benign = len(TAGS), len(COMMON), len(SCAM), len(BENIGN)
-        self.n_tail = len(TAIL)
+        self.n_tail = len(tail)
         lens = torch.tensor([len(b) for b in enc], dtype=torch.int64)
         self.lens = lens.to(device)
         self.off = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lens, 0)[:-1]]).to(device)
@@ -97,6 +127,16 @@ class _Vocab:
         self.sep_bytes = torch.from_numpy(np.frombuffer(b"".join(senc), dtype=np.uint8).copy()).to(device)
 
 
+_VOCABS: dict = {}
+
+
+def _vocab(device: torch.device, tail_words: int) -> _Vocab:
+    key = (str(device), tail_words)
+    if key not in _VOCABS:
+        _VOCABS[key] = _Vocab(device, tail_words)
+    return _VOCABS[key]
+
+
 def generate(cfg: SynthConfig = SynthConfig(), device="cpu", start: int = 0) -> tuple[PackedText, torch.Tensor]:
     """Generate dialogues ``start .. start+n`` of the stream seeded by ``cfg.seed``.
 
@@ -105,7 +145,7 @@ def generate(cfg: SynthConfig = SynthConfig(), device="cpu", start: int = 0) -> 
     and the same (seed, start, n) always yields identical bytes on any device.
     """
     device = torch.device(device)
-    V = _Vocab(device)
+    V = _vocab(device, cfg.tail_words)
     n = cfg.n
     g = torch.Generator(device="cpu").manual_seed(int(cfg.seed) * 1_000_003 + int(start))
     # per-doc draws (host RNG for determinism across devices; tiny)

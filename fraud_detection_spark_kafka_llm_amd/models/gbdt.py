@@ -60,6 +60,7 @@ class GBDTResult:
     params: GBDTParams
     history: list = field(default_factory=list)
     train_seconds: float = 0.0
+    shape: dict = field(default_factory=dict)     # Fa, TB, nnz of this rank's quantized features
 
 
 def _logit(p: float) -> float:
@@ -152,7 +153,8 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
         trees.append(pending.result().compacted())
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
-    return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0)
+    return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0,
+                      {"Fa": Q.Fa, "TB": Q.TB, "nnz": int(Q.csc_row.numel())})
 
 
 def train_margin_logloss(margin: torch.Tensor, y: torch.Tensor) -> float:

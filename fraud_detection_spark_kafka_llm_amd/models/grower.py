@@ -59,7 +59,10 @@ HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
 # levels that build at most BLK_MAX_SLOTS node slots (GBDT) take the row-blocked histogram pass
 # (models/quantize.BlockedCSC, csrc/blk_kernels.hip): row state staged in LDS per 4096-row chunk
 # instead of a global gather per entry (FDX_BLK=0: the CSC / dense passes at every level)
-BLK = os.environ.get("FDX_BLK", "1") != "0"
+# device level loop counters (bench/gbdt_train.py reports the histogram payload per level: what a
+# data-parallel level reduce-scatters, before the 1/S shard split)
+LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0}
+BLK = os.environ.get("FDX_BLK", "0") == "1"      # row-blocked pass: opt-in until it beats the CSC passes
 BLK_MAX_SLOTS = 4
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
@@ -737,6 +740,9 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             n_open, n_build = int(cnt[1]), int(cnt[2])
             if n_open == 0:
                 break
+        LEVEL_STATS["levels"] += 1
+        LEVEL_STATS["built_nodes"] += n_build
+        LEVEL_STATS["hist_bytes"] += n_build * TB * 16          # (g, h) int64 partials of the built nodes
         open_d, totals_d = st.open[cur][:n_open], st.totals[cur][:n_open]
         n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
         if shards is None:

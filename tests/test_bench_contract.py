@@ -11,7 +11,9 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
-TINY = ["--steps", "4", "--warmup", "2", "--rows", "100000", "--trees", "3", "--batch", "4096", "--pool", "2"]
+TINY = ["--steps", "4", "--warmup", "2", "--rows", "100000", "--trees", "3", "--batch", "4096", "--pool", "2",
+        "--rf-trees", "4", "--kafka-msgs", "20000", "--kafka-sec", "0.5", "--kafka-multi-msgs", "20000",
+        "--kafka-confluent-msgs", "5000", "--kafka-confluent-rate", "5000"]
 
 
 def _json_line(out: str) -> dict:
@@ -26,6 +28,9 @@ def _check(rec: dict, n: int):
     assert rec["value"] > 0 and rec["ms_per_step"] > 0 and rec["higher_is_better"] is True
     assert rec["config"]["parallelism"] == f"dp{n}" and rec["config"]["global_batch"] == 4096 * n
     assert rec["stream_accuracy"] > 0.9
+    assert rec["rf_train_sec"] > 0 and rec["rf_trees"] == 4
+    assert rec["kafka_confluent_dialogues_per_s"] > 0 and rec["kafka_multi_gpu_dialogues_per_s"] > 0
+    assert rec["kafka_all_delivered_and_committed"] and rec["kafka_multi_gpu_all_committed"]
 
 
 @pytest.mark.gpu
@@ -44,3 +49,20 @@ def test_bench_two_ranks_contract_gloo_rehearsal():
                          cwd=REPO, capture_output=True, text=True, timeout=900, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     _check(_json_line(out.stdout), 2)
+
+
+@pytest.mark.gpu
+def test_suite_xgb_and_rf_two_ranks_gloo_rehearsal():
+    """bench/suite.py xgb / rf under torchrun: --rows is global, row-sharded, one JSON line."""
+    env = {**os.environ, "FDX_DIST_BACKEND": "gloo"}
+    for which, port in (("xgb", "29549"), ("rf", "29551")):
+        out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                              "--master-addr", "127.0.0.1", "--master-port", port, "bench/suite.py", which,
+                              "--rows", "60000", "--trees", "3"], cwd=REPO, capture_output=True, text=True,
+                             timeout=900, env=env)
+        assert out.returncode == 0, out.stderr[-3000:]
+        lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, out.stdout[-2000:]
+        rec = json.loads(lines[0])
+        assert rec["bench"] == which and rec["world"] == 2 and rec["rows"] == 60000
+        assert rec["rows_per_rank"] == 30000 and rec["train_s"] > 0 and rec["trees"] == 3

@@ -573,6 +573,22 @@ def test_gpu_device_level_loop_equals_gpu_host_loop(monkeypatch):
     _same_trees(out[False][1], out[True][1])
 
 
+@pytest.mark.gpu
+def test_gpu_blocked_pass_in_the_level_loop_grows_the_same_trees(monkeypatch):
+    """FDX_BLK=1 (models/grower.py BLK): the levels building <= 4 node slots run the row-blocked
+    histogram pass; the GBDT trees are the CSC passes' trees, bit for bit."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+
+    dense, y = random_counts_matrix(9000, 150, 0.15, 61)
+    dense[:, :4] = np.random.default_rng(6).integers(0, 9, (9000, 4))
+    vc = vc_from_dense(dense)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(grower, "BLK", flag)
+        out[flag] = fit_gbdt(vc, torch.from_numpy(y), GBDTParams(n_estimators=4, max_depth=6), device="cuda:0").trees
+    _same_trees(out[False], out[True])
+
+
 @pytest.mark.parametrize("max_delta_step", [0.0, 0.7])
 def test_deferred_tree_build_equals_immediate(max_delta_step):
     """GBDT without per-round hooks builds tree t's host table during tree t + 1 and updates the
