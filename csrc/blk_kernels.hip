@@ -181,6 +181,9 @@ __device__ __forceinline__ void blk_ksteps(BlkShared<ROOT>& sh, int wid, int lan
   const int slot_sub = r / 8, q = r % 8;                 // NP = 4: 8 columns per slot, 2 slots per tile
   const int32_t span = n - base < 256 ? n - base : 256;
   const int nks = (span + 63) >> 6;
+  // rolled: unrolling it (nks <= 4) removed the accumulator copies around each step but raised the
+  // register pressure until the entry-load ring lost its static registers (every load then waited
+  // for vmcnt(0): 3.5x slower end to end, profiles/r3/NOTES.md)
 #pragma unroll 1
   for (int ks = 0; ks < nks; ++ks) {
     const int32_t lo = base + 64 * ks > 0 ? base + 64 * ks : 0;          // first live entry (segment-relative)
