@@ -383,7 +383,8 @@ void feature_order(const Tensor& indptr, const Tensor& idx, const Tensor& counts
   FDX_CHECK(indptr.is_contiguous() && idx.is_contiguous() && counts.is_contiguous(), "contiguous inputs");
   if (counts.scalar_type() == at::kFloat) feature_order_t<float>(indptr, idx, counts, F, csc_row, csc_cnt, colptr, df, maxc);
   else if (counts.scalar_type() == at::kDouble) feature_order_t<double>(indptr, idx, counts, F, csc_row, csc_cnt, colptr, df, maxc);
-  else FDX_CHECK(false, "counts must be float32 or float64");
+  else if (counts.scalar_type() == at::kInt) feature_order_t<int32_t>(indptr, idx, counts, F, csc_row, csc_cnt, colptr, df, maxc);
+  else FDX_CHECK(false, "counts must be int32, float32 or float64");
 }
 
 // out = min(in, maxv) over uint8 (bin clamp of the count path); in/out 16-byte aligned on the device

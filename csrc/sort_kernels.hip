@@ -212,5 +212,6 @@ void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, h
 
 template void launch_feature_order<float>(const FeatureOrderArgs<float>&, hipStream_t);
 template void launch_feature_order<double>(const FeatureOrderArgs<double>&, hipStream_t);
+template void launch_feature_order<int32_t>(const FeatureOrderArgs<int32_t>&, hipStream_t);
 
 }  // namespace fdx

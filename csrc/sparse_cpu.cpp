@@ -146,5 +146,6 @@ void copy_segments_cpu(const int32_t* src_row, const uint8_t* src_key, const int
 
 template void feature_order_cpu<float>(const FeatureOrderArgs<float>&);
 template void feature_order_cpu<double>(const FeatureOrderArgs<double>&);
+template void feature_order_cpu<int32_t>(const FeatureOrderArgs<int32_t>&);
 
 }  // namespace fdx

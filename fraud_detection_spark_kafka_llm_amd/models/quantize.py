@@ -295,7 +295,6 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
     dev = indptr.device
     N = int(indptr.numel() - 1)
     F = int(vc.size)
-    idx64 = idx.to(torch.int64)
     val64 = val.to(torch.float64) if val is not None else None
     if counts is None and val64.numel() and bool(torch.all(val64 >= 0)) and bool(torch.all(val64 == torch.round(val64))) \
             and float(val64.max()) < 65536:
@@ -306,6 +305,7 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
         with tracing.span("q.items"):
             _finish_items(Q, chunk, super_rows or SUPER_ROWS, HOT_DENSITY if hot_density is None else hot_density)
         return Q
+    idx64 = idx.to(torch.int64)      # generic path only (8 B per entry: never on the count path)
     with tracing.span("q.rows"):
         row = torch.repeat_interleave(torch.arange(N, device=dev, dtype=torch.int32), (indptr[1:] - indptr[:-1]),
                                       output_size=int(idx.numel()))

@@ -1,7 +1,9 @@
 """Sparse ops over ``VectorColumn`` CSR data (native: ``csrc/sparse_kernels.hip`` / ``sparse_cpu.cpp``)."""
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
+from typing import Optional
 
 import torch
 
@@ -90,20 +92,68 @@ class FeatureOrder:
     maxc: torch.Tensor
 
 
-def feature_order(indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor, num_features: int) -> FeatureOrder:
-    """CSR (rows, sorted unique feature ids per row, term counts) -> CSC by feature with a native
-    radix sort; docFreq and the per-feature max count are segmented reductions (no atomics)."""
-    C = native.lib()
+# entries radix-sorted at once by feature_order: the device sort needs 24 B of temporaries per
+# entry, so a 1.25B-entry shard sorts in row blocks of this size (each block's columns are copied
+# into place; rows stay in row order within every column, exactly the one-shot CSC)
+FO_BLOCK_ENTRIES = int(os.environ.get("FDX_FO_BLOCK_ENTRIES", 1 << 28))
+
+
+def _feature_order_one(indptr, idx, counts, num_features: int, row_buf, cnt_buf) -> tuple:
     dev = idx.device
     nnz = int(idx.numel())
-    if not counts.is_floating_point():      # integer term counts (exact in fp32 below 2^24)
-        counts = counts.to(torch.float32)
-    pad = 16
-    row_buf = torch.zeros(nnz + pad, dtype=torch.int32, device=dev)
-    cnt_buf = torch.zeros(nnz + pad, dtype=torch.uint8, device=dev)
     colptr = torch.empty(num_features + 1, dtype=torch.int64, device=dev)
     df = torch.empty(num_features, dtype=torch.int64, device=dev)
     maxc = torch.empty(num_features, dtype=torch.int32, device=dev)
-    C.feature_order(indptr.contiguous(), idx.to(torch.int32).contiguous(), counts.contiguous(), int(num_features),
-                    row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)
+    native.lib().feature_order(indptr.contiguous(), idx.to(torch.int32).contiguous(), counts.contiguous(),
+                               int(num_features), row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)
+    return colptr, df, maxc
+
+
+def feature_order(indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor, num_features: int,
+                  block_entries: Optional[int] = None) -> FeatureOrder:
+    """CSR (rows, sorted unique feature ids per row, term counts) -> CSC by feature with a native
+    radix sort; docFreq and the per-feature max count are segmented reductions (no atomics).
+    Integer counts are sorted as int32 (no float copy). Above ``block_entries`` entries the rows
+    are sorted in blocks, so the sort's temporaries stay bounded (HBM sizing)."""
+    dev = idx.device
+    nnz = int(idx.numel())
+    if counts.dtype not in (torch.float32, torch.float64, torch.int32):
+        counts = counts.to(torch.float32 if counts.is_floating_point() else torch.int32)
+    pad = 16
+    row_buf = torch.zeros(nnz + pad, dtype=torch.int32, device=dev)
+    cnt_buf = torch.zeros(nnz + pad, dtype=torch.uint8, device=dev)
+    block = int(block_entries or FO_BLOCK_ENTRIES)
+    if nnz <= block:
+        colptr, df, maxc = _feature_order_one(indptr, idx, counts, num_features, row_buf, cnt_buf)
+        return FeatureOrder(row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)
+    C = native.lib()
+    N = int(indptr.numel() - 1)
+    # row blocks of <= ~block entries (a single row larger than a block is its own block)
+    targets = torch.arange(block, nnz, block, dtype=torch.int64, device=dev)
+    cuts = torch.searchsorted(indptr, targets, right=True).clamp(1, N) - 1
+    rcuts = sorted(set([0, N] + [int(c) for c in cuts.cpu().tolist() if 0 < int(c) < N]))
+    # pass 1: per-block column sizes (one bincount per block) -> every block's column offsets
+    lens = []
+    for r0, r1 in zip(rcuts[:-1], rcuts[1:]):
+        e0, e1 = int(indptr[r0]), int(indptr[r1])
+        lens.append(torch.bincount(idx[e0:e1].to(torch.int64), minlength=num_features))
+    tot = torch.stack(lens).sum(0)
+    colptr = torch.zeros(num_features + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(tot, 0, out=colptr[1:])
+    df = tot
+    maxc = torch.zeros(num_features, dtype=torch.int32, device=dev)
+    before = torch.zeros(num_features, dtype=torch.int64, device=dev)
+    # pass 2: sort each block, add its first row, copy its columns into place
+    for (r0, r1), ln in zip(zip(rcuts[:-1], rcuts[1:]), lens):
+        e0, e1 = int(indptr[r0]), int(indptr[r1])
+        n = e1 - e0
+        brow = torch.zeros(n + pad, dtype=torch.int32, device=dev)
+        bcnt = torch.zeros(n + pad, dtype=torch.uint8, device=dev)
+        bcol, _, bmax = _feature_order_one(indptr[r0:r1 + 1] - e0, idx[e0:e1], counts[e0:e1], num_features, brow, bcnt)
+        brow[:n] += r0
+        torch.maximum(maxc, bmax, out=maxc)
+        C.copy_segments(brow[:n], bcnt[:n], bcol[:-1].contiguous(), (colptr[:-1] + before).contiguous(), ln,
+                        row_buf[:nnz], cnt_buf[:nnz], None)
+        before += ln
+        del brow, bcnt, bcol
     return FeatureOrder(row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)
