@@ -66,6 +66,7 @@ from fraud_detection_spark_kafka_llm_amd.parallel import dist as D  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.parallel.affinity import bind_to_gpu  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.ring import PinnedRing  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.utils import memory  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.utils.config import Config  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.utils.profiling import run_profiled_if_requested  # noqa: E402
 
@@ -295,6 +296,13 @@ def main():
     model = SparkXGBClassifierModel(res.trees, F, res.base_margin)
     idf_np = idf.cpu().numpy()
     gbdt_peak = torch.cuda.max_memory_allocated(dev)
+    shard_rows, shard_nnz = len(vc), vc.nnz
+    # HBM sizing rule (utils/memory.py): rows one GPU could train at this corpus' entries per row,
+    # against the device's total memory (the bench's own allocations excluded)
+    sizing = {"max_rows_per_gpu": memory.max_rows_per_gpu(
+                  shard_nnz / max(shard_rows, 1), budget_bytes=int(torch.cuda.get_device_properties(dev).total_memory * 0.9)),
+              "train_model_bytes_per_row": memory.training_bytes(shard_rows, shard_nnz) / max(shard_rows, 1),
+              "train_peak_bytes_per_row": gbdt_peak / max(shard_rows, 1)}
     del chunks
     rf = {}
     if args.rf_trees > 0:
@@ -416,6 +424,7 @@ def main():
             "gbdt_warmup_sec_untimed": warm_sec,
             "gbdt_nodes_tree0": res.trees[0].num_nodes,
             "gbdt_peak_hbm_gb": gbdt_peak_gb,
+            **sizing,
             **rf,
             "stream_accuracy": acc,
             "p50_single_dialogue_ms": p50,

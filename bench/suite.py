@@ -178,7 +178,12 @@ def bench_xgb(args) -> dict:
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=trees, max_depth=6), device=dev)
     _sync(dev)
     t_train = time.perf_counter() - t0
-    return {"bench": "xgb", "rows": rows, "world": world, "rows_per_rank": len(vc), "trees": len(res.trees),
+    from fraud_detection_spark_kafka_llm_amd.utils import memory
+
+    budget = int(torch.cuda.get_device_properties(dev).total_memory * 0.9)
+    return {"max_rows_per_gpu": memory.max_rows_per_gpu(vc.nnz / max(len(vc), 1), budget_bytes=budget),
+            "model_peak_gb": memory.training_bytes(len(vc), vc.nnz) / 2 ** 30,
+            "bench": "xgb", "rows": rows, "world": world, "rows_per_rank": len(vc), "trees": len(res.trees),
             "depth": 6, "featurize_s": _max_over_ranks(t_feat, dev), "train_s": _max_over_ranks(t_train, dev),
             "per_tree_ms": _max_over_ranks((t_train - t_feat) / trees * 1e3, dev),
             "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}

@@ -121,6 +121,13 @@ class VectorColumn:
         self._values = v
 
     @property
+    def nnz(self) -> int:
+        """Stored entries (sparse) or rows x size (dense)."""
+        if self.indices is not None:
+            return int(self.indices.numel())
+        return int(self.dense.numel()) if self.dense is not None else 0
+
+    @property
     def values_materialized(self) -> bool:
         return self._values is not None
 

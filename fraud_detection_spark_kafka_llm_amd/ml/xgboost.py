@@ -96,7 +96,7 @@ class SparkXGBClassifier(_XGBParams, Estimator):
         from ..utils.config import default_device
 
         dev = default_device()
-        nw = effective_workers(self.getOrDefault("num_workers"), len(X), dev)
+        nw = effective_workers(self.getOrDefault("num_workers"), len(X), dev, nnz=X.nnz)
         if nw > 1 and not D.is_dist():
             # N rank processes (one per GPU over RCCL, else gloo CPU ranks) behind the watchdog
             from dataclasses import asdict

@@ -1,0 +1,29 @@
+"""HBM sizing rule (utils/memory.py): the modelled peak is monotone, the row cap
+inverts it, and the estimators' launcher asks for enough ranks that each shard fits."""
+import torch
+
+from fraud_detection_spark_kafka_llm_amd.parallel import estimator_dp
+from fraud_detection_spark_kafka_llm_amd.utils import memory
+
+
+def test_max_rows_inverts_the_training_bytes_model():
+    budget = 288 * 2 ** 30 * 0.9
+    cap = memory.max_rows_per_gpu(100.0, budget_bytes=budget)
+    assert cap > 50_000_000                    # a 288 GB GPU holds far more than a 12.5M-row shard
+    assert memory.training_bytes(cap, cap * 100) <= budget < memory.training_bytes(cap + 1000, (cap + 1000) * 100)
+    assert memory.max_rows_per_gpu(200.0, budget_bytes=budget) < cap
+    assert memory.max_rows_per_gpu(100.0) == 0 or torch.cuda.is_available()   # no budget on the CPU
+    assert memory.min_workers(10 * cap, 10 * cap * 100, budget_bytes=budget) == 10
+    assert memory.min_workers(cap // 2, cap // 2 * 100, budget_bytes=budget) == 1
+
+
+def test_effective_workers_raises_ranks_when_a_shard_would_not_fit(monkeypatch):
+    monkeypatch.setattr(estimator_dp, "_resolve_device", lambda d: torch.device("cuda", 0))
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("FDX_HBM_BUDGET_GB", "20")
+    cap = memory.max_rows_per_gpu(100.0)
+    rows = 3 * cap + 10
+    assert estimator_dp.effective_workers(1, rows, "cuda:0", nnz=rows * 100) == 4
+    assert estimator_dp.effective_workers(2, rows, "cuda:0") == 2        # without nnz: as requested
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    assert estimator_dp.effective_workers(1, rows, "cuda:0", nnz=rows * 100) == 2   # capped at the GPUs
