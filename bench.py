@@ -103,8 +103,11 @@ def featurize_shard(chunks: list, dev, spec):
 
     The H2D of chunk i+1 runs on a copy stream (SDMA) while chunk i is featurized on the
     compute stream, so the PCIe transfer of the raw text hides behind the kernel."""
-    ptrs, idxs, vals, labels = [], [], [], []
-    off = 0
+    rows = sum(int(h.offsets.numel()) - 1 for h, _ in chunks)
+    indptr = torch.zeros(rows + 1, dtype=torch.int64, device=dev)
+    labels = torch.empty(rows, dtype=torch.float64, device=dev)
+    idx = counts = None
+    off = r = 0
     comp = torch.cuda.current_stream(dev)
     copy = comp if os.environ.get("FDX_BENCH_SERIAL_H2D") == "1" else torch.cuda.Stream(dev)
 
@@ -127,14 +130,29 @@ def featurize_shard(chunks: list, dev, spec):
             nxt = stage(i + 1)
         res = T.featurize_score(d, spec, want_csr=True, device=dev)
         ip, ix, v = res.csr()
-        ptrs.append(ip[1:] + off)
-        off += int(ip[-1])
-        idxs.append(ix)
-        vals.append(v)
-        labels.append(yd)
         del res, d
-    indptr = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev)] + ptrs)
-    return indptr, torch.cat(idxs), torch.cat(vals), torch.cat(labels)
+        # each chunk's entries go straight into buffers sized from the first chunk (grown if
+        # needed), so the CSR is never held twice (HBM sizing, utils/memory.py)
+        k, n = int(ip[-1]), int(ip.numel()) - 1
+        if idx is None:
+            cap = int(k / max(n, 1) * rows * 1.05) + k + 1024
+            idx = torch.empty(cap, dtype=ix.dtype, device=dev)
+            counts = torch.empty(cap, dtype=v.dtype, device=dev)
+        if off + k > idx.numel():
+            cap = int((off + k) * 1.25)
+            idx = torch.cat([idx[:off], torch.empty(cap - off, dtype=idx.dtype, device=dev)])
+            counts = torch.cat([counts[:off], torch.empty(cap - off, dtype=counts.dtype, device=dev)])
+        idx[off:off + k] = ix
+        counts[off:off + k] = v
+        indptr[r + 1:r + n + 1] = ip[1:] + off
+        labels[r:r + n] = yd
+        off += k
+        r += n
+        del ip, ix, v, yd
+    if idx is None:
+        idx = torch.empty(0, dtype=torch.int32, device=dev)
+        counts = torch.empty(0, dtype=torch.int32, device=dev)
+    return indptr, idx[:off], counts[:off], labels
 
 
 def warmup_training(dev, spec, params: GBDTParams, rf_depth: int = 0) -> None:

@@ -25,34 +25,50 @@ from fraud_detection_spark_kafka_llm_amd.utils import tracing
 
 def build_features(rows: int, dev, chunk: int = 500_000, num_features: int = 1 << 18, seed: int = 11,
                    first_row: int = 0, tail_words: int = 30000):
+    """Synthetic dialogues -> fused featurization, chunk by chunk, into one CSR. Each chunk's
+    entries are copied into buffers sized from the first chunk's entries per row (grown if a
+    later chunk needs more) and freed at once, so the CSR is never held twice (a final
+    concatenation of the chunks doubled the peak: HBM sizing, utils/memory.py)."""
     spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=num_features)
-    ptrs, idxs, vals, labels = [], [], [], []
+    indptr = torch.zeros(rows + 1, dtype=torch.int64, device=dev)
+    y = torch.empty(rows, dtype=torch.float64, device=dev)
+    idx = counts = None
     t_gen = t_feat = 0.0
     off = 0
     for start in range(0, rows, chunk):
         n = min(chunk, rows - start)
         t0 = time.perf_counter()
-        pt, y = synth.generate(synth.SynthConfig(n=n, seed=seed, tail_words=tail_words), device=dev,
-                               start=first_row + start)
+        pt, yc = synth.generate(synth.SynthConfig(n=n, seed=seed, tail_words=tail_words), device=dev,
+                                start=first_row + start)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         res = T.featurize_score(pt, spec, want_csr=True, device=dev)
         ip, ix, v = res.csr()
+        del pt, res
+        k = int(ip[-1])
+        if idx is None:
+            cap = int(k / max(n, 1) * rows * 1.05) + k + 1024
+            idx = torch.empty(cap, dtype=ix.dtype, device=dev)
+            counts = torch.empty(cap, dtype=v.dtype, device=dev)
+        if off + k > idx.numel():                 # rare: grow by 25 %
+            cap = int((off + k) * 1.25)
+            idx = torch.cat([idx[:off], torch.empty(cap - off, dtype=idx.dtype, device=dev)])
+            counts = torch.cat([counts[:off], torch.empty(cap - off, dtype=counts.dtype, device=dev)])
+        idx[off:off + k] = ix
+        counts[off:off + k] = v
+        indptr[start + 1:start + n + 1] = ip[1:] + off
+        y[start:start + n] = yc
+        off += k
+        del ip, ix, v, yc
         torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         t_gen += t1 - t0
         t_feat += t2 - t1
-        ptrs.append(ip[1:] + off)
-        off += int(ip[-1])
-        idxs.append(ix)
-        vals.append(v)
-        labels.append(y)
-        del pt, res
-    indptr = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev)] + ptrs)
-    idx = torch.cat(idxs)
-    counts = torch.cat(vals)
-    y = torch.cat(labels)
-    return indptr, idx, counts, y, t_gen, t_feat
+    if idx is None:
+        idx = torch.empty(0, dtype=torch.int32, device=dev)
+        counts = torch.empty(0, dtype=torch.int32, device=dev)
+    # views of the first nnz entries (the slack stays allocated; trimming would copy)
+    return indptr, idx[:off], counts[:off], y, t_gen, t_feat
 
 
 def main():
@@ -84,6 +100,7 @@ def main():
     vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
+    feat_peak = torch.cuda.max_memory_allocated(dev)
     torch.cuda.reset_peak_memory_stats(dev)
     for k in grower.LEVEL_STATS:
         grower.LEVEL_STATS[k] = 0
@@ -95,6 +112,7 @@ def main():
                       "gen_s": t_gen, "featurize_s": t_feat, "idf_s": t2 - t1, "gbdt_total_s": res.train_seconds,
                       "per_tree_ms": (t3 - t2) / args.trees * 1e3, "wall_s": t3 - t0,
                       "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
+                      "featurize_peak_hbm_gb": feat_peak / 2 ** 30,
                       "built_nodes_per_level": ls["built_nodes"] / max(ls["levels"], 1),
                       "dp_hist_bytes_per_level": ls["hist_bytes"] / max(ls["levels"], 1),
                       "nodes_tree0": res.trees[0].num_nodes}))

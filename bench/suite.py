@@ -175,6 +175,8 @@ def bench_xgb(args) -> dict:
     vc, y, idf = _shard_tfidf(rows, dev, seed=31)
     _sync(dev)
     t_feat = time.perf_counter() - t0
+    feat_peak = torch.cuda.max_memory_allocated(dev)
+    torch.cuda.reset_peak_memory_stats(dev)      # training peak: quantize + 1000 rounds
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=trees, max_depth=6), device=dev)
     _sync(dev)
     t_train = time.perf_counter() - t0
@@ -186,7 +188,8 @@ def bench_xgb(args) -> dict:
             "bench": "xgb", "rows": rows, "world": world, "rows_per_rank": len(vc), "trees": len(res.trees),
             "depth": 6, "featurize_s": _max_over_ranks(t_feat, dev), "train_s": _max_over_ranks(t_train, dev),
             "per_tree_ms": _max_over_ranks((t_train - t_feat) / trees * 1e3, dev),
-            "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}
+            "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev),
+            "featurize_peak_hbm_gb": _max_over_ranks(feat_peak / 2 ** 30, dev)}
 
 
 def bench_kafka(args) -> dict:
