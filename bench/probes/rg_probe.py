@@ -1,0 +1,132 @@
+"""Row-group histogram engine probe: the bench corpus (HashingTF(2^18) -> TF-IDF, 10M rows by
+default), the RowGroups build (time, groups, bytes), then the root pass and a few multi-slot
+passes timed at several workgroup counts, each checked bitwise against the CSC + dense passes.
+Prints JSON lines.
+
+    python bench/probes/rg_probe.py --rows 10000000
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np
+import torch
+
+from gbdt_train import build_features
+from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+from fraud_detection_spark_kafka_llm_amd.models import quantize as qmod
+from fraud_detection_spark_kafka_llm_amd.models.grower import Workspace, pass_ct
+from fraud_detection_spark_kafka_llm_amd.ops import native
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return best * 1e3
+
+
+def csc_passes(C, Q, ws, slot8, nslots, hist):
+    """The default engine's passes (CSC items + dense hot block) into hist."""
+    s2n = torch.arange(nslots, dtype=torch.int32, device=hist.device)
+    ct = pass_ct(4, nslots)
+    root = slot8 is None
+    for grp in Q.groups + ([] if Q.dense is not None else Q.hot_groups):
+        C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(), Q.h_row,
+                          Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, hist, Q.TB, grp.bt, ct, 4, None)
+    if Q.dense is not None:
+        for bt in (1, 2, 4):
+            gfid, gden = ws.dense_groups(bt, C.tree_dense_fg(bt, 1 if root else ct))
+            if gfid.numel():
+                C.tree_hist_dense(Q.dense, ws.digp, ws.rowdig, None if root else ws.slot8_pad, gfid, gden,
+                                  Q.boff, Q.nbins, s2n, hist, Q.TB, Q.n_rows, 32768, bt, ct, 4)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--tail-words", type=int, default=30000)
+    ap.add_argument("--wgs", default="512,1024,2048")
+    ap.add_argument("--slots", default="1,2,8,16")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    C = native.lib()
+    ip, ix, cn, y, _, _ = build_features(args.rows, dev, tail_words=args.tail_words)
+    F = 1 << 18
+    fo = feature_order(ip, ix, cn, F)
+    idf = torch.log((args.rows + 1.0) / (fo.df.double() + 1.0))
+    vc = VectorColumn.tfidf(F, ip, ix, cn, idf, fo)
+    Q = qmod.quantize(vc, max_bins=32, counts=vc.tf_counts, scale=vc.tf_scale)
+    del ip, ix, cn, fo, vc
+    n = Q.n_rows
+    ws = Workspace(Q)
+    g = torch.linspace(-1, 1, n, device=dev, dtype=torch.float32)
+    h = torch.linspace(0.01, 0.25, n, device=dev, dtype=torch.float32)
+    C.tree_quant_max(g, h, None, None, 0, 0, False, 0, n, ws.maxabs, 0)
+    C.tree_quant(g, h, None, None, 0, 0, False, 0, 4, ws.maxabs, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rg = qmod.RowGroups(Q)
+    torch.cuda.synchronize()
+    build_ms = (time.perf_counter() - t0) * 1e3
+    ge = rg.group_entries
+    print(json.dumps({"rows": n, "nnz": int(Q.csc_row.numel()), "Fa": Q.Fa, "TB": Q.TB, "G": rg.G,
+                      "complete": rg.complete, "build_ms": round(build_ms, 1), "rg_bytes": rg.nbytes,
+                      "group_entries": [int(x) for x in ge],
+                      "entries_per_row_group0": float(ge[0] / n) if ge.size else 0.0}), flush=True)
+    zb = None
+    if Q.dense is not None:
+        zb = torch.from_numpy((Q.boff_host[:-1] + Q.zbin_host)[Q.hot]).to(dev)
+    rng = np.random.default_rng(0)
+    lst = torch.empty(n, dtype=torch.int32, device=dev)
+    start = torch.zeros(66, dtype=torch.int32, device=dev)
+    work = torch.zeros(128, dtype=torch.int32, device=dev)
+    for ns in [int(x) for x in args.slots.split(",")]:
+        root = ns == 1
+        slot8 = None
+        if not root:
+            # about half the rows built (the smaller siblings), spread over ns slots
+            rn = rng.integers(0, 2 * ns, n).astype(np.int32)
+            node_slot = torch.full((2 * ns,), -1, dtype=torch.int32)
+            node_slot[:ns] = torch.arange(ns, dtype=torch.int32)
+            C.tree_slot8(torch.from_numpy(rn).to(dev), node_slot.to(dev), 0, ns, ws.slot8, None, None)
+            slot8 = ws.slot8
+        ref = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)
+        csc_ms = timed(lambda: (ref.zero_(), csc_passes(C, Q, ws, slot8, ns, ref)))
+        if zb is not None:
+            ref[:, zb] = 0
+        s2n = torch.arange(ns, dtype=torch.int32, device=dev)
+        list_ms = 0.0
+        if not root:
+            list_ms = timed(lambda: C.tree_rg_list(ws.slot8, n, ns, work, start, lst))
+        for wgs in [int(x) for x in args.wgs.split(",")]:
+            P = max(8, -(-max(1, wgs // rg.G) // 8) * 8)
+            hist = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)
+
+            def run():
+                hist.zero_()
+                C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
+                               None if root else start, ns, P, s2n, hist, Q.TB, None, 0)
+            ms = timed(run)
+            if zb is not None:
+                hist[:, zb] = 0
+            eq = bool(torch.equal(hist, ref))
+            print(json.dumps({"slots": ns, "wgs": int(P * rg.G), "P": P, "rg_ms": round(ms, 3),
+                              "list_ms": round(list_ms, 3), "csc_ms": round(csc_ms, 3), "equal": eq}), flush=True)
+            if not eq:
+                sys.exit("row-group histograms differ from the CSC passes")
+
+
+if __name__ == "__main__":
+    main()

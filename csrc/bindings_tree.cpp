@@ -530,6 +530,150 @@ void hist_blk(const Tensor& ent_row, const Tensor& ent_key, const Tensor& seg, i
 
 int64_t blk_gw(int64_t ct) { return fdx::blk_groups_per_wave((int)ct); }
 
+// Row-group CSR build from the quantized CSC. pass 0: ptr [G, N + 1] int32 (zeroed) += entry
+// counts at [g][r + 1]; pass 1: cursor [G, N] (the exclusive starts) advanced, ent (uint16 bits in
+// int16) written at gbase[g] + position.
+void rg_build(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& colptr, const Tensor& fgroup,
+              const Tensor& flocal, int64_t N, int64_t pass, const optional<Tensor>& ptr,
+              const optional<Tensor>& cursor, const optional<Tensor>& gbase, const optional<Tensor>& ent) {
+  const auto dev = csc_row.device();
+  chk(csc_row, dev, at::kInt, "csc_row");
+  chk(csc_bin, dev, at::kByte, "csc_bin");
+  chk(colptr, dev, at::kLong, "colptr");
+  chk(fgroup, dev, at::kInt, "fgroup");
+  chk(flocal, dev, at::kInt, "flocal");
+  FDX_CHECK(fgroup.numel() + 1 == colptr.numel() && flocal.numel() == fgroup.numel(), "fgroup/flocal must be [Fa]");
+  FDX_CHECK(csc_row.numel() == csc_bin.numel(), "csc_row / csc_bin sizes");
+  fdx::RgBuildArgs a{};
+  a.csc_row = csc_row.data_ptr<int32_t>();
+  a.csc_bin = csc_bin.data_ptr<uint8_t>();
+  a.colptr = colptr.data_ptr<int64_t>();
+  a.Fa = (int32_t)fgroup.numel();
+  a.nnz = csc_row.numel();
+  a.N = N;
+  a.fgroup = fgroup.data_ptr<int32_t>();
+  a.flocal = flocal.data_ptr<int32_t>();
+  if (pass == 0) {
+    FDX_CHECK(ptr.has_value(), "pass 0 needs ptr");
+    chk(*ptr, dev, at::kInt, "ptr");
+    FDX_CHECK(ptr->dim() == 2 && ptr->size(1) == N + 1, "ptr must be [G, N + 1]");
+    a.ptr = reinterpret_cast<uint32_t*>(ptr->data_ptr<int32_t>());
+  } else {
+    FDX_CHECK(cursor && gbase && ent, "pass 1 needs cursor, gbase, ent");
+    chk(*cursor, dev, at::kInt, "cursor");
+    chk(*gbase, dev, at::kLong, "gbase");
+    FDX_CHECK(cursor->dim() == 2 && cursor->size(1) == N && gbase->numel() == cursor->size(0) + 1,
+              "cursor must be [G, N], gbase [G + 1]");
+    FDX_CHECK(ent->device() == dev && ent->scalar_type() == at::kShort && ent->is_contiguous(), "ent must be int16");
+    a.cursor = reinterpret_cast<uint32_t*>(cursor->data_ptr<int32_t>());
+    a.gbase = gbase->data_ptr<int64_t>();
+    a.ent = reinterpret_cast<uint16_t*>(ent->data_ptr<int16_t>());
+  }
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rg_build(a, (int)pass, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rg_build_cpu(a, (int)pass);
+  }
+}
+
+// Built rows of a level grouped by slot: list [N] int32, slot_start [nslots + 1] int32 (device),
+// work [2 * nslots] int32 scratch (zeroed here).
+void rg_list(const Tensor& slot8, int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start,
+             const Tensor& list) {
+  const auto dev = slot8.device();
+  chk(slot8, dev, at::kByte, "slot8");
+  chk(work, dev, at::kInt, "work");
+  chk(slot_start, dev, at::kInt, "slot_start");
+  chk(list, dev, at::kInt, "list");
+  FDX_CHECK(nslots >= 1 && nslots <= fdx::kRgMaxSlots, "nslots out of range");
+  FDX_CHECK(slot8.numel() >= N && list.numel() >= N, "slot8 / list must cover the rows");
+  FDX_CHECK(work.numel() >= 2 * nslots && slot_start.numel() >= nslots + 1, "work / slot_start sizes");
+  fdx::RgListArgs a{};
+  a.slot8 = slot8.data_ptr<uint8_t>();
+  a.N = N;
+  a.nslots = (int32_t)nslots;
+  a.rows_per_block = 4096;
+  a.slot_count = work.data_ptr<int32_t>();
+  a.slot_fill = work.data_ptr<int32_t>() + nslots;
+  a.slot_start = slot_start.data_ptr<int32_t>();
+  a.list = list.data_ptr<int32_t>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    C10_HIP_CHECK(hipMemsetAsync(work.data_ptr(), 0, sizeof(int32_t) * 2 * nslots, stream(dev)));
+    fdx::launch_rg_list(a, 0, stream(dev));
+    fdx::launch_rg_list(a, 1, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rg_list_cpu(a);
+  }
+}
+
+// Row-group histogram pass: hist[(slot_node[s] * stride + off(gbin[g][b])) * 2 + stat] += exact
+// sums over the built rows (list = None: every row, one slot).
+void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Tensor& gbin, const Tensor& rowdig,
+             int64_t np, const optional<Tensor>& list, const optional<Tensor>& slot_start, int64_t nslots, int64_t P,
+             const Tensor& slot_node, const Tensor& hist, int64_t stride, const optional<Tensor>& shard_lo,
+             int64_t shard_stride) {
+  const auto dev = ptr.device();
+  chk(ptr, dev, at::kInt, "ptr");
+  chk(gbase, dev, at::kLong, "gbase");
+  chk(gbin, dev, at::kInt, "gbin");
+  chk(rowdig, dev, at::kInt, "rowdig");
+  chk(slot_node, dev, at::kInt, "slot_node");
+  chk(hist, dev, at::kLong, "hist");
+  FDX_CHECK(ent.device() == dev && ent.scalar_type() == at::kShort && ent.is_contiguous(), "ent must be int16");
+  FDX_CHECK(ptr.dim() == 2, "ptr must be [G, N + 1]");
+  const int64_t G = ptr.size(0), N = ptr.size(1) - 1;
+  FDX_CHECK(gbase.numel() == G + 1 && gbin.numel() == G * fdx::kRgBins, "gbase [G + 1] / gbin [G, kRgBins]");
+  FDX_CHECK(rowdig.dim() == 2 && rowdig.size(0) == N && rowdig.size(1) == 2, "rowdig must be [N, 2]");
+  FDX_CHECK(reinterpret_cast<uintptr_t>(ent.data_ptr()) % 16 == 0 && readable_tail(ent, 8),
+            "ent must be 16-byte aligned with 8 readable padding entries");
+  FDX_CHECK(np == 1 || np == 4, "np must be 1 or 4");
+  FDX_CHECK(P >= 8 && P % 8 == 0, "P must be a positive multiple of 8");
+  FDX_CHECK(list.has_value() == slot_start.has_value(), "list and slot_start go together");
+  if (list) {
+    chk(*list, dev, at::kInt, "list");
+    chk(*slot_start, dev, at::kInt, "slot_start");
+    FDX_CHECK(list->numel() >= N && slot_start->numel() >= nslots + 1, "list / slot_start sizes");
+    FDX_CHECK(nslots >= 1 && nslots <= fdx::kRgMaxSlots, "nslots out of range");
+  } else {
+    FDX_CHECK(nslots == 1, "the all-rows pass has one slot");
+  }
+  FDX_CHECK(slot_node.numel() >= nslots, "slot_node must cover the slots");
+  FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && hist.size(1) == stride, "hist must be [rows, stride, 2] int64");
+  fdx::RgHistArgs a{};
+  a.ptr = reinterpret_cast<const uint32_t*>(ptr.data_ptr<int32_t>());
+  a.ent = reinterpret_cast<const uint16_t*>(ent.data_ptr<int16_t>());
+  a.gbase = gbase.data_ptr<int64_t>();
+  a.gbin = gbin.data_ptr<int32_t>();
+  a.G = (int32_t)G;
+  a.N = N;
+  a.rowdig = reinterpret_cast<const uint32_t*>(rowdig.data_ptr<int32_t>());
+  a.np = (int32_t)np;
+  a.list = opt<int32_t>(list);
+  a.slot_start = opt<int32_t>(slot_start);
+  a.nslots = (int32_t)nslots;
+  a.P = (int32_t)P;
+  a.slot_node = slot_node.data_ptr<int32_t>();
+  a.hist_stride = stride;
+  a.hist = hist.data_ptr<int64_t>();
+  if (shard_lo && shard_lo->defined()) {
+    chk(*shard_lo, dev, at::kLong, "shard_lo");
+    a.nshards = (int32_t)(shard_lo->numel() - 1);
+    a.shard_lo = shard_lo->data_ptr<int64_t>();
+    a.shard_stride = shard_stride;
+  }
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rg_hist(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rg_hist_cpu(a);
+  }
+}
+
 // Dense hot-feature histograms (see DenseHistArgs): gfid/gdense [ngroups * fg] with fg =
 // tree_dense_fg(bt, ct); rows are processed in ranges of range_rows (multiple of 64).
 void hist_dense(const Tensor& dense, const Tensor& digp, const Tensor& rowdig, const optional<Tensor>& slot8_t,
@@ -925,6 +1069,9 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_blk_build", &blk_build);
   m.def("tree_hist_blk", &hist_blk);
   m.def("tree_blk_gw", &blk_gw);
+  m.def("tree_rg_build", &rg_build);
+  m.def("tree_rg_list", &rg_list);
+  m.def("tree_rg_hist", &rg_hist);
   m.def("tree_rf_sample", &rf_sample);
   m.def("tree_rf_rows", &rf_rows);
   m.def("tree_rf_slots", &rf_slots);

@@ -107,6 +107,15 @@ void launch_hist_blk(const BlkHistArgs& a, int ct, hipStream_t s);
 int blk_groups_per_wave(int ct);
 void blk_build_cpu(const BlkBuildArgs& a, int pass);
 void hist_blk_cpu(const BlkHistArgs& a);
+struct RgBuildArgs;
+struct RgListArgs;
+struct RgHistArgs;
+void launch_rg_build(const RgBuildArgs& a, int pass, hipStream_t s);
+void launch_rg_list(const RgListArgs& a, int pass, hipStream_t s);
+void launch_rg_hist(const RgHistArgs& a, hipStream_t s);
+void rg_build_cpu(const RgBuildArgs& a, int pass);
+void rg_list_cpu(const RgListArgs& a);
+void rg_hist_cpu(const RgHistArgs& a);
 void launch_hist_dense(const DenseHistArgs& a, int bt, int ct, int np, hipStream_t s);
 int dense_features_per_wave(int bt, int ct);
 int dense_waves_per_group();

@@ -188,6 +188,79 @@ FDX_HD int64_t blk_bin_offset(const BlkHistArgs& a, int64_t b) {
   return (int64_t)s * a.shard_stride + b - a.shard_lo[s];
 }
 
+// ------------------------------------------------------------------ row-group histogram engine
+// Row-group CSR ("RG", models/quantize.py RowGroups): the active features are packed, densest
+// first, into groups of at most kRgBins local bins (a feature's bins stay contiguous inside its
+// group); for group g, row r's entries are ent[gbase[g] + ptr[g][r] .. gbase[g] + ptr[g][r + 1])
+// as uint16 local bins. A level's built rows are listed by node slot (rg_list), and a workgroup
+// of the histogram pass (row_kernels.hip) takes one group and a contiguous range of that list:
+// each lane walks one row's run of entries with 16-byte loads (a row's entries are contiguous,
+// so the per-entry row gathers of the CSC passes become one gather per (row, group)) and adds the
+// row's two quantised statistics into int64 LDS histograms of the group's bins, flushed with
+// integer atomics per node slot. Integer sums are order-free: the histograms are bitwise those of
+// the CSC passes and the host.
+constexpr int kRgBins = 8192;               // local bins per group: 2 x 8192 x int64 = 128 KB of LDS
+constexpr int kRgWaves = 16;                // 1024 threads per workgroup (one workgroup per CU)
+constexpr int kRgMaxSlots = 64;
+
+struct RgBuildArgs {
+  const int32_t* csc_row;         // feature-major CSC (quantized)
+  const uint8_t* csc_bin;
+  const int64_t* colptr;          // [Fa + 1]
+  int32_t Fa;
+  int64_t nnz;
+  int64_t N;
+  const int32_t* fgroup;          // [Fa] group of each feature (-1: not in the engine)
+  const int32_t* flocal;          // [Fa] local bin of the feature's bin 0 inside its group
+  int32_t entries_per_thread;
+  uint32_t* ptr;                  // pass 0: [G][N + 1], entry counts added at [g][r + 1]
+  uint32_t* cursor;               // pass 1: [G][N] next free position of each (group, row) (advanced)
+  const int64_t* gbase;           // pass 1: [G + 1] first entry of each group
+  uint16_t* ent;                  // pass 1 out
+};
+
+struct RgListArgs {
+  const uint8_t* slot8;           // [N] pass slot of each row (0xff: not built)
+  int64_t N;
+  int32_t nslots;
+  int32_t rows_per_block;
+  int32_t* slot_count;            // [nslots] (zeroed; pass 0 adds)
+  int32_t* slot_fill;             // [nslots] (zeroed; pass 1 reserves)
+  int32_t* slot_start;            // [nslots + 1] out (pass 1)
+  int32_t* list;                  // [N] out (pass 1): built rows grouped by slot
+};
+
+struct RgHistArgs {
+  const uint32_t* ptr;            // [G][N + 1]
+  const uint16_t* ent;            // entries (readable padding behind the end)
+  const int64_t* gbase;           // [G + 1]
+  const int32_t* gbin;            // [G][kRgBins] histogram column of each local bin (-1: unused)
+  int32_t G;
+  int64_t N;
+  const uint32_t* rowdig;         // [N * 2] digit words
+  int32_t np;                     // 4: q = undigits4, 1: q = undigits1
+  const int32_t* list;            // built rows grouped by slot (nullptr: rows 0..N-1, one slot)
+  const int32_t* slot_start;      // [nslots + 1] (nullptr with list == nullptr)
+  int32_t nslots;
+  int32_t P;                      // list chunks per group (multiple of 8)
+  // output: hist[(slot_node[s] * hist_stride + off(column)) * 2 + stat] +=
+  const int32_t* slot_node;
+  int64_t hist_stride;
+  int64_t* hist;
+  int32_t nshards;                // 0: off(c) = c; else shard-major rows as BlkHistArgs
+  const int64_t* shard_lo;
+  int64_t shard_stride;
+};
+
+FDX_HD int64_t rg_col_offset(const RgHistArgs& a, int64_t b) {
+  if (a.nshards <= 0) return b;
+  int s = 0;
+  while (s + 1 < a.nshards && b >= a.shard_lo[s + 1]) ++s;
+  return (int64_t)s * a.shard_stride + b - a.shard_lo[s];
+}
+
+FDX_HD int64_t rg_q(uint32_t d, int np) { return np == 4 ? undigits4(d) : undigits1(d); }
+
 // RF batch pass: which of the (<= 64) pass slots sampled each active feature.
 struct RfSlotMaskArgs {
   uint64_t seed;

@@ -248,6 +248,71 @@ void hist_blk_cpu(const BlkHistArgs& a) {
   });
 }
 
+// Row-group CSR build (host twin of rg_build_kernel): sequential, so each (group, row) run keeps
+// the CSC order (any order gives the same exact sums).
+void rg_build_cpu(const RgBuildArgs& a, int pass) {
+  int32_t f = 0;
+  for (int64_t e = 0; e < a.nnz; ++e) {
+    while (e >= a.colptr[f + 1]) ++f;
+    const int32_t g = a.fgroup[f];
+    if (g < 0) continue;
+    const int64_t r = a.csc_row[e];
+    if (pass == 0) {
+      a.ptr[(int64_t)g * (a.N + 1) + r + 1] += 1;
+    } else {
+      const uint32_t pos = a.cursor[(int64_t)g * a.N + r]++;
+      a.ent[a.gbase[g] + pos] = (uint16_t)(a.flocal[f] + a.csc_bin[e]);
+    }
+  }
+}
+
+// Built rows grouped by slot, ascending inside each slot (the device order inside a 4096-row
+// window may differ; the histogram sums do not depend on it).
+void rg_list_cpu(const RgListArgs& a) {
+  std::vector<int64_t> cnt(a.nslots + 1, 0);
+  for (int64_t r = 0; r < a.N; ++r)
+    if (a.slot8[r] < (uint32_t)a.nslots) ++cnt[a.slot8[r] + 1];
+  for (int s = 0; s < a.nslots; ++s) cnt[s + 1] += cnt[s];
+  for (int s = 0; s <= a.nslots; ++s) a.slot_start[s] = (int32_t)cnt[s];
+  for (int s = 0; s < a.nslots; ++s) a.slot_count[s] = (int32_t)(cnt[s + 1] - cnt[s]);
+  for (int64_t r = 0; r < a.N; ++r)
+    if (a.slot8[r] < (uint32_t)a.nslots) a.list[cnt[a.slot8[r]]++] = (int32_t)r;
+}
+
+// Host twin of rg_hist_kernel, following the same (group, list chunk, slot) work split, so a host
+// test checks that the plan covers every built row of every group exactly once.
+void rg_hist_cpu(const RgHistArgs& a) {
+  const int64_t T = a.list ? (int64_t)a.slot_start[a.nslots] : a.N;
+  parallel_for((int64_t)a.G * a.P, 0, 1, [&](int64_t lo_w, int64_t hi_w) {
+    for (int64_t w = lo_w; w < hi_w; ++w) {
+      const int x = (int)(w & 7), rest = (int)(w >> 3);
+      const int g = rest % a.G, p = (rest / a.G) * 8 + x;
+      if (p >= a.P) continue;
+      const int64_t a0 = T * p / a.P, a1 = T * (p + 1) / a.P;
+      const uint32_t* ptr = a.ptr + (int64_t)g * (a.N + 1);
+      const uint16_t* ent = a.ent + a.gbase[g];
+      int s = 0;
+      if (a.list)
+        while (s + 1 < a.nslots && a.slot_start[s + 1] <= a0) ++s;
+      for (int64_t pos = a0; pos < a1; ++pos) {
+        if (a.list)
+          while (a.slot_start[s + 1] <= pos) ++s;
+        const int64_t hrow = a.slot_node[s];
+        if (hrow < 0) continue;
+        const int64_t row = a.list ? (int64_t)a.list[pos] : pos;
+        const int64_t q0 = rg_q(a.rowdig[2 * row], a.np), q1 = rg_q(a.rowdig[2 * row + 1], a.np);
+        for (uint32_t i = ptr[row]; i < ptr[row + 1]; ++i) {
+          const int32_t col = a.gbin[(int64_t)g * kRgBins + ent[i]];
+          if (col < 0) continue;
+          int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
+          __atomic_fetch_add(dst, q0, __ATOMIC_RELAXED);
+          __atomic_fetch_add(dst + 1, q1, __ATOMIC_RELAXED);
+        }
+      }
+    }
+  });
+}
+
 void hist_dense_cpu(const DenseHistArgs& a, int fg, int np) {
   parallel_for((int64_t)a.ngroups * fg, 0, 1, [&](int64_t lo, int64_t hi) {
     for (int64_t t = lo; t < hi; ++t) {

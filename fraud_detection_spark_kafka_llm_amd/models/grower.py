@@ -64,6 +64,9 @@ HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
 LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0}
 BLK = os.environ.get("FDX_BLK", "0") == "1"      # row-blocked pass: opt-in until it beats the CSC passes
 BLK_MAX_SLOTS = 4
+# row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
+# histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
+ROWHIST = os.environ.get("FDX_ROWHIST", "0") == "1"
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 
@@ -110,6 +113,20 @@ class Workspace:
         self._shards = None
         self.staging = Staging(dev)
         self._streams = None
+
+    def rowgroups(self):
+        """The row-group CSR when the row-group engine is on and covers every feature (else None),
+        plus the level's row-list buffers."""
+        if not ROWHIST:
+            return None
+        rg = self.Q.rowgroups()
+        if not rg.complete:
+            return None
+        if getattr(self, "rg_list", None) is None:
+            self.rg_list = torch.empty(self.Q.n_rows, dtype=torch.int32, device=self.dev)
+            self.rg_start = torch.zeros(66, dtype=torch.int32, device=self.dev)
+            self.rg_work = torch.zeros(128, dtype=torch.int32, device=self.dev)
+        return rg
 
     def run_concurrent(self, launches: list) -> None:
         """Run the launches on HIST_STREAMS side streams joined back into the current stream
@@ -764,10 +781,11 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
             slot8 = None
             csc_slot8, csc_dig = None, ws.rowdig
+            rg = ws.rowgroups() if (not build_all and np_ == 4) else None
             if d > 0:
                 # a single built node: the CSC passes run the root kernel on digit words zeroed
                 # outside it (no per-entry slot gather, no compaction; zero rows add nothing)
-                single = n_build == 1
+                single = n_build == 1 and rg is None
                 if single and getattr(ws, "rowdig_masked", None) is None:
                     ws.rowdig_masked = torch.empty_like(ws.rowdig)
                 C.tree_slot8(ws.row_node, st.node_slot, 0, n_build, ws.slot8, ws.rowdig if single else None,
@@ -782,7 +800,17 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 s2n = torch.arange(n_build, dtype=torch.int32, device=dev)
             ct = pass_ct(np_, n_build)
             launches = []
-            if BLK and np_ == 4 and not build_all and n_build <= BLK_MAX_SLOTS:
+            if rg is not None:
+                shard_args = (shards.bin_lo, n_build * shards.Bs) if shards is not None else (None, 0)
+                if d == 0:
+                    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, 1, rg.P, s2n,
+                                   hist_target, h_stride, *shard_args)
+                else:
+                    C.tree_rg_list(ws.slot8, Q.n_rows, n_build, ws.rg_work, ws.rg_start, ws.rg_list)
+                    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
+                                   n_build, rg.P, s2n, hist_target, h_stride, *shard_args)
+                sel_groups, use_dense = [], False
+            elif BLK and np_ == 4 and not build_all and n_build <= BLK_MAX_SLOTS:
                 # row-blocked pass: every feature (hot ones included) in one launch
                 blk = Q.blocked()
                 root = d == 0 or n_build == 1

@@ -205,6 +205,86 @@ class BlockedCSC:
         return out
 
 
+RG_BINS = 8192           # csrc/tree.h kRgBins: local bins per row group
+RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 64))
+RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 1024))   # workgroups per row-group pass (1 resident per CU)
+
+
+class RowGroups:
+    """Row-group CSR of the active features (csrc/tree.h "row-group histogram engine").
+
+    Features are packed densest first into groups of at most ``RG_BINS`` local bins (a feature's
+    bins contiguous); for group g the entries of row r are ``ent[gbase[g] + ptr[g, r] : gbase[g] +
+    ptr[g, r + 1]]`` as uint16 local bins, and ``gbin[g, b]`` is the global histogram column of
+    local bin b. Built on the device from the quantized CSC in two passes (count, place):
+    4 B per (group, row) plus 2 B per entry. ``complete`` is False when the features with entries
+    need more than ``RG_MAX_GROUPS`` groups (very wide vocabularies): the grower then keeps the
+    CSC passes."""
+
+    def __init__(self, Q: "Quantized", max_groups: int = None):
+        C = native.lib()
+        dev = Q.device
+        max_groups = RG_MAX_GROUPS if max_groups is None else max_groups
+        colptr = Q.colptr.cpu().numpy()
+        cnt = np.diff(colptr)
+        nb = Q.nbins.cpu().numpy().astype(np.int64)
+        boff = np.asarray(Q.boff_host, dtype=np.int64)
+        Fa = int(nb.size)
+        order = np.argsort(-cnt, kind="stable")
+        order = order[cnt[order] > 0]
+        cum = np.concatenate([[0], np.cumsum(nb[order])])
+        fgroup = np.full(Fa, -1, dtype=np.int32)
+        flocal = np.zeros(Fa, dtype=np.int32)
+        starts = []
+        i = 0
+        while i < order.size and len(starts) < max_groups:
+            j = int(np.searchsorted(cum, cum[i] + RG_BINS, side="right")) - 1     # features [i, j) fit
+            j = max(j, i + 1)
+            fs = order[i:j]
+            fgroup[fs] = len(starts)
+            flocal[fs] = (cum[i:j] - cum[i]).astype(np.int32)
+            starts.append(i)
+            i = j
+        self.complete = i >= order.size
+        self.G = G = max(1, len(starts))
+        self.n_rows = N = Q.n_rows
+        # global column of every local bin
+        gbin = np.full((G, RG_BINS), -1, dtype=np.int32)
+        sel = np.nonzero(fgroup >= 0)[0]
+        if sel.size:
+            rep = nb[sel]
+            f_rep = np.repeat(sel, rep)
+            k = np.arange(int(rep.sum()), dtype=np.int64) - np.repeat(np.cumsum(rep) - rep, rep)
+            gbin[fgroup[f_rep], flocal[f_rep] + k] = (boff[f_rep] + k).astype(np.int32)
+        egroup = np.zeros(G, dtype=np.int64)
+        np.add.at(egroup, fgroup[sel], cnt[sel])
+        if int(egroup.max(initial=0)) >= (1 << 31):
+            raise ValueError("row group with >= 2^31 entries: shard the rows over more ranks")
+        pad = (egroup + 7) // 8 * 8                   # 16-byte aligned group starts
+        gbase = np.concatenate([[0], np.cumsum(pad)]).astype(np.int64)
+        self.entries = int(egroup.sum())
+        self.group_entries = egroup
+        self.fgroup_host, self.flocal_host = fgroup, flocal
+        fg_t = torch.from_numpy(fgroup).to(dev)
+        fl_t = torch.from_numpy(flocal).to(dev)
+        self.gbase = torch.from_numpy(gbase).to(dev)
+        self.gbin = torch.from_numpy(gbin).to(dev)
+        ptr = torch.zeros((G, N + 1), dtype=torch.int32, device=dev)
+        C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 0, ptr, None, None, None)
+        self.ptr = torch.cumsum(ptr, dim=1, dtype=torch.int32)
+        del ptr
+        cursor = self.ptr[:, :N].clone(memory_format=torch.contiguous_format)   # (a view when G == 1)
+        # readable padding behind the end: the pass loads aligned 8-entry blocks
+        self.ent = torch.zeros(int(gbase[-1]) + 16, dtype=torch.int16, device=dev)[:int(gbase[-1])]
+        C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 1, None, cursor, self.gbase, self.ent)
+        del cursor
+        self.P = max(8, -(-max(1, RG_TARGET_WGS // G) // 8) * 8)
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.ptr.numel() * 4 + self.ent.numel() * 2 + self.gbin.numel() * 4)
+
+
 @dataclass
 class Quantized:
     n_rows: int
@@ -245,6 +325,14 @@ class Quantized:
             with tracing.span("q.blocked"):
                 b = self._blocked = BlockedCSC(self)
         return b
+
+    def rowgroups(self) -> RowGroups:
+        """The row-group CSR of the row-group histogram engine (built on first use)."""
+        r = getattr(self, "_rowgroups", None)
+        if r is None:
+            with tracing.span("q.rowgroups"):
+                r = self._rowgroups = RowGroups(self)
+        return r
 
     @property
     def n_pad(self) -> int:

@@ -1,0 +1,206 @@
+"""Row-group histogram engine (csrc/row_kernels.hip, models/quantize.RowGroups): layout coverage,
+exact histograms against the numpy int64 reference on the host and bitwise host == GPU, and the
+level loop growing the CSC passes' trees."""
+import numpy as np
+import pytest
+import torch
+
+from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+from fraud_detection_spark_kafka_llm_amd.models.grower import Workspace
+from fraud_detection_spark_kafka_llm_amd.models.quantize import RG_BINS, RowGroups, quantize
+from fraud_detection_spark_kafka_llm_amd.ops import native
+
+from test_tree_engine import QKW, _hist_ref, _same_trees, random_counts_matrix, vc_from_dense
+
+
+def _wide(n, F, seed, hi=200, dmax=0.5):
+    rng = np.random.default_rng(seed)
+    dense = (rng.random((n, F)) < np.linspace(0.001, dmax, F)) * rng.integers(1, hi, (n, F))
+    return vc_from_dense(dense.astype(np.float64))
+
+
+def _quant(ws, n, dev, np_=4):
+    C = native.lib()
+    if np_ == 4:
+        gg = torch.from_numpy(np.linspace(-1, 1, n).astype(np.float32)).to(dev)
+        hh = torch.from_numpy(np.linspace(0.01, 0.25, n).astype(np.float32)).to(dev)
+        C.tree_quant_max(gg, hh, None, None, 0, 0, False, 0, n, ws.maxabs, 0)
+        C.tree_quant(gg, hh, None, None, 0, 0, False, 0, 4, ws.maxabs, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
+    else:
+        lab = torch.from_numpy((np.arange(n) % 3 == 0).astype(np.float32)).to(dev)
+        C.tree_quant(None, None, lab, None, 5, 2, True, 1, 1, None, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
+
+
+def _q_of(ws, np_):
+    d = ws.rowdig.cpu().numpy().view(np.uint32).astype(np.int64)
+    if np_ == 4:
+        q = (d ^ 0x80808080) - 0x80808080
+    else:
+        q = ((d & 0xFF) ^ 0x80) - 0x80
+    return q[:, 0], q[:, 1]
+
+
+def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None, np_=4, P=16, max_groups=None):
+    """Histograms of node slots 0..nslots-1 through tree_rg_list + tree_rg_hist, plus q0, q1 and Q;
+    ``shards`` = (S, bin_lo) writes the shard-major DP layout (returned unpacked)."""
+    C = native.lib()
+    n = row_node_np.shape[0]
+    Q = quantize(vc.to(dev), max_bins=max_bins, **QKW)
+    ws = Workspace(Q)
+    _quant(ws, n, dev, np_)
+    rg = RowGroups(Q, max_groups=max_groups)
+    list_ = start = None
+    if not root:
+        node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
+        node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
+        C.tree_slot8(torch.from_numpy(row_node_np).to(dev), node_slot.to(dev), 0, nslots, ws.slot8, None, None)
+        list_ = torch.empty(n, dtype=torch.int32, device=dev)
+        start = torch.zeros(nslots + 1, dtype=torch.int32, device=dev)
+        work = torch.zeros(2 * nslots, dtype=torch.int32, device=dev)
+        C.tree_rg_list(ws.slot8, n, nslots, work, start, list_)
+    s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
+    q0, q1 = _q_of(ws, np_)
+    if shards is None:
+        hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
+        C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, P, s2n, hist, Q.TB,
+                       None, 0)
+        return hist.cpu().numpy(), q0, q1, Q, rg
+    S, lo = shards
+    Bs = int(np.diff(lo).max())
+    buf = torch.zeros((S, nslots, Bs, 2), dtype=torch.int64, device=dev)
+    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, P, s2n,
+                   buf.view(S * nslots, Bs, 2), Bs, torch.from_numpy(lo).to(dev), nslots * Bs)
+    b = buf.cpu().numpy()
+    hist = np.concatenate([b[k, :, : lo[k + 1] - lo[k]] for k in range(S)], axis=1)
+    return hist, q0, q1, Q, rg
+
+
+def test_row_groups_cover_every_entry_once():
+    """Every CSC entry appears once in its (group, row) run; local bins map back to the global
+    column; a group holds <= RG_BINS bins, densest features first; group starts are 16-B aligned."""
+    vc = _wide(4000, 300, 3)
+    Q = quantize(vc, max_bins=100, **QKW)
+    assert Q.TB > RG_BINS                                  # several groups
+    rg = RowGroups(Q)
+    assert rg.complete and rg.G >= 2
+    colptr, boff, rows = Q.colptr.numpy(), Q.boff.numpy(), Q.csc_row.numpy()
+    want = sorted((int(r), int(boff[f] + b)) for f in range(Q.Fa)
+                  for r, b in zip(rows[colptr[f]:colptr[f + 1]], Q.bins_of(f).numpy()))
+    ptr, ent, gbase, gbin = rg.ptr.numpy(), rg.ent.numpy().view(np.uint16), rg.gbase.numpy(), rg.gbin.numpy()
+    assert (gbase % 8 == 0).all()
+    got = []
+    for g in range(rg.G):
+        assert (np.diff(ptr[g]) >= 0).all()
+        for r in range(Q.n_rows):
+            for i in range(ptr[g, r], ptr[g, r + 1]):
+                col = int(gbin[g, ent[gbase[g] + i]])
+                assert col >= 0
+                got.append((r, col))
+    assert sorted(got) == want
+    cnt = np.diff(colptr)
+    dens = [cnt[rg.fgroup_host == g].min() for g in range(rg.G)]
+    assert all(dens[g] >= cnt[rg.fgroup_host == g + 1].max() for g in range(rg.G - 1))
+    for g in range(rg.G):
+        assert (gbin[g] >= 0).sum() <= RG_BINS
+
+
+def test_row_groups_incomplete_beyond_max_groups():
+    vc = _wide(2000, 300, 4)
+    Q = quantize(vc, max_bins=100, **QKW)
+    rg = RowGroups(Q, max_groups=1)
+    assert not rg.complete and rg.G == 1
+
+
+@pytest.mark.parametrize("nslots,root,np_,F", [(1, True, 4, 250), (2, False, 4, 250), (5, False, 4, 250),
+                                                (33, False, 4, 250), (3, False, 1, 250), (1, True, 4, 40),
+                                                (4, False, 4, 40)])
+def test_row_group_histograms_equal_host_reference(nslots, root, np_, F):
+    """Several groups (F = 250) and a single group (F = 40: the cursor copy must not alias ptr)."""
+    rng = np.random.default_rng(nslots)
+    n = 5000
+    vc = _wide(n, F, nslots)
+    row_node = rng.integers(-1, nslots + 1, n).astype(np.int32) if not root else np.zeros(n, np.int32)
+    hist, q0, q1, Q, rg = _rg_hist_on("cpu", vc, 100, nslots, row_node, root, np_=np_)
+    assert (rg.G >= 2) == (F > 100)
+    np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, nslots, q0, q1))
+
+
+def test_row_group_list_groups_built_rows_by_slot():
+    C = native.lib()
+    rng = np.random.default_rng(9)
+    n, ns = 20000, 7
+    slot8 = rng.integers(0, ns + 3, n).astype(np.uint8)
+    slot8[slot8 >= ns] = 0xFF
+    lst = torch.empty(n, dtype=torch.int32)
+    start = torch.zeros(ns + 1, dtype=torch.int32)
+    C.tree_rg_list(torch.from_numpy(slot8), n, ns, torch.zeros(2 * ns, dtype=torch.int32), start, lst)
+    st = start.numpy()
+    for s in range(ns):
+        np.testing.assert_array_equal(np.sort(lst.numpy()[st[s]:st[s + 1]]), np.nonzero(slot8 == s)[0])
+    assert st[-1] == (slot8 != 0xFF).sum()
+
+
+def test_row_group_sharded_layout_equals_plain():
+    rng = np.random.default_rng(12)
+    n = 4000
+    vc = _wide(n, 200, 12)
+    row_node = rng.integers(-1, 4, n).astype(np.int32)
+    plain, *_ , Q, _ = _rg_hist_on("cpu", vc, 100, 3, row_node)
+    lo = np.array([0, Q.TB // 3, (2 * Q.TB) // 3, Q.TB], dtype=np.int64)
+    sh, *_ = _rg_hist_on("cpu", vc, 100, 3, row_node, shards=(3, lo))
+    np.testing.assert_array_equal(plain, sh)
+
+
+@pytest.mark.parametrize("depth,hot", [(6, 0.2), (3, 0.0)])
+def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot):
+    """FDX_ROWHIST=1: every GBDT level's histograms come from the row-group engine; the trees
+    equal the CSC / dense passes' trees bit for bit (device level loop, host twins)."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower, quantize as qmod
+
+    monkeypatch.setattr(qmod, "HOT_DENSITY", hot)
+    dense, y = random_counts_matrix(3000, 300, 0.1, 21, max_count=40)
+    dense[:, :6] = np.random.default_rng(1).integers(0, 5, (3000, 6))
+    vc = vc_from_dense(dense)
+    params = GBDTParams(n_estimators=4, max_depth=depth, gamma=0.0, max_bin=64)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(grower, "ROWHIST", flag)
+        out[flag] = fit_gbdt(vc, torch.from_numpy(y), params, device="cpu")
+    _same_trees(out[False].trees, out[True].trees)
+    assert max(t.num_nodes for t in out[True].trees) > 7
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nslots,root", [(1, True), (2, False), (5, False), (32, False)])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, sharded):
+    """The row-group pass (LDS int64 atomics, 16-B row-run loads, per-slot flushes) equals the
+    host's exact int64 sums bit for bit, plain and in the shard-major DP layout."""
+    rng = np.random.default_rng(20 + nslots)
+    n = 30000
+    vc = _wide(n, 400, 20 + nslots, hi=300)
+    row_node = rng.integers(-1, nslots + 1, n).astype(np.int32) if not root else np.zeros(n, np.int32)
+    shards = None
+    if sharded:
+        Q0 = quantize(vc, max_bins=200, **QKW)
+        lo = np.array([0, Q0.TB // 3, (2 * Q0.TB) // 3, Q0.TB], dtype=np.int64)
+        shards = (3, lo)
+    a, *_ = _rg_hist_on("cpu", vc, 200, nslots, row_node, root, shards, P=24)
+    b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24)
+    assert rg.G >= 2
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_row_group_level_loop_grows_the_same_trees(monkeypatch):
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+
+    dense, y = random_counts_matrix(9000, 300, 0.1, 61, max_count=40)
+    dense[:, :4] = np.random.default_rng(6).integers(0, 9, (9000, 4))
+    vc = vc_from_dense(dense)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(grower, "ROWHIST", flag)
+        out[flag] = fit_gbdt(vc, torch.from_numpy(y), GBDTParams(n_estimators=4, max_depth=6, max_bin=64),
+                             device="cuda:0").trees
+    _same_trees(out[False], out[True])
