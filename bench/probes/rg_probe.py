@@ -59,6 +59,9 @@ def main():
     ap.add_argument("--tail-words", type=int, default=30000)
     ap.add_argument("--wgs", default="512,1024,2048")
     ap.add_argument("--slots", default="1,2,8,16")
+    ap.add_argument("--dbg", default="0", help="RgHistArgs::dbg modes (bits 1-2 give wrong sums)")
+    ap.add_argument("--alphas", default="8")
+    ap.add_argument("--bins", default="8192,4096")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     C = native.lib()
@@ -75,16 +78,18 @@ def main():
     h = torch.linspace(0.01, 0.25, n, device=dev, dtype=torch.float32)
     C.tree_quant_max(g, h, None, None, 0, 0, False, 0, n, ws.maxabs, 0)
     C.tree_quant(g, h, None, None, 0, 0, False, 0, 4, ws.maxabs, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rg = qmod.RowGroups(Q)
-    torch.cuda.synchronize()
-    build_ms = (time.perf_counter() - t0) * 1e3
-    ge = rg.group_entries
-    print(json.dumps({"rows": n, "nnz": int(Q.csc_row.numel()), "Fa": Q.Fa, "TB": Q.TB, "G": rg.G,
-                      "complete": rg.complete, "build_ms": round(build_ms, 1), "rg_bytes": rg.nbytes,
-                      "group_entries": [int(x) for x in ge],
-                      "entries_per_row_group0": float(ge[0] / n) if ge.size else 0.0}), flush=True)
+    rgs = {}
+    for B in [int(x) for x in args.bins.split(",")]:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rg = rgs[B] = qmod.RowGroups(Q, bins=B)
+        torch.cuda.synchronize()
+        build_ms = (time.perf_counter() - t0) * 1e3
+        ge = rg.group_entries
+        print(json.dumps({"rows": n, "nnz": int(Q.csc_row.numel()), "Fa": Q.Fa, "TB": Q.TB, "bins": B, "G": rg.G,
+                          "complete": rg.complete, "build_ms": round(build_ms, 1), "rg_bytes": rg.nbytes,
+                          "group_entries": [int(x) for x in ge],
+                          "entries_per_row_group0": float(ge[0] / n) if ge.size else 0.0}), flush=True)
     zb = None
     if Q.dense is not None:
         zb = torch.from_numpy((Q.boff_host[:-1] + Q.zbin_host)[Q.hot]).to(dev)
@@ -110,22 +115,26 @@ def main():
         list_ms = 0.0
         if not root:
             list_ms = timed(lambda: C.tree_rg_list(ws.slot8, n, ns, work, start, lst))
-        for wgs in [int(x) for x in args.wgs.split(",")]:
-            P = max(8, -(-max(1, wgs // rg.G) // 8) * 8)
-            hist = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)
+        for B, wgs, alpha, dbg in [(B, int(w), float(al), int(db)) for B in rgs for w in args.wgs.split(",")
+                                   for al in args.alphas.split(",") for db in args.dbg.split(",")]:
+            if True:
+                rg = rgs[B]
+                hist = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)
+                wt = rg.work(wgs, alpha)
 
-            def run():
-                hist.zero_()
-                C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
-                               None if root else start, ns, P, s2n, hist, Q.TB, None, 0)
-            ms = timed(run)
-            if zb is not None:
-                hist[:, zb] = 0
-            eq = bool(torch.equal(hist, ref))
-            print(json.dumps({"slots": ns, "wgs": int(P * rg.G), "P": P, "rg_ms": round(ms, 3),
-                              "list_ms": round(list_ms, 3), "csc_ms": round(csc_ms, 3), "equal": eq}), flush=True)
-            if not eq:
-                sys.exit("row-group histograms differ from the CSC passes")
+                def run():
+                    hist.zero_()
+                    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
+                                   None if root else start, ns, wt, s2n, hist, Q.TB, None, 0, dbg)
+                ms = timed(run)
+                if zb is not None:
+                    hist[:, zb] = 0
+                eq = bool(torch.equal(hist, ref))
+                print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "wgs": int(wt.shape[1]), "dbg": dbg,
+                                  "rg_ms": round(ms, 3),
+                                  "list_ms": round(list_ms, 3), "csc_ms": round(csc_ms, 3), "equal": eq}), flush=True)
+                if not eq and dbg < 2:
+                    sys.exit("row-group histograms differ from the CSC passes")
 
 
 if __name__ == "__main__":

@@ -611,11 +611,11 @@ void rg_list(const Tensor& slot8, int64_t N, int64_t nslots, const Tensor& work,
 }
 
 // Row-group histogram pass: hist[(slot_node[s] * stride + off(gbin[g][b])) * 2 + stat] += exact
-// sums over the built rows (list = None: every row, one slot).
+// sums over the built rows (list = None: every row, one slot). wg [3, n_wg]: the work table.
 void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Tensor& gbin, const Tensor& rowdig,
-             int64_t np, const optional<Tensor>& list, const optional<Tensor>& slot_start, int64_t nslots, int64_t P,
-             const Tensor& slot_node, const Tensor& hist, int64_t stride, const optional<Tensor>& shard_lo,
-             int64_t shard_stride) {
+             int64_t np, const optional<Tensor>& list, const optional<Tensor>& slot_start, int64_t nslots,
+             const Tensor& wg, const Tensor& slot_node, const Tensor& hist, int64_t stride,
+             const optional<Tensor>& shard_lo, int64_t shard_stride, int64_t dbg) {
   const auto dev = ptr.device();
   chk(ptr, dev, at::kInt, "ptr");
   chk(gbase, dev, at::kLong, "gbase");
@@ -626,12 +626,14 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
   FDX_CHECK(ent.device() == dev && ent.scalar_type() == at::kShort && ent.is_contiguous(), "ent must be int16");
   FDX_CHECK(ptr.dim() == 2, "ptr must be [G, N + 1]");
   const int64_t G = ptr.size(0), N = ptr.size(1) - 1;
-  FDX_CHECK(gbase.numel() == G + 1 && gbin.numel() == G * fdx::kRgBins, "gbase [G + 1] / gbin [G, kRgBins]");
+  FDX_CHECK(gbin.dim() == 2 && gbin.size(0) == G && (gbin.size(1) == 4096 || gbin.size(1) == 8192) &&
+                gbase.numel() == G + 1, "gbase [G + 1] / gbin [G, 4096 or 8192]");
   FDX_CHECK(rowdig.dim() == 2 && rowdig.size(0) == N && rowdig.size(1) == 2, "rowdig must be [N, 2]");
   FDX_CHECK(reinterpret_cast<uintptr_t>(ent.data_ptr()) % 16 == 0 && readable_tail(ent, 8),
             "ent must be 16-byte aligned with 8 readable padding entries");
   FDX_CHECK(np == 1 || np == 4, "np must be 1 or 4");
-  FDX_CHECK(P >= 8 && P % 8 == 0, "P must be a positive multiple of 8");
+  chk(wg, dev, at::kInt, "wg");
+  FDX_CHECK(wg.dim() == 2 && wg.size(0) == 3, "wg must be [3, n_wg] (group, chunk, chunks)");
   FDX_CHECK(list.has_value() == slot_start.has_value(), "list and slot_start go together");
   if (list) {
     chk(*list, dev, at::kInt, "list");
@@ -648,6 +650,7 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
   a.ent = reinterpret_cast<const uint16_t*>(ent.data_ptr<int16_t>());
   a.gbase = gbase.data_ptr<int64_t>();
   a.gbin = gbin.data_ptr<int32_t>();
+  a.gbins = (int32_t)gbin.size(1);
   a.G = (int32_t)G;
   a.N = N;
   a.rowdig = reinterpret_cast<const uint32_t*>(rowdig.data_ptr<int32_t>());
@@ -655,7 +658,11 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
   a.list = opt<int32_t>(list);
   a.slot_start = opt<int32_t>(slot_start);
   a.nslots = (int32_t)nslots;
-  a.P = (int32_t)P;
+  a.wg_g = wg.data_ptr<int32_t>();
+  a.wg_p = a.wg_g + wg.size(1);
+  a.wg_np = a.wg_p + wg.size(1);
+  a.n_wg = (int32_t)wg.size(1);
+  a.dbg = (int32_t)dbg;
   a.slot_node = slot_node.data_ptr<int32_t>();
   a.hist_stride = stride;
   a.hist = hist.data_ptr<int64_t>();

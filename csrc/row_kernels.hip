@@ -109,15 +109,17 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
   }
 }
 
+template <int BINS>
 struct RgShared {
-  int64_t hg[kRgBins];            // separate statistic arrays: a lane's 8-byte atomic spans 2 of 64 banks
-  int64_t hh[kRgBins];
+  int64_t hg[BINS];               // separate statistic arrays: a lane's 8-byte atomic spans 2 of 64 banks
+  int64_t hh[BINS];
 };
 
-__device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared& sh, int g, int s, int tid) {
+template <int BINS>
+__device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS>& sh, int g, int s, int tid) {
   const int64_t hrow = a.slot_node[s];
-  const int32_t* gbin = a.gbin + (int64_t)g * kRgBins;
-  for (int i = tid; i < kRgBins; i += kRgThreads) {
+  const int32_t* gbin = a.gbin + (int64_t)g * a.gbins;
+  for (int i = tid; i < BINS; i += kRgThreads) {
     const int64_t v0 = sh.hg[i], v1 = sh.hh[i];
     if ((v0 | v1) != 0 && hrow >= 0) {
       const int32_t col = gbin[i];
@@ -132,22 +134,57 @@ __device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared& sh, int 
   }
 }
 
-// Workgroup w: group g and list chunk p, w = ((p / 8) * G + g) * 8 + p % 8, so the G workgroups of
-// one chunk share an XCD (workgroups are dealt round-robin over the 8 XCDs) and its L2 serves the
-// chunk's row state G times. Lane = row: the row's (group) run is streamed in aligned 8-entry
-// (16-byte) blocks; every entry adds the row's two statistics into the LDS histograms.
+// Workgroup w: chunk wg_p[w] (of wg_np[w]) of the built-row list, bin group wg_g[w]. Lane = row:
+// the row's run inside the group is streamed in aligned 8-entry (16-byte) blocks and every entry
+// adds the row's two statistics into the LDS histograms; at every slot boundary of the chunk the
+// workgroup flushes its histograms to that slot's level histogram row. The pass is latency-bound
+// (per batch of 64 rows: list -> (ptr, digits) -> entry blocks), so the next batch's row state and
+// the next entry block are loaded before the current ones are consumed.
+template <int BINS>
+__device__ __forceinline__ void rg_row_run(RgShared<BINS>& sh, const uint16_t* ent, uint32_t st, uint32_t en,
+                                           unsigned long long q0, unsigned long long q1, int dbg,
+                                           unsigned long long& sink) {
+  if (en <= st) return;
+  uint32_t blk = st & ~7u;
+  uint4 v = *reinterpret_cast<const uint4*>(ent + blk);
+  for (;;) {
+    const uint32_t nxt = blk + 8;
+    uint4 vn = v;
+    if (nxt < en) vn = *reinterpret_cast<const uint4*>(ent + nxt);
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t i = blk + k;
+      if (i >= st && i < en) {
+        const uint32_t b = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        if (dbg & 2) {
+          sink += b;
+        } else if (dbg & 4) {
+          atomicAdd(reinterpret_cast<unsigned int*>(&sh.hg[b]), (unsigned int)q0);
+          atomicAdd(reinterpret_cast<unsigned int*>(&sh.hh[b]), (unsigned int)q1);
+        } else {
+          atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[b]), q0);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[b]), q1);
+        }
+      }
+    }
+    if (nxt >= en) break;
+    blk = nxt;
+    v = vn;
+  }
+}
+
+template <int BINS>
 __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
-  __shared__ RgShared sh;
+  __shared__ RgShared<BINS> sh;
   const int w = blockIdx.x;
-  const int x = w & 7, rest = w >> 3;
-  const int g = rest % a.G;
-  const int p = (rest / a.G) * 8 + x;
-  if (p >= a.P) return;
+  if (w >= a.n_wg) return;
+  const int g = a.wg_g[w], p = a.wg_p[w], np_g = a.wg_np[w];
   const int64_t T = a.list ? (int64_t)a.slot_start[a.nslots] : a.N;
-  const int64_t a0 = T * p / a.P, a1 = T * (p + 1) / a.P;
+  const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
   if (a0 >= a1) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < kRgBins; i += kRgThreads) {
+  for (int i = tid; i < BINS; i += kRgThreads) {
     sh.hg[i] = 0;
     sh.hh[i] = 0;
   }
@@ -157,43 +194,49 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
     while (s + 1 < a.nslots && a.slot_start[s + 1] <= a0) ++s;
   const uint32_t* ptr = a.ptr + (int64_t)g * (a.N + 1);
   const uint16_t* ent = a.ent + a.gbase[g];
-  const int np = a.np;
+  const int32_t* list = a.list;
+  const int np = a.np, dbg = a.dbg;
+  unsigned long long sink = 0;
   for (;;) {
-    const int64_t ss0 = a.list ? (int64_t)a.slot_start[s] : 0;
-    const int64_t ss1 = a.list ? (int64_t)a.slot_start[s + 1] : a.N;
+    const int64_t ss0 = list ? (int64_t)a.slot_start[s] : 0;
+    const int64_t ss1 = list ? (int64_t)a.slot_start[s + 1] : a.N;
     const int64_t lo = a0 > ss0 ? a0 : ss0, hi = a1 < ss1 ? a1 : ss1;
-    for (int64_t b0 = lo + wv * 64; b0 < hi; b0 += kRgThreads) {
-      const int64_t pos = b0 + lane;
-      uint32_t st = 0, en = 0;
-      unsigned long long q0 = 0, q1 = 0;
-      if (pos < hi) {
-        const int64_t row = a.list ? (int64_t)a.list[pos] : pos;
-        st = ptr[row];
-        en = ptr[row + 1];
-        if (en > st) {
-          const uint2 d = *reinterpret_cast<const uint2*>(a.rowdig + 2 * row);
-          q0 = (unsigned long long)rg_q(d.x, np);
-          q1 = (unsigned long long)rg_q(d.y, np);
-        }
-      }
-      for (uint32_t blk = st & ~7u; blk < en; blk += 8) {
-        const uint4 v = *reinterpret_cast<const uint4*>(ent + blk);
-        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t i = blk + k;
-          if (i >= st && i < en) {
-            const uint32_t b = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-            atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[b]), q0);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[b]), q1);
-          }
-        }
-      }
+    // rows of batch k are pos = lo + wv * 64 + k * kRgThreads + lane; the list entry is read two
+    // batches ahead, (ptr, digits) one batch ahead
+    int64_t pos = lo + wv * 64 + lane;
+    int64_t row_c = list ? (pos < hi ? (int64_t)list[pos] : -1) : (pos < hi ? pos : -1);
+    int64_t row_n = -1;
+    if (list && pos + kRgThreads < hi) row_n = list[pos + kRgThreads];
+    uint32_t st = 0, en = 0;
+    uint2 dg = make_uint2(0u, 0u);
+    if (row_c >= 0) {
+      st = ptr[row_c];
+      en = ptr[row_c + 1];
+      dg = *reinterpret_cast<const uint2*>(a.rowdig + 2 * row_c);
     }
+    for (int64_t b0 = lo + wv * 64; b0 < hi; b0 += kRgThreads, pos += kRgThreads) {
+      // prefetch: batch k + 1's row state, batch k + 2's list entry
+      const int64_t pn = pos + kRgThreads;
+      const int64_t rn = list ? row_n : (pn < hi ? pn : -1);
+      if (list) row_n = pn + kRgThreads < hi ? (int64_t)list[pn + kRgThreads] : -1;
+      uint32_t nst = 0, nen = 0;
+      uint2 ndg = make_uint2(0u, 0u);
+      if (rn >= 0) {
+        nst = ptr[rn];
+        nen = ptr[rn + 1];
+        ndg = *reinterpret_cast<const uint2*>(a.rowdig + 2 * rn);
+      }
+      rg_row_run<BINS>(sh, ent, st, en, (unsigned long long)rg_q(dg.x, np), (unsigned long long)rg_q(dg.y, np), dbg,
+                       sink);
+      st = nst;
+      en = nen;
+      dg = ndg;
+    }
+    if (dbg & 2) atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[lane]), sink);
     __syncthreads();
-    rg_flush(a, sh, g, s, tid);
+    rg_flush<BINS>(a, sh, g, s, tid);
     __syncthreads();
-    if (!a.list || ss1 >= a1 || s + 1 >= a.nslots) break;
+    if (!list || ss1 >= a1 || s + 1 >= a.nslots) break;
     ++s;
   }
 }
@@ -212,8 +255,12 @@ void launch_rg_list(const RgListArgs& a, int pass, hipStream_t s) {
 }
 
 void launch_rg_hist(const RgHistArgs& a, hipStream_t s) {
-  const int64_t blocks = (int64_t)a.G * a.P;
-  if (blocks > 0) hipLaunchKernelGGL(rg_hist_kernel, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
+  const int64_t blocks = a.n_wg;
+  if (blocks <= 0) return;
+  if (a.gbins == 4096)
+    hipLaunchKernelGGL(rg_hist_kernel<4096>, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(rg_hist_kernel<8192>, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
 }
 
 }  // namespace fdx

@@ -199,7 +199,8 @@ FDX_HD int64_t blk_bin_offset(const BlkHistArgs& a, int64_t b) {
 // row's two quantised statistics into int64 LDS histograms of the group's bins, flushed with
 // integer atomics per node slot. Integer sums are order-free: the histograms are bitwise those of
 // the CSC passes and the host.
-constexpr int kRgBins = 8192;               // local bins per group: 2 x 8192 x int64 = 128 KB of LDS
+constexpr int kRgBins = 8192;               // max local bins per group: 2 x 8192 x int64 = 128 KB of LDS
+                                            // (4096-bin groups: two workgroups per CU)
 constexpr int kRgWaves = 16;                // 1024 threads per workgroup (one workgroup per CU)
 constexpr int kRgMaxSlots = 64;
 
@@ -234,7 +235,8 @@ struct RgHistArgs {
   const uint32_t* ptr;            // [G][N + 1]
   const uint16_t* ent;            // entries (readable padding behind the end)
   const int64_t* gbase;           // [G + 1]
-  const int32_t* gbin;            // [G][kRgBins] histogram column of each local bin (-1: unused)
+  const int32_t* gbin;            // [G][gbins] histogram column of each local bin (-1: unused)
+  int32_t gbins;                  // local bins per group: 4096 or 8192
   int32_t G;
   int64_t N;
   const uint32_t* rowdig;         // [N * 2] digit words
@@ -242,7 +244,15 @@ struct RgHistArgs {
   const int32_t* list;            // built rows grouped by slot (nullptr: rows 0..N-1, one slot)
   const int32_t* slot_start;      // [nslots + 1] (nullptr with list == nullptr)
   int32_t nslots;
-  int32_t P;                      // list chunks per group (multiple of 8)
+  // work table: workgroup w takes chunk wg_p[w] of the wg_np[w] equal chunks of the list, for
+  // group wg_g[w] (groups get chunks in proportion to their entries)
+  const int32_t* wg_g;
+  const int32_t* wg_p;
+  const int32_t* wg_np;
+  int32_t n_wg;
+  // diagnostics (bench/probes/rg_probe.py; results wrong when set): bit 1 replaces the LDS
+  // atomics by a register sum, bit 2 adds 32-bit instead of 64-bit words
+  int32_t dbg;
   // output: hist[(slot_node[s] * hist_stride + off(column)) * 2 + stat] +=
   const int32_t* slot_node;
   int64_t hist_stride;

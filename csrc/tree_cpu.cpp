@@ -283,12 +283,10 @@ void rg_list_cpu(const RgListArgs& a) {
 // test checks that the plan covers every built row of every group exactly once.
 void rg_hist_cpu(const RgHistArgs& a) {
   const int64_t T = a.list ? (int64_t)a.slot_start[a.nslots] : a.N;
-  parallel_for((int64_t)a.G * a.P, 0, 1, [&](int64_t lo_w, int64_t hi_w) {
+  parallel_for((int64_t)a.n_wg, 0, 1, [&](int64_t lo_w, int64_t hi_w) {
     for (int64_t w = lo_w; w < hi_w; ++w) {
-      const int x = (int)(w & 7), rest = (int)(w >> 3);
-      const int g = rest % a.G, p = (rest / a.G) * 8 + x;
-      if (p >= a.P) continue;
-      const int64_t a0 = T * p / a.P, a1 = T * (p + 1) / a.P;
+      const int g = a.wg_g[w], p = a.wg_p[w], np_g = a.wg_np[w];
+      const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
       const uint32_t* ptr = a.ptr + (int64_t)g * (a.N + 1);
       const uint16_t* ent = a.ent + a.gbase[g];
       int s = 0;
@@ -302,7 +300,7 @@ void rg_hist_cpu(const RgHistArgs& a) {
         const int64_t row = a.list ? (int64_t)a.list[pos] : pos;
         const int64_t q0 = rg_q(a.rowdig[2 * row], a.np), q1 = rg_q(a.rowdig[2 * row + 1], a.np);
         for (uint32_t i = ptr[row]; i < ptr[row + 1]; ++i) {
-          const int32_t col = a.gbin[(int64_t)g * kRgBins + ent[i]];
+          const int32_t col = a.gbin[(int64_t)g * a.gbins + ent[i]];
           if (col < 0) continue;
           int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
           __atomic_fetch_add(dst, q0, __ATOMIC_RELAXED);

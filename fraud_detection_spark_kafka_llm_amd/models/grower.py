@@ -67,6 +67,7 @@ BLK_MAX_SLOTS = 4
 # row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
 # histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
 ROWHIST = os.environ.get("FDX_ROWHIST", "0") == "1"
+RG_DBG = int(os.environ.get("FDX_RG_DBG", 0))   # diagnostics only (csrc/tree.h RgHistArgs::dbg)
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 
@@ -803,12 +804,12 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             if rg is not None:
                 shard_args = (shards.bin_lo, n_build * shards.Bs) if shards is not None else (None, 0)
                 if d == 0:
-                    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, 1, rg.P, s2n,
-                                   hist_target, h_stride, *shard_args)
+                    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, 1, rg.work(), s2n,
+                                   hist_target, h_stride, *shard_args, RG_DBG)
                 else:
                     C.tree_rg_list(ws.slot8, Q.n_rows, n_build, ws.rg_work, ws.rg_start, ws.rg_list)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
-                                   n_build, rg.P, s2n, hist_target, h_stride, *shard_args)
+                                   n_build, rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG)
                 sel_groups, use_dense = [], False
             elif BLK and np_ == 4 and not build_all and n_build <= BLK_MAX_SLOTS:
                 # row-blocked pass: every feature (hot ones included) in one launch

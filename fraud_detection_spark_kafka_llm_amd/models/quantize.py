@@ -205,9 +205,12 @@ class BlockedCSC:
         return out
 
 
-RG_BINS = 8192           # csrc/tree.h kRgBins: local bins per row group
+RG_BINS = int(os.environ.get("FDX_RG_BINS", 8192))   # local bins per row group: 8192 (1 workgroup per CU) or 4096 (2)
 RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 64))
-RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 1024))   # workgroups per row-group pass (1 resident per CU)
+RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 2048))   # workgroups per row-group pass
+# work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
+# (ptr, digits) loads whether or not it has entries in the group)
+RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 8.0))
 
 
 class RowGroups:
@@ -221,10 +224,13 @@ class RowGroups:
     need more than ``RG_MAX_GROUPS`` groups (very wide vocabularies): the grower then keeps the
     CSC passes."""
 
-    def __init__(self, Q: "Quantized", max_groups: int = None):
+    def __init__(self, Q: "Quantized", max_groups: int = None, bins: int = None):
         C = native.lib()
         dev = Q.device
         max_groups = RG_MAX_GROUPS if max_groups is None else max_groups
+        self.bins = B = RG_BINS if bins is None else bins
+        if B not in (4096, 8192):
+            raise ValueError("row groups hold 4096 or 8192 bins")
         colptr = Q.colptr.cpu().numpy()
         cnt = np.diff(colptr)
         nb = Q.nbins.cpu().numpy().astype(np.int64)
@@ -238,7 +244,7 @@ class RowGroups:
         starts = []
         i = 0
         while i < order.size and len(starts) < max_groups:
-            j = int(np.searchsorted(cum, cum[i] + RG_BINS, side="right")) - 1     # features [i, j) fit
+            j = int(np.searchsorted(cum, cum[i] + B, side="right")) - 1     # features [i, j) fit
             j = max(j, i + 1)
             fs = order[i:j]
             fgroup[fs] = len(starts)
@@ -249,7 +255,7 @@ class RowGroups:
         self.G = G = max(1, len(starts))
         self.n_rows = N = Q.n_rows
         # global column of every local bin
-        gbin = np.full((G, RG_BINS), -1, dtype=np.int32)
+        gbin = np.full((G, B), -1, dtype=np.int32)
         sel = np.nonzero(fgroup >= 0)[0]
         if sel.size:
             rep = nb[sel]
@@ -278,7 +284,25 @@ class RowGroups:
         self.ent = torch.zeros(int(gbase[-1]) + 16, dtype=torch.int16, device=dev)[:int(gbase[-1])]
         C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 1, None, cursor, self.gbase, self.ent)
         del cursor
-        self.P = max(8, -(-max(1, RG_TARGET_WGS // G) // 8) * 8)
+        self._work: dict = {}
+
+    def work(self, target_wgs: int = 0, alpha: float = None) -> torch.Tensor:
+        """Work table [3, n_wg] int32 (group, chunk, chunks of that group): each group's list is cut
+        into chunks in proportion to its modelled cost alpha * rows + entries, so every workgroup
+        carries about 1/target_wgs of the pass (the densest group holds ~79% of the entries on the
+        bench corpus, but every group pays for every listed row)."""
+        target_wgs = target_wgs or RG_TARGET_WGS
+        alpha = RG_ALPHA if alpha is None else alpha
+        t = self._work.get((target_wgs, alpha))
+        if t is None:
+            e = self.group_entries.astype(np.float64) + alpha * self.n_rows
+            npg = np.maximum(1, np.rint(target_wgs * e / max(e.sum(), 1.0))).astype(np.int64)
+            g = np.repeat(np.arange(self.G), npg)
+            p = np.arange(int(npg.sum())) - np.repeat(np.cumsum(npg) - npg, npg)
+            tab = np.stack([g, p, np.repeat(npg, npg)]).astype(np.int32)
+            assert (tab[0] < self.G).all() and (tab[1] < tab[2]).all()
+            t = self._work[(target_wgs, alpha)] = torch.from_numpy(tab).to(self.gbase.device)
+        return t
 
     @property
     def nbytes(self) -> int:

@@ -7,7 +7,7 @@ import torch
 
 from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
 from fraud_detection_spark_kafka_llm_amd.models.grower import Workspace
-from fraud_detection_spark_kafka_llm_amd.models.quantize import RG_BINS, RowGroups, quantize
+from fraud_detection_spark_kafka_llm_amd.models.quantize import RowGroups, quantize
 from fraud_detection_spark_kafka_llm_amd.ops import native
 
 from test_tree_engine import QKW, _hist_ref, _same_trees, random_counts_matrix, vc_from_dense
@@ -40,7 +40,8 @@ def _q_of(ws, np_):
     return q[:, 0], q[:, 1]
 
 
-def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None, np_=4, P=16, max_groups=None):
+def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None, np_=4, P=16, max_groups=None,
+                dbg=0, bins=8192):
     """Histograms of node slots 0..nslots-1 through tree_rg_list + tree_rg_hist, plus q0, q1 and Q;
     ``shards`` = (S, bin_lo) writes the shard-major DP layout (returned unpacked)."""
     C = native.lib()
@@ -48,7 +49,7 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
     Q = quantize(vc.to(dev), max_bins=max_bins, **QKW)
     ws = Workspace(Q)
     _quant(ws, n, dev, np_)
-    rg = RowGroups(Q, max_groups=max_groups)
+    rg = RowGroups(Q, max_groups=max_groups, bins=bins)
     list_ = start = None
     if not root:
         node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
@@ -62,14 +63,14 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
     q0, q1 = _q_of(ws, np_)
     if shards is None:
         hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
-        C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, P, s2n, hist, Q.TB,
-                       None, 0)
+        C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, rg.work(P), s2n,
+                       hist, Q.TB, None, 0, dbg)
         return hist.cpu().numpy(), q0, q1, Q, rg
     S, lo = shards
     Bs = int(np.diff(lo).max())
     buf = torch.zeros((S, nslots, Bs, 2), dtype=torch.int64, device=dev)
-    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, P, s2n,
-                   buf.view(S * nslots, Bs, 2), Bs, torch.from_numpy(lo).to(dev), nslots * Bs)
+    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, rg.work(P), s2n,
+                   buf.view(S * nslots, Bs, 2), Bs, torch.from_numpy(lo).to(dev), nslots * Bs, dbg)
     b = buf.cpu().numpy()
     hist = np.concatenate([b[k, :, : lo[k + 1] - lo[k]] for k in range(S)], axis=1)
     return hist, q0, q1, Q, rg
@@ -80,8 +81,9 @@ def test_row_groups_cover_every_entry_once():
     column; a group holds <= RG_BINS bins, densest features first; group starts are 16-B aligned."""
     vc = _wide(4000, 300, 3)
     Q = quantize(vc, max_bins=100, **QKW)
-    assert Q.TB > RG_BINS                                  # several groups
-    rg = RowGroups(Q)
+    RG_BINS = 4096
+    assert Q.TB > 2 * RG_BINS                              # several groups
+    rg = RowGroups(Q, bins=RG_BINS)
     assert rg.complete and rg.G >= 2
     colptr, boff, rows = Q.colptr.numpy(), Q.boff.numpy(), Q.csc_row.numpy()
     want = sorted((int(r), int(boff[f] + b)) for f in range(Q.Fa)
@@ -111,16 +113,17 @@ def test_row_groups_incomplete_beyond_max_groups():
     assert not rg.complete and rg.G == 1
 
 
-@pytest.mark.parametrize("nslots,root,np_,F", [(1, True, 4, 250), (2, False, 4, 250), (5, False, 4, 250),
-                                                (33, False, 4, 250), (3, False, 1, 250), (1, True, 4, 40),
-                                                (4, False, 4, 40)])
-def test_row_group_histograms_equal_host_reference(nslots, root, np_, F):
+@pytest.mark.parametrize("nslots,root,np_,F,bins", [(1, True, 4, 250, 8192), (2, False, 4, 250, 4096),
+                                                     (5, False, 4, 250, 8192), (33, False, 4, 250, 4096),
+                                                     (3, False, 1, 250, 8192), (1, True, 4, 40, 8192),
+                                                     (4, False, 4, 40, 8192)])
+def test_row_group_histograms_equal_host_reference(nslots, root, np_, F, bins):
     """Several groups (F = 250) and a single group (F = 40: the cursor copy must not alias ptr)."""
     rng = np.random.default_rng(nslots)
     n = 5000
     vc = _wide(n, F, nslots)
     row_node = rng.integers(-1, nslots + 1, n).astype(np.int32) if not root else np.zeros(n, np.int32)
-    hist, q0, q1, Q, rg = _rg_hist_on("cpu", vc, 100, nslots, row_node, root, np_=np_)
+    hist, q0, q1, Q, rg = _rg_hist_on("cpu", vc, 100, nslots, row_node, root, np_=np_, bins=bins)
     assert (rg.G >= 2) == (F > 100)
     np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, nslots, q0, q1))
 
@@ -171,9 +174,9 @@ def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nslots,root", [(1, True), (2, False), (5, False), (32, False)])
+@pytest.mark.parametrize("nslots,root,bins", [(1, True, 8192), (2, False, 4096), (5, False, 8192), (32, False, 4096)])
 @pytest.mark.parametrize("sharded", [False, True])
-def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, sharded):
+def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded):
     """The row-group pass (LDS int64 atomics, 16-B row-run loads, per-slot flushes) equals the
     host's exact int64 sums bit for bit, plain and in the shard-major DP layout."""
     rng = np.random.default_rng(20 + nslots)
@@ -185,8 +188,8 @@ def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, sharded):
         Q0 = quantize(vc, max_bins=200, **QKW)
         lo = np.array([0, Q0.TB // 3, (2 * Q0.TB) // 3, Q0.TB], dtype=np.int64)
         shards = (3, lo)
-    a, *_ = _rg_hist_on("cpu", vc, 200, nslots, row_node, root, shards, P=24)
-    b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24)
+    a, *_ = _rg_hist_on("cpu", vc, 200, nslots, row_node, root, shards, P=24, bins=bins)
+    b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24, bins=bins)
     assert rg.G >= 2
     np.testing.assert_array_equal(a, b)
 
