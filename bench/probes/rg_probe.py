@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--dbg", default="0", help="RgHistArgs::dbg modes (bits 1-2 give wrong sums)")
     ap.add_argument("--alphas", default="8")
     ap.add_argument("--bins", default="8192,4096")
+    ap.add_argument("--split", action="store_true", help="also time the densest group and the rest apart")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     C = native.lib()
@@ -96,7 +97,7 @@ def main():
     rng = np.random.default_rng(0)
     lst = torch.empty(n, dtype=torch.int32, device=dev)
     start = torch.zeros(66, dtype=torch.int32, device=dev)
-    work = torch.zeros(128, dtype=torch.int32, device=dev)
+    work = torch.zeros(128 + 64 * (n // 2048 + 1), dtype=torch.int32, device=dev)
     for ns in [int(x) for x in args.slots.split(",")]:
         root = ns == 1
         slot8 = None
@@ -114,7 +115,9 @@ def main():
         s2n = torch.arange(ns, dtype=torch.int32, device=dev)
         list_ms = 0.0
         if not root:
-            list_ms = timed(lambda: C.tree_rg_list(ws.slot8, n, ns, work, start, lst))
+            rn_d = torch.from_numpy(rn).to(dev)
+            ns_d = node_slot.to(dev)
+            list_ms = timed(lambda: C.tree_rg_list(rn_d, ns_d, None, n, ns, work, start, lst))
         for B, wgs, alpha, dbg in [(B, int(w), float(al), int(db)) for B in rgs for w in args.wgs.split(",")
                                    for al in args.alphas.split(",") for db in args.dbg.split(",")]:
             if True:
@@ -135,6 +138,17 @@ def main():
                                   "list_ms": round(list_ms, 3), "csc_ms": round(csc_ms, 3), "equal": eq}), flush=True)
                 if not eq and dbg < 2:
                     sys.exit("row-group histograms differ from the CSC passes")
+                if args.split and dbg == 0:
+                    # the densest group alone, the other groups alone (which part bounds the pass)
+                    for name, keep in (("group0", wt[0] == 0), ("others", wt[0] != 0)):
+                        sub = wt[:, keep].contiguous()
+
+                        def run_sub():
+                            hist.zero_()
+                            C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
+                                           None if root else start, ns, sub, s2n, hist, Q.TB, None, 0, 0)
+                        print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "part": name,
+                                          "wgs": int(sub.shape[1]), "rg_ms": round(timed(run_sub), 3)}), flush=True)
 
 
 if __name__ == "__main__":

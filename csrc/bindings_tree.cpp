@@ -578,25 +578,39 @@ void rg_build(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& colptr
   }
 }
 
-// Built rows of a level grouped by slot: list [N] int32, slot_start [nslots + 1] int32 (device),
-// work [2 * nslots] int32 scratch (zeroed here).
-void rg_list(const Tensor& slot8, int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start,
-             const Tensor& list) {
-  const auto dev = slot8.device();
-  chk(slot8, dev, at::kByte, "slot8");
+// Built rows of a level grouped by slot: list [N] int32, slot_start [nslots + 1] int32 (device).
+// The slot of a row is node_slot[row_node[r]] (row_node given) or slot8[r]. work: int32 scratch of
+// at least 2 * nslots + 64 * ceil(N / kRgListRows) (zeroed here).
+void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot, const optional<Tensor>& slot8,
+             int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start, const Tensor& list) {
+  const auto dev = list.device();
   chk(work, dev, at::kInt, "work");
   chk(slot_start, dev, at::kInt, "slot_start");
   chk(list, dev, at::kInt, "list");
   FDX_CHECK(nslots >= 1 && nslots <= fdx::kRgMaxSlots, "nslots out of range");
-  FDX_CHECK(slot8.numel() >= N && list.numel() >= N, "slot8 / list must cover the rows");
-  FDX_CHECK(work.numel() >= 2 * nslots && slot_start.numel() >= nslots + 1, "work / slot_start sizes");
+  FDX_CHECK(list.numel() >= N && slot_start.numel() >= nslots + 1, "list / slot_start sizes");
+  const int64_t nwaves = (N + fdx::kRgListRows - 1) / fdx::kRgListRows;
+  FDX_CHECK(work.numel() >= 2 * nslots + 64 * nwaves, "work too small");
   fdx::RgListArgs a{};
-  a.slot8 = slot8.data_ptr<uint8_t>();
+  if (row_node) {
+    FDX_CHECK(node_slot.has_value(), "row_node needs node_slot");
+    chk(*row_node, dev, at::kInt, "row_node");
+    chk(*node_slot, dev, at::kInt, "node_slot");
+    FDX_CHECK(row_node->numel() >= N, "row_node must cover the rows");
+    a.row_node = row_node->data_ptr<int32_t>();
+    a.node_slot = node_slot->data_ptr<int32_t>();
+    a.num_nodes = (int32_t)node_slot->numel();
+  } else {
+    FDX_CHECK(slot8.has_value(), "slot8 or row_node required");
+    chk(*slot8, dev, at::kByte, "slot8");
+    FDX_CHECK(slot8->numel() >= N, "slot8 must cover the rows");
+    a.slot8 = slot8->data_ptr<uint8_t>();
+  }
   a.N = N;
   a.nslots = (int32_t)nslots;
-  a.rows_per_block = 4096;
   a.slot_count = work.data_ptr<int32_t>();
-  a.slot_fill = work.data_ptr<int32_t>() + nslots;
+  a.slot_fill = a.slot_count + nslots;
+  a.wave_count = a.slot_fill + nslots;
   a.slot_start = slot_start.data_ptr<int32_t>();
   a.list = list.data_ptr<int32_t>();
   if (dev.is_cuda()) {

@@ -65,54 +65,79 @@ __global__ __launch_bounds__(256) void rg_build_kernel(RgBuildArgs a, int pass) 
   }
 }
 
-// Pass 0: per-slot row counts (LDS counters, one global atomic per (block, slot)).
-// Pass 1: every block derives the slot starts from the counts, reserves its share of each slot
-// with one atomic and places its rows. Rows of one block stay within one 4096-row window of the
-// list; their order inside it depends on the LDS atomics (sums are exact: nothing depends on it).
+// One wave per kRgListRows consecutive rows, slots counted and placed with wave ballots (one
+// ballot per distinct slot among each 64 rows, no atomics on the rows): pass 0 stores the wave's
+// per-slot counts and adds them to the slot totals; pass 1 derives the slot starts (a wave scan of
+// the totals), reserves the wave's share of every slot with one atomic per slot and writes its
+// rows in ascending order.
 __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
-  __shared__ int32_t s_cnt[kRgMaxSlots];
-  __shared__ int32_t s_base[kRgMaxSlots];
-  const int tid = threadIdx.x;
-  if (tid < kRgMaxSlots) s_cnt[tid] = 0;
-  __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * a.rows_per_block;
-  const int64_t r1 = r0 + a.rows_per_block < a.N ? r0 + a.rows_per_block : a.N;
-  for (int64_t r = r0 + tid; r < r1; r += 256) {
-    const uint32_t s = a.slot8[r];
-    if (s < (uint32_t)a.nslots) atomicAdd(&s_cnt[s], 1);
-  }
-  __syncthreads();
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = wave * kRgListRows;
+  if (r0 >= a.N) return;
+  const int64_t r1 = r0 + kRgListRows < a.N ? r0 + kRgListRows : a.N;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int32_t* wc = a.wave_count + wave * 64;
   if (pass == 0) {
-    if (tid < a.nslots && s_cnt[tid] > 0) atomicAdd(a.slot_count + tid, s_cnt[tid]);
+    int32_t cnt = 0;                           // lane s: rows of slot s
+    for (int64_t rb = r0; rb < r1; rb += 64) {
+      const int64_t r = rb + lane;
+      const uint32_t sl = r < r1 ? rg_slot_of(a, r) : 0xffu;
+      uint64_t act = __ballot(sl < (uint32_t)a.nslots);
+      while (act) {
+        const uint32_t s = __shfl(sl, __ffsll((unsigned long long)act) - 1, 64);
+        const uint64_t m = __ballot(sl == s);
+        if ((uint32_t)lane == s) cnt += __popcll(m);
+        act &= ~m;
+      }
+    }
+    if (lane < a.nslots) {
+      wc[lane] = cnt;
+      if (cnt) atomicAdd(a.slot_count + lane, cnt);
+    }
     return;
   }
-  if (tid == 0) {
-    int32_t acc = 0;
-    for (int s = 0; s < a.nslots; ++s) {
-      const int32_t c = a.slot_count[s];
-      if (blockIdx.x == 0) a.slot_start[s] = acc;
-      s_base[s] = acc;
-      acc += c;
+  // slot starts: exclusive scan of the totals over lanes 0..nslots-1
+  const int32_t tot = lane < a.nslots ? a.slot_count[lane] : 0;
+  int32_t incl = tot;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  if (wave == 0) {
+    if (lane < a.nslots) a.slot_start[lane] = incl - tot;
+    if (lane == a.nslots - 1) a.slot_start[a.nslots] = incl;
+  }
+  const int32_t mine = lane < a.nslots ? wc[lane] : 0;
+  int32_t base = lane < a.nslots ? incl - tot + (mine ? atomicAdd(a.slot_fill + lane, mine) : 0) : 0;
+  for (int64_t rb = r0; rb < r1; rb += 64) {
+    const int64_t r = rb + lane;
+    const uint32_t sl = r < r1 ? rg_slot_of(a, r) : 0xffu;
+    uint64_t act = __ballot(sl < (uint32_t)a.nslots);
+    while (act) {
+      const uint32_t s = __shfl(sl, __ffsll((unsigned long long)act) - 1, 64);
+      const uint64_t m = __ballot(sl == s);
+      const int32_t b = __shfl(base, (int)s, 64);
+      if (sl == s) a.list[b + __popcll(m & lt)] = (int32_t)r;
+      if ((uint32_t)lane == s) base += __popcll(m);
+      act &= ~m;
     }
-    if (blockIdx.x == 0) a.slot_start[a.nslots] = acc;
-  }
-  __syncthreads();
-  if (tid < a.nslots) {
-    const int32_t c = s_cnt[tid];
-    s_base[tid] += c > 0 ? atomicAdd(a.slot_fill + tid, c) : 0;
-    s_cnt[tid] = 0;
-  }
-  __syncthreads();
-  for (int64_t r = r0 + tid; r < r1; r += 256) {
-    const uint32_t s = a.slot8[r];
-    if (s < (uint32_t)a.nslots) a.list[s_base[s] + atomicAdd(&s_cnt[s], 1)] = (int32_t)r;
   }
 }
 
 template <int BINS>
 struct RgShared {
-  int64_t hg[BINS];               // separate statistic arrays: a lane's 8-byte atomic spans 2 of 64 banks
-  int64_t hh[BINS];
+  // separate statistic arrays (a lane's 8-byte atomic spans 2 of 64 banks); bins BINS + lane are
+  // per-lane sinks for the lanes of a block outside their row's run (never flushed)
+  int64_t hg[BINS + 64];
+  int64_t hh[BINS + 64];
+  // per wave: the 64 rows of the current batch (run start / end, statistics, first block index)
+  uint32_t st[kRgWaves][64];
+  uint32_t en[kRgWaves][64];
+  int32_t q0[kRgWaves][64];
+  int32_t q1[kRgWaves][64];
+  uint32_t pb[kRgWaves][64];
 };
 
 template <int BINS>
@@ -134,46 +159,98 @@ __device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS>& sh
   }
 }
 
-// Workgroup w: chunk wg_p[w] (of wg_np[w]) of the built-row list, bin group wg_g[w]. Lane = row:
-// the row's run inside the group is streamed in aligned 8-entry (16-byte) blocks and every entry
-// adds the row's two statistics into the LDS histograms; at every slot boundary of the chunk the
-// workgroup flushes its histograms to that slot's level histogram row. The pass is latency-bound
-// (per batch of 64 rows: list -> (ptr, digits) -> entry blocks), so the next batch's row state and
-// the next entry block are loaded before the current ones are consumed.
-template <int BINS>
-__device__ __forceinline__ void rg_row_run(RgShared<BINS>& sh, const uint16_t* ent, uint32_t st, uint32_t en,
-                                           unsigned long long q0, unsigned long long q1, int dbg,
-                                           unsigned long long& sink) {
-  if (en <= st) return;
-  uint32_t blk = st & ~7u;
-  uint4 v = *reinterpret_cast<const uint4*>(ent + blk);
-  for (;;) {
-    const uint32_t nxt = blk + 8;
-    uint4 vn = v;
-    if (nxt < en) vn = *reinterpret_cast<const uint4*>(ent + nxt);
-    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t i = blk + k;
-      if (i >= st && i < en) {
-        const uint32_t b = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        if (dbg & 2) {
-          sink += b;
-        } else if (dbg & 4) {
-          atomicAdd(reinterpret_cast<unsigned int*>(&sh.hg[b]), (unsigned int)q0);
-          atomicAdd(reinterpret_cast<unsigned int*>(&sh.hh[b]), (unsigned int)q1);
-        } else {
-          atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[b]), q0);
-          atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[b]), q1);
-        }
-      }
-    }
-    if (nxt >= en) break;
-    blk = nxt;
-    v = vn;
-  }
+__device__ __forceinline__ uint32_t rg_nblk(uint32_t st, uint32_t en) {
+  return en > st ? ((en - 1) >> 3) - (st >> 3) + 1 : 0u;
 }
 
+// One batch of 64 rows of a wave, lane-balanced: the rows' 8-entry blocks are numbered
+// consecutively (row by row) and lane l takes the contiguous block range [l K, (l + 1) K), K =
+// ceil(blocks / 64), so every lane streams the same number of blocks whatever the row lengths
+// (rows of the dense group vary ~2x: a lane per row left ~58% of the LDS atomic slots idle).
+// Entries of a block outside its row's run go to the lane's sink bin: no divergent branches.
+template <int BINS>
+__device__ __forceinline__ void rg_batch(RgShared<BINS>& sh, const uint16_t* ent, int wv, int lane, uint32_t st,
+                                         uint32_t en, int32_t q0, int32_t q1, int dbg, unsigned long long& sink) {
+  const uint32_t nb = rg_nblk(st, en);
+  uint32_t incl = nb;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  const uint32_t total = __shfl(incl, 63, 64);
+  if (total == 0) return;
+  sh.st[wv][lane] = st;
+  sh.en[wv][lane] = en;
+  sh.q0[wv][lane] = q0;
+  sh.q1[wv][lane] = q1;
+  sh.pb[wv][lane] = incl - nb;
+  __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): this wave's row table is in LDS
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t K = (total + 63) >> 6;
+  uint32_t t = (uint32_t)lane * K;
+  const uint32_t t1 = t + K < total ? t + K : total;
+  if (t < t1) {
+    // row of block t: the largest r with pb[r] <= t (empty rows share their successor's pb)
+    int r = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+      if (r + step <= 63 && sh.pb[wv][r + step] <= t) r += step;
+    uint32_t rst = sh.st[wv][r], ren = sh.en[wv][r];
+    unsigned long long a0 = (unsigned long long)(int64_t)sh.q0[wv][r], a1 = (unsigned long long)(int64_t)sh.q1[wv][r];
+    uint32_t rnb = rg_nblk(rst, ren);
+    uint32_t j = t - sh.pb[wv][r];
+    const uint32_t sinkb = BINS + lane;
+    uint32_t blk = (rst & ~7u) + 8u * j;
+    uint4 v = *reinterpret_cast<const uint4*>(ent + blk);
+    for (;;) {
+      // next block (same row, or the next non-empty row), loaded before this one is consumed
+      const uint32_t cst = rst, cen = ren, cblk = blk;
+      const unsigned long long c0 = a0, c1 = a1;
+      ++t;
+      const bool more = t < t1;
+      uint4 vn = v;
+      if (more) {
+        if (++j == rnb) {
+          do {                                   // the next row with blocks (t < total: one exists)
+            ++r;
+          } while (rg_nblk(sh.st[wv][r], sh.en[wv][r]) == 0);
+          rst = sh.st[wv][r];
+          ren = sh.en[wv][r];
+          a0 = (unsigned long long)(int64_t)sh.q0[wv][r];
+          a1 = (unsigned long long)(int64_t)sh.q1[wv][r];
+          rnb = rg_nblk(rst, ren);
+          j = 0;
+        }
+        blk = (rst & ~7u) + 8u * j;
+        vn = *reinterpret_cast<const uint4*>(ent + blk);
+      }
+      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t i = cblk + k;
+        const uint32_t bin = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        const uint32_t b = (i >= cst && i < cen) ? bin : sinkb;
+        if (dbg & 2) {
+          sink += b;
+        } else {
+          atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[b]), c0);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[b]), c1);
+        }
+      }
+      if (!more) break;
+      v = vn;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();               // the row table is rewritten by the next batch
+}
+
+// Workgroup w: chunk wg_p[w] (of wg_np[w]) of the built-row list, bin group wg_g[w]. Each wave
+// takes batches of 64 listed rows and streams their runs inside the group in aligned 8-entry
+// (16-byte) blocks, adding every entry's row statistics into the LDS histograms; at every slot
+// boundary of the chunk the workgroup flushes its histograms to that slot's level histogram row.
+// The pass is latency-bound (list -> (ptr, digits) -> entry blocks), so the next batch's row
+// state and the next entry block are loaded before the current ones are consumed.
 template <int BINS>
 __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
   __shared__ RgShared<BINS> sh;
@@ -215,7 +292,6 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
       dg = *reinterpret_cast<const uint2*>(a.rowdig + 2 * row_c);
     }
     for (int64_t b0 = lo + wv * 64; b0 < hi; b0 += kRgThreads, pos += kRgThreads) {
-      // prefetch: batch k + 1's row state, batch k + 2's list entry
       const int64_t pn = pos + kRgThreads;
       const int64_t rn = list ? row_n : (pn < hi ? pn : -1);
       if (list) row_n = pn + kRgThreads < hi ? (int64_t)list[pn + kRgThreads] : -1;
@@ -226,8 +302,7 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
         nen = ptr[rn + 1];
         ndg = *reinterpret_cast<const uint2*>(a.rowdig + 2 * rn);
       }
-      rg_row_run<BINS>(sh, ent, st, en, (unsigned long long)rg_q(dg.x, np), (unsigned long long)rg_q(dg.y, np), dbg,
-                       sink);
+      rg_batch<BINS>(sh, ent, wv, lane, st, en, (int32_t)rg_q(dg.x, np), (int32_t)rg_q(dg.y, np), dbg, sink);
       st = nst;
       en = nen;
       dg = ndg;
@@ -250,7 +325,8 @@ void launch_rg_build(const RgBuildArgs& a, int pass, hipStream_t s) {
 }
 
 void launch_rg_list(const RgListArgs& a, int pass, hipStream_t s) {
-  const int64_t blocks = (a.N + a.rows_per_block - 1) / a.rows_per_block;
+  const int64_t waves = (a.N + kRgListRows - 1) / kRgListRows;
+  const int64_t blocks = (waves + 3) / 4;
   if (blocks > 0) hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, pass);
 }
 

@@ -220,16 +220,30 @@ struct RgBuildArgs {
   uint16_t* ent;                  // pass 1 out
 };
 
+// Built rows of a level grouped by slot. The slot of row r is node_slot[row_node[r]] when
+// row_node is given (slots outside [0, nslots): not built), else slot8[r] (0xff: not built).
+constexpr int kRgListRows = 2048;           // rows per wave of the list kernels
 struct RgListArgs {
-  const uint8_t* slot8;           // [N] pass slot of each row (0xff: not built)
+  const int32_t* row_node;        // [N] or nullptr
+  const int32_t* node_slot;       // [num_nodes] slot of each node (-1: not built)
+  int32_t num_nodes;
+  const uint8_t* slot8;           // [N] (when row_node is nullptr)
   int64_t N;
   int32_t nslots;
-  int32_t rows_per_block;
   int32_t* slot_count;            // [nslots] (zeroed; pass 0 adds)
   int32_t* slot_fill;             // [nslots] (zeroed; pass 1 reserves)
+  int32_t* wave_count;            // [ceil(N / kRgListRows)][64]: pass 0 per-wave counts
   int32_t* slot_start;            // [nslots + 1] out (pass 1)
-  int32_t* list;                  // [N] out (pass 1): built rows grouped by slot
+  int32_t* list;                  // [N] out (pass 1): built rows grouped by slot, ascending inside each
+                                  //   wave's chunk of rows
 };
+
+FDX_HD uint32_t rg_slot_of(const RgListArgs& a, int64_t r) {
+  if (!a.row_node) return a.slot8[r];
+  const int32_t n = a.row_node[r];
+  const int32_t s = (n >= 0 && n < a.num_nodes) ? a.node_slot[n] : -1;
+  return (s >= 0 && s < a.nslots) ? (uint32_t)s : 0xffu;
+}
 
 struct RgHistArgs {
   const uint32_t* ptr;            // [G][N + 1]

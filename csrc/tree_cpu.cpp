@@ -270,13 +270,17 @@ void rg_build_cpu(const RgBuildArgs& a, int pass) {
 // window may differ; the histogram sums do not depend on it).
 void rg_list_cpu(const RgListArgs& a) {
   std::vector<int64_t> cnt(a.nslots + 1, 0);
-  for (int64_t r = 0; r < a.N; ++r)
-    if (a.slot8[r] < (uint32_t)a.nslots) ++cnt[a.slot8[r] + 1];
+  for (int64_t r = 0; r < a.N; ++r) {
+    const uint32_t s = rg_slot_of(a, r);
+    if (s < (uint32_t)a.nslots) ++cnt[s + 1];
+  }
   for (int s = 0; s < a.nslots; ++s) cnt[s + 1] += cnt[s];
   for (int s = 0; s <= a.nslots; ++s) a.slot_start[s] = (int32_t)cnt[s];
   for (int s = 0; s < a.nslots; ++s) a.slot_count[s] = (int32_t)(cnt[s + 1] - cnt[s]);
-  for (int64_t r = 0; r < a.N; ++r)
-    if (a.slot8[r] < (uint32_t)a.nslots) a.list[cnt[a.slot8[r]]++] = (int32_t)r;
+  for (int64_t r = 0; r < a.N; ++r) {
+    const uint32_t s = rg_slot_of(a, r);
+    if (s < (uint32_t)a.nslots) a.list[cnt[s]++] = (int32_t)r;
+  }
 }
 
 // Host twin of rg_hist_kernel, following the same (group, list chunk, slot) work split, so a host

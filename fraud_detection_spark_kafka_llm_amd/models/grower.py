@@ -126,7 +126,8 @@ class Workspace:
         if getattr(self, "rg_list", None) is None:
             self.rg_list = torch.empty(self.Q.n_rows, dtype=torch.int32, device=self.dev)
             self.rg_start = torch.zeros(66, dtype=torch.int32, device=self.dev)
-            self.rg_work = torch.zeros(128, dtype=torch.int32, device=self.dev)
+            nw = -(-self.Q.n_rows // 2048)            # csrc/tree.h kRgListRows
+            self.rg_work = torch.zeros(128 + 64 * nw, dtype=torch.int32, device=self.dev)
         return rg
 
     def run_concurrent(self, launches: list) -> None:
@@ -789,8 +790,9 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 single = n_build == 1 and rg is None
                 if single and getattr(ws, "rowdig_masked", None) is None:
                     ws.rowdig_masked = torch.empty_like(ws.rowdig)
-                C.tree_slot8(ws.row_node, st.node_slot, 0, n_build, ws.slot8, ws.rowdig if single else None,
-                             ws.rowdig_masked if single else None)
+                if rg is None:          # (the row-group engine lists the built rows from row_node itself)
+                    C.tree_slot8(ws.row_node, st.node_slot, 0, n_build, ws.slot8, ws.rowdig if single else None,
+                                 ws.rowdig_masked if single else None)
                 slot8 = ws.slot8
                 csc_slot8, csc_dig = (None, ws.rowdig_masked) if single else (slot8, ws.rowdig)
                 s2n = st.s2n[:n_build]
@@ -807,7 +809,8 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, 1, rg.work(), s2n,
                                    hist_target, h_stride, *shard_args, RG_DBG)
                 else:
-                    C.tree_rg_list(ws.slot8, Q.n_rows, n_build, ws.rg_work, ws.rg_start, ws.rg_list)
+                    C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
+                                   ws.rg_list)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    n_build, rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG)
                 sel_groups, use_dense = [], False

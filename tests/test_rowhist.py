@@ -54,11 +54,10 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
     if not root:
         node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
         node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
-        C.tree_slot8(torch.from_numpy(row_node_np).to(dev), node_slot.to(dev), 0, nslots, ws.slot8, None, None)
         list_ = torch.empty(n, dtype=torch.int32, device=dev)
         start = torch.zeros(nslots + 1, dtype=torch.int32, device=dev)
-        work = torch.zeros(2 * nslots, dtype=torch.int32, device=dev)
-        C.tree_rg_list(ws.slot8, n, nslots, work, start, list_)
+        work = torch.zeros(2 * nslots + 64 * (n // 2048 + 1), dtype=torch.int32, device=dev)
+        C.tree_rg_list(torch.from_numpy(row_node_np).to(dev), node_slot.to(dev), None, n, nslots, work, start, list_)
     s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
     q0, q1 = _q_of(ws, np_)
     if shards is None:
@@ -128,19 +127,37 @@ def test_row_group_histograms_equal_host_reference(nslots, root, np_, F, bins):
     np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, nslots, q0, q1))
 
 
-def test_row_group_list_groups_built_rows_by_slot():
+def _list_check(dev, n, ns, seed):
     C = native.lib()
-    rng = np.random.default_rng(9)
-    n, ns = 20000, 7
-    slot8 = rng.integers(0, ns + 3, n).astype(np.uint8)
-    slot8[slot8 >= ns] = 0xFF
-    lst = torch.empty(n, dtype=torch.int32)
-    start = torch.zeros(ns + 1, dtype=torch.int32)
-    C.tree_rg_list(torch.from_numpy(slot8), n, ns, torch.zeros(2 * ns, dtype=torch.int32), start, lst)
-    st = start.numpy()
+    rng = np.random.default_rng(seed)
+    row_node = rng.integers(-1, 2 * ns + 2, n).astype(np.int32)
+    node_slot = np.full(2 * ns + 1, -1, dtype=np.int32)
+    node_slot[rng.permutation(2 * ns + 1)[:ns]] = np.arange(ns, dtype=np.int32)
+    sl = np.where((row_node >= 0) & (row_node < node_slot.size), node_slot[np.clip(row_node, 0, node_slot.size - 1)], -1)
+    lst = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    start = torch.zeros(ns + 1, dtype=torch.int32, device=dev)
+    work = torch.full((2 * ns + 64 * (n // 2048 + 1),), 99, dtype=torch.int32, device=dev)
+    C.tree_rg_list(torch.from_numpy(row_node).to(dev), torch.from_numpy(node_slot).to(dev), None, n, ns, work,
+                   start, lst)
+    st, lst = start.cpu().numpy(), lst.cpu().numpy()
     for s in range(ns):
-        np.testing.assert_array_equal(np.sort(lst.numpy()[st[s]:st[s + 1]]), np.nonzero(slot8 == s)[0])
-    assert st[-1] == (slot8 != 0xFF).sum()
+        np.testing.assert_array_equal(np.sort(lst[st[s]:st[s + 1]]), np.nonzero(sl == s)[0])
+    assert st[0] == 0 and st[-1] == (sl >= 0).sum()
+    # from slot bytes
+    slot8 = np.where(sl >= 0, sl, 0xFF).astype(np.uint8)
+    C.tree_rg_list(None, None, torch.from_numpy(slot8).to(dev), n, ns, work, start, torch.from_numpy(lst).to(dev))
+    return st
+
+
+def test_row_group_list_groups_built_rows_by_slot():
+    _list_check("cpu", 20000, 7, 9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ns", [(20000, 7), (100003, 1), (300000, 16), (70001, 64)])
+def test_gpu_row_group_list_equals_host(n, ns):
+    """Ballot-placed lists: every built row once, grouped by slot, slot starts exact."""
+    np.testing.assert_array_equal(_list_check("cuda:0", n, ns, n), _list_check("cpu", n, ns, n))
 
 
 def test_row_group_sharded_layout_equals_plain():
