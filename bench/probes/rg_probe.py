@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--alphas", default="8")
     ap.add_argument("--bins", default="8192,4096")
     ap.add_argument("--split", action="store_true", help="also time the densest group and the rest apart")
+    ap.add_argument("--modes", default="auto", help="group pass modes: auto (the layout's), 0 (lane per row), 1 (balanced)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     C = native.lib()
@@ -97,7 +98,8 @@ def main():
     rng = np.random.default_rng(0)
     lst = torch.empty(n, dtype=torch.int32, device=dev)
     start = torch.zeros(66, dtype=torch.int32, device=dev)
-    work = torch.zeros(128 + 64 * (n // 2048 + 1), dtype=torch.int32, device=dev)
+    work = torch.zeros(64 * (2 + n // 2048 + 1), dtype=torch.int32, device=dev)
+    ldig = torch.empty((n, 2), dtype=torch.int32, device=dev)
     for ns in [int(x) for x in args.slots.split(",")]:
         root = ns == 1
         slot8 = None
@@ -117,23 +119,26 @@ def main():
         if not root:
             rn_d = torch.from_numpy(rn).to(dev)
             ns_d = node_slot.to(dev)
-            list_ms = timed(lambda: C.tree_rg_list(rn_d, ns_d, None, n, ns, work, start, lst))
-        for B, wgs, alpha, dbg in [(B, int(w), float(al), int(db)) for B in rgs for w in args.wgs.split(",")
-                                   for al in args.alphas.split(",") for db in args.dbg.split(",")]:
+            list_ms = timed(lambda: C.tree_rg_list(rn_d, ns_d, None, n, ns, work, start, lst, ws.rowdig, ldig))
+        for B, wgs, alpha, dbg, mode in [(B, int(w), float(al), int(db), md) for B in rgs for w in args.wgs.split(",")
+                                         for al in args.alphas.split(",") for db in args.dbg.split(",")
+                                         for md in args.modes.split(",")]:
             if True:
                 rg = rgs[B]
+                gm = rg.gmode if mode == "auto" else torch.full_like(rg.gmode, int(mode))
                 hist = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)
                 wt = rg.work(wgs, alpha)
 
                 def run():
                     hist.zero_()
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
-                                   None if root else start, ns, wt, s2n, hist, Q.TB, None, 0, dbg)
+                                   None if root else start, None if root else ldig, ns, gm, wt, s2n, hist, Q.TB,
+                                   None, 0, dbg)
                 ms = timed(run)
                 if zb is not None:
                     hist[:, zb] = 0
                 eq = bool(torch.equal(hist, ref))
-                print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "wgs": int(wt.shape[1]), "dbg": dbg,
+                print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "mode": mode, "wgs": int(wt.shape[1]), "dbg": dbg,
                                   "rg_ms": round(ms, 3),
                                   "list_ms": round(list_ms, 3), "csc_ms": round(csc_ms, 3), "equal": eq}), flush=True)
                 if not eq and dbg < 2:
@@ -146,8 +151,9 @@ def main():
                         def run_sub():
                             hist.zero_()
                             C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
-                                           None if root else start, ns, sub, s2n, hist, Q.TB, None, 0, 0)
-                        print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "part": name,
+                                           None if root else start, None if root else ldig, ns, gm, sub, s2n, hist,
+                                           Q.TB, None, 0, dbg)
+                        print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "mode": mode, "dbg": dbg, "part": name,
                                           "wgs": int(sub.shape[1]), "rg_ms": round(timed(run_sub), 3)}), flush=True)
 
 

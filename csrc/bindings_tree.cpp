@@ -578,11 +578,70 @@ void rg_build(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& colptr
   }
 }
 
+// Row-group CSR build from a count-path CSR (indptr, idx, counts float32 / float64 / int32).
+// pass 0: ptr [G, N + 1] int32 gets the (group, row) counts at [g][r + 1] ([g][0] left as is);
+// pass 1: ptr holds the exclusive starts, ent (int16) written at gbase[g] + start + k.
+template <class V>
+void rg_build_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& counts, const Tensor& remap,
+                    int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, int64_t pass, const Tensor& ptr,
+                    const optional<Tensor>& gbase, const optional<Tensor>& ent) {
+  const auto dev = indptr.device();
+  fdx::RgCsrBuildArgs<V> a{};
+  a.indptr = indptr.data_ptr<int64_t>();
+  a.idx = idx.data_ptr<int32_t>();
+  a.counts = counts.data_ptr<V>();
+  a.N = indptr.numel() - 1;
+  a.remap = remap.data_ptr<int32_t>();
+  a.max_bin = (int32_t)max_bin;
+  a.fgroup = fgroup.data_ptr<int32_t>();
+  a.flocal = flocal.data_ptr<int32_t>();
+  a.G = (int32_t)ptr.size(0);
+  a.ptr = reinterpret_cast<uint32_t*>(ptr.data_ptr<int32_t>());
+  if (pass == 1) {
+    FDX_CHECK(gbase && ent, "pass 1 needs gbase and ent");
+    chk(*gbase, dev, at::kLong, "gbase");
+    FDX_CHECK(ent->device() == dev && ent->scalar_type() == at::kShort && ent->is_contiguous(), "ent must be int16");
+    a.gbase = gbase->data_ptr<int64_t>();
+    a.ent = reinterpret_cast<uint16_t*>(ent->data_ptr<int16_t>());
+  }
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rg_build_csr<V>(a, (int)pass, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rg_build_csr_cpu<V>(a, (int)pass);
+  }
+}
+
+void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts, const Tensor& remap,
+                  int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, int64_t pass, const Tensor& ptr,
+                  const optional<Tensor>& gbase, const optional<Tensor>& ent) {
+  const auto dev = indptr.device();
+  chk(indptr, dev, at::kLong, "indptr");
+  chk(idx, dev, at::kInt, "idx");
+  chk(remap, dev, at::kInt, "remap");
+  chk(fgroup, dev, at::kInt, "fgroup");
+  chk(flocal, dev, at::kInt, "flocal");
+  chk(ptr, dev, at::kInt, "ptr");
+  FDX_CHECK(counts.device() == dev && counts.is_contiguous() && counts.numel() >= idx.numel(), "counts");
+  FDX_CHECK(ptr.dim() == 2 && ptr.size(1) == indptr.numel() && ptr.size(0) <= fdx::kRgMaxSlots,
+            "ptr must be [G <= 64, N + 1]");
+  FDX_CHECK(fgroup.numel() == flocal.numel(), "fgroup / flocal");
+  switch (counts.scalar_type()) {
+    case at::kFloat: rg_build_csr_t<float>(indptr, idx, counts, remap, max_bin, fgroup, flocal, pass, ptr, gbase, ent); break;
+    case at::kDouble: rg_build_csr_t<double>(indptr, idx, counts, remap, max_bin, fgroup, flocal, pass, ptr, gbase, ent); break;
+    case at::kInt: rg_build_csr_t<int32_t>(indptr, idx, counts, remap, max_bin, fgroup, flocal, pass, ptr, gbase, ent); break;
+    default: FDX_CHECK(false, "counts must be float32, float64 or int32");
+  }
+}
+
 // Built rows of a level grouped by slot: list [N] int32, slot_start [nslots + 1] int32 (device).
 // The slot of a row is node_slot[row_node[r]] (row_node given) or slot8[r]. work: int32 scratch of
-// at least 2 * nslots + 64 * ceil(N / kRgListRows) (zeroed here).
+// at least nslots * (2 + ceil(N / kRgListRows)). With rowdig, listdig [N, 2] receives the digit
+// words of the listed rows by list position.
 void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot, const optional<Tensor>& slot8,
-             int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start, const Tensor& list) {
+             int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start, const Tensor& list,
+             const optional<Tensor>& rowdig, const optional<Tensor>& listdig) {
   const auto dev = list.device();
   chk(work, dev, at::kInt, "work");
   chk(slot_start, dev, at::kInt, "slot_start");
@@ -590,7 +649,7 @@ void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot
   FDX_CHECK(nslots >= 1 && nslots <= fdx::kRgMaxSlots, "nslots out of range");
   FDX_CHECK(list.numel() >= N && slot_start.numel() >= nslots + 1, "list / slot_start sizes");
   const int64_t nwaves = (N + fdx::kRgListRows - 1) / fdx::kRgListRows;
-  FDX_CHECK(work.numel() >= 2 * nslots + 64 * nwaves, "work too small");
+  FDX_CHECK(work.numel() >= 2 * nslots + nslots * nwaves, "work too small");
   fdx::RgListArgs a{};
   if (row_node) {
     FDX_CHECK(node_slot.has_value(), "row_node needs node_slot");
@@ -609,15 +668,20 @@ void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot
   a.N = N;
   a.nslots = (int32_t)nslots;
   a.slot_count = work.data_ptr<int32_t>();
-  a.slot_fill = a.slot_count + nslots;
-  a.wave_count = a.slot_fill + nslots;
+  a.wave_count = a.slot_count + 2 * nslots;
   a.slot_start = slot_start.data_ptr<int32_t>();
   a.list = list.data_ptr<int32_t>();
+  FDX_CHECK(rowdig.has_value() == listdig.has_value(), "rowdig and listdig go together");
+  if (rowdig) {
+    chk(*rowdig, dev, at::kInt, "rowdig");
+    chk(*listdig, dev, at::kInt, "listdig");
+    FDX_CHECK(rowdig->numel() >= 2 * N && listdig->numel() >= 2 * N, "rowdig / listdig must be [N, 2]");
+    a.rowdig = reinterpret_cast<const uint32_t*>(rowdig->data_ptr<int32_t>());
+    a.listdig = reinterpret_cast<uint32_t*>(listdig->data_ptr<int32_t>());
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    C10_HIP_CHECK(hipMemsetAsync(work.data_ptr(), 0, sizeof(int32_t) * 2 * nslots, stream(dev)));
-    fdx::launch_rg_list(a, 0, stream(dev));
-    fdx::launch_rg_list(a, 1, stream(dev));
+    fdx::launch_rg_list(a, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
     fdx::rg_list_cpu(a);
@@ -627,9 +691,10 @@ void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot
 // Row-group histogram pass: hist[(slot_node[s] * stride + off(gbin[g][b])) * 2 + stat] += exact
 // sums over the built rows (list = None: every row, one slot). wg [3, n_wg]: the work table.
 void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Tensor& gbin, const Tensor& rowdig,
-             int64_t np, const optional<Tensor>& list, const optional<Tensor>& slot_start, int64_t nslots,
-             const Tensor& wg, const Tensor& slot_node, const Tensor& hist, int64_t stride,
-             const optional<Tensor>& shard_lo, int64_t shard_stride, int64_t dbg) {
+             int64_t np, const optional<Tensor>& list, const optional<Tensor>& slot_start,
+             const optional<Tensor>& listdig, int64_t nslots, const Tensor& gmode, const Tensor& wg,
+             const Tensor& slot_node, const Tensor& hist, int64_t stride, const optional<Tensor>& shard_lo,
+             int64_t shard_stride, int64_t dbg) {
   const auto dev = ptr.device();
   chk(ptr, dev, at::kInt, "ptr");
   chk(gbase, dev, at::kLong, "gbase");
@@ -649,10 +714,15 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
   chk(wg, dev, at::kInt, "wg");
   FDX_CHECK(wg.dim() == 2 && wg.size(0) == 3, "wg must be [3, n_wg] (group, chunk, chunks)");
   FDX_CHECK(list.has_value() == slot_start.has_value(), "list and slot_start go together");
+  chk(gmode, dev, at::kByte, "gmode");
+  FDX_CHECK(gmode.numel() == G, "gmode must be [G]");
   if (list) {
     chk(*list, dev, at::kInt, "list");
     chk(*slot_start, dev, at::kInt, "slot_start");
-    FDX_CHECK(list->numel() >= N && slot_start->numel() >= nslots + 1, "list / slot_start sizes");
+    FDX_CHECK(listdig.has_value(), "a list pass needs listdig");
+    chk(*listdig, dev, at::kInt, "listdig");
+    FDX_CHECK(list->numel() >= N && slot_start->numel() >= nslots + 1 && listdig->numel() >= 2 * N,
+              "list / slot_start / listdig sizes");
     FDX_CHECK(nslots >= 1 && nslots <= fdx::kRgMaxSlots, "nslots out of range");
   } else {
     FDX_CHECK(nslots == 1, "the all-rows pass has one slot");
@@ -671,6 +741,8 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
   a.np = (int32_t)np;
   a.list = opt<int32_t>(list);
   a.slot_start = opt<int32_t>(slot_start);
+  a.listdig = list ? reinterpret_cast<const uint32_t*>(listdig->data_ptr<int32_t>()) : nullptr;
+  a.gmode = gmode.data_ptr<uint8_t>();
   a.nslots = (int32_t)nslots;
   a.wg_g = wg.data_ptr<int32_t>();
   a.wg_p = a.wg_g + wg.size(1);
@@ -1092,6 +1164,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_blk_gw", &blk_gw);
   m.def("tree_rg_build", &rg_build);
   m.def("tree_rg_list", &rg_list);
+  m.def("tree_rg_build_csr", &rg_build_csr);
   m.def("tree_rg_hist", &rg_hist);
   m.def("tree_rf_sample", &rf_sample);
   m.def("tree_rf_rows", &rf_rows);

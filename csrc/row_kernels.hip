@@ -65,36 +65,79 @@ __global__ __launch_bounds__(256) void rg_build_kernel(RgBuildArgs a, int pass) 
   }
 }
 
-// One wave per kRgListRows consecutive rows, slots counted and placed with wave ballots (one
-// ballot per distinct slot among each 64 rows, no atomics on the rows): pass 0 stores the wave's
-// per-slot counts and adds them to the slot totals; pass 1 derives the slot starts (a wave scan of
-// the totals), reserves the wave's share of every slot with one atomic per slot and writes its
-// rows in ascending order.
+template <class V>
+__device__ __forceinline__ int32_t rg_count_bin(V c, int32_t max_bin) {
+  if (!(c > (V)0)) return 0;
+  const double d = (double)c;
+  const int32_t b = d >= 255.0 ? 255 : (int32_t)d;
+  return b < max_bin ? b : max_bin;
+}
+
+template <class V>
+__global__ __launch_bounds__(256) void rg_build_csr_kernel(RgCsrBuildArgs<V> a, int pass) {
+  __shared__ uint32_t s_c[kRgMaxSlots][256];       // per (group, row of the block): count / cursor
+  const int tid = threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.x * 256 + tid;
+  const bool live = r < a.N;
+  for (int g = 0; g < a.G; ++g)
+    s_c[g][tid] = (pass == 1 && live) ? a.ptr[(int64_t)g * (a.N + 1) + r] : 0u;
+  if (live) {
+    const int64_t e0 = a.indptr[r], e1 = a.indptr[r + 1];
+    for (int64_t e = e0; e < e1; ++e) {
+      const int32_t fa = a.remap[a.idx[e]];
+      if (fa < 0) continue;
+      const int32_t g = a.fgroup[fa];
+      if (g < 0) continue;
+      if (pass == 0) {
+        s_c[g][tid] += 1;
+      } else {
+        const uint32_t pos = s_c[g][tid]++;
+        a.ent[a.gbase[g] + pos] = (uint16_t)(a.flocal[fa] + rg_count_bin<V>(a.counts[e], a.max_bin));
+      }
+    }
+  }
+  if (pass == 0 && live)
+    for (int g = 0; g < a.G; ++g) a.ptr[(int64_t)g * (a.N + 1) + r + 1] = s_c[g][tid];
+}
+
+// One wave per kRgListRows consecutive rows (all its row_node / slot loads issued up front), slots
+// counted and placed with wave ballots (one ballot per distinct slot among each 64 rows). Pass 0
+// stores the wave's per-slot counts; pass 2 (one block per slot) turns them into per-wave offsets
+// inside the slot plus the slot totals; pass 1 derives the slot starts (a wave scan of the totals)
+// and writes the wave's rows (and their digit words) in ascending order. No atomics: the list is
+// sorted by (slot, row), and no counter is contended (one global counter per slot, added to by
+// every wave, serialised ~39K atomics per level at 10M rows: ~1.4 ms).
+constexpr int kRgListSteps = kRgListRows / 64;
+
 __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int64_t r0 = wave * kRgListRows;
   if (r0 >= a.N) return;
-  const int64_t r1 = r0 + kRgListRows < a.N ? r0 + kRgListRows : a.N;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  int32_t* wc = a.wave_count + wave * 64;
+  int32_t* wc = a.wave_count + wave * a.nslots;
+  constexpr int KB = 8;                        // steps whose slot loads are in flight together
+  uint32_t sl[KB];
   if (pass == 0) {
     int32_t cnt = 0;                           // lane s: rows of slot s
-    for (int64_t rb = r0; rb < r1; rb += 64) {
-      const int64_t r = rb + lane;
-      const uint32_t sl = r < r1 ? rg_slot_of(a, r) : 0xffu;
-      uint64_t act = __ballot(sl < (uint32_t)a.nslots);
-      while (act) {
-        const uint32_t s = __shfl(sl, __ffsll((unsigned long long)act) - 1, 64);
-        const uint64_t m = __ballot(sl == s);
-        if ((uint32_t)lane == s) cnt += __popcll(m);
-        act &= ~m;
+    for (int k0 = 0; k0 < kRgListSteps; k0 += KB) {
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const int64_t r = r0 + 64 * (k0 + k) + lane;
+        sl[k] = r < a.N ? rg_slot_of(a, r) : 0xffu;
+      }
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        uint64_t act = __ballot(sl[k] < (uint32_t)a.nslots);
+        while (act) {
+          const uint32_t s = __shfl(sl[k], __ffsll((unsigned long long)act) - 1, 64);
+          const uint64_t m = __ballot(sl[k] == s);
+          if ((uint32_t)lane == s) cnt += __popcll(m);
+          act &= ~m;
+        }
       }
     }
-    if (lane < a.nslots) {
-      wc[lane] = cnt;
-      if (cnt) atomicAdd(a.slot_count + lane, cnt);
-    }
+    if (lane < a.nslots) wc[lane] = cnt;
     return;
   }
   // slot starts: exclusive scan of the totals over lanes 0..nslots-1
@@ -109,21 +152,63 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
     if (lane < a.nslots) a.slot_start[lane] = incl - tot;
     if (lane == a.nslots - 1) a.slot_start[a.nslots] = incl;
   }
-  const int32_t mine = lane < a.nslots ? wc[lane] : 0;
-  int32_t base = lane < a.nslots ? incl - tot + (mine ? atomicAdd(a.slot_fill + lane, mine) : 0) : 0;
-  for (int64_t rb = r0; rb < r1; rb += 64) {
-    const int64_t r = rb + lane;
-    const uint32_t sl = r < r1 ? rg_slot_of(a, r) : 0xffu;
-    uint64_t act = __ballot(sl < (uint32_t)a.nslots);
-    while (act) {
-      const uint32_t s = __shfl(sl, __ffsll((unsigned long long)act) - 1, 64);
-      const uint64_t m = __ballot(sl == s);
-      const int32_t b = __shfl(base, (int)s, 64);
-      if (sl == s) a.list[b + __popcll(m & lt)] = (int32_t)r;
-      if ((uint32_t)lane == s) base += __popcll(m);
-      act &= ~m;
+  int32_t base = lane < a.nslots ? incl - tot + wc[lane] : 0;
+  for (int k0 = 0; k0 < kRgListSteps; k0 += KB) {
+    uint2 d[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int64_t r = r0 + 64 * (k0 + k) + lane;
+      sl[k] = r < a.N ? rg_slot_of(a, r) : 0xffu;
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int64_t r = r0 + 64 * (k0 + k) + lane;
+      d[k] = (a.listdig && sl[k] < (uint32_t)a.nslots) ? *reinterpret_cast<const uint2*>(a.rowdig + 2 * r)
+                                                         : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int64_t r = r0 + 64 * (k0 + k) + lane;
+      uint64_t act = __ballot(sl[k] < (uint32_t)a.nslots);
+      while (act) {
+        const uint32_t s = __shfl(sl[k], __ffsll((unsigned long long)act) - 1, 64);
+        const uint64_t m = __ballot(sl[k] == s);
+        const int32_t b = __shfl(base, (int)s, 64);
+        if (sl[k] == s) {
+          const int64_t pos = b + __popcll(m & lt);
+          a.list[pos] = (int32_t)r;
+          if (a.listdig) *reinterpret_cast<uint2*>(a.listdig + 2 * pos) = d[k];
+        }
+        if ((uint32_t)lane == s) base += __popcll(m);
+        act &= ~m;
+      }
     }
   }
+}
+
+// Pass 2: block s scans slot s's per-wave counts into per-wave offsets (in place) and its total.
+__global__ __launch_bounds__(1024) void rg_list_scan_kernel(RgListArgs a, int64_t nwaves) {
+  __shared__ int32_t s_sum[1024];
+  const int s = blockIdx.x, t = threadIdx.x;
+  const int64_t per = (nwaves + 1023) / 1024;
+  const int64_t w0 = t * per, w1 = w0 + per < nwaves ? w0 + per : nwaves;
+  int32_t sum = 0;
+  for (int64_t w = w0; w < w1; ++w) sum += a.wave_count[w * a.nslots + s];
+  s_sum[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {           // Hillis-Steele inclusive scan of the thread sums
+    const int32_t o = t >= d ? s_sum[t - d] : 0;
+    __syncthreads();
+    s_sum[t] += o;
+    __syncthreads();
+  }
+  int32_t acc = s_sum[t] - sum;
+  for (int64_t w = w0; w < w1; ++w) {
+    const int32_t c = a.wave_count[w * a.nslots + s];
+    a.wave_count[w * a.nslots + s] = acc;
+    acc += c;
+  }
+  if (t == 1023) a.slot_count[s] = s_sum[1023];
 }
 
 template <int BINS>
@@ -245,6 +330,149 @@ __device__ __forceinline__ void rg_batch(RgShared<BINS>& sh, const uint16_t* ent
   __builtin_amdgcn_wave_barrier();               // the row table is rewritten by the next batch
 }
 
+// Dense groups: batches of 64 listed rows, block-balanced (rg_batch); the list entry is read two
+// batches ahead, (ptr, digits) one batch ahead.
+template <int BINS>
+__device__ __forceinline__ void rg_range_dense(RgShared<BINS>& sh, const RgHistArgs& a, const uint32_t* ptr,
+                                             const uint16_t* ent, const uint32_t* pdig, int64_t lo, int64_t hi,
+                                             int wv, int lane, int np, int dbg, unsigned long long& sink) {
+  const int32_t* list = a.list;
+  int64_t pos = lo + wv * 64 + lane;
+  int64_t row_c = list ? (pos < hi ? (int64_t)list[pos] : -1) : (pos < hi ? pos : -1);
+  int64_t row_n = -1;
+  if (list && pos + kRgThreads < hi) row_n = list[pos + kRgThreads];
+  uint32_t st = 0, en = 0;
+  uint2 dg = make_uint2(0u, 0u);
+  if (row_c >= 0) {
+    st = ptr[row_c];
+    en = ptr[row_c + 1];
+    dg = *reinterpret_cast<const uint2*>(pdig + 2 * pos);
+  }
+  for (int64_t b0 = lo + wv * 64; b0 < hi; b0 += kRgThreads, pos += kRgThreads) {
+    const int64_t pn = pos + kRgThreads;
+    const int64_t rn = list ? row_n : (pn < hi ? pn : -1);
+    if (list) row_n = pn + kRgThreads < hi ? (int64_t)list[pn + kRgThreads] : -1;
+    uint32_t nst = 0, nen = 0;
+    uint2 ndg = make_uint2(0u, 0u);
+    if (rn >= 0) {
+      nst = ptr[rn];
+      nen = ptr[rn + 1];
+      ndg = *reinterpret_cast<const uint2*>(pdig + 2 * pn);
+    }
+    rg_batch<BINS>(sh, ent, wv, lane, st, en, (int32_t)rg_q(dg.x, np), (int32_t)rg_q(dg.y, np), dbg, sink);
+    st = nst;
+    en = nen;
+    dg = ndg;
+  }
+}
+
+// Sparse groups (~2 entries per row): the per-batch work (~16 atomics per lane) is far shorter
+// than a memory round trip, and a lane per row, a lane-balanced batch and an entry-granular batch
+// all ran at ~1.1 ms for the 205M sparse entries of the root pass (bench/probes/rg_probe.py,
+// profiles/r3s2): each batch waited ~one HBM latency. So a wave walks its rows in super-batches
+// of kRgSB batches (a lane per row) through a 3-stage pipeline -- list entries of super-batch
+// j + 3, (ptr, digits) of j + 2, the rows' first 8-entry blocks of j + 1 -- while the atomics of
+// super-batch j run: every load has a whole super-batch of work to arrive in.
+constexpr int kRgSB = 3;
+
+template <int BINS>
+__device__ __forceinline__ void rg_run_block(RgShared<BINS>& sh, uint4 v, uint32_t blk, uint32_t st, uint32_t en,
+                                             unsigned long long c0, unsigned long long c1, uint32_t sinkb, int dbg,
+                                             unsigned long long& sink) {
+  const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t i = blk + k;
+    const uint32_t bin = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+    const uint32_t b = (i >= st && i < en) ? bin : sinkb;
+    if (dbg & 2) {
+      sink += b;
+    } else {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[b]), c0);
+      atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[b]), c1);
+    }
+  }
+}
+
+template <int BINS>
+__device__ __forceinline__ void rg_range_sparse(RgShared<BINS>& sh, const RgHistArgs& a, const uint32_t* ptr,
+                                                const uint16_t* ent, const uint32_t* pdig, int64_t lo, int64_t hi,
+                                                int wv, int lane, int np, int dbg, unsigned long long& sink) {
+  const int32_t* list = a.list;
+  const int64_t p0 = lo + wv * 64 + lane;
+  constexpr int64_t kSBStride = (int64_t)kRgSB * kRgThreads;      // positions per super-batch
+  const uint32_t sinkb = BINS + lane;
+  auto pos_of = [&](int64_t j, int i) -> int64_t { return p0 + j * kSBStride + (int64_t)i * kRgThreads; };
+  auto rows_of = [&](int64_t j, int32_t* r) {
+#pragma unroll
+    for (int i = 0; i < kRgSB; ++i) {
+      const int64_t p = pos_of(j, i);
+      r[i] = p < hi ? (list ? list[p] : (int32_t)p) : -1;
+    }
+  };
+  auto info_of = [&](int64_t j, const int32_t* r, uint32_t* st, uint32_t* en, uint2* dg) {
+#pragma unroll
+    for (int i = 0; i < kRgSB; ++i) {
+      st[i] = en[i] = 0u;
+      dg[i] = make_uint2(0u, 0u);
+      if (r[i] >= 0) {
+        st[i] = ptr[r[i]];
+        en[i] = ptr[r[i] + 1];
+        dg[i] = *reinterpret_cast<const uint2*>(pdig + 2 * pos_of(j, i));
+      }
+    }
+  };
+  auto blocks_of = [&](const uint32_t* st, const uint32_t* en, uint4* v) {
+#pragma unroll
+    for (int i = 0; i < kRgSB; ++i)
+      v[i] = en[i] > st[i] ? *reinterpret_cast<const uint4*>(ent + (st[i] & ~7u)) : make_uint4(0u, 0u, 0u, 0u);
+  };
+  if (p0 - lane >= hi) return;
+  // prologue: super-batch 0 through stage 3, 1 through stage 2, 2 through stage 1
+  int32_t r0[kRgSB], r1[kRgSB], r2[kRgSB];
+  uint32_t st0[kRgSB], en0[kRgSB], st1[kRgSB], en1[kRgSB];
+  uint2 dg0[kRgSB], dg1[kRgSB];
+  uint4 v0[kRgSB];
+  rows_of(0, r0);
+  rows_of(1, r1);
+  rows_of(2, r2);
+  info_of(0, r0, st0, en0, dg0);
+  info_of(1, r1, st1, en1, dg1);
+  blocks_of(st0, en0, v0);
+  for (int64_t j = 0; pos_of(j, 0) - lane < hi; ++j) {
+    int32_t r3[kRgSB];
+    uint32_t st2[kRgSB], en2[kRgSB];
+    uint2 dg2[kRgSB];
+    uint4 v1[kRgSB];
+    rows_of(j + 3, r3);
+    info_of(j + 2, r2, st2, en2, dg2);
+    blocks_of(st1, en1, v1);
+#pragma unroll
+    for (int i = 0; i < kRgSB; ++i) {
+      if (en0[i] > st0[i]) {
+        const unsigned long long c0 = (unsigned long long)rg_q(dg0[i].x, np);
+        const unsigned long long c1 = (unsigned long long)rg_q(dg0[i].y, np);
+        uint32_t blk = st0[i] & ~7u;
+        rg_run_block<BINS>(sh, v0[i], blk, st0[i], en0[i], c0, c1, sinkb, dbg, sink);
+        for (blk += 8; blk < en0[i]; blk += 8)        // rows longer than one block (rare here)
+          rg_run_block<BINS>(sh, *reinterpret_cast<const uint4*>(ent + blk), blk, st0[i], en0[i], c0, c1, sinkb,
+                             dbg, sink);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRgSB; ++i) {
+      st0[i] = st1[i];
+      en0[i] = en1[i];
+      dg0[i] = dg1[i];
+      v0[i] = v1[i];
+      st1[i] = st2[i];
+      en1[i] = en2[i];
+      dg1[i] = dg2[i];
+      r2[i] = r3[i];
+    }
+  }
+}
+
 // Workgroup w: chunk wg_p[w] (of wg_np[w]) of the built-row list, bin group wg_g[w]. Each wave
 // takes batches of 64 listed rows and streams their runs inside the group in aligned 8-entry
 // (16-byte) blocks, adding every entry's row statistics into the LDS histograms; at every slot
@@ -272,41 +500,19 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
   const uint32_t* ptr = a.ptr + (int64_t)g * (a.N + 1);
   const uint16_t* ent = a.ent + a.gbase[g];
   const int32_t* list = a.list;
+  // digit words by list position (coalesced): listdig with a list, rowdig at the all-rows pass
+  const uint32_t* pdig = list ? a.listdig : a.rowdig;
+  const bool bal = a.gmode[g] != 0;
   const int np = a.np, dbg = a.dbg;
   unsigned long long sink = 0;
   for (;;) {
     const int64_t ss0 = list ? (int64_t)a.slot_start[s] : 0;
     const int64_t ss1 = list ? (int64_t)a.slot_start[s + 1] : a.N;
     const int64_t lo = a0 > ss0 ? a0 : ss0, hi = a1 < ss1 ? a1 : ss1;
-    // rows of batch k are pos = lo + wv * 64 + k * kRgThreads + lane; the list entry is read two
-    // batches ahead, (ptr, digits) one batch ahead
-    int64_t pos = lo + wv * 64 + lane;
-    int64_t row_c = list ? (pos < hi ? (int64_t)list[pos] : -1) : (pos < hi ? pos : -1);
-    int64_t row_n = -1;
-    if (list && pos + kRgThreads < hi) row_n = list[pos + kRgThreads];
-    uint32_t st = 0, en = 0;
-    uint2 dg = make_uint2(0u, 0u);
-    if (row_c >= 0) {
-      st = ptr[row_c];
-      en = ptr[row_c + 1];
-      dg = *reinterpret_cast<const uint2*>(a.rowdig + 2 * row_c);
-    }
-    for (int64_t b0 = lo + wv * 64; b0 < hi; b0 += kRgThreads, pos += kRgThreads) {
-      const int64_t pn = pos + kRgThreads;
-      const int64_t rn = list ? row_n : (pn < hi ? pn : -1);
-      if (list) row_n = pn + kRgThreads < hi ? (int64_t)list[pn + kRgThreads] : -1;
-      uint32_t nst = 0, nen = 0;
-      uint2 ndg = make_uint2(0u, 0u);
-      if (rn >= 0) {
-        nst = ptr[rn];
-        nen = ptr[rn + 1];
-        ndg = *reinterpret_cast<const uint2*>(a.rowdig + 2 * rn);
-      }
-      rg_batch<BINS>(sh, ent, wv, lane, st, en, (int32_t)rg_q(dg.x, np), (int32_t)rg_q(dg.y, np), dbg, sink);
-      st = nst;
-      en = nen;
-      dg = ndg;
-    }
+    if (bal)
+      rg_range_dense<BINS>(sh, a, ptr, ent, pdig, lo, hi, wv, lane, np, dbg, sink);
+    else
+      rg_range_sparse<BINS>(sh, a, ptr, ent, pdig, lo, hi, wv, lane, np, dbg, sink);
     if (dbg & 2) atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[lane]), sink);
     __syncthreads();
     rg_flush<BINS>(a, sh, g, s, tid);
@@ -324,10 +530,22 @@ void launch_rg_build(const RgBuildArgs& a, int pass, hipStream_t s) {
   if (blocks > 0) hipLaunchKernelGGL(rg_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, pass);
 }
 
-void launch_rg_list(const RgListArgs& a, int pass, hipStream_t s) {
-  const int64_t waves = (a.N + kRgListRows - 1) / kRgListRows;
+template <class V>
+void launch_rg_build_csr(const RgCsrBuildArgs<V>& a, int pass, hipStream_t s) {
+  const int64_t blocks = (a.N + 255) / 256;
+  if (blocks > 0) hipLaunchKernelGGL(rg_build_csr_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a, pass);
+}
+template void launch_rg_build_csr<float>(const RgCsrBuildArgs<float>&, int, hipStream_t);
+template void launch_rg_build_csr<double>(const RgCsrBuildArgs<double>&, int, hipStream_t);
+template void launch_rg_build_csr<int32_t>(const RgCsrBuildArgs<int32_t>&, int, hipStream_t);
+
+void launch_rg_list(const RgListArgs& a, hipStream_t s) {
+  const int64_t waves = (a.N + kRgListRows - 1) / kRgListRows;   // 4 per block
   const int64_t blocks = (waves + 3) / 4;
-  if (blocks > 0) hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, pass);
+  if (blocks <= 0) return;
+  hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);
+  hipLaunchKernelGGL(rg_list_scan_kernel, dim3((unsigned)a.nslots), dim3(1024), 0, s, a, waves);
+  hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 1);
 }
 
 void launch_rg_hist(const RgHistArgs& a, hipStream_t s) {

@@ -220,6 +220,27 @@ struct RgBuildArgs {
   uint16_t* ent;                  // pass 1 out
 };
 
+// Row-group CSR straight from the count-path CSR (rows of term counts, the bench corpus): a
+// thread per row, per-(group, row) counters in LDS, so runs keep the CSR order and no global
+// atomics are needed (the CSC build: ~2 returning atomics per entry, ~0.1 s at 10M rows).
+// Entry (row r, feature f, count c): fa = remap[f] (-1: inactive), bin = c <= 0 ? 0 :
+// min(c, 255, max_bin) (the count path's binning), local = flocal[fa] + bin.
+template <class V>
+struct RgCsrBuildArgs {
+  const int64_t* indptr;          // [N + 1]
+  const int32_t* idx;             // [nnz] original feature ids
+  const V* counts;                // [nnz]
+  int64_t N;
+  const int32_t* remap;           // [F] active index of each feature (-1: inactive)
+  int32_t max_bin;                // max_bins - 1
+  const int32_t* fgroup;          // [Fa]
+  const int32_t* flocal;          // [Fa]
+  int32_t G;
+  uint32_t* ptr;                  // [G][N + 1]: pass 0 writes the counts at [g][r + 1]; pass 1 reads the starts
+  const int64_t* gbase;
+  uint16_t* ent;                  // pass 1 out
+};
+
 // Built rows of a level grouped by slot. The slot of row r is node_slot[row_node[r]] when
 // row_node is given (slots outside [0, nslots): not built), else slot8[r] (0xff: not built).
 constexpr int kRgListRows = 2048;           // rows per wave of the list kernels
@@ -230,12 +251,14 @@ struct RgListArgs {
   const uint8_t* slot8;           // [N] (when row_node is nullptr)
   int64_t N;
   int32_t nslots;
-  int32_t* slot_count;            // [nslots] (zeroed; pass 0 adds)
-  int32_t* slot_fill;             // [nslots] (zeroed; pass 1 reserves)
-  int32_t* wave_count;            // [ceil(N / kRgListRows)][64]: pass 0 per-wave counts
+  int32_t* slot_count;            // [nslots] totals (pass 2)
+  int32_t* wave_count;            // [ceil(N / kRgListRows)][nslots]: per-wave counts (pass 0), then
+                                  //   per-wave offsets inside each slot (pass 2)
   int32_t* slot_start;            // [nslots + 1] out (pass 1)
   int32_t* list;                  // [N] out (pass 1): built rows grouped by slot, ascending inside each
                                   //   wave's chunk of rows
+  const uint32_t* rowdig;         // optional [N * 2]: pass 1 also writes
+  uint32_t* listdig;              //   listdig[2 pos + k] = rowdig[2 list[pos] + k] (coalesced in the pass)
 };
 
 FDX_HD uint32_t rg_slot_of(const RgListArgs& a, int64_t r) {
@@ -253,9 +276,11 @@ struct RgHistArgs {
   int32_t gbins;                  // local bins per group: 4096 or 8192
   int32_t G;
   int64_t N;
-  const uint32_t* rowdig;         // [N * 2] digit words
+  const uint32_t* rowdig;         // [N * 2] digit words (by row; the list pass reads listdig)
   int32_t np;                     // 4: q = undigits4, 1: q = undigits1
   const int32_t* list;            // built rows grouped by slot (nullptr: rows 0..N-1, one slot)
+  const uint32_t* listdig;        // [T * 2] digit words by list position (with list)
+  const uint8_t* gmode;           // [G] 1: lane-balanced batches (dense groups), 0: a lane per row
   const int32_t* slot_start;      // [nslots + 1] (nullptr with list == nullptr)
   int32_t nslots;
   // work table: workgroup w takes chunk wg_p[w] of the wg_np[w] equal chunks of the list, for
@@ -264,8 +289,8 @@ struct RgHistArgs {
   const int32_t* wg_p;
   const int32_t* wg_np;
   int32_t n_wg;
-  // diagnostics (bench/probes/rg_probe.py; results wrong when set): bit 1 replaces the LDS
-  // atomics by a register sum, bit 2 adds 32-bit instead of 64-bit words
+  // diagnostics (bench/probes/rg_probe.py): bit 1 replaces the LDS atomics by a register sum
+  // (wrong sums)
   int32_t dbg;
   // output: hist[(slot_node[s] * hist_stride + off(column)) * 2 + stat] +=
   const int32_t* slot_node;

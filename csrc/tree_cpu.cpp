@@ -266,6 +266,40 @@ void rg_build_cpu(const RgBuildArgs& a, int pass) {
   }
 }
 
+// Host twin of rg_build_csr_kernel (rows in parallel: every (group, row) run is written by its row only).
+template <class V>
+void rg_build_csr_cpu(const RgCsrBuildArgs<V>& a, int pass) {
+  parallel_for(a.N, 0, 4096, [&](int64_t lo, int64_t hi) {
+    std::vector<uint32_t> c((size_t)a.G);
+    for (int64_t r = lo; r < hi; ++r) {
+      for (int g = 0; g < a.G; ++g) c[(size_t)g] = pass == 1 ? a.ptr[(int64_t)g * (a.N + 1) + r] : 0u;
+      for (int64_t e = a.indptr[r]; e < a.indptr[r + 1]; ++e) {
+        const int32_t fa = a.remap[a.idx[e]];
+        if (fa < 0) continue;
+        const int32_t g = a.fgroup[fa];
+        if (g < 0) continue;
+        if (pass == 0) {
+          ++c[(size_t)g];
+        } else {
+          const V v = a.counts[e];
+          int32_t b = 0;
+          if (v > (V)0) {
+            const double d = (double)v;
+            b = d >= 255.0 ? 255 : (int32_t)d;
+            b = b < a.max_bin ? b : a.max_bin;
+          }
+          a.ent[a.gbase[g] + c[(size_t)g]++] = (uint16_t)(a.flocal[fa] + b);
+        }
+      }
+      if (pass == 0)
+        for (int g = 0; g < a.G; ++g) a.ptr[(int64_t)g * (a.N + 1) + r + 1] = c[(size_t)g];
+    }
+  });
+}
+template void rg_build_csr_cpu<float>(const RgCsrBuildArgs<float>&, int);
+template void rg_build_csr_cpu<double>(const RgCsrBuildArgs<double>&, int);
+template void rg_build_csr_cpu<int32_t>(const RgCsrBuildArgs<int32_t>&, int);
+
 // Built rows grouped by slot, ascending inside each slot (the device order inside a 4096-row
 // window may differ; the histogram sums do not depend on it).
 void rg_list_cpu(const RgListArgs& a) {
@@ -279,7 +313,13 @@ void rg_list_cpu(const RgListArgs& a) {
   for (int s = 0; s < a.nslots; ++s) a.slot_count[s] = (int32_t)(cnt[s + 1] - cnt[s]);
   for (int64_t r = 0; r < a.N; ++r) {
     const uint32_t s = rg_slot_of(a, r);
-    if (s < (uint32_t)a.nslots) a.list[cnt[s]++] = (int32_t)r;
+    if (s >= (uint32_t)a.nslots) continue;
+    const int64_t pos = cnt[s]++;
+    a.list[pos] = (int32_t)r;
+    if (a.listdig) {
+      a.listdig[2 * pos] = a.rowdig[2 * r];
+      a.listdig[2 * pos + 1] = a.rowdig[2 * r + 1];
+    }
   }
 }
 
@@ -302,7 +342,8 @@ void rg_hist_cpu(const RgHistArgs& a) {
         const int64_t hrow = a.slot_node[s];
         if (hrow < 0) continue;
         const int64_t row = a.list ? (int64_t)a.list[pos] : pos;
-        const int64_t q0 = rg_q(a.rowdig[2 * row], a.np), q1 = rg_q(a.rowdig[2 * row + 1], a.np);
+        const uint32_t* dg = a.list ? a.listdig + 2 * pos : a.rowdig + 2 * row;
+        const int64_t q0 = rg_q(dg[0], a.np), q1 = rg_q(dg[1], a.np);
         for (uint32_t i = ptr[row]; i < ptr[row + 1]; ++i) {
           const int32_t col = a.gbin[(int64_t)g * a.gbins + ent[i]];
           if (col < 0) continue;

@@ -127,7 +127,8 @@ class Workspace:
             self.rg_list = torch.empty(self.Q.n_rows, dtype=torch.int32, device=self.dev)
             self.rg_start = torch.zeros(66, dtype=torch.int32, device=self.dev)
             nw = -(-self.Q.n_rows // 2048)            # csrc/tree.h kRgListRows
-            self.rg_work = torch.zeros(128 + 64 * nw, dtype=torch.int32, device=self.dev)
+            self.rg_work = torch.zeros(64 * (2 + nw), dtype=torch.int32, device=self.dev)
+            self.rg_listdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
         return rg
 
     def run_concurrent(self, launches: list) -> None:
@@ -806,13 +807,14 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             if rg is not None:
                 shard_args = (shards.bin_lo, n_build * shards.Bs) if shards is not None else (None, 0)
                 if d == 0:
-                    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, 1, rg.work(), s2n,
-                                   hist_target, h_stride, *shard_args, RG_DBG)
+                    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, None, 1, rg.gmode,
+                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG)
                 else:
                     C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
-                                   ws.rg_list)
+                                   ws.rg_list, ws.rowdig, ws.rg_listdig)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
-                                   n_build, rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG)
+                                   ws.rg_listdig, n_build, rg.gmode, rg.work(), s2n, hist_target, h_stride,
+                                   *shard_args, RG_DBG)
                 sel_groups, use_dense = [], False
             elif BLK and np_ == 4 and not build_all and n_build <= BLK_MAX_SLOTS:
                 # row-blocked pass: every feature (hot ones included) in one launch

@@ -211,6 +211,9 @@ RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 2048))   # workgroups per row-g
 # work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
 # (ptr, digits) loads whether or not it has entries in the group)
 RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 8.0))
+# groups with at least this many entries per row take lane-balanced batches (csrc/row_kernels.hip
+# rg_batch); sparser ones a lane per row
+RG_BAL_MIN = float(os.environ.get("FDX_RG_BAL_MIN", 8.0))
 
 
 class RowGroups:
@@ -270,20 +273,33 @@ class RowGroups:
         gbase = np.concatenate([[0], np.cumsum(pad)]).astype(np.int64)
         self.entries = int(egroup.sum())
         self.group_entries = egroup
+        self.gmode = torch.from_numpy((egroup >= RG_BAL_MIN * max(N, 1)).astype(np.uint8)).to(dev)
         self.fgroup_host, self.flocal_host = fgroup, flocal
         fg_t = torch.from_numpy(fgroup).to(dev)
         fl_t = torch.from_numpy(flocal).to(dev)
         self.gbase = torch.from_numpy(gbase).to(dev)
         self.gbin = torch.from_numpy(gbin).to(dev)
         ptr = torch.zeros((G, N + 1), dtype=torch.int32, device=dev)
-        C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 0, ptr, None, None, None)
-        self.ptr = torch.cumsum(ptr, dim=1, dtype=torch.int32)
-        del ptr
-        cursor = self.ptr[:, :N].clone(memory_format=torch.contiguous_format)   # (a view when G == 1)
         # readable padding behind the end: the pass loads aligned 8-entry blocks
         self.ent = torch.zeros(int(gbase[-1]) + 16, dtype=torch.int16, device=dev)[:int(gbase[-1])]
-        C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 1, None, cursor, self.gbase, self.ent)
-        del cursor
+        csr = getattr(Q, "csr_src", None)
+        if csr is not None and G <= 64:
+            # rows of the count-path CSR: a thread per row, runs in CSR order, no global atomics
+            indptr, idx, counts, max_bins = csr
+            remap = torch.full((Q.num_features,), -1, dtype=torch.int32, device=dev)
+            remap[Q.fid_orig] = torch.arange(Q.Fa, dtype=torch.int32, device=dev)
+            C.tree_rg_build_csr(indptr, idx, counts, remap, max_bins - 1, fg_t, fl_t, 0, ptr, None, None)
+            self.ptr = torch.cumsum(ptr, dim=1, dtype=torch.int32)
+            del ptr
+            C.tree_rg_build_csr(indptr, idx, counts, remap, max_bins - 1, fg_t, fl_t, 1, self.ptr, self.gbase,
+                                self.ent)
+        else:
+            C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 0, ptr, None, None, None)
+            self.ptr = torch.cumsum(ptr, dim=1, dtype=torch.int32)
+            del ptr
+            cursor = self.ptr[:, :N].clone(memory_format=torch.contiguous_format)   # (a view when G == 1)
+            C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 1, None, cursor, self.gbase, self.ent)
+            del cursor
         self._work: dict = {}
 
     def work(self, target_wgs: int = 0, alpha: float = None) -> torch.Tensor:
@@ -321,12 +337,14 @@ class Quantized:
     colptr: torch.Tensor         # int64 [Fa+1]
     csc_row: torch.Tensor        # int32 [nnz] (view; CSC_PAD readable entries follow)
     csc_bin: torch.Tensor        # uint8 [nnz] (view; CSC_PAD readable entries follow)
-    kbase: torch.Tensor = None   # int32 [Fa] key base of each feature in its packed work item
-    groups: list = field(default_factory=list)
-    hot_groups: list = field(default_factory=list)   # CSC items of the dense-block features
-    h_row: torch.Tensor = None   # int32: histogram CSC (all features, super-block-major)
-    h_key: torch.Tensor = None   # uint8: kbase[f] + bin
-    n_super: int = 1             # row super-blocks of the histogram CSC
+    # the CSC passes' histogram CSC and work items (built on first use: the row-group engine of
+    # GBDT never reads them) -- see the properties below
+    _kbase: torch.Tensor = None  # int32 [Fa] key base of each feature in its packed work item
+    _groups: list = field(default_factory=list)
+    _hot_groups: list = field(default_factory=list)  # CSC items of the dense-block features
+    _h_row: torch.Tensor = None  # int32: histogram CSC (all features, super-block-major)
+    _h_key: torch.Tensor = None  # uint8: kbase[f] + bin
+    _n_super: int = 1            # row super-blocks of the histogram CSC
     # dense path for high-density features (K-10 dense variant): dense[d][row] = bin of feature
     # hot[d] (its zero bin when absent), rows padded to n_pad (multiple of 64)
     hot: np.ndarray = None       # int64 [Fh] Fa indices
@@ -335,12 +353,28 @@ class Quantized:
     boff_host: np.ndarray = None
     zbin_host: np.ndarray = None
     fid_host: np.ndarray = None
-    kbase_host: np.ndarray = None
+    _kbase_host: np.ndarray = None
     row0: int = 0                # global index of row 0 (data-parallel shards; bootstrap draws)
 
     @property
     def Fa(self) -> int:  # noqa: N802
         return int(self.nbins.numel())
+
+    def _items(self) -> "Quantized":
+        pend = getattr(self, "_items_pending", None)
+        if pend is not None:
+            self._items_pending = None
+            with tracing.span("q.items"):
+                _build_items(self, *pend)
+        return self
+
+    groups = property(lambda self: self._items()._groups)
+    hot_groups = property(lambda self: self._items()._hot_groups)
+    h_row = property(lambda self: self._items()._h_row)
+    h_key = property(lambda self: self._items()._h_key)
+    kbase = property(lambda self: self._items()._kbase)
+    kbase_host = property(lambda self: self._items()._kbase_host)
+    n_super = property(lambda self: self._items()._n_super)
 
     def blocked(self) -> BlockedCSC:
         """The row-blocked CSC (built on first use)."""
@@ -414,7 +448,9 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
         scale = torch.ones(F, dtype=torch.float64, device=dev)
     if counts is not None and F < (1 << 31):
         Q = _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_max)
-        with tracing.span("q.items"):
+        if idx.dtype == torch.int32 and counts.dtype in (torch.float32, torch.float64, torch.int32):
+            Q.csr_src = (indptr, idx, counts, max_bins)     # (references) the row-group build reads rows
+        with tracing.span("q.dense_block"):
             _finish_items(Q, chunk, super_rows or SUPER_ROWS, HOT_DENSITY if hot_density is None else hot_density)
         return Q
     idx64 = idx.to(torch.int64)      # generic path only (8 B per entry: never on the count path)
@@ -457,7 +493,7 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
     Q.boff_host = boff.cpu().numpy()
     Q.zbin_host = Q.zbin.cpu().numpy()
     Q.fid_host = fid_orig.cpu().numpy()
-    with tracing.span("q.items"):
+    with tracing.span("q.dense_block"):
         _finish_items(Q, chunk, super_rows or SUPER_ROWS, HOT_DENSITY if hot_density is None else hot_density)
     return Q
 
@@ -681,19 +717,15 @@ def _split_long(rows_: np.ndarray, chunk: int) -> np.ndarray:
 
 def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS, hot_density: float = HOT_DENSITY) \
         -> None:
-    """Dense block, histogram CSC and work items (see the module docstring).
+    """Dense block now; histogram CSC and work items on first use (see the module docstring).
 
     * hot: features in >= ``hot_density`` of the rows with <= 64 bins -> dense block;
     * packed: consecutive features with <= 16 bins and few entries (<= ``chunk`` per super-block on
       average) share one <= 64-key item per super-block (stride = the largest pow2 bin count);
     * single: every other feature, per super-block, in chunks of <= ``chunk`` entries; features
       with > 64 bins get one item per 64-key window."""
-    from ..ops import native
-
-    C = native.lib()
     if not 0 < chunk <= MAX_ITEM_ENTRIES:
         raise ValueError(f"FDX_HIST_CHUNK must be in [1, {MAX_ITEM_ENTRIES}] (int32 MFMA accumulators)")
-    dev = Q.device
     colptr = Q.colptr.cpu().numpy().astype(np.int64)
     n = np.diff(colptr)
     nb = Q.nbins.cpu().numpy().astype(np.int64)
@@ -701,6 +733,19 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
     hot = (n >= hot_density * max(Q.n_rows, 1)) & (nb <= 64) & (n > 0) if hot_density > 0 else np.zeros(Fa, bool)
     with tracing.span("q.dense"):
         _build_dense(Q, np.nonzero(hot)[0])
+    Q._items_pending = (chunk, super_rows, hot)
+
+
+def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> None:
+    """The histogram CSC and work items of the CSC passes (first use of Q.groups & co.)."""
+    from ..ops import native
+
+    C = native.lib()
+    dev = Q.device
+    colptr = Q.colptr.cpu().numpy().astype(np.int64)
+    n = np.diff(colptr)
+    nb = Q.nbins.cpu().numpy().astype(np.int64)
+    Fa = int(nb.size)
     # hot features stay in the histogram CSC too (deep levels use it: only their live entries are
     # multiplied there, while the dense kernel masks every row); they are never packed
     cols = np.nonzero(n > 0)[0]
@@ -811,10 +856,10 @@ def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS
                                              meta.to(torch.int32), g[:, 7].to(torch.int32)))
         o += ix.size
 
-    Q.groups = groups[False]
-    Q.hot_groups = groups[True]
+    Q._groups = groups[False]
+    Q._hot_groups = groups[True]
     sp_g.__exit__(None, None, None)
-    Q.h_row, Q.h_key = h_row[:total], h_key[:total]
-    Q.n_super = nsb
-    Q.kbase_host = kbase.astype(np.int32)
-    Q.kbase = torch.from_numpy(Q.kbase_host).to(dev)
+    Q._h_row, Q._h_key = h_row[:total], h_key[:total]
+    Q._n_super = nsb
+    Q._kbase_host = kbase.astype(np.int32)
+    Q._kbase = torch.from_numpy(Q._kbase_host).to(dev)

@@ -40,6 +40,15 @@ def _q_of(ws, np_):
     return q[:, 0], q[:, 1]
 
 
+MODE = {"gmode": None}
+
+
+def gmode(rg):
+    """The groups' pass modes: the layout's own, or all balanced / all lane-per-row (MODE)."""
+    m = MODE["gmode"]
+    return rg.gmode if m is None else torch.full_like(rg.gmode, m)
+
+
 def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None, np_=4, P=16, max_groups=None,
                 dbg=0, bins=8192):
     """Histograms of node slots 0..nslots-1 through tree_rg_list + tree_rg_hist, plus q0, q1 and Q;
@@ -50,26 +59,28 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
     ws = Workspace(Q)
     _quant(ws, n, dev, np_)
     rg = RowGroups(Q, max_groups=max_groups, bins=bins)
-    list_ = start = None
+    list_ = start = ldig = None
     if not root:
         node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
         node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
         list_ = torch.empty(n, dtype=torch.int32, device=dev)
         start = torch.zeros(nslots + 1, dtype=torch.int32, device=dev)
-        work = torch.zeros(2 * nslots + 64 * (n // 2048 + 1), dtype=torch.int32, device=dev)
-        C.tree_rg_list(torch.from_numpy(row_node_np).to(dev), node_slot.to(dev), None, n, nslots, work, start, list_)
+        work = torch.zeros(nslots * (2 + n // 2048 + 1), dtype=torch.int32, device=dev)
+        ldig = torch.empty((n, 2), dtype=torch.int32, device=dev)
+        C.tree_rg_list(torch.from_numpy(row_node_np).to(dev), node_slot.to(dev), None, n, nslots, work, start, list_,
+                       ws.rowdig, ldig)
     s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
     q0, q1 = _q_of(ws, np_)
     if shards is None:
         hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
-        C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, rg.work(P), s2n,
-                       hist, Q.TB, None, 0, dbg)
+        C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, ldig, nslots, gmode(rg),
+                       rg.work(P), s2n, hist, Q.TB, None, 0, dbg)
         return hist.cpu().numpy(), q0, q1, Q, rg
     S, lo = shards
     Bs = int(np.diff(lo).max())
     buf = torch.zeros((S, nslots, Bs, 2), dtype=torch.int64, device=dev)
-    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, nslots, rg.work(P), s2n,
-                   buf.view(S * nslots, Bs, 2), Bs, torch.from_numpy(lo).to(dev), nslots * Bs, dbg)
+    C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, ldig, nslots, gmode(rg),
+                   rg.work(P), s2n, buf.view(S * nslots, Bs, 2), Bs, torch.from_numpy(lo).to(dev), nslots * Bs, dbg)
     b = buf.cpu().numpy()
     hist = np.concatenate([b[k, :, : lo[k + 1] - lo[k]] for k in range(S)], axis=1)
     return hist, q0, q1, Q, rg
@@ -105,6 +116,40 @@ def test_row_groups_cover_every_entry_once():
         assert (gbin[g] >= 0).sum() <= RG_BINS
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.int32, torch.float64])
+def test_row_groups_from_csr_equal_csc_build(dtype):
+    """The count-path CSR build (thread per row) gives the CSC build's layout: the same ptr and
+    the same multiset of local bins in every (group, row) run (runs in CSR order)."""
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+
+    rng = np.random.default_rng(5)
+    n, F = 3000, 400
+    dense = (rng.random((n, F)) < np.linspace(0.002, 0.6, F)) * rng.integers(1, 300, (n, F))
+    dense[rng.random((n, F)) < 0.001] = 0
+    nz = dense != 0
+    indptr = torch.from_numpy(np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64))
+    rr, cc = np.nonzero(nz)
+    cnt = torch.from_numpy(dense[rr, cc]).to(dtype)
+    scale = torch.from_numpy(rng.uniform(0.5, 2.0, F))
+    scale[::17] = 0.0                                       # inactive features
+    vc = VectorColumn.tfidf(F, indptr, torch.from_numpy(cc.astype(np.int32)), cnt, scale)
+    Q = quantize(vc, max_bins=64, counts=vc.tf_counts, scale=vc.tf_scale)
+    assert getattr(Q, "csr_src", None) is not None
+    a = RowGroups(Q, bins=4096)
+    csr = Q.csr_src
+    del Q.csr_src
+    b = RowGroups(Q, bins=4096)
+    Q.csr_src = csr
+    assert a.G == b.G >= 2
+    np.testing.assert_array_equal(a.ptr.numpy(), b.ptr.numpy())
+    ea, eb = a.ent.numpy(), b.ent.numpy()
+    pa, ga = a.ptr.numpy(), a.gbase.numpy()
+    for g in range(a.G):
+        for r in range(0, n, 7):
+            s0, s1 = ga[g] + pa[g, r], ga[g] + pa[g, r + 1]
+            np.testing.assert_array_equal(np.sort(ea[s0:s1]), np.sort(eb[s0:s1]))
+
+
 def test_row_groups_incomplete_beyond_max_groups():
     vc = _wide(2000, 300, 4)
     Q = quantize(vc, max_bins=100, **QKW)
@@ -136,16 +181,21 @@ def _list_check(dev, n, ns, seed):
     sl = np.where((row_node >= 0) & (row_node < node_slot.size), node_slot[np.clip(row_node, 0, node_slot.size - 1)], -1)
     lst = torch.full((n,), -7, dtype=torch.int32, device=dev)
     start = torch.zeros(ns + 1, dtype=torch.int32, device=dev)
-    work = torch.full((2 * ns + 64 * (n // 2048 + 1),), 99, dtype=torch.int32, device=dev)
+    work = torch.full((ns * (2 + n // 2048 + 1),), 99, dtype=torch.int32, device=dev)
+    dig = torch.from_numpy(rng.integers(0, 1 << 30, (n, 2)).astype(np.int32)).to(dev)
+    ldig = torch.zeros((n, 2), dtype=torch.int32, device=dev)
     C.tree_rg_list(torch.from_numpy(row_node).to(dev), torch.from_numpy(node_slot).to(dev), None, n, ns, work,
-                   start, lst)
-    st, lst = start.cpu().numpy(), lst.cpu().numpy()
-    for s in range(ns):
-        np.testing.assert_array_equal(np.sort(lst[st[s]:st[s + 1]]), np.nonzero(sl == s)[0])
+                   start, lst, dig, ldig)
+    st, lst, ldig = start.cpu().numpy(), lst.cpu().numpy(), ldig.cpu().numpy()
+    for s in range(ns):                 # sorted by (slot, row)
+        np.testing.assert_array_equal(lst[st[s]:st[s + 1]], np.nonzero(sl == s)[0])
     assert st[0] == 0 and st[-1] == (sl >= 0).sum()
+    np.testing.assert_array_equal(ldig[:st[-1]], dig.cpu().numpy()[lst[:st[-1]]])
     # from slot bytes
     slot8 = np.where(sl >= 0, sl, 0xFF).astype(np.uint8)
-    C.tree_rg_list(None, None, torch.from_numpy(slot8).to(dev), n, ns, work, start, torch.from_numpy(lst).to(dev))
+    lst2 = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    C.tree_rg_list(None, None, torch.from_numpy(slot8).to(dev), n, ns, work, start, lst2, None, None)
+    np.testing.assert_array_equal(lst2.cpu().numpy()[:st[-1]], lst[:st[-1]])
     return st
 
 
@@ -193,7 +243,8 @@ def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot):
 @pytest.mark.gpu
 @pytest.mark.parametrize("nslots,root,bins", [(1, True, 8192), (2, False, 4096), (5, False, 8192), (32, False, 4096)])
 @pytest.mark.parametrize("sharded", [False, True])
-def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded):
+@pytest.mark.parametrize("mode", [None, 0, 1])
+def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded, mode, monkeypatch):
     """The row-group pass (LDS int64 atomics, 16-B row-run loads, per-slot flushes) equals the
     host's exact int64 sums bit for bit, plain and in the shard-major DP layout."""
     rng = np.random.default_rng(20 + nslots)
@@ -205,6 +256,7 @@ def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded
         Q0 = quantize(vc, max_bins=200, **QKW)
         lo = np.array([0, Q0.TB // 3, (2 * Q0.TB) // 3, Q0.TB], dtype=np.int64)
         shards = (3, lo)
+    monkeypatch.setitem(MODE, "gmode", mode)
     a, *_ = _rg_hist_on("cpu", vc, 200, nslots, row_node, root, shards, P=24, bins=bins)
     b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24, bins=bins)
     assert rg.G >= 2
