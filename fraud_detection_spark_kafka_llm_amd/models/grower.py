@@ -66,7 +66,7 @@ BLK = os.environ.get("FDX_BLK", "0") == "1"      # row-blocked pass: opt-in unti
 BLK_MAX_SLOTS = 4
 # row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
 # histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
-ROWHIST = os.environ.get("FDX_ROWHIST", "0") == "1"
+ROWHIST = os.environ.get("FDX_ROWHIST", "1") == "1"
 RG_DBG = int(os.environ.get("FDX_RG_DBG", 0))   # diagnostics only (csrc/tree.h RgHistArgs::dbg)
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
