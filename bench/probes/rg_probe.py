@@ -89,7 +89,8 @@ def main():
         build_ms = (time.perf_counter() - t0) * 1e3
         ge = rg.group_entries
         print(json.dumps({"rows": n, "nnz": int(Q.csc_row.numel()), "Fa": Q.Fa, "TB": Q.TB, "bins": B, "G": rg.G,
-                          "complete": rg.complete, "build_ms": round(build_ms, 1), "rg_bytes": rg.nbytes,
+                          "complete": rg.complete, "build_ms": round(build_ms, 1), "build_phases_ms": rg.timing,
+                          "rg_bytes": rg.nbytes,
                           "group_entries": [int(x) for x in ge],
                           "entries_per_row_group0": float(ge[0] / n) if ge.size else 0.0}), flush=True)
     zb = None

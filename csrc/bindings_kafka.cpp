@@ -156,9 +156,10 @@ int64_t produce_each(py::object producer, py::object topic, py::array_t<uint8_t>
     nk_arr = py::array_t<uint8_t>::ensure(null_keys);
     nk = nk_arr.data();
   }
-  py::tuple args = py::make_tuple(topic);
-  py::dict kw;
-  kw[N.on_delivery] = cb;
+  // vectorcall: produce(topic, value=, key=, on_delivery=) without a kwargs dict per record
+  py::tuple kwnames = py::make_tuple(py::reinterpret_borrow<py::object>(N.value),
+                                     py::reinterpret_borrow<py::object>(N.key),
+                                     py::reinterpret_borrow<py::object>(N.on_delivery));
   int64_t sent = 0;
   for (int64_t i = 0; i < n; ++i) {
     py::object kobj = (nk && nk[i]) ? py::none()
@@ -166,10 +167,9 @@ int64_t produce_each(py::object producer, py::object topic, py::array_t<uint8_t>
                                           reinterpret_cast<const char*>(kb + ko[i]), ko[i + 1] - ko[i]));
     py::object vobj = py::reinterpret_steal<py::object>(
         PyBytes_FromStringAndSize(reinterpret_cast<const char*>(vb + vo[i]), vo[i + 1] - vo[i]));
-    kw[N.key] = kobj;
-    kw[N.value] = vobj;
+    PyObject* vargs[4] = {topic.ptr(), vobj.ptr(), kobj.ptr(), cb.ptr()};
     while (true) {
-      PyObject* r = PyObject_Call(produce.ptr(), args.ptr(), kw.ptr());
+      PyObject* r = PyObject_Vectorcall(produce.ptr(), vargs, 1, kwnames.ptr());
       if (r) {
         Py_DECREF(r);
         ++sent;
@@ -193,9 +193,361 @@ int64_t produce_each(py::object producer, py::object topic, py::array_t<uint8_t>
   return sent;
 }
 
+// ------------------------------------------------------------------------------------------------
+// DeliveryCounter(n, done): the per-record on_delivery callback of one output segment. Each call
+// (err, msg) counts one report; the first error is kept; the n-th call runs done(err or None).
+// A C callable: librdkafka-speed reports do not pay a Python frame per record.
+struct DeliveryCounter {
+  PyObject_HEAD
+  int64_t left;
+  PyObject* done;
+  PyObject* err;
+};
+
+void dc_dealloc(PyObject* self) {
+  auto* d = reinterpret_cast<DeliveryCounter*>(self);
+  Py_XDECREF(d->done);
+  Py_XDECREF(d->err);
+  Py_TYPE(self)->tp_free(self);
+}
+
+int dc_init(PyObject* self, PyObject* args, PyObject* kw) {
+  auto* d = reinterpret_cast<DeliveryCounter*>(self);
+  long long n = 0;
+  PyObject* done = nullptr;
+  if (!PyArg_ParseTuple(args, "LO", &n, &done)) return -1;
+  Py_INCREF(done);
+  Py_XSETREF(d->done, done);
+  Py_CLEAR(d->err);
+  d->left = n;
+  return 0;
+}
+
+PyObject* dc_call(PyObject* self, PyObject* args, PyObject* kw) {
+  auto* d = reinterpret_cast<DeliveryCounter*>(self);
+  PyObject* err = Py_None;
+  PyObject* msg = Py_None;
+  if (!PyArg_UnpackTuple(args, "DeliveryCounter", 0, 2, &err, &msg)) return nullptr;
+  if (err != Py_None && d->err == nullptr) {
+    Py_INCREF(err);
+    d->err = err;
+  }
+  if (--d->left == 0) {
+    PyObject* r = PyObject_CallOneArg(d->done, d->err ? d->err : Py_None);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+  }
+  Py_RETURN_NONE;
+}
+
+PyObject* dc_left(PyObject* self, void*) { return PyLong_FromLongLong(reinterpret_cast<DeliveryCounter*>(self)->left); }
+
+PyGetSetDef dc_getset[] = {{"left", dc_left, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+PyTypeObject DeliveryCounterType = [] {
+  PyTypeObject t{PyVarObject_HEAD_INIT(nullptr, 0)};
+  t.tp_name = "fdx.DeliveryCounter";
+  t.tp_basicsize = sizeof(DeliveryCounter);
+  t.tp_flags = Py_TPFLAGS_DEFAULT;
+  t.tp_new = PyType_GenericNew;
+  t.tp_init = dc_init;
+  t.tp_dealloc = dc_dealloc;
+  t.tp_call = dc_call;
+  t.tp_getset = dc_getset;
+  t.tp_doc = "per-record delivery callback counting one segment's reports";
+  return t;
+}();
+
+// ------------------------------------------------------------------------------------------------
+// C-level accessors for the in-memory broker's Message (a tuple subclass): method descriptors,
+// so msg.value() etc. cost a C call like cimpl.Message's instead of a Python frame.
+template <int I>
+PyObject* tuple_get(PyObject* self, PyObject*) {
+  PyObject* o = PyTuple_GET_ITEM(self, I);
+  Py_INCREF(o);
+  return o;
+}
+PyObject* tuple_ts(PyObject* self, PyObject*) { return Py_BuildValue("(iO)", 1, PyTuple_GET_ITEM(self, 6)); }
+
+PyMethodDef message_defs[] = {
+    {"topic", tuple_get<0>, METH_NOARGS, "topic"},     {"partition", tuple_get<1>, METH_NOARGS, "partition"},
+    {"offset", tuple_get<2>, METH_NOARGS, "offset"},   {"key", tuple_get<3>, METH_NOARGS, "key"},
+    {"value", tuple_get<4>, METH_NOARGS, "value"},     {"error", tuple_get<5>, METH_NOARGS, "error"},
+    {"timestamp", tuple_ts, METH_NOARGS, "timestamp"}, {nullptr, nullptr, 0, nullptr}};
+
+void install_message_accessors(py::object cls) {
+  if (!PyType_Check(cls.ptr()) || !PyType_IsSubtype(reinterpret_cast<PyTypeObject*>(cls.ptr()), &PyTuple_Type))
+    throw py::type_error("expected a tuple subclass");
+  for (PyMethodDef* d = message_defs; d->ml_name; ++d) {
+    PyObject* descr = PyDescr_NewMethod(reinterpret_cast<PyTypeObject*>(cls.ptr()), d);
+    if (!descr || PyObject_SetAttrString(cls.ptr(), d->ml_name, descr) < 0) {
+      Py_XDECREF(descr);
+      throw py::error_already_set();
+    }
+    Py_DECREF(descr);
+  }
+}
+
+PyObject* new_message(PyObject* cls, PyObject* topic, PyObject* part, PyObject* off, PyObject* key, PyObject* value,
+                      PyObject* ts) {
+  PyObject* m = reinterpret_cast<PyTypeObject*>(cls)->tp_alloc(reinterpret_cast<PyTypeObject*>(cls), 7);
+  if (!m) return nullptr;
+  PyObject* items[7] = {topic, part, off, key, value, Py_None, ts};
+  for (int i = 0; i < 7; ++i) {
+    if (i != 2 && i != 6) Py_INCREF(items[i]);
+    PyTuple_SET_ITEM(m, i, items[i]);
+  }
+  // only str / int / bytes / None inside: no reference cycle can pass through a Message, so the
+  // collector need not track it (as CPython untracks such tuples itself; with ~10^5 live records
+  // the cyclic collector's passes cost ~70% of a per-record produce)
+  if (PyObject_GC_IsTracked(m)) PyObject_GC_UnTrack(m);
+  return m;
+}
+
+// Every record of a columnar batch as a Message (bytes sliced straight out of the buffers).
+py::list build_messages(py::object cls, py::object topic, py::object partition, int64_t base,
+                        py::array_t<uint8_t> keys, py::array_t<int64_t> koff, py::array_t<uint8_t> vals,
+                        py::array_t<int64_t> voff, py::object null_keys, int64_t ts_ms) {
+  const int64_t n = voff.size() - 1;
+  const char* kb = reinterpret_cast<const char*>(keys.data());
+  const char* vb = reinterpret_cast<const char*>(vals.data());
+  const int64_t* ko = koff.data();
+  const int64_t* vo = voff.data();
+  const uint8_t* nk = nullptr;
+  py::array_t<uint8_t> nk_arr;
+  if (!null_keys.is_none()) {
+    nk_arr = py::array_t<uint8_t>::ensure(null_keys);
+    nk = nk_arr.data();
+  }
+  PyObject* out = PyList_New(n > 0 ? n : 0);
+  if (!out) throw py::error_already_set();
+  py::object ts = py::reinterpret_steal<py::object>(PyLong_FromLongLong(ts_ms));
+  for (int64_t i = 0; i < n; ++i) {
+    PyObject* k = (nk && nk[i]) ? (Py_INCREF(Py_None), Py_None) : PyBytes_FromStringAndSize(kb + ko[i], ko[i + 1] - ko[i]);
+    PyObject* v = PyBytes_FromStringAndSize(vb + vo[i], vo[i + 1] - vo[i]);
+    PyObject* off = PyLong_FromLongLong(base + i);
+    Py_INCREF(ts.ptr());
+    PyObject* m = (k && v && off) ? new_message(cls.ptr(), topic.ptr(), partition.ptr(), off, k, v, ts.ptr()) : nullptr;
+    Py_XDECREF(k);
+    Py_XDECREF(v);
+    if (!m) {
+      Py_XDECREF(off);
+      Py_DECREF(ts.ptr());
+      Py_DECREF(out);
+      throw py::error_already_set();
+    }
+    PyList_SET_ITEM(out, i, m);
+  }
+  return py::reinterpret_steal<py::list>(out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// The in-memory broker's per-record produce in C (stream/fake_kafka.py Producer.produce): the same
+// operations on the same Python objects -- under the broker's lock, route by crc32 (zlib's), two
+// list appends on the partition's tail, a Message for the delivery report -- without a Python
+// frame, as a librdkafka producer would cost. Anything unusual (fault injection, a new topic,
+// non-bytes payloads) goes to the Python implementation.
+uint32_t crc32_ieee(const uint8_t* p, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+struct FastNames {
+  PyObject *lock, *acquire, *release, *topics, *tk, *tv, *tts, *size, *waiting, *cond, *notify_all, *pending,
+      *fail_next, *slow, *callback, *partition;
+  FastNames() {
+    lock = PyUnicode_InternFromString("lock");
+    acquire = PyUnicode_InternFromString("acquire");
+    release = PyUnicode_InternFromString("release");
+    topics = PyUnicode_InternFromString("topics");
+    tk = PyUnicode_InternFromString("_tk");
+    tv = PyUnicode_InternFromString("_tv");
+    tts = PyUnicode_InternFromString("_tts");
+    size = PyUnicode_InternFromString("size");
+    waiting = PyUnicode_InternFromString("waiting");
+    cond = PyUnicode_InternFromString("cond");
+    notify_all = PyUnicode_InternFromString("notify_all");
+    pending = PyUnicode_InternFromString("_pending");
+    fail_next = PyUnicode_InternFromString("fail_next");
+    slow = PyUnicode_InternFromString("_produce_py");
+    callback = PyUnicode_InternFromString("callback");
+    partition = PyUnicode_InternFromString("partition");
+  }
+};
+const FastNames& fnames() {
+  static FastNames* n = new FastNames();
+  return *n;
+}
+
+// state = (producer, broker, Message class)
+PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  const Names& N = names();
+  const FastNames& F = fnames();
+  PyObject* producer = PyTuple_GET_ITEM(state, 0);
+  PyObject* broker = PyTuple_GET_ITEM(state, 1);
+  PyObject* cls = PyTuple_GET_ITEM(state, 2);
+  PyObject *topic = nargs > 0 ? args[0] : nullptr, *value = nargs > 1 ? args[1] : Py_None,
+           *key = nargs > 2 ? args[2] : Py_None, *part_o = nargs > 3 ? args[3] : nullptr, *cb = Py_None;
+  bool simple = nargs <= 4;
+  const Py_ssize_t nkw = kwnames ? PyTuple_GET_SIZE(kwnames) : 0;
+  for (Py_ssize_t i = 0; i < nkw && simple; ++i) {
+    PyObject* k = PyTuple_GET_ITEM(kwnames, i);
+    PyObject* v = args[nargs + i];
+    if (PyUnicode_Compare(k, N.value) == 0) value = v;
+    else if (PyUnicode_Compare(k, N.key) == 0) key = v;
+    else if (PyUnicode_Compare(k, N.on_delivery) == 0 || PyUnicode_Compare(k, F.callback) == 0) cb = v;
+    else if (PyUnicode_Compare(k, F.partition) == 0) part_o = v;
+    else simple = false;
+  }
+  long part = -1;
+  if (part_o && part_o != Py_None) {
+    part = PyLong_AsLong(part_o);
+    if (part == -1 && PyErr_Occurred()) return nullptr;
+  }
+  PyObject* fail = simple ? PyObject_GetAttr(producer, F.fail_next) : nullptr;
+  if (simple && (!fail || PyObject_IsTrue(fail))) simple = false;
+  Py_XDECREF(fail);
+  PyErr_Clear();
+  simple = simple && topic && PyUnicode_Check(topic) && (PyBytes_CheckExact(value) || value == Py_None) &&
+           (PyBytes_CheckExact(key) || key == Py_None);
+  PyObject* parts = nullptr;
+  PyObject* lock = nullptr;
+  if (simple) {
+    PyObject* topics = PyObject_GetAttr(broker, F.topics);
+    parts = topics ? PyDict_GetItemWithError(topics, topic) : nullptr;   // borrowed
+    Py_XINCREF(parts);
+    Py_XDECREF(topics);
+    if (!parts || !PyList_Check(parts) || PyList_GET_SIZE(parts) == 0) simple = false;
+  }
+  if (!simple) {                                   // the Python implementation
+    Py_XDECREF(parts);
+    PyErr_Clear();
+    PyObject* slow = PyObject_GetAttr(producer, F.slow);
+    if (!slow) return nullptr;
+    PyObject* r = PyObject_Vectorcall(slow, args, nargs, kwnames);
+    Py_DECREF(slow);
+    return r;
+  }
+  const Py_ssize_t np_ = PyList_GET_SIZE(parts);
+  if (part < 0) {
+    PyObject* src = key != Py_None && PyBytes_GET_SIZE(key) ? key : value;
+    const uint32_t c = src != Py_None ? crc32_ieee(reinterpret_cast<const uint8_t*>(PyBytes_AS_STRING(src)),
+                                                   (size_t)PyBytes_GET_SIZE(src))
+                                      : 0u;
+    part = (long)(c % (uint32_t)np_);
+  }
+  if (part >= np_) {
+    Py_DECREF(parts);
+    PyErr_SetString(PyExc_ValueError, "partition out of range");
+    return nullptr;
+  }
+  lock = PyObject_GetAttr(broker, F.lock);
+  PyObject* r = lock ? PyObject_CallMethodNoArgs(lock, F.acquire) : nullptr;
+  if (!r) {
+    Py_XDECREF(lock);
+    Py_DECREF(parts);
+    return nullptr;
+  }
+  Py_DECREF(r);
+  PyObject* pobj = PyList_GET_ITEM(parts, part);
+  PyObject* tk = PyObject_GetAttr(pobj, F.tk);
+  PyObject* tv = PyObject_GetAttr(pobj, F.tv);
+  PyObject* size = PyObject_GetAttr(pobj, F.size);
+  long long off = -1;
+  bool ok = tk && tv && size && PyList_Check(tk) && PyList_Check(tv);
+  if (ok && PyList_GET_SIZE(tk) == 0) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);                   // time.perf_counter's clock on Linux
+    PyObject* now = PyFloat_FromDouble((double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec);
+    ok = now && PyObject_SetAttr(pobj, F.tts, now) == 0;
+    Py_XDECREF(now);
+  }
+  if (ok) ok = PyList_Append(tk, key) == 0 && PyList_Append(tv, value) == 0;
+  if (ok) {
+    off = PyLong_AsLongLong(size);
+    PyObject* ns = PyLong_FromLongLong(off + 1);
+    ok = ns && PyObject_SetAttr(pobj, F.size, ns) == 0;
+    Py_XDECREF(ns);
+  }
+  if (ok) {
+    PyObject* w = PyObject_GetAttr(broker, F.waiting);
+    if (w && PyObject_IsTrue(w)) {
+      PyObject* cond = PyObject_GetAttr(broker, F.cond);
+      PyObject* rr = cond ? PyObject_CallMethodNoArgs(cond, F.notify_all) : nullptr;
+      ok = rr != nullptr;
+      Py_XDECREF(rr);
+      Py_XDECREF(cond);
+    }
+    Py_XDECREF(w);
+  }
+  // release the lock whatever happened (keep a pending error)
+  PyObject *et, *ev, *etb;
+  PyErr_Fetch(&et, &ev, &etb);
+  PyObject* rel = PyObject_CallMethodNoArgs(lock, F.release);
+  Py_XDECREF(rel);
+  if (et) PyErr_Restore(et, ev, etb);
+  Py_XDECREF(tk);
+  Py_XDECREF(tv);
+  Py_XDECREF(size);
+  Py_DECREF(lock);
+  Py_DECREF(parts);
+  if (!ok || !rel) return nullptr;
+  if (cb != Py_None) {
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    PyObject* tms = PyLong_FromLongLong((long long)ts.tv_sec * 1000 + ts.tv_nsec / 1000000);
+    PyObject* po = PyLong_FromLong(part);
+    PyObject* oo = PyLong_FromLongLong(off);
+    PyObject* msg = (tms && po && oo) ? new_message(cls, topic, po, oo, key, value, tms) : nullptr;
+    Py_XDECREF(po);
+    if (!msg) {
+      Py_XDECREF(tms);
+      Py_XDECREF(oo);
+      return nullptr;
+    }
+    PyObject* item = PyTuple_Pack(3, cb, Py_None, msg);
+    Py_DECREF(msg);
+    // a delivery-report entry lives until the next poll, which drops it: untracked like the Message
+    if (item && PyObject_GC_IsTracked(item)) PyObject_GC_UnTrack(item);
+    PyObject* pend = item ? PyObject_GetAttr(producer, F.pending) : nullptr;
+    const int rc = pend ? PyList_Append(pend, item) : -1;
+    Py_XDECREF(pend);
+    Py_XDECREF(item);
+    if (rc < 0) return nullptr;
+  }
+  Py_RETURN_NONE;
+}
+
+PyMethodDef fast_produce_def = {"produce", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(fast_produce)),
+                                METH_FASTCALL | METH_KEYWORDS, "in-memory broker produce (C)"};
+
+py::object make_fast_produce(py::object producer, py::object broker, py::object message_cls) {
+  py::tuple state = py::make_tuple(producer, broker, message_cls);
+  PyObject* f = PyCFunction_NewEx(&fast_produce_def, state.ptr(), nullptr);
+  if (!f) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(f);
+}
+
 }  // namespace
 
 void register_kafka_ops(pybind11::module& m) {
   m.def("pack_messages", &pack_messages, "consumed Message list -> columnar buffers (one pass, C loop)");
   m.def("produce_each", &produce_each, "per-record produce of one output segment from a C loop");
+  m.def("install_message_accessors", &install_message_accessors, "C method descriptors on a tuple Message class");
+  m.def("build_messages", &build_messages, "columnar batch -> list of Message (C loop)");
+  m.def("make_fast_produce", &make_fast_produce, "C produce bound to an in-memory producer");
+  if (PyType_Ready(&DeliveryCounterType) < 0) throw py::error_already_set();
+  Py_INCREF(&DeliveryCounterType);
+  m.add_object("DeliveryCounter", py::reinterpret_borrow<py::object>(reinterpret_cast<PyObject*>(&DeliveryCounterType)));
 }

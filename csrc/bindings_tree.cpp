@@ -578,13 +578,13 @@ void rg_build(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& colptr
   }
 }
 
-// Row-group CSR build from a count-path CSR (indptr, idx, counts float32 / float64 / int32).
-// pass 0: ptr [G, N + 1] int32 gets the (group, row) counts at [g][r + 1] ([g][0] left as is);
-// pass 1: ptr holds the exclusive starts, ent (int16) written at gbase[g] + start + k.
+// Row-group CSR build from a count-path CSR (indptr, idx, counts float32 / float64 / int32):
+// ptr [G, N + 1] int32 gets the exclusive starts of every (group, row) run, ent (int16) the local
+// bins at gbase[g] + start + k, in CSR order. work: int32 scratch of >= G * ceil(N / 64).
 template <class V>
 void rg_build_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& counts, const Tensor& remap,
-                    int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, int64_t pass, const Tensor& ptr,
-                    const optional<Tensor>& gbase, const optional<Tensor>& ent) {
+                    int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, const Tensor& ptr,
+                    const Tensor& gbase, const Tensor& ent, const Tensor& work) {
   const auto dev = indptr.device();
   fdx::RgCsrBuildArgs<V> a{};
   a.indptr = indptr.data_ptr<int64_t>();
@@ -597,25 +597,21 @@ void rg_build_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& count
   a.flocal = flocal.data_ptr<int32_t>();
   a.G = (int32_t)ptr.size(0);
   a.ptr = reinterpret_cast<uint32_t*>(ptr.data_ptr<int32_t>());
-  if (pass == 1) {
-    FDX_CHECK(gbase && ent, "pass 1 needs gbase and ent");
-    chk(*gbase, dev, at::kLong, "gbase");
-    FDX_CHECK(ent->device() == dev && ent->scalar_type() == at::kShort && ent->is_contiguous(), "ent must be int16");
-    a.gbase = gbase->data_ptr<int64_t>();
-    a.ent = reinterpret_cast<uint16_t*>(ent->data_ptr<int16_t>());
-  }
+  a.gbase = gbase.data_ptr<int64_t>();
+  a.ent = reinterpret_cast<uint16_t*>(ent.data_ptr<int16_t>());
+  a.wave_base = reinterpret_cast<uint32_t*>(work.data_ptr<int32_t>());
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_rg_build_csr<V>(a, (int)pass, stream(dev));
+    fdx::launch_rg_build_csr<V>(a, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
-    fdx::rg_build_csr_cpu<V>(a, (int)pass);
+    fdx::rg_build_csr_cpu<V>(a);
   }
 }
 
 void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts, const Tensor& remap,
-                  int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, int64_t pass, const Tensor& ptr,
-                  const optional<Tensor>& gbase, const optional<Tensor>& ent) {
+                  int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, const Tensor& ptr,
+                  const Tensor& gbase, const Tensor& ent, const Tensor& work) {
   const auto dev = indptr.device();
   chk(indptr, dev, at::kLong, "indptr");
   chk(idx, dev, at::kInt, "idx");
@@ -623,14 +619,19 @@ void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts,
   chk(fgroup, dev, at::kInt, "fgroup");
   chk(flocal, dev, at::kInt, "flocal");
   chk(ptr, dev, at::kInt, "ptr");
+  chk(gbase, dev, at::kLong, "gbase");
+  chk(work, dev, at::kInt, "work");
+  FDX_CHECK(ent.device() == dev && ent.scalar_type() == at::kShort && ent.is_contiguous(), "ent must be int16");
   FDX_CHECK(counts.device() == dev && counts.is_contiguous() && counts.numel() >= idx.numel(), "counts");
   FDX_CHECK(ptr.dim() == 2 && ptr.size(1) == indptr.numel() && ptr.size(0) <= fdx::kRgMaxSlots,
             "ptr must be [G <= 64, N + 1]");
+  FDX_CHECK(gbase.numel() == ptr.size(0) + 1, "gbase must be [G + 1]");
   FDX_CHECK(fgroup.numel() == flocal.numel(), "fgroup / flocal");
+  FDX_CHECK(work.numel() >= ptr.size(0) * fdx::rg_build_csr_waves(indptr.numel() - 1), "work too small");
   switch (counts.scalar_type()) {
-    case at::kFloat: rg_build_csr_t<float>(indptr, idx, counts, remap, max_bin, fgroup, flocal, pass, ptr, gbase, ent); break;
-    case at::kDouble: rg_build_csr_t<double>(indptr, idx, counts, remap, max_bin, fgroup, flocal, pass, ptr, gbase, ent); break;
-    case at::kInt: rg_build_csr_t<int32_t>(indptr, idx, counts, remap, max_bin, fgroup, flocal, pass, ptr, gbase, ent); break;
+    case at::kFloat: rg_build_csr_t<float>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work); break;
+    case at::kDouble: rg_build_csr_t<double>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work); break;
+    case at::kInt: rg_build_csr_t<int32_t>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work); break;
     default: FDX_CHECK(false, "counts must be float32, float64 or int32");
   }
 }

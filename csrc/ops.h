@@ -112,8 +112,9 @@ struct RgListArgs;
 struct RgHistArgs;
 void launch_rg_build(const RgBuildArgs& a, int pass, hipStream_t s);
 template <class V> struct RgCsrBuildArgs;
-template <class V> void launch_rg_build_csr(const RgCsrBuildArgs<V>& a, int pass, hipStream_t s);
-template <class V> void rg_build_csr_cpu(const RgCsrBuildArgs<V>& a, int pass);
+template <class V> void launch_rg_build_csr(const RgCsrBuildArgs<V>& a, hipStream_t s);
+template <class V> void rg_build_csr_cpu(const RgCsrBuildArgs<V>& a);
+int64_t rg_build_csr_waves(int64_t N);
 void launch_rg_list(const RgListArgs& a, hipStream_t s);
 void launch_rg_hist(const RgHistArgs& a, hipStream_t s);
 void rg_build_cpu(const RgBuildArgs& a, int pass);

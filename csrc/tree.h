@@ -220,9 +220,9 @@ struct RgBuildArgs {
   uint16_t* ent;                  // pass 1 out
 };
 
-// Row-group CSR straight from the count-path CSR (rows of term counts, the bench corpus): a
-// thread per row, per-(group, row) counters in LDS, so runs keep the CSR order and no global
-// atomics are needed (the CSC build: ~2 returning atomics per entry, ~0.1 s at 10M rows).
+// Row-group CSR straight from the count-path CSR (rows of term counts, the bench corpus): a wave
+// per row, groups counted / placed with ballots, so runs keep the CSR order and no atomics are
+// needed (the CSC build: ~2 returning atomics per entry, ~0.1 s at 10M rows).
 // Entry (row r, feature f, count c): fa = remap[f] (-1: inactive), bin = c <= 0 ? 0 :
 // min(c, 255, max_bin) (the count path's binning), local = flocal[fa] + bin.
 template <class V>
@@ -236,9 +236,10 @@ struct RgCsrBuildArgs {
   const int32_t* fgroup;          // [Fa]
   const int32_t* flocal;          // [Fa]
   int32_t G;
-  uint32_t* ptr;                  // [G][N + 1]: pass 0 writes the counts at [g][r + 1]; pass 1 reads the starts
+  uint32_t* ptr;                  // [G][N + 1] out: exclusive starts of every (group, row) run
   const int64_t* gbase;
-  uint16_t* ent;                  // pass 1 out
+  uint16_t* ent;                  // out
+  uint32_t* wave_base;            // [ceil(N / 64)][G] scratch: per-wave group totals, then bases
 };
 
 // Built rows of a level grouped by slot. The slot of row r is node_slot[row_node[r]] when

@@ -266,39 +266,52 @@ void rg_build_cpu(const RgBuildArgs& a, int pass) {
   }
 }
 
-// Host twin of rg_build_csr_kernel (rows in parallel: every (group, row) run is written by its row only).
+// Host twin of rg_build_csr_kernel: counts per (group, row), exclusive scan per group, placement
+// in CSR order (every (group, row) run is written by its row only).
 template <class V>
-void rg_build_csr_cpu(const RgCsrBuildArgs<V>& a, int pass) {
+void rg_build_csr_cpu(const RgCsrBuildArgs<V>& a) {
+  auto bin_of = [&](V v) {
+    int32_t b = 0;
+    if (v > (V)0) {
+      const double d = (double)v;
+      b = d >= 255.0 ? 255 : (int32_t)d;
+      b = b < a.max_bin ? b : a.max_bin;
+    }
+    return b;
+  };
+  for (int g = 0; g < a.G; ++g) a.ptr[(int64_t)g * (a.N + 1)] = 0;
   parallel_for(a.N, 0, 4096, [&](int64_t lo, int64_t hi) {
     std::vector<uint32_t> c((size_t)a.G);
     for (int64_t r = lo; r < hi; ++r) {
-      for (int g = 0; g < a.G; ++g) c[(size_t)g] = pass == 1 ? a.ptr[(int64_t)g * (a.N + 1) + r] : 0u;
+      std::fill(c.begin(), c.end(), 0u);
+      for (int64_t e = a.indptr[r]; e < a.indptr[r + 1]; ++e) {
+        const int32_t fa = a.remap[a.idx[e]];
+        if (fa >= 0 && a.fgroup[fa] >= 0) ++c[(size_t)a.fgroup[fa]];
+      }
+      for (int g = 0; g < a.G; ++g) a.ptr[(int64_t)g * (a.N + 1) + r + 1] = c[(size_t)g];
+    }
+  });
+  for (int g = 0; g < a.G; ++g) {
+    uint32_t* p = a.ptr + (int64_t)g * (a.N + 1);
+    for (int64_t r = 0; r < a.N; ++r) p[r + 1] += p[r];
+  }
+  parallel_for(a.N, 0, 4096, [&](int64_t lo, int64_t hi) {
+    std::vector<uint32_t> c((size_t)a.G);
+    for (int64_t r = lo; r < hi; ++r) {
+      for (int g = 0; g < a.G; ++g) c[(size_t)g] = a.ptr[(int64_t)g * (a.N + 1) + r];
       for (int64_t e = a.indptr[r]; e < a.indptr[r + 1]; ++e) {
         const int32_t fa = a.remap[a.idx[e]];
         if (fa < 0) continue;
         const int32_t g = a.fgroup[fa];
         if (g < 0) continue;
-        if (pass == 0) {
-          ++c[(size_t)g];
-        } else {
-          const V v = a.counts[e];
-          int32_t b = 0;
-          if (v > (V)0) {
-            const double d = (double)v;
-            b = d >= 255.0 ? 255 : (int32_t)d;
-            b = b < a.max_bin ? b : a.max_bin;
-          }
-          a.ent[a.gbase[g] + c[(size_t)g]++] = (uint16_t)(a.flocal[fa] + b);
-        }
+        a.ent[a.gbase[g] + c[(size_t)g]++] = (uint16_t)(a.flocal[fa] + bin_of(a.counts[e]));
       }
-      if (pass == 0)
-        for (int g = 0; g < a.G; ++g) a.ptr[(int64_t)g * (a.N + 1) + r + 1] = c[(size_t)g];
     }
   });
 }
-template void rg_build_csr_cpu<float>(const RgCsrBuildArgs<float>&, int);
-template void rg_build_csr_cpu<double>(const RgCsrBuildArgs<double>&, int);
-template void rg_build_csr_cpu<int32_t>(const RgCsrBuildArgs<int32_t>&, int);
+template void rg_build_csr_cpu<float>(const RgCsrBuildArgs<float>&);
+template void rg_build_csr_cpu<double>(const RgCsrBuildArgs<double>&);
+template void rg_build_csr_cpu<int32_t>(const RgCsrBuildArgs<int32_t>&);
 
 // Built rows grouped by slot, ascending inside each slot (the device order inside a 4096-row
 // window may differ; the histogram sums do not depend on it).

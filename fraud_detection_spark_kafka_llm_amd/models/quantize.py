@@ -216,6 +216,27 @@ RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 8.0))
 RG_BAL_MIN = float(os.environ.get("FDX_RG_BAL_MIN", 8.0))
 
 
+class _Ticker:
+    """Device-synchronised phase timer (FDX_RG_TIMING=1)."""
+
+    def __init__(self, dev, out: dict):
+        import time as _t
+        self._t, self.dev, self.out = _t, dev, out
+        self._sync()
+        self.t0 = _t.perf_counter()
+
+    def _sync(self):
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+
+    def __call__(self, name: str) -> bool:
+        self._sync()
+        t = self._t.perf_counter()
+        self.out[name] = round((t - self.t0) * 1e3, 2)
+        self.t0 = t
+        return True
+
+
 class RowGroups:
     """Row-group CSR of the active features (csrc/tree.h "row-group histogram engine").
 
@@ -230,6 +251,8 @@ class RowGroups:
     def __init__(self, Q: "Quantized", max_groups: int = None, bins: int = None):
         C = native.lib()
         dev = Q.device
+        self.timing: dict = {}
+        tick = _Ticker(dev, self.timing) if os.environ.get("FDX_RG_TIMING") == "1" else None
         max_groups = RG_MAX_GROUPS if max_groups is None else max_groups
         self.bins = B = RG_BINS if bins is None else bins
         if B not in (4096, 8192):
@@ -239,6 +262,7 @@ class RowGroups:
         nb = Q.nbins.cpu().numpy().astype(np.int64)
         boff = np.asarray(Q.boff_host, dtype=np.int64)
         Fa = int(nb.size)
+        tick and tick("d2h")
         order = np.argsort(-cnt, kind="stable")
         order = order[cnt[order] > 0]
         cum = np.concatenate([[0], np.cumsum(nb[order])])
@@ -279,21 +303,26 @@ class RowGroups:
         fl_t = torch.from_numpy(flocal).to(dev)
         self.gbase = torch.from_numpy(gbase).to(dev)
         self.gbin = torch.from_numpy(gbin).to(dev)
-        ptr = torch.zeros((G, N + 1), dtype=torch.int32, device=dev)
+        tick and tick("plan")
+        ptr = torch.empty((G, N + 1), dtype=torch.int32, device=dev) if N else torch.zeros((G, 1), dtype=torch.int32,
+                                                                                            device=dev)
         # readable padding behind the end: the pass loads aligned 8-entry blocks
-        self.ent = torch.zeros(int(gbase[-1]) + 16, dtype=torch.int16, device=dev)[:int(gbase[-1])]
+        self.ent = torch.empty(int(gbase[-1]) + 16, dtype=torch.int16, device=dev)[:int(gbase[-1])]
+        tick and tick("alloc")
         csr = getattr(Q, "csr_src", None)
         if csr is not None and G <= 64:
-            # rows of the count-path CSR: a thread per row, runs in CSR order, no global atomics
+            # rows of the count-path CSR: a wave per row, runs in CSR order, no global atomics
             indptr, idx, counts, max_bins = csr
             remap = torch.full((Q.num_features,), -1, dtype=torch.int32, device=dev)
             remap[Q.fid_orig] = torch.arange(Q.Fa, dtype=torch.int32, device=dev)
-            C.tree_rg_build_csr(indptr, idx, counts, remap, max_bins - 1, fg_t, fl_t, 0, ptr, None, None)
-            self.ptr = torch.cumsum(ptr, dim=1, dtype=torch.int32)
-            del ptr
-            C.tree_rg_build_csr(indptr, idx, counts, remap, max_bins - 1, fg_t, fl_t, 1, self.ptr, self.gbase,
-                                self.ent)
+            work = torch.empty(G * -(-N // 64), dtype=torch.int32, device=dev)
+            C.tree_rg_build_csr(indptr, idx, counts, remap, max_bins - 1, fg_t, fl_t, ptr, self.gbase, self.ent,
+                                work)
+            self.ptr = ptr
+            del work
+            tick and tick("build")
         else:
+            ptr.zero_()
             C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 0, ptr, None, None, None)
             self.ptr = torch.cumsum(ptr, dim=1, dtype=torch.int32)
             del ptr

@@ -643,15 +643,8 @@ class StreamingEngine:
     def _produce_each(self, seg, entry, keys, koff, nulls, vals, voff) -> None:
         """Per-record produce (confluent producers): the segment resolves when every record's
         delivery report has arrived; any error fails it."""
-        left = [seg.n_out]
-        err_box = [None]
-
-        def cb(err, msg):
-            if err is not None:
-                err_box[0] = err
-            left[0] -= 1
-            if left[0] == 0:
-                self._on_delivery(seg, entry, err_box[0])
+        # one C callable counts the segment's reports (first error kept) and resolves it at the last
+        cb = native.lib().DeliveryCounter(seg.n_out, functools.partial(self._on_delivery, seg, entry))
 
         # one C loop of produce() calls (BufferError: poll(0.05) and retry; other errors: cb(err))
         native.lib().produce_each(self.producer, self.topic, np.ascontiguousarray(keys, dtype=np.uint8),

@@ -99,6 +99,27 @@ class Message(tuple):
         return (1, self[6])
 
 
+_NATIVE = [False, None]
+
+
+def _native():
+    """The native core's broker fast paths (C-speed Message accessors, batch -> Messages, per-record
+    produce), as a librdkafka client would run them; None without the built extension or with
+    FDX_KAFKA_NATIVE=0 (the pure-Python broker)."""
+    if not _NATIVE[0]:
+        _NATIVE[0] = True
+        import os
+        if os.environ.get("FDX_KAFKA_NATIVE", "1") != "0":
+            try:
+                from ..ops import native
+                lib = native.lib()
+                lib.install_message_accessors(Message)
+                _NATIVE[1] = lib
+            except Exception:                    # noqa: BLE001 (no extension: pure Python)
+                _NATIVE[1] = None
+    return _NATIVE[1]
+
+
 def _b(v) -> Optional[bytes]:
     if v is None:
         return None
@@ -153,12 +174,19 @@ class RecordBatch:
         return Message(self.topic, self.partition, self.base_offset + i, self.key(i), self.value(i))
 
     def messages(self) -> list:
-        """Every record as a ``Message`` (bytes sliced out of one copy of each buffer)."""
+        """Every record as a ``Message`` (bytes sliced out of the buffers; one C loop when the
+        native core is loaded)."""
+        ms = int((self.ts + (time.time() - time.perf_counter())) * 1000)
+        fast = _native()
+        if fast is not None:
+            return fast.build_messages(Message, self.topic, self.partition, self.base_offset,
+                                       np.ascontiguousarray(self.keys), np.ascontiguousarray(self.key_off),
+                                       np.ascontiguousarray(self.values), np.ascontiguousarray(self.val_off),
+                                       self.null_keys, ms)
         vb, kb = self.values.tobytes(), self.keys.tobytes()
         vo, ko = self.val_off.tolist(), self.key_off.tolist()
         nk = self.null_keys
         t, p, b = self.topic, self.partition, self.base_offset
-        ms = int((self.ts + (time.time() - time.perf_counter())) * 1000)
         new = tuple.__new__
         return [new(Message, (t, p, b + i, None if (nk is not None and nk[i]) else kb[ko[i]:ko[i + 1]],
                               vb[vo[i]:vo[i + 1]], None, ms)) for i in range(len(vo) - 1)]
@@ -479,6 +507,9 @@ class Producer:
         self._pending: list = []
         self.lock = threading.Lock()
         self.fail_next = 0            # fault injection: fail the next N deliveries
+        fast = _native()
+        if fast is not None:          # per-record produce in C (falls back to _produce_py itself)
+            self.produce = fast.make_fast_produce(self, self.broker, Message)
 
     def _deliver_later(self, cb, err, what) -> None:
         if cb is not None:
@@ -494,6 +525,10 @@ class Producer:
 
     def produce(self, topic: str, value=None, key=None, partition: int = -1, on_delivery: Optional[Callable] = None,
                 callback: Optional[Callable] = None, **kw) -> None:
+        self._produce_py(topic, value, key, partition, on_delivery, callback, **kw)
+
+    def _produce_py(self, topic: str, value=None, key=None, partition: int = -1,
+                    on_delivery: Optional[Callable] = None, callback: Optional[Callable] = None, **kw) -> None:
         if topic is None:
             raise TypeError("topic must be a str (KAFKA_OUTPUT_TOPIC unset?)")
         cb = on_delivery or callback

@@ -150,6 +150,37 @@ def test_row_groups_from_csr_equal_csc_build(dtype):
             np.testing.assert_array_equal(np.sort(ea[s0:s1]), np.sort(eb[s0:s1]))
 
 
+def _csr_vc(dtype, n=3000, F=400, seed=5):
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+
+    rng = np.random.default_rng(seed)
+    dense = (rng.random((n, F)) < np.linspace(0.002, 0.6, F)) * rng.integers(1, 300, (n, F))
+    nz = dense != 0
+    indptr = torch.from_numpy(np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64))
+    rr, cc = np.nonzero(nz)
+    scale = torch.from_numpy(rng.uniform(0.5, 2.0, F))
+    scale[::17] = 0.0
+    return VectorColumn.tfidf(F, indptr, torch.from_numpy(cc.astype(np.int32)),
+                              torch.from_numpy(dense[rr, cc]).to(dtype), scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.int32])
+def test_gpu_row_groups_from_csr_equal_host(dtype):
+    """The wave-per-row ballot build on the GPU writes the host twin's layout bit for bit (runs
+    in CSR order on both)."""
+    vc = _csr_vc(dtype, n=20000, F=600, seed=8)
+    out = []
+    for dev in ("cpu", "cuda:0"):
+        Q = quantize(vc.to(dev), max_bins=64, counts=vc.to(dev).tf_counts, scale=vc.to(dev).tf_scale)
+        assert getattr(Q, "csr_src", None) is not None
+        rg = RowGroups(Q, bins=4096)
+        out.append((rg.ptr.cpu().numpy(), rg.ent.cpu().numpy(), rg.G))
+    assert out[0][2] == out[1][2] >= 2
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 def test_row_groups_incomplete_beyond_max_groups():
     vc = _wide(2000, 300, 4)
     Q = quantize(vc, max_bins=100, **QKW)
