@@ -623,8 +623,8 @@ void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts,
   chk(work, dev, at::kInt, "work");
   FDX_CHECK(ent.device() == dev && ent.scalar_type() == at::kShort && ent.is_contiguous(), "ent must be int16");
   FDX_CHECK(counts.device() == dev && counts.is_contiguous() && counts.numel() >= idx.numel(), "counts");
-  FDX_CHECK(ptr.dim() == 2 && ptr.size(1) == indptr.numel() && ptr.size(0) <= fdx::kRgMaxSlots,
-            "ptr must be [G <= 64, N + 1]");
+  FDX_CHECK(ptr.dim() == 2 && ptr.size(1) == indptr.numel() && ptr.size(0) <= 128,
+            "ptr must be [G <= 128, N + 1]");
   FDX_CHECK(gbase.numel() == ptr.size(0) + 1, "gbase must be [G + 1]");
   FDX_CHECK(fgroup.numel() == flocal.numel(), "fgroup / flocal");
   FDX_CHECK(work.numel() >= ptr.size(0) * fdx::rg_build_csr_waves(indptr.numel() - 1), "work too small");

@@ -88,11 +88,17 @@ __global__ __launch_bounds__(256) void rg_build_csr_kernel(RgCsrBuildArgs<V> a, 
   const int64_t r0 = wave * kRgBuildRowsPerWave;
   if (r0 >= a.N) return;
   const int64_t r1 = r0 + kRgBuildRowsPerWave < a.N ? r0 + kRgBuildRowsPerWave : a.N;
-  // lane g: group g's running count over the wave's rows (pass 0), its next position (pass 1)
-  uint32_t run = (pass == 1 && lane < a.G) ? a.wave_base[wave * a.G + lane] : 0u;
+  // lane l: the running count over the wave's rows (pass 0), then the next position (pass 1), of
+  // group l (run0) and of group l + 64 (run1)
+  const int ga = lane, gb = lane + 64;
+  uint32_t run0 = (pass == 1 && ga < a.G) ? a.wave_base[wave * a.G + ga] : 0u;
+  uint32_t run1 = (pass == 1 && gb < a.G) ? a.wave_base[wave * a.G + gb] : 0u;
   for (int64_t r = r0; r < r1; ++r) {
     const int64_t e0 = a.indptr[r], e1 = a.indptr[r + 1];
-    if (pass == 1 && lane < a.G) a.ptr[(int64_t)lane * (a.N + 1) + r] = run;
+    if (pass == 1) {
+      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + r] = run0;
+      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + r] = run1;
+    }
     for (int64_t eb = e0; eb < e1; eb += 64) {
       const int64_t e = eb + lane;
       int32_t g = -1, loc = 0;
@@ -107,18 +113,25 @@ __global__ __launch_bounds__(256) void rg_build_csr_kernel(RgCsrBuildArgs<V> a, 
       while (act) {
         const int32_t gs = __shfl(g, __ffsll((unsigned long long)act) - 1, 64);
         const uint64_t m = __ballot(g == gs);
+        const int owner = gs & 63;
         if (pass == 1) {
-          const uint32_t base = __shfl(run, gs, 64);
+          const uint32_t base = gs < 64 ? __shfl(run0, owner, 64) : __shfl(run1, owner, 64);
           if (g == gs) a.ent[a.gbase[gs] + base + __popcll(m & lt)] = (uint16_t)loc;
         }
-        if (lane == gs) run += __popcll(m);
+        if (lane == owner) {
+          if (gs < 64) run0 += __popcll(m);
+          else run1 += __popcll(m);
+        }
         act &= ~m;
       }
     }
   }
-  if (lane < a.G) {
-    if (pass == 0) a.wave_base[wave * a.G + lane] = run;               // the wave's total
-    else if (r1 == a.N) a.ptr[(int64_t)lane * (a.N + 1) + a.N] = run;   // the group's end
+  if (pass == 0) {
+    if (ga < a.G) a.wave_base[wave * a.G + ga] = run0;                    // the wave's totals
+    if (gb < a.G) a.wave_base[wave * a.G + gb] = run1;
+  } else if (r1 == a.N) {                                                 // the groups' ends
+    if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + a.N] = run0;
+    if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + a.N] = run1;
   }
 }
 

@@ -206,7 +206,7 @@ class BlockedCSC:
 
 
 RG_BINS = int(os.environ.get("FDX_RG_BINS", 8192))   # local bins per row group: 8192 (1 workgroup per CU) or 4096 (2)
-RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 64))
+RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
 RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 2048))   # workgroups per row-group pass
 # work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
 # (ptr, digits) loads whether or not it has entries in the group)
@@ -310,7 +310,7 @@ class RowGroups:
         self.ent = torch.empty(int(gbase[-1]) + 16, dtype=torch.int16, device=dev)[:int(gbase[-1])]
         tick and tick("alloc")
         csr = getattr(Q, "csr_src", None)
-        if csr is not None and G <= 64:
+        if csr is not None and G <= 128:
             # rows of the count-path CSR: a wave per row, runs in CSR order, no global atomics
             indptr, idx, counts, max_bins = csr
             remap = torch.full((Q.num_features,), -1, dtype=torch.int32, device=dev)

@@ -164,6 +164,50 @@ def _csr_vc(dtype, n=3000, F=400, seed=5):
                               torch.from_numpy(dense[rr, cc]).to(dtype), scale)
 
 
+def _csr_vc_wide(n=3000, F=7000, per_row=120, maxc=60, seed=4):
+    """Sparse rows over many features with many count values: > 64 row groups of 4096 bins."""
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+
+    rng = np.random.default_rng(seed)
+    cols = np.sort(np.stack([rng.choice(F, per_row, replace=False) for _ in range(n)]), axis=1)
+    cnt = rng.integers(1, maxc, (n, per_row))
+    indptr = torch.from_numpy(np.arange(n + 1, dtype=np.int64) * per_row)
+    return VectorColumn.tfidf(F, indptr, torch.from_numpy(cols.reshape(-1).astype(np.int32)),
+                              torch.from_numpy(cnt.reshape(-1).astype(np.int32)), torch.ones(F, dtype=torch.float64))
+
+
+def test_row_groups_from_csr_beyond_64_groups():
+    """Lanes hold groups l and l + 64 in the CSR build: > 64 groups give the CSC build's layout."""
+    vc = _csr_vc_wide()
+    Q = quantize(vc, max_bins=64, counts=vc.tf_counts, scale=vc.tf_scale)
+    a = RowGroups(Q, bins=4096)
+    csr = Q.csr_src
+    del Q.csr_src
+    b = RowGroups(Q, bins=4096)
+    Q.csr_src = csr
+    assert a.complete and 64 < a.G == b.G <= 128
+    np.testing.assert_array_equal(a.ptr.numpy(), b.ptr.numpy())
+    pa, ga, ea, eb = a.ptr.numpy(), a.gbase.numpy(), a.ent.numpy(), b.ent.numpy()
+    for g in range(0, a.G, 5):
+        for r in range(0, Q.n_rows, 37):
+            s0, s1 = ga[g] + pa[g, r], ga[g] + pa[g, r + 1]
+            np.testing.assert_array_equal(np.sort(ea[s0:s1]), np.sort(eb[s0:s1]))
+
+
+@pytest.mark.gpu
+def test_gpu_row_groups_from_csr_beyond_64_groups():
+    vc = _csr_vc_wide()
+    out = []
+    for dev in ("cpu", "cuda:0"):
+        v = vc.to(dev)
+        rg = RowGroups(quantize(v, max_bins=64, counts=v.tf_counts, scale=v.tf_scale), bins=4096)
+        ptr, ent, gb = rg.ptr.cpu().numpy(), rg.ent.cpu().numpy(), rg.gbase.cpu().numpy()
+        out.append((ptr, np.concatenate([ent[gb[g]: gb[g] + ptr[g, -1]] for g in range(rg.G)]), rg.G))
+    assert 64 < out[0][2] == out[1][2]
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.int32])
 def test_gpu_row_groups_from_csr_equal_host(dtype):
@@ -175,7 +219,10 @@ def test_gpu_row_groups_from_csr_equal_host(dtype):
         Q = quantize(vc.to(dev), max_bins=64, counts=vc.to(dev).tf_counts, scale=vc.to(dev).tf_scale)
         assert getattr(Q, "csr_src", None) is not None
         rg = RowGroups(Q, bins=4096)
-        out.append((rg.ptr.cpu().numpy(), rg.ent.cpu().numpy(), rg.G))
+        ptr, ent, gb = rg.ptr.cpu().numpy(), rg.ent.cpu().numpy(), rg.gbase.cpu().numpy()
+        # the runs only (the 8-entry alignment padding between groups is never written)
+        runs = np.concatenate([ent[gb[g]: gb[g] + ptr[g, -1]] for g in range(rg.G)])
+        out.append((ptr, runs, rg.G))
     assert out[0][2] == out[1][2] >= 2
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1], out[1][1])
