@@ -86,6 +86,7 @@ py::tuple pack_messages(py::list msgs) {
   voff.reserve(m + 1);
   nulls.reserve(m);
   std::string last_topic;
+  py::object last_topic_obj;
   int64_t last_part = -1;
   int32_t last_idx = -1;
   for (Py_ssize_t i = 0; i < m; ++i) {
@@ -99,8 +100,11 @@ py::tuple pack_messages(py::list msgs) {
     py::object t = py::reinterpret_steal<py::object>(call0(msg, N.topic));
     py::object p = py::reinterpret_steal<py::object>(call0(msg, N.partition));
     if (!t || !p) throw py::error_already_set();
-    const std::string topic = t.cast<std::string>();
     const int64_t part = p.cast<int64_t>();
+    // consecutive messages share the topic object: compare it before converting the string
+    const bool same_topic = t.ptr() == last_topic_obj.ptr();
+    const std::string topic = same_topic ? last_topic : t.cast<std::string>();
+    last_topic_obj = t;
     if (last_idx < 0 || part != last_part || topic != last_topic) {
       last_idx = -1;
       for (size_t k = 0; k < parts.size(); ++k)
@@ -390,13 +394,16 @@ const FastNames& fnames() {
   return *n;
 }
 
-// state = (producer, broker, Message class)
+// state = (producer, broker, Message class, broker.lock.acquire, broker.lock.release, broker.topics)
 PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
   const Names& N = names();
   const FastNames& F = fnames();
   PyObject* producer = PyTuple_GET_ITEM(state, 0);
   PyObject* broker = PyTuple_GET_ITEM(state, 1);
   PyObject* cls = PyTuple_GET_ITEM(state, 2);
+  PyObject* acquire = PyTuple_GET_ITEM(state, 3);
+  PyObject* release = PyTuple_GET_ITEM(state, 4);
+  PyObject* topics = PyTuple_GET_ITEM(state, 5);
   PyObject *topic = nargs > 0 ? args[0] : nullptr, *value = nargs > 1 ? args[1] : Py_None,
            *key = nargs > 2 ? args[2] : Py_None, *part_o = nargs > 3 ? args[3] : nullptr, *cb = Py_None;
   bool simple = nargs <= 4;
@@ -404,9 +411,11 @@ PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs,
   for (Py_ssize_t i = 0; i < nkw && simple; ++i) {
     PyObject* k = PyTuple_GET_ITEM(kwnames, i);
     PyObject* v = args[nargs + i];
-    if (PyUnicode_Compare(k, N.value) == 0) value = v;
-    else if (PyUnicode_Compare(k, N.key) == 0) key = v;
-    else if (PyUnicode_Compare(k, N.on_delivery) == 0 || PyUnicode_Compare(k, F.callback) == 0) cb = v;
+    // interned keyword names compare by identity first
+    if (k == N.value || PyUnicode_Compare(k, N.value) == 0) value = v;
+    else if (k == N.key || PyUnicode_Compare(k, N.key) == 0) key = v;
+    else if (k == N.on_delivery || PyUnicode_Compare(k, N.on_delivery) == 0 || PyUnicode_Compare(k, F.callback) == 0)
+      cb = v;
     else if (PyUnicode_Compare(k, F.partition) == 0) part_o = v;
     else simple = false;
   }
@@ -422,12 +431,9 @@ PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs,
   simple = simple && topic && PyUnicode_Check(topic) && (PyBytes_CheckExact(value) || value == Py_None) &&
            (PyBytes_CheckExact(key) || key == Py_None);
   PyObject* parts = nullptr;
-  PyObject* lock = nullptr;
   if (simple) {
-    PyObject* topics = PyObject_GetAttr(broker, F.topics);
-    parts = topics ? PyDict_GetItemWithError(topics, topic) : nullptr;   // borrowed
+    parts = PyDict_GetItemWithError(topics, topic);   // borrowed
     Py_XINCREF(parts);
-    Py_XDECREF(topics);
     if (!parts || !PyList_Check(parts) || PyList_GET_SIZE(parts) == 0) simple = false;
   }
   if (!simple) {                                   // the Python implementation
@@ -452,10 +458,8 @@ PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs,
     PyErr_SetString(PyExc_ValueError, "partition out of range");
     return nullptr;
   }
-  lock = PyObject_GetAttr(broker, F.lock);
-  PyObject* r = lock ? PyObject_CallMethodNoArgs(lock, F.acquire) : nullptr;
+  PyObject* r = PyObject_CallNoArgs(acquire);
   if (!r) {
-    Py_XDECREF(lock);
     Py_DECREF(parts);
     return nullptr;
   }
@@ -494,13 +498,12 @@ PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs,
   // release the lock whatever happened (keep a pending error)
   PyObject *et, *ev, *etb;
   PyErr_Fetch(&et, &ev, &etb);
-  PyObject* rel = PyObject_CallMethodNoArgs(lock, F.release);
+  PyObject* rel = PyObject_CallNoArgs(release);
   Py_XDECREF(rel);
   if (et) PyErr_Restore(et, ev, etb);
   Py_XDECREF(tk);
   Py_XDECREF(tv);
   Py_XDECREF(size);
-  Py_DECREF(lock);
   Py_DECREF(parts);
   if (!ok || !rel) return nullptr;
   if (cb != Py_None) {
@@ -533,7 +536,9 @@ PyMethodDef fast_produce_def = {"produce", reinterpret_cast<PyCFunction>(reinter
                                 METH_FASTCALL | METH_KEYWORDS, "in-memory broker produce (C)"};
 
 py::object make_fast_produce(py::object producer, py::object broker, py::object message_cls) {
-  py::tuple state = py::make_tuple(producer, broker, message_cls);
+  py::object lock = broker.attr("lock");
+  py::tuple state = py::make_tuple(producer, broker, message_cls, lock.attr("acquire"), lock.attr("release"),
+                                   broker.attr("topics"));
   PyObject* f = PyCFunction_NewEx(&fast_produce_def, state.ptr(), nullptr);
   if (!f) throw py::error_already_set();
   return py::reinterpret_steal<py::object>(f);
