@@ -432,7 +432,7 @@ __device__ __forceinline__ void rg_range_dense(RgShared<BINS>& sh, const RgHistA
 // of kRgSB batches (a lane per row) through a 3-stage pipeline -- list entries of super-batch
 // j + 3, (ptr, digits) of j + 2, the rows' first 8-entry blocks of j + 1 -- while the atomics of
 // super-batch j run: every load has a whole super-batch of work to arrive in.
-constexpr int kRgSB = 2;
+constexpr int kRgSB = 3;
 
 template <int BINS>
 __device__ __forceinline__ void rg_run_block(RgShared<BINS>& sh, uint4 v, uint32_t blk, uint32_t st, uint32_t en,
@@ -450,62 +450,6 @@ __device__ __forceinline__ void rg_run_block(RgShared<BINS>& sh, uint4 v, uint32
       atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[b]), c0);
       atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[b]), c1);
     }
-  }
-}
-
-// One batch of a sparse group (a lane per row, each row's first 8-entry block in registers).
-// A block holds ~2 of its row's entries, so atomics per lane-block would spend 16 LDS atomic
-// instructions (the pass's bound: ~25 cycles each) per ~2 entries. Instead the batch's valid
-// first-block entries are numbered across the wave (a wave scan of the per-lane counts) and each
-// lane takes entries lane, lane + 64, ...: it finds the owning lane by a binary search over the
-// exclusive prefix and fetches the bin and the row's statistics by cross-lane permutes
-// (ds_bpermute), so every atomic instruction carries 64 entries. Entries past a row's first
-// block (rows longer than the block: rare here) take the per-block path.
-template <int BINS>
-__device__ __forceinline__ void rg_sparse_batch(RgShared<BINS>& sh, const uint16_t* ent, int lane, uint32_t st,
-                                                uint32_t en, uint4 v, int32_t q0, int32_t q1, uint32_t sinkb,
-                                                int dbg, unsigned long long& sink) {
-  const uint32_t blk0 = st & ~7u;
-  const uint32_t s0 = st - blk0;
-  const uint32_t s1 = en > st ? (en - blk0 < 8u ? en - blk0 : 8u) : s0;
-  const uint32_t n = s1 - s0;
-  uint32_t incl = n;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
-  }
-  const uint32_t total = __shfl(incl, 63, 64);
-  const uint32_t pb = incl - n;
-  const int32_t off = (int32_t)s0 - (int32_t)pb;          // slot of entry t in its lane = t + off
-  for (uint32_t t0 = 0; t0 < total; t0 += 64) {
-    const uint32_t t = t0 + (uint32_t)lane;
-    int r = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-      const int c = r + step;
-      const uint32_t pc = __shfl(pb, c > 63 ? 63 : c, 64);
-      if (c <= 63 && pc <= t) r = c;
-    }
-    const uint32_t slot = (uint32_t)((int32_t)t + __shfl(off, r, 64));
-    const uint32_t wx = __shfl(v.x, r, 64), wy = __shfl(v.y, r, 64), wz = __shfl(v.z, r, 64), ww = __shfl(v.w, r, 64);
-    const uint32_t dw = slot >> 1;
-    const uint32_t w = dw == 0 ? wx : dw == 1 ? wy : dw == 2 ? wz : ww;
-    const uint32_t bin = (w >> (16 * (slot & 1))) & 0xffffu;
-    const int32_t a0 = __shfl(q0, r, 64), a1 = __shfl(q1, r, 64);
-    if (t < total) {
-      if (dbg & 2) {
-        sink += bin;
-      } else {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[bin]), (unsigned long long)(int64_t)a0);
-        atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[bin]), (unsigned long long)(int64_t)a1);
-      }
-    }
-  }
-  if (en > blk0 + 8) {                                    // the rest of a long row, block by block
-    const unsigned long long c0 = (unsigned long long)(int64_t)q0, c1 = (unsigned long long)(int64_t)q1;
-    for (uint32_t blk = blk0 + 8; blk < en; blk += 8)
-      rg_run_block<BINS>(sh, *reinterpret_cast<const uint4*>(ent + blk), blk, st, en, c0, c1, sinkb, dbg, sink);
   }
 }
 
@@ -563,9 +507,17 @@ __device__ __forceinline__ void rg_range_sparse(RgShared<BINS>& sh, const RgHist
     info_of(j + 2, r2, st2, en2, dg2);
     blocks_of(st1, en1, v1);
 #pragma unroll
-    for (int i = 0; i < kRgSB; ++i)
-      rg_sparse_batch<BINS>(sh, ent, lane, st0[i], en0[i], v0[i], (int32_t)rg_q(dg0[i].x, np),
-                            (int32_t)rg_q(dg0[i].y, np), sinkb, dbg, sink);
+    for (int i = 0; i < kRgSB; ++i) {
+      if (en0[i] > st0[i]) {
+        const unsigned long long c0 = (unsigned long long)rg_q(dg0[i].x, np);
+        const unsigned long long c1 = (unsigned long long)rg_q(dg0[i].y, np);
+        uint32_t blk = st0[i] & ~7u;
+        rg_run_block<BINS>(sh, v0[i], blk, st0[i], en0[i], c0, c1, sinkb, dbg, sink);
+        for (blk += 8; blk < en0[i]; blk += 8)        // rows longer than one block (rare here)
+          rg_run_block<BINS>(sh, *reinterpret_cast<const uint4*>(ent + blk), blk, st0[i], en0[i], c0, c1, sinkb,
+                             dbg, sink);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < kRgSB; ++i) {
       st0[i] = st1[i];
