@@ -620,17 +620,23 @@ struct LevelPlanArgs {
   int32_t* sub_sib;
 };
 
-FDX_HD void level_plan(const LevelPlanArgs& a) {
-  for (int32_t n = 0; n < a.max_nodes; ++n) {
+// The plan's table resets, split over nthreads workers (the device runs them on 64 lanes before
+// the single-thread plan; the host on one).
+FDX_HD void level_plan_reset(const LevelPlanArgs& a, int32_t t, int32_t nthreads) {
+  for (int32_t n = t; n < a.max_nodes; n += nthreads) {
     a.default_child[n] = -1;
     a.node_slot[n] = -1;
     if (a.node_dense) for (int k = 0; k < 4; ++k) a.node_dense[4 * n + k] = -1;
   }
-  for (int32_t i = 0; i < 2 * a.L; ++i) {
+  for (int32_t i = t; i < 2 * a.L; i += nthreads) {
     a.next_open[i] = -1;
     a.next_totals[2 * i] = a.next_totals[2 * i + 1] = 0;
   }
-  for (int32_t i = 0; i < a.L; ++i) a.s2n[i] = a.sub_dst[i] = a.sub_par[i] = a.sub_sib[i] = -1;
+  for (int32_t i = t; i < a.L; i += nthreads) a.s2n[i] = a.sub_dst[i] = a.sub_par[i] = a.sub_sib[i] = -1;
+}
+
+FDX_HD void level_plan(const LevelPlanArgs& a, bool reset = true) {
+  if (reset) level_plan_reset(a, 0, 1);
   const double thr = a.min_gain > 1e-6 ? a.min_gain : 1e-6;
   const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
   int32_t nn = *a.n_nodes, n_cs = 0, n_next = 0;

@@ -827,7 +827,10 @@ __global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, co
 }
 
 __global__ void level_plan_kernel(LevelPlanArgs a) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) level_plan(a);
+  if (blockIdx.x != 0) return;
+  level_plan_reset(a, (int32_t)threadIdx.x, (int32_t)blockDim.x);
+  __syncthreads();
+  if (threadIdx.x == 0) level_plan(a, false);
 }
 
 // ------------------------------------------------------------------ gbdt helpers

@@ -781,7 +781,6 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                              feat_thr, feat_mask, None)
         with tracing.span("tree.hist"):
             use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH and not build_all
-            sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
             slot8 = None
             csc_slot8, csc_dig = None, ws.rowdig
             rg = ws.rowgroups() if (not build_all and np_ == 4) else None
@@ -804,6 +803,8 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                 s2n = torch.arange(n_build, dtype=torch.int32, device=dev)
             ct = pass_ct(np_, n_build)
             launches = []
+            # (the CSC items are built on first use: the row-group engine never touches them)
+            sel_groups = None
             if rg is not None:
                 shard_args = (shards.bin_lo, n_build * shards.Bs) if shards is not None else (None, 0)
                 if d == 0:
@@ -829,6 +830,8 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                     shards.bin_lo if shards is not None else None,
                     n_build * shards.Bs if shards is not None else 0))
                 sel_groups, use_dense = [], False
+            if sel_groups is None:
+                sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
             for grp in sel_groups:
                 if grp.num_items == 0:
                     continue
