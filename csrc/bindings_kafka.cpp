@@ -166,6 +166,10 @@ int64_t produce_each(py::object producer, py::object topic, py::array_t<uint8_t>
                                      py::reinterpret_borrow<py::object>(N.on_delivery));
   int64_t sent = 0;
   for (int64_t i = 0; i < n; ++i) {
+    if (i && (i & 255) == 0) {                    // let the reader / client threads run between records
+      PyThreadState* ts = PyEval_SaveThread();
+      PyEval_RestoreThread(ts);
+    }
     py::object kobj = (nk && nk[i]) ? py::none()
                                     : py::reinterpret_steal<py::object>(PyBytes_FromStringAndSize(
                                           reinterpret_cast<const char*>(kb + ko[i]), ko[i + 1] - ko[i]));

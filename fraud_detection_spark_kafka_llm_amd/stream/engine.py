@@ -33,7 +33,9 @@ import concurrent.futures as cf
 import functools
 import gc
 import json
+import os
 import queue
+import sys
 import threading
 import time
 from collections import deque
@@ -235,6 +237,9 @@ def extract_texts(values: list, slot: Slot, field_name: str = "text") -> np.ndar
     slot.data[total: total + PAD] = 0
     slot.n_docs, slot.n_bytes = len(values), total
     return status
+
+
+SWITCH_INTERVAL_S = float(os.environ.get("FDX_SWITCH_INTERVAL_MS", 0.5)) / 1e3
 
 
 class _Reader(threading.Thread):
@@ -486,6 +491,10 @@ class StreamingEngine:
         # long-lived objects (model, tables, torch/numpy internals) leave the collector's young
         # generations: full collections would otherwise stall the readers for 50-100 ms
         gc.freeze()
+        # the readers, the engine thread and a client's own threads share the GIL: a 5 ms default
+        # switch interval shows up directly in per-message latency (p50 ~2 ms at 300K msgs/s)
+        if sys.getswitchinterval() > SWITCH_INTERVAL_S:
+            sys.setswitchinterval(SWITCH_INTERVAL_S)
         self._quota = max_messages
         self._readers_stop.clear()
         self._last_read = time.time()
