@@ -194,141 +194,6 @@ void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64
   }
 }
 
-// RF batch rows: rw [N, kRfTrees * 2] u8 class counts, totals [kRfTrees, 2] int64 (+=)
-void rf_rows(const Tensor& label, const Tensor& tree_ids, int64_t seed, bool bootstrap, int64_t row0,
-             const Tensor& rw, const Tensor& totals) {
-  const auto dev = label.device();
-  chk(label, dev, at::kFloat, "label");
-  chk(tree_ids, dev, at::kInt, "tree_ids");
-  chk(rw, dev, at::kByte, "rw");
-  chk(totals, dev, at::kLong, "totals");
-  FDX_CHECK(tree_ids.numel() == fdx::kRfTrees && totals.numel() == 2 * fdx::kRfTrees, "tree_ids / totals size");
-  FDX_CHECK(rw.numel() == label.numel() * 2 * fdx::kRfTrees, "rw must be [N, 2 * kRfTrees]");
-  fdx::RfRowsArgs a{label.data_ptr<float>(), tree_ids.data_ptr<int32_t>(), (uint64_t)seed, bootstrap ? 1 : 0, row0,
-                    label.numel(), rw.data_ptr<uint8_t>(), totals.data_ptr<int64_t>()};
-  if (dev.is_cuda()) {
-    c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_rf_rows(a, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  } else {
-    fdx::rf_rows_cpu(a);
-  }
-}
-
-// RF batch pass slots: rs [N, kRfTrees] u8 from row_node [kRfTrees, N] and node_slot [kRfTrees, M]
-void rf_slots(const Tensor& row_node, const Tensor& node_slot, int64_t s0, int64_t cnt, const Tensor& rs) {
-  const auto dev = row_node.device();
-  chk(row_node, dev, at::kInt, "row_node");
-  chk(node_slot, dev, at::kInt, "node_slot");
-  chk(rs, dev, at::kByte, "rs");
-  FDX_CHECK(row_node.dim() == 2 && row_node.size(0) == fdx::kRfTrees && node_slot.dim() == 2 &&
-                node_slot.size(0) == fdx::kRfTrees && rs.numel() == row_node.size(1) * fdx::kRfTrees,
-            "row_node [kRfTrees, N], node_slot [kRfTrees, M], rs [N, kRfTrees]");
-  FDX_CHECK(cnt >= 0 && cnt <= 64, "at most 64 slots per pass");
-  fdx::RfSlotsArgs a{row_node.data_ptr<int32_t>(), node_slot.data_ptr<int32_t>(), (int32_t)node_slot.size(1),
-                     (int32_t)s0, (int32_t)cnt, row_node.size(1), rs.data_ptr<uint8_t>()};
-  if (dev.is_cuda()) {
-    c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_rf_slots(a, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  } else {
-    fdx::rf_slots_cpu(a);
-  }
-}
-
-// RF batch pass: out [Fa] int64 bit masks of the pass slots that sampled each feature, any [Fa] u8
-void rf_slot_mask(int64_t seed, const Tensor& slot_tree, const Tensor& slot_node, const Tensor& thr,
-                  const Tensor& fid_orig, const Tensor& out, const Tensor& any) {
-  const auto dev = fid_orig.device();
-  chk(slot_tree, dev, at::kInt, "slot_tree");
-  chk(slot_node, dev, at::kInt, "slot_node");
-  chk(thr, dev, at::kDouble, "thr");
-  chk(fid_orig, dev, at::kLong, "fid_orig");
-  chk(out, dev, at::kLong, "out");
-  chk(any, dev, at::kByte, "any");
-  FDX_CHECK(slot_tree.numel() <= 64 && slot_node.numel() == slot_tree.numel() && thr.numel() == slot_tree.numel(),
-            "<= 64 slots");
-  FDX_CHECK(out.numel() == fid_orig.numel() && any.numel() == fid_orig.numel(), "out / any [Fa]");
-  fdx::RfSlotMaskArgs a{(uint64_t)seed, slot_tree.data_ptr<int32_t>(), slot_node.data_ptr<int32_t>(),
-                        thr.data_ptr<double>(), (int32_t)slot_tree.numel(), fid_orig.data_ptr<int64_t>(),
-                        fid_orig.numel(), reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()),
-                        any.data_ptr<uint8_t>()};
-  if (dev.is_cuda()) {
-    c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_rf_slot_mask(a, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  } else {
-    fdx::rf_slot_mask_cpu(a);
-  }
-}
-
-// Multi-tree RF histogram pass (hist_rf_kernel): slot_node / slot_tree [nslots <= 8 * ct]
-void hist_rf(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
-             const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key, const Tensor& rs,
-             const Tensor& rw, const Tensor& boff, const Tensor& nbins, const Tensor& slot_node,
-             const Tensor& slot_tree, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct,
-             const optional<Tensor>& feat_active, const optional<Tensor>& feat_slots) {
-  const auto dev = csc_row.device();
-  chk(item_start, dev, at::kLong, "item_start");
-  chk(item_end, dev, at::kLong, "item_end");
-  chk(item_f0, dev, at::kInt, "item_f0");
-  chk(item_meta, dev, at::kInt, "item_meta");
-  chk(csc_row, dev, at::kInt, "csc_row");
-  chk(csc_key, dev, at::kByte, "csc_key");
-  chk(rs, dev, at::kByte, "rs");
-  chk(rw, dev, at::kByte, "rw");
-  chk(boff, dev, at::kLong, "boff");
-  chk(nbins, dev, at::kInt, "nbins");
-  chk(slot_node, dev, at::kInt, "slot_node");
-  chk(slot_tree, dev, at::kInt, "slot_tree");
-  chk(hist, dev, at::kLong, "hist");
-  FDX_CHECK(bt == 1 || bt == 2 || bt == 4, "bt in {1,2,4}");
-  FDX_CHECK(ct == 1 || ct == 2 || ct == 4 || ct == 8, "ct in {1,2,4,8}");
-  FDX_CHECK(slot_node.numel() <= 8 * ct && slot_tree.numel() == slot_node.numel(), "slots <= 8 * ct");
-  FDX_CHECK(rs.numel() == rw.numel() / 2 && rs.numel() % fdx::kRfTrees == 0, "rs [N, kRfTrees], rw [N, 2 kRfTrees]");
-  FDX_CHECK(hist.dim() == 3 && hist.size(1) >= TB && hist.size(2) == 2, "hist [rows, >= TB, 2]");
-  FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_key, 4), "CSC views need 4 readable padding entries");
-  fdx::HistArgs a{};
-  a.item_start = item_start.data_ptr<int64_t>();
-  a.item_end = item_end.data_ptr<int64_t>();
-  a.item_f0 = item_f0.data_ptr<int32_t>();
-  a.item_meta = item_meta.data_ptr<int32_t>();
-  a.num_items = (int32_t)item_start.numel();
-  a.csc_row = csc_row.data_ptr<int32_t>();
-  a.csc_key = csc_key.data_ptr<uint8_t>();
-  a.boff = boff.data_ptr<int64_t>();
-  a.nbins = nbins.data_ptr<int32_t>();
-  a.slot_node = slot_node.data_ptr<int32_t>();
-  a.nslots = (int32_t)slot_node.numel();
-  a.hist_stride = hist.size(1);
-  a.hist = hist.data_ptr<int64_t>();
-  a.rf_rs = rs.data_ptr<uint8_t>();
-  a.rf_rw = rw.data_ptr<uint8_t>();
-  a.rf_slot_tree = slot_tree.data_ptr<int32_t>();
-  if (wave_item) {
-    chk(*wave_item, dev, at::kInt, "wave_item");
-    a.wave_item = wave_item->data_ptr<int32_t>();
-    a.num_slots = (int32_t)wave_item->numel();
-  }
-  if (feat_active) {
-    chk(*feat_active, dev, at::kByte, "feat_active");
-    FDX_CHECK(feat_active->numel() == nbins.numel(), "feat_active must be [Fa] uint8");
-    a.feat_active = feat_active->data_ptr<uint8_t>();
-  }
-  if (feat_slots) {
-    chk(*feat_slots, dev, at::kLong, "feat_slots");
-    FDX_CHECK(feat_slots->numel() == nbins.numel(), "feat_slots must be [Fa] int64 bit masks");
-    a.rf_feat_slots = reinterpret_cast<const uint64_t*>(feat_slots->data_ptr<int64_t>());
-  }
-  if (dev.is_cuda()) {
-    c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_hist_rf(a, (int)bt, (int)ct, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  } else {
-    fdx::hist_rf_cpu(a, (int)bt);
-  }
-}
-
 void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
                 const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
                 const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
@@ -1168,10 +1033,6 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rg_build_csr", &rg_build_csr);
   m.def("tree_rg_hist", &rg_hist);
   m.def("tree_rf_sample", &rf_sample);
-  m.def("tree_rf_rows", &rf_rows);
-  m.def("tree_rf_slots", &rf_slots);
-  m.def("tree_hist_rf", &hist_rf);
-  m.def("tree_rf_slot_mask", &rf_slot_mask);
   m.def("tree_hist_dense", &hist_dense);
   m.def("tree_dense_fg", &dense_fg);
   m.def("tree_dense_waves", &dense_waves);

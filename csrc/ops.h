@@ -78,19 +78,8 @@ struct SplitArgs;
 struct PartitionArgs;
 struct LevelPlanArgs;
 struct RfSampleArgs;
-struct RfRowsArgs;
-struct RfSlotsArgs;
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s);
 void rf_sample_cpu(const RfSampleArgs& a);
-void launch_rf_rows(const RfRowsArgs& a, hipStream_t s);
-void launch_rf_slots(const RfSlotsArgs& a, hipStream_t s);
-void launch_hist_rf(const HistArgs& a, int bt, int ct, hipStream_t s);
-struct RfSlotMaskArgs;
-void launch_rf_slot_mask(const RfSlotMaskArgs& a, hipStream_t s);
-void rf_slot_mask_cpu(const RfSlotMaskArgs& a);
-void rf_rows_cpu(const RfRowsArgs& a);
-void rf_slots_cpu(const RfSlotsArgs& a);
-void hist_rf_cpu(const HistArgs& h, int bt);
 void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s);
 void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);

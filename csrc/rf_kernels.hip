@@ -153,23 +153,7 @@ __global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
   }
   a.mask[f] = m;
 }
-__global__ __launch_bounds__(kThreads) void rf_slot_mask_kernel(RfSlotMaskArgs a) {
-  const int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (f >= a.Fa) return;
-  const int64_t fid = a.fid_orig[f];
-  uint64_t m = 0;
-  for (int s = 0; s < a.nslots; ++s)
-    if (feature_priority(a.seed, a.slot_tree[s], a.slot_node[s], fid) <= a.thr[s]) m |= 1ull << s;
-  a.out[f] = m;
-  a.any[f] = m ? 1 : 0;
-}
 }  // namespace
-
-void launch_rf_slot_mask(const RfSlotMaskArgs& a, hipStream_t s) {
-  if (a.Fa > 0)
-    hipLaunchKernelGGL(rf_slot_mask_kernel, dim3((unsigned)((a.Fa + kThreads - 1) / kThreads)), dim3(kThreads), 0, s,
-                       a);
-}
 
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s) {
   // k >= F (every feature) is handled by the caller: thresholds 1.0, mask all ones

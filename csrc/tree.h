@@ -104,11 +104,6 @@ struct HistArgs {
   int64_t hist_stride;            // bins per histogram row (TB, or TB + 1 when padded)
   int64_t* hist;                  // [rows][hist_stride][2], accumulated (+=)
   const uint8_t* feat_active;     // [Fa] optional: items without an active feature are skipped (RF)
-  // multi-tree RF passes (hist_rf_kernel): kRfTrees trees per pass, row-major per-row records
-  const uint8_t* rf_rs;           // [N][kRfTrees] pass slot of the row in tree j (0xff: none)
-  const uint8_t* rf_rw;           // [N][kRfTrees][2] class counts (Poisson weight x indicator, <= 32)
-  const int32_t* rf_slot_tree;    // [nslots] tree (0..kRfTrees-1) of each pass slot
-  const uint64_t* rf_feat_slots;  // [Fa] optional: bit s = pass slot s sampled the feature (tiles skipped)
 };
 
 // ------------------------------------------------------------------ row-blocked histogram engine
@@ -310,44 +305,6 @@ FDX_HD int64_t rg_col_offset(const RgHistArgs& a, int64_t b) {
 }
 
 FDX_HD int64_t rg_q(uint32_t d, int np) { return np == 4 ? undigits4(d) : undigits1(d); }
-
-// RF batch pass: which of the (<= 64) pass slots sampled each active feature.
-struct RfSlotMaskArgs {
-  uint64_t seed;
-  const int32_t* slot_tree;       // [nslots] global tree index
-  const int32_t* slot_node;       // [nslots] tree-local node id
-  const double* thr;              // [nslots] sampling threshold
-  int32_t nslots;
-  const int64_t* fid_orig;        // [Fa]
-  int64_t Fa;
-  uint64_t* out;                  // [Fa]
-  uint8_t* any;                   // [Fa] out != 0 (item filter)
-};
-
-constexpr int kRfTrees = 8;       // trees per multi-tree RF batch (one 8-byte slot record per row)
-
-// Per-row records of an RF batch: rw[row][j] = (w (1 - y), w y) with w = Poisson(1) draw of
-// (seed, tree_ids[j], row0 + row) (1 without bootstrap); totals[j] = column sums (root counts).
-struct RfRowsArgs {
-  const float* label;             // [N]
-  const int32_t* tree_ids;        // [kRfTrees] (-1: unused)
-  uint64_t seed;
-  int32_t bootstrap;
-  int64_t row0;
-  int64_t N;
-  uint8_t* rw;                    // [N][kRfTrees][2]
-  int64_t* totals;                // [kRfTrees][2] +=
-};
-
-// rs[row][j] = node_slot[j][row_node[j][row]] - s0 when inside [0, cnt), else 0xff.
-struct RfSlotsArgs {
-  const int32_t* row_node;        // [kRfTrees][N]
-  const int32_t* node_slot;       // [kRfTrees][max_nodes] pass-global slot (-1: none)
-  int32_t max_nodes;
-  int32_t s0, cnt;
-  int64_t N;
-  uint8_t* rs;                    // [N][kRfTrees]
-};
 
 // RF per-level feature sampling (rf_kernels.hip / tree_cpu.cpp): for each of `nnodes` nodes the
 // k-th smallest feature_priority over feature indices 0..F-1 (exact, as a 53-bit integer u with

@@ -94,81 +94,6 @@ void rf_sample_cpu(const RfSampleArgs& a) {
   });
 }
 
-void rf_slot_mask_cpu(const RfSlotMaskArgs& a) {
-  parallel_for(a.Fa, 0, 1024, [&](int64_t lo, int64_t hi) {
-    for (int64_t f = lo; f < hi; ++f) {
-      uint64_t m = 0;
-      for (int s = 0; s < a.nslots; ++s)
-        if (feature_priority(a.seed, a.slot_tree[s], a.slot_node[s], a.fid_orig[f]) <= a.thr[s]) m |= 1ull << s;
-      a.out[f] = m;
-      a.any[f] = m ? 1 : 0;
-    }
-  });
-}
-
-void rf_rows_cpu(const RfRowsArgs& a) {
-  std::mutex mu;
-  parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
-    int64_t tot[2 * kRfTrees] = {0};
-    for (int64_t r = lo; r < hi; ++r) {
-      const int y = a.label[r] > 0.5f ? 1 : 0;
-      for (int j = 0; j < kRfTrees; ++j) {
-        int w = 0;
-        if (a.tree_ids[j] >= 0)
-          w = a.bootstrap ? poisson1(hash_uniform(a.seed, (uint64_t)a.tree_ids[j], (uint64_t)(a.row0 + r))) : 1;
-        const int c0 = y ? 0 : w, c1 = y ? w : 0;
-        a.rw[(r * kRfTrees + j) * 2] = (uint8_t)c0;
-        a.rw[(r * kRfTrees + j) * 2 + 1] = (uint8_t)c1;
-        tot[2 * j] += c0;
-        tot[2 * j + 1] += c1;
-      }
-    }
-    std::lock_guard<std::mutex> g(mu);
-    for (int i = 0; i < 2 * kRfTrees; ++i) a.totals[i] += tot[i];
-  });
-}
-
-void rf_slots_cpu(const RfSlotsArgs& a) {
-  parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
-    for (int64_t r = lo; r < hi; ++r)
-      for (int j = 0; j < kRfTrees; ++j) {
-        const int32_t n = a.row_node[(int64_t)j * a.N + r];
-        const int32_t s = (n >= 0 && n < a.max_nodes) ? a.node_slot[(int64_t)j * a.max_nodes + n] - a.s0 : -1;
-        a.rs[r * kRfTrees + j] = (s >= 0 && s < a.cnt) ? (uint8_t)s : (uint8_t)0xff;
-      }
-  });
-}
-
-void hist_rf_cpu(const HistArgs& h, int bt) {
-  parallel_for(h.num_items, 0, 4, [&](int64_t lo, int64_t hi) {
-    for (int64_t it = lo; it < hi; ++it) {
-      if (!item_active(h, it)) continue;
-      const int32_t meta = h.item_meta[it];
-      const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta), koff = item_koff(meta);
-      const int32_t f0 = h.item_f0[it];
-      for (int64_t e = h.item_start[it]; e < h.item_end[it]; ++e) {
-        const int64_t row = h.csc_row[e];
-        const int key = h.csc_key[e];
-        if (key < koff || key >= koff + 16 * bt) continue;
-        const int fl = key >> sl2, b = key & ((1 << sl2) - 1);
-        if (fl >= nfeat) continue;
-        const int f = f0 + fl;
-        if (b >= h.nbins[f]) continue;
-        for (int j = 0; j < kRfTrees; ++j) {
-          const int s = h.rf_rs[row * kRfTrees + j];
-          if (s >= h.nslots || h.rf_slot_tree[s] != j) continue;
-          if (h.rf_feat_slots && !((h.rf_feat_slots[f] >> s) & 1ull)) continue;   // unsampled: never read
-          const int node = h.slot_node[s];
-          if (node < 0) continue;
-          int64_t* dst = h.hist + ((int64_t)node * h.hist_stride + h.boff[f] + b) * 2;
-          __atomic_fetch_add(dst, (int64_t)h.rf_rw[(row * kRfTrees + j) * 2], __ATOMIC_RELAXED);
-          __atomic_fetch_add(dst + 1, (int64_t)h.rf_rw[(row * kRfTrees + j) * 2 + 1], __ATOMIC_RELAXED);
-        }
-      }
-    }
-  });
-}
-
 void hist_cpu(const HistArgs& h, int bt, int np) {
   parallel_for(h.num_items, 0, 4, [&](int64_t lo, int64_t hi) {
     for (int64_t it = lo; it < hi; ++it) {

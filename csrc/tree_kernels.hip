@@ -597,192 +597,6 @@ __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* 
   }
 }
 
-// ------------------------------------------------------------------ multi-tree RF passes (PAR-05)
-// Count histograms of kRfTrees trees in one pass over the CSC work items. Per row the batch keeps an
-// 8-byte record of pass slots (one byte per tree) and a 16-byte record of class counts (two bytes
-// per tree), so each entry costs two vector gathers whatever the number of trees. Per K-step the
-// records of 64 entries are transposed into tree-major LDS rows; the B column (slot s, stat q) of
-// tile ct reads the rows of tree slot_tree[s] and keeps the counts whose slot byte equals s.
-__global__ __launch_bounds__(256) void rf_rows_kernel(RfRowsArgs a) {
-  __shared__ unsigned long long s_tot[2 * kRfTrees];
-  if (threadIdx.x < 2 * kRfTrees) s_tot[threadIdx.x] = 0;
-  __syncthreads();
-  int64_t tot[2 * kRfTrees];
-#pragma unroll
-  for (int i = 0; i < 2 * kRfTrees; ++i) tot[i] = 0;
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
-    const int y = a.label[r] > 0.5f ? 1 : 0;
-    uint32_t words[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int j = 0; j < kRfTrees; ++j) {
-      int w = 0;
-      if (a.tree_ids[j] >= 0)
-        w = a.bootstrap ? poisson1(hash_uniform(a.seed, (uint64_t)a.tree_ids[j], (uint64_t)(a.row0 + r))) : 1;
-      const uint32_t c0 = y ? 0u : (uint32_t)w, c1 = y ? (uint32_t)w : 0u;
-      words[j / 2] |= (c0 | (c1 << 8)) << (16 * (j & 1));
-      tot[2 * j] += c0;
-      tot[2 * j + 1] += c1;
-    }
-    reinterpret_cast<uint4*>(a.rw)[r] = make_uint4(words[0], words[1], words[2], words[3]);
-  }
-#pragma unroll
-  for (int i = 0; i < 2 * kRfTrees; ++i)
-    if (tot[i]) atomicAdd(&s_tot[i], (unsigned long long)tot[i]);
-  __syncthreads();
-  if (threadIdx.x < 2 * kRfTrees && s_tot[threadIdx.x])
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.totals) + threadIdx.x, s_tot[threadIdx.x]);
-}
-
-__global__ __launch_bounds__(256) void rf_slots_kernel(RfSlotsArgs a) {
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int j = 0; j < kRfTrees; ++j) {
-      const int32_t n = a.row_node[(int64_t)j * a.N + r];
-      int32_t s = (n >= 0 && n < a.max_nodes) ? a.node_slot[(int64_t)j * a.max_nodes + n] - a.s0 : -1;
-      const uint32_t b = (s >= 0 && s < a.cnt) ? (uint32_t)s : 0xffu;
-      if (j < 4) lo |= b << (8 * j);
-      else hi |= b << (8 * (j - 4));
-    }
-    reinterpret_cast<uint2*>(a.rs)[r] = make_uint2(lo, hi);
-  }
-}
-
-template <int BT, int CT>
-__global__ __launch_bounds__(256) void hist_rf_kernel(HistArgs a) {
-  constexpr int G = 4 * kWave;
-  constexpr int KS = 64;
-  __shared__ __attribute__((aligned(16))) uint8_t s_key[4][G];
-  __shared__ __attribute__((aligned(16))) uint8_t s_rs[4][kRfTrees][G];
-  __shared__ __attribute__((aligned(16))) uint8_t s_rw[4][2 * kRfTrees][G];
-
-  const int wid = threadIdx.x / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wslot = blockIdx.x * 4 + wid;
-  const int item = a.wave_item ? a.wave_item[wslot] : wslot;
-  if (item < 0 || item >= a.num_items) return;
-  if (!item_active(a, item)) return;
-  const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
-  const int32_t meta = a.item_meta[item];
-  const uint32_t koff = (uint32_t)item_koff(meta);
-  const bool fast7 = item_nfeat(meta) > 1 || a.nbins[a.item_f0[item]] <= 128;
-  const int r = lane & 15, g = lane >> 4;
-  const int slot_sub = r >> 1, q = r & 1;
-  // tiles whose 8 slots sampled none of the item's features are skipped (wave-uniform)
-  uint64_t im = ~0ull;
-  if (a.rf_feat_slots) {
-    im = 0;
-    const int32_t fi = a.item_f0[item];
-    const int nfi = item_nfeat(meta);
-    for (int j = 0; j < nfi; ++j) im |= a.rf_feat_slots[fi + j];
-    if (im == 0) return;
-  }
-  int jt[CT];
-  bool on[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    const int sl = ct * 8 + slot_sub;
-    jt[ct] = sl < a.nslots ? a.rf_slot_tree[sl] : -1;
-    on[ct] = ((im >> (8 * ct)) & 0xffull) != 0;
-  }
-  i32x4 acc[BT][CT];
-#pragma unroll
-  for (int bt = 0; bt < BT; ++bt)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) acc[bt][ct] = i32x4{0, 0, 0, 0};
-
-  const int64_t first = e0 & ~(int64_t)3;
-  const int64_t e_last = (e1 - 1) & ~(int64_t)3;
-  const uint2* rs = reinterpret_cast<const uint2*>(a.rf_rs);
-  const uint4* rw = reinterpret_cast<const uint4*>(a.rf_rw);
-  RowStep nx;
-  load_rows(a, first + 4 * lane, e0, e1, e_last, nx);
-  for (int64_t base = first; base < e1; base += G) {
-    const RowStep cur = nx;
-    load_rows(a, base + G + 4 * lane, e0, e1, e_last, nx);     // rows of the next step in flight
-    const int4 cr = cur.rows();
-    const int32_t rr[4] = {cr.x, cr.y, cr.z, cr.w};
-    uint2 sv[4];
-    uint4 wv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {       // unconditional loads (clamped row), then select
-      sv[i] = rs[rr[i] >= 0 ? rr[i] : 0];
-      wv[i] = rw[rr[i] >= 0 ? rr[i] : 0];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (rr[i] < 0) {
-        sv[i] = make_uint2(0xffffffffu, 0xffffffffu);
-        wv[i] = make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-    *reinterpret_cast<uint32_t*>(&s_key[wid][4 * lane]) = cur.keys4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      *reinterpret_cast<uint32_t*>(&s_rs[wid][j][4 * lane]) = gather_byte(sv[0].x, sv[1].x, sv[2].x, sv[3].x, j);
-      *reinterpret_cast<uint32_t*>(&s_rs[wid][4 + j][4 * lane]) = gather_byte(sv[0].y, sv[1].y, sv[2].y, sv[3].y, j);
-      *reinterpret_cast<uint32_t*>(&s_rw[wid][j][4 * lane]) = gather_byte(wv[0].x, wv[1].x, wv[2].x, wv[3].x, j);
-      *reinterpret_cast<uint32_t*>(&s_rw[wid][4 + j][4 * lane]) = gather_byte(wv[0].y, wv[1].y, wv[2].y, wv[3].y, j);
-      *reinterpret_cast<uint32_t*>(&s_rw[wid][8 + j][4 * lane]) = gather_byte(wv[0].z, wv[1].z, wv[2].z, wv[3].z, j);
-      *reinterpret_cast<uint32_t*>(&s_rw[wid][12 + j][4 * lane]) = gather_byte(wv[0].w, wv[1].w, wv[2].w, wv[3].w, j);
-    }
-    lds_sync();
-#pragma unroll
-    for (int ks = 0; ks < G / KS; ++ks) {
-      const int k0 = ks * KS + 16 * g;
-      const uint4 kv = *reinterpret_cast<const uint4*>(&s_key[wid][k0]);
-      i32x4 A[BT];
-      onehot_a<BT>(kv, (uint32_t)r + koff, fast7, A);
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        if (!on[ct]) continue;
-        const int j = jt[ct] < 0 ? 0 : jt[ct];
-        const uint4 s4 = *reinterpret_cast<const uint4*>(&s_rs[wid][j][k0]);
-        const uint4 d4 = *reinterpret_cast<const uint4*>(&s_rw[wid][2 * j + q][k0]);
-        const uint32_t rep = jt[ct] < 0 ? 0xfefefefeu : (uint32_t)(ct * 8 + slot_sub) * 0x01010101u;
-        const i32x4 B = {(int)(d4.x & zero_bytes_ff(s4.x ^ rep)), (int)(d4.y & zero_bytes_ff(s4.y ^ rep)),
-                         (int)(d4.z & zero_bytes_ff(s4.z ^ rep)), (int)(d4.w & zero_bytes_ff(s4.w ^ rep))};
-#pragma unroll
-        for (int bt = 0; bt < BT; ++bt)
-          acc[bt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[bt], B, acc[bt][ct], 0, 0, 0);
-      }
-    }
-    lds_sync();
-  }
-  const int32_t f0 = a.item_f0[item];
-  const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta);
-  int node_of[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    const int slot = ct * 8 + slot_sub;
-    const int n = a.slot_node[slot < a.nslots ? slot : a.nslots - 1];
-    node_of[ct] = slot < a.nslots ? n : -1;
-  }
-  int64_t bin_of[BT][4];
-#pragma unroll
-  for (int bt = 0; bt < BT; ++bt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ek = 16 * bt + 4 * g + i + (int)koff;
-      const int fl = ek >> sl2, b = ek & ((1 << sl2) - 1);
-      const int f = f0 + (fl < nfeat ? fl : 0);
-      const int nb = a.nbins[f];
-      const int64_t bo = a.boff[f];
-      bin_of[bt][i] = (fl < nfeat && b < nb) ? bo + b : -1;
-    }
-#pragma unroll
-  for (int bt = 0; bt < BT; ++bt)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t v = -(int64_t)(acc[bt][ct][i] >> 7);
-        if (v == 0 || node_of[ct] < 0 || bin_of[bt][i] < 0) continue;
-        int64_t* dst = a.hist + ((int64_t)node_of[ct] * a.hist_stride + bin_of[bt][i]) * 2 + q;
-        atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
-      }
-}
-
 // ------------------------------------------------------------------ partition
 __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
@@ -968,26 +782,6 @@ void launch_logistic_grad(const double* margin, const float* label, const float*
 
 void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s) {
   if (N > 0) hipLaunchKernelGGL(leaf_update_kernel, dim3(grid_for(N)), dim3(256), 0, s, margin, row_node, node_value, N);
-}
-
-void launch_rf_rows(const RfRowsArgs& a, hipStream_t s) {
-  if (a.N > 0) hipLaunchKernelGGL(rf_rows_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
-}
-
-void launch_rf_slots(const RfSlotsArgs& a, hipStream_t s) {
-  if (a.N > 0) hipLaunchKernelGGL(rf_slots_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
-}
-
-void launch_hist_rf(const HistArgs& a, int bt, int ct, hipStream_t s) {
-  if (a.num_items <= 0) return;
-  const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
-  const dim3 grid((slots + 3) / 4), block(256);
-#define FDX_RF_CASE(B, C) \
-  if (bt == B && ct == C) { hipLaunchKernelGGL((hist_rf_kernel<B, C>), grid, block, 0, s, a); return; }
-  FDX_RF_CASE(1, 1) FDX_RF_CASE(1, 2) FDX_RF_CASE(1, 4) FDX_RF_CASE(1, 8)
-  FDX_RF_CASE(2, 1) FDX_RF_CASE(2, 2) FDX_RF_CASE(2, 4) FDX_RF_CASE(2, 8)
-  FDX_RF_CASE(4, 1) FDX_RF_CASE(4, 2) FDX_RF_CASE(4, 4) FDX_RF_CASE(4, 8)
-#undef FDX_RF_CASE
 }
 
 }  // namespace fdx

@@ -707,7 +707,29 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                      h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
                      shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
                      bootstrap: bool = False, deferred: bool = False, on_first_wait=None):
-    """GBDT tree with the level loop on the device (same trees as grow_tree's host loop, bit for
+    """One tree through :func:`device_tree_steps`, waiting on each event it yields."""
+    return drive(device_tree_steps(Q, ws, params, tree_index, g, h, weight, coll, shards, label, bootstrap,
+                                   deferred, on_first_wait))
+
+
+def drive(steps):
+    """Run a step generator to its end, synchronising every event it yields; returns its value."""
+    try:
+        while True:
+            next(steps).synchronize()
+    except StopIteration as stop:
+        return stop.value
+
+
+def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
+                      h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
+                      shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
+                      bootstrap: bool = False, deferred: bool = False, on_first_wait=None):
+    """A generator: yields an event wherever the host must wait for the device (the next level's
+    counts, the finished node table) and returns the Tree (or PendingTree). :func:`drive` runs
+    one tree; the forest driver (models/forest_batch.py) interleaves several on their own streams.
+
+    GBDT tree with the level loop on the device (same trees as grow_tree's host loop, bit for
     bit). Per level: histogram passes -> sibling subtraction -> split search -> best split per
     node -> ``tree_level_plan`` (one thread: apply the splits to the device node table, this
     level's partition tables, the next level's open list / builds / subtraction triples) ->
@@ -755,7 +777,7 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
             if on_first_wait is not None:
                 on_first_wait()
                 on_first_wait = None
-            ev.synchronize()
+            yield ev
             cnt = st.counts_host[d - 1].tolist()
             n_open, n_build = int(cnt[1]), int(cnt[2])
             if n_open == 0:
@@ -906,6 +928,7 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
 
     if node_value is not None:
         return PendingTree(node_value, finish)
+    yield done
     return finish()
 
 
@@ -942,6 +965,9 @@ class PendingTree:
 class _Done:
     def synchronize(self):
         pass
+
+    def query(self) -> bool:
+        return True
 
 
 def _weight(st, mode) -> int:

@@ -10,7 +10,6 @@ Reference configs: /root/reference/fraud_detection_spark.py:59-74.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -22,8 +21,9 @@ from ..ml.tree_model import Tree
 from ..parallel.dist import Collectives
 from ..utils.config import default_device
 from ..utils import tracing
-from .forest_batch import K_RF_TREES, BatchWorkspace, grow_forest_batch
-from .grower import GrowParams, Workspace, grow_tree
+from . import forest_batch
+from .forest_batch import ForestLanes, grow_forest_concurrent
+from .grower import GrowParams, Workspace, device_levels_ok, grow_tree
 from .quantize import quantize
 from .rf_sampling import features_per_node
 
@@ -112,22 +112,18 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
                         seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
     ws = Workspace(Q)
     trees = ckpt.load_trees() if (ckpt is not None and resume) else []
-    # PAR-05: FDX_RF_BATCH=1 grows 8 trees per level pass (models/forest_batch.py; single-process
-    # only: the data-parallel path reduce-scatters per tree). The trees are identical, but on
-    # MI355X the per-tree passes are faster: the single-tree kernel compacts each pass to the live
-    # entries of one tree (1-byte slot, 2 count bytes per entry), the 8-tree kernel carries 24
-    # bytes of records per entry and up to 8 MFMA tiles. Measured at 10M rows, depth 5: 200 trees
-    # sqrt-sampled 1.21-1.26 s per-tree vs 1.34-1.36 s batched; 40 trees with all features
-    # 1.05 s vs 1.45 s (profiles/r2_rf_batch_ab.txt). Per-tree passes are therefore the default.
-    batch = (os.environ.get("FDX_RF_BATCH", "0") == "1" and w is None and not coll.active
-             and num_trees - len(trees) > 1)
-    bw = BatchWorkspace(Q) if batch else None
+    # PAR-05: several trees in flight, each on its own stream (models/forest_batch.py). Not under
+    # data parallelism: every rank must issue its collectives in one order on one stream.
+    inflight = 1 if coll.active else max(1, forest_batch.TREES_IN_FLIGHT)
+    lanes = None
+    if inflight > 1 and num_trees - len(trees) > 1 and device_levels_ok(params, w):
+        lanes = ForestLanes(Q, min(inflight, num_trees - len(trees)), ws)
+    chunk = max(ckpt.every if ckpt is not None else 64, 1)
     t = len(trees)
     while t < num_trees:
-        if batch:
-            ids = list(range(t, min(num_trees, t + K_RF_TREES)))
-            with tracing.span("forest.batch", first=t, trees=len(ids)):
-                grown = grow_forest_batch(Q, ws, bw, params, ids, y, bootstrap)
+        if lanes is not None:
+            ids = list(range(t, min(num_trees, t + chunk)))
+            grown = grow_forest_concurrent(Q, lanes, params, ids, y, w, bootstrap)
         else:
             ids = [t]
             with tracing.span("forest.tree", tree=t):

@@ -451,9 +451,12 @@ def test_gpu_rf_sampling_equals_host():
         assert torch.equal(h[0], g[0]) and torch.equal(h[1], g[1])
 
 
-@pytest.mark.parametrize("bootstrap,subset,n_trees", [(True, "sqrt", 11), (False, "all", 3), (True, "onethird", 9)])
-def test_multi_tree_rf_batches_equal_single_tree_growth(monkeypatch, bootstrap, subset, n_trees):
-    """PAR-05: 8 trees per level pass (tree_hist_rf) give exactly the trees of one-at-a-time growth."""
+@pytest.mark.parametrize("bootstrap,subset,n_trees,lanes", [(True, "sqrt", 11, 4), (False, "all", 3, 2),
+                                                         (True, "onethird", 9, 3)])
+def test_trees_in_flight_equal_single_tree_growth(monkeypatch, bootstrap, subset, n_trees, lanes):
+    """PAR-05: trees grown several at a time (interleaved level loops, own workspaces) are exactly
+    the trees of one-at-a-time growth."""
+    from fraud_detection_spark_kafka_llm_amd.models import forest_batch
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
 
     rng = np.random.default_rng(17)
@@ -463,16 +466,17 @@ def test_multi_tree_rf_batches_equal_single_tree_growth(monkeypatch, bootstrap, 
     vc = VectorColumn(F, dense=torch.from_numpy(dense.astype(np.float64)))
     kw = dict(num_trees=n_trees, max_depth=5, max_bins=16, bootstrap=bootstrap, feature_subset=subset, seed=7,
               device="cpu")
-    monkeypatch.setenv("FDX_RF_BATCH", "0")
+    monkeypatch.setattr(forest_batch, "TREES_IN_FLIGHT", 1)
     ref = fit_forest(vc, torch.from_numpy(y), **kw)
-    monkeypatch.setenv("FDX_RF_BATCH", "1")
+    monkeypatch.setattr(forest_batch, "TREES_IN_FLIGHT", lanes)
     got = fit_forest(vc, torch.from_numpy(y), **kw)
     sig = lambda r: [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]  # noqa: E731
     assert sig(got) == sig(ref)
 
 
 @pytest.mark.gpu
-def test_gpu_multi_tree_rf_batches_equal_single_tree_and_host(monkeypatch):
+def test_gpu_trees_in_flight_equal_single_tree_and_host(monkeypatch):
+    from fraud_detection_spark_kafka_llm_amd.models import forest_batch
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
 
     rng = np.random.default_rng(23)
@@ -482,10 +486,10 @@ def test_gpu_multi_tree_rf_batches_equal_single_tree_and_host(monkeypatch):
     vc = VectorColumn(F, dense=torch.from_numpy(dense.astype(np.float64)))
     kw = dict(num_trees=13, max_depth=5, max_bins=32, bootstrap=True, feature_subset="sqrt", seed=5)
     sig = lambda r: [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]  # noqa: E731
-    monkeypatch.setenv("FDX_RF_BATCH", "1")
+    monkeypatch.setattr(forest_batch, "TREES_IN_FLIGHT", 4)
     g = sig(fit_forest(vc, torch.from_numpy(y), device="cuda:0", **kw))
     h = sig(fit_forest(vc, torch.from_numpy(y), device="cpu", **kw))
-    monkeypatch.setenv("FDX_RF_BATCH", "0")
+    monkeypatch.setattr(forest_batch, "TREES_IN_FLIGHT", 1)
     g1 = sig(fit_forest(vc, torch.from_numpy(y), device="cuda:0", **kw))
     assert g == g1 == h
 
