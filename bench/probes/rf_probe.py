@@ -79,6 +79,16 @@ def main():
                 C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(), Q.h_row,
                                   Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, hist, Q.TB, grp.bt, ct, 1, mask)
 
+    def passes_sampled(mask, pack, ns, hist, listed=True):
+        s2n = torch.arange(ns, dtype=torch.int32, device=dev)
+        ct = pass_ct(1, ns)
+        for gi, grp in enumerate(groups):
+            if grp.num_items:
+                lst, cnt = ws.item_list(gi, grp) if listed else (None, None)
+                C.tree_hist_sampled(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
+                                    Q.h_row, Q.h_key, pack, ws.rowdig, Q.boff, Q.nbins, s2n, hist, Q.TB, grp.bt, ct,
+                                    mask, lst, cnt)
+
     for tree in [int(t) for t in args.trees.split(",")]:
         for d in range(args.depth):
             ns = 1 << d
@@ -92,20 +102,34 @@ def main():
                 act = np.array([m[a:a + b].any() for a, b in zip(f0, nf)], dtype=bool)
                 act_items += int(act.sum())
                 act_entries += int((en - st)[act].sum())
-            slot8 = None
+            slot8 = pack = None
             if d > 0:
                 rn = torch.from_numpy(rng.integers(0, ns, n).astype(np.int32)).to(dev)
                 node_slot = torch.arange(ns, dtype=torch.int32, device=dev)
                 C.tree_slot8(rn, node_slot, 0, ns, ws.slot8, None, None)
                 slot8 = ws.slot8
+                pack = ws.rowpack()
+                C.tree_slot_pack(rn, node_slot, ns, ws.rowdig, pack)
             hist = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)
-            ms = timed(lambda: passes(mask, slot8, ns, hist))
+            ms = timed(lambda: (hist.zero_(), passes(mask, slot8, ns, hist)))
+            hist2 = torch.zeros_like(hist)
+            ms_s = timed(lambda: (hist2.zero_(), passes_sampled(mask, pack, ns, hist2)))
+            same = bool(torch.equal(hist, hist2))
+            hist3 = torch.zeros_like(hist)
+            ms_p = timed(lambda: (hist3.zero_(), passes_sampled(mask, pack, ns, hist3, False)))
+            same = same and bool(torch.equal(hist, hist3))
             none = torch.zeros_like(mask)
             ms0 = timed(lambda: passes(none, slot8, ns, hist))
+            ms0_s = timed(lambda: passes_sampled(none, pack, ns, hist2))
             print(json.dumps({"tree": tree, "depth": d, "slots": ns, "sampled_feats": int(m.sum()),
                               "sampled_entries": int(colcnt[m].sum()), "active_items": act_items,
                               "active_item_entries": act_entries, "items_total": sum(len(i[0]) for i in items),
-                              "pass_ms": round(ms, 3), "empty_mask_ms": round(ms0, 3)}), flush=True)
+                              "pass_ms": round(ms, 3), "empty_mask_ms": round(ms0, 3),
+                              "sampled_pass_ms": round(ms_s, 3), "sampled_empty_ms": round(ms0_s, 3),
+                              "pack_only_ms": round(ms_p, 3),
+                              "equal": same}), flush=True)
+            if not same:
+                sys.exit("sampled pass differs from the build pass")
     for ns in (1, 16):
         slot8 = None
         if ns > 1:

@@ -12,6 +12,7 @@ namespace {
 
 using at::Tensor;
 using c10::optional;
+using c10::nullopt;
 
 #define FDX_CHECK(cond, msg) TORCH_CHECK(cond, "fdx.tree: ", msg)
 
@@ -194,11 +195,12 @@ void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64
   }
 }
 
-void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
-                const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
-                const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
-                const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np,
-                const optional<Tensor>& feat_active) {
+void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
+                     const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
+                     const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
+                     const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np,
+                     const optional<Tensor>& feat_active, const optional<Tensor>& rowpack,
+                     const optional<Tensor>& list, const optional<Tensor>& count) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
@@ -219,7 +221,8 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
   const int64_t spt = 16 / (2 * np);
   const int64_t nslots = slot_node.numel();
   FDX_CHECK(nslots >= 1 && nslots <= spt * ct, "slot_node must have 1 .. 16*ct/(2*np) entries");
-  FDX_CHECK(slot8_t || nslots == 1, "the root pass builds one slot");
+  FDX_CHECK(slot8_t || rowpack || nslots == 1, "the root pass builds one slot");
+  FDX_CHECK(!rowpack || np == 1, "packed row state: np = 1 passes");
   FDX_CHECK(csc_row.numel() == csc_key.numel(), "csc arrays");
   FDX_CHECK(rowdig.dim() == 2 && rowdig.size(1) == 2, "rowdig must be [N,2] int32");
   FDX_CHECK(reinterpret_cast<uintptr_t>(rowdig.data_ptr()) % 8 == 0, "rowdig must be 8-byte aligned");
@@ -259,12 +262,76 @@ void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& 
     FDX_CHECK(feat_active->numel() == nbins.numel(), "feat_active must be [Fa] uint8");
     a.feat_active = feat_active->data_ptr<uint8_t>();
   }
+  if (rowpack) {
+    chk(*rowpack, dev, at::kInt, "rowpack");
+    FDX_CHECK(rowpack->numel() == rowdig.size(0), "rowpack must be [N] int32");
+    a.rowpack = reinterpret_cast<const uint32_t*>(rowpack->data_ptr<int32_t>());
+  }
+  if (list) {
+    FDX_CHECK(count.has_value() && feat_active.has_value(), "a listed pass needs count and feat_active");
+    chk(*list, dev, at::kInt, "list");
+    chk(*count, dev, at::kInt, "count");
+    FDX_CHECK(list->numel() >= (wave_item ? wave_item->numel() : I) && count->numel() >= 2,
+              "list must hold every wave slot, count two int32 (count, cursor)");
+    a.active_list = list->data_ptr<int32_t>();
+    a.active_count = count->data_ptr<int32_t>();
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_hist(a, (int)bt, (int)ct, (int)np, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
     fdx::hist_cpu(a, (int)bt, (int)np);
+  }
+}
+
+void hist_build(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
+                const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
+                const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
+                const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np,
+                const optional<Tensor>& feat_active) {
+  hist_build_impl(item_start, item_end, item_f0, item_meta, wave_item, csc_row, csc_key, slot8_t, rowdig, boff, nbins,
+                  slot_node, hist, TB, bt, ct, np, feat_active, nullopt, nullopt, nullopt);
+}
+
+// RF count pass (np = 1) over the sampled features' work items: rowpack [N] int32 (tree_slot_pack;
+// None at the root: rowdig only), feat_active [Fa] u8, list [>= wave slots] / count [1] int32
+// scratch of the listed pass (the active items are compacted on the device, no host round trip;
+// None: one wave per wave slot).
+void hist_sampled(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
+                  const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
+                  const optional<Tensor>& rowpack, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
+                  const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct,
+                  const Tensor& feat_active, const optional<Tensor>& list, const optional<Tensor>& count) {
+  hist_build_impl(item_start, item_end, item_f0, item_meta, wave_item, csc_row, csc_key, nullopt, rowdig, boff, nbins,
+                  slot_node, hist, TB, bt, ct, 1, feat_active, rowpack, list, count);
+}
+
+// pack [N] int32 = slot (0xff: not built in this pass) | class-count digits << 8 (np = 1 passes)
+void slot_pack(const Tensor& row_node, const Tensor& node_slot, int64_t nslots, const Tensor& rowdig,
+               const Tensor& pack) {
+  const auto dev = row_node.device();
+  chk(row_node, dev, at::kInt, "row_node");
+  chk(node_slot, dev, at::kInt, "node_slot");
+  chk(rowdig, dev, at::kInt, "rowdig");
+  chk(pack, dev, at::kInt, "pack");
+  FDX_CHECK(nslots >= 0 && nslots <= 255, "at most 255 slots per pass");
+  FDX_CHECK(rowdig.numel() == 2 * row_node.numel() && pack.numel() == row_node.numel(),
+            "rowdig [N, 2], pack [N] int32");
+  fdx::SlotArgs a{};
+  a.row_node = row_node.data_ptr<int32_t>();
+  a.node_slot = node_slot.data_ptr<int32_t>();
+  a.num_nodes = (int32_t)node_slot.numel();
+  a.nslots = (int32_t)nslots;
+  a.N = row_node.numel();
+  a.rowdig = reinterpret_cast<const uint32_t*>(rowdig.data_ptr<int32_t>());
+  a.pack = reinterpret_cast<uint32_t*>(pack.data_ptr<int32_t>());
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_slot8(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::slot8_cpu(a);
   }
 }
 
@@ -1025,6 +1092,8 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_partition_cols", &partition_cols);
   m.def("tree_split_best", &split_best);
   m.def("tree_hist_build", &hist_build);
+  m.def("tree_hist_sampled", &hist_sampled);
+  m.def("tree_slot_pack", &slot_pack);
   m.def("tree_blk_build", &blk_build);
   m.def("tree_hist_blk", &hist_blk);
   m.def("tree_blk_gw", &blk_gw);

@@ -77,6 +77,7 @@ struct SlotArgs {
   uint8_t* slot8;             // [N] slot - slot_base, or 0xff
   const uint32_t* rowdig;     // optional (single-slot passes): rowdig [N * 2] ->
   uint32_t* masked;           //   masked [N * 2] = the row's digit words in slot 0, else 0
+  uint32_t* pack;             // optional (np = 1): pack [N] = slot | (rowdig[2r] & 0xff) << 8 | (rowdig[2r+1] & 0xff) << 16
 };
 
 // Work item meta (item_meta): stride_log2 | nfeat << 8 | koff << 16. The item covers keys
@@ -104,7 +105,13 @@ struct HistArgs {
   int64_t hist_stride;            // bins per histogram row (TB, or TB + 1 when padded)
   int64_t* hist;                  // [rows][hist_stride][2], accumulated (+=)
   const uint8_t* feat_active;     // [Fa] optional: items without an active feature are skipped (RF)
+  const uint32_t* rowpack;        // [N] optional, np = 1 passes: slot | digit0 << 8 | digit1 << 16 (slot8 unused)
+  int32_t* active_list;           // [num_slots] optional: listed pass (compacted active items) ...
+  int32_t* active_count;          //   ... [2]: their count (select kernel) and the waves' claim cursor
 };
+
+// waves of a listed histogram pass (they stride over the active items): 8 per SIMD of 256 CUs
+constexpr int32_t kListedWaves = 8192;
 
 // ------------------------------------------------------------------ row-blocked histogram engine
 // Blocked CSC ("BCSC", models/quantize.py build_blocked): the rows are cut into chunks of

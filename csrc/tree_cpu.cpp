@@ -64,7 +64,9 @@ void slot8_cpu(const SlotArgs& a) {
     for (int64_t r = lo; r < hi; ++r) {
       const int32_t node = a.row_node[r];
       const int32_t s = ((node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1) - a.slot_base;
-      a.slot8[r] = (s >= 0 && s < a.nslots) ? (uint8_t)s : (uint8_t)0xff;
+      const uint32_t sb = (s >= 0 && s < a.nslots) ? (uint32_t)s : 0xffu;
+      if (a.slot8) a.slot8[r] = (uint8_t)sb;
+      if (a.pack) a.pack[r] = sb | ((a.rowdig[2 * r] & 0xffu) << 8) | ((a.rowdig[2 * r + 1] & 0xffu) << 16);
       if (a.masked) {
         a.masked[2 * r] = s == 0 ? a.rowdig[2 * r] : 0u;
         a.masked[2 * r + 1] = s == 0 ? a.rowdig[2 * r + 1] : 0u;
@@ -103,7 +105,7 @@ void hist_cpu(const HistArgs& h, int bt, int np) {
       const int32_t f0 = h.item_f0[it];
       for (int64_t e = h.item_start[it]; e < h.item_end[it]; ++e) {
         const int64_t row = h.csc_row[e];
-        const int s = h.slot8 ? (int)h.slot8[row] : 0;
+        const int s = h.rowpack ? (int)(h.rowpack[row] & 0xffu) : h.slot8 ? (int)h.slot8[row] : 0;
         if (s >= h.nslots) continue;
         const int node = h.slot_node[s];
         const int key = h.csc_key[e];
@@ -113,8 +115,12 @@ void hist_cpu(const HistArgs& h, int bt, int np) {
         const int f = f0 + fl;
         if (b >= h.nbins[f]) continue;
         const uint32_t* d = h.rowdig + 2 * row;
-        const int64_t q0 = np == 1 ? undigits1(d[0]) : undigits4(d[0]);
-        const int64_t q1 = np == 1 ? undigits1(d[1]) : undigits4(d[1]);
+        int64_t q0 = np == 1 ? undigits1(d[0]) : undigits4(d[0]);
+        int64_t q1 = np == 1 ? undigits1(d[1]) : undigits4(d[1]);
+        if (h.rowpack) {
+          q0 = undigits1((h.rowpack[row] >> 8) & 0xffu);
+          q1 = undigits1((h.rowpack[row] >> 16) & 0xffu);
+        }
         int64_t* dst = h.hist + ((int64_t)node * h.hist_stride + h.boff[f] + b) * 2;
         __atomic_fetch_add(dst, q0, __ATOMIC_RELAXED);
         __atomic_fetch_add(dst + 1, q1, __ATOMIC_RELAXED);

@@ -90,9 +90,14 @@ __global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
     const int32_t node = a.row_node[r];
     const int32_t s = ((node >= 0 && node < a.num_nodes) ? a.node_slot[node] : -1) - a.slot_base;
-    a.slot8[r] = (s >= 0 && s < a.nslots) ? (uint8_t)s : (uint8_t)0xff;
+    const uint32_t sb = (s >= 0 && s < a.nslots) ? (uint32_t)s : 0xffu;
+    if (a.slot8) a.slot8[r] = (uint8_t)sb;
     if (a.masked)
       reinterpret_cast<uint2*>(a.masked)[r] = s == 0 ? reinterpret_cast<const uint2*>(a.rowdig)[r] : make_uint2(0u, 0u);
+    if (a.pack) {
+      const uint2 d = reinterpret_cast<const uint2*>(a.rowdig)[r];
+      a.pack[r] = sb | ((d.x & 0xffu) << 8) | ((d.y & 0xffu) << 16);
+    }
   }
 }
 
@@ -122,9 +127,18 @@ __device__ __forceinline__ void load_rows(const HistArgs& a, int64_t e, int64_t 
 }
 
 // slot byte of each of the 4 entries (0xff: outside the item or not in a node of this pass)
-template <bool ROOT>
+template <bool ROOT, bool PACK = false>
 __device__ __forceinline__ uint32_t entry_slots(const HistArgs& a, int4 r4) {
-  if constexpr (ROOT) {
+  if constexpr (PACK) {
+    // packed row state (np = 1 passes): the slot is byte 0 of the row's word
+    const uint32_t s0 = a.rowpack[r4.x >= 0 ? r4.x : 0] & 0xffu;
+    const uint32_t s1 = a.rowpack[r4.y >= 0 ? r4.y : 0] & 0xffu;
+    const uint32_t s2 = a.rowpack[r4.z >= 0 ? r4.z : 0] & 0xffu;
+    const uint32_t s3 = a.rowpack[r4.w >= 0 ? r4.w : 0] & 0xffu;
+    const uint32_t dead = (r4.x < 0 ? 0xffu : 0u) | (r4.y < 0 ? 0xff00u : 0u) | (r4.z < 0 ? 0xff0000u : 0u) |
+                          (r4.w < 0 ? 0xff000000u : 0u);
+    return (s0 | (s1 << 8) | (s2 << 16) | (s3 << 24)) | dead;
+  } else if constexpr (ROOT) {
     return (r4.x >= 0 ? 0u : 0xffu) | (r4.y >= 0 ? 0u : 0xff00u) | (r4.z >= 0 ? 0u : 0xff0000u) |
            (r4.w >= 0 ? 0u : 0xff000000u);
   } else {
@@ -158,6 +172,31 @@ __device__ __forceinline__ void gather_digits(const uint2* __restrict__ rd, int4
   }
 }
 
+// np = 1 passes over the packed row state (rowpack[r] = slot | digit0 << 8 | digit1 << 16): the
+// digits come from the word the slot was read from, one line per entry instead of two (slot byte
+// + 8-byte digit words); the second read of the word hits the cache.
+template <bool PACK>
+__device__ __forceinline__ void gather_entry_digits(const HistArgs& a, const uint2* __restrict__ rd, int4 r4,
+                                                    uint32_t slots4, uint32_t w[8]) {
+  if constexpr (PACK) {
+    const int32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool live = ((slots4 >> (8 * j)) & 0xffu) != 0xffu;
+      v[j] = a.rowpack[live ? rr[j] : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t m = ((slots4 >> (8 * j)) & 0xffu) != 0xffu ? 0xffu : 0u;
+      w[2 * j] = (v[j] >> 8) & m;
+      w[2 * j + 1] = (v[j] >> 16) & m;
+    }
+  } else {
+    gather_digits(rd, r4, slots4, w);
+  }
+}
+
 // ------------------------------------------------------------------ i8 MFMA histogram
 // One wave per work item; per step the wave takes 256 entries, 4 consecutive ones per lane (rows
 // int4, keys u32: single vector loads), with rows/keys of step i+3, slots of step i+2 and digits
@@ -175,7 +214,7 @@ __device__ __forceinline__ void gather_digits(const uint2* __restrict__ rd, int4
 // text-feature items, slower for the rest).
 // (Forcing 4 waves per SIMD on the CT = 8 pass -- 128 registers, 15 spilled -- measured no
 // faster than its 3 waves: profiles/r2s4/hist_REJECTED_w4_ab.txt)
-template <int BT, int CT, int NP, bool ROOT>
+template <int BT, int CT, int NP, bool ROOT, bool PACK = false>
 __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   constexpr int G = 4 * kWave;                 // entries per wave step
   constexpr int KS = 64;                       // entries per MFMA K-step
@@ -189,9 +228,24 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   const int wid = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
   const int wslot = blockIdx.x * 4 + wid;
-  const int item = a.wave_item ? a.wave_item[wslot] : wslot;
-  if (item < 0 || item >= a.num_items) return;
-  if (!item_active(a, item)) return;          // RF: no feature of the item is sampled at this level
+  // listed pass (RF): the waves of a fixed grid stride over the compacted list of active items;
+  // otherwise one wave per wave slot
+  const bool listed = a.active_list != nullptr;
+  const int n_listed = listed ? a.active_count[0] : 0;
+  // (claiming items through an atomic cursor instead: 8192 contended atomics cost ~0.2 ms a pass)
+  const int stride = (int)gridDim.x * 4;
+  int li = wslot;
+  for (bool once = true;; once = false, li += stride) {
+  int item;
+  if (listed) {
+    if (li >= n_listed) break;
+    item = a.active_list[li];
+  } else {
+    if (!once) break;
+    item = a.wave_item ? a.wave_item[wslot] : wslot;
+    if (item < 0 || item >= a.num_items) break;
+    if (!item_active(a, item)) break;          // RF: no feature of the item is sampled at this level
+  }
   const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
   const int32_t meta = a.item_meta[item];
   const int32_t f0 = a.item_f0[item];
@@ -216,10 +270,10 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
     RowStep g0;
     load_rows(a, first + 4 * lane, e0, e1, e_last, g0);
     load_rows(a, first + G + 4 * lane, e0, e1, e_last, g1);
-    sl0 = entry_slots<ROOT>(a, g0.rows());
+    sl0 = entry_slots<ROOT, PACK>(a, g0.rows());
     keys0 = g0.keys4;
-    sl1 = entry_slots<ROOT>(a, g1.rows());
-    gather_digits(rd, g0.rows(), sl0, w0);
+    sl1 = entry_slots<ROOT, PACK>(a, g1.rows());
+    gather_entry_digits<PACK>(a, rd, g0.rows(), sl0, w0);
     load_rows(a, first + 2 * G + 4 * lane, e0, e1, e_last, g2);
   }
   for (int64_t base = first; base < e1; base += G) {
@@ -228,8 +282,8 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) w[j] = w0[j];
     // digits of step i+1, slots of step i+2, rows of step i+3 (clamped, so unconditional)
-    gather_digits(rd, g1.rows(), sl1, w0);
-    const uint32_t sl2 = entry_slots<ROOT>(a, g2.rows());
+    gather_entry_digits<PACK>(a, rd, g1.rows(), sl1, w0);
+    const uint32_t sl2 = entry_slots<ROOT, PACK>(a, g2.rows());
     RowStep g3;
     load_rows(a, base + 3 * G + 4 * lane, e0, e1, e_last, g3);
     sl0 = sl1;
@@ -364,6 +418,24 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
           atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v);
         }
       }
+  }  // items of the wave
+}
+
+// Compacted list of the active work items of a listed pass, in wave-slot order per wave (one
+// atomic per wave: ballot + mbcnt for the positions inside it).
+__global__ __launch_bounds__(256) void hist_select_kernel(HistArgs a, int32_t* list, int32_t* count) {
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  int item = -1;
+  if (w < a.num_slots) item = a.wave_item ? a.wave_item[w] : w;
+  const bool act = item >= 0 && item < a.num_items && item_active(a, item);
+  const unsigned long long b = __ballot(act);
+  if (b == 0) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int first = __builtin_ctzll(b);
+  int base = 0;
+  if (lane == first) base = atomicAdd(count, __popcll(b));
+  base = __shfl(base, first, kWave);
+  if (act) list[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = item;
 }
 
 // ------------------------------------------------------------------ dense i8 MFMA histogram
@@ -689,11 +761,24 @@ void launch_slot8(const SlotArgs& a, hipStream_t s) {
 void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s) {
   if (a.num_items <= 0) return;
   const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
-  const dim3 grid((slots + 3) / 4), block(256);
-  const bool root = a.slot8 == nullptr;
+  dim3 grid((slots + 3) / 4);
+  const dim3 block(256);
+  const bool root = a.slot8 == nullptr && a.rowpack == nullptr;
+  if (a.active_list != nullptr) {
+    // listed pass: compact the active items, then a grid of at most kListedWaves waves strides
+    // over them (the full grid was ~300K wave slots, most of them exiting at once: ~100 us a pass)
+    HistArgs sel = a;
+    sel.num_slots = slots;
+    (void)hipMemsetAsync(const_cast<int32_t*>(a.active_count), 0, 2 * sizeof(int32_t), s);   // count, cursor
+    hipLaunchKernelGGL(hist_select_kernel, dim3((slots + 255) / 256), dim3(256), 0, s, sel,
+                       const_cast<int32_t*>(a.active_list), const_cast<int32_t*>(a.active_count));
+    const int32_t waves = slots < kListedWaves ? slots : kListedWaves;
+    grid = dim3((waves + 3) / 4);
+  }
 #define FDX_HIST_NP(B, C, P)                                                                             \
   if (np == P) {                                                                                        \
     if (root) hipLaunchKernelGGL((hist_i8_kernel<B, 1, P, true>), grid, block, 0, s, a);                \
+    else if (P == 1 && a.rowpack) hipLaunchKernelGGL((hist_i8_kernel<B, C, 1, false, true>), grid, block, 0, s, a); \
     else hipLaunchKernelGGL((hist_i8_kernel<B, C, P, false>), grid, block, 0, s, a);                    \
     return;                                                                                             \
   }

@@ -68,6 +68,10 @@ BLK_MAX_SLOTS = 4
 # histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
 ROWHIST = os.environ.get("FDX_ROWHIST", "1") == "1"
 RG_DBG = int(os.environ.get("FDX_RG_DBG", 0))   # diagnostics only (csrc/tree.h RgHistArgs::dbg)
+# RF passes over sampled features: packed row state (slot + class counts in one word per row) and
+# a device-compacted list of the active work items (tree_hist_sampled)
+SAMPLED = os.environ.get("FDX_RF_SAMPLED", "1") == "1"
+LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 
@@ -130,6 +134,25 @@ class Workspace:
             self.rg_work = torch.zeros(64 * (2 + nw), dtype=torch.int32, device=self.dev)
             self.rg_listdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
         return rg
+
+    def rowpack(self) -> torch.Tensor:
+        """[N] int32 packed row state of the sampled (RF) passes: slot | class-count digits << 8."""
+        if getattr(self, "_rowpack", None) is None:
+            self._rowpack = torch.empty(self.Q.n_rows, dtype=torch.int32, device=self.dev)
+        return self._rowpack
+
+    def item_list(self, gi: int, grp) -> tuple:
+        """(list, count) device scratch of a listed pass over item group ``gi`` (one per group: the
+        groups' passes run on concurrent streams)."""
+        lists = getattr(self, "_item_lists", None)
+        if lists is None:
+            lists = self._item_lists = {}
+        slots = grp.wave_order().numel()
+        cur = lists.get(gi)
+        if cur is None or cur[0].numel() < slots:
+            cur = lists[gi] = (torch.empty(slots, dtype=torch.int32, device=self.dev),
+                               torch.zeros(2, dtype=torch.int32, device=self.dev))
+        return cur
 
     def run_concurrent(self, launches: list) -> None:
         """Run the launches on HIST_STREAMS side streams joined back into the current stream
@@ -806,13 +829,16 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             slot8 = None
             csc_slot8, csc_dig = None, ws.rowdig
             rg = ws.rowgroups() if (not build_all and np_ == 4) else None
+            sampled = SAMPLED and build_all and np_ == 1
             if d > 0:
                 # a single built node: the CSC passes run the root kernel on digit words zeroed
                 # outside it (no per-entry slot gather, no compaction; zero rows add nothing)
                 single = n_build == 1 and rg is None
                 if single and getattr(ws, "rowdig_masked", None) is None:
                     ws.rowdig_masked = torch.empty_like(ws.rowdig)
-                if rg is None:          # (the row-group engine lists the built rows from row_node itself)
+                if rg is None and sampled and not single:
+                    C.tree_slot_pack(ws.row_node, st.node_slot, n_build, ws.rowdig, ws.rowpack())
+                elif rg is None:        # (the row-group engine lists the built rows from row_node itself)
                     C.tree_slot8(ws.row_node, st.node_slot, 0, n_build, ws.slot8, ws.rowdig if single else None,
                                  ws.rowdig_masked if single else None)
                 slot8 = ws.slot8
@@ -854,8 +880,19 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 sel_groups, use_dense = [], False
             if sel_groups is None:
                 sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
-            for grp in sel_groups:
+            for gi, grp in enumerate(sel_groups):
                 if grp.num_items == 0:
+                    continue
+                if sampled:
+                    pack = ws.rowpack() if (d > 0 and not single) else None
+                    # the listed pass wins while few items are active (<= 2 open nodes: ~0.16 vs
+                    # 0.19 ms at the root); with more, its fixed grid balances worse than a wave
+                    # per slot (profiles/r3s3/rf_probe_chunks.txt)
+                    lst, cnt = ws.item_list(gi, grp) if n_open <= LISTED_MAX_NODES else (None, None)
+                    launches.append(functools.partial(
+                        C.tree_hist_sampled, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta,
+                        grp.wave_order(), Q.h_row, Q.h_key, pack, csc_dig, h_boff, Q.nbins, s2n, hist_target, h_stride,
+                        grp.bt, ct, feat_mask, lst, cnt))
                     continue
                 launches.append(functools.partial(
                     C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),

@@ -207,6 +207,60 @@ def _hist_ref(Q, row_node, nslots, q0, q1):
     return ref
 
 
+def _sampled_vs_build(dev, nslots, root, seed=3):
+    """RF count passes over a random feature sample: tree_hist_sampled (packed row state, listed
+    active items) against tree_hist_build (slot bytes + digit words, every wave slot)."""
+    from fraud_detection_spark_kafka_llm_amd.models.grower import pass_ct
+
+    C = native.lib()
+    rng = np.random.default_rng(seed)
+    n, F = 3000, 700
+    vc = vc_from_dense(random_counts_matrix(n, F, 0.03, seed)[0])
+    Q = quantize(vc.to(dev), max_bins=32, **QKW)
+    ws = Workspace(Q)
+    lab = torch.from_numpy((np.arange(n) % 3 == 0).astype(np.float32)).to(dev)
+    C.tree_quant(None, None, lab, None, 5, 2, True, 1, 1, None, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
+    row_node = torch.from_numpy(rng.integers(0, nslots + 2, n).astype(np.int32)).to(dev)
+    node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
+    node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
+    node_slot = node_slot.to(dev)
+    mask = torch.from_numpy((rng.random(Q.Fa) < 0.2).astype(np.uint8)).to(dev)
+    s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
+    ct = pass_ct(1, nslots)
+    ref = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
+    got = torch.zeros_like(ref)
+    slot8 = pack = None
+    if not root:
+        C.tree_slot8(row_node, node_slot, 0, nslots, ws.slot8, None, None)
+        slot8 = ws.slot8
+        pack = ws.rowpack()
+        C.tree_slot_pack(row_node, node_slot, nslots, ws.rowdig, pack)
+    for gi, grp in enumerate(Q.groups + Q.hot_groups):
+        if grp.num_items == 0:
+            continue
+        C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(), Q.h_row,
+                          Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, ref, Q.TB, grp.bt, ct, 1, mask)
+        lst, cnt = ws.item_list(gi, grp)
+        C.tree_hist_sampled(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(), Q.h_row,
+                            Q.h_key, pack, ws.rowdig, Q.boff, Q.nbins, s2n, got, Q.TB, grp.bt, ct, mask, lst, cnt)
+    assert int(ref.abs().sum()) > 0
+    return ref.cpu(), got.cpu()
+
+
+@pytest.mark.parametrize("nslots,root", [(1, True), (3, False), (16, False)])
+def test_sampled_rf_pass_equals_build_pass(nslots, root):
+    ref, got = _sampled_vs_build("cpu", nslots, root)
+    assert torch.equal(ref, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nslots,root", [(1, True), (3, False), (16, False)])
+def test_gpu_sampled_rf_pass_equals_build_pass_and_host(nslots, root):
+    ref, got = _sampled_vs_build("cuda:0", nslots, root)
+    href, _ = _sampled_vs_build("cpu", nslots, root)
+    assert torch.equal(ref, got) and torch.equal(got, href)
+
+
 def test_work_items_cover_histogram_csc_once_and_wave_order_is_xcd_grouped():
     """The histogram CSC holds every entry of the non-dense features once, super-block-major;
     every entry belongs to exactly one item; packed items hold consecutive small features with
