@@ -39,27 +39,13 @@ const Names& names() {
   return *n;
 }
 
-PyObject* call0(PyObject* o, PyObject* name) { return PyObject_CallMethodObjArgs(o, name, nullptr); }
-
-// bytes / bytearray / str / None -> appended to buf; returns false for None
-bool append_bytes(PyObject* v, std::vector<uint8_t>& buf) {
-  if (v == Py_None) return false;
-  char* p = nullptr;
-  Py_ssize_t n = 0;
-  if (PyBytes_Check(v)) {
-    PyBytes_AsStringAndSize(v, &p, &n);
-  } else if (PyUnicode_Check(v)) {
-    p = const_cast<char*>(PyUnicode_AsUTF8AndSize(v, &n));
-    if (!p) throw py::error_already_set();
-  } else if (PyByteArray_Check(v)) {
-    p = PyByteArray_AsString(v);
-    n = PyByteArray_Size(v);
-  } else {
-    throw py::type_error("message key/value must be bytes, str or None");
-  }
-  buf.insert(buf.end(), reinterpret_cast<uint8_t*>(p), reinterpret_cast<uint8_t*>(p) + n);
-  return true;
+PyObject* call0(PyObject* o, PyObject* name) {
+  return PyObject_VectorcallMethod(name, &o, 1 | PY_VECTORCALL_ARGUMENTS_OFFSET, nullptr);
 }
+
+// the in-memory broker's Message class (a 7-tuple: topic, partition, offset, key, value, error,
+// timestamp ms), registered by install_message_accessors: pack_messages reads its items directly
+PyTypeObject* g_message_type = nullptr;
 
 template <class T>
 py::array_t<T> to_array(const std::vector<T>& v) {
@@ -68,37 +54,60 @@ py::array_t<T> to_array(const std::vector<T>& v) {
   return a;
 }
 
+// bytes / bytearray / str -> (pointer, size); None -> (nullptr, -1)
+std::pair<const char*, Py_ssize_t> byte_view(PyObject* v) {
+  if (v == Py_None) return {nullptr, -1};
+  if (PyBytes_Check(v)) return {PyBytes_AS_STRING(v), PyBytes_GET_SIZE(v)};
+  if (PyByteArray_Check(v)) return {PyByteArray_AS_STRING(v), PyByteArray_GET_SIZE(v)};
+  if (PyUnicode_Check(v)) {
+    Py_ssize_t n = 0;
+    const char* p = PyUnicode_AsUTF8AndSize(v, &n);
+    if (!p) throw py::error_already_set();
+    return {p, n};
+  }
+  throw py::type_error("message key/value must be bytes, str or None");
+}
+
 // -> (part_of int32[n], parts [(topic, partition)], keys u8, key_off i64[n+1], null_keys u8[n],
 //     values u8, val_off i64[n+1], offsets i64[n], ts_ms i64[n], errors [(index, error)])
-// over the messages without an error; n counts those.
-py::tuple pack_messages(py::list msgs) {
+// over the messages without an error; n counts those. Two passes: the first reads every
+// message's fields (the in-memory broker's Message items directly, other classes through their
+// methods) and sizes the buffers, the second copies the bytes once into the final arrays (a
+// growing vector plus a copy into numpy faulted in ~64 MB of fresh pages per 16K 2-KB records).
+py::tuple pack_messages(py::list msgs, py::object vals_buf) {
   const Names& N = names();
   const Py_ssize_t m = PyList_GET_SIZE(msgs.ptr());
+  struct Rec {
+    PyObject* k;
+    PyObject* v;
+    int64_t off, ts;
+  };
+  std::vector<Rec> recs;
+  std::vector<py::object> hold;          // references owned here (fields read through methods)
   std::vector<int32_t> part_of;
   std::vector<std::pair<std::string, int64_t>> parts;
   py::list parts_out, errors;
-  std::vector<uint8_t> keys, vals, nulls;
-  std::vector<int64_t> koff{0}, voff{0}, offs, ts;
+  recs.reserve(m);
   part_of.reserve(m);
-  offs.reserve(m);
-  ts.reserve(m);
-  koff.reserve(m + 1);
-  voff.reserve(m + 1);
-  nulls.reserve(m);
   std::string last_topic;
   py::object last_topic_obj;
   int64_t last_part = -1;
   int32_t last_idx = -1;
+  size_t kbytes = 0, vbytes = 0;
   for (Py_ssize_t i = 0; i < m; ++i) {
     PyObject* msg = PyList_GET_ITEM(msgs.ptr(), i);
-    py::object err = py::reinterpret_steal<py::object>(call0(msg, N.error));
+    const bool direct = g_message_type && Py_TYPE(msg) == g_message_type && PyTuple_GET_SIZE(msg) == 7;
+    py::object err = direct ? py::reinterpret_borrow<py::object>(PyTuple_GET_ITEM(msg, 5))
+                            : py::reinterpret_steal<py::object>(call0(msg, N.error));
     if (!err) throw py::error_already_set();
     if (!err.is_none()) {
       errors.append(py::make_tuple(i, err));
       continue;
     }
-    py::object t = py::reinterpret_steal<py::object>(call0(msg, N.topic));
-    py::object p = py::reinterpret_steal<py::object>(call0(msg, N.partition));
+    py::object t = direct ? py::reinterpret_borrow<py::object>(PyTuple_GET_ITEM(msg, 0))
+                          : py::reinterpret_steal<py::object>(call0(msg, N.topic));
+    py::object p = direct ? py::reinterpret_borrow<py::object>(PyTuple_GET_ITEM(msg, 1))
+                          : py::reinterpret_steal<py::object>(call0(msg, N.partition));
     if (!t || !p) throw py::error_already_set();
     const int64_t part = p.cast<int64_t>();
     // consecutive messages share the topic object: compare it before converting the string
@@ -118,26 +127,67 @@ py::tuple pack_messages(py::list msgs) {
       last_part = part;
     }
     part_of.push_back(last_idx);
-    py::object k = py::reinterpret_steal<py::object>(call0(msg, N.key));
-    py::object v = py::reinterpret_steal<py::object>(call0(msg, N.value));
-    py::object o = py::reinterpret_steal<py::object>(call0(msg, N.offset));
-    py::object ts_obj = py::reinterpret_steal<py::object>(call0(msg, N.timestamp));
-    if (!k || !v || !o || !ts_obj) throw py::error_already_set();
-    nulls.push_back(append_bytes(k.ptr(), keys) ? 0 : 1);
-    koff.push_back((int64_t)keys.size());
-    append_bytes(v.ptr(), vals);
-    voff.push_back((int64_t)vals.size());
-    offs.push_back(o.cast<int64_t>());
-    int64_t tms = -1;
-    if (PyTuple_Check(ts_obj.ptr()) && PyTuple_GET_SIZE(ts_obj.ptr()) == 2) {
-      const long kind = PyLong_AsLong(PyTuple_GET_ITEM(ts_obj.ptr(), 0));
-      if (kind != 0) tms = PyLong_AsLongLong(PyTuple_GET_ITEM(ts_obj.ptr(), 1));
+    Rec r{};
+    if (direct) {                 // borrowed items of the in-memory Message (the list keeps them)
+      PyObject* ts_item = PyTuple_GET_ITEM(msg, 6);
+      r.k = PyTuple_GET_ITEM(msg, 3);
+      r.v = PyTuple_GET_ITEM(msg, 4);
+      r.off = (int64_t)PyLong_AsLongLong(PyTuple_GET_ITEM(msg, 2));
+      r.ts = ts_item == Py_None ? -1 : (int64_t)PyLong_AsLongLong(ts_item);
       if (PyErr_Occurred()) throw py::error_already_set();
+    } else {
+      py::object k = py::reinterpret_steal<py::object>(call0(msg, N.key));
+      py::object v = py::reinterpret_steal<py::object>(call0(msg, N.value));
+      py::object o = py::reinterpret_steal<py::object>(call0(msg, N.offset));
+      py::object ts_obj = py::reinterpret_steal<py::object>(call0(msg, N.timestamp));
+      if (!k || !v || !o || !ts_obj) throw py::error_already_set();
+      r.k = k.ptr();
+      r.v = v.ptr();
+      r.off = o.cast<int64_t>();
+      r.ts = -1;
+      if (PyTuple_Check(ts_obj.ptr()) && PyTuple_GET_SIZE(ts_obj.ptr()) == 2) {
+        const long kind = PyLong_AsLong(PyTuple_GET_ITEM(ts_obj.ptr(), 0));
+        if (kind != 0) r.ts = PyLong_AsLongLong(PyTuple_GET_ITEM(ts_obj.ptr(), 1));
+        if (PyErr_Occurred()) throw py::error_already_set();
+      }
+      hold.push_back(std::move(k));
+      hold.push_back(std::move(v));
     }
-    ts.push_back(tms);
+    const auto kv = byte_view(r.k), vv = byte_view(r.v);
+    kbytes += kv.second > 0 ? (size_t)kv.second : 0;
+    vbytes += vv.second > 0 ? (size_t)vv.second : 0;
+    recs.push_back(r);
   }
-  return py::make_tuple(to_array(part_of), parts_out, to_array(keys), to_array(koff), to_array(nulls), to_array(vals),
-                        to_array(voff), to_array(offs), to_array(ts), errors);
+  const py::ssize_t n = (py::ssize_t)recs.size();
+  py::array_t<uint8_t> keys((py::ssize_t)kbytes), nulls(n);
+  // values: into the caller's reusable buffer when it is large enough (a view of it is returned;
+  // fresh 32-MB arrays are page-faulted in on every batch), else a new array
+  bool reuse = false;
+  py::array_t<uint8_t, py::array::c_style> given;
+  if (!vals_buf.is_none()) {
+    given = py::array_t<uint8_t, py::array::c_style>::ensure(vals_buf);
+    if (!given) throw py::type_error("vals_buf must be a contiguous uint8 array");
+    reuse = (size_t)given.size() >= vbytes && given.writeable();
+  }
+  py::array_t<uint8_t> vals = reuse ? py::array_t<uint8_t>(given) : py::array_t<uint8_t>((py::ssize_t)vbytes);
+  py::array_t<int64_t> koff(n + 1), voff(n + 1), offs(n), ts(n);
+  uint8_t *kp = keys.mutable_data(), *vp = vals.mutable_data(), *np_ = nulls.mutable_data();
+  int64_t *ko = koff.mutable_data(), *vo = voff.mutable_data(), *op = offs.mutable_data(), *tp = ts.mutable_data();
+  size_t kpos = 0, vpos = 0;
+  ko[0] = vo[0] = 0;
+  for (py::ssize_t i = 0; i < n; ++i) {
+    const auto kv = byte_view(recs[i].k), vv = byte_view(recs[i].v);
+    np_[i] = kv.first ? 0 : 1;
+    if (kv.second > 0) std::memcpy(kp + kpos, kv.first, (size_t)kv.second), kpos += (size_t)kv.second;
+    if (vv.second > 0) std::memcpy(vp + vpos, vv.first, (size_t)vv.second), vpos += (size_t)vv.second;
+    ko[i + 1] = (int64_t)kpos;
+    vo[i + 1] = (int64_t)vpos;
+    op[i] = recs[i].off;
+    tp[i] = recs[i].ts;
+  }
+  py::object vals_out = (size_t)vals.size() == vbytes ? py::object(vals)
+                                                       : vals[py::slice(0, (py::ssize_t)vbytes, 1)];
+  return py::make_tuple(to_array(part_of), parts_out, keys, koff, nulls, vals_out, voff, offs, ts, errors);
 }
 
 // producer.produce(topic, value=v_i, key=k_i, on_delivery=cb) for the n records of one segment
@@ -294,6 +344,8 @@ void install_message_accessors(py::object cls) {
     }
     Py_DECREF(descr);
   }
+  g_message_type = reinterpret_cast<PyTypeObject*>(cls.ptr());
+  Py_INCREF(cls.ptr());          // kept for the process lifetime
 }
 
 PyObject* new_message(PyObject* cls, PyObject* topic, PyObject* part, PyObject* off, PyObject* key, PyObject* value,
@@ -510,7 +562,16 @@ PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs,
   Py_XDECREF(size);
   Py_DECREF(parts);
   if (!ok || !rel) return nullptr;
-  if (cb != Py_None) {
+  if (cb != Py_None && Py_TYPE(cb) == &DeliveryCounterType) {
+    // a DeliveryCounter ignores the report's Message: queue (cb, None, None), no Message built
+    PyObject* item = PyTuple_Pack(3, cb, Py_None, Py_None);
+    if (item && PyObject_GC_IsTracked(item)) PyObject_GC_UnTrack(item);
+    PyObject* pend = item ? PyObject_GetAttr(producer, F.pending) : nullptr;
+    const int rc = pend ? PyList_Append(pend, item) : -1;
+    Py_XDECREF(pend);
+    Py_XDECREF(item);
+    if (rc < 0) return nullptr;
+  } else if (cb != Py_None) {
     struct timespec ts;
     clock_gettime(CLOCK_REALTIME, &ts);
     PyObject* tms = PyLong_FromLongLong((long long)ts.tv_sec * 1000 + ts.tv_nsec / 1000000);
@@ -536,6 +597,21 @@ PyObject* fast_produce(PyObject* state, PyObject* const* args, Py_ssize_t nargs,
   Py_RETURN_NONE;
 }
 
+// cb(err, what) for every (cb, err, what) of a producer's pending delivery reports, in order
+// (the in-memory producer's poll loop, without a bytecode iteration per record)
+int64_t deliver_reports(py::list pend) {
+  const Py_ssize_t n = PyList_GET_SIZE(pend.ptr());
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* it = PyList_GET_ITEM(pend.ptr(), i);
+    if (!PyTuple_Check(it) || PyTuple_GET_SIZE(it) != 3) throw py::type_error("pending report must be (cb, err, what)");
+    PyObject* args[2] = {PyTuple_GET_ITEM(it, 1), PyTuple_GET_ITEM(it, 2)};
+    PyObject* r = PyObject_Vectorcall(PyTuple_GET_ITEM(it, 0), args, 2, nullptr);
+    if (!r) throw py::error_already_set();
+    Py_DECREF(r);
+  }
+  return n;
+}
+
 PyMethodDef fast_produce_def = {"produce", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(fast_produce)),
                                 METH_FASTCALL | METH_KEYWORDS, "in-memory broker produce (C)"};
 
@@ -551,11 +627,13 @@ py::object make_fast_produce(py::object producer, py::object broker, py::object 
 }  // namespace
 
 void register_kafka_ops(pybind11::module& m) {
-  m.def("pack_messages", &pack_messages, "consumed Message list -> columnar buffers (one pass, C loop)");
+  m.def("pack_messages", &pack_messages, "consumed Message list -> columnar buffers (C loops)", py::arg("msgs"),
+        py::arg("vals_buf") = py::none());
   m.def("produce_each", &produce_each, "per-record produce of one output segment from a C loop");
   m.def("install_message_accessors", &install_message_accessors, "C method descriptors on a tuple Message class");
   m.def("build_messages", &build_messages, "columnar batch -> list of Message (C loop)");
   m.def("make_fast_produce", &make_fast_produce, "C produce bound to an in-memory producer");
+  m.def("deliver_reports", &deliver_reports, "run (cb, err, what) delivery reports in order (C loop)");
   if (PyType_Ready(&DeliveryCounterType) < 0) throw py::error_already_set();
   Py_INCREF(&DeliveryCounterType);
   m.add_object("DeliveryCounter", py::reinterpret_borrow<py::object>(reinterpret_cast<PyObject*>(&DeliveryCounterType)));

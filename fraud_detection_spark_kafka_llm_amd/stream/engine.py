@@ -272,7 +272,8 @@ class _Reader(threading.Thread):
         eng = self.eng
         want = eng._claim(want)
         if want == 0:
-            time.sleep(0.0005)        # another reader holds the remaining quota
+            if not eng._inline_on:
+                time.sleep(0.0005)    # another reader holds the remaining quota
             return
         if eng._quota is not None:    # never hold a reservation across a blocking wait
             timeout = 0
@@ -299,7 +300,7 @@ class _Reader(threading.Thread):
                 got += sum(pc.rb.n for pc in pieces)
         finally:
             eng._settle(want, got)
-        if not got and timeout == 0:
+        if not got and timeout == 0 and not eng._inline_on:
             time.sleep(0.001)
         if got:
             eng._last_read = time.time()
@@ -312,12 +313,17 @@ class _Reader(threading.Thread):
         placed: list = []
         deadline = None
         slot.offsets[0] = 0
+        polled = False
         while n < cap_d:
             if not self.carry:
                 now = time.time()
                 if (deadline is not None and now >= deadline) or eng._readers_stop.is_set() or eng._quota_done():
                     break
-                self._poll(cap_d - n, eng.poll_s if deadline is None else deadline - now)
+                if polled and deadline is None and eng._inline_on:
+                    break                 # inline: nothing arrived, back to the engine loop
+                polled = True
+                first = eng.poll_s if not eng._inline_busy() else 0.0005
+                self._poll(cap_d - n, first if deadline is None else deadline - now)
                 continue
             pc = self.carry.popleft()
             k = min(pc.rb.n, cap_d - n)
@@ -432,6 +438,12 @@ class StreamingEngine:
         self._quota: Optional[int] = None
         self._claimed = 0
         self._last_read = time.time()
+        # partition readers run on the engine thread itself (no reader threads) for per-record
+        # (confluent-surface) consumers: their work holds the GIL, so threads only convoy on it.
+        # None: inline exactly when no consumer has the columnar consume_batches.
+        env = os.environ.get("FDX_STREAM_INLINE", "")
+        self.inline = None if env == "" else env == "1"
+        self._inline_on = False
         self._pool = cf.ThreadPoolExecutor(max_workers=8) if explain == "async" else None
         self._explain_pending = 0
         self._seen = 0
@@ -482,6 +494,10 @@ class StreamingEngine:
         with self._lock:
             return self._quota is not None and self._quota <= 0 and self._claimed == 0
 
+    def _inline_busy(self) -> bool:
+        """Inline readers with micro-batches in flight: poll briefly, results are waiting."""
+        return self._inline_on and self.scorer.inflight > 0
+
     def _count(self, name: str, k: int) -> None:
         with self._lock:
             setattr(self.stats, name, getattr(self.stats, name) + k)
@@ -499,13 +515,27 @@ class StreamingEngine:
         self._readers_stop.clear()
         self._last_read = time.time()
         readers = [_Reader(self, i, c) for i, c in enumerate(self.consumers)]
-        for r in readers:
-            r.start()
+        inline = self.inline if self.inline is not None else not any(r.columnar for r in readers)
+        self._inline_on = inline
+        if not inline:
+            for r in readers:
+                r.start()
+        rr = 0
         try:
             while True:
                 if self._reader_error is not None:
                     raise self._reader_error
-                slot = self.ring.acquire_full(timeout=0.0005 if self.scorer.inflight else 0.005)
+                if inline and self.scorer.inflight < self.scorer.depth:
+                    # one slot from the next partition reader, on this thread
+                    free = self.ring.acquire_free(timeout=0)
+                    if free is not None:
+                        r = readers[rr]
+                        rr = (rr + 1) % len(readers)
+                        if r._fill(free):
+                            self.ring.publish(free)
+                        else:
+                            self.ring.release(free)
+                slot = self.ring.acquire_full(timeout=0 if inline else (0.0005 if self.scorer.inflight else 0.005))
                 if slot is not None:
                     while self.scorer.inflight >= self.scorer.depth:
                         self._finish_one()
@@ -516,14 +546,16 @@ class StreamingEngine:
                 if slot is None and not self.scorer.inflight:
                     if self._stop.is_set():
                         break
-                    alive = any(r.is_alive() for r in readers)
+                    alive = (not self._quota_done() or any(r.carry for r in readers)) if inline else \
+                        any(r.is_alive() for r in readers)
                     if not alive or time.time() - self._last_read > max(idle_timeout_s, 2 * self.max_latency_s):
                         if self.ring._full.empty():
                             break
         finally:
             self._readers_stop.set()
             for r in readers:
-                r.join(timeout=10.0)
+                if r.is_alive():
+                    r.join(timeout=10.0)
             while True:                                  # slots the readers published while stopping
                 slot = self.ring.acquire_full(timeout=0)
                 if slot is None:

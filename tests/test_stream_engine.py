@@ -86,10 +86,13 @@ def test_partition_readers_commit_only_delivered(agent, monkeypatch):
     assert recs[b"k0"]["prediction"] == 1.0 and recs[b"k0"]["original_text"] == fixtures.SCAM_SAMPLE
 
 
-def test_confluent_surface_clients_take_the_per_record_path(agent, monkeypatch):
+@pytest.mark.parametrize("inline", ["", "0"])
+def test_confluent_surface_clients_take_the_per_record_path(agent, monkeypatch, inline):
     """FDX_KAFKA_COLUMNAR=0: clients expose only the confluent_kafka API (per-record Messages and
-    produce calls) — the path a librdkafka client takes (native pack_messages / produce_each)."""
-    url = "memory://confluent-surface"
+    produce calls) — the path a librdkafka client takes (native pack_messages / produce_each).
+    Default: the partition reader runs on the engine thread (inline); "0": reader threads."""
+    monkeypatch.setenv("FDX_STREAM_INLINE", inline)
+    url = "memory://confluent-surface" + inline
     texts = [fixtures.SCAM_SAMPLE, fixtures.BENIGN_SAMPLE, "hello there"] * 40
     broker = _fill(url, "in", texts)
     nullkey = fake_kafka.Producer({"bootstrap.servers": url})
@@ -127,8 +130,10 @@ def test_failed_delivery_blocks_that_partitions_commit(agent):
     assert c.committed_offsets().get(("in", 0), 0) == 0
 
 
-def test_slot_overflow_is_carried_over_not_lost(agent):
-    url = "memory://overflow"
+@pytest.mark.parametrize("inline", ["", "1"])
+def test_slot_overflow_is_carried_over_not_lost(agent, monkeypatch, inline):
+    monkeypatch.setenv("FDX_STREAM_INLINE", inline)
+    url = "memory://overflow" + inline
     texts = [("word " * 150)[:700] + str(i) for i in range(40)] + ["x" * 5000]
     broker = _fill(url, "in", texts, parts=1)
     c = fake_kafka.Consumer(_conf(url))
@@ -191,3 +196,49 @@ def test_latency_histogram_percentiles():
     h.add(np.linspace(1.0, 100.0, 10000))
     assert h.percentile(50) == pytest.approx(50.5, rel=0.02)
     assert h.percentile(95) == pytest.approx(95.05, rel=0.02)
+
+
+def test_pack_messages_reads_any_message_class_and_reuses_buffers():
+    """pack_messages: the in-memory Message's items directly, any other class through its methods
+    (as cimpl.Message), errors listed apart; values into a caller buffer when it is large enough."""
+    from fraud_detection_spark_kafka_llm_amd.ops import native
+
+    class Msg:                                    # method surface only (like confluent_kafka's)
+        def __init__(self, t, p, o, k, v, err=None):
+            self._f = (t, p, o, k, v, err)
+
+        def topic(self):
+            return self._f[0]
+
+        def partition(self):
+            return self._f[1]
+
+        def offset(self):
+            return self._f[2]
+
+        def key(self):
+            return self._f[3]
+
+        def value(self):
+            return self._f[4]
+
+        def error(self):
+            return self._f[5]
+
+        def timestamp(self):
+            return (1, 1234)
+
+    fake_kafka._native()                          # registers the in-memory Message class
+    a = tuple.__new__(fake_kafka.Message, ("t", 0, 5, b"k1", b"value-one", None, 99))     # ts in ms
+    b = Msg("t", 0, 6, None, b"v2")
+    e = Msg("t", 0, -1, None, None, err=fake_kafka.KafkaError(1, "boom"))
+    c = tuple.__new__(fake_kafka.Message, ("t", 1, 7, b"k3", b"third", None, None))
+    for buf in (None, np.zeros(64, dtype=np.uint8), np.zeros(3, dtype=np.uint8)):
+        part_of, parts, kb, ko, nk, vb, vo, offs, ts, errs = native.lib().pack_messages([a, b, e, c], buf)
+        assert [tuple(x) for x in parts] == [("t", 0), ("t", 1)] and part_of.tolist() == [0, 0, 1]
+        assert bytes(vb) == b"value-onev2third" and vo.tolist() == [0, 9, 11, 16]
+        assert bytes(kb) == b"k1k3" and ko.tolist() == [0, 2, 2, 4] and nk.tolist() == [0, 1, 0]
+        assert offs.tolist() == [5, 6, 7] and ts.tolist() == [99, 1234, -1]
+        assert [i for i, _ in errs] == [2]
+        if buf is not None and buf.size >= 16:
+            assert bytes(buf[:16]) == b"value-onev2third"      # written in place
