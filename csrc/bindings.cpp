@@ -536,6 +536,35 @@ int64_t extract_json_field(const Tensor& in, const Tensor& in_off, const std::st
                                  status.data_ptr<int32_t>(), (int)threads);
 }
 
+// extract_json_field over a list of separate values (bytes / None) without packing
+// them into one buffer first: the buffers are located with the GIL held, read without it.
+int64_t extract_json_field_refs(pybind11::list values, int64_t count, const std::string& field, const Tensor& out,
+                                const Tensor& out_off, const Tensor& status, int64_t threads) {
+  for (const Tensor* t : {&out, &out_off, &status})
+    FDX_CHECK(!t->is_cuda() && t->is_contiguous(), "json extraction runs on host tensors");
+  FDX_CHECK(out.scalar_type() == at::kByte && out_off.scalar_type() == at::kLong && status.scalar_type() == at::kInt,
+            "dtypes u8/i64/i32");
+  const int64_t n = count;
+  FDX_CHECK(n >= 0 && n <= (int64_t)PyList_GET_SIZE(values.ptr()), "count exceeds the list");
+  FDX_CHECK(out_off.numel() >= n + 1 && status.numel() >= n, "offset/status sizes");
+  std::vector<const uint8_t*> begin((size_t)n, nullptr);
+  std::vector<int64_t> len((size_t)n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    PyObject* v = PyList_GET_ITEM(values.ptr(), i);
+    if (PyBytes_Check(v)) {
+      begin[i] = reinterpret_cast<const uint8_t*>(PyBytes_AS_STRING(v));
+      len[i] = PyBytes_GET_SIZE(v);
+    } else if (v != Py_None) {   // (immutable bytes only: read with the GIL released)
+      throw pybind11::type_error("values must be bytes or None");
+    }
+  }
+  // the list (held by the caller) keeps every buffer alive while the GIL is released
+  pybind11::gil_scoped_release nogil;
+  return fdx::extract_json_field_ptrs(begin.data(), len.data(), n, reinterpret_cast<const uint8_t*>(field.data()),
+                                      (int64_t)field.size(), out.data_ptr<uint8_t>(), out.numel(),
+                                      out_off.data_ptr<int64_t>(), status.data_ptr<int32_t>(), (int)threads);
+}
+
 }  // namespace
 
 void register_tree_ops(pybind11::module& m);
@@ -558,5 +587,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("feature_order", &feature_order, "CSR -> CSC by feature (radix sort), docFreq and max count per feature");
   m.def("encode_records", &encode_records, "json.dumps-identical classification records (batch)");
   m.def("extract_json_field", &extract_json_field, "Bulk JSON string-field extraction into a packed buffer");
+  m.def("extract_json_field_refs", &extract_json_field_refs,
+        "extract_json_field over the first count values of a list of bytes (no packing copy)");
   m.attr("gfx_arch") = "gfx950";
 }

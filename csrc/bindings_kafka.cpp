@@ -70,11 +70,13 @@ std::pair<const char*, Py_ssize_t> byte_view(PyObject* v) {
 
 // -> (part_of int32[n], parts [(topic, partition)], keys u8, key_off i64[n+1], null_keys u8[n],
 //     values u8, val_off i64[n+1], offsets i64[n], ts_ms i64[n], errors [(index, error)])
-// over the messages without an error; n counts those. Two passes: the first reads every
+// over the messages without an error; n counts those. by_ref: values is a list of the messages'
+// value objects (val_off still counts their bytes), for a consumer that reads them in place
+// (extract_json_field_refs) instead of packing them. Two passes: the first reads every
 // message's fields (the in-memory broker's Message items directly, other classes through their
 // methods) and sizes the buffers, the second copies the bytes once into the final arrays (a
 // growing vector plus a copy into numpy faulted in ~64 MB of fresh pages per 16K 2-KB records).
-py::tuple pack_messages(py::list msgs, py::object vals_buf) {
+py::tuple pack_messages(py::list msgs, py::object vals_buf, bool by_ref) {
   const Names& N = names();
   const Py_ssize_t m = PyList_GET_SIZE(msgs.ptr());
   struct Rec {
@@ -160,6 +162,17 @@ py::tuple pack_messages(py::list msgs, py::object vals_buf) {
   }
   const py::ssize_t n = (py::ssize_t)recs.size();
   py::array_t<uint8_t> keys((py::ssize_t)kbytes), nulls(n);
+  py::list refs;
+  if (by_ref) {                  // values stay in their own bytes objects: a list of references
+    refs = py::list(n);
+    for (py::ssize_t i = 0; i < n; ++i) {
+      PyObject* v = recs[i].v;
+      if (v != Py_None && !PyBytes_Check(v)) throw py::type_error("by_ref: message values must be bytes or None");
+      Py_INCREF(v);
+      PyList_SET_ITEM(refs.ptr(), i, v);
+    }
+    vbytes = 0;
+  }
   // values: into the caller's reusable buffer when it is large enough (a view of it is returned;
   // fresh 32-MB arrays are page-faulted in on every batch), else a new array
   bool reuse = false;
@@ -179,13 +192,17 @@ py::tuple pack_messages(py::list msgs, py::object vals_buf) {
     const auto kv = byte_view(recs[i].k), vv = byte_view(recs[i].v);
     np_[i] = kv.first ? 0 : 1;
     if (kv.second > 0) std::memcpy(kp + kpos, kv.first, (size_t)kv.second), kpos += (size_t)kv.second;
-    if (vv.second > 0) std::memcpy(vp + vpos, vv.first, (size_t)vv.second), vpos += (size_t)vv.second;
+    if (vv.second > 0) {
+      if (!by_ref) std::memcpy(vp + vpos, vv.first, (size_t)vv.second);
+      vpos += (size_t)vv.second;
+    }
     ko[i + 1] = (int64_t)kpos;
     vo[i + 1] = (int64_t)vpos;
     op[i] = recs[i].off;
     tp[i] = recs[i].ts;
   }
-  py::object vals_out = (size_t)vals.size() == vbytes ? py::object(vals)
+  py::object vals_out = by_ref ? py::object(refs)
+                       : (size_t)vals.size() == vbytes ? py::object(vals)
                                                        : vals[py::slice(0, (py::ssize_t)vbytes, 1)];
   return py::make_tuple(to_array(part_of), parts_out, keys, koff, nulls, vals_out, voff, offs, ts, errors);
 }
@@ -628,7 +645,7 @@ py::object make_fast_produce(py::object producer, py::object broker, py::object 
 
 void register_kafka_ops(pybind11::module& m) {
   m.def("pack_messages", &pack_messages, "consumed Message list -> columnar buffers (C loops)", py::arg("msgs"),
-        py::arg("vals_buf") = py::none());
+        py::arg("vals_buf") = py::none(), py::arg("by_ref") = false);
   m.def("produce_each", &produce_each, "per-record produce of one output segment from a C loop");
   m.def("install_message_accessors", &install_message_accessors, "C method descriptors on a tuple Message class");
   m.def("build_messages", &build_messages, "columnar batch -> list of Message (C loop)");

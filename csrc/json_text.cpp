@@ -161,16 +161,19 @@ const uint8_t* find_field(const uint8_t* p, const uint8_t* e, const uint8_t* fie
 
 }  // namespace
 
-// Returns total bytes written. out_off must have n+1 entries.
-int64_t extract_json_field(const uint8_t* in, const int64_t* in_off, int64_t n, const uint8_t* field, int64_t flen,
-                           uint8_t* out, int64_t out_cap, int64_t* out_off, int32_t* status, int threads) {
+namespace {
+
+// record i = bytes [begin(i), end(i)); a null begin is a missing value (status 1)
+template <class Begin, class End>
+int64_t extract_impl(Begin begin, End end, int64_t n, const uint8_t* field, int64_t flen, uint8_t* out,
+                     int64_t out_cap, int64_t* out_off, int32_t* status, int threads) {
   std::vector<int64_t> lens((size_t)n, 0);
   std::vector<const uint8_t*> where((size_t)n, nullptr);
   parallel_for(n, threads, 512, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
-      const uint8_t* s = in + in_off[i];
-      const uint8_t* e = in + in_off[i + 1];
-      const uint8_t* q = find_field(s, e, field, flen);
+      const uint8_t* s = begin(i);
+      const uint8_t* e = end(i);
+      const uint8_t* q = s ? find_field(s, e, field, flen) : nullptr;
       int64_t l = 0;
       if (q && parse_string(q, e, nullptr, &l)) { where[i] = q; lens[i] = l; status[i] = 0; }
       else { status[i] = 1; lens[i] = 0; }
@@ -186,10 +189,27 @@ int64_t extract_json_field(const uint8_t* in, const int64_t* in_off, int64_t n, 
     for (int64_t i = lo; i < hi; ++i) {
       if (!where[i]) continue;
       int64_t l;
-      parse_string(where[i], in + in_off[i + 1], out + out_off[i], &l);
+      parse_string(where[i], end(i), out + out_off[i], &l);
     }
   });
   return out_off[n];
+}
+
+}  // namespace
+
+// Returns total bytes written. out_off must have n+1 entries.
+int64_t extract_json_field(const uint8_t* in, const int64_t* in_off, int64_t n, const uint8_t* field, int64_t flen,
+                           uint8_t* out, int64_t out_cap, int64_t* out_off, int32_t* status, int threads) {
+  return extract_impl([&](int64_t i) { return in + in_off[i]; }, [&](int64_t i) { return in + in_off[i + 1]; }, n,
+                      field, flen, out, out_cap, out_off, status, threads);
+}
+
+// The same over n separate buffers (begin[i], len[i]); begin[i] == nullptr: a missing value.
+int64_t extract_json_field_ptrs(const uint8_t* const* begin, const int64_t* len, int64_t n, const uint8_t* field,
+                                int64_t flen, uint8_t* out, int64_t out_cap, int64_t* out_off, int32_t* status,
+                                int threads) {
+  return extract_impl([&](int64_t i) { return begin[i]; }, [&](int64_t i) { return begin[i] + len[i]; }, n, field,
+                      flen, out, out_cap, out_off, status, threads);
 }
 
 }  // namespace fdx

@@ -138,6 +138,9 @@ void leaf_update_cpu(double* margin, const int32_t* row_node, const double* node
 // json_text.cpp
 int64_t extract_json_field(const uint8_t* in, const int64_t* in_off, int64_t n, const uint8_t* field, int64_t flen,
                            uint8_t* out, int64_t out_cap, int64_t* out_off, int32_t* status, int threads);
+int64_t extract_json_field_ptrs(const uint8_t* const* begin, const int64_t* len, int64_t n, const uint8_t* field,
+                                int64_t flen, uint8_t* out, int64_t out_cap, int64_t* out_off, int32_t* status,
+                                int threads);
 
 int64_t encode_records(const double* pred, const double* conf, const uint8_t* text, const int64_t* off,
                        const int32_t* skip, int64_t n, uint8_t* out, int64_t cap, int64_t* out_off, int32_t* status,

@@ -189,11 +189,28 @@ def _subset(buf: np.ndarray, off: np.ndarray, keep: np.ndarray) -> tuple:
     return buf[off[0]:off[-1]][sel], new
 
 
+class _RefBatch(fake_kafka.RecordBatch):
+    """A RecordBatch whose values are a list of the consumed messages' own bytes objects
+    (``val_off`` still counts their bytes): the text field is extracted from them in place."""
+    __slots__ = ()
+
+    def slice(self, a: int, b: int) -> "_RefBatch":
+        ko, vo = self.key_off[a:b + 1], self.val_off[a:b + 1]
+        nk = self.null_keys[a:b] if self.null_keys is not None else None
+        return _RefBatch(self.topic, self.partition, self.base_offset + a, self.keys[ko[0]:ko[-1]], ko - ko[0],
+                         self.values[a:b], vo - vo[0], nk, self.ts)
+
+    def value(self, i: int) -> bytes:
+        v = self.values[i]
+        return b"" if v is None else v
+
+
 def _to_pieces(msgs: list) -> tuple:
     """confluent Messages -> (per-partition columnar pieces in consume order, [(index, error)]).
     One native pass over the list (csrc/bindings_kafka.cpp pack_messages): the per-message method
-    calls (error, topic, partition, key, value, offset, timestamp) run from C, not bytecode."""
-    part_of, parts, kb, ko, nk, vb, vo, offs, ts_ms, errors = native.lib().pack_messages(msgs)
+    calls (error, topic, partition, key, value, offset, timestamp) run from C, not bytecode; the
+    values are not copied (by_ref: _RefBatch), the text is extracted from them in place."""
+    part_of, parts, kb, ko, nk, vb, vo, offs, ts_ms, errors = native.lib().pack_messages(msgs, None, True)
     now = time.perf_counter()
     ts = np.where(ts_ms > 0, ts_ms / 1000.0 - (time.time() - now), now)
     out = []
@@ -204,10 +221,12 @@ def _to_pieces(msgs: list) -> tuple:
         else:                                   # several partitions in one consume: split
             sel = np.flatnonzero(part_of == pi)
             kk, kof = _subset(kb, ko, part_of == pi)
-            vv, vof = _subset(vb, vo, part_of == pi)
+            vv = [vb[i] for i in sel.tolist()]
+            vof = np.zeros(sel.size + 1, dtype=np.int64)
+            np.cumsum(np.diff(vo)[sel], out=vof[1:])
             nn, oo, tt = nk[sel], offs[sel], ts[sel]
         nulls = nn.astype(bool) if nn.any() else None
-        rb = fake_kafka.RecordBatch(t, p, int(oo[0]), kk, kof, vv, vof, nulls, float(tt.min()))
+        rb = _RefBatch(t, p, int(oo[0]), kk, kof, vv, vof, nulls, float(tt.min()))
         out.append(_Piece(rb, oo, tt))
     return out, errors
 
@@ -217,10 +236,14 @@ def extract_into(slot: Slot, pos: int, n: int, rb, field_name: str, status: np.n
     / document ``n``; returns the byte count written (``status`` 2 = did not fit)."""
     k = status.size
     cap = slot.data.numel() - PAD
-    vo = rb.val_off[: k + 1]
-    total = native.lib().extract_json_field(torch.from_numpy(rb.values), torch.from_numpy(np.ascontiguousarray(vo)),
-                                            field_name, slot.data[pos:cap], slot.offsets[n: n + k + 1],
-                                            torch.from_numpy(status), 0)
+    if isinstance(rb.values, list):         # _RefBatch: the messages' own value buffers
+        total = native.lib().extract_json_field_refs(rb.values, k, field_name, slot.data[pos:cap],
+                                                     slot.offsets[n: n + k + 1], torch.from_numpy(status), 0)
+    else:
+        vo = rb.val_off[: k + 1]
+        total = native.lib().extract_json_field(torch.from_numpy(rb.values), torch.from_numpy(np.ascontiguousarray(vo)),
+                                                field_name, slot.data[pos:cap], slot.offsets[n: n + k + 1],
+                                                torch.from_numpy(status), 0)
     if pos:
         slot.offsets[n: n + k + 1] += pos
     return int(total)

@@ -242,3 +242,28 @@ def test_pack_messages_reads_any_message_class_and_reuses_buffers():
         assert [i for i, _ in errs] == [2]
         if buf is not None and buf.size >= 16:
             assert bytes(buf[:16]) == b"value-onev2third"      # written in place
+
+
+def test_extract_from_value_references_equals_packed_extraction():
+    """extract_json_field_refs (values read in place) gives the packed path's bytes and statuses."""
+    import torch
+
+    from fraud_detection_spark_kafka_llm_amd.ops import native
+
+    vals = [json.dumps({"text": f"doc {i} " + "w" * (i % 7), "n": i}).encode() for i in range(50)]
+    vals[3], vals[9], vals[17] = None, b"{not json", json.dumps({"other": 1}).encode()
+    C = native.lib()
+    buf, off, _ = fake_kafka.pack([v if v is not None else b"" for v in vals])
+    outs = []
+    for refs in (False, True):
+        out = torch.zeros(4096, dtype=torch.uint8)
+        oo = torch.zeros(len(vals) + 1, dtype=torch.int64)
+        st = np.zeros(len(vals), dtype=np.int32)
+        if refs:
+            total = C.extract_json_field_refs(vals, len(vals), "text", out, oo, torch.from_numpy(st), 0)
+        else:
+            total = C.extract_json_field(torch.from_numpy(buf), torch.from_numpy(off), "text", out, oo,
+                                         torch.from_numpy(st), 0)
+        outs.append((bytes(out[:total].numpy()), oo.tolist(), st.tolist()))
+    assert outs[0] == outs[1]
+    assert outs[1][2][3] == outs[1][2][9] == outs[1][2][17] == 1 and outs[1][2][0] == 0
