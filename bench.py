@@ -28,7 +28,9 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      same runs through clients restricted to the confluent_kafka surface (per-record Messages,
      produce + delivery callback per record). ``kafka_multi_gpu_dialogues_per_s``: ONE 3-partition
      topic drained by one engine fanning micro-batches out to a scorer per GPU (rank 0; a 1-GPU
-     job runs 2 scorers on the device as a rehearsal).
+     job runs 2 scorers on the device as a rehearsal). ``kafka_confluent_group_*``: the confluent
+     surface as a consumer group — one client process per partition (3) around rank 0's GPU
+     scoring process, shared-memory slots page-locked for the H2D (stream/group.py).
 Data is synthetic (the reference dataset is not available) with random-init-free trained trees.
 Before the timed training, an untimed 2-tree fit on 65,536 rows loads the kernels' code objects
 (lazily loaded on first launch by ROCm) and warms the allocators (``gbdt_warmup_sec_untimed``).
@@ -202,6 +204,38 @@ def multi_gpu_kafka(args, spec, idf_np, model, dev, pool, make_engine) -> dict:
     return out
 
 
+def group_kafka(args, spec, idf_np, model, dev, pool) -> dict:
+    """Config 5 through the confluent surface as a consumer group (stream/group.py): one client
+    process per partition of the 3-partition topic (poll -> extract -> produce + commit, each
+    with its own GIL) around this rank's GPU scoring process (shared-memory slots, one GpuScorer).
+    Rank 0 only; the others wait."""
+    import gc
+
+    from fraud_detection_spark_kafka_llm_amd.stream import group as G
+
+    out = {}
+    if D.rank() == 0:
+        batch = 16384
+        sc = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=batch, max_bytes=batch * 4096, depth=3)
+        gc.collect()
+        with G.ConsumerGroup(sc, model.postprocess_numpy, args.kafka_group_clients, batch_max=batch,
+                             max_latency_ms=5.0, max_bytes=batch * 4096, pool=pool, confluent=True) as grp:
+            G.group_throughput_run(grp, 60_000, tag="warm")
+            tp = G.group_throughput_run(grp, args.kafka_group_msgs, tag="tp")
+            lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
+        out = {"kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
+               "kafka_confluent_group_clients": args.kafka_group_clients,
+               "kafka_confluent_group_msgs": args.kafka_group_msgs,
+               "kafka_confluent_group_p50_ms": lat["p50_ms"], "kafka_confluent_group_p95_ms": lat["p95_ms"],
+               "kafka_confluent_group_offered_per_s": args.kafka_group_rate,
+               "kafka_confluent_group_all_committed": bool(
+                   tp["produced"] == tp["committed"] == args.kafka_group_msgs and
+                   lat["produced"] == lat["committed"] == lat["sent"])}
+        del sc
+    D.barrier()
+    return out
+
+
 def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
     """BASELINE config 5 on this rank's GPU against its own in-memory broker (3 partitions)."""
     import gc
@@ -245,6 +279,8 @@ def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
                 "kafka_confluent_msgs": args.kafka_confluent_msgs,
                 "kafka_confluent_p50_ms": clat["p50_ms"], "kafka_confluent_p95_ms": clat["p95_ms"],
                 "kafka_confluent_offered_per_s": args.kafka_confluent_rate}
+    group = group_kafka(args, spec, idf_np, model, dev, pool) if args.kafka_group_msgs > 0 else {}
+    conf.update(group)
     multi = multi_gpu_kafka(args, spec, idf_np, model, dev, pool, make_engine=StreamingEngine) \
         if args.kafka_multi_msgs > 0 else {}
     return {**multi, "kafka_dialogues_per_s": tp["dialogues_per_s"], "kafka_msgs": args.kafka_msgs,
@@ -274,6 +310,11 @@ def main():
                     help="records of the shared 3-partition topic drained by rank 0 over every GPU (0: skip)")
     ap.add_argument("--kafka-confluent-msgs", type=int, default=300_000,
                     help="records drained through the confluent_kafka-surface clients (0: skip)")
+    ap.add_argument("--kafka-group-msgs", type=int, default=1_200_000,
+                    help="records drained by the confluent-surface consumer group (0: skip)")
+    ap.add_argument("--kafka-group-clients", type=int, default=3, help="client processes of the consumer group")
+    ap.add_argument("--kafka-group-rate", type=float, default=300_000,
+                    help="paced producer rate (whole group) of the consumer-group latency run")
     ap.add_argument("--kafka-confluent-rate", type=float, default=100_000,
                     help="paced producer rate of the confluent-surface latency run")
     Config.add_cli_args(ap)          # --gbdt-max-bin, --seed, --config, ... (utils/config.py)

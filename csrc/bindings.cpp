@@ -565,6 +565,19 @@ int64_t extract_json_field_refs(pybind11::list values, int64_t count, const std:
                                       out_off.data_ptr<int64_t>(), status.data_ptr<int32_t>(), (int)threads);
 }
 
+// Page-lock an existing host buffer (a shared-memory segment mapped by several processes) so the
+// GPU process DMAs micro-batches straight out of it; a CPU tensor over it then reports is_pinned.
+void host_register(const Tensor& t) {
+  FDX_CHECK(t.device().is_cpu() && t.is_contiguous(), "host_register needs a contiguous CPU tensor");
+  const size_t n = (size_t)t.numel() * t.element_size();
+  FDX_CHECK(hipHostRegister(t.data_ptr(), n, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess,
+            "hipHostRegister failed");
+}
+
+void host_unregister(const Tensor& t) {
+  FDX_CHECK(hipHostUnregister(t.data_ptr()) == hipSuccess, "hipHostUnregister failed");
+}
+
 }  // namespace
 
 void register_tree_ops(pybind11::module& m);
@@ -589,5 +602,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("extract_json_field", &extract_json_field, "Bulk JSON string-field extraction into a packed buffer");
   m.def("extract_json_field_refs", &extract_json_field_refs,
         "extract_json_field over the first count values of a list of bytes (no packing copy)");
+  m.def("host_register", &host_register, "hipHostRegister a CPU tensor's buffer (mapped, portable)");
+  m.def("host_unregister", &host_unregister, "hipHostUnregister a buffer registered by host_register");
   m.attr("gfx_arch") = "gfx950";
 }

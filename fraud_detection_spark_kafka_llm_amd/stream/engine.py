@@ -433,7 +433,8 @@ class StreamingEngine:
     def __init__(self, scorer, postprocess, consumer, producer, output_topic: Optional[str],
                  batch_max: int = 4096, max_latency_ms: float = 5.0, explain: str = "none", agent=None,
                  slots: int = 0, max_bytes: int = 64 << 20, field_name: str = "text", commit: bool = True,
-                 explain_every: int = 1, explain_max_pending: int = 1024, poll_ms: float = 20.0):
+                 explain_every: int = 1, explain_max_pending: int = 1024, poll_ms: float = 20.0,
+                 ring: Optional[PinnedRing] = None):
         if explain != "none" and agent is None:
             raise ValueError("explain requires an agent (LLM analyzer)")
         if output_topic is None:
@@ -451,7 +452,12 @@ class StreamingEngine:
         self.field = field_name
         self.commit = commit
         nslots = max(slots, scorer.depth + len(self.consumers) + 2)
-        self.ring = PinnedRing(slots=nslots, max_docs=self.batch_max, max_bytes=min(max_bytes, scorer.max_bytes))
+        if ring is not None:     # e.g. a consumer-group client's shared-memory slots (stream/group.py)
+            if len(ring.slots) < scorer.depth + 1 or ring.slots[0].offsets.numel() - 1 < self.batch_max:
+                raise ValueError("ring too small for the scorer depth / batch_max")
+            self.ring = ring
+        else:
+            self.ring = PinnedRing(slots=nslots, max_docs=self.batch_max, max_bytes=min(max_bytes, scorer.max_bytes))
         self.stats = EngineStats()
         self.tracker = _CommitTracker()
         self._stop = threading.Event()

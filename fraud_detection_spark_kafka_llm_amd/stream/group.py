@@ -1,0 +1,514 @@
+"""Consumer-group streaming: P client processes (one per partition) around ONE GPU scoring process.
+
+A librdkafka-shaped client costs ~1-2 us of interpreter work per record on each side (a Message
+object per consumed record, one ``produce`` call + delivery report per output record), all of it
+under one GIL: a single-process engine tops out near 0.6 M dialogues/s however fast the GPU is
+(profiles/r3s3/NOTES.md). Kafka's own answer is the consumer group, and that is the layout here —
+the reference's topics have 3 partitions (/root/reference/README.md:110-121), its loop consumes
+them one message at a time in one process (/root/reference/app_ui.py:196-226):
+
+  * each **client process** (``python -m ...stream.group``, started as a child that never touches
+    the GPU) runs an ordinary :class:`~.engine.StreamingEngine` over its partition(s): poll ->
+    native JSON extraction -> produce + delivery-gated commits, its own latency histogram. Its
+    ring slots live in a shared-memory segment, and its scorer is a :class:`RemoteScorer` that
+    only passes slot indices over a socket;
+  * the **GPU process** (:class:`ConsumerGroup`) maps every client's segment, page-locks it
+    (``hipHostRegister``: the H2D DMA reads the client's slot directly, no staging copy), feeds
+    the slots of all clients through one :class:`~.gpu_worker.GpuScorer` copy/compute pipeline
+    and writes (prediction, P(scam)) back into the slot's result rows.
+
+Per micro-batch the IPC is two 16-byte socket messages; the text bytes are written once (by the
+client's extraction) and read once (by the DMA engine).
+"""
+from __future__ import annotations
+
+import json
+import os
+import pickle
+import socket
+import struct
+import subprocess
+import sys
+import time
+from collections import deque
+from multiprocessing.connection import Connection, wait as mp_wait
+from multiprocessing import shared_memory
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ops.text import PAD
+from .ring import PinnedRing, Slot
+
+_SUB, _DONE, _CTL = b"S", b"D", b"C"
+_HDR = struct.Struct("<iiq")            # slot index, documents, bytes
+_ALIGN = 4096
+
+
+def _round(x: int) -> int:
+    return (x + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+def slot_layout(slots: int, max_docs: int, max_bytes: int) -> dict:
+    """Byte layout of one client's segment: per slot the text bytes, the int64 offsets and the
+    [max_docs, 2] float64 result rows, each page aligned."""
+    d, o, r = _round(max_bytes + PAD), _round((max_docs + 1) * 8), _round(max_docs * 16)
+    return {"slots": slots, "max_docs": max_docs, "max_bytes": max_bytes, "data": d, "offs": o, "res": r,
+            "stride": d + o + r, "size": slots * (d + o + r)}
+
+
+def _views(buf, lay: dict) -> list:
+    """(data uint8, offsets int64, result float64 [max_docs, 2]) tensors per slot over ``buf``."""
+    whole = torch.frombuffer(buf, dtype=torch.uint8, count=lay["size"])
+    out = []
+    for i in range(lay["slots"]):
+        b = i * lay["stride"]
+        data = whole[b: b + lay["max_bytes"] + PAD]
+        offs = whole[b + lay["data"]: b + lay["data"] + (lay["max_docs"] + 1) * 8].view(torch.int64)
+        res = whole[b + lay["data"] + lay["offs"]: b + lay["data"] + lay["offs"] + lay["max_docs"] * 16] \
+            .view(torch.float64).view(lay["max_docs"], 2)
+        out.append((data, offs, res))
+    return out
+
+
+class SharedRing(PinnedRing):
+    """The engine's slot ring over a shared-memory segment (same free/full queues as PinnedRing)."""
+
+    def __init__(self, views: list):
+        import queue
+        import threading
+
+        self.slots = [Slot(i, d, o) for i, (d, o, _) in enumerate(views)]
+        self.results = [r for _, _, r in views]
+        self._free, self._full = queue.Queue(), queue.Queue()
+        for s in self.slots:
+            self._free.put(s)
+        self.closed = threading.Event()
+
+
+class RemoteScorer:
+    """Client-side scorer: ``submit`` sends the slot index to the GPU process, ``collect`` returns
+    the (prediction, P(scam)) rows it wrote into the slot (FIFO, like GpuScorer)."""
+
+    def __init__(self, conn: Connection, ring: SharedRing, max_docs: int, max_bytes: int, depth: int = 2):
+        self.conn, self.ring = conn, ring
+        self.max_docs, self.max_bytes, self._depth = max_docs, max_bytes, depth
+        self._q: deque = deque()
+        self._done: deque = deque()
+
+    @property
+    def depth(self) -> int:
+        return self._depth
+
+    @property
+    def inflight(self) -> int:
+        return len(self._q)
+
+    def submit(self, slot: Slot) -> None:
+        if len(self._q) >= self._depth:
+            raise RuntimeError("pipeline full: call collect() first")
+        self.conn.send_bytes(_SUB + _HDR.pack(slot.index, slot.n_docs, slot.n_bytes))
+        self._q.append(slot)
+
+    def _recv(self) -> None:
+        m = self.conn.recv_bytes()
+        if m[:1] != _DONE:
+            raise RuntimeError(f"unexpected message from the scoring process: {m[:1]!r}")
+        self._done.append(_HDR.unpack_from(m, 1)[0])
+
+    def ready(self) -> bool:
+        while not self._done and self._q and self.conn.poll(0):
+            self._recv()
+        return bool(self._done)
+
+    def collect(self, copy: bool = True) -> tuple:
+        while not self._done:
+            self._recv()
+        i = self._done.popleft()
+        slot = self._q.popleft()
+        if slot.index != i:
+            raise RuntimeError(f"out-of-order result: slot {i}, expected {slot.index}")
+        res = self.ring.results[i][: slot.n_docs].numpy()
+        return slot, res.copy() if copy else res
+
+
+def remote_postprocess(res: np.ndarray) -> tuple:
+    """The GPU process already post-processed: rows are (prediction, P(scam))."""
+    return res[:, 0], res[:, 1]
+
+
+# ---------------------------------------------------------------------------------------------- GPU side
+class _Client:
+    def __init__(self, idx: int, shm, lay: dict, sock, proc):
+        self.idx, self.shm, self.lay, self.proc = idx, shm, lay, proc
+        self.conn = Connection(sock.detach())
+        self.views = _views(shm.buf, lay)
+        self.slots = [Slot(i, d, o) for i, (d, o, _) in enumerate(self.views)]
+        self.registered: list = []
+        self.reply = None
+
+
+class ConsumerGroup:
+    """The scoring process of a consumer group: ``n_clients`` client processes, one GpuScorer.
+
+    ``postprocess(raw) -> (pred, p1)`` runs here (the clients hold no model). ``pool`` (a
+    loadgen.MessagePool) is shared with the clients for the in-memory broker runs."""
+
+    def __init__(self, scorer, postprocess, n_clients: int, batch_max: int = 16384, max_latency_ms: float = 5.0,
+                 max_bytes: int = 64 << 20, client_depth: int = 2, pool=None, confluent: bool = True,
+                 register: Optional[bool] = None, env: Optional[dict] = None):
+        self.scorer, self.postprocess = scorer, postprocess
+        self.batch_max = min(batch_max, scorer.max_docs)
+        max_bytes = min(max_bytes, scorer.max_bytes)
+        slots = client_depth + 3
+        self.lay = slot_layout(slots, self.batch_max, max_bytes)
+        self.clients: list = []
+        self._pool_shm = None
+        pool_lay = None
+        if pool is not None:
+            pool_lay, self._pool_shm = _share_pool(pool)
+        dev = getattr(scorer, "dev", None)
+        self.register = (dev is not None and dev.type == "cuda") if register is None else register
+        base = {"layout": self.lay, "batch_max": self.batch_max, "max_latency_ms": max_latency_ms,
+                "depth": client_depth, "pool": pool_lay, "confluent": confluent, "n_clients": n_clients}
+        child_env = dict(os.environ, **(env or {}))
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        child_env["PYTHONPATH"] = root + os.pathsep + child_env.get("PYTHONPATH", "")
+        try:
+            for c in range(n_clients):
+                shm = shared_memory.SharedMemory(create=True, size=self.lay["size"])
+                a, b = socket.socketpair()
+                cfg = dict(base, index=c, shm=shm.name, fd=b.fileno())
+                # a fresh interpreter (never a fork of this GPU process); it touches no GPU
+                proc = subprocess.Popen([sys.executable, "-m", "fraud_detection_spark_kafka_llm_amd.stream.group",
+                                         json.dumps(cfg)], pass_fds=(b.fileno(),), env=child_env)
+                b.close()
+                cl = _Client(c, shm, self.lay, a, proc)
+                self.clients.append(cl)
+                if self.register:
+                    from ..ops import native
+
+                    for d, o, r in cl.views:
+                        for t in (d, o, r):
+                            native.lib().host_register(t)
+                            cl.registered.append(t)
+            for cl in self.clients:
+                msg = self._control(cl)
+                if msg[0] != "ready":
+                    raise RuntimeError(f"client {cl.idx}: {msg}")
+        except BaseException:
+            self.close()
+            raise
+
+    # ------------------------------------------------------------------ protocol
+    def _control(self, cl: _Client, timeout: float = 300.0):
+        if not cl.conn.poll(timeout):
+            raise TimeoutError(f"client {cl.idx} did not answer")
+        m = cl.conn.recv_bytes()
+        if m[:1] != _CTL:
+            raise RuntimeError(f"client {cl.idx}: expected a control message, got {m[:1]!r}")
+        return pickle.loads(m[1:])
+
+    def _send_ctl(self, cl: _Client, obj) -> None:
+        cl.conn.send_bytes(_CTL + pickle.dumps(obj))
+
+    def _finish(self) -> None:
+        slot, raw = self.scorer.collect(copy=False)
+        c, i = slot.meta
+        slot.meta = None
+        pred, p1 = self.postprocess(raw)
+        res = self.clients[c].views[i][2][: slot.n_docs].numpy()
+        res[:, 0] = pred
+        res[:, 1] = p1
+        self.clients[c].conn.send_bytes(_DONE + _HDR.pack(i, slot.n_docs, slot.n_bytes))
+
+    def run(self, spec: dict, per_client: Optional[list] = None) -> list:
+        """Send ``spec`` (merged with ``per_client[c]``) to every client, score their micro-batches
+        until each has answered; returns the clients' result dicts in client order."""
+        for cl in self.clients:
+            cl.reply = None
+            self._send_ctl(cl, ("run", dict(spec, **(per_client[cl.idx] if per_client else {}))))
+        live = {cl.conn: cl for cl in self.clients}
+        sc = self.scorer
+        while live or sc.inflight:
+            while sc.inflight and sc.ready():
+                self._finish()
+            if not live:
+                self._finish()
+                continue
+            for conn in mp_wait(list(live), timeout=0.0002 if sc.inflight else 0.05):
+                cl = live[conn]
+                try:
+                    m = conn.recv_bytes()
+                except EOFError:
+                    raise RuntimeError(f"client {cl.idx} exited (code {cl.proc.poll()})") from None
+                if m[:1] == _SUB:
+                    i, n, nb = _HDR.unpack_from(m, 1)
+                    if not (0 <= i < len(cl.slots)) or n > self.batch_max or nb > self.lay["max_bytes"]:
+                        raise RuntimeError(f"client {cl.idx}: bad slot header {(i, n, nb)}")
+                    while sc.inflight >= sc.depth:
+                        self._finish()
+                    s = cl.slots[i]
+                    s.n_docs, s.n_bytes, s.meta = n, nb, (cl.idx, i)
+                    sc.submit(s)
+                else:
+                    msg = pickle.loads(m[1:])
+                    if msg[0] == "error":
+                        raise RuntimeError(f"client {cl.idx} failed:\n{msg[1]}")
+                    cl.reply = msg[1]
+                    del live[conn]
+            for cl in list(live.values()):
+                if cl.proc.poll() is not None and not cl.conn.poll(0):
+                    raise RuntimeError(f"client {cl.idx} exited (code {cl.proc.returncode})")
+        return [cl.reply for cl in self.clients]
+
+    def close(self) -> None:
+        for cl in self.clients:
+            try:
+                self._send_ctl(cl, ("exit", {}))
+            except OSError:
+                pass
+        for cl in self.clients:
+            try:
+                cl.proc.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                cl.proc.kill()
+                cl.proc.wait()
+            if cl.registered:
+                from ..ops import native
+
+                for t in cl.registered:
+                    native.lib().host_unregister(t)
+                cl.registered = []
+            cl.conn.close()
+            cl.views = cl.slots = None
+            try:
+                cl.shm.close()
+            except BufferError:      # a tensor view still alive somewhere: the unlink still frees it
+                pass
+            cl.shm.unlink()
+        self.clients = []
+        if self._pool_shm is not None:
+            self._pool_shm.close()
+            self._pool_shm.unlink()
+            self._pool_shm = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def _share_pool(pool) -> tuple:
+    arrs = {"vals": pool.vals, "voff": pool.voff, "keys": pool.keys, "koff": pool.koff}
+    lay, pos = {}, 0
+    for k, a in arrs.items():
+        lay[k] = (pos, str(a.dtype), int(a.size))
+        pos = _round(pos + a.nbytes)
+    shm = shared_memory.SharedMemory(create=True, size=max(pos, 1))
+    for k, a in arrs.items():
+        o, dt, n = lay[k]
+        np.ndarray(n, dtype=dt, buffer=shm.buf, offset=o)[:] = a
+    lay["name"], lay["n"] = shm.name, pool.n
+    return lay, shm
+
+
+# ---------------------------------------------------------------------------------------------- aggregate runs
+def merge_results(rs: list) -> dict:
+    """Whole-group numbers: dialogues/s over the union of the clients' timed windows, exact
+    latency percentiles from the summed histograms."""
+    from .engine import LatencyHistogram
+
+    h = LatencyHistogram()
+    for r in rs:
+        h.counts += np.asarray(r["lat_counts"], dtype=np.int64)
+        h.n += int(r["lat_n"])
+    t0, t1 = min(r["t0"] for r in rs), max(r["t1"] for r in rs)
+    msgs = sum(r["messages"] for r in rs)
+    return {"dialogues_per_s": msgs / max(t1 - t0, 1e-9), "sec": t1 - t0, "messages": msgs,
+            "produced": sum(r["produced"] for r in rs), "committed": sum(r["committed"] for r in rs),
+            "sent": sum(r.get("sent", 0) for r in rs), "batches": sum(r["batches"] for r in rs),
+            "p50_ms": h.percentile(50), "p95_ms": h.percentile(95), "p99_ms": h.percentile(99),
+            "clients": len(rs), "client_dialogues_per_s": [r["messages"] / max(r["t1"] - r["t0"], 1e-9) for r in rs],
+            "client_start_spread_ms": (max(r["t0"] for r in rs) - t0) * 1e3}
+
+
+def group_throughput_run(group: ConsumerGroup, n: int, tag: str = "gtp", **extra) -> dict:
+    """Each client drains a pre-filled partition of n / P records (partition c of a P-partition
+    topic on its broker); rate over the whole group."""
+    P = len(group.clients)
+    share = [n // P + (1 if c < n % P else 0) for c in range(P)]
+    rs = group.run(dict({"kind": "throughput", "tag": tag}, **extra), [{"n": k} for k in share])
+    out = merge_results(rs)
+    if extra.get("return_outputs"):
+        out["outputs"] = [r["outputs"] for r in rs]
+    return out
+
+
+def group_latency_run(group: ConsumerGroup, rate: float, duration_s: float, warmup_s: float = 0.3,
+                      tag: str = "glat") -> dict:
+    """A paced producer per client appends rate / P records/s to its partition; per-message
+    latency (append -> output delivered) over the whole group."""
+    P = len(group.clients)
+    r = merge_results(group.run({"kind": "latency", "rate": rate / P, "duration": duration_s, "warmup": warmup_s,
+                                 "tag": tag}))
+    r["offered_per_s"] = rate
+    return r
+
+
+# ---------------------------------------------------------------------------------------------- client process
+def _client_pool(lay: dict):
+    from .loadgen import MessagePool
+
+    shm = _attach(lay["name"])
+    pool = MessagePool.__new__(MessagePool)
+    for k in ("vals", "voff", "keys", "koff"):
+        o, dt, n = lay[k]
+        setattr(pool, k, np.ndarray(n, dtype=dt, buffer=shm.buf, offset=o))
+    pool.n = lay["n"]
+    return pool, shm
+
+
+def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool) -> dict:
+    from . import fake_kafka, loadgen
+    from .engine import StreamingEngine
+
+    c, P = cfg["index"], cfg["n_clients"]
+    url = f"memory://group-{os.getpid()}-{spec['tag']}"
+    broker = fake_kafka.broker_for(url)
+    broker.create_topic("in", P)
+    broker.create_topic("out", P)
+    inner = fake_kafka.Consumer({"bootstrap.servers": url, "group.id": "fdx-group", "auto.offset.reset": "earliest",
+                                 "enable.auto.commit": False})
+    inner.assign([fake_kafka.TopicPartition("in", c)])
+    prod = fake_kafka.Producer({"bootstrap.servers": url})
+    cons, producer = (fake_kafka.ConfluentConsumer(inner), fake_kafka.ConfluentProducer(prod)) if cfg["confluent"] \
+        else (inner, prod)
+    lay = cfg["layout"]
+    scorer = RemoteScorer(conn, ring, lay["max_docs"], lay["max_bytes"], cfg["depth"])
+    eng = StreamingEngine(scorer, remote_postprocess, cons, producer, "out", batch_max=cfg["batch_max"],
+                          max_latency_ms=cfg["max_latency_ms"], max_bytes=lay["max_bytes"], ring=ring)
+    sent = 0
+    if spec["kind"] == "throughput":
+        n = int(spec["n"])
+        with broker.lock:
+            for s in range(0, n, 8192):
+                broker.topics["in"][c].append(pool.batch(c * 7919 + s, min(8192, n - s), "in", c))
+            broker.cond.notify_all()
+        t0 = time.perf_counter()
+        st = eng.run(max_messages=n, idle_timeout_s=5.0)
+        sent = n
+    else:
+        # this client's partition only: a paced producer appending to partition c
+        gen = _PartitionPacer(broker, "in", c, pool, spec["rate"], spec["duration"] + spec["warmup"])
+        import threading
+
+        def reset():
+            time.sleep(spec["warmup"])
+            eng.stats.latency.reset()
+
+        threading.Thread(target=reset, daemon=True).start()
+        gen.start()
+        t0 = time.perf_counter()
+        st = eng.run(idle_timeout_s=0.5)
+        gen.join()
+        sent = gen.sent
+    t1 = time.perf_counter()
+    committed = sum(inner.committed_offsets().values())
+    outputs = None
+    if spec.get("return_outputs"):           # tests: the produced records, in partition order
+        outputs = []
+        for part in broker.topics["out"]:
+            for it in part:       # columnar batches (produce_records) or Messages (per-record produce)
+                outputs += [(it.key(i), it.value(i)) for i in range(it.n)] if hasattr(it, "n") \
+                    else [(it.key(), it.value())]
+    loadgen._drop(url)
+    return {"outputs": outputs, "t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"], "committed": committed,
+            "batches": st["batches"], "sent": sent, "lat_counts": eng.stats.latency.counts.tolist(),
+            "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"]}
+
+
+class _PartitionPacer:
+    """loadgen.PacedProducer restricted to one partition (one client of the group)."""
+
+    def __init__(self, broker, topic: str, partition: int, pool, rate: float, duration_s: float, tick_ms: float = 1.0):
+        import threading
+
+        self.broker, self.topic, self.p, self.pool = broker, topic, partition, pool
+        self.rate, self.duration, self.tick = rate, duration_s, tick_ms / 1000.0
+        self.sent = 0
+        self._t = threading.Thread(target=self._run, name="fdx-partition-pacer", daemon=True)
+
+    def start(self) -> None:
+        self._t.start()
+
+    def join(self) -> None:
+        self._t.join()
+
+    def _run(self) -> None:
+        t0 = time.perf_counter()
+        nxt = t0
+        while time.perf_counter() - t0 < self.duration:
+            due = int((time.perf_counter() - t0) * self.rate) - self.sent
+            if due > 0:
+                with self.broker.lock:
+                    rb = self.pool.batch(self.p * 7919 + self.sent, due, self.topic, self.p, ts=time.perf_counter())
+                    self.broker.topics[self.topic][self.p].append(rb)
+                    self.sent += due
+                    self.broker.cond.notify_all()
+            nxt += self.tick
+            time.sleep(max(0.0, nxt - time.perf_counter()))
+
+
+def _attach(name: str):
+    """Attach a segment the GPU process owns (and unlinks): not this process's resource tracker's
+    to remove at exit."""
+    from multiprocessing import resource_tracker
+
+    shm = shared_memory.SharedMemory(name=name)
+    resource_tracker.unregister(shm._name, "shared_memory")
+    return shm
+
+
+def _client_main(cfg: dict) -> int:
+    conn = Connection(cfg["fd"])
+    shm = _attach(cfg["shm"])
+    pool_shm = None
+    try:
+        ring = SharedRing(_views(shm.buf, cfg["layout"]))
+        pool = None
+        if cfg["pool"] is not None:
+            pool, pool_shm = _client_pool(cfg["pool"])
+        conn.send_bytes(_CTL + pickle.dumps(("ready", {})))
+        while True:
+            m = conn.recv_bytes()
+            cmd, spec = pickle.loads(m[1:])
+            if cmd == "exit":
+                return 0
+            try:
+                r = _client_run(cfg, spec, conn, ring, pool)
+                conn.send_bytes(_CTL + pickle.dumps(("result", r)))
+            except Exception:
+                import traceback
+
+                conn.send_bytes(_CTL + pickle.dumps(("error", traceback.format_exc())))
+                return 1
+    except (EOFError, ConnectionError):
+        return 0
+    finally:
+        ring = pool = None
+        import gc
+
+        gc.collect()
+        for s in (shm, pool_shm):
+            if s is not None:
+                try:
+                    s.close()
+                except BufferError:
+                    pass
+
+
+if __name__ == "__main__":
+    sys.exit(_client_main(json.loads(sys.argv[1])))

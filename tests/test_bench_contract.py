@@ -13,7 +13,8 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config"}
 TINY = ["--steps", "4", "--warmup", "2", "--rows", "100000", "--trees", "3", "--batch", "4096", "--pool", "2",
         "--rf-trees", "4", "--kafka-msgs", "20000", "--kafka-sec", "0.5", "--kafka-multi-msgs", "20000",
-        "--kafka-confluent-msgs", "5000", "--kafka-confluent-rate", "5000"]
+        "--kafka-confluent-msgs", "5000", "--kafka-confluent-rate", "5000", "--kafka-group-msgs", "20000",
+        "--kafka-group-rate", "6000"]
 
 
 def _json_line(out: str) -> dict:
@@ -31,6 +32,8 @@ def _check(rec: dict, n: int):
     assert rec["rf_train_sec"] > 0 and rec["rf_trees"] == 4
     assert rec["kafka_confluent_dialogues_per_s"] > 0 and rec["kafka_multi_gpu_dialogues_per_s"] > 0
     assert rec["kafka_all_delivered_and_committed"] and rec["kafka_multi_gpu_all_committed"]
+    assert rec["kafka_confluent_group_dialogues_per_s"] > 0 and rec["kafka_confluent_group_clients"] == 3
+    assert rec["kafka_confluent_group_all_committed"]
 
 
 @pytest.mark.gpu

@@ -1,0 +1,88 @@
+"""Consumer-group streaming (stream/group.py): client processes with shared-memory slot rings
+around one scoring process. Every record of every partition is classified exactly like the
+single-process engine, produced once and committed (reference loop: /root/reference/app_ui.py:196-226)."""
+import json
+
+import numpy as np
+import pytest
+
+from fraud_detection_spark_kafka_llm_amd.data import synth
+from fraud_detection_spark_kafka_llm_amd.ops.text import PackedText, featurize_score
+from fraud_detection_spark_kafka_llm_amd.serve.agent import ClassificationAgent
+from fraud_detection_spark_kafka_llm_amd.serve.llm import StubLLM
+from fraud_detection_spark_kafka_llm_amd.stream import group as G
+from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import make_scorer
+from fraud_detection_spark_kafka_llm_amd.stream.loadgen import MessagePool
+
+
+@pytest.fixture(scope="module")
+def agent(shipped_model_path):
+    return ClassificationAgent(str(shipped_model_path), llm=StubLLM(), device="cpu")
+
+
+def _expected(agent, texts):
+    fp = agent.fused
+    idf = fp.idf.idf if fp.idf is not None else None
+    import torch
+    res = featurize_score(PackedText.from_strings(texts), fp.spec(True),
+                          idf=torch.as_tensor(np.asarray(idf)) if idf is not None else None,
+                          lr=fp.model.scorer(), device="cpu")
+    return fp.model.postprocess_numpy(res.raw.numpy())
+
+
+@pytest.mark.parametrize("confluent", [True, False])
+def test_group_throughput_all_records_scored_once(agent, confluent):
+    pt, _ = synth.generate(synth.SynthConfig(n=500, seed=5), device="cpu")
+    texts = pt.strings()
+    pool = MessagePool(texts)
+    fp = agent.fused
+    sc = make_scorer(fp.spec(True), fp.idf.idf if fp.idf is not None else None, fp.model.scorer(), "cpu",
+                     max_docs=256, max_bytes=256 * 4096, depth=2)
+    n = 1700                       # wraps the pool; 3 partitions of uneven size
+    with G.ConsumerGroup(sc, fp.model.postprocess_numpy, 3, batch_max=256, max_latency_ms=2.0,
+                         max_bytes=256 * 4096, pool=pool, confluent=confluent) as grp:
+        r = G.group_throughput_run(grp, n, return_outputs=True)
+        r2 = G.group_throughput_run(grp, 300)          # the clients serve several runs
+    assert r["messages"] == r["produced"] == r["committed"] == n
+    assert r2["produced"] == r2["committed"] == 300
+    pred, p1 = _expected(agent, texts)
+    from collections import Counter
+    want, got = Counter(), Counter()
+    for c in range(3):
+        share = n // 3 + (1 if c < n % 3 else 0)
+        want.update((c * 7919 + j) % pool.n for j in range(share))
+    for outs in r["outputs"]:
+        for key, val in outs:       # output partitions come from the producer's partitioner
+            i = int(key.decode()[3:])
+            rec = json.loads(val)
+            assert rec["original_text"] == texts[i]
+            assert rec["prediction"] == float(pred[i]) and rec["confidence"] == float(p1[i])
+            got[i] += 1
+    assert got == want
+    assert r["p50_ms"] > 0
+
+
+def test_group_latency_run(agent):
+    pt, _ = synth.generate(synth.SynthConfig(n=200, seed=6), device="cpu")
+    pool = MessagePool(pt.strings())
+    fp = agent.fused
+    sc = make_scorer(fp.spec(True), fp.idf.idf, fp.model.scorer(), "cpu", max_docs=128, max_bytes=128 * 4096)
+    with G.ConsumerGroup(sc, fp.model.postprocess_numpy, 2, batch_max=128, max_latency_ms=1.0,
+                         max_bytes=128 * 4096, pool=pool) as grp:
+        r = G.group_latency_run(grp, rate=4000, duration_s=0.5, warmup_s=0.1)
+    assert r["sent"] > 0 and r["produced"] == r["sent"] == r["committed"]
+    assert 0 < r["p50_ms"] <= r["p95_ms"]
+
+
+def test_client_failure_surfaces(agent):
+    fp = agent.fused
+    sc = make_scorer(fp.spec(True), fp.idf.idf, fp.model.scorer(), "cpu", max_docs=64, max_bytes=64 * 4096)
+    with G.ConsumerGroup(sc, fp.model.postprocess_numpy, 1, batch_max=64, max_bytes=64 * 4096) as grp:
+        with pytest.raises(RuntimeError, match="client 0 failed"):
+            grp.run({"kind": "throughput", "tag": "x", "n": 10})      # no pool shared: the client raises
+
+
+def test_slot_layout_page_aligned():
+    lay = G.slot_layout(5, 1000, 1 << 20)
+    assert lay["stride"] % 4096 == 0 and lay["size"] == 5 * lay["stride"]
+    assert lay["data"] >= (1 << 20) and lay["res"] >= 1000 * 16
