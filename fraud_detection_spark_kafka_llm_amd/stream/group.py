@@ -348,12 +348,12 @@ def group_throughput_run(group: ConsumerGroup, n: int, tag: str = "gtp", **extra
 
 
 def group_latency_run(group: ConsumerGroup, rate: float, duration_s: float, warmup_s: float = 0.3,
-                      tag: str = "glat") -> dict:
+                      tag: str = "glat", batch_max: int = 4096, max_latency_ms: float = 1.0) -> dict:
     """A paced producer per client appends rate / P records/s to its partition; per-message
     latency (append -> output delivered) over the whole group."""
     P = len(group.clients)
     r = merge_results(group.run({"kind": "latency", "rate": rate / P, "duration": duration_s, "warmup": warmup_s,
-                                 "tag": tag}))
+                                 "tag": tag, "batch_max": batch_max, "max_latency_ms": max_latency_ms}))
     r["offered_per_s"] = rate
     return r
 
@@ -376,6 +376,10 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
     from .engine import StreamingEngine
 
     c, P = cfg["index"], cfg["n_clients"]
+    lay = cfg["layout"]
+    scorer = RemoteScorer(conn, ring, lay["max_docs"], lay["max_bytes"], cfg["depth"])
+    if spec["kind"] == "serve":
+        return _client_serve(cfg, spec, scorer, ring)
     url = f"memory://group-{os.getpid()}-{spec['tag']}"
     broker = fake_kafka.broker_for(url)
     broker.create_topic("in", P)
@@ -386,10 +390,11 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
     prod = fake_kafka.Producer({"bootstrap.servers": url})
     cons, producer = (fake_kafka.ConfluentConsumer(inner), fake_kafka.ConfluentProducer(prod)) if cfg["confluent"] \
         else (inner, prod)
-    lay = cfg["layout"]
-    scorer = RemoteScorer(conn, ring, lay["max_docs"], lay["max_bytes"], cfg["depth"])
-    eng = StreamingEngine(scorer, remote_postprocess, cons, producer, "out", batch_max=cfg["batch_max"],
-                          max_latency_ms=cfg["max_latency_ms"], max_bytes=lay["max_bytes"], ring=ring)
+    # per-run micro-batch policy (latency runs: small batches, short fill deadline)
+    eng = StreamingEngine(scorer, remote_postprocess, cons, producer, "out",
+                          batch_max=min(spec.get("batch_max", cfg["batch_max"]), cfg["batch_max"]),
+                          max_latency_ms=spec.get("max_latency_ms", cfg["max_latency_ms"]), max_bytes=lay["max_bytes"],
+                          ring=ring)
     sent = 0
     if spec["kind"] == "throughput":
         n = int(spec["n"])
@@ -428,6 +433,31 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
     return {"outputs": outputs, "t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"], "committed": committed,
             "batches": st["batches"], "sent": sent, "lat_counts": eng.stats.latency.counts.tolist(),
             "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"]}
+
+
+def _client_serve(cfg: dict, spec: dict, scorer: RemoteScorer, ring: SharedRing) -> dict:
+    """A consumer-group member against the configured Kafka (stream/kafka.py factories, the
+    reference's environment variables): subscribes with the group id, so the broker balances the
+    topic's partitions over the group's clients; produces to KAFKA_OUTPUT_TOPIC, commits after
+    delivery."""
+    from . import kafka
+    from .engine import StreamingEngine
+
+    cons = kafka.get_kafka_consumer(group=spec.get("group"))
+    try:
+        eng = StreamingEngine(scorer, remote_postprocess, cons, kafka.get_kafka_producer(),
+                              spec.get("output_topic") or os.getenv("KAFKA_OUTPUT_TOPIC", kafka.DEFAULT_OUTPUT),
+                              batch_max=cfg["batch_max"], max_latency_ms=cfg["max_latency_ms"],
+                              max_bytes=cfg["layout"]["max_bytes"], ring=ring)
+        t0 = time.perf_counter()
+        st = eng.run(max_messages=spec.get("max_messages"), idle_timeout_s=spec.get("idle_timeout", float("inf")))
+        t1 = time.perf_counter()
+    finally:
+        cons.close()
+    return {"t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"],
+            "committed": st["committed"], "batches": st["batches"], "sent": 0,
+            "lat_counts": eng.stats.latency.counts.tolist(), "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"],
+            "summary": st}
 
 
 class _PartitionPacer:

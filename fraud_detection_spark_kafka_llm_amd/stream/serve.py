@@ -9,6 +9,9 @@ working directory is honoured): the consumer group reads KAFKA_INPUT_TOPIC, clas
 KAFKA_OUTPUT_TOPIC as JSON {prediction, confidence, analysis, historical_insight, original_text}
 keyed like the input; offsets are committed after the outputs are produced (at-least-once).
 With --gpus N the micro-batches of the consumer are spread over N devices of this process.
+With --group-clients P the Kafka clients run as P consumer-group member processes (one GIL each,
+stream/group.py) around this process's GPU scorer; the broker balances the topic's partitions over
+them (a real bootstrap only: a memory:// broker lives inside one process; --explain none).
 ``/metrics`` serves the Prometheus text format of the metrics registry when --metrics-port is set.
 """
 from __future__ import annotations
@@ -69,6 +72,8 @@ def main(argv=None) -> int:
     ap.add_argument("--metrics-port", type=int, default=0)
     ap.add_argument("--partition-readers", action="store_true",
                     help="one consumer (and reader thread) per input partition instead of one subscriber")
+    ap.add_argument("--group-clients", type=int, default=0,
+                    help="run the Kafka clients as this many consumer-group processes around this GPU process")
     Config.add_cli_args(ap)
     args = ap.parse_args(argv)
     load_dotenv()
@@ -83,6 +88,8 @@ def main(argv=None) -> int:
         devices = [torch.device("cpu")]
     llm = make_llm() if args.explain != "none" else StubLLM()   # no LLM calls without --explain
     agent = ClassificationAgent(args.model, llm=llm, device=devices[0])
+    if args.group_clients > 0:
+        return _serve_group(args, agent, devices, out_topic=os.getenv("KAFKA_OUTPUT_TOPIC", DEFAULT_OUTPUT))
     consumer = get_partition_consumers() if args.partition_readers else get_kafka_consumer()
     producer = get_kafka_producer()
     out_topic = os.getenv("KAFKA_OUTPUT_TOPIC", DEFAULT_OUTPUT)
@@ -97,6 +104,31 @@ def main(argv=None) -> int:
         for c in (consumer if isinstance(consumer, list) else [consumer]):
             c.close()
     print(json.dumps(stats), flush=True)
+    return 0
+
+
+def _serve_group(args, agent, devices, out_topic: str) -> int:
+    from .gpu_worker import make_multi_scorer
+    from .group import ConsumerGroup, merge_results
+
+    if args.explain != "none":
+        raise SystemExit("--group-clients serves classifications only (--explain none)")
+    if os.getenv("KAFKA_BOOTSTRAP_SERVERS", "").startswith("memory://") or os.getenv("FDX_KAFKA", "") == "memory":
+        raise SystemExit("--group-clients needs a real Kafka bootstrap (an in-memory broker is per process)")
+    fp = agent.fused
+    scorer = make_multi_scorer(fp.spec(True), fp.idf.idf if fp.idf is not None else None, fp.model.scorer(),
+                               devices, max_docs=args.batch, max_bytes=args.batch * 4096, depth=3)
+    if args.metrics_port:
+        start_metrics_server(args.metrics_port)
+    log.info("serving %s on %s with %d client processes -> %s", args.model, [str(d) for d in devices],
+             args.group_clients, out_topic)
+    with ConsumerGroup(scorer, fp.model.postprocess_numpy, args.group_clients, batch_max=args.batch,
+                       max_latency_ms=args.max_latency_ms, max_bytes=args.batch * 4096) as grp:
+        P, m = args.group_clients, args.max_messages
+        share = None if m is None else [{"max_messages": m // P + (1 if c < m % P else 0)} for c in range(P)]
+        rs = grp.run({"kind": "serve", "max_messages": m, "idle_timeout": args.idle_timeout,
+                      "output_topic": out_topic}, share)
+    print(json.dumps({k: v for k, v in merge_results(rs).items() if k != "client_dialogues_per_s"}), flush=True)
     return 0
 
 

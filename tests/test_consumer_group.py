@@ -16,8 +16,23 @@ from fraud_detection_spark_kafka_llm_amd.stream.loadgen import MessagePool
 
 
 @pytest.fixture(scope="module")
-def agent(shipped_model_path):
-    return ClassificationAgent(str(shipped_model_path), llm=StubLLM(), device="cpu")
+def agent(tmp_path_factory):
+    """A small HashingTF -> IDF -> LogisticRegression pipeline trained on synthetic dialogues
+    (self-contained: the GPU box has no /root/reference)."""
+    from fraud_detection_spark_kafka_llm_amd.ml import (IDF, Frame, HashingTF, LogisticRegression, Pipeline,
+                                                         StopWordsRemover, TextColumn, Tokenizer)
+
+    pt, y = synth.generate(synth.SynthConfig(n=600, seed=21))
+    raw = TextColumn(pt.strings())
+    df = Frame({"dialogue": raw, "clean_text": TextColumn.cleaned_from(raw), "labels": y.numpy()})
+    model = Pipeline(stages=[Tokenizer(inputCol="clean_text", outputCol="words"),
+                             StopWordsRemover(inputCol="words", outputCol="filtered_words"),
+                             HashingTF(inputCol="filtered_words", outputCol="raw_features", numFeatures=1 << 18),
+                             IDF(inputCol="raw_features", outputCol="features"),
+                             LogisticRegression(featuresCol="features", labelCol="labels", maxIter=10)]).fit(df)
+    path = tmp_path_factory.mktemp("group") / "model"
+    model.save(str(path))
+    return ClassificationAgent(str(path), llm=StubLLM(), device="cpu")
 
 
 def _expected(agent, texts):
@@ -86,3 +101,30 @@ def test_slot_layout_page_aligned():
     lay = G.slot_layout(5, 1000, 1 << 20)
     assert lay["stride"] % 4096 == 0 and lay["size"] == 5 * lay["stride"]
     assert lay["data"] >= (1 << 20) and lay["res"] >= 1000 * 16
+
+
+@pytest.mark.gpu
+def test_group_gpu_scorer_registered_slots(agent):
+    """The GPU process page-locks the clients' segments and DMAs from them: same records as the host."""
+    import torch
+    pt, _ = synth.generate(synth.SynthConfig(n=400, seed=8), device="cpu")
+    texts = pt.strings()
+    pool = MessagePool(texts)
+    fp = agent.fused
+    sc = make_scorer(fp.spec(True), fp.idf.idf, fp.model.scorer(), torch.device("cuda", 0), max_docs=512,
+                     max_bytes=512 * 4096, depth=3)
+    with G.ConsumerGroup(sc, fp.model.postprocess_numpy, 3, batch_max=512, max_latency_ms=2.0,
+                         max_bytes=512 * 4096, pool=pool) as grp:
+        assert grp.register
+        r = G.group_throughput_run(grp, 3000, return_outputs=True)
+    assert r["produced"] == r["committed"] == 3000
+    pred, p1 = _expected(agent, texts)
+    n = 0
+    for outs in r["outputs"]:
+        for key, val in outs:
+            i = int(key.decode()[3:])
+            rec = json.loads(val)
+            assert rec["prediction"] == float(pred[i])
+            assert abs(rec["confidence"] - float(p1[i])) <= 1e-12
+            n += 1
+    assert n == 3000
