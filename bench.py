@@ -30,7 +30,8 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      topic drained by one engine fanning micro-batches out to a scorer per GPU (rank 0; a 1-GPU
      job runs 2 scorers on the device as a rehearsal). ``kafka_confluent_group_*``: the confluent
      surface as a consumer group — one client process per partition (3) around rank 0's GPU
-     scoring process, shared-memory slots page-locked for the H2D (stream/group.py).
+     scoring process, shared-memory slots page-locked for the H2D (stream/group.py);
+     ``..._explain_*``: the same latency run with the LLM-explain stub on every 10th record.
 Data is synthetic (the reference dataset is not available) with random-init-free trained trees.
 Before the timed training, an untimed 2-tree fit on 65,536 rows loads the kernels' code objects
 (lazily loaded on first launch by ROCm) and warms the allocators (``gbdt_warmup_sec_untimed``).
@@ -223,14 +224,22 @@ def group_kafka(args, spec, idf_np, model, dev, pool) -> dict:
             G.group_throughput_run(grp, 60_000, tag="warm")
             tp = G.group_throughput_run(grp, args.kafka_group_msgs, tag="tp")
             lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
+            # the config's LLM-explain stub: every 10th classification explained asynchronously
+            # in the clients (offline stub backend), its record produced after the classification
+            ex = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat-explain", explain="async",
+                                     explain_every=10)
         out = {"kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
                "kafka_confluent_group_clients": args.kafka_group_clients,
                "kafka_confluent_group_msgs": args.kafka_group_msgs,
                "kafka_confluent_group_p50_ms": lat["p50_ms"], "kafka_confluent_group_p95_ms": lat["p95_ms"],
                "kafka_confluent_group_offered_per_s": args.kafka_group_rate,
+               "kafka_confluent_group_explain_p50_ms": ex["p50_ms"],
+               "kafka_confluent_group_explain_p95_ms": ex["p95_ms"],
+               "kafka_confluent_group_explanations": ex["explanations"],
                "kafka_confluent_group_all_committed": bool(
                    tp["produced"] == tp["committed"] == args.kafka_group_msgs and
-                   lat["produced"] == lat["committed"] == lat["sent"])}
+                   lat["produced"] == lat["committed"] == lat["sent"] and
+                   ex["produced"] == ex["committed"] == ex["sent"] and ex["explanations"] > 0)}
         del sc
     D.barrier()
     return out

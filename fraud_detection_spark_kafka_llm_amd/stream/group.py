@@ -330,6 +330,7 @@ def merge_results(rs: list) -> dict:
     return {"dialogues_per_s": msgs / max(t1 - t0, 1e-9), "sec": t1 - t0, "messages": msgs,
             "produced": sum(r["produced"] for r in rs), "committed": sum(r["committed"] for r in rs),
             "sent": sum(r.get("sent", 0) for r in rs), "batches": sum(r["batches"] for r in rs),
+            "explanations": sum(r.get("explanations", 0) for r in rs),
             "p50_ms": h.percentile(50), "p95_ms": h.percentile(95), "p99_ms": h.percentile(99),
             "clients": len(rs), "client_dialogues_per_s": [r["messages"] / max(r["t1"] - r["t0"], 1e-9) for r in rs],
             "client_start_spread_ms": (max(r["t0"] for r in rs) - t0) * 1e3}
@@ -348,12 +349,12 @@ def group_throughput_run(group: ConsumerGroup, n: int, tag: str = "gtp", **extra
 
 
 def group_latency_run(group: ConsumerGroup, rate: float, duration_s: float, warmup_s: float = 0.3,
-                      tag: str = "glat", batch_max: int = 4096, max_latency_ms: float = 1.0) -> dict:
+                      tag: str = "glat", batch_max: int = 4096, max_latency_ms: float = 1.0, **extra) -> dict:
     """A paced producer per client appends rate / P records/s to its partition; per-message
     latency (append -> output delivered) over the whole group."""
     P = len(group.clients)
     r = merge_results(group.run({"kind": "latency", "rate": rate / P, "duration": duration_s, "warmup": warmup_s,
-                                 "tag": tag, "batch_max": batch_max, "max_latency_ms": max_latency_ms}))
+                                 "tag": tag, "batch_max": batch_max, "max_latency_ms": max_latency_ms, **extra}))
     r["offered_per_s"] = rate
     return r
 
@@ -394,7 +395,7 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
     eng = StreamingEngine(scorer, remote_postprocess, cons, producer, "out",
                           batch_max=min(spec.get("batch_max", cfg["batch_max"]), cfg["batch_max"]),
                           max_latency_ms=spec.get("max_latency_ms", cfg["max_latency_ms"]), max_bytes=lay["max_bytes"],
-                          ring=ring)
+                          ring=ring, **_explain_kw(spec))
     sent = 0
     if spec["kind"] == "throughput":
         n = int(spec["n"])
@@ -431,8 +432,39 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
                     else [(it.key(), it.value())]
     loadgen._drop(url)
     return {"outputs": outputs, "t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"], "committed": committed,
-            "batches": st["batches"], "sent": sent, "lat_counts": eng.stats.latency.counts.tolist(),
+            "batches": st["batches"], "sent": sent, "explanations": st["explanations"],
+            "lat_counts": eng.stats.latency.counts.tolist(),
             "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"]}
+
+
+class _ClientExplainer:
+    """What the engine needs of an agent for LLM explanations (serve/llm.py Analyzer), without the
+    model: the GPU process classified the record already. No historical-case insight (that table
+    lives with the agent)."""
+
+    def __init__(self, llm):
+        from ..serve.llm import Analyzer
+
+        self.analyzer = Analyzer(llm)
+
+    def classify_and_explain(self, dialogue: str, temperature: float = 0.7, prediction: Optional[dict] = None,
+                             with_history: bool = True) -> dict:
+        analysis = self.analyzer.analyze_prediction(dialogue, prediction["prediction"], prediction["confidence"],
+                                                    temperature)
+        return dict(prediction, analysis=analysis, historical_insight=None)
+
+
+def _explain_kw(spec: dict) -> dict:
+    """Engine arguments of a run's ``explain`` mode ("none" | "async" | "sync"); the LLM backend is
+    ``spec["llm"]`` (serve/llm.py make_llm names; "stub" = the offline stub, optional latency)."""
+    mode = spec.get("explain", "none")
+    if mode == "none":
+        return {}
+    from ..serve.llm import StubLLM, make_llm
+
+    backend = spec.get("llm", "stub")
+    llm = StubLLM(latency_s=spec.get("llm_latency_s", 0.0)) if backend == "stub" else make_llm(backend)
+    return {"explain": mode, "agent": _ClientExplainer(llm), "explain_every": int(spec.get("explain_every", 1))}
 
 
 def _client_serve(cfg: dict, spec: dict, scorer: RemoteScorer, ring: SharedRing) -> dict:
@@ -448,7 +480,7 @@ def _client_serve(cfg: dict, spec: dict, scorer: RemoteScorer, ring: SharedRing)
         eng = StreamingEngine(scorer, remote_postprocess, cons, kafka.get_kafka_producer(),
                               spec.get("output_topic") or os.getenv("KAFKA_OUTPUT_TOPIC", kafka.DEFAULT_OUTPUT),
                               batch_max=cfg["batch_max"], max_latency_ms=cfg["max_latency_ms"],
-                              max_bytes=cfg["layout"]["max_bytes"], ring=ring)
+                              max_bytes=cfg["layout"]["max_bytes"], ring=ring, **_explain_kw(spec))
         t0 = time.perf_counter()
         st = eng.run(max_messages=spec.get("max_messages"), idle_timeout_s=spec.get("idle_timeout", float("inf")))
         t1 = time.perf_counter()

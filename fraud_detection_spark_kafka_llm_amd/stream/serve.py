@@ -11,7 +11,8 @@ keyed like the input; offsets are committed after the outputs are produced (at-l
 With --gpus N the micro-batches of the consumer are spread over N devices of this process.
 With --group-clients P the Kafka clients run as P consumer-group member processes (one GIL each,
 stream/group.py) around this process's GPU scorer; the broker balances the topic's partitions over
-them (a real bootstrap only: a memory:// broker lives inside one process; --explain none).
+them (a real bootstrap only: a memory:// broker lives inside one process). Explanations run in
+the client processes (no historical-case insight there).
 ``/metrics`` serves the Prometheus text format of the metrics registry when --metrics-port is set.
 """
 from __future__ import annotations
@@ -111,8 +112,6 @@ def _serve_group(args, agent, devices, out_topic: str) -> int:
     from .gpu_worker import make_multi_scorer
     from .group import ConsumerGroup, merge_results
 
-    if args.explain != "none":
-        raise SystemExit("--group-clients serves classifications only (--explain none)")
     if os.getenv("KAFKA_BOOTSTRAP_SERVERS", "").startswith("memory://") or os.getenv("FDX_KAFKA", "") == "memory":
         raise SystemExit("--group-clients needs a real Kafka bootstrap (an in-memory broker is per process)")
     fp = agent.fused
@@ -127,7 +126,8 @@ def _serve_group(args, agent, devices, out_topic: str) -> int:
         P, m = args.group_clients, args.max_messages
         share = None if m is None else [{"max_messages": m // P + (1 if c < m % P else 0)} for c in range(P)]
         rs = grp.run({"kind": "serve", "max_messages": m, "idle_timeout": args.idle_timeout,
-                      "output_topic": out_topic}, share)
+                      "output_topic": out_topic, "explain": args.explain,
+                      "llm": os.environ.get("FDX_LLM_BACKEND") or "deepseek"}, share)
     print(json.dumps({k: v for k, v in merge_results(rs).items() if k != "client_dialogues_per_s"}), flush=True)
     return 0
 

@@ -89,6 +89,24 @@ def test_group_latency_run(agent):
     assert 0 < r["p50_ms"] <= r["p95_ms"]
 
 
+def test_group_async_explanations(agent):
+    """Config 5's LLM-explain stub in the client processes: every 5th classification gets an
+    explanation record; classifications are produced and committed as without it."""
+    pt, _ = synth.generate(synth.SynthConfig(n=200, seed=7), device="cpu")
+    pool = MessagePool(pt.strings())
+    fp = agent.fused
+    sc = make_scorer(fp.spec(True), fp.idf.idf, fp.model.scorer(), "cpu", max_docs=128, max_bytes=128 * 4096)
+    with G.ConsumerGroup(sc, fp.model.postprocess_numpy, 2, batch_max=128, max_latency_ms=1.0,
+                         max_bytes=128 * 4096, pool=pool) as grp:
+        r = G.group_throughput_run(grp, 1000, explain="async", explain_every=5, return_outputs=True)
+    assert r["produced"] == r["committed"] == 1000
+    assert r["explanations"] == 200
+    recs = [json.loads(v) for outs in r["outputs"] for _, v in outs]
+    expl = [x for x in recs if x.get("type") == "explanation"]
+    assert len(expl) == 200 and all("stub-llm" in x["analysis"] for x in expl)
+    assert len(recs) - len(expl) == 1000
+
+
 def test_client_failure_surfaces(agent):
     fp = agent.fused
     sc = make_scorer(fp.spec(True), fp.idf.idf, fp.model.scorer(), "cpu", max_docs=64, max_bytes=64 * 4096)
