@@ -1,0 +1,60 @@
+"""Where gbdt_featurize_sec goes at 10M rows: pinned H2D alone, featurize_shard (H2D overlapped
+with the fused featurize kernel), feature_order (CSR -> CSC radix sort + docFreq), twice each.
+python bench/probes/feat_probe.py [--rows 10000000]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench as B  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops import text as T  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    B.bind_to_gpu(0)
+    spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=1 << 18)
+    chunks = B.generate_shard(0, a.rows, dev, seed=11)
+    nbytes = sum(h.data.numel() + h.offsets.numel() * 8 for h, _ in chunks)
+    small = B.generate_shard(0, 200_000, dev, seed=3)
+    B.featurize_shard(small, dev, spec)
+    torch.cuda.synchronize()
+    for rep in range(2):
+        t0 = time.perf_counter()
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            outs = [h.to(dev, non_blocking=True) for h, _ in chunks[:6]]
+        s.synchronize()
+        t_h2d6 = time.perf_counter() - t0
+        del outs
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        indptr, idx, counts, y = B.featurize_shard(chunks, dev, spec)
+        torch.cuda.synchronize()
+        t_feat = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        fo = feature_order(indptr, idx, counts, 1 << 18)
+        torch.cuda.synchronize()
+        t_fo = time.perf_counter() - t0
+        print(json.dumps({"rep": rep, "rows": a.rows, "text_gb": nbytes / 1e9, "nnz": int(idx.numel()),
+                          "h2d_6chunks_gbps": sum(h.data.numel() + h.offsets.numel() * 8 for h, _ in chunks[:6]) / t_h2d6 / 1e9,
+                          "featurize_shard_s": t_feat, "feature_order_s": t_fo,
+                          "featurize_gbps": nbytes / t_feat / 1e9}), flush=True)
+        del indptr, idx, counts, y, fo
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
