@@ -309,3 +309,14 @@ def test_gpu_scorer_long_dialogues_match_host():
     gpu = GpuScorer(spec, idf, lr, "cuda:0", max_docs=256, max_bytes=1 << 20)
     host = HostScorer(spec, idf, lr, max_docs=256, max_bytes=1 << 20)
     np.testing.assert_array_equal(gpu.score_packed(ring.slots[0]), host.score_packed(ring.slots[0]))
+
+
+def test_serve_group_clients_refuses_in_memory_broker(tmp_path, monkeypatch):
+    """--group-clients runs the Kafka clients in other processes: an in-process memory:// broker
+    cannot be shared with them, so the CLI refuses it instead of serving an empty topic."""
+    from fraud_detection_spark_kafka_llm_amd.stream import serve
+
+    model_dir = _trained_model_dir(tmp_path, "lr")
+    monkeypatch.setenv("KAFKA_BOOTSTRAP_SERVERS", "memory://serve-group")
+    with pytest.raises(SystemExit, match="real Kafka bootstrap"):
+        serve.main(["--model", model_dir, "--gpus", "0", "--group-clients", "2", "--max-messages", "10"])
