@@ -64,7 +64,7 @@ from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
 from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.ops import text as T  # noqa: E402
-from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order  # noqa: E402
+from fraud_detection_spark_kafka_llm_amd.ops.sparse import IncrementalFeatureOrder, feature_order  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.parallel import dist as D  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.parallel.affinity import bind_to_gpu  # noqa: E402
 from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import GpuScorer  # noqa: E402
@@ -101,16 +101,22 @@ def generate_shard(lo: int, hi: int, dev, seed: int, chunk: int = 500_000) -> li
     return out
 
 
-def featurize_shard(chunks: list, dev, spec):
+def featurize_shard(chunks: list, dev, spec, order: bool = False):
     """H2D + fused clean/tokenize/stop-words/murmur3 HashingTF of every chunk -> one CSR.
 
     The H2D of chunk i+1 runs on a copy stream (SDMA) while chunk i is featurized on the
-    compute stream, so the PCIe transfer of the raw text hides behind the kernel."""
+    compute stream, so the PCIe transfer of the raw text hides behind the kernel. With
+    ``order`` each chunk's entries are also sorted by feature right after its featurization
+    (ops/sparse.py IncrementalFeatureOrder), still underneath the next chunk's H2D: the
+    CSR -> CSC sort (docFreq for the IDF, the trainer's columns) is no longer a serial ~0.25 s
+    pass after the transfer (profiles/r3s4/featurize_probe_10M.jsonl). Returns the CSR (+ the
+    FeatureOrder when ``order``)."""
     rows = sum(int(h.offsets.numel()) - 1 for h, _ in chunks)
     indptr = torch.zeros(rows + 1, dtype=torch.int64, device=dev)
     labels = torch.empty(rows, dtype=torch.float64, device=dev)
     idx = counts = None
     off = r = 0
+    inc = IncrementalFeatureOrder(F, dev) if order else None
     comp = torch.cuda.current_stream(dev)
     copy = comp if os.environ.get("FDX_BENCH_SERIAL_H2D") == "1" else torch.cuda.Stream(dev)
 
@@ -149,12 +155,16 @@ def featurize_shard(chunks: list, dev, spec):
         counts[off:off + k] = v
         indptr[r + 1:r + n + 1] = ip[1:] + off
         labels[r:r + n] = yd
+        if inc is not None:
+            inc.add(ip, ix, v, r)
         off += k
         r += n
         del ip, ix, v, yd
     if idx is None:
         idx = torch.empty(0, dtype=torch.int32, device=dev)
         counts = torch.empty(0, dtype=torch.int32, device=dev)
+    if inc is not None:
+        return indptr, idx[:off], counts[:off], labels, inc.finish() if chunks else feature_order(indptr, idx, counts, F)
     return indptr, idx[:off], counts[:off], labels
 
 
@@ -351,8 +361,8 @@ def main():
     gen_sec = max_over_ranks(time.perf_counter() - t0, dev)
     sync_all(dev)
     t0 = time.perf_counter()
-    indptr, idx, counts, y = featurize_shard(chunks, dev, spec)
-    fo = feature_order(indptr, idx, counts, F)          # CSC by feature: docFreq now, quantize later
+    # CSR + CSC by feature (docFreq now, the trainer's columns later), the sort overlapped with H2D
+    indptr, idx, counts, y, fo = featurize_shard(chunks, dev, spec, order=True)
     df = D.all_reduce_sum(fo.df)
     idf = torch.log((args.rows + 1.0) / (df.double() + 1.0))
     vc = VectorColumn.tfidf(F, indptr, idx, counts, idf, fo)

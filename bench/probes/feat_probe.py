@@ -48,11 +48,18 @@ def main():
         fo = feature_order(indptr, idx, counts, 1 << 18)
         torch.cuda.synchronize()
         t_fo = time.perf_counter() - t0
+        del fo
+        t0 = time.perf_counter()
+        *_, fo2 = B.featurize_shard(chunks, dev, spec, order=True)
+        torch.cuda.synchronize()
+        t_both = time.perf_counter() - t0
+        del fo2
         print(json.dumps({"rep": rep, "rows": a.rows, "text_gb": nbytes / 1e9, "nnz": int(idx.numel()),
                           "h2d_6chunks_gbps": sum(h.data.numel() + h.offsets.numel() * 8 for h, _ in chunks[:6]) / t_h2d6 / 1e9,
                           "featurize_shard_s": t_feat, "feature_order_s": t_fo,
+                          "featurize_with_overlapped_order_s": t_both,
                           "featurize_gbps": nbytes / t_feat / 1e9}), flush=True)
-        del indptr, idx, counts, y, fo
+        del indptr, idx, counts, y
         torch.cuda.empty_cache()
 
 

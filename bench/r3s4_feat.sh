@@ -1,0 +1,12 @@
+# Overlapped CSC sort: GPU tests, featurize probe, full bench. Usage: bash bench/r3s4_feat.sh <tag>
+set -e
+OUT=gpurun_out/${1:-r3s4_feat}
+mkdir -p $OUT
+export TMPDIR=/tmp
+cat /proc/loadavg
+timeout -k 10 600 python -u -m pytest tests/test_feature_order.py tests/test_bench_contract.py -m gpu -x -v --timeout 500 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
+tail -3 $OUT/pytest.log
+timeout -k 10 300 python3 -u bench/probes/feat_probe.py > $OUT/feat_probe.jsonl 2>&1 || { tail -30 $OUT/feat_probe.jsonl; exit 1; }
+cat $OUT/feat_probe.jsonl
+timeout -k 10 900 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json

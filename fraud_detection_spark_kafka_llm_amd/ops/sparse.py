@@ -126,12 +126,12 @@ def feature_order(indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor,
     if nnz <= block:
         colptr, df, maxc = _feature_order_one(indptr, idx, counts, num_features, row_buf, cnt_buf)
         return FeatureOrder(row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)
-    C = native.lib()
     N = int(indptr.numel() - 1)
     # row blocks of <= ~block entries (a single row larger than a block is its own block)
     targets = torch.arange(block, nnz, block, dtype=torch.int64, device=dev)
     cuts = torch.searchsorted(indptr, targets, right=True).clamp(1, N) - 1
     rcuts = sorted(set([0, N] + [int(c) for c in cuts.cpu().tolist() if 0 < int(c) < N]))
+    C = native.lib()
     # pass 1: per-block column sizes (one bincount per block) -> every block's column offsets
     lens = []
     for r0, r1 in zip(rcuts[:-1], rcuts[1:]):
@@ -143,7 +143,8 @@ def feature_order(indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor,
     df = tot
     maxc = torch.zeros(num_features, dtype=torch.int32, device=dev)
     before = torch.zeros(num_features, dtype=torch.int64, device=dev)
-    # pass 2: sort each block, add its first row, copy its columns into place
+    # pass 2: sort each block, add its first row, copy its columns into place (one block's
+    # temporaries alive at a time; IncrementalFeatureOrder keeps every block until the end)
     for (r0, r1), ln in zip(zip(rcuts[:-1], rcuts[1:]), lens):
         e0, e1 = int(indptr[r0]), int(indptr[r1])
         n = e1 - e0
@@ -157,3 +158,54 @@ def feature_order(indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor,
         before += ln
         del brow, bcnt, bcol
     return FeatureOrder(row_buf[:nnz], cnt_buf[:nnz], colptr, df, maxc)
+
+
+class IncrementalFeatureOrder:
+    """feature_order built one row block at a time, as the blocks arrive (e.g. each featurized
+    chunk while the next chunk's raw text is still crossing PCIe): every block is sorted by
+    feature on its own (``add``), and ``finish`` copies each block's columns into place behind the
+    earlier blocks' entries of the same column. Rows stay ascending within every column, so the
+    result equals the one-shot CSC of the concatenated CSR. Holds every block's sorted (row, count)
+    pairs until ``finish`` (5 B per entry on top of the CSR, then the same again for the output)."""
+
+    PAD = 16
+
+    def __init__(self, num_features: int, device):
+        self.F, self.dev = int(num_features), torch.device(device)
+        self.blocks: list = []               # (block colptr, rows (global), counts u8, n entries)
+        self.maxc = torch.zeros(self.F, dtype=torch.int32, device=self.dev)
+        self.nnz = 0
+
+    def add(self, indptr: torch.Tensor, idx: torch.Tensor, counts: torch.Tensor, first_row: int) -> None:
+        """Sort one block: ``indptr`` local to the block (starts at 0), rows ``first_row + i``."""
+        if counts.dtype not in (torch.float32, torch.float64, torch.int32):
+            counts = counts.to(torch.float32 if counts.is_floating_point() else torch.int32)
+        n = int(idx.numel())
+        brow = torch.zeros(n + self.PAD, dtype=torch.int32, device=self.dev)
+        bcnt = torch.zeros(n + self.PAD, dtype=torch.uint8, device=self.dev)
+        bcol, _, bmax = _feature_order_one(indptr, idx, counts, self.F, brow, bcnt)
+        if first_row:
+            brow[:n] += int(first_row)
+        torch.maximum(self.maxc, bmax, out=self.maxc)
+        self.blocks.append((bcol, brow, bcnt, n))
+        self.nnz += n
+
+    def finish(self) -> FeatureOrder:
+        nnz, dev = self.nnz, self.dev
+        lens = [bcol[1:] - bcol[:-1] for bcol, _, _, _ in self.blocks]
+        tot = torch.stack(lens).sum(0) if lens else torch.zeros(self.F, dtype=torch.int64, device=dev)
+        colptr = torch.zeros(self.F + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(tot, 0, out=colptr[1:])
+        if len(self.blocks) == 1:               # one block: its sort is the CSC
+            _, brow, bcnt, n = self.blocks.pop()
+            return FeatureOrder(brow[:n], bcnt[:n], colptr, tot, self.maxc)
+        row_buf = torch.zeros(nnz + self.PAD, dtype=torch.int32, device=dev)
+        cnt_buf = torch.zeros(nnz + self.PAD, dtype=torch.uint8, device=dev)
+        before = torch.zeros(self.F, dtype=torch.int64, device=dev)
+        C = native.lib()
+        for (bcol, brow, bcnt, n), ln in zip(self.blocks, lens):
+            C.copy_segments(brow[:n], bcnt[:n], bcol[:-1].contiguous(), (colptr[:-1] + before).contiguous(), ln,
+                            row_buf[:nnz], cnt_buf[:nnz], None)
+            before += ln
+        self.blocks = []
+        return FeatureOrder(row_buf[:nnz], cnt_buf[:nnz], colptr, tot, self.maxc)

@@ -34,3 +34,19 @@ def test_row_blocked_feature_order_equals_one_shot(dev):
     order = np.argsort(idx.cpu().numpy(), kind="stable")
     assert np.array_equal(one.csc_row.cpu().numpy(), row[order])
     assert np.array_equal(one.csc_cnt.cpu().numpy(), np.minimum(cnt.cpu().numpy()[order], 255))
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_incremental_feature_order_equals_one_shot(dev):
+    """Blocks sorted as they arrive (bench featurize overlap) give exactly the one-shot CSC."""
+    from fraud_detection_spark_kafka_llm_amd.ops.sparse import IncrementalFeatureOrder
+
+    indptr, idx, cnt, f = _csr(seed=3)
+    indptr, idx, cnt = indptr.to(dev), idx.to(dev), cnt.to(dev)
+    one = feature_order(indptr, idx, cnt, f)
+    for cuts in ([0, 5000], [0, 1, 1234, 1235, 4000, 5000], [0, 2500, 5000]):
+        inc = IncrementalFeatureOrder(f, dev)
+        for r0, r1 in zip(cuts[:-1], cuts[1:]):
+            e0, e1 = int(indptr[r0]), int(indptr[r1])
+            inc.add(indptr[r0:r1 + 1] - e0, idx[e0:e1], cnt[e0:e1], r0)
+        _same(one, inc.finish())
