@@ -119,22 +119,33 @@ def featurize_shard(chunks: list, dev, spec, order: bool = False):
     inc = IncrementalFeatureOrder(F, dev) if order else None
     comp = torch.cuda.current_stream(dev)
     copy = comp if os.environ.get("FDX_BENCH_SERIAL_H2D") == "1" else torch.cuda.Stream(dev)
+    # two device staging buffers, allocated once (a fresh ~1 GB allocation per chunk on the copy
+    # stream left ~94 GB reserved and made the first pass 2x slower: profiles/r3s4/NOTES.md)
+    mb = max((int(h.data.numel()) for h, _ in chunks), default=0)
+    md = max((int(h.offsets.numel()) for h, _ in chunks), default=0)
+    bufs = [(torch.empty(mb, dtype=torch.uint8, device=dev), torch.empty(md, dtype=torch.int64, device=dev),
+             torch.empty(md, dtype=torch.float64, device=dev)) for _ in range(2 if chunks else 0)]
+    freed = [None, None]                 # comp-stream event: staging buffer j consumed
 
     def stage(i):
         host, y = chunks[i]
+        j = i % 2
+        bd, bo, by = bufs[j]
+        nb, no = int(host.data.numel()), int(host.offsets.numel())
         with torch.cuda.stream(copy):
-            d = host.to(dev, non_blocking=True)
-            yd = y.to(dev, non_blocking=True)
+            if freed[j] is not None:
+                copy.wait_event(freed[j])
+            bd[:nb].copy_(host.data, non_blocking=True)
+            bo[:no].copy_(host.offsets, non_blocking=True)
+            by[:no - 1].copy_(y, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(copy)
-        return d, yd, ev
+        return T.PackedText(bd[:nb], bo[:no]), by[:no - 1], ev
 
     nxt = stage(0) if chunks else None
     for i in range(len(chunks)):
         d, yd, ev = nxt
         comp.wait_event(ev)
-        for t in (d.data, d.offsets, yd):   # allocated on the copy stream, consumed on comp
-            t.record_stream(comp)
         if i + 1 < len(chunks):
             nxt = stage(i + 1)
         res = T.featurize_score(d, spec, want_csr=True, device=dev)
@@ -157,6 +168,7 @@ def featurize_shard(chunks: list, dev, spec, order: bool = False):
         labels[r:r + n] = yd
         if inc is not None:
             inc.add(ip, ix, v, r)
+        freed[i % 2] = comp.record_event()   # staging buffer free for chunk i + 2
         off += k
         r += n
         del ip, ix, v, yd

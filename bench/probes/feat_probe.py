@@ -21,11 +21,27 @@ from fraud_detection_spark_kafka_llm_amd.ops.sparse import feature_order  # noqa
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--cold", action="store_true", help="as in bench.py: only its warm-up fit, then the "
+                    "overlapped featurize twice (first = cold caching allocator)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     B.bind_to_gpu(0)
     spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=1 << 18)
+    if a.cold:
+        from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams
+
+        B.warmup_training(dev, spec, GBDTParams(n_estimators=100, max_depth=6), 5)
+        chunks = B.generate_shard(0, a.rows, dev, seed=11)
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = B.featurize_shard(chunks, dev, spec, order=True)
+            torch.cuda.synchronize()
+            print(json.dumps({"cold_rep": rep, "featurize_with_overlapped_order_s": time.perf_counter() - t0,
+                              "reserved_gb": torch.cuda.memory_reserved() / 2**30}), flush=True)
+            del out
+        return
     chunks = B.generate_shard(0, a.rows, dev, seed=11)
     nbytes = sum(h.data.numel() + h.offsets.numel() * 8 for h, _ in chunks)
     small = B.generate_shard(0, 200_000, dev, seed=3)
