@@ -231,39 +231,51 @@ def group_kafka(args, spec, idf_np, model, dev, pool) -> dict:
     """Config 5 through the confluent surface as a consumer group (stream/group.py): one client
     process per partition of the 3-partition topic (poll -> extract -> produce + commit, each
     with its own GIL) around this rank's GPU scoring process (shared-memory slots, one GpuScorer).
-    Rank 0 only; the others wait."""
+    Rank 0 only; the others wait. A failure is reported in the record, not raised."""
+    out = {}
+    if D.rank() == 0:
+        try:
+            out = _group_kafka_runs(args, spec, idf_np, model, dev, pool)
+        except Exception as e:     # the headline line must still be printed: report, do not abort
+            import traceback
+
+            traceback.print_exc()
+            out = {"kafka_confluent_group_error": f"{type(e).__name__}: {e}"}
+    D.barrier()
+    return out
+
+
+def _group_kafka_runs(args, spec, idf_np, model, dev, pool) -> dict:
+    """The consumer-group runs: warm-up, throughput, paced latency, latency with explanations."""
     import gc
 
     from fraud_detection_spark_kafka_llm_amd.stream import group as G
 
-    out = {}
-    if D.rank() == 0:
-        batch = 16384
-        sc = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=batch, max_bytes=batch * 4096, depth=3)
-        gc.collect()
-        with G.ConsumerGroup(sc, model.postprocess_numpy, args.kafka_group_clients, batch_max=batch,
-                             max_latency_ms=5.0, max_bytes=batch * 4096, pool=pool, confluent=True) as grp:
-            G.group_throughput_run(grp, 60_000, tag="warm")
-            tp = G.group_throughput_run(grp, args.kafka_group_msgs, tag="tp")
-            lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
-            # the config's LLM-explain stub: every 10th classification explained asynchronously
-            # in the clients (offline stub backend), its record produced after the classification
-            ex = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat-explain", explain="async",
-                                     explain_every=10)
-        out = {"kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
-               "kafka_confluent_group_clients": args.kafka_group_clients,
-               "kafka_confluent_group_msgs": args.kafka_group_msgs,
-               "kafka_confluent_group_p50_ms": lat["p50_ms"], "kafka_confluent_group_p95_ms": lat["p95_ms"],
-               "kafka_confluent_group_offered_per_s": args.kafka_group_rate,
-               "kafka_confluent_group_explain_p50_ms": ex["p50_ms"],
-               "kafka_confluent_group_explain_p95_ms": ex["p95_ms"],
-               "kafka_confluent_group_explanations": ex["explanations"],
-               "kafka_confluent_group_all_committed": bool(
-                   tp["produced"] == tp["committed"] == args.kafka_group_msgs and
-                   lat["produced"] == lat["committed"] == lat["sent"] and
-                   ex["produced"] == ex["committed"] == ex["sent"] and ex["explanations"] > 0)}
-        del sc
-    D.barrier()
+    batch = 16384
+    sc = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=batch, max_bytes=batch * 4096, depth=3)
+    gc.collect()
+    with G.ConsumerGroup(sc, model.postprocess_numpy, args.kafka_group_clients, batch_max=batch,
+                         max_latency_ms=5.0, max_bytes=batch * 4096, pool=pool, confluent=True) as grp:
+        G.group_throughput_run(grp, 60_000, tag="warm")
+        tp = G.group_throughput_run(grp, args.kafka_group_msgs, tag="tp")
+        lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
+        # the config's LLM-explain stub: every 10th classification explained asynchronously
+        # in the clients (offline stub backend), its record produced after the classification
+        ex = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat-explain", explain="async",
+                                 explain_every=10)
+    out = {"kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
+           "kafka_confluent_group_clients": args.kafka_group_clients,
+           "kafka_confluent_group_msgs": args.kafka_group_msgs,
+           "kafka_confluent_group_p50_ms": lat["p50_ms"], "kafka_confluent_group_p95_ms": lat["p95_ms"],
+           "kafka_confluent_group_offered_per_s": args.kafka_group_rate,
+           "kafka_confluent_group_explain_p50_ms": ex["p50_ms"],
+           "kafka_confluent_group_explain_p95_ms": ex["p95_ms"],
+           "kafka_confluent_group_explanations": ex["explanations"],
+           "kafka_confluent_group_all_committed": bool(
+               tp["produced"] == tp["committed"] == args.kafka_group_msgs and
+               lat["produced"] == lat["committed"] == lat["sent"] and
+               ex["produced"] == ex["committed"] == ex["sent"] and ex["explanations"] > 0)}
+    del sc
     return out
 
 
