@@ -264,6 +264,14 @@ class ConsumerGroup:
         return [cl.reply for cl in self.clients]
 
     def close(self) -> None:
+        # no DMA may still read a segment when it is unregistered and unmapped (a run that raised
+        # can leave micro-batches in the scorer's pipeline)
+        try:
+            while self.scorer.inflight:
+                self.scorer.collect(copy=False)
+        finally:
+            if self.register and torch.cuda.is_available():
+                torch.cuda.synchronize()
         for cl in self.clients:
             try:
                 self._send_ctl(cl, ("exit", {}))
