@@ -133,7 +133,9 @@ def bench_gbdt_1m(args) -> dict:
 def bench_rf(args) -> dict:
     """BASELINE config 3: --rows is the GLOBAL row count (default 10M), row-sharded over the
     torchrun ranks; trees equal the single-process forest (exact histograms, tests/test_distributed.py)."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
 
     rank, world, dev = _dist()
     rows = args.rows or 10_000_000
@@ -145,6 +147,7 @@ def bench_rf(args) -> dict:
     _sync(dev)
     t_feat = time.perf_counter() - t0
     torch.cuda.reset_peak_memory_stats(dev)
+    grower.reset_level_stats()
     res = fit_forest(vc, y, num_trees=trees, max_depth=5, max_bins=32, bootstrap=True, feature_subset=args.subset,
                      seed=42, device=dev)
     _sync(dev)
@@ -152,7 +155,10 @@ def bench_rf(args) -> dict:
     out = {"bench": "rf", "rows": rows, "world": world, "rows_per_rank": len(vc), "trees": trees, "depth": 5,
            "subset": args.subset, "featurize_s": _max_over_ranks(t_feat, dev),
            "train_s": _max_over_ranks(t_train, dev), "train_only_s": _max_over_ranks(t_train - t_feat, dev),
-           "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}
+           "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev),
+           "lanes": res.lanes, "collectives": bool(D.Collectives().active),
+           "level_collective_calls": grower.LEVEL_STATS["coll_calls"],
+           "level_collective_ms": _max_over_ranks(grower.level_collective_ms(), dev)}
     if rank == 0:
         tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
         raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()

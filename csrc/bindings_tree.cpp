@@ -830,6 +830,10 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
   fdx::SplitArgs a{};
   a.hist = hist.data_ptr<int64_t>();
   a.totals = totals.data_ptr<int64_t>();
+  // the node row stride is the tensor's own ([nodes, stride, 2]): a data-parallel level searches
+  // the reduce-scattered [n, Bs, 2] rows in place (Bs >= this shard's bins)
+  FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && hist.size(0) >= nodes, "hist must be [nodes, stride, 2]");
+  a.hist_stride = hist.size(1);
   a.num_nodes = nodes;
   a.Fa = Fa;
   a.boff = boff.data_ptr<int64_t>();

@@ -361,8 +361,9 @@ struct DenseHistArgs {
 };
 
 struct SplitArgs {
-  const int64_t* hist;            // [nodes][TB][2]
+  const int64_t* hist;            // [nodes][hist_stride][2]
   const int64_t* totals;          // [nodes][2]
+  int64_t hist_stride;            // bins per node row of hist (0: boff[Fa])
   int32_t num_nodes;
   int32_t Fa;
   const int64_t* boff;

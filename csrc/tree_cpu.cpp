@@ -343,7 +343,7 @@ void split_cpu(const SplitArgs& a) {
         use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <=
               a.feat_thr[n];
       if (use) {
-        const int64_t* hb = a.hist + ((int64_t)n * a.boff[a.Fa] + a.boff[f]) * 2;
+        const int64_t* hb = a.hist + ((int64_t)n * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
         gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], s0, s1, a.mode,
                                a.lambda_, a.min_child_weight, &bin, &l0, &l1);
       }

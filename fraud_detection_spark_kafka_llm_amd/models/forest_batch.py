@@ -11,9 +11,22 @@ Here up to ``TREES_IN_FLIGHT`` trees run the device level loop (grower.device_tr
 each on its own HIP stream with its own workspace (digit words, row -> node map, level state:
 ~0.2 GB per lane at 10M rows). One host thread drives them: whenever a tree reaches a point where
 it needs a device result (the next level's 16-byte counts, its finished node table) the driver
-moves on to another tree whose result is ready, so the kernels of different trees overlap on the
-device. Every tree depends only on (seed, tree index) and its own buffers, so the forest is
-bitwise the forest of one-at-a-time growth (tested on the host and the GPU).
+moves on to another tree, so the kernels of different trees overlap on the device. Every tree
+depends only on (seed, tree index) and its own buffers, so the forest is bitwise the forest of
+one-at-a-time growth (tested on the host and the GPU).
+
+Data parallelism (BASELINE config 3, RF at DP=8): each lane's levels issue a reduce-scatter and an
+all-gather on the ONE communicator, so every rank must issue them in the same order. Alone, the
+driver advances "the first lane whose event completed", an order that depends on timing; under
+collectives it advances lanes strictly in FIFO order of their pending events (always the oldest),
+an order fixed by the tree shapes, which every rank computes identically from the same reduced
+histograms. The lanes' collectives then queue on the communicator's stream in the same sequence
+everywhere, and while one lane's collective is in flight the other lanes' kernels keep the GPU
+busy (a lone tree at DP=8 does 1/8 of the histogram work per level and is latency bound).
+
+The shared read-only state the lanes read (the CSC work items and their wave order, the shard
+tables) is built on the caller's stream BEFORE the lanes fork from it, never lazily by whichever
+lane touches it first (that would leave the other lanes' streams unordered with the build).
 
 (An earlier design grew 8 trees in lockstep through one multi-tree histogram kernel with 24 bytes
 of per-row records; it lost to per-tree passes, profiles/r2_rf_batch_ab.txt, and was replaced.)
@@ -48,11 +61,30 @@ class ForestLanes:
         return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
 
 
+def build_shared_state(Q: Quantized, lanes: ForestLanes, coll=None) -> list:
+    """Build every lazily created structure more than one lane reads, on the current stream:
+    the CSC histogram items (Q.groups, Q.hot_groups, Q.h_row/h_key) and each group's wave order;
+    under data parallelism each lane's feature-shard tables. Returns the per-lane shards (or
+    Nones)."""
+    for grp in Q.groups + Q.hot_groups:
+        if grp.num_items:
+            grp.wave_order()
+    Q.h_row, Q.h_key                                           # noqa: B018 (built by the access)
+    if coll is not None and coll.active and (coll.world > 1 or getattr(coll, "force", False)):
+        return [ws.shards(coll) for ws in lanes.ws]
+    return [None] * len(lanes.ws)
+
+
 def grow_forest_concurrent(Q: Quantized, lanes: ForestLanes, params: GrowParams, tree_ids: list,
-                           label: torch.Tensor, weight: Optional[torch.Tensor], bootstrap: bool) -> list:
-    """Grow the trees ``tree_ids`` with up to ``len(lanes.ws)`` in flight; returns them in order."""
+                           label: torch.Tensor, weight: Optional[torch.Tensor], bootstrap: bool,
+                           coll=None) -> list:
+    """Grow the trees ``tree_ids`` with up to ``len(lanes.ws)`` in flight; returns them in order.
+    ``coll`` (parallel.dist.Collectives, active): data-parallel levels, lanes advanced in FIFO
+    order so that every rank issues the same collective sequence."""
     cuda = lanes.dev.type == "cuda"
-    if cuda:                                   # the lanes see everything queued before (Q, label)
+    use_coll = coll is not None and coll.active
+    shards = build_shared_state(Q, lanes, coll if use_coll else None)
+    if cuda:                                   # the lanes see everything queued before (Q, label, shared state)
         main = torch.cuda.current_stream(lanes.dev)
         start = main.record_event()
         for s in lanes.streams:
@@ -79,18 +111,24 @@ def grow_forest_concurrent(Q: Quantized, lanes: ForestLanes, params: GrowParams,
             return
         t = todo.popleft()
         with tracing.span("forest.tree", tree=t, lane=i):
-            live[i] = [t, device_tree_steps(Q, lanes.ws[i], params, t, None, None, weight, label=label,
+            live[i] = [t, device_tree_steps(Q, lanes.ws[i], params, t, None, None, weight,
+                                            coll if use_coll else None, shards[i], label=label,
                                             bootstrap=bootstrap), None]
         advance(i)
 
     for i in range(len(lanes.ws)):
         launch(i)
     while order:
-        # the first lane whose event completed, else wait for the oldest one
-        ready = next((i for i in order if live[i][2].query()), None)
-        if ready is None:
+        if use_coll:
+            # rank-deterministic: always the oldest pending event (the collective order follows)
             ready = order[0]
             live[ready][2].synchronize()
+        else:
+            # the first lane whose event completed, else wait for the oldest one
+            ready = next((i for i in order if live[i][2].query()), None)
+            if ready is None:
+                ready = order[0]
+                live[ready][2].synchronize()
         order.remove(ready)
         advance(ready)
     if cuda:

@@ -22,6 +22,7 @@ from __future__ import annotations
 import functools
 import math
 import os
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -61,7 +62,57 @@ HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
 # instead of a global gather per entry (FDX_BLK=0: the CSC / dense passes at every level)
 # device level loop counters (bench/gbdt_train.py reports the histogram payload per level: what a
 # data-parallel level reduce-scatters, before the 1/S shard split)
-LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0}
+LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0, "coll_calls": 0, "coll_ms": 0.0}
+# (begin, end) timing events of the data-parallel levels' collectives, resolved lazily by
+# level_collective_ms() so that timing never adds a host wait to the level loop
+_COLL_EVENTS: list = []
+
+
+def reset_level_stats() -> None:
+    _COLL_EVENTS.clear()
+    for k in LEVEL_STATS:
+        LEVEL_STATS[k] = 0
+
+
+def level_collective_ms() -> float:
+    """Milliseconds the level loops' streams spent in their reduce-scatter + all-gather (device
+    event pairs around the collectives, as the issuing stream sees them: a lane whose collective
+    queues behind another lane's on the communicator's stream counts that wait too)."""
+    while _COLL_EVENTS:
+        b, e = _COLL_EVENTS.pop(0)
+        e.synchronize()
+        LEVEL_STATS["coll_ms"] += b.elapsed_time(e)
+    return float(LEVEL_STATS["coll_ms"])
+
+
+class _CollTimer:
+    """Times one level's collectives on the current stream (device events; host clock on the CPU)."""
+
+    def __init__(self, dev: torch.device):
+        self.cuda = dev.type == "cuda"
+
+    def __enter__(self):
+        if self.cuda:
+            self.b = torch.cuda.Event(enable_timing=True)
+            self.b.record()
+        else:
+            self.b = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        LEVEL_STATS["coll_calls"] += 1
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            _COLL_EVENTS.append((self.b, e))
+            if len(_COLL_EVENTS) > 8192:        # bounded: resolve the oldest half (long finished)
+                for b, e in _COLL_EVENTS[:4096]:
+                    e.synchronize()
+                    LEVEL_STATS["coll_ms"] += b.elapsed_time(e)
+                del _COLL_EVENTS[:4096]
+        else:
+            LEVEL_STATS["coll_ms"] += (time.perf_counter() - self.b) * 1e3
+        return False
 BLK = os.environ.get("FDX_BLK", "0") == "1"      # row-blocked pass: opt-in until it beats the CSC passes
 BLK_MAX_SLOTS = 4
 # row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
@@ -531,17 +582,23 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                                       params, feat_thr, tree_index, Q.Fa, 0)
                 packed = packed.cpu().numpy()
         else:
-            with tracing.span("tree.reduce_scatter"):
-                cur_hist = torch.zeros((nl, shards.bins, 2), dtype=torch.int64, device=dev)
-                if nb:
-                    mine = coll.reduce_scatter(rs_buf)                         # [nb, Bs, 2]
-                    cur_hist.index_copy_(0, up[h_bidx], mine[:, : shards.bins].contiguous())
+            with tracing.span("tree.reduce_scatter"), _CollTimer(dev):
+                # rows keep the shard-major stride Bs (>= this shard's bins): the split search
+                # reads them in place; every open node is built or subtracted, so no zero fill
+                mine = coll.reduce_scatter(rs_buf) if nb else None            # [nb, Bs, 2]
+                if nb == nl and build == open_nodes:
+                    cur_hist = mine
+                else:
+                    cur_hist = torch.empty((nl, shards.Bs, 2), dtype=torch.int64, device=dev)
+                    if nb:
+                        cur_hist.index_copy_(0, up[h_bidx], mine)
             if sub_t is not None:
-                C.tree_hist_subtract(prev_hist, cur_hist, *sub_t, shards.bins)
+                C.tree_hist_subtract(prev_hist, cur_hist, *sub_t, shards.Bs)
             with tracing.span("tree.split"):
                 mine = _best_splits(C, cur_hist, totals, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
                                     node_ids, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0)
-                allt = coll.all_gather(mine)                                  # [S, nl, 5]
+                with _CollTimer(dev):
+                    allt = coll.all_gather(mine)                              # [S, nl, 5]
                 gains = allt[:, :, 0].contiguous().view(torch.float64)
                 best_s = torch.argmax(gains, dim=0)                           # ties -> lowest shard = lowest feature
                 packed = allt[best_s, torch.arange(nl, device=dev)].cpu().numpy()
@@ -909,13 +966,19 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                             gfid, gden, h_boff, Q.nbins, s2n, hist_target, h_stride, Q.n_rows, rr, bt, ct, np_))
             ws.run_concurrent(launches)
         if shards is not None:
-            with tracing.span("tree.reduce_scatter"):
+            with tracing.span("tree.reduce_scatter"), _CollTimer(dev):
                 mine = coll.reduce_scatter(rs_buf)                             # [n_build, Bs, 2]
-                cur_hist = torch.zeros((n_open, shards.bins, 2), dtype=torch.int64, device=dev)
-                cur_hist.index_copy_(0, bidx.to(torch.int64), mine[:, : shards.bins].contiguous())
+                if build_all or d == 0:
+                    # every open node built, slot k = open node k (tree.h level_plan): the reduced
+                    # rows ARE the level's histograms (stride Bs, read in place by the split search)
+                    cur_hist = mine
+                else:
+                    # built rows to their open-node rows; the subtraction fills all the others
+                    cur_hist = torch.empty((n_open, shards.Bs, 2), dtype=torch.int64, device=dev)
+                    cur_hist.index_copy_(0, bidx.to(torch.int64), mine)
         if d > 0 and not build_all:
             C.tree_hist_subtract(prev_hist, cur_hist, st.sub_dst[:n_build], st.sub_par[:n_build],
-                                 st.sub_sib[:n_build], TB if shards is None else shards.bins)
+                                 st.sub_sib[:n_build], TB if shards is None else shards.Bs)
         with tracing.span("tree.split"):
             if shards is None:
                 packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
@@ -923,7 +986,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             else:
                 mine = _best_splits(C, cur_hist, totals_d, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
                                     open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0)
-                allt = coll.all_gather(mine)                                  # [S, n_open, 5]
+                with _CollTimer(dev):
+                    allt = coll.all_gather(mine)                              # [S, n_open, 5]
                 gains = allt[:, :, 0].contiguous().view(torch.float64)
                 best_s = torch.argmax(gains, dim=0)                           # ties -> lowest shard = lowest feature
                 packed = allt[best_s, torch.arange(n_open, device=dev)].contiguous()

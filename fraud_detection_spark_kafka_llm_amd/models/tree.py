@@ -32,6 +32,7 @@ from .rf_sampling import features_per_node
 class ForestResult:
     trees: list
     num_features: int
+    lanes: int = 1                 # trees grown in flight together (PAR-05)
 
 
 def prepare(features, labels, device=None, max_bins: int = 32, coll: Collectives = None, chunk: int = None):
@@ -112,9 +113,9 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
                         seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
     ws = Workspace(Q)
     trees = ckpt.load_trees() if (ckpt is not None and resume) else []
-    # PAR-05: several trees in flight, each on its own stream (models/forest_batch.py). Not under
-    # data parallelism: every rank must issue its collectives in one order on one stream.
-    inflight = 1 if coll.active else max(1, forest_batch.TREES_IN_FLIGHT)
+    # PAR-05: several trees in flight, each on its own stream (models/forest_batch.py); under data
+    # parallelism the lanes advance in FIFO order, so every rank issues one collective sequence
+    inflight = max(1, forest_batch.TREES_IN_FLIGHT)
     lanes = None
     if inflight > 1 and num_trees - len(trees) > 1 and device_levels_ok(params, w):
         lanes = ForestLanes(Q, min(inflight, num_trees - len(trees)), ws)
@@ -123,7 +124,7 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
     while t < num_trees:
         if lanes is not None:
             ids = list(range(t, min(num_trees, t + chunk)))
-            grown = grow_forest_concurrent(Q, lanes, params, ids, y, w, bootstrap)
+            grown = grow_forest_concurrent(Q, lanes, params, ids, y, w, bootstrap, coll=coll)
         else:
             ids = [t]
             with tracing.span("forest.tree", tree=t):
@@ -136,4 +137,4 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
                 ckpt.maybe_save(len(trees), trees, 0.0, F, None, force=crossed or len(trees) == num_trees)
             maybe_fail(tid)
         t += len(ids)
-    return ForestResult(trees, F)
+    return ForestResult(trees, F, len(lanes.ws) if lanes is not None else 1)

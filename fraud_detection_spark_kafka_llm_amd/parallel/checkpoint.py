@@ -66,19 +66,35 @@ def data_fingerprint(vc, labels, coll=None) -> str:
     import torch
 
     y = labels.to(torch.float64) if isinstance(labels, torch.Tensor) else torch.as_tensor(labels, dtype=torch.float64)
+    # every sum is taken in chunks: no full-size int64 / fp64 copy of the entries is allocated
+    # (this runs right after prepare(), where the HBM sizing rule may have left little headroom)
     if getattr(vc, "dense", None) is not None:
         d = vc.dense
-        parts = [d.shape[0], int((d != 0).sum()), 0, int((d.to(torch.float64) * 1024).round().sum())]
+        parts = [d.shape[0], int((d != 0).sum()), 0, _chunked_sum(d, lambda c: (c.to(torch.float64) * 1024).round())]
     else:
         cnt = getattr(vc, "tf_counts", None)
-        v = cnt.to(torch.int64) if cnt is not None else (vc.values.to(torch.float64) * 1024).round().to(torch.int64)
-        parts = [len(vc), int(vc.indices.numel()), int(vc.indices.to(torch.int64).sum()), int(v.sum())]
+        if cnt is not None:
+            vsum = _chunked_sum(cnt, lambda c: c)
+        else:
+            vsum = _chunked_sum(vc.values, lambda c: (c.to(torch.float64) * 1024).round())
+        parts = [len(vc), int(vc.indices.numel()), _chunked_sum(vc.indices, lambda c: c), vsum]
     parts.append(int((y.cpu() * 1024).round().sum()))
     t = torch.tensor(parts, dtype=torch.int64)
     if coll is not None and coll.active:
         dev = y.device if y.is_cuda else torch.device("cpu")
         t = coll.sum(t.to(dev)).cpu()
     return "-".join(str(int(x)) for x in t.tolist())
+
+
+def _chunked_sum(x, fn, chunk: int = 1 << 24) -> int:
+    """int(sum(fn(x))) accumulated in int64 over ``chunk``-element slices of the flattened x."""
+    import torch
+
+    flat = x.reshape(-1)
+    total = 0
+    for a in range(0, flat.numel(), chunk):
+        total += int(fn(flat[a:a + chunk]).sum(dtype=torch.int64))
+    return total
 
 
 class EnsembleCheckpointer:
@@ -105,8 +121,11 @@ class EnsembleCheckpointer:
             if (d / "_resume.json").exists():
                 return d
         if self.dir.is_dir():
-            vers = sorted((p for p in self.dir.glob("ckpt-*") if (p / "_resume.json").exists()),
-                          key=lambda p: int(p.name.split("-")[1]))
+            # complete versions only: a ckpt-NNNNNN.tmp directory of a write killed before its
+            # rename may already hold _resume.json, but is never a checkpoint
+            vers = sorted((p for p in self.dir.glob("ckpt-*")
+                           if p.name[5:].isdigit() and (p / "_resume.json").exists()),
+                          key=lambda p: int(p.name[5:]))
             if vers:
                 return vers[-1]
             if (self.dir / "_resume.json").exists():

@@ -266,12 +266,18 @@ class ConsumerGroup:
     def close(self) -> None:
         # no DMA may still read a segment when it is unregistered and unmapped (a run that raised
         # can leave micro-batches in the scorer's pipeline)
+        # a drain that fails (e.g. after the GPU error that ended run()) is logged, and the
+        # clients are still stopped and the segments still released below
         try:
             while self.scorer.inflight:
                 self.scorer.collect(copy=False)
-        finally:
+        except Exception as e:                    # noqa: BLE001
+            print(f"[group] scorer drain failed during close: {type(e).__name__}: {e}", file=sys.stderr)
+        try:
             if self.register and torch.cuda.is_available():
                 torch.cuda.synchronize()
+        except Exception as e:                    # noqa: BLE001
+            print(f"[group] synchronize failed during close: {type(e).__name__}: {e}", file=sys.stderr)
         for cl in self.clients:
             try:
                 self._send_ctl(cl, ("exit", {}))

@@ -86,6 +86,8 @@ def test_checkpoint_survives_kill_between_writes_and_refuses_foreign_runs(tmp_pa
     assert (ck / "LATEST").read_text() == "ckpt-000009"
     # a later save killed before its pointer switch: a half-written tmp dir and a complete dir
     (ck / "ckpt-000012.tmp" / "model").mkdir(parents=True)
+    # (killed after its _resume.json was written, before the rename: still not a checkpoint)
+    (ck / "ckpt-000012.tmp" / "_resume.json").write_text((ck / "ckpt-000009" / "_resume.json").read_text())
     vc = VectorColumn(dense.shape[1], dense=torch.from_numpy(dense))
     did = data_fingerprint(vc, torch.from_numpy(y))
     st = EnsembleCheckpointer(str(ck), kind="gbdt", data_id=did).load()

@@ -210,3 +210,65 @@ def test_tfidf_dp_world2_trees_equal_single_process(kind):
     for trees, n_rs, nbytes in outs:
         assert n_rs > 0 and nbytes > 0
         assert trees == single
+
+
+def _train_rf_lanes(rank, world, device="cpu"):
+    """RF with several trees in flight (PAR-05) and the level collectives counted: returns the
+    trees, the lanes used and the sequence of collective calls this rank issued."""
+    import torch.distributed as td
+
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+    from fraud_detection_spark_kafka_llm_amd.parallel.dist import shard_range
+
+    seq = []
+    if td.is_initialized():
+        for name in ("reduce_scatter_tensor", "all_gather_into_tensor", "all_reduce"):
+            orig = getattr(td, name)
+
+            def wrapped(out, *a, _orig=orig, _name=name, **k):
+                seq.append((_name, tuple(out.shape)))
+                return _orig(out, *a, **k)
+
+            setattr(td, name, wrapped)
+    dense, y = _dataset(n=1500, F=120, seed=3)
+    lo, hi = shard_range(len(y), rank, world)
+    grower.reset_level_stats()
+    r = fit_forest(_vc(dense[lo:hi]), torch.from_numpy(y[lo:hi]), num_trees=9, max_depth=5, bootstrap=True,
+                   feature_subset="sqrt", seed=11, device=device)
+    trees = [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]
+    return trees, r.lanes, seq, grower.LEVEL_STATS["coll_calls"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rf_trees_in_flight_under_dp_equal_single_process(world, monkeypatch):
+    """PAR-05 under data parallelism (BASELINE config 3): 4 trees in flight per rank, lanes advanced
+    in FIFO order so that every rank issues the same reduce-scatter / all-gather sequence; the
+    forest is bitwise the DP=1 one-tree-at-a-time forest."""
+    monkeypatch.setenv("FDX_RF_INFLIGHT", "1")
+    serial = spawn(_train_rf_lanes, 1, backend="gloo")[0]
+    assert serial[1] == 1
+    monkeypatch.setenv("FDX_RF_INFLIGHT", "4")
+    outs = spawn(_train_rf_lanes, world, backend="gloo")
+    for trees, lanes, seq, n_coll in outs:
+        assert lanes == 4
+        assert trees == serial[0]
+        assert n_coll > 0
+        assert any(name == "reduce_scatter_tensor" for name, _ in seq)
+    # the same collective sequence (names and payload shapes) on every rank
+    assert all(o[2] == outs[0][2] for o in outs)
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_forced_collectives_rf_lanes_equal_serial(monkeypatch):
+    """RCCL at world 1 with 4 RF trees in flight: the lanes' reduce-scatters / all-gathers queue on
+    the communicator's stream behind each lane's kernels; the forest equals the one-tree-at-a-time
+    non-DP GPU forest (and the shared CSC items are built before the lanes fork: cold Q)."""
+    monkeypatch.setenv("FDX_RF_INFLIGHT", "1")
+    serial = spawn(_train_rf_lanes, 1, "cuda:0", backend="gloo")[0]
+    monkeypatch.setenv("FDX_RF_INFLIGHT", "4")
+    monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
+    (trees, lanes, seq, n_coll), = spawn(_train_rf_lanes, 1, "cuda:0", backend="nccl")
+    assert lanes == 4 and n_coll > 0
+    assert any(name == "reduce_scatter_tensor" for name, _ in seq)
+    assert trees == serial[0]
