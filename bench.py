@@ -26,12 +26,13 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      latency (broker append -> output delivered) under a paced producer at ``kafka_offered_per_s``.
      Per GPU (rank 0's engine on its own broker; not summed over ranks). ``kafka_confluent_*``: the
      same runs through clients restricted to the confluent_kafka surface (per-record Messages,
-     produce + delivery callback per record). ``kafka_multi_gpu_dialogues_per_s``: ONE 3-partition
-     topic drained by one engine fanning micro-batches out to a scorer per GPU (rank 0; a 1-GPU
-     job runs 2 scorers on the device as a rehearsal). ``kafka_confluent_group_*``: the confluent
-     surface as a consumer group — one client process per partition (3) around rank 0's GPU
-     scoring process, shared-memory slots page-locked for the H2D (stream/group.py);
-     ``..._explain_*``: the same latency run with the LLM-explain stub on every 10th record.
+     produce + delivery callback per record). ``kafka_confluent_group_*``: the confluent surface as
+     a consumer group over ONE 3-partition topic: one client process per partition around a
+     scoring process PER RANK, each on its own GPU (stream/group.py: rank 0 coordinates, ranks
+     1..N-1 are ScorerPeers; shared-memory slots page-locked by every scoring process for its
+     device; no process opens another rank's GPU); ``..._explain_*``: the same latency run with
+     the LLM-explain stub on every 10th record. ``kafka_multi_gpu_*``: the same N scoring
+     processes fed by columnar clients (``..._scorer_procs`` = N, batches per scoring process).
 Data is synthetic (the reference dataset is not available) with random-init-free trained trees.
 Before the timed training, an untimed 2-tree fit on 65,536 rows loads the kernels' code objects
 (lazily loaded on first launch by ROCm) and warms the allocators (``gbdt_warmup_sec_untimed``).
@@ -191,92 +192,98 @@ def warmup_training(dev, spec, params: GBDTParams, rf_depth: int = 0) -> None:
                       forest_subset="sqrt")
 
 
-def multi_gpu_kafka(args, spec, idf_np, model, dev, pool, make_engine) -> dict:
-    """BASELINE config 5's topology: ONE 3-partition topic drained by one engine (3 partition
-    readers -> one pinned ring) whose micro-batches go round-robin to a scorer per visible GPU
-    (stream/gpu_worker.py MultiGpuScorer). Run by rank 0 while the other ranks wait (their GPUs
-    are the scorers' devices); on a 1-GPU job two scorers share the device (a rehearsal of the
-    fan-out, not a multi-GPU number)."""
-    import gc
-
-    from fraud_detection_spark_kafka_llm_amd.stream import loadgen
-    from fraud_detection_spark_kafka_llm_amd.stream.gpu_worker import MultiGpuScorer
-
-    world = D.world_size()
-    out = {}
-    if D.rank() == 0:
-        n_dev = torch.cuda.device_count() if world > 1 else 1
-        devices = [torch.device("cuda", i) for i in range(min(n_dev, max(world, 1)))] if world > 1 else [dev, dev]
-        batch = 16384
-
-        def mk(consumers, producer, topic):
-            sc = MultiGpuScorer([GpuScorer(spec, idf_np, model.scorer(), d, max_docs=batch, max_bytes=batch * 4096,
-                                           depth=2) for d in devices])
-            return make_engine(sc, model.postprocess_numpy, consumers, producer, topic, batch_max=batch,
-                               max_latency_ms=5.0, max_bytes=batch * 4096)
-
-        gc.collect()
-        loadgen.throughput_run(mk, pool, 50_000, url="memory://bench-multi-warm")
-        gc.collect()
-        r = loadgen.throughput_run(mk, pool, args.kafka_multi_msgs, url="memory://bench-multi")
-        out = {"kafka_multi_gpu_dialogues_per_s": r["dialogues_per_s"],
-               "kafka_multi_gpu_n_devices": len({str(d) for d in devices}),
-               "kafka_multi_gpu_scorers": len(devices), "kafka_multi_gpu_msgs": args.kafka_multi_msgs,
-               "kafka_multi_gpu_all_committed": bool(r["committed"] == r["produced"] == args.kafka_multi_msgs)}
-    D.barrier()
-    return out
-
-
 def group_kafka(args, spec, idf_np, model, dev, pool) -> dict:
-    """Config 5 through the confluent surface as a consumer group (stream/group.py): one client
-    process per partition of the 3-partition topic (poll -> extract -> produce + commit, each
-    with its own GIL) around this rank's GPU scoring process (shared-memory slots, one GpuScorer).
-    Rank 0 only; the others wait. A failure is reported in the record, not raised."""
+    """Config 5 as a consumer group whose scoring processes are the job's ranks (stream/group.py):
+    rank 0 creates the shared-memory slots and starts one client process per partition of the
+    3-partition topic; every rank scores on ITS OWN GPU (rank 0 with a ConsumerGroup, the others
+    as ScorerPeers that page-lock the same slots for their device). Two groups run:
+      * ``kafka_confluent_group_*``: clients restricted to the confluent_kafka surface
+        (throughput, paced latency, latency with the LLM-explain stub on every 10th record);
+      * ``kafka_multi_gpu_*``: columnar clients (the throughput the N scoring processes reach when
+        the clients are cheap), with the micro-batches each scoring process took.
+    A failure is reported in the record, not raised; no rank enters a device barrier before its
+    scoring process has stopped."""
     out = {}
-    if D.rank() == 0:
+    for name, fn in (("kafka_confluent_group", _group_confluent_runs), ("kafka_multi_gpu", _group_multi_runs)):
+        if (name == "kafka_multi_gpu" and args.kafka_multi_msgs <= 0) or \
+                (name == "kafka_confluent_group" and args.kafka_group_msgs <= 0):
+            continue
         try:
-            out = _group_kafka_runs(args, spec, idf_np, model, dev, pool)
+            out.update(_group_session(name, fn, args, spec, idf_np, model, dev, pool))
         except Exception as e:     # the headline line must still be printed: report, do not abort
             import traceback
 
             traceback.print_exc()
-            out = {"kafka_confluent_group_error": f"{type(e).__name__}: {e}"}
-    D.barrier()
-    return out
+            out[f"{name}_error"] = f"{type(e).__name__}: {e}"
+        D.barrier()
+    return out if D.rank() == 0 else {}
 
 
-def _group_kafka_runs(args, spec, idf_np, model, dev, pool) -> dict:
-    """The consumer-group runs: warm-up, throughput, paced latency, latency with explanations."""
+def _group_session(name, runs, args, spec, idf_np, model, dev, pool) -> dict:
     import gc
 
     from fraud_detection_spark_kafka_llm_amd.stream import group as G
 
     batch = 16384
     sc = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=batch, max_bytes=batch * 4096, depth=3)
+    rdv = G.GroupRendezvous.from_process_group(name) if D.world_size() > 1 else None
     gc.collect()
+    if D.rank() > 0:
+        with G.ScorerPeer(sc, model.postprocess_numpy, rdv) as peer:
+            try:
+                st = peer.serve()
+            except Exception as e:                 # noqa: BLE001 (reported by rank 0)
+                st = {"batches": 0, "docs": 0, "error": f"{type(e).__name__}: {e}"}
+        rdv.publish_stats(st)
+        return {}
     with G.ConsumerGroup(sc, model.postprocess_numpy, args.kafka_group_clients, batch_max=batch,
-                         max_latency_ms=5.0, max_bytes=batch * 4096, pool=pool, confluent=True) as grp:
-        G.group_throughput_run(grp, 60_000, tag="warm")
-        tp = G.group_throughput_run(grp, args.kafka_group_msgs, tag="tp")
-        lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
-        # the config's LLM-explain stub: every 10th classification explained asynchronously
-        # in the clients (offline stub backend), its record produced after the classification
-        ex = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat-explain", explain="async",
-                                 explain_every=10)
-    out = {"kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
-           "kafka_confluent_group_clients": args.kafka_group_clients,
-           "kafka_confluent_group_msgs": args.kafka_group_msgs,
-           "kafka_confluent_group_p50_ms": lat["p50_ms"], "kafka_confluent_group_p95_ms": lat["p95_ms"],
-           "kafka_confluent_group_offered_per_s": args.kafka_group_rate,
-           "kafka_confluent_group_explain_p50_ms": ex["p50_ms"],
-           "kafka_confluent_group_explain_p95_ms": ex["p95_ms"],
-           "kafka_confluent_group_explanations": ex["explanations"],
-           "kafka_confluent_group_all_committed": bool(
-               tp["produced"] == tp["committed"] == args.kafka_group_msgs and
-               lat["produced"] == lat["committed"] == lat["sent"] and
-               ex["produced"] == ex["committed"] == ex["sent"] and ex["explanations"] > 0)}
+                         max_latency_ms=5.0, max_bytes=batch * 4096, pool=pool,
+                         confluent=(name == "kafka_confluent_group"), rendezvous=rdv) as grp:
+        out = runs(args, grp)
+        n_scorers = grp.n_scorers
+        local = grp.local_batches
+    peers = rdv.stats() if rdv is not None else []
+    out.update({f"{name}_scorer_procs": n_scorers, f"{name}_batches_per_scorer": [local] + [p["batches"] for p in peers]})
+    errs = [p["error"] for p in peers if "error" in p]
+    if errs:
+        out[f"{name}_peer_errors"] = errs
     del sc
     return out
+
+
+def _group_confluent_runs(args, grp) -> dict:
+    from fraud_detection_spark_kafka_llm_amd.stream import group as G
+
+    G.group_throughput_run(grp, 60_000, tag="warm")
+    tp = G.group_throughput_run(grp, args.kafka_group_msgs, tag="tp")
+    lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
+    # the config's LLM-explain stub: every 10th classification explained asynchronously in the
+    # clients (offline stub backend), its record produced after the classification
+    ex = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat-explain", explain="async",
+                             explain_every=10)
+    return {"kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
+            "kafka_confluent_group_clients": args.kafka_group_clients,
+            "kafka_confluent_group_msgs": args.kafka_group_msgs,
+            "kafka_confluent_group_p50_ms": lat["p50_ms"], "kafka_confluent_group_p95_ms": lat["p95_ms"],
+            "kafka_confluent_group_offered_per_s": args.kafka_group_rate,
+            "kafka_confluent_group_explain_p50_ms": ex["p50_ms"],
+            "kafka_confluent_group_explain_p95_ms": ex["p95_ms"],
+            "kafka_confluent_group_explanations": ex["explanations"],
+            "kafka_confluent_group_all_committed": bool(
+                tp["produced"] == tp["committed"] == args.kafka_group_msgs and
+                lat["produced"] == lat["committed"] == lat["sent"] and
+                ex["produced"] == ex["committed"] == ex["sent"] and ex["explanations"] > 0)}
+
+
+def _group_multi_runs(args, grp) -> dict:
+    from fraud_detection_spark_kafka_llm_amd.stream import group as G
+
+    G.group_throughput_run(grp, 60_000, tag="mwarm")
+    tp = G.group_throughput_run(grp, args.kafka_multi_msgs, tag="mtp")
+    return {"kafka_multi_gpu_dialogues_per_s": tp["dialogues_per_s"], "kafka_multi_gpu_msgs": args.kafka_multi_msgs,
+            "kafka_multi_gpu_clients": args.kafka_group_clients,
+            "kafka_multi_gpu_client_batches_per_scorer": tp["scorer_batches"],
+            "kafka_multi_gpu_all_committed": bool(tp["produced"] == tp["committed"] == args.kafka_multi_msgs)}
 
 
 def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
@@ -322,11 +329,8 @@ def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
                 "kafka_confluent_msgs": args.kafka_confluent_msgs,
                 "kafka_confluent_p50_ms": clat["p50_ms"], "kafka_confluent_p95_ms": clat["p95_ms"],
                 "kafka_confluent_offered_per_s": args.kafka_confluent_rate}
-    group = group_kafka(args, spec, idf_np, model, dev, pool) if args.kafka_group_msgs > 0 else {}
-    conf.update(group)
-    multi = multi_gpu_kafka(args, spec, idf_np, model, dev, pool, make_engine=StreamingEngine) \
-        if args.kafka_multi_msgs > 0 else {}
-    return {**multi, "kafka_dialogues_per_s": tp["dialogues_per_s"], "kafka_msgs": args.kafka_msgs,
+    conf.update(group_kafka(args, spec, idf_np, model, dev, pool))
+    return {"kafka_dialogues_per_s": tp["dialogues_per_s"], "kafka_msgs": args.kafka_msgs,
             "kafka_throughput_sec": tp["sec"], "kafka_p50_ms": lat["p50_ms"], "kafka_p95_ms": lat["p95_ms"],
             "kafka_p99_ms": lat["p99_ms"], "kafka_offered_per_s": args.kafka_rate,
             "kafka_latency_msgs": lat["sent"], "kafka_all_delivered_and_committed": bool(ok),

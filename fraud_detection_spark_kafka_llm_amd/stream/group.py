@@ -19,6 +19,17 @@ them one message at a time in one process (/root/reference/app_ui.py:196-226):
 
 Per micro-batch the IPC is two 16-byte socket messages; the text bytes are written once (by the
 client's extraction) and read once (by the DMA engine).
+
+**Several scoring processes, one per GPU** (BASELINE config 5: "3-partition topic -> 8-GPU batched
+inference"). Under torchrun every rank is one process on its own GPU; no process opens another
+rank's device. Rank 0 runs the :class:`ConsumerGroup` (it creates the segments and starts the
+clients); every other rank runs a :class:`ScorerPeer`, which maps the same segments, page-locks
+them for ITS device and serves micro-batches over a Unix socket per client. The rendezvous
+(segment names, the peers' socket names) goes through the process group's key-value store
+(:class:`GroupRendezvous`), never through a device collective. Each client's
+:class:`RemoteScorer` sends every micro-batch to the scoring process with the fewest of its
+batches outstanding (ties rotate), and hands results back to its engine in submission order.
+The peers stop when every client has closed its connection (the group's close).
 """
 from __future__ import annotations
 
@@ -43,6 +54,7 @@ from .ring import PinnedRing, Slot
 
 _SUB, _DONE, _CTL = b"S", b"D", b"C"
 _HDR = struct.Struct("<iiq")            # slot index, documents, bytes
+_HELLO = struct.Struct("<i")            # client index on a peer connection (-1: abort)
 _ALIGN = 4096
 
 
@@ -88,14 +100,20 @@ class SharedRing(PinnedRing):
 
 
 class RemoteScorer:
-    """Client-side scorer: ``submit`` sends the slot index to the GPU process, ``collect`` returns
-    the (prediction, P(scam)) rows it wrote into the slot (FIFO, like GpuScorer)."""
+    """Client-side scorer over one or more scoring processes (``conns[0]``: the group's own, the
+    others: ScorerPeers). ``submit`` sends the slot index to the scorer with the fewest of this
+    client's batches outstanding; ``collect`` returns the (prediction, P(scam)) rows written into
+    the oldest submitted slot (FIFO over all scorers, like GpuScorer)."""
 
-    def __init__(self, conn: Connection, ring: SharedRing, max_docs: int, max_bytes: int, depth: int = 2):
-        self.conn, self.ring = conn, ring
+    def __init__(self, conns, ring: SharedRing, max_docs: int, max_bytes: int, depth: int = 2):
+        self.conns = list(conns) if isinstance(conns, (list, tuple)) else [conns]
+        self.conn, self.ring = self.conns[0], ring
         self.max_docs, self.max_bytes, self._depth = max_docs, max_bytes, depth
-        self._q: deque = deque()
-        self._done: deque = deque()
+        self._q: deque = deque()                  # (slot, scorer) in submission order
+        self._out = [0] * len(self.conns)         # outstanding batches per scorer
+        self._done: set = set()                   # slot indices whose results arrived
+        self._rr = 0
+        self.sent = [0] * len(self.conns)         # batches sent per scorer (stats)
 
     @property
     def depth(self) -> int:
@@ -108,28 +126,53 @@ class RemoteScorer:
     def submit(self, slot: Slot) -> None:
         if len(self._q) >= self._depth:
             raise RuntimeError("pipeline full: call collect() first")
-        self.conn.send_bytes(_SUB + _HDR.pack(slot.index, slot.n_docs, slot.n_bytes))
-        self._q.append(slot)
+        n = len(self.conns)
+        best = self._rr
+        for j in range(1, n):
+            k = (self._rr + j) % n
+            if self._out[k] < self._out[best]:
+                best = k
+        self._rr = (best + 1) % n
+        self.conns[best].send_bytes(_SUB + _HDR.pack(slot.index, slot.n_docs, slot.n_bytes))
+        self._out[best] += 1
+        self.sent[best] += 1
+        self._q.append((slot, best))
 
-    def _recv(self) -> None:
-        m = self.conn.recv_bytes()
+    def _recv(self, k: int) -> None:
+        try:
+            m = self.conns[k].recv_bytes()
+        except EOFError:
+            raise RuntimeError(f"scoring process {k} closed its connection") from None
         if m[:1] != _DONE:
-            raise RuntimeError(f"unexpected message from the scoring process: {m[:1]!r}")
-        self._done.append(_HDR.unpack_from(m, 1)[0])
+            raise RuntimeError(f"unexpected message from scoring process {k}: {m[:1]!r}")
+        self._done.add(_HDR.unpack_from(m, 1)[0])
+        self._out[k] -= 1
+
+    def _pump(self, block: bool) -> None:
+        pending = [k for k in range(len(self.conns)) if self._out[k]]
+        if not pending:
+            return
+        if block:
+            ready = mp_wait([self.conns[k] for k in pending])
+            pending = [k for k in pending if self.conns[k] in ready]
+        for k in pending:
+            while self._out[k] and self.conns[k].poll(0):
+                self._recv(k)
 
     def ready(self) -> bool:
-        while not self._done and self._q and self.conn.poll(0):
-            self._recv()
-        return bool(self._done)
+        if self._q and self._q[0][0].index not in self._done:
+            self._pump(block=False)
+        return bool(self._q) and self._q[0][0].index in self._done
 
     def collect(self, copy: bool = True) -> tuple:
-        while not self._done:
-            self._recv()
-        i = self._done.popleft()
-        slot = self._q.popleft()
-        if slot.index != i:
-            raise RuntimeError(f"out-of-order result: slot {i}, expected {slot.index}")
-        res = self.ring.results[i][: slot.n_docs].numpy()
+        if not self._q:
+            raise RuntimeError("nothing in flight")
+        slot, _ = self._q[0]
+        while slot.index not in self._done:
+            self._pump(block=True)
+        self._q.popleft()
+        self._done.discard(slot.index)
+        res = self.ring.results[slot.index][: slot.n_docs].numpy()
         return slot, res.copy() if copy else res
 
 
@@ -140,66 +183,188 @@ def remote_postprocess(res: np.ndarray) -> tuple:
 
 # ---------------------------------------------------------------------------------------------- GPU side
 class _Client:
-    def __init__(self, idx: int, shm, lay: dict, sock, proc):
+    """A client as seen by a scoring process: its segment's slot views and its data connection."""
+
+    def __init__(self, idx: int, shm, lay: dict, conn: Optional[Connection] = None, proc=None):
         self.idx, self.shm, self.lay, self.proc = idx, shm, lay, proc
-        self.conn = Connection(sock.detach())
+        self.conn = conn
         self.views = _views(shm.buf, lay)
         self.slots = [Slot(i, d, o) for i, (d, o, _) in enumerate(self.views)]
         self.registered: list = []
         self.reply = None
 
 
-class ConsumerGroup:
-    """The scoring process of a consumer group: ``n_clients`` client processes, one GpuScorer.
+def _register(cl: _Client) -> None:
+    """Page-lock the client's slot views for this process's device (hipHostRegister): the H2D DMA
+    reads the client's bytes in place."""
+    from ..ops import native
 
-    ``postprocess(raw) -> (pred, p1)`` runs here (the clients hold no model). ``pool`` (a
-    loadgen.MessagePool) is shared with the clients for the in-memory broker runs."""
+    for d, o, r in cl.views:
+        for t in (d, o, r):
+            native.lib().host_register(t)
+            cl.registered.append(t)
+
+
+def _unregister(cl: _Client) -> None:
+    if cl.registered:
+        from ..ops import native
+
+        for t in cl.registered:
+            native.lib().host_unregister(t)
+        cl.registered = []
+
+
+class _ScoreLoop:
+    """The data plane of one scoring process: micro-batches from the clients' slots through one
+    scorer pipeline; (prediction, P(scam)) written back into the slot, then a DONE message."""
+
+    def __init__(self, scorer, postprocess, clients: list, batch_max: int, max_bytes: int):
+        self.scorer, self.postprocess, self.clients = scorer, postprocess, clients
+        self.batch_max, self.max_bytes = batch_max, max_bytes
+        self.batches = self.docs = 0
+
+    def submit(self, cl: _Client, m: bytes) -> None:
+        i, n, nb = _HDR.unpack_from(m, 1)
+        if not (0 <= i < len(cl.slots)) or n > self.batch_max or nb > self.max_bytes:
+            raise RuntimeError(f"client {cl.idx}: bad slot header {(i, n, nb)}")
+        sc = self.scorer
+        while sc.inflight >= sc.depth:
+            self.finish()
+        s = cl.slots[i]
+        s.n_docs, s.n_bytes, s.meta = n, nb, (cl.idx, i)
+        sc.submit(s)
+        self.batches += 1
+        self.docs += n
+
+    def finish(self) -> None:
+        slot, raw = self.scorer.collect(copy=False)
+        c, i = slot.meta
+        slot.meta = None
+        pred, p1 = self.postprocess(raw)
+        cl = self.clients[c]
+        res = cl.views[i][2][: slot.n_docs].numpy()
+        res[:, 0] = pred
+        res[:, 1] = p1
+        cl.conn.send_bytes(_DONE + _HDR.pack(i, slot.n_docs, slot.n_bytes))
+
+    def pump(self) -> None:
+        while self.scorer.inflight and self.scorer.ready():
+            self.finish()
+
+    def drain(self) -> None:
+        while self.scorer.inflight:
+            self.finish()
+
+
+class GroupRendezvous:
+    """Rank 0 <-> peer scoring processes: the group's segment config and the peers' socket names
+    through a key-value store (the process group's TCPStore under torchrun). ``key`` must be the
+    same on every rank and unique per group."""
+
+    def __init__(self, store, key: str, world: int, rank: int, timeout_s: float = 600.0):
+        self.store, self.key, self.world, self.rank, self.timeout_s = store, key, world, rank, timeout_s
+
+    @classmethod
+    def from_process_group(cls, key: str, timeout_s: float = 600.0) -> "GroupRendezvous":
+        import torch.distributed as td
+
+        store = td.distributed_c10d._get_default_store()
+        return cls(store, f"fdx-group/{key}", td.get_world_size(), td.get_rank(), timeout_s)
+
+    @property
+    def n_peers(self) -> int:
+        return self.world - 1
+
+    def _wait(self, k: str) -> bytes:
+        import datetime
+
+        self.store.wait([k], datetime.timedelta(seconds=self.timeout_s))
+        return self.store.get(k)
+
+    def publish_config(self, cfg: dict) -> None:
+        self.store.set(f"{self.key}/cfg", json.dumps(cfg))
+
+    def config(self) -> dict:
+        return json.loads(self._wait(f"{self.key}/cfg"))
+
+    def publish_socket(self, name: str) -> None:
+        self.store.set(f"{self.key}/sock/{self.rank}", name)
+
+    def sockets(self) -> list:
+        return [self._wait(f"{self.key}/sock/{r}").decode() for r in range(1, self.world)]
+
+    def publish_stats(self, stats: dict) -> None:
+        self.store.set(f"{self.key}/stats/{self.rank}", json.dumps(stats))
+
+    def stats(self) -> list:
+        return [json.loads(self._wait(f"{self.key}/stats/{r}")) for r in range(1, self.world)]
+
+
+class ConsumerGroup:
+    """The coordinating scoring process of a consumer group: ``n_clients`` client processes, this
+    process's scorer and, with ``rendezvous``, one :class:`ScorerPeer` per other rank.
+
+    ``postprocess(raw) -> (pred, p1)`` runs in the scoring processes (the clients hold no model).
+    ``pool`` (a loadgen.MessagePool) is shared with the clients for the in-memory broker runs."""
 
     def __init__(self, scorer, postprocess, n_clients: int, batch_max: int = 16384, max_latency_ms: float = 5.0,
                  max_bytes: int = 64 << 20, client_depth: int = 2, pool=None, confluent: bool = True,
-                 register: Optional[bool] = None, env: Optional[dict] = None):
+                 register: Optional[bool] = None, env: Optional[dict] = None,
+                 rendezvous: Optional[GroupRendezvous] = None):
         self.scorer, self.postprocess = scorer, postprocess
         self.batch_max = min(batch_max, scorer.max_docs)
         max_bytes = min(max_bytes, scorer.max_bytes)
+        self.rdv = rendezvous if (rendezvous is not None and rendezvous.n_peers > 0) else None
+        self.n_scorers = 1 + (self.rdv.n_peers if self.rdv is not None else 0)
+        # enough batches in flight per client to keep every scoring process busy
+        client_depth = max(client_depth, -(-2 * self.n_scorers // max(n_clients, 1)))
         slots = client_depth + 3
         self.lay = slot_layout(slots, self.batch_max, max_bytes)
         self.clients: list = []
         self._pool_shm = None
+        self._published = False
+        self.peer_sockets: list = []
         pool_lay = None
-        if pool is not None:
-            pool_lay, self._pool_shm = _share_pool(pool)
         dev = getattr(scorer, "dev", None)
         self.register = (dev is not None and dev.type == "cuda") if register is None else register
-        base = {"layout": self.lay, "batch_max": self.batch_max, "max_latency_ms": max_latency_ms,
-                "depth": client_depth, "pool": pool_lay, "confluent": confluent, "n_clients": n_clients}
-        child_env = dict(os.environ, **(env or {}))
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        child_env["PYTHONPATH"] = root + os.pathsep + child_env.get("PYTHONPATH", "")
         try:
-            for c in range(n_clients):
-                shm = shared_memory.SharedMemory(create=True, size=self.lay["size"])
-                a, b = socket.socketpair()
-                cfg = dict(base, index=c, shm=shm.name, fd=b.fileno())
-                # a fresh interpreter (never a fork of this GPU process); it touches no GPU
-                proc = subprocess.Popen([sys.executable, "-m", "fraud_detection_spark_kafka_llm_amd.stream.group",
-                                         json.dumps(cfg)], pass_fds=(b.fileno(),), env=child_env)
-                b.close()
-                cl = _Client(c, shm, self.lay, a, proc)
+            if pool is not None:
+                pool_lay, self._pool_shm = _share_pool(pool)
+            segs = [shared_memory.SharedMemory(create=True, size=self.lay["size"]) for _ in range(n_clients)]
+            for c, shm in enumerate(segs):
+                cl = _Client(c, shm, self.lay)
                 self.clients.append(cl)
                 if self.register:
-                    from ..ops import native
-
-                    for d, o, r in cl.views:
-                        for t in (d, o, r):
-                            native.lib().host_register(t)
-                            cl.registered.append(t)
+                    _register(cl)
+            if self.rdv is not None:
+                # the peers map the same segments and listen for the clients before they start
+                self.rdv.publish_config({"layout": self.lay, "shm": [sh.name for sh in segs],
+                                         "batch_max": self.batch_max, "max_bytes": max_bytes})
+                self._published = True
+                self.peer_sockets = self.rdv.sockets()
+            base = {"layout": self.lay, "batch_max": self.batch_max, "max_latency_ms": max_latency_ms,
+                    "depth": client_depth, "pool": pool_lay, "confluent": confluent, "n_clients": n_clients,
+                    "peers": self.peer_sockets}
+            child_env = dict(os.environ, **(env or {}))
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            child_env["PYTHONPATH"] = root + os.pathsep + child_env.get("PYTHONPATH", "")
+            for cl in self.clients:
+                a, b = socket.socketpair()
+                cfg = dict(base, index=cl.idx, shm=cl.shm.name, fd=b.fileno())
+                # a fresh interpreter (never a fork of this GPU process); it touches no GPU
+                cl.proc = subprocess.Popen([sys.executable, "-m", "fraud_detection_spark_kafka_llm_amd.stream.group",
+                                            json.dumps(cfg)], pass_fds=(b.fileno(),), env=child_env)
+                b.close()
+                cl.conn = Connection(a.detach())
             for cl in self.clients:
                 msg = self._control(cl)
                 if msg[0] != "ready":
                     raise RuntimeError(f"client {cl.idx}: {msg}")
-        except BaseException:
+        except BaseException as e:
+            self._abort_peers(f"{type(e).__name__}: {e}")
             self.close()
             raise
+        self.loop = _ScoreLoop(scorer, postprocess, self.clients, self.batch_max, self.lay["max_bytes"])
 
     # ------------------------------------------------------------------ protocol
     def _control(self, cl: _Client, timeout: float = 300.0):
@@ -213,15 +378,25 @@ class ConsumerGroup:
     def _send_ctl(self, cl: _Client, obj) -> None:
         cl.conn.send_bytes(_CTL + pickle.dumps(obj))
 
-    def _finish(self) -> None:
-        slot, raw = self.scorer.collect(copy=False)
-        c, i = slot.meta
-        slot.meta = None
-        pred, p1 = self.postprocess(raw)
-        res = self.clients[c].views[i][2][: slot.n_docs].numpy()
-        res[:, 0] = pred
-        res[:, 1] = p1
-        self.clients[c].conn.send_bytes(_DONE + _HDR.pack(i, slot.n_docs, slot.n_bytes))
+    def _abort_peers(self, why: str) -> None:
+        """Release peers still waiting for a config or for their clients (a group that failed to
+        start): an error config, or an abort hello on their sockets."""
+        if self.rdv is None:
+            return
+        try:
+            if not self._published:
+                self.rdv.publish_config({"error": why})
+                return
+            for name in self.peer_sockets:
+                try:
+                    with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as s:
+                        s.settimeout(5.0)
+                        s.connect("\0" + name)
+                        s.sendall(_HELLO.pack(-1))
+                except OSError:
+                    pass
+        except Exception:                          # noqa: BLE001 (best effort)
+            pass
 
     def run(self, spec: dict, per_client: Optional[list] = None) -> list:
         """Send ``spec`` (merged with ``per_client[c]``) to every client, score their micro-batches
@@ -230,12 +405,11 @@ class ConsumerGroup:
             cl.reply = None
             self._send_ctl(cl, ("run", dict(spec, **(per_client[cl.idx] if per_client else {}))))
         live = {cl.conn: cl for cl in self.clients}
-        sc = self.scorer
+        sc, loop = self.scorer, self.loop
         while live or sc.inflight:
-            while sc.inflight and sc.ready():
-                self._finish()
+            loop.pump()
             if not live:
-                self._finish()
+                loop.finish()
                 continue
             for conn in mp_wait(list(live), timeout=0.0002 if sc.inflight else 0.05):
                 cl = live[conn]
@@ -244,14 +418,7 @@ class ConsumerGroup:
                 except EOFError:
                     raise RuntimeError(f"client {cl.idx} exited (code {cl.proc.poll()})") from None
                 if m[:1] == _SUB:
-                    i, n, nb = _HDR.unpack_from(m, 1)
-                    if not (0 <= i < len(cl.slots)) or n > self.batch_max or nb > self.lay["max_bytes"]:
-                        raise RuntimeError(f"client {cl.idx}: bad slot header {(i, n, nb)}")
-                    while sc.inflight >= sc.depth:
-                        self._finish()
-                    s = cl.slots[i]
-                    s.n_docs, s.n_bytes, s.meta = n, nb, (cl.idx, i)
-                    sc.submit(s)
+                    loop.submit(cl, m)
                 else:
                     msg = pickle.loads(m[1:])
                     if msg[0] == "error":
@@ -263,11 +430,15 @@ class ConsumerGroup:
                     raise RuntimeError(f"client {cl.idx} exited (code {cl.proc.returncode})")
         return [cl.reply for cl in self.clients]
 
+    @property
+    def local_batches(self) -> int:
+        return self.loop.batches if getattr(self, "loop", None) is not None else 0
+
     def close(self) -> None:
         # no DMA may still read a segment when it is unregistered and unmapped (a run that raised
-        # can leave micro-batches in the scorer's pipeline)
-        # a drain that fails (e.g. after the GPU error that ended run()) is logged, and the
-        # clients are still stopped and the segments still released below
+        # can leave micro-batches in the scorer's pipeline); a drain that fails (e.g. after the GPU
+        # error that ended run()) is logged, and the clients are still stopped and the segments
+        # still released below
         try:
             while self.scorer.inflight:
                 self.scorer.collect(copy=False)
@@ -279,23 +450,22 @@ class ConsumerGroup:
         except Exception as e:                    # noqa: BLE001
             print(f"[group] synchronize failed during close: {type(e).__name__}: {e}", file=sys.stderr)
         for cl in self.clients:
+            if cl.conn is None:
+                continue
             try:
                 self._send_ctl(cl, ("exit", {}))
             except OSError:
                 pass
         for cl in self.clients:
-            try:
-                cl.proc.wait(timeout=30)
-            except subprocess.TimeoutExpired:
-                cl.proc.kill()
-                cl.proc.wait()
-            if cl.registered:
-                from ..ops import native
-
-                for t in cl.registered:
-                    native.lib().host_unregister(t)
-                cl.registered = []
-            cl.conn.close()
+            if cl.proc is not None:
+                try:
+                    cl.proc.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    cl.proc.kill()
+                    cl.proc.wait()
+            _unregister(cl)
+            if cl.conn is not None:
+                cl.conn.close()
             cl.views = cl.slots = None
             try:
                 cl.shm.close()
@@ -307,6 +477,116 @@ class ConsumerGroup:
             self._pool_shm.close()
             self._pool_shm.unlink()
             self._pool_shm = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class ScorerPeer:
+    """A scoring process of a consumer group other than the coordinator (rank r > 0 of a torchrun
+    job, on its own GPU): maps the clients' segments, page-locks them for its device, listens on
+    a Unix socket (abstract namespace) that every client connects to, and scores the micro-batches
+    the clients send it until all of them have closed their connections. ``serve()`` returns the
+    number of batches and documents it scored."""
+
+    def __init__(self, scorer, postprocess, rendezvous: GroupRendezvous, register: Optional[bool] = None,
+                 accept_timeout_s: float = 600.0):
+        import uuid
+
+        self.scorer, self.postprocess, self.rdv = scorer, postprocess, rendezvous
+        self.clients: list = []
+        self.listener = None
+        self.error = None
+        cfg = rendezvous.config()
+        if "error" in cfg:
+            self.error = cfg["error"]
+            return
+        self.lay = cfg["layout"]
+        dev = getattr(scorer, "dev", None)
+        self.register = (dev is not None and dev.type == "cuda") if register is None else register
+        try:
+            for c, name in enumerate(cfg["shm"]):
+                cl = _Client(c, _attach(name), self.lay)
+                self.clients.append(cl)
+                if self.register:
+                    _register(cl)
+            self.name = f"fdx-group-{os.getpid()}-{uuid.uuid4().hex[:12]}"
+            self.listener = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            self.listener.bind("\0" + self.name)
+            self.listener.listen(len(self.clients) + 4)
+            self.listener.settimeout(accept_timeout_s)
+        except BaseException:
+            self.close()
+            raise
+        rendezvous.publish_socket(self.name)
+        self.loop = _ScoreLoop(scorer, postprocess, self.clients, int(cfg["batch_max"]), int(cfg["max_bytes"]))
+
+    def serve(self) -> dict:
+        if self.error is not None:
+            return {"batches": 0, "docs": 0, "error": self.error}
+        pending = {cl.idx for cl in self.clients}
+        while pending:
+            s, _ = self.listener.accept()
+            s.settimeout(60.0)
+            hello = b""
+            while len(hello) < _HELLO.size:
+                chunk = s.recv(_HELLO.size - len(hello))
+                if not chunk:
+                    break
+                hello += chunk
+            idx = _HELLO.unpack(hello)[0] if len(hello) == _HELLO.size else -1
+            if idx < 0 or idx not in pending:     # the coordinator aborted the group
+                s.close()
+                return {"batches": self.loop.batches, "docs": self.loop.docs, "error": "aborted"}
+            s.settimeout(None)
+            self.clients[idx].conn = Connection(s.detach())
+            pending.discard(idx)
+        live = {cl.conn: cl for cl in self.clients}
+        sc, loop = self.scorer, self.loop
+        while live or sc.inflight:
+            loop.pump()
+            if not live:
+                loop.finish()
+                continue
+            for conn in mp_wait(list(live), timeout=0.0002 if sc.inflight else 0.05):
+                cl = live[conn]
+                try:
+                    m = conn.recv_bytes()
+                except (EOFError, ConnectionError):
+                    del live[conn]                  # the client exited: the group is closing
+                    continue
+                if m[:1] != _SUB:
+                    raise RuntimeError(f"client {cl.idx}: unexpected message {m[:1]!r} at a peer")
+                loop.submit(cl, m)
+        return {"batches": loop.batches, "docs": loop.docs}
+
+    def close(self) -> None:
+        try:
+            while self.scorer.inflight:
+                self.scorer.collect(copy=False)
+        except Exception as e:                    # noqa: BLE001
+            print(f"[group-peer] scorer drain failed during close: {type(e).__name__}: {e}", file=sys.stderr)
+        try:
+            if getattr(self, "register", False) and torch.cuda.is_available():
+                torch.cuda.synchronize()
+        except Exception as e:                    # noqa: BLE001
+            print(f"[group-peer] synchronize failed during close: {type(e).__name__}: {e}", file=sys.stderr)
+        for cl in self.clients:
+            _unregister(cl)
+            if cl.conn is not None:
+                cl.conn.close()
+            cl.views = cl.slots = None
+            try:
+                cl.shm.close()
+            except BufferError:
+                pass
+        self.clients = []
+        if self.listener is not None:
+            self.listener.close()
+            self.listener = None
 
     def __enter__(self):
         return self
@@ -345,6 +625,8 @@ def merge_results(rs: list) -> dict:
             "produced": sum(r["produced"] for r in rs), "committed": sum(r["committed"] for r in rs),
             "sent": sum(r.get("sent", 0) for r in rs), "batches": sum(r["batches"] for r in rs),
             "explanations": sum(r.get("explanations", 0) for r in rs),
+            "scorer_batches": [int(x) for x in np.sum([r["scorer_batches"] for r in rs if "scorer_batches" in r],
+                                                      axis=0)] if any("scorer_batches" in r for r in rs) else [],
             "p50_ms": h.percentile(50), "p95_ms": h.percentile(95), "p99_ms": h.percentile(99),
             "clients": len(rs), "client_dialogues_per_s": [r["messages"] / max(r["t1"] - r["t0"], 1e-9) for r in rs],
             "client_start_spread_ms": (max(r["t0"] for r in rs) - t0) * 1e3}
@@ -392,7 +674,7 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
 
     c, P = cfg["index"], cfg["n_clients"]
     lay = cfg["layout"]
-    scorer = RemoteScorer(conn, ring, lay["max_docs"], lay["max_bytes"], cfg["depth"])
+    scorer = RemoteScorer([conn] + cfg.get("peer_conns", []), ring, lay["max_docs"], lay["max_bytes"], cfg["depth"])
     if spec["kind"] == "serve":
         return _client_serve(cfg, spec, scorer, ring)
     url = f"memory://group-{os.getpid()}-{spec['tag']}"
@@ -447,6 +729,7 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
     loadgen._drop(url)
     return {"outputs": outputs, "t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"], "committed": committed,
             "batches": st["batches"], "sent": sent, "explanations": st["explanations"],
+            "scorer_batches": list(scorer.sent),
             "lat_counts": eng.stats.latency.counts.tolist(),
             "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"]}
 
@@ -503,7 +786,7 @@ def _client_serve(cfg: dict, spec: dict, scorer: RemoteScorer, ring: SharedRing)
     return {"t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"],
             "committed": st["committed"], "batches": st["batches"], "sent": 0,
             "lat_counts": eng.stats.latency.counts.tolist(), "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"],
-            "summary": st}
+            "scorer_batches": list(scorer.sent), "summary": st}
 
 
 class _PartitionPacer:
@@ -548,11 +831,24 @@ def _attach(name: str):
     return shm
 
 
+def _connect_peers(cfg: dict) -> list:
+    """This client's data connections to the group's peer scoring processes."""
+    out = []
+    for name in cfg.get("peers") or []:
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect("\0" + name)
+        s.sendall(_HELLO.pack(int(cfg["index"])))
+        out.append(Connection(s.detach()))
+    return out
+
+
 def _client_main(cfg: dict) -> int:
     conn = Connection(cfg["fd"])
     shm = _attach(cfg["shm"])
     pool_shm = None
+    peer_conns = []
     try:
+        peer_conns = cfg["peer_conns"] = _connect_peers(cfg)
         ring = SharedRing(_views(shm.buf, cfg["layout"]))
         pool = None
         if cfg["pool"] is not None:
@@ -574,6 +870,9 @@ def _client_main(cfg: dict) -> int:
     except (EOFError, ConnectionError):
         return 0
     finally:
+        for c in peer_conns:
+            c.close()
+        cfg.pop("peer_conns", None)
         ring = pool = None
         import gc
 

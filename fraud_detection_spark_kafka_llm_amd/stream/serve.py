@@ -13,6 +13,10 @@ With --group-clients P the Kafka clients run as P consumer-group member processe
 stream/group.py) around this process's GPU scorer; the broker balances the topic's partitions over
 them (a real bootstrap only: a memory:// broker lives inside one process). Explanations run in
 the client processes (no historical-case insight there).
+Under torchrun (WORLD_SIZE > 1) with --group-clients, every rank is one scoring process on its
+own GPU (LOCAL_RANK): rank 0 starts the client processes, ranks 1..N-1 join as ScorerPeers that
+page-lock the same slots for their device (BASELINE config 5, "3-partition topic -> 8-GPU
+batched inference"); the rendezvous uses the process group's store (gloo, no device collective).
 ``/metrics`` serves the Prometheus text format of the metrics registry when --metrics-port is set.
 """
 from __future__ import annotations
@@ -83,7 +87,14 @@ def main(argv=None) -> int:
     args.batch = args.batch if args.batch is not None else cfg.stream_batch
     args.max_latency_ms = args.max_latency_ms if args.max_latency_ms is not None else cfg.stream_max_latency_ms
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
-    if args.gpus > 0 and torch.cuda.is_available():
+    from ..parallel import dist as D
+
+    ranks = int(os.environ.get("WORLD_SIZE", "1"))
+    if ranks > 1 and args.group_clients > 0:
+        D.init_from_env("gloo")                 # the group's rendezvous store; no device collective
+        devices = [torch.device("cuda", D.local_rank() % torch.cuda.device_count())] \
+            if torch.cuda.is_available() else [torch.device("cpu")]
+    elif args.gpus > 0 and torch.cuda.is_available():
         devices = [torch.device("cuda", i) for i in range(min(args.gpus, torch.cuda.device_count()))]
     else:
         devices = [torch.device("cpu")]
@@ -109,20 +120,28 @@ def main(argv=None) -> int:
 
 
 def _serve_group(args, agent, devices, out_topic: str) -> int:
+    from ..parallel import dist as D
     from .gpu_worker import make_multi_scorer
-    from .group import ConsumerGroup, merge_results
+    from .group import ConsumerGroup, GroupRendezvous, ScorerPeer, merge_results
 
     if os.getenv("KAFKA_BOOTSTRAP_SERVERS", "").startswith("memory://") or os.getenv("FDX_KAFKA", "") == "memory":
         raise SystemExit("--group-clients needs a real Kafka bootstrap (an in-memory broker is per process)")
     fp = agent.fused
     scorer = make_multi_scorer(fp.spec(True), fp.idf.idf if fp.idf is not None else None, fp.model.scorer(),
                                devices, max_docs=args.batch, max_bytes=args.batch * 4096, depth=3)
+    rdv = GroupRendezvous.from_process_group("serve") if D.world_size() > 1 else None
+    if rdv is not None and D.rank() > 0:
+        log.info("rank %d: scoring process of the group on %s", D.rank(), devices[0])
+        with ScorerPeer(scorer, fp.model.postprocess_numpy, rdv) as peer:
+            st = peer.serve()
+        print(json.dumps({"rank": D.rank(), **st}), flush=True)
+        return 0
     if args.metrics_port:
         start_metrics_server(args.metrics_port)
-    log.info("serving %s on %s with %d client processes -> %s", args.model, [str(d) for d in devices],
-             args.group_clients, out_topic)
+    log.info("serving %s on %s with %d client processes (%d scoring processes) -> %s", args.model,
+             [str(d) for d in devices], args.group_clients, D.world_size(), out_topic)
     with ConsumerGroup(scorer, fp.model.postprocess_numpy, args.group_clients, batch_max=args.batch,
-                       max_latency_ms=args.max_latency_ms, max_bytes=args.batch * 4096) as grp:
+                       max_latency_ms=args.max_latency_ms, max_bytes=args.batch * 4096, rendezvous=rdv) as grp:
         P, m = args.group_clients, args.max_messages
         share = None if m is None else [{"max_messages": m // P + (1 if c < m % P else 0)} for c in range(P)]
         rs = grp.run({"kind": "serve", "max_messages": m, "idle_timeout": args.idle_timeout,

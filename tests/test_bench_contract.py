@@ -34,6 +34,9 @@ def _check(rec: dict, n: int):
     assert rec["kafka_all_delivered_and_committed"] and rec["kafka_multi_gpu_all_committed"]
     assert rec["kafka_confluent_group_dialogues_per_s"] > 0 and rec["kafka_confluent_group_clients"] == 3
     assert rec["kafka_confluent_group_all_committed"]
+    # config 5: a scoring process per rank, each on its own GPU, every one of them fed
+    assert rec["kafka_multi_gpu_scorer_procs"] == n and rec["kafka_confluent_group_scorer_procs"] == n
+    assert len(rec["kafka_multi_gpu_batches_per_scorer"]) == n and min(rec["kafka_multi_gpu_batches_per_scorer"]) > 0
 
 
 @pytest.mark.gpu

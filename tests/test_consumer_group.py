@@ -146,3 +146,72 @@ def test_group_gpu_scorer_registered_slots(agent):
             assert abs(rec["confidence"] - float(p1[i])) <= 1e-12
             n += 1
     assert n == 3000
+
+
+def _group_rank(rank, world, model_path, n, device="cpu"):
+    """One rank of a multi-process scoring group: rank 0 coordinates (segments, clients, its own
+    scorer), every other rank is a ScorerPeer on its own device."""
+    import torch
+
+    agent = ClassificationAgent(model_path, llm=StubLLM(), device="cpu")
+    fp = agent.fused
+    dev = torch.device(device)
+    sc = make_scorer(fp.spec(True), fp.idf.idf, fp.model.scorer(), dev, max_docs=256, max_bytes=256 * 4096,
+                     depth=2)
+    rdv = G.GroupRendezvous.from_process_group("test-multi")
+    if rank == 0:
+        pt, _ = synth.generate(synth.SynthConfig(n=400, seed=12), device="cpu")
+        pool = MessagePool(pt.strings())
+        with G.ConsumerGroup(sc, fp.model.postprocess_numpy, 3, batch_max=256, max_latency_ms=2.0,
+                             max_bytes=256 * 4096, pool=pool, confluent=False, rendezvous=rdv) as grp:
+            assert grp.n_scorers == world
+            r = G.group_throughput_run(grp, n, return_outputs=True)
+            local = grp.local_batches
+        outs = [(k, v) for o in r.pop("outputs") for k, v in o]
+        return {"run": r, "local_batches": local, "outputs": outs, "texts": pt.strings()}
+    with G.ScorerPeer(sc, fp.model.postprocess_numpy, rdv) as peer:
+        return {"peer": peer.serve()}
+
+
+def test_group_scores_on_every_rank_process(agent, tmp_path):
+    """BASELINE config 5 topology: one 3-partition topic, a scoring process per rank (rank 0 the
+    coordinator, rank 1 a ScorerPeer), each with its own scorer; every record scored once,
+    produced and committed, and both processes scored micro-batches."""
+    from fraud_detection_spark_kafka_llm_amd.parallel.launch import spawn
+
+    path = tmp_path / "model"
+    agent.model.save(str(path))
+    n = 6000
+    r0, r1 = spawn(_group_rank, 2, str(path), n, backend="gloo")
+    run = r0["run"]
+    assert run["messages"] == run["produced"] == run["committed"] == n
+    assert len(run["scorer_batches"]) == 2 and min(run["scorer_batches"]) > 0
+    assert r1["peer"]["batches"] == run["scorer_batches"][1] > 0
+    assert r0["local_batches"] == run["scorer_batches"][0]
+    texts = r0["texts"]
+    pred, p1 = _expected(agent, texts)
+    for key, val in r0["outputs"]:
+        i = int(key.decode()[3:])
+        rec = json.loads(val)
+        assert rec["prediction"] == float(pred[i]) and rec["confidence"] == float(p1[i])
+    assert len(r0["outputs"]) == n
+
+
+@pytest.mark.gpu
+def test_gpu_group_two_rank_processes_share_the_topic(agent, tmp_path):
+    """Two rank processes scoring one shared topic on the GPU (both on cuda:0 on a 1-GPU box: each
+    page-locks the clients' segments for its own context)."""
+    from fraud_detection_spark_kafka_llm_amd.parallel.launch import spawn
+
+    path = tmp_path / "model"
+    agent.model.save(str(path))
+    n = 20000
+    r0, r1 = spawn(_group_rank, 2, str(path), n, "cuda:0", backend="gloo")
+    run = r0["run"]
+    assert run["messages"] == run["produced"] == run["committed"] == n
+    assert min(run["scorer_batches"]) > 0 and r1["peer"]["batches"] == run["scorer_batches"][1]
+    pred, p1 = _expected(agent, r0["texts"])
+    for key, val in r0["outputs"]:
+        i = int(key.decode()[3:])
+        rec = json.loads(val)
+        assert rec["prediction"] == float(pred[i]) and abs(rec["confidence"] - float(p1[i])) <= 1e-12
