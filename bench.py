@@ -76,6 +76,7 @@ from fraud_detection_spark_kafka_llm_amd.utils.profiling import run_profiled_if_
 
 METRIC = "dialogues/sec streaming inference + GBDT train sec on 10M rows, 1/2/4/8 GPU"
 F = 1 << 18
+CHUNK_ROWS = 500_000       # rows per featurization chunk (pinned text, H2D overlapped with the kernel)
 
 
 def sync_all(dev):
@@ -185,9 +186,12 @@ def warmup_training(dev, spec, params: GBDTParams, rf_depth: int = 0) -> None:
     """Untimed: the pinned H2D copy path plus a small fit through the production path
     (models/warmup.py: lazily loaded kernel code objects, cold caching allocators). Every rank runs
     it on the same rows, so under data parallelism its collectives warm RCCL too."""
-    pt, _ = synth.generate(synth.SynthConfig(n=1 << 14, seed=5), device=dev, start=3 * 10**9)
-    host = T.PackedText(pt.data.cpu().pin_memory(), pt.offsets.cpu().pin_memory())
-    T.featurize_score(host.to(dev, non_blocking=True), spec, want_csr=True, device=dev).csr()
+    # the timed phase's featurization path itself (chunked H2D + fused kernel + the per-chunk
+    # feature-order sort and its merge) on a small pinned shard: its first run in a process cost
+    # ~0.33 s extra (kernel code objects loaded on first launch; profiles/r4/cold_*.jsonl)
+    small = generate_shard(3 * 10**9, 3 * 10**9 + (1 << 15), dev, seed=5, chunk=1 << 14)
+    featurize_shard(small, dev, spec, order=True)
+    del small
     warm_tree_kernels(dev, gbdt_depth=params.max_depth, gbdt_max_bin=params.max_bin, forest_depth=rf_depth,
                       forest_subset="sqrt")
 
@@ -385,9 +389,13 @@ def main():
     warm_sec = time.perf_counter() - t0
     lo, hi = D.shard_range(args.rows)
     t0 = time.perf_counter()
-    chunks = generate_shard(lo, hi, dev, seed=11)
+    chunks = generate_shard(lo, hi, dev, seed=11, chunk=CHUNK_ROWS)
+    text_bytes = sum(int(h.data.numel()) for h, _ in chunks)
     gen_sec = max_over_ranks(time.perf_counter() - t0, dev)
+    gen_peak = torch.cuda.max_memory_allocated(dev)
     sync_all(dev)
+    # the HBM peak of the timed phase only (the untimed corpus generation runs on the device too)
+    torch.cuda.reset_peak_memory_stats(dev)
     t0 = time.perf_counter()
     # CSR + CSC by feature (docFreq now, the trainer's columns later), the sort overlapped with H2D
     indptr, idx, counts, y, fo = featurize_shard(chunks, dev, spec, order=True)
@@ -405,10 +413,16 @@ def main():
     shard_rows, shard_nnz = len(vc), vc.nnz
     # HBM sizing rule (utils/memory.py): rows one GPU could train at this corpus' entries per row,
     # against the device's total memory (the bench's own allocations excluded)
+    shape = dict(hot_features=res.shape.get("hot", memory.DEFAULT_HOT_FEATURES),
+                 groups=res.shape.get("groups", memory.DEFAULT_GROUPS) or memory.DEFAULT_GROUPS,
+                 text_bytes_per_row=text_bytes / max(shard_rows, 1), chunk_rows=CHUNK_ROWS)
+    modeled = memory.pipeline_bytes(shard_rows, shard_nnz, **shape)
     sizing = {"max_rows_per_gpu": memory.max_rows_per_gpu(
-                  shard_nnz / max(shard_rows, 1), budget_bytes=int(torch.cuda.get_device_properties(dev).total_memory * 0.9)),
-              "train_model_bytes_per_row": memory.training_bytes(shard_rows, shard_nnz) / max(shard_rows, 1),
-              "train_peak_bytes_per_row": gbdt_peak / max(shard_rows, 1)}
+                  shard_nnz / max(shard_rows, 1), budget_bytes=int(torch.cuda.get_device_properties(dev).total_memory * 0.9),
+                  **shape),
+              "train_model_bytes_per_row": modeled / max(shard_rows, 1),
+              "train_peak_bytes_per_row": gbdt_peak / max(shard_rows, 1),
+              "train_peak_over_model": gbdt_peak / max(modeled, 1.0)}
     del chunks
     rf = {}
     if args.rf_trees > 0:
@@ -505,6 +519,7 @@ def main():
                 kafka[k] = max_over_ranks(kafka[k], dev)
 
     gbdt_peak_gb = max_over_ranks(gbdt_peak / 2 ** 30, dev)
+    gen_peak_gb = max_over_ranks(gen_peak / 2 ** 30, dev)
     docs = args.steps * args.batch * world
     if rank == 0:
         out = {
@@ -530,6 +545,7 @@ def main():
             "gbdt_warmup_sec_untimed": warm_sec,
             "gbdt_nodes_tree0": res.trees[0].num_nodes,
             "gbdt_peak_hbm_gb": gbdt_peak_gb,
+            "datagen_peak_hbm_gb_untimed": gen_peak_gb,
             **sizing,
             **rf,
             "stream_accuracy": acc,

@@ -28,13 +28,40 @@ def load(dirs, match):
     return val, disp, dur
 
 
+def per_dispatch(dirs, match, n):
+    """Counters of the first ``n`` dispatches of each matching kernel, per pass directory (e.g.
+    the root vs the deeper levels of a tree: one histogram dispatch per level)."""
+    for d in dirs:
+        rows = collections.defaultdict(lambda: collections.defaultdict(dict))
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(path)):
+                if match and match not in r["Kernel_Name"]:
+                    continue
+                k = (r["Kernel_Name"][:60], int(r["Dispatch_Id"]))
+                rows[k[0]][k[1]][r["Counter_Name"]] = float(r["Counter_Value"])
+                rows[k[0]][k[1]]["_us"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        for kern, ds in rows.items():
+            print(f"\n[{os.path.basename(d)}] {kern}")
+            for i, did in enumerate(sorted(ds)[:n]):
+                c = ds[did]
+                extra = ""
+                if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
+                    extra = f"  lds_conflict/active {c['SQ_LDS_BANK_CONFLICT'] / c['SQ_LDS_IDX_ACTIVE']:.3f}"
+                cs = "  ".join(f"{k}={v:.4g}" for k, v in sorted(c.items()) if k != "_us")
+                print(f"  #{i:3d} {c['_us']:9.1f} us{extra}  {cs}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--match", default="")
     ap.add_argument("--md", action="store_true")
+    ap.add_argument("--per-dispatch", type=int, default=0,
+                    help="also list the first N dispatches of each kernel (duration + conflict ratio), by pass")
     args = ap.parse_args()
     val, disp, dur = load(args.dirs, args.match)
+    if args.per_dispatch:
+        per_dispatch(args.dirs, args.match, args.per_dispatch)
     for k in sorted(val, key=lambda k: -sum(dur[k].values())):
         c = val[k]
         n_pass = len({d for d, _ in disp[k]})

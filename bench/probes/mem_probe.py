@@ -66,7 +66,7 @@ def main():
         st.extra = {"nnz": int(idx.numel()), "nnz_per_row": round(idx.numel() / n, 2),
                     "idx_dtype": str(idx.dtype), "counts_dtype": str(counts.dtype)}
     nnz = int(idx.numel())
-    model = memory.stage_bytes(n, nnz) if hasattr(memory, "stage_bytes") else {}
+    text_bytes = sum(int(h.data.numel()) for h, _ in chunks)
     with Stage("idf+tfidf", n) as st:
         idf = torch.log((n + 1.0) / (fo.df.double() + 1.0))
         vc = VectorColumn.tfidf(B.F, indptr, idx, counts, idf, fo)
@@ -81,7 +81,9 @@ def main():
     with Stage("fit_gbdt", n) as st:
         res = fit_gbdt(vc, y, params, device=dev)
         st.extra = {"trees": len(res.trees)}
-    print(json.dumps({"model": model, "training_bytes_model_gb": round(memory.training_bytes(n, nnz) / GB, 3),
+    shape = dict(hot_features=res.shape["hot"], groups=res.shape["groups"] or memory.DEFAULT_GROUPS)
+    print(json.dumps({"model_featurize_gb": round(memory.featurize_bytes(n, nnz, text_bytes / n) / GB, 3),
+                      "model_training_gb": round(memory.training_bytes(n, nnz, **shape) / GB, 3), **shape,
                       "max_memory_reserved_gb": round(torch.cuda.max_memory_reserved() / GB, 3)}), flush=True)
 
 

@@ -154,7 +154,8 @@ void featurize_score(const Tensor& text, const Tensor& doc_off, int64_t flags, i
   FDX_CHECK(D >= 0, "doc_off needs at least one entry");
   for (const Tensor* t : {&out_idx, &out_val, &out_nnz}) check_dev(*t, dev, "outputs");
   FDX_CHECK(out_nnz.numel() >= D && out_status.numel() >= D, "per-doc outputs too small");
-  FDX_CHECK(out_idx.numel() >= text.numel() + D || !(flags & fdx::kFlagWriteCsr), "CSR scratch too small");
+  FDX_CHECK(out_idx.numel() >= fdx::csr_capacity(text.numel(), D) || !(flags & fdx::kFlagWriteCsr),
+            "CSR scratch too small");
   FDX_CHECK(out_idx.numel() == out_val.numel(), "CSR idx/val size mismatch");
   FDX_CHECK(num_features > 0 || (flags & fdx::kFlagVocab), "num_features must be positive");
   if (flags & fdx::kFlagIdf) FDX_CHECK(idf && idf->numel() >= num_features && idf->scalar_type() == at::kDouble, "idf");

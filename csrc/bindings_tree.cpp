@@ -335,132 +335,6 @@ void slot_pack(const Tensor& row_node, const Tensor& node_slot, int64_t nslots, 
   }
 }
 
-// Blocked CSC build (tree.h "row-blocked histogram engine"): pass 0 adds the entry count of every
-// (chunk, 16-bin tile) sub-segment to counts [n_chunks * NG * 4] (int32); pass 1 writes ent_row /
-// ent_key at the sub-segment cursors [n_chunks * NG * 4] (int64, advanced).
-void blk_build(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& colptr, const Tensor& boff,
-               int64_t chunk_rows, int64_t NG, int64_t pass, const optional<Tensor>& counts,
-               const optional<Tensor>& cursor, const optional<Tensor>& ent_row, const optional<Tensor>& ent_key) {
-  const auto dev = csc_row.device();
-  chk(csc_row, dev, at::kInt, "csc_row");
-  chk(csc_bin, dev, at::kByte, "csc_bin");
-  chk(colptr, dev, at::kLong, "colptr");
-  chk(boff, dev, at::kLong, "boff");
-  FDX_CHECK(colptr.numel() == boff.numel(), "colptr / boff must both be [Fa + 1]");
-  FDX_CHECK(chunk_rows == fdx::kBlkRows, "chunk_rows must equal kBlkRows");
-  fdx::BlkBuildArgs a{};
-  a.csc_row = csc_row.data_ptr<int32_t>();
-  a.csc_bin = csc_bin.data_ptr<uint8_t>();
-  a.colptr = colptr.data_ptr<int64_t>();
-  a.boff = boff.data_ptr<int64_t>();
-  a.Fa = (int32_t)(colptr.numel() - 1);
-  a.nnz = csc_row.numel();
-  a.NG = (int32_t)NG;
-  a.chunk_rows = (int32_t)chunk_rows;
-  a.entries_per_thread = 64;
-  if (pass == 0) {
-    FDX_CHECK(counts.has_value(), "pass 0 needs counts");
-    chk(*counts, dev, at::kInt, "counts");
-    a.counts = counts->data_ptr<int32_t>();
-  } else {
-    FDX_CHECK(cursor && ent_row && ent_key, "pass 1 needs cursor, ent_row, ent_key");
-    chk(*cursor, dev, at::kLong, "cursor");
-    FDX_CHECK(ent_row->device() == dev && ent_row->scalar_type() == at::kShort && ent_row->is_contiguous(),
-              "ent_row must be int16 (uint16 bits)");
-    chk(*ent_key, dev, at::kByte, "ent_key");
-    FDX_CHECK(ent_row->numel() >= a.nnz && ent_key->numel() >= a.nnz, "entry buffers too small");
-    a.cursor = cursor->data_ptr<int64_t>();
-    a.ent_row = reinterpret_cast<uint16_t*>(ent_row->data_ptr<int16_t>());
-    a.ent_key = ent_key->data_ptr<uint8_t>();
-  }
-  if (dev.is_cuda()) {
-    c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_blk_build(a, (int)pass, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  } else {
-    fdx::blk_build_cpu(a, (int)pass);
-  }
-}
-
-// Row-blocked histogram pass: hist[(slot_node[s] * stride + off(bin)) * 2 + stat] += exact sums
-// over the BCSC segments of the work plan (wg_band / wg_c0 / wg_c1 / band_groups [bands, 7, gw]).
-// slot8 = None: root pass (every row in slot 0; rowdig may be the masked single-slot copy).
-void hist_blk(const Tensor& ent_row, const Tensor& ent_key, const Tensor& seg, int64_t NG, const Tensor& rowdig,
-              const optional<Tensor>& slot8_t, const Tensor& wg_band, const Tensor& wg_c0, const Tensor& wg_c1,
-              const Tensor& band_groups, int64_t gw, const Tensor& slot_node, const Tensor& hist, int64_t TB,
-              int64_t ct, const optional<Tensor>& shard_lo, int64_t shard_stride) {
-  const auto dev = ent_key.device();
-  FDX_CHECK(ent_row.device() == dev && ent_row.scalar_type() == at::kShort && ent_row.is_contiguous(), "ent_row");
-  chk(ent_key, dev, at::kByte, "ent_key");
-  chk(seg, dev, at::kLong, "seg");
-  chk(rowdig, dev, at::kInt, "rowdig");
-  if (slot8_t) chk(*slot8_t, dev, at::kByte, "slot8");
-  chk(wg_band, dev, at::kInt, "wg_band");
-  chk(wg_c0, dev, at::kInt, "wg_c0");
-  chk(wg_c1, dev, at::kInt, "wg_c1");
-  chk(band_groups, dev, at::kInt, "band_groups");
-  chk(slot_node, dev, at::kInt, "slot_node");
-  chk(hist, dev, at::kLong, "hist");
-  FDX_CHECK(ct == 1 || ct == 2, "the row-blocked pass builds CT <= 2 (<= 4 node slots)");
-  FDX_CHECK(slot8_t || ct == 1, "the root pass has one column tile");
-  FDX_CHECK(gw == fdx::blk_groups_per_wave(slot8_t ? (int)ct : 1), "band_groups stride != groups per wave");
-  FDX_CHECK(band_groups.numel() % (fdx::kBlkCompute * gw) == 0, "band_groups must be [bands, kBlkCompute, gw]");
-  const int64_t N = rowdig.size(0);
-  FDX_CHECK(rowdig.dim() == 2 && rowdig.size(1) == 2, "rowdig must be [N, 2] int32");
-  FDX_CHECK(reinterpret_cast<uintptr_t>(rowdig.data_ptr()) % 16 == 0, "rowdig must be 16-byte aligned");
-  FDX_CHECK(!slot8_t || (slot8_t->numel() >= N && reinterpret_cast<uintptr_t>(slot8_t->data_ptr()) % 16 == 0),
-            "slot8 must cover the rows, 16-byte aligned");
-  const int64_t n_chunks = (N + fdx::kBlkRows - 1) / fdx::kBlkRows;
-  FDX_CHECK(seg.numel() == n_chunks * NG * fdx::kBlkTiles + 1, "seg must be [n_chunks * NG * 4 + 1]");
-  FDX_CHECK(readable_tail(ent_row, 4) && readable_tail(ent_key, 4), "entry arrays need 4 readable padding entries");
-  FDX_CHECK(reinterpret_cast<uintptr_t>(ent_row.data_ptr()) % 8 == 0 &&
-                reinterpret_cast<uintptr_t>(ent_key.data_ptr()) % 4 == 0, "entry arrays alignment");
-  const int64_t nslots = slot_node.numel();
-  FDX_CHECK(nslots >= 1 && nslots <= 2 * ct, "slot_node must have 1 .. 2*ct entries");
-  FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2, "hist must be [rows, stride, 2] int64");
-  FDX_CHECK(wg_c0.numel() == wg_band.numel() && wg_c1.numel() == wg_band.numel(), "work plan arrays");
-  fdx::BlkHistArgs a{};
-  a.ent_row = reinterpret_cast<const uint16_t*>(ent_row.data_ptr<int16_t>());
-  a.ent_key = ent_key.data_ptr<uint8_t>();
-  a.seg = seg.data_ptr<int64_t>();
-  a.NG = (int32_t)NG;
-  a.n_chunks = (int32_t)n_chunks;
-  a.N = N;
-  a.rowdig = reinterpret_cast<const uint32_t*>(rowdig.data_ptr<int32_t>());
-  a.slot8 = slot8_t ? slot8_t->data_ptr<uint8_t>() : nullptr;
-  a.wg_band = wg_band.data_ptr<int32_t>();
-  a.wg_c0 = wg_c0.data_ptr<int32_t>();
-  a.wg_c1 = wg_c1.data_ptr<int32_t>();
-  a.n_wg = (int32_t)wg_band.numel();
-  a.band_groups = band_groups.data_ptr<int32_t>();
-  a.gw = (int32_t)gw;
-  a.slot_node = slot_node.data_ptr<int32_t>();
-  a.nslots = (int32_t)nslots;
-  a.TB = TB;
-  a.hist_stride = hist.size(1);
-  a.hist = hist.data_ptr<int64_t>();
-  if (shard_lo) {
-    chk(*shard_lo, dev, at::kLong, "shard_lo");
-    a.nshards = (int32_t)(shard_lo->numel() - 1);
-    a.shard_lo = shard_lo->data_ptr<int64_t>();
-    a.shard_stride = shard_stride;
-    FDX_CHECK(hist.size(0) >= a.nshards * nslots, "shard-major hist rows");
-  } else {
-    FDX_CHECK(hist.size(1) >= TB, "hist stride smaller than the total bin count");
-  }
-  const char* dbg = std::getenv("FDX_BLK_DBG");
-  a.dbg = dbg ? std::atoi(dbg) : 0;
-
-  if (dev.is_cuda()) {
-    c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_hist_blk(a, (int)ct, stream(dev));
-    C10_HIP_KERNEL_LAUNCH_CHECK();
-  } else {
-    fdx::hist_blk_cpu(a);
-  }
-}
-
-int64_t blk_gw(int64_t ct) { return fdx::blk_groups_per_wave((int)ct); }
 
 // Row-group CSR build from the quantized CSC. pass 0: ptr [G, N + 1] int32 (zeroed) += entry
 // counts at [g][r + 1]; pass 1: cursor [G, N] (the exclusive starts) advanced, ent (uint16 bits in
@@ -1098,9 +972,6 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_hist_build", &hist_build);
   m.def("tree_hist_sampled", &hist_sampled);
   m.def("tree_slot_pack", &slot_pack);
-  m.def("tree_blk_build", &blk_build);
-  m.def("tree_hist_blk", &hist_blk);
-  m.def("tree_blk_gw", &blk_gw);
   m.def("tree_rg_build", &rg_build);
   m.def("tree_rg_list", &rg_list);
   m.def("tree_rg_build_csr", &rg_build_csr);

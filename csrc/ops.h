@@ -89,13 +89,6 @@ void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const 
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
                        int64_t f0, int64_t* out, hipStream_t s);
 void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s);
-struct BlkBuildArgs;
-struct BlkHistArgs;
-void launch_blk_build(const BlkBuildArgs& a, int pass, hipStream_t s);
-void launch_hist_blk(const BlkHistArgs& a, int ct, hipStream_t s);
-int blk_groups_per_wave(int ct);
-void blk_build_cpu(const BlkBuildArgs& a, int pass);
-void hist_blk_cpu(const BlkHistArgs& a);
 struct RgBuildArgs;
 struct RgListArgs;
 struct RgHistArgs;

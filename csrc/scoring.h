@@ -5,6 +5,14 @@
 
 namespace fdx {
 
+// CSR scratch layout of the fused featurizer: a document of L bytes has at most floor((L + 1) / 2)
+// non-empty whitespace-separated tokens plus the empty one, i.e. <= floor(L / 2) + 2 distinct
+// terms, so doc d starting at byte s gets the slot range [s / 2 + 2 d, s / 2 + 2 d + L / 2 + 2)
+// (disjoint from its successor's: (s + L) / 2 - s / 2 >= L / 2). Capacity: bytes / 2 + 2 D + 1
+// -- half of a slot per byte (4 B of indices + 4 B of values per text byte before).
+FDX_HD int64_t csr_slot(int64_t s, int64_t d) { return (s >> 1) + 2 * d; }
+FDX_HD int64_t csr_capacity(int64_t bytes, int64_t docs) { return (bytes >> 1) + 2 * docs + 1; }
+
 // Flattened tree ensemble (DecisionTree / RandomForest / GBDT).
 // node is a leaf iff feat[node] < 0; leaf payload = leaf[node * K + k].
 struct TreeEnsemble {
@@ -77,7 +85,7 @@ struct FeatArgs {
   double lr_b;
   TreeEnsemble trees;
   // outputs
-  int32_t* out_idx;          // CSR scratch, capacity len+1 at doc_off[d] + d
+  int32_t* out_idx;          // CSR scratch: doc d's entries at csr_slot(doc_off[d], d) (csr_slot above)
   float* out_val;
   int32_t* out_nnz;          // [num_docs]
   int32_t* out_ntok;         // [num_docs] tokens after stop-word removal (may be null)

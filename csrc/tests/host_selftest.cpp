@@ -116,7 +116,7 @@ static void test_featurizer() {
     for (auto& t : toks)
       ref[non_negative_mod(murmur3_bytes(reinterpret_cast<const uint8_t*>(t.data()), (uint32_t)t.size(), 42u), F)] += 1;
     EXPECT(nnz[d] == (int32_t)ref.size());
-    const int64_t base = off[d] + d;
+    const int64_t base = csr_slot(off[d], d);
     for (int32_t j = 0; j < nnz[d] && j < (int32_t)ref.size(); ++j) EXPECT(ref.count(idx[base + j]) && ref[idx[base + j]] == val[base + j]);
   }
 

@@ -102,7 +102,7 @@ void process_doc(const FeatArgs& a, int32_t d, std::string& clean, std::vector<u
   }
   const bool binary = (a.flags & kFlagBinary) != 0;
   const bool use_idf = (a.flags & kFlagIdf) != 0;
-  const int64_t ob = s + d;
+  const int64_t ob = csr_slot(s, d);
   double lr = 0.0;
   const int32_t nu = (int32_t)runs.size();
   std::vector<double> vals(nu);

@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kWave * WAVES) void featurize_score_kernel(FeatArgs
   // ------------------------------------------------------------------ 6-7. values + score
   const bool binary = (a.flags & kFlagBinary) != 0;
   const bool use_idf = (a.flags & kFlagIdf) != 0;
-  const int64_t ob = s + d;   // CSR scratch base (capacity len + 1)
+  const int64_t ob = csr_slot(s, d);   // CSR scratch base (scoring.h)
   double lr_part = 0.0;
   for (int j = lane; j < nu; j += kWave) {
     const uint32_t u = s_tok[j];

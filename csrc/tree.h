@@ -113,83 +113,6 @@ struct HistArgs {
 // waves of a listed histogram pass (they stride over the active items): 8 per SIMD of 256 CUs
 constexpr int32_t kListedWaves = 8192;
 
-// ------------------------------------------------------------------ row-blocked histogram engine
-// Blocked CSC ("BCSC", models/quantize.py build_blocked): the rows are cut into chunks of
-// kBlkRows and the global bin space (all features' bins concatenated, boff) into groups of
-// kBlkKeys consecutive bins. The entries of chunk c and group g form segment c * NG + g
-// (chunk-major), each entry a (uint16 row offset inside the chunk, uint8 bin - 64 g) pair. Inside a
-// segment the entries are ordered by 16-bin tile: the offset table has one start per (chunk,
-// tile) -- seg[(c * NG + g) * 4 + t] -- so segment (c, g) is [seg[4 (c NG + g)], seg[4 (c NG + g) + 4]).
-// The histogram kernel (blk_kernels.hip) gives a workgroup a range of chunks and every wave a
-// few groups: per chunk the workgroup stages the chunk's row state (8-byte digit words, slot
-// bytes) in LDS with coalesced loads, so no entry gathers anything from global memory, and the
-// waves keep their groups' i8-MFMA accumulators in registers across the whole chunk range.
-// A workgroup is kBlkWaves waves: kBlkCompute compute waves plus one staging wave that copies the
-// next chunk's row state into the other LDS buffer while the others compute (loads retire in
-// order per wave, so a compute wave's own prefetch would be waited for at its next entry load).
-constexpr int kBlkRows = 4096;
-constexpr int kBlkKeys = 64;
-constexpr int kBlkTiles = 4;                // 16-bin MFMA row tiles per group: segments are tile-sorted
-constexpr int kBlkWaves = 8;                // 512 threads: 2 waves per SIMD, 256 registers each
-constexpr int kBlkCompute = kBlkWaves - 1;
-constexpr int kBlkGroupsMax = 8;            // groups per compute wave at CT = 1 (128 accumulator registers)
-
-struct BlkBuildArgs {
-  const int32_t* csc_row;         // feature-major CSC (quantized)
-  const uint8_t* csc_bin;
-  const int64_t* colptr;          // [Fa + 1]
-  const int64_t* boff;            // [Fa + 1]
-  int32_t Fa;
-  int64_t nnz;
-  int32_t NG;                     // bin groups
-  int32_t chunk_rows;
-  int32_t entries_per_thread;
-  int32_t* counts;                // pass 0: [n_chunks * NG * 4] += entries per (chunk, tile)
-  int64_t* cursor;                // pass 1: [n_chunks * NG * 4] next free slot of each (chunk, tile) (advanced)
-  uint16_t* ent_row;              // pass 1 out
-  uint8_t* ent_key;
-};
-
-struct BlkHistArgs {
-  const uint16_t* ent_row;        // BCSC entries (readable padding behind the end)
-  const uint8_t* ent_key;
-  const int64_t* seg;             // [n_chunks * NG * 4 + 1] (chunk, tile) starts
-  int32_t NG;
-  int32_t n_chunks;
-  int64_t N;                      // rows
-  const uint32_t* rowdig;         // [N * 2] digit words (masked ones for single-slot passes)
-  const uint8_t* slot8;           // [N] pass slot of each row (0xff none); nullptr: root pass
-  // work plan: workgroup w covers chunks [wg_c0[w], wg_c1[w]) for the groups of band wg_band[w];
-  // band b lists kBlkCompute * gw group ids (-1: none), wave-major
-  const int32_t* wg_band;
-  const int32_t* wg_c0;
-  const int32_t* wg_c1;
-  int32_t n_wg;
-  const int32_t* band_groups;
-  int32_t gw;
-  // output: hist[(slot_node[s] * hist_stride + off(bin)) * 2 + stat] +=
-  const int32_t* slot_node;
-  int32_t nslots;
-  int64_t TB;
-  int64_t hist_stride;
-  int64_t* hist;
-  // data-parallel shard-major histogram rows: bin in shard s -> s * shard_stride + bin - shard_lo[s]
-  int32_t nshards;                // 0: off(bin) = bin
-  const int64_t* shard_lo;        // [nshards + 1]
-  int64_t shard_stride;
-  // diagnostics (bench/probes/blk_probe.py; FDX_BLK_DBG, results wrong when set): bit 0 skips the
-  // K-steps, bit 1 the step staging, bit 2 the staging wave's row-state loads
-  int32_t dbg;
-};
-
-// histogram column offset of global bin b (shard-major DP layout or plain)
-FDX_HD int64_t blk_bin_offset(const BlkHistArgs& a, int64_t b) {
-  if (a.nshards <= 0) return b;
-  int s = 0;
-  while (s + 1 < a.nshards && b >= a.shard_lo[s + 1]) ++s;
-  return (int64_t)s * a.shard_stride + b - a.shard_lo[s];
-}
-
 // ------------------------------------------------------------------ row-group histogram engine
 // Row-group CSR ("RG", models/quantize.py RowGroups): the active features are packed, densest
 // first, into groups of at most kRgBins local bins (a feature's bins stay contiguous inside its
@@ -299,7 +222,8 @@ struct RgHistArgs {
   const int32_t* slot_node;
   int64_t hist_stride;
   int64_t* hist;
-  int32_t nshards;                // 0: off(c) = c; else shard-major rows as BlkHistArgs
+  int32_t nshards;                // 0: off(c) = c; else column c of shard s (shard_lo[s] <= c <
+                                  //   shard_lo[s + 1]) -> s * shard_stride + c - shard_lo[s]
   const int64_t* shard_lo;
   int64_t shard_stride;
 };

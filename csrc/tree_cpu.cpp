@@ -129,56 +129,6 @@ void hist_cpu(const HistArgs& h, int bt, int np) {
   });
 }
 
-// Blocked CSC build (host twin of blk_build_kernel): pass 0 counts the entries of every
-// (chunk, group) segment, pass 1 appends each entry at its segment's cursor (sequential, so the
-// host order inside a segment is the CSC order; any order gives the same exact sums).
-void blk_build_cpu(const BlkBuildArgs& a, int pass) {
-  int32_t f = 0;
-  for (int64_t e = 0; e < a.nnz; ++e) {
-    while (e >= a.colptr[f + 1]) ++f;
-    const int64_t gb = a.boff[f] + a.csc_bin[e];
-    const int64_t key = (int64_t)(a.csc_row[e] / a.chunk_rows) * (kBlkTiles * a.NG) + gb / 16;
-    if (pass == 0) {
-      a.counts[key] += 1;
-    } else {
-      const int64_t at = a.cursor[key]++;
-      a.ent_row[at] = (uint16_t)(a.csc_row[e] % a.chunk_rows);
-      a.ent_key[at] = (uint8_t)(gb % kBlkKeys);
-    }
-  }
-}
-
-// Host twin of hist_blk_kernel, following the same work plan (so a test on the host checks that
-// the plan covers every (chunk, group) segment exactly once).
-void hist_blk_cpu(const BlkHistArgs& a) {
-  parallel_for(a.n_wg, 0, 1, [&](int64_t lo, int64_t hi) {
-    for (int64_t w = lo; w < hi; ++w) {
-      const int band = a.wg_band[w];
-      for (int wv = 0; wv < kBlkCompute; ++wv)
-        for (int j = 0; j < a.gw; ++j) {
-          const int32_t grp = a.band_groups[((int64_t)band * kBlkCompute + wv) * a.gw + j];
-          if (grp < 0) continue;
-          for (int32_t c = a.wg_c0[w]; c < a.wg_c1[w]; ++c) {
-            const int64_t* sg = a.seg + ((int64_t)c * a.NG + grp) * kBlkTiles;
-            const int64_t s0 = sg[0], s1 = sg[kBlkTiles];
-            for (int64_t e = s0; e < s1; ++e) {
-              const int64_t row = (int64_t)c * kBlkRows + a.ent_row[e];
-              const int s = a.slot8 ? (int)a.slot8[row] : 0;
-              if (s >= a.nslots) continue;
-              const int node = a.slot_node[s];
-              const int64_t bin = (int64_t)grp * kBlkKeys + a.ent_key[e];
-              if (node < 0 || bin >= a.TB) continue;
-              const uint32_t* d = a.rowdig + 2 * row;
-              int64_t* dst = a.hist + ((int64_t)node * a.hist_stride + blk_bin_offset(a, bin)) * 2;
-              __atomic_fetch_add(dst, undigits4(d[0]), __ATOMIC_RELAXED);
-              __atomic_fetch_add(dst + 1, undigits4(d[1]), __ATOMIC_RELAXED);
-            }
-          }
-        }
-    }
-  });
-}
-
 // Row-group CSR build (host twin of rg_build_kernel): sequential, so each (group, row) run keeps
 // the CSC order (any order gives the same exact sums).
 void rg_build_cpu(const RgBuildArgs& a, int pass) {

@@ -154,7 +154,9 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0,
-                      {"Fa": Q.Fa, "TB": Q.TB, "nnz": int(Q.csc_row.numel())})
+                      {"Fa": Q.Fa, "TB": Q.TB, "nnz": int(Q.csc_row.numel()),
+                       "hot": int(Q.hot.size) if Q.hot is not None else 0,
+                       "groups": int(Q._rowgroups.G) if getattr(Q, "_rowgroups", None) is not None else 0})
 
 
 def train_margin_logloss(margin: torch.Tensor, y: torch.Tensor) -> float:

@@ -57,9 +57,6 @@ DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
 # streams: they add into disjoint feature ranges with integer atomics, so the order is free and
 # the kernels fill each other's tails
 HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
-# levels that build at most BLK_MAX_SLOTS node slots (GBDT) take the row-blocked histogram pass
-# (models/quantize.BlockedCSC, csrc/blk_kernels.hip): row state staged in LDS per 4096-row chunk
-# instead of a global gather per entry (FDX_BLK=0: the CSC / dense passes at every level)
 # device level loop counters (bench/gbdt_train.py reports the histogram payload per level: what a
 # data-parallel level reduce-scatters, before the 1/S shard split)
 LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0, "coll_calls": 0, "coll_ms": 0.0}
@@ -113,8 +110,6 @@ class _CollTimer:
         else:
             LEVEL_STATS["coll_ms"] += (time.perf_counter() - self.b) * 1e3
         return False
-BLK = os.environ.get("FDX_BLK", "0") == "1"      # row-blocked pass: opt-in until it beats the CSC passes
-BLK_MAX_SLOTS = 4
 # row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
 # histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
 ROWHIST = os.environ.get("FDX_ROWHIST", "1") == "1"
@@ -921,19 +916,6 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    ws.rg_listdig, n_build, rg.gmode, rg.work(), s2n, hist_target, h_stride,
                                    *shard_args, RG_DBG)
-                sel_groups, use_dense = [], False
-            elif BLK and np_ == 4 and not build_all and n_build <= BLK_MAX_SLOTS:
-                # row-blocked pass: every feature (hot ones included) in one launch
-                blk = Q.blocked()
-                root = d == 0 or n_build == 1
-                ct_b = 1 if root else ct
-                plan = blk.plan(int(C.tree_blk_gw(ct_b)))
-                dig = ws.rowdig if d == 0 else csc_dig
-                launches.append(functools.partial(
-                    C.tree_hist_blk, blk.ent_row, blk.ent_key, blk.seg, blk.NG, dig, None if root else slot8,
-                    *plan, int(C.tree_blk_gw(ct_b)), s2n, hist_target, TB, ct_b,
-                    shards.bin_lo if shards is not None else None,
-                    n_build * shards.Bs if shards is not None else 0))
                 sel_groups, use_dense = [], False
             if sel_groups is None:
                 sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups

@@ -122,89 +122,6 @@ def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.T
     return out
 
 
-BLK_ROWS = 4096          # csrc/tree.h kBlkRows: rows per chunk of the blocked CSC
-BLK_KEYS = 64            # kBlkKeys: global bins per group
-BLK_COMPUTE_WAVES = 7    # kBlkCompute: compute waves per workgroup of the blocked histogram pass
-# workgroups to aim for per blocked histogram launch (one per CU is resident at a time: 256 CUs)
-BLK_TARGET_WGS = int(os.environ.get("FDX_BLK_WGS", 768))
-BLK_MAX_CELL = (1 << 31) // (1 << 14) - 1     # entries one int32 (key, column) accumulator may absorb
-
-
-class BlockedCSC:
-    """Row-blocked CSC of every active feature (csrc/tree.h "row-blocked histogram engine"):
-    segment (chunk c, group g) holds the entries of rows [4096 c, 4096 (c + 1)) whose global bin
-    lies in [64 g, 64 (g + 1)) as (uint16 row offset, uint8 bin - 64 g), ordered by 16-bin tile
-    (``seg`` has one start per (chunk, tile)). Built on the device in two passes over the quantized
-    CSC (count, then place), ~3 B per entry."""
-
-    def __init__(self, Q: "Quantized"):
-        C = native.lib()
-        dev = Q.device
-        self.NG = max(1, (Q.TB + BLK_KEYS - 1) // BLK_KEYS)
-        self.n_chunks = max(1, (Q.n_rows + BLK_ROWS - 1) // BLK_ROWS)
-        ns = self.n_chunks * self.NG * 4               # (chunk, 16-bin tile) sub-segments
-        counts = torch.zeros(ns, dtype=torch.int32, device=dev)
-        C.tree_blk_build(Q.csc_row, Q.csc_bin, Q.colptr, Q.boff, BLK_ROWS, self.NG, 0, counts, None, None, None)
-        self.seg = torch.zeros(ns + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(counts, 0, out=self.seg[1:])
-        cursor = self.seg[:-1].clone()
-        nnz = int(Q.csc_row.numel())
-        # views with CSC_PAD readable (zero) entries behind the end: the kernel loads 4-entry groups
-        self.ent_row = torch.zeros(nnz + CSC_PAD, dtype=torch.int16, device=dev)[:nnz]
-        self.ent_key = torch.zeros(nnz + CSC_PAD, dtype=torch.uint8, device=dev)[:nnz]
-        C.tree_blk_build(Q.csc_row, Q.csc_bin, Q.colptr, Q.boff, BLK_ROWS, self.NG, 1, None, cursor,
-                         self.ent_row, self.ent_key)
-        self.seg_counts = counts.cpu().numpy().reshape(self.n_chunks, self.NG, 4).sum(-1).astype(np.int64)
-        self.nnz = nnz
-        self._plans: dict = {}
-
-    def plan(self, gw: int, target_wgs: int = 0) -> tuple:
-        """Work plan of the histogram pass with ``gw`` groups per compute wave: (wg_band, wg_c0,
-        wg_c1, band_groups [bands, 7, gw]) device int32 tensors. Groups are sorted by entries and
-        dealt into bands of 7 * gw (round-robin over the waves, so each wave gets groups of similar
-        rank); a band is split into contiguous chunk ranges so that a workgroup carries about
-        1 / target_wgs of all entries, and no range may let an int32 accumulator cell absorb more
-        than BLK_MAX_CELL entries (the kernel flushes only at the end)."""
-        target_wgs = target_wgs or BLK_TARGET_WGS
-        key = (gw, target_wgs)
-        if key in self._plans:
-            return self._plans[key]
-        w = self.seg_counts.sum(0)
-        maxseg = self.seg_counts.max(0) if self.n_chunks else np.zeros(self.NG, np.int64)
-        order = np.argsort(-w, kind="stable")
-        order = order[w[order] > 0]
-        per_band = BLK_COMPUTE_WAVES * gw
-        total = max(int(w.sum()), 1)
-        target = total / max(target_wgs, 1)
-        bands, wg = [], []
-        for b0 in range(0, order.size, per_band):
-            grp = order[b0:b0 + per_band]
-            slots = np.full(per_band, -1, dtype=np.int32)
-            # group k of the band -> wave k % 7, position k // 7
-            k = np.arange(grp.size)
-            slots[(k % BLK_COMPUTE_WAVES) * gw + k // BLK_COMPUTE_WAVES] = grp
-            bi = len(bands)
-            bands.append(slots)
-            wb = float(w[grp].sum())
-            L = int(min(self.n_chunks, max(1, round(wb / target))))
-            cap = max(1, BLK_MAX_CELL // max(1, int(maxseg[grp].max())))
-            L = max(L, -(-self.n_chunks // cap))
-            edges = np.linspace(0, self.n_chunks, L + 1).round().astype(np.int64)
-            for c0, c1 in zip(edges[:-1], edges[1:]):
-                if c1 > c0:
-                    wg.append((wb * (c1 - c0) / self.n_chunks, bi, c0, c1))
-        wg.sort(key=lambda t: -t[0])        # heaviest first: the tail runs the light ones
-        dev = self.seg.device
-        arr = np.asarray([(b, c0, c1) for _, b, c0, c1 in wg], dtype=np.int32).reshape(-1, 3)
-        band_groups = np.stack(bands).astype(np.int32) if bands else np.full((1, per_band), -1, np.int32)
-        out = (torch.from_numpy(np.ascontiguousarray(arr[:, 0])).to(dev),
-               torch.from_numpy(np.ascontiguousarray(arr[:, 1])).to(dev),
-               torch.from_numpy(np.ascontiguousarray(arr[:, 2])).to(dev),
-               torch.from_numpy(band_groups.reshape(-1)).to(dev))
-        self._plans[key] = out
-        return out
-
-
 RG_BINS = int(os.environ.get("FDX_RG_BINS", 8192))   # local bins per row group: 8192 (1 workgroup per CU) or 4096 (2)
 RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
 RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 2048))   # workgroups per row-group pass
@@ -405,14 +322,6 @@ class Quantized:
     kbase_host = property(lambda self: self._items()._kbase_host)
     n_super = property(lambda self: self._items()._n_super)
 
-    def blocked(self) -> BlockedCSC:
-        """The row-blocked CSC (built on first use)."""
-        b = getattr(self, "_blocked", None)
-        if b is None:
-            with tracing.span("q.blocked"):
-                b = self._blocked = BlockedCSC(self)
-        return b
-
     def rowgroups(self) -> RowGroups:
         """The row-group CSR of the row-group histogram engine (built on first use)."""
         r = getattr(self, "_rowgroups", None)
@@ -535,12 +444,14 @@ def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_
 
     dev = indptr.device
     fo = getattr(vc, "_feature_order", None)
+    scale = scale.to(device=dev, dtype=torch.float64)
+    if fo is not None and fo.dropped is not None and bool((fo.dropped & (scale > 0)).any()):
+        fo = None                        # (dropped columns are needed again: a fresh order)
     if fo is None or fo.colptr.numel() != F + 1 or fo.csc_row.device != dev:
         with tracing.span("q.order"):
             fo = feature_order(indptr, idx, counts, F)
     sp_h = tracing.span("q.head")
     sp_h.__enter__()
-    scale = scale.to(device=dev, dtype=torch.float64)
     maxb = torch.clamp(fo.maxc.to(torch.int64), max=max_bins - 1)
     maxb = torch.where(scale > 0, maxb, torch.zeros_like(maxb))
     if all_reduce_max is not None:
@@ -556,6 +467,12 @@ def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_
     k = torch.arange(TB, device=dev) - bstart[f_of_bin]
     thresholds = ((k.to(torch.float64) + 0.5) * scale[fid_orig][f_of_bin]).cpu().numpy()
     lens = fo.colptr[1:] - fo.colptr[:-1]
+    if bool(((~active) & (lens > 0)).any()):
+        # the inactive features' entries (all-zero values: IDF 0 for terms in every document)
+        # leave the shared feature order in place, so the order stays the CSC (no 5 B/entry copy)
+        with tracing.span("q.drop"):
+            fo.drop_features((~active) & (lens > 0))
+        lens = fo.colptr[1:] - fo.colptr[:-1]
     nnz_all = int(fo.colptr[-1])
     sp_h.__exit__(None, None, None)
     with tracing.span("q.csc"):

@@ -57,7 +57,7 @@ def featurize_long(data_dev: torch.Tensor, host_buf: np.ndarray, doc_off: np.nda
     from . import native
     from .sparse import score_csr
     from ..ml.linalg import VectorColumn
-    from .text import FLAG_BINARY, FLAG_WRITE_CSR, STATUS_OK, _flags
+    from .text import FLAG_BINARY, FLAG_WRITE_CSR, STATUS_OK, _flags, csr_capacity, csr_slots
 
     C = native.lib()
     bounds, seg_doc, done = [], [], np.zeros(len(docs), dtype=bool)
@@ -85,7 +85,7 @@ def featurize_long(data_dev: torch.Tensor, host_buf: np.ndarray, doc_off: np.nda
     nnz, ntok = torch.zeros(S, **i32), torch.zeros(S, **i32)
     status = torch.full((S,), -1, **i32)
     raw_dummy = torch.zeros((S, 1), dtype=torch.float64, device=device)
-    cap = int(data_dev.numel()) + S
+    cap = csr_capacity(int(data_dev.numel()), S)
     idx, val = torch.empty(cap, **i32), torch.empty(cap, dtype=torch.float32, device=device)
     flags = (_flags(spec, None, None, None, True) | FLAG_WRITE_CSR) & ~FLAG_BINARY   # raw term counts
     st, vt = spec.stop_table(), spec.vocab_table()
@@ -104,9 +104,9 @@ def featurize_long(data_dev: torch.Tensor, host_buf: np.ndarray, doc_off: np.nda
     remap = np.cumsum(done) - 1                                  # dialogue j -> row of the done dialogues
     sdoc = torch.from_numpy(remap[sdoc_old]).to(device)
     n_done = int(done.sum())
-    # gather every kept segment's CSR entries (written at base = segment start + segment index)
+    # gather every kept segment's CSR entries (written at csr_slots(segment start, segment index))
     cnt = nnz[sel].long()
-    base = offs_t[sel] + sel
+    base = csr_slots(offs_t[sel], sel)
     total = int(cnt.sum())
     starts = torch.zeros(cnt.numel() + 1, dtype=torch.int64, device=device)
     torch.cumsum(cnt, 0, out=starts[1:])

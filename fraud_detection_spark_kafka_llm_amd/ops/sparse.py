@@ -5,6 +5,7 @@ import os
 from dataclasses import dataclass
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import native
@@ -90,6 +91,43 @@ class FeatureOrder:
     colptr: torch.Tensor
     df: torch.Tensor
     maxc: torch.Tensor
+    # features whose entries were dropped from csc_row / csc_cnt (drop_features; df keeps them)
+    dropped: Optional[torch.Tensor] = None
+
+    def drop_features(self, drop: torch.Tensor) -> None:
+        """Remove the entries of the features flagged in ``drop`` [F] (bool) IN PLACE: the kept
+        columns slide left over the dropped ones, in order, so no second CSC is allocated (the
+        trainers drop features whose values are all zero, e.g. IDF 0 for terms in every
+        document, whose columns hold one entry per row: copying the rest of the CSC instead
+        cost 5 B per entry of transient HBM). Every move copies ``chunk <= shift`` entries, so
+        source and destination of one copy never overlap; copies run in stream order."""
+        colptr = self.colptr.cpu().numpy()
+        dmask = drop.cpu().numpy().astype(bool)
+        lens = np.diff(colptr)
+        dmask &= lens > 0
+        if not dmask.any():
+            return
+        nnz = int(colptr[-1])
+        # maximal runs of kept columns -> (src start, src end)
+        edges = np.flatnonzero(np.diff(np.concatenate([[1], dmask.astype(np.int8), [1]])))
+        dst = 0
+        for a, b in zip(edges[0::2], edges[1::2]):          # kept features [a, b)
+            s0, s1 = int(colptr[a]), int(colptr[b])
+            n = s1 - s0
+            if n and s0 != dst:
+                shift = s0 - dst
+                for off in range(0, n, shift):
+                    c = min(shift, n - off)
+                    self.csc_row[dst + off:dst + off + c].copy_(self.csc_row[s0 + off:s0 + off + c])
+                    self.csc_cnt[dst + off:dst + off + c].copy_(self.csc_cnt[s0 + off:s0 + off + c])
+            dst += n
+        new_lens = np.where(dmask, 0, lens)
+        newptr = np.concatenate([[0], np.cumsum(new_lens)]).astype(np.int64)
+        assert int(newptr[-1]) == dst <= nnz
+        self.colptr.copy_(torch.from_numpy(newptr))
+        self.csc_row, self.csc_cnt = self.csc_row[:dst], self.csc_cnt[:dst]
+        d = torch.from_numpy(dmask).to(self.maxc.device)
+        self.dropped = d if self.dropped is None else (self.dropped | d)
 
 
 # entries radix-sorted at once by feature_order: the device sort needs 24 B of temporaries per

@@ -301,6 +301,17 @@ def _flags(spec: FeatureSpec, idf, lr, trees, want_csr: bool) -> int:
     return f
 
 
+def csr_capacity(nbytes: int, docs: int) -> int:
+    """Entries of the fused featurizer's CSR scratch for ``docs`` documents of ``nbytes`` bytes
+    (csrc/scoring.h csr_capacity: at most L / 2 + 2 distinct terms per L-byte document)."""
+    return (int(nbytes) >> 1) + 2 * int(docs) + 1
+
+
+def csr_slots(starts: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
+    """First scratch slot of each document (csrc/scoring.h csr_slot): start / 2 + 2 * index."""
+    return (starts >> 1) + 2 * index
+
+
 LONG_DOC_BYTES = 65536   # documents up to this size stay on the GPU (long-dialogue kernel)
 
 
@@ -338,7 +349,7 @@ def featurize_score(text: PackedText, spec: FeatureSpec, idf: Optional[torch.Ten
         if idf_t.numel() < spec.dim:
             raise ValueError("idf vector shorter than the feature space")
     K = trees.K if trees is not None else 1
-    cap = (text.data.numel() + D) if want_csr else 1
+    cap = csr_capacity(text.data.numel(), D) if want_csr else 1
     i32 = dict(dtype=torch.int32, device=device)
     out = (torch.zeros(D, **i32), torch.zeros(D, **i32),
            torch.zeros((D, K), dtype=torch.float64, device=device), torch.full((D,), -1, **i32),
@@ -353,7 +364,7 @@ def featurize_score(text: PackedText, spec: FeatureSpec, idf: Optional[torch.Ten
         if long_docs.numel():
             _launch(C, text, spec, flags, idf_t, lr, trees, out, device, None, threads,
                     long_docs.to(torch.int32).contiguous())
-    base = text.offsets[:-1] + torch.arange(D, device=device, dtype=torch.int64)
+    base = csr_slots(text.offsets[:-1], torch.arange(D, device=device, dtype=torch.int64))
     res = FeatureResult(nnz, ntok, raw, status, idx if want_csr else None, val if want_csr else None, base, spec.dim)
     if device.type == "cuda" and D:
         _long_docs_on_device(res, text, host_text, spec, idf_t, lr, trees, want_csr, device)
@@ -408,7 +419,7 @@ def _finish_on_host(res: FeatureResult, text: PackedText, bad: np.ndarray, spec,
     sub_flags = flags | (0 if spec.clean else FLAG_PRELOWERED)
     D = len(sub)
     K = trees.K if trees is not None else 1
-    cap = (sub.data.numel() + D) if want_csr else 1
+    cap = csr_capacity(sub.data.numel(), D) if want_csr else 1
     i32 = dict(dtype=torch.int32)
     out = (torch.zeros(D, **i32), torch.zeros(D, **i32), torch.zeros((D, K), dtype=torch.float64),
            torch.full((D,), -1, **i32), torch.empty(cap, **i32), torch.empty(cap, dtype=torch.float32))
@@ -424,7 +435,7 @@ def _finish_on_host(res: FeatureResult, text: PackedText, bad: np.ndarray, spec,
     res.raw[bad_t] = raw.to(dev)
     res.status[bad_t] = status.to(dev)
     if want_csr:
-        sub_base = sub.offsets[:-1] + torch.arange(D, dtype=torch.int64)
+        sub_base = csr_slots(sub.offsets[:-1], torch.arange(D, dtype=torch.int64))
         n64 = nnz.to(torch.int64)
         total = int(n64.sum())
         if total:

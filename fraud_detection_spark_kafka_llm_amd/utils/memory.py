@@ -1,19 +1,31 @@
-"""HBM sizing of training shards: how many rows one GPU can train on.
+"""HBM sizing of training shards: how many rows one GPU can featurize and train.
 
-A tree ensemble (GBDT / RF / DT) trained on a count TF-IDF ``VectorColumn`` keeps, per CSR entry:
-  * the CSR itself: int32 feature ids + int32 term counts (8 B; the caller's features),
-  * the feature-major order built for the IDF and reused as the CSC: int32 rows + uint8 capped
-    counts (5 B),
-  * the bins: uint8 (1 B),
-  * the histogram CSC (super-block-major copy of the rows + uint8 keys: 5 B),
-and per row: the CSR row pointer (8 B), labels, margins, gradients, digit words, node ids and
-slot bytes (~40 B), plus one byte per hot (dense-path) feature. Transients on top: the feature
-order's radix-sort temporaries, 29 B per entry of one sort block (ops/sparse.py
-FO_BLOCK_ENTRIES), and the histogram buffers of one level.
+The peak of a shard's pipeline is the larger of two moments, each modelled from what is live
+(bytes per CSR entry "e", per row "r", per raw text byte of a featurization chunk "b"); the
+numbers are the allocations of bench.py's path, measured stage by stage on the MI355X by
+bench/probes/mem_probe.py (profiles/r4/mem_*.jsonl):
 
-``max_rows_per_gpu`` inverts that model against ``torch.cuda.mem_get_info`` (or a given byte
-budget). bench.py reports it next to the measured peak HBM per row; the estimators' data-parallel
-launcher raises the worker count when one GPU's shard would not fit.
+1. featurization, while the LAST chunk is processed (bench.featurize_shard with the feature
+   order built per chunk):
+     * the CSR being filled: int32 feature ids + fp32 term counts, capacity 1.05 x the entries
+       plus one chunk (8 B/e), row pointer + labels (16 B/r);
+     * the feature-order blocks of the chunks so far: int32 rows + uint8 counts (5 B/e);
+     * the chunk's raw text in its two device staging buffers (2 B/b of the chunk),
+       the fused kernel's CSR scratch (csrc/scoring.h csr_capacity: 1/2 slot per byte, 8 B a
+       slot = 4 B/b) and the compaction's int64 step / position arrays and gathered entries
+       (24 B per chunk entry), plus the chunk's radix-sort temporaries (24 B per chunk entry);
+   or, at the end, the merged feature order (another 5 B/e) while the blocks are still held;
+2. training (GBDT on the row-group engine; RF adds its CSC items, 5 B/e, on its own peak):
+     * the CSR (8 B/e + slack), the feature order shared as the CSC (5 B/e of active entries),
+       one uint8 bin per entry, the row-group entries (uint16: 2 B/e);
+     * per row: pointer + labels (16 B), the row-group run starts (4 B per group), one byte per
+       dense hot feature, the level loop's row state (digits, node, slot, list, margin, g, h,
+       labels: 53 B);
+     * the level histograms: (g, h) int64 per bin of each built node.
+
+``max_rows_per_gpu`` inverts the model against ``torch.cuda.mem_get_info`` (or a given byte
+budget); ``min_workers`` is the fewest equal shards that fit. bench.py reports the model next to
+the measured peak of its timed GBDT phase (featurization + training).
 """
 from __future__ import annotations
 
@@ -23,22 +35,51 @@ from typing import Optional
 
 import torch
 
-ENTRY_BYTES = 19.0          # persistent bytes per CSR entry (see the module docstring)
-ROW_BYTES = 48.0            # persistent bytes per row, without the dense hot-feature block
-SORT_TEMP_BYTES = 29.0      # radix-sort temporaries per entry of one feature-order block
+CSR_BYTES = 8.0             # int32 feature id + fp32 term count per entry
+CSR_SLACK = 1.05            # featurize_shard's capacity estimate from the first chunk
+ORDER_BYTES = 5.0           # feature order / CSC: int32 row + uint8 count per entry
+BIN_BYTES = 1.0             # uint8 bin per active entry
+RG_ENTRY_BYTES = 2.0        # row-group engine: uint16 local bin per entry
+ROW_BYTES = 16.0            # row pointer (int64) + labels (fp64) of the featurized shard
+LEVEL_ROW_BYTES = 53.0      # level-loop row state (grower.Workspace + margins, g, h, labels)
+CHUNK_TEXT_BYTES = 2.0      # two device staging buffers of one chunk's raw text
+CHUNK_SCRATCH_BYTES = 4.0   # fused featurizer CSR scratch per text byte (scoring.h csr_capacity)
+CHUNK_ENTRY_TEMP = 48.0     # per chunk entry: compaction int64 step + position + gathered entries,
+                            # and the chunk's radix-sort temporaries
 LEVEL_HIST_BYTES = 16.0     # (g, h) int64 sums per bin per node built in one level
-DEFAULT_HOT_FEATURES = 64   # dense-path features (>= 10 % of rows) of a dialogue corpus
+DEFAULT_HOT_FEATURES = 145  # dense-path features (>= 10 % of rows) of the bench dialogue corpus
+DEFAULT_GROUPS = 11         # row groups of 8192 bins (bench corpus: ~90K bins over 2^18 buckets)
 DEFAULT_BUILT_NODES = 32    # nodes built in the widest level (depth 6: 2^5)
+DEFAULT_BYTES_PER_ROW = 1940.0   # raw UTF-8 bytes per dialogue of the bench corpus
+DEFAULT_CHUNK_ROWS = 500_000     # bench featurization chunk
+
+
+def featurize_bytes(rows: int, nnz: int, text_bytes_per_row: float = DEFAULT_BYTES_PER_ROW,
+                    chunk_rows: int = DEFAULT_CHUNK_ROWS) -> float:
+    """Peak bytes of featurizing ``rows`` rows into ``nnz`` CSR entries (model, see module doc)."""
+    rows = max(int(rows), 0)
+    chunk = min(rows, int(chunk_rows))
+    chunk_entries = nnz * chunk / max(rows, 1)
+    chunk_bytes = text_bytes_per_row * chunk
+    csr = CSR_BYTES * (CSR_SLACK * nnz + chunk_entries) + ROW_BYTES * rows
+    last_chunk = csr + ORDER_BYTES * nnz + (CHUNK_TEXT_BYTES + CHUNK_SCRATCH_BYTES) * chunk_bytes \
+        + CHUNK_ENTRY_TEMP * chunk_entries
+    merge = csr + 2 * ORDER_BYTES * nnz
+    return max(last_chunk, merge)
 
 
 def training_bytes(rows: int, nnz: int, hot_features: int = DEFAULT_HOT_FEATURES, total_bins: int = 0,
-                   built_nodes: int = DEFAULT_BUILT_NODES) -> float:
-    """Model of the peak HBM bytes of training on ``rows`` rows with ``nnz`` CSR entries."""
-    from ..ops.sparse import FO_BLOCK_ENTRIES
+                   built_nodes: int = DEFAULT_BUILT_NODES, groups: int = DEFAULT_GROUPS) -> float:
+    """Peak bytes of training (GBDT, row-group engine) on ``rows`` rows with ``nnz`` entries."""
+    per_entry = CSR_BYTES * CSR_SLACK + ORDER_BYTES + BIN_BYTES + RG_ENTRY_BYTES
+    per_row = ROW_BYTES + 4.0 * groups + hot_features + LEVEL_ROW_BYTES
+    return per_entry * nnz + per_row * rows + LEVEL_HIST_BYTES * total_bins * built_nodes * 2
 
-    block = min(nnz, FO_BLOCK_ENTRIES)
-    return (ENTRY_BYTES * nnz + (ROW_BYTES + hot_features) * rows + SORT_TEMP_BYTES * block
-            + LEVEL_HIST_BYTES * total_bins * built_nodes * 2)
+
+def pipeline_bytes(rows: int, nnz: int, **kw) -> float:
+    """Peak bytes of featurization followed by training on one shard (the larger moment)."""
+    fkw = {k: kw.pop(k) for k in ("text_bytes_per_row", "chunk_rows") if k in kw}
+    return max(featurize_bytes(rows, nnz, **fkw), training_bytes(rows, nnz, **kw))
 
 
 def device_budget(device=None, headroom: float = 0.9) -> int:
@@ -54,19 +95,26 @@ def device_budget(device=None, headroom: float = 0.9) -> int:
     return int(free * headroom)
 
 
-def max_rows_per_gpu(nnz_per_row: float, device=None, budget_bytes: Optional[int] = None,
-                     hot_features: int = DEFAULT_HOT_FEATURES, total_bins: int = 0,
-                     built_nodes: int = DEFAULT_BUILT_NODES) -> int:
-    """Largest row count whose modelled training peak fits ``budget_bytes`` (default: 90 % of the
-    device's free memory). 0 when there is no device budget."""
-    from ..ops.sparse import FO_BLOCK_ENTRIES
-
+def max_rows_per_gpu(nnz_per_row: float, device=None, budget_bytes: Optional[int] = None, **kw) -> int:
+    """Largest row count whose modelled pipeline peak fits ``budget_bytes`` (default: 90 % of the
+    device's free memory). 0 when there is no device budget. The model is piecewise linear in
+    the row count (chunk terms saturate at one chunk), so the cap is found by bisection."""
     budget = device_budget(device) if budget_bytes is None else int(budget_bytes)
     if budget <= 0:
         return 0
-    fixed = SORT_TEMP_BYTES * FO_BLOCK_ENTRIES + LEVEL_HIST_BYTES * total_bins * built_nodes * 2
-    per_row = ENTRY_BYTES * nnz_per_row + ROW_BYTES + hot_features
-    return max(0, int((budget - fixed) // per_row))
+
+    def fits(r: int) -> bool:
+        return pipeline_bytes(r, int(r * nnz_per_row), **dict(kw)) <= budget
+
+    lo, hi = 0, 1
+    while fits(hi):
+        lo, hi = hi, hi * 2
+        if hi > 1 << 40:
+            return lo
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        lo, hi = (mid, hi) if fits(mid) else (lo, mid)
+    return lo
 
 
 def min_workers(rows: int, nnz: int, device=None, budget_bytes: Optional[int] = None) -> int:

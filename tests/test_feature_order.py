@@ -50,3 +50,70 @@ def test_incremental_feature_order_equals_one_shot(dev):
             e0, e1 = int(indptr[r0]), int(indptr[r1])
             inc.add(indptr[r0:r1 + 1] - e0, idx[e0:e1], cnt[e0:e1], r0)
         _same(one, inc.finish())
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_drop_features_in_place_equals_order_without_them(dev):
+    """FeatureOrder.drop_features slides the kept columns over the dropped ones in place: the
+    result is the CSC of the CSR without those features (dense columns: every row, like a term
+    in every document, and sparse ones, adjacent runs, the first and the last feature)."""
+    indptr, idx, cnt, f = _csr(seed=5, n=3000, f=50)
+    n = indptr.numel() - 1
+    # make features 0, 7, 8 and 49 present in every row (IDF 0 in a TF-IDF column)
+    rows = []
+    ip, ix, c = indptr.numpy(), idx.numpy(), cnt.numpy()
+    for r in range(n):
+        cols = dict(zip(ix[ip[r]:ip[r + 1]].tolist(), c[ip[r]:ip[r + 1]].tolist()))
+        for k in (0, 7, 8, 49):
+            cols.setdefault(k, 1 + r % 5)
+        rows.append(sorted(cols.items()))
+    indptr = torch.tensor(np.concatenate([[0], np.cumsum([len(r) for r in rows])]), dtype=torch.int64)
+    idx = torch.tensor([k for r in rows for k, _ in r], dtype=torch.int32)
+    cnt = torch.tensor([v for r in rows for _, v in r], dtype=torch.int32)
+    drop = torch.zeros(f, dtype=torch.bool)
+    drop[[0, 7, 8, 20, 49]] = True
+    fo = feature_order(indptr.to(dev), idx.to(dev), cnt.to(dev), f)
+    fo.drop_features(drop.to(dev))
+    keep = ~drop[idx.long()]
+    kptr = torch.zeros(n + 1, dtype=torch.int64)
+    torch.cumsum(torch.tensor([int(keep[indptr[r]:indptr[r + 1]].sum()) for r in range(n)]), 0, out=kptr[1:])
+    ref = feature_order(kptr.to(dev), idx[keep].to(dev), cnt[keep].to(dev), f)
+    assert torch.equal(fo.csc_row.cpu(), ref.csc_row.cpu())
+    assert torch.equal(fo.csc_cnt.cpu(), ref.csc_cnt.cpu())
+    assert torch.equal(fo.colptr.cpu(), ref.colptr.cpu())
+    assert bool(fo.dropped.cpu()[0]) and not bool(fo.dropped.cpu()[1])
+
+
+def test_trees_on_idf_zero_features_equal_trees_without_them():
+    """A TF-IDF column whose terms in every row have IDF 0 trains the same GBDT / RF as the column
+    without those terms (their entries are dropped from the shared feature order in place), and a
+    second fit on the same column (RF after GBDT, as the bench does) reuses the dropped order."""
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+    from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+
+    indptr, idx, cnt, f = _csr(seed=9, n=2000, f=60)
+    ip, ix, c = indptr.numpy(), idx.numpy(), cnt.numpy() % 7 + 1
+    rows = []
+    for r in range(2000):
+        cols = dict(zip(ix[ip[r]:ip[r + 1]].tolist(), c[ip[r]:ip[r + 1]].tolist()))
+        cols.setdefault(3, 2)                  # a term in every row
+        rows.append(sorted(cols.items()))
+    indptr = torch.tensor(np.concatenate([[0], np.cumsum([len(r) for r in rows])]), dtype=torch.int64)
+    idx = torch.tensor([k for r in rows for k, _ in r], dtype=torch.int32)
+    cnt = torch.tensor([v for r in rows for _, v in r], dtype=torch.int32)
+    y = torch.from_numpy(((idx.numpy()[indptr.numpy()[:-1]] % 2) == 0).astype(np.float32))
+    df = torch.bincount(idx.long(), minlength=f)
+    idf = torch.log((2000 + 1.0) / (df.double() + 1.0))
+    assert float(idf[3]) == 0.0
+    keep = idx != 3
+    kptr = torch.zeros(2001, dtype=torch.int64)
+    torch.cumsum(torch.tensor([int(keep[indptr[r]:indptr[r + 1]].sum()) for r in range(2000)]), 0, out=kptr[1:])
+    full = VectorColumn.tfidf(f, indptr, idx, cnt, idf, feature_order(indptr, idx, cnt, f))
+    ref = VectorColumn.tfidf(f, kptr, idx[keep], cnt[keep], idf)
+    sig = lambda r: [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]  # noqa: E731
+    p = GBDTParams(n_estimators=3, max_depth=4)
+    assert sig(fit_gbdt(full, y, p, device="cpu")) == sig(fit_gbdt(ref, y, p, device="cpu"))
+    assert full._feature_order.dropped is not None
+    kw = dict(num_trees=3, max_depth=4, bootstrap=True, feature_subset="sqrt", seed=1, device="cpu")
+    assert sig(fit_forest(full, y, **kw)) == sig(fit_forest(ref, y, **kw))

@@ -10,7 +10,9 @@ def test_max_rows_inverts_the_training_bytes_model():
     budget = 288 * 2 ** 30 * 0.9
     cap = memory.max_rows_per_gpu(100.0, budget_bytes=budget)
     assert cap > 50_000_000                    # a 288 GB GPU holds far more than a 12.5M-row shard
-    assert memory.training_bytes(cap, cap * 100) <= budget < memory.training_bytes(cap + 1000, (cap + 1000) * 100)
+    assert memory.pipeline_bytes(cap, cap * 100) <= budget < memory.pipeline_bytes(cap + 1000, (cap + 1000) * 100)
+    # featurization's last chunk dominates small shards, training's per-entry state large ones
+    assert memory.featurize_bytes(10_000_000, 10 ** 9) > memory.training_bytes(10_000_000, 10 ** 9)
     assert memory.max_rows_per_gpu(200.0, budget_bytes=budget) < cap
     assert memory.max_rows_per_gpu(100.0) == 0 or torch.cuda.is_available()   # no budget on the CPU
     assert memory.min_workers(10 * cap, 10 * cap * 100, budget_bytes=budget) == 10

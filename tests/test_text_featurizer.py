@@ -71,6 +71,25 @@ def test_native_cpu_matches_oracle(clean, stop):
         assert g == O.hashing_tf(toks, 10007), repr(d)[:80]
 
 
+# the densest possible documents for the CSR scratch bound (csrc/scoring.h csr_slot: at most
+# L / 2 + 2 distinct terms per L-byte document): distinct one-character tokens, a leading empty
+# token, every parity of start offset
+DENSE = ["".join(chr(c) + " " for c in range(33, 127)), " " + " ".join(chr(c) for c in range(33, 127)),
+         "x", "", "a b", " " * 7 + "q", "\u00e9 \u00e8 \u00ea \u00eb \u00e0 " * 3]
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_densest_documents_fit_the_csr_scratch(device):
+    docs = [d for k in range(3) for d in (DENSE[k % len(DENSE):] + DENSE[:k % len(DENSE)] + ["y" * (k + 1)])]
+    spec = T.FeatureSpec(clean=False, stopwords=None, num_features=1 << 18)
+    res = T.featurize_score(T.PackedText.from_strings(docs), spec, want_csr=True, device=device)
+    got = csr_rows(res)
+    for d, g in zip(docs, got):
+        want = O.hashing_tf(O.tokenize(d), 1 << 18)
+        assert g == want, repr(d)[:60]
+        assert len(want) <= len(d.encode()) // 2 + 2
+
+
 def test_vocab_mode_and_min_tf():
     docs = random_docs(200, seed=2)
     vocab = ["hello", "verify", "social", "security", "im", "dont", "please", "bank"]

@@ -631,22 +631,6 @@ def test_gpu_device_level_loop_equals_gpu_host_loop(monkeypatch):
     _same_trees(out[False][1], out[True][1])
 
 
-@pytest.mark.gpu
-def test_gpu_blocked_pass_in_the_level_loop_grows_the_same_trees(monkeypatch):
-    """FDX_BLK=1 (models/grower.py BLK): the levels building <= 4 node slots run the row-blocked
-    histogram pass; the GBDT trees are the CSC passes' trees, bit for bit."""
-    from fraud_detection_spark_kafka_llm_amd.models import grower
-
-    dense, y = random_counts_matrix(9000, 150, 0.15, 61)
-    dense[:, :4] = np.random.default_rng(6).integers(0, 9, (9000, 4))
-    vc = vc_from_dense(dense)
-    out = {}
-    for flag in (False, True):
-        monkeypatch.setattr(grower, "BLK", flag)
-        out[flag] = fit_gbdt(vc, torch.from_numpy(y), GBDTParams(n_estimators=4, max_depth=6), device="cuda:0").trees
-    _same_trees(out[False], out[True])
-
-
 @pytest.mark.parametrize("max_delta_step", [0.0, 0.7])
 def test_deferred_tree_build_equals_immediate(max_delta_step):
     """GBDT without per-round hooks builds tree t's host table during tree t + 1 and updates the
@@ -730,107 +714,3 @@ def test_gpu_packed_item_cannot_overflow_int32_accumulators():
     q1 = np.rint(np.ldexp(h.astype(np.float64), int(k[1]))).astype(np.int64)
     assert int(q0[0]) % 256 == 128
     np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, 1, q0, q1))
-
-
-def _blk_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None):
-    """Histograms of node slots 0..nslots-1 through the row-blocked pass (tree_hist_blk), plus the
-    exponents; ``shards`` = (S, bin_lo) writes the shard-major DP layout (returned unpacked)."""
-    C = native.lib()
-    n = row_node_np.shape[0]
-    Q = quantize(vc.to(dev), max_bins=max_bins, **QKW)
-    ws = Workspace(Q)
-    gg = torch.from_numpy(np.linspace(-1, 1, n).astype(np.float32)).to(dev)
-    hh = torch.from_numpy(np.linspace(0.01, 0.25, n).astype(np.float32)).to(dev)
-    C.tree_quant_max(gg, hh, None, None, 0, 0, False, 0, n, ws.maxabs, 0)
-    C.tree_quant(gg, hh, None, None, 0, 0, False, 0, 4, ws.maxabs, ws.rowdig, ws.kexp, ws.totals, ws.digp, 0)
-    node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
-    node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
-    slot8 = None
-    if not root:
-        C.tree_slot8(torch.from_numpy(row_node_np).to(dev), node_slot.to(dev), 0, nslots, ws.slot8, None, None)
-        slot8 = ws.slot8
-    ct = 1 if nslots <= 2 else 2
-    gw = int(C.tree_blk_gw(ct))
-    blk = Q.blocked()
-    s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
-    if shards is None:
-        hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
-        C.tree_hist_blk(blk.ent_row, blk.ent_key, blk.seg, blk.NG, ws.rowdig, slot8, *blk.plan(gw), gw, s2n, hist,
-                        Q.TB, ct, None, 0)
-        return hist.cpu().numpy(), ws.kexp.cpu().numpy(), Q
-    S, lo = shards
-    Bs = int(np.diff(lo).max())
-    buf = torch.zeros((S, nslots, Bs, 2), dtype=torch.int64, device=dev)
-    C.tree_hist_blk(blk.ent_row, blk.ent_key, blk.seg, blk.NG, ws.rowdig, slot8, *blk.plan(gw), gw, s2n,
-                    buf.view(S * nslots, Bs, 2), Q.TB, ct, torch.from_numpy(lo).to(dev), nslots * Bs)
-    b = buf.cpu().numpy()
-    hist = np.concatenate([b[k, :, : lo[k + 1] - lo[k]] for k in range(S)], axis=1)
-    return hist, ws.kexp.cpu().numpy(), Q
-
-
-def test_blocked_csc_covers_every_entry_and_plan_covers_every_segment_once():
-    rng = np.random.default_rng(3)
-    n, F = 9000, 150
-    dense = (rng.random((n, F)) < np.linspace(0.002, 0.4, F)) * rng.integers(1, 90, (n, F))
-    Q = quantize(vc_from_dense(dense.astype(np.float64)), max_bins=64, **QKW)
-    blk = Q.blocked()
-    seg = blk.seg.numpy()
-    assert seg[-1] == Q.csc_row.numel() == blk.nnz
-    # every (row, global bin) of the CSC appears once in its (chunk, group) segment
-    colptr, boff = Q.colptr.numpy(), Q.boff.numpy()
-    want = sorted((int(r), int(boff[f] + b)) for f in range(Q.Fa)
-                  for r, b in zip(Q.csc_row[colptr[f]:colptr[f + 1]].numpy(), Q.bins_of(f).numpy()))
-    got = []
-    rows, keys = blk.ent_row.numpy().view(np.uint16), blk.ent_key.numpy()
-    for c in range(blk.n_chunks):
-        for g in range(blk.NG):
-            for t in range(4):
-                a, b = seg[(c * blk.NG + g) * 4 + t], seg[(c * blk.NG + g) * 4 + t + 1]
-                assert all(int(k) // 16 == t for k in keys[a:b])          # sub-segments are tile-pure
-                got += [(c * 4096 + int(r), g * 64 + int(k)) for r, k in zip(rows[a:b], keys[a:b])]
-    assert sorted(got) == want
-    for gw in (8, 4):
-        band, c0, c1, groups = (t.numpy() for t in blk.plan(gw, target_wgs=37))
-        groups = groups.reshape(-1, 7 * gw)
-        cover = np.zeros((blk.n_chunks, blk.NG), dtype=np.int64)
-        for b, lo, hi in zip(band, c0, c1):
-            for g in groups[b][groups[b] >= 0]:
-                cover[lo:hi, g] += 1
-        assert ((cover == 1) | (blk.seg_counts == 0)).all() and (cover <= 1).all()
-
-
-@pytest.mark.parametrize("nslots,root", [(1, True), (2, False), (4, False)])
-def test_blocked_histograms_equal_host_reference(nslots, root):
-    rng = np.random.default_rng(nslots)
-    n, F = 9000, 120
-    dense = (rng.random((n, F)) < np.linspace(0.002, 0.5, F)) * rng.integers(1, 200, (n, F))
-    vc = vc_from_dense(dense.astype(np.float64))
-    row_node = rng.integers(-1, nslots + 1, n).astype(np.int32) if not root else np.zeros(n, np.int32)
-    hist, k, Q = _blk_hist_on("cpu", vc, 100, nslots, row_node, root)
-    n_ = np.arange(n)
-    q0 = np.rint(np.ldexp(np.linspace(-1, 1, n).astype(np.float32).astype(np.float64), int(k[0]))).astype(np.int64)
-    q1 = np.rint(np.ldexp(np.linspace(0.01, 0.25, n).astype(np.float32).astype(np.float64), int(k[1]))).astype(np.int64)
-    del n_
-    np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, nslots, q0, q1))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("nslots,root", [(1, True), (2, False), (3, False), (4, False)])
-@pytest.mark.parametrize("sharded", [False, True])
-def test_gpu_blocked_histograms_equal_host_bitwise(nslots, root, sharded):
-    """The row-blocked i8-MFMA pass (LDS-staged row state) equals the host's exact int64 sums bit
-    for bit, plain and in the shard-major DP layout."""
-    rng = np.random.default_rng(10 + nslots)
-    n, F = 30000, 400
-    dense = (rng.random((n, F)) < np.linspace(0.001, 0.5, F)) * rng.integers(1, 300, (n, F))
-    vc = vc_from_dense(dense.astype(np.float64))
-    row_node = rng.integers(-1, nslots + 1, n).astype(np.int32) if not root else np.zeros(n, np.int32)
-    shards = None
-    if sharded:
-        Q0 = quantize(vc, max_bins=200, **QKW)
-        lo = np.array([0, Q0.TB // 3, (2 * Q0.TB) // 3, Q0.TB], dtype=np.int64)
-        shards = (3, lo)
-    a, ka, _ = _blk_hist_on("cpu", vc, 200, nslots, row_node, root, shards)
-    b, kb, _ = _blk_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards)
-    np.testing.assert_array_equal(ka, kb)
-    np.testing.assert_array_equal(a, b)
