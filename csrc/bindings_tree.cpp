@@ -810,7 +810,11 @@ void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_dept
                           &sub_dst, &sub_par, &sub_sib})
     chk(*t, dev, at::kInt, "level_plan int32 array");
   const int64_t M = parent.numel();
-  FDX_CHECK(L >= 1 && packed.numel() >= 5 * L && open.numel() >= L, "packed [L, 5], open [L]");
+  // packed: [L, 5] or the all-gathered [S, L, 5] of a data-parallel level (best over shards here)
+  const int64_t S = packed.dim() == 3 ? packed.size(0) : 1;
+  FDX_CHECK(packed.is_contiguous() && (packed.dim() == 2 || packed.dim() == 3) && packed.size(-1) == 5 &&
+                packed.size(-2) >= L, "packed must be [L, 5] or [S, L, 5] contiguous");
+  FDX_CHECK(L >= 1 && open.numel() >= L, "open [L]");
   FDX_CHECK(stats.numel() == 2 * M && left.numel() == M && right.numel() == M && feat.numel() == M &&
                 bin.numel() == M && leaf.numel() == M && gain.numel() == M && default_child.numel() == M &&
                 node_slot.numel() == M, "node tables must be [max_nodes]");
@@ -821,6 +825,8 @@ void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_dept
   fdx::LevelPlanArgs a{};
   a.packed = packed.data_ptr<int64_t>();
   a.L = (int32_t)L;
+  a.n_shards = (int32_t)S;
+  a.shard_stride = packed.size(-2) * 5;
   a.depth = (int32_t)depth;
   a.max_depth = (int32_t)max_depth;
   a.mode = (int32_t)mode;

@@ -467,8 +467,10 @@ FDX_HD double best_split_scan(const int64_t* hb, int nb, int zb, int64_t T0, int
 // reads two counts per level and the node table once per tree. Newton gain (GBDT) and Spark's
 // gini / entropy (DT / RF, optionally building every open node for per-node feature sampling).
 struct LevelPlanArgs {
-  const int64_t* packed;          // [L][5] best split per open node {gain bits, feature, bin, left0, left1}
+  const int64_t* packed;          // [n_shards][L][5] best split per open node {gain bits, feature, bin, left0, left1}
   int32_t L;                      // open-list capacity of this level
+  int32_t n_shards;               // data parallel: the all-gathered per-shard bests (<= 1: one table);
+  int64_t shard_stride;           //   the best over shards per node, ties to the lowest shard
   int32_t depth, max_depth;
   int32_t mode;                   // 0 newton (gain > max(min_gain, 1e-6)), 1 gini / 2 entropy (gain > 0, >= min_gain)
   int32_t build_all;              // build every open node (RF: no sibling subtraction)
@@ -535,6 +537,12 @@ FDX_HD void level_plan(const LevelPlanArgs& a, bool reset = true) {
     const int64_t* p = a.packed + 5 * (int64_t)i;
     double g;
     memcpy(&g, &p[0], sizeof(double));
+    for (int32_t sh = 1; sh < a.n_shards; ++sh) {     // shard order = feature order: ties keep the lowest
+      const int64_t* q = a.packed + sh * a.shard_stride + 5 * (int64_t)i;
+      double gq;
+      memcpy(&gq, &q[0], sizeof(double));
+      if (gq > g) { g = gq; p = q; }
+    }
     const int32_t f = (int32_t)p[1], b = (int32_t)p[2];
     const bool ok = a.mode == 0 ? (b >= 0 && isfinite(g) && g > thr)
                                 : (b >= 0 && isfinite(g) && g > 0.0 && g >= a.min_gain);

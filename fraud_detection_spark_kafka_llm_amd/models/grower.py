@@ -247,6 +247,13 @@ class Workspace:
             self._dense_groups[key] = out
         return out
 
+    def iota(self, n: int) -> torch.Tensor:
+        """[0, 1, ..., n - 1] int32 on the device (cached: one allocation per workspace)."""
+        t = getattr(self, "_iota", None)
+        if t is None or t.numel() < n:
+            t = self._iota = torch.arange(max(n, 64), dtype=torch.int32, device=self.dev)
+        return t[:n]
+
     def shards(self, coll) -> "FeatureShards":
         if getattr(self, "_shards", None) is None or self._shards.S != coll.world:
             self._shards = FeatureShards(self.Q, coll.world, coll.rank)
@@ -900,7 +907,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 s2n = st.one.new_zeros(1)
             bidx = s2n
             if shards is not None:      # slot k -> partial row k
-                s2n = torch.arange(n_build, dtype=torch.int32, device=dev)
+                s2n = ws.iota(n_build)
             ct = pass_ct(np_, n_build)
             launches = []
             # (the CSC items are built on first use: the row-group engine never touches them)
@@ -969,10 +976,9 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 mine = _best_splits(C, cur_hist, totals_d, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
                                     open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0)
                 with _CollTimer(dev):
-                    allt = coll.all_gather(mine)                              # [S, n_open, 5]
-                gains = allt[:, :, 0].contiguous().view(torch.float64)
-                best_s = torch.argmax(gains, dim=0)                           # ties -> lowest shard = lowest feature
-                packed = allt[best_s, torch.arange(n_open, device=dev)].contiguous()
+                    # [S, n_open, 5]: tree_level_plan takes the best over shards per node (ties
+                    # to the lowest shard = the lowest feature), no separate argmax launches
+                    packed = coll.all_gather(mine)
         nxt = 1 - cur
         C.tree_level_plan(packed, n_open, d, params.max_depth, int(params.mode), build_all, ws.kexp,
                           float(params.min_gain), Q.zbin, st.hot_row,
