@@ -712,11 +712,172 @@ __global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, co
   }
 }
 
+// exclusive prefix count of the lanes below this one whose predicate holds, and the wave total
+__device__ __forceinline__ int32_t lp_rank(bool pred, int32_t* total) {
+  const unsigned long long m = __ballot(pred);
+  *total = __popcll(m);
+  return __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull));
+}
+
+// tree.h level_plan on one wave: lane i plans open node i (chunks of 64 with carried counters).
+// The sequential plan's only cross-node dependencies are running counters -- child ids (nn),
+// column splits (n_cs), next-level open slots (n_next), builds (nb) -- which are exclusive
+// prefix sums over per-node predicates here, so the node table, partition and next-level
+// tables are exactly the host twin's (tests: device level loop == host loop, bit for bit).
+// A node that could split but would overflow max_nodes becomes a leaf, as in the sequential
+// plan (child ids only grow, so once one split no longer fits no later one does).
+__device__ void level_plan_wave(const LevelPlanArgs& a) {
+  const int32_t lane = (int32_t)(threadIdx.x & 63);
+  const double thr = a.min_gain > 1e-6 ? a.min_gain : 1e-6;
+  const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
+  int32_t nn = *a.n_nodes, n_cs = 0, n_next = 0, nb = 0;
+  const int32_t no = *a.n_open;
+  for (int32_t base = 0; base < no; base += 64) {
+    const int32_t i = base + lane;
+    const bool live = i < no;
+    const int32_t n = live ? a.open[i] : -1;
+    double g = -1.0 / 0.0;
+    const int64_t* p = a.packed + 5 * (int64_t)(live ? i : 0);
+    int32_t f = -1, b = -1;
+    if (live) {
+      memcpy(&g, &p[0], sizeof(double));
+      for (int32_t sh = 1; sh < a.n_shards; ++sh) {
+        const int64_t* q = a.packed + sh * a.shard_stride + 5 * (int64_t)i;
+        double gq;
+        memcpy(&gq, &q[0], sizeof(double));
+        if (gq > g) { g = gq; p = q; }
+      }
+      f = (int32_t)p[1];
+      b = (int32_t)p[2];
+    }
+    const bool ok = live && (a.mode == 0 ? (b >= 0 && isfinite(g) && g > thr)
+                                         : (b >= 0 && isfinite(g) && g > 0.0 && g >= a.min_gain));
+    int32_t n_ok;
+    const int32_t r_ok = lp_rank(ok, &n_ok);
+    const bool split = ok && nn + 2 * (r_ok + 1) <= a.max_nodes;
+    int32_t n_split;
+    const int32_t r_split = lp_rank(split, &n_split);
+    if (live && !split) a.leaf[n] = 1;
+    const int32_t li = nn + 2 * r_split, ri = li + 1;
+    bool cleaf[2] = {true, true};
+    bool dense = false;
+    if (split) {
+      const int64_t l0 = p[3], l1 = p[4];
+      const int64_t t0 = a.stats[2 * n], t1 = a.stats[2 * n + 1];
+      const int64_t cs[2][2] = {{l0, l1}, {t0 - l0, t1 - l1}};
+      for (int k = 0; k < 2; ++k) {
+        const int32_t c = li + k;
+        a.stats[2 * c] = cs[k][0];
+        a.stats[2 * c + 1] = cs[k][1];
+        bool leafy = a.depth + 1 >= a.max_depth;
+        if (a.mode != 0) leafy = leafy || impurity(a.mode, (double)cs[k][0] * s0, (double)cs[k][1] * s1) == 0.0;
+        a.parent[c] = n;
+        a.left[c] = a.right[c] = -1;
+        a.feat[c] = -1;
+        a.bin[c] = -1;
+        a.gain[c] = -1.0;
+        a.leaf[c] = leafy ? 1 : 0;
+        cleaf[k] = leafy;
+      }
+      a.feat[n] = f;
+      a.bin[n] = b;
+      a.left[n] = li;
+      a.right[n] = ri;
+      a.gain[n] = g;
+      const int32_t hr = a.hot_row ? a.hot_row[f] : -1;
+      dense = a.node_dense && hr >= 0;
+      const bool left_default = a.zbin[f] <= b;
+      const int32_t dflt = left_default ? li : ri;
+      a.default_child[n] = dflt;
+      if (dense) {
+        int32_t* nd = a.node_dense + 4 * (int64_t)n;
+        nd[0] = hr; nd[1] = b; nd[2] = li; nd[3] = ri;
+      }
+    }
+    int32_t n_col;
+    const int32_t r_col = lp_rank(split && !dense, &n_col);
+    if (split && !dense) {
+      const bool left_default = a.zbin[f] <= b;
+      const int32_t k = n_cs + r_col;
+      a.cs_feat[k] = f;
+      a.cs_default[k] = left_default ? li : ri;
+      a.cs_other[k] = left_default ? ri : li;
+      a.cs_bin[k] = b;
+      a.cs_left_default[k] = left_default ? 1 : 0;
+    }
+    // next-level open slots: the node's non-leaf children in order (left, right)
+    const int32_t c_open = split ? (int32_t)!cleaf[0] + (int32_t)!cleaf[1] : 0;
+    int32_t incl = c_open;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    const int32_t tot_open = __shfl(incl, 63, 64);
+    const int32_t pos = n_next + incl - c_open;
+    if (c_open) {
+      int32_t j = pos;
+      for (int k = 0; k < 2; ++k)
+        if (!cleaf[k]) {
+          const int32_t c = li + k;
+          a.next_open[j] = c;
+          a.next_totals[2 * j] = a.stats[2 * c];
+          a.next_totals[2 * j + 1] = a.stats[2 * c + 1];
+          ++j;
+        }
+    }
+    // builds of level d + 1 (non-build_all): one per split node with an open child, in order
+    int32_t n_bld;
+    const int32_t r_bld = lp_rank(!a.build_all && c_open > 0, &n_bld);
+    if (!a.build_all && c_open > 0) {
+      const int32_t k = nb + r_bld;
+      int32_t build, jb, large = -1, jl = -1;
+      if (c_open == 2) {
+        const int64_t wl = a.mode == 0 ? a.stats[2 * li + 1] : a.stats[2 * li] + a.stats[2 * li + 1];
+        const int64_t wr = a.mode == 0 ? a.stats[2 * ri + 1] : a.stats[2 * ri] + a.stats[2 * ri + 1];
+        const bool lsmall = wl <= wr;
+        build = lsmall ? li : ri;
+        large = lsmall ? ri : li;
+        jb = lsmall ? pos : pos + 1;
+        jl = lsmall ? pos + 1 : pos;
+      } else {
+        build = cleaf[0] ? ri : li;
+        jb = pos;
+      }
+      a.node_slot[build] = k;
+      a.s2n[k] = jb;
+      if (large >= 0) {
+        a.sub_dst[k] = jl;
+        a.sub_par[k] = i;
+        a.sub_sib[k] = jb;
+      }
+    }
+    nn += 2 * n_split;
+    n_cs += n_col;
+    n_next += tot_open;
+    nb += n_bld;
+  }
+  if (a.build_all) {
+    for (int32_t j = lane; j < n_next; j += 64) {
+      a.node_slot[a.next_open[j]] = j;
+      a.s2n[j] = j;
+    }
+    nb = n_next;
+  }
+  if (lane == 0) {
+    *a.n_nodes = nn;
+    a.counts[0] = n_cs;
+    a.counts[1] = n_next;
+    a.counts[2] = nb;
+    a.counts[3] = nn;
+  }
+}
+
 __global__ void level_plan_kernel(LevelPlanArgs a) {
   if (blockIdx.x != 0) return;
   level_plan_reset(a, (int32_t)threadIdx.x, (int32_t)blockDim.x);
   __syncthreads();
-  if (threadIdx.x == 0) level_plan(a, false);
+  if (threadIdx.x < 64) level_plan_wave(a);
 }
 
 // ------------------------------------------------------------------ gbdt helpers

@@ -82,6 +82,11 @@ def level_collective_ms() -> float:
     return float(LEVEL_STATS["coll_ms"])
 
 
+# FDX_LEVEL_TIMING=0: no timing events around the level collectives (their record calls cost the
+# host thread that drives the RF lanes a few microseconds each)
+LEVEL_TIMING = os.environ.get("FDX_LEVEL_TIMING", "1") != "0"
+
+
 class _CollTimer:
     """Times one level's collectives on the current stream (device events; host clock on the CPU)."""
 
@@ -89,6 +94,8 @@ class _CollTimer:
         self.cuda = dev.type == "cuda"
 
     def __enter__(self):
+        if not LEVEL_TIMING:
+            return self
         if self.cuda:
             self.b = torch.cuda.Event(enable_timing=True)
             self.b.record()
@@ -98,6 +105,8 @@ class _CollTimer:
 
     def __exit__(self, *exc):
         LEVEL_STATS["coll_calls"] += 1
+        if not LEVEL_TIMING:
+            return False
         if self.cuda:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
