@@ -102,8 +102,7 @@ def main():
     t2 = time.perf_counter()
     feat_peak = torch.cuda.max_memory_allocated(dev)
     torch.cuda.reset_peak_memory_stats(dev)
-    for k in grower.LEVEL_STATS:
-        grower.LEVEL_STATS[k] = 0
+    grower.reset_level_stats()
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=args.trees, max_depth=args.depth), device=dev)
     t3 = time.perf_counter()
     ls = grower.LEVEL_STATS

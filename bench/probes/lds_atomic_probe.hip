@@ -26,7 +26,10 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 // mode: 0 ds_add_u64 random | 1 ds_add_u32 random (16K words) | 2 ds_add_u64 conflict-free
 // (lane-linear) | 3 ds_add_u64 one address per wave | 4 ds_add_u64, one lane active |
 // 5 ds_read_b64 + ds_write_b64 random (no atomicity) | 6 two ds_add_u64 (g, h tables) random |
-// 7 ds_add_u64 random over the hottest 256 bins | 8 ds_add_u32 x4 random (split hi/lo of g, h)
+// 7 ds_add_u64 random over the hottest 256 bins | 8 ds_add_u32 x4 random (split hi/lo of g, h) |
+// 9 ds_add_u64 conflict-free only if lanes are banked in 4 groups of 16 (lane l and l + 16 share a
+// bank pair) | 10 hot bins with 16 lane replicas: slot (random bin of 128) * 16 + lane % 16 |
+// 11 as 10 with 32 replicas over 64 bins (conflict-free for 2 groups of 32 as well)
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void probe(unsigned long long* out, uint32_t seed) {
   __shared__ unsigned long long hg[kBins];
@@ -60,6 +63,12 @@ __global__ __launch_bounds__(kThreads) void probe(unsigned long long* out, uint3
       atomicAdd(&hh[b], v);
     } else if (MODE == 7) {
       atomicAdd(&hg[h & 255], v);
+    } else if (MODE == 9) {
+      atomicAdd(&hg[((lane & 15) + 32 * (lane >> 4) + 128 * (it & 31)) & (kBins - 1)], v);
+    } else if (MODE == 10) {
+      atomicAdd(&hg[((h & 127) * 16 + (lane & 15)) & (kBins - 1)], v);
+    } else if (MODE == 11) {
+      atomicAdd(&hg[((h & 63) * 32 + (lane & 31)) & (kBins - 1)], v);
     } else if (MODE == 8) {
       const uint32_t b = h & (kBins - 1);
       atomicAdd(&w32[2 * b], 3u);
@@ -104,5 +113,8 @@ int main() {
   run<6>("2x ds_add_u64 random (g, h tables)", 2, 16);
   run<7>("ds_add_u64 random over 256 hot bins", 1, 16);
   run<8>("4x ds_add_u32 random (hi/lo g, h)", 4, 16);
+  run<9>("ds_add_u64 bank-pair shared by lanes l, l+16", 1, 16);
+  run<10>("ds_add_u64 hot bins x16 lane replicas", 1, 16);
+  run<11>("ds_add_u64 hot bins x32 lane replicas", 1, 16);
   return 0;
 }
