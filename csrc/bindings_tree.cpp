@@ -195,6 +195,34 @@ void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64
   }
 }
 
+// Compact DP layout of an RF level (tree.h RfCompactArgs): local [Fa + 1] int64, sizes [S] int64.
+void rf_compact(const Tensor& mask, const Tensor& nbins, const Tensor& fs, const Tensor& local, const Tensor& sizes) {
+  const auto dev = mask.device();
+  chk(mask, dev, at::kByte, "mask");
+  chk(nbins, dev, at::kInt, "nbins");
+  chk(fs, dev, at::kLong, "fs");
+  chk(local, dev, at::kLong, "local");
+  chk(sizes, dev, at::kLong, "sizes");
+  const int64_t Fa = mask.numel();
+  FDX_CHECK(nbins.numel() == Fa && local.numel() == Fa + 1 && fs.numel() >= 2 && sizes.numel() == fs.numel() - 1,
+            "mask/nbins [Fa], local [Fa + 1], fs [S + 1], sizes [S]");
+  fdx::RfCompactArgs a{};
+  a.mask = mask.data_ptr<uint8_t>();
+  a.nbins = nbins.data_ptr<int32_t>();
+  a.fs = fs.data_ptr<int64_t>();
+  a.S = (int32_t)(fs.numel() - 1);
+  a.Fa = Fa;
+  a.local = local.data_ptr<int64_t>();
+  a.sizes = sizes.data_ptr<int64_t>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rf_compact(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rf_compact_cpu(a);
+  }
+}
+
 void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Tensor& item_f0, const Tensor& item_meta,
                      const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
                      const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
@@ -987,6 +1015,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rg_build_csr", &rg_build_csr);
   m.def("tree_rg_hist", &rg_hist);
   m.def("tree_rf_sample", &rf_sample);
+  m.def("tree_rf_compact", &rf_compact);
   m.def("tree_hist_dense", &hist_dense);
   m.def("tree_dense_fg", &dense_fg);
   m.def("tree_dense_waves", &dense_waves);

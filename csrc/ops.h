@@ -80,6 +80,9 @@ struct LevelPlanArgs;
 struct RfSampleArgs;
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s);
 void rf_sample_cpu(const RfSampleArgs& a);
+struct RfCompactArgs;
+void launch_rf_compact(const RfCompactArgs& a, hipStream_t s);
+void rf_compact_cpu(const RfCompactArgs& a);
 void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s);
 void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);

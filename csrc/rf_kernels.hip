@@ -155,6 +155,45 @@ __global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
 }
 }  // namespace
 
+namespace {
+// One workgroup, shards one after another: each thread sums a contiguous slice of the shard's
+// masked nbins, a block scan of the 1024 partials gives every slice its start, a second pass
+// writes the offsets (unsampled features: the shard's trash start, known after the scan).
+constexpr int kCompactThreads = 1024;
+__global__ __launch_bounds__(kCompactThreads) void rf_compact_kernel(RfCompactArgs a) {
+  __shared__ int64_t part[kCompactThreads];
+  const int t = threadIdx.x;
+  for (int32_t sh = 0; sh < a.S; ++sh) {
+    const int64_t f0 = a.fs[sh], n = a.fs[sh + 1] - f0;
+    const int64_t per = (n + kCompactThreads - 1) / kCompactThreads;
+    const int64_t lo = f0 + per * t, hi = lo + per < f0 + n ? lo + per : f0 + n;
+    int64_t sum = 0;
+    for (int64_t f = lo; f < hi; ++f) sum += a.mask[f] ? a.nbins[f] : 0;
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < kCompactThreads; d <<= 1) {          // inclusive Hillis-Steele scan
+      const int64_t o = t >= d ? part[t - d] : 0;
+      __syncthreads();
+      part[t] += o;
+      __syncthreads();
+    }
+    const int64_t total = part[kCompactThreads - 1];
+    int64_t acc = part[t] - sum;
+    for (int64_t f = lo; f < hi; ++f) {
+      if (a.mask[f]) { a.local[f] = acc; acc += a.nbins[f]; }
+      else a.local[f] = total;
+    }
+    if (t == 0) a.sizes[sh] = total;
+    __syncthreads();
+  }
+  if (t == 0) a.local[a.Fa] = 0;
+}
+}  // namespace
+
+void launch_rf_compact(const RfCompactArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(rf_compact_kernel, dim3(1), dim3(kCompactThreads), 0, s, a);
+}
+
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s) {
   // k >= F (every feature) is handled by the caller: thresholds 1.0, mask all ones
   if (a.nnodes <= 0 || a.k >= a.F) return;

@@ -75,6 +75,18 @@ void slot8_cpu(const SlotArgs& a) {
   });
 }
 
+void rf_compact_cpu(const RfCompactArgs& a) {
+  for (int32_t sh = 0; sh < a.S; ++sh) {
+    int64_t acc = 0;
+    for (int64_t f = a.fs[sh]; f < a.fs[sh + 1]; ++f)
+      if (a.mask[f]) { a.local[f] = acc; acc += a.nbins[f]; }
+    for (int64_t f = a.fs[sh]; f < a.fs[sh + 1]; ++f)
+      if (!a.mask[f]) a.local[f] = acc;
+    a.sizes[sh] = acc;
+  }
+  a.local[a.Fa] = 0;
+}
+
 void rf_sample_cpu(const RfSampleArgs& a) {
   if (a.nnodes <= 0 || a.k >= a.F) return;
   parallel_for(a.nnodes, 0, 1, [&](int64_t lo, int64_t hi) {

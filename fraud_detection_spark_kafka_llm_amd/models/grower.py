@@ -129,6 +129,9 @@ SAMPLED = os.environ.get("FDX_RF_SAMPLED", "1") == "1"
 LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
+# RF levels under data parallelism reduce-scatter only the bins of the level's sampled features
+# (FeatureShards.compact; FDX_RF_COMPACT=0: every active feature's bins)
+RF_COMPACT = os.environ.get("FDX_RF_COMPACT", "1") != "0"
 
 
 # GBDT trees grow with the device-resident level loop (grow_tree_device): split application and
@@ -381,6 +384,15 @@ class FeatureShards:
         self.f0, self.Fa, self.bins = f0, f1 - f0, int(hi[rank] - lo[rank])
         self.boff = (Q.boff[f0: f1 + 1] - Q.boff[f0]).contiguous()
         self.nbins = Q.nbins[f0:f1].contiguous()
+        # compact RF levels (compact()): per-level layout buffers of this workspace
+        self._nbins_all = Q.nbins
+        self._fs_dev = torch.from_numpy(fs).to(dev)
+        self.max_nb = int(Q.nbins.max()) if Fa else 1
+        self._local_c = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
+        self._sizes = torch.zeros(S, dtype=torch.int64, device=dev)
+        self.sizes_host = torch.zeros(S, dtype=torch.int64)
+        if dev.type == "cuda":
+            self.sizes_host = self.sizes_host.pin_memory()
         self.zbin = Q.zbin[f0:f1].contiguous()
         self.fid_orig = Q.fid_orig[f0:f1].contiguous()
 
@@ -396,6 +408,24 @@ class FeatureShards:
     def target(self, nb: int, dev) -> torch.Tensor:
         """Zeroed shard-major partial histograms [S, nb, Bs, 2] of a DP level."""
         return torch.zeros((self.S, nb, self.Bs, 2), dtype=torch.int64, device=dev)
+
+    def compact(self, feat_mask: torch.Tensor):
+        """Per-level compact layout of an RF level (csrc/tree.h RfCompactArgs): the features of the
+        level's union sample mask packed per shard, the rest aimed at a per-shard trash range.
+        Queues the layout kernel and the copy of the shard sizes to ``sizes_host``; returns the
+        device offsets [Fa + 1] (read ``sizes_host`` once the returned event completed)."""
+        native.lib().tree_rf_compact(feat_mask, self._nbins_all, self._fs_dev, self._local_c, self._sizes)
+        self.sizes_host.copy_(self._sizes, non_blocking=True)
+        if self._local_c.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            ev = _Done()
+        return self._local_c, ev
+
+    def compact_stride(self) -> int:
+        """Bins per node row of a compact level: the largest shard's sampled bins plus its trash."""
+        return int(self.sizes_host.max()) + self.max_nb
 
 
 def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, params, feat_thr, tree_index, Fa,
@@ -878,13 +908,6 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         LEVEL_STATS["hist_bytes"] += n_build * TB * 16          # (g, h) int64 partials of the built nodes
         open_d, totals_d = st.open[cur][:n_open], st.totals[cur][:n_open]
         n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
-        if shards is None:
-            cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
-            h_boff, h_stride = Q.boff, TB
-        else:   # local partials of the built nodes, shard-major (reduce-scattered as they stand)
-            rs_buf = shards.target(n_build, dev)
-            hist_target = rs_buf.view(shards.S * n_build, shards.Bs, 2)
-            h_boff, h_stride = shards.boff_packed(n_build), shards.Bs
         # RF: exact k-of-F feature sample per open node and the level's union mask (device)
         feat_thr = feat_mask = None
         if build_all:
@@ -892,6 +915,24 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             feat_mask = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
             C.tree_rf_sample(seed, int(tree_index), open_d, int(Q.num_features), int(params.feat_k), Q.fid_orig,
                              feat_thr, feat_mask, None)
+        split_boff = shards.boff if shards is not None else None
+        if shards is None:
+            cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
+            h_boff, h_stride = Q.boff, TB
+        elif build_all and RF_COMPACT and params.feat_k:
+            # only the sampled features' bins travel: the layout needs the shard sizes on the host
+            # (one 8-byte-per-shard copy; the lanes of a forest run meanwhile)
+            local_c, ev_c = shards.compact(feat_mask)
+            yield ev_c
+            Bs_c = shards.compact_stride()
+            rs_buf = torch.zeros((shards.S, n_build, Bs_c, 2), dtype=torch.int64, device=dev)
+            hist_target = rs_buf.view(shards.S * n_build, Bs_c, 2)
+            h_boff, h_stride = torch.add(local_c, shards._shard_of, alpha=n_build * Bs_c), Bs_c
+            split_boff = local_c[shards.f0: shards.f0 + shards.Fa + 1]
+        else:   # local partials of the built nodes, shard-major (reduce-scattered as they stand)
+            rs_buf = shards.target(n_build, dev)
+            hist_target = rs_buf.view(shards.S * n_build, shards.Bs, 2)
+            h_boff, h_stride = shards.boff_packed(n_build), shards.Bs
         with tracing.span("tree.hist"):
             use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH and not build_all
             slot8 = None
@@ -982,7 +1023,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
                                       params, feat_thr, tree_index, Q.Fa, 0)
             else:
-                mine = _best_splits(C, cur_hist, totals_d, shards.boff, shards.nbins, shards.zbin, shards.fid_orig,
+                mine = _best_splits(C, cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig,
                                     open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0)
                 with _CollTimer(dev):
                     # [S, n_open, 5]: tree_level_plan takes the best over shards per node (ties

@@ -272,3 +272,22 @@ def test_gpu_rccl_forced_collectives_rf_lanes_equal_serial(monkeypatch):
     assert lanes == 4 and n_coll > 0
     assert any(name == "reduce_scatter_tensor" for name, _ in seq)
     assert trees == serial[0]
+
+
+def _rf_rs_bytes(rank, world):
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    D.reset_bytes()
+    trees, lanes, seq, n_coll = _train_rf_lanes(rank, world)
+    return trees, D.BYTES["reduce_scatter"]
+
+
+def test_rf_compact_levels_send_only_sampled_bins(monkeypatch):
+    """RF levels under DP reduce-scatter only the bins of the level's union feature sample
+    (FeatureShards.compact): far fewer bytes, bitwise the same forest."""
+    monkeypatch.setenv("FDX_RF_COMPACT", "0")
+    full = spawn(_rf_rs_bytes, 2, backend="gloo")
+    monkeypatch.setenv("FDX_RF_COMPACT", "1")
+    comp = spawn(_rf_rs_bytes, 2, backend="gloo")
+    assert comp[0][0] == full[0][0] == comp[1][0]
+    assert comp[0][1] < 0.7 * full[0][1], (comp[0][1], full[0][1])
