@@ -105,14 +105,14 @@ class RemoteScorer:
     client's batches outstanding; ``collect`` returns the (prediction, P(scam)) rows written into
     the oldest submitted slot (FIFO over all scorers, like GpuScorer)."""
 
-    def __init__(self, conns, ring: SharedRing, max_docs: int, max_bytes: int, depth: int = 2):
+    def __init__(self, conns, ring: SharedRing, max_docs: int, max_bytes: int, depth: int = 2, first: int = 0):
         self.conns = list(conns) if isinstance(conns, (list, tuple)) else [conns]
         self.conn, self.ring = self.conns[0], ring
         self.max_docs, self.max_bytes, self._depth = max_docs, max_bytes, depth
         self._q: deque = deque()                  # (slot, scorer) in submission order
         self._out = [0] * len(self.conns)         # outstanding batches per scorer
         self._done: set = set()                   # slot indices whose results arrived
-        self._rr = 0
+        self._rr = first % len(self.conns)        # clients start on different scorers
         self.sent = [0] * len(self.conns)         # batches sent per scorer (stats)
 
     @property
@@ -674,7 +674,8 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
 
     c, P = cfg["index"], cfg["n_clients"]
     lay = cfg["layout"]
-    scorer = RemoteScorer([conn] + cfg.get("peer_conns", []), ring, lay["max_docs"], lay["max_bytes"], cfg["depth"])
+    scorer = RemoteScorer([conn] + cfg.get("peer_conns", []), ring, lay["max_docs"], lay["max_bytes"], cfg["depth"],
+                          first=c)
     if spec["kind"] == "serve":
         return _client_serve(cfg, spec, scorer, ring)
     url = f"memory://group-{os.getpid()}-{spec['tag']}"
