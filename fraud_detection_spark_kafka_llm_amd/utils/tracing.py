@@ -3,7 +3,9 @@
 ``span(name)`` marks a region with a ROCm ``roctx`` range when the roctx library is loadable (so
 rocprofv3 ``--marker-trace`` shows the framework phases next to the kernels) and, when
 ``FDX_TRACE=<path>`` is set, appends one JSON line per span with wall-clock start/duration.
-Spans nest. When neither sink is active a span costs one attribute lookup.
+Spans nest. When neither sink is active ``span`` returns a shared no-op context manager: the
+trainers open several spans per tree level, and a generator-based context manager cost ~5 us
+each on the host thread that drives the RF lanes.
 """
 from __future__ import annotations
 
@@ -45,9 +47,36 @@ def enable(path: str) -> None:
     _trace_path = path
 
 
-@contextlib.contextmanager
+class _NullSpan:
+    __slots__ = ()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL = _NullSpan()
+_ROCTX_ON = os.environ.get("FDX_ROCTX") == "1"
+
+
+def refresh() -> None:
+    """Re-read FDX_ROCTX / FDX_TRACE (tests toggle them at run time)."""
+    global _ROCTX_ON, _trace_path
+    _ROCTX_ON = os.environ.get("FDX_ROCTX") == "1"
+    _trace_path = os.environ.get("FDX_TRACE", _trace_path)
+
+
 def span(name: str, **attrs):
-    rt = _load_roctx() if os.environ.get("FDX_ROCTX") == "1" else None
+    if not (_trace_path or _ROCTX_ON):
+        return _NULL
+    return _span(name, **attrs)
+
+
+@contextlib.contextmanager
+def _span(name: str, **attrs):
+    rt = _load_roctx() if _ROCTX_ON else None
     if rt:
         rt.roctxRangePushA(name.encode())
     t0 = time.perf_counter()
