@@ -45,6 +45,9 @@ from .grower import GrowParams, Workspace, device_tree_steps
 from .quantize import Quantized
 
 TREES_IN_FLIGHT = int(os.environ.get("FDX_RF_INFLIGHT", "4"))
+# histogram side streams per lane (grower.Workspace.run_concurrent): the lanes already overlap
+# whole trees, and every extra stream is another HW-queue mapping and cross-stream event per level
+LANE_HIST_STREAMS = int(os.environ.get("FDX_RF_LANE_STREAMS", "4"))
 
 
 class ForestLanes:
@@ -52,6 +55,8 @@ class ForestLanes:
 
     def __init__(self, Q: Quantized, lanes: int, ws0: Optional[Workspace] = None):
         self.ws = [ws0 if (i == 0 and ws0 is not None) else Workspace(Q) for i in range(lanes)]
+        for w in self.ws:
+            w.hist_streams = LANE_HIST_STREAMS
         cuda = Q.device.type == "cuda"
         self.streams = [torch.cuda.Stream(Q.device) for _ in range(lanes)] if cuda else [None] * lanes
         self.dev = Q.device

@@ -176,6 +176,7 @@ class Workspace:
         self._shards = None
         self.staging = Staging(dev)
         self._streams = None
+        self.split_cache: dict = {}          # _best_splits scratch per level shape
 
     def rowgroups(self):
         """The row-group CSR when the row-group engine is on and covers every feature (else None),
@@ -218,12 +219,13 @@ class Workspace:
         long cold-feature CSC pass) runs on the current stream and the others share the
         HIST_STREAMS - 1 side streams, so none queues behind it (a short launch behind it added
         0.15-0.25 ms to every level)."""
-        if self.dev.type != "cuda" or HIST_STREAMS <= 1 or len(launches) <= 1:
+        nstreams = getattr(self, "hist_streams", HIST_STREAMS)
+        if self.dev.type != "cuda" or nstreams <= 1 or len(launches) <= 1:
             for fn in launches:
                 fn()
             return
         if self._streams is None:
-            self._streams = [torch.cuda.Stream(self.dev) for _ in range(HIST_STREAMS - 1)]
+            self._streams = [torch.cuda.Stream(self.dev) for _ in range(nstreams - 1)]
         main = torch.cuda.current_stream(self.dev)
         start = main.record_event()
         ns = len(self._streams)
@@ -429,10 +431,12 @@ class FeatureShards:
 
 
 def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, params, feat_thr, tree_index, Fa,
-                 f0, node_tree=None):
+                 f0, node_tree=None, cache: Optional[dict] = None):
     """Per node: (gain float64, feature (+f0) int64, bin int64, left sums int64 [2]) of the best
     split over Fa features of ``hist`` [nodes, boff[Fa], 2]; gain -inf without a valid candidate.
-    Returned as one int64 tensor [nodes, 5] (gain bit-cast) for a single device->host copy."""
+    Returned as one int64 tensor [nodes, 5] (gain bit-cast) for a single device->host copy.
+    ``cache`` (a workspace dict): the per-(node, feature) scratch is allocated once per level
+    shape and reused (stream order: the previous level's split kernels are done with it)."""
     dev = hist.device
     nl = int(node_ids.numel())
     if Fa == 0:
@@ -440,9 +444,13 @@ def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, p
         out[:, 0] = torch.tensor(NEG_INF, dtype=torch.float64).view(torch.int64)
         out[:, 1:3] = -1
         return out
-    out_gain = torch.empty((nl, Fa), dtype=torch.float64, device=dev)
-    out_bin = torch.empty((nl, Fa), dtype=torch.int32, device=dev)
-    out_left = torch.empty((nl, Fa, 2), dtype=torch.int64, device=dev)
+    bufs = cache.get((nl, Fa)) if cache is not None else None
+    if bufs is None:
+        bufs = (torch.empty((nl, Fa), dtype=torch.float64, device=dev), torch.empty((nl, Fa), dtype=torch.int32, device=dev),
+                torch.empty((nl, Fa, 2), dtype=torch.int64, device=dev))
+        if cache is not None:
+            cache[(nl, Fa)] = bufs
+    out_gain, out_bin, out_left = bufs
     C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, int(params.mode),
                       float(params.lambda_), float(params.min_child), feat_thr, int(params.seed), int(tree_index),
                       out_gain, out_bin, out_left, node_tree)
@@ -768,6 +776,15 @@ class LevelState:
     """Device buffers of the level loop (node table, ping-pong open lists, partition and plan
     tables), allocated once per workspace and depth."""
 
+    def record_event(self):
+        """An event recorded on the current stream (a reused one on the device, _Done on the host)."""
+        if self._events is None:
+            return _Done()
+        ev = self._events[self._ev_i]
+        self._ev_i = (self._ev_i + 1) % len(self._events)
+        ev.record()
+        return ev
+
     def __init__(self, Q: Quantized, max_depth: int):
         dev = Q.device
         M = 2 ** (max_depth + 1)
@@ -813,6 +830,10 @@ class LevelState:
         if dev.type == "cuda":
             self.counts_host = self.counts_host.pin_memory()
         self.one = torch.ones(1, dtype=torch.int32, device=dev)
+        # events the level loop records for the host (re-recorded round robin: each one is waited on
+        # before the loop records four more)
+        self._events = [torch.cuda.Event() for _ in range(4)] if dev.type == "cuda" else None
+        self._ev_i = 0
         self.default_child, self.node_slot = i32(M), i32(M)
         self.cs = [i32(cap) for _ in range(5)]          # feat, default, other, bin, left_default
         self.s2n, self.sub_dst, self.sub_par, self.sub_sib = i32(cap), i32(cap), i32(cap), i32(cap)
@@ -1021,10 +1042,11 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         with tracing.span("tree.split"):
             if shards is None:
                 packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
-                                      params, feat_thr, tree_index, Q.Fa, 0)
+                                      params, feat_thr, tree_index, Q.Fa, 0, cache=ws.split_cache)
             else:
                 mine = _best_splits(C, cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig,
-                                    open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0)
+                                    open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0,
+                                    cache=ws.split_cache)
                 with _CollTimer(dev):
                     # [S, n_open, 5]: tree_level_plan takes the best over shards per node (ties
                     # to the lowest shard = the lowest feature), no separate argmax launches
@@ -1035,13 +1057,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                           st.n_nodes, st.stats, st.parent, st.left, st.right, st.feat, st.bin, st.leaf, st.gain,
                           open_d, n_open_ptr, st.default_child, st.node_dense, *st.cs, st.counts[d],
                           st.open[nxt], st.totals[nxt], st.node_slot, st.s2n, st.sub_dst, st.sub_par, st.sub_sib)
-        if dev.type == "cuda":
-            st.counts_host[d].copy_(st.counts[d], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-        else:
-            st.counts_host[d].copy_(st.counts[d])
-            ev = _Done()
+        st.counts_host[d].copy_(st.counts[d], non_blocking=dev.type == "cuda")
+        ev = st.record_event()
         with tracing.span("tree.partition"):
             C.tree_partition_cols(ws.row_node, st.default_child, *st.cs, st.counts[d], Q.colptr, Q.csc_row, Q.csc_bin,
                                   st.node_dense, Q.dense if st.node_dense is not None else None, n_open, PARTITION_WPS)
