@@ -540,11 +540,8 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
   FDX_CHECK(ent.device() == dev && ent.scalar_type() == at::kShort && ent.is_contiguous(), "ent must be int16");
   FDX_CHECK(ptr.dim() == 2, "ptr must be [G, N + 1]");
   const int64_t G = ptr.size(0), N = ptr.size(1) - 1;
-  // 6144-bin groups are always in the hot layout (local bins 0..kRgHot-1 = the group's hottest)
-  FDX_CHECK(gbin.dim() == 2 && gbin.size(0) == G &&
-                (gbin.size(1) == 4096 || gbin.size(1) == 6144 || gbin.size(1) == 8192) &&
-                gbase.numel() == G + 1, "gbase [G + 1] / gbin [G, 4096, 6144 or 8192]");
-  const int64_t hot = gbin.size(1) == 6144 ? fdx::kRgHot : 0;
+  FDX_CHECK(gbin.dim() == 2 && gbin.size(0) == G && (gbin.size(1) == 4096 || gbin.size(1) == 8192) &&
+                gbase.numel() == G + 1, "gbase [G + 1] / gbin [G, 4096 or 8192]");
   FDX_CHECK(rowdig.dim() == 2 && rowdig.size(0) == N && rowdig.size(1) == 2, "rowdig must be [N, 2]");
   FDX_CHECK(reinterpret_cast<uintptr_t>(ent.data_ptr()) % 16 == 0 && readable_tail(ent, 8),
             "ent must be 16-byte aligned with 8 readable padding entries");
@@ -573,7 +570,6 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
   a.gbase = gbase.data_ptr<int64_t>();
   a.gbin = gbin.data_ptr<int32_t>();
   a.gbins = (int32_t)gbin.size(1);
-  a.hot = (int32_t)hot;
   a.G = (int32_t)G;
   a.N = N;
   a.rowdig = reinterpret_cast<const uint32_t*>(rowdig.data_ptr<int32_t>());

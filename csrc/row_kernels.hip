@@ -270,24 +270,12 @@ __global__ __launch_bounds__(1024) void rg_list_scan_kernel(RgListArgs a, int64_
   if (t == 1023) a.slot_count[s] = s_sum[1023];
 }
 
-// LDS slot of local bin b for a lane: the group's HOT most frequent bins (local ids 0..HOT-1,
-// models/quantize.py RowGroups hot layout) keep 16 replicas each, one per lane of a 16-lane bank
-// group, so the many lanes of an instruction that hit the same few popular bins (on the bench
-// corpus the 256 most frequent (feature, count) bins hold ~half of all entries) neither
-// serialise on one address nor collide on a bank pair; every other bin has one slot. Sinks
-// (BINS + lane) follow the bins.
-template <int BINS, int HOT>
-__device__ __forceinline__ uint32_t rg_slot(uint32_t b, int lane) {
-  if (HOT == 0) return b;
-  return b < (uint32_t)HOT ? b * 16u + (uint32_t)(lane & 15) : b + (uint32_t)HOT * 15u;
-}
-
-template <int BINS, int HOT>
+template <int BINS>
 struct RgShared {
   // separate statistic arrays (a lane's 8-byte atomic spans 2 of 64 banks); bins BINS + lane are
   // per-lane sinks for the lanes of a block outside their row's run (never flushed)
-  int64_t hg[BINS + HOT * 15 + 64];
-  int64_t hh[BINS + HOT * 15 + 64];
+  int64_t hg[BINS + 64];
+  int64_t hh[BINS + 64];
   // per wave: the 64 rows of the current batch (run start / end, statistics, first block index)
   uint32_t st[kRgWaves][64];
   uint32_t en[kRgWaves][64];
@@ -296,19 +284,12 @@ struct RgShared {
   uint32_t pb[kRgWaves][64];
 };
 
-template <int BINS, int HOT>
-__device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS, HOT>& sh, int g, int s, int tid) {
+template <int BINS>
+__device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS>& sh, int g, int s, int tid) {
   const int64_t hrow = a.slot_node[s];
   const int32_t* gbin = a.gbin + (int64_t)g * a.gbins;
-  for (int i = tid; i < HOT; i += kRgThreads) {           // fold the hot bins' replicas
-    int64_t v0 = 0, v1 = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      v0 += sh.hg[i * 16 + r];
-      v1 += sh.hh[i * 16 + r];
-      sh.hg[i * 16 + r] = 0;
-      sh.hh[i * 16 + r] = 0;
-    }
+  for (int i = tid; i < BINS; i += kRgThreads) {
+    const int64_t v0 = sh.hg[i], v1 = sh.hh[i];
     if ((v0 | v1) != 0 && hrow >= 0) {
       const int32_t col = gbin[i];
       if (col >= 0) {
@@ -317,20 +298,8 @@ __device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS, HOT
         atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)v1);
       }
     }
-  }
-  for (int i = HOT + tid; i < BINS; i += kRgThreads) {
-    const uint32_t k = rg_slot<BINS, HOT>((uint32_t)i, 0);
-    const int64_t v0 = sh.hg[k], v1 = sh.hh[k];
-    if ((v0 | v1) != 0 && hrow >= 0) {
-      const int32_t col = gbin[i];
-      if (col >= 0) {
-        int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
-        atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v0);
-        atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)v1);
-      }
-    }
-    sh.hg[k] = 0;
-    sh.hh[k] = 0;
+    sh.hg[i] = 0;
+    sh.hh[i] = 0;
   }
 }
 
@@ -343,8 +312,8 @@ __device__ __forceinline__ uint32_t rg_nblk(uint32_t st, uint32_t en) {
 // ceil(blocks / 64), so every lane streams the same number of blocks whatever the row lengths
 // (rows of the dense group vary ~2x: a lane per row left ~58% of the LDS atomic slots idle).
 // Entries of a block outside its row's run go to the lane's sink bin: no divergent branches.
-template <int BINS, int HOT>
-__device__ __forceinline__ void rg_batch(RgShared<BINS, HOT>& sh, const uint16_t* ent, int wv, int lane, uint32_t st,
+template <int BINS>
+__device__ __forceinline__ void rg_batch(RgShared<BINS>& sh, const uint16_t* ent, int wv, int lane, uint32_t st,
                                          uint32_t en, int32_t q0, int32_t q1, int dbg, unsigned long long& sink) {
   const uint32_t nb = rg_nblk(st, en);
   uint32_t incl = nb;
@@ -375,7 +344,7 @@ __device__ __forceinline__ void rg_batch(RgShared<BINS, HOT>& sh, const uint16_t
     unsigned long long a0 = (unsigned long long)(int64_t)sh.q0[wv][r], a1 = (unsigned long long)(int64_t)sh.q1[wv][r];
     uint32_t rnb = rg_nblk(rst, ren);
     uint32_t j = t - sh.pb[wv][r];
-    const uint32_t sinkb = BINS + HOT * 15 + lane;
+    const uint32_t sinkb = BINS + lane;
     uint32_t blk = (rst & ~7u) + 8u * j;
     uint4 v = *reinterpret_cast<const uint4*>(ent + blk);
     for (;;) {
@@ -405,7 +374,7 @@ __device__ __forceinline__ void rg_batch(RgShared<BINS, HOT>& sh, const uint16_t
       for (int k = 0; k < 8; ++k) {
         const uint32_t i = cblk + k;
         const uint32_t bin = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        const uint32_t b = (i >= cst && i < cen) ? rg_slot<BINS, HOT>(bin, lane) : sinkb;
+        const uint32_t b = (i >= cst && i < cen) ? bin : sinkb;
         if (dbg & 2) {
           sink += b;
         } else {
@@ -422,8 +391,8 @@ __device__ __forceinline__ void rg_batch(RgShared<BINS, HOT>& sh, const uint16_t
 
 // Dense groups: batches of 64 listed rows, block-balanced (rg_batch); the list entry is read two
 // batches ahead, (ptr, digits) one batch ahead.
-template <int BINS, int HOT>
-__device__ __forceinline__ void rg_range_dense(RgShared<BINS, HOT>& sh, const RgHistArgs& a, const uint32_t* ptr,
+template <int BINS>
+__device__ __forceinline__ void rg_range_dense(RgShared<BINS>& sh, const RgHistArgs& a, const uint32_t* ptr,
                                              const uint16_t* ent, const uint32_t* pdig, int64_t lo, int64_t hi,
                                              int wv, int lane, int np, int dbg, unsigned long long& sink) {
   const int32_t* list = a.list;
@@ -449,7 +418,7 @@ __device__ __forceinline__ void rg_range_dense(RgShared<BINS, HOT>& sh, const Rg
       nen = ptr[rn + 1];
       ndg = *reinterpret_cast<const uint2*>(pdig + 2 * pn);
     }
-    rg_batch<BINS, HOT>(sh, ent, wv, lane, st, en, (int32_t)rg_q(dg.x, np), (int32_t)rg_q(dg.y, np), dbg, sink);
+    rg_batch<BINS>(sh, ent, wv, lane, st, en, (int32_t)rg_q(dg.x, np), (int32_t)rg_q(dg.y, np), dbg, sink);
     st = nst;
     en = nen;
     dg = ndg;
@@ -465,16 +434,16 @@ __device__ __forceinline__ void rg_range_dense(RgShared<BINS, HOT>& sh, const Rg
 // super-batch j run: every load has a whole super-batch of work to arrive in.
 constexpr int kRgSB = 3;
 
-template <int BINS, int HOT>
-__device__ __forceinline__ void rg_run_block(RgShared<BINS, HOT>& sh, uint4 v, uint32_t blk, uint32_t st, uint32_t en,
-                                             unsigned long long c0, unsigned long long c1, uint32_t sinkb, int lane,
-                                             int dbg, unsigned long long& sink) {
+template <int BINS>
+__device__ __forceinline__ void rg_run_block(RgShared<BINS>& sh, uint4 v, uint32_t blk, uint32_t st, uint32_t en,
+                                             unsigned long long c0, unsigned long long c1, uint32_t sinkb, int dbg,
+                                             unsigned long long& sink) {
   const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const uint32_t i = blk + k;
     const uint32_t bin = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-    const uint32_t b = (i >= st && i < en) ? rg_slot<BINS, HOT>(bin, lane) : sinkb;
+    const uint32_t b = (i >= st && i < en) ? bin : sinkb;
     if (dbg & 2) {
       sink += b;
     } else {
@@ -484,14 +453,14 @@ __device__ __forceinline__ void rg_run_block(RgShared<BINS, HOT>& sh, uint4 v, u
   }
 }
 
-template <int BINS, int HOT>
-__device__ __forceinline__ void rg_range_sparse(RgShared<BINS, HOT>& sh, const RgHistArgs& a, const uint32_t* ptr,
+template <int BINS>
+__device__ __forceinline__ void rg_range_sparse(RgShared<BINS>& sh, const RgHistArgs& a, const uint32_t* ptr,
                                                 const uint16_t* ent, const uint32_t* pdig, int64_t lo, int64_t hi,
                                                 int wv, int lane, int np, int dbg, unsigned long long& sink) {
   const int32_t* list = a.list;
   const int64_t p0 = lo + wv * 64 + lane;
   constexpr int64_t kSBStride = (int64_t)kRgSB * kRgThreads;      // positions per super-batch
-  const uint32_t sinkb = BINS + HOT * 15 + lane;
+  const uint32_t sinkb = BINS + lane;
   auto pos_of = [&](int64_t j, int i) -> int64_t { return p0 + j * kSBStride + (int64_t)i * kRgThreads; };
   auto rows_of = [&](int64_t j, int32_t* r) {
 #pragma unroll
@@ -543,10 +512,10 @@ __device__ __forceinline__ void rg_range_sparse(RgShared<BINS, HOT>& sh, const R
         const unsigned long long c0 = (unsigned long long)rg_q(dg0[i].x, np);
         const unsigned long long c1 = (unsigned long long)rg_q(dg0[i].y, np);
         uint32_t blk = st0[i] & ~7u;
-        rg_run_block<BINS, HOT>(sh, v0[i], blk, st0[i], en0[i], c0, c1, sinkb, lane, dbg, sink);
+        rg_run_block<BINS>(sh, v0[i], blk, st0[i], en0[i], c0, c1, sinkb, dbg, sink);
         for (blk += 8; blk < en0[i]; blk += 8)        // rows longer than one block (rare here)
-          rg_run_block<BINS, HOT>(sh, *reinterpret_cast<const uint4*>(ent + blk), blk, st0[i], en0[i], c0, c1,
-                                  sinkb, lane, dbg, sink);
+          rg_run_block<BINS>(sh, *reinterpret_cast<const uint4*>(ent + blk), blk, st0[i], en0[i], c0, c1, sinkb,
+                             dbg, sink);
       }
     }
 #pragma unroll
@@ -569,9 +538,9 @@ __device__ __forceinline__ void rg_range_sparse(RgShared<BINS, HOT>& sh, const R
 // boundary of the chunk the workgroup flushes its histograms to that slot's level histogram row.
 // The pass is latency-bound (list -> (ptr, digits) -> entry blocks), so the next batch's row
 // state and the next entry block are loaded before the current ones are consumed.
-template <int BINS, int HOT>
+template <int BINS>
 __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
-  __shared__ RgShared<BINS, HOT> sh;
+  __shared__ RgShared<BINS> sh;
   const int w = blockIdx.x;
   if (w >= a.n_wg) return;
   const int g = a.wg_g[w], p = a.wg_p[w], np_g = a.wg_np[w];
@@ -579,7 +548,7 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
   const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
   if (a0 >= a1) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < BINS + HOT * 15; i += kRgThreads) {
+  for (int i = tid; i < BINS; i += kRgThreads) {
     sh.hg[i] = 0;
     sh.hh[i] = 0;
   }
@@ -600,12 +569,12 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
     const int64_t ss1 = list ? (int64_t)a.slot_start[s + 1] : a.N;
     const int64_t lo = a0 > ss0 ? a0 : ss0, hi = a1 < ss1 ? a1 : ss1;
     if (bal)
-      rg_range_dense<BINS, HOT>(sh, a, ptr, ent, pdig, lo, hi, wv, lane, np, dbg, sink);
+      rg_range_dense<BINS>(sh, a, ptr, ent, pdig, lo, hi, wv, lane, np, dbg, sink);
     else
-      rg_range_sparse<BINS, HOT>(sh, a, ptr, ent, pdig, lo, hi, wv, lane, np, dbg, sink);
+      rg_range_sparse<BINS>(sh, a, ptr, ent, pdig, lo, hi, wv, lane, np, dbg, sink);
     if (dbg & 2) atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[lane]), sink);
     __syncthreads();
-    rg_flush<BINS, HOT>(a, sh, g, s, tid);
+    rg_flush<BINS>(a, sh, g, s, tid);
     __syncthreads();
     if (!list || ss1 >= a1 || s + 1 >= a.nslots) break;
     ++s;
@@ -647,11 +616,9 @@ void launch_rg_hist(const RgHistArgs& a, hipStream_t s) {
   const int64_t blocks = a.n_wg;
   if (blocks <= 0) return;
   if (a.gbins == 4096)
-    hipLaunchKernelGGL((rg_hist_kernel<4096, 0>), dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
-  else if (a.gbins == 6144 && a.hot == kRgHot)
-    hipLaunchKernelGGL((rg_hist_kernel<6144, kRgHot>), dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
+    hipLaunchKernelGGL(rg_hist_kernel<4096>, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((rg_hist_kernel<8192, 0>), dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
+    hipLaunchKernelGGL(rg_hist_kernel<8192>, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
 }
 
 }  // namespace fdx

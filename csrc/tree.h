@@ -127,8 +127,6 @@ constexpr int32_t kListedWaves = 8192;
 constexpr int kRgBins = 8192;               // max local bins per group: 2 x 8192 x int64 = 128 KB of LDS
                                             // (4096-bin groups: two workgroups per CU)
 constexpr int kRgWaves = 16;                // 1024 threads per workgroup (one workgroup per CU)
-constexpr int kRgHot = 128;                 // 6144-bin groups: local bins 0..127 are the group's most
-                                            // frequent, kept in 16 lane replicas (row_kernels.hip rg_slot)
 constexpr int kRgMaxSlots = 64;
 
 struct RgBuildArgs {
@@ -201,9 +199,7 @@ struct RgHistArgs {
   const uint16_t* ent;            // entries (readable padding behind the end)
   const int64_t* gbase;           // [G + 1]
   const int32_t* gbin;            // [G][gbins] histogram column of each local bin (-1: unused)
-  int32_t gbins;                  // local bins per group: 4096, 6144 (with hot == kRgHot) or 8192
-  int32_t hot;                    // local bins 0..hot-1 are the group's hottest (layout only: the sums
-                                  //   are the same for any hot count; 6144-bin groups need kRgHot)
+  int32_t gbins;                  // local bins per group: 4096 or 8192
   int32_t G;
   int64_t N;
   const uint32_t* rowdig;         // [N * 2] digit words (by row; the list pass reads listdig)

@@ -124,10 +124,6 @@ def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.T
 
 RG_BINS = int(os.environ.get("FDX_RG_BINS", 8192))   # local bins per row group: 8192 (1 workgroup per CU) or 4096 (2)
 RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
-# 6144-bin groups carry the hot layout: their RG_HOT most frequent local bins in lane replicas
-# (csrc/tree.h kRgHot; FDX_RG_BINS=6144 selects it)
-RG_HOT_BINS = 6144
-RG_HOT = 128
 RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 2048))   # workgroups per row-group pass
 # work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
 # (ptr, digits) loads whether or not it has entries in the group)
@@ -176,8 +172,8 @@ class RowGroups:
         tick = _Ticker(dev, self.timing) if os.environ.get("FDX_RG_TIMING") == "1" else None
         max_groups = RG_MAX_GROUPS if max_groups is None else max_groups
         self.bins = B = RG_BINS if bins is None else bins
-        if B not in (4096, 6144, 8192):
-            raise ValueError("row groups hold 4096, 6144 (hot layout) or 8192 bins")
+        if B not in (4096, 8192):
+            raise ValueError("row groups hold 4096 or 8192 bins")
         colptr = Q.colptr.cpu().numpy()
         cnt = np.diff(colptr)
         nb = Q.nbins.cpu().numpy().astype(np.int64)
@@ -250,43 +246,7 @@ class RowGroups:
             cursor = self.ptr[:, :N].clone(memory_format=torch.contiguous_format)   # (a view when G == 1)
             C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 1, None, cursor, self.gbase, self.ent)
             del cursor
-        self.hot = 0
-        if B == RG_HOT_BINS:
-            self._hot_layout()
         self._work: dict = {}
-
-    def _hot_layout(self) -> None:
-        """Renumber each group's local bins so that its RG_HOT most frequent bins are 0..RG_HOT-1
-        (csrc/row_kernels.hip keeps those in 16 lane replicas: on a text corpus a few hundred
-        (term, count) bins hold about half of all entries, and the lanes of one LDS atomic that hit
-        the same bin, or the same bank pair, serialise). The entries are rewritten in place and
-        the group's bin -> histogram column table permuted with them, so every histogram is the
-        same sum (only the LDS layout changes). Counting and rewriting go in chunks (no
-        full-size temporaries)."""
-        dev, G, B, H = self.ent.device, self.G, self.bins, RG_HOT
-        gbase = self.gbase.cpu().numpy()
-        chunk = 1 << 25
-        gbin = self.gbin.clone()
-        for g in range(G):
-            a0, a1 = int(gbase[g]), int(gbase[g] + self.group_entries[g])
-            cnt = torch.zeros(B, dtype=torch.int64, device=dev)
-            for a in range(a0, a1, chunk):
-                c = self.ent[a:min(a1, a + chunk)].to(torch.int32) & 0xFFFF
-                cnt += torch.bincount(c, minlength=B)[:B]
-            order = torch.sort(-cnt, stable=True).indices            # hottest first, ties by bin
-            perm = torch.empty(B, dtype=torch.int32, device=dev)
-            perm[order] = torch.arange(B, dtype=torch.int32, device=dev)
-            # hot bins keep their frequency order; the rest keep their original order behind them
-            cold = torch.sort(order[H:]).values
-            perm[cold] = torch.arange(H, B, dtype=torch.int32, device=dev)
-            for a in range(a0, a1, chunk):
-                seg = self.ent[a:min(a1, a + chunk)]
-                seg.copy_(perm[seg.to(torch.int64) & 0xFFFF].to(torch.int16))
-            newg = torch.empty_like(gbin[g])
-            newg[perm.to(torch.int64)] = self.gbin[g]
-            gbin[g] = newg
-        self.gbin = gbin.contiguous()
-        self.hot = H
 
     def work(self, target_wgs: int = 0, alpha: float = None) -> torch.Tensor:
         """Work table [3, n_wg] int32 (group, chunk, chunks of that group): each group's list is cut

@@ -238,8 +238,7 @@ def test_row_groups_incomplete_beyond_max_groups():
 @pytest.mark.parametrize("nslots,root,np_,F,bins", [(1, True, 4, 250, 8192), (2, False, 4, 250, 4096),
                                                      (5, False, 4, 250, 8192), (33, False, 4, 250, 4096),
                                                      (3, False, 1, 250, 8192), (1, True, 4, 40, 8192),
-                                                     (4, False, 4, 40, 8192), (1, True, 4, 250, 6144),
-                                                     (5, False, 4, 250, 6144), (3, False, 1, 40, 6144)])
+                                                     (4, False, 4, 40, 8192)])
 def test_row_group_histograms_equal_host_reference(nslots, root, np_, F, bins):
     """Several groups (F = 250) and a single group (F = 40: the cursor copy must not alias ptr)."""
     rng = np.random.default_rng(nslots)
@@ -248,7 +247,6 @@ def test_row_group_histograms_equal_host_reference(nslots, root, np_, F, bins):
     row_node = rng.integers(-1, nslots + 1, n).astype(np.int32) if not root else np.zeros(n, np.int32)
     hist, q0, q1, Q, rg = _rg_hist_on("cpu", vc, 100, nslots, row_node, root, np_=np_, bins=bins)
     assert (rg.G >= 2) == (F > 100)
-    assert rg.hot == (128 if bins == 6144 else 0)
     np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, nslots, q0, q1))
 
 
@@ -301,7 +299,7 @@ def test_row_group_sharded_layout_equals_plain():
     np.testing.assert_array_equal(plain, sh)
 
 
-@pytest.mark.parametrize("depth,hot,bins", [(6, 0.2, 8192), (3, 0.0, 8192), (6, 0.2, 6144)])
+@pytest.mark.parametrize("depth,hot,bins", [(6, 0.2, 8192), (3, 0.0, 8192), (6, 0.2, 4096)])
 def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot, bins):
     """FDX_ROWHIST=1: every GBDT level's histograms come from the row-group engine; the trees
     equal the CSC / dense passes' trees bit for bit (device level loop, host twins)."""
@@ -322,8 +320,7 @@ def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot, bins)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nslots,root,bins", [(1, True, 8192), (2, False, 4096), (5, False, 8192), (32, False, 4096),
-                                              (1, True, 6144), (7, False, 6144)])
+@pytest.mark.parametrize("nslots,root,bins", [(1, True, 8192), (2, False, 4096), (5, False, 8192), (32, False, 4096)])
 @pytest.mark.parametrize("sharded", [False, True])
 @pytest.mark.parametrize("mode", [None, 0, 1])
 def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded, mode, monkeypatch):
@@ -345,28 +342,8 @@ def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded
     np.testing.assert_array_equal(a, b)
 
 
-def test_hot_layout_puts_the_most_frequent_bins_first():
-    """RowGroups with 6144-bin groups renumber each group's local bins hottest first (the LDS
-    lane-replica layout): the remapped entries still address the same histogram columns."""
-    vc = _wide(4000, 250, 3)
-    Q = quantize(vc, max_bins=100, **QKW)
-    rg = RowGroups(Q, bins=6144)
-    plain = RowGroups(Q, bins=8192)
-    assert rg.hot == 128
-    gb = rg.gbase.numpy()
-    for g in range(rg.G):
-        ent = rg.ent[gb[g]:gb[g] + rg.group_entries[g]].numpy().astype(np.int64) & 0xFFFF
-        cnt = np.bincount(ent, minlength=6144)
-        hot = cnt[:128]
-        assert np.all(hot[:-1] >= hot[1:]) and (cnt[128:].max(initial=0) <= hot.min())
-    # the multiset of histogram columns the entries address is unchanged
-    cols = lambda r: np.sort(np.concatenate([r.gbin[g].numpy()[r.ent[int(r.gbase[g]):int(r.gbase[g]) + int(r.group_entries[g])].numpy().astype(np.int64) & 0xFFFF]
-                                             for g in range(r.G)]))  # noqa: E731
-    np.testing.assert_array_equal(cols(rg), cols(plain))
-
-
 @pytest.mark.gpu
-@pytest.mark.parametrize("bins", [8192, 6144])
+@pytest.mark.parametrize("bins", [8192, 4096])
 def test_gpu_row_group_level_loop_grows_the_same_trees(monkeypatch, bins):
     from fraud_detection_spark_kafka_llm_amd.models import grower, quantize as qmod
 
