@@ -33,6 +33,7 @@ __global__ __launch_bounds__(kThreads) void rf_window_kernel(RfSampleArgs a, uin
   __shared__ unsigned int s_below;
   const int i = blockIdx.y;
   const int node = a.nodes[i];
+  if (node < 0) return;                           // padding of a capacity-sized open list
   if (threadIdx.x == 0) s_below = 0;
   __syncthreads();
   unsigned int mine = 0;
@@ -62,6 +63,10 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
 
   const int node = a.nodes[blockIdx.x];
   const int tid = threadIdx.x;
+  if (node < 0) {                                 // padding: samples nothing
+    if (tid == 0) a.thr[blockIdx.x] = -1.0;
+    return;
+  }
   if (below != nullptr) {
     const int64_t r = a.k - (int64_t)below[blockIdx.x];     // rank of the k-th inside the window
     const int n = (int)ncand[blockIdx.x];
@@ -148,6 +153,7 @@ __global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
   const int64_t fid = a.fid_orig[f];
   uint8_t m = 0;
   for (int i = 0; i < a.nnodes && !m; ++i) {
+    if (a.nodes[i] < 0) continue;
     const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, i), a.nodes[i], fid);
     m = ((double)u * (1.0 / 9007199254740992.0) <= a.thr[i]) ? 1 : 0;
   }

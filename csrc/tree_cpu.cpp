@@ -92,6 +92,7 @@ void rf_sample_cpu(const RfSampleArgs& a) {
   parallel_for(a.nnodes, 0, 1, [&](int64_t lo, int64_t hi) {
     std::vector<uint64_t> u((size_t)a.F);
     for (int64_t i = lo; i < hi; ++i) {
+      if (a.nodes[i] < 0) { a.thr[i] = -1.0; continue; }   // padding of a capacity-sized open list
       for (int64_t f = 0; f < a.F; ++f) u[(size_t)f] = feature_priority_u53(a.seed, rf_tree_of(a, i), a.nodes[i], f);
       std::nth_element(u.begin(), u.begin() + (a.k - 1), u.end());
       a.thr[i] = (double)u[(size_t)(a.k - 1)] * (1.0 / 9007199254740992.0);
@@ -101,7 +102,8 @@ void rf_sample_cpu(const RfSampleArgs& a) {
     for (int64_t f = lo; f < hi; ++f) {
       uint8_t m = 0;
       for (int i = 0; i < a.nnodes && !m; ++i)
-        m = ((double)feature_priority_u53(a.seed, rf_tree_of(a, i), a.nodes[i], a.fid_orig[f]) * (1.0 / 9007199254740992.0) <=
+        m = a.nodes[i] >= 0 &&
+            ((double)feature_priority_u53(a.seed, rf_tree_of(a, i), a.nodes[i], a.fid_orig[f]) * (1.0 / 9007199254740992.0) <=
              a.thr[i]) ? 1 : 0;
       a.mask[f] = m;
     }

@@ -390,11 +390,14 @@ class FeatureShards:
         self._nbins_all = Q.nbins
         self._fs_dev = torch.from_numpy(fs).to(dev)
         self.max_nb = int(Q.nbins.max()) if Fa else 1
-        self._local_c = torch.zeros(Fa + 1, dtype=torch.int64, device=dev)
-        self._sizes = torch.zeros(S, dtype=torch.int64, device=dev)
-        self.sizes_host = torch.zeros(S, dtype=torch.int64)
+        # two sets (level parity): level d + 1's layout is computed while level d is in flight
+        self._local_c = [torch.zeros(Fa + 1, dtype=torch.int64, device=dev) for _ in range(2)]
+        self._sizes = [torch.zeros(S, dtype=torch.int64, device=dev) for _ in range(2)]
+        self.sizes_host = [torch.zeros(S, dtype=torch.int64) for _ in range(2)]
         if dev.type == "cuda":
-            self.sizes_host = self.sizes_host.pin_memory()
+            self.sizes_host = [t.pin_memory() for t in self.sizes_host]
+        self._thr = [None, None]
+        self._mask = [torch.empty(Fa, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.zbin = Q.zbin[f0:f1].contiguous()
         self.fid_orig = Q.fid_orig[f0:f1].contiguous()
 
@@ -411,23 +414,27 @@ class FeatureShards:
         """Zeroed shard-major partial histograms [S, nb, Bs, 2] of a DP level."""
         return torch.zeros((self.S, nb, self.Bs, 2), dtype=torch.int64, device=dev)
 
-    def compact(self, feat_mask: torch.Tensor):
-        """Per-level compact layout of an RF level (csrc/tree.h RfCompactArgs): the features of the
-        level's union sample mask packed per shard, the rest aimed at a per-shard trash range.
-        Queues the layout kernel and the copy of the shard sizes to ``sizes_host``; returns the
-        device offsets [Fa + 1] (read ``sizes_host`` once the returned event completed)."""
-        native.lib().tree_rf_compact(feat_mask, self._nbins_all, self._fs_dev, self._local_c, self._sizes)
-        self.sizes_host.copy_(self._sizes, non_blocking=True)
-        if self._local_c.is_cuda:
-            ev = torch.cuda.Event()
-            ev.record()
-        else:
-            ev = _Done()
-        return self._local_c, ev
+    def sample_compact(self, C, p: int, seed: int, tree: int, nodes: torch.Tensor, F: int, k: int,
+                       fid_orig: torch.Tensor) -> None:
+        """Feature sample of the open nodes ``nodes`` (-1 padding allowed) into parity-``p``
+        buffers, then the level's compact layout (csrc/tree.h RfCompactArgs): the features of the
+        union sample mask packed per shard, the rest aimed at a per-shard trash range. Queues the
+        copy of the shard sizes to ``sizes_host[p]``: read it after the next event the caller
+        records on this stream."""
+        n = int(nodes.numel())
+        thr = self._thr[p]
+        if thr is None or thr.numel() < n:
+            thr = self._thr[p] = torch.empty(max(n, 2), dtype=torch.float64, device=nodes.device)
+        C.tree_rf_sample(seed, tree, nodes, F, k, fid_orig, thr[:n], self._mask[p], None)
+        C.tree_rf_compact(self._mask[p], self._nbins_all, self._fs_dev, self._local_c[p], self._sizes[p])
+        self.sizes_host[p].copy_(self._sizes[p], non_blocking=nodes.is_cuda)
 
-    def compact_stride(self) -> int:
-        """Bins per node row of a compact level: the largest shard's sampled bins plus its trash."""
-        return int(self.sizes_host.max()) + self.max_nb
+    def compact_level(self, p: int, n_open: int):
+        """(feat_thr [n_open], feat_mask, local offsets [Fa + 1], stride) of the parity-``p`` layout
+        (its sizes must have reached the host): stride = the largest shard's sampled bins plus
+        the trash range."""
+        return (self._thr[p][:n_open], self._mask[p], self._local_c[p],
+                int(self.sizes_host[p].max()) + self.max_nb)
 
 
 def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, params, feat_thr, tree_index, Fa,
@@ -913,6 +920,14 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     n_open, n_build = 1, 1
     prev_hist = None
     ev = None
+    # RF under data parallelism: each level reduce-scatters only its sampled features' bins; level
+    # d + 1's sample and layout are computed right after level d's plan, so their shard sizes reach
+    # the host with the level's counts (one wait per level; the root's before the loop)
+    compact = shards is not None and build_all and RF_COMPACT and 0 < params.feat_k < Q.num_features
+    if compact:
+        shards.sample_compact(C, 0, seed, int(tree_index), st.open[0][:1], int(Q.num_features), int(params.feat_k),
+                              Q.fid_orig)
+        yield st.record_event()
     for d in range(params.max_depth):
         cur = d % 2
         if d > 0:
@@ -931,7 +946,9 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
         # RF: exact k-of-F feature sample per open node and the level's union mask (device)
         feat_thr = feat_mask = None
-        if build_all:
+        if compact:
+            feat_thr, feat_mask, local_c, Bs_c = shards.compact_level(cur, n_open)
+        elif build_all:
             feat_thr = torch.empty(n_open, dtype=torch.float64, device=dev)
             feat_mask = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
             C.tree_rf_sample(seed, int(tree_index), open_d, int(Q.num_features), int(params.feat_k), Q.fid_orig,
@@ -940,12 +957,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         if shards is None:
             cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
             h_boff, h_stride = Q.boff, TB
-        elif build_all and RF_COMPACT and params.feat_k:
-            # only the sampled features' bins travel: the layout needs the shard sizes on the host
-            # (one 8-byte-per-shard copy; the lanes of a forest run meanwhile)
-            local_c, ev_c = shards.compact(feat_mask)
-            yield ev_c
-            Bs_c = shards.compact_stride()
+        elif compact:
+            # only the sampled features' bins travel (FeatureShards.sample_compact)
             rs_buf = torch.zeros((shards.S, n_build, Bs_c, 2), dtype=torch.int64, device=dev)
             hist_target = rs_buf.view(shards.S * n_build, Bs_c, 2)
             h_boff, h_stride = torch.add(local_c, shards._shard_of, alpha=n_build * Bs_c), Bs_c
@@ -1057,6 +1070,10 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                           st.n_nodes, st.stats, st.parent, st.left, st.right, st.feat, st.bin, st.leaf, st.gain,
                           open_d, n_open_ptr, st.default_child, st.node_dense, *st.cs, st.counts[d],
                           st.open[nxt], st.totals[nxt], st.node_slot, st.s2n, st.sub_dst, st.sub_par, st.sub_sib)
+        if compact and d + 1 < params.max_depth:
+            # level d + 1's open list is at most 2 n_open long, -1 padded (tree.h level_plan_reset)
+            shards.sample_compact(C, nxt, seed, int(tree_index), st.open[nxt][:2 * n_open], int(Q.num_features),
+                                  int(params.feat_k), Q.fid_orig)
         st.counts_host[d].copy_(st.counts[d], non_blocking=dev.type == "cuda")
         ev = st.record_event()
         with tracing.span("tree.partition"):

@@ -480,6 +480,17 @@ def _rf_sample(dev, F=5000, k=71, nodes=(0, 1, 2, 5, 9), seed=123456789, tree=7)
     return thr.cpu(), mask.cpu(), fid.cpu()
 
 
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_rf_sampling_skips_padded_nodes(dev):
+    """-1 entries (the padding of a capacity-sized open list: the next level's sample is drawn
+    before its size reaches the host) sample nothing: threshold -1, no mask contribution."""
+    a_thr, a_mask, _ = _rf_sample(dev, nodes=(3, 8))
+    b_thr, b_mask, _ = _rf_sample(dev, nodes=(3, -1, 8, -1))
+    assert torch.equal(a_mask, b_mask)
+    assert b_thr[1] == -1.0 and b_thr[3] == -1.0
+    assert b_thr[0] == a_thr[0] and b_thr[2] == a_thr[1]
+
+
 def test_rf_sampling_native_equals_python_oracle():
     """Exactly k of F features per node: the native k-th smallest priority equals torch.kthvalue
     over the oracle priorities, and the union mask equals the oracle's."""
