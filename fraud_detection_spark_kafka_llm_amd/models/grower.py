@@ -73,18 +73,20 @@ def reset_level_stats() -> None:
 
 def level_collective_ms() -> float:
     """Milliseconds the level loops' streams spent in their reduce-scatter + all-gather (device
-    event pairs around the collectives, as the issuing stream sees them: a lane whose collective
-    queues behind another lane's on the communicator's stream counts that wait too)."""
+    event pairs around every LEVEL_TIMING-th collective, scaled by LEVEL_TIMING; as the issuing
+    stream sees them: a lane whose collective queues behind another lane's on the
+    communicator's stream counts that wait too)."""
     while _COLL_EVENTS:
         b, e = _COLL_EVENTS.pop(0)
         e.synchronize()
-        LEVEL_STATS["coll_ms"] += b.elapsed_time(e)
+        LEVEL_STATS["coll_ms"] += b.elapsed_time(e) * max(LEVEL_TIMING, 1)
     return float(LEVEL_STATS["coll_ms"])
 
 
-# FDX_LEVEL_TIMING=0: no timing events around the level collectives (their record calls cost the
-# host thread that drives the RF lanes a few microseconds each)
-LEVEL_TIMING = os.environ.get("FDX_LEVEL_TIMING", "1") != "0"
+# Timing events around the level collectives: every LEVEL_TIMING-th collective is timed and the
+# total scaled by LEVEL_TIMING (event records cost the host thread that drives the RF lanes a few
+# microseconds each: timing every call added ~5 % to a forest); 1: every call, 0: none
+LEVEL_TIMING = int(os.environ.get("FDX_LEVEL_TIMING", "8"))
 
 
 class _CollTimer:
@@ -92,9 +94,10 @@ class _CollTimer:
 
     def __init__(self, dev: torch.device):
         self.cuda = dev.type == "cuda"
+        self.on = LEVEL_TIMING > 0 and LEVEL_STATS["coll_calls"] % LEVEL_TIMING == 0
 
     def __enter__(self):
-        if not LEVEL_TIMING:
+        if not self.on:
             return self
         if self.cuda:
             self.b = torch.cuda.Event(enable_timing=True)
@@ -105,7 +108,7 @@ class _CollTimer:
 
     def __exit__(self, *exc):
         LEVEL_STATS["coll_calls"] += 1
-        if not LEVEL_TIMING:
+        if not self.on:
             return False
         if self.cuda:
             e = torch.cuda.Event(enable_timing=True)
@@ -114,10 +117,10 @@ class _CollTimer:
             if len(_COLL_EVENTS) > 8192:        # bounded: resolve the oldest half (long finished)
                 for b, e in _COLL_EVENTS[:4096]:
                     e.synchronize()
-                    LEVEL_STATS["coll_ms"] += b.elapsed_time(e)
+                    LEVEL_STATS["coll_ms"] += b.elapsed_time(e) * LEVEL_TIMING
                 del _COLL_EVENTS[:4096]
         else:
-            LEVEL_STATS["coll_ms"] += (time.perf_counter() - self.b) * 1e3
+            LEVEL_STATS["coll_ms"] += (time.perf_counter() - self.b) * 1e3 * LEVEL_TIMING
         return False
 # row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
 # histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
@@ -130,8 +133,10 @@ LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 # RF levels under data parallelism reduce-scatter only the bins of the level's sampled features
-# (FeatureShards.compact; FDX_RF_COMPACT=0: every active feature's bins)
-RF_COMPACT = os.environ.get("FDX_RF_COMPACT", "1") != "0"
+# (FeatureShards.sample_compact). "auto": when the reduce-scatter crosses ranks (world > 1; at
+# world 1 it is a local copy and the layout pass only costs); "1" always (the world-1 RCCL
+# rehearsal of the path); "0" never
+RF_COMPACT = os.environ.get("FDX_RF_COMPACT", "auto")
 
 
 # GBDT trees grow with the device-resident level loop (grow_tree_device): split application and
@@ -923,7 +928,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     # RF under data parallelism: each level reduce-scatters only its sampled features' bins; level
     # d + 1's sample and layout are computed right after level d's plan, so their shard sizes reach
     # the host with the level's counts (one wait per level; the root's before the loop)
-    compact = shards is not None and build_all and RF_COMPACT and 0 < params.feat_k < Q.num_features
+    compact = shards is not None and build_all and 0 < params.feat_k < Q.num_features and \
+        (RF_COMPACT == "1" or (RF_COMPACT == "auto" and shards.S > 1))
     if compact:
         shards.sample_compact(C, 0, seed, int(tree_index), st.open[0][:1], int(Q.num_features), int(params.feat_k),
                               Q.fid_orig)

@@ -72,3 +72,40 @@ def test_suite_xgb_and_rf_two_ranks_gloo_rehearsal():
         rec = json.loads(lines[0])
         assert rec["bench"] == which and rec["world"] == 2 and rec["rows"] == 60000
         assert rec["rows_per_rank"] == 30000 and rec["train_s"] > 0 and rec["trees"] == 3
+
+
+@pytest.mark.gpu
+def test_bench_gbdt_phase_peak_matches_the_hbm_model():
+    """bench.py's timed GBDT phase (chunked featurization with the per-chunk feature order, IDF,
+    100-tree fit) on a 2M-row shard: the caching allocator's peak is within 15 % of
+    utils/memory.py's pipeline model (the full 10M-row bench reports it as train_peak_over_model:
+    0.955 in profiles/r4/bench_full_session_f.json)."""
+    import torch
+
+    sys.path.insert(0, REPO)
+    import bench as B
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+    from fraud_detection_spark_kafka_llm_amd.ml.stopwords import ENGLISH
+    from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+    from fraud_detection_spark_kafka_llm_amd.ops import text as T
+    from fraud_detection_spark_kafka_llm_amd.utils import memory
+
+    dev = torch.device("cuda:0")
+    rows, chunk = 2_000_000, 250_000
+    spec = T.FeatureSpec(clean=True, stopwords=list(ENGLISH), num_features=B.F)
+    chunks = B.generate_shard(0, rows, dev, seed=11, chunk=chunk)
+    text_bytes = sum(int(h.data.numel()) for h, _ in chunks)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    base = torch.cuda.memory_allocated(dev)
+    torch.cuda.reset_peak_memory_stats(dev)
+    indptr, idx, counts, y, fo = B.featurize_shard(chunks, dev, spec, order=True)
+    idf = torch.log((rows + 1.0) / (fo.df.double() + 1.0))
+    vc = VectorColumn.tfidf(B.F, indptr, idx, counts, idf, fo)
+    res = fit_gbdt(vc, y, GBDTParams(n_estimators=20, max_depth=6), device=dev)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated(dev) - base
+    model = memory.pipeline_bytes(rows, int(idx.numel()), hot_features=res.shape["hot"],
+                                  groups=res.shape["groups"] or memory.DEFAULT_GROUPS,
+                                  text_bytes_per_row=text_bytes / rows, chunk_rows=chunk)
+    assert 0.85 <= peak / model <= 1.15, (peak / 2 ** 30, model / 2 ** 30)

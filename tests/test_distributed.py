@@ -268,6 +268,7 @@ def test_gpu_rccl_forced_collectives_rf_lanes_equal_serial(monkeypatch):
     serial = spawn(_train_rf_lanes, 1, "cuda:0", backend="gloo")[0]
     monkeypatch.setenv("FDX_RF_INFLIGHT", "4")
     monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
+    monkeypatch.setenv("FDX_RF_COMPACT", "1")         # the compact-level layout on the device too
     (trees, lanes, seq, n_coll), = spawn(_train_rf_lanes, 1, "cuda:0", backend="nccl")
     assert lanes == 4 and n_coll > 0
     assert any(name == "reduce_scatter_tensor" for name, _ in seq)

@@ -29,3 +29,4 @@ def test_effective_workers_raises_ranks_when_a_shard_would_not_fit(monkeypatch):
     assert estimator_dp.effective_workers(2, rows, "cuda:0") == 2        # without nnz: as requested
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
     assert estimator_dp.effective_workers(1, rows, "cuda:0", nnz=rows * 100) == 2   # capped at the GPUs
+
