@@ -44,10 +44,12 @@ from ..utils import tracing
 from .grower import GrowParams, Workspace, device_tree_steps
 from .quantize import Quantized
 
-TREES_IN_FLIGHT = int(os.environ.get("FDX_RF_INFLIGHT", "4"))
+# 500 trees x depth 5 on 10M rows (profiles/r4/rf500_sweep_*.json): 4 lanes with 4 histogram
+# streams each 1.02 s, 8 x 1 0.97 s, 12 x 1 0.95 s, 16 x 1 0.92 s (+0.27 GB of workspace per lane)
+TREES_IN_FLIGHT = int(os.environ.get("FDX_RF_INFLIGHT", "16"))
 # histogram side streams per lane (grower.Workspace.run_concurrent): the lanes already overlap
 # whole trees, and every extra stream is another HW-queue mapping and cross-stream event per level
-LANE_HIST_STREAMS = int(os.environ.get("FDX_RF_LANE_STREAMS", "4"))
+LANE_HIST_STREAMS = int(os.environ.get("FDX_RF_LANE_STREAMS", "1"))
 
 
 class ForestLanes:
