@@ -415,6 +415,7 @@ def main():
     # against the device's total memory (the bench's own allocations excluded)
     shape = dict(hot_features=res.shape.get("hot", memory.DEFAULT_HOT_FEATURES),
                  groups=res.shape.get("groups", memory.DEFAULT_GROUPS) or memory.DEFAULT_GROUPS,
+                 sparse_frac=res.shape.get("sparse_frac", memory.DEFAULT_SPARSE_FRAC),
                  text_bytes_per_row=text_bytes / max(shard_rows, 1), chunk_rows=CHUNK_ROWS)
     modeled = memory.pipeline_bytes(shard_rows, shard_nnz, **shape)
     sizing = {"max_rows_per_gpu": memory.max_rows_per_gpu(

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--split", action="store_true", help="also time the densest group and the rest apart")
     ap.add_argument("--only", default="", help="group0 / others: time only that part (PMC runs); no equality check")
     ap.add_argument("--modes", default="auto", help="group pass modes: auto (the layout's), 0 (lane per row), 1 (balanced)")
+    ap.add_argument("--em", default="1", help="entry-major sparse pass at single-slot levels: 0, 1 or 0,1")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     C = native.lib()
@@ -102,8 +103,9 @@ def main():
     start = torch.zeros(66, dtype=torch.int32, device=dev)
     work = torch.zeros(64 * (2 + n // 2048 + 1), dtype=torch.int32, device=dev)
     ldig = torch.empty((n, 2), dtype=torch.int32, device=dev)
-    for ns in [int(x) for x in args.slots.split(",")]:
-        root = ns == 1
+    for ns_s in args.slots.split(","):
+        # "1L": a listed level with one built slot (about half the rows)
+        ns, root = int(ns_s.rstrip("L")), ns_s == "1"
         slot8 = None
         if not root:
             # about half the rows built (the smaller siblings), spread over ns slots
@@ -118,15 +120,20 @@ def main():
             ref[:, zb] = 0
         s2n = torch.arange(ns, dtype=torch.int32, device=dev)
         list_ms = 0.0
+        rn_d = ns_d = None
         if not root:
             rn_d = torch.from_numpy(rn).to(dev)
             ns_d = node_slot.to(dev)
             list_ms = timed(lambda: C.tree_rg_list(rn_d, ns_d, None, n, ns, work, start, lst, ws.rowdig, ldig))
-        for B, wgs, alpha, dbg, mode in [(B, int(w), float(al), int(db), md) for B in rgs for w in args.wgs.split(",")
-                                         for al in args.alphas.split(",") for db in args.dbg.split(",")
-                                         for md in args.modes.split(",")]:
+        for B, wgs, alpha, dbg, mode, em in [(B, int(w), float(al), int(db), md, int(e)) for B in rgs
+                                             for w in args.wgs.split(",") for al in args.alphas.split(",")
+                                             for db in args.dbg.split(",") for md in args.modes.split(",")
+                                             for e in args.em.split(",")]:
             if True:
                 rg = rgs[B]
+                kw = rg.em_args(not root, rn_d, ns_d) if em else {}
+                if kw and not root:
+                    kw["em_min_rows"] = 1
                 gm = rg.gmode if mode == "auto" else torch.full_like(rg.gmode, int(mode))
                 hist = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)
                 wt = rg.work(wgs, alpha)
@@ -137,12 +144,13 @@ def main():
                     hist.zero_()
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
                                    None if root else start, None if root else ldig, ns, gm, wt, s2n, hist, Q.TB,
-                                   None, 0, dbg)
+                                   None, 0, dbg, **kw)
                 ms = timed(run)
                 if zb is not None:
                     hist[:, zb] = 0
                 eq = bool(torch.equal(hist, ref)) if not args.only else None
-                print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "mode": mode, "wgs": int(wt.shape[1]), "dbg": dbg,
+                print(json.dumps({"slots": ns_s, "em": em, "bins": B, "alpha": alpha, "mode": mode,
+                                  "wgs": int(wt.shape[1]), "dbg": dbg,
                                   "rg_ms": round(ms, 3),
                                   "list_ms": round(list_ms, 3), "csc_ms": round(csc_ms, 3), "equal": eq}), flush=True)
                 if eq is False and dbg < 2:
@@ -156,8 +164,8 @@ def main():
                             hist.zero_()
                             C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, 4, None if root else lst,
                                            None if root else start, None if root else ldig, ns, gm, sub, s2n, hist,
-                                           Q.TB, None, 0, dbg)
-                        print(json.dumps({"slots": ns, "bins": B, "alpha": alpha, "mode": mode, "dbg": dbg, "part": name,
+                                           Q.TB, None, 0, dbg, **kw)
+                        print(json.dumps({"slots": ns_s, "em": em, "bins": B, "alpha": alpha, "mode": mode, "dbg": dbg, "part": name,
                                           "wgs": int(sub.shape[1]), "rg_ms": round(timed(run_sub), 3)}), flush=True)
 
 

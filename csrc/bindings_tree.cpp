@@ -529,7 +529,8 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
              int64_t np, const optional<Tensor>& list, const optional<Tensor>& slot_start,
              const optional<Tensor>& listdig, int64_t nslots, const Tensor& gmode, const Tensor& wg,
              const Tensor& slot_node, const Tensor& hist, int64_t stride, const optional<Tensor>& shard_lo,
-             int64_t shard_stride, int64_t dbg) {
+             int64_t shard_stride, int64_t dbg, const optional<Tensor>& erow, int64_t ebase,
+             const optional<Tensor>& row_node, const optional<Tensor>& node_slot, int64_t em_min_rows) {
   const auto dev = ptr.device();
   chk(ptr, dev, at::kInt, "ptr");
   chk(gbase, dev, at::kLong, "gbase");
@@ -593,12 +594,59 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
     a.shard_lo = shard_lo->data_ptr<int64_t>();
     a.shard_stride = shard_stride;
   }
+  if (erow && erow->defined()) {
+    chk(*erow, dev, at::kInt, "erow");
+    // (ent holds exactly gbase[G] entries: no device read here)
+    FDX_CHECK(ebase >= 0 && ebase <= ent.numel() && erow->numel() >= ent.numel() - ebase,
+              "erow must cover the entries from ebase on");
+    a.erow = reinterpret_cast<const uint32_t*>(erow->data_ptr<int32_t>());
+    a.ebase = ebase;
+    a.em_min_rows = em_min_rows;
+    if (list) {
+      FDX_CHECK(row_node.has_value() && node_slot.has_value(), "a listed entry-major pass needs row_node / node_slot");
+      chk(*row_node, dev, at::kInt, "row_node");
+      chk(*node_slot, dev, at::kInt, "node_slot");
+      FDX_CHECK(row_node->numel() >= N, "row_node must cover the rows");
+      a.row_node = row_node->data_ptr<int32_t>();
+      a.node_slot = node_slot->data_ptr<int32_t>();
+      a.num_nodes = (int32_t)node_slot->numel();
+    }
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_rg_hist(a, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
     fdx::rg_hist_cpu(a);
+  }
+}
+
+// Row of every entry of the groups from g0 on (entry-major sparse pass): erow[gbase[g] - gbase[g0] + e].
+void rg_erow(const Tensor& ptr, const Tensor& gbase, int64_t g0, const Tensor& erow) {
+  const auto dev = ptr.device();
+  chk(ptr, dev, at::kInt, "ptr");
+  chk(gbase, dev, at::kLong, "gbase");
+  chk(erow, dev, at::kInt, "erow");
+  FDX_CHECK(ptr.dim() == 2 && gbase.numel() == ptr.size(0) + 1, "ptr [G, N + 1] / gbase [G + 1]");
+  const int64_t G = ptr.size(0), N = ptr.size(1) - 1;
+  FDX_CHECK(g0 >= 0 && g0 <= G, "g0 out of range");
+  const Tensor gb = gbase.cpu();
+  const int64_t* gh = gb.data_ptr<int64_t>();
+  FDX_CHECK(erow.numel() >= gh[G] - gh[g0], "erow must cover the entries from gbase[g0] on");
+  fdx::RgErowArgs a{};
+  a.ptr = reinterpret_cast<const uint32_t*>(ptr.data_ptr<int32_t>());
+  a.gbase = gbase.data_ptr<int64_t>();
+  a.G = (int32_t)G;
+  a.g0 = (int32_t)g0;
+  a.N = N;
+  a.ebase = gh[g0];
+  a.erow = reinterpret_cast<uint32_t*>(erow.data_ptr<int32_t>());
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_rg_erow(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::rg_erow_cpu(a);
   }
 }
 
@@ -1009,7 +1057,14 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rg_build", &rg_build);
   m.def("tree_rg_list", &rg_list);
   m.def("tree_rg_build_csr", &rg_build_csr);
-  m.def("tree_rg_hist", &rg_hist);
+  namespace py = pybind11;
+  m.def("tree_rg_hist", &rg_hist, py::arg("ptr"), py::arg("ent"), py::arg("gbase"), py::arg("gbin"),
+        py::arg("rowdig"), py::arg("np"), py::arg("list"), py::arg("slot_start"), py::arg("listdig"),
+        py::arg("nslots"), py::arg("gmode"), py::arg("wg"), py::arg("slot_node"), py::arg("hist"), py::arg("stride"),
+        py::arg("shard_lo"), py::arg("shard_stride"), py::arg("dbg"), py::arg("erow") = py::none(),
+        py::arg("ebase") = 0, py::arg("row_node") = py::none(), py::arg("node_slot") = py::none(),
+        py::arg("em_min_rows") = 0);
+  m.def("tree_rg_erow", &rg_erow);
   m.def("tree_rf_sample", &rf_sample);
   m.def("tree_rf_compact", &rf_compact);
   m.def("tree_hist_dense", &hist_dense);

@@ -102,6 +102,9 @@ template <class V> void rg_build_csr_cpu(const RgCsrBuildArgs<V>& a);
 int64_t rg_build_csr_waves(int64_t N);
 void launch_rg_list(const RgListArgs& a, hipStream_t s);
 void launch_rg_hist(const RgHistArgs& a, hipStream_t s);
+struct RgErowArgs;
+void launch_rg_erow(const RgErowArgs& a, hipStream_t s);
+void rg_erow_cpu(const RgErowArgs& a);
 void rg_build_cpu(const RgBuildArgs& a, int pass);
 void rg_list_cpu(const RgListArgs& a);
 void rg_hist_cpu(const RgHistArgs& a);

@@ -532,6 +532,73 @@ __device__ __forceinline__ void rg_range_sparse(RgShared<BINS>& sh, const RgHist
   }
 }
 
+// Entry-major pass of a sparse group at a single-slot level (tree.h rg_use_em). The row-list pass
+// spends a lane per row on ~2 entries: its 16 LDS atomics per 64 rows (times the longest row's
+// blocks) were ~55M of the root pass's 88M LDS instructions for 21% of its entries, and the pass
+// is LDS-issue bound (~14 CU-cycles per random ds_add_u64, bench/probes/lds_atomic_probe.hip).
+// Here a lane takes one entry: (local bin, row) from ent / erow, the row's digit word (rows of
+// consecutive entries are consecutive: coalesced), two atomics -- 2 LDS instructions per 64
+// entries. A wave streams kRgEmU entries per lane per step through a 3-stage pipeline: (bin, row)
+// of step j + 2 and the digit words of step j + 1 are in flight while step j's atomics run.
+constexpr int kRgEmU = 8;
+constexpr uint32_t kRgNoRow = 0xffffffffu;
+
+template <int BINS>
+__device__ __forceinline__ void rg_range_em(RgShared<BINS>& sh, const RgHistArgs& a, const uint16_t* ent,
+                                            const uint32_t* erow, int64_t lo, int64_t hi, int wv, int lane, int np,
+                                            int dbg, unsigned long long& sink) {
+  constexpr int64_t kStride = (int64_t)kRgThreads * kRgEmU;
+  auto load_entries = [&](int64_t base, uint32_t* r, uint32_t* b) {
+#pragma unroll
+    for (int u = 0; u < kRgEmU; ++u) {
+      const int64_t e = base + u * 64 + lane;
+      r[u] = e < hi ? erow[e] : kRgNoRow;
+      b[u] = e < hi ? (uint32_t)ent[e] : 0u;
+    }
+  };
+  auto load_digits = [&](uint32_t* r, uint2* d) {
+    if (a.list) {                                  // listed level: keep the rows of slot 0
+#pragma unroll
+      for (int u = 0; u < kRgEmU; ++u)
+        if (r[u] != kRgNoRow && rg_em_row(a, r[u]) < 0) r[u] = kRgNoRow;
+    }
+#pragma unroll
+    for (int u = 0; u < kRgEmU; ++u)
+      d[u] = r[u] != kRgNoRow ? *reinterpret_cast<const uint2*>(a.rowdig + 2 * (int64_t)r[u]) : make_uint2(0u, 0u);
+  };
+  int64_t base = lo + (int64_t)wv * 64 * kRgEmU;
+  if (base >= hi) return;
+  uint32_t r0[kRgEmU], b0[kRgEmU], r1[kRgEmU], b1[kRgEmU];
+  uint2 d0[kRgEmU];
+  load_entries(base, r0, b0);
+  load_entries(base + kStride, r1, b1);
+  load_digits(r0, d0);
+  for (; base < hi; base += kStride) {
+    uint32_t r2[kRgEmU], b2[kRgEmU];
+    uint2 d1[kRgEmU];
+    load_entries(base + 2 * kStride, r2, b2);
+    load_digits(r1, d1);
+#pragma unroll
+    for (int u = 0; u < kRgEmU; ++u) {
+      if (r0[u] == kRgNoRow) continue;
+      if (dbg & 2) {
+        sink += b0[u];
+      } else {
+        atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[b0[u]]), (unsigned long long)rg_q(d0[u].x, np));
+        atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hh[b0[u]]), (unsigned long long)rg_q(d0[u].y, np));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kRgEmU; ++u) {
+      r0[u] = r1[u];
+      b0[u] = b1[u];
+      d0[u] = d1[u];
+      r1[u] = r2[u];
+      b1[u] = b2[u];
+    }
+  }
+}
+
 // Workgroup w: chunk wg_p[w] (of wg_np[w]) of the built-row list, bin group wg_g[w]. Each wave
 // takes batches of 64 listed rows and streams their runs inside the group in aligned 8-entry
 // (16-byte) blocks, adding every entry's row statistics into the LDS histograms; at every slot
@@ -545,9 +612,26 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
   if (w >= a.n_wg) return;
   const int g = a.wg_g[w], p = a.wg_p[w], np_g = a.wg_np[w];
   const int64_t T = a.list ? (int64_t)a.slot_start[a.nslots] : a.N;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (T > 0 && rg_use_em(a, g, T)) {            // chunk p of the group's entries instead
+    const int64_t E = a.ptr[(int64_t)g * (a.N + 1) + a.N];
+    const int64_t e0 = E * p / np_g, e1 = E * (p + 1) / np_g;
+    if (e0 >= e1) return;
+    for (int i = tid; i < BINS; i += kRgThreads) {
+      sh.hg[i] = 0;
+      sh.hh[i] = 0;
+    }
+    __syncthreads();
+    unsigned long long sink = 0;
+    rg_range_em<BINS>(sh, a, a.ent + a.gbase[g], a.erow + (a.gbase[g] - a.ebase), e0, e1, wv, lane, a.np, a.dbg,
+                      sink);
+    if (a.dbg & 2) atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[lane]), sink);
+    __syncthreads();
+    rg_flush<BINS>(a, sh, g, 0, tid);
+    return;
+  }
   const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
   if (a0 >= a1) return;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < BINS; i += kRgThreads) {
     sh.hg[i] = 0;
     sh.hh[i] = 0;
@@ -610,6 +694,23 @@ void launch_rg_list(const RgListArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);
   hipLaunchKernelGGL(rg_list_scan_kernel, dim3((unsigned)a.nslots), dim3(1024), 0, s, a, waves);
   hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 1);
+}
+
+namespace {
+// Thread per (row, group from g0 on): writes the row's index over its run of the group.
+__global__ __launch_bounds__(256) void rg_erow_kernel(RgErowArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= a.N) return;
+  const int g = a.g0 + (int)blockIdx.y;
+  const uint32_t* ptr = a.ptr + (int64_t)g * (a.N + 1);
+  uint32_t* out = a.erow + (a.gbase[g] - a.ebase);
+  for (uint32_t e = ptr[r]; e < ptr[r + 1]; ++e) out[e] = (uint32_t)r;
+}
+}  // namespace
+
+void launch_rg_erow(const RgErowArgs& a, hipStream_t s) {
+  if (a.N <= 0 || a.g0 >= a.G) return;
+  hipLaunchKernelGGL(rg_erow_kernel, dim3((unsigned)((a.N + 255) / 256), (unsigned)(a.G - a.g0)), dim3(256), 0, s, a);
 }
 
 void launch_rg_hist(const RgHistArgs& a, hipStream_t s) {

@@ -226,6 +226,41 @@ struct RgHistArgs {
                                   //   shard_lo[s + 1]) -> s * shard_stride + c - shard_lo[s]
   const int64_t* shard_lo;
   int64_t shard_stride;
+  // Entry-major pass of the sparse groups (gmode 0, entries from ebase on) at single-slot levels:
+  // erow[e - ebase] = row of entry e. The all-rows pass always takes it; a listed level takes it
+  // when it lists >= em_min_rows rows, keeping the entries whose row is in slot 0 (row_node ->
+  // node_slot). nullptr erow: the row-list pass everywhere.
+  const uint32_t* erow;
+  int64_t ebase;
+  const int32_t* row_node;
+  const int32_t* node_slot;
+  int32_t num_nodes;
+  int64_t em_min_rows;
+};
+
+// Whether group g of a pass listing T rows takes the entry-major pass.
+FDX_HD bool rg_use_em(const RgHistArgs& a, int g, int64_t T) {
+  if (a.erow == nullptr || a.gmode[g] != 0 || a.gbase[g] < a.ebase || a.nslots != 1) return false;
+  if (a.list == nullptr) return true;
+  return a.row_node != nullptr && T >= a.em_min_rows;
+}
+
+// Row of an entry-major entry when it counts for slot 0 (-1: its row is not built).
+FDX_HD int64_t rg_em_row(const RgHistArgs& a, uint32_t r) {
+  if (a.list == nullptr) return (int64_t)r;
+  const int32_t n = a.row_node[r];
+  return (n >= 0 && n < a.num_nodes && a.node_slot[n] == 0) ? (int64_t)r : -1;
+}
+
+// erow of the groups from g0 on: erow[gbase[g] - gbase[g0] + e] = r for every entry e of row r.
+struct RgErowArgs {
+  const uint32_t* ptr;            // [G][N + 1]
+  const int64_t* gbase;           // [G + 1] (host copy for the CPU twin, device for the kernel)
+  int32_t G;
+  int32_t g0;
+  int64_t N;
+  int64_t ebase;                  // gbase[g0]
+  uint32_t* erow;
 };
 
 FDX_HD int64_t rg_col_offset(const RgHistArgs& a, int64_t b) {

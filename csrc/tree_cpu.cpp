@@ -231,6 +231,17 @@ void rg_list_cpu(const RgListArgs& a) {
   }
 }
 
+void rg_erow_cpu(const RgErowArgs& a) {
+  for (int g = a.g0; g < a.G; ++g) {
+    const uint32_t* ptr = a.ptr + (int64_t)g * (a.N + 1);
+    uint32_t* out = a.erow + (a.gbase[g] - a.ebase);
+    parallel_for(a.N, 0, 65536, [&](int64_t lo, int64_t hi) {
+      for (int64_t r = lo; r < hi; ++r)
+        for (uint32_t e = ptr[r]; e < ptr[r + 1]; ++e) out[e] = (uint32_t)r;
+    });
+  }
+}
+
 // Host twin of rg_hist_kernel, following the same (group, list chunk, slot) work split, so a host
 // test checks that the plan covers every built row of every group exactly once.
 void rg_hist_cpu(const RgHistArgs& a) {
@@ -238,9 +249,25 @@ void rg_hist_cpu(const RgHistArgs& a) {
   parallel_for((int64_t)a.n_wg, 0, 1, [&](int64_t lo_w, int64_t hi_w) {
     for (int64_t w = lo_w; w < hi_w; ++w) {
       const int g = a.wg_g[w], p = a.wg_p[w], np_g = a.wg_np[w];
-      const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
       const uint32_t* ptr = a.ptr + (int64_t)g * (a.N + 1);
       const uint16_t* ent = a.ent + a.gbase[g];
+      if (T > 0 && rg_use_em(a, g, T)) {         // entry-major: chunk p of the group's entries
+        const int64_t E = ptr[a.N], e0 = E * p / np_g, e1 = E * (p + 1) / np_g;
+        const uint32_t* erow = a.erow + (a.gbase[g] - a.ebase);
+        const int64_t hrow = a.slot_node[0];
+        for (int64_t e = e0; e < e1 && hrow >= 0; ++e) {
+          const int64_t row = rg_em_row(a, erow[e]);
+          if (row < 0) continue;
+          const int32_t col = a.gbin[(int64_t)g * a.gbins + ent[e]];
+          if (col < 0) continue;
+          const int64_t q0 = rg_q(a.rowdig[2 * row], a.np), q1 = rg_q(a.rowdig[2 * row + 1], a.np);
+          int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
+          __atomic_fetch_add(dst, q0, __ATOMIC_RELAXED);
+          __atomic_fetch_add(dst + 1, q1, __ATOMIC_RELAXED);
+        }
+        continue;
+      }
+      const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
       int s = 0;
       if (a.list)
         while (s + 1 < a.nslots && a.slot_start[s + 1] <= a0) ++s;

@@ -156,7 +156,15 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0,
                       {"Fa": Q.Fa, "TB": Q.TB, "nnz": int(Q.csc_row.numel()),
                        "hot": int(Q.hot.size) if Q.hot is not None else 0,
-                       "groups": int(Q._rowgroups.G) if getattr(Q, "_rowgroups", None) is not None else 0})
+                       "groups": int(Q._rowgroups.G) if getattr(Q, "_rowgroups", None) is not None else 0,
+                       "sparse_frac": _sparse_frac(getattr(Q, "_rowgroups", None))})
+
+
+def _sparse_frac(rg) -> float:
+    """Fraction of the row-group entries that carry an entry-major row (utils/memory.py)."""
+    if rg is None or rg.erow is None or not rg.entries:
+        return 0.0
+    return float(rg.group_entries[rg.em_g0:].sum()) / float(rg.entries)
 
 
 def train_margin_logloss(margin: torch.Tensor, y: torch.Tensor) -> float:

@@ -1006,13 +1006,15 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 shard_args = (shards.bin_lo, n_build * shards.Bs) if shards is not None else (None, 0)
                 if d == 0:
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, None, 1, rg.gmode,
-                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG)
+                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG,
+                                   **rg.em_args(False))
                 else:
                     C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
                                    ws.rg_list, ws.rowdig, ws.rg_listdig)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    ws.rg_listdig, n_build, rg.gmode, rg.work(), s2n, hist_target, h_stride,
-                                   *shard_args, RG_DBG)
+                                   *shard_args, RG_DBG,
+                                   **(rg.em_args(True, ws.row_node, st.node_slot) if n_build == 1 else {}))
                 sel_groups, use_dense = [], False
             if sel_groups is None:
                 sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups

@@ -124,13 +124,21 @@ def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.T
 
 RG_BINS = int(os.environ.get("FDX_RG_BINS", 8192))   # local bins per row group: 8192 (1 workgroup per CU) or 4096 (2)
 RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
-RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 2048))   # workgroups per row-group pass
+# workgroups per row-group pass: few and large -- every workgroup flushes up to 2 x 8192 int64
+# global atomics per slot it covers; 10M rows x 40 trees: 7.69 ms per tree at 2048, 6.19 at 512
+# (profiles/r4/gbdt_rg_work_sweep.txt)
+RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 512))
 # work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
 # (ptr, digits) loads whether or not it has entries in the group)
-RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 8.0))
+RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 16.0))
 # groups with at least this many entries per row take lane-balanced batches (csrc/row_kernels.hip
 # rg_batch); sparser ones a lane per row
 RG_BAL_MIN = float(os.environ.get("FDX_RG_BAL_MIN", 8.0))
+# the sparse groups (gmode 0) also get a row per entry (4 B) for the entry-major pass of
+# single-slot levels (csrc/row_kernels.hip rg_range_em); a listed level takes it when it lists at
+# least RG_EM_MIN_FRAC of the rows
+RG_EM = os.environ.get("FDX_RG_EM", "1") == "1"
+RG_EM_MIN_FRAC = float(os.environ.get("FDX_RG_EM_MIN_FRAC", 2.0))
 
 
 class _Ticker:
@@ -214,7 +222,8 @@ class RowGroups:
         gbase = np.concatenate([[0], np.cumsum(pad)]).astype(np.int64)
         self.entries = int(egroup.sum())
         self.group_entries = egroup
-        self.gmode = torch.from_numpy((egroup >= RG_BAL_MIN * max(N, 1)).astype(np.uint8)).to(dev)
+        gmode = (egroup >= RG_BAL_MIN * max(N, 1)).astype(np.uint8)
+        self.gmode = torch.from_numpy(gmode).to(dev)
         self.fgroup_host, self.flocal_host = fgroup, flocal
         fg_t = torch.from_numpy(fgroup).to(dev)
         fl_t = torch.from_numpy(flocal).to(dev)
@@ -246,6 +255,15 @@ class RowGroups:
             cursor = self.ptr[:, :N].clone(memory_format=torch.contiguous_format)   # (a view when G == 1)
             C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 1, None, cursor, self.gbase, self.ent)
             del cursor
+        # entry-major rows of the sparse tail: groups g0.. (every group after the last dense one)
+        dense = np.nonzero(gmode != 0)[0]
+        self.em_g0 = int(dense[-1]) + 1 if dense.size else 0
+        self.ebase = int(gbase[self.em_g0])
+        self.erow = None
+        if RG_EM and self.em_g0 < G and N and int(gbase[-1]) > self.ebase:
+            self.erow = torch.empty(int(gbase[-1]) - self.ebase, dtype=torch.int32, device=dev)
+            C.tree_rg_erow(self.ptr, self.gbase, self.em_g0, self.erow)
+            tick and tick("erow")
         self._work: dict = {}
 
     def work(self, target_wgs: int = 0, alpha: float = None) -> torch.Tensor:
@@ -255,7 +273,8 @@ class RowGroups:
         bench corpus, but every group pays for every listed row)."""
         target_wgs = target_wgs or RG_TARGET_WGS
         alpha = RG_ALPHA if alpha is None else alpha
-        t = self._work.get((target_wgs, alpha))
+        key = (target_wgs, alpha)
+        t = self._work.get(key)
         if t is None:
             e = self.group_entries.astype(np.float64) + alpha * self.n_rows
             npg = np.maximum(1, np.rint(target_wgs * e / max(e.sum(), 1.0))).astype(np.int64)
@@ -263,12 +282,23 @@ class RowGroups:
             p = np.arange(int(npg.sum())) - np.repeat(np.cumsum(npg) - npg, npg)
             tab = np.stack([g, p, np.repeat(npg, npg)]).astype(np.int32)
             assert (tab[0] < self.G).all() and (tab[1] < tab[2]).all()
-            t = self._work[(target_wgs, alpha)] = torch.from_numpy(tab).to(self.gbase.device)
+            t = self._work[key] = torch.from_numpy(tab).to(self.gbase.device)
         return t
 
     @property
     def nbytes(self) -> int:
-        return int(self.ptr.numel() * 4 + self.ent.numel() * 2 + self.gbin.numel() * 4)
+        em = self.erow.numel() * 4 if self.erow is not None else 0
+        return int(self.ptr.numel() * 4 + self.ent.numel() * 2 + self.gbin.numel() * 4 + em)
+
+    def em_args(self, list_rows: bool, row_node=None, node_slot=None) -> dict:
+        """Keyword arguments of tree_rg_hist for the entry-major sparse pass (empty: off)."""
+        if self.erow is None:
+            return {}
+        kw = dict(erow=self.erow, ebase=self.ebase)
+        if list_rows:
+            kw.update(row_node=row_node, node_slot=node_slot,
+                      em_min_rows=max(1, int(RG_EM_MIN_FRAC * self.n_rows)))
+        return kw
 
 
 @dataclass

@@ -17,7 +17,9 @@ bench/probes/mem_probe.py (profiles/r4/mem_*.jsonl):
    or, at the end, the merged feature order (another 5 B/e) while the blocks are still held;
 2. training (GBDT on the row-group engine; RF adds its CSC items, 5 B/e, on its own peak):
      * the CSR (8 B/e + slack), the feature order shared as the CSC (5 B/e of active entries),
-       one uint8 bin per entry, the row-group entries (uint16: 2 B/e);
+       one uint8 bin per entry, the row-group entries (uint16: 2 B/e), and the row of every
+       entry of the sparse groups (uint32, the entry-major root pass: 4 B per sparse entry, a
+       fraction ``sparse_frac`` of the entries: ~21% on the bench corpus);
      * per row: pointer + labels (16 B), the row-group run starts (4 B per group), one byte per
        dense hot feature, the level loop's row state (digits, node, slot, list, margin, g, h,
        labels: 53 B);
@@ -40,6 +42,8 @@ CSR_SLACK = 1.05            # featurize_shard's capacity estimate from the first
 ORDER_BYTES = 5.0           # feature order / CSC: int32 row + uint8 count per entry
 BIN_BYTES = 1.0             # uint8 bin per active entry
 RG_ENTRY_BYTES = 2.0        # row-group engine: uint16 local bin per entry
+RG_EROW_BYTES = 4.0         # uint32 row per entry of the sparse groups (entry-major pass)
+DEFAULT_SPARSE_FRAC = 0.21  # entries outside the dense row group (bench corpus: 205M of 968M)
 ROW_BYTES = 16.0            # row pointer (int64) + labels (fp64) of the featurized shard
 LEVEL_ROW_BYTES = 53.0      # level-loop row state (grower.Workspace + margins, g, h, labels)
 CHUNK_TEXT_BYTES = 2.0      # two device staging buffers of one chunk's raw text
@@ -69,9 +73,10 @@ def featurize_bytes(rows: int, nnz: int, text_bytes_per_row: float = DEFAULT_BYT
 
 
 def training_bytes(rows: int, nnz: int, hot_features: int = DEFAULT_HOT_FEATURES, total_bins: int = 0,
-                   built_nodes: int = DEFAULT_BUILT_NODES, groups: int = DEFAULT_GROUPS) -> float:
+                   built_nodes: int = DEFAULT_BUILT_NODES, groups: int = DEFAULT_GROUPS,
+                   sparse_frac: float = DEFAULT_SPARSE_FRAC) -> float:
     """Peak bytes of training (GBDT, row-group engine) on ``rows`` rows with ``nnz`` entries."""
-    per_entry = CSR_BYTES * CSR_SLACK + ORDER_BYTES + BIN_BYTES + RG_ENTRY_BYTES
+    per_entry = CSR_BYTES * CSR_SLACK + ORDER_BYTES + BIN_BYTES + RG_ENTRY_BYTES + RG_EROW_BYTES * sparse_frac
     per_row = ROW_BYTES + 4.0 * groups + hot_features + LEVEL_ROW_BYTES
     return per_entry * nnz + per_row * rows + LEVEL_HIST_BYTES * total_bins * built_nodes * 2
 

@@ -107,5 +107,6 @@ def test_bench_gbdt_phase_peak_matches_the_hbm_model():
     peak = torch.cuda.max_memory_allocated(dev) - base
     model = memory.pipeline_bytes(rows, int(idx.numel()), hot_features=res.shape["hot"],
                                   groups=res.shape["groups"] or memory.DEFAULT_GROUPS,
+                                  sparse_frac=res.shape["sparse_frac"],
                                   text_bytes_per_row=text_bytes / rows, chunk_rows=chunk)
     assert 0.85 <= peak / model <= 1.15, (peak / 2 ** 30, model / 2 ** 30)

@@ -50,9 +50,10 @@ def gmode(rg):
 
 
 def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None, np_=4, P=16, max_groups=None,
-                dbg=0, bins=8192):
+                dbg=0, bins=8192, em=False):
     """Histograms of node slots 0..nslots-1 through tree_rg_list + tree_rg_hist, plus q0, q1 and Q;
-    ``shards`` = (S, bin_lo) writes the shard-major DP layout (returned unpacked)."""
+    ``shards`` = (S, bin_lo) writes the shard-major DP layout (returned unpacked); ``em`` passes
+    the entry-major sparse pass's arguments (taken at single-slot levels, whatever the list size)."""
     C = native.lib()
     n = row_node_np.shape[0]
     Q = quantize(vc.to(dev), max_bins=max_bins, **QKW)
@@ -60,27 +61,35 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
     _quant(ws, n, dev, np_)
     rg = RowGroups(Q, max_groups=max_groups, bins=bins)
     list_ = start = ldig = None
+    node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
+    node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
+    node_slot = node_slot.to(dev)
+    row_node = torch.from_numpy(row_node_np).to(dev)
     if not root:
-        node_slot = torch.full((nslots + 2,), -1, dtype=torch.int32)
-        node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
         list_ = torch.empty(n, dtype=torch.int32, device=dev)
         start = torch.zeros(nslots + 1, dtype=torch.int32, device=dev)
         work = torch.zeros(nslots * (2 + n // 2048 + 1), dtype=torch.int32, device=dev)
         ldig = torch.empty((n, 2), dtype=torch.int32, device=dev)
-        C.tree_rg_list(torch.from_numpy(row_node_np).to(dev), node_slot.to(dev), None, n, nslots, work, start, list_,
-                       ws.rowdig, ldig)
+        C.tree_rg_list(row_node, node_slot, None, n, nslots, work, start, list_, ws.rowdig, ldig)
     s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
     q0, q1 = _q_of(ws, np_)
+    kw = {}
+    if em:
+        assert rg.erow is not None
+        kw = rg.em_args(not root, row_node, node_slot)
+        if not root:
+            kw["em_min_rows"] = 1
     if shards is None:
         hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
         C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, ldig, nslots, gmode(rg),
-                       rg.work(P), s2n, hist, Q.TB, None, 0, dbg)
+                       rg.work(P), s2n, hist, Q.TB, None, 0, dbg, **kw)
         return hist.cpu().numpy(), q0, q1, Q, rg
     S, lo = shards
     Bs = int(np.diff(lo).max())
     buf = torch.zeros((S, nslots, Bs, 2), dtype=torch.int64, device=dev)
     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, ldig, nslots, gmode(rg),
-                   rg.work(P), s2n, buf.view(S * nslots, Bs, 2), Bs, torch.from_numpy(lo).to(dev), nslots * Bs, dbg)
+                   rg.work(P), s2n, buf.view(S * nslots, Bs, 2), Bs, torch.from_numpy(lo).to(dev), nslots * Bs, dbg,
+                   **kw)
     b = buf.cpu().numpy()
     hist = np.concatenate([b[k, :, : lo[k + 1] - lo[k]] for k in range(S)], axis=1)
     return hist, q0, q1, Q, rg
@@ -277,6 +286,24 @@ def _list_check(dev, n, ns, seed):
     return st
 
 
+@pytest.mark.parametrize("root,np_,bins", [(True, 4, 8192), (False, 4, 8192), (False, 1, 4096), (True, 4, 4096)])
+def test_row_group_entry_major_pass_equals_host_reference(root, np_, bins):
+    """The entry-major pass of the sparse groups (a lane per entry, its row from erow, the row's
+    slot from row_node at a listed level) gives the exact sums of the row-list pass."""
+    rng = np.random.default_rng(31)
+    n = 6000
+    vc = _wide(n, 300, 31, dmax=0.6)
+    row_node = np.zeros(n, np.int32) if root else rng.integers(-1, 3, n).astype(np.int32)
+    hist, q0, q1, Q, rg = _rg_hist_on("cpu", vc, 100, 1, row_node, root, np_=np_, bins=bins, em=True)
+    assert rg.erow is not None and rg.em_g0 < rg.G           # sparse groups take the pass
+    np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, 1, q0, q1))
+    # erow: the row of every entry of the sparse tail
+    ptr, gb, erow = rg.ptr.numpy(), rg.gbase.numpy(), rg.erow.numpy()
+    for g in range(rg.em_g0, rg.G):
+        want = np.repeat(np.arange(n), np.diff(ptr[g]))
+        np.testing.assert_array_equal(erow[gb[g] - rg.ebase: gb[g] - rg.ebase + ptr[g, -1]], want)
+
+
 def test_row_group_list_groups_built_rows_by_slot():
     _list_check("cpu", 20000, 7, 9)
 
@@ -320,12 +347,16 @@ def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot, bins)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nslots,root,bins", [(1, True, 8192), (2, False, 4096), (5, False, 8192), (32, False, 4096)])
+@pytest.mark.parametrize("nslots,root,bins,em", [(1, True, 8192, False), (2, False, 4096, False),
+                                                 (5, False, 8192, False), (32, False, 4096, False),
+                                                 (1, True, 8192, True), (1, False, 8192, True),
+                                                 (1, False, 4096, True)])
 @pytest.mark.parametrize("sharded", [False, True])
 @pytest.mark.parametrize("mode", [None, 0, 1])
-def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded, mode, monkeypatch):
-    """The row-group pass (LDS int64 atomics, 16-B row-run loads, per-slot flushes) equals the
-    host's exact int64 sums bit for bit, plain and in the shard-major DP layout."""
+def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, em, sharded, mode, monkeypatch):
+    """The row-group pass (LDS int64 atomics, 16-B row-run loads, per-slot flushes; the
+    entry-major pass of the sparse groups with ``em``) equals the host's exact int64 sums bit for
+    bit, plain and in the shard-major DP layout."""
     rng = np.random.default_rng(20 + nslots)
     n = 30000
     vc = _wide(n, 400, 20 + nslots, hi=300)
@@ -337,7 +368,7 @@ def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, sharded
         shards = (3, lo)
     monkeypatch.setitem(MODE, "gmode", mode)
     a, *_ = _rg_hist_on("cpu", vc, 200, nslots, row_node, root, shards, P=24, bins=bins)
-    b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24, bins=bins)
+    b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24, bins=bins, em=em)
     assert rg.G >= 2
     np.testing.assert_array_equal(a, b)
 
