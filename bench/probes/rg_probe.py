@@ -120,19 +120,22 @@ def main():
             ref[:, zb] = 0
         s2n = torch.arange(ns, dtype=torch.int32, device=dev)
         list_ms = 0.0
-        rn_d = ns_d = None
+        rn_d = ns_d = emdig = None
         if not root:
             rn_d = torch.from_numpy(rn).to(dev)
             ns_d = node_slot.to(dev)
-            list_ms = timed(lambda: C.tree_rg_list(rn_d, ns_d, None, n, ns, work, start, lst, ws.rowdig, ldig))
+            # one slot: also every row's digit words masked to it (the entry-major listed pass)
+            emdig = torch.empty((n, 2), dtype=torch.int32, device=dev) if ns == 1 else None
+            list_ms = timed(lambda: C.tree_rg_list(rn_d, ns_d, None, n, ns, work, start, lst, ws.rowdig, ldig,
+                                                   emdig))
         for B, wgs, alpha, dbg, mode, em in [(B, int(w), float(al), int(db), md, int(e)) for B in rgs
                                              for w in args.wgs.split(",") for al in args.alphas.split(",")
                                              for db in args.dbg.split(",") for md in args.modes.split(",")
                                              for e in args.em.split(",")]:
             if True:
                 rg = rgs[B]
-                kw = rg.em_args(not root, rn_d, ns_d) if em else {}
-                if kw and not root:
+                kw = rg.em_args(emdig) if em else {}
+                if kw and emdig is not None:
                     kw["em_min_rows"] = 1
                 gm = rg.gmode if mode == "auto" else torch.full_like(rg.gmode, int(mode))
                 hist = torch.zeros((ns, Q.TB, 2), dtype=torch.int64, device=dev)

@@ -418,7 +418,8 @@ void rg_build(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& colptr
 template <class V>
 void rg_build_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& counts, const Tensor& remap,
                     int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, const Tensor& ptr,
-                    const Tensor& gbase, const Tensor& ent, const Tensor& work) {
+                    const Tensor& gbase, const Tensor& ent, const Tensor& work, const optional<Tensor>& erow,
+                    int64_t em_g0, int64_t ebase) {
   const auto dev = indptr.device();
   fdx::RgCsrBuildArgs<V> a{};
   a.indptr = indptr.data_ptr<int64_t>();
@@ -434,6 +435,11 @@ void rg_build_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& count
   a.gbase = gbase.data_ptr<int64_t>();
   a.ent = reinterpret_cast<uint16_t*>(ent.data_ptr<int16_t>());
   a.wave_base = reinterpret_cast<uint32_t*>(work.data_ptr<int32_t>());
+  if (erow && erow->defined()) {
+    a.erow = reinterpret_cast<uint32_t*>(erow->data_ptr<int32_t>());
+    a.em_g0 = (int32_t)em_g0;
+    a.ebase = ebase;
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_rg_build_csr<V>(a, stream(dev));
@@ -445,9 +451,15 @@ void rg_build_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& count
 
 void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts, const Tensor& remap,
                   int64_t max_bin, const Tensor& fgroup, const Tensor& flocal, const Tensor& ptr,
-                  const Tensor& gbase, const Tensor& ent, const Tensor& work) {
+                  const Tensor& gbase, const Tensor& ent, const Tensor& work, const optional<Tensor>& erow,
+                  int64_t em_g0, int64_t ebase) {
   const auto dev = indptr.device();
   chk(indptr, dev, at::kLong, "indptr");
+  if (erow && erow->defined()) {
+    chk(*erow, dev, at::kInt, "erow");
+    FDX_CHECK(em_g0 >= 0 && em_g0 <= ptr.size(0) && ebase >= 0 && ebase <= ent.numel() &&
+                  erow->numel() >= ent.numel() - ebase, "erow must cover the entries from ebase on");
+  }
   chk(idx, dev, at::kInt, "idx");
   chk(remap, dev, at::kInt, "remap");
   chk(fgroup, dev, at::kInt, "fgroup");
@@ -463,9 +475,12 @@ void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts,
   FDX_CHECK(fgroup.numel() == flocal.numel(), "fgroup / flocal");
   FDX_CHECK(work.numel() >= ptr.size(0) * fdx::rg_build_csr_waves(indptr.numel() - 1), "work too small");
   switch (counts.scalar_type()) {
-    case at::kFloat: rg_build_csr_t<float>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work); break;
-    case at::kDouble: rg_build_csr_t<double>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work); break;
-    case at::kInt: rg_build_csr_t<int32_t>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work); break;
+    case at::kFloat: rg_build_csr_t<float>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work, erow,
+                                               em_g0, ebase); break;
+    case at::kDouble: rg_build_csr_t<double>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work, erow,
+                                               em_g0, ebase); break;
+    case at::kInt: rg_build_csr_t<int32_t>(indptr, idx, counts, remap, max_bin, fgroup, flocal, ptr, gbase, ent, work, erow,
+                                               em_g0, ebase); break;
     default: FDX_CHECK(false, "counts must be float32, float64 or int32");
   }
 }
@@ -476,7 +491,7 @@ void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts,
 // words of the listed rows by list position.
 void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot, const optional<Tensor>& slot8,
              int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start, const Tensor& list,
-             const optional<Tensor>& rowdig, const optional<Tensor>& listdig) {
+             const optional<Tensor>& rowdig, const optional<Tensor>& listdig, const optional<Tensor>& masked) {
   const auto dev = list.device();
   chk(work, dev, at::kInt, "work");
   chk(slot_start, dev, at::kInt, "slot_start");
@@ -514,6 +529,12 @@ void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot
     a.rowdig = reinterpret_cast<const uint32_t*>(rowdig->data_ptr<int32_t>());
     a.listdig = reinterpret_cast<uint32_t*>(listdig->data_ptr<int32_t>());
   }
+  if (masked && masked->defined()) {
+    FDX_CHECK(rowdig.has_value() && nslots == 1, "masked digit words need rowdig and one slot");
+    chk(*masked, dev, at::kInt, "masked");
+    FDX_CHECK(masked->numel() >= 2 * N, "masked must be [N, 2]");
+    a.masked = reinterpret_cast<uint32_t*>(masked->data_ptr<int32_t>());
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_rg_list(a, stream(dev));
@@ -530,7 +551,7 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
              const optional<Tensor>& listdig, int64_t nslots, const Tensor& gmode, const Tensor& wg,
              const Tensor& slot_node, const Tensor& hist, int64_t stride, const optional<Tensor>& shard_lo,
              int64_t shard_stride, int64_t dbg, const optional<Tensor>& erow, int64_t ebase,
-             const optional<Tensor>& row_node, const optional<Tensor>& node_slot, int64_t em_min_rows) {
+             const optional<Tensor>& emdig, int64_t em_min_rows) {
   const auto dev = ptr.device();
   chk(ptr, dev, at::kInt, "ptr");
   chk(gbase, dev, at::kLong, "gbase");
@@ -602,14 +623,10 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
     a.erow = reinterpret_cast<const uint32_t*>(erow->data_ptr<int32_t>());
     a.ebase = ebase;
     a.em_min_rows = em_min_rows;
-    if (list) {
-      FDX_CHECK(row_node.has_value() && node_slot.has_value(), "a listed entry-major pass needs row_node / node_slot");
-      chk(*row_node, dev, at::kInt, "row_node");
-      chk(*node_slot, dev, at::kInt, "node_slot");
-      FDX_CHECK(row_node->numel() >= N, "row_node must cover the rows");
-      a.row_node = row_node->data_ptr<int32_t>();
-      a.node_slot = node_slot->data_ptr<int32_t>();
-      a.num_nodes = (int32_t)node_slot->numel();
+    if (list && emdig && emdig->defined()) {     // (without emdig a listed level keeps the row lists)
+      chk(*emdig, dev, at::kInt, "emdig");
+      FDX_CHECK(emdig->numel() >= 2 * N, "emdig must be [N, 2]");
+      a.emdig = reinterpret_cast<const uint32_t*>(emdig->data_ptr<int32_t>());
     }
   }
   if (dev.is_cuda()) {
@@ -1045,6 +1062,7 @@ void leaf_update(const Tensor& margin, const Tensor& row_node, const Tensor& nod
 }  // namespace
 
 void register_tree_ops(pybind11::module& m) {
+  namespace py = pybind11;
   m.def("tree_quant_max", &quant_max);
   m.def("tree_quant", &quant);
   m.def("tree_slot8", &slot8);
@@ -1055,15 +1073,17 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_hist_sampled", &hist_sampled);
   m.def("tree_slot_pack", &slot_pack);
   m.def("tree_rg_build", &rg_build);
-  m.def("tree_rg_list", &rg_list);
-  m.def("tree_rg_build_csr", &rg_build_csr);
-  namespace py = pybind11;
+  m.def("tree_rg_list", &rg_list, py::arg("row_node"), py::arg("node_slot"), py::arg("slot8"), py::arg("N"),
+        py::arg("nslots"), py::arg("work"), py::arg("slot_start"), py::arg("list"), py::arg("rowdig"),
+        py::arg("listdig"), py::arg("masked") = py::none());
+  m.def("tree_rg_build_csr", &rg_build_csr, py::arg("indptr"), py::arg("idx"), py::arg("counts"), py::arg("remap"),
+        py::arg("max_bin"), py::arg("fgroup"), py::arg("flocal"), py::arg("ptr"), py::arg("gbase"), py::arg("ent"),
+        py::arg("work"), py::arg("erow") = py::none(), py::arg("em_g0") = 0, py::arg("ebase") = 0);
   m.def("tree_rg_hist", &rg_hist, py::arg("ptr"), py::arg("ent"), py::arg("gbase"), py::arg("gbin"),
         py::arg("rowdig"), py::arg("np"), py::arg("list"), py::arg("slot_start"), py::arg("listdig"),
         py::arg("nslots"), py::arg("gmode"), py::arg("wg"), py::arg("slot_node"), py::arg("hist"), py::arg("stride"),
         py::arg("shard_lo"), py::arg("shard_stride"), py::arg("dbg"), py::arg("erow") = py::none(),
-        py::arg("ebase") = 0, py::arg("row_node") = py::none(), py::arg("node_slot") = py::none(),
-        py::arg("em_min_rows") = 0);
+        py::arg("ebase") = 0, py::arg("emdig") = py::none(), py::arg("em_min_rows") = 0);
   m.def("tree_rg_erow", &rg_erow);
   m.def("tree_rf_sample", &rf_sample);
   m.def("tree_rf_compact", &rf_compact);

@@ -116,7 +116,11 @@ __global__ __launch_bounds__(256) void rg_build_csr_kernel(RgCsrBuildArgs<V> a, 
         const int owner = gs & 63;
         if (pass == 1) {
           const uint32_t base = gs < 64 ? __shfl(run0, owner, 64) : __shfl(run1, owner, 64);
-          if (g == gs) a.ent[a.gbase[gs] + base + __popcll(m & lt)] = (uint16_t)loc;
+          if (g == gs) {
+            const int64_t pos = a.gbase[gs] + base + __popcll(m & lt);
+            a.ent[pos] = (uint16_t)loc;
+            if (a.erow != nullptr && gs >= a.em_g0) a.erow[pos - a.ebase] = (uint32_t)r;
+          }
         }
         if (lane == owner) {
           if (gs < 64) run0 += __popcll(m);
@@ -225,6 +229,13 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
       d[k] = (a.listdig && sl[k] < (uint32_t)a.nslots) ? *reinterpret_cast<const uint2*>(a.rowdig + 2 * r)
                                                          : make_uint2(0u, 0u);
     }
+    if (a.masked) {                              // (nslots == 1: the listed rows are slot 0's)
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const int64_t r = r0 + 64 * (k0 + k) + lane;
+        if (r < a.N) *reinterpret_cast<uint2*>(a.masked + 2 * r) = sl[k] == 0u ? d[k] : make_uint2(0u, 0u);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       const int64_t r = r0 + 64 * (k0 + k) + lane;
@@ -286,7 +297,7 @@ struct RgShared {
 
 template <int BINS>
 __device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS>& sh, int g, int s, int tid) {
-  const int64_t hrow = a.slot_node[s];
+  const int64_t hrow = (a.dbg & 4) ? -1 : a.slot_node[s];          // dbg bit 2: no flush (timing)
   const int32_t* gbin = a.gbin + (int64_t)g * a.gbins;
   for (int i = tid; i < BINS; i += kRgThreads) {
     const int64_t v0 = sh.hg[i], v1 = sh.hh[i];
@@ -556,15 +567,11 @@ __device__ __forceinline__ void rg_range_em(RgShared<BINS>& sh, const RgHistArgs
       b[u] = e < hi ? (uint32_t)ent[e] : 0u;
     }
   };
+  const uint32_t* dig = rg_em_digits(a);          // (a listed level: zero outside slot 0)
   auto load_digits = [&](uint32_t* r, uint2* d) {
-    if (a.list) {                                  // listed level: keep the rows of slot 0
-#pragma unroll
-      for (int u = 0; u < kRgEmU; ++u)
-        if (r[u] != kRgNoRow && rg_em_row(a, r[u]) < 0) r[u] = kRgNoRow;
-    }
 #pragma unroll
     for (int u = 0; u < kRgEmU; ++u)
-      d[u] = r[u] != kRgNoRow ? *reinterpret_cast<const uint2*>(a.rowdig + 2 * (int64_t)r[u]) : make_uint2(0u, 0u);
+      d[u] = r[u] != kRgNoRow ? *reinterpret_cast<const uint2*>(dig + 2 * (int64_t)r[u]) : make_uint2(0u, 0u);
   };
   int64_t base = lo + (int64_t)wv * 64 * kRgEmU;
   if (base >= hi) return;
@@ -580,7 +587,7 @@ __device__ __forceinline__ void rg_range_em(RgShared<BINS>& sh, const RgHistArgs
     load_digits(r1, d1);
 #pragma unroll
     for (int u = 0; u < kRgEmU; ++u) {
-      if (r0[u] == kRgNoRow) continue;
+      if (r0[u] == kRgNoRow || (d0[u].x | d0[u].y) == 0u) continue;
       if (dbg & 2) {
         sink += b0[u];
       } else {

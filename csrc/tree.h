@@ -165,6 +165,9 @@ struct RgCsrBuildArgs {
   const int64_t* gbase;
   uint16_t* ent;                  // out
   uint32_t* wave_base;            // [ceil(N / 64)][G] scratch: per-wave group totals, then bases
+  uint32_t* erow;                 // optional out: erow[gbase[g] - ebase + k] = row of entry k of
+  int32_t em_g0;                  //   group g >= em_g0 (the entry-major rows, RgHistArgs::erow)
+  int64_t ebase;
 };
 
 // Built rows of a level grouped by slot. The slot of row r is node_slot[row_node[r]] when
@@ -185,6 +188,8 @@ struct RgListArgs {
                                   //   wave's chunk of rows
   const uint32_t* rowdig;         // optional [N * 2]: pass 1 also writes
   uint32_t* listdig;              //   listdig[2 pos + k] = rowdig[2 list[pos] + k] (coalesced in the pass)
+  uint32_t* masked;               // optional [N * 2] (nslots == 1, with rowdig): pass 1 writes every
+                                  //   row's digit words, zero outside slot 0 (the entry-major pass)
 };
 
 FDX_HD uint32_t rg_slot_of(const RgListArgs& a, int64_t r) {
@@ -215,8 +220,8 @@ struct RgHistArgs {
   const int32_t* wg_p;
   const int32_t* wg_np;
   int32_t n_wg;
-  // diagnostics (bench/probes/rg_probe.py): bit 1 replaces the LDS atomics by a register sum
-  // (wrong sums)
+  // diagnostics (bench/probes/rg_probe.py): bit 1 replaces the LDS atomics by a register sum,
+  // bit 2 skips the flushes (wrong sums)
   int32_t dbg;
   // output: hist[(slot_node[s] * hist_stride + off(column)) * 2 + stat] +=
   const int32_t* slot_node;
@@ -227,14 +232,12 @@ struct RgHistArgs {
   const int64_t* shard_lo;
   int64_t shard_stride;
   // Entry-major pass of the sparse groups (gmode 0, entries from ebase on) at single-slot levels:
-  // erow[e - ebase] = row of entry e. The all-rows pass always takes it; a listed level takes it
-  // when it lists >= em_min_rows rows, keeping the entries whose row is in slot 0 (row_node ->
-  // node_slot). nullptr erow: the row-list pass everywhere.
+  // erow[e - ebase] = row of entry e. The all-rows pass always takes it (digits from rowdig); a
+  // listed level takes it when it lists >= em_min_rows rows, with emdig = every row's digit words
+  // zeroed outside slot 0 (RgListArgs::masked). nullptr erow: the row-list pass everywhere.
   const uint32_t* erow;
   int64_t ebase;
-  const int32_t* row_node;
-  const int32_t* node_slot;
-  int32_t num_nodes;
+  const uint32_t* emdig;
   int64_t em_min_rows;
 };
 
@@ -242,15 +245,11 @@ struct RgHistArgs {
 FDX_HD bool rg_use_em(const RgHistArgs& a, int g, int64_t T) {
   if (a.erow == nullptr || a.gmode[g] != 0 || a.gbase[g] < a.ebase || a.nslots != 1) return false;
   if (a.list == nullptr) return true;
-  return a.row_node != nullptr && T >= a.em_min_rows;
+  return a.emdig != nullptr && T >= a.em_min_rows;
 }
 
-// Row of an entry-major entry when it counts for slot 0 (-1: its row is not built).
-FDX_HD int64_t rg_em_row(const RgHistArgs& a, uint32_t r) {
-  if (a.list == nullptr) return (int64_t)r;
-  const int32_t n = a.row_node[r];
-  return (n >= 0 && n < a.num_nodes && a.node_slot[n] == 0) ? (int64_t)r : -1;
-}
+// Digit words of the entry-major pass, by row.
+FDX_HD const uint32_t* rg_em_digits(const RgHistArgs& a) { return a.list ? a.emdig : a.rowdig; }
 
 // erow of the groups from g0 on: erow[gbase[g] - gbase[g0] + e] = r for every entry e of row r.
 struct RgErowArgs {

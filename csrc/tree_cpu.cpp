@@ -199,7 +199,9 @@ void rg_build_csr_cpu(const RgCsrBuildArgs<V>& a) {
         if (fa < 0) continue;
         const int32_t g = a.fgroup[fa];
         if (g < 0) continue;
-        a.ent[a.gbase[g] + c[(size_t)g]++] = (uint16_t)(a.flocal[fa] + bin_of(a.counts[e]));
+        const int64_t pos = a.gbase[g] + c[(size_t)g]++;
+        a.ent[pos] = (uint16_t)(a.flocal[fa] + bin_of(a.counts[e]));
+        if (a.erow != nullptr && g >= a.em_g0) a.erow[pos - a.ebase] = (uint32_t)r;
       }
     }
   });
@@ -221,6 +223,10 @@ void rg_list_cpu(const RgListArgs& a) {
   for (int s = 0; s < a.nslots; ++s) a.slot_count[s] = (int32_t)(cnt[s + 1] - cnt[s]);
   for (int64_t r = 0; r < a.N; ++r) {
     const uint32_t s = rg_slot_of(a, r);
+    if (a.masked) {
+      a.masked[2 * r] = s == 0u ? a.rowdig[2 * r] : 0u;
+      a.masked[2 * r + 1] = s == 0u ? a.rowdig[2 * r + 1] : 0u;
+    }
     if (s >= (uint32_t)a.nslots) continue;
     const int64_t pos = cnt[s]++;
     a.list[pos] = (int32_t)r;
@@ -256,11 +262,11 @@ void rg_hist_cpu(const RgHistArgs& a) {
         const uint32_t* erow = a.erow + (a.gbase[g] - a.ebase);
         const int64_t hrow = a.slot_node[0];
         for (int64_t e = e0; e < e1 && hrow >= 0; ++e) {
-          const int64_t row = rg_em_row(a, erow[e]);
-          if (row < 0) continue;
+          const int64_t row = erow[e];
+          const uint32_t* dig = rg_em_digits(a) + 2 * row;     // (zero outside slot 0 when listed)
           const int32_t col = a.gbin[(int64_t)g * a.gbins + ent[e]];
           if (col < 0) continue;
-          const int64_t q0 = rg_q(a.rowdig[2 * row], a.np), q1 = rg_q(a.rowdig[2 * row + 1], a.np);
+          const int64_t q0 = rg_q(dig[0], a.np), q1 = rg_q(dig[1], a.np);
           int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
           __atomic_fetch_add(dst, q0, __ATOMIC_RELAXED);
           __atomic_fetch_add(dst + 1, q1, __ATOMIC_RELAXED);

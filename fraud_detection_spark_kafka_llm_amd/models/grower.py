@@ -32,6 +32,7 @@ import torch
 from ..ml.tree_model import Tree
 from ..ops import native
 from ..utils import tracing
+from . import quantize as qmod
 from .quantize import Quantized
 
 NEG_INF = float("-inf")
@@ -198,6 +199,12 @@ class Workspace:
             self.rg_work = torch.zeros(64 * (2 + nw), dtype=torch.int32, device=self.dev)
             self.rg_listdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
         return rg
+
+    def rg_emdig(self) -> torch.Tensor:
+        """[N, 2] digit words zeroed outside the one built node (entry-major listed pass)."""
+        if getattr(self, "_rg_emdig", None) is None:
+            self._rg_emdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
+        return self._rg_emdig
 
     def rowpack(self) -> torch.Tensor:
         """[N] int32 packed row state of the sampled (RF) passes: slot | class-count digits << 8."""
@@ -1006,15 +1013,17 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 shard_args = (shards.bin_lo, n_build * shards.Bs) if shards is not None else (None, 0)
                 if d == 0:
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, None, 1, rg.gmode,
-                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG,
-                                   **rg.em_args(False))
+                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG, **rg.em_args())
                 else:
+                    # one built node: every row's digit words zeroed outside it, for the
+                    # entry-major pass of the sparse groups (taken when the node is large)
+                    emdig = ws.rg_emdig() if (n_build == 1 and rg.erow is not None and qmod.RG_EM_MIN_FRAC <= 1.0) \
+                        else None
                     C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
-                                   ws.rg_list, ws.rowdig, ws.rg_listdig)
+                                   ws.rg_list, ws.rowdig, ws.rg_listdig, emdig)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    ws.rg_listdig, n_build, rg.gmode, rg.work(), s2n, hist_target, h_stride,
-                                   *shard_args, RG_DBG,
-                                   **(rg.em_args(True, ws.row_node, st.node_slot) if n_build == 1 else {}))
+                                   *shard_args, RG_DBG, **(rg.em_args(emdig) if emdig is not None else {}))
                 sel_groups, use_dense = [], False
             if sel_groups is None:
                 sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups

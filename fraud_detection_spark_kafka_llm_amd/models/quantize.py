@@ -136,9 +136,10 @@ RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 16.0))
 RG_BAL_MIN = float(os.environ.get("FDX_RG_BAL_MIN", 8.0))
 # the sparse groups (gmode 0) also get a row per entry (4 B) for the entry-major pass of
 # single-slot levels (csrc/row_kernels.hip rg_range_em); a listed level takes it when it lists at
-# least RG_EM_MIN_FRAC of the rows
+# least RG_EM_MIN_FRAC of the rows (> 1: never). Bench corpus, half the rows listed: sparse groups
+# 0.75 -> 0.48 ms; GBDT 10M x 40 trees 6.35 -> 6.28-6.32 ms per tree (profiles/r4)
 RG_EM = os.environ.get("FDX_RG_EM", "1") == "1"
-RG_EM_MIN_FRAC = float(os.environ.get("FDX_RG_EM_MIN_FRAC", 2.0))
+RG_EM_MIN_FRAC = float(os.environ.get("FDX_RG_EM_MIN_FRAC", 0.3))
 
 
 class _Ticker:
@@ -203,6 +204,7 @@ class RowGroups:
             flocal[fs] = (cum[i:j] - cum[i]).astype(np.int32)
             starts.append(i)
             i = j
+        tick and tick("pack")
         self.complete = i >= order.size
         self.G = G = max(1, len(starts))
         self.n_rows = N = Q.n_rows
@@ -214,6 +216,7 @@ class RowGroups:
             f_rep = np.repeat(sel, rep)
             k = np.arange(int(rep.sum()), dtype=np.int64) - np.repeat(np.cumsum(rep) - rep, rep)
             gbin[fgroup[f_rep], flocal[f_rep] + k] = (boff[f_rep] + k).astype(np.int32)
+        tick and tick("gbin")
         egroup = np.zeros(G, dtype=np.int64)
         np.add.at(egroup, fgroup[sel], cnt[sel])
         if int(egroup.max(initial=0)) >= (1 << 31):
@@ -225,6 +228,7 @@ class RowGroups:
         gmode = (egroup >= RG_BAL_MIN * max(N, 1)).astype(np.uint8)
         self.gmode = torch.from_numpy(gmode).to(dev)
         self.fgroup_host, self.flocal_host = fgroup, flocal
+        tick and tick("egroup")
         fg_t = torch.from_numpy(fgroup).to(dev)
         fl_t = torch.from_numpy(flocal).to(dev)
         self.gbase = torch.from_numpy(gbase).to(dev)
@@ -234,6 +238,13 @@ class RowGroups:
                                                                                             device=dev)
         # readable padding behind the end: the pass loads aligned 8-entry blocks
         self.ent = torch.empty(int(gbase[-1]) + 16, dtype=torch.int16, device=dev)[:int(gbase[-1])]
+        # entry-major rows of the sparse tail: groups em_g0.. (every group after the last dense one)
+        dense = np.nonzero(gmode != 0)[0]
+        self.em_g0 = int(dense[-1]) + 1 if dense.size else 0
+        self.ebase = int(gbase[self.em_g0])
+        self.erow = None
+        if RG_EM and self.em_g0 < G and N and int(gbase[-1]) > self.ebase:
+            self.erow = torch.empty(int(gbase[-1]) - self.ebase, dtype=torch.int32, device=dev)
         tick and tick("alloc")
         csr = getattr(Q, "csr_src", None)
         if csr is not None and G <= 128:
@@ -243,7 +254,7 @@ class RowGroups:
             remap[Q.fid_orig] = torch.arange(Q.Fa, dtype=torch.int32, device=dev)
             work = torch.empty(G * -(-N // 64), dtype=torch.int32, device=dev)
             C.tree_rg_build_csr(indptr, idx, counts, remap, max_bins - 1, fg_t, fl_t, ptr, self.gbase, self.ent,
-                                work)
+                                work, self.erow, self.em_g0, self.ebase)      # (erow written in the pass)
             self.ptr = ptr
             del work
             tick and tick("build")
@@ -255,15 +266,9 @@ class RowGroups:
             cursor = self.ptr[:, :N].clone(memory_format=torch.contiguous_format)   # (a view when G == 1)
             C.tree_rg_build(Q.csc_row, Q.csc_bin, Q.colptr, fg_t, fl_t, N, 1, None, cursor, self.gbase, self.ent)
             del cursor
-        # entry-major rows of the sparse tail: groups g0.. (every group after the last dense one)
-        dense = np.nonzero(gmode != 0)[0]
-        self.em_g0 = int(dense[-1]) + 1 if dense.size else 0
-        self.ebase = int(gbase[self.em_g0])
-        self.erow = None
-        if RG_EM and self.em_g0 < G and N and int(gbase[-1]) > self.ebase:
-            self.erow = torch.empty(int(gbase[-1]) - self.ebase, dtype=torch.int32, device=dev)
-            C.tree_rg_erow(self.ptr, self.gbase, self.em_g0, self.erow)
-            tick and tick("erow")
+            if self.erow is not None:
+                C.tree_rg_erow(self.ptr, self.gbase, self.em_g0, self.erow)
+                tick and tick("erow")
         self._work: dict = {}
 
     def work(self, target_wgs: int = 0, alpha: float = None) -> torch.Tensor:
@@ -290,14 +295,15 @@ class RowGroups:
         em = self.erow.numel() * 4 if self.erow is not None else 0
         return int(self.ptr.numel() * 4 + self.ent.numel() * 2 + self.gbin.numel() * 4 + em)
 
-    def em_args(self, list_rows: bool, row_node=None, node_slot=None) -> dict:
-        """Keyword arguments of tree_rg_hist for the entry-major sparse pass (empty: off)."""
+    def em_args(self, emdig=None) -> dict:
+        """Keyword arguments of tree_rg_hist for the entry-major sparse pass (empty: off). A listed
+        single-slot level passes ``emdig``, the digit words zeroed outside its slot (tree_rg_list
+        ``masked``), and takes the pass when it lists >= RG_EM_MIN_FRAC of the rows."""
         if self.erow is None:
             return {}
         kw = dict(erow=self.erow, ebase=self.ebase)
-        if list_rows:
-            kw.update(row_node=row_node, node_slot=node_slot,
-                      em_min_rows=max(1, int(RG_EM_MIN_FRAC * self.n_rows)))
+        if emdig is not None:
+            kw.update(emdig=emdig, em_min_rows=max(1, int(RG_EM_MIN_FRAC * self.n_rows)))
         return kw
 
 

@@ -65,20 +65,24 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
     node_slot[:nslots] = torch.arange(nslots, dtype=torch.int32)
     node_slot = node_slot.to(dev)
     row_node = torch.from_numpy(row_node_np).to(dev)
+    emdig = torch.full((n, 2), 7, dtype=torch.int32, device=dev) if (em and not root and nslots == 1) else None
     if not root:
         list_ = torch.empty(n, dtype=torch.int32, device=dev)
         start = torch.zeros(nslots + 1, dtype=torch.int32, device=dev)
         work = torch.zeros(nslots * (2 + n // 2048 + 1), dtype=torch.int32, device=dev)
         ldig = torch.empty((n, 2), dtype=torch.int32, device=dev)
-        C.tree_rg_list(row_node, node_slot, None, n, nslots, work, start, list_, ws.rowdig, ldig)
+        C.tree_rg_list(row_node, node_slot, None, n, nslots, work, start, list_, ws.rowdig, ldig, emdig)
     s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
     q0, q1 = _q_of(ws, np_)
     kw = {}
     if em:
         assert rg.erow is not None
-        kw = rg.em_args(not root, row_node, node_slot)
-        if not root:
+        kw = rg.em_args(emdig)
+        if emdig is not None:
             kw["em_min_rows"] = 1
+            built = (row_node_np >= 0) & (row_node_np < nslots)
+            want = np.where(built[:, None], ws.rowdig.cpu().numpy(), 0)
+            np.testing.assert_array_equal(emdig.cpu().numpy(), want)       # every row written
     if shards is None:
         hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
         C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, ldig, nslots, gmode(rg),
@@ -151,8 +155,13 @@ def test_row_groups_from_csr_equal_csc_build(dtype):
     Q.csr_src = csr
     assert a.G == b.G >= 2
     np.testing.assert_array_equal(a.ptr.numpy(), b.ptr.numpy())
-    ea, eb = a.ent.numpy(), b.ent.numpy()
+    # the entry-major rows: written inside the CSR build, by tree_rg_erow after the CSC build
+    assert a.erow is not None and a.em_g0 == b.em_g0
     pa, ga = a.ptr.numpy(), a.gbase.numpy()
+    for g in range(a.em_g0, a.G):          # the runs (the alignment padding is never written)
+        s0 = ga[g] - a.ebase
+        np.testing.assert_array_equal(a.erow.numpy()[s0: s0 + pa[g, -1]], b.erow.numpy()[s0: s0 + pa[g, -1]])
+    ea, eb = a.ent.numpy(), b.ent.numpy()
     for g in range(a.G):
         for r in range(0, n, 7):
             s0, s1 = ga[g] + pa[g, r], ga[g] + pa[g, r + 1]
@@ -231,10 +240,13 @@ def test_gpu_row_groups_from_csr_equal_host(dtype):
         ptr, ent, gb = rg.ptr.cpu().numpy(), rg.ent.cpu().numpy(), rg.gbase.cpu().numpy()
         # the runs only (the 8-entry alignment padding between groups is never written)
         runs = np.concatenate([ent[gb[g]: gb[g] + ptr[g, -1]] for g in range(rg.G)])
-        out.append((ptr, runs, rg.G))
+        er = rg.erow.cpu().numpy()
+        erow = np.concatenate([er[gb[g] - rg.ebase: gb[g] - rg.ebase + ptr[g, -1]] for g in range(rg.em_g0, rg.G)])
+        out.append((ptr, runs, rg.G, erow))
     assert out[0][2] == out[1][2] >= 2
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1], out[1][1])
+    np.testing.assert_array_equal(out[0][3], out[1][3])
 
 
 def test_row_groups_incomplete_beyond_max_groups():
@@ -326,14 +338,17 @@ def test_row_group_sharded_layout_equals_plain():
     np.testing.assert_array_equal(plain, sh)
 
 
-@pytest.mark.parametrize("depth,hot,bins", [(6, 0.2, 8192), (3, 0.0, 8192), (6, 0.2, 4096)])
-def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot, bins):
+@pytest.mark.parametrize("depth,hot,bins,em_frac", [(6, 0.2, 8192, 2.0), (3, 0.0, 8192, 2.0), (6, 0.2, 4096, 2.0),
+                                                    (6, 0.2, 8192, 0.0)])
+def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot, bins, em_frac):
     """FDX_ROWHIST=1: every GBDT level's histograms come from the row-group engine; the trees
-    equal the CSC / dense passes' trees bit for bit (device level loop, host twins)."""
+    equal the CSC / dense passes' trees bit for bit (device level loop, host twins). em_frac 0:
+    every single-node level takes the entry-major pass with masked digit words."""
     from fraud_detection_spark_kafka_llm_amd.models import grower, quantize as qmod
 
     monkeypatch.setattr(qmod, "HOT_DENSITY", hot)
     monkeypatch.setattr(qmod, "RG_BINS", bins)
+    monkeypatch.setattr(qmod, "RG_EM_MIN_FRAC", em_frac)
     dense, y = random_counts_matrix(3000, 300, 0.1, 21, max_count=40)
     dense[:, :6] = np.random.default_rng(1).integers(0, 5, (3000, 6))
     vc = vc_from_dense(dense)
@@ -374,11 +389,12 @@ def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, em, sha
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bins", [8192, 4096])
-def test_gpu_row_group_level_loop_grows_the_same_trees(monkeypatch, bins):
+@pytest.mark.parametrize("bins,em_frac", [(8192, 2.0), (4096, 2.0), (8192, 0.0)])
+def test_gpu_row_group_level_loop_grows_the_same_trees(monkeypatch, bins, em_frac):
     from fraud_detection_spark_kafka_llm_amd.models import grower, quantize as qmod
 
     monkeypatch.setattr(qmod, "RG_BINS", bins)
+    monkeypatch.setattr(qmod, "RG_EM_MIN_FRAC", em_frac)
 
     dense, y = random_counts_matrix(9000, 300, 0.1, 61, max_count=40)
     dense[:, :4] = np.random.default_rng(6).integers(0, 9, (9000, 4))
