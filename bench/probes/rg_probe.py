@@ -158,7 +158,7 @@ def main():
                                   "list_ms": round(list_ms, 3), "csc_ms": round(csc_ms, 3), "equal": eq}), flush=True)
                 if eq is False and dbg < 2:
                     sys.exit("row-group histograms differ from the CSC passes")
-                if args.split and dbg == 0:
+                if args.split:
                     # the densest group alone, the other groups alone (which part bounds the pass)
                     for name, keep in (("group0", wt[0] == 0), ("others", wt[0] != 0)):
                         sub = wt[:, keep].contiguous()
