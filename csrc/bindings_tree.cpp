@@ -848,6 +848,7 @@ void partition(const Tensor& row_node, const Tensor& default_child, const Tensor
   chk(split_left_is_default, dev, at::kInt, "split_left_is_default");
   chk(csc_row, dev, at::kInt, "csc_row");
   chk(csc_bin, dev, at::kByte, "csc_bin");
+  FDX_CHECK(reinterpret_cast<uintptr_t>(row_node.data_ptr()) % 16 == 0, "row_node must be 16-byte aligned");
   fdx::PartitionArgs a{};
   a.row_node = row_node.data_ptr<int32_t>();
   a.default_child = default_child.data_ptr<int32_t>();
@@ -990,6 +991,7 @@ void partition_cols(const Tensor& row_node, const Tensor& default_child, const T
   chk(csc_row, dev, at::kInt, "csc_row");
   chk(csc_bin, dev, at::kByte, "csc_bin");
   FDX_CHECK(cs_feat.numel() >= max_splits && wps >= 1, "cs arrays hold max_splits entries");
+  FDX_CHECK(reinterpret_cast<uintptr_t>(row_node.data_ptr()) % 16 == 0, "row_node must be 16-byte aligned");
   fdx::PartitionArgs a{};
   a.row_node = row_node.data_ptr<int32_t>();
   a.default_child = default_child.data_ptr<int32_t>();
