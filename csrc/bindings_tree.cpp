@@ -775,7 +775,8 @@ void split_best(const Tensor& gain, const Tensor& bin, const Tensor& left, int64
 void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, const Tensor& nbins, const Tensor& zbin,
                 const Tensor& fid_orig, const Tensor& node_ids, const Tensor& kexp, int64_t mode, double lambda_,
                 double mcw, const optional<Tensor>& feat_thr, int64_t seed, int64_t tree, const Tensor& out_gain,
-                const Tensor& out_bin, const Tensor& out_left, const optional<Tensor>& node_tree) {
+                const Tensor& out_bin, const Tensor& out_left, const optional<Tensor>& node_tree,
+                const optional<Tensor>& wide) {
   const auto dev = hist.device();
   chk(hist, dev, at::kLong, "hist");
   chk(totals, dev, at::kLong, "totals");
@@ -823,6 +824,11 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
   a.out_gain = out_gain.data_ptr<double>();
   a.out_bin = out_bin.data_ptr<int32_t>();
   a.out_left = out_left.data_ptr<int64_t>();
+  if (wide && wide->defined() && wide->numel() > 0) {      // (features with > kSplitWide bins)
+    chk(*wide, dev, at::kInt, "wide");
+    a.wide = wide->data_ptr<int32_t>();
+    a.n_wide = (int32_t)wide->numel();
+  }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_split(a, stream(dev));
@@ -1093,7 +1099,11 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_dense_fg", &dense_fg);
   m.def("tree_dense_waves", &dense_waves);
   m.def("tree_hist_subtract", &hist_subtract);
-  m.def("tree_split_find", &split_find);
+  m.def("tree_split_find", &split_find, py::arg("hist"), py::arg("totals"), py::arg("boff"), py::arg("nbins"),
+        py::arg("zbin"), py::arg("fid_orig"), py::arg("node_ids"), py::arg("kexp"), py::arg("mode"),
+        py::arg("lambda_"), py::arg("mcw"), py::arg("feat_thr"), py::arg("seed"), py::arg("tree"),
+        py::arg("out_gain"), py::arg("out_bin"), py::arg("out_left"), py::arg("node_tree"),
+        py::arg("wide") = py::none());
   m.def("tree_partition", &partition);
   m.def("tree_logistic_grad", &logistic_grad);
   m.def("tree_leaf_update", &leaf_update);

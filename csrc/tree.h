@@ -357,7 +357,12 @@ struct SplitArgs {
   double* out_gain;               // [nodes][Fa]
   int32_t* out_bin;               // [nodes][Fa]
   int64_t* out_left;              // [nodes][Fa][2]
+  // optional: the features with more than kSplitWide bins, searched a wave per (node, feature)
+  // (the thread-per-feature kernel skips them)
+  const int32_t* wide;
+  int32_t n_wide;
 };
+constexpr int32_t kSplitWide = 16;
 
 struct PartitionArgs {
   int32_t* row_node;              // [N]
@@ -471,9 +476,32 @@ FDX_HD double impurity(int mode, double c0, double c1) {
   return mode == 2 ? entropy2(c0, c1) : gini(c0, c1);
 }
 
+// Parent term of the split gain of a node with exact totals (T0, T1).
+FDX_HD double split_parent(int mode, int64_t T0, int64_t T1, double s0, double s1, double lambda_) {
+  const double G = (double)T0 * s0, H = (double)T1 * s1;
+  return (mode == 0) ? (G * G) / (H + lambda_) : impurity(mode, G, H);
+}
+
+// Gain of sending the left sums (l0, l1) left; false when a child violates the minimum.
+FDX_HD bool split_gain_at(int mode, int64_t l0, int64_t l1, int64_t T0, int64_t T1, double s0, double s1,
+                          double parent, double lambda_, double mcw, double* gain) {
+  const double L0 = (double)l0 * s0, L1 = (double)l1 * s1;
+  const double R0 = (double)(T0 - l0) * s0, R1 = (double)(T1 - l1) * s1;
+  if (mode == 0) {
+    if (L1 < mcw || R1 < mcw) return false;
+    *gain = (L0 * L0) / (L1 + lambda_) + (R0 * R0) / (R1 + lambda_) - parent;
+  } else {
+    const double nl = L0 + L1, nr = R0 + R1, n = nl + nr;
+    if (nl < mcw || nr < mcw || n <= 0) return false;
+    *gain = parent - (nl / n) * impurity(mode, L0, L1) - (nr / n) * impurity(mode, R0, R1);
+  }
+  return true;
+}
+
 // Best split of one (node, feature) histogram of exact integer sums: bins are scanned in value
 // order, the zero bin is node_total - sum(stored bins). s0/s1 = 2^-k of the two statistics.
-// Returns the gain (or -inf) and writes the bin and the left sums.
+// Returns the gain (or -inf) and writes the bin and the left sums: the first bin of the largest
+// gain (NaN gains never win). split_wide_kernel (tree_kernels.hip) computes the same per lane.
 // mode 0: XGBoost loss_chg = GL^2/(HL+l) + GR^2/(HR+l) - G^2/(H+l), children need H >= mcw.
 // mode 1/2: Spark impurity gain, children need (c0+c1) >= min instances.
 FDX_HD double best_split_scan(const int64_t* hb, int nb, int zb, int64_t T0, int64_t T1, double s0, double s1,
@@ -486,22 +514,12 @@ FDX_HD double best_split_scan(const int64_t* hb, int nb, int zb, int64_t T0, int
   int best_b = -1;
   int64_t bl0 = 0, bl1 = 0;
   int64_t l0 = 0, l1 = 0;
-  const double G = (double)T0 * s0, H = (double)T1 * s1;
-  const double parent = (mode == 0) ? (G * G) / (H + lambda_) : impurity(mode, G, H);
+  const double parent = split_parent(mode, T0, T1, s0, s1, lambda_);
   for (int b = 0; b + 1 < nb; ++b) {
     l0 += (b == zb) ? z0 : hb[2 * b];
     l1 += (b == zb) ? z1 : hb[2 * b + 1];
-    const double L0 = (double)l0 * s0, L1 = (double)l1 * s1;
-    const double R0 = (double)(T0 - l0) * s0, R1 = (double)(T1 - l1) * s1;
     double gain;
-    if (mode == 0) {
-      if (L1 < mcw || R1 < mcw) continue;
-      gain = (L0 * L0) / (L1 + lambda_) + (R0 * R0) / (R1 + lambda_) - parent;
-    } else {
-      const double nl = L0 + L1, nr = R0 + R1, n = nl + nr;
-      if (nl < mcw || nr < mcw || n <= 0) continue;
-      gain = parent - (nl / n) * impurity(mode, L0, L1) - (nr / n) * impurity(mode, R0, R1);
-    }
+    if (!split_gain_at(mode, l0, l1, T0, T1, s0, s1, parent, lambda_, mcw, &gain)) continue;
     if (gain > best) { best = gain; best_b = b; bl0 = l0; bl1 = l1; }
   }
   *out_bin = best_b;

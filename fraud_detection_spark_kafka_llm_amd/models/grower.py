@@ -131,6 +131,8 @@ RG_DBG = int(os.environ.get("FDX_RG_DBG", 0))   # diagnostics only (csrc/tree.h 
 # a device-compacted list of the active work items (tree_hist_sampled)
 SAMPLED = os.environ.get("FDX_RF_SAMPLED", "1") == "1"
 LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
+# split search: a wave per (node, feature) for the features with > 16 bins
+SPLIT_WIDE = os.environ.get("FDX_SPLIT_WIDE", "1") == "1"
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
 PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
 # RF levels under data parallelism reduce-scatter only the bins of the level's sampled features
@@ -470,9 +472,19 @@ def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, p
         if cache is not None:
             cache[(nl, Fa)] = bufs
     out_gain, out_bin, out_left = bufs
+    # features with > 16 bins get a wave each (tree_kernels.hip split_wide_kernel); listed once per
+    # nbins tensor
+    wide = None
+    if dev.type == "cuda" and SPLIT_WIDE:
+        key = ("wide", nbins.data_ptr(), Fa)
+        wide = cache.get(key) if cache is not None else None
+        if wide is None:
+            wide = torch.nonzero(nbins[:Fa] > 16).flatten().to(torch.int32)
+            if cache is not None:
+                cache[key] = wide
     C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, int(params.mode),
                       float(params.lambda_), float(params.min_child), feat_thr, int(params.seed), int(tree_index),
-                      out_gain, out_bin, out_left, node_tree)
+                      out_gain, out_bin, out_left, node_tree, wide)
     # best gain per node, ties to the lowest feature index (deterministic whatever the batch shape):
     # one native reduction instead of ~9 small torch launches per level
     out = torch.empty((nl, 5), dtype=torch.int64, device=dev)

@@ -725,3 +725,67 @@ def test_gpu_packed_item_cannot_overflow_int32_accumulators():
     q1 = np.rint(np.ldexp(h.astype(np.float64), int(k[1]))).astype(np.int64)
     assert int(q0[0]) % 256 == 128
     np.testing.assert_array_equal(hist, _hist_ref(Q, row_node, 1, q0, q1))
+
+
+def _split_inputs(seed, nodes=5, Fa=300, mode=0):
+    """Random exact histograms: features of 1..150 bins (wide ones span > 2 wave chunks), zero
+    bins anywhere, node totals >= the stored sums."""
+    rng = np.random.default_rng(seed)
+    nb = rng.integers(1, 40, Fa).astype(np.int32)
+    nb[rng.random(Fa) < 0.15] = rng.integers(17, 150, int((rng.random(Fa) < 0.15).sum()) or 1)[0]
+    nb[:4] = [150, 64, 65, 17]
+    zb = np.array([rng.integers(0, n) for n in nb], dtype=np.int32)
+    boff = np.concatenate([[0], np.cumsum(nb)]).astype(np.int64)
+    TB = int(boff[-1])
+    hist = np.zeros((nodes, TB + 3, 2), dtype=np.int64)                  # padded stride
+    if mode == 0:
+        hist[:, :TB, 0] = rng.integers(-(1 << 30), 1 << 30, (nodes, TB))
+        hist[:, :TB, 1] = rng.integers(0, 1 << 28, (nodes, TB))
+    else:
+        hist[:, :TB, :] = rng.integers(0, 50, (nodes, TB, 2))
+    for f in range(Fa):                                                   # zero bins hold nothing
+        hist[:, boff[f] + zb[f], :] = 0
+    totals = np.stack([hist[:, :TB, 0].sum(1) // 3 + (hist[:, :TB, 0].sum(1) if mode else 0),
+                       hist[:, :TB, 1].sum(1) + rng.integers(0, 1 << 20, nodes)], 1).astype(np.int64)
+    if mode:
+        totals[:, 0] = hist[:, :TB, 0].sum(1) + rng.integers(0, 100, nodes)
+    return hist, totals, boff, nb, zb
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,rf", [(0, False), (1, False), (2, False), (1, True)])
+def test_gpu_wide_feature_split_search_equals_host(mode, rf):
+    """split_wide_kernel (a wave per (node, wide feature): wave reductions / scans over 64-bin
+    chunks) gives the serial scan's gain, bin and left sums bit for bit, ties to the lowest bin."""
+    C = native.lib()
+    hist, totals, boff, nb, zb = _split_inputs(7 + mode, mode=mode)
+    nodes, Fa = totals.shape[0], nb.size
+    # ties: a node whose feature 3 repeats one bin pattern (equal gains at several bins)
+    hist[1, boff[3]:boff[4], :] = 0
+    args_np = (hist, totals, boff, nb, zb, np.arange(Fa, dtype=np.int64) * 7, np.array([0, 3, 4, -1, 9], np.int32)[:nodes],
+               np.array([20, 18] if mode == 0 else [0, 0], dtype=np.int32))
+    out = {}
+    for dev, use_wide in (("cpu", False), ("cuda:0", True), ("cuda:0", False)):
+        t = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in args_np]
+        thr = torch.full((nodes,), 0.6, dtype=torch.float64, device=dev) if rf else None
+        og = torch.empty((nodes, Fa), dtype=torch.float64, device=dev)
+        ob = torch.empty((nodes, Fa), dtype=torch.int32, device=dev)
+        ol = torch.empty((nodes, Fa, 2), dtype=torch.int64, device=dev)
+        wide = torch.nonzero(t[3] > 16).flatten().to(torch.int32) if use_wide else None
+        C.tree_split_find(t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], mode, 1.0, 1.0 if mode == 0 else 2.0, thr,
+                          11, 3, og, ob, ol, None, wide)
+        out[(dev, use_wide)] = (og.cpu().numpy(), ob.cpu().numpy(), ol.cpu().numpy())
+    assert (nb > 16).sum() >= 4
+
+    def same(x, y):
+        for a, b in zip(x, y):
+            np.testing.assert_array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                                          b.view(np.int64) if b.dtype == np.float64 else b)
+
+    # the wave search equals the device's serial scan bit for bit (every mode) ...
+    same(out[("cuda:0", True)], out[("cuda:0", False)])
+    # ... and the host's where no transcendental is involved (the device log of the entropy
+    # gain is not the host's correctly rounded one: its gains may differ in the last bits)
+    if mode != 2:
+        same(out[("cpu", False)], out[("cuda:0", True)])
+    assert (out[("cpu", False)][1] >= 0).any()
