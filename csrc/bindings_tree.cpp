@@ -228,7 +228,7 @@ void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Ten
                      const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
                      const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np,
                      const optional<Tensor>& feat_active, const optional<Tensor>& rowpack,
-                     const optional<Tensor>& list, const optional<Tensor>& count) {
+                     const optional<Tensor>& list, const optional<Tensor>& count, bool lds = false) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
@@ -304,6 +304,8 @@ void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Ten
     a.active_list = list->data_ptr<int32_t>();
     a.active_count = count->data_ptr<int32_t>();
   }
+  // LDS-atomic count kernel: 4 waves x 16 bt keys x nslots int64 cells must fit 64 KB
+  a.lds = (lds && np == 1 && !slot8_t && 4 * 16 * bt * nslots * 8 <= 65536) ? 1 : 0;
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
     fdx::launch_hist(a, (int)bt, (int)ct, (int)np, stream(dev));
@@ -330,9 +332,10 @@ void hist_sampled(const Tensor& item_start, const Tensor& item_end, const Tensor
                   const optional<Tensor>& wave_item, const Tensor& csc_row, const Tensor& csc_key,
                   const optional<Tensor>& rowpack, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
                   const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct,
-                  const Tensor& feat_active, const optional<Tensor>& list, const optional<Tensor>& count) {
+                  const Tensor& feat_active, const optional<Tensor>& list, const optional<Tensor>& count,
+                  bool lds) {
   hist_build_impl(item_start, item_end, item_f0, item_meta, wave_item, csc_row, csc_key, nullopt, rowdig, boff, nbins,
-                  slot_node, hist, TB, bt, ct, 1, feat_active, rowpack, list, count);
+                  slot_node, hist, TB, bt, ct, 1, feat_active, rowpack, list, count, lds);
 }
 
 // pack [N] int32 = slot (0xff: not built in this pass) | class-count digits << 8 (np = 1 passes)
@@ -1078,7 +1081,11 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_partition_cols", &partition_cols);
   m.def("tree_split_best", &split_best);
   m.def("tree_hist_build", &hist_build);
-  m.def("tree_hist_sampled", &hist_sampled);
+  m.def("tree_hist_sampled", &hist_sampled, py::arg("item_start"), py::arg("item_end"), py::arg("item_f0"),
+        py::arg("item_meta"), py::arg("wave_item"), py::arg("csc_row"), py::arg("csc_key"), py::arg("rowpack"),
+        py::arg("rowdig"), py::arg("boff"), py::arg("nbins"), py::arg("slot_node"), py::arg("hist"), py::arg("TB"),
+        py::arg("bt"), py::arg("ct"), py::arg("feat_active"), py::arg("list"), py::arg("count"),
+        py::arg("lds") = false);
   m.def("tree_slot_pack", &slot_pack);
   m.def("tree_rg_build", &rg_build);
   m.def("tree_rg_list", &rg_list, py::arg("row_node"), py::arg("node_slot"), py::arg("slot8"), py::arg("N"),

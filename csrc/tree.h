@@ -108,6 +108,7 @@ struct HistArgs {
   const uint32_t* rowpack;        // [N] optional, np = 1 passes: slot | digit0 << 8 | digit1 << 16 (slot8 unused)
   int32_t* active_list;           // [num_slots] optional: listed pass (compacted active items) ...
   int32_t* active_count;          //   ... [2]: their count (select kernel) and the waves' claim cursor
+  int32_t lds;                    // np = 1 passes: LDS-atomic kernel (hist_lds_kernel) instead of MFMA
 };
 
 // waves of a listed histogram pass (they stride over the active items): 8 per SIMD of 256 CUs

@@ -421,6 +421,108 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   }  // items of the wave
 }
 
+// ------------------------------------------------------------------ LDS-atomic count histogram
+// np = 1 passes (DT / RF class counts, |digit| <= 127): the i8 MFMA kernel's one-hot tiles and
+// live-entry compaction cost ~100 instructions per 64 entries for one (slot, key) update each,
+// ~25 G entries/s over a 500-tree forest. Here a wave per item keeps an LDS table of packed
+// counts [16 BT keys][nslots] (q0 + q1 * 2^32 in one int64: the exact sums stay below 2^31 in
+// magnitude -- an item has <= 2^15 entries -- so both halves decode exactly) and every live entry
+// is ONE ds_add_u64. The entry pipeline (rows / keys 4 per lane, slots and count words one and
+// two steps ahead) is the MFMA kernel's; the table is flushed per item with integer atomics.
+template <int BT, bool PACK>
+__global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
+  constexpr int G = 4 * kWave;
+  constexpr int KEYS = 16 * BT;
+  extern __shared__ unsigned long long s_tab[];          // [4 waves][KEYS * nslots]
+  const int wid = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wslot = blockIdx.x * 4 + wid;
+  const int ns = a.nslots;
+  const int cells = KEYS * ns;
+  unsigned long long* tab = s_tab + (int64_t)wid * cells;
+  const bool listed = a.active_list != nullptr;
+  const int n_listed = listed ? a.active_count[0] : 0;
+  const int stride = (int)gridDim.x * 4;
+  const uint2* rd = reinterpret_cast<const uint2*>(a.rowdig);
+  int li = wslot;
+  for (bool once = true;; once = false, li += stride) {
+    int item;
+    if (listed) {
+      if (li >= n_listed) break;
+      item = a.active_list[li];
+    } else {
+      if (!once) break;
+      item = a.wave_item ? a.wave_item[wslot] : wslot;
+      if (item < 0 || item >= a.num_items) break;
+      if (!item_active(a, item)) break;
+    }
+    const int64_t e0 = a.item_start[item], e1 = a.item_end[item];
+    const int32_t meta = a.item_meta[item];
+    const int32_t f0 = a.item_f0[item];
+    const uint32_t koff = (uint32_t)item_koff(meta);
+    for (int i = lane; i < cells; i += kWave) tab[i] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    const int64_t first = e0 & ~(int64_t)3;
+    const int64_t e_last = (e1 - 1) & ~(int64_t)3;
+    RowStep g1, g2;
+    uint32_t sl0, sl1, keys0, w0[8];
+    {
+      RowStep g0;
+      load_rows(a, first + 4 * lane, e0, e1, e_last, g0);
+      load_rows(a, first + G + 4 * lane, e0, e1, e_last, g1);
+      sl0 = entry_slots<!PACK, PACK>(a, g0.rows());
+      keys0 = g0.keys4;
+      sl1 = entry_slots<!PACK, PACK>(a, g1.rows());
+      gather_entry_digits<PACK>(a, rd, g0.rows(), sl0, w0);
+      load_rows(a, first + 2 * G + 4 * lane, e0, e1, e_last, g2);
+    }
+    for (int64_t base = first; base < e1; base += G) {
+      const uint32_t slots4 = sl0, keys4 = keys0;
+      uint32_t w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = w0[j];
+      gather_entry_digits<PACK>(a, rd, g1.rows(), sl1, w0);
+      const uint32_t sl2 = entry_slots<!PACK, PACK>(a, g2.rows());
+      RowStep g3;
+      load_rows(a, base + 3 * G + 4 * lane, e0, e1, e_last, g3);
+      sl0 = sl1;
+      keys0 = g1.keys4;
+      sl1 = sl2;
+      g1 = g2;
+      g2 = g3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t s = (slots4 >> (8 * j)) & 0xffu;
+        const uint32_t kk = ((keys4 >> (8 * j)) & 0xffu) - koff;     // (unsigned: keys below koff wrap)
+        const int64_t q0 = (int64_t)(int8_t)(uint8_t)(w[2 * j] & 0xffu);
+        const int64_t q1 = (int64_t)(int8_t)(uint8_t)(w[2 * j + 1] & 0xffu);
+        if (s < (uint32_t)ns && kk < (uint32_t)KEYS && (q0 | q1) != 0)
+          atomicAdd(&tab[kk * ns + s], (unsigned long long)(q0 + q1 * 4294967296ll));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // flush: (key, slot) cells with counts -> the level histogram (decode the two halves)
+    const int sl2 = item_stride_log2(meta), nfeat = item_nfeat(meta);
+    for (int i = lane; i < cells; i += kWave) {
+      const int64_t v = (int64_t)tab[i];
+      if (v == 0) continue;
+      const int kk = i / ns, s = i - kk * ns;
+      const int key = (int)koff + kk;
+      const int fl = key >> sl2, b = key & ((1 << sl2) - 1);
+      if (fl >= nfeat) continue;
+      const int f = f0 + fl;
+      const int node = a.slot_node[s];
+      if (b >= a.nbins[f] || node < 0) continue;
+      const int64_t lo = (int64_t)(int32_t)(uint32_t)(uint64_t)v;
+      const int64_t hi = (v - lo) >> 32;
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2);
+      if (lo) atomicAdd(dst, (unsigned long long)lo);
+      if (hi) atomicAdd(dst + 1, (unsigned long long)hi);
+    }
+    __builtin_amdgcn_wave_barrier();               // the table is zeroed for the next item
+  }
+}
+
 // Compacted list of the active work items of a listed pass, in wave-slot order per wave (one
 // atomic per wave: ballot + mbcnt for the positions inside it).
 __global__ __launch_bounds__(256) void hist_select_kernel(HistArgs a, int32_t* list, int32_t* count) {
@@ -1051,6 +1153,15 @@ void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s) {
                        const_cast<int32_t*>(a.active_list), const_cast<int32_t*>(a.active_count));
     const int32_t waves = slots < kListedWaves ? slots : kListedWaves;
     grid = dim3((waves + 3) / 4);
+  }
+  if (a.lds && np == 1) {
+    // (host-checked: 4 waves x 16 bt keys x nslots x 8 B <= 64 KB)
+    const size_t lds = (size_t)4 * 16 * bt * a.nslots * sizeof(unsigned long long);
+    const bool pack = a.rowpack != nullptr;
+    if (bt == 1) { if (pack) hipLaunchKernelGGL((hist_lds_kernel<1, true>), grid, block, lds, s, a); else hipLaunchKernelGGL((hist_lds_kernel<1, false>), grid, block, lds, s, a); }
+    else if (bt == 2) { if (pack) hipLaunchKernelGGL((hist_lds_kernel<2, true>), grid, block, lds, s, a); else hipLaunchKernelGGL((hist_lds_kernel<2, false>), grid, block, lds, s, a); }
+    else { if (pack) hipLaunchKernelGGL((hist_lds_kernel<4, true>), grid, block, lds, s, a); else hipLaunchKernelGGL((hist_lds_kernel<4, false>), grid, block, lds, s, a); }
+    return;
   }
 #define FDX_HIST_NP(B, C, P)                                                                             \
   if (np == P) {                                                                                        \

@@ -131,6 +131,8 @@ RG_DBG = int(os.environ.get("FDX_RG_DBG", 0))   # diagnostics only (csrc/tree.h 
 # a device-compacted list of the active work items (tree_hist_sampled)
 SAMPLED = os.environ.get("FDX_RF_SAMPLED", "1") == "1"
 LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
+# RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
+RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
 # split search: a wave per (node, feature) for the features with > 16 bins
 SPLIT_WIDE = os.environ.get("FDX_SPLIT_WIDE", "1") == "1"
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
@@ -1051,7 +1053,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                     launches.append(functools.partial(
                         C.tree_hist_sampled, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta,
                         grp.wave_order(), Q.h_row, Q.h_key, pack, csc_dig, h_boff, Q.nbins, s2n, hist_target, h_stride,
-                        grp.bt, ct, feat_mask, lst, cnt))
+                        grp.bt, ct, feat_mask, lst, cnt, RF_LDS))
                     continue
                 launches.append(functools.partial(
                     C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),

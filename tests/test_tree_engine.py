@@ -207,9 +207,10 @@ def _hist_ref(Q, row_node, nslots, q0, q1):
     return ref
 
 
-def _sampled_vs_build(dev, nslots, root, seed=3):
+def _sampled_vs_build(dev, nslots, root, seed=3, lds=False):
     """RF count passes over a random feature sample: tree_hist_sampled (packed row state, listed
-    active items) against tree_hist_build (slot bytes + digit words, every wave slot)."""
+    active items; the i8 MFMA kernel, or with ``lds`` the LDS-atomic one) against tree_hist_build
+    (slot bytes + digit words, every wave slot)."""
     from fraud_detection_spark_kafka_llm_amd.models.grower import pass_ct
 
     C = native.lib()
@@ -242,7 +243,7 @@ def _sampled_vs_build(dev, nslots, root, seed=3):
                           Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, ref, Q.TB, grp.bt, ct, 1, mask)
         lst, cnt = ws.item_list(gi, grp)
         C.tree_hist_sampled(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(), Q.h_row,
-                            Q.h_key, pack, ws.rowdig, Q.boff, Q.nbins, s2n, got, Q.TB, grp.bt, ct, mask, lst, cnt)
+                            Q.h_key, pack, ws.rowdig, Q.boff, Q.nbins, s2n, got, Q.TB, grp.bt, ct, mask, lst, cnt, lds)
     assert int(ref.abs().sum()) > 0
     return ref.cpu(), got.cpu()
 
@@ -254,9 +255,10 @@ def test_sampled_rf_pass_equals_build_pass(nslots, root):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nslots,root", [(1, True), (3, False), (16, False)])
-def test_gpu_sampled_rf_pass_equals_build_pass_and_host(nslots, root):
-    ref, got = _sampled_vs_build("cuda:0", nslots, root)
+@pytest.mark.parametrize("nslots,root", [(1, True), (3, False), (16, False), (40, False)])
+@pytest.mark.parametrize("lds", [False, True])
+def test_gpu_sampled_rf_pass_equals_build_pass_and_host(nslots, root, lds):
+    ref, got = _sampled_vs_build("cuda:0", nslots, root, lds=lds)
     href, _ = _sampled_vs_build("cpu", nslots, root)
     assert torch.equal(ref, got) and torch.equal(got, href)
 
