@@ -474,16 +474,16 @@ def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, p
         if cache is not None:
             cache[(nl, Fa)] = bufs
     out_gain, out_bin, out_left = bufs
-    # features with > 16 bins get a wave each (tree_kernels.hip split_wide_kernel); listed once per
-    # nbins tensor
+    # features with > 16 bins get a wave each (tree_kernels.hip split_wide_kernel): listed once per
+    # nbins tensor (kept on the tensor itself, shared by every forest lane; one read of the counts)
     wide = None
     if dev.type == "cuda" and SPLIT_WIDE:
-        key = ("wide", nbins.data_ptr(), Fa)
-        wide = cache.get(key) if cache is not None else None
-        if wide is None:
-            wide = torch.nonzero(nbins[:Fa] > 16).flatten().to(torch.int32)
-            if cache is not None:
-                cache[key] = wide
+        memo = getattr(nbins, "_fdx_wide", None)
+        if memo is None or memo[0] != Fa:
+            idx = np.nonzero(nbins[:Fa].cpu().numpy() > 16)[0].astype(np.int32)
+            memo = (Fa, torch.from_numpy(idx).to(dev))
+            nbins._fdx_wide = memo
+        wide = memo[1]
     C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, int(params.mode),
                       float(params.lambda_), float(params.min_child), feat_thr, int(params.seed), int(tree_index),
                       out_gain, out_bin, out_left, node_tree, wide)
