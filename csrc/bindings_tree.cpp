@@ -299,10 +299,14 @@ void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Ten
     FDX_CHECK(count.has_value() && feat_active.has_value(), "a listed pass needs count and feat_active");
     chk(*list, dev, at::kInt, "list");
     chk(*count, dev, at::kInt, "count");
-    FDX_CHECK(list->numel() >= (wave_item ? wave_item->numel() : I) && count->numel() >= 2,
-              "list must hold every wave slot, count two int32 (count, cursor)");
+    // per-XCD lists: XCD x holds the items of its wave slots (workgroups b = x mod 8, 4 slots each)
+    const int64_t slots = wave_item ? wave_item->numel() : I;
+    const int64_t cap = ((slots + 3) / 4 + 7) / 8 * 4;
+    FDX_CHECK(list->numel() >= 8 * cap && count->numel() >= 8,
+              "list must hold 8 x ceil(slots / 32) x 4 items, count 8 int32 (one per XCD)");
     a.active_list = list->data_ptr<int32_t>();
     a.active_count = count->data_ptr<int32_t>();
+    a.list_cap = (int32_t)cap;
   }
   // LDS-atomic count kernel: 4 waves x 16 bt keys x nslots int64 cells must fit 64 KB
   a.lds = (lds && np == 1 && !slot8_t && 4 * 16 * bt * nslots * 8 <= 65536) ? 1 : 0;

@@ -106,8 +106,9 @@ struct HistArgs {
   int64_t* hist;                  // [rows][hist_stride][2], accumulated (+=)
   const uint8_t* feat_active;     // [Fa] optional: items without an active feature are skipped (RF)
   const uint32_t* rowpack;        // [N] optional, np = 1 passes: slot | digit0 << 8 | digit1 << 16 (slot8 unused)
-  int32_t* active_list;           // [num_slots] optional: listed pass (compacted active items) ...
-  int32_t* active_count;          //   ... [2]: their count (select kernel) and the waves' claim cursor
+  int32_t* active_list;           // optional: listed pass, the active items compacted per XCD ...
+  int32_t* active_count;          //   ... [8]: their count per XCD (list x at x * list_cap)
+  int32_t list_cap;               // wave slots per XCD (set by the launch)
   int32_t lds;                    // np = 1 passes: LDS-atomic kernel (hist_lds_kernel) instead of MFMA
 };
 

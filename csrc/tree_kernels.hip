@@ -11,6 +11,8 @@
 // The rest of the level (sibling subtraction, split search, row partition) are small
 // bandwidth-bound kernels on the same int64 histograms.
 #include "hist_i8.h"
+#include <cstdlib>
+
 #include "ops.h"
 #include "tree.h"
 
@@ -228,18 +230,20 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
   const int wid = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
   const int wslot = blockIdx.x * 4 + wid;
-  // listed pass (RF): the waves of a fixed grid stride over the compacted list of active items;
-  // otherwise one wave per wave slot
+  // listed pass (RF): the waves of a fixed grid (a multiple of 8 workgroups) stride over their
+  // XCD's compacted list of active items (hist_select_kernel); otherwise one wave per wave slot
   const bool listed = a.active_list != nullptr;
-  const int n_listed = listed ? a.active_count[0] : 0;
+  const int xcd = blockIdx.x & 7;
+  const int n_listed = listed ? a.active_count[xcd] : 0;
+  const int32_t* xlist = listed ? a.active_list + (int64_t)xcd * a.list_cap : nullptr;
   // (claiming items through an atomic cursor instead: 8192 contended atomics cost ~0.2 ms a pass)
-  const int stride = (int)gridDim.x * 4;
-  int li = wslot;
+  const int stride = listed ? (int)(gridDim.x >> 3) * 4 : (int)gridDim.x * 4;
+  int li = listed ? (int)(blockIdx.x >> 3) * 4 + wid : wslot;
   for (bool once = true;; once = false, li += stride) {
   int item;
   if (listed) {
     if (li >= n_listed) break;
-    item = a.active_list[li];
+    item = xlist[li];
   } else {
     if (!once) break;
     item = a.wave_item ? a.wave_item[wslot] : wslot;
@@ -441,15 +445,17 @@ __global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
   const int cells = KEYS * ns;
   unsigned long long* tab = s_tab + (int64_t)wid * cells;
   const bool listed = a.active_list != nullptr;
-  const int n_listed = listed ? a.active_count[0] : 0;
-  const int stride = (int)gridDim.x * 4;
+  const int xcd = blockIdx.x & 7;
+  const int n_listed = listed ? a.active_count[xcd] : 0;
+  const int32_t* xlist = listed ? a.active_list + (int64_t)xcd * a.list_cap : nullptr;
+  const int stride = listed ? (int)(gridDim.x >> 3) * 4 : (int)gridDim.x * 4;
   const uint2* rd = reinterpret_cast<const uint2*>(a.rowdig);
-  int li = wslot;
+  int li = listed ? (int)(blockIdx.x >> 3) * 4 + wid : wslot;
   for (bool once = true;; once = false, li += stride) {
     int item;
     if (listed) {
       if (li >= n_listed) break;
-      item = a.active_list[li];
+      item = xlist[li];
     } else {
       if (!once) break;
       item = a.wave_item ? a.wave_item[wslot] : wslot;
@@ -530,14 +536,23 @@ __global__ __launch_bounds__(256) void hist_select_kernel(HistArgs a, int32_t* l
   int item = -1;
   if (w < a.num_slots) item = a.wave_item ? a.wave_item[w] : w;
   const bool act = item >= 0 && item < a.num_items && item_active(a, item);
-  const unsigned long long b = __ballot(act);
-  if (b == 0) return;
+  if (__ballot(act) == 0) return;
+  // the XCD the item's wave slot was placed on (wave_order: workgroup b = slot / 4 on XCD b % 8):
+  // each XCD's waves of the listed pass take that XCD's items, so a row block's slot and count
+  // words stay in the L2 they were placed for
+  const int x = (w >> 2) & 7;
   const int lane = threadIdx.x & (kWave - 1);
-  const int first = __builtin_ctzll(b);
-  int base = 0;
-  if (lane == first) base = atomicAdd(count, __popcll(b));
-  base = __shfl(base, first, kWave);
-  if (act) list[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = item;
+  for (int xx = 0; xx < 8; ++xx) {
+    const unsigned long long b = __ballot(act && x == xx);
+    if (b == 0) continue;
+    const int first = __builtin_ctzll(b);
+    int base = 0;
+    if (lane == first) base = atomicAdd(count + xx, __popcll(b));
+    base = __shfl(base, first, kWave);
+    if (act && x == xx)
+      list[(int64_t)xx * a.list_cap + base +
+           (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = item;
+  }
 }
 
 // ------------------------------------------------------------------ dense i8 MFMA histogram
@@ -1148,11 +1163,15 @@ void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s) {
     // over them (the full grid was ~300K wave slots, most of them exiting at once: ~100 us a pass)
     HistArgs sel = a;
     sel.num_slots = slots;
-    (void)hipMemsetAsync(const_cast<int32_t*>(a.active_count), 0, 2 * sizeof(int32_t), s);   // count, cursor
+    (void)hipMemsetAsync(const_cast<int32_t*>(a.active_count), 0, 8 * sizeof(int32_t), s);   // per-XCD counts
     hipLaunchKernelGGL(hist_select_kernel, dim3((slots + 255) / 256), dim3(256), 0, s, sel,
                        const_cast<int32_t*>(a.active_list), const_cast<int32_t*>(a.active_count));
-    const int32_t waves = slots < kListedWaves ? slots : kListedWaves;
-    grid = dim3((waves + 3) / 4);
+    static const int32_t listed_waves = [] {
+      const char* e = getenv("FDX_LISTED_WAVES");                  // (experiments: the grid of a listed pass)
+      return e ? atoi(e) : kListedWaves;
+    }();
+    const int32_t waves = slots < listed_waves ? slots : listed_waves;
+    grid = dim3((unsigned)(((waves + 3) / 4 + 7) / 8 * 8));       // whole XCD rounds of workgroups
   }
   if (a.lds && np == 1) {
     // (host-checked: 4 waves x 16 bt keys x nslots x 8 B <= 64 KB)

@@ -223,10 +223,11 @@ class Workspace:
         if lists is None:
             lists = self._item_lists = {}
         slots = grp.wave_order().numel()
+        need = 8 * ((-(-slots // 4) + 7) // 8 * 4)          # per-XCD lists (tree_kernels.hip hist_select)
         cur = lists.get(gi)
-        if cur is None or cur[0].numel() < slots:
-            cur = lists[gi] = (torch.empty(slots, dtype=torch.int32, device=self.dev),
-                               torch.zeros(2, dtype=torch.int32, device=self.dev))
+        if cur is None or cur[0].numel() < need:
+            cur = lists[gi] = (torch.empty(need, dtype=torch.int32, device=self.dev),
+                               torch.zeros(8, dtype=torch.int32, device=self.dev))
         return cur
 
     def run_concurrent(self, launches: list) -> None:
