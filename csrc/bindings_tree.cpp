@@ -71,7 +71,8 @@ void quant_max(const optional<Tensor>& g, const optional<Tensor>& h, const optio
   a.row0 = row0;
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_quant_max(a, out_max.data_ptr<double>(), stream(dev));
+    const Tensor part = at::empty({2 * (int64_t)std::max(1, fdx::quant_blocks(N))}, out_max.options().dtype(at::kLong));
+    fdx::launch_quant_max(a, out_max.data_ptr<double>(), part.data_ptr<int64_t>(), stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
     fdx::quant_max_cpu(a, out_max.data_ptr<double>());
@@ -109,7 +110,9 @@ void quant(const optional<Tensor>& g, const optional<Tensor>& h, const optional<
   const double* mx = max_abs ? max_abs->data_ptr<double>() : nullptr;
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
-    fdx::launch_quant(a, mx, stream(dev));
+    const Tensor part = at::empty({2 * (int64_t)std::max(1, fdx::quant_blocks(rowdig.size(0)))},
+                                  totals.options());
+    fdx::launch_quant(a, mx, part.data_ptr<int64_t>(), stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
     fdx::quant_cpu(a, mx);

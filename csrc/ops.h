@@ -83,8 +83,11 @@ void rf_sample_cpu(const RfSampleArgs& a);
 struct RfCompactArgs;
 void launch_rf_compact(const RfCompactArgs& a, hipStream_t s);
 void rf_compact_cpu(const RfCompactArgs& a);
-void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s);
-void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s);
+// partials: device scratch of 2 x quant_blocks(N) x 8 bytes (per-workgroup results, reduced by a
+// second one-block kernel that writes out / totals)
+int quant_blocks(int64_t n);
+void launch_quant_max(const QuantArgs& a, double* out, void* partials, hipStream_t s);
+void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);
 void launch_level_plan(const LevelPlanArgs& a, hipStream_t s);
 void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,

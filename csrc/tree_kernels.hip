@@ -36,8 +36,8 @@ __global__ __launch_bounds__(256) void quant_max_kernel(QuantArgs a, unsigned lo
     m0 = fmax(m0, __shfl_xor(m0, o, kWave));
     m1 = fmax(m1, __shfl_xor(m1, o, kWave));
   }
-  // one atomic per block: per-wave atomics on the same two addresses serialised in L2 (16K of
-  // them took ~0.2 ms per round at 10M rows)
+  // one partial per block, reduced by quant_reduce_kernel: atomics of every block on the same two
+  // addresses serialised in L2 (2048 blocks: ~40 us of a ~60 us kernel at 1M rows)
   __shared__ double s_m[2][4];
   const int w = threadIdx.x / kWave;
   if ((threadIdx.x & (kWave - 1)) == 0) { s_m[0][w] = m0; s_m[1][w] = m1; }
@@ -45,13 +45,44 @@ __global__ __launch_bounds__(256) void quant_max_kernel(QuantArgs a, unsigned lo
   if (threadIdx.x == 0) {
     m0 = fmax(fmax(s_m[0][0], s_m[0][1]), fmax(s_m[0][2], s_m[0][3]));
     m1 = fmax(fmax(s_m[1][0], s_m[1][1]), fmax(s_m[1][2], s_m[1][3]));
-    atomicMax(out, (unsigned long long)__double_as_longlong(m0));
-    atomicMax(out + 1, (unsigned long long)__double_as_longlong(m1));
+    out[2 * blockIdx.x] = (unsigned long long)__double_as_longlong(m0);
+    out[2 * blockIdx.x + 1] = (unsigned long long)__double_as_longlong(m1);
   }
 }
 
+// One block: the per-block partials (pairs) -> out: MAX of the (non-negative double) bit patterns
+// (MAX = 1) or the int64 SUM (MAX = 0). Exact and order-independent either way.
+template <bool MAX>
+__global__ __launch_bounds__(256) void quant_reduce_kernel(const unsigned long long* part, int nparts,
+                                                           unsigned long long* out) {
+  unsigned long long v0 = 0, v1 = 0;
+  for (int i = threadIdx.x; i < nparts; i += 256) {
+    const unsigned long long a0 = part[2 * i], a1 = part[2 * i + 1];
+    if (MAX) { v0 = a0 > v0 ? a0 : v0; v1 = a1 > v1 ? a1 : v1; }
+    else { v0 += a0; v1 += a1; }
+  }
+  __shared__ unsigned long long s[2][256];
+  s[0][threadIdx.x] = v0;
+  s[1][threadIdx.x] = v1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const unsigned long long b0 = s[0][threadIdx.x + o], b1 = s[1][threadIdx.x + o];
+      if (MAX) {
+        s[0][threadIdx.x] = b0 > s[0][threadIdx.x] ? b0 : s[0][threadIdx.x];
+        s[1][threadIdx.x] = b1 > s[1][threadIdx.x] ? b1 : s[1][threadIdx.x];
+      } else {
+        s[0][threadIdx.x] += b0;
+        s[1][threadIdx.x] += b1;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { out[0] = s[0][0]; out[1] = s[1][0]; }
+}
+
 // rowdig[r] = digits of (q0, q1); totals += (sum q0, sum q1) (int64 atomics, exact)
-__global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* maxv) {
+__global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* maxv, unsigned long long* part) {
   const int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) { a.kexp_out[0] = k0; a.kexp_out[1] = k1; }
   int64_t t0 = 0, t1 = 0;
@@ -76,15 +107,15 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
     t0 += __shfl_xor(t0, o, kWave);
     t1 += __shfl_xor(t1, o, kWave);
   }
-  __shared__ int64_t s_t[2][4];                 // one (exact, order-free) atomic per block
+  __shared__ int64_t s_t[2][4];                 // one partial per block (quant_reduce_kernel sums)
   const int w = threadIdx.x / kWave;
   if ((threadIdx.x & (kWave - 1)) == 0) { s_t[0][w] = t0; s_t[1][w] = t1; }
   __syncthreads();
   if (threadIdx.x == 0) {
     t0 = s_t[0][0] + s_t[0][1] + s_t[0][2] + s_t[0][3];
     t1 = s_t[1][0] + s_t[1][1] + s_t[1][2] + s_t[1][3];
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.totals), (unsigned long long)t0);
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.totals) + 1, (unsigned long long)t1);
+    part[2 * blockIdx.x] = (unsigned long long)t0;
+    part[2 * blockIdx.x + 1] = (unsigned long long)t1;
   }
 }
 
@@ -1130,22 +1161,31 @@ __global__ __launch_bounds__(256) void leaf_update_kernel(double* margin, const 
     margin[r] += node_value[row_node[r]];
 }
 
+constexpr int kQuantBlocks = 2048;      // workgroup cap of the quantisation passes (partials)
+
 inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
   const int64_t b = (n + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > cap ? cap : b));
 }
 }  // namespace
 
-void launch_quant_max(const QuantArgs& a, double* out, hipStream_t s) {
-  (void)hipMemsetAsync(out, 0, 2 * sizeof(double), s);
-  if (a.N > 0)
-    hipLaunchKernelGGL(quant_max_kernel, dim3(grid_for(a.N, 2048)), dim3(256), 0, s, a,
-                       reinterpret_cast<unsigned long long*>(out));
+int quant_blocks(int64_t n) { return (int)grid_for(n, kQuantBlocks); }
+
+void launch_quant_max(const QuantArgs& a, double* out, void* partials, hipStream_t s) {
+  auto* part = reinterpret_cast<unsigned long long*>(partials);
+  const int nb = a.N > 0 ? quant_blocks(a.N) : 0;
+  if (nb > 0) hipLaunchKernelGGL(quant_max_kernel, dim3(nb), dim3(256), 0, s, a, part);
+  hipLaunchKernelGGL(quant_reduce_kernel<true>, dim3(1), dim3(256), 0, s, part, nb,
+                     reinterpret_cast<unsigned long long*>(out));
 }
 
-void launch_quant(const QuantArgs& a, const double* maxv, hipStream_t s) {
-  (void)hipMemsetAsync(a.totals, 0, 2 * sizeof(int64_t), s);
-  hipLaunchKernelGGL(quant_kernel, dim3(grid_for(a.N, 2048)), dim3(256), 0, s, a, maxv);
+void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStream_t s) {
+  auto* part = reinterpret_cast<unsigned long long*>(partials);
+  const int nb = a.N > 0 ? quant_blocks(a.N) : 0;
+  if (nb > 0) hipLaunchKernelGGL(quant_kernel, dim3(nb), dim3(256), 0, s, a, maxv, part);
+  else hipLaunchKernelGGL(quant_kernel, dim3(1), dim3(256), 0, s, a, maxv, part);     // (writes kexp)
+  hipLaunchKernelGGL(quant_reduce_kernel<false>, dim3(1), dim3(256), 0, s, part, nb > 0 ? nb : 1,
+                     reinterpret_cast<unsigned long long*>(a.totals));
 }
 
 void launch_slot8(const SlotArgs& a, hipStream_t s) {

@@ -124,10 +124,17 @@ def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.T
 
 RG_BINS = int(os.environ.get("FDX_RG_BINS", 8192))   # local bins per row group: 8192 (1 workgroup per CU) or 4096 (2)
 RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
-# workgroups per row-group pass: few and large -- every workgroup flushes up to 2 x 8192 int64
-# global atomics per slot it covers; 10M rows x 40 trees: 7.69 ms per tree at 2048, 6.19 at 512
-# (profiles/r4/gbdt_rg_work_sweep.txt)
-RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 512))
+# workgroups per row-group pass: few and large -- every workgroup zeroes and flushes a whole
+# 8192-bin table (up to 2 x 8192 int64 global atomics per slot it covers). 10M rows x 40 trees:
+# 7.69 ms per tree at 2048, 6.19 at 512 (profiles/r4/gbdt_rg_work_sweep.txt); 1M rows x 100
+# trees: 1.95 ms at 512, 1.67 at 256, 1.79 at 128 (profiles/r4/gbdt_1M_rg_wgs_sweep.txt). Default
+# (FDX_RG_WGS unset): rows / 4096, in [128, 512], a multiple of 64.
+RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 0))
+
+
+def rg_default_wgs(n_rows: int) -> int:
+    """Workgroups of a row-group pass over ``n_rows`` rows (see RG_TARGET_WGS)."""
+    return int(min(512, max(128, round(n_rows / 4096 / 64) * 64)))
 # work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
 # (ptr, digits) loads whether or not it has entries in the group)
 RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 16.0))
@@ -276,7 +283,7 @@ class RowGroups:
         into chunks in proportion to its modelled cost alpha * rows + entries, so every workgroup
         carries about 1/target_wgs of the pass (the densest group holds ~79% of the entries on the
         bench corpus, but every group pays for every listed row)."""
-        target_wgs = target_wgs or RG_TARGET_WGS
+        target_wgs = target_wgs or RG_TARGET_WGS or rg_default_wgs(self.n_rows)
         alpha = RG_ALPHA if alpha is None else alpha
         key = (target_wgs, alpha)
         t = self._work.get(key)
