@@ -101,7 +101,7 @@ def main():
     rng = np.random.default_rng(0)
     lst = torch.empty(n, dtype=torch.int32, device=dev)
     start = torch.zeros(66, dtype=torch.int32, device=dev)
-    work = torch.zeros(64 * (2 + n // 2048 + 1), dtype=torch.int32, device=dev)
+    work = torch.zeros(64 * (2 + n // native.lib().tree_rg_list_rows(n) + 1), dtype=torch.int32, device=dev)
     ldig = torch.empty((n, 2), dtype=torch.int32, device=dev)
     for ns_s in args.slots.split(","):
         # "1L": a listed level with one built slot (about half the rows)

@@ -497,7 +497,7 @@ void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts,
 
 // Built rows of a level grouped by slot: list [N] int32, slot_start [nslots + 1] int32 (device).
 // The slot of a row is node_slot[row_node[r]] (row_node given) or slot8[r]. work: int32 scratch of
-// at least nslots * (2 + ceil(N / kRgListRows)). With rowdig, listdig [N, 2] receives the digit
+// at least nslots * (2 + ceil(N / rg_list_rows(N))). With rowdig, listdig [N, 2] receives the digit
 // words of the listed rows by list position.
 void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot, const optional<Tensor>& slot8,
              int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start, const Tensor& list,
@@ -508,7 +508,7 @@ void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot
   chk(list, dev, at::kInt, "list");
   FDX_CHECK(nslots >= 1 && nslots <= fdx::kRgMaxSlots, "nslots out of range");
   FDX_CHECK(list.numel() >= N && slot_start.numel() >= nslots + 1, "list / slot_start sizes");
-  const int64_t nwaves = (N + fdx::kRgListRows - 1) / fdx::kRgListRows;
+  const int64_t nwaves = (N + fdx::rg_list_rows(N) - 1) / fdx::rg_list_rows(N);
   FDX_CHECK(work.numel() >= 2 * nslots + nslots * nwaves, "work too small");
   fdx::RgListArgs a{};
   if (row_node) {
@@ -1107,6 +1107,7 @@ void register_tree_ops(pybind11::module& m) {
         py::arg("shard_lo"), py::arg("shard_stride"), py::arg("dbg"), py::arg("erow") = py::none(),
         py::arg("ebase") = 0, py::arg("emdig") = py::none(), py::arg("em_min_rows") = 0);
   m.def("tree_rg_erow", &rg_erow);
+  m.def("tree_rg_list_rows", [](int64_t N) { return (int64_t)fdx::rg_list_rows(N); });
   m.def("tree_rf_sample", &rf_sample);
   m.def("tree_rf_compact", &rf_compact);
   m.def("tree_hist_dense", &hist_dense);

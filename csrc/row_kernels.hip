@@ -163,19 +163,20 @@ __global__ __launch_bounds__(1024) void rg_build_scan_kernel(uint32_t* wave_base
   }
 }
 
-// One wave per kRgListRows consecutive rows (all its row_node / slot loads issued up front), slots
+// One wave per rg_list_rows(N) consecutive rows (its row_node / slot loads issued 8 steps at a time), slots
 // counted and placed with wave ballots (one ballot per distinct slot among each 64 rows). Pass 0
 // stores the wave's per-slot counts; pass 2 (one block per slot) turns them into per-wave offsets
 // inside the slot plus the slot totals; pass 1 derives the slot starts (a wave scan of the totals)
 // and writes the wave's rows (and their digit words) in ascending order. No atomics: the list is
 // sorted by (slot, row), and no counter is contended (one global counter per slot, added to by
 // every wave, serialised ~39K atomics per level at 10M rows: ~1.4 ms).
-constexpr int kRgListSteps = kRgListRows / 64;
+
 
 __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  const int64_t r0 = wave * kRgListRows;
+  const int32_t list_rows = rg_list_rows(a.N), list_steps = list_rows / 64;
+  const int64_t r0 = wave * list_rows;
   if (r0 >= a.N) return;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   int32_t* wc = a.wave_count + wave * a.nslots;
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
   uint32_t sl[KB];
   if (pass == 0) {
     int32_t cnt = 0;                           // lane s: rows of slot s
-    for (int k0 = 0; k0 < kRgListSteps; k0 += KB) {
+    for (int k0 = 0; k0 < list_steps; k0 += KB) {
 #pragma unroll
       for (int k = 0; k < KB; ++k) {
         const int64_t r = r0 + 64 * (k0 + k) + lane;
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
     if (lane == a.nslots - 1) a.slot_start[a.nslots] = incl;
   }
   int32_t base = lane < a.nslots ? incl - tot + wc[lane] : 0;
-  for (int k0 = 0; k0 < kRgListSteps; k0 += KB) {
+  for (int k0 = 0; k0 < list_steps; k0 += KB) {
     uint2 d[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
@@ -695,7 +696,7 @@ template void launch_rg_build_csr<double>(const RgCsrBuildArgs<double>&, hipStre
 template void launch_rg_build_csr<int32_t>(const RgCsrBuildArgs<int32_t>&, hipStream_t);
 
 void launch_rg_list(const RgListArgs& a, hipStream_t s) {
-  const int64_t waves = (a.N + kRgListRows - 1) / kRgListRows;   // 4 per block
+  const int64_t waves = (a.N + rg_list_rows(a.N) - 1) / rg_list_rows(a.N);   // 4 per block
   const int64_t blocks = (waves + 3) / 4;
   if (blocks <= 0) return;
   hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);

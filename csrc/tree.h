@@ -174,7 +174,9 @@ struct RgCsrBuildArgs {
 
 // Built rows of a level grouped by slot. The slot of row r is node_slot[row_node[r]] when
 // row_node is given (slots outside [0, nslots): not built), else slot8[r] (0xff: not built).
-constexpr int kRgListRows = 2048;           // rows per wave of the list kernels
+// rows per wave of the list kernels: 512 up to 4M rows (1M rows: ~2K waves; 2048-row chunks left
+// ~500 waves and 19 us per pass), 2048 beyond (profiles/r4/gbdt_list_rows_ab.txt)
+FDX_HD int32_t rg_list_rows(int64_t N) { return N <= (4ll << 20) ? 512 : 2048; }
 struct RgListArgs {
   const int32_t* row_node;        // [N] or nullptr
   const int32_t* node_slot;       // [num_nodes] slot of each node (-1: not built)
@@ -183,7 +185,7 @@ struct RgListArgs {
   int64_t N;
   int32_t nslots;
   int32_t* slot_count;            // [nslots] totals (pass 2)
-  int32_t* wave_count;            // [ceil(N / kRgListRows)][nslots]: per-wave counts (pass 0), then
+  int32_t* wave_count;            // [ceil(N / rg_list_rows(N))][nslots]: per-wave counts (pass 0), then
                                   //   per-wave offsets inside each slot (pass 2)
   int32_t* slot_start;            // [nslots + 1] out (pass 1)
   int32_t* list;                  // [N] out (pass 1): built rows grouped by slot, ascending inside each

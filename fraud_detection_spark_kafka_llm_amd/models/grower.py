@@ -199,7 +199,7 @@ class Workspace:
         if getattr(self, "rg_list", None) is None:
             self.rg_list = torch.empty(self.Q.n_rows, dtype=torch.int32, device=self.dev)
             self.rg_start = torch.zeros(66, dtype=torch.int32, device=self.dev)
-            nw = -(-self.Q.n_rows // 2048)            # csrc/tree.h kRgListRows
+            nw = -(-self.Q.n_rows // native.lib().tree_rg_list_rows(self.Q.n_rows))   # waves of the list kernels
             self.rg_work = torch.zeros(64 * (2 + nw), dtype=torch.int32, device=self.dev)
             self.rg_listdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
         return rg

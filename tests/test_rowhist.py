@@ -69,7 +69,7 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
     if not root:
         list_ = torch.empty(n, dtype=torch.int32, device=dev)
         start = torch.zeros(nslots + 1, dtype=torch.int32, device=dev)
-        work = torch.zeros(nslots * (2 + n // 2048 + 1), dtype=torch.int32, device=dev)
+        work = torch.zeros(nslots * (2 + n // native.lib().tree_rg_list_rows(n) + 1), dtype=torch.int32, device=dev)
         ldig = torch.empty((n, 2), dtype=torch.int32, device=dev)
         C.tree_rg_list(row_node, node_slot, None, n, nslots, work, start, list_, ws.rowdig, ldig, emdig)
     s2n = torch.arange(nslots, dtype=torch.int32, device=dev)
@@ -280,7 +280,7 @@ def _list_check(dev, n, ns, seed):
     sl = np.where((row_node >= 0) & (row_node < node_slot.size), node_slot[np.clip(row_node, 0, node_slot.size - 1)], -1)
     lst = torch.full((n,), -7, dtype=torch.int32, device=dev)
     start = torch.zeros(ns + 1, dtype=torch.int32, device=dev)
-    work = torch.full((ns * (2 + n // 2048 + 1),), 99, dtype=torch.int32, device=dev)
+    work = torch.full((ns * (2 + n // native.lib().tree_rg_list_rows(n) + 1),), 99, dtype=torch.int32, device=dev)
     dig = torch.from_numpy(rng.integers(0, 1 << 30, (n, 2)).astype(np.int32)).to(dev)
     ldig = torch.zeros((n, 2), dtype=torch.int32, device=dev)
     C.tree_rg_list(torch.from_numpy(row_node).to(dev), torch.from_numpy(node_slot).to(dev), None, n, ns, work,
