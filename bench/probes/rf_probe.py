@@ -79,7 +79,7 @@ def main():
                 C.tree_hist_build(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(), Q.h_row,
                                   Q.h_key, slot8, ws.rowdig, Q.boff, Q.nbins, s2n, hist, Q.TB, grp.bt, ct, 1, mask)
 
-    def passes_sampled(mask, pack, ns, hist, listed=True):
+    def passes_sampled(mask, pack, ns, hist, listed=True, lds=False):
         s2n = torch.arange(ns, dtype=torch.int32, device=dev)
         ct = pass_ct(1, ns)
         for gi, grp in enumerate(groups):
@@ -87,7 +87,7 @@ def main():
                 lst, cnt = ws.item_list(gi, grp) if listed else (None, None)
                 C.tree_hist_sampled(grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
                                     Q.h_row, Q.h_key, pack, ws.rowdig, Q.boff, Q.nbins, s2n, hist, Q.TB, grp.bt, ct,
-                                    mask, lst, cnt)
+                                    mask, lst, cnt, lds)
 
     for tree in [int(t) for t in args.trees.split(",")]:
         for d in range(args.depth):
@@ -118,15 +118,22 @@ def main():
             hist3 = torch.zeros_like(hist)
             ms_p = timed(lambda: (hist3.zero_(), passes_sampled(mask, pack, ns, hist3, False)))
             same = same and bool(torch.equal(hist, hist3))
+            hist4 = torch.zeros_like(hist)
+            ms_l = timed(lambda: (hist4.zero_(), passes_sampled(mask, pack, ns, hist4, False, True)))
+            hist5 = torch.zeros_like(hist)
+            ms_ll = timed(lambda: (hist5.zero_(), passes_sampled(mask, pack, ns, hist5, True, True)))
+            same = same and bool(torch.equal(hist, hist4)) and bool(torch.equal(hist, hist5))
             none = torch.zeros_like(mask)
             ms0 = timed(lambda: passes(none, slot8, ns, hist))
             ms0_s = timed(lambda: passes_sampled(none, pack, ns, hist2))
+            ms0_l = timed(lambda: passes_sampled(none, pack, ns, hist4, False, True))
             print(json.dumps({"tree": tree, "depth": d, "slots": ns, "sampled_feats": int(m.sum()),
                               "sampled_entries": int(colcnt[m].sum()), "active_items": act_items,
                               "active_item_entries": act_entries, "items_total": sum(len(i[0]) for i in items),
                               "pass_ms": round(ms, 3), "empty_mask_ms": round(ms0, 3),
                               "sampled_pass_ms": round(ms_s, 3), "sampled_empty_ms": round(ms0_s, 3),
-                              "pack_only_ms": round(ms_p, 3),
+                              "pack_only_ms": round(ms_p, 3), "lds_pass_ms": round(ms_l, 3),
+                              "lds_listed_ms": round(ms_ll, 3), "lds_empty_ms": round(ms0_l, 3),
                               "equal": same}), flush=True)
             if not same:
                 sys.exit("sampled pass differs from the build pass")

@@ -685,6 +685,7 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
     Q.dense = dense
 
 
+LIGHT_ENTRIES = int(os.environ.get("FDX_LIGHT_ENTRIES", 2048))    # whole-column items up to this many entries (0: off)
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
 
@@ -744,11 +745,20 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
     sb_rows = (Q.n_rows + nsb - 1) // nsb if Q.n_rows else 1
     # --- per (super-block, feature) segments of the feature-major CSC and their new offsets
     S = int(cols.size)
+    # light features (columns of <= LIGHT_ENTRIES entries) keep their whole column in row block 0:
+    # one item per column instead of one per row block, so a sampled RF pass launches fewer
+    # (mostly idle) wave slots; their entries are thousands of rows apart, so the row-block
+    # locality that the heavy columns need buys them nothing
+    ncol_all = n[cols]
+    light = (ncol_all <= LIGHT_ENTRIES) & ~hot[cols] if LIGHT_ENTRIES > 0 else np.zeros(cols.size, bool)
     if S:
         cols_t = torch.from_numpy(cols.astype(np.int32)).to(dev)
         bounds = torch.empty((S, nsb + 1), dtype=torch.int64, device=dev)
         C.block_bounds(Q.csc_row, Q.colptr, cols_t, int(nsb), int(sb_rows), bounds)
         bounds[:, -1] = Q.colptr[cols_t.to(torch.int64) + 1]
+        if light.any() and nsb > 1:
+            li = torch.from_numpy(np.nonzero(light)[0]).to(dev)
+            bounds[li, 1:nsb] = bounds[li, nsb:nsb + 1]           # every entry in row block 0
         seg_src = bounds[:, :-1].t().contiguous()                    # [nsb, S]
         seg_len = (bounds[:, 1:] - bounds[:, :-1]).t().contiguous()
         flat = seg_len.reshape(-1)
@@ -816,6 +826,11 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
             parts.append(np.stack([st[sel], en[sel], f_[sel], np.full(m, 8), np.ones(m, np.int64),
                                    np.full(m, 64 * w), btw, b_[sel]], 1))
     items = np.concatenate(parts) if parts else np.zeros((0, 8), np.int64)
+    if items.shape[0] and light.any():
+        # items holding a whole (light) column: spread over the XCDs (row block -1)
+        cl = np.concatenate([[0], np.cumsum(np.isin(np.arange(Fa), cols[light]))])
+        f0, nf = items[:, 2], items[:, 4]
+        items[(cl[f0 + nf] - cl[f0]) > 0, 7] = -1
     sp_p.__exit__(None, None, None)
     # --- the histogram CSC: (row, kbase + bin) of every (super-block, feature) segment
     if S:

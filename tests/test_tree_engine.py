@@ -263,12 +263,16 @@ def test_gpu_sampled_rf_pass_equals_build_pass_and_host(nslots, root, lds):
     assert torch.equal(ref, got) and torch.equal(got, href)
 
 
-def test_work_items_cover_histogram_csc_once_and_wave_order_is_xcd_grouped():
+@pytest.mark.parametrize("light", [True, False])
+def test_work_items_cover_histogram_csc_once_and_wave_order_is_xcd_grouped(monkeypatch, light):
     """The histogram CSC holds every entry of the non-dense features once, super-block-major;
     every entry belongs to exactly one item; packed items hold consecutive small features with
-    distinct key ranges; an item stays inside its super-block."""
+    distinct key ranges; an item stays inside its super-block, or (``light``: few-entry features)
+    holds its whole column in row block 0 and is spread over the XCDs (row block -1)."""
+    from fraud_detection_spark_kafka_llm_amd.models import quantize as qmod
     from fraud_detection_spark_kafka_llm_amd.models.quantize import wave_order
 
+    monkeypatch.setattr(qmod, "LIGHT_ENTRIES", 60 if light else 0)
     rng = np.random.default_rng(2)
     n, F = 5000, 40
     dense = (rng.random((n, F)) < np.linspace(0.002, 0.6, F)) * rng.integers(1, 5, (n, F))
@@ -288,7 +292,10 @@ def test_work_items_cover_histogram_csc_once_and_wave_order_is_xcd_grouped():
             sl2, nf = meta[i] & 0xFF, (meta[i] >> 8) & 0xFF
             single = sl2 == 8                                          # one feature, key = bin
             assert en[i] - st[i] <= 100 or not single
-            assert np.all(rows[st[i]:en[i]] // 625 == blk[i])          # 5000 rows / 8 super-blocks
+            if blk[i] >= 0:
+                assert np.all(rows[st[i]:en[i]] // 625 == blk[i])      # 5000 rows / 8 super-blocks
+            else:
+                kinds.add("column")
             kinds.add("single" if single else "packed")
             for e in range(st[i], en[i]):
                 fl = (int(keys[e]) >> sl2) if not single else 0
@@ -300,9 +307,10 @@ def test_work_items_cover_histogram_csc_once_and_wave_order_is_xcd_grouped():
         assert sorted(used.tolist()) == list(range(grp.num_items))   # every item exactly once
         slots = np.nonzero(order >= 0)[0]
         lab = (slots // 4) % 8                                     # workgroup % 8 = XCD group
-        assert np.all(blk[order[slots]] % 8 == lab)
+        blocked = blk[order[slots]] >= 0
+        assert np.all(blk[order[slots]][blocked] % 8 == lab[blocked])
     assert np.all(cover == 1)
-    assert kinds == {"packed", "single"}
+    assert kinds == ({"packed", "single", "column"} if light else {"packed", "single"})
     got = sorted((int(rows[e]), f, b) for e, (f, b) in fid_of.items())
     colptr, crow, cbin = Q.colptr.numpy(), Q.csc_row.numpy(), Q.csc_bin.numpy()
     ref = sorted((int(crow[e]), f, int(cbin[e])) for f in range(Q.Fa) for e in range(colptr[f], colptr[f + 1]))
