@@ -2,6 +2,7 @@
 // implementations (featurizer incl. token keys, JSON extraction, tree engine) on edge cases and
 // checks them against simple scalar references. Built with -fsanitize=address,undefined by
 // fraud_detection_spark_kafka_llm_amd/_build.py:build_host_selftest(); exits non-zero on failure.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -225,10 +226,100 @@ static void test_tree() {
     for (int b = 0; b < 12; ++b) EXPECT(hist[((size_t)n * 12 + b) * 2] == ref[n][b]);
 }
 
+// Row-group engine on the host: CSR layout build (with the entry-major rows of the sparse group),
+// row lists with masked digit words, and the histogram pass at the root and at a listed
+// single-node level (entry-major for the sparse group) against scalar sums.
+static void test_rowgroups() {
+  const int64_t N = 7;
+  // rows x features (counts; 0 = absent): features 0, 1 -> group 0 (balanced), 2, 3 -> group 1
+  const int cnt[7][4] = {{1, 2, 0, 1}, {3, 0, 1, 0}, {1, 1, 0, 0}, {0, 2, 2, 1}, {2, 0, 0, 3}, {1, 1, 1, 1}, {0, 0, 0, 0}};
+  std::vector<int64_t> indptr = {0};
+  std::vector<int32_t> idx, counts;
+  for (int r = 0; r < N; ++r) {
+    for (int f = 0; f < 4; ++f)
+      if (cnt[r][f]) { idx.push_back(f); counts.push_back(cnt[r][f]); }
+    indptr.push_back((int64_t)idx.size());
+  }
+  const std::vector<int32_t> remap = {0, 1, 2, 3}, fgroup = {0, 0, 1, 1}, flocal = {0, 8, 0, 8};
+  int64_t e0 = 0, e1 = 0;
+  for (int r = 0; r < N; ++r)
+    for (int f = 0; f < 4; ++f) if (cnt[r][f]) (f < 2 ? e0 : e1) += 1;
+  const std::vector<int64_t> gbase = {0, (e0 + 7) / 8 * 8, (e0 + 7) / 8 * 8 + (e1 + 7) / 8 * 8};
+  std::vector<uint32_t> ptr(2 * (N + 1));
+  std::vector<uint16_t> ent((size_t)gbase[2] + 16, 0);
+  std::vector<uint32_t> wave_base(64), erow((size_t)(gbase[2] - gbase[1]) + 8, 0xffffffffu);
+  RgCsrBuildArgs<int32_t> ba{};
+  ba.indptr = indptr.data(); ba.idx = idx.data(); ba.counts = counts.data(); ba.N = N; ba.remap = remap.data();
+  ba.max_bin = 7; ba.fgroup = fgroup.data(); ba.flocal = flocal.data(); ba.G = 2; ba.ptr = ptr.data();
+  ba.gbase = gbase.data(); ba.ent = ent.data(); ba.wave_base = wave_base.data();
+  ba.erow = erow.data(); ba.em_g0 = 1; ba.ebase = gbase[1];
+  rg_build_csr_cpu<int32_t>(ba);
+  for (int64_t i = 0; i < e1; ++i) {           // the entry-major rows of group 1: its row runs, in order
+    int64_t r = 0;
+    while (!(ptr[N + 1 + r] <= (uint32_t)i && (uint32_t)i < ptr[N + 1 + r + 1])) ++r;
+    EXPECT(erow[i] == (uint32_t)r);
+  }
+  // statistics q0 = 3 r - 7, q1 = r + 1 (digit words)
+  std::vector<uint32_t> rd(2 * N);
+  for (int r = 0; r < N; ++r) { rd[2 * r] = digits4(3 * r - 7); rd[2 * r + 1] = digits4(r + 1); }
+  const std::vector<int32_t> gbin = [] {
+    std::vector<int32_t> v(2 * 8192, -1);
+    for (int b = 0; b < 16; ++b) { v[b] = b; v[8192 + b] = 16 + b; }      // global column = 8 f + count bin
+    return v;
+  }();
+  const std::vector<uint8_t> gmode = {1, 0};
+  const std::vector<int32_t> wg_g = {0, 0, 1, 1}, wg_p = {0, 1, 0, 1}, wg_np = {2, 2, 2, 2}, slot_node = {0};
+  auto run = [&](const int32_t* list, const int32_t* slot_start, const uint32_t* listdig, const uint32_t* emdig,
+                 std::vector<int64_t>& hist) {
+    RgHistArgs ha{};
+    ha.ptr = ptr.data(); ha.ent = ent.data(); ha.gbase = gbase.data(); ha.gbin = gbin.data(); ha.gbins = 8192;
+    ha.G = 2; ha.N = N; ha.rowdig = rd.data(); ha.np = 4; ha.list = list; ha.listdig = listdig; ha.gmode = gmode.data();
+    ha.slot_start = slot_start; ha.nslots = 1; ha.wg_g = wg_g.data(); ha.wg_p = wg_p.data(); ha.wg_np = wg_np.data();
+    ha.n_wg = 4; ha.slot_node = slot_node.data(); ha.hist_stride = 32; ha.hist = hist.data();
+    ha.erow = erow.data(); ha.ebase = gbase[1]; ha.emdig = emdig; ha.em_min_rows = 1;
+    rg_hist_cpu(ha);
+  };
+  auto ref_of = [&](const std::vector<int>& built) {
+    std::vector<int64_t> ref(64, 0);
+    for (int r : built)
+      for (int f = 0; f < 4; ++f)
+        if (cnt[r][f]) {
+          const int col = 8 * f + std::min(cnt[r][f], 7);
+          ref[2 * col] += 3 * r - 7;
+          ref[2 * col + 1] += r + 1;
+        }
+    return ref;
+  };
+  std::vector<int64_t> hist(64, 0);
+  run(nullptr, nullptr, nullptr, nullptr, hist);               // root: every row, group 1 entry-major
+  EXPECT(hist == ref_of({0, 1, 2, 3, 4, 5, 6}));
+  // a listed level with one built node (rows 1, 3, 4, 5)
+  const std::vector<int32_t> row_node = {2, 1, 2, 1, 1, 1, -1}, node_slot = {-1, 0, -1};
+  std::vector<int32_t> list(N, -7), slot_start(2), work(2 + 2 * (int)((N + rg_list_rows(N) - 1) / rg_list_rows(N)));
+  std::vector<uint32_t> listdig(2 * N), masked(2 * N, 99u);
+  RgListArgs la{};
+  la.row_node = row_node.data(); la.node_slot = node_slot.data(); la.num_nodes = 3; la.N = N; la.nslots = 1;
+  la.slot_count = work.data(); la.wave_count = work.data() + 2; la.slot_start = slot_start.data(); la.list = list.data();
+  la.rowdig = rd.data(); la.listdig = listdig.data(); la.masked = masked.data();
+  rg_list_cpu(la);
+  EXPECT(slot_start[0] == 0 && slot_start[1] == 4);
+  for (int r = 0; r < N; ++r) {
+    const bool b = row_node[r] == 1;
+    EXPECT(masked[2 * r] == (b ? rd[2 * r] : 0u) && masked[2 * r + 1] == (b ? rd[2 * r + 1] : 0u));
+  }
+  std::fill(hist.begin(), hist.end(), 0);
+  run(list.data(), slot_start.data(), listdig.data(), masked.data(), hist);
+  EXPECT(hist == ref_of({1, 3, 4, 5}));
+  std::fill(hist.begin(), hist.end(), 0);
+  run(list.data(), slot_start.data(), listdig.data(), nullptr, hist);   // (row lists for both groups)
+  EXPECT(hist == ref_of({1, 3, 4, 5}));
+}
+
 int main() {
   test_featurizer();
   test_json();
   test_tree();
+  test_rowgroups();
   if (g_fail) {
     std::fprintf(stderr, "%d failures\n", g_fail);
     return 1;
