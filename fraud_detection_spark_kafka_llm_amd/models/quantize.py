@@ -685,7 +685,7 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
     Q.dense = dense
 
 
-LIGHT_ENTRIES = int(os.environ.get("FDX_LIGHT_ENTRIES", 2048))    # whole-column items up to this many entries (0: off)
+LIGHT_ENTRIES = int(os.environ.get("FDX_LIGHT_ENTRIES", 0))    # whole-column items up to this many entries (0: off; profiles/r4/rf500_light_entries_sweep.txt)
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
 
