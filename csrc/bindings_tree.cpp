@@ -1060,6 +1060,24 @@ void logistic_grad(const Tensor& margin, const Tensor& label, const optional<Ten
   }
 }
 
+// GBDT leaf values of every row of the device node table's sums (one launch per tree)
+void leaf_values(const Tensor& stats, const Tensor& kexp, double eta, double lambda, double mds, const Tensor& out) {
+  const auto dev = stats.device();
+  chk(stats, dev, at::kLong, "stats");
+  chk(kexp, dev, at::kInt, "kexp");
+  chk(out, dev, at::kDouble, "out");
+  FDX_CHECK(stats.dim() == 2 && stats.size(1) == 2 && kexp.numel() >= 2 && out.numel() == stats.size(0), "sizes");
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_leaf_values(stats.data_ptr<int64_t>(), kexp.data_ptr<int32_t>(), stats.size(0), eta, lambda, mds,
+                            out.data_ptr<double>(), stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::leaf_values_cpu(stats.data_ptr<int64_t>(), kexp.data_ptr<int32_t>(), stats.size(0), eta, lambda, mds,
+                         out.data_ptr<double>());
+  }
+}
+
 void leaf_update(const Tensor& margin, const Tensor& row_node, const Tensor& node_value) {
   const auto dev = margin.device();
   chk(margin, dev, at::kDouble, "margin");
@@ -1122,4 +1140,5 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_partition", &partition);
   m.def("tree_logistic_grad", &logistic_grad);
   m.def("tree_leaf_update", &leaf_update);
+  m.def("tree_leaf_values", &leaf_values);
 }

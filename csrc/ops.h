@@ -120,6 +120,10 @@ void launch_split(const SplitArgs& a, hipStream_t s);
 void launch_partition(const PartitionArgs& a, hipStream_t s);
 void launch_logistic_grad(const double* margin, const float* label, const float* weight, float* g, float* h,
                           int64_t N, hipStream_t s);
+void launch_leaf_values(const int64_t* stats, const int32_t* kexp, int64_t M, double eta, double lambda, double mds,
+                        double* out, hipStream_t s);
+void leaf_values_cpu(const int64_t* stats, const int32_t* kexp, int64_t M, double eta, double lambda, double mds,
+                     double* out);
 void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s);
 void quant_max_cpu(const QuantArgs& a, double* out);
 void quant_cpu(const QuantArgs& a, const double* maxv);

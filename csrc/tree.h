@@ -42,6 +42,16 @@ FDX_HD int32_t quant_exponent(double m) {
 FDX_HD int64_t quantize_value(double v, int32_t k) { return (int64_t)rint(ldexp(v, k)); }
 
 // q (|q| < 2^31 - 2^23) -> 4 balanced base-256 digits, byte i = d_i (two's complement)
+// GBDT leaf value of a node's exact sums (G, H scaled by 2^-k): eta * clip(-G / (H + lambda)),
+// the fp64 operations of TreeTable.build in the same order (bitwise the host table's value)
+FDX_HD double leaf_value(int64_t g, int64_t h, int32_t k0, int32_t k1, double eta, double lambda, double mds) {
+  const double G = (double)g * ldexp(1.0, -k0);
+  const double H = (double)h * ldexp(1.0, -k1);
+  double w = -G / (H + lambda);
+  if (mds > 0) w = w < -mds ? -mds : (w > mds ? mds : w);
+  return eta * w;
+}
+
 FDX_HD uint32_t digits4(int64_t q) { return (uint32_t)(q + 0x80808080ll) ^ 0x80808080u; }
 FDX_HD int64_t undigits4(uint32_t d) { return (int64_t)(d ^ 0x80808080u) - 0x80808080ll; }
 // NP = 1: the value itself (|q| <= 127) in byte 0

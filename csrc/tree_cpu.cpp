@@ -423,6 +423,11 @@ void logistic_grad_cpu(const double* margin, const float* label, const float* we
   }
 }
 
+void leaf_values_cpu(const int64_t* stats, const int32_t* kexp, int64_t M, double eta, double lambda, double mds,
+                     double* out) {
+  for (int64_t n = 0; n < M; ++n) out[n] = leaf_value(stats[2 * n], stats[2 * n + 1], kexp[0], kexp[1], eta, lambda, mds);
+}
+
 void leaf_update_cpu(double* margin, const int32_t* row_node, const double* node_value, int64_t N) {
   for (int64_t r = 0; r < N; ++r) margin[r] += node_value[row_node[r]];
 }

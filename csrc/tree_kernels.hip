@@ -1161,6 +1161,12 @@ __global__ __launch_bounds__(256) void leaf_update_kernel(double* margin, const 
     margin[r] += node_value[row_node[r]];
 }
 
+__global__ __launch_bounds__(256) void leaf_values_kernel(const int64_t* stats, const int32_t* kexp, int64_t M,
+                                                          double eta, double lambda, double mds, double* out) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n < M) out[n] = leaf_value(stats[2 * n], stats[2 * n + 1], kexp[0], kexp[1], eta, lambda, mds);
+}
+
 constexpr int kQuantBlocks = 2048;      // workgroup cap of the quantisation passes (partials)
 
 inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
@@ -1314,6 +1320,13 @@ void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const 
 void launch_logistic_grad(const double* margin, const float* label, const float* weight, float* g, float* h,
                           int64_t N, hipStream_t s) {
   if (N > 0) hipLaunchKernelGGL(logistic_grad_kernel, dim3(grid_for(N)), dim3(256), 0, s, margin, label, weight, g, h, N);
+}
+
+void launch_leaf_values(const int64_t* stats, const int32_t* kexp, int64_t M, double eta, double lambda, double mds,
+                        double* out, hipStream_t s) {
+  if (M > 0)
+    hipLaunchKernelGGL(leaf_values_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, stats, kexp, M, eta,
+                       lambda, mds, out);
 }
 
 void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s) {

@@ -946,6 +946,9 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     TB = Q.TB
     n_open, n_build = 1, 1
     prev_hist = None
+    # the next level's zeroed histograms (at most 2 open nodes per open node) are queued before
+    # the host waits for its counts, so the fill runs while the host sizes that level
+    pre_hist = None
     ev = None
     # RF under data parallelism: each level reduce-scatters only its sampled features' bins; level
     # d + 1's sample and layout are computed right after level d's plan, so their shard sizes reach
@@ -983,7 +986,11 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                              feat_thr, feat_mask, None)
         split_boff = shards.boff if shards is not None else None
         if shards is None:
-            cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
+            if pre_hist is not None and pre_hist.shape[0] >= n_open:
+                cur_hist = hist_target = pre_hist[:n_open]
+            else:
+                cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
+            pre_hist = None
             h_boff, h_stride = Q.boff, TB
         elif compact:
             # only the sampled features' bins travel (FeatureShards.sample_compact)
@@ -1111,6 +1118,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         with tracing.span("tree.partition"):
             C.tree_partition_cols(ws.row_node, st.default_child, *st.cs, st.counts[d], Q.colptr, Q.csc_row, Q.csc_bin,
                                   st.node_dense, Q.dense if st.node_dense is not None else None, n_open, PARTITION_WPS)
+        if shards is None and d + 1 < params.max_depth:
+            pre_hist = torch.zeros((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
         prev_hist = cur_hist
     if on_first_wait is not None:          # (a one-level tree) the previous table first
         on_first_wait()
@@ -1139,14 +1148,12 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
 
 def leaf_values_device(stats: torch.Tensor, kexp: torch.Tensor, params: GrowParams) -> torch.Tensor:
     """GBDT leaf values of the device node table, the same fp64 operations as TreeTable.build
-    (so bitwise the host's values): G, H = stats * 2^-k (exact), eta * clip(-G / (H + lambda))."""
-    scale = ((1023 - kexp.to(torch.int64)) << 52).view(torch.float64)      # exactly 2^-k
-    G = stats[:, 0].to(torch.float64) * scale[0]
-    H = stats[:, 1].to(torch.float64) * scale[1]
-    w = -G / (H + params.lambda_)
-    if params.max_delta_step > 0:
-        w = torch.clamp(w, -params.max_delta_step, params.max_delta_step)
-    return params.eta * w
+    (so bitwise the host's values): G, H = stats * 2^-k (exact), eta * clip(-G / (H + lambda)).
+    One native launch over the table (csrc/tree.h leaf_value) instead of ~10 elementwise ops."""
+    out = torch.empty(stats.shape[0], dtype=torch.float64, device=stats.device)
+    native.lib().tree_leaf_values(stats, kexp, float(params.eta), float(params.lambda_),
+                                  float(params.max_delta_step), out)
+    return out
 
 
 class PendingTree:
