@@ -844,7 +844,6 @@ __global__ __launch_bounds__(256) void split_wide_kernel(SplitArgs a) {
 // One 1024-thread block per node, 4 independent loads in flight per thread (the 256-thread
 // version was a latency-bound ~40 us per level at ~10^5 features).
 constexpr int kBestThreads = 1024;
-constexpr int kBestLoads = 16;
 __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* gain, const int32_t* bin,
                                                                   const int64_t* left, int32_t Fa, int64_t f0,
                                                                   int64_t* out) {
@@ -853,16 +852,15 @@ __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* 
   double best = -1.0 / 0.0;
   int bf = Fa;
   bool nan = false;
-  // 16 loads in flight per thread (2^18-feature tables: 2 rounds instead of 7 dependent ones)
-  for (int f = threadIdx.x; f < Fa; f += kBestLoads * kBestThreads) {
-    double v[kBestLoads];
+  for (int f = threadIdx.x; f < Fa; f += 4 * kBestThreads) {
+    double v[4];
 #pragma unroll
-    for (int u = 0; u < kBestLoads; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int fu = f + u * kBestThreads;
       v[u] = fu < Fa ? g[fu] : -1.0 / 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < kBestLoads; ++u) {  // increasing feature order per thread: ties keep the lower
+    for (int u = 0; u < 4; ++u) {           // increasing feature order per thread: ties keep the lower
       const int fu = f + u * kBestThreads;
       if (v[u] != v[u]) nan = true;
       else if (v[u] > best || (v[u] == best && fu < bf)) { best = v[u]; bf = fu; }
