@@ -161,6 +161,7 @@ def bench_rf(args) -> dict:
     t0 += t_gen
     torch.cuda.reset_peak_memory_stats(dev)
     grower.reset_level_stats()
+    D.reset_bytes()
     res = fit_forest(vc, y, num_trees=trees, max_depth=5, max_bins=32, bootstrap=True, feature_subset=args.subset,
                      seed=42, device=dev)
     _sync(dev)
@@ -171,6 +172,7 @@ def bench_rf(args) -> dict:
            "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev),
            "lanes": res.lanes, "collectives": bool(D.Collectives().active),
            "level_collective_calls": grower.LEVEL_STATS["coll_calls"],
+           "collective_calls": D.total_calls(), "collective_calls_by_kind": dict(D.CALLS),
            "level_collective_ms": _max_over_ranks(grower.level_collective_ms(), dev)}
     if rank == 0:
         tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
@@ -183,7 +185,9 @@ def bench_rf(args) -> dict:
 def bench_xgb(args) -> dict:
     """BASELINE config 4: --rows is the GLOBAL row count (default 12.5M x ranks, so each GPU holds a
     12.5M-row shard: 100M rows at DP=8); histograms are reduce-scattered per level."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
     from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
 
     rank, world, dev = _dist()
     rows = args.rows or 12_500_000 * world
@@ -199,6 +203,8 @@ def bench_xgb(args) -> dict:
     t0 += t_gen
     feat_peak = torch.cuda.max_memory_allocated(dev)
     torch.cuda.reset_peak_memory_stats(dev)      # training peak: quantize + 1000 rounds
+    grower.reset_level_stats()
+    D.reset_bytes()
     res = fit_gbdt(vc, y, GBDTParams(n_estimators=trees, max_depth=6), device=dev)
     _sync(dev)
     t_train = time.perf_counter() - t0
@@ -212,7 +218,11 @@ def bench_xgb(args) -> dict:
             "featurize_s": _max_over_ranks(t_feat, dev), "train_s": _max_over_ranks(t_train, dev),
             "per_tree_ms": _max_over_ranks((t_train - t_feat) / trees * 1e3, dev),
             "peak_hbm_gb": _max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev),
-            "featurize_peak_hbm_gb": _max_over_ranks(feat_peak / 2 ** 30, dev)}
+            "featurize_peak_hbm_gb": _max_over_ranks(feat_peak / 2 ** 30, dev),
+            "collectives": bool(D.Collectives().active), "collective_calls": D.total_calls(),
+            "collective_calls_by_kind": dict(D.CALLS),
+            "collective_calls_per_tree": D.total_calls() / max(len(res.trees), 1),
+            "level_collective_ms": _max_over_ranks(grower.level_collective_ms(), dev)}
 
 
 def bench_kafka(args) -> dict:

@@ -86,6 +86,7 @@ def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
         return t
     x, moved = _on_comm_device(t.contiguous())
     BYTES["all_reduce"] += x.numel() * x.element_size()
+    CALLS["all_reduce"] += 1
     dist.all_reduce(x, op=op)
     return x.to(t.device) if moved else x
 
@@ -113,6 +114,7 @@ def all_gather_var(*tensors: torch.Tensor) -> tuple:
         pad[: t.numel()] = t
         p, moved = _on_comm_device(pad)
         bufs = [torch.empty_like(p) for _ in range(world_size())]
+        CALLS["all_gather"] += 1
         dist.all_gather(bufs, p)
         cat = torch.cat([b[:s] for b, s in zip(bufs, sizes)])
         out.append(cat.to(t.device) if moved else cat)
@@ -145,12 +147,19 @@ def shard_range(n: int, r: Optional[int] = None, w: Optional[int] = None) -> tup
 
 
 # bytes this process handed to each collective (payload sizes, for the per-level DP accounting)
+# and the number of collective calls issued (every backend call, per kind)
 BYTES = {"reduce_scatter": 0, "all_gather": 0, "all_reduce": 0}
+CALLS = {"reduce_scatter": 0, "all_gather": 0, "all_reduce": 0}
 
 
 def reset_bytes() -> None:
     for k in BYTES:
         BYTES[k] = 0
+        CALLS[k] = 0
+
+
+def total_calls() -> int:
+    return int(sum(CALLS.values()))
 
 
 def reduce_scatter(x: torch.Tensor) -> torch.Tensor:
@@ -162,6 +171,7 @@ def reduce_scatter(x: torch.Tensor) -> torch.Tensor:
         return x[0]
     x = x.contiguous()
     BYTES["reduce_scatter"] += x.numel() * x.element_size()
+    CALLS["reduce_scatter"] += 1
     xc, moved = _on_comm_device(x)
     # flat buffers (gloo wants the concatenated form; RCCL takes either)
     out = torch.empty(xc.numel() // xc.shape[0], dtype=xc.dtype, device=xc.device)
@@ -177,6 +187,7 @@ def all_gather(x: torch.Tensor) -> torch.Tensor:
         return x.unsqueeze(0)
     x = x.contiguous()
     BYTES["all_gather"] += x.numel() * x.element_size()
+    CALLS["all_gather"] += 1
     xc, moved = _on_comm_device(x)
     out = torch.empty(world_size() * xc.numel(), dtype=xc.dtype, device=xc.device)
     dist.all_gather_into_tensor(out, xc.view(-1))
