@@ -77,6 +77,7 @@ from fraud_detection_spark_kafka_llm_amd.utils.profiling import run_profiled_if_
 METRIC = "dialogues/sec streaming inference + GBDT train sec on 10M rows, 1/2/4/8 GPU"
 F = 1 << 18
 CHUNK_ROWS = 500_000       # rows per featurization chunk (pinned text, H2D overlapped with the kernel)
+GROUP_TIMEOUT_S = 120.0    # consumer-group rendezvous waits (a peer that never starts fails the phase)
 
 
 def sync_all(dev):
@@ -207,6 +208,10 @@ def group_kafka(args, spec, idf_np, model, dev, pool) -> dict:
         the clients are cheap), with the micro-batches each scoring process took.
     A failure is reported in the record, not raised; no rank enters a device barrier before its
     scoring process has stopped."""
+    from fraud_detection_spark_kafka_llm_amd.stream.group import single_host_group
+
+    if not single_host_group():           # shared segments + Unix sockets: one host only
+        return {"kafka_group_error": "ranks span hosts (LOCAL_WORLD_SIZE != WORLD_SIZE)"} if D.rank() == 0 else {}
     out = {}
     for name, fn in (("kafka_confluent_group", _group_confluent_runs), ("kafka_multi_gpu", _group_multi_runs)):
         if (name == "kafka_multi_gpu" and args.kafka_multi_msgs <= 0) or \
@@ -229,8 +234,15 @@ def _group_session(name, runs, args, spec, idf_np, model, dev, pool) -> dict:
     from fraud_detection_spark_kafka_llm_amd.stream import group as G
 
     batch = 16384
-    sc = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=batch, max_bytes=batch * 4096, depth=3)
-    rdv = G.GroupRendezvous.from_process_group(name) if D.world_size() > 1 else None
+    rdv = G.GroupRendezvous.from_process_group(name, timeout_s=GROUP_TIMEOUT_S) if D.world_size() > 1 else None
+    try:
+        sc = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=batch, max_bytes=batch * 4096, depth=3)
+    except Exception as e:
+        # the other side of the rendezvous waits for this rank: answer with the error
+        if rdv is not None:
+            why = f"{type(e).__name__}: {e}"
+            rdv.publish_socket_error(why) if D.rank() > 0 else rdv.publish_config({"error": why})
+        raise
     gc.collect()
     if D.rank() > 0:
         with G.ScorerPeer(sc, model.postprocess_numpy, rdv) as peer:

@@ -786,7 +786,7 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
                 const Tensor& fid_orig, const Tensor& node_ids, const Tensor& kexp, int64_t mode, double lambda_,
                 double mcw, const optional<Tensor>& feat_thr, int64_t seed, int64_t tree, const Tensor& out_gain,
                 const Tensor& out_bin, const Tensor& out_left, const optional<Tensor>& node_tree,
-                const optional<Tensor>& wide) {
+                const optional<Tensor>& wide, const optional<Tensor>& row_of) {
   const auto dev = hist.device();
   chk(hist, dev, at::kLong, "hist");
   chk(totals, dev, at::kLong, "totals");
@@ -810,7 +810,15 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
   a.totals = totals.data_ptr<int64_t>();
   // the node row stride is the tensor's own ([nodes, stride, 2]): a data-parallel level searches
   // the reduce-scattered [n, Bs, 2] rows in place (Bs >= this shard's bins)
-  FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && hist.size(0) >= nodes, "hist must be [nodes, stride, 2]");
+  FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2, "hist must be [rows, stride, 2]");
+  if (row_of && row_of->defined()) {
+    // (the rows are level_rows' own: every one lies in this buffer, no device read here)
+    chk(*row_of, dev, at::kInt, "row_of");
+    FDX_CHECK(row_of->numel() >= nodes, "row_of must cover the nodes");
+    a.row_of = row_of->data_ptr<int32_t>();
+  } else {
+    FDX_CHECK(hist.size(0) >= nodes, "hist must have a row per node");
+  }
   a.hist_stride = hist.size(1);
   a.num_nodes = nodes;
   a.Fa = Fa;
@@ -899,6 +907,40 @@ void partition(const Tensor& row_node, const Tensor& default_child, const Tensor
   }
 }
 
+// Data-parallel level rows (tree.h LevelRowsArgs): nb slots, row_of [>= n_open], triples [nb].
+void level_rows(const Tensor& s2n, const Tensor& sub_dst, const Tensor& sub_par, const optional<Tensor>& prev_row_of,
+                int64_t nb, int64_t bld_base, int64_t sub_base, const Tensor& row_of, const Tensor& dst_row,
+                const Tensor& par_row, const Tensor& sib_row) {
+  const auto dev = s2n.device();
+  for (const Tensor* t : {&s2n, &sub_dst, &sub_par, &row_of, &dst_row, &par_row, &sib_row})
+    chk(*t, dev, at::kInt, "level_rows int32 array");
+  FDX_CHECK(nb >= 0 && s2n.numel() >= nb && sub_dst.numel() >= nb && sub_par.numel() >= nb && dst_row.numel() >= nb &&
+                par_row.numel() >= nb && sib_row.numel() >= nb, "level_rows: [nb] arrays");
+  FDX_CHECK(bld_base >= 0 && sub_base >= 0 && sub_base + nb <= INT32_MAX, "level_rows: bases");
+  fdx::LevelRowsArgs a{};
+  a.s2n = s2n.data_ptr<int32_t>();
+  a.sub_dst = sub_dst.data_ptr<int32_t>();
+  a.sub_par = sub_par.data_ptr<int32_t>();
+  if (prev_row_of && prev_row_of->defined()) {
+    chk(*prev_row_of, dev, at::kInt, "prev_row_of");
+    a.prev_row_of = prev_row_of->data_ptr<int32_t>();
+  }
+  a.nb = (int32_t)nb;
+  a.bld_base = (int32_t)bld_base;
+  a.sub_base = (int32_t)sub_base;
+  a.row_of = row_of.data_ptr<int32_t>();
+  a.dst_row = dst_row.data_ptr<int32_t>();
+  a.par_row = par_row.data_ptr<int32_t>();
+  a.sib_row = sib_row.data_ptr<int32_t>();
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_level_rows(a, stream(dev));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::level_rows_cpu(a);
+  }
+}
+
 // Device level loop (tree.h level_plan): applies the level's best splits and plans the next level.
 void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_depth, int64_t mode, bool build_all,
                 const Tensor& kexp, double min_gain, const Tensor& zbin,
@@ -910,7 +952,7 @@ void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_dept
                 const Tensor& next_open, const Tensor& next_totals, const Tensor& node_slot, const Tensor& s2n,
                 const Tensor& sub_dst, const Tensor& sub_par, const Tensor& sub_sib) {
   const auto dev = packed.device();
-  chk(packed, dev, at::kLong, "packed");
+  FDX_CHECK(packed.device() == dev && packed.scalar_type() == at::kLong, "packed must be int64");
   chk(stats, dev, at::kLong, "stats");
   chk(next_totals, dev, at::kLong, "next_totals");
   chk(gain, dev, at::kDouble, "gain");
@@ -920,10 +962,12 @@ void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_dept
                           &sub_dst, &sub_par, &sub_sib})
     chk(*t, dev, at::kInt, "level_plan int32 array");
   const int64_t M = parent.numel();
-  // packed: [L, 5] or the all-gathered [S, L, 5] of a data-parallel level (best over shards here)
+  // packed: [L, 5] or the all-gathered [S, L, 5] of a data-parallel level (best over shards here);
+  // the shard stride is the tensor's own, so a tree's [S, L, 5] slice of a batched all-gather
+  // ([S, sum L, 5] over the trees in flight) is read in place
   const int64_t S = packed.dim() == 3 ? packed.size(0) : 1;
-  FDX_CHECK(packed.is_contiguous() && (packed.dim() == 2 || packed.dim() == 3) && packed.size(-1) == 5 &&
-                packed.size(-2) >= L, "packed must be [L, 5] or [S, L, 5] contiguous");
+  FDX_CHECK((packed.dim() == 2 || packed.dim() == 3) && packed.size(-1) == 5 && packed.stride(-1) == 1 &&
+                packed.stride(-2) == 5 && packed.size(-2) >= L, "packed must be [L, 5] or [S, L, 5] with rows of 5");
   FDX_CHECK(L >= 1 && open.numel() >= L, "open [L]");
   FDX_CHECK(stats.numel() == 2 * M && left.numel() == M && right.numel() == M && feat.numel() == M &&
                 bin.numel() == M && leaf.numel() == M && gain.numel() == M && default_child.numel() == M &&
@@ -936,7 +980,7 @@ void level_plan(const Tensor& packed, int64_t L, int64_t depth, int64_t max_dept
   a.packed = packed.data_ptr<int64_t>();
   a.L = (int32_t)L;
   a.n_shards = (int32_t)S;
-  a.shard_stride = packed.size(-2) * 5;
+  a.shard_stride = packed.dim() == 3 ? packed.stride(0) : packed.size(-2) * 5;
   a.depth = (int32_t)depth;
   a.max_depth = (int32_t)max_depth;
   a.mode = (int32_t)mode;
@@ -1103,6 +1147,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_quant", &quant);
   m.def("tree_slot8", &slot8);
   m.def("tree_level_plan", &level_plan);
+  m.def("tree_level_rows", &level_rows);
   m.def("tree_partition_cols", &partition_cols);
   m.def("tree_split_best", &split_best);
   m.def("tree_hist_build", &hist_build);
@@ -1136,7 +1181,7 @@ void register_tree_ops(pybind11::module& m) {
         py::arg("zbin"), py::arg("fid_orig"), py::arg("node_ids"), py::arg("kexp"), py::arg("mode"),
         py::arg("lambda_"), py::arg("mcw"), py::arg("feat_thr"), py::arg("seed"), py::arg("tree"),
         py::arg("out_gain"), py::arg("out_bin"), py::arg("out_left"), py::arg("node_tree"),
-        py::arg("wide") = py::none());
+        py::arg("wide") = py::none(), py::arg("row_of") = py::none());
   m.def("tree_partition", &partition);
   m.def("tree_logistic_grad", &logistic_grad);
   m.def("tree_leaf_update", &leaf_update);

@@ -77,6 +77,7 @@ struct DenseHistArgs;
 struct SplitArgs;
 struct PartitionArgs;
 struct LevelPlanArgs;
+struct LevelRowsArgs;
 struct RfSampleArgs;
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s);
 void rf_sample_cpu(const RfSampleArgs& a);
@@ -90,6 +91,7 @@ void launch_quant_max(const QuantArgs& a, double* out, void* partials, hipStream
 void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStream_t s);
 void launch_slot8(const SlotArgs& a, hipStream_t s);
 void launch_level_plan(const LevelPlanArgs& a, hipStream_t s);
+void launch_level_rows(const LevelRowsArgs& a, hipStream_t s);
 void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
                            int32_t max_splits, int32_t wps, hipStream_t s);
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
@@ -129,6 +131,7 @@ void quant_max_cpu(const QuantArgs& a, double* out);
 void quant_cpu(const QuantArgs& a, const double* maxv);
 void slot8_cpu(const SlotArgs& a);
 void level_plan_cpu(const LevelPlanArgs& a);
+void level_rows_cpu(const LevelRowsArgs& a);
 void partition_cols_cpu(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs);
 void split_best_cpu(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa, int64_t f0,
                     int64_t* out);

@@ -375,8 +375,45 @@ struct SplitArgs {
   // (the thread-per-feature kernel skips them)
   const int32_t* wide;
   int32_t n_wide;
+  // optional: histogram row of node n (data-parallel levels: the reduce-scattered built rows and
+  // the subtracted siblings stay where they were written, see LevelRowsArgs); nullptr: row n
+  const int32_t* row_of;
 };
 constexpr int32_t kSplitWide = 16;
+
+FDX_HD int64_t split_row(const SplitArgs& a, int n) { return a.row_of ? a.row_of[n] : n; }
+
+// Data-parallel level rows (models/grower.py, DP levels of the device loop): the built nodes'
+// reduce-scattered partials stay where the collective left them (row bld_base + slot k) and the
+// larger sibling of slot k is written to row sub_base + k of the same buffer, so no histogram row
+// is ever copied into open-node order. Per built slot k: row_of[open index] for the split search,
+// and the subtraction triple as rows (dst, sib in this level's buffer; par in the previous
+// level's, through its row_of; nullptr: the previous level's rows are its open indices).
+struct LevelRowsArgs {
+  const int32_t* s2n;             // [nb] open index of slot k (tree.h level_plan)
+  const int32_t* sub_dst;         // [nb] open index of slot k's larger sibling (-1: none)
+  const int32_t* sub_par;         // [nb] open index of the parent in the previous level
+  const int32_t* prev_row_of;     // [previous n_open] or nullptr
+  int32_t nb;
+  int32_t bld_base, sub_base;
+  int32_t* row_of;                // [n_open] out
+  int32_t* dst_row;               // [nb] out (-1: no subtraction)
+  int32_t* par_row;
+  int32_t* sib_row;
+};
+
+FDX_HD void level_rows_slot(const LevelRowsArgs& a, int32_t k) {
+  const int32_t bld = a.bld_base + k, d = a.sub_dst[k];
+  a.row_of[a.s2n[k]] = bld;
+  a.sib_row[k] = bld;
+  if (d >= 0) {
+    a.row_of[d] = a.sub_base + k;
+    a.dst_row[k] = a.sub_base + k;
+    a.par_row[k] = a.prev_row_of ? a.prev_row_of[a.sub_par[k]] : a.sub_par[k];
+  } else {
+    a.dst_row[k] = a.par_row[k] = -1;
+  }
+}
 
 struct PartitionArgs {
   int32_t* row_node;              // [N]

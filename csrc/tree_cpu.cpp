@@ -340,7 +340,7 @@ void split_cpu(const SplitArgs& a) {
         use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <=
               a.feat_thr[n];
       if (use) {
-        const int64_t* hb = a.hist + ((int64_t)n * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
+        const int64_t* hb = a.hist + (split_row(a, n) * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
         gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], s0, s1, a.mode,
                                a.lambda_, a.min_child_weight, &bin, &l0, &l1);
       }
@@ -376,6 +376,9 @@ void split_best_cpu(const double* gain, const int32_t* bin, const int64_t* left,
 }
 
 void level_plan_cpu(const LevelPlanArgs& a) { level_plan(a); }
+void level_rows_cpu(const LevelRowsArgs& a) {
+  for (int32_t k = 0; k < a.nb; ++k) level_rows_slot(a, k);
+}
 
 void partition_cols_cpu(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs) {
   PartitionArgs d = a;

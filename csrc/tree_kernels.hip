@@ -745,7 +745,7 @@ __global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
   if (use && a.feat_thr)
     use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
   if (use) {
-    const int64_t* hb = a.hist + ((int64_t)n * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
+    const int64_t* hb = a.hist + (split_row(a, n) * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
     gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], ldexp(1.0, -a.kexp[0]),
                            ldexp(1.0, -a.kexp[1]), a.mode, a.lambda_, a.min_child_weight, &bin, &l0, &l1);
   }
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(256) void split_wide_kernel(SplitArgs a) {
   int best_b = -1;
   int64_t bl0 = 0, bl1 = 0;
   if (use) {
-    const int64_t* hb = a.hist + ((int64_t)n * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
+    const int64_t* hb = a.hist + (split_row(a, n) * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
     const int nb = a.nbins[f], zb = a.zbin[f];
     const int64_t T0 = a.totals[2 * n], T1 = a.totals[2 * n + 1];
     const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
@@ -1137,6 +1137,11 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
   }
 }
 
+__global__ __launch_bounds__(64) void level_rows_kernel(LevelRowsArgs a) {
+  const int32_t k = (int32_t)(blockIdx.x * 64 + threadIdx.x);
+  if (k < a.nb) level_rows_slot(a, k);
+}
+
 __global__ void level_plan_kernel(LevelPlanArgs a) {
   if (blockIdx.x != 0) return;
   level_plan_reset(a, (int32_t)threadIdx.x, (int32_t)blockDim.x);
@@ -1304,6 +1309,11 @@ void launch_split_best(const double* gain, const int32_t* bin, const int64_t* le
 void launch_partition(const PartitionArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(partition_default_kernel, dim3(grid_for((a.N + kPartRows - 1) / kPartRows)), dim3(256), 0, s, a);
   if (a.num_items > 0) hipLaunchKernelGGL(partition_column_kernel, dim3(a.num_items), dim3(256), 0, s, a);
+}
+
+void launch_level_rows(const LevelRowsArgs& a, hipStream_t s) {
+  if (a.nb <= 0) return;
+  hipLaunchKernelGGL(level_rows_kernel, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, s, a);
 }
 
 void launch_level_plan(const LevelPlanArgs& a, hipStream_t s) {

@@ -327,7 +327,7 @@ class RandomForestClassifier(_RFParams, Estimator):
         from ..utils.config import default_device
 
         dev = default_device()
-        nw = effective_workers(self.getOrDefault("numWorkers"), len(X), dev, nnz=X.nnz)
+        nw = effective_workers(self.getOrDefault("numWorkers"), len(X), dev, nnz=X.nnz, kind="rf")
         if nw > 1 and not D.is_dist():
             from ..parallel.estimator_dp import fit_data_parallel
 

@@ -15,14 +15,17 @@ moves on to another tree, so the kernels of different trees overlap on the devic
 depends only on (seed, tree index) and its own buffers, so the forest is bitwise the forest of
 one-at-a-time growth (tested on the host and the GPU).
 
-Data parallelism (BASELINE config 3, RF at DP=8): each lane's levels issue a reduce-scatter and an
-all-gather on the ONE communicator, so every rank must issue them in the same order. Alone, the
-driver advances "the first lane whose event completed", an order that depends on timing; under
-collectives it advances lanes strictly in FIFO order of their pending events (always the oldest),
-an order fixed by the tree shapes, which every rank computes identically from the same reduced
-histograms. The lanes' collectives then queue on the communicator's stream in the same sequence
-everywhere, and while one lane's collective is in flight the other lanes' kernels keep the GPU
-busy (a lone tree at DP=8 does 1/8 of the histogram work per level and is latency bound).
+Data parallelism (BASELINE config 3, RF at DP=8): the lanes are split into ``LANE_GROUPS`` groups
+that take turns. A group's turn advances every one of its trees by one level: the host waits for
+each tree's counts (refilling lanes whose tree finished), then ONE batched reduce-scatter and ONE
+all-gather (grower.LevelBatcher) carry the level histograms and best splits of all the group's
+trees -- 2 collectives per group-level instead of 2 per tree-level (500 trees x 5 levels: 5,000
+-> ~625 with 2 groups of 8), and a tree's root totals ride in its first reduce-scatter. While one
+group's collectives are in flight the other group's kernels keep the GPU busy. Turn order,
+lane order and refill order are functions of the tree shapes only, which every rank computes
+identically from the same reduced histograms, so every rank issues the same collective sequence.
+(Alone, the driver advances "the first lane whose event completed", an order that depends on
+timing and needs no agreement.)
 
 The shared read-only state the lanes read (the CSC work items and their wave order, the shard
 tables) is built on the caller's stream BEFORE the lanes fork from it, never lazily by whichever
@@ -41,7 +44,7 @@ from typing import Optional
 import torch
 
 from ..utils import tracing
-from .grower import GrowParams, Workspace, device_tree_steps
+from .grower import CollStep, GrowParams, LevelBatcher, Workspace, _Lane, device_tree_steps
 from .quantize import Quantized
 
 # 500 trees x depth 5 on 10M rows (profiles/r4/rf500_sweep_*.json): 4 lanes with 4 histogram
@@ -50,6 +53,8 @@ TREES_IN_FLIGHT = int(os.environ.get("FDX_RF_INFLIGHT", "16"))
 # histogram side streams per lane (grower.Workspace.run_concurrent): the lanes already overlap
 # whole trees, and every extra stream is another HW-queue mapping and cross-stream event per level
 LANE_HIST_STREAMS = int(os.environ.get("FDX_RF_LANE_STREAMS", "1"))
+# data parallelism: groups of lanes whose levels share one reduce-scatter + all-gather
+LANE_GROUPS = int(os.environ.get("FDX_RF_GROUPS", "2"))
 
 
 class ForestLanes:
@@ -96,6 +101,13 @@ def grow_forest_concurrent(Q: Quantized, lanes: ForestLanes, params: GrowParams,
         start = main.record_event()
         for s in lanes.streams:
             s.wait_event(start)
+    if use_coll and any(sh is not None for sh in shards):
+        out = _grow_batched(Q, lanes, params, tree_ids, label, weight, bootstrap, coll, shards,
+                            main if cuda else None)
+        if cuda:
+            for s in lanes.streams:
+                main.wait_stream(s)
+        return out
     todo = deque(tree_ids)
     out: dict = {}
     live: dict = {}                            # lane -> [tree id, steps, event]
@@ -141,4 +153,54 @@ def grow_forest_concurrent(Q: Quantized, lanes: ForestLanes, params: GrowParams,
     if cuda:
         for s in lanes.streams:
             main.wait_stream(s)
+    return [out[t] for t in tree_ids]
+
+
+def _grow_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tree_ids: list, label: torch.Tensor,
+                  weight: Optional[torch.Tensor], bootstrap: bool, coll, shards: list, coord) -> list:
+    """The data-parallel driver (module docstring): lane groups take turns; a turn waits for the
+    group's trees, refills finished lanes, and serves one batched level of collectives."""
+    nl = len(lanes.ws)
+    ng = max(1, min(LANE_GROUPS, nl))
+    groups = [list(range(g * nl // ng, (g + 1) * nl // ng)) for g in range(ng)]
+    batchers = [LevelBatcher(coll, shards[0].S, lanes.dev, coord) for _ in range(ng)]
+    todo = deque(tree_ids)
+    out: dict = {}
+    state: list = [None] * nl                  # lane -> _Lane (tid = tree id) or None
+
+    def start(i: int) -> None:
+        state[i] = None
+        if not todo:
+            return
+        t = todo.popleft()
+        with tracing.span("forest.tree", tree=t, lane=i), lanes.stream_ctx(i):
+            gen = device_tree_steps(Q, lanes.ws[i], params, t, None, None, weight, coll, shards[i], label=label,
+                                    bootstrap=bootstrap)
+            state[i] = _Lane(gen, next(gen), lanes.streams[i], t)
+
+    def resume(i: int) -> None:
+        ln = state[i]
+        ln.item.synchronize()
+        try:
+            ln.send(None)
+        except StopIteration as stop:
+            out[ln.tid] = stop.value
+            start(i)
+
+    for i in range(nl):
+        start(i)
+    turns = deque(range(ng))
+    while turns:
+        g = turns.popleft()
+        while True:          # every tree of the group up to its next collective step (or done)
+            waiting = [i for i in groups[g] if state[i] is not None and not isinstance(state[i].item, CollStep)]
+            if not waiting:
+                break
+            for i in waiting:
+                resume(i)
+        batchers[g].release()
+        live = [state[i] for i in groups[g] if state[i] is not None]
+        if live:
+            batchers[g].serve(live)
+            turns.append(g)
     return [out[t] for t in tree_ids]

@@ -123,6 +123,168 @@ class _CollTimer:
         else:
             LEVEL_STATS["coll_ms"] += (time.perf_counter() - self.b) * 1e3 * LEVEL_TIMING
         return False
+class CollStep:
+    """What a data-parallel level asks of its driver (``device_tree_steps`` yields these when it
+    has ``shards``), in this order per level:
+      ``alloc``  this level's histogram rows (``rows`` built nodes of width ``Bs`` bins, ``sub_rows``
+                 rows for the subtracted siblings, ``n_open`` best-split tuples, the root's local
+                 ``totals`` to sum) -> a :class:`LaneBufs` view into the batch's buffers;
+      ``rs``     the histograms are queued: reduce-scatter them;
+      ``ag``     the best-split tuples are queued: all-gather them -> [S, n_open, 5].
+    A :class:`LevelBatcher` serves the same step of every tree in flight with ONE collective, so
+    a forest's collective count is per batch-level, not per tree-level (SURVEY PAR-05: Spark
+    aggregates the nodes of many trees in one pass)."""
+
+    __slots__ = ("kind", "rows", "Bs", "n_open", "totals", "sub_rows")
+
+    def __init__(self, kind: str, rows: int = 0, Bs: int = 0, n_open: int = 0, totals=None, sub_rows: int = 0):
+        self.kind, self.rows, self.Bs, self.n_open, self.totals, self.sub_rows = kind, rows, Bs, n_open, totals, sub_rows
+
+
+class LaneBufs:
+    """One tree's share of a batched data-parallel level (LevelBatcher.serve). The send buffer is
+    shard-major ``target`` [S, R, Bs, 2]: the tree's built rows are rows [row0, row0 + rows) of
+    every shard chunk, so its histogram passes write with row stride Bs and shard stride R * Bs;
+    the root's local (g, h) totals ride in bin ``tot_bin`` of every chunk (the reduce-scatter then
+    sums them too: no separate all-reduce per tree). The reduced rows land in ``out`` [R + subs,
+    Bs, 2] (the collective writes rows [0, R)); rows [sub_base, sub_base + rows) take the tree's
+    subtracted siblings, so no histogram row is copied. ``ag_in`` [n_open, 5]: where the split
+    search writes the tree's best-split tuples for the batched all-gather."""
+
+    __slots__ = ("target", "row0", "rows", "R", "Bs", "tot_bin", "ag_in", "out", "sub_base")
+
+    def __init__(self, target, row0, rows, R, Bs, tot_bin, ag_in, out, sub_base):
+        self.target, self.row0, self.rows, self.R, self.Bs = target, row0, rows, R, Bs
+        self.tot_bin, self.ag_in, self.out, self.sub_base = tot_bin, ag_in, out, sub_base
+
+    @property
+    def shard_bins(self) -> int:
+        return self.R * self.Bs
+
+    def prepare(self, totals=None) -> torch.Tensor:
+        """Zero this tree's rows (its own stream), place the root totals; returns the [*, Bs, 2]
+        view the histogram passes write through (row 0 = this tree's first row of shard 0)."""
+        self.target[:, self.row0:self.row0 + self.rows].zero_()
+        if totals is not None:
+            self.target.view(self.target.shape[0], -1, 2)[:, self.tot_bin] = totals
+        return self.target.view(-1, self.Bs, 2)[self.row0:]
+
+    def mine(self) -> torch.Tensor:
+        return self.out[self.row0:self.row0 + self.rows]
+
+    def reduced_totals(self) -> torch.Tensor:
+        return self.out.view(-1, 2)[self.tot_bin]
+
+
+class _Lane:
+    """A tree in flight: its step generator, the step / event it is parked at, its stream."""
+
+    __slots__ = ("gen", "item", "stream", "tid")
+
+    def __init__(self, gen, item, stream, tid=None):
+        self.gen, self.item, self.stream, self.tid = gen, item, stream, tid
+
+    def send(self, value) -> None:
+        ctx = torch.cuda.stream(self.stream) if self.stream is not None else _NULL_CTX
+        with ctx:
+            self.item = self.gen.send(value)
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL_CTX = _NullCtx()
+
+
+class LevelBatcher:
+    """Serves the data-parallel collectives of a batch of trees in flight (each parked at an
+    ``alloc`` CollStep) with one reduce-scatter and one all-gather for the whole batch. Buffers
+    are allocated on the coordinator stream; each tree's kernels run on its own stream, joined to
+    the coordinator by events around the two collectives. The batch's buffers are held until
+    ``release()`` -- called by the driver once it has waited for every tree's next event, which
+    follows all of the tree's reads of them (so the caching allocator never hands them out early).
+    Every rank serves the same batches in the same order (the drivers' orders are functions of the
+    tree shapes, identical on every rank), so the collective sequences match."""
+
+    def __init__(self, coll, S: int, dev: torch.device, coord=None):
+        self.coll, self.S, self.dev = coll, int(S), dev
+        self.coord = coord if coord is not None else (torch.cuda.current_stream(dev) if dev.type == "cuda" else None)
+        self.hold = None
+        self.batches = 0
+
+    def release(self) -> None:
+        self.hold = None
+
+    def _ctx(self):
+        return torch.cuda.stream(self.coord) if self.coord is not None else _NULL_CTX
+
+    def _join_in(self, lanes) -> None:
+        if self.coord is None:
+            return
+        for ln in lanes:
+            if ln.stream is not None and ln.stream != self.coord:
+                self.coord.wait_stream(ln.stream)
+
+    def _join_out(self, lanes) -> None:
+        if self.coord is None:
+            return
+        ev = None
+        for ln in lanes:
+            if ln.stream is not None and ln.stream != self.coord:
+                if ev is None:
+                    ev = self.coord.record_event()
+                ln.stream.wait_event(ev)
+
+    def serve(self, lanes: list) -> None:
+        reqs = [ln.item for ln in lanes]
+        assert all(isinstance(r, CollStep) and r.kind == "alloc" for r in reqs), [getattr(r, "kind", r) for r in reqs]
+        S = self.S
+        Bs = max(max(r.Bs for r in reqs), 1)
+        nrows = sum(r.rows for r in reqs)
+        ntot = sum(1 for r in reqs if r.totals is not None)
+        R = nrows + (-(-ntot // Bs) if ntot else 0)
+        subs = sum(r.sub_rows for r in reqs)
+        nl = sum(r.n_open for r in reqs)
+        with self._ctx():
+            target = torch.empty((S, R, Bs, 2), dtype=torch.int64, device=self.dev)
+            out = torch.empty((R + subs, Bs, 2), dtype=torch.int64, device=self.dev)
+            ag_in = torch.empty((nl, 5), dtype=torch.int64, device=self.dev)
+        row0 = sub0 = l0 = t = 0
+        slots = []
+        for ln, r in zip(lanes, reqs):
+            tb = -1
+            if r.totals is not None:
+                tb = nrows * Bs + t
+                t += 1
+            bufs = LaneBufs(target, row0, r.rows, R, Bs, tb, ag_in[l0:l0 + r.n_open], out, R + sub0)
+            slots.append((l0, r.n_open))
+            row0 += r.rows
+            sub0 += r.sub_rows
+            l0 += r.n_open
+            ln.send(bufs)
+        assert all(isinstance(ln.item, CollStep) and ln.item.kind == "rs" for ln in lanes)
+        self._join_in(lanes)
+        with self._ctx(), tracing.span("tree.reduce_scatter", trees=len(lanes)), _CollTimer(self.dev):
+            self.coll.reduce_scatter(target, out=out[:R])
+        self._join_out(lanes)
+        for ln in lanes:
+            ln.send(None)
+        assert all(isinstance(ln.item, CollStep) and ln.item.kind == "ag" for ln in lanes)
+        self._join_in(lanes)
+        with self._ctx(), tracing.span("tree.all_gather", trees=len(lanes)), _CollTimer(self.dev):
+            allt = self.coll.all_gather(ag_in)                           # [S, sum n_open, 5]
+        self._join_out(lanes)
+        for ln, (a, n) in zip(lanes, slots):
+            ln.send(allt[:, a:a + n])
+        self.hold = (target, out, ag_in, allt)
+        self.batches += 1
+
+
 # row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
 # histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
 ROWHIST = os.environ.get("FDX_ROWHIST", "1") == "1"
@@ -149,6 +311,9 @@ RF_COMPACT = os.environ.get("FDX_RF_COMPACT", "auto")
 # per tree (FDX_DEVICE_LEVELS=0: host loop)
 DEVICE_LEVELS = os.environ.get("FDX_DEVICE_LEVELS", "1") != "0"
 PARTITION_WPS = int(os.environ.get("FDX_PARTITION_WPS", 256))  # blocks per column split (device partition)
+# debug: check on the host that every open node of a data-parallel level is built or subtracted
+# (its histogram row is then written before the split search reads it)
+LEVEL_CHECKS = os.environ.get("FDX_LEVEL_CHECKS", "0") == "1"
 
 
 @dataclass
@@ -431,6 +596,18 @@ class FeatureShards:
         """Zeroed shard-major partial histograms [S, nb, Bs, 2] of a DP level."""
         return torch.zeros((self.S, nb, self.Bs, 2), dtype=torch.int64, device=dev)
 
+    def boff_batched(self, shard_bins: int, local: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """[Fa+1] bin offsets into a batched level's send buffer (LaneBufs): feature f of shard s
+        at s * shard_bins + local(f) (+ the row's slot * Bs in the kernels). ``local``: a compact
+        level's per-level offsets (not cached); None: the full layout's (cached per stride)."""
+        if local is not None:
+            return torch.add(local, self._shard_of, alpha=int(shard_bins))
+        key = ("b", int(shard_bins))
+        t = self._boffp.get(key)
+        if t is None:
+            t = self._boffp[key] = (self._shard_of * int(shard_bins) + self._local).contiguous()
+        return t
+
     def sample_compact(self, C, p: int, seed: int, tree: int, nodes: torch.Tensor, F: int, k: int,
                        fid_orig: torch.Tensor) -> None:
         """Feature sample of the open nodes ``nodes`` (-1 padding allowed) into parity-``p``
@@ -455,16 +632,23 @@ class FeatureShards:
 
 
 def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, params, feat_thr, tree_index, Fa,
-                 f0, node_tree=None, cache: Optional[dict] = None):
+                 f0, node_tree=None, cache: Optional[dict] = None, out: Optional[torch.Tensor] = None,
+                 row_of: Optional[torch.Tensor] = None):
     """Per node: (gain float64, feature (+f0) int64, bin int64, left sums int64 [2]) of the best
     split over Fa features of ``hist`` [nodes, boff[Fa], 2]; gain -inf without a valid candidate.
     Returned as one int64 tensor [nodes, 5] (gain bit-cast) for a single device->host copy.
     ``cache`` (a workspace dict): the per-(node, feature) scratch is allocated once per level
-    shape and reused (stream order: the previous level's split kernels are done with it)."""
+    shape and reused (stream order: the previous level's split kernels are done with it).
+    ``out``: write the tuples there (a tree's rows of a batched all-gather). ``row_of``: the
+    histogram row of each node (data-parallel levels; default row = node index). (The kernels
+    take the row stride from hist.size(1), never from boff[Fa]: a compact RF level's boff[Fa]
+    is the next shard's first offset, not this shard's end.)"""
     dev = hist.device
     nl = int(node_ids.numel())
     if Fa == 0:
-        out = torch.zeros((nl, 5), dtype=torch.int64, device=dev)
+        if out is None:
+            out = torch.empty((nl, 5), dtype=torch.int64, device=dev)
+        out.zero_()
         out[:, 0] = torch.tensor(NEG_INF, dtype=torch.float64).view(torch.int64)
         out[:, 1:3] = -1
         return out
@@ -487,10 +671,11 @@ def _best_splits(C, hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, p
         wide = memo[1]
     C.tree_split_find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, kexp, int(params.mode),
                       float(params.lambda_), float(params.min_child), feat_thr, int(params.seed), int(tree_index),
-                      out_gain, out_bin, out_left, node_tree, wide)
+                      out_gain, out_bin, out_left, node_tree, wide, row_of)
     # best gain per node, ties to the lowest feature index (deterministic whatever the batch shape):
     # one native reduction instead of ~9 small torch launches per level
-    out = torch.empty((nl, 5), dtype=torch.int64, device=dev)
+    if out is None:
+        out = torch.empty((nl, 5), dtype=torch.int64, device=dev)
     if nl:
         C.tree_split_best(out_gain, out_bin, out_left, int(f0), out)
     return out
@@ -873,6 +1058,10 @@ class LevelState:
         self.default_child, self.node_slot = i32(M), i32(M)
         self.cs = [i32(cap) for _ in range(5)]          # feat, default, other, bin, left_default
         self.s2n, self.sub_dst, self.sub_par, self.sub_sib = i32(cap), i32(cap), i32(cap), i32(cap)
+        # data-parallel levels (tree.h LevelRowsArgs): histogram row per open node (level parity)
+        # and the subtraction triples as rows
+        self.row_of = [i32(cap), i32(cap)]
+        self.dst_row, self.par_row, self.sib_row = i32(cap), i32(cap), i32(cap)
         self.node_dense = self.hot_row = None
         if Q.dense is not None and PARTITION_DENSE:
             hot_row = np.full(Q.Fa, -1, dtype=np.int32)
@@ -886,15 +1075,23 @@ def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index
                      shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
                      bootstrap: bool = False, deferred: bool = False, on_first_wait=None):
     """One tree through :func:`device_tree_steps`, waiting on each event it yields."""
+    batcher = LevelBatcher(coll, shards.S, Q.device) if shards is not None else None
     return drive(device_tree_steps(Q, ws, params, tree_index, g, h, weight, coll, shards, label, bootstrap,
-                                   deferred, on_first_wait))
+                                   deferred, on_first_wait), batcher)
 
 
-def drive(steps):
-    """Run a step generator to its end, synchronising every event it yields; returns its value."""
+def drive(steps, batcher: Optional[LevelBatcher] = None):
+    """Run a step generator to its end, synchronising every event it yields and serving its
+    data-parallel CollSteps with ``batcher`` (a batch of one tree); returns its value."""
     try:
+        lane = _Lane(steps, next(steps), None)
         while True:
-            next(steps).synchronize()
+            if isinstance(lane.item, CollStep):
+                batcher.serve([lane])
+            else:
+                lane.item.synchronize()
+                batcher is not None and batcher.release()
+                lane.item = steps.send(None)
     except StopIteration as stop:
         return stop.value
 
@@ -942,15 +1139,17 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         else:
             C.tree_quant(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, 1, None, ws.rowdig,
                          ws.kexp, ws.totals, ws.digp, Q.row0)
-    tot = coll.sum(ws.totals) if coll is not None else ws.totals
-    # root: node 0, open list [0] with the exact totals (no host round trip)
+    # root: node 0, open list [0] with the exact totals (no host round trip); under data
+    # parallelism the totals are summed by the root level's reduce-scatter (LaneBufs.tot_bin)
     st.arena.copy_(st.arena_init, non_blocking=True)
-    st.stats[0].copy_(tot)
     st.open[0][:1].zero_()
-    st.totals[0][:1].copy_(tot[None])
+    if shards is None:
+        tot = coll.sum(ws.totals) if coll is not None else ws.totals
+        st.stats[0].copy_(tot)
+        st.totals[0][:1].copy_(tot[None])
     TB = Q.TB
     n_open, n_build = 1, 1
-    prev_hist = None
+    prev_hist = prev_row_of = None
     # the next level's zeroed histograms (at most 2 open nodes per open node) are queued before
     # the host waits for its counts, so the fill runs while the host sizes that level
     pre_hist = None
@@ -990,6 +1189,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             C.tree_rf_sample(seed, int(tree_index), open_d, int(Q.num_features), int(params.feat_k), Q.fid_orig,
                              feat_thr, feat_mask, None)
         split_boff = shards.boff if shards is not None else None
+        bufs = None
         if shards is None:
             if pre_hist is not None and pre_hist.shape[0] >= n_open:
                 cur_hist = hist_target = pre_hist[:n_open]
@@ -997,16 +1197,18 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 cur_hist = hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
             pre_hist = None
             h_boff, h_stride = Q.boff, TB
-        elif compact:
-            # only the sampled features' bins travel (FeatureShards.sample_compact)
-            rs_buf = torch.zeros((shards.S, n_build, Bs_c, 2), dtype=torch.int64, device=dev)
-            hist_target = rs_buf.view(shards.S * n_build, Bs_c, 2)
-            h_boff, h_stride = torch.add(local_c, shards._shard_of, alpha=n_build * Bs_c), Bs_c
-            split_boff = local_c[shards.f0: shards.f0 + shards.Fa + 1]
-        else:   # local partials of the built nodes, shard-major (reduce-scattered as they stand)
-            rs_buf = shards.target(n_build, dev)
-            hist_target = rs_buf.view(shards.S * n_build, shards.Bs, 2)
-            h_boff, h_stride = shards.boff_packed(n_build), shards.Bs
+        else:
+            # the built nodes' local partials go straight into this tree's rows of the batch's
+            # shard-major send buffer (LaneBufs); compact levels send only the sampled features'
+            # bins (FeatureShards.sample_compact)
+            subs = 0 if (build_all or d == 0) else n_build
+            bufs = yield CollStep("alloc", rows=n_build, Bs=Bs_c if compact else shards.Bs, n_open=n_open,
+                                  totals=ws.totals if d == 0 else None, sub_rows=subs)
+            hist_target = bufs.prepare(ws.totals if d == 0 else None)
+            h_boff = shards.boff_batched(bufs.shard_bins, local_c if compact else None)
+            h_stride = bufs.Bs
+            if compact:
+                split_boff = local_c[shards.f0: shards.f0 + shards.Fa + 1]
         with tracing.span("tree.hist"):
             use_dense = Q.dense is not None and d <= DENSE_MAX_DEPTH and not build_all
             slot8 = None
@@ -1029,7 +1231,6 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 s2n = st.s2n[:n_build]
             else:
                 s2n = st.one.new_zeros(1)
-            bidx = s2n
             if shards is not None:      # slot k -> partial row k
                 s2n = ws.iota(n_build)
             ct = pass_ct(np_, n_build)
@@ -1037,7 +1238,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             # (the CSC items are built on first use: the row-group engine never touches them)
             sel_groups = None
             if rg is not None:
-                shard_args = (shards.bin_lo, n_build * shards.Bs) if shards is not None else (None, 0)
+                shard_args = (shards.bin_lo, bufs.shard_bins) if shards is not None else (None, 0)
                 if d == 0:
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, None, 1, rg.gmode,
                                    rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG, **rg.em_args())
@@ -1082,32 +1283,45 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                             C.tree_hist_dense, Q.dense, ws.digp, ws.rowdig, None if d == 0 else ws.slot8_pad,
                             gfid, gden, h_boff, Q.nbins, s2n, hist_target, h_stride, Q.n_rows, rr, bt, ct, np_))
             ws.run_concurrent(launches)
+        row_of = None
         if shards is not None:
-            with tracing.span("tree.reduce_scatter"), _CollTimer(dev):
-                mine = coll.reduce_scatter(rs_buf)                             # [n_build, Bs, 2]
-                if build_all or d == 0:
-                    # every open node built, slot k = open node k (tree.h level_plan): the reduced
-                    # rows ARE the level's histograms (stride Bs, read in place by the split search)
-                    cur_hist = mine
-                else:
-                    # built rows to their open-node rows; the subtraction fills all the others
-                    cur_hist = torch.empty((n_open, shards.Bs, 2), dtype=torch.int64, device=dev)
-                    cur_hist.index_copy_(0, bidx.to(torch.int64), mine)
+            yield CollStep("rs")                  # (the batch's reduce-scatter, LevelBatcher.serve)
+            if d == 0:
+                tot = bufs.reduced_totals()
+                st.stats[0].copy_(tot)
+                totals_d.copy_(tot[None])
+            if build_all or d == 0:
+                # every open node built, slot k = open node k (tree.h level_plan): the reduced
+                # rows ARE the level's histograms (stride Bs, read in place by the split search)
+                cur_hist = bufs.mine()
+            else:
+                # the built rows stay where the collective wrote them and the subtraction fills
+                # rows after them: per open node its row (tree.h LevelRowsArgs), no copy
+                row_of = st.row_of[cur][:n_open]
+                C.tree_level_rows(st.s2n, st.sub_dst, st.sub_par, prev_row_of, n_build, bufs.row0, bufs.sub_base,
+                                  st.row_of[cur], st.dst_row, st.par_row, st.sib_row)
+                if LEVEL_CHECKS:
+                    n_sub = int((st.sub_dst[:n_build] >= 0).sum())
+                    assert n_build + n_sub == n_open, (d, n_build, n_sub, n_open)
+                cur_hist = bufs.out
         if d > 0 and not build_all:
-            C.tree_hist_subtract(prev_hist, cur_hist, st.sub_dst[:n_build], st.sub_par[:n_build],
-                                 st.sub_sib[:n_build], TB if shards is None else shards.Bs)
+            if shards is None:
+                C.tree_hist_subtract(prev_hist, cur_hist, st.sub_dst[:n_build], st.sub_par[:n_build],
+                                     st.sub_sib[:n_build], TB)
+            else:
+                C.tree_hist_subtract(prev_hist, cur_hist, st.dst_row[:n_build], st.par_row[:n_build],
+                                     st.sib_row[:n_build], bufs.Bs)
         with tracing.span("tree.split"):
             if shards is None:
                 packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
                                       params, feat_thr, tree_index, Q.Fa, 0, cache=ws.split_cache)
             else:
-                mine = _best_splits(C, cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig,
-                                    open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0,
-                                    cache=ws.split_cache)
-                with _CollTimer(dev):
-                    # [S, n_open, 5]: tree_level_plan takes the best over shards per node (ties
-                    # to the lowest shard = the lowest feature), no separate argmax launches
-                    packed = coll.all_gather(mine)
+                _best_splits(C, cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig,
+                             open_d, ws.kexp, params, feat_thr, tree_index, shards.Fa, shards.f0,
+                             cache=ws.split_cache, out=bufs.ag_in, row_of=row_of)
+                # [S, n_open, 5] (the batch's all-gather): tree_level_plan takes the best over
+                # shards per node (ties to the lowest shard = the lowest feature)
+                packed = yield CollStep("ag")
         nxt = 1 - cur
         C.tree_level_plan(packed, n_open, d, params.max_depth, int(params.mode), build_all, ws.kexp,
                           float(params.min_gain), Q.zbin, st.hot_row,
@@ -1126,6 +1340,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         if shards is None and d + 1 < params.max_depth:
             pre_hist = torch.zeros((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
         prev_hist = cur_hist
+        prev_row_of = row_of
     if on_first_wait is not None:          # (a one-level tree) the previous table first
         on_first_wait()
     # one read of the node table per tree: the arena (table + exponents) in one D2H copy, one wait

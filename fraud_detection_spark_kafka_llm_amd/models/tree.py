@@ -116,6 +116,12 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
     # PAR-05: several trees in flight, each on its own stream (models/forest_batch.py); under data
     # parallelism the lanes advance in FIFO order, so every rank issues one collective sequence
     inflight = max(1, forest_batch.TREES_IN_FLIGHT)
+    if Q.device.type == "cuda" and inflight > 1:
+        # each lane holds a workspace of ~27 B per row (utils/memory.py): no more lanes than half
+        # the free HBM holds
+        from ..utils.memory import rf_lanes_that_fit
+
+        inflight = rf_lanes_that_fit(Q.n_rows, inflight, torch.cuda.mem_get_info(Q.device)[0])
     lanes = None
     if inflight > 1 and num_trees - len(trees) > 1 and device_levels_ok(params, w):
         lanes = ForestLanes(Q, min(inflight, num_trees - len(trees)), ws)

@@ -162,22 +162,32 @@ def total_calls() -> int:
     return int(sum(CALLS.values()))
 
 
-def reduce_scatter(x: torch.Tensor) -> torch.Tensor:
+def reduce_scatter(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Sum ``x`` [world, ...] over ranks and return this rank's slice [...] with
     ``reduce_scatter_tensor``: each rank sends (N-1)/N of the buffer instead of an all-reduce's
     2(N-1)/N. The same call runs on RCCL (device tensors) and on gloo (host copies), so the CPU
-    multi-process tests exercise the code path the GPUs take."""
+    multi-process tests exercise the code path the GPUs take. ``out`` (contiguous, x[0]'s size):
+    the collective writes there (a prefix of a larger level buffer, no copy on RCCL)."""
     if not _comm():
-        return x[0]
+        if out is None:
+            return x[0]
+        return out.view(x.shape[1:]).copy_(x[0])
     x = x.contiguous()
     BYTES["reduce_scatter"] += x.numel() * x.element_size()
     CALLS["reduce_scatter"] += 1
     xc, moved = _on_comm_device(x)
     # flat buffers (gloo wants the concatenated form; RCCL takes either)
-    out = torch.empty(xc.numel() // xc.shape[0], dtype=xc.dtype, device=xc.device)
-    dist.reduce_scatter_tensor(out, xc.view(-1))
-    out = out.view(xc.shape[1:])
-    return out.to(x.device) if moved else out
+    n = xc.numel() // xc.shape[0]
+    if out is not None and not moved:
+        assert out.is_contiguous() and out.numel() == n and out.dtype == xc.dtype
+        dist.reduce_scatter_tensor(out.view(-1), xc.view(-1))
+        return out.view(xc.shape[1:])
+    res = torch.empty(n, dtype=xc.dtype, device=xc.device)
+    dist.reduce_scatter_tensor(res, xc.view(-1))
+    res = res.view(xc.shape[1:])
+    if out is not None:
+        return out.view(xc.shape[1:]).copy_(res)
+    return res.to(x.device) if moved else res
 
 
 def all_gather(x: torch.Tensor) -> torch.Tensor:
@@ -204,8 +214,10 @@ class Collectives:
         self.world = world_size()
         self.rank = rank()
 
-    def reduce_scatter(self, x):
-        return reduce_scatter(x) if self.active else x[0]
+    def reduce_scatter(self, x, out=None):
+        if self.active:
+            return reduce_scatter(x, out)
+        return x[0] if out is None else out.view(x.shape[1:]).copy_(x[0])
 
     def all_gather(self, x):
         return all_gather(x) if self.active else x.unsqueeze(0)

@@ -103,12 +103,13 @@ def _resolve_device(device) -> torch.device:
     return torch.device(device) if device is not None else default_device()
 
 
-def effective_workers(num_workers: int, n_rows: int, device=None, nnz: int = 0) -> int:
+def effective_workers(num_workers: int, n_rows: int, device=None, nnz: int = 0, kind: str = "gbdt") -> int:
     """Rank processes worth launching: one per GPU at most when GPUs are used (never several
     ranks on one device), and none below ``FDX_DP_MIN_ROWS`` rows per rank (default 100000) —
     a process launch costs more than training such a shard, and the model is bitwise the same
     either way (exact histograms). With ``nnz`` given on a GPU, at least as many ranks as the
-    HBM sizing rule needs for every shard to fit (utils/memory.py max_rows_per_gpu)."""
+    HBM sizing rule needs for every shard to fit (utils/memory.py max_rows_per_gpu; ``kind`` "rf":
+    with a workspace per tree in flight)."""
     n = int(num_workers)
     cuda = _resolve_device(device).type == "cuda"
     if cuda:
@@ -119,7 +120,12 @@ def effective_workers(num_workers: int, n_rows: int, device=None, nnz: int = 0) 
     if cuda and nnz > 0:
         from ..utils.memory import min_workers
 
-        need = min_workers(n_rows, nnz, _resolve_device(device))
+        lanes = 0
+        if kind == "rf":
+            from ..models import forest_batch
+
+            lanes = max(1, forest_batch.TREES_IN_FLIGHT)
+        need = min_workers(n_rows, nnz, _resolve_device(device), rf_lanes=lanes)
         if need > n:
             n = min(need, max(1, torch.cuda.device_count()))
     return max(1, n)

@@ -256,6 +256,14 @@ class _ScoreLoop:
             self.finish()
 
 
+def single_host_group() -> bool:
+    """A consumer group's scoring processes share POSIX shared-memory segments and abstract Unix
+    sockets, which exist on one host only: every rank of the job must be on this node
+    (LOCAL_WORLD_SIZE == WORLD_SIZE under torchrun)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+
+
 class GroupRendezvous:
     """Rank 0 <-> peer scoring processes: the group's segment config and the peers' socket names
     through a key-value store (the process group's TCPStore under torchrun). ``key`` must be the
@@ -290,8 +298,32 @@ class GroupRendezvous:
     def publish_socket(self, name: str) -> None:
         self.store.set(f"{self.key}/sock/{self.rank}", name)
 
+    def publish_socket_error(self, why: str) -> None:
+        """A peer that failed to start says so in its socket key, so the coordinator's wait ends
+        at once (instead of at the rendezvous timeout)."""
+        self.store.set(f"{self.key}/sock/{self.rank}", "!" + why)
+
     def sockets(self) -> list:
-        return [self._wait(f"{self.key}/sock/{r}").decode() for r in range(1, self.world)]
+        """Every peer's socket name (waits for each); raises if a peer published a start error."""
+        vals = [self._wait(f"{self.key}/sock/{r}").decode() for r in range(1, self.world)]
+        errs = [f"rank {r}: {v[1:]}" for r, v in enumerate(vals, 1) if v.startswith("!")]
+        if errs:
+            raise RuntimeError("scoring peers failed to start: " + "; ".join(errs))
+        return vals
+
+    def published_sockets(self) -> list:
+        """The socket names published so far (no waiting; start errors skipped)."""
+        out = []
+        for r in range(1, self.world):
+            k = f"{self.key}/sock/{r}"
+            try:
+                if self.store.check([k]):
+                    v = self.store.get(k).decode()
+                    if not v.startswith("!"):
+                        out.append(v)
+            except Exception:                      # noqa: BLE001 (best effort)
+                pass
+        return out
 
     def publish_stats(self, stats: dict) -> None:
         self.store.set(f"{self.key}/stats/{self.rank}", json.dumps(stats))
@@ -387,7 +419,9 @@ class ConsumerGroup:
             if not self._published:
                 self.rdv.publish_config({"error": why})
                 return
-            for name in self.peer_sockets:
+            # every peer that has published its socket so far (also when the wait for the others
+            # is what failed); peers that publish later find the clients gone and time out
+            for name in self.peer_sockets or self.rdv.published_sockets():
                 try:
                     with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as s:
                         s.settimeout(5.0)
@@ -504,10 +538,10 @@ class ScorerPeer:
         if "error" in cfg:
             self.error = cfg["error"]
             return
-        self.lay = cfg["layout"]
-        dev = getattr(scorer, "dev", None)
-        self.register = (dev is not None and dev.type == "cuda") if register is None else register
         try:
+            self.lay = cfg["layout"]
+            dev = getattr(scorer, "dev", None)
+            self.register = (dev is not None and dev.type == "cuda") if register is None else register
             for c, name in enumerate(cfg["shm"]):
                 cl = _Client(c, _attach(name), self.lay)
                 self.clients.append(cl)
@@ -518,7 +552,9 @@ class ScorerPeer:
             self.listener.bind("\0" + self.name)
             self.listener.listen(len(self.clients) + 4)
             self.listener.settimeout(accept_timeout_s)
-        except BaseException:
+        except BaseException as e:
+            # the coordinator waits for this peer's socket key: answer with the error
+            rendezvous.publish_socket_error(f"{type(e).__name__}: {e}")
             self.close()
             raise
         rendezvous.publish_socket(self.name)

@@ -91,6 +91,11 @@ def main(argv=None) -> int:
 
     ranks = int(os.environ.get("WORLD_SIZE", "1"))
     if ranks > 1 and args.group_clients > 0:
+        from .group import single_host_group
+
+        if not single_host_group():
+            raise SystemExit("--group-clients under torchrun needs every rank on one host "
+                             "(LOCAL_WORLD_SIZE != WORLD_SIZE): the group shares memory segments and Unix sockets")
         D.init_from_env("gloo")                 # the group's rendezvous store; no device collective
         devices = [torch.device("cuda", D.local_rank() % torch.cuda.device_count())] \
             if torch.cuda.is_available() else [torch.device("cpu")]

@@ -51,6 +51,9 @@ CHUNK_SCRATCH_BYTES = 4.0   # fused featurizer CSR scratch per text byte (scorin
 CHUNK_ENTRY_TEMP = 48.0     # per chunk entry: compaction int64 step + position + gathered entries,
                             # and the chunk's radix-sort temporaries
 LEVEL_HIST_BYTES = 16.0     # (g, h) int64 sums per bin per node built in one level
+RF_LANE_ROW_BYTES = 27.0    # RF: per tree in flight (models/forest_batch.py lanes), its workspace:
+                            # digit words, masked digits, row -> node, packed row state, slots
+                            # (~0.27 GB per lane at 10M rows, profiles/r4/rf500_sweep_*.json)
 DEFAULT_HOT_FEATURES = 145  # dense-path features (>= 10 % of rows) of the bench dialogue corpus
 DEFAULT_GROUPS = 11         # row groups of 8192 bins (bench corpus: ~90K bins over 2^18 buckets)
 DEFAULT_BUILT_NODES = 32    # nodes built in the widest level (depth 6: 2^5)
@@ -74,11 +77,25 @@ def featurize_bytes(rows: int, nnz: int, text_bytes_per_row: float = DEFAULT_BYT
 
 def training_bytes(rows: int, nnz: int, hot_features: int = DEFAULT_HOT_FEATURES, total_bins: int = 0,
                    built_nodes: int = DEFAULT_BUILT_NODES, groups: int = DEFAULT_GROUPS,
-                   sparse_frac: float = DEFAULT_SPARSE_FRAC) -> float:
-    """Peak bytes of training (GBDT, row-group engine) on ``rows`` rows with ``nnz`` entries."""
+                   sparse_frac: float = DEFAULT_SPARSE_FRAC, rf_lanes: int = 0) -> float:
+    """Peak bytes of training (GBDT, row-group engine) on ``rows`` rows with ``nnz`` entries.
+    ``rf_lanes`` > 0: a RandomForest with that many trees in flight instead (its CSC work items
+    and a workspace per lane on top of the shared state)."""
     per_entry = CSR_BYTES * CSR_SLACK + ORDER_BYTES + BIN_BYTES + RG_ENTRY_BYTES + RG_EROW_BYTES * sparse_frac
     per_row = ROW_BYTES + 4.0 * groups + hot_features + LEVEL_ROW_BYTES
+    if rf_lanes > 0:
+        per_entry += ORDER_BYTES
+        per_row += RF_LANE_ROW_BYTES * rf_lanes
     return per_entry * nnz + per_row * rows + LEVEL_HIST_BYTES * total_bins * built_nodes * 2
+
+
+def rf_lanes_that_fit(rows: int, want: int, free_bytes: int, headroom: float = 0.5) -> int:
+    """Trees in flight whose workspaces fit ``headroom`` of ``free_bytes`` (at least 1, at most
+    ``want``): the cap models/tree.fit_forest applies before building its lanes."""
+    if free_bytes <= 0 or rows <= 0:
+        return max(1, want)
+    per = RF_LANE_ROW_BYTES * rows
+    return int(max(1, min(want, (free_bytes * headroom) // max(per, 1.0))))
 
 
 def pipeline_bytes(rows: int, nnz: int, **kw) -> float:
@@ -122,11 +139,12 @@ def max_rows_per_gpu(nnz_per_row: float, device=None, budget_bytes: Optional[int
     return lo
 
 
-def min_workers(rows: int, nnz: int, device=None, budget_bytes: Optional[int] = None) -> int:
-    """Fewest equal row shards that each fit one GPU (1 without a device budget)."""
+def min_workers(rows: int, nnz: int, device=None, budget_bytes: Optional[int] = None, rf_lanes: int = 0) -> int:
+    """Fewest equal row shards that each fit one GPU (1 without a device budget); ``rf_lanes``:
+    size for a RandomForest with that many trees in flight (training_bytes)."""
     if rows <= 0:
         return 1
-    cap = max_rows_per_gpu(nnz / rows, device, budget_bytes)
+    cap = max_rows_per_gpu(nnz / rows, device, budget_bytes, **({"rf_lanes": rf_lanes} if rf_lanes else {}))
     if cap <= 0:
         return 1
     return max(1, math.ceil(rows / cap))

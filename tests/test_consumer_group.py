@@ -215,3 +215,56 @@ def test_gpu_group_two_rank_processes_share_the_topic(agent, tmp_path):
         i = int(key.decode()[3:])
         rec = json.loads(val)
         assert rec["prediction"] == float(pred[i]) and abs(rec["confidence"] - float(p1[i])) <= 1e-12
+
+
+def _group_rank_peer_fails(rank, world, model_path):
+    """Rank 1's ScorerPeer fails while mapping the segments: it publishes the error, so rank 0's
+    ConsumerGroup fails at once (not at the rendezvous timeout) and releases everything."""
+    import time
+
+    import torch
+
+    agent = ClassificationAgent(model_path, llm=StubLLM(), device="cpu")
+    fp = agent.fused
+    sc = make_scorer(fp.spec(True), fp.idf.idf, fp.model.scorer(), torch.device("cpu"), max_docs=64,
+                     max_bytes=64 * 4096, depth=2)
+    rdv = G.GroupRendezvous.from_process_group("test-fail", timeout_s=300.0)
+    t0 = time.perf_counter()
+    if rank == 0:
+        try:
+            with G.ConsumerGroup(sc, fp.model.postprocess_numpy, 2, batch_max=64, max_bytes=64 * 4096,
+                                 confluent=False, rendezvous=rdv):
+                return {"error": None}
+        except RuntimeError as e:
+            return {"error": str(e), "sec": time.perf_counter() - t0}
+
+    def boom(name):
+        raise OSError("injected attach failure")
+
+    G._attach = boom
+    try:
+        G.ScorerPeer(sc, fp.model.postprocess_numpy, rdv)
+    except OSError as e:
+        return {"peer_error": str(e)}
+    return {"peer_error": None}
+
+
+def test_group_peer_start_failure_fails_fast(agent, tmp_path):
+    """a peer that fails before publishing its socket no longer stalls the coordinator
+    for the whole rendezvous timeout."""
+    from fraud_detection_spark_kafka_llm_amd.parallel.launch import spawn
+
+    path = tmp_path / "model"
+    agent.model.save(str(path))
+    r0, r1 = spawn(_group_rank_peer_fails, 2, str(path), backend="gloo")
+    assert r1["peer_error"] == "injected attach failure"
+    assert "failed to start" in r0["error"] and "injected attach failure" in r0["error"]
+    assert r0["sec"] < 60
+
+
+def test_single_host_group_check(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert G.single_host_group()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert not G.single_host_group()

@@ -30,3 +30,21 @@ def test_effective_workers_raises_ranks_when_a_shard_would_not_fit(monkeypatch):
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
     assert estimator_dp.effective_workers(1, rows, "cuda:0", nnz=rows * 100) == 2   # capped at the GPUs
 
+
+
+def test_rf_lanes_enter_the_sizing_rule():
+    """RF trains with several trees in flight, each with its own ~27 B/row workspace: a shard that
+    fits the GBDT rule can need more ranks as a 16-lane forest, and fit_forest caps
+    its lanes to half the free memory."""
+    from fraud_detection_spark_kafka_llm_amd.utils import memory as M
+
+    rows, nnz = 100_000_000, 110 * 100_000_000
+    g = M.training_bytes(rows, nnz)
+    r = M.training_bytes(rows, nnz, rf_lanes=16)
+    assert r - g >= 16 * M.RF_LANE_ROW_BYTES * rows
+    budget = int(g * 1.05)
+    assert M.min_workers(rows, nnz, budget_bytes=budget) == 1
+    assert M.min_workers(rows, nnz, budget_bytes=budget, rf_lanes=16) >= 2
+    assert M.rf_lanes_that_fit(10_000_000, 16, 200 * 2 ** 30) == 16
+    assert M.rf_lanes_that_fit(10_000_000, 16, 2 * 2 ** 30) == 3
+    assert M.rf_lanes_that_fit(10_000_000, 16, 0) == 16          # no budget known (CPU)
