@@ -13,12 +13,12 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      scores straight into pinned host memory; the host then applies the sigmoid/threshold. The
      copy of step i+1 overlaps the kernel of step i. ``value`` = dialogues/s summed over all ranks
      (weak scaling: fixed micro-batch per GPU).
-  1b. RandomForest training (BASELINE config 3) — RandomForestClassifier(500 trees, depth 5,
+  3. RandomForest training (BASELINE config 3) — RandomForestClassifier(500 trees, depth 5,
      featureSubsetStrategy sqrt = ceil(sqrt(2^18)) features per node, Poisson(1) bootstrap, 32
      bins) on the SAME row-sharded 10M-row TF-IDF features (features are fitted once and shared, as
      train.py does; the reference refits them per model): ``rf_train_sec`` (max over ranks) =
      quantisation to 32 bins + 500 trees with per-level histogram reduce-scatter under DP.
-  3. Kafka end-to-end (BASELINE config 5) — an in-memory broker topic with 3 partitions of
+  4. Kafka end-to-end (BASELINE config 5) — an in-memory broker topic with 3 partitions of
      ``{"text": ...}`` JSON records -> StreamingEngine (one reader thread per partition, native JSON
      extraction into the pinned ring, GPU scoring, native output encoding, async produce, commits
      gated on delivery callbacks). ``kafka_dialogues_per_s``: a pre-filled topic drained end to end
@@ -33,12 +33,16 @@ Per rank (one process per MI355X, RCCL over xGMI when N > 1):
      device; no process opens another rank's GPU); ``..._explain_*``: the same latency run with
      the LLM-explain stub on every 10th record. ``kafka_multi_gpu_*``: the same N scoring
      processes fed by columnar clients (``..._scorer_procs`` = N, batches per scoring process).
+Phases 3 and 4 run after the headline (1, 2 and the single-dialogue latency) is measured, each
+under a PhaseGuard: a failure is reported as ``rf_error`` / ``kafka_error`` in the record and a
+hang is cut off after ``--phase-timeout`` s with the record printed as it stands.
 Data is synthetic (the reference dataset is not available) with random-init-free trained trees.
 Before the timed training, an untimed 2-tree fit on 65,536 rows loads the kernels' code objects
 (lazily loaded on first launch by ROCm) and warms the allocators (``gbdt_warmup_sec_untimed``).
 Compute dtype: the GBDT histograms are exact integer sums (gradients quantised to 2^-k with k
-from the all-reduced max, i8 MFMA digit planes, int64 accumulation) — at least fp32-accurate and
-bitwise reproducible; gains, leaves and scores are fp64; text is bytes. Reported as "fp32".
+from the all-reduced max, accumulated as int64 by LDS atomics in the row-group kernel,
+csrc/row_kernels.hip) — at least fp32-accurate and bitwise reproducible; gains, leaves and scores
+are fp64; text is bytes. Reported as "fp32".
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
   N > 1 is launched by the driver via torch.distributed.run (RANK/WORLD_SIZE/MASTER_* in env).
@@ -49,7 +53,9 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
+import traceback
 
 import numpy as np
 import torch
@@ -89,6 +95,57 @@ def sync_all(dev):
 def max_over_ranks(x: float, dev) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     return float(D.all_reduce_max(t).item())
+
+
+class PhaseGuard:
+    """Runs the phases that follow the headline measurement so that none of them can lose the
+    record. An exception lands in it as ``<phase>_error``, and the ranks agree on failure through
+    a MAX all-reduce of an error flag (a phase that failed on one rank is reported by rank 0 too).
+    A phase still running after ``timeout_s`` (a hang, e.g. a collective waiting for a rank that
+    died) is cut off by a watchdog thread: it prints the record as it stands (rank 0) and ends the
+    process with status 0, on every rank, well inside the process group's own timeout (which
+    would abort the job without a record)."""
+
+    def __init__(self, record: dict, rank: int, timeout_s: float):
+        self.record, self.rank, self.timeout_s = record, rank, float(timeout_s)
+
+    def _expire(self, name: str) -> None:
+        self.record[f"{name}_error"] = f"timeout: phase still running after {self.timeout_s:.0f} s"
+        if self.rank == 0:
+            print(json.dumps(self.record), flush=True)
+        sys.stderr.flush()
+        os._exit(0)
+
+    def run(self, name: str, fn, dev) -> None:
+        timer = threading.Timer(self.timeout_s, self._expire, args=(name,))
+        timer.daemon = True
+        timer.start()
+        err = None
+        try:
+            try:
+                self.record.update(fn() or {})
+            except Exception as e:                 # noqa: BLE001 (reported in the record)
+                traceback.print_exc()
+                err = f"{type(e).__name__}: {e}"
+            try:
+                failed = max_over_ranks(1.0 if err else 0.0, dev) > 0
+            except Exception as e:                 # noqa: BLE001
+                failed, err = True, err or f"{type(e).__name__}: {e}"
+        finally:
+            timer.cancel()
+        if failed:
+            self.record[f"{name}_error"] = err or "failed on another rank"
+
+
+
+def bench_fault(phase: str) -> None:
+    """``FDX_BENCH_FAULT=<phase>[:hang]`` (tests): raise in, or hang, the named phase on every rank."""
+    spec = os.environ.get("FDX_BENCH_FAULT", "")
+    if not spec or spec.split(":")[0] != phase:
+        return
+    if spec.endswith(":hang"):
+        time.sleep(1e9)
+    raise RuntimeError(f"injected fault in the {phase} phase")
 
 
 def generate_shard(lo: int, hi: int, dev, seed: int, chunk: int = 500_000) -> list:
@@ -380,12 +437,17 @@ def main():
                     help="paced producer rate (whole group) of the consumer-group latency run")
     ap.add_argument("--kafka-confluent-rate", type=float, default=100_000,
                     help="paced producer rate of the confluent-surface latency run")
+    ap.add_argument("--phase-timeout", type=float, default=240.0,
+                    help="seconds after which the RF / Kafka phase is cut off and the record printed as it stands")
+    ap.add_argument("--pg-timeout", type=float, default=360.0,
+                    help="process-group timeout of the bench (above --phase-timeout, inside the driver's limit)")
     Config.add_cli_args(ap)          # --gbdt-max-bin, --seed, --config, ... (utils/config.py)
     args = ap.parse_args()
     cfg = Config.from_cli(args)
     run_profiled_if_requested(cfg.profile)    # --profile: re-run under rocprofv3 (GPU untouched so far)
 
-    D.init_from_env(os.environ.get("FDX_DIST_BACKEND", "nccl"))   # gloo: rehearse N ranks on one GPU
+    # gloo: rehearse N ranks on one GPU
+    D.init_from_env(os.environ.get("FDX_DIST_BACKEND", "nccl"), timeout_s=args.pg_timeout)
     rank, world = D.rank(), D.world_size()
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
@@ -437,22 +499,6 @@ def main():
               "train_peak_bytes_per_row": gbdt_peak / max(shard_rows, 1),
               "train_peak_over_model": gbdt_peak / max(modeled, 1.0)}
     del chunks
-    rf = {}
-    if args.rf_trees > 0:
-        # ------------------------------------------------------------------ 1b. RandomForest
-        torch.cuda.empty_cache()
-        torch.cuda.reset_peak_memory_stats(dev)
-        sync_all(dev)
-        t0 = time.perf_counter()
-        forest = fit_forest(vc, y, num_trees=args.rf_trees, max_depth=args.rf_depth, max_bins=32, bootstrap=True,
-                            feature_subset="sqrt", seed=42, device=dev)
-        sync_all(dev)
-        rf = {"rf_train_sec": max_over_ranks(time.perf_counter() - t0, dev), "rf_trees": len(forest.trees),
-              "rf_depth": args.rf_depth, "rf_nodes_tree0": int(forest.trees[0].num_nodes),
-              "rf_peak_hbm_gb": max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}
-        del forest
-    del vc, indptr, idx, counts, y, fo
-    torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ 2. streaming inference
     scorer = GpuScorer(spec, idf_np, model.scorer(), dev, max_docs=args.batch, max_bytes=args.batch * 4096,
@@ -522,54 +568,85 @@ def main():
         model.postprocess_numpy(raw)
         lats.append((time.perf_counter() - t1) * 1e3)
     p50 = float(np.percentile(lats[10:], 50))
+    del scorer, lat_scorer
 
-    kafka = kafka_phase(args, spec, idf_np, model, dev, rank) if args.kafka_msgs > 0 else {}
-    if kafka:
-        # every rank drains its own broker with one GPU: reported per GPU (rank 0's engine), not
-        # summed -- the shared-topic -> N-GPU topology is kafka_multi_gpu_dialogues_per_s
-        for k in ("kafka_p50_ms", "kafka_p95_ms", "kafka_p99_ms", "kafka_confluent_p50_ms", "kafka_confluent_p95_ms"):
-            if k in kafka:
-                kafka[k] = max_over_ranks(kafka[k], dev)
-
+    # the headline record is complete here: the phases below only add to it, each one isolated
+    # (an error lands in the record as <phase>_error; a phase that hangs past --phase-timeout is
+    # cut off by the watchdog, which prints the record as it stands)
     gbdt_peak_gb = max_over_ranks(gbdt_peak / 2 ** 30, dev)
     gen_peak_gb = max_over_ranks(gen_peak / 2 ** 30, dev)
     docs = args.steps * args.batch * world
+    record = {
+        "metric": METRIC,
+        "value": docs / dt,
+        "unit": "dialogues/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {"model": f"HashingTF(2^18)->IDF->GBDT({args.trees} trees, depth {args.depth})",
+                   "global_batch": args.batch * world, "seq_len": round(avg_bytes),
+                   "parallelism": f"dp{world}"},
+        "gbdt_train_sec": train_sec,
+        "gbdt_train_rows": args.rows,
+        "gbdt_featurize_sec": feat_sec,
+        "gbdt_datagen_sec_untimed": gen_sec,
+        "gbdt_warmup_sec_untimed": warm_sec,
+        "gbdt_nodes_tree0": res.trees[0].num_nodes,
+        "gbdt_peak_hbm_gb": gbdt_peak_gb,
+        "datagen_peak_hbm_gb_untimed": gen_peak_gb,
+        **sizing,
+        "stream_accuracy": acc,
+        "p50_single_dialogue_ms": p50,
+        "numa_bind_rank0": numa,
+    }
+    guard = PhaseGuard(record, rank, args.phase_timeout)
+
+    if args.rf_trees > 0:
+        # ------------------------------------------------------------------ 3. RandomForest
+        def rf_phase():
+            torch.cuda.empty_cache()
+            torch.cuda.reset_peak_memory_stats(dev)
+            sync_all(dev)
+            t0 = time.perf_counter()
+            bench_fault("rf")
+            forest = fit_forest(vc, y, num_trees=args.rf_trees, max_depth=args.rf_depth, max_bins=32, bootstrap=True,
+                                feature_subset="sqrt", seed=42, device=dev)
+            sync_all(dev)
+            return {"rf_train_sec": max_over_ranks(time.perf_counter() - t0, dev), "rf_trees": len(forest.trees),
+                    "rf_depth": args.rf_depth, "rf_nodes_tree0": int(forest.trees[0].num_nodes),
+                    "rf_peak_hbm_gb": max_over_ranks(torch.cuda.max_memory_allocated(dev) / 2 ** 30, dev)}
+
+        guard.run("rf", rf_phase, dev)
+    del vc, indptr, idx, counts, y, fo
+    torch.cuda.empty_cache()
+
+    if args.kafka_msgs > 0:
+        # ------------------------------------------------------------------ 4. Kafka end to end
+        def kafka_run():
+            kafka = kafka_phase(args, spec, idf_np, model, dev, rank)
+            # every rank drains its own broker with one GPU: reported per GPU (rank 0's engine), not
+            # summed -- the shared-topic -> N-GPU topology is kafka_multi_gpu_dialogues_per_s
+            for k in ("kafka_p50_ms", "kafka_p95_ms", "kafka_p99_ms", "kafka_confluent_p50_ms",
+                      "kafka_confluent_p95_ms"):
+                if k in kafka:
+                    kafka[k] = max_over_ranks(kafka[k], dev)
+            return kafka
+
+        guard.run("kafka", kafka_run, dev)
     if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": docs / dt,
-            "unit": "dialogues/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic",
-            "config": {"model": f"HashingTF(2^18)->IDF->GBDT({args.trees} trees, depth {args.depth})",
-                       "global_batch": args.batch * world, "seq_len": round(avg_bytes),
-                       "parallelism": f"dp{world}"},
-            "gbdt_train_sec": train_sec,
-            "gbdt_train_rows": args.rows,
-            "gbdt_featurize_sec": feat_sec,
-            "gbdt_datagen_sec_untimed": gen_sec,
-            "gbdt_warmup_sec_untimed": warm_sec,
-            "gbdt_nodes_tree0": res.trees[0].num_nodes,
-            "gbdt_peak_hbm_gb": gbdt_peak_gb,
-            "datagen_peak_hbm_gb_untimed": gen_peak_gb,
-            **sizing,
-            **rf,
-            "stream_accuracy": acc,
-            "p50_single_dialogue_ms": p50,
-            "numa_bind_rank0": numa,
-            **kafka,
-        }
-        print(json.dumps(out), flush=True)
-    D.barrier()
-    if D.is_dist():
-        torch.distributed.destroy_process_group()
+        print(json.dumps(record), flush=True)
+    try:
+        D.barrier()
+        if D.is_dist():
+            torch.distributed.destroy_process_group()
+    except Exception:                      # noqa: BLE001 (the record is out; a failed phase may leave the group broken)
+        traceback.print_exc()
 
 
 if __name__ == "__main__":

@@ -231,7 +231,8 @@ void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Ten
                      const optional<Tensor>& slot8_t, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
                      const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct, int64_t np,
                      const optional<Tensor>& feat_active, const optional<Tensor>& rowpack,
-                     const optional<Tensor>& list, const optional<Tensor>& count, bool lds = false) {
+                     const optional<Tensor>& list, const optional<Tensor>& count, bool lds = false,
+                     int64_t listed_per_xcd = -1) {
   const auto dev = csc_row.device();
   chk(item_start, dev, at::kLong, "item_start");
   chk(item_end, dev, at::kLong, "item_end");
@@ -267,6 +268,7 @@ void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Ten
   FDX_CHECK(readable_tail(csc_row, 4) && readable_tail(csc_key, 4),
             "csc_row/csc_key need 4 readable padding entries behind their end (see quantize.CSC_PAD)");
   fdx::HistArgs a{};
+  a.listed_per_xcd = -1;
   a.item_start = item_start.data_ptr<int64_t>();
   a.item_end = item_end.data_ptr<int64_t>();
   a.item_f0 = item_f0.data_ptr<int32_t>();
@@ -310,6 +312,8 @@ void hist_build_impl(const Tensor& item_start, const Tensor& item_end, const Ten
     a.active_list = list->data_ptr<int32_t>();
     a.active_count = count->data_ptr<int32_t>();
     a.list_cap = (int32_t)cap;
+    FDX_CHECK(listed_per_xcd <= cap, "listed_per_xcd exceeds the per-XCD list capacity");
+    a.listed_per_xcd = (int32_t)listed_per_xcd;
   }
   // LDS-atomic count kernel: 4 waves x 16 bt keys x nslots int64 cells must fit 64 KB
   a.lds = (lds && np == 1 && !slot8_t && 4 * 16 * bt * nslots * 8 <= 65536) ? 1 : 0;
@@ -340,9 +344,51 @@ void hist_sampled(const Tensor& item_start, const Tensor& item_end, const Tensor
                   const optional<Tensor>& rowpack, const Tensor& rowdig, const Tensor& boff, const Tensor& nbins,
                   const Tensor& slot_node, const Tensor& hist, int64_t TB, int64_t bt, int64_t ct,
                   const Tensor& feat_active, const optional<Tensor>& list, const optional<Tensor>& count,
-                  bool lds) {
+                  bool lds, int64_t listed_per_xcd) {
   hist_build_impl(item_start, item_end, item_f0, item_meta, wave_item, csc_row, csc_key, nullopt, rowdig, boff, nbins,
-                  slot_node, hist, TB, bt, ct, 1, feat_active, rowpack, list, count, lds);
+                  slot_node, hist, TB, bt, ct, 1, feat_active, rowpack, list, count, lds, listed_per_xcd);
+}
+
+// Compact the active work items of an item group (feature in feat_active) into per-XCD lists
+// ahead of the listed pass that reads them (count [8] int32 zeroed by the caller, atomically
+// advanced here): the RF level loop queues this with the previous level's plan so the counts
+// reach the host with the level's counts and the pass launches one wave per active item.
+void hist_select(const Tensor& item_start, const Tensor& item_f0, const Tensor& item_meta,
+                 const optional<Tensor>& wave_item, const Tensor& nbins, const Tensor& feat_active, const Tensor& list,
+                 const Tensor& count) {
+  const auto dev = item_start.device();
+  chk(item_start, dev, at::kLong, "item_start");
+  chk(item_f0, dev, at::kInt, "item_f0");
+  chk(item_meta, dev, at::kInt, "item_meta");
+  chk(nbins, dev, at::kInt, "nbins");
+  chk(feat_active, dev, at::kByte, "feat_active");
+  chk(list, dev, at::kInt, "list");
+  chk(count, dev, at::kInt, "count");
+  const int64_t I = item_start.numel();
+  FDX_CHECK(item_f0.numel() == I && item_meta.numel() == I && feat_active.numel() == nbins.numel(), "item arrays");
+  const int64_t slots = wave_item ? wave_item->numel() : I;
+  const int64_t cap = ((slots + 3) / 4 + 7) / 8 * 4;
+  FDX_CHECK(list.numel() >= 8 * cap && count.numel() >= 8, "list must hold 8 x ceil(slots / 32) x 4 items, count 8");
+  fdx::HistArgs a{};
+  a.listed_per_xcd = -1;
+  a.item_start = item_start.data_ptr<int64_t>();
+  a.item_f0 = item_f0.data_ptr<int32_t>();
+  a.item_meta = item_meta.data_ptr<int32_t>();
+  a.num_items = (int32_t)I;
+  a.nbins = nbins.data_ptr<int32_t>();
+  a.feat_active = feat_active.data_ptr<uint8_t>();
+  if (wave_item) {
+    chk(*wave_item, dev, at::kInt, "wave_item");
+    a.wave_item = wave_item->data_ptr<int32_t>();
+    a.num_slots = (int32_t)wave_item->numel();
+  }
+  a.active_list = list.data_ptr<int32_t>();
+  a.active_count = count.data_ptr<int32_t>();
+  a.list_cap = (int32_t)cap;
+  FDX_CHECK(dev.is_cuda(), "hist_select: device lists only (the host pass scans every item)");
+  c10::hip::HIPGuard guard(dev.index());
+  fdx::launch_hist_select(a, stream(dev));
+  C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
 // pack [N] int32 = slot (0xff: not built in this pass) | class-count digits << 8 (np = 1 passes)
@@ -1155,7 +1201,8 @@ void register_tree_ops(pybind11::module& m) {
         py::arg("item_meta"), py::arg("wave_item"), py::arg("csc_row"), py::arg("csc_key"), py::arg("rowpack"),
         py::arg("rowdig"), py::arg("boff"), py::arg("nbins"), py::arg("slot_node"), py::arg("hist"), py::arg("TB"),
         py::arg("bt"), py::arg("ct"), py::arg("feat_active"), py::arg("list"), py::arg("count"),
-        py::arg("lds") = false);
+        py::arg("lds") = false, py::arg("listed_per_xcd") = -1);
+  m.def("tree_hist_select", &hist_select);
   m.def("tree_slot_pack", &slot_pack);
   m.def("tree_rg_build", &rg_build);
   m.def("tree_rg_list", &rg_list, py::arg("row_node"), py::arg("node_slot"), py::arg("slot8"), py::arg("N"),

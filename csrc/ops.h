@@ -97,6 +97,7 @@ void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const 
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
                        int64_t f0, int64_t* out, hipStream_t s);
 void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s);
+void launch_hist_select(const HistArgs& a, hipStream_t s);
 struct RgBuildArgs;
 struct RgListArgs;
 struct RgHistArgs;

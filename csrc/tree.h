@@ -119,6 +119,9 @@ struct HistArgs {
   int32_t* active_list;           // optional: listed pass, the active items compacted per XCD ...
   int32_t* active_count;          //   ... [8]: their count per XCD (list x at x * list_cap)
   int32_t list_cap;               // wave slots per XCD (set by the launch)
+  int32_t listed_per_xcd;         // -1: the launch compacts the list and strides a fixed grid over
+                                  // it; >= 0: the list was compacted beforehand (hist_select) and
+                                  // its largest per-XCD count is known: one wave per active item
   int32_t lds;                    // np = 1 passes: LDS-atomic kernel (hist_lds_kernel) instead of MFMA
 };
 

@@ -1203,13 +1203,27 @@ void launch_slot8(const SlotArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(slot8_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
+void launch_hist_select(const HistArgs& a, hipStream_t s) {
+  const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
+  if (slots <= 0) return;
+  HistArgs sel = a;
+  sel.num_slots = slots;
+  hipLaunchKernelGGL(hist_select_kernel, dim3((slots + 255) / 256), dim3(256), 0, s, sel,
+                     const_cast<int32_t*>(a.active_list), const_cast<int32_t*>(a.active_count));
+}
+
 void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s) {
   if (a.num_items <= 0) return;
   const int32_t slots = a.wave_item ? a.num_slots : a.num_items;
   dim3 grid((slots + 3) / 4);
   const dim3 block(256);
   const bool root = a.slot8 == nullptr && a.rowpack == nullptr;
-  if (a.active_list != nullptr) {
+  if (a.active_list != nullptr && a.listed_per_xcd >= 0) {
+    // preselected list (launch_hist_select, queued with the previous level's plan; the per-XCD
+    // counts reached the host with the level's counts): a wave per active item, none idle
+    if (a.listed_per_xcd == 0) return;
+    grid = dim3((unsigned)((a.listed_per_xcd + 3) / 4 * 8));
+  } else if (a.active_list != nullptr) {
     // listed pass: compact the active items, then a grid of at most kListedWaves waves strides
     // over them (the full grid was ~300K wave slots, most of them exiting at once: ~100 us a pass)
     HistArgs sel = a;

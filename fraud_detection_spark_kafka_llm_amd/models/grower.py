@@ -293,6 +293,9 @@ RG_DBG = int(os.environ.get("FDX_RG_DBG", 0))   # diagnostics only (csrc/tree.h 
 # a device-compacted list of the active work items (tree_hist_sampled)
 SAMPLED = os.environ.get("FDX_RF_SAMPLED", "1") == "1"
 LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
+# RF levels >= 1 launch one wave per active work item from lists compacted with the previous
+# level's plan (0: the r4 passes, a wave per item slot or a fixed listed grid)
+PRESELECT = os.environ.get("FDX_RF_PRESELECT", "1") == "1"
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
 RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
 # split search: a wave per (node, feature) for the features with > 16 bins
@@ -622,6 +625,10 @@ class FeatureShards:
         C.tree_rf_sample(seed, tree, nodes, F, k, fid_orig, thr[:n], self._mask[p], None)
         C.tree_rf_compact(self._mask[p], self._nbins_all, self._fs_dev, self._local_c[p], self._sizes[p])
         self.sizes_host[p].copy_(self._sizes[p], non_blocking=nodes.is_cuda)
+
+    def compact_mask(self, p: int) -> torch.Tensor:
+        """The parity-``p`` level's union feature mask (sample_compact)."""
+        return self._mask[p]
 
     def compact_level(self, p: int, n_open: int):
         """(feat_thr [n_open], feat_mask, local offsets [Fa + 1], stride) of the parity-``p`` layout
@@ -1006,10 +1013,15 @@ class LevelState:
         ev.record(stream)
         return ev
 
-    def __init__(self, Q: Quantized, max_depth: int):
+    def __init__(self, Q: Quantized, max_depth: int, n_sel: int = 0):
         dev = Q.device
         M = 2 ** (max_depth + 1)
         cap = 2 ** max_depth
+        # RF levels with preselected item lists (PRESELECT): per level the 4 plan counts, then
+        # 8 per-XCD active-item counts per sampled item group, read by the host in one copy
+        self.n_sel = n_sel
+        self.rf_thr = [torch.empty(cap, dtype=torch.float64, device=dev) for _ in range(2)] if n_sel else None
+        self.rf_mask = [torch.empty(Q.Fa, dtype=torch.uint8, device=dev) for _ in range(2)] if n_sel else None
         i32 = lambda n: torch.full((n,), -1, dtype=torch.int32, device=dev)   # noqa: E731
         self.M, self.cap, self.max_depth = M, cap, max_depth
         # the node table (+ the tree's quantisation exponents) lives in ONE device arena, mirrored by
@@ -1046,8 +1058,8 @@ class LevelState:
             self.arena_init = self.arena_init.pin_memory()
         self.open = [i32(cap), i32(cap)]
         self.totals = [torch.zeros((cap, 2), dtype=torch.int64, device=dev) for _ in range(2)]
-        self.counts = torch.zeros((max_depth + 1, 4), dtype=torch.int32, device=dev)
-        self.counts_host = torch.zeros((max_depth + 1, 4), dtype=torch.int32)
+        self.counts = torch.zeros((max_depth + 1, 4 + 8 * n_sel), dtype=torch.int32, device=dev)
+        self.counts_host = torch.zeros((max_depth + 1, 4 + 8 * n_sel), dtype=torch.int32)
         if dev.type == "cuda":
             self.counts_host = self.counts_host.pin_memory()
         self.one = torch.ones(1, dtype=torch.int32, device=dev)
@@ -1121,9 +1133,16 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     np_ = _choose_np(params, weight)
     mode_rs = 0 if params.mode == 0 else 1
     build_all = bool(params.feat_k)
+    sampled = SAMPLED and build_all and np_ == 1
+    # RF levels >= 1: the next level's feature sample and its active-item lists are queued right
+    # after the plan, so the per-XCD item counts reach the host with the level's counts and each
+    # histogram pass launches one wave per active item (no grid of ~300K mostly idle wave slots)
+    presel = PRESELECT and sampled and dev.type == "cuda"
+    item_groups = (Q.groups + Q.hot_groups) if sampled else []
+    sel_ids = [gi for gi, grp in enumerate(item_groups) if grp.num_items] if presel else []
     st = getattr(ws, "_levels", None)
-    if st is None or st.max_depth != params.max_depth:
-        st = ws._levels = LevelState(Q, params.max_depth)
+    if st is None or st.max_depth != params.max_depth or st.n_sel != len(sel_ids):
+        st = ws._levels = LevelState(Q, params.max_depth, len(sel_ids))
     ws.row_node.zero_()
     # every step of this generator runs on the stream current now (the forest driver advances a
     # lane inside that lane's stream context)
@@ -1174,6 +1193,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             n_open, n_build = int(cnt[1]), int(cnt[2])
             if n_open == 0:
                 break
+            if sel_ids:       # largest per-XCD active-item count of each sampled group
+                per_xcd = {gi: max(cnt[4 + 8 * j: 12 + 8 * j]) for j, gi in enumerate(sel_ids)}
         LEVEL_STATS["levels"] += 1
         LEVEL_STATS["built_nodes"] += n_build
         LEVEL_STATS["hist_bytes"] += n_build * TB * 16          # (g, h) int64 partials of the built nodes
@@ -1183,6 +1204,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         feat_thr = feat_mask = None
         if compact:
             feat_thr, feat_mask, local_c, Bs_c = shards.compact_level(cur, n_open)
+        elif build_all and sel_ids and d > 0:
+            feat_thr, feat_mask = st.rf_thr[cur][:n_open], st.rf_mask[cur]      # (queued with the plan)
         elif build_all:
             feat_thr = torch.empty(n_open, dtype=torch.float64, device=dev)
             feat_mask = torch.empty(Q.Fa, dtype=torch.uint8, device=dev)
@@ -1214,7 +1237,6 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             slot8 = None
             csc_slot8, csc_dig = None, ws.rowdig
             rg = ws.rowgroups() if (not build_all and np_ == 4) else None
-            sampled = SAMPLED and build_all and np_ == 1
             if d > 0:
                 # a single built node: the CSC passes run the root kernel on digit words zeroed
                 # outside it (no per-entry slot gather, no compaction; zero rows add nothing)
@@ -1260,14 +1282,23 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                     continue
                 if sampled:
                     pack = ws.rowpack() if (d > 0 and not single) else None
-                    # the listed pass wins while few items are active (<= 2 open nodes: ~0.16 vs
-                    # 0.19 ms at the root); with more, its fixed grid balances worse than a wave
-                    # per slot (profiles/r3s3/rf_probe_chunks.txt)
-                    lst, cnt = ws.item_list(gi, grp) if n_open <= LISTED_MAX_NODES else (None, None)
+                    if sel_ids and d > 0:
+                        # preselected: exactly one wave per active item (the lists were built with
+                        # the previous level's plan)
+                        j = sel_ids.index(gi)
+                        lst = ws.item_list(gi, grp)[0]
+                        cnt = st.counts[d - 1, 4 + 8 * j: 12 + 8 * j]
+                        npx = per_xcd[gi]
+                    else:
+                        # the listed pass wins while few items are active (<= 2 open nodes: ~0.16
+                        # vs 0.19 ms at the root); with more, its fixed grid balances worse than a
+                        # wave per slot (profiles/r3s3/rf_probe_chunks.txt)
+                        lst, cnt = ws.item_list(gi, grp) if n_open <= LISTED_MAX_NODES else (None, None)
+                        npx = -1
                     launches.append(functools.partial(
                         C.tree_hist_sampled, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta,
                         grp.wave_order(), Q.h_row, Q.h_key, pack, csc_dig, h_boff, Q.nbins, s2n, hist_target, h_stride,
-                        grp.bt, ct, feat_mask, lst, cnt, RF_LDS))
+                        grp.bt, ct, feat_mask, lst, cnt, RF_LDS, npx))
                     continue
                 launches.append(functools.partial(
                     C.tree_hist_build, grp.item_start, grp.item_end, grp.item_f0, grp.item_meta, grp.wave_order(),
@@ -1332,6 +1363,21 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             # level d + 1's open list is at most 2 n_open long, -1 padded (tree.h level_plan_reset)
             shards.sample_compact(C, nxt, seed, int(tree_index), st.open[nxt][:2 * n_open], int(Q.num_features),
                                   int(params.feat_k), Q.fid_orig)
+        if sel_ids and d + 1 < params.max_depth:
+            nxt_open = st.open[nxt][:2 * n_open]
+            if compact:
+                mask_n = shards.compact_mask(nxt)
+            else:
+                mask_n = st.rf_mask[nxt]
+                C.tree_rf_sample(seed, int(tree_index), nxt_open, int(Q.num_features), int(params.feat_k),
+                                 Q.fid_orig, st.rf_thr[nxt][:2 * n_open], mask_n, None)
+            st.counts[d, 4:].zero_()
+            sel = st.counts[d, 4:].view(len(sel_ids), 8)
+            for j, gi in enumerate(sel_ids):
+                grp = item_groups[gi]
+                lst, _ = ws.item_list(gi, grp)
+                C.tree_hist_select(grp.item_start, grp.item_f0, grp.item_meta, grp.wave_order(), Q.nbins, mask_n,
+                                   lst, sel[j])
         st.counts_host[d].copy_(st.counts[d], non_blocking=dev.type == "cuda")
         ev = st.record_event(cur_stream)
         with tracing.span("tree.partition"):

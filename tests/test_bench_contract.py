@@ -58,6 +58,35 @@ def test_bench_two_ranks_contract_gloo_rehearsal():
 
 
 @pytest.mark.gpu
+def test_bench_rf_fault_two_ranks_still_prints_the_headline():
+    """the headline phases (GBDT train, streaming, single-dialogue latency)
+    run first; an RF-phase fault on every rank (FDX_FAULT: a tree of the forest raises) lands in
+    the record as rf_error and the Kafka phase still runs."""
+    env = {**os.environ, "FDX_DIST_BACKEND": "gloo", "FDX_FAULT": "tree:1"}
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29553", "bench.py", "--gpus", "2", *TINY],
+                         cwd=REPO, capture_output=True, text=True, timeout=900, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert KEYS <= set(rec) and rec["n_gpus"] == 2 and rec["value"] > 0 and rec["gbdt_train_sec"] > 0
+    assert "injected" in rec["rf_error"] and "rf_train_sec" not in rec
+    assert rec["kafka_dialogues_per_s"] > 0 and rec["kafka_multi_gpu_scorer_procs"] == 2
+
+
+@pytest.mark.gpu
+def test_bench_phase_watchdog_prints_the_record_of_a_hung_phase():
+    """A phase that hangs (FDX_BENCH_FAULT=rf:hang) is cut off after --phase-timeout: the record
+    is printed as it stands with rf_error, and the process exits 0."""
+    env = {**os.environ, "FDX_BENCH_FAULT": "rf:hang"}
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *TINY, "--phase-timeout", "20"], cwd=REPO,
+                         capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert KEYS <= set(rec) and rec["value"] > 0 and rec["p50_single_dialogue_ms"] > 0
+    assert rec["rf_error"].startswith("timeout") and "kafka_dialogues_per_s" not in rec
+
+
+@pytest.mark.gpu
 def test_suite_xgb_and_rf_two_ranks_gloo_rehearsal():
     """bench/suite.py xgb / rf under torchrun: --rows is global, row-sharded, one JSON line."""
     env = {**os.environ, "FDX_DIST_BACKEND": "gloo"}
