@@ -29,8 +29,18 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--trees", type=int, default=500)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--forced", action="store_true",
+                    help="the data-parallel level path at world 1 over RCCL (FDX_FORCE_COLLECTIVES, compact levels)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.forced:
+        os.environ["FDX_FORCE_COLLECTIVES"] = "1"
+        os.environ["FDX_RF_COMPACT"] = "1"
+        from fraud_detection_spark_kafka_llm_amd.models import grower
+        from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+        grower.RF_COMPACT = "1"
+        D.init_from_env("nccl")
     warm_tree_kernels(dev, gbdt_depth=0, forest_depth=5, forest_subset="sqrt")
     vc, y, _ = _tfidf(args.rows, dev, seed=21)
     torch.cuda.synchronize()

@@ -136,7 +136,7 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
             if isinstance(res, PendingTree):
                 C.tree_leaf_update(margin, ws.row_node, res.node_value)
                 pending = res
-                maybe_fail(t)
+                maybe_fail(t, model="gbdt")
                 continue
             tree = res
             node_value = torch.from_numpy(np.ascontiguousarray(tree.stats[:, 0])).to(dev)
@@ -148,7 +148,7 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
             checkpoint(t, trees, base)
         if ckpt is not None:
             ckpt.maybe_save(len(trees), trees, base, F, params, force=len(trees) == params.n_estimators)
-        maybe_fail(t)
+        maybe_fail(t, model="gbdt")
     if pending is not None:
         trees.append(pending.result().compacted())
     if dev.type == "cuda":

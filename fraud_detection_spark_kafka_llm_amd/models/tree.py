@@ -141,6 +141,6 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
             if ckpt is not None:
                 crossed = (len(trees) // ckpt.every) > (before // ckpt.every)
                 ckpt.maybe_save(len(trees), trees, 0.0, F, None, force=crossed or len(trees) == num_trees)
-            maybe_fail(tid)
+            maybe_fail(tid, model="rf")
         t += len(ids)
     return ForestResult(trees, F, len(lanes.ws) if lanes is not None else 1)

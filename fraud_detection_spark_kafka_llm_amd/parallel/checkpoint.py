@@ -17,7 +17,7 @@ the margins (GBDT) and boosting continues.
 
 Fault injection: ``FDX_FAULT="rank:R,tree:T"`` (or ``tree:T`` for every rank) raises
 ``InjectedFault`` right after tree T is grown on rank R — a stand-in for a GPU/rank failure in
-tests of the recovery path.
+tests of the recovery path; ``model:rf`` / ``model:gbdt`` limits it to one trainer.
 """
 from __future__ import annotations
 
@@ -42,15 +42,19 @@ def parse_fault(spec: Optional[str] = None) -> Optional[dict]:
     out = {}
     for part in spec.split(","):
         k, _, v = part.partition(":")
-        out[k.strip()] = int(v)
+        k = k.strip()
+        out[k] = v.strip() if k == "model" else int(v)
     return out
 
 
-def maybe_fail(tree: int, fault: Optional[dict] = None) -> None:
+def maybe_fail(tree: int, fault: Optional[dict] = None, model: Optional[str] = None) -> None:
     """``attempt:A`` limits the fault to relaunch A of an elastic job; ``hard:1`` kills the
-    process outright (``os._exit``) instead of raising, like a lost GPU or an OOM kill."""
+    process outright (``os._exit``) instead of raising, like a lost GPU or an OOM kill;
+    ``model:M`` to the trainer ``model`` ("rf" / "gbdt")."""
     f = fault if fault is not None else parse_fault()
     if not f or "tree" not in f:
+        return
+    if "model" in f and f["model"] != model:
         return
     att = int(os.environ.get("FDX_ATTEMPT", "0"))
     if f["tree"] == tree and f.get("rank", dist.rank()) == dist.rank() and f.get("attempt", att) == att:

@@ -62,7 +62,7 @@ def test_bench_rf_fault_two_ranks_still_prints_the_headline():
     """the headline phases (GBDT train, streaming, single-dialogue latency)
     run first; an RF-phase fault on every rank (FDX_FAULT: a tree of the forest raises) lands in
     the record as rf_error and the Kafka phase still runs."""
-    env = {**os.environ, "FDX_DIST_BACKEND": "gloo", "FDX_FAULT": "tree:1"}
+    env = {**os.environ, "FDX_DIST_BACKEND": "gloo", "FDX_FAULT": "model:rf,tree:1"}
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                           "--master-addr", "127.0.0.1", "--master-port", "29553", "bench.py", "--gpus", "2", *TINY],
                          cwd=REPO, capture_output=True, text=True, timeout=900, env=env)
