@@ -349,6 +349,32 @@ void hist_sampled(const Tensor& item_start, const Tensor& item_end, const Tensor
                   slot_node, hist, TB, bt, ct, 1, feat_active, rowpack, list, count, lds, listed_per_xcd);
 }
 
+// hist_select over several item groups in one call: counts [G, 8] is zeroed here, then group j's
+// active items go to lists[j] / counts[j] (the RF level loop queues this with the previous level's
+// plan: one host call per level instead of a fill and a launch per group).
+void hist_select(const Tensor& item_start, const Tensor& item_f0, const Tensor& item_meta,
+                 const optional<Tensor>& wave_item, const Tensor& nbins, const Tensor& feat_active, const Tensor& list,
+                 const Tensor& count);
+
+void hist_select_groups(const std::vector<std::vector<Tensor>>& groups, const Tensor& nbins, const Tensor& feat_active,
+                        const std::vector<Tensor>& lists, const Tensor& counts) {
+  const auto dev = counts.device();
+  chk(counts, dev, at::kInt, "counts");
+  FDX_CHECK(groups.size() == lists.size() && counts.dim() == 2 && counts.size(0) == (int64_t)groups.size() &&
+                counts.size(1) == 8, "groups / lists / counts [G, 8]");
+  FDX_CHECK(dev.is_cuda(), "hist_select_groups: device lists only");
+  {
+    c10::hip::HIPGuard guard(dev.index());
+    FDX_CHECK(hipMemsetAsync(counts.data_ptr<int32_t>(), 0, counts.numel() * sizeof(int32_t), stream(dev)) == hipSuccess,
+              "hipMemsetAsync failed");
+  }
+  for (size_t j = 0; j < groups.size(); ++j) {
+    const auto& g = groups[j];
+    FDX_CHECK(g.size() == 4, "a group is (item_start, item_f0, item_meta, wave_item)");
+    hist_select(g[0], g[1], g[2], g[3], nbins, feat_active, lists[j], counts[(int64_t)j]);
+  }
+}
+
 // Compact the active work items of an item group (feature in feat_active) into per-XCD lists
 // ahead of the listed pass that reads them (count [8] int32 zeroed by the caller, atomically
 // advanced here): the RF level loop queues this with the previous level's plan so the counts
@@ -1203,6 +1229,7 @@ void register_tree_ops(pybind11::module& m) {
         py::arg("bt"), py::arg("ct"), py::arg("feat_active"), py::arg("list"), py::arg("count"),
         py::arg("lds") = false, py::arg("listed_per_xcd") = -1);
   m.def("tree_hist_select", &hist_select);
+  m.def("tree_hist_select_groups", &hist_select_groups);
   m.def("tree_slot_pack", &slot_pack);
   m.def("tree_rg_build", &rg_build);
   m.def("tree_rg_list", &rg_list, py::arg("row_node"), py::arg("node_slot"), py::arg("slot8"), py::arg("N"),

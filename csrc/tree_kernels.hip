@@ -560,30 +560,41 @@ __global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
   }
 }
 
-// Compacted list of the active work items of a listed pass, in wave-slot order per wave (one
-// atomic per wave: ballot + mbcnt for the positions inside it).
+// Compacted per-XCD lists of the active work items of a listed pass. A workgroup takes
+// kSelPerThread x 256 consecutive wave slots (coalesced reads), places its active items in LDS
+// order per XCD (LDS atomics), then reserves its runs of the 8 global lists with ONE global atomic
+// per XCD: a wave-level global atomic per XCD (the earlier version) put ~40K atomics on the same 8
+// counters per pass, ~40 us a launch. The order inside a list is free (integer histograms).
+constexpr int kSelPerThread = 16;
+
 __global__ __launch_bounds__(256) void hist_select_kernel(HistArgs a, int32_t* list, int32_t* count) {
-  const int w = blockIdx.x * 256 + threadIdx.x;
-  int item = -1;
-  if (w < a.num_slots) item = a.wave_item ? a.wave_item[w] : w;
-  const bool act = item >= 0 && item < a.num_items && item_active(a, item);
-  if (__ballot(act) == 0) return;
-  // the XCD the item's wave slot was placed on (wave_order: workgroup b = slot / 4 on XCD b % 8):
-  // each XCD's waves of the listed pass take that XCD's items, so a row block's slot and count
-  // words stay in the L2 they were placed for
-  const int x = (w >> 2) & 7;
-  const int lane = threadIdx.x & (kWave - 1);
-  for (int xx = 0; xx < 8; ++xx) {
-    const unsigned long long b = __ballot(act && x == xx);
-    if (b == 0) continue;
-    const int first = __builtin_ctzll(b);
-    int base = 0;
-    if (lane == first) base = atomicAdd(count + xx, __popcll(b));
-    base = __shfl(base, first, kWave);
-    if (act && x == xx)
-      list[(int64_t)xx * a.list_cap + base +
-           (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = item;
+  __shared__ int32_t s_cnt[8], s_base[8];
+  const int t = threadIdx.x;
+  if (t < 8) s_cnt[t] = 0;
+  __syncthreads();
+  const int64_t w0 = (int64_t)blockIdx.x * 256 * kSelPerThread;
+  int32_t item[kSelPerThread], loc[kSelPerThread];
+#pragma unroll
+  for (int j = 0; j < kSelPerThread; ++j) {
+    const int64_t w = w0 + (int64_t)j * 256 + t;
+    int it = -1;
+    if (w < a.num_slots) it = a.wave_item ? a.wave_item[w] : (int)w;
+    const bool act = it >= 0 && it < a.num_items && item_active(a, it);
+    item[j] = it;
+    // the XCD the item's wave slot was placed on (wave_order: workgroup b = slot / 4 on XCD b % 8):
+    // each XCD's waves of the listed pass take that XCD's items, so a row block's slot and count
+    // words stay in the L2 they were placed for
+    loc[j] = act ? atomicAdd(&s_cnt[(w >> 2) & 7], 1) : -1;
   }
+  __syncthreads();
+  if (t < 8) s_base[t] = s_cnt[t] ? atomicAdd(count + t, s_cnt[t]) : 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSelPerThread; ++j)
+    if (loc[j] >= 0) {
+      const int x = (int)(((w0 + (int64_t)j * 256 + t) >> 2) & 7);
+      list[(int64_t)x * a.list_cap + s_base[x] + loc[j]] = item[j];
+    }
 }
 
 // ------------------------------------------------------------------ dense i8 MFMA histogram
@@ -1208,7 +1219,7 @@ void launch_hist_select(const HistArgs& a, hipStream_t s) {
   if (slots <= 0) return;
   HistArgs sel = a;
   sel.num_slots = slots;
-  hipLaunchKernelGGL(hist_select_kernel, dim3((slots + 255) / 256), dim3(256), 0, s, sel,
+  hipLaunchKernelGGL(hist_select_kernel, dim3((slots + 256 * kSelPerThread - 1) / (256 * kSelPerThread)), dim3(256), 0, s, sel,
                      const_cast<int32_t*>(a.active_list), const_cast<int32_t*>(a.active_count));
 }
 
@@ -1229,7 +1240,7 @@ void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s) {
     HistArgs sel = a;
     sel.num_slots = slots;
     (void)hipMemsetAsync(const_cast<int32_t*>(a.active_count), 0, 8 * sizeof(int32_t), s);   // per-XCD counts
-    hipLaunchKernelGGL(hist_select_kernel, dim3((slots + 255) / 256), dim3(256), 0, s, sel,
+    hipLaunchKernelGGL(hist_select_kernel, dim3((slots + 256 * kSelPerThread - 1) / (256 * kSelPerThread)), dim3(256), 0, s, sel,
                        const_cast<int32_t*>(a.active_list), const_cast<int32_t*>(a.active_count));
     static const int32_t listed_waves = [] {
       const char* e = getenv("FDX_LISTED_WAVES");                  // (experiments: the grid of a listed pass)

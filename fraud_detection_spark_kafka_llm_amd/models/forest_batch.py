@@ -36,7 +36,6 @@ of per-row records; it lost to per-tree passes, profiles/r2_rf_batch_ab.txt, and
 """
 from __future__ import annotations
 
-import contextlib
 import os
 from collections import deque
 from typing import Optional
@@ -44,6 +43,7 @@ from typing import Optional
 import torch
 
 from ..utils import tracing
+from ..utils.streams import StreamSwitch
 from .grower import CollStep, GrowParams, LevelBatcher, Workspace, _Lane, device_tree_steps
 from .quantize import Quantized
 
@@ -66,11 +66,12 @@ class ForestLanes:
             w.hist_streams = LANE_HIST_STREAMS
         cuda = Q.device.type == "cuda"
         self.streams = [torch.cuda.Stream(Q.device) for _ in range(lanes)] if cuda else [None] * lanes
+        self.switches = [StreamSwitch(s) for s in self.streams]
+        self.events = [torch.cuda.Event() if cuda else None for _ in range(lanes)]
         self.dev = Q.device
 
     def stream_ctx(self, i: int):
-        s = self.streams[i]
-        return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
+        return self.switches[i]
 
 
 def build_shared_state(Q: Quantized, lanes: ForestLanes, coll=None) -> list:
@@ -163,7 +164,15 @@ def _grow_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tree_ids
     nl = len(lanes.ws)
     ng = max(1, min(LANE_GROUPS, nl))
     groups = [list(range(g * nl // ng, (g + 1) * nl // ng)) for g in range(ng)]
-    batchers = [LevelBatcher(coll, shards[0].S, lanes.dev, coord) for _ in range(ng)]
+    # a coordinator stream per group: a group's batch fill and collectives never queue behind the
+    # other group's (RCCL still runs them on its own stream in issue order)
+    coords = [None] * ng
+    if coord is not None:
+        start = coord.record_event()
+        coords = [torch.cuda.Stream(lanes.dev) for _ in range(ng)]
+        for c in coords:
+            c.wait_event(start)
+    batchers = [LevelBatcher(coll, shards[0].S, lanes.dev, c) for c in coords]
     todo = deque(tree_ids)
     out: dict = {}
     state: list = [None] * nl                  # lane -> _Lane (tid = tree id) or None
@@ -176,7 +185,7 @@ def _grow_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tree_ids
         with tracing.span("forest.tree", tree=t, lane=i), lanes.stream_ctx(i):
             gen = device_tree_steps(Q, lanes.ws[i], params, t, None, None, weight, coll, shards[i], label=label,
                                     bootstrap=bootstrap)
-            state[i] = _Lane(gen, next(gen), lanes.streams[i], t)
+            state[i] = _Lane(gen, next(gen), lanes.streams[i], t, lanes.switches[i], lanes.events[i])
 
     def resume(i: int) -> None:
         ln = state[i]
@@ -203,4 +212,7 @@ def _grow_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tree_ids
         if live:
             batchers[g].serve(live)
             turns.append(g)
+    if coord is not None:
+        for c in coords:
+            coord.wait_stream(c)
     return [out[t] for t in tree_ids]

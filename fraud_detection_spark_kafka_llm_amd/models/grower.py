@@ -32,6 +32,7 @@ import torch
 from ..ml.tree_model import Tree
 from ..ops import native
 from ..utils import tracing
+from ..utils.streams import StreamSwitch
 from . import quantize as qmod
 from .quantize import Quantized
 
@@ -162,9 +163,8 @@ class LaneBufs:
         return self.R * self.Bs
 
     def prepare(self, totals=None) -> torch.Tensor:
-        """Zero this tree's rows (its own stream), place the root totals; returns the [*, Bs, 2]
-        view the histogram passes write through (row 0 = this tree's first row of shard 0)."""
-        self.target[:, self.row0:self.row0 + self.rows].zero_()
+        """Place the root totals (the batch zeroed the buffer); returns the [*, Bs, 2] view the
+        histogram passes write through (row 0 = this tree's first row of shard 0)."""
         if totals is not None:
             self.target.view(self.target.shape[0], -1, 2)[:, self.tot_bin] = totals
         return self.target.view(-1, self.Bs, 2)[self.row0:]
@@ -177,28 +177,19 @@ class LaneBufs:
 
 
 class _Lane:
-    """A tree in flight: its step generator, the step / event it is parked at, its stream."""
+    """A tree in flight: its step generator, the step / event it is parked at, its stream (and
+    that stream's reusable switch and join event)."""
 
-    __slots__ = ("gen", "item", "stream", "tid")
+    __slots__ = ("gen", "item", "stream", "tid", "switch", "event")
 
-    def __init__(self, gen, item, stream, tid=None):
+    def __init__(self, gen, item, stream, tid=None, switch=None, event=None):
         self.gen, self.item, self.stream, self.tid = gen, item, stream, tid
+        self.switch = switch if switch is not None else StreamSwitch(stream)
+        self.event = event
 
     def send(self, value) -> None:
-        ctx = torch.cuda.stream(self.stream) if self.stream is not None else _NULL_CTX
-        with ctx:
+        with self.switch:
             self.item = self.gen.send(value)
-
-
-class _NullCtx:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *exc):
-        return False
-
-
-_NULL_CTX = _NullCtx()
 
 
 class LevelBatcher:
@@ -214,6 +205,8 @@ class LevelBatcher:
     def __init__(self, coll, S: int, dev: torch.device, coord=None):
         self.coll, self.S, self.dev = coll, int(S), dev
         self.coord = coord if coord is not None else (torch.cuda.current_stream(dev) if dev.type == "cuda" else None)
+        self.switch = StreamSwitch(self.coord)
+        self.coord_event = torch.cuda.Event() if self.coord is not None else None
         self.hold = None
         self.batches = 0
 
@@ -221,24 +214,29 @@ class LevelBatcher:
         self.hold = None
 
     def _ctx(self):
-        return torch.cuda.stream(self.coord) if self.coord is not None else _NULL_CTX
+        return self.switch
 
     def _join_in(self, lanes) -> None:
+        """The coordinator stream waits for every lane's queued work (reusable per-lane events)."""
         if self.coord is None:
             return
         for ln in lanes:
             if ln.stream is not None and ln.stream != self.coord:
-                self.coord.wait_stream(ln.stream)
+                if ln.event is None:
+                    ln.event = torch.cuda.Event()
+                ln.event.record(ln.stream)
+                self.coord.wait_event(ln.event)
 
     def _join_out(self, lanes) -> None:
         if self.coord is None:
             return
-        ev = None
+        recorded = False
         for ln in lanes:
             if ln.stream is not None and ln.stream != self.coord:
-                if ev is None:
-                    ev = self.coord.record_event()
-                ln.stream.wait_event(ev)
+                if not recorded:
+                    self.coord_event.record(self.coord)
+                    recorded = True
+                ln.stream.wait_event(self.coord_event)
 
     def serve(self, lanes: list) -> None:
         reqs = [ln.item for ln in lanes]
@@ -251,9 +249,12 @@ class LevelBatcher:
         subs = sum(r.sub_rows for r in reqs)
         nl = sum(r.n_open for r in reqs)
         with self._ctx():
-            target = torch.empty((S, R, Bs, 2), dtype=torch.int64, device=self.dev)
+            # one zero fill for the whole batch, on the coordinator stream; every tree's stream
+            # waits for it before its histogram passes add into the buffer
+            target = torch.zeros((S, R, Bs, 2), dtype=torch.int64, device=self.dev)
             out = torch.empty((R + subs, Bs, 2), dtype=torch.int64, device=self.dev)
             ag_in = torch.empty((nl, 5), dtype=torch.int64, device=self.dev)
+        self._join_out(lanes)
         row0 = sub0 = l0 = t = 0
         slots = []
         for ln, r in zip(lanes, reqs):
@@ -1140,6 +1141,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     presel = PRESELECT and sampled and dev.type == "cuda"
     item_groups = (Q.groups + Q.hot_groups) if sampled else []
     sel_ids = [gi for gi, grp in enumerate(item_groups) if grp.num_items] if presel else []
+    sel_args = None
     st = getattr(ws, "_levels", None)
     if st is None or st.max_depth != params.max_depth or st.n_sel != len(sel_ids):
         st = ws._levels = LevelState(Q, params.max_depth, len(sel_ids))
@@ -1371,13 +1373,12 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 mask_n = st.rf_mask[nxt]
                 C.tree_rf_sample(seed, int(tree_index), nxt_open, int(Q.num_features), int(params.feat_k),
                                  Q.fid_orig, st.rf_thr[nxt][:2 * n_open], mask_n, None)
-            st.counts[d, 4:].zero_()
-            sel = st.counts[d, 4:].view(len(sel_ids), 8)
-            for j, gi in enumerate(sel_ids):
-                grp = item_groups[gi]
-                lst, _ = ws.item_list(gi, grp)
-                C.tree_hist_select(grp.item_start, grp.item_f0, grp.item_meta, grp.wave_order(), Q.nbins, mask_n,
-                                   lst, sel[j])
+            if sel_args is None:
+                sel_args = ([[item_groups[gi].item_start, item_groups[gi].item_f0, item_groups[gi].item_meta,
+                              item_groups[gi].wave_order()] for gi in sel_ids],
+                            [ws.item_list(gi, item_groups[gi])[0] for gi in sel_ids])
+            C.tree_hist_select_groups(sel_args[0], Q.nbins, mask_n, sel_args[1],
+                                      st.counts[d, 4:].view(len(sel_ids), 8))
         st.counts_host[d].copy_(st.counts[d], non_blocking=dev.type == "cuda")
         ev = st.record_event(cur_stream)
         with tracing.span("tree.partition"):

@@ -8,6 +8,8 @@ of the measurement without skipping any work of the measured fit.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..data import synth
@@ -34,10 +36,15 @@ def warm_tree_kernels(dev, rows: int = 1 << 16, gbdt_depth: int = 6, gbdt_max_bi
     fo = feature_order(ip, ix, v, NUM_FEATURES)
     idf = torch.log((rows + 1.0) / (fo.df.double() + 1.0))
     vc = VectorColumn.tfidf(NUM_FEATURES, ip, ix, v, idf, fo)
-    if gbdt_depth > 0:
-        fit_gbdt(vc, y, GBDTParams(n_estimators=2, max_depth=gbdt_depth, max_bin=gbdt_max_bin), device=dev)
-    if forest_depth > 0:
-        fit_forest(vc, y, num_trees=2, max_depth=forest_depth, max_bins=32, bootstrap=True,
-                   feature_subset=forest_subset, seed=1, device=dev)
+    fault = os.environ.pop("FDX_FAULT", None)        # (injected faults target the measured fits)
+    try:
+        if gbdt_depth > 0:
+            fit_gbdt(vc, y, GBDTParams(n_estimators=2, max_depth=gbdt_depth, max_bin=gbdt_max_bin), device=dev)
+        if forest_depth > 0:
+            fit_forest(vc, y, num_trees=2, max_depth=forest_depth, max_bins=32, bootstrap=True,
+                       feature_subset=forest_subset, seed=1, device=dev)
+    finally:
+        if fault is not None:
+            os.environ["FDX_FAULT"] = fault
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
