@@ -1113,7 +1113,8 @@ void partition_cols(const Tensor& row_node, const Tensor& default_child, const T
                     const Tensor& cs_default, const Tensor& cs_other, const Tensor& cs_bin,
                     const Tensor& cs_left_default, const Tensor& counts, const Tensor& colptr, const Tensor& csc_row,
                     const Tensor& csc_bin, const optional<Tensor>& node_dense, const optional<Tensor>& dense,
-                    int64_t max_splits, int64_t wps) {
+                    int64_t max_splits, int64_t wps, const optional<Tensor>& pack_slot,
+                    const optional<Tensor>& pack_dig, const optional<Tensor>& pack) {
   const auto dev = row_node.device();
   chk(row_node, dev, at::kInt, "row_node");
   chk(default_child, dev, at::kInt, "default_child");
@@ -1144,6 +1145,20 @@ void partition_cols(const Tensor& row_node, const Tensor& default_child, const T
     a.node_dense = node_dense->data_ptr<int32_t>();
     a.dense = dense->data_ptr<uint8_t>();
     a.n_pad = dense->size(1);
+  }
+  FDX_CHECK(pack_slot.has_value() == pack.has_value() && pack_dig.has_value() == pack.has_value(),
+            "pack_slot, pack_dig and pack go together");
+  if (pack) {
+    chk(*pack_slot, dev, at::kInt, "pack_slot");
+    chk(*pack_dig, dev, at::kInt, "pack_dig");
+    chk(*pack, dev, at::kInt, "pack");
+    FDX_CHECK(pack_slot->numel() == a.num_nodes && pack_dig->numel() == 2 * a.N && pack->numel() == a.N,
+              "pack_slot [num_nodes], pack_dig [N, 2], pack [N]");
+    FDX_CHECK(reinterpret_cast<uintptr_t>(pack_dig->data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(pack->data_ptr()) % 16 == 0, "pack_dig / pack must be 16-byte aligned");
+    a.pack_slot = pack_slot->data_ptr<int32_t>();
+    a.pack_dig = reinterpret_cast<const uint32_t*>(pack_dig->data_ptr<int32_t>());
+    a.pack = reinterpret_cast<uint32_t*>(pack->data_ptr<int32_t>());
   }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());

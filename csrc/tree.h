@@ -439,7 +439,21 @@ struct PartitionArgs {
   const int32_t* node_dense;
   const uint8_t* dense;           // [Fh][n_pad]
   int64_t n_pad;
+  // optional (RF sampled levels): the next level's packed row state written with the partition
+  // (csrc/tree.h SlotArgs pack: slot of the row's new node | class-count digits << 8), so that
+  // level needs no row pass of its own: pack[r] from pack_slot[node] (the next level's node
+  // slots, level_plan's node_slot; -1 = not built) and the digit words pack_dig [N][2]
+  const int32_t* pack_slot;
+  const uint32_t* pack_dig;
+  uint32_t* pack;
 };
+
+FDX_HD uint32_t partition_pack_word(const PartitionArgs& a, int32_t node, int64_t r) {
+  const int32_t s = (node >= 0 && node < a.num_nodes) ? a.pack_slot[node] : -1;
+  const uint32_t sb = (s >= 0 && s < 255) ? (uint32_t)s : 0xffu;
+  const uint32_t d0 = a.pack_dig[2 * r], d1 = a.pack_dig[2 * r + 1];
+  return sb | ((d0 & 0xffu) << 8) | ((d1 & 0xffu) << 16);
+}
 
 // Child of row r of split node n in the row pass.
 FDX_HD int32_t partition_row_child(const PartitionArgs& a, int32_t n, int64_t r) {

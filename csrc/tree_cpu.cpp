@@ -391,7 +391,10 @@ void partition_cols_cpu(const PartitionArgs& a, const int64_t* colptr, const int
     for (int64_t e = colptr[f]; e < colptr[f + 1]; ++e) {
       const int32_t row = a.csc_row[e];
       const bool left = (int32_t)a.csc_bin[e] <= thr;
-      if (left != left_default && a.row_node[row] == dflt) a.row_node[row] = other;
+      if (left != left_default && a.row_node[row] == dflt) {
+        a.row_node[row] = other;
+        if (a.pack) a.pack[row] = partition_pack_word(a, other, row);
+      }
     }
   }
 }
@@ -399,11 +402,12 @@ void partition_cols_cpu(const PartitionArgs& a, const int64_t* colptr, const int
 void partition_cpu(const PartitionArgs& a) {
   parallel_for(a.N, 0, 1 << 16, [&](int64_t lo, int64_t hi) {
     for (int64_t r = lo; r < hi; ++r) {
-      const int32_t n = a.row_node[r];
+      int32_t n = a.row_node[r];
       if (n >= 0 && n < a.num_nodes) {
         const int32_t c = partition_row_child(a, n, r);
-        if (c >= 0) a.row_node[r] = c;
+        if (c >= 0) a.row_node[r] = n = c;
       }
+      if (a.pack) a.pack[r] = partition_pack_word(a, n, r);
     }
   });
   for (int it = 0; it < a.num_items; ++it) {

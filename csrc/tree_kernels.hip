@@ -943,13 +943,32 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
       for (int k = 0; k < kPartRows; ++k) n[k] = c[k] >= 0 ? c[k] : n[k];
       p[0] = make_int4(n[0], n[1], n[2], n[3]);
       p[1] = make_int4(n[4], n[5], n[6], n[7]);
+      if (a.pack != nullptr) {
+        // the next level's packed row state (8 rows: 64 B of digit words in, 32 B out)
+        const int4* dg = reinterpret_cast<const int4*>(a.pack_dig + 2 * r0);
+        uint32_t w[kPartRows];
+#pragma unroll
+        for (int k = 0; k < kPartRows / 2; ++k) {
+          const int4 d = dg[k];
+          const int32_t s0 = (n[2 * k] >= 0 && n[2 * k] < a.num_nodes) ? a.pack_slot[n[2 * k]] : -1;
+          const int32_t s1 = (n[2 * k + 1] >= 0 && n[2 * k + 1] < a.num_nodes) ? a.pack_slot[n[2 * k + 1]] : -1;
+          w[2 * k] = ((s0 >= 0 && s0 < 255) ? (uint32_t)s0 : 0xffu) | (((uint32_t)d.x & 0xffu) << 8) |
+                     (((uint32_t)d.y & 0xffu) << 16);
+          w[2 * k + 1] = ((s1 >= 0 && s1 < 255) ? (uint32_t)s1 : 0xffu) | (((uint32_t)d.z & 0xffu) << 8) |
+                         (((uint32_t)d.w & 0xffu) << 16);
+        }
+        int4* q = reinterpret_cast<int4*>(a.pack + r0);
+        q[0] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+        q[1] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
+      }
     } else {
       for (int64_t r = r0; r < a.N; ++r) {
-        const int32_t n = a.row_node[r];
+        int32_t n = a.row_node[r];
         if (n >= 0 && n < a.num_nodes) {
           const int32_t c = partition_row_child(a, n, r);
-          if (c >= 0) a.row_node[r] = c;
+          if (c >= 0) a.row_node[r] = n = c;
         }
+        if (a.pack != nullptr) a.pack[r] = partition_pack_word(a, n, r);
       }
     }
   }
@@ -983,7 +1002,10 @@ __global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, co
   for (int64_t e = colptr[f] + (int64_t)part * 256 + threadIdx.x; e < e1; e += (int64_t)wps * 256) {
     const int32_t row = a.csc_row[e];
     const bool left = (int32_t)a.csc_bin[e] <= thr;
-    if (left != left_default && a.row_node[row] == dflt) a.row_node[row] = other;
+    if (left != left_default && a.row_node[row] == dflt) {
+      a.row_node[row] = other;
+      if (a.pack != nullptr) a.pack[row] = partition_pack_word(a, other, row);
+    }
   }
 }
 

@@ -297,6 +297,10 @@ LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
 # RF levels >= 1 launch one wave per active work item from lists compacted with the previous
 # level's plan (0: the r4 passes, a wave per item slot or a fixed listed grid)
 PRESELECT = os.environ.get("FDX_RF_PRESELECT", "1") == "1"
+# RF levels >= 1 read the packed row state (slot | class-count digits) written by the previous
+# level's partition instead of a row pass of their own (slot pack / masked digits: ~87 us per level
+# at 10M rows, 173 ms of a 500-tree forest's kernel time, profiles/r5/NOTES.md)
+FUSED_PACK = os.environ.get("FDX_RF_FUSED_PACK", "1") == "1"
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
 RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
 # split search: a wave per (node, feature) for the features with > 16 bins
@@ -1241,11 +1245,15 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             rg = ws.rowgroups() if (not build_all and np_ == 4) else None
             if d > 0:
                 # a single built node: the CSC passes run the root kernel on digit words zeroed
-                # outside it (no per-entry slot gather, no compaction; zero rows add nothing)
-                single = n_build == 1 and rg is None
+                # outside it (no per-entry slot gather, no compaction; zero rows add nothing).
+                # Sampled RF levels with FUSED_PACK read the packed row state the previous level's
+                # partition wrote (no row pass here at all)
+                single = n_build == 1 and rg is None and not (sampled and FUSED_PACK)
                 if single and getattr(ws, "rowdig_masked", None) is None:
                     ws.rowdig_masked = torch.empty_like(ws.rowdig)
-                if rg is None and sampled and not single:
+                if sampled and FUSED_PACK:
+                    pass
+                elif rg is None and sampled and not single:
                     C.tree_slot_pack(ws.row_node, st.node_slot, n_build, ws.rowdig, ws.rowpack())
                 elif rg is None:        # (the row-group engine lists the built rows from row_node itself)
                     C.tree_slot8(ws.row_node, st.node_slot, 0, n_build, ws.slot8, ws.rowdig if single else None,
@@ -1382,8 +1390,11 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         st.counts_host[d].copy_(st.counts[d], non_blocking=dev.type == "cuda")
         ev = st.record_event(cur_stream)
         with tracing.span("tree.partition"):
+            # (sampled RF levels: the next level's packed row state is written on the way)
+            fuse = sampled and FUSED_PACK and d + 1 < params.max_depth
             C.tree_partition_cols(ws.row_node, st.default_child, *st.cs, st.counts[d], Q.colptr, Q.csc_row, Q.csc_bin,
-                                  st.node_dense, Q.dense if st.node_dense is not None else None, n_open, PARTITION_WPS)
+                                  st.node_dense, Q.dense if st.node_dense is not None else None, n_open, PARTITION_WPS,
+                                  *((st.node_slot, ws.rowdig, ws.rowpack()) if fuse else (None, None, None)))
         if shards is None and d + 1 < params.max_depth:
             pre_hist = torch.zeros((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
         prev_hist = cur_hist
