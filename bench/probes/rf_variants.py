@@ -34,6 +34,8 @@ VARIANTS = {
     "l32g2": {(forest_batch, "TREES_IN_FLIGHT"): 32, (forest_batch, "LANE_GROUPS"): 2},
     "l32g4": {(forest_batch, "TREES_IN_FLIGHT"): 32, (forest_batch, "LANE_GROUPS"): 4},
     "g1": {(forest_batch, "LANE_GROUPS"): 1},
+    "nonative": {(grower, "NATIVE_LEVELS"): False},
+    "nonative_nopresel": {(grower, "NATIVE_LEVELS"): False, (grower, "PRESELECT"): False},
 }
 
 

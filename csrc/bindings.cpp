@@ -583,11 +583,13 @@ void host_unregister(const Tensor& t) {
 
 void register_tree_ops(pybind11::module& m);
 void register_kafka_ops(pybind11::module& m);
+void register_level_ops(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native core of fraud_detection_spark_kafka_llm_amd";
   register_tree_ops(m);
   register_kafka_ops(m);
+  register_level_ops(m);
   m.def("token_keys", &token_keys, "CountVectorizer fit: 64-bit token keys (count pass / key pass)");
   m.def("featurize_score", &featurize_score, "Fused clean/tokenize/stopword/hash/idf/score");
   m.def("score_csr", &score_csr, "LR / tree-ensemble scoring of a CSR feature matrix");

@@ -1,0 +1,396 @@
+// Native per-level driver of the device level loop (models/grower.py device_tree_steps) for the
+// RandomForest / DecisionTree class-count trees (np = 1, sampled passes).
+//
+// A forest level is a handful of small launches (histogram passes per item group, split search,
+// best split, level plan, next level's feature sample + data-parallel layout, count copy,
+// partition). Driven from Python, each costs a pybind call that converts 10-30 tensor arguments
+// plus the interpreter glue between them: ~220 us of host time per tree-level, against a GPU that
+// finishes the level's kernels of a 1.25M-row shard (BASELINE config 3 at DP=8) much sooner -- the
+// forest was host bound (bench/probes/rf_host_probe.py --forced: ~5 % of the wall blocked on the
+// device). An RfLevels object is built once per lane workspace with every buffer that stays put
+// (item groups, CSC, node table, level tables, scratch), and a level is three calls -- hist, split,
+// tail -- whose arguments are the few per-level tensors. The kernels and their arguments are
+// exactly those of the single-purpose bindings (bindings_tree.cpp), so the trees are bitwise the
+// same (tests: the device loop with and without the runner, and every DP world size).
+#include <torch/extension.h>
+
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "ops.h"
+#include "tree.h"
+
+namespace {
+
+namespace py = pybind11;
+using at::Tensor;
+using c10::optional;
+
+#define FDX_CHECK(cond, msg) TORCH_CHECK(cond, "fdx.level: ", msg)
+
+hipStream_t cur_stream(const at::Device& d) { return c10::hip::getCurrentHIPStream(d.index()).stream(); }
+
+Tensor get(const py::dict& c, const char* k) { return c[k].cast<Tensor>(); }
+
+optional<Tensor> get_opt(const py::dict& c, const char* k) {
+  if (!c.contains(k) || c[k].is_none()) return c10::nullopt;
+  return c[k].cast<Tensor>();
+}
+
+template <class T>
+T* p(const Tensor& t) { return t.data_ptr<T>(); }
+
+template <class T>
+T* p(const optional<Tensor>& t) { return (t && t->defined()) ? t->data_ptr<T>() : nullptr; }
+
+struct ItemGroup {
+  Tensor start, end, f0, meta, wave;
+  int bt = 1;
+};
+
+class RfLevels {
+ public:
+  explicit RfLevels(const py::dict& c) {
+    for (auto g : c["groups"].cast<py::list>()) {
+      auto t = g.cast<py::tuple>();
+      ItemGroup ig;
+      ig.start = t[0].cast<Tensor>();
+      ig.end = t[1].cast<Tensor>();
+      ig.f0 = t[2].cast<Tensor>();
+      ig.meta = t[3].cast<Tensor>();
+      ig.wave = t[4].cast<Tensor>();
+      ig.bt = t[5].cast<int>();
+      groups_.push_back(ig);
+    }
+    h_row_ = get(c, "h_row");
+    h_key_ = get(c, "h_key");
+    csc_row_ = get(c, "csc_row");
+    csc_bin_ = get(c, "csc_bin");
+    colptr_ = get(c, "colptr");
+    nbins_ = get(c, "nbins");
+    zbin_ = get(c, "zbin");
+    fid_orig_ = get(c, "fid_orig");
+    dense_ = get_opt(c, "dense");
+    hot_row_ = get_opt(c, "hot_row");
+    rowdig_ = get(c, "rowdig");
+    rowpack_ = get(c, "rowpack");
+    row_node_ = get(c, "row_node");
+    kexp_ = get(c, "kexp");
+    for (const char* k : {"stats", "parent", "left", "right", "feat", "bin", "leaf", "gain", "n_nodes", "counts",
+                          "counts_host", "default_child", "cs_feat", "cs_default", "cs_other", "cs_bin",
+                          "cs_left_default", "node_slot", "s2n", "sub_dst", "sub_par", "sub_sib"})
+      st_[k] = get(c, k);
+    node_dense_ = get_opt(c, "node_dense");
+    wide_ = get_opt(c, "wide");
+    mode_ = c["mode"].cast<int>();
+    max_depth_ = c["max_depth"].cast<int>();
+    min_gain_ = c["min_gain"].cast<double>();
+    lambda_ = c["lambda_"].cast<double>();
+    mcw_ = c["mcw"].cast<double>();
+    seed_ = c["seed"].cast<int64_t>();
+    F_ = c["F"].cast<int64_t>();
+    k_ = c["k"].cast<int64_t>();
+    lds_ = c["lds"].cast<bool>();
+    wps_ = c["wps"].cast<int>();
+    dev_ = row_node_.device();
+    FDX_CHECK(dev_.is_cuda(), "the level runner drives device levels only");
+    const int64_t cap = st_["s2n"].numel();
+    scratch_ = at::empty({fdx::rf_scratch_bytes(2 * cap)}, row_node_.options().dtype(at::kByte));
+  }
+
+  // Histogram passes of level d over every item group (tree_hist_sampled per group): hist [*, stride, 2]
+  // accumulated at node rows s2n[slot]; pack: the packed row state (None at the root); lists[j] /
+  // counts[j] / npx[j]: group j's listed pass (None: a wave per item slot; npx -1: compacted here).
+  void hist(int64_t n_build, const Tensor& hist, const Tensor& boff, const Tensor& feat_mask, const Tensor& s2n,
+            const optional<Tensor>& pack, const std::vector<optional<Tensor>>& lists,
+            const std::vector<optional<Tensor>>& counts, const std::vector<int64_t>& npx) {
+    FDX_CHECK(lists.size() == groups_.size() && counts.size() == groups_.size() && npx.size() == groups_.size(),
+              "one list / count / npx per item group");
+    FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && hist.scalar_type() == at::kLong, "hist [rows, stride, 2] int64");
+    FDX_CHECK(boff.numel() == nbins_.numel() + 1 && feat_mask.numel() == nbins_.numel(), "boff [Fa + 1], mask [Fa]");
+    FDX_CHECK(n_build >= 1 && n_build <= 8 * 8 && s2n.numel() >= n_build, "slots");
+    const int ct = pass_ct(n_build);
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    for (size_t j = 0; j < groups_.size(); ++j) {
+      const ItemGroup& g = groups_[j];
+      const int64_t I = g.start.numel();
+      if (I == 0) continue;
+      fdx::HistArgs a{};
+      a.listed_per_xcd = -1;
+      a.item_start = p<int64_t>(g.start);
+      a.item_end = p<int64_t>(g.end);
+      a.item_f0 = p<int32_t>(g.f0);
+      a.item_meta = p<int32_t>(g.meta);
+      a.num_items = (int32_t)I;
+      a.csc_row = p<int32_t>(h_row_);
+      a.csc_key = p<uint8_t>(h_key_);
+      a.rowdig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
+      a.boff = p<int64_t>(boff);
+      a.nbins = p<int32_t>(nbins_);
+      a.slot_node = p<int32_t>(s2n);
+      a.nslots = (int32_t)n_build;
+      a.hist_stride = hist.size(1);
+      a.hist = p<int64_t>(hist);
+      a.wave_item = p<int32_t>(g.wave);
+      a.num_slots = (int32_t)g.wave.numel();
+      a.feat_active = p<uint8_t>(feat_mask);
+      if (pack) a.rowpack = reinterpret_cast<const uint32_t*>(p<int32_t>(*pack));
+      if (lists[j]) {
+        FDX_CHECK(counts[j].has_value(), "a listed pass needs its count");
+        const int64_t cap = ((a.num_slots + 3) / 4 + 7) / 8 * 4;
+        FDX_CHECK(lists[j]->numel() >= 8 * cap && counts[j]->numel() >= 8 && npx[j] <= cap, "list / count sizes");
+        a.active_list = p<int32_t>(*lists[j]);
+        a.active_count = p<int32_t>(*counts[j]);
+        a.list_cap = (int32_t)cap;
+        a.listed_per_xcd = (int32_t)npx[j];
+      }
+      a.lds = (lds_ && 4 * 16 * g.bt * n_build * 8 <= 65536) ? 1 : 0;
+      fdx::launch_hist(a, g.bt, ct, 1, s);
+    }
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+
+  // Split search of the open nodes (split_find + split_best): hist rows [nodes, stride, 2] (row_of:
+  // a node's row; None: node i = row i), best tuples into out [nodes, 5] with features + f0.
+  void split(const Tensor& hist, const Tensor& totals, const Tensor& boff, const Tensor& nbins, const Tensor& zbin,
+             const Tensor& fid_orig, const Tensor& node_ids, const optional<Tensor>& feat_thr, int64_t tree, int64_t f0,
+             const Tensor& out, const optional<Tensor>& row_of, const optional<Tensor>& wide) {
+    const int32_t nodes = (int32_t)node_ids.numel(), Fa = (int32_t)nbins.numel();
+    FDX_CHECK(out.numel() == 5ll * nodes && out.is_contiguous() && boff.numel() == Fa + 1, "out [nodes, 5], boff");
+    FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && (row_of || hist.size(0) >= nodes), "hist rows");
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    if (nodes == 0) return;
+    if (Fa == 0) {                         // a shard without features: no candidate anywhere
+      const double ninf = -1.0 / 0.0;
+      int64_t bits;
+      std::memcpy(&bits, &ninf, sizeof(double));
+      Tensor o = out.view({nodes, 5});
+      o.zero_();
+      o.select(1, 0).fill_(bits);
+      o.narrow(1, 1, 2).fill_(-1);
+      return;
+    }
+    const int64_t need = (int64_t)nodes * Fa;
+    if (!gain_.defined() || gain_.numel() < need) {
+      gain_ = at::empty({need}, out.options().dtype(at::kDouble));
+      sbin_ = at::empty({need}, out.options().dtype(at::kInt));
+      sleft_ = at::empty({2 * need}, out.options().dtype(at::kLong));
+    }
+    fdx::SplitArgs a{};
+    a.hist = p<int64_t>(hist);
+    a.totals = p<int64_t>(totals);
+    a.hist_stride = hist.size(1);
+    a.num_nodes = nodes;
+    a.Fa = Fa;
+    a.boff = p<int64_t>(boff);
+    a.nbins = p<int32_t>(nbins);
+    a.zbin = p<int32_t>(zbin);
+    a.fid_orig = p<int64_t>(fid_orig);
+    a.node_ids = p<int32_t>(node_ids);
+    a.kexp = p<int32_t>(kexp_);
+    a.mode = mode_;
+    a.lambda_ = lambda_;
+    a.min_child_weight = mcw_;
+    a.feat_thr = p<double>(feat_thr);
+    a.seed = (uint64_t)seed_;
+    a.tree = (int32_t)tree;
+    a.out_gain = p<double>(gain_);
+    a.out_bin = p<int32_t>(sbin_);
+    a.out_left = p<int64_t>(sleft_);
+    if (wide && wide->numel() > 0) {
+      a.wide = p<int32_t>(*wide);
+      a.n_wide = (int32_t)wide->numel();
+    }
+    a.row_of = p<int32_t>(row_of);
+    fdx::launch_split(a, s);
+    fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), nodes, Fa, f0, p<int64_t>(out), s);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+
+  // Level plan of level d (tree.h level_plan) from the best tuples packed [L, 5] / [S, L, 5]; then,
+  // for a next level, its feature sample over the (-1 padded) next open list into thr / mask, the
+  // compact DP layout (local / sizes, sizes copied to sizes_host) when given, and the per-group
+  // active-item lists (sel_lists / counts[d, 4:]); the level's counts to counts_host[d].
+  void plan(int64_t d, int64_t n_open, const Tensor& packed, const Tensor& open, const Tensor& n_open_ptr,
+            const Tensor& next_open, const Tensor& next_totals, int64_t tree, bool sample_next,
+            const optional<Tensor>& thr, const optional<Tensor>& mask, const optional<Tensor>& fs,
+            const optional<Tensor>& nbins_all, const optional<Tensor>& local, const optional<Tensor>& sizes,
+            const optional<Tensor>& sizes_host, const std::vector<optional<Tensor>>& sel_lists) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    const Tensor& counts = st_["counts"];
+    const int64_t cw = counts.size(1);
+    int32_t* counts_d = p<int32_t>(counts) + d * cw;
+    fdx::LevelPlanArgs a{};
+    a.packed = p<int64_t>(packed);
+    a.L = (int32_t)n_open;
+    a.n_shards = packed.dim() == 3 ? (int32_t)packed.size(0) : 1;
+    a.shard_stride = packed.dim() == 3 ? packed.stride(0) : packed.size(-2) * 5;
+    FDX_CHECK(packed.size(-1) == 5 && packed.stride(-1) == 1 && packed.stride(-2) == 5 && packed.size(-2) >= n_open,
+              "packed rows of 5");
+    a.depth = (int32_t)d;
+    a.max_depth = max_depth_;
+    a.mode = mode_;
+    a.build_all = 1;
+    a.kexp = p<int32_t>(kexp_);
+    a.min_gain = min_gain_;
+    a.zbin = p<int32_t>(zbin_);
+    a.hot_row = p<int32_t>(hot_row_);
+    a.max_nodes = (int32_t)st_["parent"].numel();
+    a.n_nodes = p<int32_t>(st_["n_nodes"]);
+    a.stats = p<int64_t>(st_["stats"]);
+    a.parent = p<int32_t>(st_["parent"]);
+    a.left = p<int32_t>(st_["left"]);
+    a.right = p<int32_t>(st_["right"]);
+    a.feat = p<int32_t>(st_["feat"]);
+    a.bin = p<int32_t>(st_["bin"]);
+    a.leaf = p<uint8_t>(st_["leaf"]);
+    a.gain = p<double>(st_["gain"]);
+    a.open = p<int32_t>(open);
+    a.n_open = p<int32_t>(n_open_ptr);
+    a.default_child = p<int32_t>(st_["default_child"]);
+    a.node_dense = p<int32_t>(node_dense_);
+    a.cs_feat = p<int32_t>(st_["cs_feat"]);
+    a.cs_default = p<int32_t>(st_["cs_default"]);
+    a.cs_other = p<int32_t>(st_["cs_other"]);
+    a.cs_bin = p<int32_t>(st_["cs_bin"]);
+    a.cs_left_default = p<int32_t>(st_["cs_left_default"]);
+    a.counts = counts_d;
+    a.next_open = p<int32_t>(next_open);
+    a.next_totals = p<int64_t>(next_totals);
+    a.node_slot = p<int32_t>(st_["node_slot"]);
+    a.s2n = p<int32_t>(st_["s2n"]);
+    a.sub_dst = p<int32_t>(st_["sub_dst"]);
+    a.sub_par = p<int32_t>(st_["sub_par"]);
+    a.sub_sib = p<int32_t>(st_["sub_sib"]);
+    fdx::launch_level_plan(a, s);
+    if (sample_next) {
+      FDX_CHECK(thr && mask, "a next-level sample needs thr and mask");
+      fdx::RfSampleArgs r{};
+      r.seed = (uint64_t)seed_;
+      r.tree = (int32_t)tree;
+      r.nodes = p<int32_t>(next_open);
+      r.nnodes = (int32_t)(2 * n_open);
+      r.F = F_;
+      r.k = k_;
+      r.fid_orig = p<int64_t>(fid_orig_);
+      r.Fa = fid_orig_.numel();
+      r.thr = p<double>(*thr);
+      r.mask = p<uint8_t>(*mask);
+      FDX_CHECK(next_open.numel() >= 2 * n_open && thr->numel() >= 2 * n_open && mask->numel() == r.Fa &&
+                    scratch_.numel() >= fdx::rf_scratch_bytes(r.nnodes), "next-level sample sizes");
+      r.scratch = p<uint8_t>(scratch_);
+      fdx::launch_rf_sample(r, s);
+      if (local) {
+        fdx::RfCompactArgs cp{};
+        cp.mask = p<uint8_t>(*mask);
+        cp.nbins = p<int32_t>(*nbins_all);
+        cp.fs = p<int64_t>(*fs);
+        cp.S = (int32_t)(fs->numel() - 1);
+        cp.Fa = mask->numel();
+        cp.local = p<int64_t>(*local);
+        cp.sizes = p<int64_t>(*sizes);
+        fdx::launch_rf_compact(cp, s);
+        FDX_CHECK(hipMemcpyAsync(sizes_host->data_ptr(), sizes->data_ptr(), sizes->nbytes(), hipMemcpyDeviceToHost, s) ==
+                      hipSuccess, "sizes copy");
+      }
+      if (!sel_lists.empty()) {
+        // per-XCD counts of the selected groups (the non-None lists, in group order) at counts[d, 4 + 8 js]
+        int64_t n_sel = 0;
+        for (const auto& l : sel_lists) n_sel += l ? 1 : 0;
+        FDX_CHECK(sel_lists.size() == groups_.size() && cw >= 4 + 8 * n_sel, "select lists");
+        FDX_CHECK(hipMemsetAsync(counts_d + 4, 0, 8 * n_sel * sizeof(int32_t), s) == hipSuccess, "memset");
+        int64_t js = 0;
+        for (size_t j = 0; j < groups_.size(); ++j) {
+          if (!sel_lists[j]) continue;
+          const ItemGroup& g = groups_[j];
+          fdx::HistArgs h{};
+          h.listed_per_xcd = -1;
+          h.item_start = p<int64_t>(g.start);
+          h.item_f0 = p<int32_t>(g.f0);
+          h.item_meta = p<int32_t>(g.meta);
+          h.num_items = (int32_t)g.start.numel();
+          h.nbins = p<int32_t>(nbins_);
+          h.feat_active = p<uint8_t>(*mask);
+          h.wave_item = p<int32_t>(g.wave);
+          h.num_slots = (int32_t)g.wave.numel();
+          h.active_list = p<int32_t>(*sel_lists[j]);
+          h.active_count = counts_d + 4 + 8 * js++;
+          h.list_cap = (int32_t)(((h.num_slots + 3) / 4 + 7) / 8 * 4);
+          fdx::launch_hist_select(h, s);
+        }
+      }
+    }
+    const Tensor& ch = st_["counts_host"];
+    FDX_CHECK(hipMemcpyAsync(p<int32_t>(ch) + d * cw, counts_d, cw * sizeof(int32_t), hipMemcpyDeviceToHost, s) ==
+                  hipSuccess, "counts copy");
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+
+  // Partition of level d (tree_partition_cols), writing the next level's packed row state when fuse.
+  void partition(int64_t d, int64_t n_open, bool fuse) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    fdx::PartitionArgs a{};
+    a.row_node = p<int32_t>(row_node_);
+    a.default_child = p<int32_t>(st_["default_child"]);
+    a.num_nodes = (int32_t)st_["default_child"].numel();
+    a.N = row_node_.numel();
+    a.split_default = p<int32_t>(st_["cs_default"]);
+    a.split_other = p<int32_t>(st_["cs_other"]);
+    a.split_bin = p<int32_t>(st_["cs_bin"]);
+    a.split_left_is_default = p<int32_t>(st_["cs_left_default"]);
+    a.csc_row = p<int32_t>(csc_row_);
+    a.csc_bin = p<uint8_t>(csc_bin_);
+    if (node_dense_) {
+      a.node_dense = p<int32_t>(node_dense_);
+      a.dense = p<uint8_t>(dense_);
+      a.n_pad = dense_->size(1);
+    }
+    if (fuse) {
+      a.pack_slot = p<int32_t>(st_["node_slot"]);
+      a.pack_dig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
+      a.pack = reinterpret_cast<uint32_t*>(p<int32_t>(rowpack_));
+    }
+    const Tensor& counts = st_["counts"];
+    fdx::launch_partition_cols(a, p<int64_t>(colptr_), p<int32_t>(st_["cs_feat"]), p<int32_t>(counts) + d * counts.size(1),
+                               (int32_t)n_open, (int32_t)wps_, s);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+
+ private:
+  static int pass_ct(int64_t n) {
+    int ct = 1;
+    while (ct * 8 < n) ct *= 2;          // 8 slots per 16-column tile at np = 1 (grower.pass_ct)
+    return ct;
+  }
+
+  std::vector<ItemGroup> groups_;
+  Tensor h_row_, h_key_, csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, rowpack_, row_node_, kexp_;
+  optional<Tensor> dense_, hot_row_, node_dense_, wide_;
+  std::map<std::string, Tensor> st_;
+  Tensor scratch_, gain_, sbin_, sleft_;
+  int mode_ = 1, max_depth_ = 5, wps_ = 256;
+  double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;
+  int64_t seed_ = 0, F_ = 1, k_ = 1;
+  bool lds_ = true;
+  at::Device dev_{at::kCPU};
+};
+
+}  // namespace
+
+void register_level_ops(pybind11::module& m) {
+  py::class_<RfLevels>(m, "RfLevels")
+      .def(py::init<const py::dict&>())
+      .def("hist", &RfLevels::hist)
+      .def("split", &RfLevels::split)
+      .def("plan", &RfLevels::plan)
+      .def("partition", &RfLevels::partition);
+}

@@ -301,6 +301,9 @@ PRESELECT = os.environ.get("FDX_RF_PRESELECT", "1") == "1"
 # level's partition instead of a row pass of their own (slot pack / masked digits: ~87 us per level
 # at 10M rows, 173 ms of a 500-tree forest's kernel time, profiles/r5/NOTES.md)
 FUSED_PACK = os.environ.get("FDX_RF_FUSED_PACK", "1") == "1"
+# RF device levels issue their kernels through the native per-level runner (csrc/bindings_level.cpp
+# RfLevels: hist / split / plan / partition, one host call each) instead of ~20 Python-level calls
+NATIVE_LEVELS = os.environ.get("FDX_NATIVE_LEVELS", "1") == "1"
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
 RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
 # split search: a wave per (node, feature) for the features with > 16 bins
@@ -630,6 +633,13 @@ class FeatureShards:
         C.tree_rf_sample(seed, tree, nodes, F, k, fid_orig, thr[:n], self._mask[p], None)
         C.tree_rf_compact(self._mask[p], self._nbins_all, self._fs_dev, self._local_c[p], self._sizes[p])
         self.sizes_host[p].copy_(self._sizes[p], non_blocking=nodes.is_cuda)
+
+    def compact_thr(self, p: int, n: int) -> torch.Tensor:
+        """The parity-``p`` per-node sampling thresholds, at least ``n`` long (sample_compact's)."""
+        thr = self._thr[p]
+        if thr is None or thr.numel() < n:
+            thr = self._thr[p] = torch.empty(max(n, 2), dtype=torch.float64, device=self._mask[p].device)
+        return thr
 
     def compact_mask(self, p: int) -> torch.Tensor:
         """The parity-``p`` level's union feature mask (sample_compact)."""
@@ -1113,6 +1123,41 @@ def drive(steps, batcher: Optional[LevelBatcher] = None):
         return stop.value
 
 
+def _wide_features(nbins: torch.Tensor, Fa: int) -> torch.Tensor:
+    """Indices of the features with > 16 bins (split_wide_kernel), memoised on the nbins tensor."""
+    memo = getattr(nbins, "_fdx_wide", None)
+    if memo is None or memo[0] != Fa:
+        idx = np.nonzero(nbins[:Fa].cpu().numpy() > 16)[0].astype(np.int32)
+        memo = (Fa, torch.from_numpy(idx).to(nbins.device))
+        nbins._fdx_wide = memo
+    return memo[1]
+
+
+def _rf_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowParams, item_groups: list):
+    """The lane's native level runner (csrc/bindings_level.cpp RfLevels), built once per workspace,
+    level state and tree parameters."""
+    key = (id(st), params.mode, params.max_depth, params.min_gain, params.min_child, params.seed, params.feat_k)
+    cached = getattr(ws, "_rf_runner", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    cfg = dict(groups=[(g.item_start, g.item_end, g.item_f0, g.item_meta, g.wave_order(), int(g.bt))
+                       for g in item_groups],
+               h_row=Q.h_row, h_key=Q.h_key, csc_row=Q.csc_row, csc_bin=Q.csc_bin, colptr=Q.colptr, nbins=Q.nbins,
+               zbin=Q.zbin, fid_orig=Q.fid_orig, dense=Q.dense if st.node_dense is not None else None,
+               hot_row=st.hot_row, rowdig=ws.rowdig, rowpack=ws.rowpack(), row_node=ws.row_node, kexp=ws.kexp,
+               stats=st.stats, parent=st.parent, left=st.left, right=st.right, feat=st.feat, bin=st.bin, leaf=st.leaf,
+               gain=st.gain, n_nodes=st.n_nodes, counts=st.counts, counts_host=st.counts_host,
+               default_child=st.default_child, cs_feat=st.cs[0], cs_default=st.cs[1], cs_other=st.cs[2],
+               cs_bin=st.cs[3], cs_left_default=st.cs[4], node_slot=st.node_slot, s2n=st.s2n, sub_dst=st.sub_dst,
+               sub_par=st.sub_par, sub_sib=st.sub_sib, node_dense=st.node_dense, mode=int(params.mode),
+               max_depth=int(params.max_depth), min_gain=float(params.min_gain), lambda_=float(params.lambda_),
+               mcw=float(params.min_child), seed=int(params.seed), F=int(Q.num_features), k=int(params.feat_k),
+               lds=bool(RF_LDS), wps=int(PARTITION_WPS))
+    runner = native.lib().RfLevels(cfg)
+    ws._rf_runner = (key, runner)
+    return runner
+
+
 def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
                       h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
                       shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
@@ -1149,6 +1194,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     st = getattr(ws, "_levels", None)
     if st is None or st.max_depth != params.max_depth or st.n_sel != len(sel_ids):
         st = ws._levels = LevelState(Q, params.max_depth, len(sel_ids))
+    runner = _rf_runner(Q, ws, st, params, item_groups) if (sampled and NATIVE_LEVELS and dev.type == "cuda") \
+        else None
     ws.row_node.zero_()
     # every step of this generator runs on the stream current now (the forest driver advances a
     # lane inside that lane's stream context)
@@ -1287,6 +1334,24 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 sel_groups, use_dense = [], False
             if sel_groups is None:
                 sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
+            if runner is not None:
+                pack = ws.rowpack() if (d > 0 and not single) else None
+                lists, cnts, npxs = [], [], []
+                for gi, grp in enumerate(sel_groups):
+                    lst = cnt = None
+                    npx = -1
+                    if grp.num_items and sel_ids and d > 0:
+                        j = sel_ids.index(gi)
+                        lst = ws.item_list(gi, grp)[0]
+                        cnt = st.counts[d - 1, 4 + 8 * j: 12 + 8 * j]
+                        npx = per_xcd[gi]
+                    elif grp.num_items and n_open <= LISTED_MAX_NODES:
+                        lst, cnt = ws.item_list(gi, grp)
+                    lists.append(lst)
+                    cnts.append(cnt)
+                    npxs.append(npx)
+                runner.hist(n_build, hist_target, h_boff, feat_mask, s2n, pack, lists, cnts, npxs)
+                sel_groups = []
             for gi, grp in enumerate(sel_groups):
                 if grp.num_items == 0:
                     continue
@@ -1353,7 +1418,18 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 C.tree_hist_subtract(prev_hist, cur_hist, st.dst_row[:n_build], st.par_row[:n_build],
                                      st.sib_row[:n_build], bufs.Bs)
         with tracing.span("tree.split"):
-            if shards is None:
+            if runner is not None and shards is None:
+                packed = ws.split_cache.get(("out", n_open))
+                if packed is None:
+                    packed = ws.split_cache[("out", n_open)] = torch.empty((n_open, 5), dtype=torch.int64, device=dev)
+                runner.split(cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, feat_thr, int(tree_index),
+                             0, packed, None, _wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None)
+            elif runner is not None:
+                runner.split(cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig, open_d,
+                             feat_thr, int(tree_index), shards.f0, bufs.ag_in, row_of,
+                             _wide_features(shards.nbins, shards.Fa) if SPLIT_WIDE else None)
+                packed = yield CollStep("ag")
+            elif shards is None:
                 packed = _best_splits(C, cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, ws.kexp,
                                       params, feat_thr, tree_index, Q.Fa, 0, cache=ws.split_cache)
             else:
@@ -1364,6 +1440,32 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 # shards per node (ties to the lowest shard = the lowest feature)
                 packed = yield CollStep("ag")
         nxt = 1 - cur
+        if runner is not None:
+            more = d + 1 < params.max_depth
+            sample_next = more and (compact or bool(sel_ids))
+            if sample_next and compact:
+                thr_n, mask_n = shards.compact_thr(nxt, 2 * n_open), shards.compact_mask(nxt)
+                lay = (shards._fs_dev, Q.nbins, shards._local_c[nxt], shards._sizes[nxt], shards.sizes_host[nxt])
+            elif sample_next:
+                thr_n, mask_n, lay = st.rf_thr[nxt], st.rf_mask[nxt], (None,) * 5
+            else:
+                thr_n = mask_n = None
+                lay = (None,) * 5
+            if sel_ids and more:
+                if sel_args is None:
+                    sel_args = [ws.item_list(gi, grp)[0] if gi in sel_ids else None
+                                for gi, grp in enumerate(item_groups)]
+                sel = sel_args
+            else:
+                sel = []
+            runner.plan(d, n_open, packed, open_d, n_open_ptr, st.open[nxt], st.totals[nxt], int(tree_index),
+                        sample_next, thr_n, mask_n, *lay, sel)
+            ev = st.record_event(cur_stream)
+            with tracing.span("tree.partition"):
+                runner.partition(d, n_open, bool(FUSED_PACK and more))
+            prev_hist = cur_hist
+            prev_row_of = row_of
+            continue
         C.tree_level_plan(packed, n_open, d, params.max_depth, int(params.mode), build_all, ws.kexp,
                           float(params.min_gain), Q.zbin, st.hot_row,
                           st.n_nodes, st.stats, st.parent, st.left, st.right, st.feat, st.bin, st.leaf, st.gain,
