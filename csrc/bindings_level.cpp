@@ -108,7 +108,8 @@ class RfLevels {
   // counts[j] / npx[j]: group j's listed pass (None: a wave per item slot; npx -1: compacted here).
   void hist(int64_t n_build, const Tensor& hist, const Tensor& boff, const Tensor& feat_mask, const Tensor& s2n,
             const optional<Tensor>& pack, const std::vector<optional<Tensor>>& lists,
-            const std::vector<optional<Tensor>>& counts, const std::vector<int64_t>& npx) {
+            const std::vector<optional<Tensor>>& counts, const std::vector<int64_t>& npx,
+            const optional<Tensor>& shard_of, int64_t shard_bins) {
     FDX_CHECK(lists.size() == groups_.size() && counts.size() == groups_.size() && npx.size() == groups_.size(),
               "one list / count / npx per item group");
     FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && hist.scalar_type() == at::kLong, "hist [rows, stride, 2] int64");
@@ -140,6 +141,11 @@ class RfLevels {
       a.wave_item = p<int32_t>(g.wave);
       a.num_slots = (int32_t)g.wave.numel();
       a.feat_active = p<uint8_t>(feat_mask);
+      if (shard_of) {
+        FDX_CHECK(shard_of->numel() == boff.numel(), "shard_of [Fa + 1]");
+        a.shard_of = p<int64_t>(*shard_of);
+        a.shard_bins = shard_bins;
+      }
       if (pack) a.rowpack = reinterpret_cast<const uint32_t*>(p<int32_t>(*pack));
       if (lists[j]) {
         FDX_CHECK(counts[j].has_value(), "a listed pass needs its count");
@@ -222,7 +228,8 @@ class RfLevels {
             const Tensor& next_open, const Tensor& next_totals, int64_t tree, bool sample_next,
             const optional<Tensor>& thr, const optional<Tensor>& mask, const optional<Tensor>& fs,
             const optional<Tensor>& nbins_all, const optional<Tensor>& local, const optional<Tensor>& sizes,
-            const optional<Tensor>& sizes_host, const std::vector<optional<Tensor>>& sel_lists) {
+            const optional<Tensor>& sizes_host, int64_t max_shard_features,
+            const std::vector<optional<Tensor>>& sel_lists) {
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
     const Tensor& counts = st_["counts"];
@@ -297,6 +304,12 @@ class RfLevels {
         cp.Fa = mask->numel();
         cp.local = p<int64_t>(*local);
         cp.sizes = p<int64_t>(*sizes);
+        if (max_shard_features > 0) {
+          cp.chunk_stride = fdx::rf_compact_chunks(max_shard_features);
+          if (!chunk_sums_.defined() || chunk_sums_.numel() < cp.S * cp.chunk_stride)
+            chunk_sums_ = at::empty({cp.S * cp.chunk_stride}, local->options());
+          cp.chunk_sums = p<int64_t>(chunk_sums_);
+        }
         fdx::launch_rf_compact(cp, s);
         FDX_CHECK(hipMemcpyAsync(sizes_host->data_ptr(), sizes->data_ptr(), sizes->nbytes(), hipMemcpyDeviceToHost, s) ==
                       hipSuccess, "sizes copy");
@@ -376,7 +389,7 @@ class RfLevels {
   Tensor h_row_, h_key_, csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, rowpack_, row_node_, kexp_;
   optional<Tensor> dense_, hot_row_, node_dense_, wide_;
   std::map<std::string, Tensor> st_;
-  Tensor scratch_, gain_, sbin_, sleft_;
+  Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_;
   int mode_ = 1, max_depth_ = 5, wps_ = 256;
   double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;
   int64_t seed_ = 0, F_ = 1, k_ = 1;

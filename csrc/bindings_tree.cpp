@@ -199,7 +199,8 @@ void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64
 }
 
 // Compact DP layout of an RF level (tree.h RfCompactArgs): local [Fa + 1] int64, sizes [S] int64.
-void rf_compact(const Tensor& mask, const Tensor& nbins, const Tensor& fs, const Tensor& local, const Tensor& sizes) {
+void rf_compact(const Tensor& mask, const Tensor& nbins, const Tensor& fs, const Tensor& local, const Tensor& sizes,
+                int64_t max_shard_features) {
   const auto dev = mask.device();
   chk(mask, dev, at::kByte, "mask");
   chk(nbins, dev, at::kInt, "nbins");
@@ -219,6 +220,12 @@ void rf_compact(const Tensor& mask, const Tensor& nbins, const Tensor& fs, const
   a.sizes = sizes.data_ptr<int64_t>();
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
+    Tensor chunk_sums;
+    if (max_shard_features > 0) {      // the multi-workgroup layout (max_shard_features: the largest shard's)
+      a.chunk_stride = fdx::rf_compact_chunks(max_shard_features);
+      chunk_sums = at::empty({a.S * a.chunk_stride}, local.options());
+      a.chunk_sums = chunk_sums.data_ptr<int64_t>();
+    }
     fdx::launch_rf_compact(a, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
@@ -1261,7 +1268,8 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rg_erow", &rg_erow);
   m.def("tree_rg_list_rows", [](int64_t N) { return (int64_t)fdx::rg_list_rows(N); });
   m.def("tree_rf_sample", &rf_sample);
-  m.def("tree_rf_compact", &rf_compact);
+  m.def("tree_rf_compact", &rf_compact, py::arg("mask"), py::arg("nbins"), py::arg("fs"), py::arg("local"),
+        py::arg("sizes"), py::arg("max_shard_features") = 0);
   m.def("tree_hist_dense", &hist_dense);
   m.def("tree_dense_fg", &dense_fg);
   m.def("tree_dense_waves", &dense_waves);

@@ -83,6 +83,7 @@ void launch_rf_sample(const RfSampleArgs& a, hipStream_t s);
 void rf_sample_cpu(const RfSampleArgs& a);
 struct RfCompactArgs;
 void launch_rf_compact(const RfCompactArgs& a, hipStream_t s);
+int64_t rf_compact_chunks(int64_t max_shard_features);
 void rf_compact_cpu(const RfCompactArgs& a);
 // partials: device scratch of 2 x quant_blocks(N) x 8 bytes (per-workgroup results, reduced by a
 // second one-block kernel that writes out / totals)

@@ -194,10 +194,86 @@ __global__ __launch_bounds__(kCompactThreads) void rf_compact_kernel(RfCompactAr
   }
   if (t == 0) a.local[a.Fa] = 0;
 }
+
+// Multi-workgroup layout (chunk_sums given): shard s's features in chunks of kChunkFeat, workgroup
+// (c, s) on chunk c. Pass 0 sums the chunk's masked nbins; pass 1 takes its start from the sums of
+// the shard's earlier chunks, scans the chunk (8 consecutive features per thread, a wave scan and
+// the 4 wave totals) and writes the offsets, the shard's total as the trash start of unsampled
+// features. The single-workgroup kernel above walked ~90K features in one block: ~42 us a level,
+// on every tree-level of a data-parallel forest (profiles/r5/NOTES.md).
+constexpr int kChunkThreads = 256, kChunkPer = 8, kChunkFeat = kChunkThreads * kChunkPer;
+
+__device__ __forceinline__ int64_t chunk_wave_incl(int64_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kChunkThreads) void rf_compact_chunks_kernel(RfCompactArgs a, int pass) {
+  const int sh = blockIdx.y, c = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t f0 = a.fs[sh], f1 = a.fs[sh + 1];
+  const int64_t lo = f0 + (int64_t)c * kChunkFeat;
+  const int64_t nchunks = (f1 - f0 + kChunkFeat - 1) / kChunkFeat;
+  if (lo >= f1 && !(pass == 1 && c == 0)) return;
+  const int64_t base = lo + (int64_t)t * kChunkPer;
+  int64_t v[kChunkPer];
+  int64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kChunkPer; ++j) {
+    const int64_t f = base + j;
+    v[j] = (f < f1 && a.mask[f]) ? (int64_t)a.nbins[f] : 0;
+    sum += v[j];
+  }
+  __shared__ int64_t s_w[4];
+  __shared__ int64_t s_start, s_total;
+  const int64_t incl = chunk_wave_incl(sum, lane);
+  if (lane == 63) s_w[w] = incl;
+  if (pass == 1 && t == 0) {
+    int64_t before = 0, total = 0;
+    for (int64_t k = 0; k < nchunks; ++k) {
+      const int64_t cs = a.chunk_sums[(int64_t)sh * a.chunk_stride + k];
+      if (k < c) before += cs;
+      total += cs;
+    }
+    s_start = before;
+    s_total = total;
+  }
+  __syncthreads();
+  if (pass == 0) {
+    if (t == 0) a.chunk_sums[(int64_t)sh * a.chunk_stride + c] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    return;
+  }
+  int64_t acc = s_start + incl - sum;
+  for (int k = 0; k < w; ++k) acc += s_w[k];
+  const int64_t total = s_total;
+#pragma unroll
+  for (int j = 0; j < kChunkPer; ++j) {
+    const int64_t f = base + j;
+    if (f < f1) {
+      a.local[f] = a.mask[f] ? acc : total;
+      acc += v[j];
+    }
+  }
+  if (c == 0 && t == 0) {
+    a.sizes[sh] = total;
+    if (sh == 0) a.local[a.Fa] = 0;
+  }
+}
 }  // namespace
 
+int64_t rf_compact_chunks(int64_t max_shard_features) { return (max_shard_features + kChunkFeat - 1) / kChunkFeat; }
+
 void launch_rf_compact(const RfCompactArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(rf_compact_kernel, dim3(1), dim3(kCompactThreads), 0, s, a);
+  if (a.chunk_sums == nullptr) {
+    hipLaunchKernelGGL(rf_compact_kernel, dim3(1), dim3(kCompactThreads), 0, s, a);
+    return;
+  }
+  const dim3 grid((unsigned)(a.chunk_stride > 0 ? a.chunk_stride : 1), (unsigned)a.S);
+  hipLaunchKernelGGL(rf_compact_chunks_kernel, grid, dim3(kChunkThreads), 0, s, a, 0);
+  hipLaunchKernelGGL(rf_compact_chunks_kernel, grid, dim3(kChunkThreads), 0, s, a, 1);
 }
 
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s) {

@@ -119,6 +119,11 @@ struct HistArgs {
   int32_t* active_list;           // optional: listed pass, the active items compacted per XCD ...
   int32_t* active_count;          //   ... [8]: their count per XCD (list x at x * list_cap)
   int32_t list_cap;               // wave slots per XCD (set by the launch)
+  // optional (data-parallel batched levels): feature f's bins start at boff[f] + shard_of[f] *
+  // shard_bins (its shard's chunk of the batch's send buffer), so the per-level offsets need no
+  // separate add pass
+  const int64_t* shard_of;
+  int64_t shard_bins;
   int32_t listed_per_xcd;         // -1: the launch compacts the list and strides a fixed grid over
                                   // it; >= 0: the list was compacted beforehand (hist_select) and
                                   // its largest per-XCD count is known: one wave per active item
@@ -127,6 +132,10 @@ struct HistArgs {
 
 // waves of a listed histogram pass (they stride over the active items): 8 per SIMD of 256 CUs
 constexpr int32_t kListedWaves = 8192;
+
+FDX_HD int64_t hist_boff(const HistArgs& a, int32_t f) {
+  return a.boff[f] + (a.shard_of ? a.shard_of[f] * a.shard_bins : 0);
+}
 
 // ------------------------------------------------------------------ row-group histogram engine
 // Row-group CSR ("RG", models/quantize.py RowGroups): the active features are packed, densest
@@ -323,6 +332,8 @@ struct RfCompactArgs {
   int64_t Fa;
   int64_t* local;                 // [Fa + 1] out: offset inside the feature's shard row (local[Fa] = 0)
   int64_t* sizes;                 // [S] out: masked bins per shard (= the trash range start)
+  int64_t* chunk_sums;            // optional: [S][chunk_stride] scratch of the multi-workgroup layout
+  int64_t chunk_stride;           //   (rf_compact_chunks(largest shard's feature count) per shard)
 };
 
 inline int64_t rf_scratch_bytes(int64_t nnodes) { return 8 * ((2 * nnodes * 4 + 7) / 8) + nnodes * 2048 * 8; }

@@ -135,7 +135,7 @@ void hist_cpu(const HistArgs& h, int bt, int np) {
           q0 = undigits1((h.rowpack[row] >> 8) & 0xffu);
           q1 = undigits1((h.rowpack[row] >> 16) & 0xffu);
         }
-        int64_t* dst = h.hist + ((int64_t)node * h.hist_stride + h.boff[f] + b) * 2;
+        int64_t* dst = h.hist + ((int64_t)node * h.hist_stride + hist_boff(h, f) + b) * 2;
         __atomic_fetch_add(dst, q0, __ATOMIC_RELAXED);
         __atomic_fetch_add(dst + 1, q1, __ATOMIC_RELAXED);
       }

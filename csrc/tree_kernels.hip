@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
       const int fl = ek >> sl2, b = ek & ((1 << sl2) - 1);
       const int f = f0 + (fl < nfeat ? fl : 0);
       const int nb = a.nbins[f];
-      const int64_t bo = a.boff[f];
+      const int64_t bo = hist_boff(a, f);
       bin_of[bt][i] = (fl < nfeat && b < nb) ? bo + b : -1;
     }
   const int stat = q / NP;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
       if (b >= a.nbins[f] || node < 0) continue;
       const int64_t lo = (int64_t)(int32_t)(uint32_t)(uint64_t)v;
       const int64_t hi = (v - lo) >> 32;
-      unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.hist + ((int64_t)node * a.hist_stride + a.boff[f] + b) * 2);
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.hist + ((int64_t)node * a.hist_stride + hist_boff(a, f) + b) * 2);
       if (lo) atomicAdd(dst, (unsigned long long)lo);
       if (hi) atomicAdd(dst + 1, (unsigned long long)hi);
     }

@@ -565,6 +565,7 @@ class FeatureShards:
         fs = np.maximum.accumulate(fs)
         lo, hi = boff[fs[:-1]], boff[fs[1:]]
         self.S, self.fs = S, fs
+        self.max_shard_features = int((fs[1:] - fs[:-1]).max()) if S else 0
         self.Bs = max(1, int((hi - lo).max()))
         dev = Q.device
         shard_of = np.searchsorted(fs[1:], np.arange(Fa + 1), side="right").clip(0, S - 1).astype(np.int64)
@@ -631,7 +632,8 @@ class FeatureShards:
         if thr is None or thr.numel() < n:
             thr = self._thr[p] = torch.empty(max(n, 2), dtype=torch.float64, device=nodes.device)
         C.tree_rf_sample(seed, tree, nodes, F, k, fid_orig, thr[:n], self._mask[p], None)
-        C.tree_rf_compact(self._mask[p], self._nbins_all, self._fs_dev, self._local_c[p], self._sizes[p])
+        C.tree_rf_compact(self._mask[p], self._nbins_all, self._fs_dev, self._local_c[p], self._sizes[p],
+                          self.max_shard_features)
         self.sizes_host[p].copy_(self._sizes[p], non_blocking=nodes.is_cuda)
 
     def compact_thr(self, p: int, n: int) -> torch.Tensor:
@@ -1136,10 +1138,10 @@ def _wide_features(nbins: torch.Tensor, Fa: int) -> torch.Tensor:
 def _rf_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowParams, item_groups: list):
     """The lane's native level runner (csrc/bindings_level.cpp RfLevels), built once per workspace,
     level state and tree parameters."""
-    key = (id(st), params.mode, params.max_depth, params.min_gain, params.min_child, params.seed, params.feat_k)
+    key = (params.mode, params.max_depth, params.min_gain, params.min_child, params.seed, params.feat_k)
     cached = getattr(ws, "_rf_runner", None)
-    if cached is not None and cached[0] == key:
-        return cached[1]
+    if cached is not None and cached[0] is st and cached[1] == key:
+        return cached[2]
     cfg = dict(groups=[(g.item_start, g.item_end, g.item_f0, g.item_meta, g.wave_order(), int(g.bt))
                        for g in item_groups],
                h_row=Q.h_row, h_key=Q.h_key, csc_row=Q.csc_row, csc_bin=Q.csc_bin, colptr=Q.colptr, nbins=Q.nbins,
@@ -1154,7 +1156,7 @@ def _rf_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowParams
                mcw=float(params.min_child), seed=int(params.seed), F=int(Q.num_features), k=int(params.feat_k),
                lds=bool(RF_LDS), wps=int(PARTITION_WPS))
     runner = native.lib().RfLevels(cfg)
-    ws._rf_runner = (key, runner)
+    ws._rf_runner = (st, key, runner)
     return runner
 
 
@@ -1281,7 +1283,10 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             bufs = yield CollStep("alloc", rows=n_build, Bs=Bs_c if compact else shards.Bs, n_open=n_open,
                                   totals=ws.totals if d == 0 else None, sub_rows=subs)
             hist_target = bufs.prepare(ws.totals if d == 0 else None)
-            h_boff = shards.boff_batched(bufs.shard_bins, local_c if compact else None)
+            if runner is not None:      # (the runner's kernels add the shard offsets themselves)
+                h_boff = local_c if compact else shards._local
+            else:
+                h_boff = shards.boff_batched(bufs.shard_bins, local_c if compact else None)
             h_stride = bufs.Bs
             if compact:
                 split_boff = local_c[shards.f0: shards.f0 + shards.Fa + 1]
@@ -1350,7 +1355,9 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                     lists.append(lst)
                     cnts.append(cnt)
                     npxs.append(npx)
-                runner.hist(n_build, hist_target, h_boff, feat_mask, s2n, pack, lists, cnts, npxs)
+                runner.hist(n_build, hist_target, h_boff, feat_mask, s2n, pack, lists, cnts, npxs,
+                            shards._shard_of if shards is not None else None,
+                            bufs.shard_bins if shards is not None else 0)
                 sel_groups = []
             for gi, grp in enumerate(sel_groups):
                 if grp.num_items == 0:
@@ -1445,12 +1452,13 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             sample_next = more and (compact or bool(sel_ids))
             if sample_next and compact:
                 thr_n, mask_n = shards.compact_thr(nxt, 2 * n_open), shards.compact_mask(nxt)
-                lay = (shards._fs_dev, Q.nbins, shards._local_c[nxt], shards._sizes[nxt], shards.sizes_host[nxt])
+                lay = (shards._fs_dev, Q.nbins, shards._local_c[nxt], shards._sizes[nxt], shards.sizes_host[nxt],
+                       shards.max_shard_features)
             elif sample_next:
-                thr_n, mask_n, lay = st.rf_thr[nxt], st.rf_mask[nxt], (None,) * 5
+                thr_n, mask_n, lay = st.rf_thr[nxt], st.rf_mask[nxt], (None,) * 5 + (0,)
             else:
                 thr_n = mask_n = None
-                lay = (None,) * 5
+                lay = (None,) * 5 + (0,)
             if sel_ids and more:
                 if sel_args is None:
                     sel_args = [ws.item_list(gi, grp)[0] if gi in sel_ids else None

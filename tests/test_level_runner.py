@@ -1,0 +1,61 @@
+"""The native per-level runner of RF device levels (csrc/bindings_level.cpp RfLevels) and the
+kernels it brought: same forests as the Python-driven levels, multi-workgroup compact layout
+equal to the host twin."""
+import numpy as np
+import pytest
+import torch
+
+from fraud_detection_spark_kafka_llm_amd.ops import native
+
+
+def _forest(device, n=6000, F=400, trees=6, depth=5, seed=7):
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+    from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
+
+    rng = np.random.default_rng(seed)
+    p = 0.5 / (1.0 + np.arange(F)) ** 0.7
+    counts = (rng.random((n, F)) < p) * rng.integers(1, 4, (n, F))
+    y = ((counts[:, 1] > 0) ^ (counts[:, 5] >= 2)).astype(np.float32)
+    flip = rng.random(n) < 0.05
+    y[flip] = 1 - y[flip]
+    vc = VectorColumn(F, dense=torch.from_numpy(counts.astype(np.float64)))
+    r = fit_forest(vc, torch.from_numpy(y), num_trees=trees, max_depth=depth, bootstrap=True, feature_subset="sqrt",
+                   seed=seed, device=device)
+    return [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inflight", [1, 4])
+def test_gpu_native_levels_equal_python_levels(inflight, monkeypatch):
+    from fraud_detection_spark_kafka_llm_amd.models import forest_batch, grower
+
+    monkeypatch.setattr(forest_batch, "TREES_IN_FLIGHT", inflight)
+    monkeypatch.setattr(grower, "NATIVE_LEVELS", False)
+    ref = _forest("cuda:0")
+    monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
+    assert _forest("cuda:0") == ref
+    for presel, fused in ((False, True), (True, False)):
+        monkeypatch.setattr(grower, "PRESELECT", presel)
+        monkeypatch.setattr(grower, "FUSED_PACK", fused)
+        assert _forest("cuda:0") == ref
+    assert _forest("cpu") == ref
+
+
+@pytest.mark.gpu
+def test_gpu_rf_compact_chunked_equals_host():
+    C = native.lib()
+    rng = np.random.default_rng(3)
+    Fa = 20000
+    nbins = torch.from_numpy(rng.integers(1, 33, Fa).astype(np.int32))
+    mask = torch.from_numpy((rng.random(Fa) < 0.07).astype(np.uint8))
+    fs = torch.tensor([0, 3000, 3000, 15000, Fa], dtype=torch.int64)      # an empty shard too
+    S = fs.numel() - 1
+    ref_local = torch.zeros(Fa + 1, dtype=torch.int64)
+    ref_sizes = torch.zeros(S, dtype=torch.int64)
+    C.tree_rf_compact(mask, nbins, fs, ref_local, ref_sizes)
+    dev = torch.device("cuda:0")
+    for chunks in (0, int((fs[1:] - fs[:-1]).max())):
+        local = torch.full((Fa + 1,), -7, dtype=torch.int64, device=dev)
+        sizes = torch.full((S,), -7, dtype=torch.int64, device=dev)
+        C.tree_rf_compact(mask.to(dev), nbins.to(dev), fs.to(dev), local, sizes, chunks)
+        assert torch.equal(local.cpu(), ref_local) and torch.equal(sizes.cpu(), ref_sizes), chunks
