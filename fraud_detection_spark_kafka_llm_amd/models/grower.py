@@ -297,6 +297,10 @@ LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
 # RF levels >= 1 launch one wave per active work item from lists compacted with the previous
 # level's plan (0: the r4 passes, a wave per item slot or a fixed listed grid)
 PRESELECT = os.environ.get("FDX_RF_PRESELECT", "1") == "1"
+# ... on shards of at least this many rows: on a 1.25M-row shard (DP=8) the listed passes ran
+# slower per launch than the wave-per-slot ones (143 -> 207 us, profiles/r5/rf_dp_trace_ab.txt),
+# at 10M rows they win (0.768 -> 0.747 s a forest, profiles/r5/rf_variants_10M.jsonl)
+PRESELECT_MIN_ROWS = int(os.environ.get("FDX_RF_PRESELECT_ROWS", 4_000_000))
 # RF levels >= 1 read the packed row state (slot | class-count digits) written by the previous
 # level's partition instead of a row pass of their own (slot pack / masked digits: ~87 us per level
 # at 10M rows, 173 ms of a 500-tree forest's kernel time, profiles/r5/NOTES.md)
@@ -1189,7 +1193,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     # RF levels >= 1: the next level's feature sample and its active-item lists are queued right
     # after the plan, so the per-XCD item counts reach the host with the level's counts and each
     # histogram pass launches one wave per active item (no grid of ~300K mostly idle wave slots)
-    presel = PRESELECT and sampled and dev.type == "cuda"
+    presel = PRESELECT and sampled and dev.type == "cuda" and Q.n_rows >= PRESELECT_MIN_ROWS
     item_groups = (Q.groups + Q.hot_groups) if sampled else []
     sel_ids = [gi for gi, grp in enumerate(item_groups) if grp.num_items] if presel else []
     sel_args = None

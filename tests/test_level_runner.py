@@ -34,6 +34,7 @@ def test_gpu_native_levels_equal_python_levels(inflight, monkeypatch):
     ref = _forest("cuda:0")
     monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
     assert _forest("cuda:0") == ref
+    monkeypatch.setattr(grower, "PRESELECT_MIN_ROWS", 0)
     for presel, fused in ((False, True), (True, False)):
         monkeypatch.setattr(grower, "PRESELECT", presel)
         monkeypatch.setattr(grower, "FUSED_PACK", fused)
