@@ -63,14 +63,20 @@ def _int_features(n: int, seed: int) -> tuple:
     return X, y
 
 
-def test_decision_tree_equals_sklearn_on_lossless_integer_features():
+DEVICES = ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_decision_tree_equals_sklearn_on_lossless_integer_features(device):
+    """(cuda:0: the default device engines, checked against sklearn directly, not only through the
+    bitwise host twin)"""
     from sklearn.tree import DecisionTreeClassifier
 
     X, y = _int_features(24000, 5)
     tr, te = slice(0, 18000), slice(18000, None)
     assert max(len(np.unique(X[:, f])) for f in range(X.shape[1])) <= 32
     ours = fit_forest(_csr_vc(X[tr]), torch.from_numpy(y[tr]), num_trees=1, max_depth=5, max_bins=32,
-                      feature_subset="all", device="cpu")
+                      feature_subset="all", device=device)
     arr = ensemble_arrays(ours.trees, "counts")
     sk = DecisionTreeClassifier(max_depth=5, criterion="gini", random_state=0).fit(X[tr], y[tr])
     for part in (tr, te):
@@ -95,7 +101,8 @@ def _tfidf_corpus(n: int, seed: int, F: int = 1 << 14):
     return ip, ix, cnt.to(torch.int32), y.to(torch.float32), F
 
 
-def test_random_forest_accuracy_matches_sklearn_within_one_point():
+@pytest.mark.parametrize("device", DEVICES)
+def test_random_forest_accuracy_matches_sklearn_within_one_point(device):
     import scipy.sparse as sp
     from sklearn.ensemble import RandomForestClassifier
 
@@ -116,7 +123,7 @@ def test_random_forest_accuracy_matches_sklearn_within_one_point():
     vtr = VectorColumn.tfidf(F, p_tr, x_tr, c_tr, idf)
     vte = VectorColumn.tfidf(F, p_te, x_te, c_te, idf)
     ours = fit_forest(vtr, y[:ntr], num_trees=100, max_depth=5, max_bins=32, bootstrap=True, feature_subset="sqrt",
-                      seed=42, device="cpu")
+                      seed=42, device=device)
     raw = score_csr(vte, ensemble_arrays(ours.trees, "normalized")).numpy()
     acc_ours = float(((raw[:, 1] > raw[:, 0]).astype(np.float32) == y[ntr:].numpy()).mean())
 
@@ -192,15 +199,20 @@ def _oracle_tree(Xb, thr_vals, g, h, params, depth_max):
     return leaf_value, leaves
 
 
+@pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("gamma,mcw", [(0.5, 2.0), (30.0, 40.0)])
-def test_gbdt_equals_numpy_exact_histogram_oracle(gamma, mcw):
+def test_gbdt_equals_numpy_exact_histogram_oracle(gamma, mcw, device):
     X, y = _int_features(6000, 11)
     # value -> bin index per feature (sorted distinct values: bin b <=> x <= thr_vals[f][b])
     thr_vals = [np.unique(X[:, f]) for f in range(X.shape[1])]
     Xb = np.stack([np.searchsorted(thr_vals[f], X[:, f]) for f in range(X.shape[1])], 1)
     params = GBDTParams(n_estimators=4, max_depth=3, learning_rate=0.3, reg_lambda=1.0, gamma=gamma,
                         min_child_weight=mcw, max_bin=64)
-    ours = fit_gbdt(_csr_vc(X), torch.from_numpy(y), params, device="cpu")
+    ours = fit_gbdt(_csr_vc(X), torch.from_numpy(y), params, device=device)
+    if device != "cpu":
+        from fraud_detection_spark_kafka_llm_amd.models import grower
+
+        assert grower.ROWHIST           # the default row-group engine ran (not the CSC passes)
     ybar = float(y.astype(np.float64).mean())
     base = math.log(ybar / (1 - ybar))
     assert ours.base_margin == pytest.approx(base, abs=1e-12)
