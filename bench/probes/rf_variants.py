@@ -35,6 +35,7 @@ VARIANTS = {
     "l32g4": {(forest_batch, "TREES_IN_FLIGHT"): 32, (forest_batch, "LANE_GROUPS"): 4},
     "g1": {(forest_batch, "LANE_GROUPS"): 1},
     "nonative": {(grower, "NATIVE_LEVELS"): False},
+    "mfma": {(grower, "RF_LDS"): False},
     "nonative_nopresel": {(grower, "NATIVE_LEVELS"): False, (grower, "PRESELECT"): False},
 }
 
