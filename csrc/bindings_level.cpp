@@ -67,8 +67,8 @@ class RfLevels {
       ig.bt = t[5].cast<int>();
       groups_.push_back(ig);
     }
-    h_row_ = get(c, "h_row");
-    h_key_ = get(c, "h_key");
+    h_row_ = get_opt(c, "h_row");
+    h_key_ = get_opt(c, "h_key");
     csc_row_ = get(c, "csc_row");
     csc_bin_ = get(c, "csc_bin");
     colptr_ = get(c, "colptr");
@@ -78,7 +78,9 @@ class RfLevels {
     dense_ = get_opt(c, "dense");
     hot_row_ = get_opt(c, "hot_row");
     rowdig_ = get(c, "rowdig");
-    rowpack_ = get(c, "rowpack");
+    rowpack_ = get_opt(c, "rowpack");
+    build_all_ = c["build_all"].cast<bool>();
+    for (const char* k : {"arena_stats", "open0", "totals0", "kexp_slot"}) st_[k] = get(c, k);
     row_node_ = get(c, "row_node");
     kexp_ = get(c, "kexp");
     for (const char* k : {"stats", "parent", "left", "right", "feat", "bin", "leaf", "gain", "n_nodes", "counts",
@@ -101,6 +103,61 @@ class RfLevels {
     FDX_CHECK(dev_.is_cuda(), "the level runner drives device levels only");
     const int64_t cap = st_["s2n"].numel();
     scratch_ = at::empty({fdx::rf_scratch_bytes(2 * cap)}, row_node_.options().dtype(at::kByte));
+    ticket_ = at::zeros({4}, row_node_.options());
+    parts_ = at::empty({2 * (int64_t)fdx::quant_blocks(row_node_.numel())}, row_node_.options().dtype(at::kLong));
+  }
+
+  // Tree prologue, one launch each: quantisation of the row statistics (GBDT: the fused logistic
+  // gradient + max |g|, |h| launch first, when margin is given) whose last workgroup reduces the
+  // totals and writes the root state (stats[0], the level-0 totals, open[0], the arena's
+  // exponents) and row_node = 0 -- what quant_max + 2 reductions + 4 fills / copies did.
+  void prologue(const optional<Tensor>& margin, const optional<Tensor>& g, const optional<Tensor>& h,
+                const optional<Tensor>& label, const optional<Tensor>& weight, int64_t tree, bool bootstrap,
+                int64_t np, const optional<Tensor>& maxabs, const Tensor& totals, const optional<Tensor>& digp,
+                int64_t row0) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    const int64_t N = row_node_.numel();
+    if (margin) {
+      FDX_CHECK(g && h && label && maxabs && !weight && mode_ == 0, "the fused gradient prologue: unweighted GBDT");
+      fdx::launch_grad_max(p<double>(*margin), p<float>(*label), p<float>(*g), p<float>(*h), N, p<int64_t>(parts_),
+                           reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)), p<double>(*maxabs), s);
+    }
+    fdx::QuantArgs a{};
+    a.g = p<float>(g);
+    a.h = p<float>(h);
+    a.label = p<float>(label);
+    a.weight = p<float>(weight);
+    a.seed = (uint64_t)seed_;
+    a.tree = (int32_t)tree;
+    a.bootstrap = bootstrap ? 1 : 0;
+    a.mode = mode_ == 0 ? 0 : 1;
+    a.np = (int32_t)np;
+    a.N = N;
+    a.row0 = row0;
+    a.kexp_out = p<int32_t>(kexp_);
+    a.rowdig = reinterpret_cast<uint32_t*>(p<int32_t>(rowdig_));
+    a.totals = p<int64_t>(totals);
+    if (digp) {
+      a.digp = p<uint8_t>(*digp);
+      a.n_pad = digp->size(1);
+    }
+    a.ticket = reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 1;
+    a.root_stats = p<int64_t>(st_["arena_stats"]);
+    a.root_totals = p<int64_t>(st_["totals0"]);
+    a.root_open = p<int32_t>(st_["open0"]);
+    a.kexp_copy = p<int32_t>(st_["kexp_slot"]);
+    a.row_node = p<int32_t>(row_node_);
+    fdx::launch_quant(a, maxabs ? p<double>(*maxabs) : nullptr, p<int64_t>(parts_), s);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+
+  // GBDT leaf update from the node table (leaf_values + leaf_update in one launch)
+  void leaf_update(const Tensor& margin, double eta, double lambda, double mds) {
+    c10::hip::HIPGuard guard(dev_.index());
+    fdx::launch_leaf_update_stats(p<double>(margin), p<int32_t>(row_node_), p<int64_t>(st_["stats"]), p<int32_t>(kexp_),
+                                  eta, lambda, mds, row_node_.numel(), cur_stream(dev_));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 
   // Histogram passes of level d over every item group (tree_hist_sampled per group): hist [*, stride, 2]
@@ -115,6 +172,7 @@ class RfLevels {
     FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && hist.scalar_type() == at::kLong, "hist [rows, stride, 2] int64");
     FDX_CHECK(boff.numel() == nbins_.numel() + 1 && feat_mask.numel() == nbins_.numel(), "boff [Fa + 1], mask [Fa]");
     FDX_CHECK(n_build >= 1 && n_build <= 8 * 8 && s2n.numel() >= n_build, "slots");
+    FDX_CHECK(h_row_.has_value() && h_key_.has_value(), "the CSC passes need the histogram CSC");
     const int ct = pass_ct(n_build);
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
@@ -129,8 +187,8 @@ class RfLevels {
       a.item_f0 = p<int32_t>(g.f0);
       a.item_meta = p<int32_t>(g.meta);
       a.num_items = (int32_t)I;
-      a.csc_row = p<int32_t>(h_row_);
-      a.csc_key = p<uint8_t>(h_key_);
+      a.csc_row = p<int32_t>(*h_row_);
+      a.csc_key = p<uint8_t>(*h_key_);
       a.rowdig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
       a.boff = p<int64_t>(boff);
       a.nbins = p<int32_t>(nbins_);
@@ -167,12 +225,23 @@ class RfLevels {
   void split(const Tensor& hist, const Tensor& totals, const Tensor& boff, const Tensor& nbins, const Tensor& zbin,
              const Tensor& fid_orig, const Tensor& node_ids, const optional<Tensor>& feat_thr, int64_t tree, int64_t f0,
              const Tensor& out, const optional<Tensor>& row_of, const optional<Tensor>& wide) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    const int32_t nodes = (int32_t)node_ids.numel(), Fa = (int32_t)nbins.numel();
+    if (!find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, feat_thr, tree, out, row_of, wide, s)) return;
+    fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), nodes, Fa, f0, p<int64_t>(out), s);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+
+  // split_find into the runner's scratch (gain_, sbin_, sleft_); false when there is nothing to
+  // search (out then holds "no candidate" tuples for every node)
+  bool find(const Tensor& hist, const Tensor& totals, const Tensor& boff, const Tensor& nbins, const Tensor& zbin,
+            const Tensor& fid_orig, const Tensor& node_ids, const optional<Tensor>& feat_thr, int64_t tree,
+            const Tensor& out, const optional<Tensor>& row_of, const optional<Tensor>& wide, hipStream_t s) {
     const int32_t nodes = (int32_t)node_ids.numel(), Fa = (int32_t)nbins.numel();
     FDX_CHECK(out.numel() == 5ll * nodes && out.is_contiguous() && boff.numel() == Fa + 1, "out [nodes, 5], boff");
     FDX_CHECK(hist.dim() == 3 && hist.size(2) == 2 && (row_of || hist.size(0) >= nodes), "hist rows");
-    c10::hip::HIPGuard guard(dev_.index());
-    const hipStream_t s = cur_stream(dev_);
-    if (nodes == 0) return;
+    if (nodes == 0) return false;
     if (Fa == 0) {                         // a shard without features: no candidate anywhere
       const double ninf = -1.0 / 0.0;
       int64_t bits;
@@ -181,7 +250,7 @@ class RfLevels {
       o.zero_();
       o.select(1, 0).fill_(bits);
       o.narrow(1, 1, 2).fill_(-1);
-      return;
+      return false;
     }
     const int64_t need = (int64_t)nodes * Fa;
     if (!gain_.defined() || gain_.numel() < need) {
@@ -216,25 +285,12 @@ class RfLevels {
     }
     a.row_of = p<int32_t>(row_of);
     fdx::launch_split(a, s);
-    fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), nodes, Fa, f0, p<int64_t>(out), s);
-    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return true;
   }
 
-  // Level plan of level d (tree.h level_plan) from the best tuples packed [L, 5] / [S, L, 5]; then,
-  // for a next level, its feature sample over the (-1 padded) next open list into thr / mask, the
-  // compact DP layout (local / sizes, sizes copied to sizes_host) when given, and the per-group
-  // active-item lists (sel_lists / counts[d, 4:]); the level's counts to counts_host[d].
-  void plan(int64_t d, int64_t n_open, const Tensor& packed, const Tensor& open, const Tensor& n_open_ptr,
-            const Tensor& next_open, const Tensor& next_totals, int64_t tree, bool sample_next,
-            const optional<Tensor>& thr, const optional<Tensor>& mask, const optional<Tensor>& fs,
-            const optional<Tensor>& nbins_all, const optional<Tensor>& local, const optional<Tensor>& sizes,
-            const optional<Tensor>& sizes_host, int64_t max_shard_features,
-            const std::vector<optional<Tensor>>& sel_lists) {
-    c10::hip::HIPGuard guard(dev_.index());
-    const hipStream_t s = cur_stream(dev_);
+  fdx::LevelPlanArgs plan_args(int64_t d, int64_t n_open, const Tensor& packed, const Tensor& open,
+                               const Tensor& n_open_ptr, const Tensor& next_open, const Tensor& next_totals) {
     const Tensor& counts = st_["counts"];
-    const int64_t cw = counts.size(1);
-    int32_t* counts_d = p<int32_t>(counts) + d * cw;
     fdx::LevelPlanArgs a{};
     a.packed = p<int64_t>(packed);
     a.L = (int32_t)n_open;
@@ -245,7 +301,7 @@ class RfLevels {
     a.depth = (int32_t)d;
     a.max_depth = max_depth_;
     a.mode = mode_;
-    a.build_all = 1;
+    a.build_all = build_all_ ? 1 : 0;
     a.kexp = p<int32_t>(kexp_);
     a.min_gain = min_gain_;
     a.zbin = p<int32_t>(zbin_);
@@ -269,7 +325,7 @@ class RfLevels {
     a.cs_other = p<int32_t>(st_["cs_other"]);
     a.cs_bin = p<int32_t>(st_["cs_bin"]);
     a.cs_left_default = p<int32_t>(st_["cs_left_default"]);
-    a.counts = counts_d;
+    a.counts = p<int32_t>(counts) + d * counts.size(1);
     a.next_open = p<int32_t>(next_open);
     a.next_totals = p<int64_t>(next_totals);
     a.node_slot = p<int32_t>(st_["node_slot"]);
@@ -277,7 +333,57 @@ class RfLevels {
     a.sub_dst = p<int32_t>(st_["sub_dst"]);
     a.sub_par = p<int32_t>(st_["sub_par"]);
     a.sub_sib = p<int32_t>(st_["sub_sib"]);
-    fdx::launch_level_plan(a, s);
+    return a;
+  }
+
+  // Level plan of level d (tree.h level_plan) from the best tuples packed [L, 5] / [S, L, 5]; then
+  // the after-plan work of after_plan().
+  void plan(int64_t d, int64_t n_open, const Tensor& packed, const Tensor& open, const Tensor& n_open_ptr,
+            const Tensor& next_open, const Tensor& next_totals, int64_t tree, bool sample_next,
+            const optional<Tensor>& thr, const optional<Tensor>& mask, const optional<Tensor>& fs,
+            const optional<Tensor>& nbins_all, const optional<Tensor>& local, const optional<Tensor>& sizes,
+            const optional<Tensor>& sizes_host, int64_t max_shard_features,
+            const std::vector<optional<Tensor>>& sel_lists) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    fdx::launch_level_plan(plan_args(d, n_open, packed, open, n_open_ptr, next_open, next_totals), s);
+    after_plan(d, n_open, next_open, tree, sample_next, thr, mask, fs, nbins_all, local, sizes, sizes_host,
+               max_shard_features, sel_lists, s);
+  }
+
+  // Split search + best split + level plan with no collective between them (split_all_kernel, then
+  // split_best_plan_kernel: the last node's workgroup plans the level), then after_plan().
+  void split_plan(int64_t d, int64_t n_open, const Tensor& hist, const Tensor& totals, const Tensor& boff,
+                  const optional<Tensor>& feat_thr, int64_t tree, const Tensor& out, const optional<Tensor>& wide,
+                  const Tensor& open, const Tensor& n_open_ptr, const Tensor& next_open, const Tensor& next_totals,
+                  bool sample_next, const optional<Tensor>& thr, const optional<Tensor>& mask,
+                  const std::vector<optional<Tensor>>& sel_lists) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    const int32_t Fa = (int32_t)nbins_.numel();
+    FDX_CHECK(open.numel() == n_open, "open [n_open]");
+    const bool any = find(hist, totals, boff, nbins_, zbin_, fid_orig_, open, feat_thr, tree, out, c10::nullopt, wide, s);
+    const fdx::LevelPlanArgs a = plan_args(d, n_open, out, open, n_open_ptr, next_open, next_totals);
+    if (any)
+      fdx::launch_split_best_plan(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), (int32_t)n_open, Fa, 0,
+                                  p<int64_t>(out), a, reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 2, s);
+    else                                   // (no features: out holds "no candidate" tuples)
+      fdx::launch_level_plan(a, s);
+    after_plan(d, n_open, next_open, tree, sample_next, thr, mask, c10::nullopt, c10::nullopt, c10::nullopt,
+               c10::nullopt, c10::nullopt, 0, sel_lists, s);
+  }
+
+  // For a next level: its feature sample over the (-1 padded) next open list into thr / mask, the
+  // compact DP layout (local / sizes, sizes copied to sizes_host) when given, and the per-group
+  // active-item lists (sel_lists / counts[d, 4:]); then the level's counts to counts_host[d].
+  void after_plan(int64_t d, int64_t n_open, const Tensor& next_open, int64_t tree, bool sample_next,
+                  const optional<Tensor>& thr, const optional<Tensor>& mask, const optional<Tensor>& fs,
+                  const optional<Tensor>& nbins_all, const optional<Tensor>& local, const optional<Tensor>& sizes,
+                  const optional<Tensor>& sizes_host, int64_t max_shard_features,
+                  const std::vector<optional<Tensor>>& sel_lists, hipStream_t s) {
+    const Tensor& counts = st_["counts"];
+    const int64_t cw = counts.size(1);
+    int32_t* counts_d = p<int32_t>(counts) + d * cw;
     if (sample_next) {
       FDX_CHECK(thr && mask, "a next-level sample needs thr and mask");
       fdx::RfSampleArgs r{};
@@ -348,7 +454,7 @@ class RfLevels {
   }
 
   // Partition of level d (tree_partition_cols), writing the next level's packed row state when fuse.
-  void partition(int64_t d, int64_t n_open, bool fuse) {
+  void partition(int64_t d, int64_t n_open, bool fuse, const optional<Tensor>& zero) {
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
     fdx::PartitionArgs a{};
@@ -368,9 +474,16 @@ class RfLevels {
       a.n_pad = dense_->size(1);
     }
     if (fuse) {
+      FDX_CHECK(rowpack_.has_value(), "a fused partition writes the packed row state");
       a.pack_slot = p<int32_t>(st_["node_slot"]);
       a.pack_dig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
-      a.pack = reinterpret_cast<uint32_t*>(p<int32_t>(rowpack_));
+      a.pack = reinterpret_cast<uint32_t*>(p<int32_t>(*rowpack_));
+    }
+    if (zero) {
+      FDX_CHECK(zero->scalar_type() == at::kLong && zero->is_contiguous() && zero->numel() % 2 == 0 &&
+                    reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0, "zero: contiguous int64, 16-byte aligned");
+      a.zero = p<int64_t>(*zero);
+      a.zero_n = zero->numel();
     }
     const Tensor& counts = st_["counts"];
     fdx::launch_partition_cols(a, p<int64_t>(colptr_), p<int32_t>(st_["cs_feat"]), p<int32_t>(counts) + d * counts.size(1),
@@ -386,10 +499,11 @@ class RfLevels {
   }
 
   std::vector<ItemGroup> groups_;
-  Tensor h_row_, h_key_, csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, rowpack_, row_node_, kexp_;
-  optional<Tensor> dense_, hot_row_, node_dense_, wide_;
+  Tensor csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, row_node_, kexp_;
+  optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_;
   std::map<std::string, Tensor> st_;
-  Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_;
+  Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_, ticket_, parts_;
+  bool build_all_ = true;
   int mode_ = 1, max_depth_ = 5, wps_ = 256;
   double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;
   int64_t seed_ = 0, F_ = 1, k_ = 1;
@@ -405,5 +519,8 @@ void register_level_ops(pybind11::module& m) {
       .def("hist", &RfLevels::hist)
       .def("split", &RfLevels::split)
       .def("plan", &RfLevels::plan)
-      .def("partition", &RfLevels::partition);
+      .def("partition", &RfLevels::partition)
+      .def("split_plan", &RfLevels::split_plan)
+      .def("prologue", &RfLevels::prologue)
+      .def("leaf_update", &RfLevels::leaf_update);
 }

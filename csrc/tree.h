@@ -75,6 +75,16 @@ struct QuantArgs {
   uint8_t* digp;              // optional plane-major copy [2 * np][n_pad] (dense histogram path)
   int64_t n_pad;
   int64_t row0;               // global index of row 0 of this shard (bootstrap draws are per global row)
+  // optional, one-launch forms (device level loop, models/grower.py): the last workgroup to finish
+  // (ticket) reduces the per-workgroup partials itself instead of a second launch, and then
+  // writes the root state of the tree: stats[0] = totals[0] row = the exact totals, open[0] = 0,
+  // the exponents into the node-table arena; row_node[r] = 0 for every row on the way
+  unsigned int* ticket;
+  int64_t* root_stats;
+  int64_t* root_totals;
+  int32_t* root_open;
+  int32_t* kexp_copy;
+  int32_t* row_node;
 };
 
 struct SlotArgs {
@@ -457,6 +467,9 @@ struct PartitionArgs {
   const int32_t* pack_slot;
   const uint32_t* pack_dig;
   uint32_t* pack;
+  // optional: zero this int64 range on the way (the next level's histograms: no fill launch)
+  int64_t* zero;
+  int64_t zero_n;
 };
 
 FDX_HD uint32_t partition_pack_word(const PartitionArgs& a, int32_t node, int64_t r) {

@@ -81,6 +81,85 @@ __global__ __launch_bounds__(256) void quant_reduce_kernel(const unsigned long l
   if (threadIdx.x == 0) { out[0] = s[0][0]; out[1] = s[1][0]; }
 }
 
+// The last workgroup of a partials pass (ticket: a zeroed counter, reset here for the next
+// launch): true for one workgroup, after every other workgroup's partial is visible.
+__device__ __forceinline__ bool last_workgroup(unsigned int* ticket) {
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int t = atomicAdd(ticket, 1u);
+    s_last = (t == gridDim.x - 1) ? 1 : 0;
+    if (s_last) atomicExch(ticket, 0u);
+  }
+  __syncthreads();
+  if (!s_last) return false;
+  __threadfence();
+  return true;
+}
+
+// quant_reduce_kernel's body for the calling 256-thread workgroup
+template <bool MAX>
+__device__ void reduce_parts_block(const unsigned long long* part, int nparts, unsigned long long* out) {
+  unsigned long long v0 = 0, v1 = 0;
+  for (int i = threadIdx.x; i < nparts; i += 256) {
+    const unsigned long long a0 = part[2 * i], a1 = part[2 * i + 1];
+    if (MAX) { v0 = a0 > v0 ? a0 : v0; v1 = a1 > v1 ? a1 : v1; }
+    else { v0 += a0; v1 += a1; }
+  }
+  __shared__ unsigned long long s[2][256];
+  s[0][threadIdx.x] = v0;
+  s[1][threadIdx.x] = v1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const unsigned long long b0 = s[0][threadIdx.x + o], b1 = s[1][threadIdx.x + o];
+      if (MAX) {
+        s[0][threadIdx.x] = b0 > s[0][threadIdx.x] ? b0 : s[0][threadIdx.x];
+        s[1][threadIdx.x] = b1 > s[1][threadIdx.x] ? b1 : s[1][threadIdx.x];
+      } else {
+        s[0][threadIdx.x] += b0;
+        s[1][threadIdx.x] += b1;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { out[0] = s[0][0]; out[1] = s[1][0]; }
+}
+
+// GBDT round prologue in one launch: g = p - y, h = max(p (1 - p), 1e-16) from the margins
+// (logistic_grad_kernel's arithmetic), max |g|, |h| per workgroup, the last workgroup reducing the
+// partials into maxv (quant_max_kernel + quant_reduce_kernel<true> of the unweighted case).
+__global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, const float* label, float* g, float* h,
+                                                       int64_t N, unsigned long long* part, unsigned int* ticket,
+                                                       unsigned long long* maxv) {
+  double m0 = 0.0, m1 = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256) {
+    const double p = 1.0 / (1.0 + exp(-margin[r]));
+    const float gv = (float)(p - (double)label[r]);
+    const float hv = (float)fmax(p * (1.0 - p), 1e-16);
+    g[r] = gv;
+    h[r] = hv;
+    m0 = fmax(m0, fabs((double)gv));
+    m1 = fmax(m1, fabs((double)hv));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    m0 = fmax(m0, __shfl_xor(m0, o, kWave));
+    m1 = fmax(m1, __shfl_xor(m1, o, kWave));
+  }
+  __shared__ double s_m[2][4];
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) { s_m[0][w] = m0; s_m[1][w] = m1; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m0 = fmax(fmax(s_m[0][0], s_m[0][1]), fmax(s_m[0][2], s_m[0][3]));
+    m1 = fmax(fmax(s_m[1][0], s_m[1][1]), fmax(s_m[1][2], s_m[1][3]));
+    part[2 * blockIdx.x] = (unsigned long long)__double_as_longlong(m0);
+    part[2 * blockIdx.x + 1] = (unsigned long long)__double_as_longlong(m1);
+  }
+  if (last_workgroup(ticket)) reduce_parts_block<true>(part, (int)gridDim.x, maxv);
+}
+
 // rowdig[r] = digits of (q0, q1); totals += (sum q0, sum q1) (int64 atomics, exact)
 __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* maxv, unsigned long long* part) {
   const int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
@@ -96,6 +175,7 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
     d.x = a.np == 1 ? digits1(q0) : digits4(q0);
     d.y = a.np == 1 ? digits1(q1) : digits4(q1);
     reinterpret_cast<uint2*>(a.rowdig)[r] = d;
+    if (a.row_node) a.row_node[r] = 0;
     if (a.digp) {
       for (int p = 0; p < a.np; ++p) {
         a.digp[(int64_t)p * a.n_pad + r] = (uint8_t)(d.x >> (8 * p));
@@ -116,6 +196,16 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
     t1 = s_t[1][0] + s_t[1][1] + s_t[1][2] + s_t[1][3];
     part[2 * blockIdx.x] = (unsigned long long)t0;
     part[2 * blockIdx.x + 1] = (unsigned long long)t1;
+  }
+  if (a.ticket == nullptr || !last_workgroup(a.ticket)) return;
+  // the last workgroup: the exact totals, then the tree's root state
+  reduce_parts_block<false>(part, (int)gridDim.x, reinterpret_cast<unsigned long long*>(a.totals));
+  if (threadIdx.x == 0) {
+    const int64_t T0 = a.totals[0], T1 = a.totals[1];
+    if (a.root_stats) { a.root_stats[0] = T0; a.root_stats[1] = T1; }
+    if (a.root_totals) { a.root_totals[0] = T0; a.root_totals[1] = T1; }
+    if (a.root_open) a.root_open[0] = 0;
+    if (a.kexp_copy) { a.kexp_copy[0] = k0; a.kexp_copy[1] = k1; }
   }
 }
 
@@ -744,8 +834,7 @@ __global__ __launch_bounds__(256) void hist_subtract_kernel(const int64_t* paren
 }
 
 // ------------------------------------------------------------------ split search
-__global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void split_narrow_at(const SplitArgs& a, int64_t t) {
   if (t >= (int64_t)a.num_nodes * a.Fa) return;
   const int n = (int)(t / a.Fa), f = (int)(t % a.Fa);
   if (a.wide != nullptr && a.nbins[f] > kSplitWide) return;     // split_wide_kernel's
@@ -764,6 +853,10 @@ __global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
   a.out_bin[t] = bin;
   a.out_left[2 * t] = l0;
   a.out_left[2 * t + 1] = l1;
+}
+
+__global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
+  split_narrow_at(a, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
 // Wide features (> kSplitWide bins: the hot words' count bins): a wave per (node, feature), lane
@@ -787,9 +880,7 @@ __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void split_wide_kernel(SplitArgs a) {
-  const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+__device__ __forceinline__ void split_wide_at(const SplitArgs& a, int64_t w, int lane) {
   if (w >= (int64_t)a.num_nodes * a.n_wide) return;                 // (wave-uniform)
   const int n = (int)(w / a.n_wide), f = a.wide[w % a.n_wide];
   const int64_t t = (int64_t)n * a.Fa + f;
@@ -849,16 +940,28 @@ __global__ __launch_bounds__(256) void split_wide_kernel(SplitArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void split_wide_kernel(SplitArgs a) {
+  split_wide_at(a, ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6, threadIdx.x & 63);
+}
+
+// split_kernel and split_wide_kernel in one launch: workgroups [0, nb_narrow) search the narrow
+// features (a thread per (node, feature)), the rest the wide ones (a wave per (node, feature))
+__global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb_narrow) {
+  if (blockIdx.x < nb_narrow) {
+    split_narrow_at(a, (int64_t)blockIdx.x * 256 + threadIdx.x);
+  } else {
+    split_wide_at(a, ((int64_t)(blockIdx.x - nb_narrow) * 256 + threadIdx.x) >> 6, threadIdx.x & 63);
+  }
+}
+
 // Best split per node over the per-feature results of split_kernel, as one int64 row
 // {gain bits, feature + f0, bin, left0, left1}: the largest gain, ties to the lowest feature; a
 // NaN gain anywhere makes the node's gain NaN (feature 0), like the torch max/where it replaces.
 // One 1024-thread block per node, 4 independent loads in flight per thread (the 256-thread
 // version was a latency-bound ~40 us per level at ~10^5 features).
 constexpr int kBestThreads = 1024;
-__global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* gain, const int32_t* bin,
-                                                                  const int64_t* left, int32_t Fa, int64_t f0,
-                                                                  int64_t* out) {
-  const int n = blockIdx.x;
+__device__ __forceinline__ void split_best_node(const double* gain, const int32_t* bin, const int64_t* left,
+                                                int32_t Fa, int64_t f0, int64_t* out, int n) {
   const double* g = gain + (int64_t)n * Fa;
   double best = -1.0 / 0.0;
   int bf = Fa;
@@ -912,6 +1015,12 @@ __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* 
   }
 }
 
+__global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* gain, const int32_t* bin,
+                                                                  const int64_t* left, int32_t Fa, int64_t f0,
+                                                                  int64_t* out) {
+  split_best_node(gain, bin, left, Fa, f0, out, blockIdx.x);
+}
+
 // ------------------------------------------------------------------ partition
 // kPartRows consecutive rows per thread: the row -> node -> (default child, hot split) -> bin byte
 // chain of dependent loads is paid once per 8 rows (16-byte row_node loads and stores) instead
@@ -920,6 +1029,12 @@ __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* 
 constexpr int kPartRows = 8;
 
 __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) {
+  if (a.zero != nullptr) {           // the next level's histograms, zeroed on the way (16-byte stores)
+    int4* z = reinterpret_cast<int4*>(a.zero);
+    const int64_t nz = a.zero_n / 2;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nz; i += (int64_t)gridDim.x * 256)
+      z[i] = make_int4(0, 0, 0, 0);
+  }
   const int64_t stride = (int64_t)gridDim.x * 256 * kPartRows;
   for (int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kPartRows; r0 < a.N; r0 += stride) {
     if (r0 + kPartRows <= a.N) {
@@ -1182,6 +1297,21 @@ __global__ void level_plan_kernel(LevelPlanArgs a) {
   if (threadIdx.x < 64) level_plan_wave(a);
 }
 
+// split_best_kernel + level_plan_kernel in one launch (levels without a collective between the
+// split search and the plan): a workgroup per node writes its best split tuple, and the last
+// workgroup to finish (ticket) plans the level from all of them -- the same two bodies, so the
+// same node table bit for bit, one launch and one kernel boundary less per level.
+__global__ __launch_bounds__(kBestThreads) void split_best_plan_kernel(const double* gain, const int32_t* bin,
+                                                                       const int64_t* left, int32_t Fa, int64_t f0,
+                                                                       int64_t* out, LevelPlanArgs p,
+                                                                       unsigned int* ticket) {
+  split_best_node(gain, bin, left, Fa, f0, out, blockIdx.x);
+  if (!last_workgroup(ticket)) return;
+  level_plan_reset(p, (int32_t)threadIdx.x, (int32_t)blockDim.x);
+  __syncthreads();
+  if (threadIdx.x < 64) level_plan_wave(p);
+}
+
 // ------------------------------------------------------------------ gbdt helpers
 __global__ __launch_bounds__(256) void logistic_grad_kernel(const double* margin, const float* label,
                                                             const float* weight, float* g, float* h, int64_t N) {
@@ -1197,6 +1327,18 @@ __global__ __launch_bounds__(256) void leaf_update_kernel(double* margin, const 
                                                           const double* node_value, int64_t N) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256)
     margin[r] += node_value[row_node[r]];
+}
+
+// margin[r] += the leaf value of the row's node, computed from the node table (leaf_value: the
+// same fp64 operations as leaf_values_kernel, so bitwise leaf_values + leaf_update in one launch)
+__global__ __launch_bounds__(256) void leaf_update_stats_kernel(double* margin, const int32_t* row_node,
+                                                               const int64_t* stats, const int32_t* kexp, double eta,
+                                                               double lambda, double mds, int64_t N) {
+  const int32_t k0 = kexp[0], k1 = kexp[1];
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256) {
+    const int32_t n = row_node[r];
+    margin[r] += leaf_value(stats[2 * n], stats[2 * n + 1], k0, k1, eta, lambda, mds);
+  }
 }
 
 __global__ __launch_bounds__(256) void leaf_values_kernel(const int64_t* stats, const int32_t* kexp, int64_t M,
@@ -1223,9 +1365,20 @@ void launch_quant_max(const QuantArgs& a, double* out, void* partials, hipStream
                      reinterpret_cast<unsigned long long*>(out));
 }
 
+void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, void* partials,
+                     unsigned int* ticket, double* maxv, hipStream_t s) {
+  const int nb = quant_blocks(N > 0 ? N : 1);
+  hipLaunchKernelGGL(grad_max_kernel, dim3(nb), dim3(256), 0, s, margin, label, g, h, N,
+                     reinterpret_cast<unsigned long long*>(partials), ticket, reinterpret_cast<unsigned long long*>(maxv));
+}
+
 void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStream_t s) {
   auto* part = reinterpret_cast<unsigned long long*>(partials);
   const int nb = a.N > 0 ? quant_blocks(a.N) : 0;
+  if (a.ticket != nullptr) {             // one launch: the last workgroup reduces (quant_kernel)
+    hipLaunchKernelGGL(quant_kernel, dim3(nb > 0 ? nb : 1), dim3(256), 0, s, a, maxv, part);
+    return;
+  }
   if (nb > 0) hipLaunchKernelGGL(quant_kernel, dim3(nb), dim3(256), 0, s, a, maxv, part);
   else hipLaunchKernelGGL(quant_kernel, dim3(1), dim3(256), 0, s, a, maxv, part);     // (writes kexp)
   hipLaunchKernelGGL(quant_reduce_kernel<false>, dim3(1), dim3(256), 0, s, part, nb > 0 ? nb : 1,
@@ -1340,11 +1493,19 @@ void launch_hist_subtract(const int64_t* parent, int64_t* cur, const int32_t* ds
 void launch_split(const SplitArgs& a, hipStream_t s) {
   const int64_t n = (int64_t)a.num_nodes * a.Fa;
   if (n <= 0) return;
-  hipLaunchKernelGGL(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
-  if (a.wide != nullptr && a.n_wide > 0) {
-    const int64_t waves = (int64_t)a.num_nodes * a.n_wide;
-    hipLaunchKernelGGL(split_wide_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a);
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  const int64_t waves = (a.wide != nullptr && a.n_wide > 0) ? (int64_t)a.num_nodes * a.n_wide : 0;
+  hipLaunchKernelGGL(split_all_kernel, dim3(nb + (unsigned)((waves + 3) / 4)), dim3(256), 0, s, a, nb);
+}
+
+void launch_split_best_plan(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
+                            int64_t f0, int64_t* out, const LevelPlanArgs& p, unsigned int* ticket, hipStream_t s) {
+  if (nodes <= 0 || Fa <= 0) {                  // (no candidates: the caller filled out)
+    hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(64), 0, s, p);
+    return;
   }
+  hipLaunchKernelGGL(split_best_plan_kernel, dim3(nodes), dim3(kBestThreads), 0, s, gain, bin, left, Fa, f0, out, p,
+                     ticket);
 }
 
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
@@ -1384,6 +1545,13 @@ void launch_leaf_values(const int64_t* stats, const int32_t* kexp, int64_t M, do
   if (M > 0)
     hipLaunchKernelGGL(leaf_values_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, stats, kexp, M, eta,
                        lambda, mds, out);
+}
+
+void launch_leaf_update_stats(double* margin, const int32_t* row_node, const int64_t* stats, const int32_t* kexp,
+                              double eta, double lambda, double mds, int64_t N, hipStream_t s) {
+  if (N > 0)
+    hipLaunchKernelGGL(leaf_update_stats_kernel, dim3(grid_for(N)), dim3(256), 0, s, margin, row_node, stats, kexp, eta,
+                       lambda, mds, N);
 }
 
 void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s) {

@@ -104,8 +104,6 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     else:
         base = _logit(float(params.base_score))
     margin = torch.full((N,), base, dtype=torch.float64, device=dev)
-    g = torch.empty(N, dtype=torch.float32, device=dev)
-    h = torch.empty(N, dtype=torch.float32, device=dev)
     gp = GrowParams(max_depth=params.max_depth, mode=0, lambda_=params.reg_lambda, min_child=params.min_child_weight,
                     min_gain=params.gamma, seed=params.seed, eta=params.learning_rate,
                     max_delta_step=params.max_delta_step)
@@ -127,14 +125,15 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     pending = None
     for t in range(len(trees), params.n_estimators):
         with tracing.span("gbdt.round", round=t):
-            C.tree_logistic_grad(margin, y, w, g, h)
-            res = grow_tree(Q, ws, gp, t, g=g, h=h, coll=coll, deferred=defer,
+            # the round's gradients: computed inside the tree's prologue (fused with the max |g|,
+            # |h| pass on the device loop's native runner) from the margins and labels
+            res = grow_tree(Q, ws, gp, t, label=y, weight=w, coll=coll, deferred=defer, margin=margin,
                             on_first_wait=pending.finish if pending is not None else None)
             if pending is not None:
                 trees.append(pending.result().compacted())
                 pending = None
             if isinstance(res, PendingTree):
-                C.tree_leaf_update(margin, ws.row_node, res.node_value)
+                res.update_margin(margin, ws.row_node)
                 pending = res
                 maybe_fail(t, model="gbdt")
                 continue

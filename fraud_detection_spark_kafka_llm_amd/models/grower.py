@@ -458,6 +458,13 @@ class Workspace:
             self._dense_groups[key] = out
         return out
 
+    def gh(self) -> tuple:
+        """[N] float32 g, h buffers of the GBDT rounds (computed on the device per round)."""
+        if getattr(self, "_gh", None) is None:
+            self._gh = (torch.empty(self.Q.n_rows, dtype=torch.float32, device=self.dev),
+                        torch.empty(self.Q.n_rows, dtype=torch.float32, device=self.dev))
+        return self._gh
+
     def iota(self, n: int) -> torch.Tensor:
         """[0, 1, ..., n - 1] int32 on the device (cached: one allocation per workspace)."""
         t = getattr(self, "_iota", None)
@@ -718,7 +725,8 @@ def _choose_np(params: GrowParams, weight) -> int:
 def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
               g: Optional[torch.Tensor] = None, h: Optional[torch.Tensor] = None,
               label: Optional[torch.Tensor] = None, weight: Optional[torch.Tensor] = None,
-              bootstrap: bool = False, coll=None, deferred: bool = False, on_first_wait=None):
+              bootstrap: bool = False, coll=None, deferred: bool = False, on_first_wait=None,
+              margin: Optional[torch.Tensor] = None):
     """``coll`` (parallel.dist.Collectives): data-parallel level with feature-sharded split
     finding when world > 1 -- partial histograms are reduce-scattered by feature shard, every
     rank searches splits of its own shard, and the per-node best tuples are all-gathered
@@ -728,7 +736,11 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
     shards = ws.shards(coll) if use_coll and (coll.world > 1 or getattr(coll, "force", False)) else None
     if device_levels_ok(params, weight):
         return grow_tree_device(Q, ws, params, tree_index, g, h, weight, coll if use_coll else None, shards,
-                                label=label, bootstrap=bootstrap, deferred=deferred, on_first_wait=on_first_wait)
+                                label=label, bootstrap=bootstrap, deferred=deferred, on_first_wait=on_first_wait,
+                                margin=margin)
+    if margin is not None and g is None:           # (GBDT: this round's gradients)
+        g, h = ws.gh()
+        C.tree_logistic_grad(margin, label, weight, g, h)
     if on_first_wait is not None:
         on_first_wait()
     dev = Q.device
@@ -1106,11 +1118,12 @@ class LevelState:
 def grow_tree_device(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
                      h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
                      shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
-                     bootstrap: bool = False, deferred: bool = False, on_first_wait=None):
+                     bootstrap: bool = False, deferred: bool = False, on_first_wait=None,
+                     margin: Optional[torch.Tensor] = None):
     """One tree through :func:`device_tree_steps`, waiting on each event it yields."""
     batcher = LevelBatcher(coll, shards.S, Q.device) if shards is not None else None
     return drive(device_tree_steps(Q, ws, params, tree_index, g, h, weight, coll, shards, label, bootstrap,
-                                   deferred, on_first_wait), batcher)
+                                   deferred, on_first_wait, margin), batcher)
 
 
 def drive(steps, batcher: Optional[LevelBatcher] = None):
@@ -1139,18 +1152,24 @@ def _wide_features(nbins: torch.Tensor, Fa: int) -> torch.Tensor:
     return memo[1]
 
 
-def _rf_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowParams, item_groups: list):
+def _level_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowParams, item_groups: list,
+                  sampled: bool):
     """The lane's native level runner (csrc/bindings_level.cpp RfLevels), built once per workspace,
-    level state and tree parameters."""
-    key = (params.mode, params.max_depth, params.min_gain, params.min_child, params.seed, params.feat_k)
+    level state and tree parameters. RF (``sampled``): every kernel of a level; GBDT: the tree
+    prologue, the fused split + plan and the partition (the row-group passes stay in Python)."""
+    key = (params.mode, params.max_depth, params.min_gain, params.min_child, params.seed, params.feat_k,
+           params.lambda_, sampled)
     cached = getattr(ws, "_rf_runner", None)
     if cached is not None and cached[0] is st and cached[1] == key:
         return cached[2]
     cfg = dict(groups=[(g.item_start, g.item_end, g.item_f0, g.item_meta, g.wave_order(), int(g.bt))
                        for g in item_groups],
-               h_row=Q.h_row, h_key=Q.h_key, csc_row=Q.csc_row, csc_bin=Q.csc_bin, colptr=Q.colptr, nbins=Q.nbins,
+               h_row=Q.h_row if sampled else None, h_key=Q.h_key if sampled else None, csc_row=Q.csc_row,
+               csc_bin=Q.csc_bin, colptr=Q.colptr, nbins=Q.nbins,
                zbin=Q.zbin, fid_orig=Q.fid_orig, dense=Q.dense if st.node_dense is not None else None,
-               hot_row=st.hot_row, rowdig=ws.rowdig, rowpack=ws.rowpack(), row_node=ws.row_node, kexp=ws.kexp,
+               hot_row=st.hot_row, rowdig=ws.rowdig, rowpack=ws.rowpack() if sampled else None, row_node=ws.row_node,
+               kexp=ws.kexp, build_all=bool(params.feat_k), arena_stats=st.stats[0], open0=st.open[0],
+               totals0=st.totals[0], kexp_slot=st.kexp_slot,
                stats=st.stats, parent=st.parent, left=st.left, right=st.right, feat=st.feat, bin=st.bin, leaf=st.leaf,
                gain=st.gain, n_nodes=st.n_nodes, counts=st.counts, counts_host=st.counts_host,
                default_child=st.default_child, cs_feat=st.cs[0], cs_default=st.cs[1], cs_other=st.cs[2],
@@ -1167,7 +1186,8 @@ def _rf_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowParams
 def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
                       h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
                       shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
-                      bootstrap: bool = False, deferred: bool = False, on_first_wait=None):
+                      bootstrap: bool = False, deferred: bool = False, on_first_wait=None,
+                      margin: Optional[torch.Tensor] = None):
     """A generator: yields an event wherever the host must wait for the device (the next level's
     counts, the finished node table) and returns the Tree (or PendingTree). :func:`drive` runs
     one tree; the forest driver (models/forest_batch.py) interleaves several on their own streams.
@@ -1183,7 +1203,9 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     every rank plans the identical next level from the identical gathered splits.
     ``deferred`` (GBDT): return a :class:`PendingTree` whose leaf values were computed on the
     device; the host table is built later (``on_first_wait`` of the next tree runs it while that
-    tree's root level is on the GPU), so the GPU never idles on the host's tree build."""
+    tree's root level is on the GPU), so the GPU never idles on the host's tree build.
+    ``margin`` (GBDT, with ``label`` and g = h = None): the round's gradients are computed here,
+    fused into the tree's prologue when the native runner drives the levels."""
     C = native.lib()
     dev = Q.device
     np_ = _choose_np(params, weight)
@@ -1200,15 +1222,44 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     st = getattr(ws, "_levels", None)
     if st is None or st.max_depth != params.max_depth or st.n_sel != len(sel_ids):
         st = ws._levels = LevelState(Q, params.max_depth, len(sel_ids))
-    runner = _rf_runner(Q, ws, st, params, item_groups) if (sampled and NATIVE_LEVELS and dev.type == "cuda") \
-        else None
-    ws.row_node.zero_()
+    # the native runner: RF levels (any world size); GBDT single-process levels (whose prologue,
+    # split + plan and partition it fuses)
+    gbdt_native = NATIVE_LEVELS and dev.type == "cuda" and params.mode == 0 and shards is None and coll is None \
+        and weight is None and not build_all
+    runner = _level_runner(Q, ws, st, params, item_groups, sampled) \
+        if (NATIVE_LEVELS and dev.type == "cuda" and (sampled or gbdt_native)) else None
     # every step of this generator runs on the stream current now (the forest driver advances a
     # lane inside that lane's stream context)
     cur_stream = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
     seed = int(params.seed)
+    native_prologue = runner is not None and shards is None and coll is None
+    if native_prologue:
+        # arena image first: the prologue's last workgroup writes the root state into it
+        st.arena.copy_(st.arena_init, non_blocking=True)
+        with tracing.span("tree.quant"):
+            # (the dense-block digit planes only feed the MFMA dense path, off with the row groups)
+            digp = ws.digp if (ws.digp is not None and not build_all and ws.rowgroups() is None) else None
+            if np_ == 4 and margin is not None and g is None:
+                g, h = ws.gh()
+                runner.prologue(margin, g, h, label, None, int(tree_index), False, 4, ws.maxabs, ws.totals, digp,
+                                Q.row0)
+            elif np_ == 4:
+                C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
+                                 ws.maxabs, Q.row0)
+                runner.prologue(None, g, h, label, weight, int(tree_index), bool(bootstrap), 4, ws.maxabs, ws.totals,
+                                digp, Q.row0)
+            else:
+                runner.prologue(None, g, h, label, weight, int(tree_index), bool(bootstrap), 1, None, ws.totals, digp,
+                                Q.row0)
+    else:
+        if margin is not None and g is None:
+            g, h = ws.gh()
+            C.tree_logistic_grad(margin, label, weight, g, h)
+        ws.row_node.zero_()
     with tracing.span("tree.quant"):
-        if np_ == 4:
+        if native_prologue:
+            pass
+        elif np_ == 4:
             C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
                              ws.maxabs, Q.row0)
             mx = coll.max(ws.maxabs) if coll is not None else ws.maxabs
@@ -1219,9 +1270,10 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                          ws.kexp, ws.totals, ws.digp, Q.row0)
     # root: node 0, open list [0] with the exact totals (no host round trip); under data
     # parallelism the totals are summed by the root level's reduce-scatter (LaneBufs.tot_bin)
-    st.arena.copy_(st.arena_init, non_blocking=True)
-    st.open[0][:1].zero_()
-    if shards is None:
+    if not native_prologue:
+        st.arena.copy_(st.arena_init, non_blocking=True)
+        st.open[0][:1].zero_()
+    if shards is None and not native_prologue:
         tot = coll.sum(ws.totals) if coll is not None else ws.totals
         st.stats[0].copy_(tot)
         st.totals[0][:1].copy_(tot[None])
@@ -1343,7 +1395,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 sel_groups, use_dense = [], False
             if sel_groups is None:
                 sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups
-            if runner is not None:
+            if runner is not None and sampled:
                 pack = ws.rowpack() if (d > 0 and not single) else None
                 lists, cnts, npxs = [], [], []
                 for gi, grp in enumerate(sel_groups):
@@ -1433,8 +1485,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 packed = ws.split_cache.get(("out", n_open))
                 if packed is None:
                     packed = ws.split_cache[("out", n_open)] = torch.empty((n_open, 5), dtype=torch.int64, device=dev)
-                runner.split(cur_hist, totals_d, Q.boff, Q.nbins, Q.zbin, Q.fid_orig, open_d, feat_thr, int(tree_index),
-                             0, packed, None, _wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None)
+                # (split search, best split and level plan: 2 launches, below)
             elif runner is not None:
                 runner.split(cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig, open_d,
                              feat_thr, int(tree_index), shards.f0, bufs.ag_in, row_of,
@@ -1470,11 +1521,20 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 sel = sel_args
             else:
                 sel = []
-            runner.plan(d, n_open, packed, open_d, n_open_ptr, st.open[nxt], st.totals[nxt], int(tree_index),
-                        sample_next, thr_n, mask_n, *lay, sel)
+            if shards is None:
+                runner.split_plan(d, n_open, cur_hist, totals_d, Q.boff, feat_thr, int(tree_index), packed,
+                                  _wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, open_d, n_open_ptr,
+                                  st.open[nxt], st.totals[nxt], sample_next, thr_n, mask_n, sel)
+            else:
+                runner.plan(d, n_open, packed, open_d, n_open_ptr, st.open[nxt], st.totals[nxt], int(tree_index),
+                            sample_next, thr_n, mask_n, *lay, sel)
             ev = st.record_event(cur_stream)
+            zero = None
+            if shards is None and more and not build_all:
+                # the next level's histograms, zeroed by the partition kernel on the way
+                pre_hist = zero = torch.empty((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
             with tracing.span("tree.partition"):
-                runner.partition(d, n_open, bool(FUSED_PACK and more))
+                runner.partition(d, n_open, bool(sampled and FUSED_PACK and more), zero)
             prev_hist = cur_hist
             prev_row_of = row_of
             continue
@@ -1516,8 +1576,12 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     if on_first_wait is not None:          # (a one-level tree) the previous table first
         on_first_wait()
     # one read of the node table per tree: the arena (table + exponents) in one D2H copy, one wait
-    st.kexp_slot.copy_(ws.kexp)
-    node_value = leaf_values_device(st.stats, ws.kexp, params) if deferred and params.mode == 0 else None
+    if not native_prologue:                # (the prologue's last workgroup wrote them)
+        st.kexp_slot.copy_(ws.kexp)
+    node_value = None
+    if deferred and params.mode == 0:
+        # the margin update reads the device node table (one launch with the runner)
+        node_value = (runner, params) if runner is not None else leaf_values_device(st.stats, ws.kexp, params)
     st.arena_host.copy_(st.arena, non_blocking=True)
     done = torch.cuda.Event() if dev.type == "cuda" else _Done()
     if dev.type == "cuda":
@@ -1550,12 +1614,21 @@ def leaf_values_device(stats: torch.Tensor, kexp: torch.Tensor, params: GrowPara
 
 class PendingTree:
     """A grown GBDT tree whose host table is not built yet: ``node_value`` (device, per node id)
-    is ready in stream order for the margin update; ``result()`` builds the Tree once."""
+    is ready in stream order for the margin update -- or (runner, params): the native runner
+    updates the margins from the device node table itself; ``result()`` builds the Tree once."""
 
-    def __init__(self, node_value: torch.Tensor, finish):
+    def __init__(self, node_value, finish):
         self.node_value = node_value
         self._finish = finish
         self._tree = None
+
+    def update_margin(self, margin: torch.Tensor, row_node: torch.Tensor) -> None:
+        """margin[r] += the leaf value of row r's node (queued on the current stream)."""
+        if isinstance(self.node_value, tuple):
+            runner, p = self.node_value
+            runner.leaf_update(margin, float(p.eta), float(p.lambda_), float(p.max_delta_step))
+        else:
+            native.lib().tree_leaf_update(margin, row_node, self.node_value)
 
     def finish(self) -> None:
         if self._tree is None:
