@@ -1,6 +1,7 @@
 """Per-boosting-round breakdown of a rocprofv3 kernel trace (``*_kernel_trace.csv``).
 
-Rounds are delimited by the ``logistic_grad`` kernel that starts each GBDT round. Prints, for a
+Rounds are delimited by the kernel that starts each GBDT round (``logistic_grad``, or the fused
+``grad_max`` of the native level runner). Prints, for a
 few rounds, the wall time between round starts, the summed kernel time (GPU busy) and the
 per-kernel split of one round.
 
@@ -15,12 +16,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--round", type=int, default=6)
-    ap.add_argument("--marker", default="logistic_grad")
+    ap.add_argument("--marker", default=None, help="round-start kernel (default: logistic_grad, else grad_max)")
     ap.add_argument("--sequence", action="store_true", help="also list the kernels of the round in order")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]]
+    markers = [args.marker] if args.marker else ["logistic_grad", "grad_max_kernel"]
+    idx = []
+    for m in markers:
+        idx = [i for i, r in enumerate(rows) if m in r["Kernel_Name"]]
+        if idx:
+            break
+    if len(idx) < 3:
+        print(f"{len(idx)} rounds: too few to split")
+        return
     print(f"{len(idx)} rounds")
     for a, b in zip(idx[1:-1], idx[2:]):
         seg = rows[a:b]

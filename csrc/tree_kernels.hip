@@ -83,11 +83,15 @@ __global__ __launch_bounds__(256) void quant_reduce_kernel(const unsigned long l
 
 // The last workgroup of a partials pass (ticket: a zeroed counter, reset here for the next
 // launch): true for one workgroup, after every other workgroup's partial is visible.
+// One device-scope release per workgroup, from the ticket thread only, after the barrier has
+// drained every wave's stores: an agent-scope fence writes the XCD's L2 back, and one per wave
+// of a 2048-workgroup grid cost ~140 us per pass (profiles/r5/NOTES.md); the acquire side runs
+// in the last workgroup alone.
 __device__ __forceinline__ bool last_workgroup(unsigned int* ticket) {
   __shared__ int s_last;
-  __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) {
+    __threadfence();
     const unsigned int t = atomicAdd(ticket, 1u);
     s_last = (t == gridDim.x - 1) ? 1 : 0;
     if (s_last) atomicExch(ticket, 0u);
@@ -1348,6 +1352,7 @@ __global__ __launch_bounds__(256) void leaf_values_kernel(const int64_t* stats, 
 }
 
 constexpr int kQuantBlocks = 2048;      // workgroup cap of the quantisation passes (partials)
+constexpr int kTicketBlocks = 512;      // ... of the single-launch (last-workgroup) passes
 
 inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
   const int64_t b = (n + 255) / 256;
@@ -1367,7 +1372,7 @@ void launch_quant_max(const QuantArgs& a, double* out, void* partials, hipStream
 
 void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, void* partials,
                      unsigned int* ticket, double* maxv, hipStream_t s) {
-  const int nb = quant_blocks(N > 0 ? N : 1);
+  const int nb = (int)grid_for(N > 0 ? N : 1, kTicketBlocks);
   hipLaunchKernelGGL(grad_max_kernel, dim3(nb), dim3(256), 0, s, margin, label, g, h, N,
                      reinterpret_cast<unsigned long long*>(partials), ticket, reinterpret_cast<unsigned long long*>(maxv));
 }
@@ -1376,7 +1381,8 @@ void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStr
   auto* part = reinterpret_cast<unsigned long long*>(partials);
   const int nb = a.N > 0 ? quant_blocks(a.N) : 0;
   if (a.ticket != nullptr) {             // one launch: the last workgroup reduces (quant_kernel)
-    hipLaunchKernelGGL(quant_kernel, dim3(nb > 0 ? nb : 1), dim3(256), 0, s, a, maxv, part);
+    const int nt = a.N > 0 ? (int)grid_for(a.N, kTicketBlocks) : 1;
+    hipLaunchKernelGGL(quant_kernel, dim3(nt), dim3(256), 0, s, a, maxv, part);
     return;
   }
   if (nb > 0) hipLaunchKernelGGL(quant_kernel, dim3(nb), dim3(256), 0, s, a, maxv, part);
