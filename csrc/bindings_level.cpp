@@ -88,6 +88,14 @@ class RfLevels {
                           "cs_left_default", "node_slot", "s2n", "sub_dst", "sub_par", "sub_sib"})
       st_[k] = get(c, k);
     node_dense_ = get_opt(c, "node_dense");
+    arena_ = get_opt(c, "arena");
+    {
+      // the counts' pinned host rows as the device sees them: the plan writes the 4 counts there
+      // itself (no D2H copy launch per level); none when the pointer is not mappable
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, st_["counts_host"].data_ptr(), 0) == hipSuccess) counts_host_dev_ = (int32_t*)dp;
+      else (void)hipGetLastError();
+    }
     wide_ = get_opt(c, "wide");
     mode_ = c["mode"].cast<int>();
     max_depth_ = c["max_depth"].cast<int>();
@@ -104,6 +112,7 @@ class RfLevels {
     const int64_t cap = st_["s2n"].numel();
     scratch_ = at::empty({fdx::rf_scratch_bytes(2 * cap)}, row_node_.options().dtype(at::kByte));
     ticket_ = at::zeros({4}, row_node_.options());
+    maxv_ = at::zeros({4}, row_node_.options().dtype(at::kLong));
     parts_ = at::empty({2 * (int64_t)fdx::quant_blocks(row_node_.numel())}, row_node_.options().dtype(at::kLong));
   }
 
@@ -111,17 +120,40 @@ class RfLevels {
   // gradient + max |g|, |h| launch first, when margin is given) whose last workgroup reduces the
   // totals and writes the root state (stats[0], the level-0 totals, open[0], the arena's
   // exponents) and row_node = 0 -- what quant_max + 2 reductions + 4 fills / copies did.
+  // No grid-wide completion test anywhere (QuantArgs atomic_root): the max |g|, |h| are 64-bit
+  // atomic maxima into this round's parity slot of maxv_ (the previous round cleared it), the
+  // totals atomic adds into stats[0]. With margin, the first launch also copies the arena image
+  // in (arena_init, device) and zeroes the root histogram (zero); without, quant zeroes it and
+  // the caller has copied the arena image.
   void prologue(const optional<Tensor>& margin, const optional<Tensor>& g, const optional<Tensor>& h,
                 const optional<Tensor>& label, const optional<Tensor>& weight, int64_t tree, bool bootstrap,
                 int64_t np, const optional<Tensor>& maxabs, const Tensor& totals, const optional<Tensor>& digp,
-                int64_t row0) {
+                int64_t row0, const optional<Tensor>& zero, const optional<Tensor>& arena_init) {
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
     const int64_t N = row_node_.numel();
+    if (zero)
+      FDX_CHECK(zero->scalar_type() == at::kLong && zero->is_contiguous() &&
+                    reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0, "zero: contiguous int64, 16-byte aligned");
+    const double* maxv = maxabs ? p<double>(*maxabs) : nullptr;
     if (margin) {
-      FDX_CHECK(g && h && label && maxabs && !weight && mode_ == 0, "the fused gradient prologue: unweighted GBDT");
-      fdx::launch_grad_max(p<double>(*margin), p<float>(*label), p<float>(*g), p<float>(*h), N, p<int64_t>(parts_),
-                           reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)), p<double>(*maxabs), s);
+      FDX_CHECK(g && h && label && !weight && mode_ == 0, "the fused gradient prologue: unweighted GBDT");
+      FDX_CHECK(arena_init && arena_ && arena_init->numel() == arena_->numel() && arena_->numel() % 8 == 0,
+                "arena image [arena bytes], a multiple of 8");
+      fdx::PrologueInit pi{};
+      pi.init_src = reinterpret_cast<const uint64_t*>(arena_init->data_ptr());
+      pi.init_dst = reinterpret_cast<uint64_t*>(arena_->data_ptr());
+      pi.init_n = arena_->numel() / 8;
+      if (zero) {
+        pi.zero = p<int64_t>(*zero);
+        pi.zero_n = zero->numel();
+      }
+      unsigned long long* mv = reinterpret_cast<unsigned long long*>(p<int64_t>(maxv_));
+      pi.max_clear = mv + 2 * (1 - parity_);
+      fdx::launch_grad_max(p<double>(*margin), p<float>(*label), p<float>(*g), p<float>(*h), N,
+                           reinterpret_cast<double*>(mv + 2 * parity_), pi, s);
+      maxv = reinterpret_cast<const double*>(mv + 2 * parity_);
+      parity_ ^= 1;
     }
     fdx::QuantArgs a{};
     a.g = p<float>(g);
@@ -142,13 +174,16 @@ class RfLevels {
       a.digp = p<uint8_t>(*digp);
       a.n_pad = digp->size(1);
     }
-    a.ticket = reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 1;
+    a.atomic_root = 1;
     a.root_stats = p<int64_t>(st_["arena_stats"]);
-    a.root_totals = p<int64_t>(st_["totals0"]);
     a.root_open = p<int32_t>(st_["open0"]);
     a.kexp_copy = p<int32_t>(st_["kexp_slot"]);
     a.row_node = p<int32_t>(row_node_);
-    fdx::launch_quant(a, maxabs ? p<double>(*maxabs) : nullptr, p<int64_t>(parts_), s);
+    if (zero && !margin) {
+      a.zero = p<int64_t>(*zero);
+      a.zero_n = zero->numel();
+    }
+    fdx::launch_quant(a, maxv, p<int64_t>(parts_), s);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 
@@ -346,9 +381,22 @@ class RfLevels {
             const std::vector<optional<Tensor>>& sel_lists) {
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
-    fdx::launch_level_plan(plan_args(d, n_open, packed, open, n_open_ptr, next_open, next_totals), s);
+    fdx::LevelPlanArgs a = plan_args(d, n_open, packed, open, n_open_ptr, next_open, next_totals);
+    const bool zc = counts_zero_copy(a, d, sample_next, sel_lists);
+    fdx::launch_level_plan(a, s);
     after_plan(d, n_open, next_open, tree, sample_next, thr, mask, fs, nbins_all, local, sizes, sizes_host,
-               max_shard_features, sel_lists, s);
+               max_shard_features, sel_lists, s, zc);
+  }
+
+  // The plan writes the level's counts into the host-mapped row itself unless the per-XCD
+  // item counts of a preselected next level follow it (then one D2H copy of the whole row).
+  bool counts_zero_copy(fdx::LevelPlanArgs& a, int64_t d, bool sample_next,
+                        const std::vector<optional<Tensor>>& sel_lists) const {
+    bool sel = false;
+    for (const auto& l : sel_lists) sel = sel || l.has_value();
+    if (counts_host_dev_ == nullptr || (sample_next && sel)) return false;
+    a.counts_host = counts_host_dev_ + d * st_.at("counts").size(1);
+    return true;
   }
 
   // Split search + best split + level plan with no collective between them (split_all_kernel, then
@@ -363,14 +411,15 @@ class RfLevels {
     const int32_t Fa = (int32_t)nbins_.numel();
     FDX_CHECK(open.numel() == n_open, "open [n_open]");
     const bool any = find(hist, totals, boff, nbins_, zbin_, fid_orig_, open, feat_thr, tree, out, c10::nullopt, wide, s);
-    const fdx::LevelPlanArgs a = plan_args(d, n_open, out, open, n_open_ptr, next_open, next_totals);
+    fdx::LevelPlanArgs a = plan_args(d, n_open, out, open, n_open_ptr, next_open, next_totals);
+    const bool zc = counts_zero_copy(a, d, sample_next, sel_lists);
     if (any)
       fdx::launch_split_best_plan(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), (int32_t)n_open, Fa, 0,
                                   p<int64_t>(out), a, reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 2, s);
     else                                   // (no features: out holds "no candidate" tuples)
       fdx::launch_level_plan(a, s);
     after_plan(d, n_open, next_open, tree, sample_next, thr, mask, c10::nullopt, c10::nullopt, c10::nullopt,
-               c10::nullopt, c10::nullopt, 0, sel_lists, s);
+               c10::nullopt, c10::nullopt, 0, sel_lists, s, zc);
   }
 
   // For a next level: its feature sample over the (-1 padded) next open list into thr / mask, the
@@ -380,7 +429,7 @@ class RfLevels {
                   const optional<Tensor>& thr, const optional<Tensor>& mask, const optional<Tensor>& fs,
                   const optional<Tensor>& nbins_all, const optional<Tensor>& local, const optional<Tensor>& sizes,
                   const optional<Tensor>& sizes_host, int64_t max_shard_features,
-                  const std::vector<optional<Tensor>>& sel_lists, hipStream_t s) {
+                  const std::vector<optional<Tensor>>& sel_lists, hipStream_t s, bool counts_written) {
     const Tensor& counts = st_["counts"];
     const int64_t cw = counts.size(1);
     int32_t* counts_d = p<int32_t>(counts) + d * cw;
@@ -447,6 +496,10 @@ class RfLevels {
         }
       }
     }
+    if (counts_written) {
+      C10_HIP_KERNEL_LAUNCH_CHECK();
+      return;
+    }
     const Tensor& ch = st_["counts_host"];
     FDX_CHECK(hipMemcpyAsync(p<int32_t>(ch) + d * cw, counts_d, cw * sizeof(int32_t), hipMemcpyDeviceToHost, s) ==
                   hipSuccess, "counts copy");
@@ -502,7 +555,10 @@ class RfLevels {
   Tensor csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, row_node_, kexp_;
   optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_;
   std::map<std::string, Tensor> st_;
-  Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_, ticket_, parts_;
+  Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_, ticket_, parts_, maxv_;
+  optional<Tensor> arena_;
+  int32_t* counts_host_dev_ = nullptr;
+  int parity_ = 0;
   bool build_all_ = true;
   int mode_ = 1, max_depth_ = 5, wps_ = 256;
   double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;

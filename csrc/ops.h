@@ -85,8 +85,9 @@ struct RfCompactArgs;
 void launch_rf_compact(const RfCompactArgs& a, hipStream_t s);
 void launch_split_best_plan(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
                             int64_t f0, int64_t* out, const LevelPlanArgs& p, unsigned int* ticket, hipStream_t s);
-void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, void* partials,
-                     unsigned int* ticket, double* maxv, hipStream_t s);
+struct PrologueInit;
+void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, double* maxv,
+                     const PrologueInit& pi, hipStream_t s);
 void launch_leaf_update_stats(double* margin, const int32_t* row_node, const int64_t* stats, const int32_t* kexp,
                               double eta, double lambda, double mds, int64_t N, hipStream_t s);
 int64_t rf_compact_chunks(int64_t max_shard_features);

@@ -85,6 +85,25 @@ struct QuantArgs {
   int32_t* root_open;
   int32_t* kexp_copy;
   int32_t* row_node;
+  // ... or with no ticket (atomic_root): every workgroup adds its partial sums straight into
+  // root_stats (zero beforehand: the arena image) and workgroup 0 writes open[0] and the
+  // exponents -- no grid-wide completion test, whose per-workgroup device-scope release was the
+  // cost of the ticketed form; the level-0 split reads the totals from stats[0]
+  int32_t atomic_root;
+  int64_t* zero;              // optional: [zero_n] int64 zeroed on the way (the root histogram)
+  int64_t zero_n;
+};
+
+// Tree-start work folded into the first launch of a GBDT round (grad_max_kernel): the node-table
+// arena image copied in (init_n 8-byte words), the root histogram zeroed, and the other parity's
+// max |g|, |h| slot cleared for the next round's atomics.
+struct PrologueInit {
+  const uint64_t* init_src;
+  uint64_t* init_dst;
+  int64_t init_n;
+  int64_t* zero;
+  int64_t zero_n;
+  unsigned long long* max_clear;   // [2]
 };
 
 struct SlotArgs {
@@ -662,6 +681,7 @@ struct LevelPlanArgs {
   int32_t* cs_bin;
   int32_t* cs_left_default;
   int32_t* counts;                // [4] out: n_cs, n_next_open, n_build, n_nodes
+  int32_t* counts_host;           // optional host-mapped copy of the 4 counts (pinned; no D2H copy)
   // level d + 1 (out; capacity 2L open, L built)
   int32_t* next_open;             // [2L] (-1 pad)
   int64_t* next_totals;           // [2L][2]
@@ -804,6 +824,8 @@ FDX_HD void level_plan(const LevelPlanArgs& a, bool reset = true) {
   a.counts[1] = n_next;
   a.counts[2] = nb;
   a.counts[3] = nn;
+  if (a.counts_host)
+    for (int k = 0; k < 4; ++k) a.counts_host[k] = a.counts[k];
 }
 
 }  // namespace fdx

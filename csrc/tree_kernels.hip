@@ -131,12 +131,23 @@ __device__ void reduce_parts_block(const unsigned long long* part, int nparts, u
   if (threadIdx.x == 0) { out[0] = s[0][0]; out[1] = s[1][0]; }
 }
 
+// zero [n] int64 (16-byte stores where aligned) and copy [m] 8-byte words, grid-stride
+__device__ __forceinline__ void prologue_fill(int64_t* zero, int64_t n, const uint64_t* src, uint64_t* dst, int64_t m) {
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+  if (zero) {
+    const int64_t n2 = n >> 1;
+    for (int64_t i = t0; i < n2; i += step) reinterpret_cast<int4*>(zero)[i] = make_int4(0, 0, 0, 0);
+    if ((n & 1) && t0 == 0) zero[n - 1] = 0;
+  }
+  for (int64_t i = t0; i < m; i += step) dst[i] = src[i];
+}
+
 // GBDT round prologue in one launch: g = p - y, h = max(p (1 - p), 1e-16) from the margins
-// (logistic_grad_kernel's arithmetic), max |g|, |h| per workgroup, the last workgroup reducing the
-// partials into maxv (quant_max_kernel + quant_reduce_kernel<true> of the unweighted case).
+// (logistic_grad_kernel's arithmetic) and max |g|, |h| into maxv with one 64-bit atomic max per
+// workgroup and statistic (non-negative doubles order as their bit patterns; maxv zero at entry:
+// the previous round cleared this parity's slot), plus the tree-start work of PrologueInit.
 __global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, const float* label, float* g, float* h,
-                                                       int64_t N, unsigned long long* part, unsigned int* ticket,
-                                                       unsigned long long* maxv) {
+                                                       int64_t N, unsigned long long* maxv, PrologueInit pi) {
   double m0 = 0.0, m1 = 0.0;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256) {
     const double p = 1.0 / (1.0 + exp(-margin[r]));
@@ -147,6 +158,8 @@ __global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, con
     m0 = fmax(m0, fabs((double)gv));
     m1 = fmax(m1, fabs((double)hv));
   }
+  prologue_fill(pi.zero, pi.zero_n, pi.init_src, pi.init_dst, pi.init_n);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && pi.max_clear) { pi.max_clear[0] = 0ull; pi.max_clear[1] = 0ull; }
   for (int o = 32; o > 0; o >>= 1) {
     m0 = fmax(m0, __shfl_xor(m0, o, kWave));
     m1 = fmax(m1, __shfl_xor(m1, o, kWave));
@@ -158,10 +171,9 @@ __global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, con
   if (threadIdx.x == 0) {
     m0 = fmax(fmax(s_m[0][0], s_m[0][1]), fmax(s_m[0][2], s_m[0][3]));
     m1 = fmax(fmax(s_m[1][0], s_m[1][1]), fmax(s_m[1][2], s_m[1][3]));
-    part[2 * blockIdx.x] = (unsigned long long)__double_as_longlong(m0);
-    part[2 * blockIdx.x + 1] = (unsigned long long)__double_as_longlong(m1);
+    atomicMax(maxv, (unsigned long long)__double_as_longlong(m0));
+    atomicMax(maxv + 1, (unsigned long long)__double_as_longlong(m1));
   }
-  if (last_workgroup(ticket)) reduce_parts_block<true>(part, (int)gridDim.x, maxv);
 }
 
 // rowdig[r] = digits of (q0, q1); totals += (sum q0, sum q1) (int64 atomics, exact)
@@ -195,13 +207,23 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
   const int w = threadIdx.x / kWave;
   if ((threadIdx.x & (kWave - 1)) == 0) { s_t[0][w] = t0; s_t[1][w] = t1; }
   __syncthreads();
+  if (a.zero) prologue_fill(a.zero, a.zero_n, nullptr, nullptr, 0);
   if (threadIdx.x == 0) {
     t0 = s_t[0][0] + s_t[0][1] + s_t[0][2] + s_t[0][3];
     t1 = s_t[1][0] + s_t[1][1] + s_t[1][2] + s_t[1][3];
-    part[2 * blockIdx.x] = (unsigned long long)t0;
-    part[2 * blockIdx.x + 1] = (unsigned long long)t1;
+    if (a.atomic_root) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.root_stats), (unsigned long long)t0);
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.root_stats) + 1, (unsigned long long)t1);
+      if (blockIdx.x == 0) {
+        if (a.root_open) a.root_open[0] = 0;
+        if (a.kexp_copy) { a.kexp_copy[0] = k0; a.kexp_copy[1] = k1; }
+      }
+    } else {
+      part[2 * blockIdx.x] = (unsigned long long)t0;
+      part[2 * blockIdx.x + 1] = (unsigned long long)t1;
+    }
   }
-  if (a.ticket == nullptr || !last_workgroup(a.ticket)) return;
+  if (a.atomic_root || a.ticket == nullptr || !last_workgroup(a.ticket)) return;
   // the last workgroup: the exact totals, then the tree's root state
   reduce_parts_block<false>(part, (int)gridDim.x, reinterpret_cast<unsigned long long*>(a.totals));
   if (threadIdx.x == 0) {
@@ -1286,6 +1308,12 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
     a.counts[1] = n_next;
     a.counts[2] = nb;
     a.counts[3] = nn;
+    if (a.counts_host) {         // host-mapped pinned row: visible to the host at the kernel's end
+      a.counts_host[0] = n_cs;
+      a.counts_host[1] = n_next;
+      a.counts_host[2] = nb;
+      a.counts_host[3] = nn;
+    }
   }
 }
 
@@ -1370,17 +1398,17 @@ void launch_quant_max(const QuantArgs& a, double* out, void* partials, hipStream
                      reinterpret_cast<unsigned long long*>(out));
 }
 
-void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, void* partials,
-                     unsigned int* ticket, double* maxv, hipStream_t s) {
+void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, double* maxv,
+                     const PrologueInit& pi, hipStream_t s) {
   const int nb = (int)grid_for(N > 0 ? N : 1, kTicketBlocks);
   hipLaunchKernelGGL(grad_max_kernel, dim3(nb), dim3(256), 0, s, margin, label, g, h, N,
-                     reinterpret_cast<unsigned long long*>(partials), ticket, reinterpret_cast<unsigned long long*>(maxv));
+                     reinterpret_cast<unsigned long long*>(maxv), pi);
 }
 
 void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStream_t s) {
   auto* part = reinterpret_cast<unsigned long long*>(partials);
   const int nb = a.N > 0 ? quant_blocks(a.N) : 0;
-  if (a.ticket != nullptr) {             // one launch: the last workgroup reduces (quant_kernel)
+  if (a.ticket != nullptr || a.atomic_root) {     // one launch (quant_kernel)
     const int nt = a.N > 0 ? (int)grid_for(a.N, kTicketBlocks) : 1;
     hipLaunchKernelGGL(quant_kernel, dim3(nt), dim3(256), 0, s, a, maxv, part);
     return;

@@ -1070,6 +1070,7 @@ class LevelState:
             nbytes = (nbytes + 7) // 8 * 8
             offs.append(nbytes)
             nbytes += isz * int(np.prod(shape))
+        nbytes = (nbytes + 7) // 8 * 8         # (copied in 8-byte words by the GBDT prologue)
         self.arena = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
         self.arena_host = torch.zeros(nbytes, dtype=torch.uint8)
         if dev.type == "cuda":
@@ -1089,6 +1090,8 @@ class LevelState:
         self.arena_init = self.arena.to("cpu", copy=True)       # (a copy also when dev is the CPU)
         if dev.type == "cuda":
             self.arena_init = self.arena_init.pin_memory()
+        self.arena_init_dev = self.arena.clone()       # (the fused GBDT prologue copies it in on the device)
+        self.zero1 = torch.zeros(1, dtype=torch.int32, device=dev)      # the root level's slot -> row table
         self.open = [i32(cap), i32(cap)]
         self.totals = [torch.zeros((cap, 2), dtype=torch.int64, device=dev) for _ in range(2)]
         self.counts = torch.zeros((max_depth + 1, 4 + 8 * n_sel), dtype=torch.int32, device=dev)
@@ -1177,7 +1180,7 @@ def _level_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowPar
                sub_par=st.sub_par, sub_sib=st.sub_sib, node_dense=st.node_dense, mode=int(params.mode),
                max_depth=int(params.max_depth), min_gain=float(params.min_gain), lambda_=float(params.lambda_),
                mcw=float(params.min_child), seed=int(params.seed), F=int(Q.num_features), k=int(params.feat_k),
-               lds=bool(RF_LDS), wps=int(PARTITION_WPS))
+               lds=bool(RF_LDS), wps=int(PARTITION_WPS), arena=st.arena)
     runner = native.lib().RfLevels(cfg)
     ws._rf_runner = (st, key, runner)
     return runner
@@ -1233,24 +1236,32 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     cur_stream = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
     seed = int(params.seed)
     native_prologue = runner is not None and shards is None and coll is None
+    TB = Q.TB
+    # the next level's zeroed histograms (at most 2 open nodes per open node) are queued before
+    # the host waits for its counts, so the fill runs while the host sizes that level
+    pre_hist = None
     if native_prologue:
-        # arena image first: the prologue's last workgroup writes the root state into it
-        st.arena.copy_(st.arena_init, non_blocking=True)
+        # the root histogram is zeroed by the prologue's first launch
+        pre_hist = torch.empty((1, TB, 2), dtype=torch.int64, device=dev)
         with tracing.span("tree.quant"):
             # (the dense-block digit planes only feed the MFMA dense path, off with the row groups)
             digp = ws.digp if (ws.digp is not None and not build_all and ws.rowgroups() is None) else None
             if np_ == 4 and margin is not None and g is None:
+                # gradients + max |g|, |h| + arena image + root histogram zero, then quant: 2 launches
                 g, h = ws.gh()
-                runner.prologue(margin, g, h, label, None, int(tree_index), False, 4, ws.maxabs, ws.totals, digp,
-                                Q.row0)
-            elif np_ == 4:
-                C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
-                                 ws.maxabs, Q.row0)
-                runner.prologue(None, g, h, label, weight, int(tree_index), bool(bootstrap), 4, ws.maxabs, ws.totals,
-                                digp, Q.row0)
+                runner.prologue(margin, g, h, label, None, int(tree_index), False, 4, None, ws.totals, digp,
+                                Q.row0, pre_hist, st.arena_init_dev)
             else:
-                runner.prologue(None, g, h, label, weight, int(tree_index), bool(bootstrap), 1, None, ws.totals, digp,
-                                Q.row0)
+                # arena image first: the quantisation adds the root totals into it
+                st.arena.copy_(st.arena_init, non_blocking=True)
+                if np_ == 4:
+                    C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
+                                     ws.maxabs, Q.row0)
+                    runner.prologue(None, g, h, label, weight, int(tree_index), bool(bootstrap), 4, ws.maxabs,
+                                    ws.totals, digp, Q.row0, pre_hist, None)
+                else:
+                    runner.prologue(None, g, h, label, weight, int(tree_index), bool(bootstrap), 1, None, ws.totals,
+                                    digp, Q.row0, pre_hist, None)
     else:
         if margin is not None and g is None:
             g, h = ws.gh()
@@ -1277,12 +1288,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         tot = coll.sum(ws.totals) if coll is not None else ws.totals
         st.stats[0].copy_(tot)
         st.totals[0][:1].copy_(tot[None])
-    TB = Q.TB
     n_open, n_build = 1, 1
     prev_hist = prev_row_of = None
-    # the next level's zeroed histograms (at most 2 open nodes per open node) are queued before
-    # the host waits for its counts, so the fill runs while the host sizes that level
-    pre_hist = None
     ev = None
     # RF under data parallelism: each level reduce-scatters only its sampled features' bins; level
     # d + 1's sample and layout are computed right after level d's plan, so their shard sizes reach
@@ -1310,6 +1317,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         LEVEL_STATS["built_nodes"] += n_build
         LEVEL_STATS["hist_bytes"] += n_build * TB * 16          # (g, h) int64 partials of the built nodes
         open_d, totals_d = st.open[cur][:n_open], st.totals[cur][:n_open]
+        if d == 0 and native_prologue:
+            totals_d = st.stats[:1]             # (the prologue added the root totals there)
         n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
         # RF: exact k-of-F feature sample per open node and the level's union mask (device)
         feat_thr = feat_mask = None
@@ -1370,7 +1379,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 csc_slot8, csc_dig = (None, ws.rowdig_masked) if single else (slot8, ws.rowdig)
                 s2n = st.s2n[:n_build]
             else:
-                s2n = st.one.new_zeros(1)
+                s2n = st.zero1
             if shards is not None:      # slot k -> partial row k
                 s2n = ws.iota(n_build)
             ct = pass_ct(np_, n_build)
