@@ -264,7 +264,8 @@ class RfLevels {
     const hipStream_t s = cur_stream(dev_);
     const int32_t nodes = (int32_t)node_ids.numel(), Fa = (int32_t)nbins.numel();
     if (!find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, feat_thr, tree, out, row_of, wide, s)) return;
-    fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), nodes, Fa, f0, p<int64_t>(out), s);
+    fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), nodes, Fa, f0, p<int64_t>(out), s,
+                           &last_split_);
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 
@@ -319,7 +320,17 @@ class RfLevels {
       a.n_wide = (int32_t)wide->numel();
     }
     a.row_of = p<int32_t>(row_of);
+    const int64_t np_ = fdx::split_partials(nodes, Fa);
+    if (np_ > 0) {
+      if (!part_gain_.defined() || part_gain_.numel() < np_) {
+        part_gain_ = at::empty({np_}, out.options().dtype(at::kDouble));
+        part_f_ = at::empty({np_}, out.options().dtype(at::kInt));
+      }
+      a.part_gain = p<double>(part_gain_);
+      a.part_f = p<int32_t>(part_f_);
+    }
     fdx::launch_split(a, s);
+    last_split_ = a;
     return true;
   }
 
@@ -415,7 +426,8 @@ class RfLevels {
     const bool zc = counts_zero_copy(a, d, sample_next, sel_lists);
     if (any)
       fdx::launch_split_best_plan(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), (int32_t)n_open, Fa, 0,
-                                  p<int64_t>(out), a, reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 2, s);
+                                  p<int64_t>(out), a, reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 2, s,
+                                  &last_split_);
     else                                   // (no features: out holds "no candidate" tuples)
       fdx::launch_level_plan(a, s);
     after_plan(d, n_open, next_open, tree, sample_next, thr, mask, c10::nullopt, c10::nullopt, c10::nullopt,
@@ -555,7 +567,8 @@ class RfLevels {
   Tensor csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, row_node_, kexp_;
   optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_;
   std::map<std::string, Tensor> st_;
-  Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_, ticket_, parts_, maxv_;
+  Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_, ticket_, parts_, maxv_, part_gain_, part_f_;
+  fdx::SplitArgs last_split_{};           // the last search (its partials feed the best-split pass)
   optional<Tensor> arena_;
   int32_t* counts_host_dev_ = nullptr;
   int parity_ = 0;

@@ -83,8 +83,13 @@ void launch_rf_sample(const RfSampleArgs& a, hipStream_t s);
 void rf_sample_cpu(const RfSampleArgs& a);
 struct RfCompactArgs;
 void launch_rf_compact(const RfCompactArgs& a, hipStream_t s);
+// partials: the SplitArgs of the split search whose per-workgroup partials (part_gain) replace
+// the full per-feature scan (nullptr / no part_gain: the full scan)
 void launch_split_best_plan(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
-                            int64_t f0, int64_t* out, const LevelPlanArgs& p, unsigned int* ticket, hipStream_t s);
+                            int64_t f0, int64_t* out, const LevelPlanArgs& p, unsigned int* ticket, hipStream_t s,
+                            const SplitArgs* partials = nullptr);
+// entries of SplitArgs part_gain / part_f for a search of nodes x Fa (0: Fa < 256, no partials)
+int64_t split_partials(int32_t nodes, int32_t Fa);
 struct PrologueInit;
 void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, double* maxv,
                      const PrologueInit& pi, hipStream_t s);
@@ -103,7 +108,7 @@ void launch_level_rows(const LevelRowsArgs& a, hipStream_t s);
 void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
                            int32_t max_splits, int32_t wps, hipStream_t s);
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
-                       int64_t f0, int64_t* out, hipStream_t s);
+                       int64_t f0, int64_t* out, hipStream_t s, const SplitArgs* partials = nullptr);
 void launch_hist(const HistArgs& a, int bt, int ct, int np, hipStream_t s);
 void launch_hist_select(const HistArgs& a, hipStream_t s);
 struct RgBuildArgs;

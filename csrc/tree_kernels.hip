@@ -131,6 +131,8 @@ __device__ void reduce_parts_block(const unsigned long long* part, int nparts, u
   if (threadIdx.x == 0) { out[0] = s[0][0]; out[1] = s[1][0]; }
 }
 
+constexpr int kPrologueU = 4;           // rows per thread per step of the prologue passes
+
 // zero [n] int64 (16-byte stores where aligned) and copy [m] 8-byte words, grid-stride
 __device__ __forceinline__ void prologue_fill(int64_t* zero, int64_t n, const uint64_t* src, uint64_t* dst, int64_t m) {
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
@@ -148,15 +150,32 @@ __device__ __forceinline__ void prologue_fill(int64_t* zero, int64_t n, const ui
 // the previous round cleared this parity's slot), plus the tree-start work of PrologueInit.
 __global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, const float* label, float* g, float* h,
                                                        int64_t N, unsigned long long* maxv, PrologueInit pi) {
+  // kPrologueU rows per thread per step, every load issued before the first store: the grid is
+  // kept small (one 64-bit atomic per workgroup and statistic), so each wave needs several loads
+  // in flight (a row at a time left the pass at ~19 us for 1M rows, latency bound)
   double m0 = 0.0, m1 = 0.0;
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256) {
-    const double p = 1.0 / (1.0 + exp(-margin[r]));
-    const float gv = (float)(p - (double)label[r]);
-    const float hv = (float)fmax(p * (1.0 - p), 1e-16);
-    g[r] = gv;
-    h[r] = hv;
-    m0 = fmax(m0, fabs((double)gv));
-    m1 = fmax(m1, fabs((double)hv));
+  const int64_t step = (int64_t)gridDim.x * 256 * kPrologueU;
+  for (int64_t r0 = (int64_t)blockIdx.x * 256 * kPrologueU + threadIdx.x; r0 < N; r0 += step) {
+    double mg[kPrologueU];
+    float lb[kPrologueU];
+#pragma unroll
+    for (int u = 0; u < kPrologueU; ++u) {
+      const int64_t r = r0 + 256 * u;
+      mg[u] = r < N ? margin[r] : 0.0;
+      lb[u] = r < N ? label[r] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kPrologueU; ++u) {
+      const int64_t r = r0 + 256 * u;
+      if (r >= N) break;
+      const double p = 1.0 / (1.0 + exp(-mg[u]));
+      const float gv = (float)(p - (double)lb[u]);
+      const float hv = (float)fmax(p * (1.0 - p), 1e-16);
+      g[r] = gv;
+      h[r] = hv;
+      m0 = fmax(m0, fabs((double)gv));
+      m1 = fmax(m1, fabs((double)hv));
+    }
   }
   prologue_fill(pi.zero, pi.zero_n, pi.init_src, pi.init_dst, pi.init_n);
   if (blockIdx.x == 0 && threadIdx.x == 0 && pi.max_clear) { pi.max_clear[0] = 0ull; pi.max_clear[1] = 0ull; }
@@ -181,21 +200,34 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
   const int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) { a.kexp_out[0] = k0; a.kexp_out[1] = k1; }
   int64_t t0 = 0, t1 = 0;
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
-    double v0, v1;
-    row_stats(a, r, &v0, &v1);
-    const int64_t q0 = quantize_value(v0, k0), q1 = quantize_value(v1, k1);
-    t0 += q0;
-    t1 += q1;
-    uint2 d;
-    d.x = a.np == 1 ? digits1(q0) : digits4(q0);
-    d.y = a.np == 1 ? digits1(q1) : digits4(q1);
-    reinterpret_cast<uint2*>(a.rowdig)[r] = d;
-    if (a.row_node) a.row_node[r] = 0;
-    if (a.digp) {
-      for (int p = 0; p < a.np; ++p) {
-        a.digp[(int64_t)p * a.n_pad + r] = (uint8_t)(d.x >> (8 * p));
-        a.digp[(int64_t)(a.np + p) * a.n_pad + r] = (uint8_t)(d.y >> (8 * p));
+  // kPrologueU rows per thread per step, the row statistics loaded before any store (see
+  // grad_max_kernel)
+  const int64_t step = (int64_t)gridDim.x * 256 * kPrologueU;
+  for (int64_t r0 = (int64_t)blockIdx.x * 256 * kPrologueU + threadIdx.x; r0 < a.N; r0 += step) {
+    double sv0[kPrologueU], sv1[kPrologueU];
+#pragma unroll
+    for (int u = 0; u < kPrologueU; ++u) {
+      sv0[u] = sv1[u] = 0.0;
+      if (r0 + 256 * u < a.N) row_stats(a, r0 + 256 * u, &sv0[u], &sv1[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kPrologueU; ++u) {
+      const int64_t r = r0 + 256 * u;
+      if (r >= a.N) break;
+      const double v0 = sv0[u], v1 = sv1[u];
+      const int64_t q0 = quantize_value(v0, k0), q1 = quantize_value(v1, k1);
+      t0 += q0;
+      t1 += q1;
+      uint2 d;
+      d.x = a.np == 1 ? digits1(q0) : digits4(q0);
+      d.y = a.np == 1 ? digits1(q1) : digits4(q1);
+      reinterpret_cast<uint2*>(a.rowdig)[r] = d;
+      if (a.row_node) a.row_node[r] = 0;
+      if (a.digp) {
+        for (int p = 0; p < a.np; ++p) {
+          a.digp[(int64_t)p * a.n_pad + r] = (uint8_t)(d.x >> (8 * p));
+          a.digp[(int64_t)(a.np + p) * a.n_pad + r] = (uint8_t)(d.y >> (8 * p));
+        }
       }
     }
   }
@@ -860,10 +892,12 @@ __global__ __launch_bounds__(256) void hist_subtract_kernel(const int64_t* paren
 }
 
 // ------------------------------------------------------------------ split search
-__device__ __forceinline__ void split_narrow_at(const SplitArgs& a, int64_t t) {
-  if (t >= (int64_t)a.num_nodes * a.Fa) return;
+// Returns the feature's gain; -inf with *fo = INT32_MAX when t holds no narrow feature.
+__device__ __forceinline__ double split_narrow_at(const SplitArgs& a, int64_t t, int* fo) {
+  *fo = INT32_MAX;
+  if (t >= (int64_t)a.num_nodes * a.Fa) return -1.0 / 0.0;
   const int n = (int)(t / a.Fa), f = (int)(t % a.Fa);
-  if (a.wide != nullptr && a.nbins[f] > kSplitWide) return;     // split_wide_kernel's
+  if (a.wide != nullptr && a.nbins[f] > kSplitWide) return -1.0 / 0.0;     // split_wide_kernel's
   double gain = -1.0 / 0.0;
   int bin = -1;
   int64_t l0 = 0, l1 = 0;
@@ -879,10 +913,53 @@ __device__ __forceinline__ void split_narrow_at(const SplitArgs& a, int64_t t) {
   a.out_bin[t] = bin;
   a.out_left[2 * t] = l0;
   a.out_left[2 * t + 1] = l1;
+  *fo = f;
+  return gain;
+}
+
+// (gain, feature) order of the best split: the larger gain, ties to the lower feature; a NaN
+// anywhere is sticky (split_best_node makes the node's gain NaN)
+__device__ __forceinline__ void best_merge(double& g, int& f, double og, int of) {
+  if (g != g || og != og) { g = __longlong_as_double(0x7ff8000000000000ll); return; }
+  if (og > g || (og == g && of < f)) { g = og; f = of; }
+}
+
+// This workgroup's partials (SplitArgs part_gain / part_f): segment 0 = the node of its first
+// thread, segment 1 = any later node (Fa >= 256: at most one)
+__device__ __forceinline__ void split_block_partial(const SplitArgs& a, int64_t t, double gain, int f) {
+  const int64_t tb = (int64_t)blockIdx.x * 256;
+  const int nf = (int)(tb / a.Fa);
+  const bool in = t < (int64_t)a.num_nodes * a.Fa;
+  const int seg = in && (int)(t / a.Fa) != nf ? 1 : 0;
+  double g0 = -1.0 / 0.0, g1 = -1.0 / 0.0;
+  int f0 = INT32_MAX, f1 = INT32_MAX;
+  if (in && seg == 0) { g0 = gain; f0 = f; }
+  if (in && seg == 1) { g1 = gain; f1 = f; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    best_merge(g0, f0, __shfl_xor(g0, o, kWave), __shfl_xor(f0, o, kWave));
+    best_merge(g1, f1, __shfl_xor(g1, o, kWave), __shfl_xor(f1, o, kWave));
+  }
+  __shared__ double s_g[2][4];
+  __shared__ int s_f[2][4];
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) { s_g[0][w] = g0; s_f[0][w] = f0; s_g[1][w] = g1; s_f[1][w] = f1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int k = threadIdx.x;
+    double g = s_g[k][0];
+    int ff = s_f[k][0];
+    for (int i = 1; i < 4; ++i) best_merge(g, ff, s_g[k][i], s_f[k][i]);
+    a.part_gain[2 * blockIdx.x + k] = g;
+    a.part_f[2 * blockIdx.x + k] = ff;
+  }
 }
 
 __global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
-  split_narrow_at(a, (int64_t)blockIdx.x * 256 + threadIdx.x);
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int f;
+  const double g = split_narrow_at(a, t, &f);
+  if (a.part_gain) split_block_partial(a, t, g, f);
 }
 
 // Wide features (> kSplitWide bins: the hot words' count bins): a wave per (node, feature), lane
@@ -974,7 +1051,10 @@ __global__ __launch_bounds__(256) void split_wide_kernel(SplitArgs a) {
 // features (a thread per (node, feature)), the rest the wide ones (a wave per (node, feature))
 __global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb_narrow) {
   if (blockIdx.x < nb_narrow) {
-    split_narrow_at(a, (int64_t)blockIdx.x * 256 + threadIdx.x);
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    int f;
+    const double g = split_narrow_at(a, t, &f);
+    if (a.part_gain) split_block_partial(a, t, g, f);     // (workgroup-uniform)
   } else {
     split_wide_at(a, ((int64_t)(blockIdx.x - nb_narrow) * 256 + threadIdx.x) >> 6, threadIdx.x & 63);
   }
@@ -986,13 +1066,41 @@ __global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb
 // One 1024-thread block per node, 4 independent loads in flight per thread (the 256-thread
 // version was a latency-bound ~40 us per level at ~10^5 features).
 constexpr int kBestThreads = 1024;
+// With the narrow search's per-workgroup partials (bp.part_gain): their ~Fa / 256 values per node
+// and the wide features' gains instead of all Fa gains -- the same maximum and tie rule, one
+// round of loads per thread (the full scan was ~17 us per level whatever the node count).
+struct BestPartials {
+  const double* part_gain;
+  const int32_t* part_f;
+  const int32_t* wide;
+  int32_t n_wide;
+};
+
 __device__ __forceinline__ void split_best_node(const double* gain, const int32_t* bin, const int64_t* left,
-                                                int32_t Fa, int64_t f0, int64_t* out, int n) {
+                                                int32_t Fa, int64_t f0, int64_t* out, int n,
+                                                const BestPartials& bp) {
   const double* g = gain + (int64_t)n * Fa;
   double best = -1.0 / 0.0;
   int bf = Fa;
   bool nan = false;
-  for (int f = threadIdx.x; f < Fa; f += 4 * kBestThreads) {
+  if (bp.part_gain) {
+    const int64_t t0 = (int64_t)n * Fa;
+    const int64_t b0 = t0 / 256, b1 = (t0 + Fa - 1) / 256;
+    for (int64_t b = b0 + threadIdx.x; b <= b1; b += kBestThreads) {
+      const int k = (b * 256) / Fa == n ? 0 : 1;
+      const double v = bp.part_gain[2 * b + k];
+      const int fu = bp.part_f[2 * b + k];
+      if (v != v) nan = true;
+      else if (fu < Fa && (v > best || (v == best && fu < bf))) { best = v; bf = fu; }
+    }
+    for (int j = threadIdx.x; j < bp.n_wide; j += kBestThreads) {
+      const int fu = bp.wide[j];
+      const double v = g[fu];
+      if (v != v) nan = true;
+      else if (v > best || (v == best && fu < bf)) { best = v; bf = fu; }
+    }
+  }
+  for (int f = threadIdx.x; f < Fa && !bp.part_gain; f += 4 * kBestThreads) {
     double v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1043,8 +1151,8 @@ __device__ __forceinline__ void split_best_node(const double* gain, const int32_
 
 __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* gain, const int32_t* bin,
                                                                   const int64_t* left, int32_t Fa, int64_t f0,
-                                                                  int64_t* out) {
-  split_best_node(gain, bin, left, Fa, f0, out, blockIdx.x);
+                                                                  int64_t* out, BestPartials bp) {
+  split_best_node(gain, bin, left, Fa, f0, out, blockIdx.x, bp);
 }
 
 // ------------------------------------------------------------------ partition
@@ -1336,8 +1444,8 @@ __global__ void level_plan_kernel(LevelPlanArgs a) {
 __global__ __launch_bounds__(kBestThreads) void split_best_plan_kernel(const double* gain, const int32_t* bin,
                                                                        const int64_t* left, int32_t Fa, int64_t f0,
                                                                        int64_t* out, LevelPlanArgs p,
-                                                                       unsigned int* ticket) {
-  split_best_node(gain, bin, left, Fa, f0, out, blockIdx.x);
+                                                                       unsigned int* ticket, BestPartials bp) {
+  split_best_node(gain, bin, left, Fa, f0, out, blockIdx.x, bp);
   if (!last_workgroup(ticket)) return;
   level_plan_reset(p, (int32_t)threadIdx.x, (int32_t)blockDim.x);
   __syncthreads();
@@ -1532,20 +1640,32 @@ void launch_split(const SplitArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(split_all_kernel, dim3(nb + (unsigned)((waves + 3) / 4)), dim3(256), 0, s, a, nb);
 }
 
+static BestPartials best_partials(const SplitArgs* sa) {
+  BestPartials bp{};
+  if (sa && sa->part_gain) bp = BestPartials{sa->part_gain, sa->part_f, sa->wide, sa->wide ? sa->n_wide : 0};
+  return bp;
+}
+
 void launch_split_best_plan(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
-                            int64_t f0, int64_t* out, const LevelPlanArgs& p, unsigned int* ticket, hipStream_t s) {
+                            int64_t f0, int64_t* out, const LevelPlanArgs& p, unsigned int* ticket, hipStream_t s,
+                            const SplitArgs* partials) {
   if (nodes <= 0 || Fa <= 0) {                  // (no candidates: the caller filled out)
     hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(64), 0, s, p);
     return;
   }
   hipLaunchKernelGGL(split_best_plan_kernel, dim3(nodes), dim3(kBestThreads), 0, s, gain, bin, left, Fa, f0, out, p,
-                     ticket);
+                     ticket, best_partials(partials));
 }
 
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
-                       int64_t f0, int64_t* out, hipStream_t s) {
+                       int64_t f0, int64_t* out, hipStream_t s, const SplitArgs* partials) {
   if (nodes > 0 && Fa > 0)
-    hipLaunchKernelGGL(split_best_kernel, dim3(nodes), dim3(kBestThreads), 0, s, gain, bin, left, Fa, f0, out);
+    hipLaunchKernelGGL(split_best_kernel, dim3(nodes), dim3(kBestThreads), 0, s, gain, bin, left, Fa, f0, out,
+                       best_partials(partials));
+}
+
+int64_t split_partials(int32_t nodes, int32_t Fa) {
+  return Fa >= 256 ? 2 * (((int64_t)nodes * Fa + 255) / 256) : 0;
 }
 
 void launch_partition(const PartitionArgs& a, hipStream_t s) {
