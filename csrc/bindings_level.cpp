@@ -112,7 +112,9 @@ class RfLevels {
     const int64_t cap = st_["s2n"].numel();
     scratch_ = at::empty({fdx::rf_scratch_bytes(2 * cap)}, row_node_.options().dtype(at::kByte));
     ticket_ = at::zeros({4}, row_node_.options());
-    maxv_ = at::zeros({4}, row_node_.options().dtype(at::kLong));
+    // per parity: kRootSlots slots of the max |g|, |h| bit patterns / of the root's sums
+    maxv_ = at::zeros({2 * fdx::kRootSlots * fdx::kRootStride}, row_node_.options().dtype(at::kLong));
+    root_parts_ = at::zeros({2 * fdx::kRootSlots * fdx::kRootStride}, row_node_.options().dtype(at::kLong));
     parts_ = at::empty({2 * (int64_t)fdx::quant_blocks(row_node_.numel())}, row_node_.options().dtype(at::kLong));
   }
 
@@ -136,6 +138,7 @@ class RfLevels {
       FDX_CHECK(zero->scalar_type() == at::kLong && zero->is_contiguous() &&
                     reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0, "zero: contiguous int64, 16-byte aligned");
     const double* maxv = maxabs ? p<double>(*maxabs) : nullptr;
+    const unsigned long long* max_parts = nullptr;
     if (margin) {
       FDX_CHECK(g && h && label && !weight && mode_ == 0, "the fused gradient prologue: unweighted GBDT");
       FDX_CHECK(arena_init && arena_ && arena_init->numel() == arena_->numel() && arena_->numel() % 8 == 0,
@@ -148,11 +151,13 @@ class RfLevels {
         pi.zero = p<int64_t>(*zero);
         pi.zero_n = zero->numel();
       }
+      constexpr int64_t kSet = fdx::kRootSlots * fdx::kRootStride;
       unsigned long long* mv = reinterpret_cast<unsigned long long*>(p<int64_t>(maxv_));
-      pi.max_clear = mv + 2 * (1 - parity_);
+      pi.max_clear = mv + kSet * (1 - parity_);
       fdx::launch_grad_max(p<double>(*margin), p<float>(*label), p<float>(*g), p<float>(*h), N,
-                           reinterpret_cast<double*>(mv + 2 * parity_), pi, s);
-      maxv = reinterpret_cast<const double*>(mv + 2 * parity_);
+                           reinterpret_cast<double*>(mv + kSet * parity_), pi, s);
+      max_parts = mv + kSet * parity_;
+      maxv = nullptr;
       parity_ ^= 1;
     }
     fdx::QuantArgs a{};
@@ -174,8 +179,13 @@ class RfLevels {
       a.digp = p<uint8_t>(*digp);
       a.n_pad = digp->size(1);
     }
+    constexpr int64_t kSet = fdx::kRootSlots * fdx::kRootStride;
     a.atomic_root = 1;
-    a.root_stats = p<int64_t>(st_["arena_stats"]);
+    a.root_parts = p<int64_t>(root_parts_) + kSet * tparity_;
+    a.root_parts_clear = p<int64_t>(root_parts_) + kSet * (1 - tparity_);
+    a.max_parts = max_parts;
+    root_pending_ = a.root_parts;          // (level 0's split search and plan sum the slots)
+    tparity_ ^= 1;
     a.root_open = p<int32_t>(st_["open0"]);
     a.kexp_copy = p<int32_t>(st_["kexp_slot"]);
     a.row_node = p<int32_t>(row_node_);
@@ -320,6 +330,7 @@ class RfLevels {
       a.n_wide = (int32_t)wide->numel();
     }
     a.row_of = p<int32_t>(row_of);
+    a.root_parts = find_root_;
     const int64_t np_ = fdx::split_partials(nodes, Fa);
     if (np_ > 0) {
       if (!part_gain_.defined() || part_gain_.numel() < np_) {
@@ -421,8 +432,13 @@ class RfLevels {
     const hipStream_t s = cur_stream(dev_);
     const int32_t Fa = (int32_t)nbins_.numel();
     FDX_CHECK(open.numel() == n_open, "open [n_open]");
+    const int64_t* root = d == 0 ? root_pending_ : nullptr;
+    root_pending_ = nullptr;
+    find_root_ = root;
     const bool any = find(hist, totals, boff, nbins_, zbin_, fid_orig_, open, feat_thr, tree, out, c10::nullopt, wide, s);
+    find_root_ = nullptr;
     fdx::LevelPlanArgs a = plan_args(d, n_open, out, open, n_open_ptr, next_open, next_totals);
+    a.root_parts = root;
     const bool zc = counts_zero_copy(a, d, sample_next, sel_lists);
     if (any)
       fdx::launch_split_best_plan(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), (int32_t)n_open, Fa, 0,
@@ -571,7 +587,10 @@ class RfLevels {
   fdx::SplitArgs last_split_{};           // the last search (its partials feed the best-split pass)
   optional<Tensor> arena_;
   int32_t* counts_host_dev_ = nullptr;
-  int parity_ = 0;
+  int parity_ = 0, tparity_ = 0;
+  Tensor root_parts_;
+  const int64_t* root_pending_ = nullptr;   // the last prologue's root slots, until level 0's split
+  const int64_t* find_root_ = nullptr;
   bool build_all_ = true;
   int mode_ = 1, max_depth_ = 5, wps_ = 256;
   double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;

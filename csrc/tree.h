@@ -85,14 +85,33 @@ struct QuantArgs {
   int32_t* root_open;
   int32_t* kexp_copy;
   int32_t* row_node;
-  // ... or with no ticket (atomic_root): every workgroup adds its partial sums straight into
-  // root_stats (zero beforehand: the arena image) and workgroup 0 writes open[0] and the
-  // exponents -- no grid-wide completion test, whose per-workgroup device-scope release was the
-  // cost of the ticketed form; the level-0 split reads the totals from stats[0]
+  // ... or with no ticket (atomic_root): every workgroup adds its partial sums into one of
+  // kRootSlots slots of root_parts (slot = workgroup % kRootSlots, a 128-byte line each; the
+  // same-address form serialised at ~11 ns per atomic, bench/probes/atomic_contention.hip) and
+  // workgroup 0 writes open[0], the exponents and zeroes root_parts_clear (the next tree's slots).
+  // The level-0 split search and plan sum the slots themselves (SplitArgs / LevelPlanArgs
+  // root_parts) -- no grid-wide completion test and no reduction launch.
   int32_t atomic_root;
+  int64_t* root_parts;        // [kRootSlots][kRootStride] (words 0, 1: the two sums)
+  int64_t* root_parts_clear;
+  // max |g|, |h| as kRootSlots slots of bit patterns (grad_max_kernel); nullptr: maxv
+  const unsigned long long* max_parts;
   int64_t* zero;              // optional: [zero_n] int64 zeroed on the way (the root histogram)
   int64_t zero_n;
 };
+constexpr int kRootSlots = 32;
+constexpr int kRootStride = 16;           // int64 words per slot (one 128-byte line)
+
+// the root's exact sums from the kRootSlots slots (a wave: lanes 0..31 one slot each)
+FDX_HD void root_sums(const int64_t* parts, int64_t* t0, int64_t* t1) {
+  int64_t a = 0, b = 0;
+  for (int k = 0; k < kRootSlots; ++k) {
+    a += parts[kRootStride * k];
+    b += parts[kRootStride * k + 1];
+  }
+  *t0 = a;
+  *t1 = b;
+}
 
 // Tree-start work folded into the first launch of a GBDT round (grad_max_kernel): the node-table
 // arena image copied in (init_n 8-byte words), the root histogram zeroed, and the other parity's
@@ -103,7 +122,7 @@ struct PrologueInit {
   int64_t init_n;
   int64_t* zero;
   int64_t zero_n;
-  unsigned long long* max_clear;   // [2]
+  unsigned long long* max_clear;   // [kRootSlots][kRootStride]: the next round's max slots
 };
 
 struct SlotArgs {
@@ -426,6 +445,8 @@ struct SplitArgs {
   // segment). The best-split pass then reads ~Fa / 256 partials per node instead of Fa gains.
   double* part_gain;
   int32_t* part_f;
+  // optional: the root's totals as QuantArgs root_parts slots (level 0 of the fused prologue)
+  const int64_t* root_parts;
 };
 constexpr int32_t kSplitWide = 16;
 
@@ -687,6 +708,8 @@ struct LevelPlanArgs {
   int32_t* cs_left_default;
   int32_t* counts;                // [4] out: n_cs, n_next_open, n_build, n_nodes
   int32_t* counts_host;           // optional host-mapped copy of the 4 counts (pinned; no D2H copy)
+  const int64_t* root_parts;      // optional (depth 0): the root's totals as QuantArgs root_parts
+                                  //   slots, summed here into stats[0]
   // level d + 1 (out; capacity 2L open, L built)
   int32_t* next_open;             // [2L] (-1 pad)
   int64_t* next_totals;           // [2L][2]
@@ -714,6 +737,7 @@ FDX_HD void level_plan_reset(const LevelPlanArgs& a, int32_t t, int32_t nthreads
 
 FDX_HD void level_plan(const LevelPlanArgs& a, bool reset = true) {
   if (reset) level_plan_reset(a, 0, 1);
+  if (a.root_parts) root_sums(a.root_parts, &a.stats[0], &a.stats[1]);
   const double thr = a.min_gain > 1e-6 ? a.min_gain : 1e-6;
   const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
   int32_t nn = *a.n_nodes, n_cs = 0, n_next = 0;

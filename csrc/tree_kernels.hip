@@ -178,7 +178,10 @@ __global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, con
     }
   }
   prologue_fill(pi.zero, pi.zero_n, pi.init_src, pi.init_dst, pi.init_n);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && pi.max_clear) { pi.max_clear[0] = 0ull; pi.max_clear[1] = 0ull; }
+  if (blockIdx.x == 0 && threadIdx.x < kRootSlots && pi.max_clear) {
+    pi.max_clear[kRootStride * threadIdx.x] = 0ull;
+    pi.max_clear[kRootStride * threadIdx.x + 1] = 0ull;
+  }
   for (int o = 32; o > 0; o >>= 1) {
     m0 = fmax(m0, __shfl_xor(m0, o, kWave));
     m1 = fmax(m1, __shfl_xor(m1, o, kWave));
@@ -190,14 +193,28 @@ __global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, con
   if (threadIdx.x == 0) {
     m0 = fmax(fmax(s_m[0][0], s_m[0][1]), fmax(s_m[0][2], s_m[0][3]));
     m1 = fmax(fmax(s_m[1][0], s_m[1][1]), fmax(s_m[1][2], s_m[1][3]));
-    atomicMax(maxv, (unsigned long long)__double_as_longlong(m0));
-    atomicMax(maxv + 1, (unsigned long long)__double_as_longlong(m1));
+    unsigned long long* slot = maxv + kRootStride * (blockIdx.x % kRootSlots);
+    atomicMax(slot, (unsigned long long)__double_as_longlong(m0));
+    atomicMax(slot + 1, (unsigned long long)__double_as_longlong(m1));
   }
 }
 
 // rowdig[r] = digits of (q0, q1); totals += (sum q0, sum q1) (int64 atomics, exact)
 __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* maxv, unsigned long long* part) {
-  const int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
+  int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
+  if (a.max_parts) {                       // the max over grad_max_kernel's slots (every wave)
+    const int lane = threadIdx.x & 63;
+    unsigned long long b0 = lane < kRootSlots ? a.max_parts[kRootStride * lane] : 0ull;
+    unsigned long long b1 = lane < kRootSlots ? a.max_parts[kRootStride * lane + 1] : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long c0 = __shfl_xor(b0, o, kWave), c1 = __shfl_xor(b1, o, kWave);
+      b0 = c0 > b0 ? c0 : b0;
+      b1 = c1 > b1 ? c1 : b1;
+    }
+    k0 = quant_exponent(__longlong_as_double((long long)b0));
+    k1 = quant_exponent(__longlong_as_double((long long)b1));
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) { a.kexp_out[0] = k0; a.kexp_out[1] = k1; }
   int64_t t0 = 0, t1 = 0;
   // kPrologueU rows per thread per step, the row statistics loaded before any store (see
@@ -244,8 +261,9 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
     t0 = s_t[0][0] + s_t[0][1] + s_t[0][2] + s_t[0][3];
     t1 = s_t[1][0] + s_t[1][1] + s_t[1][2] + s_t[1][3];
     if (a.atomic_root) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.root_stats), (unsigned long long)t0);
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.root_stats) + 1, (unsigned long long)t1);
+      unsigned long long* slot = reinterpret_cast<unsigned long long*>(a.root_parts) + kRootStride * (blockIdx.x % kRootSlots);
+      atomicAdd(slot, (unsigned long long)t0);
+      atomicAdd(slot + 1, (unsigned long long)t1);
       if (blockIdx.x == 0) {
         if (a.root_open) a.root_open[0] = 0;
         if (a.kexp_copy) { a.kexp_copy[0] = k0; a.kexp_copy[1] = k1; }
@@ -254,6 +272,10 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
       part[2 * blockIdx.x] = (unsigned long long)t0;
       part[2 * blockIdx.x + 1] = (unsigned long long)t1;
     }
+  }
+  if (a.atomic_root && blockIdx.x == 0 && threadIdx.x < kRootSlots) {
+    a.root_parts_clear[kRootStride * threadIdx.x] = 0;
+    a.root_parts_clear[kRootStride * threadIdx.x + 1] = 0;
   }
   if (a.atomic_root || a.ticket == nullptr || !last_workgroup(a.ticket)) return;
   // the last workgroup: the exact totals, then the tree's root state
@@ -892,6 +914,16 @@ __global__ __launch_bounds__(256) void hist_subtract_kernel(const int64_t* paren
 }
 
 // ------------------------------------------------------------------ split search
+// node n's exact sums (level 0 of the fused prologue: from the quantisation's slots)
+__device__ __forceinline__ void split_totals(const SplitArgs& a, int n, int64_t* t0, int64_t* t1) {
+  if (a.root_parts) {
+    root_sums(a.root_parts, t0, t1);
+  } else {
+    *t0 = a.totals[2 * n];
+    *t1 = a.totals[2 * n + 1];
+  }
+}
+
 // Returns the feature's gain; -inf with *fo = INT32_MAX when t holds no narrow feature.
 __device__ __forceinline__ double split_narrow_at(const SplitArgs& a, int64_t t, int* fo) {
   *fo = INT32_MAX;
@@ -906,7 +938,9 @@ __device__ __forceinline__ double split_narrow_at(const SplitArgs& a, int64_t t,
     use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
   if (use) {
     const int64_t* hb = a.hist + (split_row(a, n) * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
-    gain = best_split_scan(hb, a.nbins[f], a.zbin[f], a.totals[2 * n], a.totals[2 * n + 1], ldexp(1.0, -a.kexp[0]),
+    int64_t T0, T1;
+    split_totals(a, n, &T0, &T1);
+    gain = best_split_scan(hb, a.nbins[f], a.zbin[f], T0, T1, ldexp(1.0, -a.kexp[0]),
                            ldexp(1.0, -a.kexp[1]), a.mode, a.lambda_, a.min_child_weight, &bin, &l0, &l1);
   }
   a.out_gain[t] = gain;
@@ -996,7 +1030,8 @@ __device__ __forceinline__ void split_wide_at(const SplitArgs& a, int64_t w, int
   if (use) {
     const int64_t* hb = a.hist + (split_row(a, n) * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
     const int nb = a.nbins[f], zb = a.zbin[f];
-    const int64_t T0 = a.totals[2 * n], T1 = a.totals[2 * n + 1];
+    int64_t T0, T1;
+    split_totals(a, n, &T0, &T1);
     const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
     int64_t a0 = 0, a1 = 0;
     for (int b0 = 0; b0 < nb; b0 += 64) {
@@ -1278,6 +1313,17 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
   const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
   int32_t nn = *a.n_nodes, n_cs = 0, n_next = 0, nb = 0;
   const int32_t no = *a.n_open;
+  int64_t R0 = 0, R1 = 0;                  // (depth 0 of the fused prologue) the root's sums
+  if (a.root_parts) {
+    R0 = lane < kRootSlots ? a.root_parts[kRootStride * lane] : 0;
+    R1 = lane < kRootSlots ? a.root_parts[kRootStride * lane + 1] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      R0 += __shfl_xor(R0, o, 64);
+      R1 += __shfl_xor(R1, o, 64);
+    }
+    if (lane == 0) { a.stats[0] = R0; a.stats[1] = R1; }
+  }
   for (int32_t base = 0; base < no; base += 64) {
     const int32_t i = base + lane;
     const bool live = i < no;
@@ -1309,7 +1355,8 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
     bool dense = false;
     if (split) {
       const int64_t l0 = p[3], l1 = p[4];
-      const int64_t t0 = a.stats[2 * n], t1 = a.stats[2 * n + 1];
+      const bool root = a.root_parts && n == 0;
+      const int64_t t0 = root ? R0 : a.stats[2 * n], t1 = root ? R1 : a.stats[2 * n + 1];
       const int64_t cs[2][2] = {{l0, l1}, {t0 - l0, t1 - l1}};
       for (int k = 0; k < 2; ++k) {
         const int32_t c = li + k;

@@ -1229,8 +1229,9 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     # split + plan and partition it fuses)
     gbdt_native = NATIVE_LEVELS and dev.type == "cuda" and params.mode == 0 and shards is None and coll is None \
         and weight is None and not build_all
+    # (the runner's level 0 completes the root's sums: at least one level)
     runner = _level_runner(Q, ws, st, params, item_groups, sampled) \
-        if (NATIVE_LEVELS and dev.type == "cuda" and (sampled or gbdt_native)) else None
+        if (NATIVE_LEVELS and dev.type == "cuda" and (sampled or gbdt_native) and params.max_depth >= 1) else None
     # every step of this generator runs on the stream current now (the forest driver advances a
     # lane inside that lane's stream context)
     cur_stream = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
@@ -1318,7 +1319,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         LEVEL_STATS["hist_bytes"] += n_build * TB * 16          # (g, h) int64 partials of the built nodes
         open_d, totals_d = st.open[cur][:n_open], st.totals[cur][:n_open]
         if d == 0 and native_prologue:
-            totals_d = st.stats[:1]             # (the prologue added the root totals there)
+            totals_d = st.stats[:1]             # (unread: the runner sums the prologue's root slots)
         n_open_ptr = st.one if d == 0 else st.counts[d - 1, 1:2]
         # RF: exact k-of-F feature sample per open node and the level's union mask (device)
         feat_thr = feat_mask = None
