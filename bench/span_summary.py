@@ -1,22 +1,27 @@
-"""Summarise an ``FDX_TRACE`` span log: total / count / mean wall time per span name.
+"""Sum a FDX_TRACE span log (utils/tracing.py JSONL) by span name: calls, total and mean ms.
 
-Usage: python bench/span_summary.py trace.jsonl
+Usage: python bench/span_summary.py trace.jsonl [--depth 1]
 """
+import argparse
 import collections
 import json
-import sys
 
 
-def main(path):
-    agg = collections.defaultdict(lambda: [0, 0.0])
-    for line in open(path):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--depth", type=int, default=99, help="only spans at nesting depth <= this")
+    args = ap.parse_args()
+    tot = collections.defaultdict(lambda: [0, 0.0])
+    for line in open(args.trace):
         r = json.loads(line)
-        a = agg[r["name"]]
-        a[0] += 1
-        a[1] += r.get("dur_ms", r.get("ms", 0.0))
-    for name, (n, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
-        print(f"{t:10.1f} ms {n:7d}  {t / n:8.3f} ms/call  {name}")
+        if r.get("depth", 0) > args.depth:
+            continue
+        tot[(r.get("depth", 0), r["name"])][0] += 1
+        tot[(r.get("depth", 0), r["name"])][1] += r["dur_ms"]
+    for (d, name), (n, ms) in sorted(tot.items(), key=lambda x: (-x[1][1])):
+        print(f"{'  ' * d}{name:<28s} {n:6d} calls {ms:10.2f} ms  ({ms / n:8.3f} ms each)")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main()

@@ -80,7 +80,8 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     C = native.lib()
     coll = Collectives()
     t0 = time.perf_counter()
-    Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll)
+    with tracing.span("gbdt.prepare"):
+        Q, y, F, vc = prepare(features, labels, device, params.max_bin, coll)
     ckpt = None
     if checkpoint_dir:
         ckpt = EnsembleCheckpointer(checkpoint_dir, checkpoint_every, "gbdt", data_fingerprint(vc, y, coll),
@@ -107,7 +108,8 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     gp = GrowParams(max_depth=params.max_depth, mode=0, lambda_=params.reg_lambda, min_child=params.min_child_weight,
                     min_gain=params.gamma, seed=params.seed, eta=params.learning_rate,
                     max_delta_step=params.max_delta_step)
-    ws = Workspace(Q)
+    with tracing.span("gbdt.workspace"):
+        ws = Workspace(Q)
     trees = list(start_trees or [])
     if trees:   # resume: replay the checkpointed trees on this rank's training rows
         from ..ml.tree_model import ensemble_arrays

@@ -94,7 +94,8 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
     if subsampling_rate != 1.0:
         raise NotImplementedError("subsamplingRate != 1.0 is not supported (Poisson(1) bootstrap only)")
     coll = Collectives()
-    Q, y, F, vc = prepare(features, labels, device, max_bins, coll)
+    with tracing.span("forest.prepare"):
+        Q, y, F, vc = prepare(features, labels, device, max_bins, coll)
     ckpt = None
     if checkpoint_dir:
         shape = dict(num_trees=num_trees, max_depth=max_depth, max_bins=max_bins, min_instances=min_instances,
@@ -111,7 +112,8 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
     params = GrowParams(max_depth=max_depth, mode=2 if impurity == "entropy" else 1, min_child=float(min_instances),
                         min_gain=float(min_info_gain), feat_k=0 if k >= F else int(k),
                         seed=int(seed) & 0x7FFFFFFFFFFFFFFF)
-    ws = Workspace(Q)
+    with tracing.span("forest.workspace"):
+        ws = Workspace(Q)
     trees = ckpt.load_trees() if (ckpt is not None and resume) else []
     # PAR-05: several trees in flight, each on its own stream (models/forest_batch.py); under data
     # parallelism the lanes advance in FIFO order, so every rank issues one collective sequence
@@ -124,7 +126,8 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
         inflight = rf_lanes_that_fit(Q.n_rows, inflight, torch.cuda.mem_get_info(Q.device)[0])
     lanes = None
     if inflight > 1 and num_trees - len(trees) > 1 and device_levels_ok(params, w):
-        lanes = ForestLanes(Q, min(inflight, num_trees - len(trees)), ws)
+        with tracing.span("forest.lanes"):
+            lanes = ForestLanes(Q, min(inflight, num_trees - len(trees)), ws)
     chunk = max(ckpt.every if ckpt is not None else 64, 1)
     t = len(trees)
     while t < num_trees:
