@@ -88,7 +88,7 @@ void launch_rf_compact(const RfCompactArgs& a, hipStream_t s);
 void launch_split_best_plan(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
                             int64_t f0, int64_t* out, const LevelPlanArgs& p, unsigned int* ticket, hipStream_t s,
                             const SplitArgs* partials = nullptr);
-// entries of SplitArgs part_gain / part_f for a search of nodes x Fa (0: Fa < 256, no partials)
+// entries of SplitArgs part_gain / part_f for a search of nodes x Fa (0: Fa < 64, no partials)
 int64_t split_partials(int32_t nodes, int32_t Fa);
 struct PrologueInit;
 void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, double* maxv,

@@ -440,9 +440,9 @@ struct SplitArgs {
   // optional: histogram row of node n (data-parallel levels: the reduce-scattered built rows and
   // the subtracted siblings stay where they were written, see LevelRowsArgs); nullptr: row n
   const int32_t* row_of;
-  // optional (Fa >= 256): per 256-thread workgroup of the narrow search, the best (gain, feature)
-  // of each of the <= 2 nodes its features belong to ([2 * workgroups]; NaN gain: a NaN in the
-  // segment). The best-split pass then reads ~Fa / 256 partials per node instead of Fa gains.
+  // optional (Fa >= 64): per wave of the narrow search, the best (gain, feature) of each of the
+  // <= 2 nodes its features belong to ([2 * waves]; NaN gain: a NaN in the segment). The
+  // best-split pass then reads ~Fa / 64 partials per node instead of Fa gains.
   double* part_gain;
   int32_t* part_f;
   // optional: the root's totals as QuantArgs root_parts slots (level 0 of the fused prologue)

@@ -958,11 +958,12 @@ __device__ __forceinline__ void best_merge(double& g, int& f, double og, int of)
   if (og > g || (og == g && of < f)) { g = og; f = of; }
 }
 
-// This workgroup's partials (SplitArgs part_gain / part_f): segment 0 = the node of its first
-// thread, segment 1 = any later node (Fa >= 256: at most one)
-__device__ __forceinline__ void split_block_partial(const SplitArgs& a, int64_t t, double gain, int f) {
-  const int64_t tb = (int64_t)blockIdx.x * 256;
-  const int nf = (int)(tb / a.Fa);
+// This wave's partials (SplitArgs part_gain / part_f, indexed by global wave t / 64): segment 0
+// = the node of its first lane, segment 1 = a later node (Fa >= 64: at most one). Shuffles only:
+// no barrier, so a wave whose scans end early leaves at once.
+__device__ __forceinline__ void split_wave_partial(const SplitArgs& a, int64_t t, double gain, int f) {
+  const int64_t tw = t & ~(int64_t)(kWave - 1);
+  const int nf = (int)(tw / a.Fa);
   const bool in = t < (int64_t)a.num_nodes * a.Fa;
   const int seg = in && (int)(t / a.Fa) != nf ? 1 : 0;
   double g0 = -1.0 / 0.0, g1 = -1.0 / 0.0;
@@ -974,26 +975,17 @@ __device__ __forceinline__ void split_block_partial(const SplitArgs& a, int64_t 
     best_merge(g0, f0, __shfl_xor(g0, o, kWave), __shfl_xor(f0, o, kWave));
     best_merge(g1, f1, __shfl_xor(g1, o, kWave), __shfl_xor(f1, o, kWave));
   }
-  __shared__ double s_g[2][4];
-  __shared__ int s_f[2][4];
-  const int w = threadIdx.x / kWave;
-  if ((threadIdx.x & (kWave - 1)) == 0) { s_g[0][w] = g0; s_f[0][w] = f0; s_g[1][w] = g1; s_f[1][w] = f1; }
-  __syncthreads();
-  if (threadIdx.x < 2) {
-    const int k = threadIdx.x;
-    double g = s_g[k][0];
-    int ff = s_f[k][0];
-    for (int i = 1; i < 4; ++i) best_merge(g, ff, s_g[k][i], s_f[k][i]);
-    a.part_gain[2 * blockIdx.x + k] = g;
-    a.part_f[2 * blockIdx.x + k] = ff;
-  }
+  const int lane = (int)(t & (kWave - 1));
+  const int64_t w = tw / kWave;
+  if (lane == 0) { a.part_gain[2 * w] = g0; a.part_f[2 * w] = f0; }
+  if (lane == 1) { a.part_gain[2 * w + 1] = g1; a.part_f[2 * w + 1] = f1; }
 }
 
 __global__ __launch_bounds__(256) void split_kernel(SplitArgs a) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   int f;
   const double g = split_narrow_at(a, t, &f);
-  if (a.part_gain) split_block_partial(a, t, g, f);
+  if (a.part_gain) split_wave_partial(a, t, g, f);
 }
 
 // Wide features (> kSplitWide bins: the hot words' count bins): a wave per (node, feature), lane
@@ -1089,7 +1081,7 @@ __global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     int f;
     const double g = split_narrow_at(a, t, &f);
-    if (a.part_gain) split_block_partial(a, t, g, f);     // (workgroup-uniform)
+    if (a.part_gain) split_wave_partial(a, t, g, f);
   } else {
     split_wide_at(a, ((int64_t)(blockIdx.x - nb_narrow) * 256 + threadIdx.x) >> 6, threadIdx.x & 63);
   }
@@ -1101,7 +1093,7 @@ __global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb
 // One 1024-thread block per node, 4 independent loads in flight per thread (the 256-thread
 // version was a latency-bound ~40 us per level at ~10^5 features).
 constexpr int kBestThreads = 1024;
-// With the narrow search's per-workgroup partials (bp.part_gain): their ~Fa / 256 values per node
+// With the narrow search's per-wave partials (bp.part_gain): their ~Fa / 64 values per node
 // and the wide features' gains instead of all Fa gains -- the same maximum and tie rule, one
 // round of loads per thread (the full scan was ~17 us per level whatever the node count).
 struct BestPartials {
@@ -1120,9 +1112,9 @@ __device__ __forceinline__ void split_best_node(const double* gain, const int32_
   bool nan = false;
   if (bp.part_gain) {
     const int64_t t0 = (int64_t)n * Fa;
-    const int64_t b0 = t0 / 256, b1 = (t0 + Fa - 1) / 256;
+    const int64_t b0 = t0 / kWave, b1 = (t0 + Fa - 1) / kWave;
     for (int64_t b = b0 + threadIdx.x; b <= b1; b += kBestThreads) {
-      const int k = (b * 256) / Fa == n ? 0 : 1;
+      const int k = (b * kWave) / Fa == n ? 0 : 1;
       const double v = bp.part_gain[2 * b + k];
       const int fu = bp.part_f[2 * b + k];
       if (v != v) nan = true;
@@ -1536,6 +1528,7 @@ __global__ __launch_bounds__(256) void leaf_values_kernel(const int64_t* stats, 
 
 constexpr int kQuantBlocks = 2048;      // workgroup cap of the quantisation passes (partials)
 constexpr int kTicketBlocks = 512;      // ... of the single-launch (last-workgroup) passes
+constexpr int kSlotBlocks = 2048;       // ... of the spread-slot passes (64 atomics per slot at most)
 
 inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
   const int64_t b = (n + 255) / 256;
@@ -1555,7 +1548,7 @@ void launch_quant_max(const QuantArgs& a, double* out, void* partials, hipStream
 
 void launch_grad_max(const double* margin, const float* label, float* g, float* h, int64_t N, double* maxv,
                      const PrologueInit& pi, hipStream_t s) {
-  const int nb = (int)grid_for(N > 0 ? N : 1, kTicketBlocks);
+  const int nb = (int)grid_for((N > 0 ? N : 1) / kPrologueU + 1, kSlotBlocks);
   hipLaunchKernelGGL(grad_max_kernel, dim3(nb), dim3(256), 0, s, margin, label, g, h, N,
                      reinterpret_cast<unsigned long long*>(maxv), pi);
 }
@@ -1564,7 +1557,7 @@ void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStr
   auto* part = reinterpret_cast<unsigned long long*>(partials);
   const int nb = a.N > 0 ? quant_blocks(a.N) : 0;
   if (a.ticket != nullptr || a.atomic_root) {     // one launch (quant_kernel)
-    const int nt = a.N > 0 ? (int)grid_for(a.N, kTicketBlocks) : 1;
+    const int nt = a.N > 0 ? (int)grid_for(a.N / kPrologueU + 1, a.atomic_root ? kSlotBlocks : kTicketBlocks) : 1;
     hipLaunchKernelGGL(quant_kernel, dim3(nt), dim3(256), 0, s, a, maxv, part);
     return;
   }
@@ -1712,7 +1705,7 @@ void launch_split_best(const double* gain, const int32_t* bin, const int64_t* le
 }
 
 int64_t split_partials(int32_t nodes, int32_t Fa) {
-  return Fa >= 256 ? 2 * (((int64_t)nodes * Fa + 255) / 256) : 0;
+  return Fa >= kWave ? 2 * (((int64_t)nodes * Fa + 255) / 256) * 4 : 0;     // (every wave of the narrow grid)
 }
 
 void launch_partition(const PartitionArgs& a, hipStream_t s) {
