@@ -173,7 +173,10 @@ def bench_rf(args) -> dict:
            "lanes": res.lanes, "collectives": bool(D.Collectives().active),
            "level_collective_calls": grower.LEVEL_STATS["coll_calls"],
            "collective_calls": D.total_calls(), "collective_calls_by_kind": dict(D.CALLS),
-           "level_collective_ms": _max_over_ranks(grower.level_collective_ms(), dev)}
+           "level_collective_ms": _max_over_ranks(grower.level_collective_ms(), dev),
+           "listed_passes": grower.LEVEL_STATS["listed_passes"],
+           "listed_active_items": grower.LEVEL_STATS["listed_active_items"],
+           "listed_grid_waves": grower.LEVEL_STATS["listed_grid_waves"]}
     if rank == 0:
         tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
         raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()

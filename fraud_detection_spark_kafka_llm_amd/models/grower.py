@@ -61,7 +61,9 @@ DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
 HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
 # device level loop counters (bench/gbdt_train.py reports the histogram payload per level: what a
 # data-parallel level reduce-scatters, before the 1/S shard split)
-LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0, "coll_calls": 0, "coll_ms": 0.0}
+LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0, "coll_calls": 0, "coll_ms": 0.0,
+               # preselected RF passes (a wave per active item): items active vs waves launched
+               "listed_passes": 0, "listed_active_items": 0, "listed_grid_waves": 0}
 # (begin, end) timing events of the data-parallel levels' collectives, resolved lazily by
 # level_collective_ms() so that timing never adds a host wait to the level loop
 _COLL_EVENTS: list = []
@@ -1314,6 +1316,11 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 break
             if sel_ids:       # largest per-XCD active-item count of each sampled group
                 per_xcd = {gi: max(cnt[4 + 8 * j: 12 + 8 * j]) for j, gi in enumerate(sel_ids)}
+                for j, gi in enumerate(sel_ids):
+                    if per_xcd[gi]:           # (launch_hist: (npx + 3) / 4 x 8 workgroups of 4 waves)
+                        LEVEL_STATS["listed_passes"] += 1
+                        LEVEL_STATS["listed_active_items"] += sum(cnt[4 + 8 * j: 12 + 8 * j])
+                        LEVEL_STATS["listed_grid_waves"] += (per_xcd[gi] + 3) // 4 * 8 * 4
         LEVEL_STATS["levels"] += 1
         LEVEL_STATS["built_nodes"] += n_build
         LEVEL_STATS["hist_bytes"] += n_build * TB * 16          # (g, h) int64 partials of the built nodes

@@ -754,7 +754,8 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
     if S:
         cols_t = torch.from_numpy(cols.astype(np.int32)).to(dev)
         bounds = torch.empty((S, nsb + 1), dtype=torch.int64, device=dev)
-        C.block_bounds(Q.csc_row, Q.colptr, cols_t, int(nsb), int(sb_rows), bounds)
+        with tracing.span("q.bsearch"):
+            C.block_bounds(Q.csc_row, Q.colptr, cols_t, int(nsb), int(sb_rows), bounds)
         bounds[:, -1] = Q.colptr[cols_t.to(torch.int64) + 1]
         if light.any() and nsb > 1:
             li = torch.from_numpy(np.nonzero(light)[0]).to(dev)
@@ -764,8 +765,9 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
         flat = seg_len.reshape(-1)
         seg_dst = torch.cumsum(flat, 0) - flat
         total = int(flat.sum())
-        h_row = torch.zeros(total + CSC_PAD, dtype=torch.int32, device=dev)
-        h_key = torch.full((total + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
+        with tracing.span("q.alloc"):
+            h_row = torch.zeros(total + CSC_PAD, dtype=torch.int32, device=dev)
+            h_key = torch.full((total + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
         hptr = np.zeros((nsb, S + 1), dtype=np.int64)                  # [sb][i] start of cols[i] in super-block sb
         dst_host = seg_dst.cpu().numpy().reshape(nsb, S)
         hptr[:, :S] = dst_host
