@@ -111,6 +111,7 @@ class RfLevels {
     FDX_CHECK(dev_.is_cuda(), "the level runner drives device levels only");
     const int64_t cap = st_["s2n"].numel();
     scratch_ = at::empty({fdx::rf_scratch_bytes(2 * cap)}, row_node_.options().dtype(at::kByte));
+    sample_counts_ = at::zeros({3 * 2 * cap}, row_node_.options());     // (left zero by every sample launch)
     ticket_ = at::zeros({4}, row_node_.options());
     // per parity: kRootSlots slots of the max |g|, |h| bit patterns / of the root's sums
     maxv_ = at::zeros({2 * fdx::kRootSlots * fdx::kRootStride}, row_node_.options().dtype(at::kLong));
@@ -416,6 +417,11 @@ class RfLevels {
                         const std::vector<optional<Tensor>>& sel_lists) const {
     bool sel = false;
     for (const auto& l : sel_lists) sel = sel || l.has_value();
+    if (sample_next && sel) {               // the select's per-XCD counts, zeroed by the plan
+      int64_t n_sel = 0;
+      for (const auto& l : sel_lists) n_sel += l ? 1 : 0;
+      a.counts_tail = (int32_t)(8 * n_sel);
+    }
     if (counts_host_dev_ == nullptr || (sample_next && sel)) return false;
     a.counts_host = counts_host_dev_ + d * st_.at("counts").size(1);
     return true;
@@ -477,6 +483,8 @@ class RfLevels {
       FDX_CHECK(next_open.numel() >= 2 * n_open && thr->numel() >= 2 * n_open && mask->numel() == r.Fa &&
                     scratch_.numel() >= fdx::rf_scratch_bytes(r.nnodes), "next-level sample sizes");
       r.scratch = p<uint8_t>(scratch_);
+      r.fused_counts = reinterpret_cast<uint32_t*>(p<int32_t>(sample_counts_));
+      r.fused_cap = (int32_t)(sample_counts_.numel() / 3);
       fdx::launch_rf_sample(r, s);
       if (local) {
         fdx::RfCompactArgs cp{};
@@ -501,27 +509,25 @@ class RfLevels {
         // per-XCD counts of the selected groups (the non-None lists, in group order) at counts[d, 4 + 8 js]
         int64_t n_sel = 0;
         for (const auto& l : sel_lists) n_sel += l ? 1 : 0;
-        FDX_CHECK(sel_lists.size() == groups_.size() && cw >= 4 + 8 * n_sel, "select lists");
-        FDX_CHECK(hipMemsetAsync(counts_d + 4, 0, 8 * n_sel * sizeof(int32_t), s) == hipSuccess, "memset");
-        int64_t js = 0;
+        FDX_CHECK(sel_lists.size() == groups_.size() && cw >= 4 + 8 * n_sel && n_sel <= fdx::kSelGroups,
+                  "select lists");
+        // (counts[d, 4:] zeroed by the plan: LevelPlanArgs counts_tail)
+        fdx::SelectArgs sa{};
+        sa.feat_active = p<uint8_t>(*mask);
         for (size_t j = 0; j < groups_.size(); ++j) {
           if (!sel_lists[j]) continue;
           const ItemGroup& g = groups_[j];
-          fdx::HistArgs h{};
-          h.listed_per_xcd = -1;
-          h.item_start = p<int64_t>(g.start);
-          h.item_f0 = p<int32_t>(g.f0);
-          h.item_meta = p<int32_t>(g.meta);
-          h.num_items = (int32_t)g.start.numel();
-          h.nbins = p<int32_t>(nbins_);
-          h.feat_active = p<uint8_t>(*mask);
-          h.wave_item = p<int32_t>(g.wave);
-          h.num_slots = (int32_t)g.wave.numel();
-          h.active_list = p<int32_t>(*sel_lists[j]);
-          h.active_count = counts_d + 4 + 8 * js++;
-          h.list_cap = (int32_t)(((h.num_slots + 3) / 4 + 7) / 8 * 4);
-          fdx::launch_hist_select(h, s);
+          const int k = sa.n++;
+          sa.item_f0[k] = p<int32_t>(g.f0);
+          sa.item_meta[k] = p<int32_t>(g.meta);
+          sa.wave_item[k] = p<int32_t>(g.wave);
+          sa.num_items[k] = (int32_t)g.start.numel();
+          sa.num_slots[k] = (int32_t)g.wave.numel();
+          sa.list_cap[k] = (int32_t)(((sa.num_slots[k] + 3) / 4 + 7) / 8 * 4);
+          sa.list[k] = p<int32_t>(*sel_lists[j]);
+          sa.count[k] = counts_d + 4 + 8 * k;
         }
+        fdx::launch_hist_select_groups(sa, s);
       }
     }
     if (counts_written) {
@@ -588,7 +594,7 @@ class RfLevels {
   optional<Tensor> arena_;
   int32_t* counts_host_dev_ = nullptr;
   int parity_ = 0, tparity_ = 0;
-  Tensor root_parts_;
+  Tensor root_parts_, sample_counts_;
   const int64_t* root_pending_ = nullptr;   // the last prologue's root slots, until level 0's split
   const int64_t* find_root_ = nullptr;
   bool build_all_ = true;

@@ -51,8 +51,11 @@ __global__ __launch_bounds__(kThreads) void rf_window_kernel(RfSampleArgs a, uin
   if (threadIdx.x == 0 && s_below) atomicAdd(&below[i], s_below);
 }
 
-__global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, const unsigned int* below,
-                                                                const unsigned int* ncand, const uint64_t* cand) {
+// Node bi's threshold (its k-th smallest priority), by the calling workgroup: from the window
+// pass's candidates when the window holds the k-th (below / ncand / cand non-null), else by the
+// exact radix search. Workgroup-uniform control flow (barriers inside).
+__device__ void rf_threshold_node(const RfSampleArgs& a, int bi, const unsigned int* below,
+                                  const unsigned int* ncand, const uint64_t* cand) {
   __shared__ uint32_t s_hist[kBuckets];
   __shared__ uint64_t s_cand[kCap];
   __shared__ uint32_t s_ncand;
@@ -61,17 +64,17 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
   __shared__ int64_t s_k;
   __shared__ int64_t s_count;
 
-  const int node = a.nodes[blockIdx.x];
+  const int node = a.nodes[bi];
   const int tid = threadIdx.x;
   if (node < 0) {                                 // padding: samples nothing
-    if (tid == 0) a.thr[blockIdx.x] = -1.0;
+    if (tid == 0) a.thr[bi] = -1.0;
     return;
   }
   if (below != nullptr) {
-    const int64_t r = a.k - (int64_t)below[blockIdx.x];     // rank of the k-th inside the window
-    const int n = (int)ncand[blockIdx.x];
+    const int64_t r = a.k - (int64_t)below[bi];     // rank of the k-th inside the window
+    const int n = (int)ncand[bi];
     if (r >= 1 && r <= n && n <= kCap) {
-      for (int j = tid; j < n; j += kThreads) s_cand[j] = cand[(int64_t)blockIdx.x * kCap + j];
+      for (int j = tid; j < n; j += kThreads) s_cand[j] = cand[(int64_t)bi * kCap + j];
       __syncthreads();
       for (int j = tid; j < n; j += kThreads) {
         const uint64_t uj = s_cand[j];
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
           less += s_cand[t] < uj;
           eq += s_cand[t] == uj;
         }
-        if (less < r && r <= less + eq) a.thr[blockIdx.x] = (double)uj * (1.0 / 9007199254740992.0);
+        if (less < r && r <= less + eq) a.thr[bi] = (double)uj * (1.0 / 9007199254740992.0);
       }
       return;                  // uniform per workgroup: every thread took this branch
     }
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
     for (int i = tid; i < kBuckets; i += kThreads) s_hist[i] = 0;
     __syncthreads();
     for (int64_t f = tid; f < a.F; f += kThreads) {
-      const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, blockIdx.x), node, f);
+      const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, bi), node, f);
       if (known == 0 || (u >> (53 - known)) == prefix)
         atomicAdd(&s_hist[(u >> shift) & ((1u << nbits) - 1)], 1u);
     }
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
   const int known = s_known;
   const uint64_t prefix = s_prefix;
   for (int64_t f = tid; f < a.F; f += kThreads) {
-    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, blockIdx.x), node, f);
+    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, bi), node, f);
     if (known == 0 || (u >> (53 - known)) == prefix) {
       const uint32_t i = atomicAdd(&s_ncand, 1u);
       if (i < (uint32_t)kCap) s_cand[i] = u;
@@ -143,7 +146,61 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
       eq += s_cand[j] == ui;
     }
     if (less < k && k <= less + eq)    // ties: every holder of the k-th value writes the same result
-      a.thr[blockIdx.x] = (double)ui * (1.0 / 9007199254740992.0);
+      a.thr[bi] = (double)ui * (1.0 / 9007199254740992.0);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, const unsigned int* below,
+                                                                const unsigned int* ncand, const uint64_t* cand) {
+  rf_threshold_node(a, blockIdx.x, below, ncand, cand);
+}
+
+// Window pass + threshold in one launch (RfSampleArgs fused_counts): the window kernel's body,
+// then per node a ticket; the node's last workgroup (one device-scope release per workgroup, see
+// tree_kernels.hip last_workgroup) ranks the candidates and zeroes the node's counters for the
+// next launch -- no memset and no second launch per level.
+__global__ __launch_bounds__(kThreads) void rf_window_threshold_kernel(RfSampleArgs a, uint64_t ulo, uint64_t uhi,
+                                                                       uint64_t* cand) {
+  __shared__ unsigned int s_below;
+  __shared__ int s_last;
+  const int i = blockIdx.y;
+  const int node = a.nodes[i];
+  unsigned int* ticket = a.fused_counts;
+  unsigned int* below = a.fused_counts + a.fused_cap;
+  unsigned int* ncand = a.fused_counts + 2 * a.fused_cap;
+  if (node < 0) {                                 // padding: samples nothing (uniform per node)
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.thr[i] = -1.0;
+    return;
+  }
+  if (threadIdx.x == 0) s_below = 0;
+  __syncthreads();
+  unsigned int mine = 0;
+  for (int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x; f < a.F; f += (int64_t)gridDim.x * kThreads) {
+    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, i), node, f);
+    if (u < ulo) {
+      ++mine;
+    } else if (u <= uhi) {
+      const unsigned int j = atomicAdd(&ncand[i], 1u);
+      if (j < (unsigned int)kCap) cand[(int64_t)i * kCap + j] = u;
+    }
+  }
+  atomicAdd(&s_below, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_below) atomicAdd(&below[i], s_below);
+    __threadfence();
+    const unsigned int t = atomicAdd(&ticket[i], 1u);
+    s_last = t == gridDim.x - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  rf_threshold_node(a, i, below, ncand, cand);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    below[i] = 0;
+    ncand[i] = 0;
+    ticket[i] = 0;
   }
 }
 
@@ -288,6 +345,12 @@ void launch_rf_sample(const RfSampleArgs& a, hipStream_t s) {
     unsigned int* below = reinterpret_cast<unsigned int*>(a.scratch);
     unsigned int* ncand = below + a.nnodes;
     uint64_t* cand = reinterpret_cast<uint64_t*>(a.scratch + 8 * ((2 * a.nnodes * 4 + 7) / 8));
+    if (a.fused_counts != nullptr && a.nnodes <= a.fused_cap) {
+      hipLaunchKernelGGL(rf_window_threshold_kernel, dim3(kSlices, a.nnodes), dim3(kThreads), 0, s, a, ulo, uhi, cand);
+      if (a.Fa > 0)
+        hipLaunchKernelGGL(rf_mask_kernel, dim3((unsigned)((a.Fa + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
+      return;
+    }
     hipMemsetAsync(below, 0, sizeof(unsigned int) * 2 * (size_t)a.nnodes, s);
     hipLaunchKernelGGL(rf_window_kernel, dim3(kSlices, a.nnodes), dim3(kThreads), 0, s, a, ulo, uhi, below, ncand,
                        cand);

@@ -361,6 +361,11 @@ struct RfSampleArgs {
   double* thr;                    // [nnodes] out
   uint8_t* mask;                  // [Fa] out
   uint8_t* scratch;               // device: rf_scratch_bytes(nnodes) for the window fast path (or null)
+  // optional (with scratch): one launch for window + threshold. [3 * fused_cap] uint32, zero at
+  // the first use and left zero by every launch: per node its workgroup ticket, the count below
+  // the window and the candidate count (the last window workgroup of a node ranks its candidates)
+  uint32_t* fused_counts;
+  int32_t fused_cap;
 };
 
 FDX_HD int32_t rf_tree_of(const RfSampleArgs& a, int64_t i) { return a.node_trees ? a.node_trees[i] : a.tree; }
@@ -560,6 +565,22 @@ FDX_HD uint64_t feature_priority_u53(uint64_t seed, int32_t tree, int32_t node, 
 }
 
 // Work item `item` holds at least one active feature (always true without a mask).
+// The active-item selects of one level's sampled item groups in one launch (grid row g = group
+// g): hist_select_kernel's body per group; counts zeroed beforehand (LevelPlanArgs counts_tail).
+constexpr int kSelGroups = 4;
+struct SelectArgs {
+  const int32_t* item_f0[kSelGroups];
+  const int32_t* item_meta[kSelGroups];
+  const int32_t* wave_item[kSelGroups];
+  int32_t num_items[kSelGroups];
+  int32_t num_slots[kSelGroups];
+  int32_t list_cap[kSelGroups];
+  int32_t* list[kSelGroups];
+  int32_t* count[kSelGroups];       // [8] per-XCD counts of the group
+  int32_t n;
+  const uint8_t* feat_active;
+};
+
 FDX_HD bool item_active(const HistArgs& a, int64_t item) {
   if (!a.feat_active) return true;
   const int32_t f0 = a.item_f0[item];
@@ -708,6 +729,7 @@ struct LevelPlanArgs {
   int32_t* cs_left_default;
   int32_t* counts;                // [4] out: n_cs, n_next_open, n_build, n_nodes
   int32_t* counts_host;           // optional host-mapped copy of the 4 counts (pinned; no D2H copy)
+  int32_t counts_tail;            // counts[4 .. 4 + counts_tail) zeroed (the next level's select counts)
   const int64_t* root_parts;      // optional (depth 0): the root's totals as QuantArgs root_parts
                                   //   slots, summed here into stats[0]
   // level d + 1 (out; capacity 2L open, L built)

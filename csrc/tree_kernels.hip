@@ -1455,6 +1455,7 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
     a.counts[1] = n_next;
     a.counts[2] = nb;
     a.counts[3] = nn;
+    for (int k = 0; k < a.counts_tail; ++k) a.counts[4 + k] = 0;
     if (a.counts_host) {         // host-mapped pinned row: visible to the host at the kernel's end
       a.counts_host[0] = n_cs;
       a.counts_host[1] = n_next;
@@ -1569,6 +1570,51 @@ void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStr
 
 void launch_slot8(const SlotArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(slot8_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void hist_select_groups_kernel(SelectArgs a) {
+  const int g = blockIdx.y;
+  const int64_t w0 = (int64_t)blockIdx.x * 256 * kSelPerThread;
+  if (w0 >= a.num_slots[g]) return;                 // (workgroup-uniform)
+  __shared__ int32_t s_cnt[8], s_base[8];
+  const int t = threadIdx.x;
+  if (t < 8) s_cnt[t] = 0;
+  __syncthreads();
+  const int32_t* wave_item = a.wave_item[g];
+  const int32_t* item_f0 = a.item_f0[g];
+  const int32_t* item_meta = a.item_meta[g];
+  int32_t item[kSelPerThread], loc[kSelPerThread];
+#pragma unroll
+  for (int j = 0; j < kSelPerThread; ++j) {
+    const int64_t w = w0 + (int64_t)j * 256 + t;
+    int it = -1;
+    if (w < a.num_slots[g]) it = wave_item ? wave_item[w] : (int)w;
+    bool act = false;
+    if (it >= 0 && it < a.num_items[g]) {
+      const int32_t f0 = item_f0[it];
+      const int nf = (item_meta[it] >> 8) & 0xFF;
+      for (int k = 0; k < nf && !act; ++k) act = a.feat_active[f0 + k] != 0;
+    }
+    item[j] = it;
+    loc[j] = act ? atomicAdd(&s_cnt[(w >> 2) & 7], 1) : -1;      // (hist_select_kernel: XCD of the slot)
+  }
+  __syncthreads();
+  if (t < 8) s_base[t] = s_cnt[t] ? atomicAdd(a.count[g] + t, s_cnt[t]) : 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSelPerThread; ++j)
+    if (loc[j] >= 0) {
+      const int x = (int)(((w0 + (int64_t)j * 256 + t) >> 2) & 7);
+      a.list[g][(int64_t)x * a.list_cap[g] + s_base[x] + loc[j]] = item[j];
+    }
+}
+
+void launch_hist_select_groups(const SelectArgs& a, hipStream_t s) {
+  int32_t most = 0;
+  for (int g = 0; g < a.n; ++g) most = a.num_slots[g] > most ? a.num_slots[g] : most;
+  if (a.n <= 0 || most <= 0) return;
+  hipLaunchKernelGGL(hist_select_groups_kernel, dim3((most + 256 * kSelPerThread - 1) / (256 * kSelPerThread), a.n),
+                     dim3(256), 0, s, a);
 }
 
 void launch_hist_select(const HistArgs& a, hipStream_t s) {
