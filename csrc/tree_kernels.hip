@@ -667,6 +667,14 @@ __global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
     const int32_t meta = a.item_meta[item];
     const int32_t f0 = a.item_f0[item];
     const uint32_t koff = (uint32_t)item_koff(meta);
+    // keys of the item's sampled features (lane k tests key koff + k): a packed item is active
+    // when ANY of its features is, and its other features' entries (typically most of them at
+    // k = sqrt(F)) are skipped instead of counted and flushed into bins nobody reads
+    uint64_t amask = ~0ull;
+    if (a.feat_active != nullptr && item_nfeat(meta) > 1) {
+      const int fl = ((int)koff + lane) >> item_stride_log2(meta);
+      amask = __ballot(lane < KEYS && fl < item_nfeat(meta) && a.feat_active[f0 + fl] != 0);
+    }
     for (int i = lane; i < cells; i += kWave) tab[i] = 0ull;
     __builtin_amdgcn_wave_barrier();
     const int64_t first = e0 & ~(int64_t)3;
@@ -703,7 +711,7 @@ __global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
         const uint32_t kk = ((keys4 >> (8 * j)) & 0xffu) - koff;     // (unsigned: keys below koff wrap)
         const int64_t q0 = (int64_t)(int8_t)(uint8_t)(w[2 * j] & 0xffu);
         const int64_t q1 = (int64_t)(int8_t)(uint8_t)(w[2 * j + 1] & 0xffu);
-        if (s < (uint32_t)ns && kk < (uint32_t)KEYS && (q0 | q1) != 0)
+        if (s < (uint32_t)ns && kk < (uint32_t)KEYS && (q0 | q1) != 0 && ((amask >> kk) & 1ull))
           atomicAdd(&tab[kk * ns + s], (unsigned long long)(q0 + q1 * 4294967296ll));
       }
     }
