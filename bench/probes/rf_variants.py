@@ -30,6 +30,9 @@ VARIANTS = {
     "r4": {(grower, "PRESELECT"): False, (grower, "FUSED_PACK"): False},
     "lanes8": {(forest_batch, "TREES_IN_FLIGHT"): 8},
     "lanes24": {(forest_batch, "TREES_IN_FLIGHT"): 24},
+    "lanes12": {(forest_batch, "TREES_IN_FLIGHT"): 12},
+    "lanes6": {(forest_batch, "TREES_IN_FLIGHT"): 6},
+    "l24g3": {(forest_batch, "TREES_IN_FLIGHT"): 24, (forest_batch, "LANE_GROUPS"): 3},
     "lanes32": {(forest_batch, "TREES_IN_FLIGHT"): 32},
     "l32g2": {(forest_batch, "TREES_IN_FLIGHT"): 32, (forest_batch, "LANE_GROUPS"): 2},
     "l32g4": {(forest_batch, "TREES_IN_FLIGHT"): 32, (forest_batch, "LANE_GROUPS"): 4},
