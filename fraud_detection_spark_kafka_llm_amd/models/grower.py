@@ -1188,6 +1188,171 @@ def _level_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowPar
     return runner
 
 
+class _RfViews:
+    """Views of a LevelState's buffers the sampled RF level loop slices every level, made once
+    (a tensor slice costs 2-5 us of host time; the loop is host bound at small shards)."""
+
+    def __init__(self, st: "LevelState"):
+        self.st = st
+        self._m = {}
+
+    def get(self, key, make):
+        v = self._m.get(key)
+        if v is None:
+            v = self._m[key] = make()
+        return v
+
+
+def _rf_runner_levels(Q, ws, st, params, tree_index, seed, shards, runner, sel_ids, item_groups, compact,
+                      native_prologue, cur_stream, on_first_wait, pre_hist):
+    """The level loop of a sampled RF tree on the native runner (device_tree_steps' generic loop
+    with runner and sampled and FUSED_PACK, launch for launch): every level's feature sample is
+    queued by the previous level's plan (runner.plan / split_plan sample_next), the per-level
+    tensor views are memoised (_RfViews) and the branches of the other tree kinds are gone.
+    ``pre_hist``: the root histogram the prologue zeroed (single process). Returns the
+    on_first_wait callback if it is still pending."""
+    C = native.lib()
+    dev = Q.device
+    V = getattr(st, "_rfv", None)
+    if V is None:
+        V = st._rfv = _RfViews(st)
+    if st.rf_thr is None:                     # (the next level's sample goes here; no preselection)
+        st.rf_thr = [torch.empty(st.cap, dtype=torch.float64, device=dev) for _ in range(2)]
+        st.rf_mask = [torch.empty(Q.Fa, dtype=torch.uint8, device=dev) for _ in range(2)]
+    TB = Q.TB
+    F, k = int(Q.num_features), int(params.feat_k)
+    groups = item_groups
+    wide = (_wide_features(shards.nbins, shards.Fa) if shards is not None else _wide_features(Q.nbins, Q.Fa)) \
+        if SPLIT_WIDE else None
+    sel_args = [ws.item_list(gi, grp)[0] if gi in sel_ids else None for gi, grp in enumerate(groups)] \
+        if sel_ids else []
+    sel_j = {gi: j for j, gi in enumerate(sel_ids)}
+    listed = [ws.item_list(gi, grp) if grp.num_items else (None, None) for gi, grp in enumerate(groups)]
+    empty_lay = (None,) * 5 + (0,)
+    n_open, n_build = 1, 1
+    per_xcd = None
+    ev = None
+    for d in range(params.max_depth):
+        cur = d & 1
+        nxt = cur ^ 1
+        if d > 0:
+            if on_first_wait is not None:
+                on_first_wait()
+                on_first_wait = None
+            yield ev
+            cnt = st.counts_host[d - 1].tolist()
+            n_open, n_build = cnt[1], cnt[2]
+            if n_open == 0:
+                break
+            if sel_ids:       # largest per-XCD active-item count of each sampled group
+                per_xcd = {}
+                for j, gi in enumerate(sel_ids):
+                    row = cnt[4 + 8 * j: 12 + 8 * j]
+                    per_xcd[gi] = m = max(row)
+                    if m:           # (launch_hist: (npx + 3) / 4 x 8 workgroups of 4 waves)
+                        LEVEL_STATS["listed_passes"] += 1
+                        LEVEL_STATS["listed_active_items"] += sum(row)
+                        LEVEL_STATS["listed_grid_waves"] += (m + 3) // 4 * 8 * 4
+        LEVEL_STATS["levels"] += 1
+        LEVEL_STATS["built_nodes"] += n_build
+        LEVEL_STATS["hist_bytes"] += n_build * TB * 16
+        open_d = V.get(("open", cur, n_open), lambda: st.open[cur][:n_open])
+        if d == 0 and native_prologue:
+            totals_d = V.get(("root",), lambda: st.stats[:1])
+        else:
+            totals_d = V.get(("tot", cur, n_open), lambda: st.totals[cur][:n_open])
+        n_open_ptr = st.one if d == 0 else V.get(("nop", d), lambda: st.counts[d - 1, 1:2])
+        more = d + 1 < params.max_depth
+        # the level's k-of-F sample: queued with the previous level's plan (the root's here)
+        if compact:
+            feat_thr, feat_mask, local_c, Bs_c = shards.compact_level(cur, n_open)
+        elif d > 0:
+            feat_thr = V.get(("thr", cur, n_open), lambda: st.rf_thr[cur][:n_open])
+            feat_mask = st.rf_mask[cur]
+        else:
+            feat_thr = V.get(("thr", cur, n_open), lambda: st.rf_thr[cur][:n_open])
+            feat_mask = st.rf_mask[cur]
+            C.tree_rf_sample(seed, tree_index, open_d, F, k, Q.fid_orig, feat_thr, feat_mask, None)
+        bufs = None
+        if shards is None:
+            if pre_hist is not None and pre_hist.shape[0] >= n_open:
+                hist_target = pre_hist[:n_open]
+            else:
+                hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
+            pre_hist = None
+            h_boff = Q.boff
+            s2n = st.zero1 if d == 0 else V.get(("s2n", n_build), lambda: st.s2n[:n_build])
+        else:
+            bufs = yield CollStep("alloc", rows=n_build, Bs=Bs_c if compact else shards.Bs, n_open=n_open,
+                                  totals=ws.totals if d == 0 else None, sub_rows=0)
+            hist_target = bufs.prepare(ws.totals if d == 0 else None)
+            h_boff = local_c if compact else shards._local
+            s2n = ws.iota(n_build)
+        with tracing.span("tree.hist"):
+            pack = ws.rowpack() if d > 0 else None
+            lists, cnts, npxs = [], [], []
+            for gi, grp in enumerate(groups):
+                if grp.num_items and sel_ids and d > 0:
+                    j = sel_j[gi]
+                    lists.append(sel_args[gi])
+                    cnts.append(V.get(("cnt", d, j), lambda: st.counts[d - 1, 4 + 8 * j: 12 + 8 * j]))
+                    npxs.append(per_xcd[gi])
+                elif grp.num_items and n_open <= LISTED_MAX_NODES:
+                    lists.append(listed[gi][0])
+                    cnts.append(listed[gi][1])
+                    npxs.append(-1)
+                else:
+                    lists.append(None)
+                    cnts.append(None)
+                    npxs.append(-1)
+            runner.hist(n_build, hist_target, h_boff, feat_mask, s2n, pack, lists, cnts, npxs,
+                        shards._shard_of if shards is not None else None,
+                        bufs.shard_bins if shards is not None else 0)
+        if shards is not None:
+            yield CollStep("rs")                  # (the batch's reduce-scatter, LevelBatcher.serve)
+            if d == 0:
+                tot = bufs.reduced_totals()
+                st.stats[0].copy_(tot)
+                totals_d.copy_(tot[None])
+            # every open node built, slot k = open node k: the reduced rows ARE the histograms
+            cur_hist = bufs.mine()
+            with tracing.span("tree.split"):
+                split_boff = local_c[shards.f0: shards.f0 + shards.Fa + 1] if compact else shards.boff
+                runner.split(cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig, open_d,
+                             feat_thr, tree_index, shards.f0, bufs.ag_in, None, wide)
+                packed = yield CollStep("ag")
+        else:
+            cur_hist = hist_target
+            packed = ws.split_cache.get(("out", n_open))
+            if packed is None:
+                packed = ws.split_cache[("out", n_open)] = torch.empty((n_open, 5), dtype=torch.int64, device=dev)
+        if more and compact:
+            thr_n, mask_n = shards.compact_thr(nxt, 2 * n_open), shards.compact_mask(nxt)
+            lay = (shards._fs_dev, Q.nbins, shards._local_c[nxt], shards._sizes[nxt], shards.sizes_host[nxt],
+                   shards.max_shard_features)
+        elif more:
+            thr_n, mask_n, lay = st.rf_thr[nxt], st.rf_mask[nxt], empty_lay
+        else:
+            thr_n = mask_n = None
+            lay = empty_lay
+        sel = sel_args if (sel_ids and more) else []
+        if shards is None:
+            runner.split_plan(d, n_open, cur_hist, totals_d, Q.boff, feat_thr, tree_index, packed, wide, open_d,
+                              n_open_ptr, st.open[nxt], st.totals[nxt], more, thr_n, mask_n, sel)
+        else:
+            runner.plan(d, n_open, packed, open_d, n_open_ptr, st.open[nxt], st.totals[nxt], tree_index, more,
+                        thr_n, mask_n, *lay, sel)
+        ev = st.record_event(cur_stream)
+        zero = None
+        if shards is None and more:
+            # the next level's histograms (every open node built: <= 2 n_open rows), zeroed by the
+            # partition kernel on the way
+            pre_hist = zero = torch.empty((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
+        with tracing.span("tree.partition"):
+            runner.partition(d, n_open, more, zero)
+    return on_first_wait
+
+
 def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
                       h: torch.Tensor, weight: Optional[torch.Tensor] = None, coll=None,
                       shards: Optional["FeatureShards"] = None, label: Optional[torch.Tensor] = None,
@@ -1303,7 +1468,14 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
         shards.sample_compact(C, 0, seed, int(tree_index), st.open[0][:1], int(Q.num_features), int(params.feat_k),
                               Q.fid_orig)
         yield st.record_event(cur_stream)
-    for d in range(params.max_depth):
+    generic_depth = params.max_depth
+    if runner is not None and sampled and FUSED_PACK:
+        # sampled RF levels on the native runner: the lean loop (same launches, far less Python)
+        on_first_wait = yield from _rf_runner_levels(Q, ws, st, params, int(tree_index), seed, shards, runner,
+                                                     sel_ids, item_groups, compact, native_prologue, cur_stream,
+                                                     on_first_wait, pre_hist)
+        generic_depth = 0
+    for d in range(generic_depth):
         cur = d % 2
         if d > 0:
             if on_first_wait is not None:
