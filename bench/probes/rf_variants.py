@@ -38,6 +38,9 @@ VARIANTS = {
     "l32g4": {(forest_batch, "TREES_IN_FLIGHT"): 32, (forest_batch, "LANE_GROUPS"): 4},
     "g1": {(forest_batch, "LANE_GROUPS"): 1},
     "nonative": {(grower, "NATIVE_LEVELS"): False},
+    "nolean": {(grower, "LEAN_RF"): False},
+    "presel_all": {(grower, "PRESELECT_MIN_ROWS"): 0},
+    "presel_4m": {(grower, "PRESELECT_MIN_ROWS"): 4_000_000},
     "mfma": {(grower, "RF_LDS"): False},
     "nonative_nopresel": {(grower, "NATIVE_LEVELS"): False, (grower, "PRESELECT"): False},
 }

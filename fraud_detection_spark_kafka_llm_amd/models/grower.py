@@ -299,10 +299,11 @@ LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
 # RF levels >= 1 launch one wave per active work item from lists compacted with the previous
 # level's plan (0: the r4 passes, a wave per item slot or a fixed listed grid)
 PRESELECT = os.environ.get("FDX_RF_PRESELECT", "1") == "1"
-# ... on shards of at least this many rows: on a 1.25M-row shard (DP=8) the listed passes ran
-# slower per launch than the wave-per-slot ones (143 -> 207 us, profiles/r5/rf_dp_trace_ab.txt),
-# at 10M rows they win (0.768 -> 0.747 s a forest, profiles/r5/rf_variants_10M.jsonl)
-PRESELECT_MIN_ROWS = int(os.environ.get("FDX_RF_PRESELECT_ROWS", 4_000_000))
+# ... on shards of at least this many rows. Once the packed items skip their unsampled features
+# and the selects of a level are one launch, the listed passes win at 1.25M rows too (DP=8 shard,
+# forced collectives: 0.456 -> 0.446 s a forest, profiles/r5/rf_lean_presel_ab_1M.jsonl; before,
+# 143 -> 207 us a pass the other way); at 10M rows they win (0.768 -> 0.747 s)
+PRESELECT_MIN_ROWS = int(os.environ.get("FDX_RF_PRESELECT_ROWS", 0))
 # RF levels >= 1 read the packed row state (slot | class-count digits) written by the previous
 # level's partition instead of a row pass of their own (slot pack / masked digits: ~87 us per level
 # at 10M rows, 173 ms of a 500-tree forest's kernel time, profiles/r5/NOTES.md)
@@ -310,6 +311,8 @@ FUSED_PACK = os.environ.get("FDX_RF_FUSED_PACK", "1") == "1"
 # RF device levels issue their kernels through the native per-level runner (csrc/bindings_level.cpp
 # RfLevels: hist / split / plan / partition, one host call each) instead of ~20 Python-level calls
 NATIVE_LEVELS = os.environ.get("FDX_NATIVE_LEVELS", "1") == "1"
+# sampled RF trees on the runner take the lean level loop (_rf_runner_levels; 0: the generic loop)
+LEAN_RF = os.environ.get("FDX_RF_LEAN", "1") == "1"
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
 RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
 # split search: a wave per (node, feature) for the features with > 16 bins
@@ -1469,7 +1472,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                               Q.fid_orig)
         yield st.record_event(cur_stream)
     generic_depth = params.max_depth
-    if runner is not None and sampled and FUSED_PACK:
+    if runner is not None and sampled and FUSED_PACK and LEAN_RF:
         # sampled RF levels on the native runner: the lean loop (same launches, far less Python)
         on_first_wait = yield from _rf_runner_levels(Q, ws, st, params, int(tree_index), seed, shards, runner,
                                                      sel_ids, item_groups, compact, native_prologue, cur_stream,
