@@ -20,6 +20,7 @@ import torch
 
 from suite import _tfidf
 from fraud_detection_spark_kafka_llm_amd.models import forest_batch, grower
+from fraud_detection_spark_kafka_llm_amd.models import quantize as qmod
 from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
 from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels
 
@@ -41,6 +42,10 @@ VARIANTS = {
     "nolean": {(grower, "LEAN_RF"): False},
     "presel_all": {(grower, "PRESELECT_MIN_ROWS"): 0},
     "presel_4m": {(grower, "PRESELECT_MIN_ROWS"): 4_000_000},
+    "chunk2k": {(qmod, "CHUNK"): 2048},
+    "chunk4k": {(qmod, "CHUNK"): 4096},
+    "chunk8k": {(qmod, "CHUNK"): 8192},
+    "chunk16k": {(qmod, "CHUNK"): 16384},
     "mfma": {(grower, "RF_LDS"): False},
     "nonative_nopresel": {(grower, "NATIVE_LEVELS"): False, (grower, "PRESELECT"): False},
 }

@@ -40,7 +40,14 @@ from ..utils import tracing
 
 CSC_PAD = 16
 
-CHUNK = int(os.environ.get("FDX_HIST_CHUNK", 32768))   # entries per histogram work item (one wavefront)
+# entries per histogram work item (one wavefront); 0: by the row count. A wave walks its item
+# serially (the pass ends with its longest wave): RF 500 x depth 5 on a 1.25M-row shard 0.46 ->
+# 0.41 s with 4K-entry items, on 10M rows 0.76 -> 0.72 s with 16K (profiles/r5/rf_chunk_sweep_*.jsonl)
+CHUNK = int(os.environ.get("FDX_HIST_CHUNK", 0))
+
+
+def default_chunk(n_rows: int) -> int:
+    return CHUNK or (16384 if n_rows >= 4_000_000 else 4096)
 # A work item's int32 MFMA accumulators gain at most 128 * 128 = 2^14 per entry, so one item may
 # hold at most this many entries before a (key, column) sum could overflow (csrc/tree_kernels.hip)
 MAX_ITEM_ENTRIES = (1 << 31) // (1 << 14) - 1
@@ -409,7 +416,7 @@ def _decode_f32_bits(k: torch.Tensor) -> torch.Tensor:
 
 def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
              all_reduce_max: Optional[Callable] = None, all_gather: Optional[Callable] = None,
-             chunk: int = CHUNK, super_rows: int = None, hot_density: float = None) -> Quantized:
+             chunk: int = None, super_rows: int = None, hot_density: float = None) -> Quantized:
     """Bin a ``VectorColumn`` and build the CSC. ``counts``/``scale`` select the count path
     (per-entry integer counts and per-feature positive scale); integral non-negative values
     take it automatically with scale 1."""
@@ -422,6 +429,7 @@ def quantize(vc, max_bins: int = 32, counts: Optional[torch.Tensor] = None, scal
     dev = indptr.device
     N = int(indptr.numel() - 1)
     F = int(vc.size)
+    chunk = chunk or default_chunk(N)       # (read at call time: experiments set the module value)
     val64 = val.to(torch.float64) if val is not None else None
     if counts is None and val64.numel() and bool(torch.all(val64 >= 0)) and bool(torch.all(val64 == torch.round(val64))) \
             and float(val64.max()) < 65536:
@@ -705,7 +713,7 @@ def _split_long(rows_: np.ndarray, chunk: int) -> np.ndarray:
     return out
 
 
-def _finish_items(Q: Quantized, chunk: int = CHUNK, super_rows: int = SUPER_ROWS, hot_density: float = HOT_DENSITY) \
+def _finish_items(Q: Quantized, chunk: int = 0, super_rows: int = SUPER_ROWS, hot_density: float = HOT_DENSITY) \
         -> None:
     """Dense block now; histogram CSC and work items on first use (see the module docstring).
 
