@@ -1,6 +1,6 @@
-"""The native per-level runner of RF device levels (csrc/bindings_level.cpp RfLevels) and the
-kernels it brought: same forests as the Python-driven levels, multi-workgroup compact layout
-equal to the host twin."""
+"""The native per-level runner (csrc/bindings_level.cpp RfLevels) and the kernels it brought:
+same forests and boosters as the Python-driven levels, multi-workgroup compact layout equal to
+the host twin."""
 import numpy as np
 import pytest
 import torch
@@ -34,12 +34,45 @@ def test_gpu_native_levels_equal_python_levels(inflight, monkeypatch):
     ref = _forest("cuda:0")
     monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
     assert _forest("cuda:0") == ref
+    monkeypatch.setattr(grower, "LEAN_RF", False)            # the generic loop on the runner
+    assert _forest("cuda:0") == ref
+    monkeypatch.setattr(grower, "LEAN_RF", True)
     monkeypatch.setattr(grower, "PRESELECT_MIN_ROWS", 0)
     for presel, fused in ((False, True), (True, False)):
         monkeypatch.setattr(grower, "PRESELECT", presel)
         monkeypatch.setattr(grower, "FUSED_PACK", fused)
         assert _forest("cuda:0") == ref
     assert _forest("cpu") == ref
+
+
+def _booster(device, n=5000, F=300, trees=8, depth=6, seed=11):
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+    from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
+
+    rng = np.random.default_rng(seed)
+    p = 0.5 / (1.0 + np.arange(F)) ** 0.6
+    vals = (rng.random((n, F)) < p) * rng.integers(1, 6, (n, F))        # (counts: the row-group engine)
+    y = ((vals[:, 0] >= 2) ^ (vals[:, 3] >= 3)).astype(np.float32)
+    flip = rng.random(n) < 0.05
+    y[flip] = 1 - y[flip]
+    vc = VectorColumn(F, dense=torch.from_numpy(vals.astype(np.float64)))
+    r = fit_gbdt(vc, torch.from_numpy(y), GBDTParams(n_estimators=trees, max_depth=depth, learning_rate=0.3),
+                 device=device)
+    return [(t.feature.tolist(), t.threshold.tolist(), t.stats.tolist()) for t in r.trees]
+
+
+@pytest.mark.gpu
+def test_gpu_gbdt_native_round_equals_python_levels(monkeypatch):
+    """The fused boosting round (gradient prologue, split + plan, partition zeroing, leaf update
+    from the node table; csrc/bindings_level.cpp) grows the same trees, bit for bit, as the
+    Python-issued levels and as the host."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+
+    monkeypatch.setattr(grower, "NATIVE_LEVELS", False)
+    ref = _booster("cuda:0")
+    monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
+    assert _booster("cuda:0") == ref
+    assert _booster("cpu") == ref
 
 
 @pytest.mark.gpu
