@@ -1395,10 +1395,10 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     st = getattr(ws, "_levels", None)
     if st is None or st.max_depth != params.max_depth or st.n_sel != len(sel_ids):
         st = ws._levels = LevelState(Q, params.max_depth, len(sel_ids))
-    # the native runner: RF levels (any world size); GBDT single-process levels (whose prologue,
-    # split + plan and partition it fuses)
-    gbdt_native = NATIVE_LEVELS and dev.type == "cuda" and params.mode == 0 and shards is None and coll is None \
-        and weight is None and not build_all
+    # the native runner: RF levels and GBDT levels (any world size). A single process also fuses
+    # the GBDT prologue and the split + plan; under data parallelism the quantisation max is an
+    # all-reduce and the levels split around the reduce-scatter / all-gather
+    gbdt_native = NATIVE_LEVELS and dev.type == "cuda" and params.mode == 0 and weight is None and not build_all
     # (the runner's level 0 completes the root's sums: at least one level)
     runner = _level_runner(Q, ws, st, params, item_groups, sampled) \
         if (NATIVE_LEVELS and dev.type == "cuda" and (sampled or gbdt_native) and params.max_depth >= 1) else None
