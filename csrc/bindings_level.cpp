@@ -79,6 +79,9 @@ class RfLevels {
     hot_row_ = get_opt(c, "hot_row");
     rowdig_ = get(c, "rowdig");
     rowpack_ = get_opt(c, "rowpack");
+    dig16_ = get_opt(c, "dig16");
+    if (dig16_) FDX_CHECK(dig16_->scalar_type() == at::kShort && dig16_->numel() >= row_node_.numel() &&
+                              reinterpret_cast<uintptr_t>(dig16_->data_ptr()) % 16 == 0, "dig16 [N] int16, 16-byte aligned");
     build_all_ = c["build_all"].cast<bool>();
     for (const char* k : {"arena_stats", "open0", "totals0", "kexp_slot"}) st_[k] = get(c, k);
     row_node_ = get(c, "row_node");
@@ -175,6 +178,7 @@ class RfLevels {
     a.row0 = row0;
     a.kexp_out = p<int32_t>(kexp_);
     a.rowdig = reinterpret_cast<uint32_t*>(p<int32_t>(rowdig_));
+    if (dig16_ && np == 1) a.dig16 = reinterpret_cast<uint16_t*>(dig16_->data_ptr());
     a.totals = p<int64_t>(totals);
     if (digp) {
       a.digp = p<uint8_t>(*digp);
@@ -540,8 +544,9 @@ class RfLevels {
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 
-  // Partition of level d (tree_partition_cols), writing the next level's packed row state when fuse.
-  void partition(int64_t d, int64_t n_open, bool fuse, const optional<Tensor>& zero) {
+  // Partition of level d (tree_partition_cols), writing the next level's packed row state when fuse
+  // (its count digits from dig16 when this tree's prologue ran here and wrote them: dig16).
+  void partition(int64_t d, int64_t n_open, bool fuse, const optional<Tensor>& zero, bool dig16) {
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
     fdx::PartitionArgs a{};
@@ -564,6 +569,7 @@ class RfLevels {
       FDX_CHECK(rowpack_.has_value(), "a fused partition writes the packed row state");
       a.pack_slot = p<int32_t>(st_["node_slot"]);
       a.pack_dig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
+      if (dig16_ && dig16) a.pack_dig16 = reinterpret_cast<const uint16_t*>(dig16_->data_ptr());
       a.pack = reinterpret_cast<uint32_t*>(p<int32_t>(*rowpack_));
     }
     if (zero) {
@@ -587,7 +593,7 @@ class RfLevels {
 
   std::vector<ItemGroup> groups_;
   Tensor csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, row_node_, kexp_;
-  optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_;
+  optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_, dig16_;
   std::map<std::string, Tensor> st_;
   Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_, ticket_, parts_, maxv_, part_gain_, part_f_;
   fdx::SplitArgs last_split_{};           // the last search (its partials feed the best-split pass)

@@ -91,6 +91,7 @@ struct QuantArgs {
   // workgroup 0 writes open[0], the exponents and zeroes root_parts_clear (the next tree's slots).
   // The level-0 split search and plan sum the slots themselves (SplitArgs / LevelPlanArgs
   // root_parts) -- no grid-wide completion test and no reduction launch.
+  uint16_t* dig16;            // optional (np == 1): [N] the row's two count digits (byte 0: q0, byte 1: q1)
   int32_t atomic_root;
   int64_t* root_parts;        // [kRootSlots][kRootStride] (words 0, 1: the two sums)
   int64_t* root_parts_clear;
@@ -517,6 +518,8 @@ struct PartitionArgs {
   const int32_t* pack_slot;
   const uint32_t* pack_dig;
   uint32_t* pack;
+  // ... or the digits as [N] uint16 (QuantArgs dig16: 2 bytes a row read instead of 8)
+  const uint16_t* pack_dig16;
   // optional: zero this int64 range on the way (the next level's histograms: no fill launch)
   int64_t* zero;
   int64_t zero_n;
@@ -525,6 +528,7 @@ struct PartitionArgs {
 FDX_HD uint32_t partition_pack_word(const PartitionArgs& a, int32_t node, int64_t r) {
   const int32_t s = (node >= 0 && node < a.num_nodes) ? a.pack_slot[node] : -1;
   const uint32_t sb = (s >= 0 && s < 255) ? (uint32_t)s : 0xffu;
+  if (a.pack_dig16) return sb | ((uint32_t)a.pack_dig16[r] << 8);
   const uint32_t d0 = a.pack_dig[2 * r], d1 = a.pack_dig[2 * r + 1];
   return sb | ((d0 & 0xffu) << 8) | ((d1 & 0xffu) << 16);
 }

@@ -239,6 +239,7 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
       d.x = a.np == 1 ? digits1(q0) : digits4(q0);
       d.y = a.np == 1 ? digits1(q1) : digits4(q1);
       reinterpret_cast<uint2*>(a.rowdig)[r] = d;
+      if (a.dig16) a.dig16[r] = (uint16_t)((d.x & 0xffu) | ((d.y & 0xffu) << 8));
       if (a.row_node) a.row_node[r] = 0;
       if (a.digp) {
         for (int p = 0; p < a.np; ++p) {
@@ -1227,7 +1228,20 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
       for (int k = 0; k < kPartRows; ++k) n[k] = c[k] >= 0 ? c[k] : n[k];
       p[0] = make_int4(n[0], n[1], n[2], n[3]);
       p[1] = make_int4(n[4], n[5], n[6], n[7]);
-      if (a.pack != nullptr) {
+      if (a.pack != nullptr && a.pack_dig16 != nullptr) {
+        // the next level's packed row state (8 rows: 16 B of count digits in, 32 B out)
+        const int4 dg = *reinterpret_cast<const int4*>(a.pack_dig16 + r0);
+        const uint32_t dw[4] = {(uint32_t)dg.x, (uint32_t)dg.y, (uint32_t)dg.z, (uint32_t)dg.w};
+        uint32_t w[kPartRows];
+#pragma unroll
+        for (int k = 0; k < kPartRows; ++k) {
+          const int32_t sk = (n[k] >= 0 && n[k] < a.num_nodes) ? a.pack_slot[n[k]] : -1;
+          w[k] = ((sk >= 0 && sk < 255) ? (uint32_t)sk : 0xffu) | (((dw[k >> 1] >> (16 * (k & 1))) & 0xffffu) << 8);
+        }
+        int4* q = reinterpret_cast<int4*>(a.pack + r0);
+        q[0] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+        q[1] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
+      } else if (a.pack != nullptr) {
         // the next level's packed row state (8 rows: 64 B of digit words in, 32 B out)
         const int4* dg = reinterpret_cast<const int4*>(a.pack_dig + 2 * r0);
         uint32_t w[kPartRows];

@@ -395,6 +395,13 @@ class Workspace:
             self._rg_emdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
         return self._rg_emdig
 
+    def dig16(self) -> torch.Tensor:
+        """[N] int16: the rows' two class-count digits (RF), written by the runner's quantisation
+        for the fused partition's packed row state (2 bytes a row instead of the 8-byte word)."""
+        if getattr(self, "_dig16", None) is None:
+            self._dig16 = torch.empty(self.Q.n_rows + 8, dtype=torch.int16, device=self.dev)
+        return self._dig16
+
     def rowpack(self) -> torch.Tensor:
         """[N] int32 packed row state of the sampled (RF) passes: slot | class-count digits << 8."""
         if getattr(self, "_rowpack", None) is None:
@@ -1185,7 +1192,7 @@ def _level_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowPar
                sub_par=st.sub_par, sub_sib=st.sub_sib, node_dense=st.node_dense, mode=int(params.mode),
                max_depth=int(params.max_depth), min_gain=float(params.min_gain), lambda_=float(params.lambda_),
                mcw=float(params.min_child), seed=int(params.seed), F=int(Q.num_features), k=int(params.feat_k),
-               lds=bool(RF_LDS), wps=int(PARTITION_WPS), arena=st.arena)
+               lds=bool(RF_LDS), wps=int(PARTITION_WPS), arena=st.arena, dig16=ws.dig16() if sampled else None)
     runner = native.lib().RfLevels(cfg)
     ws._rf_runner = (st, key, runner)
     return runner
@@ -1352,7 +1359,7 @@ def _rf_runner_levels(Q, ws, st, params, tree_index, seed, shards, runner, sel_i
             # partition kernel on the way
             pre_hist = zero = torch.empty((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
         with tracing.span("tree.partition"):
-            runner.partition(d, n_open, more, zero)
+            runner.partition(d, n_open, more, zero, native_prologue)
     return on_first_wait
 
 
@@ -1726,7 +1733,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 # the next level's histograms, zeroed by the partition kernel on the way
                 pre_hist = zero = torch.empty((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
             with tracing.span("tree.partition"):
-                runner.partition(d, n_open, bool(sampled and FUSED_PACK and more), zero)
+                runner.partition(d, n_open, bool(sampled and FUSED_PACK and more), zero, native_prologue and sampled)
             prev_hist = cur_hist
             prev_row_of = row_of
             continue
