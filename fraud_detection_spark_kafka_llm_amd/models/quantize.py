@@ -29,6 +29,7 @@ holds identical bins.
 from __future__ import annotations
 
 import os
+import time
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -734,6 +735,29 @@ def _finish_items(Q: Quantized, chunk: int = 0, super_rows: int = SUPER_ROWS, ho
     Q._items_pending = (chunk, super_rows, hot)
 
 
+class _Checkpoints:
+    """FDX_ITEMS_TIMING=1: synchronised wall time between named points of _build_items, printed
+    once at its end (diagnostics: bench/probes/items_profile.py)."""
+
+    def __init__(self):
+        self.on = os.environ.get("FDX_ITEMS_TIMING") == "1"
+        self.t = time.perf_counter()
+        self.parts = []
+
+    def __call__(self, name):
+        if not self.on:
+            return
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        t = time.perf_counter()
+        self.parts.append((name, round(1e3 * (t - self.t), 2)))
+        self.t = t
+
+    def report(self):
+        if self.on:
+            print("items timing (ms):", self.parts, flush=True)
+
+
 def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> None:
     """The histogram CSC and work items of the CSC passes (first use of Q.groups & co.)."""
     from ..ops import native
@@ -741,12 +765,14 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
     C = native.lib()
     dev = Q.device
     colptr = Q.colptr.cpu().numpy().astype(np.int64)
+    ck = _Checkpoints()
     n = np.diff(colptr)
     nb = Q.nbins.cpu().numpy().astype(np.int64)
     Fa = int(nb.size)
     # hot features stay in the histogram CSC too (deep levels use it: only their live entries are
     # multiplied there, while the dense kernel masks every row); they are never packed
     cols = np.nonzero(n > 0)[0]
+    ck("host_cols")
     sp_b = tracing.span("q.bounds")
     sp_b.__enter__()
     nsb = max(1, (Q.n_rows + super_rows - 1) // super_rows)
@@ -764,6 +790,7 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
         bounds = torch.empty((S, nsb + 1), dtype=torch.int64, device=dev)
         with tracing.span("q.bsearch"):
             C.block_bounds(Q.csc_row, Q.colptr, cols_t, int(nsb), int(sb_rows), bounds)
+        ck("bsearch")
         bounds[:, -1] = Q.colptr[cols_t.to(torch.int64) + 1]
         if light.any() and nsb > 1:
             li = torch.from_numpy(np.nonzero(light)[0]).to(dev)
@@ -773,13 +800,16 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
         flat = seg_len.reshape(-1)
         seg_dst = torch.cumsum(flat, 0) - flat
         total = int(flat.sum())
+        ck("segments")
         with tracing.span("q.alloc"):
             h_row = torch.zeros(total + CSC_PAD, dtype=torch.int32, device=dev)
             h_key = torch.full((total + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
+        ck("alloc")
         hptr = np.zeros((nsb, S + 1), dtype=np.int64)                  # [sb][i] start of cols[i] in super-block sb
         dst_host = seg_dst.cpu().numpy().reshape(nsb, S)
         hptr[:, :S] = dst_host
         hptr[:, S] = np.append(dst_host[1:, 0], total) if nsb > 1 else total
+        ck("d2h_dst")
         seg_n = seg_len.cpu().numpy()                                  # [nsb, S]
     else:
         h_row = torch.zeros(CSC_PAD, dtype=torch.int32, device=dev)
@@ -788,6 +818,7 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
         seg_n = np.zeros((nsb, 0), dtype=np.int64)
     total = int(hptr[-1, -1]) if S else 0
     sp_b.__exit__(None, None, None)
+    ck("d2h_len")
     sp_p = tracing.span("q.pack")
     sp_p.__enter__()
     # --- packing (global: the same kbase in every super-block)
@@ -816,6 +847,7 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
                           np.tile(i1s - i0s, nsb), np.zeros(nsb * G, np.int64), np.tile(bts, nsb),
                           np.repeat(np.arange(nsb), G)], 1)
         parts.append(_split_long(rows_[rows_[:, 1] > rows_[:, 0]], chunk))
+    ck("pack_runs")
     single = np.nonzero(~packable)[0]
     if single.size:
         a0 = hptr[:, single].reshape(-1)                   # [nsb * len(single)]
@@ -835,6 +867,7 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
             m = int(sel.sum())
             parts.append(np.stack([st[sel], en[sel], f_[sel], np.full(m, 8), np.ones(m, np.int64),
                                    np.full(m, 64 * w), btw, b_[sel]], 1))
+    ck("singles")
     items = np.concatenate(parts) if parts else np.zeros((0, 8), np.int64)
     if items.shape[0] and light.any():
         # items holding a whole (light) column: spread over the XCDs (row block -1)
@@ -842,11 +875,13 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
         f0, nf = items[:, 2], items[:, 4]
         items[(cl[f0 + nf] - cl[f0]) > 0, 7] = -1
     sp_p.__exit__(None, None, None)
+    ck("items")
     # --- the histogram CSC: (row, kbase + bin) of every (super-block, feature) segment
     if S:
         with tracing.span("q.copy"):
             kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev) if kbase.any() else None
             C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total], kb)
+    ck("copy")
     sp_g = tracing.span("q.groups")
     sp_g.__enter__()
     arr = np.asarray(items, dtype=np.int64)
@@ -858,8 +893,10 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
         for bt in (1, 2, 4):
             ix = np.nonzero(sel & (arr[:, 6] == bt))[0]
             sels.append((sel is is_hot, bt, ix[np.argsort(arr[ix, 0], kind="stable")]))
+    ck("group_sort")
     arr_d = _h2d(arr, dev)
     all_ix = _h2d(np.concatenate([ix for _, _, ix in sels]) if sels else np.zeros(0, np.int64), dev)
+    ck("h2d")
     groups = {False: [], True: []}
     o = 0
     for hot_sel, bt, ix in sels:
@@ -877,3 +914,5 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
     Q._n_super = nsb
     Q._kbase_host = kbase.astype(np.int32)
     Q._kbase = torch.from_numpy(Q._kbase_host).to(dev)
+    ck("groups")
+    ck.report()
