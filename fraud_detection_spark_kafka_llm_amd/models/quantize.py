@@ -90,15 +90,6 @@ class ItemGroup:
         return self._order
 
 
-def _h2d(x: np.ndarray, dev) -> torch.Tensor:
-    """Host array -> device through a pinned staging copy (one async DMA instead of ROCm's
-    synchronous pageable path)."""
-    t = torch.from_numpy(np.ascontiguousarray(x))
-    if torch.device(dev).type != "cuda":
-        return t.to(dev)
-    return t.pin_memory().to(dev, non_blocking=True)
-
-
 def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.Tensor:
     """XCD-aware item placement. Workgroups are dealt round-robin over the 8 XCDs (observed
     dispatch, speed only), so workgroups b and b + 8 share an L2: the 4 wave slots of workgroup
@@ -698,20 +689,17 @@ LIGHT_ENTRIES = int(os.environ.get("FDX_LIGHT_ENTRIES", 0))    # whole-column it
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
 
-def _split_long(rows_: np.ndarray, chunk: int) -> np.ndarray:
-    """Items (start, end, ...) longer than ``chunk`` entries -> consecutive pieces of <= chunk (a
-    packed run can gather more than ``chunk`` entries inside one super-block; item sums are
-    order-free, so any split gives the same histogram)."""
-    ln = rows_[:, 1] - rows_[:, 0]
-    if rows_.shape[0] == 0 or int(ln.max()) <= chunk:
-        return rows_
-    nc = (ln + chunk - 1) // chunk
-    rep = np.repeat(np.arange(rows_.shape[0]), nc)
-    k = np.arange(rep.size) - np.repeat(np.cumsum(nc) - nc, nc)
-    out = rows_[rep].copy()
-    out[:, 0] = rows_[rep, 0] + k * chunk
-    out[:, 1] = np.minimum(out[:, 0] + chunk, rows_[rep, 1])
-    return out
+def _split_items(st: torch.Tensor, en: torch.Tensor, per: torch.Tensor, blk: torch.Tensor, chunk: int) -> torch.Tensor:
+    """Entry ranges [st, en) -> consecutive pieces of <= ``chunk`` entries, as item rows
+    (start, end, *per, blk) -- per: [m, 5] (f0, sl2, nfeat, koff, bt) or [m, 1] (f0 only); item
+    sums are order-free, so any split gives the same histogram. On the ranges' device."""
+    nc = (en - st + chunk - 1) // chunk
+    total = int(nc.sum())
+    rep = torch.repeat_interleave(torch.arange(st.numel(), device=st.device), nc, output_size=total)
+    k = torch.arange(total, device=st.device) - (torch.cumsum(nc, 0) - nc)[rep]
+    s0 = st[rep] + k * chunk
+    e0 = torch.minimum(s0 + chunk, en[rep])
+    return torch.cat([s0[:, None], e0[:, None], per[rep], blk[rep][:, None]], 1)
 
 
 def _finish_items(Q: Quantized, chunk: int = 0, super_rows: int = SUPER_ROWS, hot_density: float = HOT_DENSITY) \
@@ -805,18 +793,21 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
             h_row = torch.zeros(total + CSC_PAD, dtype=torch.int32, device=dev)
             h_key = torch.full((total + CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
         ck("alloc")
-        hptr = np.zeros((nsb, S + 1), dtype=np.int64)                  # [sb][i] start of cols[i] in super-block sb
-        dst_host = seg_dst.cpu().numpy().reshape(nsb, S)
-        hptr[:, :S] = dst_host
-        hptr[:, S] = np.append(dst_host[1:, 0], total) if nsb > 1 else total
-        ck("d2h_dst")
-        seg_n = seg_len.cpu().numpy()                                  # [nsb, S]
+        # [sb][i] start of cols[i] in super-block sb (on the device: the item table is built there,
+        # no [nsb, S] host copies -- fresh host arrays of that size cost ~100 ms of page faults in
+        # a process's first fit, profiles/r5/NOTES.md)
+        hptr = torch.empty((nsb, S + 1), dtype=torch.int64, device=dev)
+        hptr[:, :S] = seg_dst.view(nsb, S)
+        if nsb > 1:
+            hptr[:-1, S] = hptr[1:, 0]
+        hptr[-1, S] = total
+        seg_n = seg_len                                                 # [nsb, S]
     else:
         h_row = torch.zeros(CSC_PAD, dtype=torch.int32, device=dev)
         h_key = torch.full((CSC_PAD,), 0xFF, dtype=torch.uint8, device=dev)
-        hptr = np.zeros((nsb, 1), dtype=np.int64)
-        seg_n = np.zeros((nsb, 0), dtype=np.int64)
-    total = int(hptr[-1, -1]) if S else 0
+        hptr = torch.zeros((nsb, 1), dtype=torch.int64, device=dev)
+        seg_n = torch.zeros((nsb, 0), dtype=torch.int64, device=dev)
+        total = 0
     sp_b.__exit__(None, None, None)
     ck("d2h_len")
     sp_p = tracing.span("q.pack")
@@ -835,43 +826,48 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
         run_len = gp[:, 1] - gp[:, 0]
         pos = np.arange(int(run_len.sum())) - np.repeat(np.cumsum(run_len) - run_len, run_len)
         kbase[cols[np.repeat(gp[:, 0], run_len) + pos]] = pos << np.repeat(gp[:, 2], run_len)
-    parts = []   # arrays of (start, end, f0, sl2, nfeat, koff, bt, blk)
+    L = lambda x: torch.from_numpy(np.ascontiguousarray(x, dtype=np.int64)).to(dev)   # noqa: E731
+    sb_ids = torch.arange(nsb, dtype=torch.int64, device=dev)
+    parts = []   # [m, 8] int64 (start, end, f0, sl2, nfeat, koff, bt, blk)
     if gp.shape[0]:
         i0s, i1s, sl2s = gp[:, 0], gp[:, 1], gp[:, 2]
         keys = (i1s - i0s) << sl2s
         bts = np.where(keys <= 16, 1, np.where(keys <= 32, 2, 4))
-        a = hptr[:, i0s]                                   # [nsb, G]: consecutive features are contiguous
-        e = hptr[:, i1s - 1] + seg_n[:, i1s - 1]
         G = gp.shape[0]
-        rows_ = np.stack([a.reshape(-1), e.reshape(-1), np.tile(cols[i0s], nsb), np.tile(sl2s, nsb),
-                          np.tile(i1s - i0s, nsb), np.zeros(nsb * G, np.int64), np.tile(bts, nsb),
-                          np.repeat(np.arange(nsb), G)], 1)
-        parts.append(_split_long(rows_[rows_[:, 1] > rows_[:, 0]], chunk))
+        st = hptr[:, L(i0s)].reshape(-1)                   # [nsb, G]: consecutive features are contiguous
+        en = (hptr[:, L(i1s - 1)] + seg_n[:, L(i1s - 1)]).reshape(-1)
+        per = torch.stack([L(cols[i0s]), L(sl2s), L(i1s - i0s), torch.zeros(G, dtype=torch.int64, device=dev),
+                           L(bts)], 1).repeat(nsb, 1)      # [nsb * G, 5] (f0, sl2, nfeat, koff, bt)
+        blk = sb_ids.repeat_interleave(G)
+        keep = en > st
+        parts.append(_split_items(st[keep], en[keep], per[keep], blk[keep], chunk))
     ck("pack_runs")
     single = np.nonzero(~packable)[0]
     if single.size:
-        a0 = hptr[:, single].reshape(-1)                   # [nsb * len(single)]
-        ln = seg_n[:, single].reshape(-1)
-        fs = np.tile(cols[single], nsb)
-        bk = np.repeat(np.arange(nsb), single.size)
-        nc = (ln + chunk - 1) // chunk
-        seg = np.repeat(np.arange(ln.size), nc)
-        k = np.arange(seg.size) - np.repeat(np.cumsum(nc) - nc, nc)
-        st = a0[seg] + k * chunk
-        en = np.minimum(st + chunk, a0[seg] + ln[seg])
-        f_, b_ = fs[seg], bk[seg]
-        for w in range(int((nb[f_].max() + 63) // 64) if f_.size else 0):
-            sel = nb[f_] > 64 * w
-            nbw = np.minimum(nb[f_[sel]] - 64 * w, 64)
-            btw = np.where(nbw <= 16, 1, np.where(nbw <= 32, 2, 4))
-            m = int(sel.sum())
-            parts.append(np.stack([st[sel], en[sel], f_[sel], np.full(m, 8), np.ones(m, np.int64),
-                                   np.full(m, 64 * w), btw, b_[sel]], 1))
+        sg = L(single)
+        st = hptr[:, sg].reshape(-1)                       # [nsb * len(single)]
+        ln = seg_n[:, sg].reshape(-1)
+        f_all = L(cols[single]).repeat(nsb)
+        b_all = sb_ids.repeat_interleave(single.size)
+        nbs = L(nb)
+        keep = ln > 0
+        one = torch.ones(1, dtype=torch.int64, device=dev)
+        z = torch.zeros(1, dtype=torch.int64, device=dev)
+        pieces = _split_items(st[keep], st[keep] + ln[keep], f_all[keep][:, None], b_all[keep], chunk)
+        f_ = pieces[:, 2]
+        for w in range(int((int(nb[cols[single]].max()) + 63) // 64)):
+            sel = nbs[f_] > 64 * w
+            pw = pieces[sel]
+            nbw = torch.clamp(nbs[pw[:, 2]] - 64 * w, max=64)
+            btw = torch.where(nbw <= 16, one, torch.where(nbw <= 32, one * 2, one * 4))
+            m = pw.shape[0]
+            parts.append(torch.stack([pw[:, 0], pw[:, 1], pw[:, 2], (z + 8).expand(m), one.expand(m),
+                                      (z + 64 * w).expand(m), btw, pw[:, 3]], 1))
     ck("singles")
-    items = np.concatenate(parts) if parts else np.zeros((0, 8), np.int64)
+    items = torch.cat(parts) if parts else torch.zeros((0, 8), dtype=torch.int64, device=dev)
     if items.shape[0] and light.any():
         # items holding a whole (light) column: spread over the XCDs (row block -1)
-        cl = np.concatenate([[0], np.cumsum(np.isin(np.arange(Fa), cols[light]))])
+        cl = L(np.concatenate([[0], np.cumsum(np.isin(np.arange(Fa), cols[light]))]))
         f0, nf = items[:, 2], items[:, 4]
         items[(cl[f0 + nf] - cl[f0]) > 0, 7] = -1
     sp_p.__exit__(None, None, None)
@@ -884,28 +880,22 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
     ck("copy")
     sp_g = tracing.span("q.groups")
     sp_g.__enter__()
-    arr = np.asarray(items, dtype=np.int64)
-    is_hot = hot[arr[:, 2]] & (arr[:, 4] == 1) if arr.shape[0] else np.zeros(0, bool)
-    # the item table and every group's row order (by entry offset; the parts are sorted runs, so
-    # the stable host sort is linear) go up in two pinned copies instead of five per group
-    sels = []
-    for sel in (~is_hot, is_hot):
-        for bt in (1, 2, 4):
-            ix = np.nonzero(sel & (arr[:, 6] == bt))[0]
-            sels.append((sel is is_hot, bt, ix[np.argsort(arr[ix, 0], kind="stable")]))
-    ck("group_sort")
-    arr_d = _h2d(arr, dev)
-    all_ix = _h2d(np.concatenate([ix for _, _, ix in sels]) if sels else np.zeros(0, np.int64), dev)
-    ck("h2d")
+    hot_d = torch.from_numpy(hot.astype(np.bool_)).to(dev)
+    is_hot = hot_d[items[:, 2]] & (items[:, 4] == 1)
     groups = {False: [], True: []}
-    o = 0
-    for hot_sel, bt, ix in sels:
-        if ix.size:
-            g = arr_d[all_ix[o:o + ix.size]]
+    # every group's items ordered by entry offset (stable: ties keep the table order)
+    for hot_sel in (False, True):
+        sel_h = is_hot if hot_sel else ~is_hot
+        for bt in (1, 2, 4):
+            ix = torch.nonzero(sel_h & (items[:, 6] == bt)).flatten()
+            if ix.numel() == 0:
+                continue
+            ix = ix[torch.sort(items[ix, 0], stable=True).indices]
+            g = items[ix]
             meta = g[:, 3] | (g[:, 4] << 8) | (g[:, 5] << 16)
             groups[hot_sel].append(ItemGroup(bt, g[:, 0].contiguous(), g[:, 1].contiguous(), g[:, 2].to(torch.int32),
                                              meta.to(torch.int32), g[:, 7].to(torch.int32)))
-        o += ix.size
+    ck("group_sort")
 
     Q._groups = groups[False]
     Q._hot_groups = groups[True]
