@@ -685,6 +685,7 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
     Q.dense = dense
 
 
+COPY_PIECE = 8192      # entries per workgroup of the histogram CSC copy
 LIGHT_ENTRIES = int(os.environ.get("FDX_LIGHT_ENTRIES", 0))    # whole-column items up to this many entries (0: off; profiles/r4/rf500_light_entries_sweep.txt)
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
@@ -876,7 +877,19 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
     if S:
         with tracing.span("q.copy"):
             kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev) if kbase.any() else None
-            C.copy_segments(Q.csc_row, Q.csc_bin, seg_src.reshape(-1), seg_dst, flat, h_row[:total], h_key[:total], kb)
+            # a workgroup per <= COPY_PIECE entries: the hot features' segments hold ~10^5 entries
+            # each, and a workgroup per segment left the copy to its longest ones (~20 ms at 10M rows)
+            src_p, dst_p, len_p = seg_src.reshape(-1), seg_dst, flat
+            npc = (len_p + COPY_PIECE - 1) // COPY_PIECE
+            npieces = int(npc.sum())
+            if npieces > len_p.numel():
+                rep = torch.repeat_interleave(torch.arange(len_p.numel(), device=dev), npc, output_size=npieces)
+                k = (torch.arange(npieces, device=dev) - (torch.cumsum(npc, 0) - npc)[rep]) * COPY_PIECE
+                src_p, dst_p = src_p[rep] + k, dst_p[rep] + k
+                len_p = torch.minimum(len_p[rep] - k, torch.full_like(k, COPY_PIECE))
+                kb = kb[rep] if kb is not None else None
+            C.copy_segments(Q.csc_row, Q.csc_bin, src_p.contiguous(), dst_p.contiguous(), len_p.contiguous(),
+                            h_row[:total], h_key[:total], kb.contiguous() if kb is not None else None)
     ck("copy")
     sp_g = tracing.span("q.groups")
     sp_g.__enter__()

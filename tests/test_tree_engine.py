@@ -803,3 +803,19 @@ def test_gpu_wide_feature_split_search_equals_host(mode, rf):
     if mode != 2:
         same(out[("cpu", False)], out[("cuda:0", True)])
     assert (out[("cpu", False)][1] >= 0).any()
+
+
+def test_histogram_csc_copy_pieces(monkeypatch):
+    """The histogram CSC copy split into fixed-size pieces (quantize.COPY_PIECE) writes the same
+    layout as one workgroup per segment."""
+    from fraud_detection_spark_kafka_llm_amd.models import quantize as qmod
+
+    dense, _ = random_counts_matrix(2000, 40, 0.3, 9)
+    ref = quantize(vc_from_dense(dense), max_bins=32, **QKW)
+    _ = ref.groups
+    monkeypatch.setattr(qmod, "COPY_PIECE", 7)
+    got = quantize(vc_from_dense(dense), max_bins=32, **QKW)
+    _ = got.groups
+    assert torch.equal(ref.h_row, got.h_row) and torch.equal(ref.h_key, got.h_key)
+    for a, b in zip(ref.groups + ref.hot_groups, got.groups + got.hot_groups):
+        assert torch.equal(a.item_start, b.item_start) and torch.equal(a.item_meta, b.item_meta)
