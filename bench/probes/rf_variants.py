@@ -21,7 +21,6 @@ import torch
 from suite import _tfidf
 from fraud_detection_spark_kafka_llm_amd.models import forest_batch, grower
 from fraud_detection_spark_kafka_llm_amd.models import quantize as qmod
-from fraud_detection_spark_kafka_llm_amd.utils import gc_pause
 from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
 from fraud_detection_spark_kafka_llm_amd.models.warmup import warm_tree_kernels
 
@@ -43,7 +42,6 @@ VARIANTS = {
     "nolean": {(grower, "LEAN_RF"): False},
     "presel_all": {(grower, "PRESELECT_MIN_ROWS"): 0},
     "presel_4m": {(grower, "PRESELECT_MIN_ROWS"): 4_000_000},
-    "gcon": {(gc_pause, "ENABLED"): False},
     "chunk2k": {(qmod, "CHUNK"): 2048},
     "chunk4k": {(qmod, "CHUNK"): 4096},
     "chunk8k": {(qmod, "CHUNK"): 8192},

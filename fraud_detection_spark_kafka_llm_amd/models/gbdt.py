@@ -31,7 +31,6 @@ from ..ml.tree_model import Tree
 from ..ops import native
 from ..parallel.dist import Collectives
 from ..utils import tracing
-from ..utils.gc_pause import gc_paused
 from .grower import GrowParams, PendingTree, Workspace, grow_tree
 from .tree import prepare
 
@@ -126,34 +125,33 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
     # the GPU (its leaf values come from the device node table, bitwise the host's)
     defer = eval_fn is None and checkpoint is None and ckpt is None
     pending = None
-    with gc_paused():      # (the round loop's short-lived objects: utils/gc_pause.py)
-        for t in range(len(trees), params.n_estimators):
-            with tracing.span("gbdt.round", round=t):
-                # the round's gradients: computed inside the tree's prologue (fused with the max |g|,
-                # |h| pass on the device loop's native runner) from the margins and labels
-                res = grow_tree(Q, ws, gp, t, label=y, weight=w, coll=coll, deferred=defer, margin=margin,
-                                on_first_wait=pending.finish if pending is not None else None)
-                if pending is not None:
-                    trees.append(pending.result().compacted())
-                    pending = None
-                if isinstance(res, PendingTree):
-                    res.update_margin(margin, ws.row_node)
-                    pending = res
-                    maybe_fail(t, model="gbdt")
-                    continue
-                tree = res
-                node_value = torch.from_numpy(np.ascontiguousarray(tree.stats[:, 0])).to(dev)
-                C.tree_leaf_update(margin, ws.row_node, node_value)
-            trees.append(tree.compacted())
-            if eval_fn is not None:
-                history.append(eval_fn(t, trees, margin))
-            if checkpoint is not None:
-                checkpoint(t, trees, base)
-            if ckpt is not None:
-                ckpt.maybe_save(len(trees), trees, base, F, params, force=len(trees) == params.n_estimators)
-            maybe_fail(t, model="gbdt")
-        if pending is not None:
-            trees.append(pending.result().compacted())
+    for t in range(len(trees), params.n_estimators):
+        with tracing.span("gbdt.round", round=t):
+            # the round's gradients: computed inside the tree's prologue (fused with the max |g|,
+            # |h| pass on the device loop's native runner) from the margins and labels
+            res = grow_tree(Q, ws, gp, t, label=y, weight=w, coll=coll, deferred=defer, margin=margin,
+                            on_first_wait=pending.finish if pending is not None else None)
+            if pending is not None:
+                trees.append(pending.result().compacted())
+                pending = None
+            if isinstance(res, PendingTree):
+                res.update_margin(margin, ws.row_node)
+                pending = res
+                maybe_fail(t, model="gbdt")
+                continue
+            tree = res
+            node_value = torch.from_numpy(np.ascontiguousarray(tree.stats[:, 0])).to(dev)
+            C.tree_leaf_update(margin, ws.row_node, node_value)
+        trees.append(tree.compacted())
+        if eval_fn is not None:
+            history.append(eval_fn(t, trees, margin))
+        if checkpoint is not None:
+            checkpoint(t, trees, base)
+        if ckpt is not None:
+            ckpt.maybe_save(len(trees), trees, base, F, params, force=len(trees) == params.n_estimators)
+        maybe_fail(t, model="gbdt")
+    if pending is not None:
+        trees.append(pending.result().compacted())
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0,

@@ -21,7 +21,6 @@ from ..ml.tree_model import Tree
 from ..parallel.dist import Collectives
 from ..utils.config import default_device
 from ..utils import tracing
-from ..utils.gc_pause import gc_paused
 from . import forest_batch
 from .forest_batch import ForestLanes, grow_forest_concurrent
 from .grower import GrowParams, Workspace, device_levels_ok, grow_tree
@@ -130,15 +129,6 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
         with tracing.span("forest.lanes"):
             lanes = ForestLanes(Q, min(inflight, num_trees - len(trees)), ws)
     chunk = max(ckpt.every if ckpt is not None else 64, 1)
-    with gc_paused():
-        trees = _grow_forest_trees(Q, ws, lanes, params, trees, num_trees, chunk, y, w, bootstrap, coll, ckpt, prune, F)
-    return ForestResult(trees, F, len(lanes.ws) if lanes is not None else 1)
-
-
-def _grow_forest_trees(Q, ws, lanes, params, trees, num_trees, chunk, y, w, bootstrap, coll, ckpt, prune, F):
-    """fit_forest's tree loop (checkpoints and fault injection included)."""
-    from ..parallel.checkpoint import maybe_fail
-
     t = len(trees)
     while t < num_trees:
         if lanes is not None:
@@ -156,4 +146,4 @@ def _grow_forest_trees(Q, ws, lanes, params, trees, num_trees, chunk, y, w, boot
                 ckpt.maybe_save(len(trees), trees, 0.0, F, None, force=crossed or len(trees) == num_trees)
             maybe_fail(tid, model="rf")
         t += len(ids)
-    return trees
+    return ForestResult(trees, F, len(lanes.ws) if lanes is not None else 1)
