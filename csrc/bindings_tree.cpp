@@ -640,7 +640,8 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
              const optional<Tensor>& listdig, int64_t nslots, const Tensor& gmode, const Tensor& wg,
              const Tensor& slot_node, const Tensor& hist, int64_t stride, const optional<Tensor>& shard_lo,
              int64_t shard_stride, int64_t dbg, const optional<Tensor>& erow, int64_t ebase,
-             const optional<Tensor>& emdig, int64_t em_min_rows) {
+             const optional<Tensor>& emdig, int64_t em_min_rows, const optional<Tensor>& part,
+             const optional<Tensor>& wg_first) {
   const auto dev = ptr.device();
   chk(ptr, dev, at::kInt, "ptr");
   chk(gbase, dev, at::kLong, "gbase");
@@ -717,6 +718,15 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
       FDX_CHECK(emdig->numel() >= 2 * N, "emdig must be [N, 2]");
       a.emdig = reinterpret_cast<const uint32_t*>(emdig->data_ptr<int32_t>());
     }
+  }
+  if (part && part->defined() && dev.is_cuda()) {     // (the host twin adds straight into hist)
+    FDX_CHECK(nslots == 1 && wg_first.has_value(), "partial tables: single-slot passes with wg_first");
+    chk(*part, dev, at::kLong, "part");
+    chk(*wg_first, dev, at::kInt, "wg_first");
+    FDX_CHECK(part->numel() >= 2 * a.n_wg * (int64_t)a.gbins && wg_first->numel() == G + 1 &&
+                  reinterpret_cast<uintptr_t>(part->data_ptr()) % 16 == 0, "part [n_wg, gbins, 2], wg_first [G + 1]");
+    a.part = part->data_ptr<int64_t>();
+    a.wg_first = wg_first->data_ptr<int32_t>();
   }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
@@ -1264,7 +1274,8 @@ void register_tree_ops(pybind11::module& m) {
         py::arg("rowdig"), py::arg("np"), py::arg("list"), py::arg("slot_start"), py::arg("listdig"),
         py::arg("nslots"), py::arg("gmode"), py::arg("wg"), py::arg("slot_node"), py::arg("hist"), py::arg("stride"),
         py::arg("shard_lo"), py::arg("shard_stride"), py::arg("dbg"), py::arg("erow") = py::none(),
-        py::arg("ebase") = 0, py::arg("emdig") = py::none(), py::arg("em_min_rows") = 0);
+        py::arg("ebase") = 0, py::arg("emdig") = py::none(), py::arg("em_min_rows") = 0,
+        py::arg("part") = py::none(), py::arg("wg_first") = py::none());
   m.def("tree_rg_erow", &rg_erow);
   m.def("tree_rg_list_rows", [](int64_t N) { return (int64_t)fdx::rg_list_rows(N); });
   m.def("tree_rf_sample", &rf_sample);

@@ -296,8 +296,25 @@ struct RgShared {
   uint32_t pb[kRgWaves][64];
 };
 
+// (part) workgroup w's table of a single-slot pass, every bin, zeros included
+template <int BINS>
+__device__ __forceinline__ void rg_store_part(const RgHistArgs& a, RgShared<BINS>& sh, int tid, bool zero) {
+  longlong2* dst = reinterpret_cast<longlong2*>(a.part) + (int64_t)blockIdx.x * BINS;
+  for (int i = tid; i < BINS; i += kRgThreads) {
+    dst[i] = zero ? make_longlong2(0, 0) : make_longlong2(sh.hg[i], sh.hh[i]);
+    if (!zero) {
+      sh.hg[i] = 0;
+      sh.hh[i] = 0;
+    }
+  }
+}
+
 template <int BINS>
 __device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS>& sh, int g, int s, int tid) {
+  if (a.part != nullptr) {
+    rg_store_part<BINS>(a, sh, tid, false);
+    return;
+  }
   const int64_t hrow = (a.dbg & 4) ? -1 : a.slot_node[s];          // dbg bit 2: no flush (timing)
   const int32_t* gbin = a.gbin + (int64_t)g * a.gbins;
   for (int i = tid; i < BINS; i += kRgThreads) {
@@ -624,7 +641,10 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
   if (T > 0 && rg_use_em(a, g, T)) {            // chunk p of the group's entries instead
     const int64_t E = a.ptr[(int64_t)g * (a.N + 1) + a.N];
     const int64_t e0 = E * p / np_g, e1 = E * (p + 1) / np_g;
-    if (e0 >= e1) return;
+    if (e0 >= e1) {
+      if (a.part != nullptr) rg_store_part<BINS>(a, sh, tid, true);
+      return;
+    }
     for (int i = tid; i < BINS; i += kRgThreads) {
       sh.hg[i] = 0;
       sh.hh[i] = 0;
@@ -639,7 +659,10 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
     return;
   }
   const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
-  if (a0 >= a1) return;
+  if (a0 >= a1) {
+    if (a.part != nullptr) rg_store_part<BINS>(a, sh, tid, true);
+    return;
+  }
   for (int i = tid; i < BINS; i += kRgThreads) {
     sh.hg[i] = 0;
     sh.hh[i] = 0;
@@ -721,6 +744,31 @@ void launch_rg_erow(const RgErowArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(rg_erow_kernel, dim3((unsigned)((a.N + 255) / 256), (unsigned)(a.G - a.g0)), dim3(256), 0, s, a);
 }
 
+namespace {
+// The single-slot pass's partial tables summed per group into the level histogram: a thread per
+// (group, local bin), its group's workgroups read in order (coalesced over the bins).
+__global__ __launch_bounds__(256) void rg_reduce_kernel(RgHistArgs a) {
+  const int g = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.gbins) return;
+  const int32_t col = a.gbin[(int64_t)g * a.gbins + i];
+  const int64_t hrow = a.slot_node[0];
+  if (col < 0 || hrow < 0) return;
+  const longlong2* part = reinterpret_cast<const longlong2*>(a.part);
+  int64_t s0 = 0, s1 = 0;
+  for (int w = a.wg_first[g]; w < a.wg_first[g + 1]; ++w) {
+    const longlong2 v = part[(int64_t)w * a.gbins + i];
+    s0 += v.x;
+    s1 += v.y;
+  }
+  if ((s0 | s1) == 0) return;
+  int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
+  atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)s0);
+  atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)s1);
+}
+
+}  // namespace
+
 void launch_rg_hist(const RgHistArgs& a, hipStream_t s) {
   const int64_t blocks = a.n_wg;
   if (blocks <= 0) return;
@@ -728,6 +776,8 @@ void launch_rg_hist(const RgHistArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(rg_hist_kernel<4096>, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
   else
     hipLaunchKernelGGL(rg_hist_kernel<8192>, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
+  if (a.part != nullptr && !(a.dbg & 4))
+    hipLaunchKernelGGL(rg_reduce_kernel, dim3((unsigned)((a.gbins + 255) / 256), (unsigned)a.G), dim3(256), 0, s, a);
 }
 
 }  // namespace fdx

@@ -314,6 +314,13 @@ struct RgHistArgs {
   int64_t ebase;
   const uint32_t* emdig;
   int64_t em_min_rows;
+  // optional, single-slot passes: workgroup w stores its whole LDS table to part[w][gbins][2]
+  // (plain stores) and rg_reduce_kernel sums the workgroups of each group (work-table entries
+  // wg_first[g] .. wg_first[g + 1]) into the level histogram, instead of every workgroup adding
+  // its table into the same bins with integer atomics (~30 % of the root pass at 1M rows with
+  // ~200 workgroups on the dense group, profiles/r5/NOTES.md)
+  int64_t* part;
+  const int32_t* wg_first;
 };
 
 // Whether group g of a pass listing T rows takes the entry-major pass.

@@ -311,6 +311,8 @@ FUSED_PACK = os.environ.get("FDX_RF_FUSED_PACK", "1") == "1"
 # RF device levels issue their kernels through the native per-level runner (csrc/bindings_level.cpp
 # RfLevels: hist / split / plan / partition, one host call each) instead of ~20 Python-level calls
 NATIVE_LEVELS = os.environ.get("FDX_NATIVE_LEVELS", "1") == "1"
+# single-slot row-group passes reduce per-workgroup partial tables (0: every workgroup's atomics)
+RG_PARTIALS = os.environ.get("FDX_RG_PARTIALS", "1") == "1"
 # sampled RF trees on the runner take the lean level loop (_rf_runner_levels; 0: the generic loop)
 LEAN_RF = os.environ.get("FDX_RF_LEAN", "1") == "1"
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
@@ -394,6 +396,14 @@ class Workspace:
         if getattr(self, "_rg_emdig", None) is None:
             self._rg_emdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
         return self._rg_emdig
+
+    def rg_part(self, rg) -> torch.Tensor:
+        """[n_wg, gbins, 2] int64 scratch of a single-slot row-group pass's partial tables."""
+        need = int(rg.work().shape[1]) * int(rg.gbin.shape[1]) * 2
+        t = getattr(self, "_rg_part", None)
+        if t is None or t.numel() < need:
+            t = self._rg_part = torch.empty(need, dtype=torch.int64, device=self.dev)
+        return t
 
     def dig16(self) -> torch.Tensor:
         """[N] int16: the rows' two class-count digits (RF), written by the runner's quantisation
@@ -1578,9 +1588,13 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             sel_groups = None
             if rg is not None:
                 shard_args = (shards.bin_lo, bufs.shard_bins) if shards is not None else (None, 0)
+                # single-slot passes: per-workgroup partial tables summed by one reduction instead
+                # of every workgroup's atomics on the same bins (RgHistArgs part)
+                part = dict(part=ws.rg_part(rg), wg_first=rg.work_first()) if (RG_PARTIALS and n_build == 1 and
+                                                                                 dev.type == "cuda") else {}
                 if d == 0:
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, None, 1, rg.gmode,
-                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG, **rg.em_args())
+                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG, **rg.em_args(), **part)
                 else:
                     # one built node: every row's digit words zeroed outside it, for the
                     # entry-major pass of the sparse groups (taken when the node is large)
@@ -1590,7 +1604,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                                    ws.rg_list, ws.rowdig, ws.rg_listdig, emdig)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    ws.rg_listdig, n_build, rg.gmode, rg.work(), s2n, hist_target, h_stride,
-                                   *shard_args, RG_DBG, **(rg.em_args(emdig) if emdig is not None else {}))
+                                   *shard_args, RG_DBG, **(rg.em_args(emdig) if emdig is not None else {}), **part)
                 sel_groups, use_dense = [], False
             if sel_groups is None:
                 sel_groups = Q.groups if use_dense else Q.groups + Q.hot_groups

@@ -296,6 +296,17 @@ class RowGroups:
             t = self._work[key] = torch.from_numpy(tab).to(self.gbase.device)
         return t
 
+    def work_first(self, target_wgs: int = 0, alpha: float = None) -> torch.Tensor:
+        """[G + 1] int32: the first work-table entry of each group (work() lists a group's chunks
+        consecutively), for the reduction of a single-slot pass's partial tables."""
+        tab = self.work(target_wgs, alpha)
+        key = ("first", tab.data_ptr())
+        t = self._work.get(key)
+        if t is None:
+            cnt = torch.bincount(tab[0].long(), minlength=self.G)
+            t = self._work[key] = torch.cat([cnt.new_zeros(1), torch.cumsum(cnt, 0)]).to(torch.int32)
+        return t
+
     @property
     def nbytes(self) -> int:
         em = self.erow.numel() * 4 if self.erow is not None else 0
