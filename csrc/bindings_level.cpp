@@ -546,7 +546,8 @@ class RfLevels {
 
   // Partition of level d (tree_partition_cols), writing the next level's packed row state when fuse
   // (its count digits from dig16 when this tree's prologue ran here and wrote them: dig16).
-  void partition(int64_t d, int64_t n_open, bool fuse, const optional<Tensor>& zero, bool dig16) {
+  void partition(int64_t d, int64_t n_open, bool fuse, const optional<Tensor>& zero, bool dig16,
+                 const optional<Tensor>& count_work) {
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
     fdx::PartitionArgs a{};
@@ -579,6 +580,13 @@ class RfLevels {
       a.zero_n = zero->numel();
     }
     const Tensor& counts = st_["counts"];
+    a.node_parent = p<int32_t>(st_["parent"]);    // (column pass first: the row pass sees final nodes)
+    if (count_work) {                                // the next level's row-list counts (RgListArgs pass 0)
+      FDX_CHECK(fdx::partition_counts_ok(a.N) && count_work->scalar_type() == at::kInt, "row-list counts: N / work");
+      a.count_work = p<int32_t>(*count_work);
+      a.count_slot = p<int32_t>(st_["node_slot"]);
+      a.count_nslots = p<int32_t>(counts) + d * counts.size(1) + 2;
+    }
     fdx::launch_partition_cols(a, p<int64_t>(colptr_), p<int32_t>(st_["cs_feat"]), p<int32_t>(counts) + d * counts.size(1),
                                (int32_t)n_open, (int32_t)wps_, s);
     C10_HIP_KERNEL_LAUNCH_CHECK();

@@ -580,7 +580,8 @@ void rg_build_csr(const Tensor& indptr, const Tensor& idx, const Tensor& counts,
 // words of the listed rows by list position.
 void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot, const optional<Tensor>& slot8,
              int64_t N, int64_t nslots, const Tensor& work, const Tensor& slot_start, const Tensor& list,
-             const optional<Tensor>& rowdig, const optional<Tensor>& listdig, const optional<Tensor>& masked) {
+             const optional<Tensor>& rowdig, const optional<Tensor>& listdig, const optional<Tensor>& masked,
+             bool counted) {
   const auto dev = list.device();
   chk(work, dev, at::kInt, "work");
   chk(slot_start, dev, at::kInt, "slot_start");
@@ -606,6 +607,7 @@ void rg_list(const optional<Tensor>& row_node, const optional<Tensor>& node_slot
   }
   a.N = N;
   a.nslots = (int32_t)nslots;
+  a.counted = counted ? 1 : 0;        // (the partition's row pass wrote pass 0's counts)
   a.slot_count = work.data_ptr<int32_t>();
   a.wave_count = a.slot_count + 2 * nslots;
   a.slot_start = slot_start.data_ptr<int32_t>();
@@ -1266,7 +1268,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rg_build", &rg_build);
   m.def("tree_rg_list", &rg_list, py::arg("row_node"), py::arg("node_slot"), py::arg("slot8"), py::arg("N"),
         py::arg("nslots"), py::arg("work"), py::arg("slot_start"), py::arg("list"), py::arg("rowdig"),
-        py::arg("listdig"), py::arg("masked") = py::none());
+        py::arg("listdig"), py::arg("masked") = py::none(), py::arg("counted") = false);
   m.def("tree_rg_build_csr", &rg_build_csr, py::arg("indptr"), py::arg("idx"), py::arg("counts"), py::arg("remap"),
         py::arg("max_bin"), py::arg("fgroup"), py::arg("flocal"), py::arg("ptr"), py::arg("gbase"), py::arg("ent"),
         py::arg("work"), py::arg("erow") = py::none(), py::arg("em_g0") = 0, py::arg("ebase") = 0);
@@ -1278,6 +1280,7 @@ void register_tree_ops(pybind11::module& m) {
         py::arg("part") = py::none(), py::arg("wg_first") = py::none());
   m.def("tree_rg_erow", &rg_erow);
   m.def("tree_rg_list_rows", [](int64_t N) { return (int64_t)fdx::rg_list_rows(N); });
+  m.def("tree_partition_counts_ok", &fdx::partition_counts_ok);
   m.def("tree_rf_sample", &rf_sample);
   m.def("tree_rf_compact", &rf_compact, py::arg("mask"), py::arg("nbins"), py::arg("fs"), py::arg("local"),
         py::arg("sizes"), py::arg("max_shard_features") = 0);

@@ -108,6 +108,9 @@ void launch_level_rows(const LevelRowsArgs& a, hipStream_t s);
 void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
                            int32_t max_splits, int32_t wps, hipStream_t s);
 struct SelectArgs;
+// the partition's row pass may write the next level's row-list counts (PartitionArgs count_work):
+// 512-row list waves and one grid pass over the rows
+bool partition_counts_ok(int64_t N);
 void launch_hist_select_groups(const SelectArgs& a, hipStream_t s);
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
                        int64_t f0, int64_t* out, hipStream_t s, const SplitArgs* partials = nullptr);

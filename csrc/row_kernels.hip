@@ -722,7 +722,7 @@ void launch_rg_list(const RgListArgs& a, hipStream_t s) {
   const int64_t waves = (a.N + rg_list_rows(a.N) - 1) / rg_list_rows(a.N);   // 4 per block
   const int64_t blocks = (waves + 3) / 4;
   if (blocks <= 0) return;
-  hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);
+  if (!a.counted) hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);
   hipLaunchKernelGGL(rg_list_scan_kernel, dim3((unsigned)a.nslots), dim3(1024), 0, s, a, waves);
   hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 1);
 }

@@ -265,6 +265,7 @@ struct RgListArgs {
   uint32_t* listdig;              //   listdig[2 pos + k] = rowdig[2 list[pos] + k] (coalesced in the pass)
   uint32_t* masked;               // optional [N * 2] (nslots == 1, with rowdig): pass 1 writes every
                                   //   row's digit words, zero outside slot 0 (the entry-major pass)
+  int32_t counted;                // pass 0's per-wave counts already written (PartitionArgs count_work)
 };
 
 FDX_HD uint32_t rg_slot_of(const RgListArgs& a, int64_t r) {
@@ -527,6 +528,16 @@ struct PartitionArgs {
   uint32_t* pack;
   // ... or the digits as [N] uint16 (QuantArgs dig16: 2 bytes a row read instead of 8)
   const uint16_t* pack_dig16;
+  // optional: the node table's parent array. Then the column pass runs FIRST (moving a split
+  // node's rows present in its column to the other child: row_node == parent[default child]) and
+  // the row pass second, so the row pass sees every row's final node -- it writes the packed
+  // state of all rows and, with count_work, the next level's per-wave slot counts (RgListArgs
+  // pass 0: count_work[2 ns + w ns + s] for the 512-row wave w, ns = *count_nslots slots of
+  // count_slot[node]) -- one pass over the rows less per level
+  const int32_t* node_parent;
+  int32_t* count_work;
+  const int32_t* count_slot;
+  const int32_t* count_nslots;
   // optional: zero this int64 range on the way (the next level's histograms: no fill launch)
   int64_t* zero;
   int64_t zero_n;

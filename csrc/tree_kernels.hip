@@ -1206,6 +1206,10 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
       z[i] = make_int4(0, 0, 0, 0);
   }
   const int64_t stride = (int64_t)gridDim.x * 256 * kPartRows;
+  uint32_t csl[kPartRows];                 // (count_work) the rows' next-level slots, 0xff: none
+#pragma unroll
+  for (int k = 0; k < kPartRows; ++k) csl[k] = 0xffu;
+  const int32_t cns = a.count_work != nullptr ? *a.count_nslots : 0;
   for (int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kPartRows; r0 < a.N; r0 += stride) {
     if (r0 + kPartRows <= a.N) {
       int4* p = reinterpret_cast<int4*>(a.row_node + r0);      // (row_node: 16-byte aligned, r0 % 8 == 0)
@@ -1228,6 +1232,13 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
       for (int k = 0; k < kPartRows; ++k) n[k] = c[k] >= 0 ? c[k] : n[k];
       p[0] = make_int4(n[0], n[1], n[2], n[3]);
       p[1] = make_int4(n[4], n[5], n[6], n[7]);
+      if (a.count_work != nullptr) {
+#pragma unroll
+        for (int k = 0; k < kPartRows; ++k) {
+          const int32_t sk = (n[k] >= 0 && n[k] < a.num_nodes) ? a.count_slot[n[k]] : -1;
+          csl[k] = (sk >= 0 && sk < cns) ? (uint32_t)sk : 0xffu;
+        }
+      }
       if (a.pack != nullptr && a.pack_dig16 != nullptr) {
         // the next level's packed row state (8 rows: 16 B of count digits in, 32 B out)
         const int4 dg = *reinterpret_cast<const int4*>(a.pack_dig16 + r0);
@@ -1267,8 +1278,31 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
           if (c >= 0) a.row_node[r] = n = c;
         }
         if (a.pack != nullptr) a.pack[r] = partition_pack_word(a, n, r);
+        if (a.count_work != nullptr) {
+          const int32_t sk = (n >= 0 && n < a.num_nodes) ? a.count_slot[n] : -1;
+          csl[r - r0] = (sk >= 0 && sk < cns) ? (uint32_t)sk : 0xffu;
+        }
       }
     }
+  }
+  if (a.count_work != nullptr) {
+    // the wave's 512 rows (64 lanes x 8, one grid pass: host-checked) = RgListArgs pass 0's wave
+    // w: per slot, its rows counted with ballots, lane s holding slot s's count
+    const int lane = threadIdx.x & 63;
+    const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (w * 64 * kPartRows >= a.N) return;       // (wave-uniform)
+    int32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPartRows; ++k) {
+      uint64_t act = __ballot(csl[k] != 0xffu);
+      while (act) {
+        const uint32_t sv = __shfl(csl[k], __ffsll((unsigned long long)act) - 1, 64);
+        const uint64_t m = __ballot(csl[k] == sv);
+        if ((uint32_t)lane == sv) cnt += __popcll(m);
+        act &= ~m;
+      }
+    }
+    if (lane < cns) a.count_work[2 * cns + w * cns + lane] = cnt;
   }
 }
 
@@ -1297,12 +1331,14 @@ __global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, co
   const bool left_default = a.split_left_is_default[sp] != 0;
   const int32_t f = cs_feat[sp];
   const int64_t e1 = colptr[f + 1];
+  // (column pass first: the rows are still at the split node; else at its default child)
+  const int32_t from = a.node_parent != nullptr ? a.node_parent[dflt] : dflt;
   for (int64_t e = colptr[f] + (int64_t)part * 256 + threadIdx.x; e < e1; e += (int64_t)wps * 256) {
     const int32_t row = a.csc_row[e];
     const bool left = (int32_t)a.csc_bin[e] <= thr;
-    if (left != left_default && a.row_node[row] == dflt) {
+    if (left != left_default && a.row_node[row] == from) {
       a.row_node[row] = other;
-      if (a.pack != nullptr) a.pack[row] = partition_pack_word(a, other, row);
+      if (a.pack != nullptr && a.node_parent == nullptr) a.pack[row] = partition_pack_word(a, other, row);
     }
   }
 }
@@ -1792,9 +1828,17 @@ void launch_level_plan(const LevelPlanArgs& a, hipStream_t s) {
 
 void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
                            int32_t max_splits, int32_t wps, hipStream_t s) {
+  const auto cols = [&] {
+    if (max_splits > 0)
+      hipLaunchKernelGGL(partition_cols_kernel, dim3(max_splits * wps), dim3(256), 0, s, a, colptr, cs_feat, n_cs, wps);
+  };
+  if (a.node_parent != nullptr) cols();   // (column pass first: PartitionArgs node_parent)
   if (a.N > 0) hipLaunchKernelGGL(partition_default_kernel, dim3(grid_for((a.N + kPartRows - 1) / kPartRows)), dim3(256), 0, s, a);
-  if (max_splits > 0)
-    hipLaunchKernelGGL(partition_cols_kernel, dim3(max_splits * wps), dim3(256), 0, s, a, colptr, cs_feat, n_cs, wps);
+  if (a.node_parent == nullptr) cols();
+}
+
+bool partition_counts_ok(int64_t N) {
+  return rg_list_rows(N) == 64 * kPartRows && (N + kPartRows - 1) / kPartRows <= 8192ll * 256;
 }
 
 void launch_logistic_grad(const double* margin, const float* label, const float* weight, float* g, float* h,

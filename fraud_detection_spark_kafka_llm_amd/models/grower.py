@@ -311,6 +311,8 @@ FUSED_PACK = os.environ.get("FDX_RF_FUSED_PACK", "1") == "1"
 # RF device levels issue their kernels through the native per-level runner (csrc/bindings_level.cpp
 # RfLevels: hist / split / plan / partition, one host call each) instead of ~20 Python-level calls
 NATIVE_LEVELS = os.environ.get("FDX_NATIVE_LEVELS", "1") == "1"
+# the partition's row pass writes the next level's row-list counts (runner levels, <= 4M rows)
+PARTITION_COUNTS = os.environ.get("FDX_PARTITION_COUNTS", "1") == "1"
 # single-slot row-group passes reduce per-workgroup partial tables (0: every workgroup's atomics)
 RG_PARTIALS = os.environ.get("FDX_RG_PARTIALS", "1") == "1"
 # sampled RF trees on the runner take the lean level loop (_rf_runner_levels; 0: the generic loop)
@@ -1369,7 +1371,7 @@ def _rf_runner_levels(Q, ws, st, params, tree_index, seed, shards, runner, sel_i
             # partition kernel on the way
             pre_hist = zero = torch.empty((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
         with tracing.span("tree.partition"):
-            runner.partition(d, n_open, more, zero, native_prologue)
+            runner.partition(d, n_open, more, zero, native_prologue, None)
     return on_first_wait
 
 
@@ -1479,6 +1481,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     n_open, n_build = 1, 1
     prev_hist = prev_row_of = None
     ev = None
+    rg_counted = False
     # RF under data parallelism: each level reduce-scatters only its sampled features' bins; level
     # d + 1's sample and layout are computed right after level d's plan, so their shard sizes reach
     # the host with the level's counts (one wait per level; the root's before the loop)
@@ -1601,7 +1604,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                     emdig = ws.rg_emdig() if (n_build == 1 and rg.erow is not None and qmod.RG_EM_MIN_FRAC <= 1.0) \
                         else None
                     C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
-                                   ws.rg_list, ws.rowdig, ws.rg_listdig, emdig)
+                                   ws.rg_list, ws.rowdig, ws.rg_listdig, emdig, counted=rg_counted)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    ws.rg_listdig, n_build, rg.gmode, rg.work(), s2n, hist_target, h_stride,
                                    *shard_args, RG_DBG, **(rg.em_args(emdig) if emdig is not None else {}), **part)
@@ -1746,8 +1749,11 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             if shards is None and more and not build_all:
                 # the next level's histograms, zeroed by the partition kernel on the way
                 pre_hist = zero = torch.empty((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
+            # the next level's row-list counts written by the partition's row pass (one pass less)
+            rg_counted = bool(more and rg is not None and PARTITION_COUNTS and C.tree_partition_counts_ok(Q.n_rows))
             with tracing.span("tree.partition"):
-                runner.partition(d, n_open, bool(sampled and FUSED_PACK and more), zero, native_prologue and sampled)
+                runner.partition(d, n_open, bool(sampled and FUSED_PACK and more), zero, native_prologue and sampled,
+                                 ws.rg_work if rg_counted else None)
             prev_hist = cur_hist
             prev_row_of = row_of
             continue
