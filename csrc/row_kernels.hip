@@ -746,20 +746,28 @@ void launch_rg_erow(const RgErowArgs& a, hipStream_t s) {
 
 namespace {
 // The single-slot pass's partial tables summed per group into the level histogram: a thread per
-// (group, local bin), its group's workgroups read in order (coalesced over the bins).
+// (group, local bin, run of kRedRun workgroups), the run's tables read kRedU at a time (coalesced
+// over the bins; one thread walking the dense group's ~200 tables serially took ~32 us).
+constexpr int kRedRun = 32, kRedU = 8;
 __global__ __launch_bounds__(256) void rg_reduce_kernel(RgHistArgs a) {
   const int g = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.gbins) return;
+  const int w0 = a.wg_first[g] + (int)blockIdx.z * kRedRun, w1 = min(w0 + kRedRun, a.wg_first[g + 1]);
+  if (i >= a.gbins || w0 >= w1) return;
   const int32_t col = a.gbin[(int64_t)g * a.gbins + i];
   const int64_t hrow = a.slot_node[0];
   if (col < 0 || hrow < 0) return;
   const longlong2* part = reinterpret_cast<const longlong2*>(a.part);
   int64_t s0 = 0, s1 = 0;
-  for (int w = a.wg_first[g]; w < a.wg_first[g + 1]; ++w) {
-    const longlong2 v = part[(int64_t)w * a.gbins + i];
-    s0 += v.x;
-    s1 += v.y;
+  for (int w = w0; w < w1; w += kRedU) {
+    longlong2 v[kRedU];
+#pragma unroll
+    for (int u = 0; u < kRedU; ++u) v[u] = w + u < w1 ? part[(int64_t)(w + u) * a.gbins + i] : make_longlong2(0, 0);
+#pragma unroll
+    for (int u = 0; u < kRedU; ++u) {
+      s0 += v[u].x;
+      s1 += v[u].y;
+    }
   }
   if ((s0 | s1) == 0) return;
   int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
@@ -777,7 +785,8 @@ void launch_rg_hist(const RgHistArgs& a, hipStream_t s) {
   else
     hipLaunchKernelGGL(rg_hist_kernel<8192>, dim3((unsigned)blocks), dim3(kRgThreads), 0, s, a);
   if (a.part != nullptr && !(a.dbg & 4))
-    hipLaunchKernelGGL(rg_reduce_kernel, dim3((unsigned)((a.gbins + 255) / 256), (unsigned)a.G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(rg_reduce_kernel, dim3((unsigned)((a.gbins + 255) / 256), (unsigned)a.G,
+                                              (unsigned)((a.n_wg + kRedRun - 1) / kRedRun)), dim3(256), 0, s, a);
 }
 
 }  // namespace fdx
