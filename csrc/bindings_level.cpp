@@ -91,6 +91,7 @@ class RfLevels {
                           "cs_left_default", "node_slot", "s2n", "sub_dst", "sub_par", "sub_sib"})
       st_[k] = get(c, k);
     node_dense_ = get_opt(c, "node_dense");
+    sub_of_ = get_opt(c, "sub_of");
     arena_ = get_opt(c, "arena");
     {
       // the counts' pinned host rows as the device sees them: the plan writes the 4 counts there
@@ -336,6 +337,12 @@ class RfLevels {
     }
     a.row_of = p<int32_t>(row_of);
     a.root_parts = find_root_;
+    if (find_prev_) {
+      a.parent_hist = find_prev_;
+      a.sub_of = p<int32_t>(*sub_of_);
+      a.sub_par = p<int32_t>(st_["sub_par"]);
+      a.sub_sib = p<int32_t>(st_["sub_sib"]);
+    }
     const int64_t np_ = fdx::split_partials(nodes, Fa);
     if (np_ > 0) {
       if (!part_gain_.defined() || part_gain_.numel() < np_) {
@@ -395,6 +402,7 @@ class RfLevels {
     a.sub_dst = p<int32_t>(st_["sub_dst"]);
     a.sub_par = p<int32_t>(st_["sub_par"]);
     a.sub_sib = p<int32_t>(st_["sub_sib"]);
+    a.sub_of = p<int32_t>(sub_of_);
     return a;
   }
 
@@ -437,16 +445,22 @@ class RfLevels {
                   const optional<Tensor>& feat_thr, int64_t tree, const Tensor& out, const optional<Tensor>& wide,
                   const Tensor& open, const Tensor& n_open_ptr, const Tensor& next_open, const Tensor& next_totals,
                   bool sample_next, const optional<Tensor>& thr, const optional<Tensor>& mask,
-                  const std::vector<optional<Tensor>>& sel_lists) {
+                  const std::vector<optional<Tensor>>& sel_lists, const optional<Tensor>& prev_hist) {
     c10::hip::HIPGuard guard(dev_.index());
     const hipStream_t s = cur_stream(dev_);
     const int32_t Fa = (int32_t)nbins_.numel();
+    if (prev_hist) {          // this level's sibling subtraction inside the search (SplitArgs sub_of)
+      FDX_CHECK(sub_of_.has_value() && d > 0 && prev_hist->scalar_type() == at::kLong && prev_hist->dim() == 3 &&
+                    prev_hist->size(1) == hist.size(1), "prev_hist [rows, stride, 2] int64 with sub_of");
+      find_prev_ = p<int64_t>(*prev_hist);
+    }
     FDX_CHECK(open.numel() == n_open, "open [n_open]");
     const int64_t* root = d == 0 ? root_pending_ : nullptr;
     root_pending_ = nullptr;
     find_root_ = root;
     const bool any = find(hist, totals, boff, nbins_, zbin_, fid_orig_, open, feat_thr, tree, out, c10::nullopt, wide, s);
     find_root_ = nullptr;
+    find_prev_ = nullptr;
     fdx::LevelPlanArgs a = plan_args(d, n_open, out, open, n_open_ptr, next_open, next_totals);
     a.root_parts = root;
     const bool zc = counts_zero_copy(a, d, sample_next, sel_lists);
@@ -611,6 +625,8 @@ class RfLevels {
   Tensor root_parts_, sample_counts_;
   const int64_t* root_pending_ = nullptr;   // the last prologue's root slots, until level 0's split
   const int64_t* find_root_ = nullptr;
+  const int64_t* find_prev_ = nullptr;
+  optional<Tensor> sub_of_;
   bool build_all_ = true;
   int mode_ = 1, max_depth_ = 5, wps_ = 256;
   double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;

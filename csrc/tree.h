@@ -461,6 +461,14 @@ struct SplitArgs {
   int32_t* part_f;
   // optional: the root's totals as QuantArgs root_parts slots (level 0 of the fused prologue)
   const int64_t* root_parts;
+  // optional (single-process levels >= 1): the sibling subtraction inside the search. Open node n
+  // with sub_of[n] = k >= 0 has no histogram yet: (n, f)'s bins are parent_hist row sub_par[k] -
+  // hist row sub_sib[k], written to row n as they are searched (hist_subtract_kernel's result,
+  // without its launch and its second pass over the rows)
+  const int32_t* sub_of;
+  const int32_t* sub_par;
+  const int32_t* sub_sib;
+  const int64_t* parent_hist;
 };
 constexpr int32_t kSplitWide = 16;
 
@@ -762,6 +770,7 @@ struct LevelPlanArgs {
   int32_t* sub_dst;               // [L] subtraction: larger sibling (row in level d + 1) =
   int32_t* sub_par;               //     parent (row in level d) - smaller sibling (row in level d + 1)
   int32_t* sub_sib;
+  int32_t* sub_of;                // optional [2L]: per level d + 1 open index, its subtraction slot (-1)
 };
 
 // The plan's table resets, split over nthreads workers (the device runs them on 64 lanes before
@@ -774,6 +783,7 @@ FDX_HD void level_plan_reset(const LevelPlanArgs& a, int32_t t, int32_t nthreads
   }
   for (int32_t i = t; i < 2 * a.L; i += nthreads) {
     a.next_open[i] = -1;
+    if (a.sub_of) a.sub_of[i] = -1;
     a.next_totals[2 * i] = a.next_totals[2 * i + 1] = 0;
   }
   for (int32_t i = t; i < a.L; i += nthreads) a.s2n[i] = a.sub_dst[i] = a.sub_par[i] = a.sub_sib[i] = -1;
@@ -887,6 +897,7 @@ FDX_HD void level_plan(const LevelPlanArgs& a, bool reset = true) {
     a.s2n[nb] = jb;
     if (large >= 0) {
       a.sub_dst[nb] = jl;
+      if (a.sub_of) a.sub_of[jl] = nb;
       a.sub_par[nb] = ip;
       a.sub_sib[nb] = jb;
     }

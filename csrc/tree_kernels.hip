@@ -946,7 +946,15 @@ __device__ __forceinline__ double split_narrow_at(const SplitArgs& a, int64_t t,
   if (use && a.feat_thr)
     use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
   if (use) {
-    const int64_t* hb = a.hist + (split_row(a, n) * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
+    const int64_t stride = a.hist_stride ? a.hist_stride : a.boff[a.Fa];
+    const int64_t* hb = a.hist + (split_row(a, n) * stride + a.boff[f]) * 2;
+    const int32_t k = a.sub_of ? a.sub_of[n] : -1;
+    if (k >= 0) {            // the sibling subtraction of (n, f), written to row n (then read back)
+      const int64_t* pb = a.parent_hist + ((int64_t)a.sub_par[k] * stride + a.boff[f]) * 2;
+      const int64_t* sb = a.hist + ((int64_t)a.sub_sib[k] * stride + a.boff[f]) * 2;
+      int64_t* ob = const_cast<int64_t*>(hb);
+      for (int b = 0; b < 2 * a.nbins[f]; ++b) ob[b] = pb[b] - sb[b];
+    }
     int64_t T0, T1;
     split_totals(a, n, &T0, &T1);
     gain = best_split_scan(hb, a.nbins[f], a.zbin[f], T0, T1, ldexp(1.0, -a.kexp[0]),
@@ -1029,8 +1037,21 @@ __device__ __forceinline__ void split_wide_at(const SplitArgs& a, int64_t w, int
   int best_b = -1;
   int64_t bl0 = 0, bl1 = 0;
   if (use) {
-    const int64_t* hb = a.hist + (split_row(a, n) * (a.hist_stride ? a.hist_stride : a.boff[a.Fa]) + a.boff[f]) * 2;
+    const int64_t stride = a.hist_stride ? a.hist_stride : a.boff[a.Fa];
+    const int64_t* hb = a.hist + (split_row(a, n) * stride + a.boff[f]) * 2;
     const int nb = a.nbins[f], zb = a.zbin[f];
+    const int32_t ks = a.sub_of ? a.sub_of[n] : -1;
+    if (ks >= 0) {           // the sibling subtraction of (n, f): lane b writes bins b, b + 64, ...
+      const int64_t* pb = a.parent_hist + ((int64_t)a.sub_par[ks] * stride + a.boff[f]) * 2;
+      const int64_t* sb = a.hist + ((int64_t)a.sub_sib[ks] * stride + a.boff[f]) * 2;
+      int64_t* ob = const_cast<int64_t*>(hb);
+      for (int b = lane; b < nb; b += 64) {
+        ob[2 * b] = pb[2 * b] - sb[2 * b];
+        ob[2 * b + 1] = pb[2 * b + 1] - sb[2 * b + 1];
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+    }
     int64_t T0, T1;
     split_totals(a, n, &T0, &T1);
     const double s0 = ldexp(1.0, -a.kexp[0]), s1 = ldexp(1.0, -a.kexp[1]);
@@ -1491,6 +1512,7 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
       a.s2n[k] = jb;
       if (large >= 0) {
         a.sub_dst[k] = jl;
+        if (a.sub_of) a.sub_of[jl] = k;
         a.sub_par[k] = i;
         a.sub_sib[k] = jb;
       }

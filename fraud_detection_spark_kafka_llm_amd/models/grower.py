@@ -311,6 +311,8 @@ FUSED_PACK = os.environ.get("FDX_RF_FUSED_PACK", "1") == "1"
 # RF device levels issue their kernels through the native per-level runner (csrc/bindings_level.cpp
 # RfLevels: hist / split / plan / partition, one host call each) instead of ~20 Python-level calls
 NATIVE_LEVELS = os.environ.get("FDX_NATIVE_LEVELS", "1") == "1"
+# single-process runner levels subtract the larger siblings inside the split search
+SPLIT_SUBTRACT = os.environ.get("FDX_SPLIT_SUBTRACT", "1") == "1"
 # the partition's row pass writes the next level's row-list counts (runner levels, <= 4M rows)
 PARTITION_COUNTS = os.environ.get("FDX_PARTITION_COUNTS", "1") == "1"
 # single-slot row-group passes reduce per-workgroup partial tables (0: every workgroup's atomics)
@@ -1130,6 +1132,7 @@ class LevelState:
         self.default_child, self.node_slot = i32(M), i32(M)
         self.cs = [i32(cap) for _ in range(5)]          # feat, default, other, bin, left_default
         self.s2n, self.sub_dst, self.sub_par, self.sub_sib = i32(cap), i32(cap), i32(cap), i32(cap)
+        self.sub_of = i32(cap)          # (runner levels) open index -> subtraction slot (-1)
         # data-parallel levels (tree.h LevelRowsArgs): histogram row per open node (level parity)
         # and the subtraction triples as rows
         self.row_of = [i32(cap), i32(cap)]
@@ -1201,7 +1204,7 @@ def _level_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowPar
                gain=st.gain, n_nodes=st.n_nodes, counts=st.counts, counts_host=st.counts_host,
                default_child=st.default_child, cs_feat=st.cs[0], cs_default=st.cs[1], cs_other=st.cs[2],
                cs_bin=st.cs[3], cs_left_default=st.cs[4], node_slot=st.node_slot, s2n=st.s2n, sub_dst=st.sub_dst,
-               sub_par=st.sub_par, sub_sib=st.sub_sib, node_dense=st.node_dense, mode=int(params.mode),
+               sub_par=st.sub_par, sub_sib=st.sub_sib, sub_of=st.sub_of, node_dense=st.node_dense, mode=int(params.mode),
                max_depth=int(params.max_depth), min_gain=float(params.min_gain), lambda_=float(params.lambda_),
                mcw=float(params.min_child), seed=int(params.seed), F=int(Q.num_features), k=int(params.feat_k),
                lds=bool(RF_LDS), wps=int(PARTITION_WPS), arena=st.arena, dig16=ws.dig16() if sampled else None)
@@ -1360,7 +1363,7 @@ def _rf_runner_levels(Q, ws, st, params, tree_index, seed, shards, runner, sel_i
         sel = sel_args if (sel_ids and more) else []
         if shards is None:
             runner.split_plan(d, n_open, cur_hist, totals_d, Q.boff, feat_thr, tree_index, packed, wide, open_d,
-                              n_open_ptr, st.open[nxt], st.totals[nxt], more, thr_n, mask_n, sel)
+                              n_open_ptr, st.open[nxt], st.totals[nxt], more, thr_n, mask_n, sel, None)
         else:
             runner.plan(d, n_open, packed, open_d, n_open_ptr, st.open[nxt], st.totals[nxt], tree_index, more,
                         thr_n, mask_n, *lay, sel)
@@ -1689,7 +1692,9 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                     n_sub = int((st.sub_dst[:n_build] >= 0).sum())
                     assert n_build + n_sub == n_open, (d, n_build, n_sub, n_open)
                 cur_hist = bufs.out
-        if d > 0 and not build_all:
+        # (single-process runner levels subtract inside the split search: split_plan prev_hist)
+        fused_sub = runner is not None and shards is None and d > 0 and not build_all and SPLIT_SUBTRACT
+        if d > 0 and not build_all and not fused_sub:
             if shards is None:
                 C.tree_hist_subtract(prev_hist, cur_hist, st.sub_dst[:n_build], st.sub_par[:n_build],
                                      st.sub_sib[:n_build], TB)
@@ -1740,7 +1745,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             if shards is None:
                 runner.split_plan(d, n_open, cur_hist, totals_d, Q.boff, feat_thr, int(tree_index), packed,
                                   _wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, open_d, n_open_ptr,
-                                  st.open[nxt], st.totals[nxt], sample_next, thr_n, mask_n, sel)
+                                  st.open[nxt], st.totals[nxt], sample_next, thr_n, mask_n, sel,
+                                  prev_hist if fused_sub else None)
             else:
                 runner.plan(d, n_open, packed, open_d, n_open_ptr, st.open[nxt], st.totals[nxt], int(tree_index),
                             sample_next, thr_n, mask_n, *lay, sel)
