@@ -203,6 +203,137 @@ class RfLevels {
     C10_HIP_KERNEL_LAUNCH_CHECK();
   }
 
+  ~RfLevels() {
+    if (g_ev_) (void)hipEventDestroy(g_ev_);
+  }
+  RfLevels(const RfLevels&) = delete;
+  RfLevels& operator=(const RfLevels&) = delete;
+
+  // ---- GBDT trees of one process on the row-group engine: the whole level loop in here --------
+  // grower.device_tree_steps' generic loop spends ~33 us of interpreter time per level between the
+  // plan's counts and the next level's first launch (profiles/r5/gbdt_host_profile_*.txt), which
+  // the GPU sees as idle time at 1M rows. gbdt_root queues level 0 after the prologue; gbdt_levels
+  // runs levels 1.. -- wait for the previous plan's event, read its counts from the pinned row the
+  // plan wrote, queue row lists + row-group pass + split/plan (sibling subtraction inside) +
+  // partition -- with the same kernels and arguments as the Python loop (trees bitwise equal:
+  // tests/test_level_runner.py). Buffers are fixed: the level histograms alternate between two
+  // tensors (each sized for its parity's widest level), the partition zeroing the next one.
+  void gbdt_setup(const py::dict& c) {
+    const Tensor ptr = get(c, "rg_ptr"), ent = get(c, "rg_ent"), gbase = get(c, "rg_gbase"),
+                 gbin = get(c, "rg_gbin"), gmode = get(c, "rg_gmode"), wg = get(c, "rg_wg");
+    const int64_t G = ptr.size(0), N = ptr.size(1) - 1;
+    FDX_CHECK(N == row_node_.numel() && gbin.dim() == 2 && gbin.size(0) == G && gbase.numel() == G + 1 &&
+                  gmode.numel() == G && wg.dim() == 2 && wg.size(0) == 3 && ent.scalar_type() == at::kShort &&
+                  reinterpret_cast<uintptr_t>(ent.data_ptr()) % 16 == 0 && !build_all_ && mode_ == 0,
+              "gbdt_setup: row groups of this runner's rows, GBDT");
+    g_keep_ = {ptr, ent, gbase, gbin, gmode, wg};
+    fdx::RgHistArgs& a = gh_;
+    a = fdx::RgHistArgs{};
+    a.ptr = reinterpret_cast<const uint32_t*>(p<int32_t>(ptr));
+    a.ent = reinterpret_cast<const uint16_t*>(ent.data_ptr());
+    a.gbase = p<int64_t>(gbase);
+    a.gbin = p<int32_t>(gbin);
+    a.gbins = (int32_t)gbin.size(1);
+    a.G = (int32_t)G;
+    a.N = N;
+    a.rowdig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
+    a.np = 4;
+    a.gmode = p<uint8_t>(gmode);
+    a.wg_g = p<int32_t>(wg);
+    a.wg_p = a.wg_g + wg.size(1);
+    a.wg_np = a.wg_p + wg.size(1);
+    a.n_wg = (int32_t)wg.size(1);
+    a.dbg = c["dbg"].cast<int32_t>();
+    g_erow_ = get_opt(c, "rg_erow");
+    if (g_erow_) {
+      a.erow = reinterpret_cast<const uint32_t*>(p<int32_t>(*g_erow_));
+      a.ebase = c["rg_ebase"].cast<int64_t>();
+    }
+    g_emdig_ = get_opt(c, "emdig");
+    g_em_min_rows_ = c["em_min_rows"].cast<int64_t>();
+    g_part_ = get_opt(c, "rg_part");
+    g_wg_first_ = get_opt(c, "rg_wg_first");
+    FDX_CHECK(!g_part_ || (g_wg_first_ && g_part_->numel() >= 2 * a.n_wg * (int64_t)a.gbins &&
+                           g_wg_first_->numel() == G + 1), "gbdt_setup: part [n_wg, gbins, 2], wg_first [G + 1]");
+    g_list_work_ = get(c, "list_work");
+    g_rg_start_ = get(c, "rg_start");
+    g_rg_list_ = get(c, "rg_list");
+    g_rg_listdig_ = get(c, "rg_listdig");
+    const int64_t nwaves = (N + fdx::rg_list_rows(N) - 1) / fdx::rg_list_rows(N);
+    FDX_CHECK(g_list_work_.numel() >= fdx::kRgMaxSlots * (2 + nwaves) && g_rg_list_.numel() >= N &&
+                  g_rg_start_.numel() >= fdx::kRgMaxSlots + 1 && g_rg_listdig_.numel() >= 2 * N,
+              "gbdt_setup: row-list buffers");
+    fdx::RgListArgs& l = gl_;
+    l = fdx::RgListArgs{};
+    l.row_node = p<int32_t>(row_node_);
+    l.node_slot = p<int32_t>(st_["node_slot"]);
+    l.num_nodes = (int32_t)st_["node_slot"].numel();
+    l.N = N;
+    l.slot_count = p<int32_t>(g_list_work_);
+    l.slot_start = p<int32_t>(g_rg_start_);
+    l.list = p<int32_t>(g_rg_list_);
+    l.rowdig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
+    l.listdig = reinterpret_cast<uint32_t*>(p<int32_t>(g_rg_listdig_));
+    for (int k = 0; k < 2; ++k) {
+      g_hist_[k] = get(c, k ? "hist_b" : "hist_a");
+      int64_t need = 1;                     // (level d opens at most 2^d nodes)
+      for (int64_t d = k; d < max_depth_; d += 2) need = int64_t{1} << d;
+      FDX_CHECK(g_hist_[k].scalar_type() == at::kLong && g_hist_[k].dim() == 3 && g_hist_[k].size(2) == 2 &&
+                    g_hist_[k].is_contiguous() && g_hist_[k].size(0) >= need &&
+                    reinterpret_cast<uintptr_t>(g_hist_[k].data_ptr()) % 16 == 0,
+                "gbdt_setup: hist_a / hist_b [rows >= widest level of the parity, TB, 2] int64");
+    }
+    a.hist_stride = g_hist_[0].size(1);
+    FDX_CHECK(g_hist_[1].size(1) == a.hist_stride, "gbdt_setup: hist strides");
+    g_packed_ = get(c, "packed");
+    FDX_CHECK(g_packed_.scalar_type() == at::kLong && g_packed_.dim() == 2 && g_packed_.size(1) == 5 &&
+                  g_packed_.is_contiguous() && g_packed_.size(0) >= (int64_t{1} << (max_depth_ - 1)),
+              "gbdt_setup: packed [widest level, 5] int64");
+    g_one_ = get(c, "one");
+    g_zero1_ = get(c, "zero1");
+    g_open_[0] = st_["open0"];
+    g_open_[1] = get(c, "open1");
+    g_totals_[0] = st_["totals0"];
+    g_totals_[1] = get(c, "totals1");
+    g_boff_ = get(c, "boff");
+    g_wide_ = get_opt(c, "wide");
+    g_counted_ok_ = c["counted"].cast<bool>() && fdx::partition_counts_ok(N);
+    FDX_CHECK(sub_of_.has_value() && counts_host_dev_ != nullptr, "gbdt_setup: sub_of and mapped counts");
+    if (!g_ev_) FDX_CHECK(hipEventCreateWithFlags(&g_ev_, hipEventDisableTiming) == hipSuccess, "event");
+  }
+
+  // Level 0 of a tree whose prologue just ran (its root histogram: hist_a row 0, zeroed there).
+  void gbdt_root(int64_t tree) {
+    FDX_CHECK(g_ev_ != nullptr, "gbdt_root before gbdt_setup");
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    gbdt_level(0, 1, 1, tree, s);
+  }
+
+  // Levels 1 .. max_depth - 1; returns (n_open, n_build) of every level run, the root's first.
+  std::vector<int64_t> gbdt_levels(int64_t tree) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    std::vector<int64_t> shape{1, 1};
+    const Tensor& ch = st_["counts_host"];
+    const int64_t cw = ch.size(1);
+    for (int64_t d = 1; d < max_depth_; ++d) {
+      hipError_t e;
+      while ((e = hipEventQuery(g_ev_)) == hipErrorNotReady) {
+      }
+      FDX_CHECK(e == hipSuccess, "level event");
+      const volatile int32_t* row = p<int32_t>(ch) + (d - 1) * cw;     // (written by the plan itself)
+      const int32_t n_open = row[1], n_build = row[2];
+      if (n_open == 0) break;
+      FDX_CHECK(n_open <= g_hist_[d & 1].size(0) && n_build >= 1 && n_build <= fdx::kRgMaxSlots && n_build <= n_open,
+                "level counts");
+      gbdt_level(d, n_open, n_build, tree, s);
+      shape.push_back(n_open);
+      shape.push_back(n_build);
+    }
+    return shape;
+  }
+
   // GBDT leaf update from the node table (leaf_values + leaf_update in one launch)
   void leaf_update(const Tensor& margin, double eta, double lambda, double mds) {
     c10::hip::HIPGuard guard(dev_.index());
@@ -613,6 +744,57 @@ class RfLevels {
     return ct;
   }
 
+  // One GBDT level (the generic loop's rg branch + split_plan + partition, launch for launch).
+  void gbdt_level(int64_t d, int32_t n_open, int32_t n_build, int64_t tree, hipStream_t s) {
+    const int cur = (int)(d & 1), nxt = cur ^ 1;
+    const bool more = d + 1 < max_depth_;
+    const Tensor& hist = g_hist_[cur];
+    fdx::RgHistArgs a = gh_;
+    a.hist = p<int64_t>(hist);
+    a.nslots = n_build;
+    if (d == 0) {
+      a.slot_node = p<int32_t>(g_zero1_);
+    } else {
+      // the built rows grouped by slot (pass 0's per-wave counts from the last partition when
+      // counted); a single built node also gets every row's digit words zeroed outside it
+      const bool em = n_build == 1 && g_emdig_.has_value();
+      fdx::RgListArgs l = gl_;
+      l.nslots = n_build;
+      l.wave_count = l.slot_count + 2 * n_build;
+      l.counted = g_counted_ ? 1 : 0;
+      l.masked = em ? reinterpret_cast<uint32_t*>(p<int32_t>(*g_emdig_)) : nullptr;
+      fdx::launch_rg_list(l, s);
+      a.list = l.list;
+      a.slot_start = l.slot_start;
+      a.listdig = l.listdig;
+      a.slot_node = p<int32_t>(st_["s2n"]);
+      if (a.erow && em) {
+        a.emdig = l.masked;
+        a.em_min_rows = g_em_min_rows_;
+      }
+    }
+    if (n_build == 1 && g_part_) {
+      a.part = p<int64_t>(*g_part_);
+      a.wg_first = p<int32_t>(*g_wg_first_);
+    }
+    fdx::launch_rg_hist(a, s);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    const Tensor n_open_ptr = d == 0 ? g_one_ : st_["counts"].select(0, d - 1).narrow(0, 1, 1);
+    const optional<Tensor> prev = d == 0 ? optional<Tensor>() : optional<Tensor>(g_hist_[nxt]);
+    split_plan(d, n_open, hist.narrow(0, 0, n_open),
+               d == 0 ? st_["stats"].narrow(0, 0, 1) : g_totals_[cur].narrow(0, 0, n_open), g_boff_, c10::nullopt,
+               tree, g_packed_.narrow(0, 0, n_open), g_wide_, g_open_[cur].narrow(0, 0, n_open), n_open_ptr,
+               g_open_[nxt], g_totals_[nxt], false, c10::nullopt, c10::nullopt, {}, prev);
+    FDX_CHECK(hipEventRecord(g_ev_, s) == hipSuccess, "level event record");
+    optional<Tensor> zero;
+    if (more) {
+      FDX_CHECK(2 * (int64_t)n_open <= g_hist_[nxt].size(0), "next level rows");
+      zero = g_hist_[nxt].narrow(0, 0, 2 * (int64_t)n_open);
+    }
+    g_counted_ = more && g_counted_ok_;
+    partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
+  }
+
   std::vector<ItemGroup> groups_;
   Tensor csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, row_node_, kexp_;
   optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_, dig16_;
@@ -633,6 +815,16 @@ class RfLevels {
   int64_t seed_ = 0, F_ = 1, k_ = 1;
   bool lds_ = true;
   at::Device dev_{at::kCPU};
+  // GBDT level loop (gbdt_setup)
+  fdx::RgHistArgs gh_{};
+  fdx::RgListArgs gl_{};
+  std::vector<Tensor> g_keep_;
+  Tensor g_hist_[2], g_open_[2], g_totals_[2], g_packed_, g_one_, g_zero1_, g_boff_, g_list_work_, g_rg_start_,
+      g_rg_list_, g_rg_listdig_;
+  optional<Tensor> g_erow_, g_emdig_, g_part_, g_wg_first_, g_wide_;
+  int64_t g_em_min_rows_ = 0;
+  bool g_counted_ok_ = false, g_counted_ = false;
+  hipEvent_t g_ev_ = nullptr;
 };
 
 }  // namespace
@@ -646,5 +838,8 @@ void register_level_ops(pybind11::module& m) {
       .def("partition", &RfLevels::partition)
       .def("split_plan", &RfLevels::split_plan)
       .def("prologue", &RfLevels::prologue)
-      .def("leaf_update", &RfLevels::leaf_update);
+      .def("leaf_update", &RfLevels::leaf_update)
+      .def("gbdt_setup", &RfLevels::gbdt_setup)
+      .def("gbdt_root", &RfLevels::gbdt_root)
+      .def("gbdt_levels", &RfLevels::gbdt_levels);
 }

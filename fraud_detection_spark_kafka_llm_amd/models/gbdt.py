@@ -131,11 +131,13 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
             # |h| pass on the device loop's native runner) from the margins and labels
             res = grow_tree(Q, ws, gp, t, label=y, weight=w, coll=coll, deferred=defer, margin=margin,
                             on_first_wait=pending.finish if pending is not None else None)
+            if isinstance(res, PendingTree):
+                # queued first: the host-side compaction below overlaps the margin update
+                res.update_margin(margin, ws.row_node)
             if pending is not None:
                 trees.append(pending.result().compacted())
                 pending = None
             if isinstance(res, PendingTree):
-                res.update_margin(margin, ws.row_node)
                 pending = res
                 maybe_fail(t, model="gbdt")
                 continue

@@ -319,6 +319,9 @@ PARTITION_COUNTS = os.environ.get("FDX_PARTITION_COUNTS", "1") == "1"
 RG_PARTIALS = os.environ.get("FDX_RG_PARTIALS", "1") == "1"
 # sampled RF trees on the runner take the lean level loop (_rf_runner_levels; 0: the generic loop)
 LEAN_RF = os.environ.get("FDX_RF_LEAN", "1") == "1"
+# single-process GBDT trees on the row-group engine: the level loop runs in the runner (C++,
+# RfLevels.gbdt_levels; 0: the generic Python loop)
+GBDT_CXX_LEVELS = os.environ.get("FDX_GBDT_CXX_LEVELS", "1") == "1"
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
 RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
 # split search: a wave per (node, feature) for the features with > 16 bins
@@ -1213,6 +1216,45 @@ def _level_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowPar
     return runner
 
 
+def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
+    """Hands the runner the row-group tables and fixed level buffers of its C++ GBDT level loop
+    (RfLevels.gbdt_setup), once per runner; returns the two level-histogram tensors (the root's
+    is row 0 of the first, zeroed by the prologue)."""
+    cached = getattr(ws, "_gbdt_levels", None)
+    if cached is not None and cached[0] is runner:
+        return cached[1]
+    dev, TB, D = Q.device, Q.TB, int(params.max_depth)
+    # level d opens at most 2^d nodes; even and odd levels alternate between the two tensors
+    rows = [max([1] + [1 << d for d in range(k, D, 2)]) for k in (0, 1)]
+    hists = [torch.empty((r, TB, 2), dtype=torch.int64, device=dev) for r in rows]
+    em = rg.erow is not None and qmod.RG_EM_MIN_FRAC <= 1.0
+    runner.gbdt_setup(dict(
+        rg_ptr=rg.ptr, rg_ent=rg.ent, rg_gbase=rg.gbase, rg_gbin=rg.gbin, rg_gmode=rg.gmode, rg_wg=rg.work(),
+        rg_erow=rg.erow, rg_ebase=int(rg.ebase) if rg.erow is not None else 0,
+        emdig=ws.rg_emdig() if em else None, em_min_rows=max(1, int(qmod.RG_EM_MIN_FRAC * Q.n_rows)),
+        rg_part=ws.rg_part(rg) if RG_PARTIALS else None, rg_wg_first=rg.work_first() if RG_PARTIALS else None,
+        list_work=ws.rg_work, rg_start=ws.rg_start, rg_list=ws.rg_list, rg_listdig=ws.rg_listdig,
+        hist_a=hists[0], hist_b=hists[1], packed=torch.empty((1 << (D - 1), 5), dtype=torch.int64, device=dev),
+        one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff,
+        wide=_wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, counted=PARTITION_COUNTS, dbg=RG_DBG))
+    ws._gbdt_levels = (runner, hists)
+    return hists
+
+
+def _gbdt_runner_levels(Q, runner, tree_index, on_first_wait):
+    """The level loop of a single-process GBDT tree in the runner (C++): level 0 is queued, the
+    previous tree's host table is built while it runs (on_first_wait), then levels 1.. run with
+    the host waits inside the runner. Same launches and trees as the generic loop."""
+    runner.gbdt_root(tree_index)
+    if on_first_wait is not None:
+        on_first_wait()
+    shape = runner.gbdt_levels(tree_index)
+    for j in range(0, len(shape), 2):
+        LEVEL_STATS["levels"] += 1
+        LEVEL_STATS["built_nodes"] += shape[j + 1]
+        LEVEL_STATS["hist_bytes"] += shape[j + 1] * Q.TB * 16
+
+
 class _RfViews:
     """Views of a LevelState's buffers the sampled RF level loop slices every level, made once
     (a tensor slice costs 2-5 us of host time; the loop is host bound at small shards)."""
@@ -1433,9 +1475,15 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     # the next level's zeroed histograms (at most 2 open nodes per open node) are queued before
     # the host waits for its counts, so the fill runs while the host sizes that level
     pre_hist = None
+    # single-process GBDT rounds on the row-group engine: the level loop runs in the runner
+    rg_cxx = ws.rowgroups() if (native_prologue and gbdt_native and GBDT_CXX_LEVELS and SPLIT_SUBTRACT and
+                                np_ == 4 and margin is not None and g is None) else None
     if native_prologue:
         # the root histogram is zeroed by the prologue's first launch
-        pre_hist = torch.empty((1, TB, 2), dtype=torch.int64, device=dev)
+        if rg_cxx is not None:
+            pre_hist = _gbdt_levels_setup(Q, ws, st, params, runner, rg_cxx)[0][:1]
+        else:
+            pre_hist = torch.empty((1, TB, 2), dtype=torch.int64, device=dev)
         with tracing.span("tree.quant"):
             # (the dense-block digit planes only feed the MFMA dense path, off with the row groups)
             digp = ws.digp if (ws.digp is not None and not build_all and ws.rowgroups() is None) else None
@@ -1495,7 +1543,11 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                               Q.fid_orig)
         yield st.record_event(cur_stream)
     generic_depth = params.max_depth
-    if runner is not None and sampled and FUSED_PACK and LEAN_RF:
+    if rg_cxx is not None:
+        _gbdt_runner_levels(Q, runner, int(tree_index), on_first_wait)
+        on_first_wait = None
+        generic_depth = 0
+    elif runner is not None and sampled and FUSED_PACK and LEAN_RF:
         # sampled RF levels on the native runner: the lean loop (same launches, far less Python)
         on_first_wait = yield from _rf_runner_levels(Q, ws, st, params, int(tree_index), seed, shards, runner,
                                                      sel_ids, item_groups, compact, native_prologue, cur_stream,

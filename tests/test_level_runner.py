@@ -71,8 +71,20 @@ def test_gpu_gbdt_native_round_equals_python_levels(monkeypatch):
     monkeypatch.setattr(grower, "NATIVE_LEVELS", False)
     ref = _booster("cuda:0")
     monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
+    assert _booster("cuda:0") == ref                         # the level loop in the runner (C++)
+    monkeypatch.setattr(grower, "GBDT_CXX_LEVELS", False)    # the generic Python loop on the runner
     assert _booster("cuda:0") == ref
+    monkeypatch.setattr(grower, "GBDT_CXX_LEVELS", True)
+    for flag in ("RG_PARTIALS", "PARTITION_COUNTS"):
+        monkeypatch.setattr(grower, flag, False)
+        assert _booster("cuda:0") == ref, flag
+        monkeypatch.setattr(grower, flag, True)
     assert _booster("cpu") == ref
+    for depth in (1, 3):                                     # (a one-level tree: gbdt_root only)
+        monkeypatch.setattr(grower, "NATIVE_LEVELS", False)
+        ref_d = _booster("cuda:0", depth=depth)
+        monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
+        assert _booster("cuda:0", depth=depth) == ref_d, depth
 
 
 @pytest.mark.gpu
