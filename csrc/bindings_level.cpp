@@ -298,6 +298,7 @@ class RfLevels {
     g_boff_ = get(c, "boff");
     g_wide_ = get_opt(c, "wide");
     g_counted_ok_ = c["counted"].cast<bool>() && fdx::partition_counts_ok(N);
+    g_part_multi_ = c["part_multi"].cast<bool>();
     FDX_CHECK(sub_of_.has_value() && counts_host_dev_ != nullptr, "gbdt_setup: sub_of and mapped counts");
     if (!g_ev_) FDX_CHECK(hipEventCreateWithFlags(&g_ev_, hipEventDisableTiming) == hipSuccess, "event");
   }
@@ -773,7 +774,7 @@ class RfLevels {
         a.em_min_rows = g_em_min_rows_;
       }
     }
-    if (n_build == 1 && g_part_) {
+    if (g_part_ && (n_build == 1 || g_part_multi_)) {
       a.part = p<int64_t>(*g_part_);
       a.wg_first = p<int32_t>(*g_wg_first_);
     }
@@ -823,7 +824,7 @@ class RfLevels {
       g_rg_list_, g_rg_listdig_;
   optional<Tensor> g_erow_, g_emdig_, g_part_, g_wg_first_, g_wide_;
   int64_t g_em_min_rows_ = 0;
-  bool g_counted_ok_ = false, g_counted_ = false;
+  bool g_counted_ok_ = false, g_counted_ = false, g_part_multi_ = false;
   hipEvent_t g_ev_ = nullptr;
 };
 

@@ -722,7 +722,7 @@ void rg_hist(const Tensor& ptr, const Tensor& ent, const Tensor& gbase, const Te
     }
   }
   if (part && part->defined() && dev.is_cuda()) {     // (the host twin adds straight into hist)
-    FDX_CHECK(nslots == 1 && wg_first.has_value(), "partial tables: single-slot passes with wg_first");
+    FDX_CHECK(wg_first.has_value() && (nslots == 1 || list), "partial tables: wg_first (several slots: a list pass)");
     chk(*part, dev, at::kLong, "part");
     chk(*wg_first, dev, at::kInt, "wg_first");
     FDX_CHECK(part->numel() >= 2 * a.n_wg * (int64_t)a.gbins && wg_first->numel() == G + 1 &&

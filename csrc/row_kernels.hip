@@ -309,9 +309,11 @@ __device__ __forceinline__ void rg_store_part(const RgHistArgs& a, RgShared<BINS
   }
 }
 
+// whole: the workgroup's chunk lies inside slot s (its table may go to the partials)
 template <int BINS>
-__device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS>& sh, int g, int s, int tid) {
-  if (a.part != nullptr) {
+__device__ __forceinline__ void rg_flush(const RgHistArgs& a, RgShared<BINS>& sh, int g, int s, int tid,
+                                         bool whole = true) {
+  if (a.part != nullptr && (a.nslots == 1 || whole)) {
     rg_store_part<BINS>(a, sh, tid, false);
     return;
   }
@@ -659,8 +661,8 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
     return;
   }
   const int64_t a0 = T * p / np_g, a1 = T * (p + 1) / np_g;
-  if (a0 >= a1) {
-    if (a.part != nullptr) rg_store_part<BINS>(a, sh, tid, true);
+  if (a0 >= a1) {                    // (several slots: the reduction skips an empty chunk itself)
+    if (a.part != nullptr && a.nslots == 1) rg_store_part<BINS>(a, sh, tid, true);
     return;
   }
   for (int i = tid; i < BINS; i += kRgThreads) {
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
       rg_range_sparse<BINS>(sh, a, ptr, ent, pdig, lo, hi, wv, lane, np, dbg, sink);
     if (dbg & 2) atomicAdd(reinterpret_cast<unsigned long long*>(&sh.hg[lane]), sink);
     __syncthreads();
-    rg_flush<BINS>(a, sh, g, s, tid);
+    rg_flush<BINS>(a, sh, g, s, tid, a0 >= ss0 && a1 <= ss1);
     __syncthreads();
     if (!list || ss1 >= a1 || s + 1 >= a.nslots) break;
     ++s;
@@ -748,31 +750,54 @@ namespace {
 // The single-slot pass's partial tables summed per group into the level histogram: a thread per
 // (group, local bin, run of kRedRun workgroups), the run's tables read kRedU at a time (coalesced
 // over the bins; one thread walking the dense group's ~200 tables serially took ~32 us).
+// Several slots: the run's workgroups that stored a table (rg_part_slot >= 0) are summed per slot
+// (a group's chunks follow the list order, so a slot's tables are consecutive) and each slot's sum
+// is added to its node's row.
 constexpr int kRedRun = 32, kRedU = 8;
+__device__ __forceinline__ void rg_reduce_add(const RgHistArgs& a, int slot, int32_t col, int64_t s0, int64_t s1) {
+  const int64_t hrow = slot >= 0 ? a.slot_node[slot] : -1;
+  if ((s0 | s1) == 0 || hrow < 0) return;
+  int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
+  atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)s0);
+  atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)s1);
+}
+
 __global__ __launch_bounds__(256) void rg_reduce_kernel(RgHistArgs a) {
+  __shared__ int32_t wslot[kRedRun];
   const int g = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int w0 = a.wg_first[g] + (int)blockIdx.z * kRedRun, w1 = min(w0 + kRedRun, a.wg_first[g + 1]);
-  if (i >= a.gbins || w0 >= w1) return;
+  if (w0 >= w1) return;                                   // (uniform over the block)
+  if (threadIdx.x < w1 - w0) {
+    const int64_t T = a.list ? (int64_t)a.slot_start[a.nslots] : a.N;
+    wslot[threadIdx.x] = a.nslots == 1 ? 0 : rg_part_slot(a, w0 + (int)threadIdx.x, T);
+  }
+  __syncthreads();
+  if (i >= a.gbins) return;
   const int32_t col = a.gbin[(int64_t)g * a.gbins + i];
-  const int64_t hrow = a.slot_node[0];
-  if (col < 0 || hrow < 0) return;
+  if (col < 0) return;
   const longlong2* part = reinterpret_cast<const longlong2*>(a.part);
   int64_t s0 = 0, s1 = 0;
+  int cur = -1;
   for (int w = w0; w < w1; w += kRedU) {
     longlong2 v[kRedU];
 #pragma unroll
-    for (int u = 0; u < kRedU; ++u) v[u] = w + u < w1 ? part[(int64_t)(w + u) * a.gbins + i] : make_longlong2(0, 0);
+    for (int u = 0; u < kRedU; ++u)
+      v[u] = (w + u < w1 && wslot[w + u - w0] >= 0) ? part[(int64_t)(w + u) * a.gbins + i] : make_longlong2(0, 0);
 #pragma unroll
     for (int u = 0; u < kRedU; ++u) {
+      const int ws = w + u < w1 ? wslot[w + u - w0] : -1;
+      if (ws < 0) continue;
+      if (ws != cur) {
+        rg_reduce_add(a, cur, col, s0, s1);
+        cur = ws;
+        s0 = s1 = 0;
+      }
       s0 += v[u].x;
       s1 += v[u].y;
     }
   }
-  if ((s0 | s1) == 0) return;
-  int64_t* dst = a.hist + (hrow * a.hist_stride + rg_col_offset(a, col)) * 2;
-  atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)s0);
-  atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)s1);
+  rg_reduce_add(a, cur, col, s0, s1);
 }
 
 }  // namespace

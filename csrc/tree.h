@@ -315,11 +315,13 @@ struct RgHistArgs {
   int64_t ebase;
   const uint32_t* emdig;
   int64_t em_min_rows;
-  // optional, single-slot passes: workgroup w stores its whole LDS table to part[w][gbins][2]
-  // (plain stores) and rg_reduce_kernel sums the workgroups of each group (work-table entries
-  // wg_first[g] .. wg_first[g + 1]) into the level histogram, instead of every workgroup adding
-  // its table into the same bins with integer atomics (~30 % of the root pass at 1M rows with
-  // ~200 workgroups on the dense group, profiles/r5/NOTES.md)
+  // optional: workgroup w stores its whole LDS table to part[w][gbins][2] (plain stores) and
+  // rg_reduce_kernel sums the workgroups of each group (work-table entries wg_first[g] ..
+  // wg_first[g + 1]) into the level histogram, instead of every workgroup adding its table into
+  // the same bins with integer atomics (~30 % of the root pass at 1M rows with ~200 workgroups on
+  // the dense group; ~50 us of every listed level there, profiles/r5/NOTES.md). Several slots:
+  // only a workgroup whose chunk lies inside one slot stores its table (rg_part_slot); the few
+  // across a slot boundary flush with atomics
   int64_t* part;
   const int32_t* wg_first;
 };
@@ -329,6 +331,19 @@ FDX_HD bool rg_use_em(const RgHistArgs& a, int g, int64_t T) {
   if (a.erow == nullptr || a.gmode[g] != 0 || a.gbase[g] < a.ebase || a.nslots != 1) return false;
   if (a.list == nullptr) return true;
   return a.emdig != nullptr && T >= a.em_min_rows;
+}
+
+// Partial tables of a listed pass over several slots: the slot whose list range holds workgroup
+// w's whole chunk [T p / np, T (p + 1) / np) -- its table goes to part[w] -- else -1 (an empty
+// chunk, or one across a slot boundary: that workgroup flushes with atomics). The same slot search
+// as rg_hist_kernel's.
+FDX_HD int rg_part_slot(const RgHistArgs& a, int w, int64_t T) {
+  const int64_t p = a.wg_p[w], np = a.wg_np[w];
+  const int64_t a0 = T * p / np, a1 = T * (p + 1) / np;
+  if (a0 >= a1) return -1;
+  int s = 0;
+  while (s + 1 < a.nslots && a.slot_start[s + 1] <= a0) ++s;
+  return a1 <= (int64_t)a.slot_start[s + 1] ? s : -1;
 }
 
 // Digit words of the entry-major pass, by row.

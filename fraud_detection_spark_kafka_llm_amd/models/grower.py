@@ -317,6 +317,9 @@ SPLIT_SUBTRACT = os.environ.get("FDX_SPLIT_SUBTRACT", "1") == "1"
 PARTITION_COUNTS = os.environ.get("FDX_PARTITION_COUNTS", "1") == "1"
 # single-slot row-group passes reduce per-workgroup partial tables (0: every workgroup's atomics)
 RG_PARTIALS = os.environ.get("FDX_RG_PARTIALS", "1") == "1"
+# ... and so do the listed passes over several slots (a workgroup whose chunk straddles a slot
+# boundary still flushes with atomics)
+RG_PARTIALS_MULTI = os.environ.get("FDX_RG_PARTIALS_MULTI", "1") == "1"
 # sampled RF trees on the runner take the lean level loop (_rf_runner_levels; 0: the generic loop)
 LEAN_RF = os.environ.get("FDX_RF_LEAN", "1") == "1"
 # single-process GBDT trees on the row-group engine: the level loop runs in the runner (C++,
@@ -1236,7 +1239,8 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
         list_work=ws.rg_work, rg_start=ws.rg_start, rg_list=ws.rg_list, rg_listdig=ws.rg_listdig,
         hist_a=hists[0], hist_b=hists[1], packed=torch.empty((1 << (D - 1), 5), dtype=torch.int64, device=dev),
         one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff,
-        wide=_wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, counted=PARTITION_COUNTS, dbg=RG_DBG))
+        wide=_wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, counted=PARTITION_COUNTS, dbg=RG_DBG,
+        part_multi=RG_PARTIALS_MULTI))
     ws._gbdt_levels = (runner, hists)
     return hists
 
@@ -1648,8 +1652,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 shard_args = (shards.bin_lo, bufs.shard_bins) if shards is not None else (None, 0)
                 # single-slot passes: per-workgroup partial tables summed by one reduction instead
                 # of every workgroup's atomics on the same bins (RgHistArgs part)
-                part = dict(part=ws.rg_part(rg), wg_first=rg.work_first()) if (RG_PARTIALS and n_build == 1 and
-                                                                                 dev.type == "cuda") else {}
+                part = dict(part=ws.rg_part(rg), wg_first=rg.work_first()) \
+                    if (RG_PARTIALS and (n_build == 1 or RG_PARTIALS_MULTI) and dev.type == "cuda") else {}
                 if d == 0:
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, None, 1, rg.gmode,
                                    rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG, **rg.em_args(), **part)

@@ -50,7 +50,7 @@ def gmode(rg):
 
 
 def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None, np_=4, P=16, max_groups=None,
-                dbg=0, bins=8192, em=False):
+                dbg=0, bins=8192, em=False, part=False):
     """Histograms of node slots 0..nslots-1 through tree_rg_list + tree_rg_hist, plus q0, q1 and Q;
     ``shards`` = (S, bin_lo) writes the shard-major DP layout (returned unpacked); ``em`` passes
     the entry-major sparse pass's arguments (taken at single-slot levels, whatever the list size)."""
@@ -83,6 +83,9 @@ def _rg_hist_on(dev, vc, max_bins, nslots, row_node_np, root=False, shards=None,
             built = (row_node_np >= 0) & (row_node_np < nslots)
             want = np.where(built[:, None], ws.rowdig.cpu().numpy(), 0)
             np.testing.assert_array_equal(emdig.cpu().numpy(), want)       # every row written
+    if part:        # per-workgroup partial tables + the reduction (straddling chunks: atomics)
+        kw["part"] = torch.empty(rg.work(P).shape[1] * bins * 2, dtype=torch.int64, device=dev)
+        kw["wg_first"] = rg.work_first(P)
     if shards is None:
         hist = torch.zeros((nslots, Q.TB, 2), dtype=torch.int64, device=dev)
         C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, list_, start, ldig, nslots, gmode(rg),
@@ -368,10 +371,14 @@ def test_row_group_level_loop_grows_the_csc_trees(monkeypatch, depth, hot, bins,
                                                  (1, False, 4096, True)])
 @pytest.mark.parametrize("sharded", [False, True])
 @pytest.mark.parametrize("mode", [None, 0, 1])
-def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, em, sharded, mode, monkeypatch):
+@pytest.mark.parametrize("part", [False, True])
+def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, em, sharded, mode, part, monkeypatch):
     """The row-group pass (LDS int64 atomics, 16-B row-run loads, per-slot flushes; the
-    entry-major pass of the sparse groups with ``em``) equals the host's exact int64 sums bit for
-    bit, plain and in the shard-major DP layout."""
+    entry-major pass of the sparse groups with ``em``; with ``part`` the workgroups' partial
+    tables and their reduction) equals the host's exact int64 sums bit for bit, plain and in the
+    shard-major DP layout."""
+    if part and mode is not None:
+        pytest.skip("partial tables: the layout's own pass modes")
     rng = np.random.default_rng(20 + nslots)
     n = 30000
     vc = _wide(n, 400, 20 + nslots, hi=300)
@@ -383,7 +390,7 @@ def test_gpu_row_group_histograms_equal_host_bitwise(nslots, root, bins, em, sha
         shards = (3, lo)
     monkeypatch.setitem(MODE, "gmode", mode)
     a, *_ = _rg_hist_on("cpu", vc, 200, nslots, row_node, root, shards, P=24, bins=bins)
-    b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24, bins=bins, em=em)
+    b, *_ , Q, rg = _rg_hist_on("cuda:0", vc, 200, nslots, row_node, root, shards, P=24, bins=bins, em=em, part=part)
     assert rg.G >= 2
     np.testing.assert_array_equal(a, b)
 
