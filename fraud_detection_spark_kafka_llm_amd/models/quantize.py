@@ -126,14 +126,17 @@ RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
 # workgroups per row-group pass: few and large -- every workgroup zeroes and flushes a whole
 # 8192-bin table (up to 2 x 8192 int64 global atomics per slot it covers). 10M rows x 40 trees:
 # 7.69 ms per tree at 2048, 6.19 at 512 (profiles/r4/gbdt_rg_work_sweep.txt); 1M rows x 100
-# trees: 1.95 ms at 512, 1.67 at 256, 1.79 at 128 (profiles/r4/gbdt_1M_rg_wgs_sweep.txt). Default
-# (FDX_RG_WGS unset): rows / 4096, in [128, 512], a multiple of 64.
+# trees: 1.95 ms at 512, 1.67 at 256, 1.79 at 128 (profiles/r4/gbdt_1M_rg_wgs_sweep.txt). Since
+# every pass stores per-workgroup tables instead (RgHistArgs part), more workgroups pay off: 1M rows
+# fit 0.142 s at 128, 0.124 at 192, 0.116 at 256, 0.1145 at 384, 0.117 at 512; 10M rows 6.48 ms a
+# tree at 512, 6.96 at 768, 6.68 at 1024 (profiles/r5/gbdt_rg_wgs_sweep_partials.txt). Default
+# (FDX_RG_WGS unset): rows / 2731, in [128, 512], a multiple of 64.
 RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 0))
 
 
 def rg_default_wgs(n_rows: int) -> int:
     """Workgroups of a row-group pass over ``n_rows`` rows (see RG_TARGET_WGS)."""
-    return int(min(512, max(128, round(n_rows / 4096 / 64) * 64)))
+    return int(min(512, max(128, round(n_rows * 1.5 / 4096 / 64) * 64)))
 # work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
 # (ptr, digits) loads whether or not it has entries in the group)
 RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 16.0))
