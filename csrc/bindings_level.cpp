@@ -255,6 +255,21 @@ class RfLevels {
     g_wg_first_ = get_opt(c, "rg_wg_first");
     FDX_CHECK(!g_part_ || (g_wg_first_ && g_part_->numel() >= 2 * a.n_wg * (int64_t)a.gbins &&
                            g_wg_first_->numel() == G + 1), "gbdt_setup: part [n_wg, gbins, 2], wg_first [G + 1]");
+    // optional: the listed levels' own work table (fewer rows than the root's all-rows pass)
+    const optional<Tensor> wl = get_opt(c, "rg_wg_list");
+    g_wl_ = {a.wg_g, a.wg_p, a.wg_np, a.n_wg};
+    g_wg_first_list_ = g_wg_first_;
+    if (wl) {
+      FDX_CHECK(wl->dim() == 2 && wl->size(0) == 3 && wl->scalar_type() == at::kInt, "rg_wg_list [3, n_wg] int32");
+      g_keep_.push_back(*wl);
+      g_wl_.g = p<int32_t>(*wl);
+      g_wl_.p = g_wl_.g + wl->size(1);
+      g_wl_.np = g_wl_.p + wl->size(1);
+      g_wl_.n = (int32_t)wl->size(1);
+      g_wg_first_list_ = get_opt(c, "rg_wg_first_list");
+      FDX_CHECK(!g_part_ || (g_wg_first_list_ && g_wg_first_list_->numel() == G + 1 &&
+                             g_part_->numel() >= 2 * g_wl_.n * (int64_t)a.gbins), "rg_wg_first_list / part size");
+    }
     g_list_work_ = get(c, "list_work");
     g_rg_start_ = get(c, "rg_start");
     g_rg_list_ = get(c, "rg_list");
@@ -769,6 +784,10 @@ class RfLevels {
       a.slot_start = l.slot_start;
       a.listdig = l.listdig;
       a.slot_node = p<int32_t>(st_["s2n"]);
+      a.wg_g = g_wl_.g;
+      a.wg_p = g_wl_.p;
+      a.wg_np = g_wl_.np;
+      a.n_wg = g_wl_.n;
       if (a.erow && em) {
         a.emdig = l.masked;
         a.em_min_rows = g_em_min_rows_;
@@ -776,7 +795,7 @@ class RfLevels {
     }
     if (g_part_ && (n_build == 1 || g_part_multi_)) {
       a.part = p<int64_t>(*g_part_);
-      a.wg_first = p<int32_t>(*g_wg_first_);
+      a.wg_first = p<int32_t>(d == 0 ? *g_wg_first_ : *g_wg_first_list_);
     }
     fdx::launch_rg_hist(a, s);
     C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -822,7 +841,11 @@ class RfLevels {
   std::vector<Tensor> g_keep_;
   Tensor g_hist_[2], g_open_[2], g_totals_[2], g_packed_, g_one_, g_zero1_, g_boff_, g_list_work_, g_rg_start_,
       g_rg_list_, g_rg_listdig_;
-  optional<Tensor> g_erow_, g_emdig_, g_part_, g_wg_first_, g_wide_;
+  optional<Tensor> g_erow_, g_emdig_, g_part_, g_wg_first_, g_wg_first_list_, g_wide_;
+  struct {
+    const int32_t *g, *p, *np;
+    int32_t n;
+  } g_wl_{};                               // the listed levels' work table
   int64_t g_em_min_rows_ = 0;
   bool g_counted_ok_ = false, g_counted_ = false, g_part_multi_ = false;
   hipEvent_t g_ev_ = nullptr;

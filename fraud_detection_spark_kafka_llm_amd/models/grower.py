@@ -407,9 +407,11 @@ class Workspace:
             self._rg_emdig = torch.empty((self.Q.n_rows, 2), dtype=torch.int32, device=self.dev)
         return self._rg_emdig
 
-    def rg_part(self, rg) -> torch.Tensor:
-        """[n_wg, gbins, 2] int64 scratch of a single-slot row-group pass's partial tables."""
-        need = int(rg.work().shape[1]) * int(rg.gbin.shape[1]) * 2
+    def rg_part(self, rg, other_work=None) -> torch.Tensor:
+        """[n_wg, gbins, 2] int64 scratch of a row-group pass's partial tables (sized for the
+        larger of rg.work() and ``other_work``)."""
+        n_wg = max(int(rg.work().shape[1]), int(other_work.shape[1]) if other_work is not None else 0)
+        need = n_wg * int(rg.gbin.shape[1]) * 2
         t = getattr(self, "_rg_part", None)
         if t is None or t.numel() < need:
             t = self._rg_part = torch.empty(need, dtype=torch.int64, device=self.dev)
@@ -1231,11 +1233,13 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
     rows = [max([1] + [1 << d for d in range(k, D, 2)]) for k in (0, 1)]
     hists = [torch.empty((r, TB, 2), dtype=torch.int64, device=dev) for r in rows]
     em = rg.erow is not None and qmod.RG_EM_MIN_FRAC <= 1.0
+    part = ws.rg_part(rg, rg.list_work()) if RG_PARTIALS else None
     runner.gbdt_setup(dict(
+        rg_wg_list=rg.list_work(), rg_wg_first_list=rg.list_work_first() if RG_PARTIALS else None,
         rg_ptr=rg.ptr, rg_ent=rg.ent, rg_gbase=rg.gbase, rg_gbin=rg.gbin, rg_gmode=rg.gmode, rg_wg=rg.work(),
         rg_erow=rg.erow, rg_ebase=int(rg.ebase) if rg.erow is not None else 0,
         emdig=ws.rg_emdig() if em else None, em_min_rows=max(1, int(qmod.RG_EM_MIN_FRAC * Q.n_rows)),
-        rg_part=ws.rg_part(rg) if RG_PARTIALS else None, rg_wg_first=rg.work_first() if RG_PARTIALS else None,
+        rg_part=part, rg_wg_first=rg.work_first() if RG_PARTIALS else None,
         list_work=ws.rg_work, rg_start=ws.rg_start, rg_list=ws.rg_list, rg_listdig=ws.rg_listdig,
         hist_a=hists[0], hist_b=hists[1], packed=torch.empty((1 << (D - 1), 5), dtype=torch.int64, device=dev),
         one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff,
@@ -1652,11 +1656,14 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                 shard_args = (shards.bin_lo, bufs.shard_bins) if shards is not None else (None, 0)
                 # single-slot passes: per-workgroup partial tables summed by one reduction instead
                 # of every workgroup's atomics on the same bins (RgHistArgs part)
-                part = dict(part=ws.rg_part(rg), wg_first=rg.work_first()) \
+                # (the listed levels have their own, smaller work table: RowGroups.list_work)
+                wtab = rg.work() if d == 0 else rg.list_work()
+                part = dict(part=ws.rg_part(rg, rg.list_work()), wg_first=rg.work_first() if d == 0 else
+                            rg.list_work_first()) \
                     if (RG_PARTIALS and (n_build == 1 or RG_PARTIALS_MULTI) and dev.type == "cuda") else {}
                 if d == 0:
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, None, None, None, 1, rg.gmode,
-                                   rg.work(), s2n, hist_target, h_stride, *shard_args, RG_DBG, **rg.em_args(), **part)
+                                   wtab, s2n, hist_target, h_stride, *shard_args, RG_DBG, **rg.em_args(), **part)
                 else:
                     # one built node: every row's digit words zeroed outside it, for the
                     # entry-major pass of the sparse groups (taken when the node is large)
@@ -1665,7 +1672,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                     C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
                                    ws.rg_list, ws.rowdig, ws.rg_listdig, emdig, counted=rg_counted)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
-                                   ws.rg_listdig, n_build, rg.gmode, rg.work(), s2n, hist_target, h_stride,
+                                   ws.rg_listdig, n_build, rg.gmode, wtab, s2n, hist_target, h_stride,
                                    *shard_args, RG_DBG, **(rg.em_args(emdig) if emdig is not None else {}), **part)
                 sel_groups, use_dense = [], False
             if sel_groups is None:

@@ -132,11 +132,21 @@ RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
 # tree at 512, 6.96 at 768, 6.68 at 1024 (profiles/r5/gbdt_rg_wgs_sweep_partials.txt). Default
 # (FDX_RG_WGS unset): rows / 2731, in [128, 512], a multiple of 64.
 RG_TARGET_WGS = int(os.environ.get("FDX_RG_WGS", 0))
+# workgroups of the listed (level >= 1) passes, which cover fewer rows than the root's: 1M rows
+# fit 0.1146 s at 384 (the root's), 0.1105-0.1114 at 256, 0.112 at 192, 0.120 at 128; 10M rows
+# 6.40-6.45 ms a tree at 512 (the root's), 6.53-6.61 at 384 (profiles/r5/gbdt_rg_list_wgs_sweep.txt).
+# Default (FDX_RG_LIST_WGS unset): rows / 4096, in [128, 512], a multiple of 64.
+RG_LIST_WGS = int(os.environ.get("FDX_RG_LIST_WGS", 0))
 
 
 def rg_default_wgs(n_rows: int) -> int:
     """Workgroups of a row-group pass over ``n_rows`` rows (see RG_TARGET_WGS)."""
     return int(min(512, max(128, round(n_rows * 1.5 / 4096 / 64) * 64)))
+
+
+def rg_list_default_wgs(n_rows: int) -> int:
+    """Workgroups of a listed (level >= 1) row-group pass (see RG_LIST_WGS)."""
+    return int(min(512, max(128, round(n_rows / 4096 / 64) * 64)))
 # work model of a (group, chunk) workgroup: cost ~ RG_ALPHA * rows + entries (a row costs its
 # (ptr, digits) loads whether or not it has entries in the group)
 RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 16.0))
@@ -298,6 +308,13 @@ class RowGroups:
             assert (tab[0] < self.G).all() and (tab[1] < tab[2]).all()
             t = self._work[key] = torch.from_numpy(tab).to(self.gbase.device)
         return t
+
+    def list_work(self) -> torch.Tensor:
+        """The work table of the listed (level >= 1) passes (RG_LIST_WGS)."""
+        return self.work(RG_LIST_WGS or rg_list_default_wgs(self.n_rows))
+
+    def list_work_first(self) -> torch.Tensor:
+        return self.work_first(RG_LIST_WGS or rg_list_default_wgs(self.n_rows))
 
     def work_first(self, target_wgs: int = 0, alpha: float = None) -> torch.Tensor:
         """[G + 1] int32: the first work-table entry of each group (work() lists a group's chunks
