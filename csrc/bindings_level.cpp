@@ -313,6 +313,10 @@ class RfLevels {
     g_boff_ = get(c, "boff");
     g_wide_ = get_opt(c, "wide");
     g_counted_ok_ = c["counted"].cast<bool>() && fdx::partition_counts_ok(N);
+    // fewest-rows builds (LevelChooseArgs) where the row lists are counted by their own pass; the
+    // partition counts the rows in one grid pass (8 rows a thread, <= 8192 blocks)
+    g_choose_ = c["choose_rows"].cast<bool>() && (N + 7) / 8 <= 8192ll * 256;
+    if (g_choose_ && !g_rows_.defined()) g_rows_ = at::zeros({32 * 64}, row_node_.options());
     g_part_multi_ = c["part_multi"].cast<bool>();
     FDX_CHECK(sub_of_.has_value() && counts_host_dev_ != nullptr, "gbdt_setup: sub_of and mapped counts");
     if (!g_ev_) FDX_CHECK(hipEventCreateWithFlags(&g_ev_, hipEventDisableTiming) == hipSuccess, "event");
@@ -742,6 +746,10 @@ class RfLevels {
     }
     const Tensor& counts = st_["counts"];
     a.node_parent = p<int32_t>(st_["parent"]);    // (column pass first: the row pass sees final nodes)
+    if (rows_base_) {                                // (gbdt_level: rows per next-level node)
+      a.rows_out = p<int32_t>(g_rows_);
+      a.rows_base = rows_base_;
+    }
     if (count_work) {                                // the next level's row-list counts (RgListArgs pass 0)
       FDX_CHECK(fdx::partition_counts_ok(a.N) && count_work->scalar_type() == at::kInt, "row-list counts: N / work");
       a.count_work = p<int32_t>(*count_work);
@@ -812,7 +820,26 @@ class RfLevels {
       zero = g_hist_[nxt].narrow(0, 0, 2 * (int64_t)n_open);
     }
     g_counted_ = more && g_counted_ok_;
+    const bool choose = more && g_choose_ && !g_counted_;
+    const Tensor& counts = st_["counts"];
+    const int32_t* base = d == 0 ? p<int32_t>(g_one_) : p<int32_t>(counts) + (d - 1) * counts.size(1) + 3;
+    rows_base_ = choose ? base : nullptr;         // (read by partition())
     partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
+    rows_base_ = nullptr;
+    if (choose) {
+      fdx::LevelChooseArgs ca{};
+      ca.counts = p<int32_t>(counts) + d * counts.size(1);
+      ca.rows_base = base;
+      ca.rows_out = p<int32_t>(g_rows_);
+      ca.next_open = p<int32_t>(g_open_[nxt]);
+      ca.node_slot = p<int32_t>(st_["node_slot"]);
+      ca.s2n = p<int32_t>(st_["s2n"]);
+      ca.sub_dst = p<int32_t>(st_["sub_dst"]);
+      ca.sub_sib = p<int32_t>(st_["sub_sib"]);
+      ca.sub_of = p<int32_t>(sub_of_);
+      fdx::launch_level_choose_builds(ca, s);
+      C10_HIP_KERNEL_LAUNCH_CHECK();
+    }
   }
 
   std::vector<ItemGroup> groups_;
@@ -847,7 +874,9 @@ class RfLevels {
     int32_t n;
   } g_wl_{};                               // the listed levels' work table
   int64_t g_em_min_rows_ = 0;
-  bool g_counted_ok_ = false, g_counted_ = false, g_part_multi_ = false;
+  bool g_counted_ok_ = false, g_counted_ = false, g_part_multi_ = false, g_choose_ = false;
+  Tensor g_rows_;
+  const int32_t* rows_base_ = nullptr;
   hipEvent_t g_ev_ = nullptr;
 };
 

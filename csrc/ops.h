@@ -70,6 +70,7 @@ void block_bounds_cpu(const int32_t* csc_row, const int64_t* colptr, const int32
                       int64_t row_block, int64_t* bounds);
 
 // ---------------------------------------------------------------- tree engine (tree_kernels.hip / tree_cpu.cpp)
+struct LevelChooseArgs;
 struct QuantArgs;
 struct SlotArgs;
 struct HistArgs;
@@ -111,6 +112,7 @@ struct SelectArgs;
 // the partition's row pass may write the next level's row-list counts (PartitionArgs count_work):
 // 512-row list waves and one grid pass over the rows
 bool partition_counts_ok(int64_t N);
+void launch_level_choose_builds(const LevelChooseArgs& a, hipStream_t s);
 void launch_hist_select_groups(const SelectArgs& a, hipStream_t s);
 void launch_split_best(const double* gain, const int32_t* bin, const int64_t* left, int32_t nodes, int32_t Fa,
                        int64_t f0, int64_t* out, hipStream_t s, const SplitArgs* partials = nullptr);

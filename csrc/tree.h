@@ -326,6 +326,23 @@ struct RgHistArgs {
   const int32_t* wg_first;
 };
 
+// After a level's partition: per sibling pair of the next level, build the child with FEWER ROWS
+// (rows from PartitionArgs rows_out) instead of the plan's smaller hessian sum, rewriting the
+// plan's build tables (node_slot, s2n, sub_dst, sub_sib, sub_of). The histograms are exact
+// integer sums, so the trees do not depend on which sibling is built; the row lists get shorter
+// (bench/probes/list_oracle.py: the hessian rule listed 6-24 % more rows than needed).
+struct LevelChooseArgs {
+  const int32_t* counts;          // the level's counts row ([2] = builds of the next level)
+  const int32_t* rows_base;       // first node id of the next level
+  int32_t* rows_out;              // [32][64] spread row counts (read and zeroed here)
+  const int32_t* next_open;
+  int32_t* node_slot;
+  int32_t* s2n;
+  int32_t* sub_dst;
+  int32_t* sub_sib;
+  int32_t* sub_of;                // optional
+};
+
 // Whether group g of a pass listing T rows takes the entry-major pass.
 FDX_HD bool rg_use_em(const RgHistArgs& a, int g, int64_t T) {
   if (a.erow == nullptr || a.gmode[g] != 0 || a.gbase[g] < a.ebase || a.nslots != 1) return false;
@@ -561,6 +578,10 @@ struct PartitionArgs {
   int32_t* count_work;
   const int32_t* count_slot;
   const int32_t* count_nslots;
+  // optional (one grid pass over the rows): the rows of each next-level node, node id *rows_base + i
+  // for i < 64, added into rows_out[(block % 32) * 64 + i] (32 spread copies; LevelChooseArgs)
+  int32_t* rows_out;
+  const int32_t* rows_base;
   // optional: zero this int64 range on the way (the next level's histograms: no fill launch)
   int64_t* zero;
   int64_t zero_n;

@@ -1228,8 +1228,10 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
   }
   const int64_t stride = (int64_t)gridDim.x * 256 * kPartRows;
   uint32_t csl[kPartRows];                 // (count_work) the rows' next-level slots, 0xff: none
+  uint32_t rix[kPartRows];                 // (rows_out) the rows' next-level node index, 0xff: none
 #pragma unroll
-  for (int k = 0; k < kPartRows; ++k) csl[k] = 0xffu;
+  for (int k = 0; k < kPartRows; ++k) csl[k] = rix[k] = 0xffu;
+  const int32_t rbase = a.rows_out != nullptr ? *a.rows_base : 0;
   const int32_t cns = a.count_work != nullptr ? *a.count_nslots : 0;
   for (int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kPartRows; r0 < a.N; r0 += stride) {
     if (r0 + kPartRows <= a.N) {
@@ -1251,6 +1253,13 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
       }
 #pragma unroll
       for (int k = 0; k < kPartRows; ++k) n[k] = c[k] >= 0 ? c[k] : n[k];
+      if (a.rows_out != nullptr) {
+#pragma unroll
+        for (int k = 0; k < kPartRows; ++k) {
+          const int32_t i = n[k] - rbase;
+          rix[k] = (i >= 0 && i < 64) ? (uint32_t)i : 0xffu;
+        }
+      }
       p[0] = make_int4(n[0], n[1], n[2], n[3]);
       p[1] = make_int4(n[4], n[5], n[6], n[7]);
       if (a.count_work != nullptr) {
@@ -1303,15 +1312,18 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
           const int32_t sk = (n >= 0 && n < a.num_nodes) ? a.count_slot[n] : -1;
           csl[r - r0] = (sk >= 0 && sk < cns) ? (uint32_t)sk : 0xffu;
         }
+        if (a.rows_out != nullptr) {
+          const int32_t i = n - rbase;
+          rix[r - r0] = (i >= 0 && i < 64) ? (uint32_t)i : 0xffu;
+        }
       }
     }
   }
-  if (a.count_work != nullptr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (a.count_work != nullptr && w * 64 * kPartRows < a.N) {       // (wave-uniform)
     // the wave's 512 rows (64 lanes x 8, one grid pass: host-checked) = RgListArgs pass 0's wave
     // w: per slot, its rows counted with ballots, lane s holding slot s's count
-    const int lane = threadIdx.x & 63;
-    const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-    if (w * 64 * kPartRows >= a.N) return;       // (wave-uniform)
     int32_t cnt = 0;
 #pragma unroll
     for (int k = 0; k < kPartRows; ++k) {
@@ -1324,6 +1336,59 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
       }
     }
     if (lane < cns) a.count_work[2 * cns + w * cns + lane] = cnt;
+  }
+  if (a.rows_out != nullptr) {             // (block-uniform; one grid pass: host-checked)
+    // rows per next-level node: wave ballots -> the block's LDS counts -> 64 spread atomics
+    __shared__ int32_t s_rows[64];
+    if (threadIdx.x < 64) s_rows[threadIdx.x] = 0;
+    __syncthreads();
+    int32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPartRows; ++k) {
+      uint64_t act = __ballot(rix[k] != 0xffu);
+      while (act) {
+        const uint32_t sv = __shfl(rix[k], __ffsll((unsigned long long)act) - 1, 64);
+        const uint64_t m = __ballot(rix[k] == sv);
+        if ((uint32_t)lane == sv) cnt += __popcll(m);
+        act &= ~m;
+      }
+    }
+    if (cnt) atomicAdd(&s_rows[lane], cnt);
+    __syncthreads();
+    if (threadIdx.x < 64 && s_rows[threadIdx.x])
+      atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);
+  }
+}
+
+// LevelChooseArgs: one wave; lane i sums node i's 32 spread row counts (and zeroes them), then
+// lane b < builds takes build b's sibling pair.
+__global__ __launch_bounds__(64) void level_choose_builds_kernel(LevelChooseArgs a) {
+  __shared__ int32_t rows[64];
+  const int t = threadIdx.x;
+  int32_t sum = 0;
+  for (int c = 0; c < 32; ++c) {
+    sum += a.rows_out[c * 64 + t];
+    a.rows_out[c * 64 + t] = 0;
+  }
+  rows[t] = sum;
+  __syncthreads();
+  const int32_t nb = a.counts[2], base = *a.rows_base;
+  for (int32_t b = t; b < nb; b += 64) {
+    const int32_t jl = a.sub_dst[b];
+    if (jl < 0) continue;                            // a lone open child: built anyway
+    const int32_t jb = a.s2n[b];
+    const int32_t nbuilt = a.next_open[jb], nlarge = a.next_open[jl];
+    const int32_t ib = nbuilt - base, il = nlarge - base;
+    if (ib < 0 || ib >= 64 || il < 0 || il >= 64 || rows[il] >= rows[ib]) continue;
+    a.node_slot[nbuilt] = -1;
+    a.node_slot[nlarge] = b;
+    a.s2n[b] = jl;
+    a.sub_dst[b] = jb;
+    a.sub_sib[b] = jl;
+    if (a.sub_of != nullptr) {
+      a.sub_of[jl] = -1;
+      a.sub_of[jb] = b;
+    }
   }
 }
 
@@ -1857,6 +1922,10 @@ void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const 
   if (a.node_parent != nullptr) cols();   // (column pass first: PartitionArgs node_parent)
   if (a.N > 0) hipLaunchKernelGGL(partition_default_kernel, dim3(grid_for((a.N + kPartRows - 1) / kPartRows)), dim3(256), 0, s, a);
   if (a.node_parent == nullptr) cols();
+}
+
+void launch_level_choose_builds(const LevelChooseArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(level_choose_builds_kernel, dim3(1), dim3(64), 0, s, a);
 }
 
 bool partition_counts_ok(int64_t N) {

@@ -325,6 +325,26 @@ LEAN_RF = os.environ.get("FDX_RF_LEAN", "1") == "1"
 # single-process GBDT trees on the row-group engine: the level loop runs in the runner (C++,
 # RfLevels.gbdt_levels; 0: the generic Python loop)
 GBDT_CXX_LEVELS = os.environ.get("FDX_GBDT_CXX_LEVELS", "1") == "1"
+# ... which builds the sibling with fewer rows (not the smaller hessian sum) where the row lists
+# count their own rows (above 4M rows, or FDX_PARTITION_COUNTS=0): same trees, shorter lists
+GBDT_CHOOSE_ROWS = os.environ.get("FDX_GBDT_CHOOSE_ROWS", "1") == "1"
+# diagnostics (bench/probes/list_oracle.py; generic loop, syncs every level): per listed level,
+# (tree, depth, rows listed, rows a fewest-rows sibling choice would list) into LIST_ORACLE_LOG
+LIST_ORACLE = os.environ.get("FDX_LIST_ORACLE", "0") == "1"
+LIST_ORACLE_LOG = []
+
+
+def _list_oracle(st, ws, cur, n_open, n_build, tree_index, d):
+    """Rows the level's row lists hold vs the fewest possible (per sibling pair the child with
+    fewer rows; a lone open child is built anyway)."""
+    T = int(ws.rg_start[n_build])
+    cnt = torch.bincount(ws.row_node.long().clamp(min=0), minlength=st.parent.numel()).cpu().numpy()
+    open_ = st.open[cur][:n_open].cpu().numpy()
+    par = st.parent.cpu().numpy()[open_]
+    best = {}
+    for node, p in zip(open_, par):
+        best[p] = min(best.get(p, 1 << 62), int(cnt[node]))
+    LIST_ORACLE_LOG.append((int(tree_index), int(d), T, int(sum(best.values()))))
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
 RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
 # split search: a wave per (node, feature) for the features with > 16 bins
@@ -1244,7 +1264,7 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
         hist_a=hists[0], hist_b=hists[1], packed=torch.empty((1 << (D - 1), 5), dtype=torch.int64, device=dev),
         one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff,
         wide=_wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, counted=PARTITION_COUNTS, dbg=RG_DBG,
-        part_multi=RG_PARTIALS_MULTI))
+        part_multi=RG_PARTIALS_MULTI, choose_rows=GBDT_CHOOSE_ROWS))
     ws._gbdt_levels = (runner, hists)
     return hists
 
@@ -1671,6 +1691,8 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                         else None
                     C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
                                    ws.rg_list, ws.rowdig, ws.rg_listdig, emdig, counted=rg_counted)
+                    if LIST_ORACLE:
+                        _list_oracle(st, ws, cur, n_open, n_build, tree_index, d)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    ws.rg_listdig, n_build, rg.gmode, wtab, s2n, hist_target, h_stride,
                                    *shard_args, RG_DBG, **(rg.em_args(emdig) if emdig is not None else {}), **part)
