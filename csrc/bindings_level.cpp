@@ -461,6 +461,9 @@ class RfLevels {
       sbin_ = at::empty({need}, out.options().dtype(at::kInt));
       sleft_ = at::empty({2 * need}, out.options().dtype(at::kLong));
     }
+    // (the row stride always comes from hist: a compact DP level's boff[Fa] is the next shard's
+    // offset, not this shard's bin total, so the kernels' boff[Fa] fallback must never be taken)
+    FDX_CHECK(hist.size(1) > 0, "hist rows of at least one bin");
     fdx::SplitArgs a{};
     a.hist = p<int64_t>(hist);
     a.totals = p<int64_t>(totals);

@@ -910,6 +910,9 @@ void split_find(const Tensor& hist, const Tensor& totals, const Tensor& boff, co
   } else {
     FDX_CHECK(hist.size(0) >= nodes, "hist must have a row per node");
   }
+  // (the row stride comes from hist, never the kernels' boff[Fa] fallback: a compact DP level's
+  // boff[Fa] is the next shard's offset, not this shard's bin total)
+  FDX_CHECK(hist.size(1) > 0, "hist rows of at least one bin");
   a.hist_stride = hist.size(1);
   a.num_nodes = nodes;
   a.Fa = Fa;

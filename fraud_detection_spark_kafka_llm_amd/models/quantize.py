@@ -541,6 +541,12 @@ def _quantize_counts(vc, indptr, idx, counts, scale, N, F, max_bins, all_reduce_
     k = torch.arange(TB, device=dev) - bstart[f_of_bin]
     thresholds = ((k.to(torch.float64) + 0.5) * scale[fid_orig][f_of_bin]).cpu().numpy()
     lens = fo.colptr[1:] - fo.colptr[:-1]
+    if fo.dropped is not None and bool(((~active) & (lens > 0)).any()):
+        # the order was already compacted in place for an earlier quantisation whose CSC may still
+        # alias it: a larger drop set gets an order of its own instead of sliding entries under it
+        with tracing.span("q.order"):
+            fo = feature_order(indptr, idx, counts, F)
+        lens = fo.colptr[1:] - fo.colptr[:-1]
     if bool(((~active) & (lens > 0)).any()):
         # the inactive features' entries (all-zero values: IDF 0 for terms in every document)
         # leave the shared feature order in place, so the order stays the CSC (no 5 B/entry copy)

@@ -117,3 +117,26 @@ def test_trees_on_idf_zero_features_equal_trees_without_them():
     assert full._feature_order.dropped is not None
     kw = dict(num_trees=3, max_depth=4, bootstrap=True, feature_subset="sqrt", seed=1, device="cpu")
     assert sig(fit_forest(full, y, **kw)) == sig(fit_forest(ref, y, **kw))
+
+
+def test_larger_drop_set_does_not_move_an_earlier_csc():
+    """A second quantisation of the same column that needs MORE features dropped builds an order
+    of its own: the first one's CSC (an alias of the shared, already compacted order) is left as
+    it was, and both quantisations equal fresh ones."""
+    from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
+    from fraud_detection_spark_kafka_llm_amd.models.quantize import quantize
+
+    indptr, idx, cnt, f = _csr(seed=11, n=1500, f=40)
+    cnt = cnt % 7 + 1
+    idf1 = torch.ones(f, dtype=torch.float64)
+    idf1[[3, 9]] = 0.0
+    idf2 = idf1.clone()
+    idf2[[5, 21]] = 0.0
+    vc = VectorColumn.tfidf(f, indptr, idx, cnt, idf1, feature_order(indptr, idx, cnt, f))
+    q1 = quantize(vc, max_bins=16, counts=vc.tf_counts, scale=idf1)
+    row1, col1 = q1.csc_row.clone(), q1.colptr.clone()
+    q2 = quantize(vc, max_bins=16, counts=vc.tf_counts, scale=idf2)
+    assert torch.equal(q1.csc_row, row1) and torch.equal(q1.colptr, col1)
+    for q, idf in ((q1, idf1), (q2, idf2)):
+        fresh = quantize(VectorColumn.tfidf(f, indptr, idx, cnt, idf), max_bins=16, counts=cnt, scale=idf)
+        assert torch.equal(q.csc_row, fresh.csc_row) and torch.equal(q.colptr, fresh.colptr)
