@@ -103,7 +103,7 @@ class PhaseGuard:
     a MAX all-reduce of an error flag (a phase that failed on one rank is reported by rank 0 too).
     A phase still running after ``timeout_s`` (a hang, e.g. a collective waiting for a rank that
     died) is cut off by a watchdog thread: it prints the record as it stands (rank 0) and ends the
-    process with status 0, on every rank, well inside the process group's own timeout (which
+    process with status 3 (a hang is a failure, not a clean run), on every rank, well inside the process group's own timeout (which
     would abort the job without a record)."""
 
     def __init__(self, record: dict, rank: int, timeout_s: float):
@@ -114,7 +114,7 @@ class PhaseGuard:
         if self.rank == 0:
             print(json.dumps(self.record), flush=True)
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(3)
 
     def run(self, name: str, fn, dev) -> None:
         timer = threading.Timer(self.timeout_s, self._expire, args=(name,))

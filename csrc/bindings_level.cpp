@@ -14,8 +14,11 @@
 // same (tests: the device loop with and without the runner, and every DP world size).
 #include <torch/extension.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -31,7 +34,7 @@ namespace py = pybind11;
 using at::Tensor;
 using c10::optional;
 
-#define FDX_CHECK(cond, msg) TORCH_CHECK(cond, "fdx.level: ", msg)
+#define FDX_CHECK(cond, ...) TORCH_CHECK(cond, "fdx.level: ", __VA_ARGS__)
 
 hipStream_t cur_stream(const at::Device& d) { return c10::hip::getCurrentHIPStream(d.index()).stream(); }
 
@@ -44,6 +47,27 @@ optional<Tensor> get_opt(const py::dict& c, const char* k) {
 
 template <class T>
 T* p(const Tensor& t) { return t.data_ptr<T>(); }
+
+// Host wait for a level's event, called with the GIL released: spins on hipEventQuery while the
+// wait is short (a level's counts usually arrive within 3-40 us), then yields, then sleeps; raises
+// after FDX_LEVEL_TIMEOUT_S (default 600 s) so a hung device never spins forever.
+void wait_event(hipEvent_t ev) {
+  static const double timeout_s = [] {
+    const char* e = std::getenv("FDX_LEVEL_TIMEOUT_S");
+    return e ? std::atof(e) : 600.0;
+  }();
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return;
+    FDX_CHECK(e == hipErrorNotReady, "level event: ", hipGetErrorString(e));
+    const double el = std::chrono::duration<double>(clk::now() - t0).count();
+    FDX_CHECK(el < timeout_s, "level event still pending after ", timeout_s, " s (FDX_LEVEL_TIMEOUT_S)");
+    if (el > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    else if (el > 2e-4) std::this_thread::yield();
+  }
+}
 
 template <class T>
 T* p(const optional<Tensor>& t) { return (t && t->defined()) ? t->data_ptr<T>() : nullptr; }
@@ -338,10 +362,7 @@ class RfLevels {
     const Tensor& ch = st_["counts_host"];
     const int64_t cw = ch.size(1);
     for (int64_t d = 1; d < max_depth_; ++d) {
-      hipError_t e;
-      while ((e = hipEventQuery(g_ev_)) == hipErrorNotReady) {
-      }
-      FDX_CHECK(e == hipSuccess, "level event");
+      wait_event(g_ev_);
       const volatile int32_t* row = p<int32_t>(ch) + (d - 1) * cw;     // (written by the plan itself)
       const int32_t n_open = row[1], n_build = row[2];
       if (n_open == 0) break;
@@ -897,5 +918,7 @@ void register_level_ops(pybind11::module& m) {
       .def("leaf_update", &RfLevels::leaf_update)
       .def("gbdt_setup", &RfLevels::gbdt_setup)
       .def("gbdt_root", &RfLevels::gbdt_root)
-      .def("gbdt_levels", &RfLevels::gbdt_levels);
+      // (no Python objects inside: the GIL is released for the level loop and its host waits, so a
+      // concurrent forest thread keeps running)
+      .def("gbdt_levels", &RfLevels::gbdt_levels, py::call_guard<py::gil_scoped_release>());
 }

@@ -948,6 +948,8 @@ def grow_tree(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int,
                 # rows keep the shard-major stride Bs (>= this shard's bins): the split search
                 # reads them in place; every open node is built or subtracted, so no zero fill
                 mine = coll.reduce_scatter(rs_buf) if nb else None            # [nb, Bs, 2]
+                # (cur_hist below is left uninitialised: every open node must be built or subtracted)
+                assert nb + len(subtract) == nl, (d, nb, len(subtract), nl)
                 if nb == nl and build == open_nodes:
                     cur_hist = mine
                 else:

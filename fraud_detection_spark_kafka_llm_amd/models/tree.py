@@ -80,6 +80,17 @@ def prune_same_prediction(t: Tree) -> Tree:
     return Tree(feat, t.threshold, left, right, t.stats, t.impurity, gain, t.raw_count, t.prediction, t.root).compacted()
 
 
+def _local_lane_cap(Q) -> int:
+    """Trees this rank can keep in flight: FDX_RF_INFLIGHT, and on the device no more lanes than
+    half the free HBM holds (each lane holds a workspace of ~27 B per row, utils/memory.py)."""
+    inflight = max(1, forest_batch.TREES_IN_FLIGHT)
+    if Q.device.type == "cuda" and inflight > 1:
+        from ..utils.memory import rf_lanes_that_fit
+
+        inflight = rf_lanes_that_fit(Q.n_rows, inflight, torch.cuda.mem_get_info(Q.device)[0])
+    return inflight
+
+
 def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bins: int = 32, min_instances: int = 1,
                min_info_gain: float = 0.0, bootstrap: bool = False, feature_subset: str = "all", seed: int = 0,
                impurity: str = "gini", subsampling_rate: float = 1.0, device=None, weights=None,
@@ -117,13 +128,12 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
     trees = ckpt.load_trees() if (ckpt is not None and resume) else []
     # PAR-05: several trees in flight, each on its own stream (models/forest_batch.py); under data
     # parallelism the lanes advance in FIFO order, so every rank issues one collective sequence
-    inflight = max(1, forest_batch.TREES_IN_FLIGHT)
-    if Q.device.type == "cuda" and inflight > 1:
-        # each lane holds a workspace of ~27 B per row (utils/memory.py): no more lanes than half
-        # the free HBM holds
-        from ..utils.memory import rf_lanes_that_fit
-
-        inflight = rf_lanes_that_fit(Q.n_rows, inflight, torch.cuda.mem_get_info(Q.device)[0])
+    inflight = _local_lane_cap(Q)
+    if coll.active:
+        # every rank must take the same path with the same lane count (ForestLanes, the lane groups
+        # and their batched collective sizes, or the per-tree grow_tree fallback issue different
+        # collective sequences): the smallest rank's cap wins
+        inflight = int(coll.min(torch.tensor([inflight], dtype=torch.int64, device=Q.device)).item())
     lanes = None
     if inflight > 1 and num_trees - len(trees) > 1 and device_levels_ok(params, w):
         with tracing.span("forest.lanes"):

@@ -228,5 +228,8 @@ class Collectives:
     def max(self, t):
         return all_reduce_max(t) if self.active else t
 
+    def min(self, t):
+        return all_reduce(t, dist.ReduceOp.MIN) if self.active else t
+
     def gather_keys(self, keys, counts):
         return all_gather_var(keys, counts) if self.active else (keys, counts)

@@ -15,7 +15,7 @@ import torch
 class StreamSwitch:
     """Reusable context manager: make ``stream`` current (no-op for None), restore on exit."""
 
-    __slots__ = ("sid", "didx", "dtype", "prev")
+    __slots__ = ("sid", "didx", "dtype", "prev", "prev_dev")
 
     def __init__(self, stream):
         if stream is None:
@@ -25,6 +25,8 @@ class StreamSwitch:
 
     def __enter__(self):
         if self.sid is not None:
+            # (_cuda_setStream also makes the stream's device current: restored on exit)
+            self.prev_dev = torch._C._cuda_getDevice()
             self.prev = torch._C._cuda_getCurrentStream(self.didx)
             torch._C._cuda_setStream(stream_id=self.sid, device_index=self.didx, device_type=self.dtype)
         return self
@@ -33,6 +35,8 @@ class StreamSwitch:
         if self.sid is not None:
             p = self.prev
             torch._C._cuda_setStream(stream_id=p[0], device_index=p[1], device_type=p[2])
+            if self.prev_dev != self.didx:
+                torch._C._cuda_setDevice(self.prev_dev)
         return False
 
 

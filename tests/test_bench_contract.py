@@ -76,11 +76,11 @@ def test_bench_rf_fault_two_ranks_still_prints_the_headline():
 @pytest.mark.gpu
 def test_bench_phase_watchdog_prints_the_record_of_a_hung_phase():
     """A phase that hangs (FDX_BENCH_FAULT=rf:hang) is cut off after --phase-timeout: the record
-    is printed as it stands with rf_error, and the process exits 0."""
+    is printed as it stands with rf_error, and the process exits 3 (a hang is not a clean run)."""
     env = {**os.environ, "FDX_BENCH_FAULT": "rf:hang"}
     out = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *TINY, "--phase-timeout", "20"], cwd=REPO,
                          capture_output=True, text=True, timeout=600, env=env)
-    assert out.returncode == 0, out.stderr[-3000:]
+    assert out.returncode == 3, out.stderr[-3000:]
     rec = _json_line(out.stdout)
     assert KEYS <= set(rec) and rec["value"] > 0 and rec["p50_single_dialogue_ms"] > 0
     assert rec["rf_error"].startswith("timeout") and "kafka_dialogues_per_s" not in rec
