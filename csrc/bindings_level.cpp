@@ -14,6 +14,7 @@
 // same (tests: the device loop with and without the runner, and every DP world size).
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -186,6 +187,9 @@ class RfLevels {
       fdx::launch_grad_max(p<double>(*margin), p<float>(*label), p<float>(*g), p<float>(*h), N,
                            reinterpret_cast<double*>(mv + kSet * parity_), pi, s);
       max_parts = mv + kSet * parity_;
+      // data parallel: the max |g|, |h| slots all-reduced (MAX of the bit patterns of non-negative
+      // doubles) before the quantisation reads them, so every rank quantises with one exponent
+      if (dp_) dp_max_cb_(maxv_.narrow(0, kSet * parity_, kSet));
       maxv = nullptr;
       parity_ ^= 1;
     }
@@ -243,6 +247,32 @@ class RfLevels {
   // tests/test_level_runner.py). Buffers are fixed: the level histograms alternate between two
   // tensors (each sized for its parity's widest level), the partition zeroing the next one.
   void gbdt_setup(const py::dict& c) {
+    rg_setup(c);
+    for (int k = 0; k < 2; ++k) {
+      g_hist_[k] = get(c, k ? "hist_b" : "hist_a");
+      int64_t need = 1;                     // (level d opens at most 2^d nodes)
+      for (int64_t d = k; d < max_depth_; d += 2) need = int64_t{1} << d;
+      FDX_CHECK(g_hist_[k].scalar_type() == at::kLong && g_hist_[k].dim() == 3 && g_hist_[k].size(2) == 2 &&
+                    g_hist_[k].is_contiguous() && g_hist_[k].size(0) >= need &&
+                    reinterpret_cast<uintptr_t>(g_hist_[k].data_ptr()) % 16 == 0,
+                "gbdt_setup: hist_a / hist_b [rows >= widest level of the parity, TB, 2] int64");
+    }
+    gh_.hist_stride = g_hist_[0].size(1);
+    FDX_CHECK(g_hist_[1].size(1) == gh_.hist_stride, "gbdt_setup: hist strides");
+    g_packed_ = get(c, "packed");
+    FDX_CHECK(g_packed_.scalar_type() == at::kLong && g_packed_.dim() == 2 && g_packed_.size(1) == 5 &&
+                  g_packed_.is_contiguous() && g_packed_.size(0) >= (int64_t{1} << (max_depth_ - 1)),
+              "gbdt_setup: packed [widest level, 5] int64");
+    // fewest-rows builds (LevelChooseArgs) where the row lists are counted by their own pass; the
+    // partition counts the rows in one grid pass (8 rows a thread, <= 8192 blocks)
+    const int64_t N = row_node_.numel();
+    g_choose_ = c["choose_rows"].cast<bool>() && (N + 7) / 8 <= 8192ll * 256;
+    if (g_choose_ && !g_rows_.defined()) g_rows_ = at::zeros({32 * 64}, row_node_.options());
+  }
+
+  // The row-group tables and fixed level buffers shared by the single-process (gbdt_setup) and
+  // the data-parallel (gbdt_dp_setup) GBDT level loops.
+  void rg_setup(const py::dict& c) {
     const Tensor ptr = get(c, "rg_ptr"), ent = get(c, "rg_ent"), gbase = get(c, "rg_gbase"),
                  gbin = get(c, "rg_gbin"), gmode = get(c, "rg_gmode"), wg = get(c, "rg_wg");
     const int64_t G = ptr.size(0), N = ptr.size(1) - 1;
@@ -313,21 +343,6 @@ class RfLevels {
     l.list = p<int32_t>(g_rg_list_);
     l.rowdig = reinterpret_cast<const uint32_t*>(p<int32_t>(rowdig_));
     l.listdig = reinterpret_cast<uint32_t*>(p<int32_t>(g_rg_listdig_));
-    for (int k = 0; k < 2; ++k) {
-      g_hist_[k] = get(c, k ? "hist_b" : "hist_a");
-      int64_t need = 1;                     // (level d opens at most 2^d nodes)
-      for (int64_t d = k; d < max_depth_; d += 2) need = int64_t{1} << d;
-      FDX_CHECK(g_hist_[k].scalar_type() == at::kLong && g_hist_[k].dim() == 3 && g_hist_[k].size(2) == 2 &&
-                    g_hist_[k].is_contiguous() && g_hist_[k].size(0) >= need &&
-                    reinterpret_cast<uintptr_t>(g_hist_[k].data_ptr()) % 16 == 0,
-                "gbdt_setup: hist_a / hist_b [rows >= widest level of the parity, TB, 2] int64");
-    }
-    a.hist_stride = g_hist_[0].size(1);
-    FDX_CHECK(g_hist_[1].size(1) == a.hist_stride, "gbdt_setup: hist strides");
-    g_packed_ = get(c, "packed");
-    FDX_CHECK(g_packed_.scalar_type() == at::kLong && g_packed_.dim() == 2 && g_packed_.size(1) == 5 &&
-                  g_packed_.is_contiguous() && g_packed_.size(0) >= (int64_t{1} << (max_depth_ - 1)),
-              "gbdt_setup: packed [widest level, 5] int64");
     g_one_ = get(c, "one");
     g_zero1_ = get(c, "zero1");
     g_open_[0] = st_["open0"];
@@ -337,10 +352,6 @@ class RfLevels {
     g_boff_ = get(c, "boff");
     g_wide_ = get_opt(c, "wide");
     g_counted_ok_ = c["counted"].cast<bool>() && fdx::partition_counts_ok(N);
-    // fewest-rows builds (LevelChooseArgs) where the row lists are counted by their own pass; the
-    // partition counts the rows in one grid pass (8 rows a thread, <= 8192 blocks)
-    g_choose_ = c["choose_rows"].cast<bool>() && (N + 7) / 8 <= 8192ll * 256;
-    if (g_choose_ && !g_rows_.defined()) g_rows_ = at::zeros({32 * 64}, row_node_.options());
     g_part_multi_ = c["part_multi"].cast<bool>();
     FDX_CHECK(sub_of_.has_value() && counts_host_dev_ != nullptr, "gbdt_setup: sub_of and mapped counts");
     if (!g_ev_) FDX_CHECK(hipEventCreateWithFlags(&g_ev_, hipEventDisableTiming) == hipSuccess, "event");
@@ -372,6 +383,93 @@ class RfLevels {
       shape.push_back(n_open);
       shape.push_back(n_build);
     }
+    return shape;
+  }
+
+  // ---- GBDT trees under data parallelism: the same level loop around the level's collectives ----
+  // A DP level (grower.device_tree_steps' shards branch, launch for launch): the row-group pass
+  // writes the built nodes' partial histograms straight into the shard-major send buffer, ONE
+  // reduce-scatter (callback rs) leaves this rank's feature shard of them in out[cur], the split
+  // search runs over the shard (the larger siblings subtracted inside it, rows from level_rows),
+  // ONE all-gather (callback ag) of the best-split tuples feeds the level plan (best over shards),
+  // then the partition zeroes the next level's send region on the way. The root totals ride in the
+  // root's reduce-scatter (dp_root phase 0 / 1) and the quantisation max is one all-reduce (callback
+  // mx, inside prologue()): 13 collectives per depth-6 tree. The callbacks are Python (the process
+  // group's collectives on the current stream); every other launch and the host waits are here.
+  // Sibling choice by rows is off: rows are rank-local, and every rank must build the same nodes.
+  void gbdt_dp_setup(const py::dict& c) {
+    rg_setup(c);
+    dp_ = true;
+    dp_rs_cb_ = c["rs"];
+    dp_ag_cb_ = c["ag"];
+    dp_max_cb_ = c["mx"];
+    dp_S_ = c["S"].cast<int64_t>();
+    dp_Bs_ = c["Bs"].cast<int64_t>();
+    dp_bin_lo_ = get(c, "bin_lo");
+    dp_send_ = get(c, "send");
+    for (int k = 0; k < 2; ++k) {
+      dp_out_[k] = get(c, k ? "out_b" : "out_a");
+      dp_row_of_[k] = get(c, k ? "row_of1" : "row_of0");
+    }
+    dp_ag_in_ = get(c, "ag_in");
+    dp_boff_ = get(c, "sboff");
+    dp_nbins_ = get(c, "snbins");
+    dp_zbin_ = get(c, "szbin");
+    dp_fid_ = get(c, "sfid");
+    dp_f0_ = c["f0"].cast<int64_t>();
+    dp_wide_ = get_opt(c, "swide");
+    dp_dst_row_ = get(c, "dst_row");
+    dp_par_row_ = get(c, "par_row");
+    dp_sib_row_ = get(c, "sib_row");
+    dp_iota_ = get(c, "iota");
+    const int64_t widest = int64_t{1} << std::max<int64_t>(max_depth_ - 1, 1);
+    FDX_CHECK(dp_S_ >= 1 && dp_Bs_ >= 1 && dp_bin_lo_.numel() == dp_S_ + 1 && dp_bin_lo_.scalar_type() == at::kLong,
+              "gbdt_dp_setup: S, Bs, bin_lo [S + 1]");
+    FDX_CHECK(dp_send_.scalar_type() == at::kLong && dp_send_.is_contiguous() &&
+                  dp_send_.numel() >= dp_S_ * std::max<int64_t>(widest, 2) * dp_Bs_ * 2 &&
+                  reinterpret_cast<uintptr_t>(dp_send_.data_ptr()) % 16 == 0,
+              "gbdt_dp_setup: send [S * max(2, widest level) * Bs * 2] int64");
+    for (int k = 0; k < 2; ++k)
+      FDX_CHECK(dp_out_[k].scalar_type() == at::kLong && dp_out_[k].dim() == 3 && dp_out_[k].size(1) == dp_Bs_ &&
+                    dp_out_[k].size(2) == 2 && dp_out_[k].is_contiguous() && dp_out_[k].size(0) >= std::max<int64_t>(widest, 2) &&
+                    dp_row_of_[k].numel() >= widest,
+                "gbdt_dp_setup: out [max(2, widest level), Bs, 2], row_of");
+    FDX_CHECK(dp_ag_in_.scalar_type() == at::kLong && dp_ag_in_.dim() == 2 && dp_ag_in_.size(1) == 5 &&
+                  dp_ag_in_.size(0) >= widest && dp_iota_.numel() >= fdx::kRgMaxSlots &&
+                  dp_boff_.numel() == dp_nbins_.numel() + 1,
+              "gbdt_dp_setup: ag_in [widest, 5], iota, shard tables");
+  }
+
+  // Prologue (with its max all-reduce) done by the caller; level 0 of a DP tree.
+  void gbdt_dp_root(int64_t tree) {
+    FDX_CHECK(dp_ && g_ev_ != nullptr, "gbdt_dp_root before gbdt_dp_setup");
+    c10::hip::HIPGuard guard(dev_.index());
+    gbdt_dp_level(0, 1, 1, tree, cur_stream(dev_));
+  }
+
+  // Levels 1 .. max_depth - 1 of a DP tree (host waits with the GIL released; the collective
+  // callbacks take it back); returns (n_open, n_build) of every level, the root's first.
+  std::vector<int64_t> gbdt_dp_levels(int64_t tree) {
+    c10::hip::HIPGuard guard(dev_.index());
+    const hipStream_t s = cur_stream(dev_);
+    std::vector<int64_t> shape{1, 1};
+    const Tensor& ch = st_["counts_host"];
+    const int64_t cw = ch.size(1);
+    for (int64_t d = 1; d < max_depth_; ++d) {
+      {
+        py::gil_scoped_release nogil;
+        wait_event(g_ev_);
+      }
+      const volatile int32_t* row = p<int32_t>(ch) + (d - 1) * cw;
+      const int32_t n_open = row[1], n_build = row[2];
+      if (n_open == 0) break;
+      FDX_CHECK(n_open <= dp_ag_in_.size(0) && n_build >= 1 && n_build <= fdx::kRgMaxSlots && n_build <= n_open,
+                "dp level counts");
+      gbdt_dp_level(d, n_open, n_build, tree, s);
+      shape.push_back(n_open);
+      shape.push_back(n_build);
+    }
+    dp_allt_ = Tensor();
     return shape;
   }
 
@@ -515,8 +613,9 @@ class RfLevels {
     if (find_prev_) {
       a.parent_hist = find_prev_;
       a.sub_of = p<int32_t>(*sub_of_);
-      a.sub_par = p<int32_t>(st_["sub_par"]);
-      a.sub_sib = p<int32_t>(st_["sub_sib"]);
+      // (data-parallel levels: the subtraction triples as rows, LevelRowsArgs par_row / sib_row)
+      a.sub_par = find_sub_par_ ? find_sub_par_ : p<int32_t>(st_["sub_par"]);
+      a.sub_sib = find_sub_sib_ ? find_sub_sib_ : p<int32_t>(st_["sub_sib"]);
     }
     const int64_t np_ = fdx::split_partials(nodes, Fa);
     if (np_ > 0) {
@@ -866,6 +965,118 @@ class RfLevels {
     }
   }
 
+  void gbdt_dp_level(int64_t d, int32_t n_open, int32_t n_build, int64_t tree, hipStream_t s) {
+    const int cur = (int)(d & 1), nxt = cur ^ 1;
+    const bool more = d + 1 < max_depth_;
+    const int64_t S = dp_S_, Bs = dp_Bs_;
+    const int64_t R = n_build + (d == 0 ? 1 : 0), subs = d == 0 ? 0 : n_build;   // (root: + the totals row)
+    const int64_t chunk = R * Bs;
+    FDX_CHECK(R + subs <= dp_out_[cur].size(0) && S * chunk * 2 <= dp_send_.numel(), "dp level rows");
+    Tensor send = dp_send_.narrow(0, 0, S * chunk * 2).view({S, R, Bs, 2});
+    const Tensor& out = dp_out_[cur];
+    // the built nodes' partial histograms, shard-major (slot k -> row k of every shard chunk)
+    fdx::RgHistArgs a = gh_;
+    a.hist = p<int64_t>(send);
+    a.hist_stride = Bs;
+    a.nslots = n_build;
+    a.nshards = (int32_t)S;
+    a.shard_lo = p<int64_t>(dp_bin_lo_);
+    a.shard_stride = chunk;
+    if (d == 0) {
+      a.slot_node = p<int32_t>(g_zero1_);
+    } else {
+      const bool em = n_build == 1 && g_emdig_.has_value();
+      fdx::RgListArgs l = gl_;
+      l.nslots = n_build;
+      l.wave_count = l.slot_count + 2 * n_build;
+      l.counted = g_counted_ ? 1 : 0;
+      l.masked = em ? reinterpret_cast<uint32_t*>(p<int32_t>(*g_emdig_)) : nullptr;
+      fdx::launch_rg_list(l, s);
+      a.list = l.list;
+      a.slot_start = l.slot_start;
+      a.listdig = l.listdig;
+      a.slot_node = p<int32_t>(dp_iota_);
+      a.wg_g = g_wl_.g;
+      a.wg_p = g_wl_.p;
+      a.wg_np = g_wl_.np;
+      a.n_wg = g_wl_.n;
+      if (a.erow && em) {
+        a.emdig = l.masked;
+        a.em_min_rows = g_em_min_rows_;
+      }
+    }
+    if (g_part_ && (n_build == 1 || g_part_multi_)) {
+      a.part = p<int64_t>(*g_part_);
+      a.wg_first = p<int32_t>(d == 0 ? *g_wg_first_ : *g_wg_first_list_);
+    }
+    fdx::launch_rg_hist(a, s);
+    fdx::DpRootArgs ra{};
+    if (d == 0) {                 // the local root sums into the totals row of every shard chunk
+      FDX_CHECK(root_pending_ != nullptr, "dp root level without its prologue");
+      ra.root_parts = root_pending_;
+      ra.send = p<int64_t>(send);
+      ra.S = (int32_t)S;
+      ra.chunk_words = chunk * 2;
+      ra.tot_word = (R - 1) * Bs * 2;
+      ra.reduced = p<int64_t>(out) + (R - 1) * Bs * 2;
+      ra.stats = p<int64_t>(st_["stats"]);
+      ra.totals = p<int64_t>(g_totals_[0]);
+      fdx::launch_dp_root(ra, 0, s);
+      root_pending_ = nullptr;
+    }
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    dp_rs_cb_(send, out.narrow(0, 0, R));
+    if (d == 0) {
+      fdx::launch_dp_root(ra, 1, s);
+    } else {
+      // the built rows stay where the collective wrote them, the larger siblings go behind them
+      fdx::LevelRowsArgs lr{};
+      lr.s2n = p<int32_t>(st_["s2n"]);
+      lr.sub_dst = p<int32_t>(st_["sub_dst"]);
+      lr.sub_par = p<int32_t>(st_["sub_par"]);
+      lr.prev_row_of = d > 1 ? p<int32_t>(dp_row_of_[nxt]) : nullptr;
+      lr.nb = n_build;
+      lr.bld_base = 0;
+      lr.sub_base = (int32_t)R;
+      lr.row_of = p<int32_t>(dp_row_of_[cur]);
+      lr.dst_row = p<int32_t>(dp_dst_row_);
+      lr.par_row = p<int32_t>(dp_par_row_);
+      lr.sib_row = p<int32_t>(dp_sib_row_);
+      fdx::launch_level_rows(lr, s);
+      find_prev_ = p<int64_t>(dp_out_[nxt]);
+      find_sub_par_ = lr.par_row;
+      find_sub_sib_ = lr.sib_row;
+    }
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    // split search over this rank's features (+ the fused subtraction), best tuples into ag_in
+    Tensor ag_in = dp_ag_in_.narrow(0, 0, n_open);
+    const Tensor open = g_open_[cur].narrow(0, 0, n_open);
+    const Tensor totals = g_totals_[cur].narrow(0, 0, n_open);
+    const bool any = find(out, totals, dp_boff_, dp_nbins_, dp_zbin_, dp_fid_, open, c10::nullopt, tree, ag_in,
+                          d > 0 ? optional<Tensor>(dp_row_of_[cur]) : c10::nullopt, dp_wide_, s);
+    find_prev_ = nullptr;
+    find_sub_par_ = find_sub_sib_ = nullptr;
+    if (any)
+      fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), n_open,
+                             (int32_t)dp_nbins_.numel(), dp_f0_, p<int64_t>(ag_in), s, &last_split_);
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    dp_allt_ = dp_ag_cb_(ag_in).cast<Tensor>();           // [S, n_open, 5]
+    FDX_CHECK(dp_allt_.dim() == 3 && dp_allt_.size(0) == S && dp_allt_.size(1) == n_open && dp_allt_.is_contiguous(),
+              "all-gathered best splits [S, n_open, 5]");
+    const Tensor n_open_ptr = d == 0 ? g_one_ : st_["counts"].select(0, d - 1).narrow(0, 1, 1);
+    fdx::LevelPlanArgs pa = plan_args(d, n_open, dp_allt_, open, n_open_ptr, g_open_[nxt], g_totals_[nxt]);
+    const bool zc = counts_zero_copy(pa, d, false, {});
+    fdx::launch_level_plan(pa, s);
+    after_plan(d, n_open, g_open_[nxt], tree, false, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt,
+               c10::nullopt, c10::nullopt, c10::nullopt, 0, {}, s, zc);
+    FDX_CHECK(hipEventRecord(g_ev_, s) == hipSuccess, "level event record");
+    // the partition zeroes the next level's send region (its builds <= this level's open nodes)
+    optional<Tensor> zero;
+    if (more) zero = dp_send_.narrow(0, 0, S * n_open * Bs * 2);
+    g_counted_ = more && g_counted_ok_;
+    partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
+  }
+
   std::vector<ItemGroup> groups_;
   Tensor csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, row_node_, kexp_;
   optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_, dig16_;
@@ -879,7 +1090,16 @@ class RfLevels {
   const int64_t* root_pending_ = nullptr;   // the last prologue's root slots, until level 0's split
   const int64_t* find_root_ = nullptr;
   const int64_t* find_prev_ = nullptr;
+  const int32_t* find_sub_par_ = nullptr;
+  const int32_t* find_sub_sib_ = nullptr;
   optional<Tensor> sub_of_;
+  // data-parallel GBDT level loop (gbdt_dp_setup)
+  bool dp_ = false;
+  py::object dp_rs_cb_, dp_ag_cb_, dp_max_cb_;
+  int64_t dp_S_ = 1, dp_Bs_ = 1, dp_f0_ = 0;
+  Tensor dp_bin_lo_, dp_send_, dp_out_[2], dp_row_of_[2], dp_ag_in_, dp_boff_, dp_nbins_, dp_zbin_, dp_fid_,
+      dp_dst_row_, dp_par_row_, dp_sib_row_, dp_iota_, dp_allt_;
+  optional<Tensor> dp_wide_;
   bool build_all_ = true;
   int mode_ = 1, max_depth_ = 5, wps_ = 256;
   double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;
@@ -918,6 +1138,9 @@ void register_level_ops(pybind11::module& m) {
       .def("leaf_update", &RfLevels::leaf_update)
       .def("gbdt_setup", &RfLevels::gbdt_setup)
       .def("gbdt_root", &RfLevels::gbdt_root)
+      .def("gbdt_dp_setup", &RfLevels::gbdt_dp_setup)
+      .def("gbdt_dp_root", &RfLevels::gbdt_dp_root)
+      .def("gbdt_dp_levels", &RfLevels::gbdt_dp_levels)
       // (no Python objects inside: the GIL is released for the level loop and its host waits, so a
       // concurrent forest thread keeps running)
       .def("gbdt_levels", &RfLevels::gbdt_levels, py::call_guard<py::gil_scoped_release>());

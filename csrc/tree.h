@@ -538,6 +538,22 @@ FDX_HD void level_rows_slot(const LevelRowsArgs& a, int32_t k) {
   }
 }
 
+// Data-parallel GBDT root (bindings_level.cpp gbdt_dp_level). Phase 0, before the root level's
+// reduce-scatter: the local root sums (the quantisation's kRootSlots slots) go to words tot_word,
+// tot_word + 1 of every shard chunk of the send buffer (the reduce-scatter then sums them across
+// ranks: no all-reduce of its own). Phase 1, after it: the reduced sums become the root state
+// (stats[0] and the level-0 totals row).
+struct DpRootArgs {
+  const int64_t* root_parts;
+  int64_t* send;
+  int32_t S;
+  int64_t chunk_words;
+  int64_t tot_word;
+  const int64_t* reduced;
+  int64_t* stats;
+  int64_t* totals;
+};
+
 struct PartitionArgs {
   int32_t* row_node;              // [N]
   const int32_t* default_child;   // [num_nodes] child for rows absent from the split column (-1: not split)

@@ -1615,6 +1615,23 @@ __global__ __launch_bounds__(64) void level_rows_kernel(LevelRowsArgs a) {
   if (k < a.nb) level_rows_slot(a, k);
 }
 
+__global__ __launch_bounds__(64) void dp_root_kernel(DpRootArgs a, int phase) {
+  if (phase == 0) {
+    int64_t t0, t1;
+    root_sums(a.root_parts, &t0, &t1);
+    for (int32_t s = (int32_t)threadIdx.x; s < a.S; s += 64) {
+      a.send[s * a.chunk_words + a.tot_word] = t0;
+      a.send[s * a.chunk_words + a.tot_word + 1] = t1;
+    }
+  } else if (threadIdx.x == 0) {
+    const int64_t t0 = a.reduced[0], t1 = a.reduced[1];
+    a.stats[0] = t0;
+    a.stats[1] = t1;
+    a.totals[0] = t0;
+    a.totals[1] = t1;
+  }
+}
+
 __global__ void level_plan_kernel(LevelPlanArgs a) {
   if (blockIdx.x != 0) return;
   level_plan_reset(a, (int32_t)threadIdx.x, (int32_t)blockDim.x);
@@ -1907,6 +1924,10 @@ void launch_partition(const PartitionArgs& a, hipStream_t s) {
 void launch_level_rows(const LevelRowsArgs& a, hipStream_t s) {
   if (a.nb <= 0) return;
   hipLaunchKernelGGL(level_rows_kernel, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, s, a);
+}
+
+void launch_dp_root(const DpRootArgs& a, int phase, hipStream_t s) {
+  hipLaunchKernelGGL(dp_root_kernel, dim3(1), dim3(64), 0, s, a, phase);
 }
 
 void launch_level_plan(const LevelPlanArgs& a, hipStream_t s) {

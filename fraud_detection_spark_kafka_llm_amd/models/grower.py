@@ -1271,6 +1271,62 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
     return hists
 
 
+class _DpCollectives:
+    """The level collectives the runner's data-parallel GBDT loop calls back into
+    (csrc/bindings_level.cpp gbdt_dp_level): the level's reduce-scatter into the runner's buffer,
+    the all-gather of the best-split tuples, the quantisation max (in place)."""
+
+    def __init__(self, coll, dev: torch.device):
+        self.coll, self.dev = coll, dev
+
+    def rs(self, send: torch.Tensor, out: torch.Tensor) -> None:
+        with tracing.span("tree.reduce_scatter"), _CollTimer(self.dev):
+            self.coll.reduce_scatter(send, out=out)
+
+    def ag(self, x: torch.Tensor) -> torch.Tensor:
+        with tracing.span("tree.all_gather"), _CollTimer(self.dev):
+            return self.coll.all_gather(x).contiguous()
+
+    def mx(self, t: torch.Tensor) -> None:
+        r = self.coll.max(t)
+        if r is not t:
+            t.copy_(r)
+
+
+def _gbdt_dp_setup(Q, ws, st, params, runner, rg, shards, coll) -> torch.Tensor:
+    """Hands the runner its data-parallel GBDT level loop (RfLevels.gbdt_dp_setup): the row-group
+    tables, the shard-major send buffer, the two reduced-level buffers, the feature shard's split
+    tables and the collective callbacks; once per runner. Returns the root level's send region
+    (zeroed by the prologue)."""
+    cached = getattr(ws, "_gbdt_dp", None)
+    if cached is not None and cached[0] is runner:
+        return cached[1]
+    dev, D, S, Bs = Q.device, int(params.max_depth), int(shards.S), int(shards.Bs)
+    widest = max(1 << max(D - 1, 1), 2)
+    send = torch.empty(S * widest * Bs * 2, dtype=torch.int64, device=dev)
+    outs = [torch.empty((widest, Bs, 2), dtype=torch.int64, device=dev) for _ in range(2)]
+    em = rg.erow is not None and qmod.RG_EM_MIN_FRAC <= 1.0
+    cb = _DpCollectives(coll, dev)
+    runner.gbdt_dp_setup(dict(
+        rg_wg_list=rg.list_work(), rg_wg_first_list=rg.list_work_first() if RG_PARTIALS else None,
+        rg_ptr=rg.ptr, rg_ent=rg.ent, rg_gbase=rg.gbase, rg_gbin=rg.gbin, rg_gmode=rg.gmode, rg_wg=rg.work(),
+        rg_erow=rg.erow, rg_ebase=int(rg.ebase) if rg.erow is not None else 0,
+        emdig=ws.rg_emdig() if em else None, em_min_rows=max(1, int(qmod.RG_EM_MIN_FRAC * Q.n_rows)),
+        rg_part=ws.rg_part(rg, rg.list_work()) if RG_PARTIALS else None,
+        rg_wg_first=rg.work_first() if RG_PARTIALS else None,
+        list_work=ws.rg_work, rg_start=ws.rg_start, rg_list=ws.rg_list, rg_listdig=ws.rg_listdig,
+        one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff, wide=None,
+        counted=PARTITION_COUNTS, dbg=RG_DBG, part_multi=RG_PARTIALS_MULTI,
+        rs=cb.rs, ag=cb.ag, mx=cb.mx, S=S, Bs=Bs, bin_lo=shards.bin_lo, send=send, out_a=outs[0], out_b=outs[1],
+        row_of0=st.row_of[0], row_of1=st.row_of[1], ag_in=torch.empty((widest, 5), dtype=torch.int64, device=dev),
+        sboff=shards.boff, snbins=shards.nbins, szbin=shards.zbin, sfid=shards.fid_orig, f0=int(shards.f0),
+        swide=_wide_features(shards.nbins, shards.Fa) if SPLIT_WIDE else None, dst_row=st.dst_row,
+        par_row=st.par_row, sib_row=st.sib_row, iota=ws.iota(64)))
+    root = send[:S * 2 * Bs * 2]
+    ws._gbdt_dp = (runner, root)
+    return root
+
+
 def _gbdt_runner_levels(Q, runner, tree_index, on_first_wait):
     """The level loop of a single-process GBDT tree in the runner (C++): level 0 is queued, the
     previous tree's host table is built while it runs (on_first_wait), then levels 1.. run with
@@ -1508,7 +1564,19 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     # single-process GBDT rounds on the row-group engine: the level loop runs in the runner
     rg_cxx = ws.rowgroups() if (native_prologue and gbdt_native and GBDT_CXX_LEVELS and SPLIT_SUBTRACT and
                                 np_ == 4 and margin is not None and g is None) else None
-    if native_prologue:
+    # data-parallel GBDT rounds on the row-group engine: the same runner loop around the level
+    # collectives (RfLevels.gbdt_dp_levels; the collectives are Python callbacks)
+    rg_dp = ws.rowgroups() if (runner is not None and shards is not None and gbdt_native and GBDT_CXX_LEVELS and
+                               SPLIT_SUBTRACT and np_ == 4 and margin is not None and g is None) else None
+    if rg_dp is not None:
+        with tracing.span("tree.quant"):
+            root_zero = _gbdt_dp_setup(Q, ws, st, params, runner, rg_dp, shards, coll)
+            g, h = ws.gh()
+            # gradients + max slots (all-reduced by the runner's callback) + arena image + the root's
+            # send region zeroed, then the quantisation
+            runner.prologue(margin, g, h, label, None, int(tree_index), False, 4, None, ws.totals, None, Q.row0,
+                            root_zero, st.arena_init_dev)
+    elif native_prologue:
         # the root histogram is zeroed by the prologue's first launch
         if rg_cxx is not None:
             pre_hist = _gbdt_levels_setup(Q, ws, st, params, runner, rg_cxx)[0][:1]
@@ -1539,7 +1607,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             C.tree_logistic_grad(margin, label, weight, g, h)
         ws.row_node.zero_()
     with tracing.span("tree.quant"):
-        if native_prologue:
+        if native_prologue or rg_dp is not None:
             pass
         elif np_ == 4:
             C.tree_quant_max(g, h, label, weight, seed, int(tree_index), bool(bootstrap), mode_rs, Q.n_rows,
@@ -1552,7 +1620,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                          ws.kexp, ws.totals, ws.digp, Q.row0)
     # root: node 0, open list [0] with the exact totals (no host round trip); under data
     # parallelism the totals are summed by the root level's reduce-scatter (LaneBufs.tot_bin)
-    if not native_prologue:
+    if not native_prologue and rg_dp is None:
         st.arena.copy_(st.arena_init, non_blocking=True)
         st.open[0][:1].zero_()
     if shards is None and not native_prologue:
@@ -1576,6 +1644,17 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     if rg_cxx is not None:
         _gbdt_runner_levels(Q, runner, int(tree_index), on_first_wait)
         on_first_wait = None
+        generic_depth = 0
+    elif rg_dp is not None:
+        runner.gbdt_dp_root(int(tree_index))
+        if on_first_wait is not None:
+            on_first_wait()
+            on_first_wait = None
+        shape = runner.gbdt_dp_levels(int(tree_index))
+        for j in range(0, len(shape), 2):
+            LEVEL_STATS["levels"] += 1
+            LEVEL_STATS["built_nodes"] += shape[j + 1]
+            LEVEL_STATS["hist_bytes"] += shape[j + 1] * TB * 16
         generic_depth = 0
     elif runner is not None and sampled and FUSED_PACK and LEAN_RF:
         # sampled RF levels on the native runner: the lean loop (same launches, far less Python)
@@ -1888,7 +1967,7 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
     if on_first_wait is not None:          # (a one-level tree) the previous table first
         on_first_wait()
     # one read of the node table per tree: the arena (table + exponents) in one D2H copy, one wait
-    if not native_prologue:                # (the prologue's last workgroup wrote them)
+    if not native_prologue and rg_dp is None:      # (the prologue's quantisation wrote them)
         st.kexp_slot.copy_(ws.kexp)
     node_value = None
     if deferred and params.mode == 0:

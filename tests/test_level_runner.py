@@ -45,7 +45,7 @@ def test_gpu_native_levels_equal_python_levels(inflight, monkeypatch):
     assert _forest("cpu") == ref
 
 
-def _booster(device, n=5000, F=300, trees=8, depth=6, seed=11):
+def _booster(device, n=5000, F=300, trees=8, depth=6, seed=11, rows=None):
     from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
     from fraud_detection_spark_kafka_llm_amd.models.gbdt import GBDTParams, fit_gbdt
 
@@ -55,6 +55,8 @@ def _booster(device, n=5000, F=300, trees=8, depth=6, seed=11):
     y = ((vals[:, 0] >= 2) ^ (vals[:, 3] >= 3)).astype(np.float32)
     flip = rng.random(n) < 0.05
     y[flip] = 1 - y[flip]
+    if rows is not None:                                     # (this rank's shard)
+        vals, y = vals[rows[0]:rows[1]], y[rows[0]:rows[1]]
     vc = VectorColumn(F, dense=torch.from_numpy(vals.astype(np.float64)))
     r = fit_gbdt(vc, torch.from_numpy(y), GBDTParams(n_estimators=trees, max_depth=depth, learning_rate=0.3),
                  device=device)
@@ -85,6 +87,41 @@ def test_gpu_gbdt_native_round_equals_python_levels(monkeypatch):
         ref_d = _booster("cuda:0", depth=depth)
         monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
         assert _booster("cuda:0", depth=depth) == ref_d, depth
+
+
+def _dp_booster(rank, world, device, cxx):
+    """One rank's booster under data parallelism, with its collective calls counted."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    grower.GBDT_CXX_LEVELS = cxx
+    lo, hi = D.shard_range(5000, rank, world)
+    D.reset_bytes()
+    trees = _booster(device, rows=(lo, hi))
+    return trees, dict(D.CALLS), grower.LEVEL_STATS["coll_calls"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,backend", [(1, "nccl"), (2, "gloo")])
+def test_gpu_gbdt_dp_runner_levels_equal_single_process(world, backend, monkeypatch):
+    """the data-parallel GBDT level loop in the runner (RfLevels.gbdt_dp_levels:
+    the level's reduce-scatter / all-gather / the quantisation max as callbacks, the sibling
+    subtraction inside the shard's split search) grows the single-process trees bit for bit -- at
+    world 1 through RCCL and at world 2 (two ranks on this GPU over gloo: 2 feature shards) -- as
+    does the Python-issued DP level loop; 13 collectives per tree."""
+    from fraud_detection_spark_kafka_llm_amd.parallel.launch import spawn
+
+    ref = _booster("cuda:0")
+    monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
+    trees = 8
+    for cxx in (True, False):
+        outs = spawn(_dp_booster, world, "cuda:0", cxx, backend=backend)
+        for got, calls, level_calls in outs:
+            assert got == ref, (cxx, world)
+            assert level_calls > 0
+            # (+ fit_gbdt's base score and the quantisation's max / key gathers)
+            assert calls["reduce_scatter"] + calls["all_gather"] <= 12 * trees + 4, calls
+            assert calls["all_reduce"] <= trees + 3, calls
 
 
 @pytest.mark.gpu
