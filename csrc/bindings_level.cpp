@@ -25,6 +25,8 @@
 
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 
 #include "ops.h"
 #include "tree.h"
@@ -72,6 +74,34 @@ void wait_event(hipEvent_t ev) {
 
 template <class T>
 T* p(const optional<Tensor>& t) { return (t && t->defined()) ? t->data_ptr<T>() : nullptr; }
+
+// RCCL called from the runner on the level's stream. The communicator is the process group's own
+// (ProcessGroupNCCL._comm_ptr) and the entry points come from the librccl.so instance torch already
+// loaded (dlopen RTLD_NOLOAD), so no second RCCL and no second communicator is created; every
+// rank issues its collectives from one host thread in the same order as the Python path did.
+struct Rccl {
+  using RsFn = ncclResult_t (*)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  using AgFn = ncclResult_t (*)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+  using ErrFn = const char* (*)(ncclResult_t);
+  RsFn rs = nullptr, ar = nullptr;
+  AgFn ag = nullptr;
+  ErrFn err = nullptr;
+  ncclComm_t comm = nullptr;
+
+  bool load(const std::string& lib, int64_t comm_ptr) {
+    void* h = dlopen(lib.c_str(), RTLD_NOW | RTLD_NOLOAD);
+    if (h == nullptr || comm_ptr == 0) return false;
+    rs = reinterpret_cast<RsFn>(dlsym(h, "ncclReduceScatter"));
+    ar = reinterpret_cast<RsFn>(dlsym(h, "ncclAllReduce"));
+    ag = reinterpret_cast<AgFn>(dlsym(h, "ncclAllGather"));
+    err = reinterpret_cast<ErrFn>(dlsym(h, "ncclGetErrorString"));
+    comm = reinterpret_cast<ncclComm_t>(comm_ptr);
+    return rs && ar && ag && err;
+  }
+  void check(ncclResult_t r, const char* what) const {
+    FDX_CHECK(r == ncclSuccess, what, ": ", err ? err(r) : "rccl error");
+  }
+};
 
 struct ItemGroup {
   Tensor start, end, f0, meta, wave;
@@ -189,7 +219,7 @@ class RfLevels {
       max_parts = mv + kSet * parity_;
       // data parallel: the max |g|, |h| slots all-reduced (MAX of the bit patterns of non-negative
       // doubles) before the quantisation reads them, so every rank quantises with one exponent
-      if (dp_) dp_max_cb_(maxv_.narrow(0, kSet * parity_, kSet));
+      if (dp_) dp_all_reduce_max(maxv_.narrow(0, kSet * parity_, kSet), s);
       maxv = nullptr;
       parity_ ^= 1;
     }
@@ -233,6 +263,10 @@ class RfLevels {
 
   ~RfLevels() {
     if (g_ev_) (void)hipEventDestroy(g_ev_);
+    for (auto& e : dp_timing_) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
   }
   RfLevels(const RfLevels&) = delete;
   RfLevels& operator=(const RfLevels&) = delete;
@@ -422,6 +456,8 @@ class RfLevels {
     dp_par_row_ = get(c, "par_row");
     dp_sib_row_ = get(c, "sib_row");
     dp_iota_ = get(c, "iota");
+    dp_direct_ = c.contains("comm") && !c["comm"].is_none() &&
+                 rccl_.load(c["rccl_lib"].cast<std::string>(), c["comm"].cast<int64_t>());
     const int64_t widest = int64_t{1} << std::max<int64_t>(max_depth_ - 1, 1);
     FDX_CHECK(dp_S_ >= 1 && dp_Bs_ >= 1 && dp_bin_lo_.numel() == dp_S_ + 1 && dp_bin_lo_.scalar_type() == at::kLong,
               "gbdt_dp_setup: S, Bs, bin_lo [S + 1]");
@@ -438,7 +474,28 @@ class RfLevels {
                   dp_ag_in_.size(0) >= widest && dp_iota_.numel() >= fdx::kRgMaxSlots &&
                   dp_boff_.numel() == dp_nbins_.numel() + 1,
               "gbdt_dp_setup: ag_in [widest, 5], iota, shard tables");
+    if (dp_direct_) dp_allt_buf_ = at::empty({dp_S_ * widest * 5}, dp_ag_in_.options());
   }
+
+  // The direct-RCCL collectives issued so far (reduce-scatter, all-gather, all-reduce) and the
+  // milliseconds of the timed ones (every 8th, scaled; events resolved here: call after a sync
+  // point, e.g. once per fit); the counters restart.
+  std::vector<double> dp_coll_stats() {
+    double ms = 0.0;
+    for (auto& e : dp_timing_) {
+      float t = 0.f;
+      if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&t, e.first, e.second) == hipSuccess)
+        ms += 8.0 * t;
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    dp_timing_.clear();
+    std::vector<double> out{(double)dp_calls_[0], (double)dp_calls_[1], (double)dp_calls_[2], ms};
+    dp_calls_[0] = dp_calls_[1] = dp_calls_[2] = 0;
+    return out;
+  }
+
+  bool dp_direct() const { return dp_direct_; }
 
   // Prologue (with its max all-reduce) done by the caller; level 0 of a DP tree.
   void gbdt_dp_root(int64_t tree) {
@@ -1009,49 +1066,26 @@ class RfLevels {
       a.part = p<int64_t>(*g_part_);
       a.wg_first = p<int32_t>(d == 0 ? *g_wg_first_ : *g_wg_first_list_);
     }
-    fdx::launch_rg_hist(a, s);
-    fdx::DpRootArgs ra{};
-    if (d == 0) {                 // the local root sums into the totals row of every shard chunk
+    if (d == 0) {                 // (+ the local root sums into the totals row of every shard chunk)
       FDX_CHECK(root_pending_ != nullptr, "dp root level without its prologue");
-      ra.root_parts = root_pending_;
-      ra.send = p<int64_t>(send);
-      ra.S = (int32_t)S;
-      ra.chunk_words = chunk * 2;
-      ra.tot_word = (R - 1) * Bs * 2;
-      ra.reduced = p<int64_t>(out) + (R - 1) * Bs * 2;
-      ra.stats = p<int64_t>(st_["stats"]);
-      ra.totals = p<int64_t>(g_totals_[0]);
-      fdx::launch_dp_root(ra, 0, s);
+      a.root_parts = root_pending_;
       root_pending_ = nullptr;
     }
+    fdx::launch_rg_hist(a, s);
     C10_HIP_KERNEL_LAUNCH_CHECK();
-    dp_rs_cb_(send, out.narrow(0, 0, R));
-    if (d == 0) {
-      fdx::launch_dp_root(ra, 1, s);
-    } else {
-      // the built rows stay where the collective wrote them, the larger siblings go behind them
-      fdx::LevelRowsArgs lr{};
-      lr.s2n = p<int32_t>(st_["s2n"]);
-      lr.sub_dst = p<int32_t>(st_["sub_dst"]);
-      lr.sub_par = p<int32_t>(st_["sub_par"]);
-      lr.prev_row_of = d > 1 ? p<int32_t>(dp_row_of_[nxt]) : nullptr;
-      lr.nb = n_build;
-      lr.bld_base = 0;
-      lr.sub_base = (int32_t)R;
-      lr.row_of = p<int32_t>(dp_row_of_[cur]);
-      lr.dst_row = p<int32_t>(dp_dst_row_);
-      lr.par_row = p<int32_t>(dp_par_row_);
-      lr.sib_row = p<int32_t>(dp_sib_row_);
-      fdx::launch_level_rows(lr, s);
+    dp_reduce_scatter(send, out.narrow(0, 0, R), s);
+    if (d > 0) {
+      // the built rows stay where the collective wrote them, the larger siblings behind them (rows
+      // written by the previous level's plan: LevelPlanArgs lr_*), subtracted inside the search
       find_prev_ = p<int64_t>(dp_out_[nxt]);
-      find_sub_par_ = lr.par_row;
-      find_sub_sib_ = lr.sib_row;
+      find_sub_par_ = p<int32_t>(dp_par_row_);
+      find_sub_sib_ = p<int32_t>(dp_sib_row_);
     }
-    C10_HIP_KERNEL_LAUNCH_CHECK();
     // split search over this rank's features (+ the fused subtraction), best tuples into ag_in
     Tensor ag_in = dp_ag_in_.narrow(0, 0, n_open);
     const Tensor open = g_open_[cur].narrow(0, 0, n_open);
-    const Tensor totals = g_totals_[cur].narrow(0, 0, n_open);
+    // (the root's totals: the reduced totals row)
+    const Tensor totals = d == 0 ? out.select(0, R - 1).narrow(0, 0, 1) : g_totals_[cur].narrow(0, 0, n_open);
     const bool any = find(out, totals, dp_boff_, dp_nbins_, dp_zbin_, dp_fid_, open, c10::nullopt, tree, ag_in,
                           d > 0 ? optional<Tensor>(dp_row_of_[cur]) : c10::nullopt, dp_wide_, s);
     find_prev_ = nullptr;
@@ -1060,11 +1094,19 @@ class RfLevels {
       fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), n_open,
                              (int32_t)dp_nbins_.numel(), dp_f0_, p<int64_t>(ag_in), s, &last_split_);
     C10_HIP_KERNEL_LAUNCH_CHECK();
-    dp_allt_ = dp_ag_cb_(ag_in).cast<Tensor>();           // [S, n_open, 5]
+    dp_allt_ = dp_all_gather(ag_in, s);                  // [S, n_open, 5]
     FDX_CHECK(dp_allt_.dim() == 3 && dp_allt_.size(0) == S && dp_allt_.size(1) == n_open && dp_allt_.is_contiguous(),
               "all-gathered best splits [S, n_open, 5]");
     const Tensor n_open_ptr = d == 0 ? g_one_ : st_["counts"].select(0, d - 1).narrow(0, 1, 1);
     fdx::LevelPlanArgs pa = plan_args(d, n_open, dp_allt_, open, n_open_ptr, g_open_[nxt], g_totals_[nxt]);
+    if (d == 0) pa.root_tot = p<int64_t>(totals);
+    if (more) {                   // the next level's histogram rows
+      pa.lr_prev = d > 0 ? p<int32_t>(dp_row_of_[cur]) : nullptr;
+      pa.lr_row_of = p<int32_t>(dp_row_of_[nxt]);
+      pa.lr_dst = p<int32_t>(dp_dst_row_);
+      pa.lr_par = p<int32_t>(dp_par_row_);
+      pa.lr_sib = p<int32_t>(dp_sib_row_);
+    }
     const bool zc = counts_zero_copy(pa, d, false, {});
     fdx::launch_level_plan(pa, s);
     after_plan(d, n_open, g_open_[nxt], tree, false, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt,
@@ -1075,6 +1117,49 @@ class RfLevels {
     if (more) zero = dp_send_.narrow(0, 0, S * n_open * Bs * 2);
     g_counted_ = more && g_counted_ok_;
     partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
+  }
+
+  // timing events around every 8th direct collective (dp_coll_stats)
+  struct CollTimer {
+    RfLevels* r;
+    hipStream_t s;
+    hipEvent_t b = nullptr;
+    CollTimer(RfLevels* r_, hipStream_t s_, int kind) : r(r_), s(s_) {
+      ++r->dp_calls_[kind];
+      if ((r->dp_timed_++ & 7) == 0 && hipEventCreate(&b) == hipSuccess) (void)hipEventRecord(b, s);
+    }
+    ~CollTimer() {
+      hipEvent_t e = nullptr;
+      if (b && hipEventCreate(&e) == hipSuccess && hipEventRecord(e, s) == hipSuccess) r->dp_timing_.emplace_back(b, e);
+    }
+  };
+
+  void dp_reduce_scatter(const Tensor& send, const Tensor& out, hipStream_t s) {
+    if (!dp_direct_) {
+      dp_rs_cb_(send, out);
+      return;
+    }
+    CollTimer t(this, s, 0);
+    rccl_.check(rccl_.rs(send.data_ptr(), out.data_ptr(), (size_t)out.numel(), ncclInt64, ncclSum, rccl_.comm, s),
+                "ncclReduceScatter");
+  }
+
+  Tensor dp_all_gather(const Tensor& in, hipStream_t s) {
+    if (!dp_direct_) return dp_ag_cb_(in).cast<Tensor>();
+    CollTimer t(this, s, 1);
+    Tensor out = dp_allt_buf_.narrow(0, 0, dp_S_ * in.numel()).view({dp_S_, in.size(0), in.size(1)});
+    rccl_.check(rccl_.ag(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), ncclInt64, rccl_.comm, s), "ncclAllGather");
+    return out;
+  }
+
+  void dp_all_reduce_max(const Tensor& buf, hipStream_t s) {
+    if (!dp_direct_) {
+      dp_max_cb_(buf);
+      return;
+    }
+    CollTimer t(this, s, 2);
+    rccl_.check(rccl_.ar(buf.data_ptr(), buf.data_ptr(), (size_t)buf.numel(), ncclInt64, ncclMax, rccl_.comm, s),
+                "ncclAllReduce");
   }
 
   std::vector<ItemGroup> groups_;
@@ -1100,6 +1185,11 @@ class RfLevels {
   Tensor dp_bin_lo_, dp_send_, dp_out_[2], dp_row_of_[2], dp_ag_in_, dp_boff_, dp_nbins_, dp_zbin_, dp_fid_,
       dp_dst_row_, dp_par_row_, dp_sib_row_, dp_iota_, dp_allt_;
   optional<Tensor> dp_wide_;
+  bool dp_direct_ = false;
+  Rccl rccl_;
+  Tensor dp_allt_buf_;
+  int64_t dp_calls_[3] = {0, 0, 0}, dp_timed_ = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> dp_timing_;
   bool build_all_ = true;
   int mode_ = 1, max_depth_ = 5, wps_ = 256;
   double min_gain_ = 0.0, lambda_ = 1.0, mcw_ = 1.0;
@@ -1141,6 +1231,8 @@ void register_level_ops(pybind11::module& m) {
       .def("gbdt_dp_setup", &RfLevels::gbdt_dp_setup)
       .def("gbdt_dp_root", &RfLevels::gbdt_dp_root)
       .def("gbdt_dp_levels", &RfLevels::gbdt_dp_levels)
+      .def("dp_coll_stats", &RfLevels::dp_coll_stats)
+      .def("dp_direct", &RfLevels::dp_direct)
       // (no Python objects inside: the GIL is released for the level loop and its host waits, so a
       // concurrent forest thread keeps running)
       .def("gbdt_levels", &RfLevels::gbdt_levels, py::call_guard<py::gil_scoped_release>());

@@ -79,7 +79,6 @@ struct SplitArgs;
 struct PartitionArgs;
 struct LevelPlanArgs;
 struct LevelRowsArgs;
-struct DpRootArgs;
 struct RfSampleArgs;
 void launch_rf_sample(const RfSampleArgs& a, hipStream_t s);
 void rf_sample_cpu(const RfSampleArgs& a);
@@ -107,7 +106,6 @@ void launch_quant(const QuantArgs& a, const double* maxv, void* partials, hipStr
 void launch_slot8(const SlotArgs& a, hipStream_t s);
 void launch_level_plan(const LevelPlanArgs& a, hipStream_t s);
 void launch_level_rows(const LevelRowsArgs& a, hipStream_t s);
-void launch_dp_root(const DpRootArgs& a, int phase, hipStream_t s);
 void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
                            int32_t max_splits, int32_t wps, hipStream_t s);
 struct SelectArgs;

@@ -637,6 +637,13 @@ __global__ __launch_bounds__(kRgThreads) void rg_hist_kernel(RgHistArgs a) {
   __shared__ RgShared<BINS> sh;
   const int w = blockIdx.x;
   if (w >= a.n_wg) return;
+  if (a.root_parts != nullptr && w == 0 && (int)threadIdx.x < a.nshards) {   // (the DP root's totals row)
+    int64_t t0, t1;
+    root_sums(a.root_parts, &t0, &t1);
+    int64_t* dst = a.hist + ((int64_t)threadIdx.x * a.shard_stride + (int64_t)a.nslots * a.hist_stride) * 2;
+    dst[0] = t0;
+    dst[1] = t1;
+  }
   const int g = a.wg_g[w], p = a.wg_p[w], np_g = a.wg_np[w];
   const int64_t T = a.list ? (int64_t)a.slot_start[a.nslots] : a.N;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;

@@ -315,6 +315,10 @@ struct RgHistArgs {
   int64_t ebase;
   const uint32_t* emdig;
   int64_t em_min_rows;
+  // optional (data-parallel root level): workgroup 0 also writes the root's sums (the
+  // quantisation's kRootSlots slots) into bin 0 of row nslots of every shard chunk (the totals
+  // row the reduce-scatter sums across ranks)
+  const int64_t* root_parts;
   // optional: workgroup w stores its whole LDS table to part[w][gbins][2] (plain stores) and
   // rg_reduce_kernel sums the workgroups of each group (work-table entries wg_first[g] ..
   // wg_first[g + 1]) into the level histogram, instead of every workgroup adding its table into
@@ -537,22 +541,6 @@ FDX_HD void level_rows_slot(const LevelRowsArgs& a, int32_t k) {
     a.dst_row[k] = a.par_row[k] = -1;
   }
 }
-
-// Data-parallel GBDT root (bindings_level.cpp gbdt_dp_level). Phase 0, before the root level's
-// reduce-scatter: the local root sums (the quantisation's kRootSlots slots) go to words tot_word,
-// tot_word + 1 of every shard chunk of the send buffer (the reduce-scatter then sums them across
-// ranks: no all-reduce of its own). Phase 1, after it: the reduced sums become the root state
-// (stats[0] and the level-0 totals row).
-struct DpRootArgs {
-  const int64_t* root_parts;
-  int64_t* send;
-  int32_t S;
-  int64_t chunk_words;
-  int64_t tot_word;
-  const int64_t* reduced;
-  int64_t* stats;
-  int64_t* totals;
-};
 
 struct PartitionArgs {
   int32_t* row_node;              // [N]
@@ -814,6 +802,15 @@ struct LevelPlanArgs {
   int32_t counts_tail;            // counts[4 .. 4 + counts_tail) zeroed (the next level's select counts)
   const int64_t* root_parts;      // optional (depth 0): the root's totals as QuantArgs root_parts
                                   //   slots, summed here into stats[0]
+  const int64_t* root_tot;        // optional (depth 0, data parallel): the root's reduced sums [2]
+  // optional (data-parallel levels, device plan only): level d + 1's histogram rows as
+  // level_rows_kernel writes them (LevelRowsArgs with bld_base 0, sub_base = level d + 1's builds,
+  // prev_row_of = lr_prev: this level's rows, nullptr at depth 0), so they need no launch
+  const int32_t* lr_prev;
+  int32_t* lr_row_of;
+  int32_t* lr_dst;
+  int32_t* lr_par;
+  int32_t* lr_sib;
   // level d + 1 (out; capacity 2L open, L built)
   int32_t* next_open;             // [2L] (-1 pad)
   int64_t* next_totals;           // [2L][2]

@@ -1459,6 +1459,10 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
       R1 += __shfl_xor(R1, o, 64);
     }
     if (lane == 0) { a.stats[0] = R0; a.stats[1] = R1; }
+  } else if (a.root_tot) {
+    R0 = a.root_tot[0];
+    R1 = a.root_tot[1];
+    if (lane == 0) { a.stats[0] = R0; a.stats[1] = R1; }
   }
   for (int32_t base = 0; base < no; base += 64) {
     const int32_t i = base + lane;
@@ -1491,7 +1495,7 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
     bool dense = false;
     if (split) {
       const int64_t l0 = p[3], l1 = p[4];
-      const bool root = a.root_parts && n == 0;
+      const bool root = (a.root_parts || a.root_tot) && n == 0;
       const int64_t t0 = root ? R0 : a.stats[2 * n], t1 = root ? R1 : a.stats[2 * n + 1];
       const int64_t cs[2][2] = {{l0, l1}, {t0 - l0, t1 - l1}};
       for (int k = 0; k < 2; ++k) {
@@ -1608,28 +1612,28 @@ __device__ void level_plan_wave(const LevelPlanArgs& a) {
       a.counts_host[3] = nn;
     }
   }
+  if (a.lr_row_of) {             // (the build tables written above by other lanes of this wave)
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    LevelRowsArgs r{};
+    r.s2n = a.s2n;
+    r.sub_dst = a.sub_dst;
+    r.sub_par = a.sub_par;
+    r.prev_row_of = a.lr_prev;
+    r.nb = nb;
+    r.bld_base = 0;
+    r.sub_base = nb;
+    r.row_of = a.lr_row_of;
+    r.dst_row = a.lr_dst;
+    r.par_row = a.lr_par;
+    r.sib_row = a.lr_sib;
+    for (int32_t k = lane; k < nb; k += 64) level_rows_slot(r, k);
+  }
 }
 
 __global__ __launch_bounds__(64) void level_rows_kernel(LevelRowsArgs a) {
   const int32_t k = (int32_t)(blockIdx.x * 64 + threadIdx.x);
   if (k < a.nb) level_rows_slot(a, k);
-}
-
-__global__ __launch_bounds__(64) void dp_root_kernel(DpRootArgs a, int phase) {
-  if (phase == 0) {
-    int64_t t0, t1;
-    root_sums(a.root_parts, &t0, &t1);
-    for (int32_t s = (int32_t)threadIdx.x; s < a.S; s += 64) {
-      a.send[s * a.chunk_words + a.tot_word] = t0;
-      a.send[s * a.chunk_words + a.tot_word + 1] = t1;
-    }
-  } else if (threadIdx.x == 0) {
-    const int64_t t0 = a.reduced[0], t1 = a.reduced[1];
-    a.stats[0] = t0;
-    a.stats[1] = t1;
-    a.totals[0] = t0;
-    a.totals[1] = t1;
-  }
 }
 
 __global__ void level_plan_kernel(LevelPlanArgs a) {
@@ -1924,10 +1928,6 @@ void launch_partition(const PartitionArgs& a, hipStream_t s) {
 void launch_level_rows(const LevelRowsArgs& a, hipStream_t s) {
   if (a.nb <= 0) return;
   hipLaunchKernelGGL(level_rows_kernel, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, s, a);
-}
-
-void launch_dp_root(const DpRootArgs& a, int phase, hipStream_t s) {
-  hipLaunchKernelGGL(dp_root_kernel, dim3(1), dim3(64), 0, s, a, phase);
 }
 
 void launch_level_plan(const LevelPlanArgs& a, hipStream_t s) {

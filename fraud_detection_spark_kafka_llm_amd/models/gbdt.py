@@ -156,6 +156,9 @@ def fit_gbdt(features, labels, params: GBDTParams = GBDTParams(), device=None, w
         trees.append(pending.result().compacted())
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+        from .grower import dp_runner_stats
+
+        dp_runner_stats()             # (the runner's own RCCL calls into parallel.dist.CALLS)
     return GBDTResult(trees, F, base, params, history, time.perf_counter() - t0,
                       {"Fa": Q.Fa, "TB": Q.TB, "nnz": int(Q.csc_row.numel()),
                        "hot": int(Q.hot.size) if Q.hot is not None else 0,

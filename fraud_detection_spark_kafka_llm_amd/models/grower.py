@@ -70,12 +70,19 @@ _COLL_EVENTS: list = []
 
 
 def reset_level_stats() -> None:
+    for r in _DP_RUNNERS:                   # (their counters restart too)
+        r.dp_coll_stats()
     _COLL_EVENTS.clear()
     for k in LEVEL_STATS:
         LEVEL_STATS[k] = 0
 
 
 def level_collective_ms() -> float:
+    dp_runner_stats()
+    return _level_collective_ms()
+
+
+def _level_collective_ms() -> float:
     """Milliseconds the level loops' streams spent in their reduce-scatter + all-gather (device
     event pairs around every LEVEL_TIMING-th collective, scaled by LEVEL_TIMING; as the issuing
     stream sees them: a lane whose collective queues behind another lane's on the
@@ -1293,6 +1300,43 @@ class _DpCollectives:
             t.copy_(r)
 
 
+# data-parallel GBDT runners that issue RCCL themselves (their collective counts / timings are
+# pulled into parallel.dist.CALLS and LEVEL_STATS by dp_runner_stats)
+_DP_RUNNERS: list = []
+# the DP runner calls RCCL directly on the process group's communicator (0: through Python)
+DP_DIRECT_RCCL = os.environ.get("FDX_DP_DIRECT_RCCL", "1") == "1"
+
+
+def _rccl_comm(dev: torch.device) -> tuple:
+    """(ncclComm_t as int, path of torch's librccl.so) of the default process group on ``dev``, or
+    (None, None) when the backend is not RCCL (gloo) or the communicator is not reachable."""
+    import torch.distributed as dist
+
+    try:
+        if not DP_DIRECT_RCCL or dev.type != "cuda" or dist.get_backend() != "nccl":
+            return None, None
+        pg = dist.distributed_c10d._get_default_group()
+        ptr = int(pg._get_backend(dev)._comm_ptr())
+    except Exception:                                       # noqa: BLE001 (the callbacks then)
+        return None, None
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return (ptr, lib) if ptr and os.path.exists(lib) else (None, None)
+
+
+def dp_runner_stats() -> None:
+    """Adds the direct-RCCL runners' collective calls and timed milliseconds to
+    parallel.dist.CALLS and LEVEL_STATS (resolves their timing events: a sync point)."""
+    from ..parallel import dist as D
+
+    for r in _DP_RUNNERS:
+        rs, ag, ar, ms = r.dp_coll_stats()
+        D.CALLS["reduce_scatter"] += int(rs)
+        D.CALLS["all_gather"] += int(ag)
+        D.CALLS["all_reduce"] += int(ar)
+        LEVEL_STATS["coll_calls"] += int(rs + ag)
+        LEVEL_STATS["coll_ms"] += ms
+
+
 def _gbdt_dp_setup(Q, ws, st, params, runner, rg, shards, coll) -> torch.Tensor:
     """Hands the runner its data-parallel GBDT level loop (RfLevels.gbdt_dp_setup): the row-group
     tables, the shard-major send buffer, the two reduced-level buffers, the feature shard's split
@@ -1307,7 +1351,9 @@ def _gbdt_dp_setup(Q, ws, st, params, runner, rg, shards, coll) -> torch.Tensor:
     outs = [torch.empty((widest, Bs, 2), dtype=torch.int64, device=dev) for _ in range(2)]
     em = rg.erow is not None and qmod.RG_EM_MIN_FRAC <= 1.0
     cb = _DpCollectives(coll, dev)
+    comm, lib = _rccl_comm(dev)
     runner.gbdt_dp_setup(dict(
+        comm=comm, rccl_lib=lib,
         rg_wg_list=rg.list_work(), rg_wg_first_list=rg.list_work_first() if RG_PARTIALS else None,
         rg_ptr=rg.ptr, rg_ent=rg.ent, rg_gbase=rg.gbase, rg_gbin=rg.gbin, rg_gmode=rg.gmode, rg_wg=rg.work(),
         rg_erow=rg.erow, rg_ebase=int(rg.ebase) if rg.erow is not None else 0,
@@ -1324,6 +1370,8 @@ def _gbdt_dp_setup(Q, ws, st, params, runner, rg, shards, coll) -> torch.Tensor:
         par_row=st.par_row, sib_row=st.sib_row, iota=ws.iota(64)))
     root = send[:S * 2 * Bs * 2]
     ws._gbdt_dp = (runner, root)
+    if runner.dp_direct():
+        _DP_RUNNERS.append(runner)
     return root
 
 

@@ -89,12 +89,13 @@ def test_gpu_gbdt_native_round_equals_python_levels(monkeypatch):
         assert _booster("cuda:0", depth=depth) == ref_d, depth
 
 
-def _dp_booster(rank, world, device, cxx):
+def _dp_booster(rank, world, device, cxx, direct=True):
     """One rank's booster under data parallelism, with its collective calls counted."""
     from fraud_detection_spark_kafka_llm_amd.models import grower
     from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
 
     grower.GBDT_CXX_LEVELS = cxx
+    grower.DP_DIRECT_RCCL = direct
     lo, hi = D.shard_range(5000, rank, world)
     D.reset_bytes()
     trees = _booster(device, rows=(lo, hi))
@@ -114,10 +115,12 @@ def test_gpu_gbdt_dp_runner_levels_equal_single_process(world, backend, monkeypa
     ref = _booster("cuda:0")
     monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
     trees = 8
-    for cxx in (True, False):
-        outs = spawn(_dp_booster, world, "cuda:0", cxx, backend=backend)
+    # (the runner calls RCCL itself on the process group's communicator; direct=False: through
+    # the Python callbacks, as on gloo)
+    for cxx, direct in ((True, True), (True, False), (False, True)):
+        outs = spawn(_dp_booster, world, "cuda:0", cxx, direct, backend=backend)
         for got, calls, level_calls in outs:
-            assert got == ref, (cxx, world)
+            assert got == ref, (cxx, direct, world)
             assert level_calls > 0
             # (+ fit_gbdt's base score and the quantisation's max / key gathers)
             assert calls["reduce_scatter"] + calls["all_gather"] <= 12 * trees + 4, calls
