@@ -51,6 +51,13 @@ optional<Tensor> get_opt(const py::dict& c, const char* k) {
 template <class T>
 T* p(const Tensor& t) { return t.data_ptr<T>(); }
 
+// the split search's per-wave partials for the best-split pass (tree_kernels.hip best_partials)
+fdx::BestPartials best_partials(const fdx::SplitArgs& sa) {
+  fdx::BestPartials bp{};
+  if (sa.part_gain) bp = fdx::BestPartials{sa.part_gain, sa.part_f, sa.wide, sa.wide ? sa.n_wide : 0};
+  return bp;
+}
+
 // Host wait for a level's event, called with the GIL released: spins on hipEventQuery while the
 // wait is short (a level's counts usually arrive within 3-40 us), then yields, then sleeps; raises
 // after FDX_LEVEL_TIMEOUT_S (default 600 s) so a hung device never spins forever.
@@ -108,8 +115,38 @@ struct ItemGroup {
   int bt = 1;
 };
 
+// What one lane (tree in flight) of an RfBatch queued during a stage: the launches its per-tree
+// calls would have made, kept as argument structs (tree.h "lane-batched launches") and issued by
+// RfBatch::flush as ONE launch per position for all the batch's lanes.
+enum RecKind : int { kRecQuant, kRecHist, kRecSplit, kRecSplitBest, kRecSplitBestPlan, kRecLevelPlan, kRecRfSample,
+                     kRecRfCompact, kRecSelectGroups, kRecPartition, kRecCopy, kRecRootSend };
+struct RecCopy {
+  void* dst;
+  const void* src;
+  size_t bytes;
+  bool to_host;                  // dst is pinned host memory (written through its device mapping)
+};
+struct RecEntry {
+  int kind;
+  int aux;                       // (kRecHist: the group's bt)
+  std::vector<uint8_t> bytes;
+};
+struct LaneRec {
+  std::vector<RecEntry> entries;
+  template <class T>
+  void add(int kind, const T& v, int aux = 0) {
+    RecEntry e{kind, aux, std::vector<uint8_t>(sizeof(T))};
+    std::memcpy(e.bytes.data(), &v, sizeof(T));
+    entries.push_back(std::move(e));
+  }
+};
+
 class RfLevels {
  public:
+  LaneRec* rec_ = nullptr;       // set by RfBatch while it drives this lane: launches are recorded
+  const int64_t* plan_root_tot_ = nullptr;   // (RfBatch, DP root level) LevelPlanArgs root_tot
+  friend class RfBatch;
+
   explicit RfLevels(const py::dict& c) {
     for (auto g : c["groups"].cast<py::list>()) {
       auto t = g.cast<py::tuple>();
@@ -256,6 +293,11 @@ class RfLevels {
     if (zero && !margin) {
       a.zero = p<int64_t>(*zero);
       a.zero_n = zero->numel();
+    }
+    if (rec_) {
+      FDX_CHECK(a.atomic_root && maxv == nullptr, "a batched prologue: counts (np 1), atomic root");
+      rec_->add(kRecQuant, fdx::QuantLane{a, maxv, reinterpret_cast<unsigned long long*>(p<int64_t>(parts_))});
+      return;
     }
     fdx::launch_quant(a, maxv, p<int64_t>(parts_), s);
     C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -593,6 +635,11 @@ class RfLevels {
         a.listed_per_xcd = (int32_t)npx[j];
       }
       a.lds = (lds_ && 4 * 16 * g.bt * n_build * 8 <= 65536) ? 1 : 0;
+      if (rec_) {
+        FDX_CHECK(a.lds, "batched histogram passes: the LDS-atomic kernel");
+        rec_->add(kRecHist, a, g.bt);
+        continue;
+      }
       fdx::launch_hist(a, g.bt, ct, 1, s);
     }
     C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -607,6 +654,11 @@ class RfLevels {
     const hipStream_t s = cur_stream(dev_);
     const int32_t nodes = (int32_t)node_ids.numel(), Fa = (int32_t)nbins.numel();
     if (!find(hist, totals, boff, nbins, zbin, fid_orig, node_ids, feat_thr, tree, out, row_of, wide, s)) return;
+    if (rec_) {
+      rec_->add(kRecSplitBest, fdx::SplitBestLane{p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), nodes, Fa, f0,
+                                                  p<int64_t>(out), best_partials(last_split_)});
+      return;
+    }
     fdx::launch_split_best(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), nodes, Fa, f0, p<int64_t>(out), s,
                            &last_split_);
     C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -683,7 +735,8 @@ class RfLevels {
       a.part_gain = p<double>(part_gain_);
       a.part_f = p<int32_t>(part_f_);
     }
-    fdx::launch_split(a, s);
+    if (rec_) rec_->add(kRecSplit, a);
+    else fdx::launch_split(a, s);
     last_split_ = a;
     return true;
   }
@@ -734,6 +787,7 @@ class RfLevels {
     a.sub_par = p<int32_t>(st_["sub_par"]);
     a.sub_sib = p<int32_t>(st_["sub_sib"]);
     a.sub_of = p<int32_t>(sub_of_);
+    a.root_tot = plan_root_tot_;
     return a;
   }
 
@@ -749,7 +803,8 @@ class RfLevels {
     const hipStream_t s = cur_stream(dev_);
     fdx::LevelPlanArgs a = plan_args(d, n_open, packed, open, n_open_ptr, next_open, next_totals);
     const bool zc = counts_zero_copy(a, d, sample_next, sel_lists);
-    fdx::launch_level_plan(a, s);
+    if (rec_) rec_->add(kRecLevelPlan, a);
+    else fdx::launch_level_plan(a, s);
     after_plan(d, n_open, next_open, tree, sample_next, thr, mask, fs, nbins_all, local, sizes, sizes_host,
                max_shard_features, sel_lists, s, zc);
   }
@@ -795,7 +850,15 @@ class RfLevels {
     fdx::LevelPlanArgs a = plan_args(d, n_open, out, open, n_open_ptr, next_open, next_totals);
     a.root_parts = root;
     const bool zc = counts_zero_copy(a, d, sample_next, sel_lists);
-    if (any)
+    if (rec_ && any)
+      rec_->add(kRecSplitBestPlan,
+                fdx::SplitBestPlanLane{fdx::SplitBestLane{p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_),
+                                                          (int32_t)n_open, Fa, 0, p<int64_t>(out),
+                                                          best_partials(last_split_)},
+                                       a, reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 2});
+    else if (rec_)
+      rec_->add(kRecLevelPlan, a);
+    else if (any)
       fdx::launch_split_best_plan(p<double>(gain_), p<int32_t>(sbin_), p<int64_t>(sleft_), (int32_t)n_open, Fa, 0,
                                   p<int64_t>(out), a, reinterpret_cast<unsigned int*>(p<int32_t>(ticket_)) + 2, s,
                                   &last_split_);
@@ -803,6 +866,57 @@ class RfLevels {
       fdx::launch_level_plan(a, s);
     after_plan(d, n_open, next_open, tree, sample_next, thr, mask, c10::nullopt, c10::nullopt, c10::nullopt,
                c10::nullopt, c10::nullopt, 0, sel_lists, s, zc);
+  }
+
+  // The k-of-F feature sample of the (-1 padded) nodes [nnodes] into thr / mask, then the compact
+  // DP layout (local / sizes, sizes copied to sizes_host) when given.
+  void sample_level(const Tensor& nodes, int64_t nnodes, int64_t tree, const optional<Tensor>& thr,
+                    const optional<Tensor>& mask, const optional<Tensor>& fs, const optional<Tensor>& nbins_all,
+                    const optional<Tensor>& local, const optional<Tensor>& sizes, const optional<Tensor>& sizes_host,
+                    int64_t max_shard_features, hipStream_t s) {
+    FDX_CHECK(thr && mask, "a next-level sample needs thr and mask");
+    fdx::RfSampleArgs r{};
+    r.seed = (uint64_t)seed_;
+    r.tree = (int32_t)tree;
+    r.nodes = p<int32_t>(nodes);
+    r.nnodes = (int32_t)nnodes;
+    r.F = F_;
+    r.k = k_;
+    r.fid_orig = p<int64_t>(fid_orig_);
+    r.Fa = fid_orig_.numel();
+    r.thr = p<double>(*thr);
+    r.mask = p<uint8_t>(*mask);
+    FDX_CHECK(nodes.numel() >= nnodes && thr->numel() >= nnodes && mask->numel() == r.Fa &&
+                  scratch_.numel() >= fdx::rf_scratch_bytes(r.nnodes), "next-level sample sizes");
+    r.scratch = p<uint8_t>(scratch_);
+    r.fused_counts = reinterpret_cast<uint32_t*>(p<int32_t>(sample_counts_));
+    r.fused_cap = (int32_t)(sample_counts_.numel() / 3);
+    if (rec_) rec_->add(kRecRfSample, r);
+    else fdx::launch_rf_sample(r, s);
+    if (local) {
+      fdx::RfCompactArgs cp{};
+      cp.mask = p<uint8_t>(*mask);
+      cp.nbins = p<int32_t>(*nbins_all);
+      cp.fs = p<int64_t>(*fs);
+      cp.S = (int32_t)(fs->numel() - 1);
+      cp.Fa = mask->numel();
+      cp.local = p<int64_t>(*local);
+      cp.sizes = p<int64_t>(*sizes);
+      if (max_shard_features > 0) {
+        cp.chunk_stride = fdx::rf_compact_chunks(max_shard_features);
+        if (!chunk_sums_.defined() || chunk_sums_.numel() < cp.S * cp.chunk_stride)
+          chunk_sums_ = at::empty({cp.S * cp.chunk_stride}, local->options());
+        cp.chunk_sums = p<int64_t>(chunk_sums_);
+      }
+      if (rec_) {
+        rec_->add(kRecRfCompact, cp);
+        rec_->add(kRecCopy, RecCopy{sizes_host->data_ptr(), sizes->data_ptr(), (size_t)sizes->nbytes(), true});
+      } else {
+        fdx::launch_rf_compact(cp, s);
+        FDX_CHECK(hipMemcpyAsync(sizes_host->data_ptr(), sizes->data_ptr(), sizes->nbytes(), hipMemcpyDeviceToHost,
+                                 s) == hipSuccess, "sizes copy");
+      }
+    }
   }
 
   // For a next level: its feature sample over the (-1 padded) next open list into thr / mask, the
@@ -817,43 +931,8 @@ class RfLevels {
     const int64_t cw = counts.size(1);
     int32_t* counts_d = p<int32_t>(counts) + d * cw;
     if (sample_next) {
-      FDX_CHECK(thr && mask, "a next-level sample needs thr and mask");
-      fdx::RfSampleArgs r{};
-      r.seed = (uint64_t)seed_;
-      r.tree = (int32_t)tree;
-      r.nodes = p<int32_t>(next_open);
-      r.nnodes = (int32_t)(2 * n_open);
-      r.F = F_;
-      r.k = k_;
-      r.fid_orig = p<int64_t>(fid_orig_);
-      r.Fa = fid_orig_.numel();
-      r.thr = p<double>(*thr);
-      r.mask = p<uint8_t>(*mask);
-      FDX_CHECK(next_open.numel() >= 2 * n_open && thr->numel() >= 2 * n_open && mask->numel() == r.Fa &&
-                    scratch_.numel() >= fdx::rf_scratch_bytes(r.nnodes), "next-level sample sizes");
-      r.scratch = p<uint8_t>(scratch_);
-      r.fused_counts = reinterpret_cast<uint32_t*>(p<int32_t>(sample_counts_));
-      r.fused_cap = (int32_t)(sample_counts_.numel() / 3);
-      fdx::launch_rf_sample(r, s);
-      if (local) {
-        fdx::RfCompactArgs cp{};
-        cp.mask = p<uint8_t>(*mask);
-        cp.nbins = p<int32_t>(*nbins_all);
-        cp.fs = p<int64_t>(*fs);
-        cp.S = (int32_t)(fs->numel() - 1);
-        cp.Fa = mask->numel();
-        cp.local = p<int64_t>(*local);
-        cp.sizes = p<int64_t>(*sizes);
-        if (max_shard_features > 0) {
-          cp.chunk_stride = fdx::rf_compact_chunks(max_shard_features);
-          if (!chunk_sums_.defined() || chunk_sums_.numel() < cp.S * cp.chunk_stride)
-            chunk_sums_ = at::empty({cp.S * cp.chunk_stride}, local->options());
-          cp.chunk_sums = p<int64_t>(chunk_sums_);
-        }
-        fdx::launch_rf_compact(cp, s);
-        FDX_CHECK(hipMemcpyAsync(sizes_host->data_ptr(), sizes->data_ptr(), sizes->nbytes(), hipMemcpyDeviceToHost, s) ==
-                      hipSuccess, "sizes copy");
-      }
+      FDX_CHECK(next_open.numel() >= 2 * n_open, "next-level sample: the open list");
+      sample_level(next_open, 2 * n_open, tree, thr, mask, fs, nbins_all, local, sizes, sizes_host, max_shard_features, s);
       if (!sel_lists.empty()) {
         // per-XCD counts of the selected groups (the non-None lists, in group order) at counts[d, 4 + 8 js]
         int64_t n_sel = 0;
@@ -876,7 +955,8 @@ class RfLevels {
           sa.list[k] = p<int32_t>(*sel_lists[j]);
           sa.count[k] = counts_d + 4 + 8 * k;
         }
-        fdx::launch_hist_select_groups(sa, s);
+        if (rec_) rec_->add(kRecSelectGroups, sa);
+        else fdx::launch_hist_select_groups(sa, s);
       }
     }
     if (counts_written) {
@@ -884,6 +964,10 @@ class RfLevels {
       return;
     }
     const Tensor& ch = st_["counts_host"];
+    if (rec_) {
+      rec_->add(kRecCopy, RecCopy{p<int32_t>(ch) + d * cw, counts_d, cw * sizeof(int32_t), true});
+      return;
+    }
     FDX_CHECK(hipMemcpyAsync(p<int32_t>(ch) + d * cw, counts_d, cw * sizeof(int32_t), hipMemcpyDeviceToHost, s) ==
                   hipSuccess, "counts copy");
     C10_HIP_KERNEL_LAUNCH_CHECK();
@@ -935,6 +1019,11 @@ class RfLevels {
       a.count_work = p<int32_t>(*count_work);
       a.count_slot = p<int32_t>(st_["node_slot"]);
       a.count_nslots = p<int32_t>(counts) + d * counts.size(1) + 2;
+    }
+    if (rec_) {
+      rec_->add(kRecPartition, fdx::PartColsLane{a, p<int64_t>(colptr_), p<int32_t>(st_["cs_feat"]),
+                                                 p<int32_t>(counts) + d * counts.size(1), (int32_t)n_open, (int32_t)wps_});
+      return;
     }
     fdx::launch_partition_cols(a, p<int64_t>(colptr_), p<int32_t>(st_["cs_feat"]), p<int32_t>(counts) + d * counts.size(1),
                                (int32_t)n_open, (int32_t)wps_, s);
@@ -1214,6 +1303,543 @@ class RfLevels {
   hipEvent_t g_ev_ = nullptr;
 };
 
+// ---- RandomForest trees in flight as lockstep batches (PAR-05) -------------------------------
+// Spark grows the nodes of many trees per pass over the data (SURVEY PAR-05; reference
+// /root/reference/fraud_detection_spark.py:67-74). Here up to `lanes` trees grow level by level in
+// lockstep: every stage of a level -- histogram passes per item group, split search, best split +
+// plan (+ the next level's feature sample, DP layout and item selects), partition -- is recorded
+// per lane by the lane's own runner (RfLevels with rec_ set: the exact argument structs of its
+// per-tree launches) and issued as ONE lane-batched launch (tree.h "lane-batched launches"), so a
+// forest level costs ~12 launches for all its trees instead of ~18 per tree, and the host does no
+// per-tree interpreter work at all. Under data parallelism a level's histograms of all the lanes
+// go out in ONE reduce-scatter and their best splits in ONE all-gather (RCCL called here on the
+// process group's communicator, or Python callbacks on gloo). Every lane's arguments are the ones
+// its per-tree level loop (grower._rf_runner_levels) passes, so the forest is bitwise the same.
+class RfBatch {
+ public:
+  explicit RfBatch(const py::dict& c) {
+    for (auto item : c["lanes"].cast<py::list>()) {
+      const py::dict d = item.cast<py::dict>();
+      Lane ln;
+      ln.obj = d["runner"];
+      ln.r = ln.obj.cast<RfLevels*>();
+      for (int k = 0; k < 2; ++k) {
+        ln.open[k] = get(d, k ? "open1" : "open0");
+        ln.totals[k] = get(d, k ? "totals1" : "totals0");
+        ln.thr[k] = get(d, k ? "thr1" : "thr0");
+        ln.mask[k] = get(d, k ? "mask1" : "mask0");
+      }
+      ln.arena = get(d, "arena");
+      ln.arena_init = get(d, "arena_init");
+      ln.arena_host[0] = get(d, "arena_host0");
+      ln.arena_host[1] = get(d, "arena_host1");
+      ln.tot_scratch = get(d, "tot_scratch");
+      ln.hist = get_opt(d, "hist");
+      ln.packed = get_opt(d, "packed");
+      ln.rowpack = get(d, "rowpack");
+      for (auto t : d["sel"].cast<py::list>()) ln.sel.push_back(t.is_none() ? optional<Tensor>() : t.cast<Tensor>());
+      for (auto t : d["listed"].cast<py::list>()) {
+        auto pr = t.cast<py::tuple>();
+        ln.listed.push_back(pr[0].is_none() ? optional<Tensor>() : pr[0].cast<Tensor>());
+        ln.listed_cnt.push_back(pr[1].is_none() ? optional<Tensor>() : pr[1].cast<Tensor>());
+      }
+      if (d.contains("sh_local0")) {
+        for (int k = 0; k < 2; ++k) {
+          ln.sh_local[k] = get(d, k ? "sh_local1" : "sh_local0");
+          ln.sh_sizes[k] = get(d, k ? "sh_sizes1" : "sh_sizes0");
+          ln.sh_sizes_host[k] = get(d, k ? "sh_sizes_host1" : "sh_sizes_host0");
+        }
+      }
+      FDX_CHECK(ln.r->groups_.size() == ln.sel.size() && ln.sel.size() == ln.listed.size(), "lane group lists");
+      lanes_.push_back(std::move(ln));
+    }
+    FDX_CHECK(!lanes_.empty(), "RfBatch: at least one lane");
+    D_ = c["max_depth"].cast<int64_t>();
+    boff_ = get(c, "boff");
+    wide_ = get_opt(c, "wide");
+    listed_max_ = c["listed_max_nodes"].cast<int64_t>();
+    presel_ = c["presel"].cast<bool>();
+    one_ = get(c, "one");
+    zero1_ = get(c, "zero1");
+    iota_ = get(c, "iota");
+    dp_ = c["dp"].cast<bool>();
+    if (dp_) {
+      S_ = c["S"].cast<int64_t>();
+      Bs_full_ = c["Bs"].cast<int64_t>();
+      max_nb_ = c["max_nb"].cast<int64_t>();
+      compact_ = c["compact"].cast<bool>();
+      shard_of_ = get(c, "shard_of");
+      sh_local_full_ = get(c, "sh_local");
+      sh_boff_ = get(c, "sh_boff");
+      sh_nbins_ = get(c, "sh_nbins");
+      sh_zbin_ = get(c, "sh_zbin");
+      sh_fid_ = get(c, "sh_fid");
+      sh_fs_ = get(c, "sh_fs");
+      nbins_all_ = get(c, "nbins_all");
+      f0_ = c["f0"].cast<int64_t>();
+      Fa_s_ = c["Fa_s"].cast<int64_t>();
+      max_shard_features_ = c["max_shard_features"].cast<int64_t>();
+      rs_cb_ = c["rs"];
+      ag_cb_ = c["ag"];
+      direct_ = c.contains("comm") && !c["comm"].is_none() &&
+                rccl_.load(c["rccl_lib"].cast<std::string>(), c["comm"].cast<int64_t>());
+    }
+    const auto dev = lanes_[0].r->dev_;
+    host_ = at::empty({kRegions * kRegion}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+    dev_args_ = at::empty({kRegions * kRegion}, at::TensorOptions().dtype(at::kByte).device(dev));
+    i64_ = at::TensorOptions().dtype(at::kLong).device(dev);
+    FDX_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming) == hipSuccess, "event");
+    for (auto& e : half_ev_) FDX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "event");
+    FDX_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming) == hipSuccess, "event");
+  }
+  ~RfBatch() {
+    for (hipEvent_t e : half_ev_)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_, done_})
+      if (e) (void)hipEventDestroy(e);
+    for (auto& ln : lanes_) ln.r->rec_ = nullptr;
+  }
+  RfBatch(const RfBatch&) = delete;
+  RfBatch& operator=(const RfBatch&) = delete;
+
+  // Grows trees[l] on lane l (l < number of trees <= lanes): every launch queued on the current
+  // stream, host waits (GIL released) only for each level's counts. The lanes' node tables are
+  // copied into their arena_host[parity] at the end (wait()); on_wait (if not None) is called once,
+  // before the first host wait (the caller builds the previous batch's trees meanwhile). Returns the level counters: levels,
+  // built nodes, listed passes, listed active items, listed grid waves, reduce-scatters,
+  // all-gathers.
+  std::vector<int64_t> grow(const std::vector<int64_t>& trees, const Tensor& label, const optional<Tensor>& weight,
+                            bool bootstrap, int64_t row0, int64_t parity, const py::object& on_wait) {
+    const int64_t L = (int64_t)trees.size();
+    FDX_CHECK(L >= 1 && L <= (int64_t)lanes_.size(), "RfBatch.grow: 1 .. lanes trees");
+    c10::hip::HIPGuard guard(lanes_[0].r->dev_.index());
+    const hipStream_t s = cur_stream(lanes_[0].r->dev_);
+    std::vector<int64_t> stat(7, 0);
+    live_.clear();
+    for (int64_t l = 0; l < L; ++l) {
+      Lane& ln = lanes_[l];
+      ln.tree = trees[l];
+      ln.n_open = ln.n_build = 1;
+      live_.push_back((int)l);
+    }
+    level_ = 0;
+    begin_region();
+    // tree prologue: the node-table image in, the quantisation (bootstrap counts, digits, row_node
+    // = 0, open[0] = root; single process: the root histogram zeroed), then the root's sample
+    for (int l : live_) {
+      Lane& ln = lanes_[l];
+      // (the node-table image first: one batched copy kernel, recorded like the count rows)
+      ln.rec.add(kRecCopy, RecCopy{ln.arena.data_ptr(), ln.arena_init.data_ptr(), (size_t)ln.arena.nbytes(), false});
+      ln.r->rec_ = &ln.rec;
+      ln.r->prologue(c10::nullopt, c10::nullopt, c10::nullopt, label, weight, ln.tree, bootstrap, 1, c10::nullopt,
+                     ln.tot_scratch, c10::nullopt, row0, dp_ ? optional<Tensor>() : optional<Tensor>(ln.hist->narrow(0, 0, 1)),
+                     c10::nullopt);
+      ln.r->sample_level(ln.open[0], 1, ln.tree, ln.thr[0], ln.mask[0], sh_fs(), nbins_all(), sh_local(ln, 0),
+                         sh_sizes(ln, 0), sh_sizes_host(ln, 0), max_shard_features_, s);
+    }
+    flush(s);
+    if (dp_ && compact_) FDX_CHECK(hipEventRecord(ev_, s) == hipSuccess, "event");
+    for (int64_t d = 0; d < D_; ++d) {
+      const int cur = (int)(d & 1), nxt = cur ^ 1;
+      const bool more = d + 1 < D_;
+      if (d > 0 || (dp_ && compact_)) {
+        if (!on_wait.is_none() && !on_wait_done_) {
+          on_wait_done_ = true;
+          on_wait();
+        }
+        py::gil_scoped_release nogil;
+        wait_event(ev_);
+      }
+      level_ = d;
+      begin_region();
+      if (d > 0) {               // the counts of the previous plan, the lanes whose trees go on
+        std::vector<int> still;
+        for (int l : live_) {
+          Lane& ln = lanes_[l];
+          const Tensor& ch = ln.r->st_["counts_host"];
+          const int32_t* row = p<int32_t>(ch) + (d - 1) * ch.size(1);
+          ln.n_open = row[1];
+          ln.n_build = row[2];
+          if (ln.n_open > 0) still.push_back(l);
+        }
+        live_ = still;
+      }
+      if (live_.empty()) break;
+      for (int l : live_) {
+        Lane& ln = lanes_[l];
+        stat[0] += 1;
+        stat[1] += ln.n_build;
+        ln.npx.assign(ln.r->groups_.size(), -1);
+        if (presel_ && d > 0) {
+          const Tensor& ch = ln.r->st_["counts_host"];
+          const int32_t* row = p<int32_t>(ch) + (d - 1) * ch.size(1);
+          int j = 0;
+          for (size_t gi = 0; gi < ln.r->groups_.size(); ++gi) {
+            if (!ln.sel[gi]) continue;
+            int32_t m = 0, sum = 0;
+            for (int x = 0; x < 8; ++x) {
+              m = std::max(m, row[4 + 8 * j + x]);
+              sum += row[4 + 8 * j + x];
+            }
+            ln.npx[gi] = m;
+            ln.sel_j.resize(ln.r->groups_.size());
+            ln.sel_j[gi] = j;
+            if (m) {
+              stat[2] += 1;
+              stat[3] += sum;
+              stat[4] += (m + 3) / 4 * 8 * 4;
+            }
+            ++j;
+          }
+        }
+      }
+      level(d, cur, nxt, more, s, stat);
+    }
+    // the node tables to the host (one batched copy kernel into the mapped pinned tables)
+    live_.clear();
+    for (int64_t l = 0; l < L; ++l) {
+      Lane& ln = lanes_[l];
+      ln.r->rec_ = nullptr;
+      ln.rec.add(kRecCopy,
+                 RecCopy{ln.arena_host[parity & 1].data_ptr(), ln.arena.data_ptr(), (size_t)ln.arena.nbytes(), true});
+      live_.push_back((int)l);
+    }
+    flush(s);
+    FDX_CHECK(hipEventRecord(done_, s) == hipSuccess, "event");
+    if (!on_wait.is_none() && !on_wait_done_) on_wait();
+    on_wait_done_ = false;
+    stat[5] = rs_calls_;
+    stat[6] = ag_calls_;
+    rs_calls_ = ag_calls_ = 0;
+    return stat;
+  }
+
+  bool direct() const { return direct_; }
+
+  // The last grow's node tables are in the lanes' arena_host (GIL released while waiting).
+  void wait() {
+    py::gil_scoped_release nogil;
+    wait_event(done_);
+  }
+
+ private:
+  // argument staging: a ring of kRegions regions, one per level (and prologue) in turn; a region is
+  // reused kRegions levels later, after its copy (event) completed -- long since, as every level
+  // waits for the previous one's counts
+  static constexpr int kRegions = 4;
+  static constexpr int64_t kRegion = 1 << 19;
+
+  struct Lane {
+    py::object obj;
+    RfLevels* r = nullptr;
+    Tensor open[2], totals[2], thr[2], mask[2], arena, arena_init, arena_host[2], tot_scratch, rowpack;
+    optional<Tensor> hist, packed;
+    std::vector<optional<Tensor>> sel, listed, listed_cnt;
+    Tensor sh_local[2], sh_sizes[2], sh_sizes_host[2];
+    LaneRec rec;
+    int64_t tree = 0;
+    int32_t n_open = 0, n_build = 0;
+    std::vector<int32_t> npx;
+    std::vector<int> sel_j;
+    int64_t row0 = 0, l0 = 0, tb = -1, Bs = 0;
+  };
+
+  optional<Tensor> sh_fs() const { return dp_ && compact_ ? optional<Tensor>(sh_fs_) : c10::nullopt; }
+  optional<Tensor> nbins_all() const { return dp_ && compact_ ? optional<Tensor>(nbins_all_) : c10::nullopt; }
+  optional<Tensor> sh_local(const Lane& ln, int k) const {
+    return dp_ && compact_ ? optional<Tensor>(ln.sh_local[k]) : c10::nullopt;
+  }
+  optional<Tensor> sh_sizes(const Lane& ln, int k) const {
+    return dp_ && compact_ ? optional<Tensor>(ln.sh_sizes[k]) : c10::nullopt;
+  }
+  optional<Tensor> sh_sizes_host(const Lane& ln, int k) const {
+    return dp_ && compact_ ? optional<Tensor>(ln.sh_sizes_host[k]) : c10::nullopt;
+  }
+
+  void begin_region() {
+    half_ = (half_ + 1) % kRegions;
+    off_ = 0;
+    if (half_used_[half_]) (void)hipEventSynchronize(half_ev_[half_]);
+  }
+
+  void level(int64_t d, int cur, int nxt, bool more, hipStream_t s, std::vector<int64_t>& stat) {
+    // ---- histogram passes (DP: into the batch's shard-major send buffer)
+    Tensor send, out;
+    int64_t R = 0, Bs = 0, nrows = 0, nopen = 0;
+    if (dp_) {
+      for (int l : live_) {
+        Lane& ln = lanes_[l];
+        ln.Bs = Bs_full_;
+        if (compact_) {
+          const int64_t* sz = p<int64_t>(ln.sh_sizes_host[cur]);
+          int64_t m = 0;
+          for (int64_t k = 0; k < S_; ++k) m = std::max(m, sz[k]);
+          ln.Bs = m + max_nb_;
+        }
+        Bs = std::max(Bs, ln.Bs);
+        ln.row0 = nrows;
+        ln.l0 = nopen;
+        nrows += ln.n_build;
+        nopen += ln.n_open;
+      }
+      Bs = std::max<int64_t>(Bs, 1);
+      const int64_t ntot = d == 0 ? (int64_t)live_.size() : 0;
+      R = nrows + (ntot + Bs - 1) / Bs;
+      int64_t t = 0;
+      for (int l : live_) lanes_[l].tb = d == 0 ? nrows * Bs + t++ : -1;
+      send = buffer(send_, S_ * R * Bs * 2).view({S_, R, Bs, 2});
+      out = buffer(out_, R * Bs * 2).view({R, Bs, 2});
+      FDX_CHECK(hipMemsetAsync(send.data_ptr(), 0, send.nbytes(), s) == hipSuccess, "send zero");
+    }
+    for (int l : live_) {
+      Lane& ln = lanes_[l];
+      std::vector<optional<Tensor>> lists, cnts;
+      std::vector<int64_t> npxs;
+      for (size_t gi = 0; gi < ln.r->groups_.size(); ++gi) {
+        const bool items = ln.r->groups_[gi].start.numel() > 0;
+        if (items && presel_ && d > 0 && ln.sel[gi]) {
+          lists.push_back(ln.sel[gi]);
+          cnts.push_back(ln.r->st_["counts"].select(0, d - 1).narrow(0, 4 + 8 * ln.sel_j[gi], 8));
+          npxs.push_back(ln.npx[gi]);
+        } else if (items && ln.n_open <= listed_max_) {
+          lists.push_back(ln.listed[gi]);
+          cnts.push_back(ln.listed_cnt[gi]);
+          npxs.push_back(-1);
+        } else {
+          lists.push_back(c10::nullopt);
+          cnts.push_back(c10::nullopt);
+          npxs.push_back(-1);
+        }
+      }
+      const optional<Tensor> pack = d > 0 ? optional<Tensor>(ln.rowpack) : c10::nullopt;
+      const Tensor& mask = ln.mask[cur];
+      if (!dp_) {
+        const Tensor s2n = d == 0 ? zero1_ : ln.r->st_["s2n"].narrow(0, 0, ln.n_build);
+        ln.r->hist(ln.n_build, ln.hist->narrow(0, 0, ln.n_open), boff_, mask, s2n, pack, lists, cnts, npxs,
+                   c10::nullopt, 0);
+      } else {
+        const Tensor tgt = send.view({-1, Bs, 2}).narrow(0, ln.row0, S_ * R - ln.row0);
+        const Tensor& hb = compact_ ? ln.sh_local[cur] : sh_local_full_;
+        ln.r->hist(ln.n_build, tgt, hb, mask, iota_.narrow(0, 0, ln.n_build), pack, lists, cnts, npxs, shard_of_, R * Bs);
+        if (d == 0)
+          ln.rec.add(kRecRootSend, fdx::RootSendLane{ln.r->root_pending_, p<int64_t>(send), (int32_t)S_, R * Bs * 2,
+                                                     ln.tb * 2});
+      }
+    }
+    flush(s);
+    // ---- split search (+ best split + plan in one launch without a collective between them)
+    Tensor allt;
+    if (dp_) {
+      reduce_scatter(send, out, s);
+      Tensor ag_in = buffer(ag_in_, nopen * 5).view({nopen, 5});
+      for (int l : live_) {
+        Lane& ln = lanes_[l];
+        const Tensor open = ln.open[cur].narrow(0, 0, ln.n_open);
+        const Tensor totals = d == 0 ? out.view({-1, 2}).narrow(0, ln.tb, 1) : ln.totals[cur].narrow(0, 0, ln.n_open);
+        const Tensor split_boff = compact_ ? ln.sh_local[cur].narrow(0, f0_, Fa_s_ + 1) : sh_boff_;
+        ln.r->split(out.narrow(0, ln.row0, ln.n_build), totals, split_boff, sh_nbins_, sh_zbin_, sh_fid_, open,
+                    ln.thr[cur].narrow(0, 0, ln.n_open), ln.tree, f0_, ag_in.narrow(0, ln.l0, ln.n_open),
+                    c10::nullopt, wide_);
+      }
+      flush(s);
+      allt = all_gather(ag_in, s);
+    }
+    for (int l : live_) {
+      Lane& ln = lanes_[l];
+      const Tensor open = ln.open[cur].narrow(0, 0, ln.n_open);
+      const Tensor n_open_ptr = d == 0 ? one_ : ln.r->st_["counts"].select(0, d - 1).narrow(0, 1, 1);
+      std::vector<optional<Tensor>> sel;
+      if (presel_ && more) sel = ln.sel;
+      const optional<Tensor> thr_n = more ? optional<Tensor>(ln.thr[nxt]) : c10::nullopt;
+      const optional<Tensor> mask_n = more ? optional<Tensor>(ln.mask[nxt]) : c10::nullopt;
+      if (!dp_) {
+        const Tensor totals = d == 0 ? ln.r->st_["stats"].narrow(0, 0, 1) : ln.totals[cur].narrow(0, 0, ln.n_open);
+        ln.r->split_plan(d, ln.n_open, ln.hist->narrow(0, 0, ln.n_open), totals, boff_,
+                         ln.thr[cur].narrow(0, 0, ln.n_open), ln.tree, ln.packed->narrow(0, 0, ln.n_open), wide_, open,
+                         n_open_ptr, ln.open[nxt], ln.totals[nxt], more, thr_n, mask_n, sel, c10::nullopt);
+      } else {
+        ln.r->root_pending_ = nullptr;
+        if (d == 0) ln.r->plan_root_tot_ = p<int64_t>(out) + ln.tb * 2;
+        ln.r->plan(d, ln.n_open, allt.narrow(1, ln.l0, ln.n_open), open, n_open_ptr, ln.open[nxt], ln.totals[nxt], ln.tree,
+                   more, thr_n, mask_n, more ? sh_fs() : c10::nullopt, more ? nbins_all() : c10::nullopt,
+                   more ? sh_local(ln, nxt) : c10::nullopt, more ? sh_sizes(ln, nxt) : c10::nullopt,
+                   more ? sh_sizes_host(ln, nxt) : c10::nullopt, max_shard_features_, sel);
+        ln.r->plan_root_tot_ = nullptr;
+      }
+    }
+    flush(s);
+    FDX_CHECK(hipEventRecord(ev_, s) == hipSuccess, "level event");
+    // ---- partition (writes the next level's packed row state; single process: zeroes its histograms)
+    for (int l : live_) {
+      Lane& ln = lanes_[l];
+      const optional<Tensor> zero =
+          (!dp_ && more) ? optional<Tensor>(ln.hist->narrow(0, 0, 2 * (int64_t)ln.n_open)) : c10::nullopt;
+      ln.r->partition(d, ln.n_open, more, zero, true, c10::nullopt);
+    }
+    flush(s);
+    (void)stat;
+  }
+
+  // the device's view of a pinned host pointer (memoised per pointer)
+  void* mapped(void* host) {
+    auto it = mapped_.find(host);
+    if (it != mapped_.end()) return it->second;
+    void* d = nullptr;
+    FDX_CHECK(hipHostGetDevicePointer(&d, host, 0) == hipSuccess && d != nullptr, "pinned host rows must be mapped");
+    mapped_[host] = d;
+    return d;
+  }
+
+  Tensor buffer(Tensor& b, int64_t n) {
+    if (!b.defined() || b.numel() < n) b = at::empty({std::max<int64_t>(n, 1)}, i64_);
+    return b.narrow(0, 0, n);
+  }
+
+  void reduce_scatter(const Tensor& send, const Tensor& out, hipStream_t s) {
+    ++rs_calls_;
+    if (!direct_) {
+      rs_cb_(send, out);
+      return;
+    }
+    rccl_.check(rccl_.rs(send.data_ptr(), out.data_ptr(), (size_t)out.numel(), ncclInt64, ncclSum, rccl_.comm, s),
+                "ncclReduceScatter");
+  }
+
+  Tensor all_gather(const Tensor& in, hipStream_t s) {
+    ++ag_calls_;
+    if (!direct_) return ag_cb_(in).cast<Tensor>();
+    Tensor out = buffer(allt_, S_ * in.numel()).view({S_, in.size(0), 5});
+    rccl_.check(rccl_.ag(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), ncclInt64, rccl_.comm, s), "ncclAllGather");
+    return out;
+  }
+
+  // Issues what the live lanes recorded: position i of every lane's record is one lane-batched
+  // launch (the lanes recorded the same sequence). The argument arrays go to the device in one copy.
+  void flush(hipStream_t s) {
+    if (live_.empty()) return;
+    const int L = (int)live_.size();
+    const auto& E0 = lanes_[live_[0]].rec.entries;
+    for (int l : live_) {
+      const auto& E = lanes_[l].rec.entries;
+      FDX_CHECK(E.size() == E0.size(), "lanes recorded different stages");
+      for (size_t i = 0; i < E.size(); ++i)
+        FDX_CHECK(E[i].kind == E0[i].kind && E[i].aux == E0[i].aux && E[i].bytes.size() == E0[i].bytes.size(),
+                  "lanes recorded different launches");
+    }
+    uint8_t* host = p<uint8_t>(host_) + half_ * kRegion;
+    uint8_t* dev = p<uint8_t>(dev_args_) + half_ * kRegion;
+    const int64_t start = off_;
+    std::vector<int64_t> offs(E0.size(), -1), offs2(E0.size(), -1);
+    for (size_t i = 0; i < E0.size(); ++i) {
+      if (E0[i].kind == kRecCopy) {            // D2H rows: one kernel writing the host-mapped rows
+        off_ = (off_ + 15) & ~int64_t{15};
+        FDX_CHECK(off_ + L * (int64_t)sizeof(fdx::CopyLane) <= kRegion, "argument staging overflow");
+        offs[i] = off_;
+        for (int k = 0; k < L; ++k) {
+          RecCopy c;
+          std::memcpy(&c, lanes_[live_[k]].rec.entries[i].bytes.data(), sizeof(c));
+          const fdx::CopyLane cl{c.to_host ? mapped(c.dst) : c.dst, c.src, (int64_t)c.bytes};
+          std::memcpy(host + off_ + k * sizeof(fdx::CopyLane), &cl, sizeof(cl));
+        }
+        off_ += L * (int64_t)sizeof(fdx::CopyLane);
+        continue;
+      }
+      const int64_t sz = (int64_t)E0[i].bytes.size();
+      off_ = (off_ + 15) & ~int64_t{15};
+      FDX_CHECK(off_ + L * sz + L * (int64_t)sizeof(fdx::PartitionArgs) + 16 <= kRegion, "argument staging overflow");
+      offs[i] = off_;
+      for (int k = 0; k < L; ++k) std::memcpy(host + off_ + k * sz, lanes_[live_[k]].rec.entries[i].bytes.data(), sz);
+      off_ += L * sz;
+      if (E0[i].kind == kRecPartition) {       // (the row pass takes the PartitionArgs alone)
+        off_ = (off_ + 15) & ~int64_t{15};
+        offs2[i] = off_;
+        for (int k = 0; k < L; ++k) {
+          fdx::PartColsLane q;
+          std::memcpy(&q, lanes_[live_[k]].rec.entries[i].bytes.data(), sizeof(q));
+          std::memcpy(host + off_ + k * sizeof(fdx::PartitionArgs), &q.a, sizeof(fdx::PartitionArgs));
+        }
+        off_ += L * (int64_t)sizeof(fdx::PartitionArgs);
+      }
+    }
+    if (off_ > start) {
+      FDX_CHECK(hipMemcpyAsync(dev + start, host + start, off_ - start, hipMemcpyHostToDevice, s) == hipSuccess,
+                "argument copy");
+      FDX_CHECK(hipEventRecord(half_ev_[half_], s) == hipSuccess, "event");
+      half_used_[half_] = true;
+    }
+    for (size_t i = 0; i < E0.size(); ++i) {
+      const int64_t o = offs[i];
+      switch (E0[i].kind) {
+        case kRecQuant:
+          fdx::launch_quant_lanes((const fdx::QuantLane*)(host + o), (const fdx::QuantLane*)(dev + o), L, s);
+          break;
+        case kRecHist:
+          fdx::launch_hist_lanes((const fdx::HistArgs*)(host + o), (const fdx::HistArgs*)(dev + o), L, E0[i].aux, s);
+          break;
+        case kRecSplit:
+          fdx::launch_split_lanes((const fdx::SplitArgs*)(host + o), (const fdx::SplitArgs*)(dev + o), L, s);
+          break;
+        case kRecSplitBest:
+          fdx::launch_split_best_lanes((const fdx::SplitBestLane*)(host + o), (const fdx::SplitBestLane*)(dev + o), L, s);
+          break;
+        case kRecSplitBestPlan:
+          fdx::launch_split_best_plan_lanes((const fdx::SplitBestPlanLane*)(host + o),
+                                            (const fdx::SplitBestPlanLane*)(dev + o), L, s);
+          break;
+        case kRecLevelPlan:
+          fdx::launch_level_plan_lanes((const fdx::LevelPlanArgs*)(dev + o), L, s);
+          break;
+        case kRecRfSample:
+          fdx::launch_rf_sample_lanes((const fdx::RfSampleArgs*)(host + o), (const fdx::RfSampleArgs*)(dev + o), L, s);
+          break;
+        case kRecRfCompact:
+          fdx::launch_rf_compact_lanes((const fdx::RfCompactArgs*)(host + o), (const fdx::RfCompactArgs*)(dev + o), L, s);
+          break;
+        case kRecSelectGroups:
+          fdx::launch_select_groups_lanes((const fdx::SelectArgs*)(host + o), (const fdx::SelectArgs*)(dev + o), L, s);
+          break;
+        case kRecPartition:
+          fdx::launch_partition_lanes((const fdx::PartColsLane*)(host + o), (const fdx::PartColsLane*)(dev + o),
+                                      (const fdx::PartitionArgs*)(dev + offs2[i]), L, s);
+          break;
+        case kRecRootSend:
+          fdx::launch_root_send_lanes((const fdx::RootSendLane*)(dev + o), L, s);
+          break;
+        case kRecCopy:
+          fdx::launch_copy_lanes((const fdx::CopyLane*)(host + o), (const fdx::CopyLane*)(dev + o), L, s);
+          break;
+        default:
+          FDX_CHECK(false, "unknown recorded launch");
+      }
+    }
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    for (int l : live_) lanes_[l].rec.entries.clear();
+  }
+
+  std::vector<Lane> lanes_;
+  std::vector<int> live_;
+  int64_t D_ = 5, listed_max_ = 2, level_ = 0;
+  bool presel_ = true, dp_ = false, compact_ = false, direct_ = false;
+  Tensor boff_, one_, zero1_, iota_;
+  optional<Tensor> wide_;
+  // data parallel
+  int64_t S_ = 1, Bs_full_ = 1, max_nb_ = 1, f0_ = 0, Fa_s_ = 0, max_shard_features_ = 0;
+  Tensor shard_of_, sh_local_full_, sh_boff_, sh_nbins_, sh_zbin_, sh_fid_, sh_fs_, nbins_all_;
+  py::object rs_cb_, ag_cb_;
+  Rccl rccl_;
+  Tensor send_, out_, ag_in_, allt_;
+  int64_t rs_calls_ = 0, ag_calls_ = 0;
+  // argument staging (pinned host + device, two halves by level parity)
+  Tensor host_, dev_args_;
+  int half_ = -1;
+  int64_t off_ = 0;
+  bool half_used_[kRegions] = {};
+  bool on_wait_done_ = false;
+  hipEvent_t ev_ = nullptr, half_ev_[kRegions] = {}, done_ = nullptr;
+  at::TensorOptions i64_;
+  std::map<void*, void*> mapped_;
+};
+
 }  // namespace
 
 void register_level_ops(pybind11::module& m) {
@@ -1236,4 +1862,9 @@ void register_level_ops(pybind11::module& m) {
       // (no Python objects inside: the GIL is released for the level loop and its host waits, so a
       // concurrent forest thread keeps running)
       .def("gbdt_levels", &RfLevels::gbdt_levels, py::call_guard<py::gil_scoped_release>());
+  py::class_<RfBatch>(m, "RfBatch")
+      .def(py::init<const py::dict&>())
+      .def("grow", &RfBatch::grow)
+      .def("wait", &RfBatch::wait)
+      .def("direct", &RfBatch::direct);
 }

@@ -2,7 +2,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <stdexcept>
+
 #include "scoring.h"
+
+// host-side argument checks of the launchers (pybind turns the exception into a RuntimeError)
+#define FDX_LANES_CHECK(c)                                                     \
+  do {                                                                         \
+    if (!(c)) throw std::runtime_error("fdx lane-batched launch: " #c);        \
+  } while (0)
 
 namespace fdx {
 
@@ -109,6 +117,26 @@ void launch_level_rows(const LevelRowsArgs& a, hipStream_t s);
 void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const int32_t* cs_feat, const int32_t* n_cs,
                            int32_t max_splits, int32_t wps, hipStream_t s);
 struct SelectArgs;
+// lane-batched launches (tree.h "lane-batched launches"): h on the host, d the same array on the device
+struct QuantLane;
+struct SplitBestLane;
+struct SplitBestPlanLane;
+struct PartColsLane;
+struct RootSendLane;
+struct CopyLane;
+void launch_copy_lanes(const CopyLane* h, const CopyLane* d, int L, hipStream_t s);
+void launch_root_send_lanes(const RootSendLane* d, int L, hipStream_t s);
+void launch_quant_lanes(const QuantLane* h, const QuantLane* d, int L, hipStream_t s);
+void launch_hist_lanes(const HistArgs* h, const HistArgs* d, int L, int bt, hipStream_t s);
+void launch_split_lanes(const SplitArgs* h, const SplitArgs* d, int L, hipStream_t s);
+void launch_split_best_lanes(const SplitBestLane* h, const SplitBestLane* d, int L, hipStream_t s);
+void launch_split_best_plan_lanes(const SplitBestPlanLane* h, const SplitBestPlanLane* d, int L, hipStream_t s);
+void launch_level_plan_lanes(const LevelPlanArgs* d, int L, hipStream_t s);
+void launch_select_groups_lanes(const SelectArgs* h, const SelectArgs* d, int L, hipStream_t s);
+void launch_partition_lanes(const PartColsLane* h, const PartColsLane* d, const PartitionArgs* dp, int L,
+                            hipStream_t s);
+void launch_rf_sample_lanes(const RfSampleArgs* h, const RfSampleArgs* d, int L, hipStream_t s);
+void launch_rf_compact_lanes(const RfCompactArgs* h, const RfCompactArgs* d, int L, hipStream_t s);
 // the partition's row pass may write the next level's row-list counts (PartitionArgs count_work):
 // 512-row list waves and one grid pass over the rows
 bool partition_counts_ok(int64_t N);

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kThreads) void rf_threshold_kernel(RfSampleArgs a, 
 // then per node a ticket; the node's last workgroup (one device-scope release per workgroup, see
 // tree_kernels.hip last_workgroup) ranks the candidates and zeroes the node's counters for the
 // next launch -- no memset and no second launch per level.
-__global__ __launch_bounds__(kThreads) void rf_window_threshold_kernel(RfSampleArgs a, uint64_t ulo, uint64_t uhi,
+__device__ __forceinline__ void rf_window_threshold_kernel_body(RfSampleArgs a, uint64_t ulo, uint64_t uhi,
                                                                        uint64_t* cand) {
   __shared__ unsigned int s_below;
   __shared__ int s_last;
@@ -203,8 +203,10 @@ __global__ __launch_bounds__(kThreads) void rf_window_threshold_kernel(RfSampleA
     ticket[i] = 0;
   }
 }
+__global__ __launch_bounds__(kThreads) void rf_window_threshold_kernel(RfSampleArgs a, uint64_t ulo, uint64_t uhi,
+                                                                       uint64_t* cand) { rf_window_threshold_kernel_body(a, ulo, uhi, cand); }
 
-__global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
+__device__ __forceinline__ void rf_mask_kernel_body(RfSampleArgs a) {
   const int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (f >= a.Fa) return;
   const int64_t fid = a.fid_orig[f];
@@ -215,6 +217,20 @@ __global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) {
     m = ((double)u * (1.0 / 9007199254740992.0) <= a.thr[i]) ? 1 : 0;
   }
   a.mask[f] = m;
+}
+__global__ __launch_bounds__(kThreads) void rf_mask_kernel(RfSampleArgs a) { rf_mask_kernel_body(a); }
+
+// lane-batched forms (tree.h "lane-batched launches"): lane l = blockIdx.z
+__global__ __launch_bounds__(kThreads) void rf_window_threshold_lanes_kernel(const RfSampleArgs* __restrict__ args,
+                                                                             uint64_t ulo, uint64_t uhi) {
+  const RfSampleArgs a = args[blockIdx.z];
+  if ((int)blockIdx.y >= a.nnodes) return;
+  uint64_t* cand = reinterpret_cast<uint64_t*>(a.scratch + 8 * ((2 * a.nnodes * 4 + 7) / 8));
+  rf_window_threshold_kernel_body(a, ulo, uhi, cand);
+}
+
+__global__ __launch_bounds__(kThreads) void rf_mask_lanes_kernel(const RfSampleArgs* __restrict__ args) {
+  rf_mask_kernel_body(args[blockIdx.z]);
 }
 }  // namespace
 
@@ -269,7 +285,7 @@ __device__ __forceinline__ int64_t chunk_wave_incl(int64_t v, int lane) {
   return v;
 }
 
-__global__ __launch_bounds__(kChunkThreads) void rf_compact_chunks_kernel(RfCompactArgs a, int pass) {
+__device__ __forceinline__ void rf_compact_chunks_kernel_body(RfCompactArgs a, int pass) {
   const int sh = blockIdx.y, c = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t f0 = a.fs[sh], f1 = a.fs[sh + 1];
   const int64_t lo = f0 + (int64_t)c * kChunkFeat;
@@ -319,6 +335,11 @@ __global__ __launch_bounds__(kChunkThreads) void rf_compact_chunks_kernel(RfComp
     if (sh == 0) a.local[a.Fa] = 0;
   }
 }
+__global__ __launch_bounds__(kChunkThreads) void rf_compact_chunks_kernel(RfCompactArgs a, int pass) { rf_compact_chunks_kernel_body(a, pass); }
+__global__ __launch_bounds__(kChunkThreads) void rf_compact_chunks_lanes_kernel(const RfCompactArgs* __restrict__ args,
+                                                                               int pass) {
+  rf_compact_chunks_kernel_body(args[blockIdx.z], pass);
+}
 }  // namespace
 
 int64_t rf_compact_chunks(int64_t max_shard_features) { return (max_shard_features + kChunkFeat - 1) / kChunkFeat; }
@@ -360,6 +381,40 @@ void launch_rf_sample(const RfSampleArgs& a, hipStream_t s) {
   }
   if (a.Fa > 0)
     hipLaunchKernelGGL(rf_mask_kernel, dim3((unsigned)((a.Fa + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
+}
+
+// window bounds of the fused sample (launch_rf_sample)
+static void rf_window(const RfSampleArgs& a, uint64_t* ulo, uint64_t* uhi) {
+  const double sd = 8.0 * sqrt((double)a.k) + 8.0;
+  const double lo = fmax(0.0, (double)a.k - sd) / (double)a.F, hi = fmin((double)a.F, (double)a.k + sd) / (double)a.F;
+  *ulo = (uint64_t)(lo * 9007199254740992.0);
+  *uhi = hi >= 1.0 ? (1ull << 53) : (uint64_t)(hi * 9007199254740992.0);
+}
+
+void launch_rf_sample_lanes(const RfSampleArgs* h, const RfSampleArgs* d, int L, hipStream_t s) {
+  if (L <= 0 || h[0].k >= h[0].F) return;
+  int32_t ny = 0;
+  for (int l = 0; l < L; ++l) {
+    FDX_LANES_CHECK(h[l].k == h[0].k && h[l].F == h[0].F && h[l].Fa == h[0].Fa && h[l].scratch != nullptr &&
+                    h[l].fused_counts != nullptr && h[l].nnodes <= h[l].fused_cap);
+    ny = h[l].nnodes > ny ? h[l].nnodes : ny;
+  }
+  if (ny <= 0) return;
+  uint64_t ulo, uhi;
+  rf_window(h[0], &ulo, &uhi);
+  hipLaunchKernelGGL(rf_window_threshold_lanes_kernel, dim3(kSlices, ny, L), dim3(kThreads), 0, s, d, ulo, uhi);
+  if (h[0].Fa > 0)
+    hipLaunchKernelGGL(rf_mask_lanes_kernel, dim3((unsigned)((h[0].Fa + kThreads - 1) / kThreads), 1, L), dim3(kThreads),
+                       0, s, d);
+}
+
+void launch_rf_compact_lanes(const RfCompactArgs* h, const RfCompactArgs* d, int L, hipStream_t s) {
+  if (L <= 0) return;
+  for (int l = 0; l < L; ++l)
+    FDX_LANES_CHECK(h[l].chunk_sums != nullptr && h[l].chunk_stride == h[0].chunk_stride && h[l].S == h[0].S);
+  const dim3 grid((unsigned)(h[0].chunk_stride > 0 ? h[0].chunk_stride : 1), (unsigned)h[0].S, L);
+  hipLaunchKernelGGL(rf_compact_chunks_lanes_kernel, grid, dim3(kChunkThreads), 0, s, d, 0);
+  hipLaunchKernelGGL(rf_compact_chunks_lanes_kernel, grid, dim3(kChunkThreads), 0, s, d, 1);
 }
 
 }  // namespace fdx

@@ -961,4 +961,60 @@ FDX_HD void level_plan(const LevelPlanArgs& a, bool reset = true) {
     for (int k = 0; k < 4; ++k) a.counts_host[k] = a.counts[k];
 }
 
+// ------------------------------------------------------------------ lane-batched launches
+// A forest's trees in flight grow in lockstep batches (bindings_level.cpp RfBatch): every stage
+// of a level is ONE launch for all the batch's trees, tree (lane) l's arguments at args[l] in
+// device memory (blockIdx.z = l), the grid the largest lane's; each kernel returns early from the
+// blocks beyond its own lane's grid. The per-lane arguments are exactly those of the per-tree
+// launches, so the trees are bitwise the same (tests/test_level_runner.py).
+struct BestPartials {              // (split_best_node: the narrow search's per-wave partials)
+  const double* part_gain;
+  const int32_t* part_f;
+  const int32_t* wide;
+  int32_t n_wide;
+};
+struct QuantLane {
+  QuantArgs a;
+  const double* maxv;
+  unsigned long long* part;
+};
+struct SplitBestLane {
+  const double* gain;
+  const int32_t* bin;
+  const int64_t* left;
+  int32_t nodes;
+  int32_t Fa;
+  int64_t f0;
+  int64_t* out;
+  BestPartials bp;
+};
+struct SplitBestPlanLane {
+  SplitBestLane b;
+  LevelPlanArgs p;
+  unsigned int* ticket;
+};
+// (data-parallel batches) the lane's root sums (its quantisation's kRootSlots slots) into words
+// tot_word, tot_word + 1 of every shard chunk of the batch's send buffer
+struct RootSendLane {
+  const int64_t* root_parts;
+  int64_t* send;
+  int32_t S;
+  int64_t chunk_words;
+  int64_t tot_word;
+};
+// a small copy per lane (node-table images, a level's count rows into host-mapped pinned rows)
+struct CopyLane {
+  void* dst;
+  const void* src;
+  int64_t bytes;
+};
+struct PartColsLane {
+  PartitionArgs a;
+  const int64_t* colptr;
+  const int32_t* cs_feat;
+  const int32_t* n_cs;
+  int32_t max_splits;
+  int32_t wps;
+};
+
 }  // namespace fdx

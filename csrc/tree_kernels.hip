@@ -87,13 +87,13 @@ __global__ __launch_bounds__(256) void quant_reduce_kernel(const unsigned long l
 // drained every wave's stores: an agent-scope fence writes the XCD's L2 back, and one per wave
 // of a 2048-workgroup grid cost ~140 us per pass (profiles/r5/NOTES.md); the acquire side runs
 // in the last workgroup alone.
-__device__ __forceinline__ bool last_workgroup(unsigned int* ticket) {
+__device__ __forceinline__ bool last_workgroup(unsigned int* ticket, unsigned total = 0) {
   __shared__ int s_last;
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
     const unsigned int t = atomicAdd(ticket, 1u);
-    s_last = (t == gridDim.x - 1) ? 1 : 0;
+    s_last = (t == (total ? total : gridDim.x) - 1) ? 1 : 0;
     if (s_last) atomicExch(ticket, 0u);
   }
   __syncthreads();
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void grad_max_kernel(const double* margin, con
 }
 
 // rowdig[r] = digits of (q0, q1); totals += (sum q0, sum q1) (int64 atomics, exact)
-__global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* maxv, unsigned long long* part) {
+__device__ __forceinline__ void quant_kernel_body(QuantArgs a, const double* maxv, unsigned long long* part) {
   int32_t k0 = maxv ? quant_exponent(maxv[0]) : 0, k1 = maxv ? quant_exponent(maxv[1]) : 0;
   if (a.max_parts) {                       // the max over grad_max_kernel's slots (every wave)
     const int lane = threadIdx.x & 63;
@@ -289,6 +289,7 @@ __global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* m
     if (a.kexp_copy) { a.kexp_copy[0] = k0; a.kexp_copy[1] = k1; }
   }
 }
+__global__ __launch_bounds__(256) void quant_kernel(QuantArgs a, const double* maxv, unsigned long long* part) { quant_kernel_body(a, maxv, part); }
 
 __global__ __launch_bounds__(256) void slot8_kernel(SlotArgs a) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.N; r += (int64_t)gridDim.x * 256) {
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(256) void hist_i8_kernel(HistArgs a) {
 // is ONE ds_add_u64. The entry pipeline (rows / keys 4 per lane, slots and count words one and
 // two steps ahead) is the MFMA kernel's; the table is flushed per item with integer atomics.
 template <int BT, bool PACK>
-__global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
+__device__ __forceinline__ void hist_lds_kernel_body(HistArgs a) {
   constexpr int G = 4 * kWave;
   constexpr int KEYS = 16 * BT;
   extern __shared__ unsigned long long s_tab[];          // [4 waves][KEYS * nslots]
@@ -738,6 +739,8 @@ __global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
     __builtin_amdgcn_wave_barrier();               // the table is zeroed for the next item
   }
 }
+template <int BT, bool PACK>
+__global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) { hist_lds_kernel_body<BT, PACK>(a); }
 
 // Compacted per-XCD lists of the active work items of a listed pass. A workgroup takes
 // kSelPerThread x 256 consecutive wave slots (coalesced reads), places its active items in LDS
@@ -746,7 +749,7 @@ __global__ __launch_bounds__(256) void hist_lds_kernel(HistArgs a) {
 // counters per pass, ~40 us a launch. The order inside a list is free (integer histograms).
 constexpr int kSelPerThread = 16;
 
-__global__ __launch_bounds__(256) void hist_select_kernel(HistArgs a, int32_t* list, int32_t* count) {
+__device__ __forceinline__ void hist_select_kernel_body(HistArgs a, int32_t* list, int32_t* count) {
   __shared__ int32_t s_cnt[8], s_base[8];
   const int t = threadIdx.x;
   if (t < 8) s_cnt[t] = 0;
@@ -775,6 +778,7 @@ __global__ __launch_bounds__(256) void hist_select_kernel(HistArgs a, int32_t* l
       list[(int64_t)x * a.list_cap + s_base[x] + loc[j]] = item[j];
     }
 }
+__global__ __launch_bounds__(256) void hist_select_kernel(HistArgs a, int32_t* list, int32_t* count) { hist_select_kernel_body(a, list, count); }
 
 // ------------------------------------------------------------------ dense i8 MFMA histogram
 // Same tile as hist_i8_kernel; the K dimension runs over 64 consecutive rows, so the row state
@@ -1106,7 +1110,7 @@ __global__ __launch_bounds__(256) void split_wide_kernel(SplitArgs a) {
 
 // split_kernel and split_wide_kernel in one launch: workgroups [0, nb_narrow) search the narrow
 // features (a thread per (node, feature)), the rest the wide ones (a wave per (node, feature))
-__global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb_narrow) {
+__device__ __forceinline__ void split_all_kernel_body(SplitArgs a, unsigned nb_narrow) {
   if (blockIdx.x < nb_narrow) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     int f;
@@ -1116,6 +1120,7 @@ __global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb
     split_wide_at(a, ((int64_t)(blockIdx.x - nb_narrow) * 256 + threadIdx.x) >> 6, threadIdx.x & 63);
   }
 }
+__global__ __launch_bounds__(256) void split_all_kernel(SplitArgs a, unsigned nb_narrow) { split_all_kernel_body(a, nb_narrow); }
 
 // Best split per node over the per-feature results of split_kernel, as one int64 row
 // {gain bits, feature + f0, bin, left0, left1}: the largest gain, ties to the lowest feature; a
@@ -1126,12 +1131,6 @@ constexpr int kBestThreads = 1024;
 // With the narrow search's per-wave partials (bp.part_gain): their ~Fa / 64 values per node
 // and the wide features' gains instead of all Fa gains -- the same maximum and tie rule, one
 // round of loads per thread (the full scan was ~17 us per level whatever the node count).
-struct BestPartials {
-  const double* part_gain;
-  const int32_t* part_f;
-  const int32_t* wide;
-  int32_t n_wide;
-};
 
 __device__ __forceinline__ void split_best_node(const double* gain, const int32_t* bin, const int64_t* left,
                                                 int32_t Fa, int64_t f0, int64_t* out, int n,
@@ -1219,7 +1218,7 @@ __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* 
 // profiles/r4/gbdt_10M_round_timeline_partition8.txt).
 constexpr int kPartRows = 8;
 
-__global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) {
+__device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   if (a.zero != nullptr) {           // the next level's histograms, zeroed on the way (16-byte stores)
     int4* z = reinterpret_cast<int4*>(a.zero);
     const int64_t nz = a.zero_n / 2;
@@ -1359,6 +1358,7 @@ __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a)
       atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);
   }
 }
+__global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) { partition_default_kernel_body(a); }
 
 // LevelChooseArgs: one wave; lane i sums node i's 32 spread row counts (and zeroes them), then
 // lane b < builds takes build b's sibling pair.
@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(256) void partition_column_kernel(PartitionArgs a) 
 
 // Column pass of the device level loop: block b handles split b / wps, entries
 // part = b % wps of its column, grid-strided (the splits and their count live on the device).
-__global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, const int64_t* colptr, const int32_t* cs_feat,
+__device__ __forceinline__ void partition_cols_kernel_body(PartitionArgs a, const int64_t* colptr, const int32_t* cs_feat,
                                                              const int32_t* n_cs, int32_t wps) {
   const int sp = blockIdx.x / wps, part = blockIdx.x % wps;
   if (sp >= *n_cs) return;
@@ -1428,6 +1428,8 @@ __global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, co
     }
   }
 }
+__global__ __launch_bounds__(256) void partition_cols_kernel(PartitionArgs a, const int64_t* colptr, const int32_t* cs_feat,
+                                                             const int32_t* n_cs, int32_t wps) { partition_cols_kernel_body(a, colptr, cs_feat, n_cs, wps); }
 
 // exclusive prefix count of the lanes below this one whose predicate holds, and the wave total
 __device__ __forceinline__ int32_t lp_rank(bool pred, int32_t* total) {
@@ -1636,27 +1638,33 @@ __global__ __launch_bounds__(64) void level_rows_kernel(LevelRowsArgs a) {
   if (k < a.nb) level_rows_slot(a, k);
 }
 
-__global__ void level_plan_kernel(LevelPlanArgs a) {
+__device__ __forceinline__ void level_plan_kernel_body(LevelPlanArgs a) {
   if (blockIdx.x != 0) return;
   level_plan_reset(a, (int32_t)threadIdx.x, (int32_t)blockDim.x);
   __syncthreads();
   if (threadIdx.x < 64) level_plan_wave(a);
 }
+__global__ void level_plan_kernel(LevelPlanArgs a) { level_plan_kernel_body(a); }
 
 // split_best_kernel + level_plan_kernel in one launch (levels without a collective between the
 // split search and the plan): a workgroup per node writes its best split tuple, and the last
 // workgroup to finish (ticket) plans the level from all of them -- the same two bodies, so the
 // same node table bit for bit, one launch and one kernel boundary less per level.
-__global__ __launch_bounds__(kBestThreads) void split_best_plan_kernel(const double* gain, const int32_t* bin,
+__device__ __forceinline__ void split_best_plan_kernel_body(const double* gain, const int32_t* bin,
                                                                        const int64_t* left, int32_t Fa, int64_t f0,
                                                                        int64_t* out, LevelPlanArgs p,
-                                                                       unsigned int* ticket, BestPartials bp) {
+                                                                       unsigned int* ticket, BestPartials bp,
+                                                                       unsigned nblocks = 0) {
   split_best_node(gain, bin, left, Fa, f0, out, blockIdx.x, bp);
-  if (!last_workgroup(ticket)) return;
+  if (!last_workgroup(ticket, nblocks)) return;
   level_plan_reset(p, (int32_t)threadIdx.x, (int32_t)blockDim.x);
   __syncthreads();
   if (threadIdx.x < 64) level_plan_wave(p);
 }
+__global__ __launch_bounds__(kBestThreads) void split_best_plan_kernel(const double* gain, const int32_t* bin,
+                                                                       const int64_t* left, int32_t Fa, int64_t f0,
+                                                                       int64_t* out, LevelPlanArgs p,
+                                                                       unsigned int* ticket, BestPartials bp) { split_best_plan_kernel_body(gain, bin, left, Fa, f0, out, p, ticket, bp); }
 
 // ------------------------------------------------------------------ gbdt helpers
 __global__ __launch_bounds__(256) void logistic_grad_kernel(const double* margin, const float* label,
@@ -1691,6 +1699,85 @@ __global__ __launch_bounds__(256) void leaf_values_kernel(const int64_t* stats, 
                                                           double eta, double lambda, double mds, double* out) {
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n < M) out[n] = leaf_value(stats[2 * n], stats[2 * n + 1], kexp[0], kexp[1], eta, lambda, mds);
+}
+
+// ------------------------------------------------------------------ lane-batched kernels
+// (tree.h "lane-batched launches": lane l = blockIdx.z, its arguments copied out of args[l])
+__global__ __launch_bounds__(256) void quant_lanes_kernel(const QuantLane* __restrict__ args) {
+  const QuantLane q = args[blockIdx.z];
+  quant_kernel_body(q.a, q.maxv, q.part);
+}
+
+template <int BT, bool PACK>
+__global__ __launch_bounds__(256) void hist_lds_lanes_kernel(const HistArgs* __restrict__ args) {
+  const HistArgs a = args[blockIdx.z];
+  if (a.active_list == nullptr && (int)blockIdx.x * 4 >= (a.wave_item ? a.num_slots : a.num_items)) return;
+  hist_lds_kernel_body<BT, PACK>(a);
+}
+
+__global__ __launch_bounds__(64) void hist_count_zero_lanes_kernel(const HistArgs* __restrict__ args) {
+  if (threadIdx.x < 8) args[blockIdx.z].active_count[threadIdx.x] = 0;
+}
+
+__global__ __launch_bounds__(256) void hist_select_lanes_kernel(const HistArgs* __restrict__ args) {
+  HistArgs a = args[blockIdx.z];
+  a.num_slots = a.wave_item ? a.num_slots : a.num_items;
+  if ((int64_t)blockIdx.x * 256 * kSelPerThread >= a.num_slots) return;
+  hist_select_kernel_body(a, a.active_list, a.active_count);
+}
+
+__global__ __launch_bounds__(256) void split_all_lanes_kernel(const SplitArgs* __restrict__ args) {
+  const SplitArgs a = args[blockIdx.z];
+  const int64_t n = (int64_t)a.num_nodes * a.Fa;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  const int64_t waves = (a.wide != nullptr && a.n_wide > 0) ? (int64_t)a.num_nodes * a.n_wide : 0;
+  if (n <= 0 || blockIdx.x >= nb + (unsigned)((waves + 3) / 4)) return;
+  split_all_kernel_body(a, nb);
+}
+
+__global__ __launch_bounds__(kBestThreads) void split_best_lanes_kernel(const SplitBestLane* __restrict__ args) {
+  const SplitBestLane b = args[blockIdx.z];
+  if ((int)blockIdx.x >= b.nodes || b.Fa <= 0) return;
+  split_best_node(b.gain, b.bin, b.left, b.Fa, b.f0, b.out, blockIdx.x, b.bp);
+}
+
+__global__ __launch_bounds__(kBestThreads) void split_best_plan_lanes_kernel(const SplitBestPlanLane* __restrict__ args) {
+  const SplitBestPlanLane q = args[blockIdx.z];
+  if ((int)blockIdx.x >= q.b.nodes) return;
+  split_best_plan_kernel_body(q.b.gain, q.b.bin, q.b.left, q.b.Fa, q.b.f0, q.b.out, q.p, q.ticket, q.b.bp,
+                              (unsigned)q.b.nodes);
+}
+
+__global__ void level_plan_lanes_kernel(const LevelPlanArgs* __restrict__ args) { level_plan_kernel_body(args[blockIdx.z]); }
+
+__global__ __launch_bounds__(256) void partition_cols_lanes_kernel(const PartColsLane* __restrict__ args) {
+  const PartColsLane q = args[blockIdx.z];
+  if ((int)blockIdx.x >= q.max_splits * q.wps) return;
+  partition_cols_kernel_body(q.a, q.colptr, q.cs_feat, q.n_cs, q.wps);
+}
+
+__global__ __launch_bounds__(64) void root_send_lanes_kernel(const RootSendLane* __restrict__ args) {
+  const RootSendLane a = args[blockIdx.z];
+  int64_t t0, t1;
+  root_sums(a.root_parts, &t0, &t1);
+  for (int32_t sh = (int32_t)threadIdx.x; sh < a.S; sh += 64) {
+    a.send[sh * a.chunk_words + a.tot_word] = t0;
+    a.send[sh * a.chunk_words + a.tot_word + 1] = t1;
+  }
+}
+
+__global__ __launch_bounds__(256) void copy_lanes_kernel(const CopyLane* __restrict__ args) {
+  const CopyLane c = args[blockIdx.z];
+  const bool words = ((reinterpret_cast<uintptr_t>(c.dst) | reinterpret_cast<uintptr_t>(c.src) | (uintptr_t)c.bytes) & 7) == 0;
+  const int64_t n = words ? c.bytes / 8 : c.bytes;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (words) reinterpret_cast<uint64_t*>(c.dst)[i] = reinterpret_cast<const uint64_t*>(c.src)[i];
+    else reinterpret_cast<uint8_t*>(c.dst)[i] = reinterpret_cast<const uint8_t*>(c.src)[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void partition_default_lanes_kernel(const PartitionArgs* __restrict__ args) {
+  partition_default_kernel_body(args[blockIdx.z]);
 }
 
 constexpr int kQuantBlocks = 2048;      // workgroup cap of the quantisation passes (partials)
@@ -1738,7 +1825,7 @@ void launch_slot8(const SlotArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(slot8_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
-__global__ __launch_bounds__(256) void hist_select_groups_kernel(SelectArgs a) {
+__device__ __forceinline__ void hist_select_groups_kernel_body(SelectArgs a) {
   const int g = blockIdx.y;
   const int64_t w0 = (int64_t)blockIdx.x * 256 * kSelPerThread;
   if (w0 >= a.num_slots[g]) return;                 // (workgroup-uniform)
@@ -1773,6 +1860,10 @@ __global__ __launch_bounds__(256) void hist_select_groups_kernel(SelectArgs a) {
       const int x = (int)(((w0 + (int64_t)j * 256 + t) >> 2) & 7);
       a.list[g][(int64_t)x * a.list_cap[g] + s_base[x] + loc[j]] = item[j];
     }
+}
+__global__ __launch_bounds__(256) void hist_select_groups_kernel(SelectArgs a) { hist_select_groups_kernel_body(a); }
+__global__ __launch_bounds__(256) void hist_select_groups_lanes_kernel(const SelectArgs* __restrict__ args) {
+  hist_select_groups_kernel_body(args[blockIdx.z]);
 }
 
 void launch_hist_select_groups(const SelectArgs& a, hipStream_t s) {
@@ -1974,6 +2065,124 @@ void launch_leaf_update_stats(double* margin, const int32_t* row_node, const int
 
 void launch_leaf_update(double* margin, const int32_t* row_node, const double* node_value, int64_t N, hipStream_t s) {
   if (N > 0) hipLaunchKernelGGL(leaf_update_kernel, dim3(grid_for(N)), dim3(256), 0, s, margin, row_node, node_value, N);
+}
+
+// ------------------------------------------------------------------ lane-batched launchers
+// h: the lanes' arguments on the host (grid sizing), d: the same array in device memory
+void launch_quant_lanes(const QuantLane* h, const QuantLane* d, int L, hipStream_t s) {
+  if (L <= 0) return;
+  unsigned gx = 1;
+  for (int l = 0; l < L; ++l) {
+    const QuantArgs& a = h[l].a;
+    FDX_LANES_CHECK(a.atomic_root && a.ticket == nullptr);
+    const unsigned nt = a.N > 0 ? grid_for(a.N / kPrologueU + 1, kSlotBlocks) : 1;
+    gx = nt > gx ? nt : gx;
+  }
+  hipLaunchKernelGGL(quant_lanes_kernel, dim3(gx, 1, L), dim3(256), 0, s, d);
+}
+
+void launch_hist_lanes(const HistArgs* h, const HistArgs* d, int L, int bt, hipStream_t s) {
+  if (L <= 0 || h[0].num_items <= 0) return;
+  const int32_t slots = h[0].wave_item ? h[0].num_slots : h[0].num_items;
+  const bool listed = h[0].active_list != nullptr, presel = listed && h[0].listed_per_xcd >= 0;
+  const bool pack = h[0].rowpack != nullptr;
+  unsigned gx = (unsigned)((slots + 3) / 4);
+  int32_t ns = 1;
+  for (int l = 0; l < L; ++l) {
+    FDX_LANES_CHECK((h[l].active_list != nullptr) == listed && (h[l].listed_per_xcd >= 0) == presel &&
+                     (h[l].rowpack != nullptr) == pack && h[l].lds);
+    ns = h[l].nslots > ns ? h[l].nslots : ns;
+  }
+  if (presel) {
+    int32_t most = 0;
+    for (int l = 0; l < L; ++l) most = h[l].listed_per_xcd > most ? h[l].listed_per_xcd : most;
+    if (most == 0) return;
+    gx = (unsigned)((most + 3) / 4 * 8);
+  } else if (listed) {
+    hipLaunchKernelGGL(hist_count_zero_lanes_kernel, dim3(1, 1, L), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(hist_select_lanes_kernel, dim3((slots + 256 * kSelPerThread - 1) / (256 * kSelPerThread), 1, L),
+                       dim3(256), 0, s, d);
+    const int32_t waves = slots < kListedWaves ? slots : kListedWaves;
+    gx = (unsigned)(((waves + 3) / 4 + 7) / 8 * 8);
+  }
+  const size_t lds = (size_t)4 * 16 * bt * ns * sizeof(unsigned long long);
+  const dim3 grid(gx, 1, L), block(256);
+#define FDX_HL(B, P) hipLaunchKernelGGL((hist_lds_lanes_kernel<B, P>), grid, block, lds, s, d)
+  if (bt == 1) { if (pack) FDX_HL(1, true); else FDX_HL(1, false); }
+  else if (bt == 2) { if (pack) FDX_HL(2, true); else FDX_HL(2, false); }
+  else { if (pack) FDX_HL(4, true); else FDX_HL(4, false); }
+#undef FDX_HL
+}
+
+void launch_split_lanes(const SplitArgs* h, const SplitArgs* d, int L, hipStream_t s) {
+  unsigned gx = 0;
+  for (int l = 0; l < L; ++l) {
+    const int64_t n = (int64_t)h[l].num_nodes * h[l].Fa;
+    const int64_t waves = (h[l].wide != nullptr && h[l].n_wide > 0) ? (int64_t)h[l].num_nodes * h[l].n_wide : 0;
+    const unsigned g = n > 0 ? (unsigned)((n + 255) / 256) + (unsigned)((waves + 3) / 4) : 0;
+    gx = g > gx ? g : gx;
+  }
+  if (L > 0 && gx > 0) hipLaunchKernelGGL(split_all_lanes_kernel, dim3(gx, 1, L), dim3(256), 0, s, d);
+}
+
+void launch_split_best_lanes(const SplitBestLane* h, const SplitBestLane* d, int L, hipStream_t s) {
+  int32_t gx = 0;
+  for (int l = 0; l < L; ++l) gx = (h[l].Fa > 0 && h[l].nodes > gx) ? h[l].nodes : gx;
+  if (L > 0 && gx > 0) hipLaunchKernelGGL(split_best_lanes_kernel, dim3(gx, 1, L), dim3(kBestThreads), 0, s, d);
+}
+
+void launch_split_best_plan_lanes(const SplitBestPlanLane* h, const SplitBestPlanLane* d, int L, hipStream_t s) {
+  int32_t gx = 0;
+  for (int l = 0; l < L; ++l) {
+    FDX_LANES_CHECK(h[l].b.nodes > 0 && h[l].b.Fa > 0);
+    gx = h[l].b.nodes > gx ? h[l].b.nodes : gx;
+  }
+  if (L > 0) hipLaunchKernelGGL(split_best_plan_lanes_kernel, dim3(gx, 1, L), dim3(kBestThreads), 0, s, d);
+}
+
+void launch_copy_lanes(const CopyLane* h, const CopyLane* d, int L, hipStream_t s) {
+  int64_t most = 0;
+  for (int l = 0; l < L; ++l) most = h[l].bytes > most ? h[l].bytes : most;
+  if (L <= 0 || most <= 0) return;
+  const int64_t blocks = (most / 8 + 255) / 256;
+  hipLaunchKernelGGL(copy_lanes_kernel, dim3((unsigned)(blocks < 1 ? 1 : (blocks > 64 ? 64 : blocks)), 1, L), dim3(256), 0,
+                     s, d);
+}
+
+void launch_root_send_lanes(const RootSendLane* d, int L, hipStream_t s) {
+  if (L > 0) hipLaunchKernelGGL(root_send_lanes_kernel, dim3(1, 1, L), dim3(64), 0, s, d);
+}
+
+void launch_level_plan_lanes(const LevelPlanArgs* d, int L, hipStream_t s) {
+  if (L > 0) hipLaunchKernelGGL(level_plan_lanes_kernel, dim3(1, 1, L), dim3(64), 0, s, d);
+}
+
+void launch_select_groups_lanes(const SelectArgs* h, const SelectArgs* d, int L, hipStream_t s) {
+  if (L <= 0 || h[0].n <= 0) return;
+  int32_t most = 0;
+  for (int g = 0; g < h[0].n; ++g) most = h[0].num_slots[g] > most ? h[0].num_slots[g] : most;
+  for (int l = 0; l < L; ++l) FDX_LANES_CHECK(h[l].n == h[0].n);
+  if (most <= 0) return;
+  hipLaunchKernelGGL(hist_select_groups_lanes_kernel,
+                     dim3((most + 256 * kSelPerThread - 1) / (256 * kSelPerThread), h[0].n, L), dim3(256), 0, s, d);
+}
+
+void launch_partition_lanes(const PartColsLane* h, const PartColsLane* d, const PartitionArgs* dp, int L,
+                            hipStream_t s) {
+  if (L <= 0) return;
+  int32_t gx = 0;
+  for (int l = 0; l < L; ++l) {
+    FDX_LANES_CHECK(h[l].a.N == h[0].a.N && (h[l].a.node_parent != nullptr) == (h[0].a.node_parent != nullptr));
+    gx = h[l].max_splits * h[l].wps > gx ? h[l].max_splits * h[l].wps : gx;
+  }
+  const auto cols = [&] {
+    if (gx > 0) hipLaunchKernelGGL(partition_cols_lanes_kernel, dim3(gx, 1, L), dim3(256), 0, s, d);
+  };
+  if (h[0].a.node_parent != nullptr) cols();
+  if (h[0].a.N > 0)
+    hipLaunchKernelGGL(partition_default_lanes_kernel, dim3(grid_for((h[0].a.N + kPartRows - 1) / kPartRows), 1, L),
+                       dim3(256), 0, s, dp);
+  if (h[0].a.node_parent == nullptr) cols();
 }
 
 }  // namespace fdx

@@ -42,8 +42,12 @@ from typing import Optional
 
 import torch
 
+import numpy as np
+
+from ..ops import native
 from ..utils import tracing
 from ..utils.streams import StreamSwitch
+from . import grower as G
 from .grower import CollStep, GrowParams, LevelBatcher, Workspace, _Lane, device_tree_steps
 from .quantize import Quantized
 
@@ -55,6 +59,10 @@ TREES_IN_FLIGHT = int(os.environ.get("FDX_RF_INFLIGHT", "16"))
 LANE_HIST_STREAMS = int(os.environ.get("FDX_RF_LANE_STREAMS", "1"))
 # data parallelism: groups of lanes whose levels share one reduce-scatter + all-gather
 LANE_GROUPS = int(os.environ.get("FDX_RF_GROUPS", "2"))
+# sampled RF trees grow in lockstep batches on the native runner (csrc/bindings_level.cpp RfBatch):
+# every stage of a level is ONE lane-batched launch for all the trees in flight and the level loop
+# runs in C++ (0: the per-tree lanes driven from Python)
+BATCH = os.environ.get("FDX_RF_BATCH", "1") == "1"
 
 
 class ForestLanes:
@@ -72,6 +80,139 @@ class ForestLanes:
 
     def stream_ctx(self, i: int):
         return self.switches[i]
+
+
+def batch_ok(Q: Quantized, params: GrowParams, weight) -> bool:
+    """The lockstep batch covers the default sampled-RF configuration on the device (the lean
+    runner level loop with fused packed row state and the LDS-atomic count passes)."""
+    return (BATCH and Q.device.type == "cuda" and G.NATIVE_LEVELS and G.SAMPLED and G.FUSED_PACK and G.LEAN_RF and
+            G.RF_LDS and params.feat_k > 0 and G._choose_np(params, weight) == 1 and params.max_depth >= 1 and
+            G.device_levels_ok(params, weight))
+
+
+class ForestBatch:
+    """The lanes' workspaces, level states and runners handed to one native RfBatch (built once
+    per ForestLanes and tree parameters): per lane the level buffers of grower._rf_runner_levels
+    plus two pinned node-table copies (the host builds one batch's trees while the next grows)."""
+
+    def __init__(self, Q: Quantized, lanes: ForestLanes, params: GrowParams, coll=None, shards: list = None):
+        dev = Q.device
+        presel = G.PRESELECT and Q.n_rows >= G.PRESELECT_MIN_ROWS
+        item_groups = Q.groups + Q.hot_groups
+        sel_ids = [gi for gi, grp in enumerate(item_groups) if grp.num_items] if presel else []
+        dp = shards is not None and shards[0] is not None
+        compact = dp and 0 < params.feat_k < Q.num_features and \
+            (G.RF_COMPACT == "1" or (G.RF_COMPACT == "auto" and shards[0].S > 1))
+        D = int(params.max_depth)
+        self.Q, self.params, self.dp = Q, params, dp
+        self.views, lane_cfg = [], []
+        for i, ws in enumerate(lanes.ws):
+            st = getattr(ws, "_levels", None)
+            if st is None or st.max_depth != D or st.n_sel != len(sel_ids):
+                st = ws._levels = G.LevelState(Q, D, len(sel_ids))
+            runner = G._level_runner(Q, ws, st, params, item_groups, True)
+            if st.rf_thr is None:
+                st.rf_thr = [torch.empty(st.cap, dtype=torch.float64, device=dev) for _ in range(2)]
+                st.rf_mask = [torch.empty(Q.Fa, dtype=torch.uint8, device=dev) for _ in range(2)]
+            hosts = [st.arena_host, torch.zeros_like(st.arena_host).pin_memory()]
+            self.views.append([st.host_views(h) for h in hosts])
+            lc = dict(runner=runner, open0=st.open[0], open1=st.open[1], totals0=st.totals[0], totals1=st.totals[1],
+                      arena=st.arena, arena_init=st.arena_init_dev, arena_host0=hosts[0], arena_host1=hosts[1],
+                      tot_scratch=ws.totals, rowpack=ws.rowpack(),
+                      sel=[ws.item_list(gi, grp)[0] if gi in sel_ids else None for gi, grp in enumerate(item_groups)],
+                      listed=[ws.item_list(gi, grp) if grp.num_items else (None, None)
+                              for gi, grp in enumerate(item_groups)])
+            if compact:
+                sh = shards[i]
+                for p in (0, 1):
+                    lc[f"thr{p}"] = sh.compact_thr(p, st.cap)
+                    lc[f"mask{p}"] = sh.compact_mask(p)
+                    lc[f"sh_local{p}"] = sh._local_c[p]
+                    lc[f"sh_sizes{p}"] = sh._sizes[p]
+                    lc[f"sh_sizes_host{p}"] = sh.sizes_host[p]
+            else:
+                for p in (0, 1):
+                    lc[f"thr{p}"] = st.rf_thr[p]
+                    lc[f"mask{p}"] = st.rf_mask[p]
+            if not dp:
+                # the level's histograms: every open node built, the deepest level opens 2^(D-1)
+                lc["hist"] = torch.empty((max(1, 1 << (D - 1)), Q.TB, 2), dtype=torch.int64, device=dev)
+                lc["packed"] = torch.empty((st.cap, 5), dtype=torch.int64, device=dev)
+            lane_cfg.append(lc)
+        st0 = lanes.ws[0]._levels
+        cfg = dict(lanes=lane_cfg, max_depth=D, boff=Q.boff, listed_max_nodes=G.LISTED_MAX_NODES, presel=bool(sel_ids),
+                   one=st0.one, zero1=st0.zero1, iota=lanes.ws[0].iota(64), dp=dp)
+        if dp:
+            sh = shards[0]
+            cfg.update(S=int(sh.S), Bs=int(sh.Bs), max_nb=int(sh.max_nb), compact=bool(compact), shard_of=sh._shard_of,
+                       sh_local=sh._local, sh_boff=sh.boff, sh_nbins=sh.nbins, sh_zbin=sh.zbin, sh_fid=sh.fid_orig,
+                       sh_fs=sh._fs_dev, nbins_all=Q.nbins, f0=int(sh.f0), Fa_s=int(sh.Fa),
+                       max_shard_features=int(sh.max_shard_features),
+                       wide=G._wide_features(sh.nbins, sh.Fa) if G.SPLIT_WIDE else None)
+        else:
+            cfg["wide"] = G._wide_features(Q.nbins, Q.Fa) if G.SPLIT_WIDE else None
+        self.cfg = cfg
+        self.native = None
+
+    def bind(self, coll) -> None:
+        """Creates the native batch (with the collectives of ``coll`` under data parallelism)."""
+        if self.native is not None:
+            return
+        cfg = dict(self.cfg)
+        if self.dp:
+            cb = G._DpCollectives(coll, self.Q.device)
+            comm, lib = G._rccl_comm(self.Q.device)
+            cfg.update(rs=cb.rs, ag=cb.ag, comm=comm, rccl_lib=lib)
+        self.native = native.lib().RfBatch(cfg)
+
+
+def grow_forest_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tree_ids: list, label: torch.Tensor,
+                        weight: Optional[torch.Tensor], bootstrap: bool, coll=None) -> list:
+    """Grows ``tree_ids`` in lockstep batches of ``len(lanes.ws)`` trees (RfBatch); returns them in
+    order. Batch b + 1's levels run while the host builds batch b's trees (at its first wait)."""
+    use_coll = coll is not None and coll.active
+    shards = build_shared_state(Q, lanes, coll if use_coll else None)
+    key = (params.max_depth, params.mode, params.min_gain, params.min_child, params.seed, params.feat_k,
+           shards[0] is not None)
+    fb = getattr(lanes, "_batch", None)
+    if fb is None or fb[0] != key:
+        fb = lanes._batch = (key, ForestBatch(Q, lanes, params, coll if use_coll else None, shards))
+    fb = fb[1]
+    fb.bind(coll if use_coll else None)
+    nl = len(lanes.ws)
+    out: list = []
+    pending = []
+
+    def build_pending() -> None:
+        # (called inside the next grow, before its first host wait: the previous batch's node
+        # tables were queued before this batch's launches -- its event, not yet re-recorded)
+        fb.native.wait()
+        while pending:
+            par, ids = pending.pop(0)
+            for lane, t in enumerate(ids):
+                out.append(G.tree_from_host(Q, params, fb.views[lane][par]))
+
+    from ..parallel import dist as D
+
+    for b, i in enumerate(range(0, len(tree_ids), nl)):
+        ids = tree_ids[i:i + nl]
+        with tracing.span("forest.batch", trees=len(ids)):
+            stat = fb.native.grow(ids, label, weight, bool(bootstrap), int(Q.row0), b & 1,
+                                  build_pending if pending else None)
+        G.LEVEL_STATS["levels"] += stat[0]
+        G.LEVEL_STATS["built_nodes"] += stat[1]
+        G.LEVEL_STATS["hist_bytes"] += stat[1] * Q.TB * 16
+        G.LEVEL_STATS["listed_passes"] += stat[2]
+        G.LEVEL_STATS["listed_active_items"] += stat[3]
+        G.LEVEL_STATS["listed_grid_waves"] += stat[4]
+        if fb.dp and fb.native.direct():    # (RCCL called by the batch itself; the callbacks count their own)
+            G.LEVEL_STATS["coll_calls"] += stat[5] + stat[6]
+            D.CALLS["reduce_scatter"] += stat[5]
+            D.CALLS["all_gather"] += stat[6]
+        pending.append((b & 1, ids))
+    fb.native.wait()
+    build_pending()
+    return out
 
 
 def build_shared_state(Q: Quantized, lanes: ForestLanes, coll=None) -> list:
@@ -96,6 +237,8 @@ def grow_forest_concurrent(Q: Quantized, lanes: ForestLanes, params: GrowParams,
     order so that every rank issues the same collective sequence."""
     cuda = lanes.dev.type == "cuda"
     use_coll = coll is not None and coll.active
+    if batch_ok(Q, params, weight):
+        return grow_forest_batched(Q, lanes, params, tree_ids, label, weight, bootstrap, coll)
     shards = build_shared_state(Q, lanes, coll if use_coll else None)
     if cuda:                                   # the lanes see everything queued before (Q, label, shared state)
         main = torch.cuda.current_stream(lanes.dev)

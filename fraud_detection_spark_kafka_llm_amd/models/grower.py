@@ -1109,6 +1109,10 @@ class LevelState:
         ev.record(stream)
         return ev
 
+    def host_views(self, buf: torch.Tensor) -> dict:
+        """Named views of a host copy of the arena (node table fields + exponents)."""
+        return {name: buf[o:o + n].view(dt).view(shape) for name, dt, shape, o, n in self._layout}
+
     def __init__(self, Q: Quantized, max_depth: int, n_sel: int = 0):
         dev = Q.device
         M = 2 ** (max_depth + 1)
@@ -1138,12 +1142,12 @@ class LevelState:
         self.arena_host = torch.zeros(nbytes, dtype=torch.uint8)
         if dev.type == "cuda":
             self.arena_host = self.arena_host.pin_memory()
-        host = {}
+        self._layout = []
         for (name, dt, shape), o in zip(layout, offs):
             n = torch.empty(0, dtype=dt).element_size() * int(np.prod(shape))
             setattr(self, name if name != "kexp" else "kexp_slot", self.arena[o:o + n].view(dt).view(shape))
-            host[name] = self.arena_host[o:o + n].view(dt).view(shape)
-        self.host = host
+            self._layout.append((name, dt, shape, o, n))
+        self.host = self.host_views(self.arena_host)
         self.n_nodes.fill_(1)
         for t_ in (self.parent, self.left, self.right, self.feat, self.bin):
             t_.fill_(-1)
@@ -2028,17 +2032,21 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
 
     def finish() -> Tree:
         done.synchronize()
-        hv = st.host
-        nn = int(hv["n_nodes"][0])
-        arr = [hv[k][:nn].numpy().copy() for k in ("parent", "feat", "bin", "left", "right", "gain", "stats", "leaf")]
-        kexp = hv["kexp"].numpy().astype(np.int64)
-        tab = TreeTable.from_arrays(Q, *arr)
-        return tab.build(Q, params, np.ldexp(1.0, -kexp))
+        return tree_from_host(Q, params, st.host)
 
     if node_value is not None:
         return PendingTree(node_value, finish)
     yield done
     return finish()
+
+
+def tree_from_host(Q: Quantized, params: GrowParams, hv: dict) -> Tree:
+    """The Tree of a device node table copied to the host (LevelState.host views of the arena)."""
+    nn = int(hv["n_nodes"][0])
+    arr = [hv[k][:nn].numpy().copy() for k in ("parent", "feat", "bin", "left", "right", "gain", "stats", "leaf")]
+    kexp = hv["kexp"].numpy().astype(np.int64)
+    tab = TreeTable.from_arrays(Q, *arr)
+    return tab.build(Q, params, np.ldexp(1.0, -kexp))
 
 
 def leaf_values_device(stats: torch.Tensor, kexp: torch.Tensor, params: GrowParams) -> torch.Tensor:

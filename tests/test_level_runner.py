@@ -8,7 +8,7 @@ import torch
 from fraud_detection_spark_kafka_llm_amd.ops import native
 
 
-def _forest(device, n=6000, F=400, trees=6, depth=5, seed=7):
+def _forest(device, n=6000, F=400, trees=6, depth=5, seed=7, rows=None):
     from fraud_detection_spark_kafka_llm_amd.ml.linalg import VectorColumn
     from fraud_detection_spark_kafka_llm_amd.models.tree import fit_forest
 
@@ -18,6 +18,8 @@ def _forest(device, n=6000, F=400, trees=6, depth=5, seed=7):
     y = ((counts[:, 1] > 0) ^ (counts[:, 5] >= 2)).astype(np.float32)
     flip = rng.random(n) < 0.05
     y[flip] = 1 - y[flip]
+    if rows is not None:                                     # (this rank's shard)
+        counts, y = counts[rows[0]:rows[1]], y[rows[0]:rows[1]]
     vc = VectorColumn(F, dense=torch.from_numpy(counts.astype(np.float64)))
     r = fit_forest(vc, torch.from_numpy(y), num_trees=trees, max_depth=depth, bootstrap=True, feature_subset="sqrt",
                    seed=seed, device=device)
@@ -43,6 +45,61 @@ def test_gpu_native_levels_equal_python_levels(inflight, monkeypatch):
         monkeypatch.setattr(grower, "FUSED_PACK", fused)
         assert _forest("cuda:0") == ref
     assert _forest("cpu") == ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inflight,depth", [(2, 5), (3, 3), (8, 5), (16, 6)])
+def test_gpu_rf_lockstep_batch_equals_per_tree_lanes(inflight, depth, monkeypatch):
+    """the trees in flight grown in lockstep batches (csrc/bindings_level.cpp
+    RfBatch: one lane-batched launch per stage of a level, the level loop in C++) are bitwise the
+    per-tree lanes' forest, with and without preselected item lists."""
+    from fraud_detection_spark_kafka_llm_amd.models import forest_batch, grower
+
+    monkeypatch.setattr(forest_batch, "TREES_IN_FLIGHT", inflight)
+    for presel in (True, False):
+        monkeypatch.setattr(grower, "PRESELECT", presel)
+        monkeypatch.setattr(forest_batch, "BATCH", False)
+        ref = _forest("cuda:0", trees=7, depth=depth)
+        monkeypatch.setattr(forest_batch, "BATCH", True)
+        assert _forest("cuda:0", trees=7, depth=depth) == ref, presel
+
+
+def _dp_forest(rank, world, device, batch, compact):
+    """One rank's forest under data parallelism (lockstep batches or per-tree lanes)."""
+    from fraud_detection_spark_kafka_llm_amd.models import forest_batch, grower
+    from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
+
+    forest_batch.BATCH = batch
+    forest_batch.TREES_IN_FLIGHT = 4
+    grower.RF_COMPACT = compact
+    lo, hi = D.shard_range(6000, rank, world)
+    D.reset_bytes()
+    grower.reset_level_stats()
+    trees = _forest(device, trees=7, rows=(lo, hi))
+    return trees, dict(D.CALLS), grower.LEVEL_STATS["coll_calls"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,backend,compact", [(1, "nccl", "1"), (1, "nccl", "0"), (2, "gloo", "auto")])
+def test_gpu_rf_lockstep_batch_dp_equals_single_process(world, backend, compact, monkeypatch):
+    """The lockstep batches under data parallelism: ONE reduce-scatter and ONE all-gather per
+    batch-level (RCCL from the batch on the process group's communicator at world 1; Python
+    callbacks over gloo with two ranks on this GPU), compact and full layouts: the single-process
+    forest bit for bit."""
+    from fraud_detection_spark_kafka_llm_amd.models import forest_batch
+    from fraud_detection_spark_kafka_llm_amd.parallel.launch import spawn
+
+    monkeypatch.setattr(forest_batch, "BATCH", False)
+    monkeypatch.setattr(forest_batch, "TREES_IN_FLIGHT", 4)
+    ref = _forest("cuda:0", trees=7)
+    monkeypatch.setenv("FDX_FORCE_COLLECTIVES", "1")
+    outs = spawn(_dp_forest, world, "cuda:0", True, compact, backend=backend)
+    for trees, calls, level_calls in outs:
+        assert trees == ref
+        # 7 trees in batches of 4 x 5 levels: 2 per batch-level (+ quantisation's own)
+        assert 0 < level_calls <= 2 * 2 * 5, level_calls
+        assert calls["reduce_scatter"] <= 10, calls
+    assert all(o[1] == outs[0][1] for o in outs)
 
 
 def _booster(device, n=5000, F=300, trees=8, depth=6, seed=11, rows=None):
