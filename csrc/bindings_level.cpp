@@ -1397,6 +1397,10 @@ class RfBatch {
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_, done_})
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : timing_) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
     for (auto& ln : lanes_) ln.r->rec_ = nullptr;
   }
   RfBatch(const RfBatch&) = delete;
@@ -1515,6 +1519,21 @@ class RfBatch {
   }
 
   bool direct() const { return direct_; }
+
+  // Milliseconds of the direct collectives since the last call (every 8th timed, scaled; waits for
+  // their events)
+  double coll_ms() {
+    double ms = 0.0;
+    for (auto& e : timing_) {
+      float t = 0.f;
+      if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&t, e.first, e.second) == hipSuccess)
+        ms += 8.0 * t;
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    timing_.clear();
+    return ms;
+  }
 
   // The last grow's node tables are in the lanes' arena_host (GIL released while waiting).
   void wait() {
@@ -1695,12 +1714,27 @@ class RfBatch {
     return b.narrow(0, 0, n);
   }
 
+  // timing events around every 8th direct collective (coll_ms)
+  struct Timed {
+    RfBatch* b;
+    hipStream_t s;
+    hipEvent_t e0 = nullptr;
+    Timed(RfBatch* b_, hipStream_t s_) : b(b_), s(s_) {
+      if ((b->timed_++ & 7) == 0 && hipEventCreate(&e0) == hipSuccess) (void)hipEventRecord(e0, s);
+    }
+    ~Timed() {
+      hipEvent_t e1 = nullptr;
+      if (e0 && hipEventCreate(&e1) == hipSuccess && hipEventRecord(e1, s) == hipSuccess) b->timing_.emplace_back(e0, e1);
+    }
+  };
+
   void reduce_scatter(const Tensor& send, const Tensor& out, hipStream_t s) {
     ++rs_calls_;
     if (!direct_) {
       rs_cb_(send, out);
       return;
     }
+    Timed t(this, s);
     rccl_.check(rccl_.rs(send.data_ptr(), out.data_ptr(), (size_t)out.numel(), ncclInt64, ncclSum, rccl_.comm, s),
                 "ncclReduceScatter");
   }
@@ -1708,6 +1742,7 @@ class RfBatch {
   Tensor all_gather(const Tensor& in, hipStream_t s) {
     ++ag_calls_;
     if (!direct_) return ag_cb_(in).cast<Tensor>();
+    Timed t(this, s);
     Tensor out = buffer(allt_, S_ * in.numel()).view({S_, in.size(0), 5});
     rccl_.check(rccl_.ag(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), ncclInt64, rccl_.comm, s), "ncclAllGather");
     return out;
@@ -1828,7 +1863,8 @@ class RfBatch {
   py::object rs_cb_, ag_cb_;
   Rccl rccl_;
   Tensor send_, out_, ag_in_, allt_;
-  int64_t rs_calls_ = 0, ag_calls_ = 0;
+  int64_t rs_calls_ = 0, ag_calls_ = 0, timed_ = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_;
   // argument staging (pinned host + device, two halves by level parity)
   Tensor host_, dev_args_;
   int half_ = -1;
@@ -1866,5 +1902,6 @@ void register_level_ops(pybind11::module& m) {
       .def(py::init<const py::dict&>())
       .def("grow", &RfBatch::grow)
       .def("wait", &RfBatch::wait)
-      .def("direct", &RfBatch::direct);
+      .def("direct", &RfBatch::direct)
+      .def("coll_ms", &RfBatch::coll_ms);
 }

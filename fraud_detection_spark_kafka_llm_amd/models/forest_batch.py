@@ -212,6 +212,8 @@ def grow_forest_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tr
         pending.append((b & 1, ids))
     fb.native.wait()
     build_pending()
+    if fb.dp and fb.native.direct():
+        G.LEVEL_STATS["coll_ms"] += fb.native.coll_ms()
     return out
 
 

@@ -38,6 +38,7 @@ import torch
 
 from ..ops import native
 from ..utils import tracing
+from ..utils.memory import RG_GROUP_MAX_ENTRIES
 
 CSC_PAD = 16
 
@@ -193,7 +194,7 @@ class RowGroups:
     need more than ``RG_MAX_GROUPS`` groups (very wide vocabularies): the grower then keeps the
     CSC passes."""
 
-    def __init__(self, Q: "Quantized", max_groups: int = None, bins: int = None):
+    def __init__(self, Q: "Quantized", max_groups: int = None, bins: int = None, max_group_entries: int = None):
         C = native.lib()
         dev = Q.device
         self.timing: dict = {}
@@ -211,12 +212,17 @@ class RowGroups:
         order = np.argsort(-cnt, kind="stable")
         order = order[cnt[order] > 0]
         cum = np.concatenate([[0], np.cumsum(nb[order])])
+        # a group's entry offsets are uint32 (ptr): a group closes before RG_GROUP_MAX_ENTRIES
+        # entries, so a large shard gets more groups instead of a row limit (utils/memory.py)
+        cum_e = np.concatenate([[0], np.cumsum(cnt[order])])
+        cap_e = RG_GROUP_MAX_ENTRIES if max_group_entries is None else int(max_group_entries)
         fgroup = np.full(Fa, -1, dtype=np.int32)
         flocal = np.zeros(Fa, dtype=np.int32)
         starts = []
         i = 0
         while i < order.size and len(starts) < max_groups:
             j = int(np.searchsorted(cum, cum[i] + B, side="right")) - 1     # features [i, j) fit
+            j = min(j, int(np.searchsorted(cum_e, cum_e[i] + cap_e, side="right")) - 1)
             j = max(j, i + 1)
             fs = order[i:j]
             fgroup[fs] = len(starts)
@@ -238,8 +244,8 @@ class RowGroups:
         tick and tick("gbin")
         egroup = np.zeros(G, dtype=np.int64)
         np.add.at(egroup, fgroup[sel], cnt[sel])
-        if int(egroup.max(initial=0)) >= (1 << 31):
-            raise ValueError("row group with >= 2^31 entries: shard the rows over more ranks")
+        if int(egroup.max(initial=0)) > RG_GROUP_MAX_ENTRIES:      # (one feature alone: > 2^31 rows)
+            raise ValueError("row group over 2^31 - 1 entries: shard the rows over more ranks")
         pad = (egroup + 7) // 8 * 8                   # 16-byte aligned group starts
         gbase = np.concatenate([[0], np.cumsum(pad)]).astype(np.int64)
         self.entries = int(egroup.sum())

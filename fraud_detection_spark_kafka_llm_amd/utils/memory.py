@@ -26,7 +26,9 @@ bench/probes/mem_probe.py (profiles/r4/mem_*.jsonl):
      * the level histograms: (g, h) int64 per bin of each built node.
 
 ``max_rows_per_gpu`` inverts the model against ``torch.cuda.mem_get_info`` (or a given byte
-budget); ``min_workers`` is the fewest equal shards that fit. bench.py reports the model next to
+budget), capped at the engine's index limits (ENGINE_MAX_ROWS; a row group's entry offsets are
+kept below RG_GROUP_MAX_ENTRIES by splitting the group, which the model counts as extra groups);
+``min_workers`` is the fewest equal shards that fit. bench.py reports the model next to
 the measured peak of its timed GBDT phase (featurization + training).
 """
 from __future__ import annotations
@@ -59,6 +61,18 @@ DEFAULT_GROUPS = 11         # row groups of 8192 bins (bench corpus: ~90K bins o
 DEFAULT_BUILT_NODES = 32    # nodes built in the widest level (depth 6: 2^5)
 DEFAULT_BYTES_PER_ROW = 1940.0   # raw UTF-8 bytes per dialogue of the bench corpus
 DEFAULT_CHUNK_ROWS = 500_000     # bench featurization chunk
+# index widths of the engine: int32 row ids (CSC rows, level row lists, entry-major rows, the
+# partition's row pass), and uint32 entry offsets inside one row group (models/quantize.RowGroups
+# splits a group before it reaches this many entries, so more rows mean more groups, not a limit)
+ENGINE_MAX_ROWS = (1 << 31) - 1
+RG_GROUP_MAX_ENTRIES = (1 << 31) - 1
+
+
+def row_groups_for(nnz: int, groups: int = DEFAULT_GROUPS, sparse_frac: float = DEFAULT_SPARSE_FRAC) -> int:
+    """Row groups of a shard with ``nnz`` entries: the bin-limited groups plus the extra groups the
+    dense entries need under the per-group entry cap (RowGroups)."""
+    dense = nnz * (1.0 - sparse_frac)
+    return int(groups + max(0, math.ceil(dense / RG_GROUP_MAX_ENTRIES) - 1))
 
 
 def featurize_bytes(rows: int, nnz: int, text_bytes_per_row: float = DEFAULT_BYTES_PER_ROW,
@@ -82,7 +96,7 @@ def training_bytes(rows: int, nnz: int, hot_features: int = DEFAULT_HOT_FEATURES
     ``rf_lanes`` > 0: a RandomForest with that many trees in flight instead (its CSC work items
     and a workspace per lane on top of the shared state)."""
     per_entry = CSR_BYTES * CSR_SLACK + ORDER_BYTES + BIN_BYTES + RG_ENTRY_BYTES + RG_EROW_BYTES * sparse_frac
-    per_row = ROW_BYTES + 4.0 * groups + hot_features + LEVEL_ROW_BYTES
+    per_row = ROW_BYTES + 4.0 * row_groups_for(nnz, groups, sparse_frac) + hot_features + LEVEL_ROW_BYTES
     if rf_lanes > 0:
         per_entry += ORDER_BYTES
         per_row += RF_LANE_ROW_BYTES * rf_lanes
@@ -126,7 +140,7 @@ def max_rows_per_gpu(nnz_per_row: float, device=None, budget_bytes: Optional[int
         return 0
 
     def fits(r: int) -> bool:
-        return pipeline_bytes(r, int(r * nnz_per_row), **dict(kw)) <= budget
+        return r <= ENGINE_MAX_ROWS and pipeline_bytes(r, int(r * nnz_per_row), **dict(kw)) <= budget
 
     lo, hi = 0, 1
     while fits(hi):

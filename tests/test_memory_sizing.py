@@ -48,3 +48,19 @@ def test_rf_lanes_enter_the_sizing_rule():
     assert M.rf_lanes_that_fit(10_000_000, 16, 200 * 2 ** 30) == 16
     assert M.rf_lanes_that_fit(10_000_000, 16, 2 * 2 ** 30) == 3
     assert M.rf_lanes_that_fit(10_000_000, 16, 0) == 16          # no budget known (CPU)
+
+
+def test_max_rows_never_exceeds_the_engine_index_limits():
+    """whatever the HBM budget, the row cap stays within the engine's index
+    widths (int32 row ids); the row groups' uint32 entry offsets are no row limit because the
+    groups split (RowGroups), and the model charges the extra groups' run starts per row."""
+    huge = 64 * 2 ** 40                       # 64 TB: far beyond any device
+    cap = memory.max_rows_per_gpu(97.0, budget_bytes=huge)
+    assert 0 < cap <= memory.ENGINE_MAX_ROWS
+    assert memory.min_workers(3 * memory.ENGINE_MAX_ROWS, 0, budget_bytes=huge) >= 3
+    # 100M rows x 97 entries: the dense group's ~7.7G entries need 4 groups of < 2^31 entries
+    assert memory.row_groups_for(100_000_000 * 97) == memory.DEFAULT_GROUPS + 3
+    assert memory.row_groups_for(10_000_000 * 97) == memory.DEFAULT_GROUPS
+    small = memory.training_bytes(10_000_000, 10_000_000 * 97)
+    big = memory.training_bytes(100_000_000, 100_000_000 * 97)
+    assert big > 10 * small                   # (the extra groups' per-row run starts)

@@ -410,3 +410,24 @@ def test_gpu_row_group_level_loop_grows_the_same_trees(monkeypatch, bins, em_fra
         out[flag] = fit_gbdt(vc, torch.from_numpy(y), GBDTParams(n_estimators=4, max_depth=6, max_bin=64),
                              device="cuda:0").trees
     _same_trees(out[False], out[True])
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_row_group_entry_cap_splits_groups_same_trees(monkeypatch, device):
+    """a row group closes before RG_GROUP_MAX_ENTRIES entries (its uint32
+    offsets), so a large shard gets more groups instead of raising at 2^31 entries. Forced here to
+    a small cap: more groups, the same trees bit for bit."""
+    from fraud_detection_spark_kafka_llm_amd.models import quantize as qmod
+
+    dense, y = random_counts_matrix(4000, 300, 0.1, 23, max_count=40)
+    dense[:, :6] = np.random.default_rng(3).integers(0, 5, (4000, 6))
+    vc = vc_from_dense(dense)
+    params = GBDTParams(n_estimators=3, max_depth=5, gamma=0.0, max_bin=64)
+    ref = fit_gbdt(vc, torch.from_numpy(y), params, device=device)
+    monkeypatch.setattr(qmod, "RG_GROUP_MAX_ENTRIES", 6000)
+    capped = fit_gbdt(vc, torch.from_numpy(y), params, device=device)
+    _same_trees(ref.trees, capped.trees)
+    assert capped.shape["groups"] > ref.shape["groups"] >= 1
+    Q = quantize(vc_from_dense(dense), max_bins=64, **QKW)
+    rg = RowGroups(Q)
+    assert int(rg.group_entries.max()) <= 6000 and rg.G == capped.shape["groups"]
