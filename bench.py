@@ -328,13 +328,23 @@ def _group_confluent_runs(args, grp) -> dict:
     from fraud_detection_spark_kafka_llm_amd.stream import group as G
 
     G.group_throughput_run(grp, 60_000, tag="warm")
+    cg0 = G.cgroup_cpu()
     tp = G.group_throughput_run(grp, args.kafka_group_msgs, tag="tp")
+    cg1 = G.cgroup_cpu()
     lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
     # the config's LLM-explain stub: every 10th classification explained asynchronously in the
     # clients (offline stub backend), its record produced after the classification
     ex = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat-explain", explain="async",
                              explain_every=10)
-    return {"kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
+    place = {"kafka_confluent_group_client_dialogues_per_s": [round(v) for v in tp["client_dialogues_per_s"]],
+             "kafka_confluent_group_client_cpu_util": tp["client_cpu_util"],
+             "kafka_confluent_group_client_cpus": tp["client_cpus"],
+             "kafka_confluent_group_client_numa": tp["client_numa"],
+             "kafka_confluent_group_pinned": grp.client_cpus is not None,
+             "kafka_confluent_group_cgroup_quota_cpus": cg1.get("quota_cpus"),
+             "kafka_confluent_group_throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0))
+                                                         / 1e3, 1)}
+    return {**place, "kafka_confluent_group_dialogues_per_s": tp["dialogues_per_s"],
             "kafka_confluent_group_clients": args.kafka_group_clients,
             "kafka_confluent_group_msgs": args.kafka_group_msgs,
             "kafka_confluent_group_p50_ms": lat["p50_ms"], "kafka_confluent_group_p95_ms": lat["p95_ms"],

@@ -332,6 +332,56 @@ class GroupRendezvous:
         return [json.loads(self._wait(f"{self.key}/stats/{r}")) for r in range(1, self.world)]
 
 
+# Client placement (the consumer-group rate fell between two boxes with nothing in the
+# record to explain it). With FDX_GROUP_PIN=1 (default) every client process gets CPUs of its own
+# from the end of this process's allowed set and the scoring process keeps the rest, so a client
+# never competes with the scorer's Python threads for a core; the record carries each client's
+# CPUs, NUMA node, CPU seconds and rate, and the cgroup's CPU quota and throttling during the run.
+GROUP_PIN = os.environ.get("FDX_GROUP_PIN", "1") == "1"
+GROUP_CPUS_PER_CLIENT = int(os.environ.get("FDX_GROUP_CPUS_PER_CLIENT", "2"))
+
+
+def client_cpu_plan(allowed: list, n_clients: int, per_client: int = GROUP_CPUS_PER_CLIENT) -> tuple:
+    """(per-client CPU lists, the scorer's CPUs): clients take ``per_client`` CPUs each from the
+    end of ``allowed`` when at least as many remain for the scorer; else no pinning (None)."""
+    allowed = sorted(allowed)
+    need = n_clients * per_client
+    if n_clients <= 0 or per_client <= 0 or len(allowed) < 2 * need:
+        return None, None
+    tail = allowed[len(allowed) - need:]
+    return [tail[c * per_client:(c + 1) * per_client] for c in range(n_clients)], allowed[:len(allowed) - need]
+
+
+def numa_node_of(cpu: int, sysfs: str = "/sys/devices/system/cpu") -> int:
+    try:
+        for name in os.listdir(os.path.join(sysfs, f"cpu{cpu}")):
+            if name.startswith("node") and name[4:].isdigit():
+                return int(name[4:])
+    except OSError:
+        pass
+    return -1
+
+
+def cgroup_cpu() -> dict:
+    """The cgroup v2 CPU quota (cpus) and throttling counters of this process (empty if unknown)."""
+    out = {}
+    try:
+        with open("/proc/self/cgroup") as fh:
+            rel = fh.read().strip().split("::")[-1].strip()
+        base = os.path.join("/sys/fs/cgroup", rel.lstrip("/"))
+        with open(os.path.join(base, "cpu.max")) as fh:
+            q, per = fh.read().split()
+            out["quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+        with open(os.path.join(base, "cpu.stat")) as fh:
+            for line in fh:
+                k, v = line.split()
+                if k in ("nr_throttled", "throttled_usec", "usage_usec"):
+                    out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 class ConsumerGroup:
     """The coordinating scoring process of a consumer group: ``n_clients`` client processes, this
     process's scorer and, with ``rendezvous``, one :class:`ScorerPeer` per other rank.
@@ -377,12 +427,21 @@ class ConsumerGroup:
             base = {"layout": self.lay, "batch_max": self.batch_max, "max_latency_ms": max_latency_ms,
                     "depth": client_depth, "pool": pool_lay, "confluent": confluent, "n_clients": n_clients,
                     "peers": self.peer_sockets}
+            self._saved_affinity = None
+            plan = None
+            if GROUP_PIN and hasattr(os, "sched_getaffinity"):
+                plan, mine = client_cpu_plan(list(os.sched_getaffinity(0)), n_clients)
+                if plan is not None:
+                    self._saved_affinity = os.sched_getaffinity(0)
+                    os.sched_setaffinity(0, mine)
+            self.client_cpus = plan
             child_env = dict(os.environ, **(env or {}))
             root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             child_env["PYTHONPATH"] = root + os.pathsep + child_env.get("PYTHONPATH", "")
             for cl in self.clients:
                 a, b = socket.socketpair()
-                cfg = dict(base, index=cl.idx, shm=cl.shm.name, fd=b.fileno())
+                cfg = dict(base, index=cl.idx, shm=cl.shm.name, fd=b.fileno(),
+                           cpus=plan[cl.idx] if plan is not None else None)
                 # a fresh interpreter (never a fork of this GPU process); it touches no GPU
                 cl.proc = subprocess.Popen([sys.executable, "-m", "fraud_detection_spark_kafka_llm_amd.stream.group",
                                             json.dumps(cfg)], pass_fds=(b.fileno(),), env=child_env)
@@ -469,6 +528,10 @@ class ConsumerGroup:
         return self.loop.batches if getattr(self, "loop", None) is not None else 0
 
     def close(self) -> None:
+        saved = getattr(self, "_saved_affinity", None)
+        if saved is not None:                     # (the scorer's CPUs back as they were)
+            os.sched_setaffinity(0, saved)
+            self._saved_affinity = None
         # no DMA may still read a segment when it is unregistered and unmapped (a run that raised
         # can leave micro-batches in the scorer's pipeline); a drain that fails (e.g. after the GPU
         # error that ended run()) is logged, and the clients are still stopped and the segments
@@ -665,6 +728,10 @@ def merge_results(rs: list) -> dict:
                                                       axis=0)] if any("scorer_batches" in r for r in rs) else [],
             "p50_ms": h.percentile(50), "p95_ms": h.percentile(95), "p99_ms": h.percentile(99),
             "clients": len(rs), "client_dialogues_per_s": [r["messages"] / max(r["t1"] - r["t0"], 1e-9) for r in rs],
+            # per client: CPU seconds over its window (1.0 = one core busy), its CPUs and NUMA node
+            "client_cpu_util": [round(r.get("cpu_s", 0.0) / max(r["t1"] - r["t0"], 1e-9), 3) for r in rs],
+            "client_cpus": [r.get("cpus", []) or r.get("n_cpus", 0) for r in rs],
+            "client_numa": [r.get("numa", -1) for r in rs],
             "client_start_spread_ms": (max(r["t0"] for r in rs) - t0) * 1e3}
 
 
@@ -730,6 +797,9 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
                           max_latency_ms=spec.get("max_latency_ms", cfg["max_latency_ms"]), max_bytes=lay["max_bytes"],
                           ring=ring, **_explain_kw(spec))
     sent = 0
+    import resource
+
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     if spec["kind"] == "throughput":
         n = int(spec["n"])
         with broker.lock:
@@ -755,6 +825,9 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
         gen.join()
         sent = gen.sent
     t1 = time.perf_counter()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
     committed = sum(inner.committed_offsets().values())
     outputs = None
     if spec.get("return_outputs"):           # tests: the produced records, in partition order
@@ -766,7 +839,8 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
     loadgen._drop(url)
     return {"outputs": outputs, "t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"], "committed": committed,
             "batches": st["batches"], "sent": sent, "explanations": st["explanations"],
-            "scorer_batches": list(scorer.sent),
+            "scorer_batches": list(scorer.sent), "cpu_s": cpu_s, "n_cpus": len(cpus),
+            "cpus": cpus if len(cpus) <= 8 else [], "numa": numa_node_of(cpus[0]) if cpus else -1,
             "lat_counts": eng.stats.latency.counts.tolist(),
             "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"]}
 
@@ -880,6 +954,8 @@ def _connect_peers(cfg: dict) -> list:
 
 
 def _client_main(cfg: dict) -> int:
+    if cfg.get("cpus") and hasattr(os, "sched_setaffinity"):
+        os.sched_setaffinity(0, cfg["cpus"])
     conn = Connection(cfg["fd"])
     shm = _attach(cfg["shm"])
     pool_shm = None

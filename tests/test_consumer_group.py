@@ -268,3 +268,15 @@ def test_single_host_group_check(monkeypatch):
     assert G.single_host_group()
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
     assert not G.single_host_group()
+
+
+def test_client_cpu_plan_gives_each_client_its_own_cpus():
+    """client processes get CPUs of their own, disjoint from the scoring
+    process's (which keeps at least as many); too few CPUs: no pinning."""
+    from fraud_detection_spark_kafka_llm_amd.stream.group import client_cpu_plan
+
+    plan, mine = client_cpu_plan(list(range(16)), 3, per_client=2)
+    assert plan == [[10, 11], [12, 13], [14, 15]] and mine == list(range(10))
+    flat = [c for p in plan for c in p]
+    assert not set(flat) & set(mine) and len(set(flat)) == 6
+    assert client_cpu_plan(list(range(8)), 3, per_client=2) == (None, None)
