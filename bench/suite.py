@@ -162,6 +162,10 @@ def bench_rf(args) -> dict:
     torch.cuda.reset_peak_memory_stats(dev)
     grower.reset_level_stats()
     D.reset_bytes()
+    from fraud_detection_spark_kafka_llm_amd.models import forest_batch
+
+    for k in forest_batch.HOST_TIMES:
+        forest_batch.HOST_TIMES[k] = 0.0
     res = fit_forest(vc, y, num_trees=trees, max_depth=5, max_bins=32, bootstrap=True, feature_subset=args.subset,
                      seed=42, device=dev)
     _sync(dev)
@@ -176,7 +180,8 @@ def bench_rf(args) -> dict:
            "level_collective_ms": _max_over_ranks(grower.level_collective_ms(), dev),
            "listed_passes": grower.LEVEL_STATS["listed_passes"],
            "listed_active_items": grower.LEVEL_STATS["listed_active_items"],
-           "listed_grid_waves": grower.LEVEL_STATS["listed_grid_waves"]}
+           "listed_grid_waves": grower.LEVEL_STATS["listed_grid_waves"],
+           "batch_host_s": {k: round(v, 4) for k, v in forest_batch.HOST_TIMES.items()}}
     if rank == 0:
         tv, ty, _ = _tfidf(200_000, dev, seed=21, first_row=10 ** 9, idf=idf)
         raw = score_csr(tv, ensemble_arrays(res.trees, "normalized")).cpu().numpy()

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <map>
 #include <thread>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -145,6 +146,10 @@ class RfLevels {
  public:
   LaneRec* rec_ = nullptr;       // set by RfBatch while it drives this lane: launches are recorded
   const int64_t* plan_root_tot_ = nullptr;   // (RfBatch, DP root level) LevelPlanArgs root_tot
+  fdx::LevelPlanArgs plan_base_{};           // plan_args' fixed fields (built on first use)
+  bool plan_base_ready_ = false;
+  int32_t* counts_ptr_ = nullptr;
+  int64_t counts_w_ = 0;
   friend class RfBatch;
 
   explicit RfLevels(const py::dict& c) {
@@ -743,8 +748,44 @@ class RfLevels {
 
   fdx::LevelPlanArgs plan_args(int64_t d, int64_t n_open, const Tensor& packed, const Tensor& open,
                                const Tensor& n_open_ptr, const Tensor& next_open, const Tensor& next_totals) {
-    const Tensor& counts = st_["counts"];
-    fdx::LevelPlanArgs a{};
+    if (!plan_base_ready_) {               // (the node table and level tables never move: once)
+      fdx::LevelPlanArgs& a = plan_base_;
+      a = fdx::LevelPlanArgs{};
+      a.max_depth = max_depth_;
+      a.mode = mode_;
+      a.build_all = build_all_ ? 1 : 0;
+      a.kexp = p<int32_t>(kexp_);
+      a.min_gain = min_gain_;
+      a.zbin = p<int32_t>(zbin_);
+      a.hot_row = p<int32_t>(hot_row_);
+      a.max_nodes = (int32_t)st_["parent"].numel();
+      a.n_nodes = p<int32_t>(st_["n_nodes"]);
+      a.stats = p<int64_t>(st_["stats"]);
+      a.parent = p<int32_t>(st_["parent"]);
+      a.left = p<int32_t>(st_["left"]);
+      a.right = p<int32_t>(st_["right"]);
+      a.feat = p<int32_t>(st_["feat"]);
+      a.bin = p<int32_t>(st_["bin"]);
+      a.leaf = p<uint8_t>(st_["leaf"]);
+      a.gain = p<double>(st_["gain"]);
+      a.default_child = p<int32_t>(st_["default_child"]);
+      a.node_dense = p<int32_t>(node_dense_);
+      a.cs_feat = p<int32_t>(st_["cs_feat"]);
+      a.cs_default = p<int32_t>(st_["cs_default"]);
+      a.cs_other = p<int32_t>(st_["cs_other"]);
+      a.cs_bin = p<int32_t>(st_["cs_bin"]);
+      a.cs_left_default = p<int32_t>(st_["cs_left_default"]);
+      a.node_slot = p<int32_t>(st_["node_slot"]);
+      a.s2n = p<int32_t>(st_["s2n"]);
+      a.sub_dst = p<int32_t>(st_["sub_dst"]);
+      a.sub_par = p<int32_t>(st_["sub_par"]);
+      a.sub_sib = p<int32_t>(st_["sub_sib"]);
+      a.sub_of = p<int32_t>(sub_of_);
+      counts_ptr_ = p<int32_t>(st_["counts"]);
+      counts_w_ = st_["counts"].size(1);
+      plan_base_ready_ = true;
+    }
+    fdx::LevelPlanArgs a = plan_base_;
     a.packed = p<int64_t>(packed);
     a.L = (int32_t)n_open;
     a.n_shards = packed.dim() == 3 ? (int32_t)packed.size(0) : 1;
@@ -752,41 +793,11 @@ class RfLevels {
     FDX_CHECK(packed.size(-1) == 5 && packed.stride(-1) == 1 && packed.stride(-2) == 5 && packed.size(-2) >= n_open,
               "packed rows of 5");
     a.depth = (int32_t)d;
-    a.max_depth = max_depth_;
-    a.mode = mode_;
-    a.build_all = build_all_ ? 1 : 0;
-    a.kexp = p<int32_t>(kexp_);
-    a.min_gain = min_gain_;
-    a.zbin = p<int32_t>(zbin_);
-    a.hot_row = p<int32_t>(hot_row_);
-    a.max_nodes = (int32_t)st_["parent"].numel();
-    a.n_nodes = p<int32_t>(st_["n_nodes"]);
-    a.stats = p<int64_t>(st_["stats"]);
-    a.parent = p<int32_t>(st_["parent"]);
-    a.left = p<int32_t>(st_["left"]);
-    a.right = p<int32_t>(st_["right"]);
-    a.feat = p<int32_t>(st_["feat"]);
-    a.bin = p<int32_t>(st_["bin"]);
-    a.leaf = p<uint8_t>(st_["leaf"]);
-    a.gain = p<double>(st_["gain"]);
     a.open = p<int32_t>(open);
     a.n_open = p<int32_t>(n_open_ptr);
-    a.default_child = p<int32_t>(st_["default_child"]);
-    a.node_dense = p<int32_t>(node_dense_);
-    a.cs_feat = p<int32_t>(st_["cs_feat"]);
-    a.cs_default = p<int32_t>(st_["cs_default"]);
-    a.cs_other = p<int32_t>(st_["cs_other"]);
-    a.cs_bin = p<int32_t>(st_["cs_bin"]);
-    a.cs_left_default = p<int32_t>(st_["cs_left_default"]);
-    a.counts = p<int32_t>(counts) + d * counts.size(1);
+    a.counts = counts_ptr_ + d * counts_w_;
     a.next_open = p<int32_t>(next_open);
     a.next_totals = p<int64_t>(next_totals);
-    a.node_slot = p<int32_t>(st_["node_slot"]);
-    a.s2n = p<int32_t>(st_["s2n"]);
-    a.sub_dst = p<int32_t>(st_["sub_dst"]);
-    a.sub_par = p<int32_t>(st_["sub_par"]);
-    a.sub_sib = p<int32_t>(st_["sub_sib"]);
-    a.sub_of = p<int32_t>(sub_of_);
     a.root_tot = plan_root_tot_;
     return a;
   }
@@ -1406,19 +1417,25 @@ class RfBatch {
   RfBatch(const RfBatch&) = delete;
   RfBatch& operator=(const RfBatch&) = delete;
 
-  // Grows trees[l] on lane l (l < number of trees <= lanes): every launch queued on the current
-  // stream, host waits (GIL released) only for each level's counts. The lanes' node tables are
-  // copied into their arena_host[parity] at the end (wait()); on_wait (if not None) is called once,
-  // before the first host wait (the caller builds the previous batch's trees meanwhile). Returns the level counters: levels,
-  // built nodes, listed passes, listed active items, listed grid waves, reduce-scatters,
-  // all-gathers.
-  std::vector<int64_t> grow(const std::vector<int64_t>& trees, const Tensor& label, const optional<Tensor>& weight,
-                            bool bootstrap, int64_t row0, int64_t parity, const py::object& on_wait) {
+  // A batch of trees in three calls, so that a driver can interleave two batches on one stream
+  // (the host prepares one batch's level while the GPU runs the other's):
+  //   start(trees)  lane l grows trees[l] (l < number of trees <= lanes): node-table images in, the
+  //                 prologue (bootstrap counts, digits, row_node = 0, root) and the root's sample
+  //                 queued; level 0 too unless it needs the root's compact layout sizes first;
+  //   step()        waits (GIL released) for the last queued level's counts and queues the next
+  //                 level of the lanes whose trees go on; false when every tree is finished;
+  //   finish(p)     queues the node tables into the lanes' arena_host[p] and records the batch's
+  //                 event (wait()); returns the level counters since start: levels, built nodes,
+  //                 listed passes, listed active items, listed grid waves, reduce-scatters,
+  //                 all-gathers.
+  void start(const std::vector<int64_t>& trees, const Tensor& label, const optional<Tensor>& weight, bool bootstrap,
+             int64_t row0) {
     const int64_t L = (int64_t)trees.size();
-    FDX_CHECK(L >= 1 && L <= (int64_t)lanes_.size(), "RfBatch.grow: 1 .. lanes trees");
+    FDX_CHECK(L >= 1 && L <= (int64_t)lanes_.size(), "RfBatch.start: 1 .. lanes trees");
     c10::hip::HIPGuard guard(lanes_[0].r->dev_.index());
     const hipStream_t s = cur_stream(lanes_[0].r->dev_);
-    std::vector<int64_t> stat(7, 0);
+    stat_.assign(7, 0);
+    n_trees_ = L;
     live_.clear();
     for (int64_t l = 0; l < L; ++l) {
       Lane& ln = lanes_[l];
@@ -1426,10 +1443,7 @@ class RfBatch {
       ln.n_open = ln.n_build = 1;
       live_.push_back((int)l);
     }
-    level_ = 0;
     begin_region();
-    // tree prologue: the node-table image in, the quantisation (bootstrap counts, digits, row_node
-    // = 0, open[0] = root; single process: the root histogram zeroed), then the root's sample
     for (int l : live_) {
       Lane& ln = lanes_[l];
       // (the node-table image first: one batched copy kernel, recorded like the count rows)
@@ -1442,66 +1456,47 @@ class RfBatch {
                          sh_sizes(ln, 0), sh_sizes_host(ln, 0), max_shard_features_, s);
     }
     flush(s);
-    if (dp_ && compact_) FDX_CHECK(hipEventRecord(ev_, s) == hipSuccess, "event");
-    for (int64_t d = 0; d < D_; ++d) {
-      const int cur = (int)(d & 1), nxt = cur ^ 1;
-      const bool more = d + 1 < D_;
-      if (d > 0 || (dp_ && compact_)) {
-        if (!on_wait.is_none() && !on_wait_done_) {
-          on_wait_done_ = true;
-          on_wait();
-        }
-        py::gil_scoped_release nogil;
-        wait_event(ev_);
-      }
-      level_ = d;
-      begin_region();
-      if (d > 0) {               // the counts of the previous plan, the lanes whose trees go on
-        std::vector<int> still;
-        for (int l : live_) {
-          Lane& ln = lanes_[l];
-          const Tensor& ch = ln.r->st_["counts_host"];
-          const int32_t* row = p<int32_t>(ch) + (d - 1) * ch.size(1);
-          ln.n_open = row[1];
-          ln.n_build = row[2];
-          if (ln.n_open > 0) still.push_back(l);
-        }
-        live_ = still;
-      }
-      if (live_.empty()) break;
+    d_ = 0;
+    if (dp_ && compact_) {
+      FDX_CHECK(hipEventRecord(ev_, s) == hipSuccess, "event");        // (level 0 needs the root's sizes)
+    } else {
+      run_level(s);
+    }
+  }
+
+  bool step() {
+    if (d_ >= D_ || live_.empty()) return false;
+    c10::hip::HIPGuard guard(lanes_[0].r->dev_.index());
+    const hipStream_t s = cur_stream(lanes_[0].r->dev_);
+    {
+      const auto t0 = std::chrono::steady_clock::now();
+      py::gil_scoped_release nogil;
+      wait_event(ev_);
+      host_s_[2] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    if (d_ > 0) {                // the counts of the previous plan, the lanes whose trees go on
+      std::vector<int> still;
       for (int l : live_) {
         Lane& ln = lanes_[l];
-        stat[0] += 1;
-        stat[1] += ln.n_build;
-        ln.npx.assign(ln.r->groups_.size(), -1);
-        if (presel_ && d > 0) {
-          const Tensor& ch = ln.r->st_["counts_host"];
-          const int32_t* row = p<int32_t>(ch) + (d - 1) * ch.size(1);
-          int j = 0;
-          for (size_t gi = 0; gi < ln.r->groups_.size(); ++gi) {
-            if (!ln.sel[gi]) continue;
-            int32_t m = 0, sum = 0;
-            for (int x = 0; x < 8; ++x) {
-              m = std::max(m, row[4 + 8 * j + x]);
-              sum += row[4 + 8 * j + x];
-            }
-            ln.npx[gi] = m;
-            ln.sel_j.resize(ln.r->groups_.size());
-            ln.sel_j[gi] = j;
-            if (m) {
-              stat[2] += 1;
-              stat[3] += sum;
-              stat[4] += (m + 3) / 4 * 8 * 4;
-            }
-            ++j;
-          }
-        }
+        const Tensor& ch = ln.r->st_["counts_host"];
+        const int32_t* row = p<int32_t>(ch) + (d_ - 1) * ch.size(1);
+        ln.n_open = row[1];
+        ln.n_build = row[2];
+        if (ln.n_open > 0) still.push_back(l);
       }
-      level(d, cur, nxt, more, s, stat);
+      live_ = still;
+      if (live_.empty()) return false;
     }
-    // the node tables to the host (one batched copy kernel into the mapped pinned tables)
+    run_level(s);
+    return true;
+  }
+
+  std::vector<int64_t> finish(int64_t parity) {
+    c10::hip::HIPGuard guard(lanes_[0].r->dev_.index());
+    const hipStream_t s = cur_stream(lanes_[0].r->dev_);
+    begin_region();
     live_.clear();
-    for (int64_t l = 0; l < L; ++l) {
+    for (int64_t l = 0; l < n_trees_; ++l) {
       Lane& ln = lanes_[l];
       ln.r->rec_ = nullptr;
       ln.rec.add(kRecCopy,
@@ -1509,16 +1504,34 @@ class RfBatch {
       live_.push_back((int)l);
     }
     flush(s);
+    live_.clear();
     FDX_CHECK(hipEventRecord(done_, s) == hipSuccess, "event");
-    if (!on_wait.is_none() && !on_wait_done_) on_wait();
-    on_wait_done_ = false;
-    stat[5] = rs_calls_;
-    stat[6] = ag_calls_;
+    stat_[5] = rs_calls_;
+    stat_[6] = ag_calls_;
     rs_calls_ = ag_calls_ = 0;
-    return stat;
+    return stat_;
+  }
+
+  // start + every step + finish (one batch alone); on_wait (if not None) is called once, before
+  // the first host wait (the caller builds the previous batch's trees meanwhile)
+  std::vector<int64_t> grow(const std::vector<int64_t>& trees, const Tensor& label, const optional<Tensor>& weight,
+                            bool bootstrap, int64_t row0, int64_t parity, const py::object& on_wait) {
+    start(trees, label, weight, bootstrap, row0);
+    if (!on_wait.is_none()) on_wait();
+    while (step()) {
+    }
+    return finish(parity);
   }
 
   bool direct() const { return direct_; }
+
+  // host seconds since the last call: queuing the levels (recording + flushes), of which the
+  // flushes (argument packing, copies, launches), and the waits for level counts
+  std::vector<double> host_times() {
+    std::vector<double> out{host_s_[0], host_s_[1], host_s_[2]};
+    host_s_[0] = host_s_[1] = host_s_[2] = 0.0;
+    return out;
+  }
 
   // Milliseconds of the direct collectives since the last call (every 8th timed, scaled; waits for
   // their events)
@@ -1556,6 +1569,16 @@ class RfBatch {
     std::vector<optional<Tensor>> sel, listed, listed_cnt;
     Tensor sh_local[2], sh_sizes[2], sh_sizes_host[2];
     LaneRec rec;
+    // views of the lane's fixed buffers, made once (an ATen view costs ~1-2 us of host time and a
+    // level asked for ~15 per lane)
+    std::unordered_map<uint64_t, Tensor> views;
+    template <class F>
+    const Tensor& view(uint64_t tag, int64_t a, int64_t b, F make) {
+      const uint64_t key = (tag << 56) | ((uint64_t)(a & 0xffffff) << 28) | (uint64_t)(b & 0xfffffff);
+      auto it = views.find(key);
+      if (it != views.end()) return it->second;
+      return views.emplace(key, make()).first->second;
+    }
     int64_t tree = 0;
     int32_t n_open = 0, n_build = 0;
     std::vector<int32_t> npx;
@@ -1579,6 +1602,44 @@ class RfBatch {
     half_ = (half_ + 1) % kRegions;
     off_ = 0;
     if (half_used_[half_]) (void)hipEventSynchronize(half_ev_[half_]);
+  }
+
+  // Queues level d_ of the live lanes (their n_open / n_build read) and advances d_.
+  void run_level(hipStream_t s) {
+    const int64_t d = d_;
+    begin_region();
+    for (int l : live_) {
+      Lane& ln = lanes_[l];
+      stat_[0] += 1;
+      stat_[1] += ln.n_build;
+      ln.npx.assign(ln.r->groups_.size(), -1);
+      ln.sel_j.assign(ln.r->groups_.size(), -1);
+      if (presel_ && d > 0) {
+        const Tensor& ch = ln.r->st_["counts_host"];
+        const int32_t* row = p<int32_t>(ch) + (d - 1) * ch.size(1);
+        int j = 0;
+        for (size_t gi = 0; gi < ln.r->groups_.size(); ++gi) {
+          if (!ln.sel[gi]) continue;
+          int32_t m = 0, sum = 0;
+          for (int x = 0; x < 8; ++x) {
+            m = std::max(m, row[4 + 8 * j + x]);
+            sum += row[4 + 8 * j + x];
+          }
+          ln.npx[gi] = m;
+          ln.sel_j[gi] = j;
+          if (m) {
+            stat_[2] += 1;
+            stat_[3] += sum;
+            stat_[4] += (m + 3) / 4 * 8 * 4;
+          }
+          ++j;
+        }
+      }
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    level(d, (int)(d & 1), (int)(d & 1) ^ 1, d + 1 < D_, s, stat_);
+    host_s_[0] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    ++d_;
   }
 
   void level(int64_t d, int cur, int nxt, bool more, hipStream_t s, std::vector<int64_t>& stat) {
@@ -1618,7 +1679,9 @@ class RfBatch {
         const bool items = ln.r->groups_[gi].start.numel() > 0;
         if (items && presel_ && d > 0 && ln.sel[gi]) {
           lists.push_back(ln.sel[gi]);
-          cnts.push_back(ln.r->st_["counts"].select(0, d - 1).narrow(0, 4 + 8 * ln.sel_j[gi], 8));
+          cnts.push_back(ln.view(1, d, ln.sel_j[gi], [&] {
+            return ln.r->st_["counts"].select(0, d - 1).narrow(0, 4 + 8 * ln.sel_j[gi], 8);
+          }));
           npxs.push_back(ln.npx[gi]);
         } else if (items && ln.n_open <= listed_max_) {
           lists.push_back(ln.listed[gi]);
@@ -1633,13 +1696,15 @@ class RfBatch {
       const optional<Tensor> pack = d > 0 ? optional<Tensor>(ln.rowpack) : c10::nullopt;
       const Tensor& mask = ln.mask[cur];
       if (!dp_) {
-        const Tensor s2n = d == 0 ? zero1_ : ln.r->st_["s2n"].narrow(0, 0, ln.n_build);
-        ln.r->hist(ln.n_build, ln.hist->narrow(0, 0, ln.n_open), boff_, mask, s2n, pack, lists, cnts, npxs,
-                   c10::nullopt, 0);
+        const Tensor& s2n =
+            d == 0 ? zero1_ : ln.view(2, ln.n_build, 0, [&] { return ln.r->st_["s2n"].narrow(0, 0, ln.n_build); });
+        ln.r->hist(ln.n_build, ln.view(3, ln.n_open, 0, [&] { return ln.hist->narrow(0, 0, ln.n_open); }), boff_, mask,
+                   s2n, pack, lists, cnts, npxs, c10::nullopt, 0);
       } else {
         const Tensor tgt = send.view({-1, Bs, 2}).narrow(0, ln.row0, S_ * R - ln.row0);
         const Tensor& hb = compact_ ? ln.sh_local[cur] : sh_local_full_;
-        ln.r->hist(ln.n_build, tgt, hb, mask, iota_.narrow(0, 0, ln.n_build), pack, lists, cnts, npxs, shard_of_, R * Bs);
+        ln.r->hist(ln.n_build, tgt, hb, mask, ln.view(4, ln.n_build, 0, [&] { return iota_.narrow(0, 0, ln.n_build); }),
+                   pack, lists, cnts, npxs, shard_of_, R * Bs);
         if (d == 0)
           ln.rec.add(kRecRootSend, fdx::RootSendLane{ln.r->root_pending_, p<int64_t>(send), (int32_t)S_, R * Bs * 2,
                                                      ln.tb * 2});
@@ -1653,28 +1718,33 @@ class RfBatch {
       Tensor ag_in = buffer(ag_in_, nopen * 5).view({nopen, 5});
       for (int l : live_) {
         Lane& ln = lanes_[l];
-        const Tensor open = ln.open[cur].narrow(0, 0, ln.n_open);
-        const Tensor totals = d == 0 ? out.view({-1, 2}).narrow(0, ln.tb, 1) : ln.totals[cur].narrow(0, 0, ln.n_open);
-        const Tensor split_boff = compact_ ? ln.sh_local[cur].narrow(0, f0_, Fa_s_ + 1) : sh_boff_;
+        const Tensor& open = ln.view(5, cur, ln.n_open, [&] { return ln.open[cur].narrow(0, 0, ln.n_open); });
+        const Tensor totals = d == 0 ? out.view({-1, 2}).narrow(0, ln.tb, 1)
+                                     : ln.view(6, cur, ln.n_open, [&] { return ln.totals[cur].narrow(0, 0, ln.n_open); });
+        const Tensor& split_boff =
+            compact_ ? ln.view(7, cur, 0, [&] { return ln.sh_local[cur].narrow(0, f0_, Fa_s_ + 1); }) : sh_boff_;
         ln.r->split(out.narrow(0, ln.row0, ln.n_build), totals, split_boff, sh_nbins_, sh_zbin_, sh_fid_, open,
-                    ln.thr[cur].narrow(0, 0, ln.n_open), ln.tree, f0_, ag_in.narrow(0, ln.l0, ln.n_open),
-                    c10::nullopt, wide_);
+                    ln.view(8, cur, ln.n_open, [&] { return ln.thr[cur].narrow(0, 0, ln.n_open); }), ln.tree, f0_,
+                    ag_in.narrow(0, ln.l0, ln.n_open), c10::nullopt, wide_);
       }
       flush(s);
       allt = all_gather(ag_in, s);
     }
     for (int l : live_) {
       Lane& ln = lanes_[l];
-      const Tensor open = ln.open[cur].narrow(0, 0, ln.n_open);
-      const Tensor n_open_ptr = d == 0 ? one_ : ln.r->st_["counts"].select(0, d - 1).narrow(0, 1, 1);
+      const Tensor& open = ln.view(5, cur, ln.n_open, [&] { return ln.open[cur].narrow(0, 0, ln.n_open); });
+      const Tensor& n_open_ptr =
+          d == 0 ? one_ : ln.view(9, d, 0, [&] { return ln.r->st_["counts"].select(0, d - 1).narrow(0, 1, 1); });
       std::vector<optional<Tensor>> sel;
       if (presel_ && more) sel = ln.sel;
       const optional<Tensor> thr_n = more ? optional<Tensor>(ln.thr[nxt]) : c10::nullopt;
       const optional<Tensor> mask_n = more ? optional<Tensor>(ln.mask[nxt]) : c10::nullopt;
       if (!dp_) {
-        const Tensor totals = d == 0 ? ln.r->st_["stats"].narrow(0, 0, 1) : ln.totals[cur].narrow(0, 0, ln.n_open);
-        ln.r->split_plan(d, ln.n_open, ln.hist->narrow(0, 0, ln.n_open), totals, boff_,
-                         ln.thr[cur].narrow(0, 0, ln.n_open), ln.tree, ln.packed->narrow(0, 0, ln.n_open), wide_, open,
+        const Tensor& totals = d == 0 ? ln.view(10, 0, 0, [&] { return ln.r->st_["stats"].narrow(0, 0, 1); })
+                                      : ln.view(6, cur, ln.n_open, [&] { return ln.totals[cur].narrow(0, 0, ln.n_open); });
+        ln.r->split_plan(d, ln.n_open, ln.view(3, ln.n_open, 0, [&] { return ln.hist->narrow(0, 0, ln.n_open); }), totals,
+                         boff_, ln.view(8, cur, ln.n_open, [&] { return ln.thr[cur].narrow(0, 0, ln.n_open); }), ln.tree,
+                         ln.view(11, ln.n_open, 0, [&] { return ln.packed->narrow(0, 0, ln.n_open); }), wide_, open,
                          n_open_ptr, ln.open[nxt], ln.totals[nxt], more, thr_n, mask_n, sel, c10::nullopt);
       } else {
         ln.r->root_pending_ = nullptr;
@@ -1692,7 +1762,9 @@ class RfBatch {
     for (int l : live_) {
       Lane& ln = lanes_[l];
       const optional<Tensor> zero =
-          (!dp_ && more) ? optional<Tensor>(ln.hist->narrow(0, 0, 2 * (int64_t)ln.n_open)) : c10::nullopt;
+          (!dp_ && more) ? optional<Tensor>(ln.view(3, 2 * (int64_t)ln.n_open, 0,
+                                                    [&] { return ln.hist->narrow(0, 0, 2 * (int64_t)ln.n_open); }))
+                         : c10::nullopt;
       ln.r->partition(d, ln.n_open, more, zero, true, c10::nullopt);
     }
     flush(s);
@@ -1752,6 +1824,12 @@ class RfBatch {
   // launch (the lanes recorded the same sequence). The argument arrays go to the device in one copy.
   void flush(hipStream_t s) {
     if (live_.empty()) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Acc {
+      double& a;
+      std::chrono::steady_clock::time_point t;
+      ~Acc() { a += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count(); }
+    } acc{host_s_[1], t0};
     const int L = (int)live_.size();
     const auto& E0 = lanes_[live_[0]].rec.entries;
     for (int l : live_) {
@@ -1853,7 +1931,9 @@ class RfBatch {
 
   std::vector<Lane> lanes_;
   std::vector<int> live_;
-  int64_t D_ = 5, listed_max_ = 2, level_ = 0;
+  int64_t D_ = 5, listed_max_ = 2, d_ = 0, n_trees_ = 0;
+  double host_s_[3] = {0.0, 0.0, 0.0};
+  std::vector<int64_t> stat_;
   bool presel_ = true, dp_ = false, compact_ = false, direct_ = false;
   Tensor boff_, one_, zero1_, iota_;
   optional<Tensor> wide_;
@@ -1870,7 +1950,6 @@ class RfBatch {
   int half_ = -1;
   int64_t off_ = 0;
   bool half_used_[kRegions] = {};
-  bool on_wait_done_ = false;
   hipEvent_t ev_ = nullptr, half_ev_[kRegions] = {}, done_ = nullptr;
   at::TensorOptions i64_;
   std::map<void*, void*> mapped_;
@@ -1901,7 +1980,11 @@ void register_level_ops(pybind11::module& m) {
   py::class_<RfBatch>(m, "RfBatch")
       .def(py::init<const py::dict&>())
       .def("grow", &RfBatch::grow)
+      .def("start", &RfBatch::start)
+      .def("step", &RfBatch::step)
+      .def("finish", &RfBatch::finish)
       .def("wait", &RfBatch::wait)
       .def("direct", &RfBatch::direct)
-      .def("coll_ms", &RfBatch::coll_ms);
+      .def("coll_ms", &RfBatch::coll_ms)
+      .def("host_times", &RfBatch::host_times);
 }

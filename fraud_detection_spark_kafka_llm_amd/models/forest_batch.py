@@ -63,6 +63,11 @@ LANE_GROUPS = int(os.environ.get("FDX_RF_GROUPS", "2"))
 # every stage of a level is ONE lane-batched launch for all the trees in flight and the level loop
 # runs in C++ (0: the per-tree lanes driven from Python)
 BATCH = os.environ.get("FDX_RF_BATCH", "1") == "1"
+# ... in this many batches that take turns on the stream (1: the host-side level work is ~0.15 ms
+# per batch-level, RfBatch.host_times; 2 batches of 8 measured 0.26 vs 0.22 s on the DP=8 shard,
+# profiles/r6/rf_batches_sweep.txt): while the host waits for one batch's
+# level counts and queues its next level, the GPU runs the other batch's level
+BATCHES = int(os.environ.get("FDX_RF_BATCHES", "1"))
 
 
 class ForestLanes:
@@ -95,7 +100,7 @@ class ForestBatch:
     per ForestLanes and tree parameters): per lane the level buffers of grower._rf_runner_levels
     plus two pinned node-table copies (the host builds one batch's trees while the next grows)."""
 
-    def __init__(self, Q: Quantized, lanes: ForestLanes, params: GrowParams, coll=None, shards: list = None):
+    def __init__(self, Q: Quantized, wss: list, params: GrowParams, coll=None, shards: list = None):
         dev = Q.device
         presel = G.PRESELECT and Q.n_rows >= G.PRESELECT_MIN_ROWS
         item_groups = Q.groups + Q.hot_groups
@@ -106,7 +111,9 @@ class ForestBatch:
         D = int(params.max_depth)
         self.Q, self.params, self.dp = Q, params, dp
         self.views, lane_cfg = [], []
-        for i, ws in enumerate(lanes.ws):
+        self.n_lanes = len(wss)
+        self.parity = 0
+        for i, ws in enumerate(wss):
             st = getattr(ws, "_levels", None)
             if st is None or st.max_depth != D or st.n_sel != len(sel_ids):
                 st = ws._levels = G.LevelState(Q, D, len(sel_ids))
@@ -139,9 +146,9 @@ class ForestBatch:
                 lc["hist"] = torch.empty((max(1, 1 << (D - 1)), Q.TB, 2), dtype=torch.int64, device=dev)
                 lc["packed"] = torch.empty((st.cap, 5), dtype=torch.int64, device=dev)
             lane_cfg.append(lc)
-        st0 = lanes.ws[0]._levels
+        st0 = wss[0]._levels
         cfg = dict(lanes=lane_cfg, max_depth=D, boff=Q.boff, listed_max_nodes=G.LISTED_MAX_NODES, presel=bool(sel_ids),
-                   one=st0.one, zero1=st0.zero1, iota=lanes.ws[0].iota(64), dp=dp)
+                   one=st0.one, zero1=st0.zero1, iota=wss[0].iota(64), dp=dp)
         if dp:
             sh = shards[0]
             cfg.update(S=int(sh.S), Bs=int(sh.Bs), max_nb=int(sh.max_nb), compact=bool(compact), shard_of=sh._shard_of,
@@ -168,37 +175,44 @@ class ForestBatch:
 
 def grow_forest_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tree_ids: list, label: torch.Tensor,
                         weight: Optional[torch.Tensor], bootstrap: bool, coll=None) -> list:
-    """Grows ``tree_ids`` in lockstep batches of ``len(lanes.ws)`` trees (RfBatch); returns them in
-    order. Batch b + 1's levels run while the host builds batch b's trees (at its first wait)."""
+    """Grows ``tree_ids`` in lockstep batches (RfBatch); returns them in order. The lanes are split
+    into BATCHES batches that take turns on the one stream: each turn waits for one batch's level
+    counts and queues its next level, so the GPU runs the other batch's level meanwhile; a batch
+    whose trees finished queues its node tables and starts the next trees at once, and the host
+    builds the finished trees while that batch's new root level runs. The turn order depends on
+    the tree shapes only, so under data parallelism every rank issues the same collectives."""
     use_coll = coll is not None and coll.active
     shards = build_shared_state(Q, lanes, coll if use_coll else None)
-    key = (params.max_depth, params.mode, params.min_gain, params.min_child, params.seed, params.feat_k,
-           shards[0] is not None)
-    fb = getattr(lanes, "_batch", None)
-    if fb is None or fb[0] != key:
-        fb = lanes._batch = (key, ForestBatch(Q, lanes, params, coll if use_coll else None, shards))
-    fb = fb[1]
-    fb.bind(coll if use_coll else None)
     nl = len(lanes.ws)
-    out: list = []
-    pending = []
-
-    def build_pending() -> None:
-        # (called inside the next grow, before its first host wait: the previous batch's node
-        # tables were queued before this batch's launches -- its event, not yet re-recorded)
-        fb.native.wait()
-        while pending:
-            par, ids = pending.pop(0)
-            for lane, t in enumerate(ids):
-                out.append(G.tree_from_host(Q, params, fb.views[lane][par]))
-
+    nb = max(1, min(BATCHES, nl))
+    key = (params.max_depth, params.mode, params.min_gain, params.min_child, params.seed, params.feat_k,
+           shards[0] is not None, nb)
+    cached = getattr(lanes, "_batch", None)
+    if cached is None or cached[0] != key:
+        parts = [range(g * nl // nb, (g + 1) * nl // nb) for g in range(nb)]
+        cached = lanes._batch = (key, [ForestBatch(Q, [lanes.ws[i] for i in r], params, coll if use_coll else None,
+                                                   [shards[i] for i in r]) for r in parts])
+    fbs = cached[1]
+    for fb in fbs:
+        fb.bind(coll if use_coll else None)
     from ..parallel import dist as D
 
-    for b, i in enumerate(range(0, len(tree_ids), nl)):
-        ids = tree_ids[i:i + nl]
+    todo = deque(tree_ids)
+    out: dict = {}
+    running: list = [None] * nb
+
+    def launch(i: int) -> None:
+        running[i] = None
+        if not todo:
+            return
+        fb = fbs[i]
+        ids = [todo.popleft() for _ in range(min(fb.n_lanes, len(todo)))]
+        fb.parity ^= 1
         with tracing.span("forest.batch", trees=len(ids)):
-            stat = fb.native.grow(ids, label, weight, bool(bootstrap), int(Q.row0), b & 1,
-                                  build_pending if pending else None)
+            fb.native.start(ids, label, weight, bool(bootstrap), int(Q.row0))
+        running[i] = ids
+
+    def account(fb, stat) -> None:
         G.LEVEL_STATS["levels"] += stat[0]
         G.LEVEL_STATS["built_nodes"] += stat[1]
         G.LEVEL_STATS["hist_bytes"] += stat[1] * Q.TB * 16
@@ -209,12 +223,33 @@ def grow_forest_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tr
             G.LEVEL_STATS["coll_calls"] += stat[5] + stat[6]
             D.CALLS["reduce_scatter"] += stat[5]
             D.CALLS["all_gather"] += stat[6]
-        pending.append((b & 1, ids))
-    fb.native.wait()
-    build_pending()
-    if fb.dp and fb.native.direct():
-        G.LEVEL_STATS["coll_ms"] += fb.native.coll_ms()
-    return out
+
+    for i in range(nb):
+        launch(i)
+    while any(r is not None for r in running):
+        for i in range(nb):
+            ids = running[i]
+            if ids is None or fbs[i].native.step():
+                continue
+            fb = fbs[i]
+            par = fb.parity
+            account(fb, fb.native.finish(par))
+            launch(i)                     # the slot's next trees, queued before the host builds these
+            fb.native.wait()              # (its event: the node tables just queued, not re-recorded yet)
+            for lane, t in enumerate(ids):
+                out[t] = G.tree_from_host(Q, params, fb.views[lane][par])
+    for fb in fbs:
+        if fb.dp and fb.native.direct():
+            G.LEVEL_STATS["coll_ms"] += fb.native.coll_ms()
+        lv, fl, wt = fb.native.host_times()
+        HOST_TIMES["levels_s"] += lv
+        HOST_TIMES["flush_s"] += fl
+        HOST_TIMES["wait_s"] += wt
+    return [out[t] for t in tree_ids]
+
+
+# host seconds of the lockstep batches (RfBatch.host_times): queuing levels, of which flushes, waits
+HOST_TIMES = {"levels_s": 0.0, "flush_s": 0.0, "wait_s": 0.0}
 
 
 def build_shared_state(Q: Quantized, lanes: ForestLanes, coll=None) -> list:

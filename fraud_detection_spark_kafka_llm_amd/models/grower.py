@@ -1,21 +1,25 @@
 """Level-wise histogram tree grower shared by DecisionTree, RandomForest and GBDT (X-09, X-10, X-13).
 
-Per tree: ``tree_quant`` quantises the two row statistics (GBDT g*w, h*w, or class counts
-w*[y==0], w*[y==1]) to integers q = rint(v * 2^k) stored as i8 digit planes (csrc/tree.h); the
-exponent k comes from the global max |v| (all-reduced under data parallelism). Per level (all
-nodes of the level batched into every launch):
-  1. ``tree_slot8``         1-byte slot of the node being built per row (0xff: not built)
-  2. ``tree_hist_build``    i8-MFMA histograms of the smaller child of each sibling pair: exact
-                            int64 sums added straight into the level's histogram
-  3. reduce-scatter         int64 histograms of the built nodes across data-parallel ranks (RCCL);
-                            sums of integers are exact, so every rank holds the same bits
-  4. ``tree_hist_subtract`` larger sibling = parent - built sibling (exact)
-  5. ``tree_split_find``    best (feature, bin) per (node, feature); argmax per node on device
-  6. host: create children (tiny D2H of one best split per node)
-  7. ``tree_partition``     rows -> children (default side for rows absent from the split column)
-Every rank makes identical decisions from identical reduced histograms, so no split broadcast is
-needed. Node statistics of children come from the parent's split (as in Spark and XGBoost), as
-exact integers; leaf values / class counts are scaled by 2^-k only when the tree is emitted.
+Per tree, ``tree_quant`` quantises the two row statistics (GBDT g*w, h*w; classification
+w*[y==0], w*[y==1]) to integers q = rint(v * 2^k) (csrc/tree.h); the exponent k comes from the
+global max |v| (all-reduced under data parallelism). Every histogram is then an exact int64 sum,
+so trees are bitwise identical on the host, on the device and at any world size. A level (all its
+nodes batched into every launch):
+  1. histograms of the built nodes -- GBDT: the row-group engine (csrc/row_kernels.hip: row lists
+     of the built rows, LDS int64 tables per bin group, the smaller sibling only); RF / DT: the CSC
+     work items of the sampled features (csrc/tree_kernels.hip hist_lds_kernel, LDS atomics);
+  2. data parallel: ONE reduce-scatter of the level's partials by feature shard (RCCL);
+  3. split search over this rank's features (the larger sibling subtracted inside it), best
+     split per node; data parallel: ONE all-gather of the per-shard best tuples;
+  4. ``level_plan`` on the device: applies the splits to the device node table and plans the
+     next level (open list, builds, subtraction rows; RF: the next level's feature sample and its
+     active work items);
+  5. partition of the rows to the children (zeroing the next level's histograms on the way).
+The host reads a 16-byte count row per level and the node table once per tree. Drivers, fastest
+first: the native runner's C++ level loops (csrc/bindings_level.cpp: RfLevels.gbdt_levels /
+gbdt_dp_levels for GBDT, RfBatch for RF trees in lockstep batches, models/forest_batch.py), the
+Python device loop ``device_tree_steps`` (the test oracle of the native loops, and the CPU path
+through the kernels' host twins), and the host loop ``grow_tree`` (deep trees).
 """
 from __future__ import annotations
 
