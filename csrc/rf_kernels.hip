@@ -74,17 +74,26 @@ __device__ void rf_threshold_node(const RfSampleArgs& a, int bi, const unsigned 
     const int64_t r = a.k - (int64_t)below[bi];     // rank of the k-th inside the window
     const int n = (int)ncand[bi];
     if (r >= 1 && r <= n && n <= kCap) {
-      for (int j = tid; j < n; j += kThreads) s_cand[j] = cand[(int64_t)bi * kCap + j];
+      // the window's candidates sorted in LDS (bitonic, padded to a power of two with the largest
+      // value): the r-th smallest is then s_cand[r - 1] -- ~45 barrier steps for ~400 candidates
+      // instead of an all-pairs rank (n^2 LDS reads per node, the larger part of this kernel)
+      int m = 1;
+      while (m < n) m <<= 1;
+      for (int j = tid; j < m; j += kThreads) s_cand[j] = j < n ? cand[(int64_t)bi * kCap + j] : ~0ull;
       __syncthreads();
-      for (int j = tid; j < n; j += kThreads) {
-        const uint64_t uj = s_cand[j];
-        int64_t less = 0, eq = 0;
-        for (int t = 0; t < n; ++t) {
-          less += s_cand[t] < uj;
-          eq += s_cand[t] == uj;
+      for (int size = 2; size <= m; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int i = tid; i < (m >> 1); i += kThreads) {
+            const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+            const uint64_t x = s_cand[lo], y = s_cand[hi];
+            if ((x > y) == ((lo & size) == 0)) {
+              s_cand[lo] = y;
+              s_cand[hi] = x;
+            }
+          }
+          __syncthreads();
         }
-        if (less < r && r <= less + eq) a.thr[bi] = (double)uj * (1.0 / 9007199254740992.0);
-      }
+      if (tid == 0) a.thr[bi] = (double)s_cand[r - 1] * (1.0 / 9007199254740992.0);
       return;                  // uniform per workgroup: every thread took this branch
     }
   }

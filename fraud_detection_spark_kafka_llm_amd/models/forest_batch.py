@@ -122,7 +122,7 @@ class ForestBatch:
                 st.rf_thr = [torch.empty(st.cap, dtype=torch.float64, device=dev) for _ in range(2)]
                 st.rf_mask = [torch.empty(Q.Fa, dtype=torch.uint8, device=dev) for _ in range(2)]
             hosts = [st.arena_host, torch.zeros_like(st.arena_host).pin_memory()]
-            self.views.append([st.host_views(h) for h in hosts])
+            self.views.append([{k: v.numpy() for k, v in st.host_views(h).items()} for h in hosts])
             lc = dict(runner=runner, open0=st.open[0], open1=st.open[1], totals0=st.totals[0], totals1=st.totals[1],
                       arena=st.arena, arena_init=st.arena_init_dev, arena_host0=hosts[0], arena_host1=hosts[1],
                       tot_scratch=ws.totals, rowpack=ws.rowpack(),
