@@ -198,6 +198,8 @@ class RfLevels {
       else (void)hipGetLastError();
     }
     wide_ = get_opt(c, "wide");
+    fmix_ = get_opt(c, "fmix");
+    if (fmix_) FDX_CHECK(fmix_->scalar_type() == at::kLong && fmix_->numel() == c["F"].cast<int64_t>(), "fmix [F] int64");
     mode_ = c["mode"].cast<int>();
     max_depth_ = c["max_depth"].cast<int>();
     min_gain_ = c["min_gain"].cast<double>();
@@ -715,6 +717,7 @@ class RfLevels {
     a.feat_thr = p<double>(feat_thr);
     a.seed = (uint64_t)seed_;
     a.tree = (int32_t)tree;
+    if (fmix_ && feat_thr) a.fmix = reinterpret_cast<const uint64_t*>(p<int64_t>(*fmix_));
     a.out_gain = p<double>(gain_);
     a.out_bin = p<int32_t>(sbin_);
     a.out_left = p<int64_t>(sleft_);
@@ -902,6 +905,7 @@ class RfLevels {
     r.scratch = p<uint8_t>(scratch_);
     r.fused_counts = reinterpret_cast<uint32_t*>(p<int32_t>(sample_counts_));
     r.fused_cap = (int32_t)(sample_counts_.numel() / 3);
+    if (fmix_) r.fmix = reinterpret_cast<const uint64_t*>(p<int64_t>(*fmix_));
     if (rec_) rec_->add(kRecRfSample, r);
     else fdx::launch_rf_sample(r, s);
     if (local) {
@@ -1264,7 +1268,7 @@ class RfLevels {
 
   std::vector<ItemGroup> groups_;
   Tensor csc_row_, csc_bin_, colptr_, nbins_, zbin_, fid_orig_, rowdig_, row_node_, kexp_;
-  optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_, dig16_;
+  optional<Tensor> h_row_, h_key_, rowpack_, dense_, hot_row_, node_dense_, wide_, dig16_, fmix_;
   std::map<std::string, Tensor> st_;
   Tensor scratch_, gain_, sbin_, sleft_, chunk_sums_, ticket_, parts_, maxv_, part_gain_, part_f_;
   fdx::SplitArgs last_split_{};           // the last search (its partials feed the best-split pass)

@@ -157,6 +157,16 @@ void slot8(const Tensor& row_node, const Tensor& node_slot, int64_t slot_base, i
 // the listed work items whose row is in slot s of this pass (slot8 = None: root pass, slot 0).
 // RF per-level sampling: thr [n] f64 (k-th smallest priority of each node over 0..F-1) and the
 // union mask [Fa] u8 over the active features fid_orig.
+// mix64(f) for f in [0, F) (the priorities' per-feature hash, RfSampleArgs / SplitArgs fmix), on
+// the device of `like`
+Tensor feature_mix(int64_t F, const Tensor& like) {
+  FDX_CHECK(F >= 1, "F >= 1");
+  Tensor h = at::empty({F}, at::TensorOptions().dtype(at::kLong));
+  uint64_t* p = reinterpret_cast<uint64_t*>(h.data_ptr<int64_t>());
+  for (int64_t f = 0; f < F; ++f) p[f] = fdx::mix64((uint64_t)f);
+  return h.to(like.device());
+}
+
 void rf_sample(int64_t seed, int64_t tree, const Tensor& nodes, int64_t F, int64_t k, const Tensor& fid_orig,
                const Tensor& thr, const Tensor& mask, const optional<Tensor>& node_trees) {
   const auto dev = fid_orig.device();
@@ -1285,6 +1295,7 @@ void register_tree_ops(pybind11::module& m) {
   m.def("tree_rg_list_rows", [](int64_t N) { return (int64_t)fdx::rg_list_rows(N); });
   m.def("tree_partition_counts_ok", &fdx::partition_counts_ok);
   m.def("tree_rf_sample", &rf_sample);
+  m.def("tree_feature_mix", &feature_mix);
   m.def("tree_rf_compact", &rf_compact, py::arg("mask"), py::arg("nbins"), py::arg("fs"), py::arg("local"),
         py::arg("sizes"), py::arg("max_shard_features") = 0);
   m.def("tree_hist_dense", &hist_dense);

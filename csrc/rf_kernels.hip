@@ -23,6 +23,10 @@ constexpr int kCap = 2048;
 
 constexpr int kSlices = 64;       // workgroups per node of the window scan
 
+__device__ __forceinline__ uint64_t rf_priority(const RfSampleArgs& a, int32_t tree, int32_t node, int64_t f) {
+  return a.fmix ? feature_priority_u53_pre(a.seed, tree, node, a.fmix[f]) : feature_priority_u53(a.seed, tree, node, f);
+}
+
 // Fast path, pass 1: every priority below the window [ulo, uhi] is counted, those inside are
 // appended to the node's candidate list. The window holds the k-th smallest with probability
 // 1 - 1e-15 (+-8 sigma of the binomial count around k); rf_select_kernel checks it and falls back
@@ -38,7 +42,7 @@ __global__ __launch_bounds__(kThreads) void rf_window_kernel(RfSampleArgs a, uin
   __syncthreads();
   unsigned int mine = 0;
   for (int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x; f < a.F; f += (int64_t)gridDim.x * kThreads) {
-    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, i), node, f);
+    const uint64_t u = rf_priority(a, rf_tree_of(a, i), node, f);
     if (u < ulo) {
       ++mine;
     } else if (u <= uhi) {
@@ -113,7 +117,7 @@ __device__ void rf_threshold_node(const RfSampleArgs& a, int bi, const unsigned 
     for (int i = tid; i < kBuckets; i += kThreads) s_hist[i] = 0;
     __syncthreads();
     for (int64_t f = tid; f < a.F; f += kThreads) {
-      const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, bi), node, f);
+      const uint64_t u = rf_priority(a, rf_tree_of(a, bi), node, f);
       if (known == 0 || (u >> (53 - known)) == prefix)
         atomicAdd(&s_hist[(u >> shift) & ((1u << nbits) - 1)], 1u);
     }
@@ -138,7 +142,7 @@ __device__ void rf_threshold_node(const RfSampleArgs& a, int bi, const unsigned 
   const int known = s_known;
   const uint64_t prefix = s_prefix;
   for (int64_t f = tid; f < a.F; f += kThreads) {
-    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, bi), node, f);
+    const uint64_t u = rf_priority(a, rf_tree_of(a, bi), node, f);
     if (known == 0 || (u >> (53 - known)) == prefix) {
       const uint32_t i = atomicAdd(&s_ncand, 1u);
       if (i < (uint32_t)kCap) s_cand[i] = u;
@@ -185,7 +189,7 @@ __device__ __forceinline__ void rf_window_threshold_kernel_body(RfSampleArgs a, 
   __syncthreads();
   unsigned int mine = 0;
   for (int64_t f = (int64_t)blockIdx.x * kThreads + threadIdx.x; f < a.F; f += (int64_t)gridDim.x * kThreads) {
-    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, i), node, f);
+    const uint64_t u = rf_priority(a, rf_tree_of(a, i), node, f);
     if (u < ulo) {
       ++mine;
     } else if (u <= uhi) {
@@ -222,7 +226,7 @@ __device__ __forceinline__ void rf_mask_kernel_body(RfSampleArgs a) {
   uint8_t m = 0;
   for (int i = 0; i < a.nnodes && !m; ++i) {
     if (a.nodes[i] < 0) continue;
-    const uint64_t u = feature_priority_u53(a.seed, rf_tree_of(a, i), a.nodes[i], fid);
+    const uint64_t u = rf_priority(a, rf_tree_of(a, i), a.nodes[i], fid);
     m = ((double)u * (1.0 / 9007199254740992.0) <= a.thr[i]) ? 1 : 0;
   }
   a.mask[f] = m;

@@ -411,6 +411,7 @@ struct RfSampleArgs {
   // the window and the candidate count (the last window workgroup of a node ranks its candidates)
   uint32_t* fused_counts;
   int32_t fused_cap;
+  const uint64_t* fmix;           // optional [F]: mix64(f) (feature_priority_u53_pre)
 };
 
 FDX_HD int32_t rf_tree_of(const RfSampleArgs& a, int64_t i) { return a.node_trees ? a.node_trees[i] : a.tree; }
@@ -480,6 +481,7 @@ struct SplitArgs {
   uint64_t seed;
   int32_t tree;
   const int32_t* node_tree;       // RF batches: [nodes] tree index of each node (nullptr: `tree`)
+  const uint64_t* fmix;           // optional [F]: mix64(f) of the sampling priorities
   double* out_gain;               // [nodes][Fa]
   int32_t* out_bin;               // [nodes][Fa]
   int64_t* out_left;              // [nodes][Fa][2]
@@ -632,6 +634,12 @@ FDX_HD uint64_t feature_priority_u53(uint64_t seed, int32_t tree, int32_t node, 
   const uint64_t x = mix64((seed ^ 0x5bd1e995ull) ^
                            mix64((((uint64_t)(uint32_t)tree << 32) | (uint32_t)node) ^ mix64((uint64_t)fid)));
   return x >> 11;
+}
+
+// feature_priority_u53 with mix64(fid) looked up (RfSampleArgs / SplitArgs fmix: the table of
+// mix64(f) over the F features, shared by every node and tree): one mix64 of three per priority
+FDX_HD uint64_t feature_priority_u53_pre(uint64_t seed, int32_t tree, int32_t node, uint64_t mf) {
+  return mix64((seed ^ 0x5bd1e995ull) ^ mix64((((uint64_t)(uint32_t)tree << 32) | (uint32_t)node) ^ mf)) >> 11;
 }
 
 // Work item `item` holds at least one active feature (always true without a mask).

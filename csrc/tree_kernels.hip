@@ -928,6 +928,13 @@ __global__ __launch_bounds__(256) void hist_subtract_kernel(const int64_t* paren
 
 // ------------------------------------------------------------------ split search
 // node n's exact sums (level 0 of the fused prologue: from the quantisation's slots)
+// feature_priority of (node n, feature f) as a double (fmix: mix64 of the original feature id looked up)
+__device__ __forceinline__ double split_priority(const SplitArgs& a, int n, int f) {
+  const int32_t tree = a.node_tree ? a.node_tree[n] : a.tree;
+  if (a.fmix == nullptr) return feature_priority(a.seed, tree, a.node_ids[n], a.fid_orig[f]);
+  return (double)feature_priority_u53_pre(a.seed, tree, a.node_ids[n], a.fmix[a.fid_orig[f]]) * (1.0 / 9007199254740992.0);
+}
+
 __device__ __forceinline__ void split_totals(const SplitArgs& a, int n, int64_t* t0, int64_t* t1) {
   if (a.root_parts) {
     root_sums(a.root_parts, t0, t1);
@@ -948,7 +955,7 @@ __device__ __forceinline__ double split_narrow_at(const SplitArgs& a, int64_t t,
   int64_t l0 = 0, l1 = 0;
   bool use = a.node_ids[n] >= 0;              // -1: padded row of a device level loop
   if (use && a.feat_thr)
-    use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
+    use = split_priority(a, n, f) <= a.feat_thr[n];
   if (use) {
     const int64_t stride = a.hist_stride ? a.hist_stride : a.boff[a.Fa];
     const int64_t* hb = a.hist + (split_row(a, n) * stride + a.boff[f]) * 2;
@@ -1036,7 +1043,7 @@ __device__ __forceinline__ void split_wide_at(const SplitArgs& a, int64_t w, int
   const int64_t t = (int64_t)n * a.Fa + f;
   bool use = a.node_ids[n] >= 0;
   if (use && a.feat_thr)
-    use = feature_priority(a.seed, a.node_tree ? a.node_tree[n] : a.tree, a.node_ids[n], a.fid_orig[f]) <= a.feat_thr[n];
+    use = split_priority(a, n, f) <= a.feat_thr[n];
   double best = -1.0 / 0.0;
   int best_b = -1;
   int64_t bl0 = 0, bl1 = 0;

@@ -56,7 +56,7 @@ from .quantize import Quantized
 TREES_IN_FLIGHT = int(os.environ.get("FDX_RF_INFLIGHT", "16"))
 # histogram side streams per lane (grower.Workspace.run_concurrent): the lanes already overlap
 # whole trees, and every extra stream is another HW-queue mapping and cross-stream event per level
-LANE_HIST_STREAMS = int(os.environ.get("FDX_RF_LANE_STREAMS", "1"))
+LANE_HIST_STREAMS = 1
 # data parallelism: groups of lanes whose levels share one reduce-scatter + all-gather
 LANE_GROUPS = int(os.environ.get("FDX_RF_GROUPS", "2"))
 # sampled RF trees grow in lockstep batches on the native runner (csrc/bindings_level.cpp RfBatch):
@@ -90,14 +90,14 @@ class ForestLanes:
 def batch_ok(Q: Quantized, params: GrowParams, weight) -> bool:
     """The lockstep batch covers the default sampled-RF configuration on the device (the lean
     runner level loop with fused packed row state and the LDS-atomic count passes)."""
-    return (BATCH and Q.device.type == "cuda" and G.NATIVE_LEVELS and G.SAMPLED and G.FUSED_PACK and G.LEAN_RF and
+    return (BATCH and Q.device.type == "cuda" and G.NATIVE_LEVELS and G.SAMPLED and G.FUSED_PACK and
             G.RF_LDS and params.feat_k > 0 and G._choose_np(params, weight) == 1 and params.max_depth >= 1 and
             G.device_levels_ok(params, weight))
 
 
 class ForestBatch:
     """The lanes' workspaces, level states and runners handed to one native RfBatch (built once
-    per ForestLanes and tree parameters): per lane the level buffers of grower._rf_runner_levels
+    per ForestLanes and tree parameters): per lane the level buffers of the runner's level loop
     plus two pinned node-table copies (the host builds one batch's trees while the next grows)."""
 
     def __init__(self, Q: Quantized, wss: list, params: GrowParams, coll=None, shards: list = None):

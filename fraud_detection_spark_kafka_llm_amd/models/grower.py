@@ -43,26 +43,19 @@ from .quantize import Quantized
 NEG_INF = float("-inf")
 MAX_CT = 8                      # column tiles per pass (csrc/tree_kernels.hip launch_hist)
 DENSE_RANGE_ROWS = 32768        # max rows per wave of the dense hot-feature histogram kernel
-# waves per dense launch to aim for (>= ~8 per SIMD on 1024 SIMDs): launches with few feature
-# groups (e.g. the handful of hot features with 17..64 bins) get proportionally shorter row ranges
-DENSE_TARGET_WAVES = int(os.environ.get("FDX_DENSE_WAVES", 0))   # 0: always DENSE_RANGE_ROWS
-DENSE_MIN_RANGE = 2048
 
 
 def dense_range_rows(n_rows: int, ngroups: int) -> int:
-    """Rows per wave (multiple of 64) so that ceil(n / rows) * ngroups reaches DENSE_TARGET_WAVES."""
-    if DENSE_TARGET_WAVES <= 0:
-        return DENSE_RANGE_ROWS
-    want = -(-max(n_rows, 1) * max(ngroups, 1) // DENSE_TARGET_WAVES)
-    rows = -(-want // 64) * 64
-    return int(min(DENSE_RANGE_ROWS, max(DENSE_MIN_RANGE, rows)))
+    """Rows per wave of the dense hot-feature kernel (fixed: shorter ranges for launches with few
+    feature groups measured no better, profiles/r2_gbdt_knob_sweep.txt)."""
+    return DENSE_RANGE_ROWS
 # levels 0..DENSE_MAX_DEPTH build the hot features' histograms with the dense kernel (every row
 # streamed, slot-masked); deeper levels use their CSC items (only live entries multiplied)
-DENSE_MAX_DEPTH = int(os.environ.get("FDX_DENSE_MAX_DEPTH", 2))
+DENSE_MAX_DEPTH = 2
 # histogram launches of one pass (CSC groups, dense groups) run concurrently on this many HIP
 # streams: they add into disjoint feature ranges with integer atomics, so the order is free and
 # the kernels fill each other's tails
-HIST_STREAMS = int(os.environ.get("FDX_HIST_STREAMS", 4))
+HIST_STREAMS = 4
 # device level loop counters (bench/gbdt_train.py reports the histogram payload per level: what a
 # data-parallel level reduce-scatters, before the 1/S shard split)
 LEVEL_STATS = {"levels": 0, "built_nodes": 0, "hist_bytes": 0, "coll_calls": 0, "coll_ms": 0.0,
@@ -101,7 +94,7 @@ def _level_collective_ms() -> float:
 # Timing events around the level collectives: every LEVEL_TIMING-th collective is timed and the
 # total scaled by LEVEL_TIMING (event records cost the host thread that drives the RF lanes a few
 # microseconds each: timing every call added ~5 % to a forest); 1: every call, 0: none
-LEVEL_TIMING = int(os.environ.get("FDX_LEVEL_TIMING", "8"))
+LEVEL_TIMING = 8
 
 
 class _CollTimer:
@@ -301,67 +294,48 @@ class LevelBatcher:
 
 # row-group histogram engine (models/quantize.RowGroups, csrc/row_kernels.hip): every level's
 # histograms from the row-group CSR of the built rows, in place of the CSC / dense passes
-ROWHIST = os.environ.get("FDX_ROWHIST", "1") == "1"
-RG_DBG = int(os.environ.get("FDX_RG_DBG", 0))   # diagnostics only (csrc/tree.h RgHistArgs::dbg)
+ROWHIST = True
+RG_DBG = 0   # diagnostics only (csrc/tree.h RgHistArgs::dbg)
 # RF passes over sampled features: packed row state (slot + class counts in one word per row) and
 # a device-compacted list of the active work items (tree_hist_sampled)
-SAMPLED = os.environ.get("FDX_RF_SAMPLED", "1") == "1"
-LISTED_MAX_NODES = int(os.environ.get("FDX_RF_LISTED_NODES", 2))
+SAMPLED = True
+LISTED_MAX_NODES = 2
 # RF levels >= 1 launch one wave per active work item from lists compacted with the previous
 # level's plan (0: the r4 passes, a wave per item slot or a fixed listed grid)
-PRESELECT = os.environ.get("FDX_RF_PRESELECT", "1") == "1"
+PRESELECT = True
 # ... on shards of at least this many rows. Once the packed items skip their unsampled features
 # and the selects of a level are one launch, the listed passes win at 1.25M rows too (DP=8 shard,
 # forced collectives: 0.456 -> 0.446 s a forest, profiles/r5/rf_lean_presel_ab_1M.jsonl; before,
 # 143 -> 207 us a pass the other way); at 10M rows they win (0.768 -> 0.747 s)
-PRESELECT_MIN_ROWS = int(os.environ.get("FDX_RF_PRESELECT_ROWS", 0))
+PRESELECT_MIN_ROWS = 0
 # RF levels >= 1 read the packed row state (slot | class-count digits) written by the previous
 # level's partition instead of a row pass of their own (slot pack / masked digits: ~87 us per level
 # at 10M rows, 173 ms of a 500-tree forest's kernel time, profiles/r5/NOTES.md)
-FUSED_PACK = os.environ.get("FDX_RF_FUSED_PACK", "1") == "1"
+FUSED_PACK = True
 # RF device levels issue their kernels through the native per-level runner (csrc/bindings_level.cpp
 # RfLevels: hist / split / plan / partition, one host call each) instead of ~20 Python-level calls
-NATIVE_LEVELS = os.environ.get("FDX_NATIVE_LEVELS", "1") == "1"
+NATIVE_LEVELS = True
 # single-process runner levels subtract the larger siblings inside the split search
-SPLIT_SUBTRACT = os.environ.get("FDX_SPLIT_SUBTRACT", "1") == "1"
+SPLIT_SUBTRACT = True
 # the partition's row pass writes the next level's row-list counts (runner levels, <= 4M rows)
-PARTITION_COUNTS = os.environ.get("FDX_PARTITION_COUNTS", "1") == "1"
+PARTITION_COUNTS = True
 # single-slot row-group passes reduce per-workgroup partial tables (0: every workgroup's atomics)
-RG_PARTIALS = os.environ.get("FDX_RG_PARTIALS", "1") == "1"
+RG_PARTIALS = True
 # ... and so do the listed passes over several slots (a workgroup whose chunk straddles a slot
 # boundary still flushes with atomics)
-RG_PARTIALS_MULTI = os.environ.get("FDX_RG_PARTIALS_MULTI", "1") == "1"
-# sampled RF trees on the runner take the lean level loop (_rf_runner_levels; 0: the generic loop)
-LEAN_RF = os.environ.get("FDX_RF_LEAN", "1") == "1"
+RG_PARTIALS_MULTI = True
 # single-process GBDT trees on the row-group engine: the level loop runs in the runner (C++,
 # RfLevels.gbdt_levels; 0: the generic Python loop)
-GBDT_CXX_LEVELS = os.environ.get("FDX_GBDT_CXX_LEVELS", "1") == "1"
+GBDT_CXX_LEVELS = True
 # ... which builds the sibling with fewer rows (not the smaller hessian sum) where the row lists
 # count their own rows (above 4M rows, or FDX_PARTITION_COUNTS=0): same trees, shorter lists
-GBDT_CHOOSE_ROWS = os.environ.get("FDX_GBDT_CHOOSE_ROWS", "1") == "1"
-# diagnostics (bench/probes/list_oracle.py; generic loop, syncs every level): per listed level,
-# (tree, depth, rows listed, rows a fewest-rows sibling choice would list) into LIST_ORACLE_LOG
-LIST_ORACLE = os.environ.get("FDX_LIST_ORACLE", "0") == "1"
-LIST_ORACLE_LOG = []
-
-
-def _list_oracle(st, ws, cur, n_open, n_build, tree_index, d):
-    """Rows the level's row lists hold vs the fewest possible (per sibling pair the child with
-    fewer rows; a lone open child is built anyway)."""
-    T = int(ws.rg_start[n_build])
-    cnt = torch.bincount(ws.row_node.long().clamp(min=0), minlength=st.parent.numel()).cpu().numpy()
-    open_ = st.open[cur][:n_open].cpu().numpy()
-    par = st.parent.cpu().numpy()[open_]
-    best = {}
-    for node, p in zip(open_, par):
-        best[p] = min(best.get(p, 1 << 62), int(cnt[node]))
-    LIST_ORACLE_LOG.append((int(tree_index), int(d), T, int(sum(best.values()))))
+GBDT_CHOOSE_ROWS = True
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
-RF_LDS = os.environ.get("FDX_RF_LDS", "1") == "1"
+RF_LDS = True
 # split search: a wave per (node, feature) for the features with > 16 bins
-SPLIT_WIDE = os.environ.get("FDX_SPLIT_WIDE", "1") == "1"
+SPLIT_WIDE = True
 # partition splits on dense-block features in the row pass (FDX_PARTITION_DENSE=0: CSC column pass)
-PARTITION_DENSE = os.environ.get("FDX_PARTITION_DENSE", "1") != "0"
+PARTITION_DENSE = True
 # RF levels under data parallelism reduce-scatter only the bins of the level's sampled features
 # (FeatureShards.sample_compact). "auto": when the reduce-scatter crosses ranks (world > 1; at
 # world 1 it is a local copy and the layout pass only costs); "1" always (the world-1 RCCL
@@ -372,8 +346,8 @@ RF_COMPACT = os.environ.get("FDX_RF_COMPACT", "auto")
 # GBDT trees grow with the device-resident level loop (grow_tree_device): split application and
 # next-level planning run on the GPU, the host reads 16 bytes per level and the node table once
 # per tree (FDX_DEVICE_LEVELS=0: host loop)
-DEVICE_LEVELS = os.environ.get("FDX_DEVICE_LEVELS", "1") != "0"
-PARTITION_WPS = int(os.environ.get("FDX_PARTITION_WPS", 256))  # blocks per column split (device partition)
+DEVICE_LEVELS = True
+PARTITION_WPS = 256  # blocks per column split (device partition)
 # debug: check on the host that every open node of a data-parallel level is built or subtracted
 # (its histogram row is then written before the split search reads it)
 LEVEL_CHECKS = os.environ.get("FDX_LEVEL_CHECKS", "0") == "1"
@@ -1252,10 +1226,26 @@ def _level_runner(Q: Quantized, ws: Workspace, st: "LevelState", params: GrowPar
                sub_par=st.sub_par, sub_sib=st.sub_sib, sub_of=st.sub_of, node_dense=st.node_dense, mode=int(params.mode),
                max_depth=int(params.max_depth), min_gain=float(params.min_gain), lambda_=float(params.lambda_),
                mcw=float(params.min_child), seed=int(params.seed), F=int(Q.num_features), k=int(params.feat_k),
-               lds=bool(RF_LDS), wps=int(PARTITION_WPS), arena=st.arena, dig16=ws.dig16() if sampled else None)
+               lds=bool(RF_LDS), wps=int(PARTITION_WPS), arena=st.arena, dig16=ws.dig16() if sampled else None,
+               fmix=_feature_mix(Q) if (params.feat_k and FEATURE_MIX) else None)
     runner = native.lib().RfLevels(cfg)
     ws._rf_runner = (st, key, runner)
     return runner
+
+
+# the sampler and split search look mix64(feature) up in a table instead of recomputing it: off,
+# the table reads cost more than the hash (rf_window_threshold 24.6 -> 27.2 ms a forest,
+# profiles/r6/rf_dp_busy_fmix_REJECTED.txt); kept for the record, host twins ignore it
+FEATURE_MIX = False
+
+
+def _feature_mix(Q: Quantized) -> torch.Tensor:
+    """mix64(f) over the F features on the device (the RF priorities' per-feature hash, looked up
+    by the sampler and the split search instead of recomputed per node), once per Q."""
+    t = getattr(Q, "_fmix", None)
+    if t is None:
+        t = Q._fmix = native.lib().tree_feature_mix(int(Q.num_features), Q.nbins)
+    return t
 
 
 def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
@@ -1395,171 +1385,6 @@ def _gbdt_runner_levels(Q, runner, tree_index, on_first_wait):
         LEVEL_STATS["levels"] += 1
         LEVEL_STATS["built_nodes"] += shape[j + 1]
         LEVEL_STATS["hist_bytes"] += shape[j + 1] * Q.TB * 16
-
-
-class _RfViews:
-    """Views of a LevelState's buffers the sampled RF level loop slices every level, made once
-    (a tensor slice costs 2-5 us of host time; the loop is host bound at small shards)."""
-
-    def __init__(self, st: "LevelState"):
-        self.st = st
-        self._m = {}
-
-    def get(self, key, make):
-        v = self._m.get(key)
-        if v is None:
-            v = self._m[key] = make()
-        return v
-
-
-def _rf_runner_levels(Q, ws, st, params, tree_index, seed, shards, runner, sel_ids, item_groups, compact,
-                      native_prologue, cur_stream, on_first_wait, pre_hist):
-    """The level loop of a sampled RF tree on the native runner (device_tree_steps' generic loop
-    with runner and sampled and FUSED_PACK, launch for launch): every level's feature sample is
-    queued by the previous level's plan (runner.plan / split_plan sample_next), the per-level
-    tensor views are memoised (_RfViews) and the branches of the other tree kinds are gone.
-    ``pre_hist``: the root histogram the prologue zeroed (single process). Returns the
-    on_first_wait callback if it is still pending."""
-    C = native.lib()
-    dev = Q.device
-    V = getattr(st, "_rfv", None)
-    if V is None:
-        V = st._rfv = _RfViews(st)
-    if st.rf_thr is None:                     # (the next level's sample goes here; no preselection)
-        st.rf_thr = [torch.empty(st.cap, dtype=torch.float64, device=dev) for _ in range(2)]
-        st.rf_mask = [torch.empty(Q.Fa, dtype=torch.uint8, device=dev) for _ in range(2)]
-    TB = Q.TB
-    F, k = int(Q.num_features), int(params.feat_k)
-    groups = item_groups
-    wide = (_wide_features(shards.nbins, shards.Fa) if shards is not None else _wide_features(Q.nbins, Q.Fa)) \
-        if SPLIT_WIDE else None
-    sel_args = [ws.item_list(gi, grp)[0] if gi in sel_ids else None for gi, grp in enumerate(groups)] \
-        if sel_ids else []
-    sel_j = {gi: j for j, gi in enumerate(sel_ids)}
-    listed = [ws.item_list(gi, grp) if grp.num_items else (None, None) for gi, grp in enumerate(groups)]
-    empty_lay = (None,) * 5 + (0,)
-    n_open, n_build = 1, 1
-    per_xcd = None
-    ev = None
-    for d in range(params.max_depth):
-        cur = d & 1
-        nxt = cur ^ 1
-        if d > 0:
-            if on_first_wait is not None:
-                on_first_wait()
-                on_first_wait = None
-            yield ev
-            cnt = st.counts_host[d - 1].tolist()
-            n_open, n_build = cnt[1], cnt[2]
-            if n_open == 0:
-                break
-            if sel_ids:       # largest per-XCD active-item count of each sampled group
-                per_xcd = {}
-                for j, gi in enumerate(sel_ids):
-                    row = cnt[4 + 8 * j: 12 + 8 * j]
-                    per_xcd[gi] = m = max(row)
-                    if m:           # (launch_hist: (npx + 3) / 4 x 8 workgroups of 4 waves)
-                        LEVEL_STATS["listed_passes"] += 1
-                        LEVEL_STATS["listed_active_items"] += sum(row)
-                        LEVEL_STATS["listed_grid_waves"] += (m + 3) // 4 * 8 * 4
-        LEVEL_STATS["levels"] += 1
-        LEVEL_STATS["built_nodes"] += n_build
-        LEVEL_STATS["hist_bytes"] += n_build * TB * 16
-        open_d = V.get(("open", cur, n_open), lambda: st.open[cur][:n_open])
-        if d == 0 and native_prologue:
-            totals_d = V.get(("root",), lambda: st.stats[:1])
-        else:
-            totals_d = V.get(("tot", cur, n_open), lambda: st.totals[cur][:n_open])
-        n_open_ptr = st.one if d == 0 else V.get(("nop", d), lambda: st.counts[d - 1, 1:2])
-        more = d + 1 < params.max_depth
-        # the level's k-of-F sample: queued with the previous level's plan (the root's here)
-        if compact:
-            feat_thr, feat_mask, local_c, Bs_c = shards.compact_level(cur, n_open)
-        elif d > 0:
-            feat_thr = V.get(("thr", cur, n_open), lambda: st.rf_thr[cur][:n_open])
-            feat_mask = st.rf_mask[cur]
-        else:
-            feat_thr = V.get(("thr", cur, n_open), lambda: st.rf_thr[cur][:n_open])
-            feat_mask = st.rf_mask[cur]
-            C.tree_rf_sample(seed, tree_index, open_d, F, k, Q.fid_orig, feat_thr, feat_mask, None)
-        bufs = None
-        if shards is None:
-            if pre_hist is not None and pre_hist.shape[0] >= n_open:
-                hist_target = pre_hist[:n_open]
-            else:
-                hist_target = torch.zeros((n_open, TB, 2), dtype=torch.int64, device=dev)
-            pre_hist = None
-            h_boff = Q.boff
-            s2n = st.zero1 if d == 0 else V.get(("s2n", n_build), lambda: st.s2n[:n_build])
-        else:
-            bufs = yield CollStep("alloc", rows=n_build, Bs=Bs_c if compact else shards.Bs, n_open=n_open,
-                                  totals=ws.totals if d == 0 else None, sub_rows=0)
-            hist_target = bufs.prepare(ws.totals if d == 0 else None)
-            h_boff = local_c if compact else shards._local
-            s2n = ws.iota(n_build)
-        with tracing.span("tree.hist"):
-            pack = ws.rowpack() if d > 0 else None
-            lists, cnts, npxs = [], [], []
-            for gi, grp in enumerate(groups):
-                if grp.num_items and sel_ids and d > 0:
-                    j = sel_j[gi]
-                    lists.append(sel_args[gi])
-                    cnts.append(V.get(("cnt", d, j), lambda: st.counts[d - 1, 4 + 8 * j: 12 + 8 * j]))
-                    npxs.append(per_xcd[gi])
-                elif grp.num_items and n_open <= LISTED_MAX_NODES:
-                    lists.append(listed[gi][0])
-                    cnts.append(listed[gi][1])
-                    npxs.append(-1)
-                else:
-                    lists.append(None)
-                    cnts.append(None)
-                    npxs.append(-1)
-            runner.hist(n_build, hist_target, h_boff, feat_mask, s2n, pack, lists, cnts, npxs,
-                        shards._shard_of if shards is not None else None,
-                        bufs.shard_bins if shards is not None else 0)
-        if shards is not None:
-            yield CollStep("rs")                  # (the batch's reduce-scatter, LevelBatcher.serve)
-            if d == 0:
-                tot = bufs.reduced_totals()
-                st.stats[0].copy_(tot)
-                totals_d.copy_(tot[None])
-            # every open node built, slot k = open node k: the reduced rows ARE the histograms
-            cur_hist = bufs.mine()
-            with tracing.span("tree.split"):
-                split_boff = local_c[shards.f0: shards.f0 + shards.Fa + 1] if compact else shards.boff
-                runner.split(cur_hist, totals_d, split_boff, shards.nbins, shards.zbin, shards.fid_orig, open_d,
-                             feat_thr, tree_index, shards.f0, bufs.ag_in, None, wide)
-                packed = yield CollStep("ag")
-        else:
-            cur_hist = hist_target
-            packed = ws.split_cache.get(("out", n_open))
-            if packed is None:
-                packed = ws.split_cache[("out", n_open)] = torch.empty((n_open, 5), dtype=torch.int64, device=dev)
-        if more and compact:
-            thr_n, mask_n = shards.compact_thr(nxt, 2 * n_open), shards.compact_mask(nxt)
-            lay = (shards._fs_dev, Q.nbins, shards._local_c[nxt], shards._sizes[nxt], shards.sizes_host[nxt],
-                   shards.max_shard_features)
-        elif more:
-            thr_n, mask_n, lay = st.rf_thr[nxt], st.rf_mask[nxt], empty_lay
-        else:
-            thr_n = mask_n = None
-            lay = empty_lay
-        sel = sel_args if (sel_ids and more) else []
-        if shards is None:
-            runner.split_plan(d, n_open, cur_hist, totals_d, Q.boff, feat_thr, tree_index, packed, wide, open_d,
-                              n_open_ptr, st.open[nxt], st.totals[nxt], more, thr_n, mask_n, sel, None)
-        else:
-            runner.plan(d, n_open, packed, open_d, n_open_ptr, st.open[nxt], st.totals[nxt], tree_index, more,
-                        thr_n, mask_n, *lay, sel)
-        ev = st.record_event(cur_stream)
-        zero = None
-        if shards is None and more:
-            # the next level's histograms (every open node built: <= 2 n_open rows), zeroed by the
-            # partition kernel on the way
-            pre_hist = zero = torch.empty((2 * n_open, TB, 2), dtype=torch.int64, device=dev)
-        with tracing.span("tree.partition"):
-            runner.partition(d, n_open, more, zero, native_prologue, None)
-    return on_first_wait
 
 
 def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_index: int, g: torch.Tensor,
@@ -1712,12 +1537,6 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
             LEVEL_STATS["built_nodes"] += shape[j + 1]
             LEVEL_STATS["hist_bytes"] += shape[j + 1] * TB * 16
         generic_depth = 0
-    elif runner is not None and sampled and FUSED_PACK and LEAN_RF:
-        # sampled RF levels on the native runner: the lean loop (same launches, far less Python)
-        on_first_wait = yield from _rf_runner_levels(Q, ws, st, params, int(tree_index), seed, shards, runner,
-                                                     sel_ids, item_groups, compact, native_prologue, cur_stream,
-                                                     on_first_wait, pre_hist)
-        generic_depth = 0
     for d in range(generic_depth):
         cur = d % 2
         if d > 0:
@@ -1828,8 +1647,6 @@ def device_tree_steps(Q: Quantized, ws: Workspace, params: GrowParams, tree_inde
                         else None
                     C.tree_rg_list(ws.row_node, st.node_slot, None, Q.n_rows, n_build, ws.rg_work, ws.rg_start,
                                    ws.rg_list, ws.rowdig, ws.rg_listdig, emdig, counted=rg_counted)
-                    if LIST_ORACLE:
-                        _list_oracle(st, ws, cur, n_open, n_build, tree_index, d)
                     C.tree_rg_hist(rg.ptr, rg.ent, rg.gbase, rg.gbin, ws.rowdig, np_, ws.rg_list, ws.rg_start,
                                    ws.rg_listdig, n_build, rg.gmode, wtab, s2n, hist_target, h_stride,
                                    *shard_args, RG_DBG, **(rg.em_args(emdig) if emdig is not None else {}), **part)

@@ -135,9 +135,11 @@ def fit_forest(features, labels, num_trees: int = 1, max_depth: int = 5, max_bin
         # collective sequences): the smallest rank's cap wins
         inflight = int(coll.min(torch.tensor([inflight], dtype=torch.int64, device=Q.device)).item())
     lanes = None
-    if inflight > 1 and num_trees - len(trees) > 1 and device_levels_ok(params, w):
+    left = num_trees - len(trees)
+    # (on the device every sampled forest, a single tree too, grows on the lockstep batch)
+    if left > 0 and device_levels_ok(params, w) and (forest_batch.batch_ok(Q, params, w) or (inflight > 1 and left > 1)):
         with tracing.span("forest.lanes"):
-            lanes = ForestLanes(Q, min(inflight, num_trees - len(trees)), ws)
+            lanes = ForestLanes(Q, max(1, min(inflight, left)), ws)
     chunk = max(ckpt.every if ckpt is not None else 64, 1)
     t = len(trees)
     while t < num_trees:

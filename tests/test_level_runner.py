@@ -35,11 +35,10 @@ def test_gpu_native_levels_equal_python_levels(inflight, monkeypatch):
     monkeypatch.setattr(grower, "NATIVE_LEVELS", False)
     ref = _forest("cuda:0")
     monkeypatch.setattr(grower, "NATIVE_LEVELS", True)
+    assert _forest("cuda:0") == ref                           # the lockstep batch (RfBatch)
+    monkeypatch.setattr(forest_batch, "BATCH", False)         # the generic loop on the runner, per tree
     assert _forest("cuda:0") == ref
-    monkeypatch.setattr(grower, "LEAN_RF", False)            # the generic loop on the runner
-    assert _forest("cuda:0") == ref
-    monkeypatch.setattr(grower, "LEAN_RF", True)
-    monkeypatch.setattr(grower, "PRESELECT_MIN_ROWS", 0)
+    monkeypatch.setattr(forest_batch, "BATCH", True)
     for presel, fused in ((False, True), (True, False)):
         monkeypatch.setattr(grower, "PRESELECT", presel)
         monkeypatch.setattr(grower, "FUSED_PACK", fused)
