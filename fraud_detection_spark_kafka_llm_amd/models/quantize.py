@@ -53,7 +53,7 @@ def default_chunk(n_rows: int) -> int:
 # A work item's int32 MFMA accumulators gain at most 128 * 128 = 2^14 per entry, so one item may
 # hold at most this many entries before a (key, column) sum could overflow (csrc/tree_kernels.hip)
 MAX_ITEM_ENTRIES = (1 << 31) // (1 << 14) - 1
-PACK_KEYS = int(os.environ.get("FDX_PACK_KEYS", 16))   # keys of a packed multi-feature item (16 = one MFMA row tile)
+PACK_KEYS = 16   # keys of a packed multi-feature item (16 = one MFMA row tile)
 
 
 @dataclass
@@ -123,7 +123,7 @@ def wave_order(item_blk: Optional[torch.Tensor], num_items: int, dev) -> torch.T
 
 
 RG_BINS = int(os.environ.get("FDX_RG_BINS", 8192))   # local bins per row group: 8192 (1 workgroup per CU) or 4096 (2)
-RG_MAX_GROUPS = int(os.environ.get("FDX_RG_MAX_GROUPS", 128))
+RG_MAX_GROUPS = 128
 # workgroups per row-group pass: few and large -- every workgroup zeroes and flushes a whole
 # 8192-bin table (up to 2 x 8192 int64 global atomics per slot it covers). 10M rows x 40 trees:
 # 7.69 ms per tree at 2048, 6.19 at 512 (profiles/r4/gbdt_rg_work_sweep.txt); 1M rows x 100
@@ -153,12 +153,12 @@ def rg_list_default_wgs(n_rows: int) -> int:
 RG_ALPHA = float(os.environ.get("FDX_RG_ALPHA", 16.0))
 # groups with at least this many entries per row take lane-balanced batches (csrc/row_kernels.hip
 # rg_batch); sparser ones a lane per row
-RG_BAL_MIN = float(os.environ.get("FDX_RG_BAL_MIN", 8.0))
+RG_BAL_MIN = 8.0
 # the sparse groups (gmode 0) also get a row per entry (4 B) for the entry-major pass of
 # single-slot levels (csrc/row_kernels.hip rg_range_em); a listed level takes it when it lists at
 # least RG_EM_MIN_FRAC of the rows (> 1: never). Bench corpus, half the rows listed: sparse groups
 # 0.75 -> 0.48 ms; GBDT 10M x 40 trees 6.35 -> 6.28-6.32 ms per tree (profiles/r4)
-RG_EM = os.environ.get("FDX_RG_EM", "1") == "1"
+RG_EM = True
 RG_EM_MIN_FRAC = float(os.environ.get("FDX_RG_EM_MIN_FRAC", 0.3))
 
 
@@ -698,7 +698,7 @@ def _generic_path(idx, val, F, max_bins, all_gather):
     return remap, nbins, zb.to(torch.int32), thresholds, eb, full_keep
 
 
-HOT_DENSITY = float(os.environ.get("FDX_HOT_DENSITY", 0.1))  # dense path for features in >= this fraction of rows
+HOT_DENSITY = 0.1  # dense path for features in >= this fraction of rows
 
 
 def _pow2_at_least(x: np.ndarray, lo: int = 1) -> np.ndarray:
@@ -729,7 +729,7 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
 
 
 COPY_PIECE = 8192      # entries per workgroup of the histogram CSC copy
-LIGHT_ENTRIES = int(os.environ.get("FDX_LIGHT_ENTRIES", 0))    # whole-column items up to this many entries (0: off; profiles/r4/rf500_light_entries_sweep.txt)
+LIGHT_ENTRIES = 0    # whole-column items up to this many entries (0: off; profiles/r4/rf500_light_entries_sweep.txt)
 SUPER_ROWS = int(os.environ.get("FDX_SUPER_ROWS", 1 << 18))  # rows per super-block: 256 KB slots + 2 MB digits
 
 
