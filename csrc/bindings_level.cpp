@@ -1647,8 +1647,12 @@ class RfBatch {
   }
 
   void level(int64_t d, int cur, int nxt, bool more, hipStream_t s, std::vector<int64_t>& stat) {
+    // Every stage of the level is recorded first (the arguments depend only on host-known sizes and
+    // buffers fixed for the level), packed in one copy and then issued segment by segment with the
+    // collectives in between: the GPU runs the level's stages back to back instead of idling while
+    // the host records the next one (profiles/r6/rf_dp_busy_*.txt: the idle sat before each flush).
     // ---- histogram passes (DP: into the batch's shard-major send buffer)
-    Tensor send, out;
+    Tensor send, out, ag_in, allt;
     int64_t R = 0, Bs = 0, nrows = 0, nopen = 0;
     if (dp_) {
       for (int l : live_) {
@@ -1673,6 +1677,8 @@ class RfBatch {
       for (int l : live_) lanes_[l].tb = d == 0 ? nrows * Bs + t++ : -1;
       send = buffer(send_, S_ * R * Bs * 2).view({S_, R, Bs, 2});
       out = buffer(out_, R * Bs * 2).view({R, Bs, 2});
+      ag_in = buffer(ag_in_, nopen * 5).view({nopen, 5});
+      allt = buffer(allt_, S_ * nopen * 5).view({S_, nopen, 5});
       FDX_CHECK(hipMemsetAsync(send.data_ptr(), 0, send.nbytes(), s) == hipSuccess, "send zero");
     }
     for (int l : live_) {
@@ -1714,12 +1720,9 @@ class RfBatch {
                                                      ln.tb * 2});
       }
     }
-    flush(s);
+    const int64_t m_hist = mark();
     // ---- split search (+ best split + plan in one launch without a collective between them)
-    Tensor allt;
     if (dp_) {
-      reduce_scatter(send, out, s);
-      Tensor ag_in = buffer(ag_in_, nopen * 5).view({nopen, 5});
       for (int l : live_) {
         Lane& ln = lanes_[l];
         const Tensor& open = ln.view(5, cur, ln.n_open, [&] { return ln.open[cur].narrow(0, 0, ln.n_open); });
@@ -1731,9 +1734,8 @@ class RfBatch {
                     ln.view(8, cur, ln.n_open, [&] { return ln.thr[cur].narrow(0, 0, ln.n_open); }), ln.tree, f0_,
                     ag_in.narrow(0, ln.l0, ln.n_open), c10::nullopt, wide_);
       }
-      flush(s);
-      allt = all_gather(ag_in, s);
     }
+    const int64_t m_split = mark();
     for (int l : live_) {
       Lane& ln = lanes_[l];
       const Tensor& open = ln.view(5, cur, ln.n_open, [&] { return ln.open[cur].narrow(0, 0, ln.n_open); });
@@ -1760,8 +1762,7 @@ class RfBatch {
         ln.r->plan_root_tot_ = nullptr;
       }
     }
-    flush(s);
-    FDX_CHECK(hipEventRecord(ev_, s) == hipSuccess, "level event");
+    const int64_t m_plan = mark();
     // ---- partition (writes the next level's packed row state; single process: zeroes its histograms)
     for (int l : live_) {
       Lane& ln = lanes_[l];
@@ -1771,7 +1772,19 @@ class RfBatch {
                          : c10::nullopt;
       ln.r->partition(d, ln.n_open, more, zero, true, c10::nullopt);
     }
-    flush(s);
+    const int64_t m_end = mark();
+    if (live_.empty()) return;
+    pack(s);
+    launch(0, m_hist, s);
+    if (dp_) {
+      reduce_scatter(send, out, s);
+      launch(m_hist, m_split, s);
+      all_gather(ag_in, allt, s);
+    }
+    launch(m_split, m_plan, s);
+    FDX_CHECK(hipEventRecord(ev_, s) == hipSuccess, "level event");
+    launch(m_plan, m_end, s);
+    done();
     (void)stat;
   }
 
@@ -1815,25 +1828,41 @@ class RfBatch {
                 "ncclReduceScatter");
   }
 
-  Tensor all_gather(const Tensor& in, hipStream_t s) {
+  // in [n, 5] from every rank into out [S, n, 5] (the callback's result is copied there on the stream)
+  void all_gather(const Tensor& in, const Tensor& out, hipStream_t s) {
     ++ag_calls_;
-    if (!direct_) return ag_cb_(in).cast<Tensor>();
+    if (!direct_) {
+      const Tensor r = ag_cb_(in).cast<Tensor>();
+      FDX_CHECK(r.numel() == out.numel(), "all-gather callback result size");
+      out.copy_(r.view_as(out));
+      return;
+    }
     Timed t(this, s);
-    Tensor out = buffer(allt_, S_ * in.numel()).view({S_, in.size(0), 5});
     rccl_.check(rccl_.ag(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), ncclInt64, rccl_.comm, s), "ncclAllGather");
-    return out;
   }
 
   // Issues what the live lanes recorded: position i of every lane's record is one lane-batched
   // launch (the lanes recorded the same sequence). The argument arrays go to the device in one copy.
   void flush(hipStream_t s) {
     if (live_.empty()) return;
-    const auto t0 = std::chrono::steady_clock::now();
-    struct Acc {
-      double& a;
-      std::chrono::steady_clock::time_point t;
-      ~Acc() { a += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count(); }
-    } acc{host_s_[1], t0};
+    pack(s);
+    launch(0, (int64_t)pk_offs_.size(), s);
+    done();
+  }
+
+  // the number of launches the live lanes recorded so far (a segment boundary for launch())
+  int64_t mark() const { return live_.empty() ? 0 : (int64_t)lanes_[live_[0]].rec.entries.size(); }
+
+  struct Acc {
+    double& a;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    ~Acc() { a += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count(); }
+  };
+
+  // Packs every recorded launch's lane arguments into the staging region and copies them to the
+  // device in one H2D copy; launch(i0, i1) then issues positions [i0, i1), done() clears the records.
+  void pack(hipStream_t s) {
+    Acc acc{host_s_[1]};
     const int L = (int)live_.size();
     const auto& E0 = lanes_[live_[0]].rec.entries;
     for (int l : live_) {
@@ -1845,8 +1874,12 @@ class RfBatch {
     }
     uint8_t* host = p<uint8_t>(host_) + half_ * kRegion;
     uint8_t* dev = p<uint8_t>(dev_args_) + half_ * kRegion;
+    off_ = (off_ + 15) & ~int64_t{15};
     const int64_t start = off_;
-    std::vector<int64_t> offs(E0.size(), -1), offs2(E0.size(), -1);
+    std::vector<int64_t>& offs = pk_offs_;
+    std::vector<int64_t>& offs2 = pk_offs2_;
+    offs.assign(E0.size(), -1);
+    offs2.assign(E0.size(), -1);
     for (size_t i = 0; i < E0.size(); ++i) {
       if (E0[i].kind == kRecCopy) {            // D2H rows: one kernel writing the host-mapped rows
         off_ = (off_ + 15) & ~int64_t{15};
@@ -1878,14 +1911,31 @@ class RfBatch {
         off_ += L * (int64_t)sizeof(fdx::PartitionArgs);
       }
     }
+    off_ = (off_ + 15) & ~int64_t{15};
     if (off_ > start) {
-      FDX_CHECK(hipMemcpyAsync(dev + start, host + start, off_ - start, hipMemcpyHostToDevice, s) == hipSuccess,
-                "argument copy");
+      FDX_CHECK(off_ <= kRegion, "argument staging overflow");
+      // (read by a kernel through the pinned region's device mapping: no runtime H2D path)
+      uint8_t* src = static_cast<uint8_t*>(mapped(p<uint8_t>(host_))) + half_ * kRegion;
+      fdx::launch_stage_copy(dev + start, src + start, off_ - start, s);
       FDX_CHECK(hipEventRecord(half_ev_[half_], s) == hipSuccess, "event");
       half_used_[half_] = true;
     }
-    for (size_t i = 0; i < E0.size(); ++i) {
-      const int64_t o = offs[i];
+    pk_host_ = host;
+    pk_dev_ = dev;
+    pk_L_ = L;
+  }
+
+  void launch(int64_t i0, int64_t i1, hipStream_t s) {
+    Acc acc{host_s_[1]};
+    const int L = pk_L_;
+    const auto& E0 = lanes_[live_[0]].rec.entries;
+    FDX_CHECK(i0 >= 0 && i0 <= i1 && i1 <= (int64_t)pk_offs_.size() && pk_offs_.size() == E0.size(),
+              "launch range of the packed records");
+    uint8_t* host = pk_host_;
+    uint8_t* dev = pk_dev_;
+    const std::vector<int64_t>& offs2 = pk_offs2_;
+    for (int64_t i = i0; i < i1; ++i) {
+      const int64_t o = pk_offs_[i];
       switch (E0[i].kind) {
         case kRecQuant:
           fdx::launch_quant_lanes((const fdx::QuantLane*)(host + o), (const fdx::QuantLane*)(dev + o), L, s);
@@ -1930,7 +1980,12 @@ class RfBatch {
       }
     }
     C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+
+  void done() {
     for (int l : live_) lanes_[l].rec.entries.clear();
+    pk_offs_.clear();
+    pk_offs2_.clear();
   }
 
   std::vector<Lane> lanes_;
@@ -1953,6 +2008,11 @@ class RfBatch {
   Tensor host_, dev_args_;
   int half_ = -1;
   int64_t off_ = 0;
+  // the packed records (pack -> launch -> done)
+  std::vector<int64_t> pk_offs_, pk_offs2_;
+  uint8_t* pk_host_ = nullptr;
+  uint8_t* pk_dev_ = nullptr;
+  int pk_L_ = 0;
   bool half_used_[kRegions] = {};
   hipEvent_t ev_ = nullptr, half_ev_[kRegions] = {}, done_ = nullptr;
   at::TensorOptions i64_;

@@ -124,6 +124,9 @@ struct SplitBestPlanLane;
 struct PartColsLane;
 struct RootSendLane;
 struct CopyLane;
+// 16-byte words (bytes % 16 == 0, both 16-byte aligned) from src (may be a pinned host page's
+// device mapping) to dst, on the stream
+void launch_stage_copy(void* dst, const void* src, int64_t bytes, hipStream_t s);
 void launch_copy_lanes(const CopyLane* h, const CopyLane* d, int L, hipStream_t s);
 void launch_root_send_lanes(const RootSendLane* d, int L, hipStream_t s);
 void launch_quant_lanes(const QuantLane* h, const QuantLane* d, int L, hipStream_t s);

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(1024) void rg_build_scan_kernel(uint32_t* wave_base
 __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  const int32_t list_rows = rg_list_rows(a.N), list_steps = list_rows / 64;
+  const int32_t list_rows = a.list_rows, list_steps = list_rows / 64;
   const int64_t r0 = wave * list_rows;
   if (r0 >= a.N) return;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -727,8 +727,10 @@ template void launch_rg_build_csr<float>(const RgCsrBuildArgs<float>&, hipStream
 template void launch_rg_build_csr<double>(const RgCsrBuildArgs<double>&, hipStream_t);
 template void launch_rg_build_csr<int32_t>(const RgCsrBuildArgs<int32_t>&, hipStream_t);
 
-void launch_rg_list(const RgListArgs& a, hipStream_t s) {
-  const int64_t waves = (a.N + rg_list_rows(a.N) - 1) / rg_list_rows(a.N);   // 4 per block
+void launch_rg_list(const RgListArgs& a0, hipStream_t s) {
+  RgListArgs a = a0;
+  a.list_rows = rg_list_rows(a.N);
+  const int64_t waves = (a.N + a.list_rows - 1) / a.list_rows;   // 4 per block
   const int64_t blocks = (waves + 3) / 4;
   if (blocks <= 0) return;
   if (!a.counted) hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);

@@ -246,8 +246,11 @@ struct RgCsrBuildArgs {
 // Built rows of a level grouped by slot. The slot of row r is node_slot[row_node[r]] when
 // row_node is given (slots outside [0, nslots): not built), else slot8[r] (0xff: not built).
 // rows per wave of the list kernels: 512 up to 4M rows (1M rows: ~2K waves; 2048-row chunks left
-// ~500 waves and 19 us per pass), 2048 beyond (profiles/r4/gbdt_list_rows_ab.txt)
-FDX_HD int32_t rg_list_rows(int64_t N) { return N <= (4ll << 20) ? 512 : 2048; }
+// ~500 waves and 19 us per pass), 2048 beyond (profiles/r4/gbdt_list_rows_ab.txt). Host only (the
+// kernel takes RgListArgs::list_rows); tests lower the 4M threshold to run the large-shard paths
+// (2048-row waves, no partition row counts, fewest-rows sibling choice) on small data.
+inline int64_t g_rg_list_big_rows = 4ll << 20;
+inline int32_t rg_list_rows(int64_t N) { return N <= g_rg_list_big_rows ? 512 : 2048; }
 struct RgListArgs {
   const int32_t* row_node;        // [N] or nullptr
   const int32_t* node_slot;       // [num_nodes] slot of each node (-1: not built)
@@ -256,6 +259,7 @@ struct RgListArgs {
   int64_t N;
   int32_t nslots;
   int32_t* slot_count;            // [nslots] totals (pass 2)
+  int32_t list_rows;              // rg_list_rows(N) (set by launch_rg_list)
   int32_t* wave_count;            // [ceil(N / rg_list_rows(N))][nslots]: per-wave counts (pass 0), then
                                   //   per-wave offsets inside each slot (pass 2)
   int32_t* slot_start;            // [nslots + 1] out (pass 1)

@@ -1783,6 +1783,15 @@ __global__ __launch_bounds__(256) void copy_lanes_kernel(const CopyLane* __restr
   }
 }
 
+// The lane-argument staging copy: 16-byte words from pinned host memory (read through its device
+// mapping) into device memory. A kernel on the stream instead of hipMemcpyAsync: the runtime's H2D
+// path put ~40 us (SDMA) to ~0.5 ms (a blit at a batch start) between a level's stages
+// (profiles/r6/rf_dp_busy_gaps_*.txt).
+__global__ __launch_bounds__(256) void stage_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                         int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
 __global__ __launch_bounds__(256) void partition_default_lanes_kernel(const PartitionArgs* __restrict__ args) {
   partition_default_kernel_body(args[blockIdx.z]);
 }
@@ -2154,6 +2163,14 @@ void launch_copy_lanes(const CopyLane* h, const CopyLane* d, int L, hipStream_t 
   const int64_t blocks = (most / 8 + 255) / 256;
   hipLaunchKernelGGL(copy_lanes_kernel, dim3((unsigned)(blocks < 1 ? 1 : (blocks > 64 ? 64 : blocks)), 1, L), dim3(256), 0,
                      s, d);
+}
+
+void launch_stage_copy(void* dst, const void* src, int64_t bytes, hipStream_t s) {
+  const int64_t n = bytes / 16;
+  if (n <= 0) return;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(stage_copy_kernel, dim3((unsigned)(blocks > 32 ? 32 : blocks)), dim3(256), 0, s,
+                     reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), n);
 }
 
 void launch_root_send_lanes(const RootSendLane* d, int L, hipStream_t s) {

@@ -36,6 +36,7 @@ of per-row records; it lost to per-tree passes, profiles/r2_rf_batch_ab.txt, and
 """
 from __future__ import annotations
 
+import time
 import os
 from collections import deque
 from typing import Optional
@@ -109,7 +110,7 @@ class ForestBatch:
         compact = dp and 0 < params.feat_k < Q.num_features and \
             (G.RF_COMPACT == "1" or (G.RF_COMPACT == "auto" and shards[0].S > 1))
         D = int(params.max_depth)
-        self.Q, self.params, self.dp = Q, params, dp
+        self.Q, self.params, self.dp, self.compact = Q, params, dp, bool(compact)
         self.views, lane_cfg = [], []
         self.n_lanes = len(wss)
         self.parity = 0
@@ -208,8 +209,10 @@ def grow_forest_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tr
         fb = fbs[i]
         ids = [todo.popleft() for _ in range(min(fb.n_lanes, len(todo)))]
         fb.parity ^= 1
+        t0 = time.perf_counter()
         with tracing.span("forest.batch", trees=len(ids)):
             fb.native.start(ids, label, weight, bool(bootstrap), int(Q.row0))
+        HOST_TIMES["start_s"] += time.perf_counter() - t0
         running[i] = ids
 
     def account(fb, stat) -> None:
@@ -224,20 +227,53 @@ def grow_forest_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tr
             D.CALLS["reduce_scatter"] += stat[5]
             D.CALLS["all_gather"] += stat[6]
 
+    if EVENT_PROBE:
+        p0 = torch.cuda.Event(enable_timing=True)
+        p0.record()
     for i in range(nb):
         launch(i)
     while any(r is not None for r in running):
         for i in range(nb):
             ids = running[i]
+            ts = time.perf_counter()
             if ids is None or fbs[i].native.step():
                 continue
             fb = fbs[i]
             par = fb.parity
+            t0 = time.perf_counter()
+            HOST_TIMES["last_step_s"] += t0 - ts
             account(fb, fb.native.finish(par))
+            t1 = time.perf_counter()
+            if EVENT_PROBE:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
             launch(i)                     # the slot's next trees, queued before the host builds these
+            if EVENT_PROBE and running[i] is not None:
+                e2 = torch.cuda.Event(enable_timing=True)
+                e2.record()
+                _probe.append((e1, e2))
+            HOST_TIMES["turn_s"] += time.perf_counter() - ts
+            if running[i] is not None and fb.compact:
+                # (a compact DP batch queues its root level once the root's shard sizes are back:
+                # that wait is short, and the GPU then runs the level while the host builds trees)
+                fb.native.step()
+            t2 = time.perf_counter()
             fb.native.wait()              # (its event: the node tables just queued, not re-recorded yet)
+            t3 = time.perf_counter()
             for lane, t in enumerate(ids):
                 out[t] = G.tree_from_host(Q, params, fb.views[lane][par])
+            HOST_TIMES["finish_s"] += t1 - t0
+            HOST_TIMES["tables_wait_s"] += t3 - t2
+            HOST_TIMES["build_s"] += time.perf_counter() - t3
+    if EVENT_PROBE:
+        p1 = torch.cuda.Event(enable_timing=True)
+        p1.record()
+        torch.cuda.synchronize()
+        HOST_TIMES["gpu_phase_ms"] += p0.elapsed_time(p1)
+    if EVENT_PROBE and _probe:
+        torch.cuda.synchronize()
+        HOST_TIMES["gpu_turn_ms"] += sum(a.elapsed_time(b) for a, b in _probe)
+        _probe.clear()
     for fb in fbs:
         if fb.dp and fb.native.direct():
             G.LEVEL_STATS["coll_ms"] += fb.native.coll_ms()
@@ -249,7 +285,11 @@ def grow_forest_batched(Q: Quantized, lanes: ForestLanes, params: GrowParams, tr
 
 
 # host seconds of the lockstep batches (RfBatch.host_times): queuing levels, of which flushes, waits
-HOST_TIMES = {"levels_s": 0.0, "flush_s": 0.0, "wait_s": 0.0}
+HOST_TIMES = {"levels_s": 0.0, "flush_s": 0.0, "wait_s": 0.0, "start_s": 0.0, "finish_s": 0.0, "tables_wait_s": 0.0,
+              "build_s": 0.0, "last_step_s": 0.0, "turn_s": 0.0, "gpu_turn_ms": 0.0,
+              "gpu_phase_ms": 0.0}
+EVENT_PROBE = os.environ.get("FDX_RF_EVENT_PROBE") == "1"
+_probe: list = []
 
 
 def build_shared_state(Q: Quantized, lanes: ForestLanes, coll=None) -> list:

@@ -337,19 +337,79 @@ class GroupRendezvous:
 # from the end of this process's allowed set and the scoring process keeps the rest, so a client
 # never competes with the scorer's Python threads for a core; the record carries each client's
 # CPUs, NUMA node, CPU seconds and rate, and the cgroup's CPU quota and throttling during the run.
+# Measured on the 1-GPU boxes (profiles/r6/kafka/NOTES.md): a confluent-surface client keeps ~2.2
+# CPUs busy (its poll / extraction / delivery threads), so 2 logical CPUs of its own cut it to
+# 1.14-1.24 M/s for the group, 2-3 whole cores of its own to 1.24-1.39; the clients sharing 8 whole
+# cores each (24 cores, SMT siblings included) away from the scorer's gave 1.65-1.74 M/s against
+# 1.59-1.63 unpinned. Columnar clients (per-batch work) ran faster unpinned: only confluent-surface
+# groups are pinned.
 GROUP_PIN = os.environ.get("FDX_GROUP_PIN", "1") == "1"
-GROUP_CPUS_PER_CLIENT = int(os.environ.get("FDX_GROUP_CPUS_PER_CLIENT", "2"))
+GROUP_CPUS_PER_CLIENT = int(os.environ.get("FDX_GROUP_CPUS_PER_CLIENT", "8"))
+GROUP_WHOLE_CORES = os.environ.get("FDX_GROUP_WHOLE_CORES", "1") == "1"
+GROUP_SHARED = os.environ.get("FDX_GROUP_SHARED", "1") == "1"
 
 
-def client_cpu_plan(allowed: list, n_clients: int, per_client: int = GROUP_CPUS_PER_CLIENT) -> tuple:
-    """(per-client CPU lists, the scorer's CPUs): clients take ``per_client`` CPUs each from the
-    end of ``allowed`` when at least as many remain for the scorer; else no pinning (None)."""
+def cpu_list_str(cpus) -> str:
+    """Compact sorted CPU list: [0, 1, 2, 5, 128, 129] -> "0-2,5,128-129"."""
+    out, run = [], []
+    for c in sorted(cpus):
+        if run and c == run[-1] + 1:
+            run.append(c)
+            continue
+        if run:
+            out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+        run = [c]
+    if run:
+        out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+    return ",".join(out)
+
+
+def core_siblings(cpu: int, sysfs: str = "/sys/devices/system/cpu") -> tuple:
+    """The logical CPUs sharing ``cpu``'s physical core (SMT siblings), ``(cpu,)`` if unknown."""
+    try:
+        with open(os.path.join(sysfs, f"cpu{cpu}", "topology", "thread_siblings_list")) as fh:
+            out = []
+            for part in fh.read().strip().split(","):
+                a, _, b = part.partition("-")
+                out.extend(range(int(a), int(b or a) + 1))
+            return tuple(sorted(out)) or (cpu,)
+    except (OSError, ValueError):
+        return (cpu,)
+
+
+def client_cpu_plan(allowed: list, n_clients: int, per_client: int = GROUP_CPUS_PER_CLIENT,
+                    siblings=None, shared: bool = GROUP_SHARED) -> tuple:
+    """(per-client CPU lists, the scorer's CPUs): clients take ``per_client`` physical cores each
+    (every allowed SMT sibling of a core goes with it, so a client never shares a core with the
+    scorer's threads) from the end of ``allowed``, when at least as many cores remain for the
+    scorer; else no pinning (None). ``siblings(cpu)`` gives a CPU's core (default: sysfs; with
+    FDX_GROUP_WHOLE_CORES=0 every logical CPU counts as a core of its own). ``shared``: the clients
+    pool their cores (every client may run on all of them)."""
     allowed = sorted(allowed)
-    need = n_clients * per_client
-    if n_clients <= 0 or per_client <= 0 or len(allowed) < 2 * need:
+    if siblings is None:
+        siblings = core_siblings if GROUP_WHOLE_CORES else (lambda c: (c,))
+    cores, seen = [], set()
+    for c in allowed:
+        if c in seen:
+            continue
+        core = [s for s in siblings(c) if s in allowed and s not in seen] or [c]
+        seen.update(core)
+        cores.append(core)
+    cores.sort(key=lambda core: core[0])
+    if n_clients <= 0 or per_client <= 0:
         return None, None
-    tail = allowed[len(allowed) - need:]
-    return [tail[c * per_client:(c + 1) * per_client] for c in range(n_clients)], allowed[:len(allowed) - need]
+    if shared:                       # (a smaller machine: fewer cores each, the scorer keeps half)
+        per_client = min(per_client, len(cores) // (2 * n_clients))
+        if per_client <= 0:
+            return None, None
+    need = n_clients * per_client
+    if len(cores) < 2 * need:
+        return None, None
+    tail = cores[len(cores) - need:]
+    plan = [sorted(c for core in tail[i * per_client:(i + 1) * per_client] for c in core) for i in range(n_clients)]
+    if shared:
+        plan = [sorted(c for p in plan for c in p)] * n_clients
+    return plan, sorted(c for core in cores[:len(cores) - need] for c in core)
 
 
 def numa_node_of(cpu: int, sysfs: str = "/sys/devices/system/cpu") -> int:
@@ -362,17 +422,33 @@ def numa_node_of(cpu: int, sysfs: str = "/sys/devices/system/cpu") -> int:
     return -1
 
 
-def cgroup_cpu() -> dict:
-    """The cgroup v2 CPU quota (cpus) and throttling counters of this process (empty if unknown)."""
-    out = {}
+def cgroup_cpu(root: str = "/sys/fs/cgroup") -> dict:
+    """The cgroup v2 CPU quota (cpus) of this process and the throttling counters of the level that
+    sets it: the process's own cgroup and its ancestors up to ``root`` are read, the tightest
+    ``cpu.max`` wins (a box's quota usually sits above the process's own cgroup). Empty if unknown."""
+    out: dict = {}
     try:
         with open("/proc/self/cgroup") as fh:
-            rel = fh.read().strip().split("::")[-1].strip()
-        base = os.path.join("/sys/fs/cgroup", rel.lstrip("/"))
-        with open(os.path.join(base, "cpu.max")) as fh:
-            q, per = fh.read().split()
-            out["quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
-        with open(os.path.join(base, "cpu.stat")) as fh:
+            rel = fh.read().strip().split("::")[-1].strip().strip("/")
+    except OSError:
+        rel = ""
+    parts = rel.split("/") if rel else []
+    best = None
+    for k in range(len(parts), -1, -1):
+        base = os.path.join(root, *parts[:k])
+        try:
+            with open(os.path.join(base, "cpu.max")) as fh:
+                q, per = fh.read().split()
+        except (OSError, ValueError):
+            continue
+        cpus = None if q == "max" else int(q) / int(per)
+        if best is None or (cpus is not None and (best[0] is None or cpus < best[0])):
+            best = (cpus, base)
+    if best is None:
+        return out
+    out["quota_cpus"] = None if best[0] is None else round(best[0], 2)
+    try:
+        with open(os.path.join(best[1], "cpu.stat")) as fh:
             for line in fh:
                 k, v = line.split()
                 if k in ("nr_throttled", "throttled_usec", "usage_usec"):
@@ -380,6 +456,18 @@ def cgroup_cpu() -> dict:
     except (OSError, ValueError):
         pass
     return out
+
+
+def host_cpu_times(path: str = "/proc/stat") -> tuple:
+    """(busy, total) jiffies of the whole host from ``/proc/stat`` (other tenants' work included):
+    the busy-CPU count over an interval is d(busy) / d(total) * CPUs."""
+    try:
+        with open(path) as fh:
+            v = [int(x) for x in fh.readline().split()[1:]]
+    except (OSError, ValueError):
+        return 0, 0
+    idle = v[3] + (v[4] if len(v) > 4 else 0)
+    return sum(v) - idle, sum(v)
 
 
 class ConsumerGroup:
@@ -429,7 +517,7 @@ class ConsumerGroup:
                     "peers": self.peer_sockets}
             self._saved_affinity = None
             plan = None
-            if GROUP_PIN and hasattr(os, "sched_getaffinity"):
+            if GROUP_PIN and confluent and hasattr(os, "sched_getaffinity"):
                 plan, mine = client_cpu_plan(list(os.sched_getaffinity(0)), n_clients)
                 if plan is not None:
                     self._saved_affinity = os.sched_getaffinity(0)
@@ -840,7 +928,7 @@ def _client_run(cfg: dict, spec: dict, conn: Connection, ring: SharedRing, pool)
     return {"outputs": outputs, "t0": t0, "t1": t1, "messages": st["messages"], "produced": st["produced"], "committed": committed,
             "batches": st["batches"], "sent": sent, "explanations": st["explanations"],
             "scorer_batches": list(scorer.sent), "cpu_s": cpu_s, "n_cpus": len(cpus),
-            "cpus": cpus if len(cpus) <= 8 else [], "numa": numa_node_of(cpus[0]) if cpus else -1,
+            "cpus": cpu_list_str(cpus), "numa": numa_node_of(cpus[0]) if cpus else -1,
             "lat_counts": eng.stats.latency.counts.tolist(),
             "lat_n": eng.stats.latency.n, "p50_ms": st["p50_ms"]}
 

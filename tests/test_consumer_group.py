@@ -275,8 +275,26 @@ def test_client_cpu_plan_gives_each_client_its_own_cpus():
     process's (which keeps at least as many); too few CPUs: no pinning."""
     from fraud_detection_spark_kafka_llm_amd.stream.group import client_cpu_plan
 
-    plan, mine = client_cpu_plan(list(range(16)), 3, per_client=2)
+    alone = lambda c: (c,)                      # noqa: E731 (no SMT)
+    plan, mine = client_cpu_plan(list(range(16)), 3, per_client=2, siblings=alone, shared=False)
     assert plan == [[10, 11], [12, 13], [14, 15]] and mine == list(range(10))
     flat = [c for p in plan for c in p]
     assert not set(flat) & set(mine) and len(set(flat)) == 6
-    assert client_cpu_plan(list(range(8)), 3, per_client=2) == (None, None)
+    assert client_cpu_plan(list(range(8)), 3, per_client=2, siblings=alone, shared=False) == (None, None)
+    # SMT: cpu c and c + 16 share a core; a client takes whole cores, the scorer none of them
+    smt = lambda c: (c % 16, c % 16 + 16)       # noqa: E731
+    plan, mine = client_cpu_plan(list(range(32)), 3, per_client=2, siblings=smt, shared=False)
+    assert plan == [[10, 11, 26, 27], [12, 13, 28, 29], [14, 15, 30, 31]]
+    assert mine == list(range(10)) + list(range(16, 26))
+    # siblings outside the allowed set are ignored
+    plan, mine = client_cpu_plan(list(range(16)), 3, per_client=2, siblings=smt, shared=False)
+    assert plan == [[10, 11], [12, 13], [14, 15]]
+    # shared: every client on the pooled cores
+    plan, mine = client_cpu_plan(list(range(16)), 3, per_client=2, siblings=alone, shared=True)
+    assert plan == [list(range(10, 16))] * 3 and mine == list(range(10))
+    # shared on a machine too small for per_client cores each: fewer each, the scorer keeps half
+    plan, mine = client_cpu_plan(list(range(16)), 3, per_client=8, siblings=alone, shared=True)
+    assert plan == [list(range(10, 16))] * 3 and mine == list(range(10))
+    assert client_cpu_plan(list(range(4)), 3, per_client=8, siblings=alone, shared=True) == (None, None)
+    from fraud_detection_spark_kafka_llm_amd.stream.group import cpu_list_str
+    assert cpu_list_str([129, 0, 1, 2, 5, 128]) == "0-2,5,128-129" and cpu_list_str([]) == ""

@@ -146,6 +146,28 @@ def test_gpu_gbdt_native_round_equals_python_levels(monkeypatch):
         assert _booster("cuda:0", depth=depth) == ref_d, depth
 
 
+@pytest.mark.gpu
+def test_gpu_gbdt_large_shard_paths_equal_host(monkeypatch):
+    """the >4M-row regime on small data -- the list kernels' 2048-row waves, no
+    partition row counts (partition_counts_ok false) and the fewest-rows sibling choice -- grows
+    the host's trees bit for bit, with the choice on and off, on the C++ and the Python level loop."""
+    from fraud_detection_spark_kafka_llm_amd.models import grower
+
+    C = native.lib()
+    ref = _booster("cpu")
+    old = C.tree_set_list_big_rows(1000)
+    try:
+        assert C.tree_rg_list_rows(5000) == 2048 and not C.tree_partition_counts_ok(5000)
+        for cxx in (True, False):
+            monkeypatch.setattr(grower, "GBDT_CXX_LEVELS", cxx)
+            for choose in (True, False):
+                monkeypatch.setattr(grower, "GBDT_CHOOSE_ROWS", choose)
+                assert _booster("cuda:0") == ref, (cxx, choose)
+    finally:
+        C.tree_set_list_big_rows(old)
+    assert C.tree_rg_list_rows(5000) == 512
+
+
 def _dp_booster(rank, world, device, cxx, direct=True):
     """One rank's booster under data parallelism, with its collective calls counted."""
     from fraud_detection_spark_kafka_llm_amd.models import grower
