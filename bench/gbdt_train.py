@@ -80,7 +80,10 @@ def main():
     ap.add_argument("--tail-words", type=int, default=30000,
                     help="synthetic long-tail vocabulary (1000000: >200K active features of 2^18)")
     ap.add_argument("--no-warmup", action="store_true", help="skip the untimed warm-up fit (models/warmup.py)")
+    ap.add_argument("--rg-dbg", type=int, default=None, help="grower.RG_DBG (csrc/tree.h RgHistArgs::dbg) for A/Bs")
     args = ap.parse_args()
+    if args.rg_dbg is not None:
+        grower.RG_DBG = args.rg_dbg
     dev = torch.device("cuda:0")
     # CPUs of the GPU's NUMA node, as bench.py does (without it, the first quantize on the box
     # showed a ~0.1 s host stall: profiles/r2s4/NOTES.md)

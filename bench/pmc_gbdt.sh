@@ -15,7 +15,7 @@ for group in "$@"; do
   i=$((i + 1))
   # shellcheck disable=SC2086
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $group --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 bench/gbdt_train.py --no-warmup --rows "$ROWS" --trees "$TREES" > "$OUT/p$i.log" 2>&1
+    python3 bench/gbdt_train.py --no-warmup --rows "$ROWS" --trees "$TREES" ${RG_DBG:+--rg-dbg $RG_DBG} > "$OUT/p$i.log" 2>&1
   dirs+=("$OUT/p$i")
 done
 # the raw per-dispatch CSVs of a 10M-row run exceed what gpurun copies back: keep the summary

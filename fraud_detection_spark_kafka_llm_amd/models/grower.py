@@ -1252,8 +1252,9 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
     """Hands the runner the row-group tables and fixed level buffers of its C++ GBDT level loop
     (RfLevels.gbdt_setup), once per runner; returns the two level-histogram tensors (the root's
     is row 0 of the first, zeroed by the prologue)."""
+    key = (RG_DBG, GBDT_CHOOSE_ROWS, PARTITION_COUNTS, RG_PARTIALS, RG_PARTIALS_MULTI, SPLIT_WIDE)
     cached = getattr(ws, "_gbdt_levels", None)
-    if cached is not None and cached[0] is runner:
+    if cached is not None and cached[0] is runner and cached[2] == key:     # (in-process A/Bs flip these)
         return cached[1]
     dev, TB, D = Q.device, Q.TB, int(params.max_depth)
     # level d opens at most 2^d nodes; even and odd levels alternate between the two tensors
@@ -1272,7 +1273,7 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
         one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff,
         wide=_wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, counted=PARTITION_COUNTS, dbg=RG_DBG,
         part_multi=RG_PARTIALS_MULTI, choose_rows=GBDT_CHOOSE_ROWS))
-    ws._gbdt_levels = (runner, hists)
+    ws._gbdt_levels = (runner, hists, key)
     return hists
 
 
