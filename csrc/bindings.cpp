@@ -442,6 +442,29 @@ void copy_segments(const Tensor& src_row, const Tensor& src_key, const Tensor& s
   }
 }
 
+// The hot features' dense block: dense [nseg, n_pad] uint8 (pre-filled with the zero bins) gets
+// row seg_src[i].. of the CSC (row, bin) of segment i scattered into its row i.
+void dense_scatter(const Tensor& csc_row, const Tensor& csc_bin, const Tensor& seg_src, const Tensor& seg_len,
+                   const Tensor& dense, int64_t max_len) {
+  const auto dev = csc_row.device();
+  for (const Tensor* t : {&csc_bin, &seg_src, &seg_len, &dense}) check_dev(*t, dev, "dense_scatter");
+  TORCH_CHECK(csc_row.scalar_type() == at::kInt && csc_bin.scalar_type() == at::kByte && seg_src.scalar_type() == at::kLong &&
+                  seg_len.scalar_type() == at::kLong && dense.scalar_type() == at::kByte && dense.dim() == 2 &&
+                  dense.is_contiguous() && seg_src.numel() == dense.size(0) && seg_len.numel() == dense.size(0),
+              "dense_scatter: int32 rows, uint8 bins, int64 [nseg] segments, uint8 dense [nseg, n_pad]");
+  const int64_t nseg = dense.size(0), n_pad = dense.size(1);
+  if (dev.is_cuda()) {
+    c10::hip::HIPGuard guard(dev.index());
+    fdx::launch_dense_scatter(csc_row.data_ptr<int32_t>(), csc_bin.data_ptr<uint8_t>(), seg_src.data_ptr<int64_t>(),
+                              seg_len.data_ptr<int64_t>(), nseg, max_len, n_pad, dense.data_ptr<uint8_t>(),
+                              c10::hip::getCurrentHIPStream(dev.index()).stream());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    fdx::dense_scatter_cpu(csc_row.data_ptr<int32_t>(), csc_bin.data_ptr<uint8_t>(), seg_src.data_ptr<int64_t>(),
+                           seg_len.data_ptr<int64_t>(), nseg, n_pad, dense.data_ptr<uint8_t>());
+  }
+}
+
 // Greedy packing of histogram work items (models/quantize.py _finish_items): runs of consecutive
 // packable features, each run at most `pack_keys` keys at the run's largest stride and at most
 // `max_entries` entries. Returns [runs, 3] int64 (first, end, log2 stride). Host-only.
@@ -598,6 +621,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("doc_freq", &doc_freq, "IDF document frequencies (device)");
   m.def("clamp_u8", &clamp_u8, "uint8 clamp (bins)");
   m.def("copy_segments", &copy_segments, "segment copy of (row, key) arrays (+ per-segment key offset)");
+  m.def("dense_scatter", &dense_scatter, "the hot features' dense bin block from their CSC segments");
   m.def("pack_runs", &pack_runs, "greedy packing runs of histogram work items (host)");
   m.def("block_bounds", &block_bounds, "row-block segment bounds of sorted-row columns");
   m.def("feature_order", &feature_order, "CSR -> CSC by feature (radix sort), docFreq and max count per feature");

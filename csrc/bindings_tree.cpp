@@ -1293,6 +1293,7 @@ void register_tree_ops(pybind11::module& m) {
         py::arg("part") = py::none(), py::arg("wg_first") = py::none());
   m.def("tree_rg_erow", &rg_erow);
   m.def("tree_rg_list_rows", [](int64_t N) { return (int64_t)fdx::rg_list_rows(N); });
+  m.def("tree_rg_build_csr_waves", &fdx::rg_build_csr_waves);
   // (tests) rows above which the list kernels take 2048-row waves; returns the previous value
   m.def("tree_set_list_big_rows", [](int64_t n) {
     const int64_t old = fdx::g_rg_list_big_rows;

@@ -69,6 +69,12 @@ template <class V> void feature_order_cpu(const FeatureOrderArgs<V>& a);
 void launch_clamp_u8(const uint8_t* in, int64_t n, uint8_t maxv, uint8_t* out, hipStream_t s);
 void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const int32_t* cols, int32_t ncols, int32_t nblk,
                          int64_t row_block, int64_t* bounds, hipStream_t s);
+// dense[i * n_pad + row[seg_src[i] + k]] = bin[seg_src[i] + k] for k < seg_len[i] (the hot features'
+// dense block; max_len: the longest segment)
+void launch_dense_scatter(const int32_t* row, const uint8_t* bin, const int64_t* seg_src, const int64_t* seg_len,
+                          int64_t nseg, int64_t max_len, int64_t n_pad, uint8_t* dense, hipStream_t s);
+void dense_scatter_cpu(const int32_t* row, const uint8_t* bin, const int64_t* seg_src, const int64_t* seg_len,
+                       int64_t nseg, int64_t n_pad, uint8_t* dense);
 void launch_copy_segments(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,
                           const int64_t* seg_len, int64_t nseg, const uint8_t* seg_add, int32_t* dst_row, uint8_t* dst_key,
                           hipStream_t s);

@@ -73,80 +73,216 @@ __device__ __forceinline__ int32_t rg_count_bin(V c, int32_t max_bin) {
   return b < max_bin ? b : max_bin;
 }
 
-// A wave per 64 consecutive rows, one row at a time, lanes over the row's entries (coalesced CSR
-// reads): each entry's group comes from two small-table lookups, and the entries of one group are
-// counted / placed with one ballot per distinct group among the 64 (lane g keeps group g's
-// count, then cursor, for the current row). Runs keep the CSR order; no LDS, no atomics.
-// (A thread per row streamed ~97 entries serially at 2 blocks per CU: ~0.17 s at 10M rows.)
-constexpr int kRgBuildRowsPerWave = 64;
+// A wave per 16 consecutive rows; their entries are consecutive in the CSR and are taken in chunks
+// of up to 64 (a chunk never crosses a row), lanes over the chunk's entries (coalesced CSR reads).
+// An entry's group comes from a chain of dependent loads (idx -> remap -> fgroup / flocal), so the
+// chunks go through a 3-stage pipeline: the idx / count loads of chunk k + 3, the remap loads of
+// k + 2 and the group loads of k + 1 are in flight while chunk k is placed. The entries of one
+// group are counted / placed with one ballot per distinct group among the 64 lanes (lane g keeps
+// group g's count, then cursor). Runs keep the CSR order; no LDS, no atomics. (A thread per row
+// streamed ~97 entries serially at 2 blocks per CU: ~0.17 s at 10M rows; a wave per 64 rows
+// without the pipeline: 34 ms at 10M rows, latency-bound.)
+constexpr int kRgBuildRowsPerWave = 16;
+// Pass 1 stages a wave's placed entries in LDS (local bin | row in the wave << 16), group by
+// group, and writes each group's run of them with coalesced stores at the end: placing them
+// straight into HBM was 2-byte stores scattered over the groups' regions, 22 ms of the 34 ms
+// build at 10M rows. A wave with more entries than kRgStage places them directly.
+constexpr int kRgStage = 2048;
 
-template <class V>
-__global__ __launch_bounds__(256) void rg_build_csr_kernel(RgCsrBuildArgs<V> a, int pass) {
+__host__ __device__ __forceinline__ int64_t rg_build_waves(int64_t N) {
+  return (N + kRgBuildRowsPerWave - 1) / kRgBuildRowsPerWave;
+}
+
+template <class V, int pass>
+__device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, uint32_t* stage) {
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
+  const int64_t wstride = rg_build_waves(a.N) + 1;      // wave_base [G][waves + 1] (+ the totals)
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t r0 = wave * kRgBuildRowsPerWave;
   if (r0 >= a.N) return;
-  const int64_t r1 = r0 + kRgBuildRowsPerWave < a.N ? r0 + kRgBuildRowsPerWave : a.N;
+  const int R = (int)(r0 + kRgBuildRowsPerWave < a.N ? kRgBuildRowsPerWave : a.N - r0);
+  // lane j <= R: the start of row r0 + j (row j's entries: [start(j), start(j + 1)))
+  const int64_t rb = lane <= R ? a.indptr[r0 + lane] : 0;
+  auto start = [&](int j) -> int64_t {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rb, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)rb >> 32), j);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  struct Chunk {
+    int j;                         // row (R: past the wave's last chunk)
+    int64_t e, end;                // entries [e, min(e + 64, end))
+  };
+  auto settle = [&](Chunk c) {     // skip past rows without (further) entries
+    while (c.j < R && c.e >= c.end) {
+      ++c.j;
+      if (c.j < R) {
+        c.e = start(c.j);
+        c.end = start(c.j + 1);
+      }
+    }
+    return c;
+  };
+  auto next = [&](Chunk c) {
+    if (c.j >= R) return c;
+    c.e += 64;
+    return settle(c);
+  };
+  // stage 1: ids and counts; stage 2: active index; stage 3: group and local bin
+  auto load_ids = [&](const Chunk& c, int32_t& id, V& cnt) {
+    const int64_t e = c.e + lane;
+    const bool ok = c.j < R && e < c.end;
+    id = ok ? a.idx[e] : -1;
+    cnt = (ok && pass == 1) ? a.counts[e] : (V)0;
+  };
+  auto load_fa = [&](int32_t id) -> int32_t { return id >= 0 ? a.remap[id] : -1; };
+  auto load_group = [&](int32_t fa, V cnt, int32_t& g, int32_t& loc) {
+    g = fa >= 0 ? a.fgroup[fa] : -1;
+    loc = (pass == 1 && g >= 0) ? a.flocal[fa] + rg_count_bin<V>(cnt, a.max_bin) : 0;
+  };
   // lane l: the running count over the wave's rows (pass 0), then the next position (pass 1), of
   // group l (run0) and of group l + 64 (run1)
   const int ga = lane, gb = lane + 64;
-  uint32_t run0 = (pass == 1 && ga < a.G) ? a.wave_base[wave * a.G + ga] : 0u;
-  uint32_t run1 = (pass == 1 && gb < a.G) ? a.wave_base[wave * a.G + gb] : 0u;
-  for (int64_t r = r0; r < r1; ++r) {
-    const int64_t e0 = a.indptr[r], e1 = a.indptr[r + 1];
-    if (pass == 1) {
-      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + r] = run0;
-      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + r] = run1;
+  // pass 1: the wave's bases and counts per group; staged: run0 / run1 count from the group's
+  // offset in the stage (sh0 / sh1 turn them back into group positions)
+  uint32_t wb0 = 0, wb1 = 0, c0n = 0, c1n = 0;
+  if (pass == 1) {
+    if (ga < a.G) {
+      wb0 = a.wave_base[ga * wstride + wave];
+      c0n = a.wave_base[ga * wstride + wave + 1] - wb0;
     }
-    for (int64_t eb = e0; eb < e1; eb += 64) {
-      const int64_t e = eb + lane;
-      int32_t g = -1, loc = 0;
-      if (e < e1) {
-        const int32_t fa = a.remap[a.idx[e]];
-        if (fa >= 0) {
-          g = a.fgroup[fa];
-          if (pass == 1 && g >= 0) loc = a.flocal[fa] + rg_count_bin<V>(a.counts[e], a.max_bin);
-        }
-      }
-      uint64_t act = __ballot(g >= 0);
-      while (act) {
-        const int32_t gs = __shfl(g, __ffsll((unsigned long long)act) - 1, 64);
-        const uint64_t m = __ballot(g == gs);
-        const int owner = gs & 63;
-        if (pass == 1) {
-          const uint32_t base = gs < 64 ? __shfl(run0, owner, 64) : __shfl(run1, owner, 64);
-          if (g == gs) {
+    if (gb < a.G) {
+      wb1 = a.wave_base[gb * wstride + wave];
+      c1n = a.wave_base[gb * wstride + wave + 1] - wb1;
+    }
+  }
+  uint32_t o0 = c0n, o1 = c1n;               // inclusive, then exclusive offsets in the stage
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t x0 = __shfl_up(o0, d, 64), x1 = __shfl_up(o1, d, 64);
+    if (lane >= d) {
+      o0 += x0;
+      o1 += x1;
+    }
+  }
+  const uint32_t tot0 = __shfl(o0, 63, 64);
+  o0 -= c0n;
+  o1 += tot0 - c1n;
+  const bool staged = pass == 1 && tot0 + __shfl(o1 + c1n, 63, 64) - tot0 <= (uint32_t)kRgStage;
+  uint32_t run0 = pass == 1 ? (staged ? o0 : wb0) : 0u;
+  uint32_t run1 = pass == 1 ? (staged ? o1 : wb1) : 0u;
+  const uint32_t sh0 = staged ? wb0 - o0 : 0u, sh1 = staged ? wb1 - o1 : 0u;
+  int pj = 0;                      // (pass 1) rows whose run starts are not written yet: pj..
+  auto write_starts = [&](int upto) {   // rows pj .. upto - 1 start at the current counts
+    for (; pj < upto; ++pj) {
+      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + r0 + pj] = run0 + sh0;
+      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + r0 + pj] = run1 + sh1;
+    }
+  };
+  Chunk c0 = settle(Chunk{0, start(0), start(1)});
+  Chunk c1 = next(c0), c2 = next(c1);
+  int32_t id0, id1, id2, fa0, fa1, g0, loc0;
+  V n0, n1, n2;
+  load_ids(c0, id0, n0);
+  load_ids(c1, id1, n1);
+  load_ids(c2, id2, n2);
+  fa0 = load_fa(id0);
+  fa1 = load_fa(id1);
+  load_group(fa0, n0, g0, loc0);
+  while (c0.j < R) {
+    const Chunk c3 = next(c2);
+    int32_t id3;
+    V n3;
+    load_ids(c3, id3, n3);                     // chunk k + 3
+    const int32_t fa2 = load_fa(id2);          // chunk k + 2
+    int32_t g1, loc1;
+    load_group(fa1, n1, g1, loc1);             // chunk k + 1
+    // chunk k: place (pass 1) / count its entries
+    if (pass == 1) write_starts(c0.j + 1);
+    const int64_t r = r0 + c0.j;
+    uint64_t act = __ballot(g0 >= 0);
+    while (act) {
+      const int32_t gs = __shfl(g0, __ffsll((unsigned long long)act) - 1, 64);
+      const uint64_t m = __ballot(g0 == gs);
+      const int owner = gs & 63;
+      if (pass == 1) {
+        const uint32_t base = gs < 64 ? __shfl(run0, owner, 64) : __shfl(run1, owner, 64);
+        if (g0 == gs) {
+          if (staged) {
+            stage[base + __popcll(m & lt)] = (uint32_t)loc0 | ((uint32_t)c0.j << 16);
+          } else {
             const int64_t pos = a.gbase[gs] + base + __popcll(m & lt);
-            a.ent[pos] = (uint16_t)loc;
+            a.ent[pos] = (uint16_t)loc0;
             if (a.erow != nullptr && gs >= a.em_g0) a.erow[pos - a.ebase] = (uint32_t)r;
           }
         }
-        if (lane == owner) {
-          if (gs < 64) run0 += __popcll(m);
-          else run1 += __popcll(m);
-        }
-        act &= ~m;
       }
+      if (lane == owner) {
+        if (gs < 64) run0 += __popcll(m);
+        else run1 += __popcll(m);
+      }
+      act &= ~m;
     }
+    c0 = c1;
+    g0 = g1;
+    loc0 = loc1;
+    c1 = c2;
+    fa1 = fa2;
+    n1 = n2;
+    c2 = c3;
+    id2 = id3;
+    n2 = n3;
   }
   if (pass == 0) {
-    if (ga < a.G) a.wave_base[wave * a.G + ga] = run0;                    // the wave's totals
-    if (gb < a.G) a.wave_base[wave * a.G + gb] = run1;
-  } else if (r1 == a.N) {                                                 // the groups' ends
-    if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + a.N] = run0;
-    if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + a.N] = run1;
+    if (ga < a.G) a.wave_base[ga * wstride + wave] = run0;                // the wave's totals
+    if (gb < a.G) a.wave_base[gb * wstride + wave] = run1;
+  } else {
+    write_starts(R);                                                      // (trailing empty rows)
+    if (staged) {                  // each group's staged run to its place, coalesced
+      __builtin_amdgcn_s_waitcnt(0xc07f);                                 // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+      for (int g = 0; g < a.G; ++g) {
+        const int src = g & 63;
+        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)(g < 64 ? c0n : c1n), src);
+        if (cnt == 0) continue;
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)(g < 64 ? o0 : o1), src);
+        const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)(g < 64 ? wb0 : wb1), src);
+        const int64_t dst = a.gbase[g] + wb;
+        const bool rows = a.erow != nullptr && g >= a.em_g0;
+        for (uint32_t i = lane; i < cnt; i += 64) {
+          const uint32_t v = stage[off + i];
+          a.ent[dst + i] = (uint16_t)(v & 0xffffu);
+          if (rows) a.erow[dst + i - a.ebase] = (uint32_t)(r0 + (v >> 16));
+        }
+      }
+    }
+    if (r0 + R == a.N) {                                                  // the groups' ends
+      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + a.N] = run0 + sh0;
+      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + a.N] = run1 + sh1;
+    }
   }
+}
+
+template <class V>
+__global__ __launch_bounds__(256) void rg_build_csr_count_kernel(RgCsrBuildArgs<V> a) {
+  rg_build_csr_wave<V, 0>(a, nullptr);
+}
+
+template <class V>
+__global__ __launch_bounds__(256) void rg_build_csr_place_kernel(RgCsrBuildArgs<V> a) {
+  __shared__ uint32_t stage[4][kRgStage];
+  rg_build_csr_wave<V, 1>(a, stage[threadIdx.x >> 6]);
 }
 
 // Block g: group g's per-wave totals -> exclusive per-wave bases (in place).
 __global__ __launch_bounds__(1024) void rg_build_scan_kernel(uint32_t* wave_base, int64_t nwaves, int32_t G) {
   __shared__ uint32_t s_sum[1024];
   const int g = blockIdx.x, t = threadIdx.x;
+  uint32_t* wbg = wave_base + (int64_t)g * (nwaves + 1);      // group g's waves, then its total
   const int64_t per = (nwaves + 1023) / 1024;
   const int64_t w0 = t * per, w1 = w0 + per < nwaves ? w0 + per : nwaves;
   uint32_t sum = 0;
-  for (int64_t w = w0; w < w1; ++w) sum += wave_base[w * G + g];
+  for (int64_t w = w0; w < w1; ++w) sum += wbg[w];
   s_sum[t] = sum;
   __syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {
@@ -157,10 +293,11 @@ __global__ __launch_bounds__(1024) void rg_build_scan_kernel(uint32_t* wave_base
   }
   uint32_t acc = s_sum[t] - sum;
   for (int64_t w = w0; w < w1; ++w) {
-    const uint32_t c = wave_base[w * G + g];
-    wave_base[w * G + g] = acc;
+    const uint32_t c = wbg[w];
+    wbg[w] = acc;
     acc += c;
   }
+  if (t == 1023) wbg[nwaves] = s_sum[1023];
 }
 
 // One wave per rg_list_rows(N) consecutive rows (its row_node / slot loads issued 8 steps at a time), slots
@@ -715,14 +852,14 @@ void launch_rg_build(const RgBuildArgs& a, int pass, hipStream_t s) {
 
 template <class V>
 void launch_rg_build_csr(const RgCsrBuildArgs<V>& a, hipStream_t s) {
-  const int64_t waves = (a.N + kRgBuildRowsPerWave - 1) / kRgBuildRowsPerWave;
+  const int64_t waves = rg_build_waves(a.N);
   const int64_t blocks = (waves + 3) / 4;
   if (blocks <= 0) return;
-  hipLaunchKernelGGL(rg_build_csr_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);
+  hipLaunchKernelGGL(rg_build_csr_count_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
   hipLaunchKernelGGL(rg_build_scan_kernel, dim3((unsigned)a.G), dim3(1024), 0, s, a.wave_base, waves, a.G);
-  hipLaunchKernelGGL(rg_build_csr_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a, 1);
+  hipLaunchKernelGGL(rg_build_csr_place_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }
-int64_t rg_build_csr_waves(int64_t N) { return (N + kRgBuildRowsPerWave - 1) / kRgBuildRowsPerWave; }
+int64_t rg_build_csr_waves(int64_t N) { return rg_build_waves(N) + 1; }     // (per group: the waves + the total)
 template void launch_rg_build_csr<float>(const RgCsrBuildArgs<float>&, hipStream_t);
 template void launch_rg_build_csr<double>(const RgCsrBuildArgs<double>&, hipStream_t);
 template void launch_rg_build_csr<int32_t>(const RgCsrBuildArgs<int32_t>&, hipStream_t);

@@ -128,6 +128,20 @@ __global__ __launch_bounds__(256) void copy_segments_kernel(const int32_t* __res
   }
 }
 
+// The dense block of the hot features (models/quantize.py _build_dense): segment i (= hot feature
+// i's CSC range) scatters its entries' bins into row i of dense [nseg, n_pad] (pre-filled with the
+// features' zero bins). Workgroups (x, i): a grid-stride over segment i's entries.
+__global__ __launch_bounds__(256) void dense_scatter_kernel(const int32_t* __restrict__ row, const uint8_t* __restrict__ bin,
+                                                            const int64_t* __restrict__ seg_src,
+                                                            const int64_t* __restrict__ seg_len, int64_t n_pad,
+                                                            uint8_t* __restrict__ dense) {
+  const int64_t i = blockIdx.y;
+  const int64_t a = seg_src[i], n = seg_len[i];
+  uint8_t* out = dense + i * n_pad;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256)
+    out[row[a + k]] = bin[a + k];
+}
+
 __global__ __launch_bounds__(256) void clamp_u8_kernel(const uint8_t* __restrict__ in, int64_t n, uint8_t maxv,
                                                        uint8_t* __restrict__ out) {
   const int64_t n16 = n / 16;
@@ -195,6 +209,14 @@ void launch_block_bounds(const int32_t* csc_row, const int64_t* colptr, const in
   if (n > 0)
     hipLaunchKernelGGL(block_bounds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, csc_row, colptr, cols, ncols,
                        nblk, row_block, bounds);
+}
+
+void launch_dense_scatter(const int32_t* row, const uint8_t* bin, const int64_t* seg_src, const int64_t* seg_len,
+                          int64_t nseg, int64_t max_len, int64_t n_pad, uint8_t* dense, hipStream_t s) {
+  if (nseg <= 0 || max_len <= 0) return;
+  const int64_t bx = (max_len + 255) / 256;
+  hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)(bx < 256 ? bx : 256), (unsigned)nseg), dim3(256), 0, s, row, bin,
+                     seg_src, seg_len, n_pad, dense);
 }
 
 void launch_copy_segments(const int32_t* src_row, const uint8_t* src_key, const int64_t* seg_src, const int64_t* seg_dst,

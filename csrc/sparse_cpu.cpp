@@ -144,6 +144,14 @@ void copy_segments_cpu(const int32_t* src_row, const uint8_t* src_key, const int
   });
 }
 
+void dense_scatter_cpu(const int32_t* row, const uint8_t* bin, const int64_t* seg_src, const int64_t* seg_len,
+                       int64_t nseg, int64_t n_pad, uint8_t* dense) {
+  parallel_for(nseg, 0, 1, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i)
+      for (int64_t k = 0; k < seg_len[i]; ++k) dense[i * n_pad + row[seg_src[i] + k]] = bin[seg_src[i] + k];
+  });
+}
+
 template void feature_order_cpu<float>(const FeatureOrderArgs<float>&);
 template void feature_order_cpu<double>(const FeatureOrderArgs<double>&);
 template void feature_order_cpu<int32_t>(const FeatureOrderArgs<int32_t>&);

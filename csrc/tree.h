@@ -237,7 +237,7 @@ struct RgCsrBuildArgs {
   uint32_t* ptr;                  // [G][N + 1] out: exclusive starts of every (group, row) run
   const int64_t* gbase;
   uint16_t* ent;                  // out
-  uint32_t* wave_base;            // [ceil(N / 64)][G] scratch: per-wave group totals, then bases
+  uint32_t* wave_base;            // [G][waves + 1] scratch: per-wave group totals, then bases (+ totals)
   uint32_t* erow;                 // optional out: erow[gbase[g] - ebase + k] = row of entry k of
   int32_t em_g0;                  //   group g >= em_g0 (the entry-major rows, RgHistArgs::erow)
   int64_t ebase;

@@ -277,7 +277,7 @@ class RowGroups:
             indptr, idx, counts, max_bins = csr
             remap = torch.full((Q.num_features,), -1, dtype=torch.int32, device=dev)
             remap[Q.fid_orig] = torch.arange(Q.Fa, dtype=torch.int32, device=dev)
-            work = torch.empty(G * -(-N // 64), dtype=torch.int32, device=dev)
+            work = torch.empty(G * C.tree_rg_build_csr_waves(N), dtype=torch.int32, device=dev)
             C.tree_rg_build_csr(indptr, idx, counts, remap, max_bins - 1, fg_t, fl_t, ptr, self.gbase, self.ent,
                                 work, self.erow, self.em_g0, self.ebase)      # (erow written in the pass)
             self.ptr = ptr
@@ -718,13 +718,15 @@ def _build_dense(Q: Quantized, hot: np.ndarray) -> None:
     if not hot.size:
         Q.dense = None
         return
-    zb = Q.zbin.cpu().numpy()[Q.hot]
-    dense = torch.empty((hot.size, Q.n_pad), dtype=torch.uint8, device=Q.device)
+    dev = Q.device
+    hot_t = torch.from_numpy(Q.hot).to(dev)
+    # every column filled with its zero bin, then the hot features' CSC entries scattered: two
+    # launches (a fill + index_copy per feature was ~290 launches, ~2 ms a fit)
+    dense = Q.zbin[hot_t].to(torch.uint8)[:, None].expand(hot.size, Q.n_pad).contiguous()
     colptr = Q.colptr.cpu().numpy()
-    for d, f in enumerate(Q.hot.tolist()):
-        dense[d].fill_(int(zb[d]))
-        a, b = int(colptr[f]), int(colptr[f + 1])
-        dense[d].index_copy_(0, Q.csc_row[a:b].to(torch.int64), Q.csc_bin[a:b])
+    seg_src = torch.from_numpy(colptr[Q.hot]).to(dev)
+    lens = colptr[Q.hot + 1] - colptr[Q.hot]
+    native.lib().dense_scatter(Q.csc_row, Q.csc_bin, seg_src, torch.from_numpy(lens).to(dev), dense, int(lens.max()))
     Q.dense = dense
 
 
