@@ -541,6 +541,14 @@ void rg_build_csr_t(const Tensor& indptr, const Tensor& idx, const Tensor& count
   }
   if (dev.is_cuda()) {
     c10::hip::HIPGuard guard(dev.index());
+    // one [F] lookup instead of the remap -> fgroup / flocal chain (freed in stream order)
+    Tensor fgl = at::full({remap.numel()}, -1, remap.options());
+    if (fgroup.numel() > 0) {
+      const Tensor fa = remap.clamp_min(0).to(at::kLong);
+      const Tensor g = fgroup.index_select(0, fa), l = flocal.index_select(0, fa);
+      fgl = at::where((remap >= 0) & (g >= 0), g.__lshift__(16).bitwise_or(l), fgl).contiguous();
+    }
+    a.fgl = fgl.data_ptr<int32_t>();
     fdx::launch_rg_build_csr<V>(a, stream(dev));
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {

@@ -233,11 +233,13 @@ struct RgCsrBuildArgs {
   int32_t max_bin;                // max_bins - 1
   const int32_t* fgroup;          // [Fa]
   const int32_t* flocal;          // [Fa]
+  const int32_t* fgl;             // (device) [F] group << 16 | local offset of each feature, -1:
+                                  //   none (remap, fgroup and flocal folded into one lookup)
   int32_t G;
   uint32_t* ptr;                  // [G][N + 1] out: exclusive starts of every (group, row) run
   const int64_t* gbase;
   uint16_t* ent;                  // out
-  uint32_t* wave_base;            // [G][waves + 1] scratch: per-wave group totals, then bases (+ totals)
+  uint32_t* wave_base;            // [G][stride] scratch: per-wave group totals, then bases (+ totals)
   uint32_t* erow;                 // optional out: erow[gbase[g] - ebase + k] = row of entry k of
   int32_t em_g0;                  //   group g >= em_g0 (the entry-major rows, RgHistArgs::erow)
   int64_t ebase;
