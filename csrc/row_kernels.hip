@@ -77,11 +77,11 @@ __device__ __forceinline__ int32_t rg_count_bin(V c, int32_t max_bin) {
 // of up to 64 (a chunk never crosses a row), lanes over the chunk's entries (coalesced CSR reads).
 // An entry's group and local offset come from one [F] lookup (fgl) of its feature id, so the chunks
 // go through a 2-stage pipeline: the id / count loads of chunk k + 2 and the lookups of k + 1 are
-// in flight while chunk k is placed. The entries of one
-// group are counted / placed with one ballot per distinct group among the 64 lanes (lane g keeps
-// group g's count, then cursor). Runs keep the CSR order; no LDS, no atomics. (A thread per row
-// streamed ~97 entries serially at 2 blocks per CU: ~0.17 s at 10M rows; a wave per 64 rows
-// without the pipeline: 34 ms at 10M rows, latency-bound.)
+// in flight while chunk k is placed. Every lane finds the lanes of its own group with one ballot
+// per bit of the group id (4 for 11 groups; a ballot per distinct group was ~9 a chunk) and the
+// groups' counts, then cursors, live in a per-wave LDS row. Runs keep the CSR order; no atomics.
+// (A thread per row streamed ~97 entries serially at 2 blocks per CU: ~0.17 s at 10M rows; a wave
+// per 64 rows, one row at a time: 34 ms.)
 constexpr int kRgBuildRowsPerWave = 16;
 // Pass 1 stages a wave's placed entries in LDS (local bin | row in the wave << 16), group by
 // group, and writes each group's run of them with coalesced stores at the end: placing them
@@ -96,7 +96,7 @@ __host__ __device__ __forceinline__ int64_t rg_build_waves(int64_t N) {
 __host__ __device__ __forceinline__ int64_t rg_build_stride(int64_t nwaves) { return (nwaves + 1 + 3) / 4 * 4; }
 
 template <class V, int pass>
-__device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, uint32_t* stage) {
+__device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, uint32_t* stage, uint32_t* runs) {
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int64_t wstride = rg_build_stride(rg_build_waves(a.N));   // wave_base [G][stride] (+ the totals)
@@ -142,8 +142,8 @@ __device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, ui
     g = v >= 0 ? (v >> 16) : -1;
     loc = (pass == 1 && g >= 0) ? (v & 0xffff) + rg_count_bin<V>(cnt, a.max_bin) : 0;
   };
-  // lane l: the running count over the wave's rows (pass 0), then the next position (pass 1), of
-  // group l (run0) and of group l + 64 (run1)
+  // runs[g] (the wave's LDS row): group g's running count over the wave's rows (pass 0), then its
+  // next position (pass 1)
   const int ga = lane, gb = lane + 64;
   // pass 1: the wave's bases and counts per group; staged: run0 / run1 count from the group's
   // offset in the stage (sh0 / sh1 turn them back into group positions)
@@ -171,14 +171,16 @@ __device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, ui
   o0 -= c0n;
   o1 += tot0 - c1n;
   const bool staged = pass == 1 && tot0 + __shfl(o1 + c1n, 63, 64) - tot0 <= (uint32_t)kRgStage;
-  uint32_t run0 = pass == 1 ? (staged ? o0 : wb0) : 0u;
-  uint32_t run1 = pass == 1 ? (staged ? o1 : wb1) : 0u;
+  runs[ga] = pass == 1 ? (staged ? o0 : wb0) : 0u;
+  runs[gb] = pass == 1 ? (staged ? o1 : wb1) : 0u;
   const uint32_t sh0 = staged ? wb0 - o0 : 0u, sh1 = staged ? wb1 - o1 : 0u;
+  // bits of a group id: one ballot per bit gives every lane the lanes of its own group
+  const int nbits = a.G > 1 ? 32 - __clz((unsigned)(a.G - 1)) : 0;
   int pj = 0;                      // (pass 1) rows whose run starts are not written yet: pj..
   auto write_starts = [&](int upto) {   // rows pj .. upto - 1 start at the current counts
     for (; pj < upto; ++pj) {
-      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + r0 + pj] = run0 + sh0;
-      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + r0 + pj] = run1 + sh1;
+      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + r0 + pj] = runs[ga] + sh0;
+      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + r0 + pj] = runs[gb] + sh1;
     }
   };
   Chunk c0 = settle(Chunk{0, start(0), start(1)});
@@ -198,28 +200,26 @@ __device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, ui
     // chunk k: place (pass 1) / count its entries
     if (pass == 1) write_starts(c0.j + 1);
     const int64_t r = r0 + c0.j;
-    uint64_t act = __ballot(g0 >= 0);
-    while (act) {
-      const int32_t gs = __shfl(g0, __ffsll((unsigned long long)act) - 1, 64);
-      const uint64_t m = __ballot(g0 == gs);
-      const int owner = gs & 63;
+    const bool act = g0 >= 0;
+    uint64_t same = __ballot(act);             // -> the lanes whose group is this lane's
+    for (int b = 0; b < nbits; ++b) {
+      const bool bit = (g0 >> b) & 1;
+      const uint64_t mb = __ballot(act && bit);
+      same &= bit ? mb : ~mb;
+    }
+    if (act) {
+      const uint32_t rank = __popcll(same & lt);
+      const uint32_t base = runs[g0];          // (every lane reads before the leaders write)
       if (pass == 1) {
-        const uint32_t base = gs < 64 ? __shfl(run0, owner, 64) : __shfl(run1, owner, 64);
-        if (g0 == gs) {
-          if (staged) {
-            stage[base + __popcll(m & lt)] = (uint32_t)loc0 | ((uint32_t)c0.j << 16);
-          } else {
-            const int64_t pos = a.gbase[gs] + base + __popcll(m & lt);
-            a.ent[pos] = (uint16_t)loc0;
-            if (a.erow != nullptr && gs >= a.em_g0) a.erow[pos - a.ebase] = (uint32_t)r;
-          }
+        if (staged) {
+          stage[base + rank] = (uint32_t)loc0 | ((uint32_t)c0.j << 16);
+        } else {
+          const int64_t pos = a.gbase[g0] + base + rank;
+          a.ent[pos] = (uint16_t)loc0;
+          if (a.erow != nullptr && g0 >= a.em_g0) a.erow[pos - a.ebase] = (uint32_t)r;
         }
       }
-      if (lane == owner) {
-        if (gs < 64) run0 += __popcll(m);
-        else run1 += __popcll(m);
-      }
-      act &= ~m;
+      if (rank == 0) runs[g0] = base + __popcll(same);
     }
     c0 = c1;
     g0 = g1;
@@ -229,8 +229,8 @@ __device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, ui
     n1 = n2;
   }
   if (pass == 0) {
-    if (ga < a.G) a.wave_base[ga * wstride + wave] = run0;                // the wave's totals
-    if (gb < a.G) a.wave_base[gb * wstride + wave] = run1;
+    if (ga < a.G) a.wave_base[ga * wstride + wave] = runs[ga];            // the wave's totals
+    if (gb < a.G) a.wave_base[gb * wstride + wave] = runs[gb];
   } else {
     write_starts(R);                                                      // (trailing empty rows)
     if (staged) {                  // each group's staged run to its place, coalesced
@@ -252,21 +252,23 @@ __device__ __forceinline__ void rg_build_csr_wave(const RgCsrBuildArgs<V>& a, ui
       }
     }
     if (r0 + R == a.N) {                                                  // the groups' ends
-      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + a.N] = run0 + sh0;
-      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + a.N] = run1 + sh1;
+      if (ga < a.G) a.ptr[(int64_t)ga * (a.N + 1) + a.N] = runs[ga] + sh0;
+      if (gb < a.G) a.ptr[(int64_t)gb * (a.N + 1) + a.N] = runs[gb] + sh1;
     }
   }
 }
 
 template <class V>
 __global__ __launch_bounds__(256) void rg_build_csr_count_kernel(RgCsrBuildArgs<V> a) {
-  rg_build_csr_wave<V, 0>(a, nullptr);
+  __shared__ uint32_t runs[4][128];
+  rg_build_csr_wave<V, 0>(a, nullptr, runs[threadIdx.x >> 6]);
 }
 
 template <class V>
 __global__ __launch_bounds__(256) void rg_build_csr_place_kernel(RgCsrBuildArgs<V> a) {
   __shared__ uint32_t stage[4][kRgStage];
-  rg_build_csr_wave<V, 1>(a, stage[threadIdx.x >> 6]);
+  __shared__ uint32_t runs[4][128];
+  rg_build_csr_wave<V, 1>(a, stage[threadIdx.x >> 6], runs[threadIdx.x >> 6]);
 }
 
 // Block g: group g's per-wave totals -> exclusive per-wave bases (in place), the group's total
