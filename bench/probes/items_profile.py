@@ -24,6 +24,18 @@ def main():
     warm_tree_kernels(dev, gbdt_depth=0, forest_depth=5, forest_subset="sqrt")
     vc, y, _ = _tfidf(rows, dev, seed=21, times={})
     torch.cuda.synchronize()
+    if os.environ.get("WARM_BIG_OPS") == "1":     # (large-size torch kernels loaded: A/B)
+        n = torch.ones(3_000_000, dtype=torch.int64, device=dev)
+        c = torch.cumsum(n, 0)
+        r = torch.repeat_interleave(torch.arange(3_000_000, device=dev), n, output_size=3_000_000)
+        torch.minimum(c[r] - r, torch.full_like(r, 8192))
+        torch.cuda.synchronize()
+    pre = float(os.environ.get("PREALLOC_GB", 0))
+    if pre > 0:       # (a cached-allocator segment of this size made and freed: fresh-memory A/B)
+        x = torch.empty(int(pre * 2 ** 30), dtype=torch.uint8, device=dev)
+        x.fill_(0)
+        del x
+        torch.cuda.synchronize()
     for rep in range(2):
         t0 = time.perf_counter()
         Q, _, _, _ = prepare(vc, y, dev, 32)

@@ -921,7 +921,9 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
     # --- the histogram CSC: (row, kbase + bin) of every (super-block, feature) segment
     if S:
         with tracing.span("q.copy"):
-            kb = torch.from_numpy(np.tile(kbase[cols], nsb).astype(np.uint8)).to(dev) if kbase.any() else None
+            # (the per-feature key bases copied once and tiled over the super-blocks on the device: a
+            # host tile and its pageable copy cost ~25 ms in a process's first build)
+            kb = torch.from_numpy(kbase[cols].astype(np.uint8)).to(dev).repeat(nsb) if kbase.any() else None
             # a workgroup per <= COPY_PIECE entries: the hot features' segments hold ~10^5 entries
             # each, and a workgroup per segment left the copy to its longest ones (~20 ms at 10M rows)
             src_p, dst_p, len_p = seg_src.reshape(-1), seg_dst, flat
@@ -933,6 +935,7 @@ def _build_items(Q: Quantized, chunk: int, super_rows: int, hot: np.ndarray) -> 
                 src_p, dst_p = src_p[rep] + k, dst_p[rep] + k
                 len_p = torch.minimum(len_p[rep] - k, torch.full_like(k, COPY_PIECE))
                 kb = kb[rep] if kb is not None else None
+            ck("copy_pieces")
             C.copy_segments(Q.csc_row, Q.csc_bin, src_p.contiguous(), dst_p.contiguous(), len_p.contiguous(),
                             h_row[:total], h_key[:total], kb.contiguous() if kb is not None else None)
     ck("copy")
