@@ -339,10 +339,12 @@ def _group_confluent_runs(args, grp) -> dict:
     tp = tps[1]
     cg1, h1, w1 = G.cgroup_cpu(), G.host_cpu_times(), time.perf_counter()
     host_busy = (h1[0] - h0[0]) / max(h1[1] - h0[1], 1) * (os.cpu_count() or 1)
-    lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat")
+    lat = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat",
+                              max_latency_ms=args.kafka_confluent_fill_ms)
     # the config's LLM-explain stub: every 10th classification explained asynchronously in the
     # clients (offline stub backend), its record produced after the classification
     ex = G.group_latency_run(grp, args.kafka_group_rate, args.kafka_sec, tag="lat-explain", explain="async",
+                             max_latency_ms=args.kafka_confluent_fill_ms,
                              explain_every=10)
     place = {"kafka_confluent_group_client_dialogues_per_s": [round(v) for v in tp["client_dialogues_per_s"]],
              "kafka_confluent_group_client_cpu_util": tp["client_cpu_util"],
@@ -411,7 +413,7 @@ def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
     tps.sort(key=lambda r: r["dialogues_per_s"])
     tp = tps[1]
     gc.collect()
-    lat = loadgen.latency_run(make(4096, 1.0), pool, args.kafka_rate, args.kafka_sec,
+    lat = loadgen.latency_run(make(4096, args.kafka_fill_ms), pool, args.kafka_rate, args.kafka_sec,
                               url=f"memory://bench-lat-{rank}")
     ok = tp["produced"] == args.kafka_msgs and tp["committed"] == args.kafka_msgs and lat["produced"] == lat["sent"]
     conf = {}
@@ -424,7 +426,8 @@ def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
         ctp = loadgen.throughput_run(make(16384, 5.0), pool, args.kafka_confluent_msgs,
                                      url=f"memory://bench-ctp-{rank}", confluent=True)
         gc.collect()
-        clat = loadgen.latency_run(make(4096, 1.0), pool, args.kafka_confluent_rate, args.kafka_sec,
+        clat = loadgen.latency_run(make(4096, args.kafka_confluent_fill_ms), pool, args.kafka_confluent_rate,
+                                   args.kafka_sec,
                                    url=f"memory://bench-clat-{rank}", confluent=True)
         ok = ok and ctp["produced"] == ctp["committed"] == args.kafka_confluent_msgs and \
             clat["produced"] == clat["sent"]
@@ -437,6 +440,7 @@ def kafka_phase(args, spec, idf_np, model, dev, rank: int) -> dict:
             "kafka_runs_dialogues_per_s": [round(r["dialogues_per_s"]) for r in tps],
             "kafka_throughput_sec": tp["sec"], "kafka_p50_ms": lat["p50_ms"], "kafka_p95_ms": lat["p95_ms"],
             "kafka_p99_ms": lat["p99_ms"], "kafka_offered_per_s": args.kafka_rate,
+            "kafka_latency_fill_ms": args.kafka_fill_ms, "kafka_confluent_latency_fill_ms": args.kafka_confluent_fill_ms,
             "kafka_latency_msgs": lat["sent"], "kafka_all_delivered_and_committed": bool(ok),
             "kafka_avg_record_bytes": round(pool.avg_bytes, 1), "kafka_api": "columnar (in-memory broker)", **conf}
 
@@ -457,6 +461,11 @@ def main():
     ap.add_argument("--kafka-msgs", type=int, default=1_000_000, help="records drained in the Kafka throughput run")
     ap.add_argument("--kafka-rate", type=float, default=300_000, help="paced producer rate of the latency run")
     ap.add_argument("--kafka-sec", type=float, default=2.0, help="duration of the latency run")
+    ap.add_argument("--kafka-fill-ms", type=float, default=1.0,
+                    help="micro-batch fill deadline of the columnar engine's latency run (throughput runs: 5 ms)")
+    ap.add_argument("--kafka-confluent-fill-ms", type=float, default=0.5,
+                    help="... of the confluent-surface latency runs (one process, the group): per-record client "
+                         "work queues behind a longer fill (profiles/r6/kafka/fill_ab.jsonl)")
     ap.add_argument("--kafka-multi-msgs", type=int, default=1_000_000,
                     help="records of the shared 3-partition topic drained by rank 0 over every GPU (0: skip)")
     ap.add_argument("--kafka-confluent-msgs", type=int, default=300_000,
