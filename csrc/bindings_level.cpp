@@ -351,6 +351,13 @@ class RfLevels {
     const int64_t N = row_node_.numel();
     g_choose_ = c["choose_rows"].cast<bool>() && (N + 7) / 8 <= 8192ll * 256;
     if (g_choose_ && !g_rows_.defined()) g_rows_ = at::zeros({32 * 64}, row_node_.options());
+    // the same pass also keeps its counts per 512-row wave for the next level's row lists
+    // (PartitionArgs node_counts): no counting pass over row_node per level
+    const bool nc = g_choose_ && (c.contains("node_counts") ? c["node_counts"].cast<bool>() : true) &&
+                    fdx::rg_list_rows(N) % fdx::kPartWaveRows == 0;
+    g_node_counts_ = nc ? at::empty({64 * ((N + fdx::kPartWaveRows - 1) / fdx::kPartWaveRows)}, row_node_.options())
+                        : Tensor();
+    nc_base_ = nullptr;
   }
 
   // The row-group tables and fixed level buffers shared by the single-process (gbdt_setup) and
@@ -1028,6 +1035,7 @@ class RfLevels {
     if (rows_base_) {                                // (gbdt_level: rows per next-level node)
       a.rows_out = p<int32_t>(g_rows_);
       a.rows_base = rows_base_;
+      if (g_node_counts_.defined()) a.node_counts = p<int32_t>(g_node_counts_);
     }
     if (count_work) {                                // the next level's row-list counts (RgListArgs pass 0)
       FDX_CHECK(fdx::partition_counts_ok(a.N) && count_work->scalar_type() == at::kInt, "row-list counts: N / work");
@@ -1071,6 +1079,10 @@ class RfLevels {
       l.wave_count = l.slot_count + 2 * n_build;
       l.counted = g_counted_ ? 1 : 0;
       l.masked = em ? reinterpret_cast<uint32_t*>(p<int32_t>(*g_emdig_)) : nullptr;
+      if (nc_base_ != nullptr) {                  // (the last partition's counts per node)
+        l.node_counts = p<int32_t>(g_node_counts_);
+        l.nc_base = nc_base_;
+      }
       fdx::launch_rg_list(l, s);
       a.list = l.list;
       a.slot_start = l.slot_start;
@@ -1110,6 +1122,7 @@ class RfLevels {
     rows_base_ = choose ? base : nullptr;         // (read by partition())
     partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
     rows_base_ = nullptr;
+    nc_base_ = choose && g_node_counts_.defined() ? base : nullptr;
     if (choose) {
       fdx::LevelChooseArgs ca{};
       ca.counts = p<int32_t>(counts) + d * counts.size(1);
@@ -1315,6 +1328,8 @@ class RfLevels {
   bool g_counted_ok_ = false, g_counted_ = false, g_part_multi_ = false, g_choose_ = false;
   Tensor g_rows_;
   const int32_t* rows_base_ = nullptr;
+  const int32_t* nc_base_ = nullptr;             // first node id of the level whose partition wrote
+  Tensor g_node_counts_;                         //   g_node_counts_ (PartitionArgs node_counts)
   hipEvent_t g_ev_ = nullptr;
 };
 

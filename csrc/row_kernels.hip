@@ -409,13 +409,38 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
 }
 
 // Pass 2: block s scans slot s's per-wave counts into per-wave offsets (in place) and its total.
+// With node_counts, a wave's count is the sum of its 512-row partition waves' counts of the node
+// whose slot is s (that level's nodes *nc_base + i, i < 64).
+__device__ __forceinline__ int32_t rg_node_wave_count(const RgListArgs& a, int node_i, int64_t w) {
+  if (node_i < 0) return 0;
+  const int64_t per = a.list_rows / kPartWaveRows, pw_end = (a.N + kPartWaveRows - 1) / kPartWaveRows;
+  int32_t c = 0;
+  const int32_t* nc = a.node_counts + (int64_t)node_i * pw_end;
+  for (int64_t pw = w * per; pw < (w + 1) * per && pw < pw_end; ++pw) c += nc[pw];
+  return c;
+}
+
 __global__ __launch_bounds__(1024) void rg_list_scan_kernel(RgListArgs a, int64_t nwaves) {
   __shared__ int32_t s_sum[1024];
+  __shared__ int32_t s_node;
   const int s = blockIdx.x, t = threadIdx.x;
+  if (a.node_counts != nullptr) {
+    if (t == 0) s_node = -1;
+    __syncthreads();
+    if (t < 64) {
+      const int32_t node = *a.nc_base + t;
+      if (node >= 0 && node < a.num_nodes && a.node_slot[node] == s) s_node = t;
+    }
+    __syncthreads();
+  }
+  const int node_i = a.node_counts != nullptr ? s_node : -1;
+  auto count_of = [&](int64_t w) {
+    return a.node_counts != nullptr ? rg_node_wave_count(a, node_i, w) : a.wave_count[w * a.nslots + s];
+  };
   const int64_t per = (nwaves + 1023) / 1024;
   const int64_t w0 = t * per, w1 = w0 + per < nwaves ? w0 + per : nwaves;
   int32_t sum = 0;
-  for (int64_t w = w0; w < w1; ++w) sum += a.wave_count[w * a.nslots + s];
+  for (int64_t w = w0; w < w1; ++w) sum += count_of(w);
   s_sum[t] = sum;
   __syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {           // Hillis-Steele inclusive scan of the thread sums
@@ -426,7 +451,7 @@ __global__ __launch_bounds__(1024) void rg_list_scan_kernel(RgListArgs a, int64_
   }
   int32_t acc = s_sum[t] - sum;
   for (int64_t w = w0; w < w1; ++w) {
-    const int32_t c = a.wave_count[w * a.nslots + s];
+    const int32_t c = count_of(w);
     a.wave_count[w * a.nslots + s] = acc;
     acc += c;
   }
@@ -884,7 +909,8 @@ void launch_rg_list(const RgListArgs& a0, hipStream_t s) {
   const int64_t waves = (a.N + a.list_rows - 1) / a.list_rows;   // 4 per block
   const int64_t blocks = (waves + 3) / 4;
   if (blocks <= 0) return;
-  if (!a.counted) hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);
+  if (a.node_counts != nullptr && (a.row_node == nullptr || a.list_rows % kPartWaveRows != 0)) a.node_counts = nullptr;
+  if (!a.counted && a.node_counts == nullptr) hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 0);
   hipLaunchKernelGGL(rg_list_scan_kernel, dim3((unsigned)a.nslots), dim3(1024), 0, s, a, waves);
   hipLaunchKernelGGL(rg_list_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, 1);
 }

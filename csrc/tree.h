@@ -272,7 +272,13 @@ struct RgListArgs {
   uint32_t* masked;               // optional [N * 2] (nslots == 1, with rowdig): pass 1 writes every
                                   //   row's digit words, zero outside slot 0 (the entry-major pass)
   int32_t counted;                // pass 0's per-wave counts already written (PartitionArgs count_work)
+  // optional (row_node mode): the partition's rows per next-level node per 512-row wave
+  // (PartitionArgs node_counts) and that level's first node id (*nc_base): the scan (pass 2) sums
+  // a list wave's 512-row waves for its slot's node, and pass 0 is skipped
+  const int32_t* node_counts;
+  const int32_t* nc_base;
 };
+constexpr int32_t kPartWaveRows = 512;   // rows of one partition wave (64 lanes x 8 rows)
 
 FDX_HD uint32_t rg_slot_of(const RgListArgs& a, int64_t r) {
   if (!a.row_node) return a.slot8[r];
@@ -594,6 +600,10 @@ struct PartitionArgs {
   // for i < 64, added into rows_out[(block % 32) * 64 + i] (32 spread copies; LevelChooseArgs)
   int32_t* rows_out;
   const int32_t* rows_base;
+  // optional (with rows_out): the same counts per 512-row wave w, node_counts[i * ceil(N / 512) + w]
+  // (every lane written), from which the next level's row lists take their per-wave slot counts
+  // (RgListArgs node_counts) instead of a counting pass over row_node
+  int32_t* node_counts;
   // optional: zero this int64 range on the way (the next level's histograms: no fill launch)
   int64_t* zero;
   int64_t zero_n;

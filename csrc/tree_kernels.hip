@@ -1224,6 +1224,7 @@ __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* 
 // of once per row and grid-stride step (10M rows: 0.315 -> 0.232 ms per tree over 6 levels,
 // profiles/r4/gbdt_10M_round_timeline_partition8.txt).
 constexpr int kPartRows = 8;
+static_assert(64 * kPartRows == kPartWaveRows, "partition wave rows");
 
 __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   if (a.zero != nullptr) {           // the next level's histograms, zeroed on the way (16-byte stores)
@@ -1360,6 +1361,8 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
       }
     }
     if (cnt) atomicAdd(&s_rows[lane], cnt);
+    if (a.node_counts != nullptr && w * kPartWaveRows < a.N)
+      a.node_counts[(int64_t)lane * ((a.N + kPartWaveRows - 1) / kPartWaveRows) + w] = cnt;
     __syncthreads();
     if (threadIdx.x < 64 && s_rows[threadIdx.x])
       atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);

@@ -97,8 +97,10 @@ RG_PARTIALS_MULTI = True
 # RfLevels.gbdt_levels; 0: the generic Python loop)
 GBDT_CXX_LEVELS = True
 # ... which builds the sibling with fewer rows (not the smaller hessian sum) where the row lists
-# count their own rows (above 4M rows, or FDX_PARTITION_COUNTS=0): same trees, shorter lists
+# count their own rows (above 4M rows, or FDX_PARTITION_COUNTS=0): same trees, shorter lists;
+# the partition's rows per node, kept per 512-row wave, also stand in for the lists' counting pass
 GBDT_CHOOSE_ROWS = True
+LIST_NODE_COUNTS = True
 # RF / DT count passes: the LDS-atomic kernel (one ds_add_u64 per entry) instead of i8 MFMA
 RF_LDS = True
 # split search: a wave per (node, feature) for the features with > 16 bins
@@ -786,7 +788,7 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
     """Hands the runner the row-group tables and fixed level buffers of its C++ GBDT level loop
     (RfLevels.gbdt_setup), once per runner; returns the two level-histogram tensors (the root's
     is row 0 of the first, zeroed by the prologue)."""
-    key = (RG_DBG, GBDT_CHOOSE_ROWS, PARTITION_COUNTS, RG_PARTIALS, RG_PARTIALS_MULTI, SPLIT_WIDE)
+    key = (RG_DBG, GBDT_CHOOSE_ROWS, LIST_NODE_COUNTS, PARTITION_COUNTS, RG_PARTIALS, RG_PARTIALS_MULTI, SPLIT_WIDE)
     cached = getattr(ws, "_gbdt_levels", None)
     if cached is not None and cached[0] is runner and cached[2] == key:     # (in-process A/Bs flip these)
         return cached[1]
@@ -806,7 +808,7 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
         hist_a=hists[0], hist_b=hists[1], packed=torch.empty((1 << (D - 1), 5), dtype=torch.int64, device=dev),
         one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff,
         wide=_wide_features(Q.nbins, Q.Fa) if SPLIT_WIDE else None, counted=PARTITION_COUNTS, dbg=RG_DBG,
-        part_multi=RG_PARTIALS_MULTI, choose_rows=GBDT_CHOOSE_ROWS))
+        part_multi=RG_PARTIALS_MULTI, choose_rows=GBDT_CHOOSE_ROWS, node_counts=LIST_NODE_COUNTS))
     ws._gbdt_levels = (runner, hists, key)
     return hists
 # the DP runner calls RCCL directly on the process group's communicator (0: through Python)
