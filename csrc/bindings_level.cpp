@@ -351,13 +351,6 @@ class RfLevels {
     const int64_t N = row_node_.numel();
     g_choose_ = c["choose_rows"].cast<bool>() && (N + 7) / 8 <= 8192ll * 256;
     if (g_choose_ && !g_rows_.defined()) g_rows_ = at::zeros({32 * 64}, row_node_.options());
-    // the same pass also keeps its counts per 512-row wave for the next level's row lists
-    // (PartitionArgs node_counts): no counting pass over row_node per level
-    const bool nc = g_choose_ && (c.contains("node_counts") ? c["node_counts"].cast<bool>() : true) &&
-                    fdx::rg_list_rows(N) % fdx::kPartWaveRows == 0;
-    g_node_counts_ = nc ? at::empty({64 * ((N + fdx::kPartWaveRows - 1) / fdx::kPartWaveRows)}, row_node_.options())
-                        : Tensor();
-    nc_base_ = nullptr;
   }
 
   // The row-group tables and fixed level buffers shared by the single-process (gbdt_setup) and
@@ -442,6 +435,14 @@ class RfLevels {
     g_boff_ = get(c, "boff");
     g_wide_ = get_opt(c, "wide");
     g_counted_ok_ = c["counted"].cast<bool>() && fdx::partition_counts_ok(N);
+    // where the partition does not write the row lists' per-slot counts (above 4M rows: 2048-row
+    // list waves), it keeps its rows per next-level node per 512-row wave (PartitionArgs
+    // node_counts; one grid pass) and the lists skip their counting pass over row_node
+    const bool nc = !g_counted_ok_ && (c.contains("node_counts") ? c["node_counts"].cast<bool>() : true) &&
+                    (N + 7) / 8 <= 8192ll * 256 && fdx::rg_list_rows(N) % fdx::kPartWaveRows == 0;
+    g_node_counts_ = nc ? at::empty({64 * ((N + fdx::kPartWaveRows - 1) / fdx::kPartWaveRows)}, row_node_.options())
+                        : Tensor();
+    nc_base_ = nullptr;
     g_part_multi_ = c["part_multi"].cast<bool>();
     FDX_CHECK(sub_of_.has_value() && counts_host_dev_ != nullptr, "gbdt_setup: sub_of and mapped counts");
     if (!g_ev_) FDX_CHECK(hipEventCreateWithFlags(&g_ev_, hipEventDisableTiming) == hipSuccess, "event");
@@ -1032,9 +1033,9 @@ class RfLevels {
     }
     const Tensor& counts = st_["counts"];
     a.node_parent = p<int32_t>(st_["parent"]);    // (column pass first: the row pass sees final nodes)
-    if (rows_base_) {                                // (gbdt_level: rows per next-level node)
-      a.rows_out = p<int32_t>(g_rows_);
+    if (rows_base_) {                                // (GBDT levels: rows per next-level node)
       a.rows_base = rows_base_;
+      if (rows_choose_) a.rows_out = p<int32_t>(g_rows_);
       if (g_node_counts_.defined()) a.node_counts = p<int32_t>(g_node_counts_);
     }
     if (count_work) {                                // the next level's row-list counts (RgListArgs pass 0)
@@ -1119,10 +1120,13 @@ class RfLevels {
     const bool choose = more && g_choose_ && !g_counted_;
     const Tensor& counts = st_["counts"];
     const int32_t* base = d == 0 ? p<int32_t>(g_one_) : p<int32_t>(counts) + (d - 1) * counts.size(1) + 3;
-    rows_base_ = choose ? base : nullptr;         // (read by partition())
+    const bool nc = more && !g_counted_ && g_node_counts_.defined();
+    rows_base_ = choose || nc ? base : nullptr;   // (read by partition())
+    rows_choose_ = choose;
     partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
     rows_base_ = nullptr;
-    nc_base_ = choose && g_node_counts_.defined() ? base : nullptr;
+    rows_choose_ = false;
+    nc_base_ = nc ? base : nullptr;
     if (choose) {
       fdx::LevelChooseArgs ca{};
       ca.counts = p<int32_t>(counts) + d * counts.size(1);
@@ -1165,6 +1169,10 @@ class RfLevels {
       l.wave_count = l.slot_count + 2 * n_build;
       l.counted = g_counted_ ? 1 : 0;
       l.masked = em ? reinterpret_cast<uint32_t*>(p<int32_t>(*g_emdig_)) : nullptr;
+      if (nc_base_ != nullptr) {                  // (the last partition's counts per node)
+        l.node_counts = p<int32_t>(g_node_counts_);
+        l.nc_base = nc_base_;
+      }
       fdx::launch_rg_list(l, s);
       a.list = l.list;
       a.slot_start = l.slot_start;
@@ -1233,7 +1241,12 @@ class RfLevels {
     optional<Tensor> zero;
     if (more) zero = dp_send_.narrow(0, 0, S * n_open * Bs * 2);
     g_counted_ = more && g_counted_ok_;
+    const bool nc = more && !g_counted_ && g_node_counts_.defined();
+    const int32_t* base = d == 0 ? p<int32_t>(g_one_) : p<int32_t>(st_["counts"]) + (d - 1) * st_["counts"].size(1) + 3;
+    rows_base_ = nc ? base : nullptr;
     partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
+    rows_base_ = nullptr;
+    nc_base_ = nc ? base : nullptr;
   }
 
   // timing events around every 8th direct collective (dp_coll_stats)
@@ -1328,6 +1341,7 @@ class RfLevels {
   bool g_counted_ok_ = false, g_counted_ = false, g_part_multi_ = false, g_choose_ = false;
   Tensor g_rows_;
   const int32_t* rows_base_ = nullptr;
+  bool rows_choose_ = false;                     // (partition(): rows_out for LevelChooseArgs)
   const int32_t* nc_base_ = nullptr;             // first node id of the level whose partition wrote
   Tensor g_node_counts_;                         //   g_node_counts_ (PartitionArgs node_counts)
   hipEvent_t g_ev_ = nullptr;

@@ -1235,10 +1235,10 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   }
   const int64_t stride = (int64_t)gridDim.x * 256 * kPartRows;
   uint32_t csl[kPartRows];                 // (count_work) the rows' next-level slots, 0xff: none
-  uint32_t rix[kPartRows];                 // (rows_out) the rows' next-level node index, 0xff: none
+  uint32_t rix[kPartRows];                 // (rows_base) the rows' next-level node index, 0xff: none
 #pragma unroll
   for (int k = 0; k < kPartRows; ++k) csl[k] = rix[k] = 0xffu;
-  const int32_t rbase = a.rows_out != nullptr ? *a.rows_base : 0;
+  const int32_t rbase = a.rows_base != nullptr ? *a.rows_base : 0;
   const int32_t cns = a.count_work != nullptr ? *a.count_nslots : 0;
   for (int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kPartRows; r0 < a.N; r0 += stride) {
     if (r0 + kPartRows <= a.N) {
@@ -1260,7 +1260,7 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < kPartRows; ++k) n[k] = c[k] >= 0 ? c[k] : n[k];
-      if (a.rows_out != nullptr) {
+      if (a.rows_base != nullptr) {
 #pragma unroll
         for (int k = 0; k < kPartRows; ++k) {
           const int32_t i = n[k] - rbase;
@@ -1319,7 +1319,7 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
           const int32_t sk = (n >= 0 && n < a.num_nodes) ? a.count_slot[n] : -1;
           csl[r - r0] = (sk >= 0 && sk < cns) ? (uint32_t)sk : 0xffu;
         }
-        if (a.rows_out != nullptr) {
+        if (a.rows_base != nullptr) {
           const int32_t i = n - rbase;
           rix[r - r0] = (i >= 0 && i < 64) ? (uint32_t)i : 0xffu;
         }
@@ -1344,11 +1344,13 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
     }
     if (lane < cns) a.count_work[2 * cns + w * cns + lane] = cnt;
   }
-  if (a.rows_out != nullptr) {             // (block-uniform; one grid pass: host-checked)
+  if (a.rows_base != nullptr) {            // (block-uniform; one grid pass: host-checked)
     // rows per next-level node: wave ballots -> the block's LDS counts -> 64 spread atomics
     __shared__ int32_t s_rows[64];
-    if (threadIdx.x < 64) s_rows[threadIdx.x] = 0;
-    __syncthreads();
+    if (a.rows_out != nullptr) {
+      if (threadIdx.x < 64) s_rows[threadIdx.x] = 0;
+      __syncthreads();
+    }
     int32_t cnt = 0;
 #pragma unroll
     for (int k = 0; k < kPartRows; ++k) {
@@ -1360,12 +1362,14 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
         act &= ~m;
       }
     }
-    if (cnt) atomicAdd(&s_rows[lane], cnt);
     if (a.node_counts != nullptr && w * kPartWaveRows < a.N)
       a.node_counts[(int64_t)lane * ((a.N + kPartWaveRows - 1) / kPartWaveRows) + w] = cnt;
-    __syncthreads();
-    if (threadIdx.x < 64 && s_rows[threadIdx.x])
-      atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);
+    if (a.rows_out != nullptr) {
+      if (cnt) atomicAdd(&s_rows[lane], cnt);
+      __syncthreads();
+      if (threadIdx.x < 64 && s_rows[threadIdx.x])
+        atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);
+    }
   }
 }
 __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) { partition_default_kernel_body(a); }

@@ -840,7 +840,7 @@ def _gbdt_dp_setup(Q, ws, st, params, runner, rg, shards, coll) -> torch.Tensor:
         rg_wg_first=rg.work_first() if RG_PARTIALS else None,
         list_work=ws.rg_work, rg_start=ws.rg_start, rg_list=ws.rg_list, rg_listdig=ws.rg_listdig,
         one=st.one, zero1=st.zero1, open1=st.open[1], totals1=st.totals[1], boff=Q.boff, wide=None,
-        counted=PARTITION_COUNTS, dbg=RG_DBG, part_multi=RG_PARTIALS_MULTI,
+        counted=PARTITION_COUNTS, node_counts=LIST_NODE_COUNTS, dbg=RG_DBG, part_multi=RG_PARTIALS_MULTI,
         rs=cb.rs, ag=cb.ag, mx=cb.mx, S=S, Bs=Bs, bin_lo=shards.bin_lo, send=send, out_a=outs[0], out_b=outs[1],
         row_of0=st.row_of[0], row_of1=st.row_of[1], ag_in=torch.empty((widest, 5), dtype=torch.int64, device=dev),
         sboff=shards.boff, snbins=shards.nbins, szbin=shards.zbin, sfid=shards.fid_orig, f0=int(shards.f0),

@@ -168,11 +168,15 @@ def test_gpu_gbdt_large_shard_paths_equal_host(monkeypatch):
     assert C.tree_rg_list_rows(5000) == 512
 
 
-def _dp_booster(rank, world, device, cxx, direct=True):
-    """One rank's booster under data parallelism, with its collective calls counted."""
+def _dp_booster(rank, world, device, cxx, direct=True, big=False):
+    """One rank's booster under data parallelism, with its collective calls counted (big: the
+    >4M-row list regime on this small shard -- 2048-row list waves, the partition's per-node
+    counts instead of the lists' counting pass)."""
     from fraud_detection_spark_kafka_llm_amd.models import grower
     from fraud_detection_spark_kafka_llm_amd.parallel import dist as D
 
+    if big:
+        native.lib().tree_set_list_big_rows(1000)
     grower.GBDT_CXX_LEVELS = cxx
     grower.DP_DIRECT_RCCL = direct
     lo, hi = D.shard_range(5000, rank, world)
@@ -196,10 +200,10 @@ def test_gpu_gbdt_dp_runner_levels_equal_single_process(world, backend, monkeypa
     trees = 8
     # (the runner calls RCCL itself on the process group's communicator; direct=False: through
     # the Python callbacks, as on gloo)
-    for cxx, direct in ((True, True), (True, False), (False, True)):
-        outs = spawn(_dp_booster, world, "cuda:0", cxx, direct, backend=backend)
+    for cxx, direct, big in ((True, True, False), (True, False, False), (False, True, False), (True, True, True)):
+        outs = spawn(_dp_booster, world, "cuda:0", cxx, direct, big, backend=backend)
         for got, calls, level_calls in outs:
-            assert got == ref, (cxx, direct, world)
+            assert got == ref, (cxx, direct, big, world)
             assert level_calls > 0
             # (+ fit_gbdt's base score and the quantisation's max / key gathers)
             assert calls["reduce_scatter"] + calls["all_gather"] <= 12 * trees + 4, calls
