@@ -1061,7 +1061,15 @@ def _client_main(cfg: dict) -> int:
             if cmd == "exit":
                 return 0
             try:
-                r = _client_run(cfg, spec, conn, ring, pool)
+                prof_to = os.environ.get("FDX_CLIENT_PROFILE")      # (diagnostics: cProfile per run)
+                if prof_to:
+                    import cProfile
+
+                    pr = cProfile.Profile()
+                    r = pr.runcall(_client_run, cfg, spec, conn, ring, pool)
+                    pr.dump_stats(f"{prof_to}.{cfg['index']}")
+                else:
+                    r = _client_run(cfg, spec, conn, ring, pool)
                 conn.send_bytes(_CTL + pickle.dumps(("result", r)))
             except Exception:
                 import traceback
