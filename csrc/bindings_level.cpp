@@ -1033,6 +1033,7 @@ class RfLevels {
     }
     const Tensor& counts = st_["counts"];
     a.node_parent = p<int32_t>(st_["parent"]);    // (column pass first: the row pass sees final nodes)
+    a.count_ballot = 2 * n_open <= 4 ? 1 : 0;        // (next-level nodes: at most 2 n_open)
     if (rows_base_) {                                // (GBDT levels: rows per next-level node)
       a.rows_base = rows_base_;
       if (rows_choose_) a.rows_out = p<int32_t>(g_rows_);

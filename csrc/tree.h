@@ -604,6 +604,7 @@ struct PartitionArgs {
   int32_t* rows_out;
   const int32_t* rows_base;
   int32_t* node_counts;
+  int32_t count_ballot;           // the counts above and count_work's by wave ballots (<= 4 values)
   // optional: zero this int64 range on the way (the next level's histograms: no fill launch)
   int64_t* zero;
   int64_t zero_n;

@@ -1226,6 +1226,40 @@ __global__ __launch_bounds__(kBestThreads) void split_best_kernel(const double* 
 constexpr int kPartRows = 8;
 static_assert(64 * kPartRows == kPartWaveRows, "partition wave rows");
 
+// Lane i of the wave gets the number of (lane, k) with v[k] == i (v[k] < 64; 0xff: none): LDS
+// atomics into the wave's own row, or with few distinct values a ballot per value. (Ballots alone
+// took up to 64 rounds per k at the deep levels; atomics alone serialise on 2-4 addresses at the
+// first levels. 10M rows, per level: 36 / 41 / 54 / 67 / 79 us with ballots, 45 / 45 / 52 / 59 /
+// 63 with atomics: profiles/r6/gbdt_late/NOTES.md.)
+__device__ __forceinline__ int32_t wave_count64(int32_t* row, const uint32_t (&v)[kPartRows], int lane, bool ballot) {
+  if (ballot) {                      // (few distinct values: a ballot each beats same-address atomics)
+    int32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPartRows; ++k) {
+      uint64_t act = __ballot(v[k] < 64u);
+      while (act) {
+        const uint32_t sv = __shfl(v[k], __ffsll((unsigned long long)act) - 1, 64);
+        const uint64_t m = __ballot(v[k] == sv);
+        if ((uint32_t)lane == sv) cnt += __popcll(m);
+        act &= ~m;
+      }
+    }
+    return cnt;
+  }
+  row[lane] = 0;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < kPartRows; ++k)
+    if (v[k] < 64u) atomicAdd(&row[v[k]], 1);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const int32_t c = row[lane];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  return c;
+}
+
 __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   if (a.zero != nullptr) {           // the next level's histograms, zeroed on the way (16-byte stores)
     int4* z = reinterpret_cast<int4*>(a.zero);
@@ -1328,40 +1362,21 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   }
   const int lane = threadIdx.x & 63;
   const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  __shared__ int32_t s_wcnt[4][64];                 // (wave_count64: a row per wave of the block)
   if (a.count_work != nullptr && w * 64 * kPartRows < a.N) {       // (wave-uniform)
     // the wave's 512 rows (64 lanes x 8, one grid pass: host-checked) = RgListArgs pass 0's wave
-    // w: per slot, its rows counted with ballots, lane s holding slot s's count
-    int32_t cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kPartRows; ++k) {
-      uint64_t act = __ballot(csl[k] != 0xffu);
-      while (act) {
-        const uint32_t sv = __shfl(csl[k], __ffsll((unsigned long long)act) - 1, 64);
-        const uint64_t m = __ballot(csl[k] == sv);
-        if ((uint32_t)lane == sv) cnt += __popcll(m);
-        act &= ~m;
-      }
-    }
+    // w: lane s holds slot s's count
+    const int32_t cnt = wave_count64(s_wcnt[threadIdx.x >> 6], csl, lane, a.count_ballot != 0);
     if (lane < cns) a.count_work[2 * cns + w * cns + lane] = cnt;
   }
   if (a.rows_base != nullptr) {            // (block-uniform; one grid pass: host-checked)
-    // rows per next-level node: wave ballots -> the block's LDS counts -> 64 spread atomics
+    // rows per next-level node: the wave's counts -> the block's LDS counts -> 64 spread atomics
     __shared__ int32_t s_rows[64];
     if (a.rows_out != nullptr) {
       if (threadIdx.x < 64) s_rows[threadIdx.x] = 0;
       __syncthreads();
     }
-    int32_t cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kPartRows; ++k) {
-      uint64_t act = __ballot(rix[k] != 0xffu);
-      while (act) {
-        const uint32_t sv = __shfl(rix[k], __ffsll((unsigned long long)act) - 1, 64);
-        const uint64_t m = __ballot(rix[k] == sv);
-        if ((uint32_t)lane == sv) cnt += __popcll(m);
-        act &= ~m;
-      }
-    }
+    const int32_t cnt = wave_count64(s_wcnt[threadIdx.x >> 6], rix, lane, a.count_ballot != 0);
     if (a.node_counts != nullptr && w * kPartWaveRows < a.N)
       a.node_counts[(int64_t)lane * ((a.N + kPartWaveRows - 1) / kPartWaveRows) + w] = cnt;
     if (a.rows_out != nullptr) {
