@@ -421,9 +421,9 @@ __device__ __forceinline__ int32_t rg_node_wave_count(const RgListArgs& a, int n
 }
 
 __global__ __launch_bounds__(1024) void rg_list_scan_kernel(RgListArgs a, int64_t nwaves) {
-  __shared__ int32_t s_sum[1024];
+  __shared__ int32_t s_wsum[16];
   __shared__ int32_t s_node;
-  const int s = blockIdx.x, t = threadIdx.x;
+  const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
   if (a.node_counts != nullptr) {
     if (t == 0) s_node = -1;
     __syncthreads();
@@ -437,25 +437,52 @@ __global__ __launch_bounds__(1024) void rg_list_scan_kernel(RgListArgs a, int64_
   auto count_of = [&](int64_t w) {
     return a.node_counts != nullptr ? rg_node_wave_count(a, node_i, w) : a.wave_count[w * a.nslots + s];
   };
+  // thread t: waves [w0, w1), their counts kept in registers (up to 8 a thread: 16M rows at
+  // 2048-row waves; beyond, read again)
+  constexpr int kKeep = 8;
   const int64_t per = (nwaves + 1023) / 1024;
   const int64_t w0 = t * per, w1 = w0 + per < nwaves ? w0 + per : nwaves;
+  int32_t keep[kKeep];
   int32_t sum = 0;
-  for (int64_t w = w0; w < w1; ++w) sum += count_of(w);
-  s_sum[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {           // Hillis-Steele inclusive scan of the thread sums
-    const int32_t o = t >= d ? s_sum[t - d] : 0;
-    __syncthreads();
-    s_sum[t] += o;
-    __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kKeep; ++i) {
+    keep[i] = w0 + i < w1 ? count_of(w0 + i) : 0;
+    sum += keep[i];
   }
-  int32_t acc = s_sum[t] - sum;
-  for (int64_t w = w0; w < w1; ++w) {
+  for (int64_t w = w0 + kKeep; w < w1; ++w) sum += count_of(w);
+  // block exclusive scan of the thread sums: wave scans, then a scan of the 16 wave totals
+  int32_t incl = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) s_wsum[wid] = incl;
+  __syncthreads();
+  if (wid == 0) {
+    int32_t x = lane < 16 ? s_wsum[lane] : 0;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const int32_t o = __shfl_up(x, d, 64);
+      if (lane >= d) x += o;
+    }
+    if (lane < 16) s_wsum[lane] = x;
+  }
+  __syncthreads();
+  int32_t acc = incl - sum + (wid > 0 ? s_wsum[wid - 1] : 0);
+#pragma unroll
+  for (int i = 0; i < kKeep; ++i) {
+    if (w0 + i < w1) {
+      a.wave_count[(w0 + i) * a.nslots + s] = acc;
+      acc += keep[i];
+    }
+  }
+  for (int64_t w = w0 + kKeep; w < w1; ++w) {
     const int32_t c = count_of(w);
     a.wave_count[w * a.nslots + s] = acc;
     acc += c;
   }
-  if (t == 1023) a.slot_count[s] = s_sum[1023];
+  if (t == 0) a.slot_count[s] = s_wsum[15];
 }
 
 template <int BINS>
