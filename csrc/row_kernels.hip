@@ -367,7 +367,15 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
     if (lane < a.nslots) a.slot_start[lane] = incl - tot;
     if (lane == a.nslots - 1) a.slot_start[a.nslots] = incl;
   }
-  int32_t base = lane < a.nslots ? incl - tot + wc[lane] : 0;
+  // the wave's running position in each slot (lane s writes slot s's), read by every lane of the
+  // slot: one ballot per slot-id bit finds a lane's slot mates (a ballot per distinct slot took up
+  // to ~16 rounds per step at the deep levels)
+  __shared__ int32_t s_base[4][64];
+  int32_t* base = s_base[threadIdx.x >> 6];
+  if (lane < a.nslots) base[lane] = incl - tot + wc[lane];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const int nbits = a.nslots > 1 ? 32 - __clz((unsigned)(a.nslots - 1)) : 0;
   for (int k0 = 0; k0 < list_steps; k0 += KB) {
     uint2 d[KB];
 #pragma unroll
@@ -391,19 +399,23 @@ __global__ __launch_bounds__(256) void rg_list_kernel(RgListArgs a, int pass) {
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       const int64_t r = r0 + 64 * (k0 + k) + lane;
-      uint64_t act = __ballot(sl[k] < (uint32_t)a.nslots);
-      while (act) {
-        const uint32_t s = __shfl(sl[k], __ffsll((unsigned long long)act) - 1, 64);
-        const uint64_t m = __ballot(sl[k] == s);
-        const int32_t b = __shfl(base, (int)s, 64);
-        if (sl[k] == s) {
-          const int64_t pos = b + __popcll(m & lt);
-          a.list[pos] = (int32_t)r;
-          if (a.listdig) *reinterpret_cast<uint2*>(a.listdig + 2 * pos) = d[k];
-        }
-        if ((uint32_t)lane == s) base += __popcll(m);
-        act &= ~m;
+      const bool act = sl[k] < (uint32_t)a.nslots;
+      uint64_t same = __ballot(act);
+      for (int b = 0; b < nbits; ++b) {
+        const bool bit = (sl[k] >> b) & 1u;
+        const uint64_t mb = __ballot(act && bit);
+        same &= bit ? mb : ~mb;
       }
+      if (act) {
+        const uint32_t rank = __popcll(same & lt);
+        const int32_t b0 = base[sl[k]];          // (every lane reads before the leaders write)
+        const int64_t pos = b0 + rank;
+        a.list[pos] = (int32_t)r;
+        if (a.listdig) *reinterpret_cast<uint2*>(a.listdig + 2 * pos) = d[k];
+        if (rank == 0) base[sl[k]] = b0 + __popcll(same);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
