@@ -436,10 +436,10 @@ class RfLevels {
     g_wide_ = get_opt(c, "wide");
     g_counted_ok_ = c["counted"].cast<bool>() && fdx::partition_counts_ok(N);
     // where the partition does not write the row lists' per-slot counts (above 4M rows: 2048-row
-    // list waves), it keeps its rows per next-level node per 512-row wave (PartitionArgs
-    // node_counts; one grid pass) and the lists skip their counting pass over row_node
+    // list waves), it keeps its rows per next-level node per 512-row chunk (PartitionArgs
+    // node_counts) and the lists skip their counting pass over row_node
     const bool nc = !g_counted_ok_ && (c.contains("node_counts") ? c["node_counts"].cast<bool>() : true) &&
-                    (N + 7) / 8 <= 8192ll * 256 && fdx::rg_list_rows(N) % fdx::kPartWaveRows == 0;
+                    fdx::rg_list_rows(N) % fdx::kPartWaveRows == 0;
     g_node_counts_ = nc ? at::empty({64 * ((N + fdx::kPartWaveRows - 1) / fdx::kPartWaveRows)}, row_node_.options())
                         : Tensor();
     nc_base_ = nullptr;

@@ -596,10 +596,10 @@ struct PartitionArgs {
   int32_t* count_work;
   const int32_t* count_slot;
   const int32_t* count_nslots;
-  // optional (one grid pass over the rows; rows_base given): the rows of each next-level node, node
-  // id *rows_base + i for i < 64, added into rows_out[(block % 32) * 64 + i] (32 spread copies;
-  // LevelChooseArgs), and / or kept per 512-row wave w in node_counts[i * ceil(N / 512) + w] (every
-  // lane written), from which the next level's row lists take their per-wave slot counts
+  // optional (rows_base given): the rows of each next-level node, node id *rows_base + i for i < 64,
+  // added into rows_out[(block % 32) * 64 + i] (32 spread copies; LevelChooseArgs; one grid pass
+  // over the rows), and / or kept per 512-row chunk w in node_counts[i * ceil(N / 512) + w] (every
+  // lane written; any grid), from which the next level's row lists take their per-wave slot counts
   // (RgListArgs node_counts) instead of a counting pass over row_node
   int32_t* rows_out;
   const int32_t* rows_base;

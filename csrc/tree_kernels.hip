@@ -1274,8 +1274,21 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   for (int k = 0; k < kPartRows; ++k) csl[k] = rix[k] = 0xffu;
   const int32_t rbase = a.rows_base != nullptr ? *a.rows_base : 0;
   const int32_t cns = a.count_work != nullptr ? *a.count_nslots : 0;
-  for (int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kPartRows; r0 < a.N; r0 += stride) {
-    if (r0 + kPartRows <= a.N) {
+  const int lane = threadIdx.x & 63;
+  __shared__ int32_t s_wcnt[4][64];                 // (wave_count64: a row per wave of the block)
+  // node_counts without rows_out: counted per 512-row chunk inside the loop (any grid); with
+  // rows_out (one grid pass) after it
+  const bool nc_loop = a.node_counts != nullptr && a.rows_out == nullptr;
+  const int64_t npw = (a.N + kPartWaveRows - 1) / kPartWaveRows;
+  // the loop is wave-uniform: lane l takes rows wb + 8 l .. of the wave's 512-row chunk wb
+  for (int64_t wb = ((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) * kPartRows; wb < a.N; wb += stride) {
+    const int64_t r0 = wb + (int64_t)lane * kPartRows;
+    if (nc_loop) {
+#pragma unroll
+      for (int k = 0; k < kPartRows; ++k) rix[k] = 0xffu;
+    }
+    if (r0 >= a.N) {
+    } else if (r0 + kPartRows <= a.N) {
       int4* p = reinterpret_cast<int4*>(a.row_node + r0);      // (row_node: 16-byte aligned, r0 % 8 == 0)
       const int4 x0 = p[0], x1 = p[1];
       int32_t n[kPartRows] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -1359,32 +1372,29 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
         }
       }
     }
+    if (nc_loop) {
+      const int32_t cnt = wave_count64(s_wcnt[threadIdx.x >> 6], rix, lane, a.count_ballot != 0);
+      a.node_counts[(int64_t)lane * npw + wb / kPartWaveRows] = cnt;
+    }
   }
-  const int lane = threadIdx.x & 63;
   const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  __shared__ int32_t s_wcnt[4][64];                 // (wave_count64: a row per wave of the block)
   if (a.count_work != nullptr && w * 64 * kPartRows < a.N) {       // (wave-uniform)
     // the wave's 512 rows (64 lanes x 8, one grid pass: host-checked) = RgListArgs pass 0's wave
     // w: lane s holds slot s's count
     const int32_t cnt = wave_count64(s_wcnt[threadIdx.x >> 6], csl, lane, a.count_ballot != 0);
     if (lane < cns) a.count_work[2 * cns + w * cns + lane] = cnt;
   }
-  if (a.rows_base != nullptr) {            // (block-uniform; one grid pass: host-checked)
+  if (a.rows_out != nullptr) {             // (block-uniform; one grid pass: host-checked)
     // rows per next-level node: the wave's counts -> the block's LDS counts -> 64 spread atomics
     __shared__ int32_t s_rows[64];
-    if (a.rows_out != nullptr) {
-      if (threadIdx.x < 64) s_rows[threadIdx.x] = 0;
-      __syncthreads();
-    }
+    if (threadIdx.x < 64) s_rows[threadIdx.x] = 0;
+    __syncthreads();
     const int32_t cnt = wave_count64(s_wcnt[threadIdx.x >> 6], rix, lane, a.count_ballot != 0);
-    if (a.node_counts != nullptr && w * kPartWaveRows < a.N)
-      a.node_counts[(int64_t)lane * ((a.N + kPartWaveRows - 1) / kPartWaveRows) + w] = cnt;
-    if (a.rows_out != nullptr) {
-      if (cnt) atomicAdd(&s_rows[lane], cnt);
-      __syncthreads();
-      if (threadIdx.x < 64 && s_rows[threadIdx.x])
-        atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);
-    }
+    if (a.node_counts != nullptr && w * kPartWaveRows < a.N) a.node_counts[(int64_t)lane * npw + w] = cnt;
+    if (cnt) atomicAdd(&s_rows[lane], cnt);
+    __syncthreads();
+    if (threadIdx.x < 64 && s_rows[threadIdx.x])
+      atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);
   }
 }
 __global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) { partition_default_kernel_body(a); }
