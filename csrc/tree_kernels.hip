@@ -1260,6 +1260,12 @@ __device__ __forceinline__ int32_t wave_count64(int32_t* row, const uint32_t (&v
   return c;
 }
 
+// kCount: 0 no next-level row counts (the RF lanes, plain partitions: 49 VGPRs); 1 count_work, one
+// grid pass, counted after the loop; 2 node_counts alone, counted per 512-row chunk inside the
+// loop (any grid); 3 rows_out (+ node_counts), one grid pass, after the loop. Each variant holds
+// only its own registers (one kernel for all of them took 81 VGPRs and 5 waves per SIMD: ~7 %
+// slower at 10M rows).
+template <int kCount>
 __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   if (a.zero != nullptr) {           // the next level's histograms, zeroed on the way (16-byte stores)
     int4* z = reinterpret_cast<int4*>(a.zero);
@@ -1272,13 +1278,13 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
   uint32_t rix[kPartRows];                 // (rows_base) the rows' next-level node index, 0xff: none
 #pragma unroll
   for (int k = 0; k < kPartRows; ++k) csl[k] = rix[k] = 0xffu;
-  const int32_t rbase = a.rows_base != nullptr ? *a.rows_base : 0;
-  const int32_t cns = a.count_work != nullptr ? *a.count_nslots : 0;
+  const int32_t rbase = (kCount == 2 || kCount == 3) && a.rows_base != nullptr ? *a.rows_base : 0;
+  const int32_t cns = kCount == 1 && a.count_work != nullptr ? *a.count_nslots : 0;
   const int lane = threadIdx.x & 63;
   __shared__ int32_t s_wcnt[4][64];                 // (wave_count64: a row per wave of the block)
   // node_counts without rows_out: counted per 512-row chunk inside the loop (any grid); with
   // rows_out (one grid pass) after it
-  const bool nc_loop = a.node_counts != nullptr && a.rows_out == nullptr;
+  const bool nc_loop = kCount == 2 && a.node_counts != nullptr;
   const int64_t npw = (a.N + kPartWaveRows - 1) / kPartWaveRows;
   // the loop is wave-uniform: lane l takes rows wb + 8 l .. of the wave's 512-row chunk wb
   for (int64_t wb = ((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) * kPartRows; wb < a.N; wb += stride) {
@@ -1307,7 +1313,7 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < kPartRows; ++k) n[k] = c[k] >= 0 ? c[k] : n[k];
-      if (a.rows_base != nullptr) {
+      if ((kCount == 2 || kCount == 3) && a.rows_base != nullptr) {
 #pragma unroll
         for (int k = 0; k < kPartRows; ++k) {
           const int32_t i = n[k] - rbase;
@@ -1316,7 +1322,7 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
       }
       p[0] = make_int4(n[0], n[1], n[2], n[3]);
       p[1] = make_int4(n[4], n[5], n[6], n[7]);
-      if (a.count_work != nullptr) {
+      if (kCount == 1 && a.count_work != nullptr) {
 #pragma unroll
         for (int k = 0; k < kPartRows; ++k) {
           const int32_t sk = (n[k] >= 0 && n[k] < a.num_nodes) ? a.count_slot[n[k]] : -1;
@@ -1362,11 +1368,11 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
           if (c >= 0) a.row_node[r] = n = c;
         }
         if (a.pack != nullptr) a.pack[r] = partition_pack_word(a, n, r);
-        if (a.count_work != nullptr) {
+        if (kCount == 1 && a.count_work != nullptr) {
           const int32_t sk = (n >= 0 && n < a.num_nodes) ? a.count_slot[n] : -1;
           csl[r - r0] = (sk >= 0 && sk < cns) ? (uint32_t)sk : 0xffu;
         }
-        if (a.rows_base != nullptr) {
+        if ((kCount == 2 || kCount == 3) && a.rows_base != nullptr) {
           const int32_t i = n - rbase;
           rix[r - r0] = (i >= 0 && i < 64) ? (uint32_t)i : 0xffu;
         }
@@ -1378,13 +1384,13 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
     }
   }
   const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  if (a.count_work != nullptr && w * 64 * kPartRows < a.N) {       // (wave-uniform)
+  if (kCount == 1 && a.count_work != nullptr && w * 64 * kPartRows < a.N) {       // (wave-uniform)
     // the wave's 512 rows (64 lanes x 8, one grid pass: host-checked) = RgListArgs pass 0's wave
     // w: lane s holds slot s's count
     const int32_t cnt = wave_count64(s_wcnt[threadIdx.x >> 6], csl, lane, a.count_ballot != 0);
     if (lane < cns) a.count_work[2 * cns + w * cns + lane] = cnt;
   }
-  if (a.rows_out != nullptr) {             // (block-uniform; one grid pass: host-checked)
+  if (kCount == 3 && a.rows_out != nullptr) {   // (block-uniform; one grid pass: host-checked)
     // rows per next-level node: the wave's counts -> the block's LDS counts -> 64 spread atomics
     __shared__ int32_t s_rows[64];
     if (threadIdx.x < 64) s_rows[threadIdx.x] = 0;
@@ -1397,7 +1403,9 @@ __device__ __forceinline__ void partition_default_kernel_body(PartitionArgs a) {
       atomicAdd(&a.rows_out[(blockIdx.x & 31) * 64 + threadIdx.x], s_rows[threadIdx.x]);
   }
 }
-__global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) { partition_default_kernel_body(a); }
+template <int kCount>
+__global__ __launch_bounds__(256) void partition_default_kernel(PartitionArgs a) { partition_default_kernel_body<kCount>(a); }
+
 
 // LevelChooseArgs: one wave; lane i sums node i's 32 spread row counts (and zeroes them), then
 // lane b < builds takes build b's sibling pair.
@@ -1824,8 +1832,9 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(uint4* __restrict__ dst
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
 }
 
+template <int kCount>
 __global__ __launch_bounds__(256) void partition_default_lanes_kernel(const PartitionArgs* __restrict__ args) {
-  partition_default_kernel_body(args[blockIdx.z]);
+  partition_default_kernel_body<kCount>(args[blockIdx.z]);
 }
 
 constexpr int kQuantBlocks = 2048;      // workgroup cap of the quantisation passes (partials)
@@ -1835,6 +1844,21 @@ constexpr int kSlotBlocks = 2048;       // ... of the spread-slot passes (64 ato
 inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
   const int64_t b = (n + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+// the partition's row pass, with the counting variant where any count is asked for
+void launch_partition_default(const PartitionArgs& a, hipStream_t s) {
+  if (a.N <= 0) return;
+  const dim3 grid(grid_for((a.N + kPartRows - 1) / kPartRows));
+  FDX_LANES_CHECK(a.count_work == nullptr || a.rows_base == nullptr);   // (one counting mode at a time)
+  if (a.count_work != nullptr)
+    hipLaunchKernelGGL(partition_default_kernel<1>, grid, dim3(256), 0, s, a);
+  else if (a.rows_out != nullptr && a.count_work == nullptr)
+    hipLaunchKernelGGL(partition_default_kernel<3>, grid, dim3(256), 0, s, a);
+  else if (a.rows_base != nullptr && a.node_counts != nullptr)
+    hipLaunchKernelGGL(partition_default_kernel<2>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(partition_default_kernel<0>, grid, dim3(256), 0, s, a);
 }
 }  // namespace
 
@@ -2060,7 +2084,7 @@ int64_t split_partials(int32_t nodes, int32_t Fa) {
 }
 
 void launch_partition(const PartitionArgs& a, hipStream_t s) {
-  if (a.N > 0) hipLaunchKernelGGL(partition_default_kernel, dim3(grid_for((a.N + kPartRows - 1) / kPartRows)), dim3(256), 0, s, a);
+  launch_partition_default(a, s);
   if (a.num_items > 0) hipLaunchKernelGGL(partition_column_kernel, dim3(a.num_items), dim3(256), 0, s, a);
 }
 
@@ -2080,7 +2104,7 @@ void launch_partition_cols(const PartitionArgs& a, const int64_t* colptr, const 
       hipLaunchKernelGGL(partition_cols_kernel, dim3(max_splits * wps), dim3(256), 0, s, a, colptr, cs_feat, n_cs, wps);
   };
   if (a.node_parent != nullptr) cols();   // (column pass first: PartitionArgs node_parent)
-  if (a.N > 0) hipLaunchKernelGGL(partition_default_kernel, dim3(grid_for((a.N + kPartRows - 1) / kPartRows)), dim3(256), 0, s, a);
+  launch_partition_default(a, s);
   if (a.node_parent == nullptr) cols();
 }
 
@@ -2235,9 +2259,24 @@ void launch_partition_lanes(const PartColsLane* h, const PartColsLane* d, const 
     if (gx > 0) hipLaunchKernelGGL(partition_cols_lanes_kernel, dim3(gx, 1, L), dim3(256), 0, s, d);
   };
   if (h[0].a.node_parent != nullptr) cols();
-  if (h[0].a.N > 0)
-    hipLaunchKernelGGL(partition_default_lanes_kernel, dim3(grid_for((h[0].a.N + kPartRows - 1) / kPartRows), 1, L),
-                       dim3(256), 0, s, dp);
+  if (h[0].a.N > 0) {
+    int mode = 0;                        // (a counting variant if a lane asks for counts)
+    for (int l = 0; l < L; ++l) {
+      const PartitionArgs& x = h[l].a;
+      const int m = x.count_work != nullptr ? 1 : x.rows_out != nullptr ? 3 : x.node_counts != nullptr ? 2 : 0;
+      FDX_LANES_CHECK(mode == 0 || m == 0 || m == mode);
+      mode = m ? m : mode;
+    }
+    const dim3 grid(grid_for((h[0].a.N + kPartRows - 1) / kPartRows), 1, L);
+    if (mode == 1)
+      hipLaunchKernelGGL(partition_default_lanes_kernel<1>, grid, dim3(256), 0, s, dp);
+    else if (mode == 3)
+      hipLaunchKernelGGL(partition_default_lanes_kernel<3>, grid, dim3(256), 0, s, dp);
+    else if (mode == 2)
+      hipLaunchKernelGGL(partition_default_lanes_kernel<2>, grid, dim3(256), 0, s, dp);
+    else
+      hipLaunchKernelGGL(partition_default_lanes_kernel<0>, grid, dim3(256), 0, s, dp);
+  }
   if (h[0].a.node_parent == nullptr) cols();
 }
 
