@@ -1121,7 +1121,8 @@ class RfLevels {
     const bool choose = more && g_choose_ && !g_counted_;
     const Tensor& counts = st_["counts"];
     const int32_t* base = d == 0 ? p<int32_t>(g_one_) : p<int32_t>(counts) + (d - 1) * counts.size(1) + 3;
-    const bool nc = more && !g_counted_ && g_node_counts_.defined();
+    // (per-node counts cover the next level's first 64 nodes: 2 n_open of them)
+    const bool nc = more && !g_counted_ && g_node_counts_.defined() && 2 * (int64_t)n_open <= 64;
     rows_base_ = choose || nc ? base : nullptr;   // (read by partition())
     rows_choose_ = choose;
     partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);
@@ -1242,7 +1243,7 @@ class RfLevels {
     optional<Tensor> zero;
     if (more) zero = dp_send_.narrow(0, 0, S * n_open * Bs * 2);
     g_counted_ = more && g_counted_ok_;
-    const bool nc = more && !g_counted_ && g_node_counts_.defined();
+    const bool nc = more && !g_counted_ && g_node_counts_.defined() && 2 * (int64_t)n_open <= 64;
     const int32_t* base = d == 0 ? p<int32_t>(g_one_) : p<int32_t>(st_["counts"]) + (d - 1) * st_["counts"].size(1) + 3;
     rows_base_ = nc ? base : nullptr;
     partition(d, n_open, false, zero, false, g_counted_ ? optional<Tensor>(g_list_work_) : c10::nullopt);

@@ -155,6 +155,7 @@ def test_gpu_gbdt_large_shard_paths_equal_host(monkeypatch):
 
     C = native.lib()
     ref = _booster("cpu")
+    ref8 = _booster("cpu", depth=8)            # (levels with more than 64 next-level nodes)
     old = C.tree_set_list_big_rows(1000)
     try:
         assert C.tree_rg_list_rows(5000) == 2048 and not C.tree_partition_counts_ok(5000)
@@ -163,6 +164,7 @@ def test_gpu_gbdt_large_shard_paths_equal_host(monkeypatch):
             for choose in (True, False):
                 monkeypatch.setattr(grower, "GBDT_CHOOSE_ROWS", choose)
                 assert _booster("cuda:0") == ref, (cxx, choose)
+                assert _booster("cuda:0", depth=8) == ref8, (cxx, choose, 8)
     finally:
         C.tree_set_list_big_rows(old)
     assert C.tree_rg_list_rows(5000) == 512
