@@ -788,7 +788,8 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
     """Hands the runner the row-group tables and fixed level buffers of its C++ GBDT level loop
     (RfLevels.gbdt_setup), once per runner; returns the two level-histogram tensors (the root's
     is row 0 of the first, zeroed by the prologue)."""
-    key = (RG_DBG, GBDT_CHOOSE_ROWS, LIST_NODE_COUNTS, PARTITION_COUNTS, RG_PARTIALS, RG_PARTIALS_MULTI, SPLIT_WIDE)
+    key = (RG_DBG, GBDT_CHOOSE_ROWS, LIST_NODE_COUNTS, PARTITION_COUNTS, RG_PARTIALS, RG_PARTIALS_MULTI, SPLIT_WIDE,
+           qmod.RG_LIST_WGS)
     cached = getattr(ws, "_gbdt_levels", None)
     if cached is not None and cached[0] is runner and cached[2] == key:     # (in-process A/Bs flip these)
         return cached[1]
