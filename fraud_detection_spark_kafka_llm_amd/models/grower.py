@@ -789,7 +789,7 @@ def _gbdt_levels_setup(Q, ws, st, params, runner, rg):
     (RfLevels.gbdt_setup), once per runner; returns the two level-histogram tensors (the root's
     is row 0 of the first, zeroed by the prologue)."""
     key = (RG_DBG, GBDT_CHOOSE_ROWS, LIST_NODE_COUNTS, PARTITION_COUNTS, RG_PARTIALS, RG_PARTIALS_MULTI, SPLIT_WIDE,
-           qmod.RG_LIST_WGS, qmod.RG_ALPHA)
+           qmod.RG_LIST_WGS, qmod.RG_ALPHA, qmod.RG_EM_MIN_FRAC)
     cached = getattr(ws, "_gbdt_levels", None)
     if cached is not None and cached[0] is runner and cached[2] == key:     # (in-process A/Bs flip these)
         return cached[1]
