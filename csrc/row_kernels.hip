@@ -678,7 +678,9 @@ __device__ __forceinline__ void rg_range_dense(RgShared<BINS>& sh, const RgHistA
 // of kRgSB batches (a lane per row) through a 3-stage pipeline -- list entries of super-batch
 // j + 3, (ptr, digits) of j + 2, the rows' first 8-entry blocks of j + 1 -- while the atomics of
 // super-batch j run: every load has a whole super-batch of work to arrive in.
-constexpr int kRgSB = 3;
+// (3 spilled 48 B per lane of rg_hist_kernel<8192> and fit 10M rows in 0.5098 s against 0.5015 s
+// with 2, same trees: profiles/r6/gbdt_late/NOTES.md §14)
+constexpr int kRgSB = 2;
 
 template <int BINS>
 __device__ __forceinline__ void rg_run_block(RgShared<BINS>& sh, uint4 v, uint32_t blk, uint32_t st, uint32_t en,
