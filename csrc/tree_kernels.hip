@@ -1897,7 +1897,7 @@ void launch_slot8(const SlotArgs& a, hipStream_t s) {
   if (a.N > 0) hipLaunchKernelGGL(slot8_kernel, dim3(grid_for(a.N)), dim3(256), 0, s, a);
 }
 
-__device__ __forceinline__ void hist_select_groups_kernel_body(SelectArgs a) {
+__device__ __forceinline__ void hist_select_groups_kernel_body(const SelectArgs& a) {
   const int g = blockIdx.y;
   const int64_t w0 = (int64_t)blockIdx.x * 256 * kSelPerThread;
   if (w0 >= a.num_slots[g]) return;                 // (workgroup-uniform)
